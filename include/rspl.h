@@ -1,0 +1,221 @@
+/*
+ * rspl.h -- C ABI of the MI355X-native SuperPoint -> SuperGlue -> local-BA hot path.
+ *
+ * Drop-in boundary for the reference's C++ API (llliuqingyu/RSPL-SLAM):
+ *   SuperPoint      include/super_point.h:20-66     -> rspl_sp_*
+ *   SuperGlue       include/super_glue.h:20-71      -> rspl_sg_*
+ *   PointMatching   include/point_matching.h:7-18   -> rspl_pm_*
+ *   LocalmapOptimization
+ *                   include/g2o_optimization/g2o_optimization.h:15-19 -> rspl_ba_*
+ * Plain pointers and sizes only; no Eigen / OpenCV / torch types.  Every call
+ * returns RSPL_OK (0) or a negative RSPL_E_* code (rspl_last_error() has the
+ * text).  Handles are NOT thread-safe: callers serialise, exactly as the
+ * reference's MapBuilder::_gpu_mutex does (src/map_builder.cc:276-278).
+ * Device memory is owned by the handle and allocated once at create time
+ * (no per-call allocation, unlike Thirdparty/TensorRTBuffer buffers.h:209-233).
+ *
+ * Feature layout (SuperPoint output / SuperGlue input) is the reference's
+ * Eigen::Matrix<double,259,Dynamic> column-major storage
+ * (src/super_point.cpp:368-387): feature i occupies doubles [259*i, 259*i+259):
+ *   [0] score, [1] x, [2] y, [3..258] L2-normalised descriptor.
+ */
+#ifndef RSPL_H_
+#define RSPL_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RSPL_OK 0
+#define RSPL_E_ARG (-1)      /* bad argument / shape */
+#define RSPL_E_WEIGHTS (-2)  /* weight blob missing or malformed */
+#define RSPL_E_DEVICE (-3)   /* HIP runtime error */
+#define RSPL_E_CAPACITY (-4) /* output or arena capacity exceeded */
+#define RSPL_E_SOLVER (-5)   /* linear solve failed */
+
+#define RSPL_FEATURE_ROWS 259
+
+enum { RSPL_PREC_FP32 = 0, RSPL_PREC_FP16 = 1 };
+
+const char* rspl_last_error(void);
+const char* rspl_version(void);
+
+/* ------------------------------------------------------------------------ */
+/* SuperPoint: SuperPointConfig (include/read_configs.h:9-18) minus TRT-only */
+/* fields; max_height/max_width size the device arena like the TRT profile   */
+/* kMAX does (src/super_point.cpp:113-123).                                 */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int max_keypoints;         /* top-k; -1 keeps all (src/super_point.cpp:263) */
+  double keypoint_threshold; /* scores > threshold (src/super_point.cpp:228) */
+  int remove_borders;        /* border in pixels (src/super_point.cpp:244-245) */
+  int max_height;            /* arena sizing; H, W must be multiples of 8 */
+  int max_width;
+  int max_batch;             /* images per batched device call (>= 1) */
+  int precision;             /* RSPL_PREC_FP32 (parity) or RSPL_PREC_FP16 */
+  int device;                /* HIP device ordinal */
+} rspl_sp_config;
+
+typedef struct rspl_sp rspl_sp;
+
+/* SuperPoint::SuperPoint + build() (src/super_point.cpp:83-156).
+ * weights_path: RSPLWT01 blob holding the reference state_dict
+ * (convert2onnx/superpoint.py:86-105). */
+int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_path, rspl_sp** out);
+
+/* SuperPoint::infer (src/super_point.cpp:174-205): rectified u8 image
+ * (row stride in bytes) -> features[259 * capacity]; *n_out = keypoints. */
+int rspl_sp_infer(rspl_sp* sp, const uint8_t* image, int height, int width, int stride,
+                  double* features, int capacity, int* n_out);
+
+/* Device-resident batched form: B images in device memory
+ * (d_images + b*image_pitch), features to d_features + b*259*capacity,
+ * counts to d_counts[b] (device int32).  stream may be NULL (handle stream). */
+int rspl_sp_infer_device(rspl_sp* sp, const uint8_t* d_images, int batch, int height, int width,
+                         int stride, size_t image_pitch, double* d_features, int capacity,
+                         int32_t* d_counts, void* stream);
+
+/* Intermediate maps of the last device call for image b (for tests):
+ * scores [H*W] f32 after NMS, desc [256*(H/8)*(W/8)] f32 channel-major. */
+int rspl_sp_debug_maps(rspl_sp* sp, int b, float* scores, float* desc);
+
+void rspl_sp_destroy(rspl_sp* sp);
+
+/* ------------------------------------------------------------------------ */
+/* SuperGlue: SuperGlueConfig (include/read_configs.h:20-28).               */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int image_width;   /* used by PointMatching::NormalizeKeypoints */
+  int image_height;
+  int max_keypoints; /* per image; arena sizing (the TRT profile allows 1024, src/super_glue.cpp:54-75) */
+  int max_batch;     /* pairs per batched device call */
+  int sinkhorn_iterations; /* 100 (convert2onnx/superglue.py:216) */
+  int precision;
+  int device;
+} rspl_sg_config;
+
+typedef struct rspl_sg rspl_sg;
+
+int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_path, rspl_sg** out);
+
+/* SuperGlue::infer (src/super_glue.cpp:137-197): f0/f1 are 259 x n feature
+ * matrices whose keypoints are ALREADY normalised (as PointMatching passes
+ * them).  Outputs: indices0[n0], indices1[n1] (-1 = unmatched), mscores0[n0],
+ * mscores1[n1]  (decode: src/super_glue.cpp:339-367). */
+int rspl_sg_infer(rspl_sg* sg, const double* f0, int n0, const double* f1, int n1,
+                  int32_t* indices0, int32_t* indices1, double* mscores0, double* mscores1);
+
+/* Device-resident batched form.  Pair p reads f0 = d_feat0 + p*259*stride_feat,
+ * n0 = counts0[p] (HOST ints), likewise image 1; writes d_idx0 + p*max_kp etc.
+ * normalize != 0 applies PointMatching::NormalizeKeypoints on device first. */
+int rspl_sg_infer_device(rspl_sg* sg, int batch, const double* d_feat0, const int* n0,
+                         const double* d_feat1, const int* n1, int stride_feat, int normalize,
+                         int32_t* d_idx0, int32_t* d_idx1, double* d_ms0, double* d_ms1,
+                         void* stream);
+
+/* Log-assignment Z [(n0+1)*(n1+1)] f32 of the last call, pair p (for tests). */
+int rspl_sg_debug_scores(rspl_sg* sg, int p, float* Z);
+
+void rspl_sg_destroy(rspl_sg* sg);
+
+/* ------------------------------------------------------------------------ */
+/* PointMatching (src/point_matching.cc): normalise, SuperGlue, mutual check, */
+/* DMatch(i, j, 1 - (ms0 + ms1)/2).  outlier_rejection (F-matrix RANSAC,     */
+/* default off in the reference) is not implemented: RSPL_E_ARG if set.      */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int32_t query_idx;
+  int32_t train_idx;
+  float distance;
+} rspl_dmatch;
+
+int rspl_pm_match(rspl_sg* sg, const double* f0, int n0, const double* f1, int n1,
+                  rspl_dmatch* matches, int capacity, int* n_matches, int outlier_rejection);
+
+/* ------------------------------------------------------------------------ */
+/* Local bundle adjustment: LocalmapOptimization                            */
+/* (src/g2o_optimization/g2o_optimization.cc:21-252).  Vertex ids of the    */
+/* reference's std::maps are remapped to dense indices by the caller.       */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int n_cameras;
+  const double* cameras;        /* [n][5] fx, fy, cx, cy, bf (include/camera.h:25-29) */
+
+  int n_poses;
+  const double* pose_q;         /* [n][4] rotation of T_wc, Eigen coeffs order (x, y, z, w) */
+  const double* pose_p;         /* [n][3] translation of T_wc */
+  const uint8_t* pose_fixed;    /* [n] Pose3d::fixed */
+
+  int n_points;
+  const double* points;         /* [n][3] world position */
+
+  int n_lines;
+  const double* lines;          /* [n][6] g2o::Line3D Pluecker (w, d) */
+
+  int n_mono;                   /* MonoPointConstraint (types.h:54-78) */
+  const int32_t* mono_pose;
+  const int32_t* mono_point;
+  const int32_t* mono_camera;   /* may be NULL -> camera 0 */
+  const double* mono_obs;       /* [n][2] */
+
+  int n_stereo;                 /* StereoPointConstraint (types.h:81-105) */
+  const int32_t* stereo_pose;
+  const int32_t* stereo_point;
+  const int32_t* stereo_camera;
+  const double* stereo_obs;     /* [n][3] u, v, u_right */
+
+  int n_mono_line;              /* MonoLineConstraint (types.h:124-148) */
+  const int32_t* mono_line_pose;
+  const int32_t* mono_line_line;
+  const int32_t* mono_line_camera;
+  const double* mono_line_obs;  /* [n][4] x1 y1 x2 y2 */
+
+  int n_stereo_line;            /* StereoLineConstraint (types.h:151-174) */
+  const int32_t* stereo_line_pose;
+  const int32_t* stereo_line_line;
+  const int32_t* stereo_line_camera;
+  const double* stereo_line_obs; /* [n][8] left x1 y1 x2 y2, right x1 y1 x2 y2 */
+
+  /* OptimizationConfig (include/read_configs.h:50-56): chi2 thresholds; the
+   * Huber deltas are (float)sqrt(threshold) (g2o_optimization.cc:77-78,125-126) */
+  double th_mono_point, th_stereo_point, th_mono_line, th_stereo_line;
+  int iterations_first;   /* 10 (g2o_optimization.cc:173) */
+  int iterations_second;  /* 5  (g2o_optimization.cc:210) */
+} rspl_ba_problem;
+
+typedef struct {
+  double* pose_q;     /* [n_poses][4] optimised T_wc rotation (x, y, z, w) */
+  double* pose_p;     /* [n_poses][3] */
+  double* points;     /* [n_points][3] */
+  double* lines;      /* [n_lines][6] */
+  uint8_t* mono_inlier;
+  uint8_t* stereo_inlier;
+  uint8_t* mono_line_inlier;
+  uint8_t* stereo_line_inlier;
+  double chi2_first;  /* robust chi2 at the end of the first optimize() */
+  double chi2_second; /* chi2 at the end of the second optimize() */
+  int iterations_done_first;
+  int iterations_done_second;
+} rspl_ba_result;
+
+typedef struct {
+  int max_poses;
+  int max_points;
+  int max_lines;
+  int max_edges;      /* per edge type */
+  int device;
+} rspl_ba_config;
+
+typedef struct rspl_ba rspl_ba;
+
+int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out);
+int rspl_ba_local(rspl_ba* ba, const rspl_ba_problem* problem, rspl_ba_result* result);
+void rspl_ba_destroy(rspl_ba* ba);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* RSPL_H_ */

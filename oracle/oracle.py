@@ -1,0 +1,116 @@
+"""ORACLE (test infrastructure only) -- ctypes front-end of oracle/build/liboracle.so,
+the C restatement of the reference path (see oracle/*.c headers for citations).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module, and only as the checker / baseline -- never as the product path.
+Pinned against tests/golden/* (generated from the reference's own PyTorch
+modules) by tests/test_oracle.py.  The BA restatement is parity UNPINNED at the
+g2o boundary (g2o is not vendored in the reference): it is checked against
+scipy least-squares optima and noise-free known answers instead.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import pathlib
+import subprocess
+
+import numpy as np
+
+HERE = pathlib.Path(__file__).resolve().parent
+LIB_PATH = HERE / "build" / "liboracle.so"
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        _lib = C.CDLL(str(LIB_PATH))
+        f32p = np.ctypeslib.ndpointer(np.float32, flags="C_CONTIGUOUS")
+        _lib.orc_sp_forward.argtypes = [C.c_char_p, f32p, C.c_int, C.c_int, f32p, f32p]
+        _lib.orc_sp_forward.restype = C.c_int
+        _lib.orc_simple_nms.argtypes = [f32p, C.c_int, C.c_int]
+        _lib.orc_sg_forward.argtypes = [C.c_char_p, f32p, f32p, f32p, C.c_int, f32p, f32p, f32p, C.c_int,
+                                        C.c_int, f32p]
+        _lib.orc_sg_forward.restype = C.c_int
+        _lib.orc_log_optimal_transport.argtypes = [f32p, C.c_int, C.c_int, C.c_float, C.c_int, f32p]
+        _lib.orc_ba_local.argtypes = [C.c_void_p, C.c_void_p]
+        _lib.orc_ba_local.restype = C.c_int
+        f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+        _lib.orc_line_oplus.argtypes = [f64p, f64p]
+    return _lib
+
+
+def set_threads(n: int):
+    os.environ["OMP_NUM_THREADS"] = str(n)
+    try:
+        C.CDLL("libgomp.so.1").omp_set_num_threads(int(n))
+    except OSError:
+        pass
+
+
+def sp_forward(weights_path: str, x: np.ndarray):
+    """x: [H, W] float32 (u8/255).  Returns (scores [H, W] post-NMS, desc [256, H/8, W/8])."""
+    x = np.ascontiguousarray(x, np.float32)
+    H, W = x.shape
+    s = np.zeros((H, W), np.float32)
+    d = np.zeros((256, H // 8, W // 8), np.float32)
+    rc = lib().orc_sp_forward(str(weights_path).encode(), x, H, W, s, d)
+    if rc:
+        raise RuntimeError(f"orc_sp_forward rc={rc}")
+    return s, d
+
+
+def simple_nms(scores: np.ndarray) -> np.ndarray:
+    s = np.ascontiguousarray(scores, np.float32).copy()
+    lib().orc_simple_nms(s, s.shape[0], s.shape[1])
+    return s
+
+
+def sg_forward(weights_path: str, k0, s0, d0, k1, s1, d1, iters: int = 100) -> np.ndarray:
+    """kpts [N,2], scores [N], desc [256,N] (float32, keypoints normalised) -> Z [(N+1),(M+1)]."""
+    a = lambda v: np.ascontiguousarray(v, np.float32)
+    k0, s0, d0, k1, s1, d1 = map(a, (k0, s0, d0, k1, s1, d1))
+    n0, n1 = k0.shape[0], k1.shape[0]
+    Z = np.zeros((n0 + 1, n1 + 1), np.float32)
+    rc = lib().orc_sg_forward(str(weights_path).encode(), k0.reshape(-1) if n0 else np.zeros(1, np.float32),
+                              s0 if n0 else np.zeros(1, np.float32), d0.reshape(-1) if n0 else np.zeros(1, np.float32), n0,
+                              k1.reshape(-1) if n1 else np.zeros(1, np.float32),
+                              s1 if n1 else np.zeros(1, np.float32), d1.reshape(-1) if n1 else np.zeros(1, np.float32), n1,
+                              iters, Z)
+    if rc:
+        raise RuntimeError(f"orc_sg_forward rc={rc}")
+    return Z
+
+
+def log_optimal_transport(scores: np.ndarray, alpha: float, iters: int = 100) -> np.ndarray:
+    s = np.ascontiguousarray(scores, np.float32)
+    m, n = s.shape
+    Z = np.zeros((m + 1, n + 1), np.float32)
+    lib().orc_log_optimal_transport(s if s.size else np.zeros(1, np.float32), m, n, alpha, iters, Z)
+    return Z
+
+
+def ba_local(problem):
+    """problem: rspl_slam_amd.ba_types.DenseProblem -> DenseResult."""
+    from rspl_slam_amd.ba_types import DenseResult
+    res = DenseResult.alloc(problem)
+    P = problem.to_ctypes()
+    R = res.to_ctypes()
+    rc = lib().orc_ba_local(C.byref(P), C.byref(R))
+    if rc:
+        raise RuntimeError(f"orc_ba_local rc={rc}")
+    res.read_back(R)
+    return res
+
+
+def line_oplus(L: np.ndarray, v: np.ndarray) -> np.ndarray:
+    L = np.ascontiguousarray(L, np.float64).copy()
+    lib().orc_line_oplus(L, np.ascontiguousarray(v, np.float64))
+    return L

@@ -1,0 +1,215 @@
+"""Seeded synthetic inputs shaped like the reference's workloads.
+
+EuRoC / OIVIO images are not available, so benches and tests
+use seeded textured images with EuRoC geometry (752x480 u8), synthetic
+SuperGlue keypoint sets, and synthetic local-BA problems with ground truth.
+Everything here is numpy, deterministic for a given seed.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+# EuRoC rectified intrinsics: configs/euroc.yaml:7 (bf) and LEFT.P (:32-36)
+EUROC_FX = 435.2046959714599
+EUROC_FY = 435.2046959714599
+EUROC_CX = 367.4517211914062
+EUROC_CY = 252.2008514404297
+EUROC_BF = 47.90639384423901
+
+
+def textured_image(h: int, w: int, seed: int, n_blobs: int = 60) -> np.ndarray:
+    """Smooth texture + gaussian blobs + pixel noise, u8 [h, w]."""
+    rng = np.random.default_rng(seed)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    img = 128 + 40 * np.sin(xx / 7.3) * np.cos(yy / 5.1) + 30 * np.sin((xx + yy) / 13.7)
+    for _ in range(n_blobs):
+        cx, cy, r = rng.uniform(0, w), rng.uniform(0, h), rng.uniform(3, 25)
+        img += rng.uniform(-60, 60) * np.exp(-((xx - cx) ** 2 + (yy - cy) ** 2) / (2 * r * r))
+    img += rng.normal(0, 6, size=img.shape)
+    return np.clip(img, 0, 255).astype(np.uint8)
+
+
+def stereo_pair(h: int, w: int, seed: int, disparity: int = 12):
+    """Left/right u8 images: the right view is the left texture shifted by a constant disparity
+    plus independent sensor noise (rectified stereo, as after Camera::UndistortImage)."""
+    base = textured_image(h, w + disparity, seed).astype(np.float64)
+    rng = np.random.default_rng(seed + 1000)
+    left = base[:, disparity:]
+    right = base[:, :w]
+    right = right + rng.normal(0, 2, size=right.shape)
+    return left.astype(np.uint8), np.clip(right, 0, 255).astype(np.uint8)
+
+
+def sg_problem(n0: int, n1: int, n_common: int, seed: int, width: int = 752, height: int = 480):
+    """Two 259 x n feature matrices (score, x, y, desc[256]) in IMAGE coordinates (not normalised),
+    where n_common keypoints of image 1 are noisy copies of image-0 keypoints.
+    Returns (F0, F1, gt) with gt[j] = index in image 0 of image-1 keypoint j or -1."""
+    rng = np.random.default_rng(seed)
+    k0 = rng.uniform([0, 0], [width, height], size=(n0, 2))
+    d0 = rng.normal(size=(256, n0))
+    d0 /= np.linalg.norm(d0, axis=0)
+    n_common = min(n_common, n0, n1)
+    perm = rng.permutation(n0)[:n_common]
+    k1 = np.concatenate([k0[perm] + rng.normal(0, 1.0, size=(n_common, 2)),
+                         rng.uniform([0, 0], [width, height], size=(n1 - n_common, 2))])
+    d1 = np.concatenate([d0[:, perm] + 0.5 * rng.normal(size=(256, n_common)) / 16,
+                         rng.normal(size=(256, n1 - n_common))], 1)
+    d1 /= np.linalg.norm(d1, axis=0)
+    s0 = rng.uniform(size=n0)
+    s1 = rng.uniform(size=n1)
+    F0 = np.concatenate([s0[None], k0.T, d0], 0)
+    F1 = np.concatenate([s1[None], k1.T, d1], 0)
+    gt = np.full(n1, -1, np.int64)
+    gt[:n_common] = perm
+    return np.ascontiguousarray(F0), np.ascontiguousarray(F1), gt
+
+
+# ----------------------------------------------------------------------------
+# Synthetic local-BA problems (Map::LocalMapOptimization shapes, src/map.cc:537-707)
+# ----------------------------------------------------------------------------
+def _rotvec_to_R(r):
+    th = np.linalg.norm(r)
+    if th < 1e-12:
+        return np.eye(3)
+    k = r / th
+    Kx = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * Kx + (1 - np.cos(th)) * Kx @ Kx
+
+
+def R_to_quat_xyzw(R):
+    t = np.trace(R)
+    if t > 0:
+        s = np.sqrt(t + 1.0) * 2
+        w, x, y, z = 0.25 * s, (R[2, 1] - R[1, 2]) / s, (R[0, 2] - R[2, 0]) / s, (R[1, 0] - R[0, 1]) / s
+    else:
+        i = int(np.argmax(np.diag(R)))
+        j, k = (i + 1) % 3, (i + 2) % 3
+        s = np.sqrt(R[i, i] - R[j, j] - R[k, k] + 1.0) * 2
+        v = np.zeros(3)
+        v[i] = 0.25 * s
+        w = (R[k, j] - R[j, k]) / s
+        v[j] = (R[j, i] + R[i, j]) / s
+        v[k] = (R[k, i] + R[i, k]) / s
+        x, y, z = v
+    q = np.array([x, y, z, w])
+    return q / np.linalg.norm(q) * (1 if w >= 0 else -1)
+
+
+def quat_xyzw_to_R(q):
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def ba_problem(n_poses: int = 10, n_points: int = 2000, n_lines: int = 50, obs_per_point: int = 6,
+               pixel_sigma: float = 0.8, outlier_frac: float = 0.05, seed: int = 0,
+               init_noise: float = 1.0, width: int = 752, height: int = 480, n_fixed: int = 1,
+               cam=(EUROC_FX, EUROC_FY, EUROC_CX, EUROC_CY, EUROC_BF)):
+    """Seeded local-BA problem with ground truth.
+
+    Returns (DenseProblem, gt) where gt = dict(pose_q, pose_p, points, lines).  Points are observed
+    by ``obs_per_point`` random poses that see them; observations are stereo when the right-image
+    coordinate is valid (Frame::AddRightFeatures-style depth range), else mono; ``outlier_frac``
+    of the observations get gross (30-80 px) errors.  The first ``n_fixed`` poses are fixed.
+    ``init_noise`` scales the perturbation of the initial estimate (0 = start at ground truth).
+    """
+    from .ba_types import DenseProblem
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = cam
+    # trajectory: forward-moving camera with small yaw/pitch wobble (T_wc)
+    Rwc, twc = [], []
+    for i in range(n_poses):
+        r = np.array([0.02 * np.sin(0.7 * i), 0.05 * np.sin(0.3 * i), 0.01 * i])
+        Rwc.append(_rotvec_to_R(r))
+        twc.append(np.array([0.15 * i, 0.03 * np.sin(0.5 * i), 0.08 * i]))
+    # points in front of the rig
+    pts = np.stack([rng.uniform(-4, 4 + 0.15 * n_poses, n_points), rng.uniform(-2.5, 2.5, n_points),
+                    rng.uniform(3.0, 14.0, n_points) + 0.08 * n_poses * rng.uniform(0, 1, n_points)], 1)
+
+    def project(i, X):
+        Xc = Rwc[i].T @ (X - twc[i])
+        if Xc[2] <= 0.1:
+            return None
+        u = fx * Xc[0] / Xc[2] + cx
+        v = fy * Xc[1] / Xc[2] + cy
+        if not (0 <= u < width and 0 <= v < height):
+            return None
+        return np.array([u, v, u - bf / Xc[2]]), Xc[2]
+
+    mono = dict(pose=[], lm=[], obs=[])
+    stereo = dict(pose=[], lm=[], obs=[])
+    keep = []
+    for j in range(n_points):
+        vis = [i for i in range(n_poses) if project(i, pts[j]) is not None]
+        if len(vis) < 2:
+            continue
+        sel = rng.permutation(vis)[:obs_per_point]
+        jj = len(keep)
+        keep.append(j)
+        for i in sorted(sel):
+            uvr, z = project(i, pts[j])
+            noisy = uvr + rng.normal(0, pixel_sigma, 3)
+            if rng.uniform() < outlier_frac:
+                noisy[:2] += rng.uniform(30, 80, 2) * rng.choice([-1, 1], 2)
+            if uvr[2] > 0 and z < 10.0 and rng.uniform() < 0.7:   # stereo (right coordinate valid)
+                stereo["pose"].append(i); stereo["lm"].append(jj); stereo["obs"].append(noisy)
+            else:
+                mono["pose"].append(i); mono["lm"].append(jj); mono["obs"].append(noisy[:2])
+    pts = pts[keep]
+
+    # lines: segments in front of the rig; Pluecker (w = p x d, d unit)
+    lines_gt, mline, sline = [], dict(pose=[], lm=[], obs=[]), dict(pose=[], lm=[], obs=[])
+    for _ in range(n_lines):
+        p0 = np.array([rng.uniform(-3, 3 + 0.15 * n_poses), rng.uniform(-2, 2), rng.uniform(4, 10)])
+        dvec = rng.normal(size=3)
+        dvec /= np.linalg.norm(dvec)
+        p1 = p0 + dvec * rng.uniform(0.8, 2.0)
+        obs_i = []
+        for i in range(n_poses):
+            a, b = project(i, p0), project(i, p1)
+            if a is None or b is None:
+                continue
+            obs_i.append((i, a[0], b[0]))
+        if len(obs_i) < 2:
+            continue
+        li = len(lines_gt)
+        lines_gt.append(np.concatenate([np.cross(p0, dvec), dvec]))
+        for (i, a, b) in obs_i[:obs_per_point]:
+            nL = rng.normal(0, pixel_sigma, 4)
+            ol = np.array([a[0], a[1], b[0], b[1]]) + nL
+            if a[2] > 0 and b[2] > 0 and rng.uniform() < 0.5:
+                orr = np.array([a[2], a[1], b[2], b[1]]) + rng.normal(0, pixel_sigma, 4)
+                sline["pose"].append(i); sline["lm"].append(li); sline["obs"].append(np.concatenate([ol, orr]))
+            else:
+                mline["pose"].append(i); mline["lm"].append(li); mline["obs"].append(ol)
+    lines_gt = np.array(lines_gt).reshape(-1, 6)
+
+    q_gt = np.array([R_to_quat_xyzw(R) for R in Rwc])
+    p_gt = np.array(twc)
+    # perturbed initial estimate
+    q0, p0s = q_gt.copy(), p_gt.copy()
+    for i in range(n_fixed, n_poses):
+        dR = _rotvec_to_R(rng.normal(0, 0.005 * init_noise, 3))
+        q0[i] = R_to_quat_xyzw(dR @ quat_xyzw_to_R(q_gt[i]))
+        p0s[i] = p_gt[i] + rng.normal(0, 0.02 * init_noise, 3)
+    pts0 = pts + rng.normal(0, 0.05 * init_noise, pts.shape)
+    lines0 = lines_gt.copy()
+    for k in range(lines0.shape[0]):
+        # move the line by a small rigid perturbation of two points on it, then re-derive (w, d)
+        d = lines0[k, 3:]
+        w = lines0[k, :3]
+        pc = np.cross(d, w)   # closest point to origin (|d| = 1)
+        pa = pc + rng.normal(0, 0.03 * init_noise, 3)
+        da = d + rng.normal(0, 0.01 * init_noise, 3)
+        da /= np.linalg.norm(da)
+        lines0[k] = np.concatenate([np.cross(pa, da), da])
+    fixed = np.zeros(n_poses, np.uint8)
+    fixed[:n_fixed] = 1
+    arr = lambda d, od: dict(pose=np.array(d["pose"], np.int32), lm=np.array(d["lm"], np.int32),
+                             obs=np.array(d["obs"], np.float64).reshape(-1, od))
+    prob = DenseProblem(cameras=np.array([cam], np.float64), pose_q=q0, pose_p=p0s, pose_fixed=fixed,
+                        points=pts0, lines=lines0, mono=arr(mono, 2), stereo=arr(stereo, 3),
+                        mono_line=arr(mline, 4), stereo_line=arr(sline, 8))
+    gt = dict(pose_q=q_gt, pose_p=p_gt, points=pts, lines=lines_gt)
+    return prob, gt

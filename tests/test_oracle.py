@@ -1,0 +1,96 @@
+"""Pin the oracle (oracle/*.c, oracle/post.py) to the reference's own outputs
+(tests/golden, generated from convert2onnx/superpoint.py & superglue.py)."""
+import numpy as np
+import pytest
+
+import oracle
+import post
+from helpers import compare_features
+
+
+def test_weight_generator_pinned(golden):
+    from rspl_slam_amd import weights as W
+    g = golden("weights_pin")
+    sp, sg = W.superpoint_synth(1), W.superglue_synth(2)
+    for key in g.files:
+        name = key.replace("__", ".")
+        src = sp if name in sp else sg
+        np.testing.assert_array_equal(src[name].reshape(-1)[:16], g[key])
+
+
+def test_blob_roundtrip(tmp_path):
+    from rspl_slam_amd import weights as W
+    t = W.superpoint_synth(3)
+    W.write_blob(tmp_path / "w.bin", t)
+    r = W.read_blob(tmp_path / "w.bin")
+    assert list(r) == list(t)
+    for k in t:
+        np.testing.assert_array_equal(r[k], t[k])
+
+
+def test_sp_small_forward(golden, weight_blobs):
+    g = golden("sp_small")
+    s, d = oracle.sp_forward(weight_blobs[0], post.image_to_input(g["image"]))
+    np.testing.assert_allclose(s, g["scores"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(d, g["desc"], rtol=1e-3, atol=1e-5)
+    F = post.sp_postprocess(s, d, float(g["threshold"]), int(g["border"]), int(g["k"]))
+    compare_features(F, g["features"])
+
+
+def test_sp_euroc_forward(golden, weight_blobs):
+    g = golden("sp_euroc")
+    s, d = oracle.sp_forward(weight_blobs[0], post.image_to_input(g["image"]))
+    nz = np.nonzero(s.reshape(-1))[0]
+    np.testing.assert_array_equal(nz, g["nms_idx"])
+    np.testing.assert_allclose(s.reshape(-1)[nz], g["nms_val"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(d.reshape(-1)[g["desc_sample_idx"]], g["desc_sample_val"], rtol=1e-3, atol=1e-5)
+    F = post.sp_postprocess(s, d, 0.004, 4, 400)
+    G = np.concatenate([g["feat_head"], g["feat_desc"].astype(np.float64)])
+    compare_features(F, G)
+
+
+@pytest.mark.parametrize("i", [0, 1, 2])
+def test_nms_unit(golden, i):
+    g = golden("nms_unit")
+    np.testing.assert_array_equal(oracle.simple_nms(g[f"in{i}"]), g[f"out{i}"])
+
+
+def test_sinkhorn_unit(golden):
+    g = golden("sinkhorn_unit")
+    Z = oracle.log_optimal_transport(g["scores"], float(g["alpha"]), int(g["iters"]))
+    np.testing.assert_allclose(Z, g["Z"], atol=1e-4, rtol=0)
+
+
+def test_decode_unit(golden):
+    g = golden("sinkhorn_unit")
+    for pre, Z in (("", g["Z"]), ("t_", g["Z_ties"])):
+        i0, i1, m0, m1 = post.decode(Z)
+        np.testing.assert_array_equal(i0, g[pre + "idx0"])
+        np.testing.assert_array_equal(i1, g[pre + "idx1"])
+        np.testing.assert_array_equal(m0, g[pre + "ms0"])
+        np.testing.assert_array_equal(m1, g[pre + "ms1"])
+
+
+@pytest.mark.parametrize("name", ["sg_small", "sg_400"])
+def test_sg_forward(golden, weight_blobs, name):
+    g = golden(name)
+    F0, F1 = g["F0"].astype(np.float64), g["F1"].astype(np.float64)
+    w, h = int(g["width"]), int(g["height"])
+    a = post.sg_inputs(post.normalize_keypoints(F0, w, h))
+    b = post.sg_inputs(post.normalize_keypoints(F1, w, h))
+    Z = oracle.sg_forward(weight_blobs[1], *a, *b)
+    np.testing.assert_allclose(Z, g["Z"], atol=1e-3 if name == "sg_400" else 1e-4, rtol=1e-5)
+    i0, i1, m0, m1 = post.decode(Z)
+    np.testing.assert_array_equal(i0, g["idx0"])
+    np.testing.assert_array_equal(i1, g["idx1"])
+    np.testing.assert_allclose(m0, g["ms0"], rtol=1e-4, atol=1e-6)
+    mt, md = post.match_points(i0, i1, m0, m1)
+    np.testing.assert_array_equal(mt, g["matches"])
+    np.testing.assert_allclose(md, g["distances"], atol=1e-5)
+
+
+def test_sg_empty(weight_blobs):
+    k = np.zeros((0, 2), np.float32)
+    Z = oracle.sg_forward(weight_blobs[1], k, np.zeros(0, np.float32), np.zeros((256, 0), np.float32),
+                          k, np.zeros(0, np.float32), np.zeros((256, 0), np.float32))
+    assert Z.shape == (1, 1)
