@@ -44,6 +44,30 @@ const char* rspl_last_error(void);
 const char* rspl_version(void);
 
 /* ------------------------------------------------------------------------ */
+/* Runtime helpers (system ROCm HIP runtime).  Callers that share a process  */
+/* with another HIP runtime (e.g. PyTorch's bundled one) use these instead,  */
+/* so only one runtime ever touches the device.                              */
+/* ------------------------------------------------------------------------ */
+int rspl_device_count(int* count);
+int rspl_set_device(int device);
+int rspl_malloc(void** ptr, size_t bytes);
+int rspl_free(void* ptr);
+int rspl_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
+int rspl_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
+int rspl_memset(void* dst, int value, size_t bytes, void* stream);
+int rspl_stream_create(void** stream);
+int rspl_stream_destroy(void* stream);
+int rspl_stream_synchronize(void* stream);
+int rspl_device_synchronize(void);
+/* HIP-event timer on a stream: rspl_timer_record(t, 0|1, stream) marks
+ * start / stop; rspl_timer_elapsed_ms waits for stop and returns ms. */
+typedef struct rspl_timer rspl_timer;
+int rspl_timer_create(rspl_timer** t);
+int rspl_timer_record(rspl_timer* t, int which, void* stream);
+int rspl_timer_elapsed_ms(rspl_timer* t, float* ms);
+void rspl_timer_destroy(rspl_timer* t);
+
+/* ------------------------------------------------------------------------ */
 /* SuperPoint: SuperPointConfig (include/read_configs.h:9-18) minus TRT-only */
 /* fields; max_height/max_width size the device arena like the TRT profile   */
 /* kMAX does (src/super_point.cpp:113-123).                                 */

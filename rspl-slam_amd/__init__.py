@@ -1,5 +1,19 @@
 """rspl_slam_amd -- MI355X-native SuperPoint -> SuperGlue -> local-BA hot path.
 
-Import via ``rspl_loader.load()`` (the directory name carries a dash, so it is
-loaded by path as the module ``rspl_slam_amd``).
+Loaded by path as the module ``rspl_slam_amd`` (see rspl_loader.py; the
+directory name carries a dash).  The compute path is librspl.so (HIP, gfx950);
+this package only mirrors the reference's C++ interface over its C ABI.
 """
+import importlib
+
+from . import capi, weights, synthetic, ba_types  # noqa: F401
+
+_API = ("SuperPoint", "SuperPointConfig", "SuperGlue", "SuperGlueConfig", "PointMatching",
+        "LocalmapOptimization")
+
+
+def __getattr__(name):
+    # the API module is imported lazily so CPU-only tooling (weights, synthetic) never loads librspl.so
+    if name in _API:
+        return getattr(importlib.import_module(__name__ + ".api"), name)
+    raise AttributeError(name)

@@ -1,0 +1,205 @@
+"""ctypes binding of librspl.so (the C ABI declared in include/rspl.h).
+
+This is the product path: every call goes to the HIP library.  There is no CPU
+fallback -- if librspl.so is missing or no HIP device is visible, calls raise.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import pathlib
+
+PKG = pathlib.Path(__file__).resolve().parent
+LIB_PATH = PKG / "librspl.so"
+
+RSPL_OK = 0
+RSPL_PREC_FP32 = 0
+RSPL_PREC_FP16 = 1
+
+EXPORTS = [
+    "rspl_last_error", "rspl_version",
+    "rspl_device_count", "rspl_set_device", "rspl_malloc", "rspl_free", "rspl_memcpy_h2d", "rspl_memcpy_d2h",
+    "rspl_memset", "rspl_stream_create", "rspl_stream_destroy", "rspl_stream_synchronize",
+    "rspl_device_synchronize", "rspl_timer_create", "rspl_timer_record", "rspl_timer_elapsed_ms",
+    "rspl_timer_destroy",
+    "rspl_sp_create", "rspl_sp_infer", "rspl_sp_infer_device", "rspl_sp_debug_maps", "rspl_sp_destroy",
+    "rspl_sg_create", "rspl_sg_infer", "rspl_sg_infer_device", "rspl_sg_debug_scores", "rspl_sg_destroy",
+    "rspl_pm_match",
+    "rspl_ba_create", "rspl_ba_local", "rspl_ba_destroy",
+]
+
+
+class SpConfig(C.Structure):
+    _fields_ = [("max_keypoints", C.c_int), ("keypoint_threshold", C.c_double), ("remove_borders", C.c_int),
+                ("max_height", C.c_int), ("max_width", C.c_int), ("max_batch", C.c_int),
+                ("precision", C.c_int), ("device", C.c_int)]
+
+
+class SgConfig(C.Structure):
+    _fields_ = [("image_width", C.c_int), ("image_height", C.c_int), ("max_keypoints", C.c_int),
+                ("max_batch", C.c_int), ("sinkhorn_iterations", C.c_int), ("precision", C.c_int),
+                ("device", C.c_int)]
+
+
+class DMatch(C.Structure):
+    _fields_ = [("query_idx", C.c_int32), ("train_idx", C.c_int32), ("distance", C.c_float)]
+
+
+class BaConfig(C.Structure):
+    _fields_ = [("max_poses", C.c_int), ("max_points", C.c_int), ("max_lines", C.c_int),
+                ("max_edges", C.c_int), ("device", C.c_int)]
+
+
+class RsplError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def load(path: pathlib.Path = LIB_PATH):
+    """Load librspl.so and declare the C ABI.  Raises if the library is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not path.exists():
+        raise RsplError(f"{path} not built: run __graft_entry__.build() (no CPU fallback exists)")
+    lib = C.CDLL(str(path))
+    vp, ip, dp = C.c_void_p, C.c_int, C.c_double
+    lib.rspl_last_error.restype = C.c_char_p
+    lib.rspl_version.restype = C.c_char_p
+    lib.rspl_sp_create.argtypes = [C.POINTER(SpConfig), C.c_char_p, C.POINTER(vp)]
+    lib.rspl_sp_infer.argtypes = [vp, vp, ip, ip, ip, vp, ip, C.POINTER(ip)]
+    lib.rspl_sp_infer_device.argtypes = [vp, vp, ip, ip, ip, ip, C.c_size_t, vp, ip, vp, vp]
+    lib.rspl_sp_debug_maps.argtypes = [vp, ip, vp, vp]
+    lib.rspl_sp_destroy.argtypes = [vp]
+    lib.rspl_sp_destroy.restype = None
+    lib.rspl_device_count.argtypes = [C.POINTER(ip)]
+    lib.rspl_set_device.argtypes = [ip]
+    lib.rspl_malloc.argtypes = [C.POINTER(vp), C.c_size_t]
+    lib.rspl_free.argtypes = [vp]
+    lib.rspl_memcpy_h2d.argtypes = [vp, vp, C.c_size_t, vp]
+    lib.rspl_memcpy_d2h.argtypes = [vp, vp, C.c_size_t, vp]
+    lib.rspl_memset.argtypes = [vp, ip, C.c_size_t, vp]
+    lib.rspl_stream_create.argtypes = [C.POINTER(vp)]
+    lib.rspl_stream_destroy.argtypes = [vp]
+    lib.rspl_stream_synchronize.argtypes = [vp]
+    lib.rspl_timer_create.argtypes = [C.POINTER(vp)]
+    lib.rspl_timer_record.argtypes = [vp, ip, vp]
+    lib.rspl_timer_elapsed_ms.argtypes = [vp, C.POINTER(C.c_float)]
+    lib.rspl_timer_destroy.argtypes = [vp]
+    lib.rspl_timer_destroy.restype = None
+    if hasattr(lib, "rspl_sg_create"):
+        lib.rspl_sg_create.argtypes = [C.POINTER(SgConfig), C.c_char_p, C.POINTER(vp)]
+        lib.rspl_sg_infer.argtypes = [vp, vp, ip, vp, ip, vp, vp, vp, vp]
+        lib.rspl_sg_infer_device.argtypes = [vp, ip, vp, vp, vp, vp, ip, ip, vp, vp, vp, vp, vp]
+        lib.rspl_sg_debug_scores.argtypes = [vp, ip, vp]
+        lib.rspl_sg_destroy.argtypes = [vp]
+        lib.rspl_sg_destroy.restype = None
+        lib.rspl_pm_match.argtypes = [vp, vp, ip, vp, ip, C.POINTER(DMatch), ip, C.POINTER(ip), ip]
+    if hasattr(lib, "rspl_ba_create"):
+        lib.rspl_ba_create.argtypes = [C.POINTER(BaConfig), C.POINTER(vp)]
+        lib.rspl_ba_local.argtypes = [vp, vp, vp]
+        lib.rspl_ba_destroy.argtypes = [vp]
+        lib.rspl_ba_destroy.restype = None
+    _lib = lib
+    return lib
+
+
+def check(rc: int, what: str):
+    if rc != RSPL_OK:
+        msg = load().rspl_last_error().decode(errors="replace")
+        raise RsplError(f"{what} failed (rc={rc}): {msg}")
+
+
+# ---------------------------------------------------------------------------
+# Device memory / stream / timer wrappers over librspl's own (system ROCm) HIP
+# runtime.  Python code in this repo uses these instead of torch.cuda, so only
+# one HIP runtime ever drives the device from a process.
+# ---------------------------------------------------------------------------
+import numpy as _np
+
+
+class DeviceBuffer:
+    def __init__(self, nbytes: int):
+        self.nbytes = int(nbytes)
+        self._p = C.c_void_p()
+        check(load().rspl_malloc(C.byref(self._p), self.nbytes), "rspl_malloc")
+
+    @property
+    def ptr(self) -> int:
+        return self._p.value
+
+    def offset(self, nbytes: int) -> int:
+        return self._p.value + int(nbytes)
+
+    def upload(self, arr: _np.ndarray, stream=None, offset: int = 0):
+        a = _np.ascontiguousarray(arr)
+        assert offset + a.nbytes <= self.nbytes
+        check(load().rspl_memcpy_h2d(self._p.value + offset, a.ctypes.data, a.nbytes, stream), "rspl_memcpy_h2d")
+        return self
+
+    def download(self, shape, dtype, stream=None, offset: int = 0) -> _np.ndarray:
+        out = _np.empty(shape, dtype)
+        assert offset + out.nbytes <= self.nbytes
+        check(load().rspl_memcpy_d2h(out.ctypes.data, self._p.value + offset, out.nbytes, stream), "rspl_memcpy_d2h")
+        return out
+
+    def zero(self, stream=None):
+        check(load().rspl_memset(self._p.value, 0, self.nbytes, stream), "rspl_memset")
+
+    def __del__(self):
+        if self._p.value:
+            load().rspl_free(self._p)
+            self._p = C.c_void_p()
+
+
+class Stream:
+    def __init__(self):
+        self._s = C.c_void_p()
+        check(load().rspl_stream_create(C.byref(self._s)), "rspl_stream_create")
+
+    @property
+    def handle(self) -> int:
+        return self._s.value
+
+    def synchronize(self):
+        check(load().rspl_stream_synchronize(self._s), "rspl_stream_synchronize")
+
+    def __del__(self):
+        if self._s.value:
+            load().rspl_stream_destroy(self._s)
+            self._s = C.c_void_p()
+
+
+class Timer:
+    """HIP-event timer recorded on the stream the kernels run on."""
+
+    def __init__(self):
+        self._t = C.c_void_p()
+        check(load().rspl_timer_create(C.byref(self._t)), "rspl_timer_create")
+
+    def start(self, stream):
+        check(load().rspl_timer_record(self._t, 0, stream.handle if isinstance(stream, Stream) else stream), "timer")
+
+    def stop(self, stream):
+        check(load().rspl_timer_record(self._t, 1, stream.handle if isinstance(stream, Stream) else stream), "timer")
+
+    def elapsed_ms(self) -> float:
+        ms = C.c_float()
+        check(load().rspl_timer_elapsed_ms(self._t, C.byref(ms)), "rspl_timer_elapsed_ms")
+        return ms.value
+
+    def __del__(self):
+        if self._t.value:
+            load().rspl_timer_destroy(self._t)
+            self._t = C.c_void_p()
+
+
+def device_count() -> int:
+    n = C.c_int(0)
+    rc = load().rspl_device_count(C.byref(n))
+    return n.value if rc == RSPL_OK else 0
+
+
+def synchronize():
+    check(load().rspl_device_synchronize(), "rspl_device_synchronize")

@@ -1,0 +1,93 @@
+// Runtime helpers of the C ABI (include/rspl.h): device memory, streams,
+// HIP-event timers -- all on the system ROCm runtime librspl links against.
+#include "common.hpp"
+
+using namespace rspl;
+
+struct rspl_timer {
+  hipEvent_t ev[2] = {nullptr, nullptr};
+};
+
+extern "C" {
+
+int rspl_device_count(int* count) {
+  RSPL_CHECK_ARG(count, "NULL count");
+  RSPL_HIP(hipGetDeviceCount(count));
+  return RSPL_OK;
+}
+int rspl_set_device(int device) {
+  RSPL_HIP(hipSetDevice(device));
+  return RSPL_OK;
+}
+int rspl_malloc(void** ptr, size_t bytes) {
+  RSPL_CHECK_ARG(ptr, "NULL ptr");
+  RSPL_HIP(hipMalloc(ptr, bytes ? bytes : 1));
+  return RSPL_OK;
+}
+int rspl_free(void* ptr) {
+  RSPL_HIP(hipFree(ptr));
+  return RSPL_OK;
+}
+int rspl_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream) {
+  if (!bytes) return RSPL_OK;
+  RSPL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, (hipStream_t)stream));
+  RSPL_HIP(hipStreamSynchronize((hipStream_t)stream));
+  return RSPL_OK;
+}
+int rspl_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream) {
+  if (!bytes) return RSPL_OK;
+  RSPL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, (hipStream_t)stream));
+  RSPL_HIP(hipStreamSynchronize((hipStream_t)stream));
+  return RSPL_OK;
+}
+int rspl_memset(void* dst, int value, size_t bytes, void* stream) {
+  RSPL_HIP(hipMemsetAsync(dst, value, bytes, (hipStream_t)stream));
+  return RSPL_OK;
+}
+int rspl_stream_create(void** stream) {
+  RSPL_CHECK_ARG(stream, "NULL stream");
+  RSPL_HIP(hipStreamCreateWithFlags((hipStream_t*)stream, hipStreamNonBlocking));
+  return RSPL_OK;
+}
+int rspl_stream_destroy(void* stream) {
+  RSPL_HIP(hipStreamDestroy((hipStream_t)stream));
+  return RSPL_OK;
+}
+int rspl_stream_synchronize(void* stream) {
+  RSPL_HIP(hipStreamSynchronize((hipStream_t)stream));
+  return RSPL_OK;
+}
+int rspl_device_synchronize(void) {
+  RSPL_HIP(hipDeviceSynchronize());
+  return RSPL_OK;
+}
+int rspl_timer_create(rspl_timer** t) {
+  RSPL_CHECK_ARG(t, "NULL timer");
+  auto* x = new rspl_timer();
+  if (hipEventCreate(&x->ev[0]) != hipSuccess || hipEventCreate(&x->ev[1]) != hipSuccess) {
+    set_error("hipEventCreate failed");
+    delete x;
+    return RSPL_E_DEVICE;
+  }
+  *t = x;
+  return RSPL_OK;
+}
+int rspl_timer_record(rspl_timer* t, int which, void* stream) {
+  RSPL_CHECK_ARG(t && (which == 0 || which == 1), "bad timer / which");
+  RSPL_HIP(hipEventRecord(t->ev[which], (hipStream_t)stream));
+  return RSPL_OK;
+}
+int rspl_timer_elapsed_ms(rspl_timer* t, float* ms) {
+  RSPL_CHECK_ARG(t && ms, "bad timer");
+  RSPL_HIP(hipEventSynchronize(t->ev[1]));
+  RSPL_HIP(hipEventElapsedTime(ms, t->ev[0], t->ev[1]));
+  return RSPL_OK;
+}
+void rspl_timer_destroy(rspl_timer* t) {
+  if (!t) return;
+  for (auto& e : t->ev)
+    if (e) (void)hipEventDestroy(e);
+  delete t;
+}
+
+}  // extern "C"

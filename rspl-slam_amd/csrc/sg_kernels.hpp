@@ -1,0 +1,98 @@
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace rspl {
+namespace sg {
+
+// C[m][n] = epi(alpha * sum_k A[m][k] B[k][n] + bias[n]) for m < M, n < N, per batch z.
+//   A columns [0, ksplit) come from A, [ksplit, K) from A2 (both row stride lda).
+//   B is [K][N] (ldb) or, with b_nt, [N][K] (ldb).
+//   epi: 0 = none, 1 = ReLU, 2 = residual (C += result).
+//   mcount / ncount (device, may be null) override M / N per batch.
+struct GemmArgs {
+  const float* A;
+  const float* A2;
+  int lda, ksplit;
+  const float* B;
+  int ldb, b_nt;
+  const float* bias;
+  float* C;
+  int ldc;
+  int M, N, K;
+  float alpha;
+  int epi;
+  long long sA, sB, sC;
+  const int* mcount;
+  const int* ncount;
+  int count_stride;  // ints between consecutive batches in mcount/ncount
+};
+
+struct PrepArgs {
+  const double* f0;   // [B][stride][259]
+  const double* f1;
+  const int* n0;      // device counts [B]
+  const int* n1;
+  int stride;         // features per batch entry
+  int normalize;      // apply PointMatching::NormalizeKeypoints
+  int width, height;
+  int nmax;
+  float* kin;         // [B][2][nmax][16] keypoint-encoder input (x, y, score, 0...)
+  float* X;           // [B][2][nmax][256] descriptors
+  int B;
+};
+
+struct AttnArgs {
+  const float* qkv;   // [B][2][nmax][768] = Q | K | V, head-contiguous channels
+  float* O;           // [B][2][nmax][256]
+  const int* n0;
+  const int* n1;
+  int nmax;
+  int cross;          // 0: self (source = same image), 1: cross
+};
+
+struct BinsArgs {
+  float* cpl;         // [B][(nmax+1)^2], row stride nmax+1
+  const int* n0;
+  const int* n1;
+  const float* alpha; // bin_score (device scalar)
+  int nmax;
+};
+
+struct SinkArgs {
+  const float* cpl;   // couplings [B][ld*ld]
+  float* Z;           // [B][ld*ld]
+  float* part;        // [B][2][G][ld] column partial LSEs
+  unsigned* ctr;      // [B] arrival counters (zeroed per call)
+  unsigned* err;      // [B] timeout flags
+  const int* n0;
+  const int* n1;
+  int nmax, G, iters;
+};
+
+struct DecodeArgs {
+  const float* Z;     // [B][ld*ld]
+  const int* n0;
+  const int* n1;
+  int nmax;
+  int* max0;          // [B][nmax]
+  float* val0;
+  int* max1;
+  int32_t* idx0;      // [B][nmax]
+  int32_t* idx1;
+  double* ms0;
+  double* ms1;
+  float threshold;
+};
+
+hipError_t gemm(const GemmArgs& a, int batch, hipStream_t s);
+hipError_t prep(const PrepArgs& a, hipStream_t s);
+hipError_t attention(const AttnArgs& a, int B, hipStream_t s);
+hipError_t bins(const BinsArgs& a, int B, hipStream_t s);
+hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s);
+hipError_t decode(const DecodeArgs& a, int B, hipStream_t s);
+size_t sinkhorn_lds_bytes(int nmax, int G);
+
+}  // namespace sg
+}  // namespace rspl

@@ -1,0 +1,563 @@
+// SuperPoint forward + post-processing on gfx950 (CDNA4), fp32 MFMA path.
+//
+// Reference semantics:
+//   network  convert2onnx/superpoint.py:114-161  (encoder, detector & descriptor heads)
+//   NMS      convert2onnx/superpoint.py:16-33    (simple_nms, radius 4)
+//   host     src/super_point.cpp:207-389         (u8/255, threshold, borders, top-k,
+//                                                 bilinear sampling in double, packing)
+// Layout: activations NHWC fp32 (channels contiguous), one batch of B images.
+// Convolutions are implicit GEMMs (M = pixels, N = output channels, K = 9*Cin)
+// on v_mfma_f32_32x32x2_f32 (exact fp32: one rounding per product, like fmaf).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "sp_kernels.hpp"
+
+namespace rspl {
+namespace sp {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------
+// 3x3 conv, pad 1, bias + ReLU (+ 2x2 max-pool) as an implicit GEMM.
+//   block  = 4 waves; tile = TH rows x 16 cols of output pixels x 64 channels
+//   wave   = TH/4 rows (TH/8 M-tiles of 2 rows x 16 cols) x 2 N-tiles of 32 ch
+//   K loop = Cin in chunks of CK=16, staged in LDS with the 1-pixel halo;
+//            weights staged as [9][CK][64].
+// FUSE1A: the input tile is conv1a(relu) computed on the fly from the u8
+// image (src/super_point.cpp:216-220 normalisation via LUT), so the 64-channel
+// full-resolution conv1a map never touches HBM.
+// ---------------------------------------------------------------------------
+constexpr int CK = 16;
+constexpr int CKP = CK + 1;  // LDS pixel stride (odd: conflict-free A reads)
+constexpr int TW = 16;
+
+template <int CIN, int TH, bool POOL, bool FUSE1A>
+__global__ __launch_bounds__(256) void conv3x3_kernel(ConvArgs a) {
+  static_assert(CIN % CK == 0, "Cin must be a multiple of 16");
+  constexpr int HX = TW + 2, HY = TH + 2;
+  constexpr int MT = TH / 8;  // M-tiles per wave
+  __shared__ float halo[HY * HX * CKP];
+  __shared__ float wts[9 * CK * 64];
+  __shared__ float patch[FUSE1A ? (TH + 4) * (TW + 4) : 1];
+  __shared__ float w1a[FUSE1A ? 64 * 10 : 1];
+
+  const int H = a.H, W = a.W, COUT = a.cout;
+  const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
+  const int per_img = tiles_x * tiles_y;
+  const int bi = blockIdx.x / per_img;
+  const int t = blockIdx.x % per_img;
+  const int y0 = (t / tiles_x) * TH, x0 = (t % tiles_x) * TW;
+  const int co0 = blockIdx.y * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ml = lane & 31, kl = lane >> 5;
+
+  if constexpr (FUSE1A) {
+    // image patch (TH+4) x (TW+4), rows y0-2.., cols x0-2.., zero outside (conv1a padding)
+    const uint8_t* img = a.img + (size_t)bi * a.img_pitch;
+    for (int i = tid; i < (TH + 4) * (TW + 4); i += 256) {
+      const int py = i / (TW + 4), px = i % (TW + 4);
+      const int y = y0 - 2 + py, x = x0 - 2 + px;
+      patch[i] = (y >= 0 && y < H && x >= 0 && x < W) ? a.lut[img[(size_t)y * a.img_stride + x]] : 0.f;
+    }
+    for (int i = tid; i < 64 * 10; i += 256) w1a[i] = (i % 10 < 9) ? a.w1a[(i / 10) * 9 + i % 10] : a.b1a[i / 10];
+  }
+
+  floatx16 acc[MT][2];
+#pragma unroll
+  for (int m = 0; m < MT; m++)
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc[m][n][r] = 0.f;
+
+  for (int c0 = 0; c0 < CIN; c0 += CK) {
+    __syncthreads();
+    // ---- stage input halo (chunk c0..c0+CK) ----
+    if constexpr (FUSE1A) {
+      for (int i = tid; i < HY * HX * CK; i += 256) {
+        const int c = i % CK, pix = i / CK;
+        const int hy = pix / HX, hx = pix % HX;
+        const int y = y0 - 1 + hy, x = x0 - 1 + hx;
+        float v = 0.f;
+        if (y >= 0 && y < H && x >= 0 && x < W) {
+          const float* wc = &w1a[(c0 + c) * 10];
+          float s = wc[9];
+#pragma unroll
+          for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+            for (int kx = 0; kx < 3; kx++) s += wc[ky * 3 + kx] * patch[(hy + ky) * (TW + 4) + hx + kx];
+          v = s > 0.f ? s : 0.f;
+        }
+        halo[pix * CKP + c] = v;
+      }
+    } else {
+      const float* in = a.in + (size_t)bi * H * W * CIN;
+      for (int i = tid; i < HY * HX * (CK / 4); i += 256) {
+        const int q = i % (CK / 4), pix = i / (CK / 4);
+        const int hy = pix / HX, hx = pix % HX;
+        const int y = y0 - 1 + hy, x = x0 - 1 + hx;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (y >= 0 && y < H && x >= 0 && x < W)
+          v = *reinterpret_cast<const float4*>(in + ((size_t)y * W + x) * CIN + c0 + 4 * q);
+        float* d = &halo[pix * CKP + 4 * q];
+        d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+      }
+    }
+    // ---- stage weights [9][CK][64] ----
+    for (int i = tid; i < 9 * CK * 16; i += 256) {
+      const int n4 = i % 16, r = i / 16;  // r = kk*CK + ci
+      const int kk = r / CK, ci = r % CK;
+      const float4 v = *reinterpret_cast<const float4*>(a.w + ((size_t)(kk * CIN + c0 + ci)) * COUT + co0 + 4 * n4);
+      *reinterpret_cast<float4*>(&wts[r * 64 + 4 * n4]) = v;
+    }
+    __syncthreads();
+    // ---- MFMA over this chunk ----
+#pragma unroll
+    for (int kk = 0; kk < 9; kk++) {
+      const int ky = kk / 3, kx = kk % 3;
+#pragma unroll
+      for (int kc = 0; kc < CK; kc += 2) {
+        float av[MT], bv[2];
+#pragma unroll
+        for (int m = 0; m < MT; m++) {
+          const int ly = wv * (TH / 4) + 2 * m + (ml >> 4);
+          av[m] = halo[((ly + ky) * HX + (ml & 15) + kx) * CKP + kc + kl];
+        }
+#pragma unroll
+        for (int n = 0; n < 2; n++) bv[n] = wts[(kk * CK + kc + kl) * 64 + n * 32 + ml];
+#pragma unroll
+        for (int m = 0; m < MT; m++)
+#pragma unroll
+          for (int n = 0; n < 2; n++) acc[m][n] = mfma32(av[m], bv[n], acc[m][n]);
+      }
+    }
+  }
+
+  // ---- epilogue: bias + ReLU (+ pool), NHWC store ----
+#pragma unroll
+  for (int n = 0; n < 2; n++) {
+    const int co = co0 + n * 32 + ml;
+    const float bias = a.bias[co];
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
+      const int ly = wv * (TH / 4) + 2 * m;  // first of the M-tile's two rows
+      if constexpr (POOL) {
+        const int H2 = H / 2, W2 = W / 2;
+        float* out = a.out + (size_t)bi * H2 * W2 * COUT;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+          const int r0 = (g & 1) * 2 + (g >> 1) * 4;
+          const int pc = (r0 & 3) + 8 * ((r0 >> 2) & 1) + 4 * kl;
+          float v = fmaxf(fmaxf(acc[m][n][r0], acc[m][n][r0 + 1]), fmaxf(acc[m][n][r0 + 8], acc[m][n][r0 + 9]));
+          v += bias;
+          v = v > 0.f ? v : 0.f;
+          const int py = (y0 + ly) >> 1, px = (x0 + pc) >> 1;
+          if (py < H2 && px < W2) out[((size_t)py * W2 + px) * COUT + co] = v;
+        }
+      } else {
+        float* out = a.out + (size_t)bi * H * W * COUT;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int mm = (r & 3) + 8 * (r >> 2) + 4 * kl;
+          const int y = y0 + ly + (mm >> 4), x = x0 + (mm & 15);
+          float v = acc[m][n][r] + bias;
+          v = v > 0.f ? v : 0.f;
+          if (y < H && x < W) out[((size_t)y * W + x) * COUT + co] = v;
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// 1x1 heads on the H/8 x W/8 cell grid.  in = [P][512] (convPa | convDa, ReLU'd).
+//   MODE 0: convPb 256->65, softmax over 65, drop dustbin, depth-to-space ->
+//           scores [H][W]  (superpoint.py:131-135)
+//   MODE 1: convDb 256->256, per-cell L2 normalise -> desc [P][256]
+//           (superpoint.py:160-161)
+// One wave owns 32 cells; block = 4 waves = 128 cells.  K = 256 staged in LDS
+// in chunks of 32.  Weights pre-transposed to [256][NPAD] (NPAD = 96 / 256).
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
+  constexpr int NT = MODE == 0 ? 3 : 8;  // N-tiles of 32
+  constexpr int NP = NT * 32;
+  constexpr int KC = 32;
+  __shared__ float As[KC][128 + 1];
+  __shared__ float Bs[KC][NP];
+  const int P = a.P;  // cells per image
+  const int cell0 = blockIdx.x * 128;  // flattened over batch
+  const int total = a.B * P;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, ml = lane & 31, kl = lane >> 5;
+  const int in_off = MODE == 0 ? 0 : 256;
+
+  floatx16 acc[NT];
+#pragma unroll
+  for (int n = 0; n < NT; n++)
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[n][r] = 0.f;
+
+  for (int k0 = 0; k0 < 256; k0 += KC) {
+    __syncthreads();
+    for (int i = tid; i < 128 * (KC / 4); i += 256) {
+      const int q = i % (KC / 4), c = i / (KC / 4);
+      const int cell = cell0 + c;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (cell < total) v = *reinterpret_cast<const float4*>(a.in + (size_t)cell * 512 + in_off + k0 + 4 * q);
+      As[4 * q + 0][c] = v.x; As[4 * q + 1][c] = v.y; As[4 * q + 2][c] = v.z; As[4 * q + 3][c] = v.w;
+    }
+    for (int i = tid; i < KC * (NP / 4); i += 256) {
+      const int q = i % (NP / 4), k = i / (NP / 4);
+      *reinterpret_cast<float4*>(&Bs[k][4 * q]) = *reinterpret_cast<const float4*>(a.w + (size_t)(k0 + k) * NP + 4 * q);
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int kc = 0; kc < KC; kc += 2) {
+      const float av = As[kc + kl][wv * 32 + ml];
+#pragma unroll
+      for (int n = 0; n < NT; n++) acc[n] = mfma32(av, Bs[kc + kl][n * 32 + ml], acc[n]);
+    }
+  }
+
+  // epilogue: rows (cells) on registers, channels on lanes (col = ml within N-tile)
+#pragma unroll
+  for (int n = 0; n < NT; n++) {
+    const float b = a.bias[n * 32 + ml];
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[n][r] += b;
+  }
+  if constexpr (MODE == 0) {
+    // channels >= 65 are padding: exclude from the softmax
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      float m = -INFINITY;
+#pragma unroll
+      for (int n = 0; n < NT; n++) {
+        const int c = n * 32 + ml;
+        if (c < 65) m = fmaxf(m, acc[n][r]);
+      }
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 32));
+      float e[NT];
+      float s = 0.f;
+#pragma unroll
+      for (int n = 0; n < NT; n++) {
+        const int c = n * 32 + ml;
+        e[n] = (c < 65) ? expf(acc[n][r] - m) : 0.f;
+        s += e[n];
+      }
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) s += __shfl_xor(s, o, 32);
+      const int cell = cell0 + wv * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+      if (cell < total) {
+        const int bi = cell / P, p = cell % P;
+        const int cy = p / a.W8, cx = p % a.W8;
+        float* sc = a.scores + (size_t)bi * P * 64;
+        const int Wf = a.W8 * 8;
+#pragma unroll
+        for (int n = 0; n < 2; n++) {  // channels 0..63 live in N-tiles 0,1
+          const int c = n * 32 + ml;
+          sc[(size_t)(cy * 8 + (c >> 3)) * Wf + cx * 8 + (c & 7)] = e[n] / s;
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      float s = 0.f;
+#pragma unroll
+      for (int n = 0; n < NT; n++) s += acc[n][r] * acc[n][r];
+#pragma unroll
+      for (int o = 16; o >= 1; o >>= 1) s += __shfl_xor(s, o, 32);
+      float nrm = sqrtf(s);
+      nrm = nrm < 1e-12f ? 1e-12f : nrm;
+      const int cell = cell0 + wv * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+      if (cell < total) {
+#pragma unroll
+        for (int n = 0; n < NT; n++) a.desc[(size_t)cell * 256 + n * 32 + ml] = acc[n][r] / nrm;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Fused simple_nms (5 x 9x9 max-pools) + threshold / border candidate
+// extraction.  Tile 32x32 outputs, halo 20, separable LDS max.  Scores are
+// softmax outputs (>= 0) and every window contains its centre, so zero padding
+// outside the image equals MaxPool2d's -inf padding here.
+// ---------------------------------------------------------------------------
+constexpr int NT_ = 32, NH = 20, NR = NT_ + 2 * NH;  // 72
+
+// dst[y][x] = max_{|k|<=4} src[y][x+k]  over the rectangle [y0,y1) x [x0,x1)
+__device__ __forceinline__ void rowpass(const float* src, float* dst, int y0, int y1, int x0, int x1) {
+  const int w = x1 - x0, n = (y1 - y0) * w;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int y = y0 + i / w, x = x0 + i % w;
+    const float* s = src + y * NR + x - 4;
+    float m = s[0];
+#pragma unroll
+    for (int k = 1; k < 9; k++) m = fmaxf(m, s[k]);
+    dst[y * NR + x] = m;
+  }
+}
+// dst[y][x] = max_{|k|<=4} src[y+k][x]
+__device__ __forceinline__ void colpass(const float* src, float* dst, int y0, int y1, int x0, int x1) {
+  const int w = x1 - x0, n = (y1 - y0) * w;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int y = y0 + i / w, x = x0 + i % w;
+    const float* s = src + (y - 4) * NR + x;
+    float m = s[0];
+#pragma unroll
+    for (int k = 1; k < 9; k++) m = fmaxf(m, s[k * NR]);
+    dst[y * NR + x] = m;
+  }
+}
+
+__global__ __launch_bounds__(256) void nms_kernel(NmsArgs a) {
+  __shared__ float S[NR * NR];          // scores (0 outside the image)
+  __shared__ float T[NR * NR];          // row-pass scratch
+  __shared__ float M[NR * NR];          // max-pool result / supp flag
+  __shared__ float F[NR * NR];          // mask as float / supp_scores
+  __shared__ unsigned char K[NR * NR];  // max_mask
+  const int H = a.H, W = a.W;
+  const int tiles_x = (W + NT_ - 1) / NT_, tiles_y = (H + NT_ - 1) / NT_;
+  const int per = tiles_x * tiles_y;
+  const int bi = blockIdx.x / per, t = blockIdx.x % per;
+  const int y0 = (t / tiles_x) * NT_ - NH, x0 = (t % tiles_x) * NT_ - NH;
+  const float* sc = a.scores + (size_t)bi * H * W;
+  for (int i = threadIdx.x; i < NR * NR; i += blockDim.x) {
+    const int y = y0 + i / NR, x = x0 + i % NR;
+    S[i] = (y >= 0 && y < H && x >= 0 && x < W) ? sc[(size_t)y * W + x] : 0.f;
+  }
+  __syncthreads();
+  // max_mask = scores == max_pool(scores), valid on [4, NR-4)^2
+  rowpass(S, T, 0, NR, 4, NR - 4);
+  __syncthreads();
+  colpass(T, M, 4, NR - 4, 4, NR - 4);
+  __syncthreads();
+  for (int i = threadIdx.x; i < NR * NR; i += blockDim.x) {
+    const int y = i / NR, x = i % NR;
+    K[i] = (y >= 4 && y < NR - 4 && x >= 4 && x < NR - 4) ? (S[i] == M[i]) : 0;
+  }
+  __syncthreads();
+  for (int it = 0; it < 2; it++) {
+    const int lo = 4 + 8 * it;  // K valid on [lo, NR-lo)^2
+    const int l1 = lo + 4, l2 = lo + 8;
+    for (int i = threadIdx.x; i < NR * NR; i += blockDim.x) F[i] = K[i] ? 1.f : 0.f;
+    __syncthreads();
+    // supp_mask = max_pool(max_mask) > 0, valid on [l1, NR-l1)^2
+    rowpass(F, T, lo, NR - lo, l1, NR - l1);
+    __syncthreads();
+    colpass(T, M, l1, NR - l1, l1, NR - l1);
+    __syncthreads();
+    // supp_scores = where(supp_mask, 0, scores)
+    for (int i = threadIdx.x; i < NR * NR; i += blockDim.x) {
+      const int y = i / NR, x = i % NR;
+      if (y >= l1 && y < NR - l1 && x >= l1 && x < NR - l1) {
+        const bool supp = M[i] > 0.f;
+        M[i] = supp ? 1.f : 0.f;
+        F[i] = supp ? 0.f : S[i];
+      }
+    }
+    __syncthreads();
+    // new_max_mask = supp_scores == max_pool(supp_scores), valid on [l2, NR-l2)^2
+    rowpass(F, T, l1, NR - l1, l2, NR - l2);
+    __syncthreads();
+    for (int i = threadIdx.x; i < NR * NR; i += blockDim.x) {
+      const int y = i / NR, x = i % NR;
+      if (y >= l2 && y < NR - l2 && x >= l2 && x < NR - l2) {
+        const float* s = T + (y - 4) * NR + x;
+        float m = s[0];
+#pragma unroll
+        for (int k = 1; k < 9; k++) m = fmaxf(m, s[k * NR]);
+        // max_mask | (new_max_mask & ~supp_mask)
+        K[i] = K[i] | ((F[i] == m) && !(M[i] > 0.f));
+      } else {
+        K[i] = 0;
+      }
+    }
+    __syncthreads();
+  }
+  // output region [NH, NH+NT_)^2: NMS'd map + candidates
+  for (int i = threadIdx.x; i < NT_ * NT_; i += blockDim.x) {
+    const int ly = NH + i / NT_, lx = NH + i % NT_;
+    const int y = y0 + ly, x = x0 + lx;
+    if (y >= H || x >= W) continue;
+    const float v = K[ly * NR + lx] ? S[ly * NR + lx] : 0.f;
+    if (a.nms_out) a.nms_out[(size_t)bi * H * W + (size_t)y * W + x] = v;
+    // find_high_score_index: float score > double threshold (src/super_point.cpp:228);
+    // remove_borders: border <= y < H-border, border <= x < W-border (:244-245)
+    if ((double)v > a.threshold && y >= a.border && y < H - a.border && x >= a.border && x < W - a.border) {
+      const int slot = atomicAdd(&a.cand_count[bi], 1);
+      if (slot < a.cand_cap) {
+        const unsigned long long key =
+            ((unsigned long long)(0xFFFFFFFFu - __float_as_uint(v)) << 32) | (unsigned)(y * W + x);
+        a.cand[(size_t)bi * a.cand_cap + slot] = key;
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Top-k selection: one workgroup per image, bitonic sort in LDS.
+// Key = (~score_bits << 32) | flat_index: ascending key order = score desc,
+// then flat index asc (documented tie-break for the reference's non-stable
+// std::sort, src/super_point.cpp:255-260).  If n <= k the reference does not
+// sort: keypoints stay in row-major scan order (flat index asc).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(1024) void topk_kernel(TopkArgs a) {
+  extern __shared__ unsigned long long keys[];
+  const int bi = blockIdx.x;
+  int n = a.cand_count[bi];
+  if (n > a.cand_cap) n = a.cand_cap;
+  const bool sorted_by_score = (a.k != -1 && a.k < n);
+  int L = 1;
+  while (L < n) L <<= 1;
+  const unsigned long long* src = a.cand + (size_t)bi * a.cand_cap;
+  for (int i = threadIdx.x; i < L; i += blockDim.x) {
+    unsigned long long key = ~0ull;
+    if (i < n) {
+      key = src[i];
+      if (!sorted_by_score) key &= 0xFFFFFFFFull;  // flat index only
+    }
+    keys[i] = key;
+  }
+  __syncthreads();
+  for (int size = 2; size <= L; size <<= 1) {
+    for (int stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int i = threadIdx.x; i < L / 2; i += blockDim.x) {
+        const int lo = 2 * i - (i & (stride - 1));
+        const int hi = lo + stride;
+        const bool up = ((lo & size) == 0);
+        const unsigned long long x = keys[lo], y = keys[hi];
+        if ((x > y) == up) {
+          keys[lo] = y;
+          keys[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  const int kout = sorted_by_score ? a.k : n;
+  for (int i = threadIdx.x; i < kout; i += blockDim.x) a.sel[(size_t)bi * a.sel_cap + i] = (unsigned)(keys[i] & 0xFFFFFFFFull);
+  if (threadIdx.x == 0) a.sel_count[bi] = kout;
+}
+
+// ---------------------------------------------------------------------------
+// Descriptor sampling + packing (src/super_point.cpp:276-387), fp64.
+// One wave per keypoint, 4 channels per lane.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void sample_kernel(SampleArgs a) {
+  const int wv = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const int lane = threadIdx.x & 63;
+  const int bi = wv / a.per_image, i = wv % a.per_image;
+  if (bi >= a.B) return;
+  const int n = a.sel_count[bi];
+  if (lane == 0 && i == 0) a.counts[bi] = n;
+  if (i >= n) return;
+  const int H = a.H, W = a.W, h = H / 8, w = W / 8;
+  const unsigned flat = a.sel[(size_t)bi * a.sel_stride + i];
+  const int y = flat / W, x = flat % W;
+  const float score = a.nms[(size_t)bi * H * W + flat];
+  // normalize_keypoints (:276-287): s/2 is integer division
+  const double gx = ((double)x - 8 / 2 + 0.5) / (w * 8 - 8 / 2 - 0.5) * 2 - 1;
+  const double gy = ((double)y - 8 / 2 + 0.5) / (h * 8 - 8 / 2 - 0.5) * 2 - 1;
+  // grid_sample (:294-332), align_corners=True
+  const double ix = ((gx + 1) / 2) * (w - 1), iy = ((gy + 1) / 2) * (h - 1);
+  auto clip = [](int v, int m) { return v < 0 ? 0 : (v < m - 1 ? v : m - 1); };
+  const int ix_nw = clip((int)floor(ix), w), iy_nw = clip((int)floor(iy), h);
+  const int ix_ne = clip(ix_nw + 1, w), iy_ne = clip(iy_nw, h);
+  const int ix_sw = clip(ix_nw, w), iy_sw = clip(iy_nw + 1, h);
+  const int ix_se = clip(ix_nw + 1, w), iy_se = clip(iy_nw + 1, h);
+  const double nw = (ix_se - ix) * (iy_se - iy);
+  const double ne = (ix - ix_sw) * (iy_sw - iy);
+  const double sw = (ix_ne - ix) * (iy - iy_ne);
+  const double se = (ix - ix_nw) * (iy - iy_nw);
+  const float* d = a.desc + (size_t)bi * h * w * 256;
+  const float4 vnw = *reinterpret_cast<const float4*>(d + ((size_t)iy_nw * w + ix_nw) * 256 + 4 * lane);
+  const float4 vne = *reinterpret_cast<const float4*>(d + ((size_t)iy_ne * w + ix_ne) * 256 + 4 * lane);
+  const float4 vsw = *reinterpret_cast<const float4*>(d + ((size_t)iy_sw * w + ix_sw) * 256 + 4 * lane);
+  const float4 vse = *reinterpret_cast<const float4*>(d + ((size_t)iy_se * w + ix_se) * 256 + 4 * lane);
+  double v[4];
+  v[0] = (double)vnw.x * nw + (double)vne.x * ne + (double)vsw.x * sw + (double)vse.x * se;
+  v[1] = (double)vnw.y * nw + (double)vne.y * ne + (double)vsw.y * sw + (double)vse.y * se;
+  v[2] = (double)vnw.z * nw + (double)vne.z * ne + (double)vsw.z * sw + (double)vse.z * se;
+  v[3] = (double)vnw.w * nw + (double)vne.w * ne + (double)vsw.w * sw + (double)vse.w * se;
+  double ss = v[0] * v[0] + v[1] * v[1] + v[2] * v[2] + v[3] * v[3];
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) ss += __shfl_xor(ss, o, 64);
+  const double inv = 1.0 / sqrt(ss);
+  double* f = a.features + ((size_t)bi * a.feat_cap + i) * 259;
+  if (lane == 0) {
+    f[0] = (double)score;
+    f[1] = (double)x;
+    f[2] = (double)y;
+  }
+#pragma unroll
+  for (int j = 0; j < 4; j++) f[3 + 4 * lane + j] = inv * v[j];
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+template <int CIN, int TH, bool POOL, bool FUSE1A>
+static hipError_t launch_conv(const ConvArgs& a, int B, hipStream_t s) {
+  const int tiles = ((a.W + TW - 1) / TW) * ((a.H + TH - 1) / TH);
+  dim3 grid(B * tiles, a.cout / 64);
+  hipLaunchKernelGGL((conv3x3_kernel<CIN, TH, POOL, FUSE1A>), grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hipStream_t s) {
+  const bool small = (a.H * a.W) <= 128 * 192;  // more, smaller tiles for the low-res layers
+  if (fuse1a) return launch_conv<64, 16, true, true>(a, B, s);
+  if (cin == 64 && pool) return launch_conv<64, 16, true, false>(a, B, s);
+  if (cin == 64 && !pool) return small ? launch_conv<64, 8, false, false>(a, B, s) : launch_conv<64, 16, false, false>(a, B, s);
+  if (cin == 128 && pool) return launch_conv<128, 16, true, false>(a, B, s);
+  if (cin == 128 && !pool) return small ? launch_conv<128, 8, false, false>(a, B, s) : launch_conv<128, 16, false, false>(a, B, s);
+  return hipErrorInvalidValue;
+}
+
+hipError_t heads(const HeadArgs& a, int mode, hipStream_t s) {
+  const int blocks = (a.B * a.P + 127) / 128;
+  if (mode == 0)
+    hipLaunchKernelGGL(head_kernel<0>, dim3(blocks), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL(head_kernel<1>, dim3(blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t nms(const NmsArgs& a, int B, hipStream_t s) {
+  const int tiles = ((a.W + NT_ - 1) / NT_) * ((a.H + NT_ - 1) / NT_);
+  hipLaunchKernelGGL(nms_kernel, dim3(B * tiles), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t topk(const TopkArgs& a, int B, hipStream_t s) {
+  int L = 1;
+  while (L < a.cand_cap) L <<= 1;
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute((const void*)topk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)(L * sizeof(unsigned long long)));
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(topk_kernel, dim3(B), dim3(1024), L * sizeof(unsigned long long), s, a);
+  return hipGetLastError();
+}
+
+hipError_t sample(const SampleArgs& a, hipStream_t s) {
+  const int waves = a.B * a.per_image;
+  hipLaunchKernelGGL(sample_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace sp
+}  // namespace rspl

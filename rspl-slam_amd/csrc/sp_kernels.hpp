@@ -1,0 +1,74 @@
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace rspl {
+namespace sp {
+
+struct ConvArgs {
+  const float* in;       // NHWC [B][H][W][Cin] (unused when fused with conv1a)
+  const float* w;        // [9][Cin][Cout]
+  const float* bias;     // [Cout]
+  float* out;            // NHWC [B][H(/2)][W(/2)][Cout]
+  int H, W, cout;
+  // conv1a fusion (conv1b only)
+  const uint8_t* img;    // u8 images, row stride img_stride, image pitch img_pitch
+  int img_stride;
+  size_t img_pitch;
+  const float* lut;      // [256] (float)(u / 255.0)
+  const float* w1a;      // [64][9]
+  const float* b1a;      // [64]
+};
+
+struct HeadArgs {
+  const float* in;       // [B*P][512] (convPa | convDa)
+  const float* w;        // [256][NPAD]
+  const float* bias;     // [NPAD]
+  float* scores;         // mode 0: [B][H][W]
+  float* desc;           // mode 1: [B*P][256]
+  int B, P, W8;
+};
+
+struct NmsArgs {
+  const float* scores;   // [B][H][W]
+  float* nms_out;        // [B][H][W]
+  unsigned long long* cand;  // [B][cand_cap]
+  int* cand_count;       // [B]
+  int cand_cap;
+  int H, W;
+  double threshold;
+  int border;
+};
+
+struct TopkArgs {
+  const unsigned long long* cand;
+  const int* cand_count;
+  int cand_cap;
+  int k;                 // -1 = keep all
+  unsigned* sel;         // [B][sel_cap] flat indices
+  int* sel_count;        // [B]
+  int sel_cap;
+};
+
+struct SampleArgs {
+  const unsigned* sel;
+  const int* sel_count;
+  int sel_stride;        // row stride of sel
+  int per_image;         // waves launched per image (>= max selected)
+  const float* nms;      // [B][H][W]
+  const float* desc;     // [B][H/8][W/8][256]
+  double* features;      // [B][feat_cap][259]
+  int feat_cap;
+  int32_t* counts;       // [B]
+  int B, H, W;
+};
+
+hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hipStream_t s);
+hipError_t heads(const HeadArgs& a, int mode, hipStream_t s);
+hipError_t nms(const NmsArgs& a, int B, hipStream_t s);
+hipError_t topk(const TopkArgs& a, int B, hipStream_t s);
+hipError_t sample(const SampleArgs& a, hipStream_t s);
+
+}  // namespace sp
+}  // namespace rspl

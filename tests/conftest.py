@@ -10,7 +10,13 @@ sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "oracle"))
 import rspl_loader  # noqa: E402
 
-rspl_loader.load()
+pkg = rspl_loader.load()
+# Load librspl.so (system ROCm HIP runtime) before anything can pull in torch's
+# bundled runtime: one HIP runtime per process.
+try:
+    pkg.capi.load()
+except pkg.capi.RsplError:
+    pass
 GOLDEN = ROOT / "tests" / "golden"
 
 

@@ -2,7 +2,7 @@
 import numpy as np
 
 
-def compare_features(F, G, score_atol=1e-5, desc_atol=1e-5, desc_rtol=1e-3):
+def compare_features(F, G, score_atol=1e-5, desc_atol=1e-5, desc_rtol=1e-3, order_atol=None):
     """Compare two 259 x n feature matrices of the same image.
 
     Keypoint SET must be identical; columns are matched by (x, y).  Column order must agree except
@@ -19,6 +19,7 @@ def compare_features(F, G, score_atol=1e-5, desc_atol=1e-5, desc_rtol=1e-3):
     Gp = G[:, perm]
     np.testing.assert_allclose(F[0], Gp[0], atol=score_atol, rtol=0)
     np.testing.assert_allclose(F[3:], Gp[3:], atol=desc_atol, rtol=desc_rtol)
+    order_atol = score_atol if order_atol is None else order_atol
     moved = np.nonzero(perm != np.arange(len(perm)))[0]
     for i in moved:
-        assert abs(G[0, i] - G[0, perm[i]]) < score_atol, f"order differs beyond score tolerance at column {i}"
+        assert abs(G[0, i] - G[0, perm[i]]) < order_atol, f"order differs beyond score tolerance at column {i}"

@@ -1,0 +1,104 @@
+"""GPU parity: SuperPoint through the C ABI vs the reference outputs (golden) and the oracle."""
+import numpy as np
+import pytest
+
+import oracle
+import post
+from helpers import compare_features
+
+pytestmark = pytest.mark.gpu
+
+
+def _sp(pkg, w, k, H, W, B=1, thr=0.004, border=4):
+    sp = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=k, keypoint_threshold=thr, remove_borders=border,
+                                             weights=w, max_height=H, max_width=W, max_batch=B))
+    assert sp.build(), sp.error
+    return sp
+
+
+@pytest.fixture(scope="module")
+def pkg():
+    import rspl_loader
+    return rspl_loader.load()
+
+
+def test_sp_small_maps_and_features(pkg, golden, weight_blobs):
+    g = golden("sp_small")
+    sp = _sp(pkg, weight_blobs[0], 32, 64, 96)
+    ok, F = sp.infer(g["image"])
+    assert ok, sp.error
+    s, d = sp.debug_maps(0, 64, 96)
+    np.testing.assert_allclose(d, g["desc"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(s, g["scores"], rtol=1e-3, atol=1e-5)
+    compare_features(F, g["features"])
+
+
+def test_sp_euroc_vs_reference(pkg, golden, weight_blobs):
+    g = golden("sp_euroc")
+    sp = _sp(pkg, weight_blobs[0], 400, 480, 752)
+    ok, F = sp.infer(g["image"])
+    assert ok, sp.error
+    s, d = sp.debug_maps(0, 480, 752)
+    nz = np.nonzero(s.reshape(-1))[0]
+    np.testing.assert_array_equal(nz, g["nms_idx"])
+    np.testing.assert_allclose(s.reshape(-1)[nz], g["nms_val"], rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(d.reshape(-1)[g["desc_sample_idx"]], g["desc_sample_val"], rtol=1e-3, atol=1e-5)
+    G = np.concatenate([g["feat_head"], g["feat_desc"].astype(np.float64)])
+    compare_features(F, G)
+
+
+def test_sp_keep_all_and_empty(pkg, weight_blobs):
+    from rspl_slam_amd import synthetic as SY
+    img = SY.textured_image(96, 128, seed=11, n_blobs=10)
+    s, d = oracle.sp_forward(weight_blobs[0], post.image_to_input(img))
+    # k = -1: no sort, keypoints in row-major scan order (src/super_point.cpp:263)
+    sp = _sp(pkg, weight_blobs[0], -1, 96, 128)
+    ok, F = sp.infer(img)
+    assert ok, sp.error
+    G = post.sp_postprocess(s, d, 0.004, 4, -1)
+    compare_features(F, G, order_atol=0.0)   # order is exact (flat index)
+    # threshold above every score: zero keypoints
+    sp = _sp(pkg, weight_blobs[0], 400, 96, 128, thr=0.99)
+    ok, F = sp.infer(img)
+    assert ok and F.shape == (259, 0)
+    # k larger than the candidate count: all candidates, scan order
+    sp = _sp(pkg, weight_blobs[0], 5000, 96, 128)
+    ok, F = sp.infer(img)
+    compare_features(F, post.sp_postprocess(s, d, 0.004, 4, 5000), order_atol=0.0)
+
+
+def test_sp_large_border_and_flat_image(pkg, weight_blobs):
+    img = np.full((64, 64), 128, np.uint8)     # flat image: plateau scores, NMS ties
+    s, d = oracle.sp_forward(weight_blobs[0], post.image_to_input(img))
+    sp = _sp(pkg, weight_blobs[0], 50, 64, 64, border=12)
+    ok, F = sp.infer(img)
+    assert ok, sp.error
+    compare_features(F, post.sp_postprocess(s, d, 0.004, 12, 50))
+
+
+def test_sp_rejects_bad_shapes(pkg, weight_blobs):
+    sp = _sp(pkg, weight_blobs[0], 400, 64, 64)
+    ok, _ = sp.infer(np.zeros((60, 64), np.uint8))
+    assert not ok and "multiples of 8" in sp.error
+    ok, _ = sp.infer(np.zeros((72, 64), np.uint8))
+    assert not ok
+
+
+def test_sp_batched_device_path(pkg, weight_blobs):
+    from rspl_slam_amd import capi
+    from rspl_slam_amd import synthetic as SY
+    H, W, k = 480, 752, 400
+    left, right = SY.stereo_pair(H, W, seed=3)
+    sp = _sp(pkg, weight_blobs[0], k, H, W, B=2)
+    st = capi.Stream()
+    imgs = capi.DeviceBuffer(2 * H * W).upload(np.stack([left, right]))
+    feats = capi.DeviceBuffer(2 * k * 259 * 8)
+    counts = capi.DeviceBuffer(2 * 4)
+    sp.infer_device(imgs.ptr, 2, H, W, W, H * W, feats.ptr, k, counts.ptr, st.handle)
+    st.synchronize()
+    F = feats.download((2, k, 259), np.float64)
+    cnt = counts.download((2,), np.int32)
+    for b, img in enumerate((left, right)):
+        s, d = oracle.sp_forward(weight_blobs[0], post.image_to_input(img))
+        G = post.sp_postprocess(s, d, 0.004, 4, k)
+        compare_features(F[b, :cnt[b]].T, G)
