@@ -55,6 +55,7 @@ int rspl_free(void* ptr);
 int rspl_memcpy_h2d(void* dst, const void* src, size_t bytes, void* stream);
 int rspl_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
 int rspl_memset(void* dst, int value, size_t bytes, void* stream);
+int rspl_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 int rspl_stream_create(void** stream);
 int rspl_stream_destroy(void* stream);
 int rspl_stream_synchronize(void* stream);
@@ -106,6 +107,14 @@ int rspl_sp_infer_device(rspl_sp* sp, const uint8_t* d_images, int batch, int he
  * scores [H*W] f32 after NMS, desc [256*(H/8)*(W/8)] f32 channel-major. */
 int rspl_sp_debug_maps(rspl_sp* sp, int b, float* scores, float* desc);
 
+/* Per-stage device time (HIP events on the launch stream) summed over the calls
+ * made since rspl_sp_profile(sp, 1).  Stages: 0 conv1a+conv1b+pool (fused),
+ * 1 conv2a..conv4b, 2 convPa|convDa, 3 1x1 heads (softmax/d2s, L2 norm),
+ * 4 NMS + candidates, 5 top-k, 6 descriptor sampling. */
+#define RSPL_SP_STAGES 7
+int rspl_sp_profile(rspl_sp* sp, int enable);
+int rspl_sp_stage_times(rspl_sp* sp, float* ms, int* calls);
+
 void rspl_sp_destroy(rspl_sp* sp);
 
 /* ------------------------------------------------------------------------ */
@@ -142,6 +151,12 @@ int rspl_sg_infer_device(rspl_sg* sg, int batch, const double* d_feat0, const in
 
 /* Log-assignment Z [(n0+1)*(n1+1)] f32 of the last call, pair p (for tests). */
 int rspl_sg_debug_scores(rspl_sg* sg, int p, float* Z);
+
+/* Stages: 0 prep + keypoint encoder, 1 18 GNN layers, 2 final_proj + scores + bins,
+ * 3 log-Sinkhorn, 4 decode. */
+#define RSPL_SG_STAGES 5
+int rspl_sg_profile(rspl_sg* sg, int enable);
+int rspl_sg_stage_times(rspl_sg* sg, float* ms, int* calls);
 
 void rspl_sg_destroy(rspl_sg* sg);
 

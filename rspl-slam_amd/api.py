@@ -71,6 +71,15 @@ class SuperPoint:
         capi.check(self._lib.rspl_sp_infer_device(self._h, d_images, batch, height, width, stride, pitch,
                                                   d_features, capacity, d_counts, stream), "rspl_sp_infer_device")
 
+    STAGES = ("conv1a+1b+pool", "conv2a..conv4b", "convPa|convDa", "heads 1x1", "nms", "topk", "sample")
+
+    def profile(self, enable: bool = True):
+        capi.check(self._lib.rspl_sp_profile(self._h, int(enable)), "rspl_sp_profile")
+
+    def stage_times(self):
+        """(per-stage summed ms, calls) since profile(True)"""
+        return capi.stage_times(None, self._lib.rspl_sp_stage_times, self._h, len(self.STAGES))
+
     def debug_maps(self, b: int, height: int, width: int):
         s = np.empty((height, width), np.float32)
         d = np.empty((256, height // 8, width // 8), np.float32)
@@ -81,3 +90,162 @@ class SuperPoint:
         if getattr(self, "_h", None) and self._h.value:
             self._lib.rspl_sp_destroy(self._h)
             self._h = C.c_void_p()
+
+
+@dataclass
+class SuperGlueConfig:                # include/read_configs.h:20-28 (+ arena sizing)
+    image_width: int = 752
+    image_height: int = 480
+    weights: str = ""                 # RSPLWT01 blob (replaces onnx_file / engine_file)
+    max_keypoints: int = 400
+    max_batch: int = 2
+    sinkhorn_iterations: int = 100
+    precision: int = capi.RSPL_PREC_FP32
+    device: int = 0
+
+
+class SuperGlue:
+    """Mirror of class SuperGlue (include/super_glue.h:20-71)."""
+
+    def __init__(self, superglue_config: SuperGlueConfig):
+        self.config = superglue_config
+        self._h = C.c_void_p()
+        self._lib = capi.load()
+        self.error = None
+
+    def build(self) -> bool:
+        c = self.config
+        cfg = capi.SgConfig(c.image_width, c.image_height, c.max_keypoints, c.max_batch, c.sinkhorn_iterations,
+                            c.precision, c.device)
+        rc = self._lib.rspl_sg_create(C.byref(cfg), c.weights.encode(), C.byref(self._h))
+        self.error = None if rc == 0 else self._lib.rspl_last_error().decode()
+        return rc == 0
+
+    def infer(self, features0: np.ndarray, features1: np.ndarray):
+        """SuperGlue::infer (src/super_glue.cpp:137-197) on NORMALISED 259 x n features.
+        Returns (ok, indices0, indices1, mscores0, mscores1)."""
+        f0 = np.ascontiguousarray(np.asarray(features0, np.float64).T)
+        f1 = np.ascontiguousarray(np.asarray(features1, np.float64).T)
+        n0, n1 = f0.shape[0], f1.shape[0]
+        i0, i1 = np.empty(n0, np.int32), np.empty(n1, np.int32)
+        m0, m1 = np.empty(n0, np.float64), np.empty(n1, np.float64)
+        rc = self._lib.rspl_sg_infer(self._h, f0.ctypes.data, n0, f1.ctypes.data, n1, i0.ctypes.data, i1.ctypes.data,
+                                     m0.ctypes.data, m1.ctypes.data)
+        if rc != 0:
+            self.error = self._lib.rspl_last_error().decode()
+            return False, i0, i1, m0, m1
+        return True, i0, i1, m0, m1
+
+    def infer_device(self, batch: int, d_feat0: int, d_n0: int, d_feat1: int, d_n1: int, stride_feat: int,
+                     normalize: bool, d_idx0: int, d_idx1: int, d_ms0: int, d_ms1: int, stream=None) -> None:
+        capi.check(self._lib.rspl_sg_infer_device(self._h, batch, d_feat0, d_n0, d_feat1, d_n1, stride_feat,
+                                                  int(normalize), d_idx0, d_idx1, d_ms0, d_ms1, stream),
+                   "rspl_sg_infer_device")
+
+    STAGES = ("prep+kenc", "gnn x18", "final+scores", "sinkhorn", "decode")
+
+    def profile(self, enable: bool = True):
+        capi.check(self._lib.rspl_sg_profile(self._h, int(enable)), "rspl_sg_profile")
+
+    def stage_times(self):
+        return capi.stage_times(None, self._lib.rspl_sg_stage_times, self._h, len(self.STAGES))
+
+    def debug_scores(self, p: int, n0: int, n1: int) -> np.ndarray:
+        Z = np.empty((n0 + 1, n1 + 1), np.float32)
+        capi.check(self._lib.rspl_sg_debug_scores(self._h, p, Z.ctypes.data), "rspl_sg_debug_scores")
+        return Z
+
+    @property
+    def handle(self):
+        return self._h
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._lib.rspl_sg_destroy(self._h)
+            self._h = C.c_void_p()
+
+
+class PointMatching:
+    """Mirror of class PointMatching (include/point_matching.h:7-18, src/point_matching.cc)."""
+
+    def __init__(self, superglue_config: SuperGlueConfig):
+        self._superglue_config = superglue_config
+        self.superglue = SuperGlue(superglue_config)
+        if not self.superglue.build():
+            print("Erron in superglue building")   # src/point_matching.cc:8 (message kept verbatim)
+
+    def MatchingPoints(self, features0: np.ndarray, features1: np.ndarray, outlier_rejection: bool = False):
+        """Returns (num_matches, [(queryIdx, trainIdx, distance)])."""
+        f0 = np.ascontiguousarray(np.asarray(features0, np.float64).T)
+        f1 = np.ascontiguousarray(np.asarray(features1, np.float64).T)
+        cap = max(1, min(f0.shape[0], f1.shape[0]))
+        out = (capi.DMatch * cap)()
+        n = C.c_int(0)
+        capi.check(self.superglue._lib.rspl_pm_match(self.superglue.handle, f0.ctypes.data, f0.shape[0],
+                                                     f1.ctypes.data, f1.shape[0], out, cap, C.byref(n),
+                                                     int(outlier_rejection)), "rspl_pm_match")
+        matches = [(out[i].query_idx, out[i].train_idx, out[i].distance) for i in range(n.value)]
+        return n.value, matches
+
+    @staticmethod
+    def NormalizeKeypoints(features: np.ndarray, width: int, height: int) -> np.ndarray:
+        """src/point_matching.cc:72-84 (host helper; the device path normalises in-kernel)."""
+        g = np.array(features, np.float64, copy=True)
+        scale = max(width, height) * 0.7
+        g[1] = (features[1] - width // 2) / scale
+        g[2] = (features[2] - height // 2) / scale
+        return g
+
+
+# ---------------------------------------------------------------------------
+# Local BA: LocalmapOptimization (include/g2o_optimization/g2o_optimization.h:15-19)
+# ---------------------------------------------------------------------------
+class LocalBA:
+    """Owns one rspl_ba handle (device arena sized once) and runs dense problems."""
+
+    def __init__(self, max_poses=32, max_points=20000, max_lines=2000, max_edges=200000, device=0):
+        self._lib = capi.load()
+        self._h = C.c_void_p()
+        cfg = capi.BaConfig(max_poses, max_points, max_lines, max_edges, device)
+        capi.check(self._lib.rspl_ba_create(C.byref(cfg), C.byref(self._h)), "rspl_ba_create")
+
+    def run(self, problem):
+        """problem: ba_types.DenseProblem -> ba_types.DenseResult"""
+        from .ba_types import DenseResult
+        res = DenseResult.alloc(problem)
+        P, R = problem.to_ctypes(), res.to_ctypes()
+        capi.check(self._lib.rspl_ba_local(self._h, C.byref(P), C.byref(R)), "rspl_ba_local")
+        res.read_back(R)
+        return res
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._lib.rspl_ba_destroy(self._h)
+            self._h = C.c_void_p()
+
+
+_default_ba = None
+
+
+def LocalmapOptimization(poses, points, lines, camera_list, mono_point_constraints, stereo_point_constraints,
+                         mono_line_constraints, stereo_line_constraints, cfg) -> None:
+    """Same signature and in-place semantics as the reference (g2o_optimization.cc:21-252):
+    poses / points / lines (dict id -> Pose3d / Position3d / Line3d) are updated, constraint
+    ``inlier`` flags are written."""
+    from . import ba_types as BT
+    global _default_ba
+    dp, ids = BT.pack_problem(poses, points, lines, camera_list, mono_point_constraints, stereo_point_constraints,
+                              mono_line_constraints, stereo_line_constraints, cfg)
+    need = (len(poses), len(points), len(lines),
+            max(len(mono_point_constraints), len(stereo_point_constraints), len(mono_line_constraints),
+                len(stereo_line_constraints)))
+    if _default_ba is None or any(n > c for n, c in zip(need, _default_ba_caps)):
+        caps = tuple(max(n, c) for n, c in zip(need, (32, 20000, 2000, 200000)))
+        _default_ba = LocalBA(*caps)
+        globals()["_default_ba_caps"] = caps
+    res = _default_ba.run(dp)
+    BT.unpack_result(res, ids, poses, points, lines, mono_point_constraints, stereo_point_constraints,
+                     mono_line_constraints, stereo_line_constraints)
+
+
+_default_ba_caps = (0, 0, 0, 0)

@@ -18,11 +18,13 @@ RSPL_PREC_FP16 = 1
 EXPORTS = [
     "rspl_last_error", "rspl_version",
     "rspl_device_count", "rspl_set_device", "rspl_malloc", "rspl_free", "rspl_memcpy_h2d", "rspl_memcpy_d2h",
-    "rspl_memset", "rspl_stream_create", "rspl_stream_destroy", "rspl_stream_synchronize",
+    "rspl_memset", "rspl_memcpy_d2d", "rspl_stream_create", "rspl_stream_destroy", "rspl_stream_synchronize",
     "rspl_device_synchronize", "rspl_timer_create", "rspl_timer_record", "rspl_timer_elapsed_ms",
     "rspl_timer_destroy",
-    "rspl_sp_create", "rspl_sp_infer", "rspl_sp_infer_device", "rspl_sp_debug_maps", "rspl_sp_destroy",
-    "rspl_sg_create", "rspl_sg_infer", "rspl_sg_infer_device", "rspl_sg_debug_scores", "rspl_sg_destroy",
+    "rspl_sp_create", "rspl_sp_infer", "rspl_sp_infer_device", "rspl_sp_debug_maps", "rspl_sp_profile",
+    "rspl_sp_stage_times", "rspl_sp_destroy",
+    "rspl_sg_create", "rspl_sg_infer", "rspl_sg_infer_device", "rspl_sg_debug_scores", "rspl_sg_profile",
+    "rspl_sg_stage_times", "rspl_sg_destroy",
     "rspl_pm_match",
     "rspl_ba_create", "rspl_ba_local", "rspl_ba_destroy",
 ]
@@ -80,6 +82,9 @@ def load(path: pathlib.Path = LIB_PATH):
     lib.rspl_memcpy_h2d.argtypes = [vp, vp, C.c_size_t, vp]
     lib.rspl_memcpy_d2h.argtypes = [vp, vp, C.c_size_t, vp]
     lib.rspl_memset.argtypes = [vp, ip, C.c_size_t, vp]
+    lib.rspl_memcpy_d2d.argtypes = [vp, vp, C.c_size_t, vp]
+    lib.rspl_sp_profile.argtypes = [vp, ip]
+    lib.rspl_sp_stage_times.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(ip)]
     lib.rspl_stream_create.argtypes = [C.POINTER(vp)]
     lib.rspl_stream_destroy.argtypes = [vp]
     lib.rspl_stream_synchronize.argtypes = [vp]
@@ -93,6 +98,8 @@ def load(path: pathlib.Path = LIB_PATH):
         lib.rspl_sg_infer.argtypes = [vp, vp, ip, vp, ip, vp, vp, vp, vp]
         lib.rspl_sg_infer_device.argtypes = [vp, ip, vp, vp, vp, vp, ip, ip, vp, vp, vp, vp, vp]
         lib.rspl_sg_debug_scores.argtypes = [vp, ip, vp]
+        lib.rspl_sg_profile.argtypes = [vp, ip]
+        lib.rspl_sg_stage_times.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(ip)]
         lib.rspl_sg_destroy.argtypes = [vp]
         lib.rspl_sg_destroy.restype = None
         lib.rspl_pm_match.argtypes = [vp, vp, ip, vp, ip, C.POINTER(DMatch), ip, C.POINTER(ip), ip]
@@ -151,6 +158,17 @@ class DeviceBuffer:
         if self._p.value:
             load().rspl_free(self._p)
             self._p = C.c_void_p()
+
+
+def memcpy_d2d(dst: int, src: int, nbytes: int, stream=None):
+    check(load().rspl_memcpy_d2d(dst, src, nbytes, stream), "rspl_memcpy_d2d")
+
+
+def stage_times(fn_profile, fn_times, handle, nstages):
+    ms = (C.c_float * nstages)()
+    calls = C.c_int(0)
+    check(fn_times(handle, ms, C.byref(calls)), "stage_times")
+    return [ms[i] for i in range(nstages)], calls.value
 
 
 class Stream:

@@ -70,6 +70,65 @@ struct Sizer {
   }
 };
 
+// Per-stage device timing: HIP events recorded on the launch stream at stage
+// boundaries of each profiled call, kept in a ring and harvested lazily so the
+// profiling never adds a host synchronisation to the pipeline.
+struct StageTimer {
+  static constexpr int kRing = 64, kMax = 8;
+  int n = 0;
+  bool enabled = false;
+  hipEvent_t ev[kRing][kMax + 1] = {};
+  bool pending[kRing] = {};
+  int head = 0;
+  double acc[kMax] = {};
+  long calls = 0;
+  int init(int nstages) {
+    n = nstages;
+    for (int r = 0; r < kRing; r++)
+      for (int i = 0; i <= n; i++)
+        if (hipEventCreate(&ev[r][i]) != hipSuccess) return RSPL_E_DEVICE;
+    return RSPL_OK;
+  }
+  void destroy() {
+    for (int r = 0; r < kRing; r++)
+      for (int i = 0; i <= n; i++)
+        if (ev[r][i]) (void)hipEventDestroy(ev[r][i]);
+  }
+  void mark(int i, hipStream_t s) {
+    if (enabled) (void)hipEventRecord(ev[head][i], s);
+  }
+  void harvest(int r) {
+    if (!pending[r]) return;
+    (void)hipEventSynchronize(ev[r][n]);
+    for (int i = 0; i < n; i++) {
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, ev[r][i], ev[r][i + 1]);
+      acc[i] += ms;
+    }
+    pending[r] = false;
+    calls++;
+  }
+  void end_call() {
+    if (!enabled) return;
+    pending[head] = true;
+    head = (head + 1) % kRing;
+    harvest(head);  // the slot about to be reused: its call is kRing calls old
+  }
+  void reset(bool on) {
+    for (int r = 0; r < kRing; r++) pending[r] = false;
+    for (double& a : acc) a = 0;
+    calls = 0;
+    head = 0;
+    enabled = on;
+  }
+  int query(float* ms, int* ncalls) {
+    for (int k = 0; k < kRing; k++) harvest((head + k) % kRing);
+    for (int i = 0; i < n; i++) ms[i] = (float)acc[i];
+    if (ncalls) *ncalls = (int)calls;
+    return RSPL_OK;
+  }
+};
+
 // RSPLWT01 weight blob (format: rspl-slam_amd/weights.py).
 struct Tensor {
   std::string name;

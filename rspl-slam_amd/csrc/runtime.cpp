@@ -44,6 +44,11 @@ int rspl_memset(void* dst, int value, size_t bytes, void* stream) {
   RSPL_HIP(hipMemsetAsync(dst, value, bytes, (hipStream_t)stream));
   return RSPL_OK;
 }
+int rspl_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream) {
+  if (!bytes) return RSPL_OK;
+  RSPL_HIP(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+  return RSPL_OK;
+}
 int rspl_stream_create(void** stream) {
   RSPL_CHECK_ARG(stream, "NULL stream");
   RSPL_HIP(hipStreamCreateWithFlags((hipStream_t*)stream, hipStreamNonBlocking));

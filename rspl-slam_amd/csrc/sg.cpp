@@ -1,0 +1,421 @@
+// SuperGlue + PointMatching handle: C ABI (include/rspl.h) over sg_kernels.hip.
+// Mirrors SuperGlue::build / infer / process_output (src/super_glue.cpp:21-472) and
+// PointMatching::MatchingPoints (src/point_matching.cc:34-70).
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "common.hpp"
+#include "sg_kernels.hpp"
+
+using namespace rspl;
+
+namespace {
+constexpr int kLayers = 18;
+constexpr int kKencIn = 16;  // keypoint-encoder input (x, y, score) zero-padded to the GEMM K step
+const int kKencCh[6] = {3, 32, 64, 128, 256, 256};
+}  // namespace
+
+struct rspl_sg {
+  rspl_sg_config cfg{};
+  hipStream_t stream = nullptr;
+  Arena arena;
+  int nmax = 0, B = 0, G = 0, ld = 0;
+  // weights
+  float* kw[5];
+  float* kb[5];
+  float *wqkv, *bqkv, *wm, *bm, *w1, *b1, *w2, *b2;  // [18] stacked
+  float *wf, *bf, *bin;
+  // activations
+  float *kin, *h1, *h2, *X, *QKV, *O, *MSG, *HID, *cpl, *Z, *part, *val0;
+  unsigned *ctr, *err;
+  int *max0, *max1, *n0, *n1;
+  int32_t *idx0, *idx1;
+  double *ms0, *ms1, *f0, *f1;
+  // host pinned staging
+  double* h_f = nullptr;
+  int32_t* h_idx = nullptr;
+  double* h_ms = nullptr;
+  int last_n0 = 0, last_n1 = 0, last_B = 0;
+  StageTimer timer;
+};
+
+namespace {
+
+template <typename F>
+void carve(F& ar, rspl_sg* s) {
+  const size_t T = (size_t)s->B * 2 * s->nmax, ld = s->ld, B = s->B;
+  auto take = [&](auto*& p, size_t n) {
+    using Tp = std::remove_pointer_t<std::remove_reference_t<decltype(p)>>;
+    if constexpr (std::is_same_v<F, Arena>) p = ar.template take<Tp>(n);
+    else ar.template take<Tp>(n);
+  };
+  for (int i = 0; i < 5; i++) {
+    const int cin = i == 0 ? kKencIn : kKencCh[i];
+    take(s->kw[i], (size_t)cin * kKencCh[i + 1]);
+    take(s->kb[i], kKencCh[i + 1]);
+  }
+  take(s->wqkv, (size_t)kLayers * 256 * 768); take(s->bqkv, (size_t)kLayers * 768);
+  take(s->wm, (size_t)kLayers * 256 * 256); take(s->bm, (size_t)kLayers * 256);
+  take(s->w1, (size_t)kLayers * 512 * 512); take(s->b1, (size_t)kLayers * 512);
+  take(s->w2, (size_t)kLayers * 512 * 256); take(s->b2, (size_t)kLayers * 256);
+  take(s->wf, 256 * 256); take(s->bf, 256); take(s->bin, 4);
+  take(s->kin, T * kKencIn); take(s->h1, T * 256); take(s->h2, T * 256);
+  take(s->X, T * 256); take(s->QKV, T * 768); take(s->O, T * 256); take(s->MSG, T * 256); take(s->HID, T * 512);
+  take(s->cpl, B * ld * ld); take(s->Z, B * ld * ld); take(s->part, B * 2 * s->G * ld);
+  take(s->ctr, B); take(s->err, B);
+  take(s->max0, B * s->nmax); take(s->val0, B * s->nmax); take(s->max1, B * s->nmax);
+  take(s->idx0, B * s->nmax); take(s->idx1, B * s->nmax); take(s->ms0, B * s->nmax); take(s->ms1, B * s->nmax);
+  take(s->n0, B); take(s->n1, B);
+  take(s->f0, B * s->nmax * 259); take(s->f1, B * s->nmax * 259);
+}
+
+struct Up {
+  bool ok = true;
+  void operator()(float* dst, const std::vector<float>& v) {
+    ok &= hipMemcpy(dst, v.data(), v.size() * sizeof(float), hipMemcpyHostToDevice) == hipSuccess;
+  }
+};
+
+// BatchNorm1d eval fold (eps 1e-5): returns per-channel (scale, shift) so that
+// BN(conv(x)) = conv'(x) with W' = scale * W, b' = scale * (b - mean) + beta.
+bool bn_fold(const std::vector<Tensor>& ts, const std::string& pre, int c, std::vector<double>& sc,
+             std::vector<double>& sh) {
+  const Tensor* g = find(ts, pre + ".weight", c);
+  const Tensor* b = find(ts, pre + ".bias", c);
+  const Tensor* m = find(ts, pre + ".running_mean", c);
+  const Tensor* v = find(ts, pre + ".running_var", c);
+  if (!g || !b || !m || !v) return false;
+  sc.resize(c);
+  sh.resize(c);
+  for (int i = 0; i < c; i++) {
+    sc[i] = (double)g->data[i] / std::sqrt((double)v->data[i] + 1e-5);
+    sh[i] = (double)b->data[i] - (double)m->data[i] * sc[i];
+  }
+  return true;
+}
+
+int upload_weights(rspl_sg* s, const std::vector<Tensor>& ts) {
+  Up up;
+  // KeypointEncoder (superglue.py:75-85): conv1d [co][ci][1] -> W^T [ci][co], BN folded
+  for (int i = 0; i < 5; i++) {
+    const int li = 3 * i, ci = kKencCh[i], co = kKencCh[i + 1], cip = i == 0 ? kKencIn : ci;
+    const Tensor* w = find(ts, "kenc.encoder." + std::to_string(li) + ".weight", (int64_t)co * ci);
+    const Tensor* b = find(ts, "kenc.encoder." + std::to_string(li) + ".bias", co);
+    if (!w || !b) return RSPL_E_WEIGHTS;
+    std::vector<double> sc(co, 1.0), sh(co, 0.0);
+    if (i < 4 && !bn_fold(ts, "kenc.encoder." + std::to_string(li + 1), co, sc, sh)) return RSPL_E_WEIGHTS;
+    std::vector<float> wt((size_t)cip * co, 0.f), bt(co);
+    for (int o = 0; o < co; o++) {
+      for (int k = 0; k < ci; k++) wt[(size_t)k * co + o] = (float)(sc[o] * w->data[(size_t)o * ci + k]);
+      bt[o] = (float)(sc[o] * b->data[o] + sh[o]);
+    }
+    up(s->kw[i], wt);
+    up(s->kb[i], bt);
+  }
+  // GNN layers (superglue.py:126-173)
+  for (int l = 0; l < kLayers; l++) {
+    const std::string p = "gnn.layers." + std::to_string(l);
+    std::vector<float> wqkv((size_t)256 * 768), bqkv(768);
+    for (int j = 0; j < 3; j++) {
+      const Tensor* w = find(ts, p + ".attn.proj." + std::to_string(j) + ".weight", 65536);
+      const Tensor* b = find(ts, p + ".attn.proj." + std::to_string(j) + ".bias", 256);
+      if (!w || !b) return RSPL_E_WEIGHTS;
+      for (int h = 0; h < 4; h++)
+        for (int d = 0; d < 64; d++) {
+          const int c = d * 4 + h, o = j * 256 + h * 64 + d;  // view(b, 64, 4, N): c = d*4 + h
+          bqkv[o] = b->data[c];
+          for (int k = 0; k < 256; k++) wqkv[(size_t)k * 768 + o] = w->data[(size_t)c * 256 + k];
+        }
+    }
+    up(s->wqkv + (size_t)l * 256 * 768, wqkv);
+    up(s->bqkv + (size_t)l * 768, bqkv);
+    const Tensor* wm = find(ts, p + ".attn.merge.weight", 65536);
+    const Tensor* bm = find(ts, p + ".attn.merge.bias", 256);
+    const Tensor* w0 = find(ts, p + ".mlp.0.weight", 512 * 512);
+    const Tensor* b0 = find(ts, p + ".mlp.0.bias", 512);
+    const Tensor* w3 = find(ts, p + ".mlp.3.weight", 256 * 512);
+    const Tensor* b3 = find(ts, p + ".mlp.3.bias", 256);
+    std::vector<double> sc, sh;
+    if (!wm || !bm || !w0 || !b0 || !w3 || !b3 || !bn_fold(ts, p + ".mlp.1", 512, sc, sh)) return RSPL_E_WEIGHTS;
+    std::vector<float> wmt((size_t)256 * 256);
+    for (int o = 0; o < 256; o++)
+      for (int h = 0; h < 4; h++)
+        for (int d = 0; d < 64; d++) wmt[(size_t)(h * 64 + d) * 256 + o] = wm->data[(size_t)o * 256 + d * 4 + h];
+    up(s->wm + (size_t)l * 65536, wmt);
+    up(s->bm + (size_t)l * 256, bm->data);
+    std::vector<float> w1t((size_t)512 * 512), b1t(512);
+    for (int o = 0; o < 512; o++) {
+      for (int k = 0; k < 512; k++) w1t[(size_t)k * 512 + o] = (float)(sc[o] * w0->data[(size_t)o * 512 + k]);
+      b1t[o] = (float)(sc[o] * b0->data[o] + sh[o]);
+    }
+    up(s->w1 + (size_t)l * 512 * 512, w1t);
+    up(s->b1 + (size_t)l * 512, b1t);
+    std::vector<float> w2t((size_t)512 * 256);
+    for (int o = 0; o < 256; o++)
+      for (int k = 0; k < 512; k++) w2t[(size_t)k * 256 + o] = w3->data[(size_t)o * 512 + k];
+    up(s->w2 + (size_t)l * 512 * 256, w2t);
+    up(s->b2 + (size_t)l * 256, b3->data);
+  }
+  const Tensor* wf = find(ts, "final_proj.weight", 65536);
+  const Tensor* bf = find(ts, "final_proj.bias", 256);
+  const Tensor* bin = find(ts, "bin_score", 1);
+  if (!wf || !bf || !bin) return RSPL_E_WEIGHTS;
+  std::vector<float> wft((size_t)256 * 256);
+  for (int o = 0; o < 256; o++)
+    for (int k = 0; k < 256; k++) wft[(size_t)k * 256 + o] = wf->data[(size_t)o * 256 + k];
+  up(s->wf, wft);
+  up(s->bf, bf->data);
+  up(s->bin, std::vector<float>{bin->data[0], 0.f, 0.f, 0.f});
+  if (!up.ok) {
+    set_error("SuperGlue weight upload failed");
+    return RSPL_E_DEVICE;
+  }
+  return RSPL_OK;
+}
+
+sg::GemmArgs G_(const float* A, int lda, const float* B, int ldb, const float* bias, float* C, int ldc, int M, int N,
+                int K, int epi) {
+  sg::GemmArgs g{};
+  g.A = A; g.lda = lda; g.ksplit = K; g.B = B; g.ldb = ldb; g.bias = bias; g.C = C; g.ldc = ldc;
+  g.M = M; g.N = N; g.K = K; g.alpha = 1.f; g.epi = epi;
+  return g;
+}
+
+}  // namespace
+
+extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_path, rspl_sg** out) {
+  RSPL_CHECK_ARG(cfg && out, "rspl_sg_create: NULL argument");
+  RSPL_CHECK_ARG(cfg->max_keypoints > 0 && cfg->max_keypoints <= 4096, "max_keypoints must be in [1, 4096]");
+  RSPL_CHECK_ARG(cfg->precision == RSPL_PREC_FP32, "only RSPL_PREC_FP32 is implemented");
+  RSPL_CHECK_ARG(cfg->image_width > 0 && cfg->image_height > 0, "image size must be positive");
+  *out = nullptr;
+  std::vector<Tensor> ts;
+  int rc = load_blob(weights_path, ts);
+  if (rc) return rc;
+  RSPL_HIP(hipSetDevice(cfg->device));
+  auto* s = new rspl_sg();
+  s->cfg = *cfg;
+  if (s->cfg.max_batch < 1) s->cfg.max_batch = 1;
+  if (s->cfg.sinkhorn_iterations <= 0) s->cfg.sinkhorn_iterations = 100;
+  s->B = s->cfg.max_batch;
+  s->nmax = cfg->max_keypoints;  // output stride per pair (rspl.h)
+  s->ld = s->nmax + 1;
+  s->G = std::min(32, std::max(1, (s->ld + 25) / 26));
+  if (s->B * s->G > 256) {
+    set_error("max_batch * sinkhorn workgroups (%d) exceeds the CU count: co-residency required", s->B * s->G);
+    delete s;
+    return RSPL_E_ARG;
+  }
+  Sizer sz;
+  carve(sz, s);
+  if ((rc = s->arena.reserve(sz.used))) { delete s; return rc; }
+  carve(s->arena, s);
+  const size_t nm = s->nmax;
+  if (s->timer.init(RSPL_SG_STAGES) != RSPL_OK || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipHostMalloc(&s->h_f, sizeof(double) * nm * 259 * 2) != hipSuccess ||
+      hipHostMalloc(&s->h_idx, sizeof(int32_t) * nm * 2 + 16) != hipSuccess ||
+      hipHostMalloc(&s->h_ms, sizeof(double) * nm * 2) != hipSuccess) {
+    set_error("stream / pinned allocation failed");
+    rspl_sg_destroy(s);
+    return RSPL_E_DEVICE;
+  }
+  if ((rc = upload_weights(s, ts))) { rspl_sg_destroy(s); return rc; }
+  *out = s;
+  return RSPL_OK;
+}
+
+extern "C" void rspl_sg_destroy(rspl_sg* s) {
+  if (!s) return;
+  if (s->stream) (void)hipStreamSynchronize(s->stream);
+  s->arena.release();
+  s->timer.destroy();
+  if (s->h_f) (void)hipHostFree(s->h_f);
+  if (s->h_idx) (void)hipHostFree(s->h_idx);
+  if (s->h_ms) (void)hipHostFree(s->h_ms);
+  if (s->stream) (void)hipStreamDestroy(s->stream);
+  delete s;
+}
+
+extern "C" int rspl_sg_infer_device(rspl_sg* s, int B, const double* d_feat0, const int* d_n0, const double* d_feat1,
+                                    const int* d_n1, int stride_feat, int normalize, int32_t* d_idx0, int32_t* d_idx1,
+                                    double* d_ms0, double* d_ms1, void* stream_) {
+  RSPL_CHECK_ARG(s && d_feat0 && d_feat1 && d_n0 && d_n1 && d_idx0 && d_idx1 && d_ms0 && d_ms1,
+                 "rspl_sg_infer_device: NULL argument");
+  RSPL_CHECK_ARG(B >= 1 && B <= s->B, "batch %d outside [1, %d]", B, s->B);
+  RSPL_CHECK_ARG(stride_feat >= 1, "stride_feat must be >= 1");
+  hipStream_t st = stream_ ? (hipStream_t)stream_ : s->stream;
+  const int nm = s->nmax, T = B * 2 * nm;
+  // process_input (+ NormalizeKeypoints when called as PointMatching)
+  s->timer.mark(0, st);
+  sg::PrepArgs pa{};
+  pa.f0 = d_feat0; pa.f1 = d_feat1; pa.n0 = d_n0; pa.n1 = d_n1; pa.stride = stride_feat;
+  pa.normalize = normalize; pa.width = s->cfg.image_width; pa.height = s->cfg.image_height;
+  pa.nmax = nm; pa.kin = s->kin; pa.X = s->X; pa.B = B;
+  RSPL_HIP(sg::prep(pa, st));
+  // KeypointEncoder: desc += kenc([x, y, score]) (superglue.py:288-289)
+  const float* in = s->kin;
+  int cin = kKencIn;
+  float* bufs[2] = {s->h1, s->h2};
+  for (int i = 0; i < 5; i++) {
+    const int co = kKencCh[i + 1];
+    float* outp = i == 4 ? s->X : bufs[i & 1];
+    RSPL_HIP(sg::gemm(G_(in, cin, s->kw[i], co, s->kb[i], outp, co, T, co, cin, i == 4 ? 2 : 1), 1, st));
+    in = outp;
+    cin = co;
+  }
+  s->timer.mark(1, st);
+  // AttentionalGNN (superglue.py:165-173): ['self', 'cross'] * 9; both images read pre-layer descs
+  for (int l = 0; l < kLayers; l++) {
+    RSPL_HIP(sg::gemm(G_(s->X, 256, s->wqkv + (size_t)l * 256 * 768, 768, s->bqkv + (size_t)l * 768, s->QKV, 768, T,
+                         768, 256, 0), 1, st));
+    sg::AttnArgs at{};
+    at.qkv = s->QKV; at.O = s->O; at.n0 = d_n0; at.n1 = d_n1; at.nmax = nm; at.cross = l & 1;
+    RSPL_HIP(sg::attention(at, B, st));
+    RSPL_HIP(sg::gemm(G_(s->O, 256, s->wm + (size_t)l * 65536, 256, s->bm + (size_t)l * 256, s->MSG, 256, T, 256, 256,
+                         0), 1, st));
+    sg::GemmArgs g1 = G_(s->X, 256, s->w1 + (size_t)l * 512 * 512, 512, s->b1 + (size_t)l * 512, s->HID, 512, T, 512,
+                         512, 1);
+    g1.A2 = s->MSG;  // torch.cat([x, message], dim=1)
+    g1.ksplit = 256;
+    RSPL_HIP(sg::gemm(g1, 1, st));
+    RSPL_HIP(sg::gemm(G_(s->HID, 512, s->w2 + (size_t)l * 512 * 256, 256, s->b2 + (size_t)l * 256, s->X, 256, T, 256,
+                         512, 2), 1, st));
+  }
+  s->timer.mark(2, st);
+  // final_proj + scores / descriptor_dim**.5 (superglue.py:295-300)
+  float* MD = s->MSG;
+  RSPL_HIP(sg::gemm(G_(s->X, 256, s->wf, 256, s->bf, MD, 256, T, 256, 256, 0), 1, st));
+  {
+    sg::GemmArgs g = G_(MD, 256, MD + (size_t)nm * 256, 256, nullptr, s->cpl, s->ld, nm, nm, 256, 0);
+    g.b_nt = 1;
+    g.alpha = 1.f / 16.f;
+    g.sA = g.sB = (long long)2 * nm * 256;
+    g.sC = (long long)s->ld * s->ld;
+    g.mcount = d_n0; g.ncount = d_n1; g.count_stride = 1;
+    RSPL_HIP(sg::gemm(g, B, st));
+  }
+  sg::BinsArgs bn{};
+  bn.cpl = s->cpl; bn.n0 = d_n0; bn.n1 = d_n1; bn.alpha = s->bin; bn.nmax = nm;
+  RSPL_HIP(sg::bins(bn, B, st));
+  s->timer.mark(3, st);
+  // log_optimal_transport (superglue.py:185-205)
+  RSPL_HIP(hipMemsetAsync(s->ctr, 0, sizeof(unsigned) * B, st));
+  RSPL_HIP(hipMemsetAsync(s->err, 0, sizeof(unsigned) * B, st));
+  sg::SinkArgs sk{};
+  sk.cpl = s->cpl; sk.Z = s->Z; sk.part = s->part; sk.ctr = s->ctr; sk.err = s->err; sk.n0 = d_n0; sk.n1 = d_n1;
+  sk.nmax = nm; sk.G = s->G; sk.iters = s->cfg.sinkhorn_iterations;
+  RSPL_HIP(sg::sinkhorn(sk, B, st));
+  s->timer.mark(4, st);
+  // decode (super_glue.cpp:339-367), threshold 0.2 hard-coded as in the reference (:355)
+  sg::DecodeArgs dc{};
+  dc.Z = s->Z; dc.n0 = d_n0; dc.n1 = d_n1; dc.nmax = nm; dc.max0 = s->max0; dc.val0 = s->val0; dc.max1 = s->max1;
+  dc.idx0 = d_idx0; dc.idx1 = d_idx1; dc.ms0 = d_ms0; dc.ms1 = d_ms1; dc.threshold = 0.2f;
+  RSPL_HIP(sg::decode(dc, B, st));
+  s->timer.mark(5, st);
+  s->timer.end_call();
+  s->last_B = B;
+  return RSPL_OK;
+}
+
+static int sg_host_run(rspl_sg* s, const double* f0, int n0, const double* f1, int n1, int normalize) {
+  RSPL_CHECK_ARG(n0 >= 0 && n1 >= 0 && n0 <= s->cfg.max_keypoints && n1 <= s->cfg.max_keypoints,
+                 "keypoint counts (%d, %d) outside [0, %d]", n0, n1, s->cfg.max_keypoints);
+  RSPL_CHECK_ARG((f0 || !n0) && (f1 || !n1), "NULL feature matrix");
+  const size_t nm = s->nmax;
+  memcpy(s->h_f, f0, sizeof(double) * 259 * n0);
+  memcpy(s->h_f + nm * 259, f1, sizeof(double) * 259 * n1);
+  int32_t counts[2] = {n0, n1};
+  RSPL_HIP(hipMemcpyAsync(s->f0, s->h_f, sizeof(double) * 259 * n0, hipMemcpyHostToDevice, s->stream));
+  RSPL_HIP(hipMemcpyAsync(s->f1, s->h_f + nm * 259, sizeof(double) * 259 * n1, hipMemcpyHostToDevice, s->stream));
+  RSPL_HIP(hipMemcpyAsync(s->n0, &counts[0], sizeof(int32_t), hipMemcpyHostToDevice, s->stream));
+  RSPL_HIP(hipMemcpyAsync(s->n1, &counts[1], sizeof(int32_t), hipMemcpyHostToDevice, s->stream));
+  int rc = rspl_sg_infer_device(s, 1, s->f0, s->n0, s->f1, s->n1, (int)nm, normalize, s->idx0, s->idx1, s->ms0, s->ms1,
+                                s->stream);
+  if (rc) return rc;
+  RSPL_HIP(hipMemcpyAsync(s->h_idx, s->idx0, sizeof(int32_t) * n0, hipMemcpyDeviceToHost, s->stream));
+  RSPL_HIP(hipMemcpyAsync(s->h_idx + nm, s->idx1, sizeof(int32_t) * n1, hipMemcpyDeviceToHost, s->stream));
+  RSPL_HIP(hipMemcpyAsync(s->h_ms, s->ms0, sizeof(double) * n0, hipMemcpyDeviceToHost, s->stream));
+  RSPL_HIP(hipMemcpyAsync(s->h_ms + nm, s->ms1, sizeof(double) * n1, hipMemcpyDeviceToHost, s->stream));
+  unsigned err = 0;
+  RSPL_HIP(hipMemcpyAsync(s->h_idx + 2 * nm, s->err, sizeof(unsigned), hipMemcpyDeviceToHost, s->stream));
+  RSPL_HIP(hipStreamSynchronize(s->stream));
+  memcpy(&err, s->h_idx + 2 * nm, sizeof(unsigned));
+  if (err) {
+    set_error("sinkhorn: cross-workgroup exchange timed out");
+    return RSPL_E_DEVICE;
+  }
+  s->last_n0 = n0;
+  s->last_n1 = n1;
+  if (n0 == 0 || n1 == 0) {  // no couplings: every keypoint unmatched
+    for (int i = 0; i < n0; i++) { s->h_idx[i] = -1; s->h_ms[i] = 0; }
+    for (int j = 0; j < n1; j++) { s->h_idx[nm + j] = -1; s->h_ms[nm + j] = 0; }
+  }
+  return RSPL_OK;
+}
+
+extern "C" int rspl_sg_infer(rspl_sg* s, const double* f0, int n0, const double* f1, int n1, int32_t* indices0,
+                             int32_t* indices1, double* mscores0, double* mscores1) {
+  RSPL_CHECK_ARG(s && (indices0 || !n0) && (indices1 || !n1) && (mscores0 || !n0) && (mscores1 || !n1),
+                 "rspl_sg_infer: NULL argument");
+  int rc = sg_host_run(s, f0, n0, f1, n1, 0);
+  if (rc) return rc;
+  const size_t nm = s->nmax;
+  memcpy(indices0, s->h_idx, sizeof(int32_t) * n0);
+  memcpy(indices1, s->h_idx + nm, sizeof(int32_t) * n1);
+  memcpy(mscores0, s->h_ms, sizeof(double) * n0);
+  memcpy(mscores1, s->h_ms + nm, sizeof(double) * n1);
+  return RSPL_OK;
+}
+
+extern "C" int rspl_pm_match(rspl_sg* s, const double* f0, int n0, const double* f1, int n1, rspl_dmatch* matches,
+                             int capacity, int* n_matches, int outlier_rejection) {
+  RSPL_CHECK_ARG(s && n_matches && (matches || capacity == 0), "rspl_pm_match: NULL argument");
+  RSPL_CHECK_ARG(!outlier_rejection, "outlier_rejection (cv::findFundamentalMat RANSAC) is not implemented");
+  int rc = sg_host_run(s, f0, n0, f1, n1, 1);  // NormalizeKeypoints on device
+  if (rc) return rc;
+  const size_t nm = s->nmax;
+  const int32_t* i0 = s->h_idx;
+  const int32_t* i1 = s->h_idx + nm;
+  const double* m0 = s->h_ms;
+  const double* m1 = s->h_ms + nm;
+  int k = 0;
+  for (int i = 0; i < n0; i++) {  // src/point_matching.cc:46-54
+    const int j = i0[i];
+    if (j < n1 && j >= 0 && i1[j] == i) {
+      if (k >= capacity) {
+        set_error("more than %d matches", capacity);
+        return RSPL_E_CAPACITY;
+      }
+      const double d = 1.0 - (m0[i] + m1[j]) / 2.0;
+      matches[k].query_idx = i;
+      matches[k].train_idx = j;
+      matches[k].distance = (float)d;
+      k++;
+    }
+  }
+  *n_matches = k;
+  return RSPL_OK;
+}
+
+extern "C" int rspl_sg_debug_scores(rspl_sg* s, int p, float* Z) {
+  RSPL_CHECK_ARG(s && Z && p >= 0 && p < s->last_B, "rspl_sg_debug_scores: bad argument");
+  RSPL_HIP(hipStreamSynchronize(s->stream));
+  const int R = s->last_n0 + 1, Cc = s->last_n1 + 1;
+  RSPL_HIP(hipMemcpy2D(Z, sizeof(float) * Cc, s->Z + (size_t)p * s->ld * s->ld, sizeof(float) * s->ld,
+                       sizeof(float) * Cc, R, hipMemcpyDeviceToHost));
+  return RSPL_OK;
+}
+
+extern "C" int rspl_sg_profile(rspl_sg* s, int enable) {
+  RSPL_CHECK_ARG(s, "NULL handle");
+  s->timer.reset(enable != 0);
+  return RSPL_OK;
+}
+
+extern "C" int rspl_sg_stage_times(rspl_sg* s, float* ms, int* calls) {
+  RSPL_CHECK_ARG(s && ms, "NULL argument");
+  return s->timer.query(ms, calls);
+}

@@ -1,0 +1,528 @@
+// SuperGlue forward + log-optimal-transport + decode on gfx950 (CDNA4), fp32 MFMA.
+//
+// Reference semantics (convert2onnx/superglue.py; src/super_glue.cpp):
+//   KeypointEncoder :75-85, attention/MHA :88-142 (channel c = d*4 + h), GNN :145-173,
+//   final_proj + scores/16 :295-300, log_optimal_transport :176-205,
+//   decode (argmax / mutual / exp / 0.2) super_glue.cpp:258-367,
+//   process_input (double -> float packing) super_glue.cpp:199-246,
+//   PointMatching::NormalizeKeypoints point_matching.cc:72-84.
+// Layout: token-major.  Token t = (pair*2 + image)*nmax + i; descriptors X[t][256].
+// Q/K/V channels are stored head-contiguous (h*64 + d); the weight rows are
+// permuted once on the host so this equals the reference's d*4 + h interleave.
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+#include "sg_kernels.hpp"
+
+namespace rspl {
+namespace sg {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------
+// Generic fp32 MFMA GEMM: 64x64 tile, BK = 16, 4 waves (2x2) of 32x32.
+// ---------------------------------------------------------------------------
+template <int EPI, bool BNT>
+__global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
+  __shared__ float As[16][64 + 4];
+  __shared__ float Bs[16][64 + 4];
+  const int z = blockIdx.z;
+  int M = a.M, N = a.N;
+  if (a.mcount) M = a.mcount[(size_t)z * a.count_stride];
+  if (a.ncount) N = a.ncount[(size_t)z * a.count_stride];
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  if (m0 >= M || n0 >= N) return;
+  const float* A = a.A + z * a.sA;
+  const float* A2 = a.A2 ? a.A2 + z * a.sA : nullptr;
+  const float* B = a.B + z * a.sB;
+  float* C = a.C + z * a.sC;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, ml = lane & 31, kl = lane >> 5;
+  const int wm = wv >> 1, wn = wv & 1;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; r++) acc[r] = 0.f;
+  for (int k0 = 0; k0 < a.K; k0 += 16) {
+    {
+      const int row = tid >> 2, k4 = (tid & 3) * 4, m = m0 + row;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m < M) {
+        const float* src = (A2 && k0 >= a.ksplit) ? A2 + (size_t)m * a.lda + (k0 - a.ksplit) + k4
+                                                  : A + (size_t)m * a.lda + k0 + k4;
+        v = *reinterpret_cast<const float4*>(src);
+      }
+      As[k4 + 0][row] = v.x; As[k4 + 1][row] = v.y; As[k4 + 2][row] = v.z; As[k4 + 3][row] = v.w;
+    }
+    if constexpr (!BNT) {
+      const int k = tid >> 4, n4 = (tid & 15) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (n0 + n4 < N) v = *reinterpret_cast<const float4*>(B + (size_t)(k0 + k) * a.ldb + n0 + n4);
+      *reinterpret_cast<float4*>(&Bs[k][n4]) = v;
+    } else {
+      const int n = tid >> 2, k4 = (tid & 3) * 4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (n0 + n < N) v = *reinterpret_cast<const float4*>(B + (size_t)(n0 + n) * a.ldb + k0 + k4);
+      Bs[k4 + 0][n] = v.x; Bs[k4 + 1][n] = v.y; Bs[k4 + 2][n] = v.z; Bs[k4 + 3][n] = v.w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 16; kk += 2) acc = mfma32(As[kk + kl][wm * 32 + ml], Bs[kk + kl][wn * 32 + ml], acc);
+    __syncthreads();
+  }
+  const int n = n0 + wn * 32 + ml;
+  if (n >= N) return;
+  const float b = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const int m = m0 + wm * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+    if (m < M) {
+      float v = acc[r] * a.alpha + b;
+      float* dst = C + (size_t)m * a.ldc + n;
+      if constexpr (EPI == 1) v = v > 0.f ? v : 0.f;
+      if constexpr (EPI == 2) v = *dst + v;
+      *dst = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// process_input + NormalizeKeypoints: one wave per token.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
+  const int w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+  const int total = a.B * 2 * a.nmax;
+  if (w >= total) return;
+  const int i = w % a.nmax, pi = w / a.nmax, p = pi >> 1, img = pi & 1;
+  const int n = img ? a.n1[p] : a.n0[p];
+  float* X = a.X + (size_t)w * 256;
+  float* kin = a.kin + (size_t)w * 16;
+  if (i >= n) {  // padding tokens: zeros (finite everywhere downstream)
+    *reinterpret_cast<float4*>(X + 4 * lane) = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (lane < 16) kin[lane] = 0.f;
+    return;
+  }
+  const double* f = (img ? a.f1 : a.f0) + ((size_t)p * a.stride + i) * 259;
+  if (lane < 16) {
+    float v = 0.f;
+    if (lane == 0 || lane == 1) {
+      double c = f[1 + lane];
+      if (a.normalize) {
+        const int half = (lane == 0 ? a.width : a.height) / 2;  // integer division (point_matching.cc:79-81)
+        c = (c - half) / ((a.width > a.height ? a.width : a.height) * 0.7);
+      }
+      v = (float)c;
+    } else if (lane == 2) {
+      v = (float)f[0];
+    }
+    kin[lane] = v;
+  }
+  float4 d;
+  d.x = (float)f[3 + 4 * lane + 0];
+  d.y = (float)f[3 + 4 * lane + 1];
+  d.z = (float)f[3 + 4 * lane + 2];
+  d.w = (float)f[3 + 4 * lane + 3];
+  *reinterpret_cast<float4*>(X + 4 * lane) = d;
+}
+
+// ---------------------------------------------------------------------------
+// Multi-head attention, one head and 32 queries per block; the 4 waves split
+// the keys (flash split-K) and merge through LDS.  "Swapped" product
+// S^T = K Q^T puts keys on registers and queries on lanes, so the softmax
+// reductions are in-lane (+ one xor-32 swap) and S^T feeds O^T = V^T P^T as
+// the MFMA B operand with no data movement (keys taken in register order).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
+  __shared__ float Ks[4][32][65];
+  __shared__ float Vs[4][32][64];
+  __shared__ float Ml[4][32], Ll[4][32];
+  const int pz = blockIdx.z, p = pz >> 1, img = pz & 1;
+  const int simg = a.cross ? 1 - img : img;
+  const int nq = img ? a.n1[p] : a.n0[p];
+  const int nk = simg ? a.n1[p] : a.n0[p];
+  const int q0 = blockIdx.x * 32;
+  if (q0 >= nq || nk <= 0) return;
+  const int h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, ml = lane & 31, kl = lane >> 5;
+  const float* Qb = a.qkv + (size_t)(p * 2 + img) * a.nmax * 768 + h * 64;
+  const float* Kb = a.qkv + (size_t)(p * 2 + simg) * a.nmax * 768 + 256 + h * 64;
+  const float* Vb = a.qkv + (size_t)(p * 2 + simg) * a.nmax * 768 + 512 + h * 64;
+  float qf[32];
+  {
+    const int q = min(q0 + ml, nq - 1);
+    const float* qr = Qb + (size_t)q * 768;
+#pragma unroll
+    for (int s = 0; s < 32; s++) qf[s] = qr[2 * s + kl];
+  }
+  floatx16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; r++) { o0[r] = 0.f; o1[r] = 0.f; }
+  float m_run = -INFINITY, l_run = 0.f;
+  const int ntiles = (nk + 31) / 32;
+  for (int base = 0; base < ntiles; base += 4) {
+    const int t = base + wv;
+    __syncthreads();
+    if (t < ntiles) {
+      for (int i = lane; i < 32 * 16; i += 64) {
+        const int row = i >> 4, c4 = (i & 15) * 4, key = t * 32 + row;
+        float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
+        if (key < nk) {
+          kv = *reinterpret_cast<const float4*>(Kb + (size_t)key * 768 + c4);
+          vv = *reinterpret_cast<const float4*>(Vb + (size_t)key * 768 + c4);
+        }
+        Ks[wv][row][c4 + 0] = kv.x; Ks[wv][row][c4 + 1] = kv.y;
+        Ks[wv][row][c4 + 2] = kv.z; Ks[wv][row][c4 + 3] = kv.w;
+        *reinterpret_cast<float4*>(&Vs[wv][row][c4]) = vv;
+      }
+    }
+    __syncthreads();
+    if (t < ntiles) {
+      floatx16 st;
+#pragma unroll
+      for (int r = 0; r < 16; r++) st[r] = 0.f;
+#pragma unroll
+      for (int s = 0; s < 32; s++) st = mfma32(Ks[wv][ml][2 * s + kl], qf[s], st);
+      float x[16];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int key = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+        x[r] = key < nk ? st[r] * 0.125f : -INFINITY;  // scores / dim**.5 (superglue.py:90)
+        mx = fmaxf(mx, x[r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = __expf(m_run - m_new);
+      float sum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        x[r] = expf(x[r] - m_new);
+        sum += x[r];
+      }
+      sum += __shfl_xor(sum, 32);
+      l_run = l_run * alpha + sum;
+      m_run = m_new;
+#pragma unroll
+      for (int r = 0; r < 16; r++) { o0[r] *= alpha; o1[r] *= alpha; }
+#pragma unroll
+      for (int s = 0; s < 16; s++) {
+        const int key = (s & 3) + 8 * (s >> 2) + 4 * kl;
+        o0 = mfma32(Vs[wv][key][ml], x[s], o0);
+        o1 = mfma32(Vs[wv][key][32 + ml], x[s], o1);
+      }
+    }
+  }
+  __syncthreads();
+  float* Om = &Ks[0][0][0];  // reuse: [4][64][32]
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const int d = (r & 3) + 8 * (r >> 2) + 4 * kl;
+    Om[(wv * 64 + d) * 32 + ml] = o0[r];
+    Om[(wv * 64 + 32 + d) * 32 + ml] = o1[r];
+  }
+  if (kl == 0) {
+    Ml[wv][ml] = m_run;
+    Ll[wv][ml] = l_run;
+  }
+  __syncthreads();
+  float* O = a.O + (size_t)(p * 2 + img) * a.nmax * 256 + h * 64;
+  for (int idx = tid; idx < 32 * 64; idx += 256) {
+    const int q = idx >> 6, d = idx & 63;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; w++) M = fmaxf(M, Ml[w][q]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      const float e = (Ml[w][q] == -INFINITY) ? 0.f : __expf(Ml[w][q] - M);
+      L += e * Ll[w][q];
+      acc += e * Om[(w * 64 + d) * 32 + q];
+    }
+    if (q0 + q < nq) O[(size_t)(q0 + q) * 256 + d] = acc / L;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Dustbin couplings (superglue.py:191-196): column n, row m and the corner = bin_score.
+// ---------------------------------------------------------------------------
+__global__ void bins_kernel(BinsArgs a) {
+  const int p = blockIdx.y;
+  const int m = a.n0[p], n = a.n1[p], ld = a.nmax + 1;
+  float* C = a.cpl + (size_t)p * ld * ld;
+  const float al = *a.alpha;
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i <= m + n; i += gridDim.x * blockDim.x) {
+    if (i < m) C[(size_t)i * ld + n] = al;        // bins0
+    else C[(size_t)m * ld + (i - m)] = al;         // bins1 + corner
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent log-domain Sinkhorn (superglue.py:176-205).
+// G workgroups per pair; workgroup g owns a slab of rows (held in LDS when it
+// fits).  Per iteration: u for own rows (row LSE) -> per-slab column LSE
+// partials published write-through (sc1) -> one arrival counter -> every
+// workgroup combines the G partials into v.  One cross-workgroup exchange per
+// iteration; spins are bounded (timeout flag, no hang).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+__device__ __forceinline__ void st_sc1(float* p, float v) {
+  __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __uint_as_float(
+      __hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+}
+
+template <bool SLAB_IN_LDS>
+__global__ __launch_bounds__(256) void sinkhorn_kernel(SinkArgs a) {
+  extern __shared__ float sm[];
+  const int p = blockIdx.y, g = blockIdx.x, G = a.G;
+  const int m = a.n0[p], n = a.n1[p];
+  if (m <= 0 || n <= 0) return;
+  const int R = m + 1, Cc = n + 1, ld = a.nmax + 1;
+  const int rows = (R + G - 1) / G;
+  const int r0 = g * rows;
+  const int nr = max(0, min(R, r0 + rows) - r0);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* Cg = a.cpl + (size_t)p * ld * ld + (size_t)r0 * ld;
+  float* u = sm;
+  float* v = u + rows;
+  float* flag = v + ld;     // timeout broadcast
+  float* Cs = flag + 1;     // slab, only used when SLAB_IN_LDS
+  const float* Cr = SLAB_IN_LDS ? Cs : Cg;
+  if constexpr (SLAB_IN_LDS) {
+    for (int i = tid; i < nr * Cc; i += 256) {
+      const int r = i / Cc, j = i % Cc;
+      Cs[r * ld + j] = Cg[(size_t)r * ld + j];
+    }
+  }
+  for (int j = tid; j < Cc; j += 256) v[j] = 0.f;
+  // log_mu / log_nu (superglue.py:198-200), float arithmetic as the module
+  const float fm = (float)m, fn = (float)n;
+  const float norm = -logf(fm + fn);
+  const float lmu_bin = logf(fn) + norm, lnu_bin = logf(fm) + norm;
+  unsigned* ctr = a.ctr + p;
+  if (tid == 0) *flag = 0.f;
+  __syncthreads();
+  for (int it = 0; it < a.iters; it++) {
+    // u_i = log_mu_i - LSE_j(C_ij + v_j)
+    for (int r = wv; r < nr; r += 4) {
+      const float* row = Cr + (size_t)r * ld;
+      float mx = -INFINITY;
+      for (int j = lane; j < Cc; j += 64) mx = fmaxf(mx, row[j] + v[j]);
+      mx = wave_max(mx);
+      float s = 0.f;
+      for (int j = lane; j < Cc; j += 64) s += expf(row[j] + v[j] - mx);
+      s = wave_sum(s);
+      if (lane == 0) u[r] = ((r0 + r) < m ? norm : lmu_bin) - (logf(s) + mx);
+    }
+    __syncthreads();
+    // column partial LSE over this slab, published write-through
+    float* part = a.part + ((size_t)(p * 2 + (it & 1)) * G) * ld;
+    for (int j = tid; j < Cc; j += 256) {
+      float mx = -INFINITY;
+      for (int r = 0; r < nr; r++) mx = fmaxf(mx, Cr[(size_t)r * ld + j] + u[r]);
+      float s = 0.f;
+      for (int r = 0; r < nr; r++) s += expf(Cr[(size_t)r * ld + j] + u[r] - mx);
+      st_sc1(part + (size_t)g * ld + j, nr ? logf(s) + mx : -INFINITY);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned target = (unsigned)G * (unsigned)(it + 1);
+      unsigned spins = 0;
+      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+        __builtin_amdgcn_s_sleep(1);
+        if (++spins > (1u << 24)) {
+          __hip_atomic_store(a.err + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          *flag = 1.f;
+          break;
+        }
+      }
+    }
+    __syncthreads();
+    if (*flag != 0.f) break;
+    // v_j = log_nu_j - LSE_g(partial_g,j)   (online LSE over the G partials)
+    for (int j = tid; j < Cc; j += 256) {
+      float mx = -INFINITY, s = 0.f;
+      for (int gg = 0; gg < G; gg++) {
+        const float pv = ld_sc1(part + (size_t)gg * ld + j);
+        if (pv == -INFINITY) continue;
+        if (pv > mx) {
+          s = s * expf(mx - pv) + 1.f;
+          mx = pv;
+        } else {
+          s += expf(pv - mx);
+        }
+      }
+      v[j] = (j < n ? norm : lnu_bin) - (logf(s) + mx);
+    }
+    __syncthreads();
+  }
+  // Z = couplings + u + v - norm
+  float* Z = a.Z + (size_t)p * ld * ld + (size_t)r0 * ld;
+  for (int i = tid; i < nr * Cc; i += 256) {
+    const int r = i / Cc, j = i % Cc;
+    Z[(size_t)r * ld + j] = ((Cr[(size_t)r * ld + j] + u[r]) + v[j]) - norm;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// decode (super_glue.cpp:339-367).  Pass 1: row / column argmax (strict '<'
+// from -FLT_MAX: first maximum wins).  Pass 2: mutual check, exp, threshold.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void argmax_kernel(DecodeArgs a) {
+  const int p = blockIdx.z, ld = a.nmax + 1;
+  const int m = a.n0[p], n = a.n1[p];
+  const float* Z = a.Z + (size_t)p * ld * ld;
+  if (blockIdx.y == 0) {  // rows: one wave per row
+    const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
+    if (i >= m) return;
+    float best = -FLT_MAX;
+    int idx = 0;
+    for (int j = lane; j < n; j += 64) {
+      const float x = Z[(size_t)i * ld + j];
+      if (best < x) { best = x; idx = j; }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float ob = __shfl_xor(best, o);
+      const int oi = __shfl_xor(idx, o);
+      if (ob > best || (ob == best && oi < idx)) { best = ob; idx = oi; }
+    }
+    if (lane == 0) {
+      a.max0[(size_t)p * a.nmax + i] = idx;
+      a.val0[(size_t)p * a.nmax + i] = best;
+    }
+  } else {  // columns: one thread per column
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    float best = -FLT_MAX;
+    int idx = 0;
+    for (int i = 0; i < m; i++) {
+      const float x = Z[(size_t)i * ld + j];
+      if (best < x) { best = x; idx = i; }
+    }
+    a.max1[(size_t)p * a.nmax + j] = idx;
+  }
+}
+
+__device__ __forceinline__ bool mutual0_of(const DecodeArgs& a, int p, int i, int m, int n) {
+  if (n <= 0 || m <= 0) return false;
+  const int j = a.max0[(size_t)p * a.nmax + i];
+  return a.max1[(size_t)p * a.nmax + j] == i;
+}
+
+__global__ __launch_bounds__(256) void finalize_kernel(DecodeArgs a) {
+  const int p = blockIdx.z;
+  const int m = a.n0[p], n = a.n1[p];
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (blockIdx.y == 0) {
+    if (t >= m) return;
+    const bool mu = mutual0_of(a, p, t, m, n);
+    const double ms = mu ? (double)expf(a.val0[(size_t)p * a.nmax + t]) : 0.0;  // std::exp(float)
+    const bool valid = mu && ms > (double)a.threshold;
+    a.ms0[(size_t)p * a.nmax + t] = ms;
+    a.idx0[(size_t)p * a.nmax + t] = valid ? a.max0[(size_t)p * a.nmax + t] : -1;
+  } else {
+    if (t >= n) return;
+    bool mu1 = false;
+    int i = 0;
+    if (m > 0) {
+      i = a.max1[(size_t)p * a.nmax + t];
+      mu1 = a.max0[(size_t)p * a.nmax + i] == t;
+    }
+    double ms1 = 0.0;
+    bool valid1 = false;
+    if (mu1) {
+      const bool mu0 = mutual0_of(a, p, i, m, n);
+      const double ms0 = mu0 ? (double)expf(a.val0[(size_t)p * a.nmax + i]) : 0.0;
+      ms1 = ms0;
+      valid1 = mu0 && ms0 > (double)a.threshold;
+    }
+    a.ms1[(size_t)p * a.nmax + t] = ms1;
+    a.idx1[(size_t)p * a.nmax + t] = valid1 ? i : -1;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+hipError_t gemm(const GemmArgs& a, int batch, hipStream_t s) {
+  dim3 grid((a.N + 63) / 64, (a.M + 63) / 64, batch);
+  if (a.b_nt) {
+    hipLaunchKernelGGL((gemm_kernel<0, true>), grid, dim3(256), 0, s, a);
+  } else if (a.epi == 1) {
+    hipLaunchKernelGGL((gemm_kernel<1, false>), grid, dim3(256), 0, s, a);
+  } else if (a.epi == 2) {
+    hipLaunchKernelGGL((gemm_kernel<2, false>), grid, dim3(256), 0, s, a);
+  } else {
+    hipLaunchKernelGGL((gemm_kernel<0, false>), grid, dim3(256), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t prep(const PrepArgs& a, hipStream_t s) {
+  const int waves = a.B * 2 * a.nmax;
+  hipLaunchKernelGGL(prep_kernel, dim3((waves + 3) / 4), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t attention(const AttnArgs& a, int B, hipStream_t s) {
+  hipLaunchKernelGGL(attn_kernel, dim3((a.nmax + 31) / 32, 4, B * 2), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t bins(const BinsArgs& a, int B, hipStream_t s) {
+  hipLaunchKernelGGL(bins_kernel, dim3((2 * a.nmax + 256) / 256, B), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+static size_t slab_rows(int nmax, int G) { return (size_t)(nmax + 1 + G - 1) / G; }
+
+size_t sinkhorn_lds_bytes(int nmax, int G) {
+  const size_t ld = nmax + 1, rows = slab_rows(nmax, G);
+  return sizeof(float) * (rows + ld + 1 + rows * ld);  // u, v, flag, slab
+}
+
+hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s) {
+  const size_t ld = a.nmax + 1, rows = slab_rows(a.nmax, a.G);
+  const size_t full = sinkhorn_lds_bytes(a.nmax, a.G);
+  dim3 grid(a.G, B);
+  if (full <= 96 * 1024) {
+    static size_t attr = 0;
+    if (attr < full) {
+      hipError_t e = hipFuncSetAttribute((const void*)sinkhorn_kernel<true>,
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)full);
+      if (e != hipSuccess) return e;
+      attr = full;
+    }
+    hipLaunchKernelGGL(sinkhorn_kernel<true>, grid, dim3(256), full, s, a);
+  } else {
+    hipLaunchKernelGGL(sinkhorn_kernel<false>, grid, dim3(256), sizeof(float) * (rows + ld + 1), s, a);
+  }
+  return hipGetLastError();
+}
+
+hipError_t decode(const DecodeArgs& a, int B, hipStream_t s) {
+  hipLaunchKernelGGL(argmax_kernel, dim3((a.nmax * 64 + 255) / 256, 2, B), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(finalize_kernel, dim3((a.nmax + 255) / 256, 2, B), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace sg
+}  // namespace rspl

@@ -34,6 +34,7 @@ struct rspl_sp {
   int32_t* h_counts = nullptr;
   uint8_t* h_image = nullptr;
   int last_B = 0, last_H = 0, last_W = 0;
+  StageTimer timer;
 };
 
 namespace {
@@ -102,7 +103,7 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
   carve(sz, s, B, H, W, s->feat_cap);
   if ((rc = s->arena.reserve(sz.used))) { delete s; return rc; }
   carve(s->arena, s, B, H, W, s->feat_cap);
-  if (hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+  if (s->timer.init(RSPL_SP_STAGES) != RSPL_OK || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(&s->h_features, sizeof(double) * s->feat_cap * 259) != hipSuccess ||
       hipHostMalloc(&s->h_counts, sizeof(int32_t) * B) != hipSuccess ||
       hipHostMalloc(&s->h_image, (size_t)H * W) != hipSuccess) {
@@ -174,6 +175,7 @@ extern "C" void rspl_sp_destroy(rspl_sp* s) {
   if (!s) return;
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   s->arena.release();
+  s->timer.destroy();
   if (s->h_features) (void)hipHostFree(s->h_features);
   if (s->h_counts) (void)hipHostFree(s->h_counts);
   if (s->h_image) (void)hipHostFree(s->h_image);
@@ -203,8 +205,10 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
   c.w1a = s->w1a;
   c.b1a = s->b1a;
   // encoder (superpoint.py:117-127)
+  s->timer.mark(0, st);
   c.H = H; c.W = W; c.cout = 64; c.w = s->w1b; c.bias = s->b1b; c.out = s->actA;
   RSPL_HIP(conv3x3(c, 64, true, true, B, st));                               // conv1a+1b+pool
+  s->timer.mark(1, st);
   c.H = H2; c.W = W2; c.cout = 64; c.in = s->actA; c.w = s->w2a; c.bias = s->b2a; c.out = s->actB;
   RSPL_HIP(conv3x3(c, 64, false, false, B, st));                             // conv2a
   c.in = s->actB; c.w = s->w2b; c.bias = s->b2b; c.out = s->actA;
@@ -217,8 +221,10 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
   RSPL_HIP(conv3x3(c, 128, false, false, B, st));                            // conv4a
   c.in = s->actB; c.w = s->w4b; c.bias = s->b4b; c.out = s->actA;
   RSPL_HIP(conv3x3(c, 128, false, false, B, st));                            // conv4b
+  s->timer.mark(2, st);
   c.cout = 512; c.in = s->actA; c.w = s->wPD; c.bias = s->bPD; c.out = s->cells;
   RSPL_HIP(conv3x3(c, 128, false, false, B, st));                            // convPa | convDa
+  s->timer.mark(3, st);
   // heads (superpoint.py:130-135, 159-161)
   HeadArgs h{};
   h.in = s->cells; h.B = B; h.P = P; h.W8 = W8;
@@ -227,22 +233,27 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
   h.w = s->wDb; h.bias = s->bDb; h.desc = s->desc;
   RSPL_HIP(heads(h, 1, st));
   // NMS + threshold + borders (superpoint.py:16-33, super_point.cpp:224-253)
+  s->timer.mark(4, st);
   RSPL_HIP(hipMemsetAsync(s->cand_count, 0, sizeof(int) * B, st));
   NmsArgs n{};
   n.scores = s->scores; n.nms_out = s->nms; n.cand = s->cand; n.cand_count = s->cand_count; n.cand_cap = kCandCap;
   n.H = H; n.W = W; n.threshold = s->cfg.keypoint_threshold; n.border = s->cfg.remove_borders;
   RSPL_HIP(nms(n, B, st));
   // top-k (super_point.cpp:255-274)
+  s->timer.mark(5, st);
   TopkArgs t{};
   t.cand = s->cand; t.cand_count = s->cand_count; t.cand_cap = kCandCap; t.k = k;
   t.sel = s->sel; t.sel_count = s->sel_count; t.sel_cap = kCandCap;
   RSPL_HIP(topk(t, B, st));
   // descriptor sampling + packing (super_point.cpp:276-387)
+  s->timer.mark(6, st);
   SampleArgs sa{};
   sa.sel = s->sel; sa.sel_count = s->sel_count; sa.sel_stride = kCandCap; sa.per_image = (k > 0 ? k : kCandCap);
   sa.nms = s->nms; sa.desc = s->desc; sa.features = d_features; sa.feat_cap = capacity;
   sa.counts = d_counts; sa.B = B; sa.H = H; sa.W = W;
   RSPL_HIP(sample(sa, st));
+  s->timer.mark(7, st);
+  s->timer.end_call();
   s->last_B = B; s->last_H = H; s->last_W = W;
   return RSPL_OK;
 }
@@ -293,4 +304,15 @@ extern "C" int rspl_sp_debug_maps(rspl_sp* s, int b, float* scores, float* desc)
       for (int c = 0; c < 256; c++) desc[c * P + p] = tmp[p * 256 + c];
   }
   return RSPL_OK;
+}
+
+extern "C" int rspl_sp_profile(rspl_sp* s, int enable) {
+  RSPL_CHECK_ARG(s, "NULL handle");
+  s->timer.reset(enable != 0);
+  return RSPL_OK;
+}
+
+extern "C" int rspl_sp_stage_times(rspl_sp* s, float* ms, int* calls) {
+  RSPL_CHECK_ARG(s && ms, "NULL argument");
+  return s->timer.query(ms, calls);
 }

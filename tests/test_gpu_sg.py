@@ -1,0 +1,98 @@
+"""GPU parity: SuperGlue / PointMatching through the C ABI vs the reference outputs (golden) and the oracle."""
+import numpy as np
+import pytest
+
+import oracle
+import post
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pkg():
+    import rspl_loader
+    return rspl_loader.load()
+
+
+def _sg(pkg, w, nmax=400, B=1):
+    sg = pkg.SuperGlue(pkg.SuperGlueConfig(weights=w, max_keypoints=nmax, max_batch=B))
+    assert sg.build(), sg.error
+    return sg
+
+
+@pytest.mark.parametrize("name,atol", [("sg_small", 1e-4), ("sg_400", 1e-3)])
+def test_sg_vs_reference(pkg, golden, weight_blobs, name, atol):
+    g = golden(name)
+    F0, F1 = g["F0"].astype(np.float64), g["F1"].astype(np.float64)
+    G0, G1 = post.normalize_keypoints(F0, 752, 480), post.normalize_keypoints(F1, 752, 480)
+    sg = _sg(pkg, weight_blobs[1], nmax=max(F0.shape[1], F1.shape[1]))
+    ok, i0, i1, m0, m1 = sg.infer(G0, G1)
+    assert ok, sg.error
+    Z = sg.debug_scores(0, F0.shape[1], F1.shape[1])
+    np.testing.assert_allclose(Z, g["Z"], atol=atol, rtol=1e-5)
+    np.testing.assert_array_equal(i0, g["idx0"])
+    np.testing.assert_array_equal(i1, g["idx1"])
+    np.testing.assert_allclose(m0, g["ms0"], rtol=1e-4, atol=1e-6)
+    np.testing.assert_allclose(m1, g["ms1"], rtol=1e-4, atol=1e-6)
+    # decode on our own Z must be exactly the restated reference decode
+    d = post.decode(Z)
+    np.testing.assert_array_equal(i0, d[0])
+    np.testing.assert_array_equal(i1, d[1])
+    np.testing.assert_allclose(m0, d[2], rtol=2e-7, atol=0)
+
+
+def test_point_matching_vs_reference(pkg, golden, weight_blobs):
+    g = golden("sg_400")
+    pm = pkg.PointMatching(pkg.SuperGlueConfig(weights=weight_blobs[1], max_keypoints=400, max_batch=1))
+    n, matches = pm.MatchingPoints(g["F0"].astype(np.float64), g["F1"].astype(np.float64))
+    assert n == len(g["matches"])
+    np.testing.assert_array_equal(np.array([(q, t) for q, t, _ in matches]), g["matches"])
+    np.testing.assert_allclose(np.array([d for _, _, d in matches]), g["distances"], atol=1e-5)
+
+
+def test_sg_ragged_and_empty(pkg, weight_blobs):
+    from rspl_slam_amd import synthetic as SY
+    sg = _sg(pkg, weight_blobs[1], nmax=96)
+    for n0, n1 in [(1, 1), (1, 7), (33, 5), (96, 95), (64, 64)]:
+        F0, F1, _ = SY.sg_problem(n0, n1, min(n0, n1) // 2, seed=n0 * 100 + n1)
+        G0, G1 = post.normalize_keypoints(F0, 752, 480), post.normalize_keypoints(F1, 752, 480)
+        ok, i0, i1, m0, m1 = sg.infer(G0, G1)
+        assert ok, sg.error
+        Zo = oracle.sg_forward(weight_blobs[1], *post.sg_inputs(G0), *post.sg_inputs(G1))
+        Z = sg.debug_scores(0, n0, n1)
+        np.testing.assert_allclose(Z, Zo, atol=1e-3, rtol=1e-5, err_msg=f"{n0}x{n1}")
+        d = post.decode(Z)
+        np.testing.assert_array_equal(i0, d[0])
+        np.testing.assert_array_equal(i1, d[1])
+    F0, _, _ = SY.sg_problem(8, 8, 4, seed=1)
+    ok, i0, i1, m0, m1 = sg.infer(F0, np.zeros((259, 0)))
+    assert ok and (i0 == -1).all() and (m0 == 0).all() and i1.size == 0
+    ok, *_ = sg.infer(np.zeros((259, 97)), F0)        # above max_keypoints: rejected
+    assert not ok
+
+
+def test_sg_batched_device_path(pkg, weight_blobs):
+    from rspl_slam_amd import capi
+    from rspl_slam_amd import synthetic as SY
+    nmax, B = 400, 2
+    probs = [SY.sg_problem(400, 380, 300, seed=10), SY.sg_problem(350, 400, 200, seed=11)]
+    sg = _sg(pkg, weight_blobs[1], nmax=nmax, B=B)
+    f0 = np.zeros((B, nmax, 259)); f1 = np.zeros((B, nmax, 259))
+    n0 = np.zeros(B, np.int32); n1 = np.zeros(B, np.int32)
+    for p, (F0, F1, _) in enumerate(probs):
+        f0[p, :F0.shape[1]] = F0.T; f1[p, :F1.shape[1]] = F1.T
+        n0[p], n1[p] = F0.shape[1], F1.shape[1]
+    st = capi.Stream()
+    bufs = {k: capi.DeviceBuffer(v.nbytes).upload(v) for k, v in dict(f0=f0, f1=f1, n0=n0, n1=n1).items()}
+    out = {k: capi.DeviceBuffer(B * nmax * sz) for k, sz in dict(i0=4, i1=4, m0=8, m1=8).items()}
+    sg.infer_device(B, bufs["f0"].ptr, bufs["n0"].ptr, bufs["f1"].ptr, bufs["n1"].ptr, nmax, True,
+                    out["i0"].ptr, out["i1"].ptr, out["m0"].ptr, out["m1"].ptr, st.handle)
+    st.synchronize()
+    I0 = out["i0"].download((B, nmax), np.int32)
+    I1 = out["i1"].download((B, nmax), np.int32)
+    for p, (F0, F1, _) in enumerate(probs):
+        G0, G1 = post.normalize_keypoints(F0, 752, 480), post.normalize_keypoints(F1, 752, 480)
+        Zo = oracle.sg_forward(weight_blobs[1], *post.sg_inputs(G0), *post.sg_inputs(G1))
+        d = post.decode(Zo)
+        np.testing.assert_array_equal(I0[p, :n0[p]], d[0])
+        np.testing.assert_array_equal(I1[p, :n1[p]], d[1])
