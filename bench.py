@@ -1,0 +1,201 @@
+#!/usr/bin/env python3
+"""Headline benchmark: stereo frames/sec through SuperPoint -> SuperGlue -> local BA @ 752x480.
+
+Workload (BASELINE.json configs[2], "C3", all-keyframe worst case of SURVEY.md §8d): every
+step is one stereo keyframe of a synthetic EuRoC-shaped stream:
+  * SuperPoint on the rectified stereo pair (batch 2, 480x752, top-400),
+  * SuperGlue/PointMatching on 2 pairs: left(t) vs left(t-1) keyframe, left(t) vs right(t),
+  * one local BA (LocalmapOptimization) of a C3-sized problem: 10 keyframes (1 fixed),
+    ~4k points / ~10^4 point observations, 100 lines (synthetic, with ground truth).
+Inputs (images) are resident in HBM before timing.  BA is host-driven and runs on its own
+stream, overlapping the frame's SP/SG exactly as the reference's tracking thread overlaps
+its feature thread (src/map_builder.cc:48-49).  The BA problem is handed over as host
+arrays (the reference's std::map containers), so its H2D upload is inside the step.
+
+Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU, each
+rank runs its own stereo sequence (replicas, weak scaling, no data-path collective); the
+gloo process group only provides the barrier and the max-over-ranks timing, so a single
+HIP runtime (librspl's system ROCm) drives each GPU.
+"""
+import argparse
+import json
+import os
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parent
+sys.path.insert(0, str(ROOT))
+import rspl_loader  # noqa: E402
+
+pkg = rspl_loader.load()
+capi = pkg.capi
+capi.load()  # librspl's HIP runtime first: one runtime per process
+
+H, W, K = 480, 752, 400
+FP32_MFMA_PEAK = 157.3  # TFLOP/s, MI355X_MICROARCH.md (v_mfma_f32_32x32x2_f32, dense)
+CONV1_GFLOP_PER_IMAGE = 2 * H * W * 64 * 9 / 1e9 + 2 * H * W * 64 * 576 / 1e9  # conv1a + conv1b
+
+
+def log(msg):
+    print(msg, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(sp_w, sg_w, frames, threads):
+    """The oracle's C restatement (oracle/*.c) of the same per-keyframe work on host cores."""
+    sys.path.insert(0, str(ROOT / "oracle"))
+    import oracle  # checker/baseline only
+    import post
+    oracle.set_threads(threads)
+    syn = pkg.synthetic
+    probs = [syn.ba_problem(n_poses=10, n_points=4000, n_lines=100, seed=100 + i)[0] for i in range(frames)]
+    pairs = [syn.stereo_pair(H, W, seed=200 + i) for i in range(frames + 1)]
+    prev = None
+    t0 = time.perf_counter()
+    for f in range(frames):
+        L, R = pairs[f]
+        feats = []
+        for img in (L, R):
+            s, d = oracle.sp_forward(sp_w, post.image_to_input(img))
+            feats.append(post.sp_postprocess(s, d, 0.004, 4, K))
+        if prev is None:
+            prev = feats[0]
+        for a, b in ((feats[0], prev), (feats[0], feats[1])):
+            ga, gb = post.normalize_keypoints(a, W, H), post.normalize_keypoints(b, W, H)
+            Z = oracle.sg_forward(sg_w, *post.sg_inputs(ga), *post.sg_inputs(gb))
+            post.decode(Z)
+        oracle.ba_local(probs[f])
+        prev = feats[0]
+    dt = time.perf_counter() - t0
+    return {"value": frames / dt, "unit": "frames/s", "cores": threads, "kind": "port",
+            "sample": f"{frames} stereo keyframes (2xSP + 2xSG + 1 local BA each, same shapes) "
+                      f"through the oracle's C restatement, OMP_NUM_THREADS={threads}, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=30)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--cpu-frames", type=int, default=4, help="keyframes in the bounded CPU-baseline sample")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local = int(os.environ.get("LOCAL_RANK", 0))
+    dist = None
+    if world > 1:
+        import torch
+        import torch.distributed as dist
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    capi.check(capi.load().rspl_set_device(local), "rspl_set_device")
+
+    sp_w, sg_w = pkg.weights.ensure_blobs(str(ROOT / "weights"))
+    sp = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=K, weights=sp_w, max_height=H, max_width=W,
+                                             max_batch=2, device=local))
+    assert sp.build(), sp.error
+    sg = pkg.SuperGlue(pkg.SuperGlueConfig(image_width=W, image_height=H, weights=sg_w, max_keypoints=K,
+                                           max_batch=2, device=local))
+    assert sg.build(), sg.error
+    ba = pkg.LocalBA(max_poses=16, max_points=6000, max_lines=200, max_edges=40000, device=local)
+
+    syn = pkg.synthetic
+    NP = 4
+    pool = capi.DeviceBuffer(NP * 2 * H * W)
+    for i in range(NP):
+        L, R = syn.stereo_pair(H, W, seed=1000 * rank + i)
+        pool.upload(np.stack([L, R]), offset=i * 2 * H * W)
+    problems = [syn.ba_problem(n_poses=10, n_points=4000, n_lines=100, seed=1000 * rank + 50 + i)[0]
+                for i in range(3)]
+    FB = K * 259 * 8
+    feats = [capi.DeviceBuffer(2 * FB) for _ in range(2)]
+    counts = [capi.DeviceBuffer(8) for _ in range(2)]
+    f0, f1 = capi.DeviceBuffer(2 * FB), capi.DeviceBuffer(2 * FB)
+    n0, n1 = capi.DeviceBuffer(8), capi.DeviceBuffer(8)
+    outs = [capi.DeviceBuffer(2 * K * sz) for sz in (4, 4, 8, 8)]
+    st = capi.Stream()
+    ba_ms = []
+
+    def step(i):
+        cur, prev = feats[i % 2], feats[(i + 1) % 2]
+        ccur, cprev = counts[i % 2], counts[(i + 1) % 2]
+        sp.infer_device(pool.offset((i % NP) * 2 * H * W), 2, H, W, W, H * W, cur.ptr, K, ccur.ptr, st.handle)
+        # PointMatching pairs: (L_t, L_kf) and (L_t, R_t)
+        capi.memcpy_d2d(f0.ptr, cur.ptr, FB, st.handle)
+        capi.memcpy_d2d(f0.offset(FB), cur.ptr, FB, st.handle)
+        capi.memcpy_d2d(f1.ptr, prev.ptr, FB, st.handle)
+        capi.memcpy_d2d(f1.offset(FB), cur.offset(FB), FB, st.handle)
+        capi.memcpy_d2d(n0.ptr, ccur.ptr, 4, st.handle)
+        capi.memcpy_d2d(n0.offset(4), ccur.ptr, 4, st.handle)
+        capi.memcpy_d2d(n1.ptr, cprev.ptr, 4, st.handle)
+        capi.memcpy_d2d(n1.offset(4), ccur.offset(4), 4, st.handle)
+        sg.infer_device(2, f0.ptr, n0.ptr, f1.ptr, n1.ptr, K, True, outs[0].ptr, outs[1].ptr, outs[2].ptr,
+                        outs[3].ptr, st.handle)
+        t = time.perf_counter()
+        ba.run(problems[i % len(problems)])     # overlaps the SP/SG work queued above
+        ba_ms.append((time.perf_counter() - t) * 1e3)
+        st.synchronize()
+
+    for i in range(args.warmup):
+        step(i)
+    capi.synchronize()
+    if dist:
+        dist.barrier()
+    sp.profile(True)
+    sg.profile(True)
+    ba_ms.clear()
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        step(args.warmup + i)
+    capi.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist:
+        import torch
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t[0])
+        dist.barrier()
+
+    sp_ms, sp_calls = sp.stage_times()
+    sg_ms, sg_calls = sg.stage_times()
+    conv1_ms = sp_ms[0] / max(1, sp_calls)
+    achieved = 2 * CONV1_GFLOP_PER_IMAGE / conv1_ms  # GFLOP / ms = TFLOP/s
+    value = world * args.steps / elapsed
+    if rank != 0:
+        return
+    out = {
+        "metric": "stereo frames/sec SuperPoint+SuperGlue+localBA @752x480 (all-keyframe: 2xSP, 2xSG, 1 BA per frame)",
+        "value": round(value, 3),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32 (SuperPoint/SuperGlue MFMA), fp64 (BA)",
+        "data": "synthetic (seeded textured stereo 752x480, seeded weights, synthetic C3 local-BA problems)",
+        "config": {"workload": "C3 EuRoC 752x480 stereo keyframe stream: SP batch 2 top-400, SG 2 pairs N=400, "
+                               "local BA 10 poses / ~4k points / 100 lines",
+                   "global_batch": world, "parallelism": f"replicas x{world} (one sequence per GPU)"},
+        "roofline": {"kernel": "conv3x3_kernel<64,16,true,true> (conv1a+conv1b+ReLU+pool, fused)",
+                     "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK, "unit": "TFLOP/s",
+                     "frac": round(achieved / FP32_MFMA_PEAK, 4), "traffic": None,
+                     "algorithmic": f"{2 * CONV1_GFLOP_PER_IMAGE:.3f} GFLOP per launch (2 images)",
+                     "avg_launch_ms": round(conv1_ms, 4)},
+        "stages_ms_per_step": {**{f"sp:{n}": round(v / max(1, sp_calls), 4) for n, v in zip(sp.STAGES, sp_ms)},
+                               **{f"sg:{n}": round(v / max(1, sg_calls), 4) for n, v in zip(sg.STAGES, sg_ms)},
+                               "ba:wall": round(float(np.mean(ba_ms)), 4) if ba_ms else None},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        threads = min(16, os.cpu_count() or 1)
+        out["cpu_baseline"] = cpu_baseline(sp_w, sg_w, args.cpu_frames, threads)
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

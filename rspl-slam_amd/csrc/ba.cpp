@@ -3,10 +3,17 @@
 //   optimize(10) with Huber kernels -> chi2/depth outlier levels, kernels removed ->
 //   initializeOptimization(0) + optimize(5) -> inlier flags -> write back T_wc, points, lines.
 // The Levenberg-Marquardt control (g2o OptimizationAlgorithmLevenberg: tau 1e-5,
-// good-step factor clamp [1/3, 2/3], ni doubling, 10 trials) runs on the host; each
-// trial reads back 32 bytes (chi2, scale, fail).
+// good-step factor clamp [1/3, 2/3], ni doubling, 10 trials) runs on the host.  Each
+// trial is 5 kernels; the last block of the cost kernel posts {chi2, scale, fail} and a
+// sequence number to a pinned host-mapped mailbox that the host spins on (no stream
+// synchronisation, no D2H copy on the critical path).  Host->device traffic goes through
+// one pinned staging buffer (async copies only).
+#include <immintrin.h>
+
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <limits>
 #include <numeric>
@@ -21,25 +28,38 @@ struct rspl_ba {
   rspl_ba_config cfg{};
   hipStream_t stream = nullptr;
   Arena arena;
-  int maxE = 0, maxL = 0, maxK = 0;
-  // problem
+  int maxE = 0, maxL = 0, maxK = 0, maxV = 0;
+  // problem (T/X/L current state, Tb/Xb/Lb the candidate: ping-pong)
   double *cams, *T, *Tb, *X, *Xb, *L, *Lb, *eobs;
   int8_t* etype;
   int *epose, *elm, *ecam;
-  // linearisation
-  double *err, *rho0, *Hpp_e, *bp_e, *Hll_e, *bl_e, *Hpl_e, *Y_e;
-  // active structure
-  int *act_edges, *pidx, *lm_off, *lm_edges, *pose_of, *ps_off, *ps_edges, *ps_lm, *pairs;
-  uint8_t *lm_act, *level, *inlier;
+  // per-edge linearisation records
+  double *err, *rho0, *Hpp_e, *bp_e, *Hll_e, *bl_e, *Hpl_e;
+  uint8_t *level, *inlier;
   // system
-  double *Hll, *bl, *Dinv, *Hpp, *bp, *S, *x, *partial, *out;
-  int* fail;
-  double* h_out = nullptr;
+  double *Hll, *bl, *bp, *S, *x, *partial, *partial2, *out;
+  int* flags;  // [0] fail, [1] error-kernel ticket counter
+  // per-phase active structure + Schur chunk partials (growable device buffer)
+  char* phase_buf = nullptr;
+  size_t phase_cap = 0;
+  // pinned host staging for uploads / downloads
+  char* stage = nullptr;
+  size_t stage_cap = 0;
+  // host-mapped mailbox
+  ba::Mail* mail = nullptr;
+  ba::Mail* mail_dev = nullptr;
+  unsigned long long seq = 0;
+  struct Workspace {  // host scratch reused across calls (capacity persists)
+    std::vector<int> pidx, lm_off, lm_edges, lm_pose, ps_cnt, pp_cnt, fill, fill2, act;
+    std::vector<uint8_t> pact, lact;
+  } ws;
 };
 
 namespace {
 
 constexpr int kMaxCams = 16;
+
+inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
 template <typename F>
 void carve(F& ar, rspl_ba* b) {
@@ -55,13 +75,68 @@ void carve(F& ar, rspl_ba* b) {
   take(b->L, nl * 6); take(b->Lb, nl * 6);
   take(b->eobs, E * 8); take(b->etype, E); take(b->epose, E); take(b->elm, E); take(b->ecam, E);
   take(b->err, E * 4); take(b->rho0, E); take(b->Hpp_e, E * 36); take(b->bp_e, E * 6); take(b->Hll_e, E * 16);
-  take(b->bl_e, E * 4); take(b->Hpl_e, E * 24); take(b->Y_e, E * 24);
-  take(b->act_edges, E); take(b->pidx, K); take(b->lm_off, NL + 1); take(b->lm_edges, E); take(b->pose_of, K);
-  take(b->ps_off, K + 1); take(b->ps_edges, E); take(b->ps_lm, E); take(b->pairs, K * (K + 1));
-  take(b->lm_act, NL); take(b->level, E); take(b->inlier, E);
-  take(b->Hll, NL * 16); take(b->bl, NL * 4); take(b->Dinv, NL * 16); take(b->Hpp, K * 36); take(b->bp, K * 6);
-  take(b->S, 36 * K * K); take(b->x, 6 * K + 4 * NL); take(b->partial, E / 256 + 2); take(b->out, 8);
-  take(b->fail, 4);
+  take(b->bl_e, E * 4); take(b->Hpl_e, E * 24);
+  take(b->level, E); take(b->inlier, E);
+  take(b->Hll, NL * 16); take(b->bl, NL * 4); take(b->bp, K * 6);
+  take(b->S, 36 * K * K); take(b->x, 6 * K); take(b->partial, E / 256 + 2);
+  take(b->partial2, (size_t)b->maxV / 256 + 2); take(b->out, 8); take(b->flags, 4);
+}
+
+int ensure_stage(rspl_ba* b, size_t bytes) {
+  if (bytes <= b->stage_cap) return RSPL_OK;
+  // copies from the old buffer may still be in flight
+  RSPL_HIP(hipStreamSynchronize(b->stream));
+  if (b->stage) (void)hipHostFree(b->stage);
+  b->stage = nullptr;
+  const size_t cap = std::max(bytes, b->stage_cap * 2);
+  b->stage_cap = 0;
+  RSPL_HIP(hipHostMalloc((void**)&b->stage, cap, hipHostMallocDefault));
+  b->stage_cap = cap;
+  return RSPL_OK;
+}
+
+int ensure_phase(rspl_ba* b, size_t bytes) {
+  if (bytes <= b->phase_cap) return RSPL_OK;
+  RSPL_HIP(hipStreamSynchronize(b->stream));
+  if (b->phase_buf) (void)hipFree(b->phase_buf);
+  b->phase_buf = nullptr;
+  const size_t cap = std::max(bytes, b->phase_cap * 2);
+  b->phase_cap = 0;
+  RSPL_HIP(hipMalloc((void**)&b->phase_buf, cap));
+  b->phase_cap = cap;
+  return RSPL_OK;
+}
+
+// Spin on the mailbox until the kernel chain tagged `seq` has posted; surface stream
+// errors and bound the wait.
+int wait_mail(rspl_ba* b, unsigned long long seq, double* v) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  for (unsigned it = 1;; it++) {
+    if (__atomic_load_n(&b->mail->seq, __ATOMIC_ACQUIRE) == seq) break;
+    if ((it & 4095) == 0) {
+      const hipError_t q = hipStreamQuery(b->stream);
+      if (q != hipSuccess && q != hipErrorNotReady) {
+        set_error("BA stream failed: %s", hipGetErrorString(q));
+        return RSPL_E_DEVICE;
+      }
+      if (q == hipSuccess) {
+        if (__atomic_load_n(&b->mail->seq, __ATOMIC_ACQUIRE) == seq) break;
+        set_error("BA mailbox: stream idle but sequence %llu never posted", seq);
+        return RSPL_E_DEVICE;
+      }
+      if (clk::now() - t0 > std::chrono::seconds(60)) {
+        set_error("BA mailbox: timed out waiting for sequence %llu", seq);
+        return RSPL_E_DEVICE;
+      }
+    }
+    _mm_pause();
+  }
+  if (v) {
+    volatile const double* mv = b->mail->v;
+    for (int k = 0; k < 4; k++) v[k] = mv[k];
+  }
+  return RSPL_OK;
 }
 
 struct Se3h {  // host SE3Quat (w x y z, t)
@@ -95,113 +170,179 @@ Se3h inverse(const Se3h& T) {  // SE3Quat::inverse
   return r;
 }
 
-struct Phase {
-  ba::Active A{};
-  int nblocks = 0;
-};
-
+// Host-side construction of one phase's active structure (CSR lists, pose pairs, Schur
+// chunks): counting sorts over the landmark CSR, written straight into the pinned staging
+// buffer at `soff` and uploaded with one async copy.
 int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>& epose, const std::vector<int>& elm,
-                 const uint8_t* fixed, int np, int nL, int robust, Phase& ph) {
-  std::vector<uint8_t> pact(np, 0), lact(nL, 0);
-  for (int e : act) {
-    pact[epose[e]] = 1;
-    lact[elm[e]] = 1;
-  }
-  std::vector<int> pidx(np, -1), pose_of;
-  for (int p = 0; p < np; p++)
-    if (pact[p] && !fixed[p]) {
-      pidx[p] = (int)pose_of.size();
-      pose_of.push_back(p);
+                 const std::vector<int8_t>& etype, const uint8_t* fixed, int np, int nL, int robust, size_t soff,
+                 ba::Active& A, ba::Sys& S) {
+  auto& w = b->ws;
+  const int Ea = (int)act.size();
+  w.pidx.assign(np, -1);
+  w.lact.assign(nL, 0);
+  {
+    w.pact.assign(np, 0);
+    for (int e : act) {
+      w.pact[epose[e]] = 1;
+      w.lact[elm[e]] = 1;
     }
-  const int K = (int)pose_of.size();
-  std::vector<int> lm_off(nL + 1, 0), lm_edges(act.size());
-  for (int e : act) lm_off[elm[e] + 1]++;
-  for (int g = 0; g < nL; g++) lm_off[g + 1] += lm_off[g];
-  {
-    std::vector<int> fill(lm_off.begin(), lm_off.end() - 1);
-    for (int e : act) lm_edges[fill[elm[e]]++] = e;
   }
-  std::vector<int> ps_off(K + 1, 0), ps_edges, ps_lm;
+  int K = 0;
+  for (int p = 0; p < np; p++)
+    if (w.pact[p] && !fixed[p]) w.pidx[p] = K++;
+  // landmark CSR (edges in input order within a landmark)
+  w.lm_off.assign(nL + 1, 0);
+  for (int e : act) w.lm_off[elm[e] + 1]++;
+  for (int g = 0; g < nL; g++) w.lm_off[g + 1] += w.lm_off[g];
+  w.lm_edges.resize(Ea);
+  w.lm_pose.resize(Ea);
   {
-    std::vector<std::vector<int>> per(K);
-    for (int e : act)
-      if (pidx[epose[e]] >= 0) per[pidx[epose[e]]].push_back(e);
-    for (int a = 0; a < K; a++) {
-      std::stable_sort(per[a].begin(), per[a].end(), [&](int x, int y) { return elm[x] < elm[y]; });
-      ps_off[a + 1] = ps_off[a] + (int)per[a].size();
-      for (int e : per[a]) {
-        ps_edges.push_back(e);
-        ps_lm.push_back(elm[e]);
+    w.fill.assign(w.lm_off.begin(), w.lm_off.end() - 1);
+    for (int e : act) {
+      const int k = w.fill[elm[e]]++;
+      w.lm_edges[k] = e;
+      w.lm_pose[k] = w.pidx[epose[e]];
+    }
+  }
+  // counts: edges per reduced pose, edge pairs per pose pair (a <= c)
+  const int npairs = K * (K + 1) / 2;
+  auto pid = [K](int a, int c) { return a * K - a * (a - 1) / 2 + (c - a); };
+  w.ps_cnt.assign(K + 1, 0);
+  w.pp_cnt.assign(npairs + 1, 0);
+  for (int g = 0; g < nL; g++) {
+    const int k0 = w.lm_off[g], k1 = w.lm_off[g + 1];
+    for (int i = k0; i < k1; i++) {
+      const int ai = w.lm_pose[i];
+      if (ai < 0) continue;
+      w.ps_cnt[ai + 1]++;
+      for (int j = k0; j < k1; j++) {
+        const int aj = w.lm_pose[j];
+        if (aj >= ai) w.pp_cnt[pid(ai, aj) + 1]++;
       }
     }
   }
-  std::vector<int> pairs;
-  for (int a = 0; a < K; a++)
-    for (int c = a; c < K; c++) {
-      pairs.push_back(a);
-      pairs.push_back(c);
-    }
-  auto up = [&](auto* dst, const auto& v) {
-    if (!v.empty()) return hipMemcpy(dst, v.data(), v.size() * sizeof(v[0]), hipMemcpyHostToDevice) == hipSuccess;
-    return true;
+  for (int a = 0; a < K; a++) w.ps_cnt[a + 1] += w.ps_cnt[a];
+  int nch = 0;
+  for (int p = 0; p < npairs; p++) nch += (w.pp_cnt[p + 1] + ba::kChunk - 1) / ba::kChunk;
+  for (int p = 0; p < npairs; p++) w.pp_cnt[p + 1] += w.pp_cnt[p];
+  const int npp = w.pp_cnt[npairs], nps = w.ps_cnt[K];
+  // layout (identical in staging and device buffer)
+  size_t off = 0;
+  auto place = [&](size_t bytes) {
+    const size_t o = off;
+    off = al256(off + bytes);
+    return o;
   };
-  bool ok = up(b->act_edges, act) && up(b->pidx, pidx) && up(b->lm_off, lm_off) && up(b->lm_edges, lm_edges) &&
-            up(b->pose_of, pose_of) && up(b->ps_off, ps_off) && up(b->ps_edges, ps_edges) && up(b->ps_lm, ps_lm) &&
-            up(b->pairs, pairs) && up(b->lm_act, lact);
-  if (!ok) {
-    set_error("BA active-structure upload failed");
-    return RSPL_E_DEVICE;
+  const size_t o_act = place(4 * (size_t)Ea), o_pidx = place(4 * (size_t)np), o_lmoff = place(4 * (size_t)(nL + 1)),
+               o_lme = place(4 * (size_t)Ea), o_lmp = place(4 * (size_t)Ea), o_lact = place(nL),
+               o_psoff = place(4 * (size_t)(K + 1)), o_pse = place(4 * (size_t)nps),
+               o_pairs = place(8 * (size_t)npairs), o_choff = place(4 * (size_t)(npairs + 1)),
+               o_chb = place(4 * (size_t)nch), o_che = place(4 * (size_t)nch), o_e1 = place(4 * (size_t)npp),
+               o_e2 = place(4 * (size_t)npp);
+  const size_t upload = off;
+  const size_t o_chunk = place(sizeof(double) * 48 * (size_t)std::max(nch, 1));
+  int rc;
+  if ((rc = ensure_phase(b, off))) return rc;
+  if ((rc = ensure_stage(b, soff + upload))) return rc;
+  char* st = b->stage + soff;
+  auto I = [&](size_t o) { return reinterpret_cast<int*>(st + o); };
+  if (Ea) memcpy(st + o_act, act.data(), 4 * (size_t)Ea);
+  if (np) memcpy(st + o_pidx, w.pidx.data(), 4 * (size_t)np);
+  memcpy(st + o_lmoff, w.lm_off.data(), 4 * (size_t)(nL + 1));
+  if (Ea) {
+    memcpy(st + o_lme, w.lm_edges.data(), 4 * (size_t)Ea);
+    memcpy(st + o_lmp, w.lm_pose.data(), 4 * (size_t)Ea);
   }
-  ba::Active& A = ph.A;
-  A.edges = b->act_edges; A.Ea = (int)act.size(); A.pidx = b->pidx; A.lm_off = b->lm_off; A.lm_edges = b->lm_edges;
-  A.lm_act = b->lm_act; A.pose_of = b->pose_of; A.ps_off = b->ps_off; A.ps_edges = b->ps_edges; A.ps_lm = b->ps_lm;
-  A.pairs = b->pairs; A.npairs = (int)pairs.size() / 2; A.K = K; A.nL = nL; A.robust = robust;
-  ph.nblocks = ba::errors_blocks(A.Ea);
+  if (nL) memcpy(st + o_lact, w.lact.data(), nL);
+  memcpy(st + o_psoff, w.ps_cnt.data(), 4 * (size_t)(K + 1));
+  {
+    int* pairs = I(o_pairs);
+    int* choff = I(o_choff);
+    int* chb = I(o_chb);
+    int* che = I(o_che);
+    int c = 0;
+    for (int a = 0, p = 0; a < K; a++)
+      for (int cc = a; cc < K; cc++, p++) {
+        pairs[2 * p] = a;
+        pairs[2 * p + 1] = cc;
+        choff[p] = c;
+        for (int s = w.pp_cnt[p]; s < w.pp_cnt[p + 1]; s += ba::kChunk, c++) {
+          chb[c] = s;
+          che[c] = std::min(s + ba::kChunk, w.pp_cnt[p + 1]);
+        }
+      }
+    choff[npairs] = c;
+  }
+  {  // fills in landmark order: per-pose edge lists and per-pair edge pairs come out landmark-sorted
+    int* pse = I(o_pse);
+    int* e1 = I(o_e1);
+    int* e2 = I(o_e2);
+    w.fill.assign(w.ps_cnt.begin(), w.ps_cnt.end() - 1);
+    w.fill2.assign(w.pp_cnt.begin(), w.pp_cnt.end() - 1);
+    for (int g = 0; g < nL; g++) {
+      const int k0 = w.lm_off[g], k1 = w.lm_off[g + 1];
+      for (int i = k0; i < k1; i++) {
+        const int ai = w.lm_pose[i];
+        if (ai < 0) continue;
+        pse[w.fill[ai]++] = w.lm_edges[i];
+        for (int j = k0; j < k1; j++) {
+          const int aj = w.lm_pose[j];
+          if (aj < ai) continue;
+          const int q = w.fill2[pid(ai, aj)]++;
+          e1[q] = w.lm_edges[i];
+          e2[q] = w.lm_edges[j];
+        }
+      }
+    }
+  }
+  int n_line_edges = 0;
+  for (int e : act)
+    if (etype[e] >= 2) n_line_edges++;
+  RSPL_HIP(hipMemcpyAsync(b->phase_buf, st, upload, hipMemcpyHostToDevice, b->stream));
+  auto dptr = [&](size_t o) { return reinterpret_cast<const int*>(b->phase_buf + o); };
+  A.edges = dptr(o_act); A.Ea = Ea; A.pidx = dptr(o_pidx); A.lm_off = dptr(o_lmoff);
+  A.lm_edges = dptr(o_lme); A.lm_pose = dptr(o_lmp);
+  A.lm_act = reinterpret_cast<const uint8_t*>(b->phase_buf + o_lact);
+  A.ps_off = dptr(o_psoff); A.ps_edges = dptr(o_pse); A.pairs = dptr(o_pairs); A.npairs = npairs;
+  A.pair_choff = dptr(o_choff); A.ch_beg = dptr(o_chb); A.ch_end = dptr(o_che); A.nch = nch;
+  A.pp_e1 = dptr(o_e1); A.pp_e2 = dptr(o_e2); A.n_line_edges = n_line_edges; A.nL = nL; A.robust = robust;
+  A.K = K;
+  S.chunk = reinterpret_cast<double*>(b->phase_buf + o_chunk);
   return RSPL_OK;
 }
 
 // one g2o SparseOptimizer::optimize(iters) with OptimizationAlgorithmLevenberg
-int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, Phase& ph, int iters, int np, int nq, int nl, double* chi2_out,
-             int* done_out) {
+int optimize(rspl_ba* b, ba::Problem& P, const ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
+             double* chi2_out, int* done_out) {
   hipStream_t st = b->stream;
-  ba::Sys S{};
-  S.Hll = b->Hll; S.bl = b->bl; S.Dinv = b->Dinv; S.Hpp = b->Hpp; S.bp = b->bp; S.S = b->S; S.x = b->x;
-  S.partial = b->partial; S.out = b->out; S.fail = b->fail;
-  const ba::Active& A = ph.A;
-  auto read_out = [&]() -> int {
-    RSPL_HIP(hipMemcpyAsync(b->h_out, b->out, sizeof(double) * 4, hipMemcpyDeviceToHost, st));
-    RSPL_HIP(hipStreamSynchronize(st));
-    return RSPL_OK;
-  };
+  double v[4];
   int rc;
-  RSPL_HIP(ba::compute_errors(P, Lr, A, S, ph.nblocks, st));
-  if ((rc = read_out())) return rc;
-  double currentChi = b->h_out[0];
+  unsigned long long q = ++b->seq;
+  RSPL_HIP(ba::compute_errors(P, Lr, A, S, q, st));
+  if ((rc = wait_mail(b, q, v))) return rc;
+  double currentChi = v[0];
   double lambda = 0, ni = 2;
   int done = 0;
   for (int it = 0; it < iters; it++) {
     RSPL_HIP(ba::linearize(P, Lr, A, st));
-    RSPL_HIP(hipMemsetAsync(b->out + 2, 0, sizeof(double), st));
-    RSPL_HIP(ba::reduce_blocks(P, Lr, A, S, st));
+    RSPL_HIP(ba::reduce_blocks(P, Lr, A, S, it == 0, st));
     if (it == 0) {
-      if ((rc = read_out())) return rc;
-      lambda = 1e-5 * b->h_out[2];  // computeLambdaInit: tau * max diagonal
+      q = ++b->seq;
+      RSPL_HIP(ba::post(S, q, st));
+      if ((rc = wait_mail(b, q, v))) return rc;
+      lambda = 1e-5 * v[2];  // computeLambdaInit: tau * max diagonal
       ni = 2;
     }
     double rho = 0;
     int qmax = 0;
     do {
-      RSPL_HIP(hipMemcpyAsync(b->Tb, b->T, sizeof(double) * 8 * np, hipMemcpyDeviceToDevice, st));
-      RSPL_HIP(hipMemcpyAsync(b->Xb, b->X, sizeof(double) * 3 * nq, hipMemcpyDeviceToDevice, st));
-      RSPL_HIP(hipMemcpyAsync(b->Lb, b->L, sizeof(double) * 6 * nl, hipMemcpyDeviceToDevice, st));
-      RSPL_HIP(hipMemsetAsync(b->fail, 0, sizeof(int), st));
-      RSPL_HIP(ba::schur(P, Lr, A, S, lambda, st));
-      RSPL_HIP(ba::solve_update(P, Lr, A, S, lambda, st));
-      if ((rc = read_out())) return rc;
-      const bool ok = b->h_out[3] == 0.0;
-      const double tempChi = ok ? b->h_out[0] : std::numeric_limits<double>::max();
+      q = ++b->seq;
+      RSPL_HIP(ba::trial(P, Lr, A, S, lambda, q, st));
+      if ((rc = wait_mail(b, q, v))) return rc;
+      const bool ok = v[3] == 0.0;
+      const double tempChi = ok ? v[0] : std::numeric_limits<double>::max();
       rho = currentChi - tempChi;
-      const double scale = ok ? b->h_out[1] + 1e-3 : 1.0;
+      const double scale = ok ? v[1] + 1e-3 : 1.0;
       rho /= scale;
       if (rho > 0 && std::isfinite(tempChi) && ok) {
         double alpha = 1. - std::pow(2 * rho - 1, 3);
@@ -209,12 +350,12 @@ int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, Phase& ph, int iters, int 
         lambda *= std::max(1. / 3., alpha);
         ni = 2;
         currentChi = tempChi;
+        std::swap(P.T, P.Tn);  // accept: the candidate becomes the current state
+        std::swap(P.X, P.Xn);
+        std::swap(P.L, P.Ln);
       } else {
-        lambda *= ni;
+        lambda *= ni;  // reject: the current state was never modified (no restore needed)
         ni *= 2;
-        RSPL_HIP(hipMemcpyAsync(b->T, b->Tb, sizeof(double) * 8 * np, hipMemcpyDeviceToDevice, st));
-        RSPL_HIP(hipMemcpyAsync(b->X, b->Xb, sizeof(double) * 3 * nq, hipMemcpyDeviceToDevice, st));
-        RSPL_HIP(hipMemcpyAsync(b->L, b->Lb, sizeof(double) * 6 * nl, hipMemcpyDeviceToDevice, st));
         if (!std::isfinite(lambda)) break;
       }
       qmax++;
@@ -241,17 +382,21 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
   b->maxE = 4 * cfg->max_edges;
   b->maxL = cfg->max_points + cfg->max_lines;
   b->maxK = cfg->max_poses;
+  b->maxV = cfg->max_poses + cfg->max_points + cfg->max_lines;
   Sizer sz;
   carve(sz, b);
   int rc = b->arena.reserve(sz.used);
   if (rc) { delete b; return rc; }
   carve(b->arena, b);
   if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc(&b->h_out, sizeof(double) * 8) != hipSuccess) {
-    set_error("stream / pinned allocation failed");
+      hipHostMalloc((void**)&b->mail, sizeof(ba::Mail), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&b->mail_dev, b->mail, 0) != hipSuccess ||
+      hipMemset(b->flags, 0, 4 * sizeof(int)) != hipSuccess || hipMemset(b->out, 0, 8 * sizeof(double)) != hipSuccess) {
+    set_error("BA stream / mailbox allocation failed");
     rspl_ba_destroy(b);
     return RSPL_E_DEVICE;
   }
+  memset(b->mail, 0, sizeof(ba::Mail));
   *out = b;
   return RSPL_OK;
 }
@@ -260,7 +405,9 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
   if (!b) return;
   if (b->stream) (void)hipStreamSynchronize(b->stream);
   b->arena.release();
-  if (b->h_out) (void)hipHostFree(b->h_out);
+  if (b->phase_buf) (void)hipFree(b->phase_buf);
+  if (b->stage) (void)hipHostFree(b->stage);
+  if (b->mail) (void)hipHostFree(b->mail);
   if (b->stream) (void)hipStreamDestroy(b->stream);
   delete b;
 }
@@ -275,8 +422,18 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   for (int t = 0; t < 4; t++) RSPL_CHECK_ARG(ne[t] >= 0 && ne[t] <= b->cfg.max_edges, "edge capacity exceeded");
   RSPL_CHECK_ARG(pr->n_cameras >= 1 && pr->n_cameras <= kMaxCams && pr->cameras, "1..16 cameras required");
   RSPL_CHECK_ARG(res->pose_q && res->pose_p && (res->points || !nq) && (res->lines || !nl), "NULL result arrays");
+  RSPL_CHECK_ARG(np == 0 || pr->pose_fixed, "NULL pose_fixed");
   hipStream_t st = b->stream;
   const int E = ne[0] + ne[1] + ne[2] + ne[3], nL = nq + nl;
+  // optional host-side stage timing (RSPL_BA_TIMING=1): prep, build1, opt1, classify, build2, opt2, final
+  static const bool timing = getenv("RSPL_BA_TIMING") != nullptr;
+  using clk = std::chrono::steady_clock;
+  clk::time_point tmark[8];
+  int ntm = 0;
+  auto mark = [&]() {
+    if (timing) tmark[ntm++] = clk::now();
+  };
+  mark();
   // ---- vertices: VertexSE3Expmap estimate = SE3Quat(q, p).inverse() (g2o_optimization.cc:42) ----
   std::vector<double> T(8 * (size_t)np);
   for (int p = 0; p < np; p++) {
@@ -295,12 +452,28 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   // ---- edges (unified, input order) ----
   std::vector<int8_t> etype(E);
   std::vector<int> epose(E), elm(E), ecam(E);
-  std::vector<double> eobs(8 * (size_t)E, 0.0);
   const int32_t* poses[4] = {pr->mono_pose, pr->stereo_pose, pr->mono_line_pose, pr->stereo_line_pose};
   const int32_t* lms[4] = {pr->mono_point, pr->stereo_point, pr->mono_line_line, pr->stereo_line_line};
   const int32_t* cams[4] = {pr->mono_camera, pr->stereo_camera, pr->mono_line_camera, pr->stereo_line_camera};
   const double* obs[4] = {pr->mono_obs, pr->stereo_obs, pr->mono_line_obs, pr->stereo_line_obs};
   const int od[4] = {2, 3, 4, 8};
+  // staging layout of the call's uploads
+  size_t so = 0;
+  auto place = [&](size_t bytes) {
+    const size_t o = so;
+    so = al256(so + bytes);
+    return o;
+  };
+  const size_t o_cams = place(sizeof(double) * 5 * pr->n_cameras), o_T = place(sizeof(double) * 8 * np),
+               o_X = place(sizeof(double) * 3 * nq), o_L = place(sizeof(double) * 6 * nl),
+               o_obs = place(sizeof(double) * 8 * E), o_type = place(E), o_pose = place(4 * (size_t)E),
+               o_lm = place(4 * (size_t)E), o_cam = place(4 * (size_t)E);
+  const size_t call_bytes = so;
+  const size_t down_bytes = al256(E) + al256(sizeof(double) * 8 * np) + al256(sizeof(double) * 3 * nq) +
+                            al256(sizeof(double) * 6 * nl);
+  int rc;
+  if ((rc = ensure_stage(b, std::max(call_bytes, down_bytes)))) return rc;
+  double* eobs = reinterpret_cast<double*>(b->stage + o_obs);
   int e = 0;
   for (int t = 0; t < 4; t++)
     for (int i = 0; i < ne[t]; i++, e++) {
@@ -312,24 +485,35 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
       epose[e] = p;
       elm[e] = t < 2 ? l : nq + l;
       ecam[e] = c;
-      for (int k = 0; k < od[t]; k++) eobs[8 * (size_t)e + k] = obs[t][(size_t)od[t] * i + k];
+      double* o = eobs + 8 * (size_t)e;
+      for (int k = 0; k < 8; k++) o[k] = k < od[t] ? obs[t][(size_t)od[t] * i + k] : 0.0;
     }
-  auto up = [&](void* dst, const void* src, size_t bytes) {
-    return bytes == 0 || hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
+  memcpy(b->stage + o_cams, pr->cameras, sizeof(double) * 5 * pr->n_cameras);
+  if (np) memcpy(b->stage + o_T, T.data(), sizeof(double) * 8 * np);
+  if (nq) memcpy(b->stage + o_X, pr->points, sizeof(double) * 3 * nq);
+  if (nl) memcpy(b->stage + o_L, pr->lines, sizeof(double) * 6 * nl);
+  if (E) {
+    memcpy(b->stage + o_type, etype.data(), E);
+    memcpy(b->stage + o_pose, epose.data(), 4 * (size_t)E);
+    memcpy(b->stage + o_lm, elm.data(), 4 * (size_t)E);
+    memcpy(b->stage + o_cam, ecam.data(), 4 * (size_t)E);
+  }
+  auto up = [&](void* dst, size_t o, size_t bytes) {
+    return bytes == 0 || hipMemcpyAsync(dst, b->stage + o, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
   };
-  if (!(up(b->cams, pr->cameras, sizeof(double) * 5 * pr->n_cameras) && up(b->T, T.data(), sizeof(double) * T.size()) &&
-        up(b->X, pr->points, sizeof(double) * 3 * nq) && up(b->L, pr->lines, sizeof(double) * 6 * nl) &&
-        up(b->etype, etype.data(), E) && up(b->epose, epose.data(), 4 * (size_t)E) &&
-        up(b->elm, elm.data(), 4 * (size_t)E) && up(b->ecam, ecam.data(), 4 * (size_t)E) &&
-        up(b->eobs, eobs.data(), 8 * 8 * (size_t)E))) {
+  if (!(up(b->cams, o_cams, sizeof(double) * 5 * pr->n_cameras) && up(b->T, o_T, sizeof(double) * 8 * np) &&
+        up(b->X, o_X, sizeof(double) * 3 * nq) && up(b->L, o_L, sizeof(double) * 6 * nl) &&
+        up(b->eobs, o_obs, sizeof(double) * 8 * E) && up(b->etype, o_type, E) &&
+        up(b->epose, o_pose, 4 * (size_t)E) && up(b->elm, o_lm, 4 * (size_t)E) && up(b->ecam, o_cam, 4 * (size_t)E))) {
     set_error("BA upload failed");
     return RSPL_E_DEVICE;
   }
-  RSPL_HIP(hipMemsetAsync(b->level, 0, E ? E : 1, st));
-  RSPL_HIP(hipMemsetAsync(b->err, 0, sizeof(double) * 4 * (E ? E : 1), st));
-  RSPL_HIP(hipStreamSynchronize(st));
+  if (E) RSPL_HIP(hipMemsetAsync(b->level, 0, E, st));
+  RSPL_HIP(hipMemsetAsync(b->flags, 0, 4 * sizeof(int), st));
+  RSPL_HIP(hipMemsetAsync(b->out, 0, 8 * sizeof(double), st));
   ba::Problem P{};
   P.cams = b->cams; P.T = b->T; P.X = b->X; P.L = b->L; P.np = np; P.nq = nq; P.nl = nl;
+  P.Tn = b->Tb; P.Xn = b->Xb; P.Ln = b->Lb;
   P.etype = b->etype; P.epose = b->epose; P.elm = b->elm; P.ecam = b->ecam; P.eobs = b->eobs;
   const double th[4] = {pr->th_mono_point, pr->th_stereo_point, pr->th_mono_line, pr->th_stereo_line};
   for (int t = 0; t < 4; t++) {
@@ -338,55 +522,77 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   }
   ba::Lin Lr{};
   Lr.err = b->err; Lr.rho0 = b->rho0; Lr.Hpp = b->Hpp_e; Lr.bp = b->bp_e; Lr.Hll = b->Hll_e; Lr.bl = b->bl_e;
-  Lr.Hpl = b->Hpl_e; Lr.Y = b->Y_e;
-  int rc;
+  Lr.Hpl = b->Hpl_e;
+  ba::Sys S{};
+  S.Hll = b->Hll; S.bl = b->bl; S.bp = b->bp; S.S = b->S; S.x = b->x; S.partial = b->partial;
+  S.partial2 = b->partial2; S.out = b->out; S.fail = b->flags; S.counter = reinterpret_cast<unsigned*>(b->flags + 1);
+  S.mail = b->mail_dev;
+  const size_t phase_soff = al256(call_bytes);
   // ---- phase 1: all edges, Huber ----
   {
     std::vector<int> act(E);
     std::iota(act.begin(), act.end(), 0);
-    Phase ph;
-    if ((rc = build_active(b, act, epose, elm, pr->pose_fixed, np, nL, 1, ph))) return rc;
-    if ((rc = optimize(b, P, Lr, ph, pr->iterations_first, np, nq, nl, &res->chi2_first, &res->iterations_done_first)))
+    ba::Active A{};
+    mark();
+    if ((rc = build_active(b, act, epose, elm, etype, pr->pose_fixed, np, nL, 1, phase_soff, A, S))) return rc;
+    mark();
+    if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first)))
       return rc;
+    mark();
   }
   RSPL_HIP(ba::classify(P, Lr, E, b->level, nullptr, 0, st));
-  std::vector<uint8_t> level(E);
-  if (E) RSPL_HIP(hipMemcpyAsync(level.data(), b->level, E, hipMemcpyDeviceToHost, st));
-  RSPL_HIP(hipStreamSynchronize(st));
+  if (E) RSPL_HIP(hipMemcpyAsync(b->stage, b->level, E, hipMemcpyDeviceToHost, st));
+  unsigned long long q = ++b->seq;
+  RSPL_HIP(ba::post(S, q, st));
+  if ((rc = wait_mail(b, q, nullptr))) return rc;
   // ---- phase 2: level-0 edges, no kernel ----
   {
     std::vector<int> act;
+    act.reserve(E);
     for (int i = 0; i < E; i++)
-      if (!level[i]) act.push_back(i);
-    Phase ph;
-    if ((rc = build_active(b, act, epose, elm, pr->pose_fixed, np, nL, 0, ph))) return rc;
-    if ((rc = optimize(b, P, Lr, ph, pr->iterations_second, np, nq, nl, &res->chi2_second,
-                       &res->iterations_done_second)))
+      if (!b->stage[i]) act.push_back(i);
+    ba::Active A{};
+    mark();
+    if ((rc = build_active(b, act, epose, elm, etype, pr->pose_fixed, np, nL, 0, phase_soff, A, S))) return rc;
+    mark();
+    if ((rc = optimize(b, P, Lr, S, A, pr->iterations_second, &res->chi2_second, &res->iterations_done_second)))
       return rc;
+    mark();
   }
   RSPL_HIP(ba::classify(P, Lr, E, nullptr, b->inlier, 1, st));
-  std::vector<uint8_t> inl(E);
-  if (E) RSPL_HIP(hipMemcpyAsync(inl.data(), b->inlier, E, hipMemcpyDeviceToHost, st));
-  RSPL_HIP(hipMemcpyAsync(T.data(), b->T, sizeof(double) * T.size(), hipMemcpyDeviceToHost, st));
-  if (nq) RSPL_HIP(hipMemcpyAsync(res->points, b->X, sizeof(double) * 3 * nq, hipMemcpyDeviceToHost, st));
-  if (nl) RSPL_HIP(hipMemcpyAsync(res->lines, b->L, sizeof(double) * 6 * nl, hipMemcpyDeviceToHost, st));
-  RSPL_HIP(hipStreamSynchronize(st));
+  const size_t d_T = al256(E), d_X = d_T + al256(sizeof(double) * 8 * np), d_L = d_X + al256(sizeof(double) * 3 * nq);
+  if (E) RSPL_HIP(hipMemcpyAsync(b->stage, b->inlier, E, hipMemcpyDeviceToHost, st));
+  if (np) RSPL_HIP(hipMemcpyAsync(b->stage + d_T, P.T, sizeof(double) * 8 * np, hipMemcpyDeviceToHost, st));
+  if (nq) RSPL_HIP(hipMemcpyAsync(b->stage + d_X, P.X, sizeof(double) * 3 * nq, hipMemcpyDeviceToHost, st));
+  if (nl) RSPL_HIP(hipMemcpyAsync(b->stage + d_L, P.L, sizeof(double) * 6 * nl, hipMemcpyDeviceToHost, st));
+  q = ++b->seq;
+  RSPL_HIP(ba::post(S, q, st));
+  if ((rc = wait_mail(b, q, nullptr))) return rc;
+  if (nq) memcpy(res->points, b->stage + d_X, sizeof(double) * 3 * nq);
+  if (nl) memcpy(res->lines, b->stage + d_L, sizeof(double) * 6 * nl);
+  const double* Tout = reinterpret_cast<const double*>(b->stage + d_T);
   uint8_t* outs[4] = {res->mono_inlier, res->stereo_inlier, res->mono_line_inlier, res->stereo_line_inlier};
   e = 0;
   for (int t = 0; t < 4; t++)
     for (int i = 0; i < ne[t]; i++, e++)
-      if (outs[t]) outs[t][i] = inl[e];
+      if (outs[t]) outs[t][i] = (uint8_t)b->stage[e];
   // write back T_wc = estimate().inverse() (:235-240)
   for (int p = 0; p < np; p++) {
     Se3h Tcw;
-    for (int k = 0; k < 4; k++) Tcw.q[k] = T[8 * p + k];
-    for (int k = 0; k < 3; k++) Tcw.t[k] = T[8 * p + 4 + k];
+    for (int k = 0; k < 4; k++) Tcw.q[k] = Tout[8 * p + k];
+    for (int k = 0; k < 3; k++) Tcw.t[k] = Tout[8 * p + 4 + k];
     const Se3h Twc = inverse(Tcw);
     res->pose_q[4 * p + 0] = Twc.q[1];
     res->pose_q[4 * p + 1] = Twc.q[2];
     res->pose_q[4 * p + 2] = Twc.q[3];
     res->pose_q[4 * p + 3] = Twc.q[0];
     for (int k = 0; k < 3; k++) res->pose_p[3 * p + k] = Twc.t[k];
+  }
+  mark();
+  if (timing && ntm == 8) {
+    auto us = [&](int i) { return std::chrono::duration<double, std::micro>(tmark[i + 1] - tmark[i]).count(); };
+    fprintf(stderr, "rspl_ba_local us: prep %.0f build1 %.0f opt1 %.0f classify %.0f build2 %.0f opt2 %.0f final %.0f\n",
+            us(0), us(1), us(2), us(3), us(4), us(5), us(6));
   }
   return RSPL_OK;
 }

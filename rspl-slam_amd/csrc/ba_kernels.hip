@@ -229,11 +229,29 @@ __device__ __forceinline__ void huber(double e2, double delta, double& r0, doubl
   }
 }
 
+
 // ---------------------------------------------------------------------------
-// errors + robust chi2 per active edge; block partial sums (fixed tree)
+// errors + robust chi2 per active edge.  The last block to finish (ticket counter)
+// sums the block partials -- and the update kernel's scale partials -- in a fixed
+// order, posts {chi2, scale, maxdiag, fail} + seq to the host-mapped mailbox and
+// re-arms the device state (counter, fail flag, maxdiag) for the next trial.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A, double* partial) {
+__device__ __forceinline__ double block_sum256(double v, double* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int s = 128; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  const double r = red[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A, Sys S, int nb_scale,
+                                                     unsigned long long seq) {
   __shared__ double red[256];
+  __shared__ int last;
   const int i = blockIdx.x * 256 + threadIdx.x;
   double c = 0.0;
   if (i < A.Ea) {
@@ -254,166 +272,309 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
     }
     L.rho0[e] = c;
   }
-  red[threadIdx.x] = c;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
-    __syncthreads();
+  const double bsum = block_sum256(c, red);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(S.partial + blockIdx.x, bsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned tk = __hip_atomic_fetch_add(S.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = tk == gridDim.x - 1;
   }
-  if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+  __syncthreads();
+  if (!last) return;
+  double c2 = 0, sc = 0;
+  for (int k = threadIdx.x; k < (int)gridDim.x; k += 256)
+    c2 += __hip_atomic_load(S.partial + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = threadIdx.x; k < nb_scale; k += 256) sc += S.partial2[k];
+  const double chi2 = block_sum256(c2, red);
+  const double scale = block_sum256(sc, red);
+  if (threadIdx.x == 0) {
+    const double f = (double)__hip_atomic_load(S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double mx = S.out[2];
+    S.out[0] = chi2;
+    S.out[1] = scale;
+    S.out[3] = f;
+    Mail* m = S.mail;
+    m->v[0] = chi2;
+    m->v[1] = scale;
+    m->v[2] = mx;
+    m->v[3] = f;
+    __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(S.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    S.out[2] = 0.0;
+    __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// mailbox post of the lambda-init statistic (max Hessian diagonal) after the first linearisation
+__global__ void post_kernel(Sys S, unsigned long long seq) {
+  if (threadIdx.x != 0) return;
+  Mail* m = S.mail;
+  m->v[0] = S.out[0];
+  m->v[1] = S.out[1];
+  m->v[2] = S.out[2];
+  m->v[3] = (double)__hip_atomic_load(S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
 // per-edge Jacobians + weighted normal-equation contributions
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(128) void linearize_kernel(Problem P, Lin L, Active A) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= A.Ea) return;
-  const int e = A.edges[i];
-  const int t = P.etype[e], rows = edim(t), ld = ldim(t);
-  const int pose = P.epose[e], g = P.elm[e];
-  const double* cam = P.cams + 5 * P.ecam[e];
-  const double* obs = P.eobs + 8 * e;
-  const SE3 T = load_T(P.T + 8 * pose);
-  double Jp[4][6], Jl[4][4];
-  if (t < 2) {  // analytic (g2o types_sba), J = -dproj/dXc * dXc/dparam
-    const double fx = cam[0], fy = cam[1], bf = cam[4];
-    const double* X = P.X + 3 * g;
-    double R[9], Xc[3];
-    q_to_R(T.q, R);
-    mat3_vec(R, X, Xc);
-    for (int k = 0; k < 3; k++) Xc[k] += T.t[k];
-    const double x = Xc[0], y = Xc[1], z = Xc[2], iz = 1.0 / z, iz2 = iz * iz;
-    const double D[3][3] = {{fx * iz, 0, -fx * x * iz2}, {0, fy * iz, -fy * y * iz2}, {fx * iz, 0, -fx * x * iz2 + bf * iz2}};
-    const double SX[9] = {0, -z, y, z, 0, -x, -y, x, 0};
-    for (int r = 0; r < rows; r++)
-      for (int c = 0; c < 3; c++) {
-        double s = 0, sl = 0;
-        for (int k = 0; k < 3; k++) {
-          s += D[r][k] * SX[k * 3 + c];
-          sl += D[r][k] * R[k * 3 + c];
-        }
-        Jp[r][c] = s;
-        Jp[r][3 + c] = -D[r][c];
-        Jl[r][c] = -sl;
-      }
-  } else {  // numeric central difference, delta 1e-9 (g2o BaseBinaryEdge::linearizeOplus)
-    const double delta = 1e-9, scal = 1.0 / (2 * delta);
-    const double* L0 = P.L + 6 * (g - P.nq);
-    double ep[4], em[4], Lp[6];
-    for (int d = 0; d < 4; d++) {
-      double v[4] = {0, 0, 0, 0};
-      v[d] = delta;
-      for (int k = 0; k < 6; k++) Lp[k] = L0[k];
-      line_oplus(Lp, v);
-      edge_error(t, cam, obs, T, Lp, ep);
-      v[d] = -delta;
-      for (int k = 0; k < 6; k++) Lp[k] = L0[k];
-      line_oplus(Lp, v);
-      edge_error(t, cam, obs, T, Lp, em);
-      for (int r = 0; r < rows; r++) Jl[r][d] = scal * (ep[r] - em[r]);
-    }
-    for (int d = 0; d < 6; d++) {
-      double u[6] = {0, 0, 0, 0, 0, 0};
-      u[d] = delta;
-      SE3 Tp = se3_mul(se3_exp(u), T);
-      edge_error(t, cam, obs, Tp, L0, ep);
-      u[d] = -delta;
-      Tp = se3_mul(se3_exp(u), T);
-      edge_error(t, cam, obs, Tp, L0, em);
-      for (int r = 0; r < rows; r++) Jp[r][d] = scal * (ep[r] - em[r]);
-    }
+// Writes the 86 contributions of one edge (Hll, bl, and -- for an optimised pose -- Hpp, bp, Hpl).
+__device__ __forceinline__ double contrib(int o, int rows, int ld, double w, const double* er, const double* Jp,
+                                          const double* Jl) {
+  // o in [0, 86): 0..15 Hll (ld x ld), 16..19 bl, 20..55 Hpp, 56..61 bp, 62..85 Hpl (6 x 4)
+  double s = 0;
+  if (o < 16) {
+    const int a = o / ld, b = o % ld;
+    if (o >= ld * ld) return 0;
+    for (int r = 0; r < rows; r++) s += Jl[r * 4 + a] * Jl[r * 4 + b];
+    return w * s;
   }
-  const double* er = L.err + 4 * e;
+  if (o < 20) {
+    const int a = o - 16;
+    if (a >= ld) return 0;
+    for (int r = 0; r < rows; r++) s += Jl[r * 4 + a] * er[r];
+    return -w * s;
+  }
+  if (o < 56) {
+    const int a = (o - 20) / 6, b = (o - 20) % 6;
+    for (int r = 0; r < rows; r++) s += Jp[r * 6 + a] * Jp[r * 6 + b];
+    return w * s;
+  }
+  if (o < 62) {
+    const int a = o - 56;
+    for (int r = 0; r < rows; r++) s += Jp[r * 6 + a] * er[r];
+    return -w * s;
+  }
+  const int a = (o - 62) / 4, b = (o - 62) % 4;
+  if (b >= ld) return 0;
+  for (int r = 0; r < rows; r++) s += Jp[r * 6 + a] * Jl[r * 4 + b];
+  return w * s;
+}
+
+__device__ __forceinline__ void store_contrib(const Lin& L, int e, int o, double v, bool pose_opt) {
+  if (o < 16) L.Hll[16 * e + o] = v;
+  else if (o < 20) L.bl[4 * e + o - 16] = v;
+  else if (!pose_opt) return;
+  else if (o < 56) L.Hpp[36 * e + o - 20] = v;
+  else if (o < 62) L.bp[6 * e + o - 56] = v;
+  else L.Hpl[24 * e + o - 62] = v;
+}
+
+__device__ __forceinline__ double edge_weight(const Problem& P, const Lin& L, const Active& A, int e, int t) {
   double w = einfo(t);
   if (A.robust) {
+    const double* er = L.err + 4 * e;
     double chi2 = 0;
-    for (int k = 0; k < rows; k++) chi2 += er[k] * er[k];
+    for (int k = 0; k < edim(t); k++) chi2 += er[k] * er[k];
     chi2 *= einfo(t);
     double r0, r1;
     huber(chi2, P.delta[t], r0, r1);
     w *= r1;  // robustInformation = rho'(chi2) * Omega
   }
+  return w;
+}
+
+// point edges: analytic Jacobians (g2o types_sba), one thread per edge.  Mono edges
+// carry a zero third row, so every index below is a compile-time constant
+// (register resident, no scratch).
+__global__ __launch_bounds__(256) void linearize_points_kernel(Problem P, Lin L, Active A) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= A.Ea - A.n_line_edges) return;
+  const int e = A.edges[i];
+  const int t = P.etype[e];
+  const int pose = P.epose[e], g = P.elm[e];
+  const double* cam = P.cams + 5 * P.ecam[e];
+  const SE3 T = load_T(P.T + 8 * pose);
+  const double fx = cam[0], fy = cam[1], bf = cam[4];
+  double R[9], Xc[3];
+  q_to_R(T.q, R);
+  mat3_vec(R, P.X + 3 * g, Xc);
+#pragma unroll
+  for (int k = 0; k < 3; k++) Xc[k] += T.t[k];
+  const double x = Xc[0], y = Xc[1], z = Xc[2], iz = 1.0 / z, iz2 = iz * iz;
+  const bool st = t == 1;
+  const double D[3][3] = {{fx * iz, 0, -fx * x * iz2},
+                          {0, fy * iz, -fy * y * iz2},
+                          {st ? fx * iz : 0.0, 0, st ? -fx * x * iz2 + bf * iz2 : 0.0}};
+  const double SX[9] = {0, -z, y, z, 0, -x, -y, x, 0};
+  double Jp[3][6], Jl[3][3];
+#pragma unroll
+  for (int r = 0; r < 3; r++)
+#pragma unroll
+    for (int c = 0; c < 3; c++) {
+      double s = 0, sl = 0;
+#pragma unroll
+      for (int k = 0; k < 3; k++) {
+        s += D[r][k] * SX[k * 3 + c];
+        sl += D[r][k] * R[k * 3 + c];
+      }
+      Jp[r][c] = s;            // -D * (-[Xc]x)
+      Jp[r][3 + c] = -D[r][c]; // -D * I
+      Jl[r][c] = -sl;          // -D * R
+    }
+  const double w = edge_weight(P, L, A, e, t);
+  const double* er4 = L.err + 4 * e;
+  const double er[3] = {er4[0], er4[1], st ? er4[2] : 0.0};
   double* Hll = L.Hll + 16 * e;
+#pragma unroll
+  for (int a = 0; a < 3; a++)
+#pragma unroll
+    for (int b = 0; b < 3; b++) Hll[a * 3 + b] = w * (Jl[0][a] * Jl[0][b] + Jl[1][a] * Jl[1][b] + Jl[2][a] * Jl[2][b]);
+#pragma unroll
+  for (int k = 9; k < 16; k++) Hll[k] = 0.0;
   double* bl = L.bl + 4 * e;
-  for (int a = 0; a < ld; a++) {
-    double s = 0;
-    for (int r = 0; r < rows; r++) s += Jl[r][a] * er[r];
-    bl[a] = -w * s;
-    for (int b = 0; b < ld; b++) {
-      double h = 0;
-      for (int r = 0; r < rows; r++) h += Jl[r][a] * Jl[r][b];
-      Hll[a * ld + b] = w * h;
-    }
-  }
-  if (A.pidx[pose] >= 0) {
-    double* Hpp = L.Hpp + 36 * e;
-    double* bp = L.bp + 6 * e;
-    double* Hpl = L.Hpl + 24 * e;
-    for (int a = 0; a < 6; a++) {
-      double s = 0;
-      for (int r = 0; r < rows; r++) s += Jp[r][a] * er[r];
-      bp[a] = -w * s;
-      for (int b = 0; b < 6; b++) {
-        double h = 0;
-        for (int r = 0; r < rows; r++) h += Jp[r][a] * Jp[r][b];
-        Hpp[a * 6 + b] = w * h;
-      }
-      for (int b = 0; b < ld; b++) {
-        double h = 0;
-        for (int r = 0; r < rows; r++) h += Jp[r][a] * Jl[r][b];
-        Hpl[a * 4 + b] = w * h;
-      }
-    }
+#pragma unroll
+  for (int a = 0; a < 3; a++) bl[a] = -w * (Jl[0][a] * er[0] + Jl[1][a] * er[1] + Jl[2][a] * er[2]);
+  bl[3] = 0.0;
+  if (A.pidx[pose] < 0) return;
+  double* Hpp = L.Hpp + 36 * e;
+  double* bp = L.bp + 6 * e;
+  double* Hpl = L.Hpl + 24 * e;
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+#pragma unroll
+    for (int b = 0; b < 6; b++) Hpp[a * 6 + b] = w * (Jp[0][a] * Jp[0][b] + Jp[1][a] * Jp[1][b] + Jp[2][a] * Jp[2][b]);
+    bp[a] = -w * (Jp[0][a] * er[0] + Jp[1][a] * er[1] + Jp[2][a] * er[2]);
+#pragma unroll
+    for (int b = 0; b < 3; b++) Hpl[a * 4 + b] = w * (Jp[0][a] * Jl[0][b] + Jp[1][a] * Jl[1][b] + Jp[2][a] * Jl[2][b]);
+    Hpl[a * 4 + 3] = 0.0;
   }
 }
 
+// line edges: g2o's numeric central difference (delta 1e-9), one wave per edge,
+// the 20 perturbed error evaluations (+-delta on 4 line + 6 pose dims) in parallel lanes.
+__global__ __launch_bounds__(256) void linearize_lines_kernel(Problem P, Lin L, Active A) {
+  __shared__ double ev[4][20][4];
+  __shared__ double J[4][4 * 6 + 4 * 4];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + wv;
+  const bool live = i < A.n_line_edges;
+  int e = 0, t = 2, rows = 2;
+  if (live) {
+    e = A.edges[A.Ea - A.n_line_edges + i];
+    t = P.etype[e];
+    rows = edim(t);
+  }
+  const int pose = live ? P.epose[e] : 0, g = live ? P.elm[e] : P.nq;
+  const double* cam = P.cams + 5 * (live ? P.ecam[e] : 0);
+  const double* obs = P.eobs + 8 * e;
+  const double delta = 1e-9, scal = 1.0 / (2 * delta);
+  if (live && lane < 20) {
+    const int d = lane >> 1;
+    const double sgn = (lane & 1) ? -delta : delta;
+    const SE3 T = load_T(P.T + 8 * pose);
+    double Lp[6];
+    const double* L0 = P.L + 6 * (g - P.nq);
+    for (int k = 0; k < 6; k++) Lp[k] = L0[k];
+    double er[4] = {0, 0, 0, 0};
+    if (d < 4) {
+      double v[4] = {0, 0, 0, 0};
+      v[d] = sgn;
+      line_oplus(Lp, v);
+      edge_error(t, cam, obs, T, Lp, er);
+    } else {
+      double u[6] = {0, 0, 0, 0, 0, 0};
+      u[d - 4] = sgn;
+      edge_error(t, cam, obs, se3_mul(se3_exp(u), T), Lp, er);
+    }
+    for (int k = 0; k < 4; k++) ev[wv][lane][k] = er[k];
+  }
+  __syncthreads();
+  // J layout: Jp [4][6] at 0, Jl [4][4] at 24
+  if (live && lane < 40) {
+    const int r = lane / 10, d = lane % 10;
+    if (r < rows) {
+      const double v = scal * (ev[wv][2 * d][r] - ev[wv][2 * d + 1][r]);
+      if (d < 4) J[wv][24 + r * 4 + d] = v;
+      else J[wv][r * 6 + (d - 4)] = v;
+    }
+  }
+  __syncthreads();
+  if (!live) return;
+  const double w = edge_weight(P, L, A, e, t);
+  const double* er = L.err + 4 * e;
+  const bool pose_opt = A.pidx[pose] >= 0;
+  for (int o = lane; o < 86; o += 64) store_contrib(L, e, o, contrib(o, rows, 4, w, er, &J[wv][0], &J[wv][24]), pose_opt);
+}
 __device__ __forceinline__ void atomic_max_pos(double* addr, double v) {
   // non-negative doubles order like their bit patterns
   atomicMax(reinterpret_cast<unsigned long long*>(addr), (unsigned long long)__double_as_longlong(v));
 }
 
-// landmark blocks: Hll = sum_e Hll_e, bl = sum_e bl_e (edge order of the CSR list)
+// landmark blocks: Hll = sum_e Hll_e, bl = sum_e bl_e (edge order of the CSR list).
+// Edge ids are fetched 8 at a time (clamped, unconditional) so the record loads of a
+// batch are in flight together instead of one dependent chain per edge.
 __global__ __launch_bounds__(256) void landmark_reduce_kernel(Problem P, Lin L, Active A, Sys S) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= A.nL || !A.lm_act[g]) return;
   const int ld = g < P.nq ? 3 : 4;
   double H[16] = {0}, b[4] = {0};
-  for (int k = A.lm_off[g]; k < A.lm_off[g + 1]; k++) {
-    const int e = A.lm_edges[k];
-    for (int i = 0; i < ld * ld; i++) H[i] += L.Hll[16 * e + i];
-    for (int i = 0; i < ld; i++) b[i] += L.bl[4 * e + i];
+  const int k0 = A.lm_off[g], k1 = A.lm_off[g + 1];
+  for (int kb = k0; kb < k1; kb += 8) {
+    int es[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) es[u] = A.lm_edges[min(kb + u, k1 - 1)];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const bool on = kb + u < k1;
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        const double v = L.Hll[16 * es[u] + i];
+        H[i] += on ? v : 0.0;
+      }
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        const double v = L.bl[4 * es[u] + i];
+        b[i] += on ? v : 0.0;
+      }
+    }
   }
   double mx = 0;
+#pragma unroll
   for (int i = 0; i < 16; i++) S.Hll[16 * g + i] = H[i];
+#pragma unroll
   for (int i = 0; i < 4; i++) S.bl[4 * g + i] = b[i];
   for (int i = 0; i < ld; i++) mx = fmax(mx, fabs(H[i * ld + i]));
   atomic_max_pos(S.out + 2, mx);
 }
 
-// pose blocks: Hpp = sum_e Hpp_e, bp = sum_e bp_e over the pose's edges; fixed reduction tree
-__global__ __launch_bounds__(128) void pose_reduce_kernel(Problem P, Lin L, Active A, Sys S) {
-  __shared__ double red[42][128];
-  const int a = blockIdx.x, tid = threadIdx.x;
-  double acc[42];
-  for (int i = 0; i < 42; i++) acc[i] = 0;
-  for (int k = A.ps_off[a] + tid; k < A.ps_off[a + 1]; k += 128) {
-    const int e = A.ps_edges[k];
-    for (int i = 0; i < 36; i++) acc[i] += L.Hpp[36 * e + i];
-    for (int i = 0; i < 6; i++) acc[36 + i] += L.bp[6 * e + i];
+// deterministic block reduction of NV values per thread: wave shuffles, then waves in order
+template <int NV>
+__device__ __forceinline__ void block_reduce(double (&acc)[NV], double* lds /* [nwaves][NV] */) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+  for (int i = 0; i < NV; i++) {
+    double v = acc[i];
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    acc[i] = v;
   }
-  for (int i = 0; i < 42; i++) red[i][tid] = acc[i];
+  if (lane == 0)
+#pragma unroll
+    for (int i = 0; i < NV; i++) lds[wv * NV + i] = acc[i];
   __syncthreads();
-  for (int s = 64; s > 0; s >>= 1) {
-    if (tid < s)
-      for (int i = 0; i < 42; i++) red[i][tid] += red[i][tid + s];
-    __syncthreads();
+  if (threadIdx.x < NV) {
+    double s = 0;
+    for (int w = 0; w < nw; w++) s += lds[w * NV + threadIdx.x];
+    lds[threadIdx.x] = s;  // result in lds[0..NV)
   }
-  if (tid < 36) S.Hpp[36 * a + tid] = red[tid][0];
-  if (tid < 6) S.bp[6 * a + tid] = red[36 + tid][0];
+  __syncthreads();
+}
+
+// max diagonal of the pose blocks (computeLambdaInit), first iteration only
+__global__ __launch_bounds__(256) void pose_diag_kernel(Problem P, Lin L, Active A, Sys S) {
+  __shared__ double red[4 * 6];
+  const int a = blockIdx.x, tid = threadIdx.x;
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  for (int k = A.ps_off[a] + tid; k < A.ps_off[a + 1]; k += 256) {
+    const double* H = L.Hpp + 36 * A.ps_edges[k];
+#pragma unroll
+    for (int i = 0; i < 6; i++) acc[i] += H[i * 7];
+  }
+  block_reduce<6>(acc, red);
   if (tid == 0) {
     double mx = 0;
-    for (int i = 0; i < 6; i++) mx = fmax(mx, fabs(red[i * 7][0]));
+    for (int i = 0; i < 6; i++) mx = fmax(mx, fabs(red[i]));
     atomic_max_pos(S.out + 2, mx);
   }
 }
@@ -421,123 +582,305 @@ __global__ __launch_bounds__(128) void pose_reduce_kernel(Problem P, Lin L, Acti
 // ---------------------------------------------------------------------------
 // Schur complement for damping lambda
 // ---------------------------------------------------------------------------
-__device__ bool small_inv(const double* A, double* I, int n) {
-  double M[4][8];
-  for (int i = 0; i < n; i++)
-    for (int j = 0; j < n; j++) {
-      M[i][j] = A[i * n + j];
-      M[i][n + j] = (i == j);
+// ---------------------------------------------------------------------------
+// Schur complement for damping lambda
+// ---------------------------------------------------------------------------
+// Gauss-Jordan inverse with partial pivoting, fully unrolled (register resident).
+// Progressive conditional row swaps select the same pivot as a max search.
+template <int N>
+__device__ __forceinline__ bool small_inv(const double* A, double* I) {
+  double M[N][2 * N];
+#pragma unroll
+  for (int i = 0; i < N; i++)
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      M[i][j] = A[i * N + j];
+      M[i][N + j] = (i == j) ? 1.0 : 0.0;
     }
-  for (int c = 0; c < n; c++) {
-    int p = c;
-    for (int r = c + 1; r < n; r++)
-      if (fabs(M[r][c]) > fabs(M[p][c])) p = r;
-    if (M[p][c] == 0) return false;
-    if (p != c)
-      for (int k = 0; k < 2 * n; k++) {
-        const double t = M[c][k];
-        M[c][k] = M[p][k];
-        M[p][k] = t;
+  bool ok = true;
+#pragma unroll
+  for (int c = 0; c < N; c++) {
+#pragma unroll
+    for (int r = c + 1; r < N; r++) {
+      const bool sw = fabs(M[r][c]) > fabs(M[c][c]);
+#pragma unroll
+      for (int k = 0; k < 2 * N; k++) {
+        const double a = M[c][k], b = M[r][k];
+        M[c][k] = sw ? b : a;
+        M[r][k] = sw ? a : b;
       }
+    }
+    ok = ok && (M[c][c] != 0.0);
     const double iv = 1.0 / M[c][c];
-    for (int k = 0; k < 2 * n; k++) M[c][k] *= iv;
-    for (int r = 0; r < n; r++)
+#pragma unroll
+    for (int k = 0; k < 2 * N; k++) M[c][k] *= iv;
+#pragma unroll
+    for (int r = 0; r < N; r++)
       if (r != c) {
         const double f = M[r][c];
-        for (int k = 0; k < 2 * n; k++) M[r][k] -= f * M[c][k];
+#pragma unroll
+        for (int k = 0; k < 2 * N; k++) M[r][k] -= f * M[c][k];
       }
   }
-  for (int i = 0; i < n; i++)
-    for (int j = 0; j < n; j++) I[i * n + j] = M[i][n + j];
-  return true;
+#pragma unroll
+  for (int i = 0; i < N; i++)
+#pragma unroll
+    for (int j = 0; j < N; j++) I[i * N + j] = M[i][N + j];
+  return ok;
 }
 
-__global__ __launch_bounds__(256) void landmark_schur_kernel(Problem P, Lin L, Active A, Sys S, double lambda) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= A.nL || !A.lm_act[g]) return;
-  const int ld = g < P.nq ? 3 : 4;
-  double H[16], D[16];
-  for (int i = 0; i < ld * ld; i++) H[i] = S.Hll[16 * g + i];
-  for (int i = 0; i < ld; i++) H[i * ld + i] += lambda;
-  if (!small_inv(H, D, ld)) {
-    atomicOr(S.fail, 1);
-    return;
+// (Hll_g + lambda I)^-1, zero-padded to 4x4 for points
+__device__ __forceinline__ bool lm_dinv(const double* Hll, bool point, double lambda, double (&D)[16]) {
+  if (point) {
+    double H[9], Di[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) H[i] = Hll[i];
+    H[0] += lambda;
+    H[4] += lambda;
+    H[8] += lambda;
+    const bool ok = small_inv<3>(H, Di);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) D[i * 4 + j] = (i < 3 && j < 3) ? Di[i * 3 + j] : 0.0;
+    return ok;
   }
-  for (int i = 0; i < ld * ld; i++) S.Dinv[16 * g + i] = D[i];
-  for (int k = A.lm_off[g]; k < A.lm_off[g + 1]; k++) {
-    const int e = A.lm_edges[k];
-    if (A.pidx[P.epose[e]] < 0) continue;
-    const double* B = L.Hpl + 24 * e;
-    double* Y = L.Y + 24 * e;
-    for (int r = 0; r < 6; r++)
-      for (int c = 0; c < ld; c++) {
-        double s = 0;
-        for (int k2 = 0; k2 < ld; k2++) s += B[r * 4 + k2] * D[k2 * ld + c];
-        Y[r * 4 + c] = s;
-      }
-  }
+  double H[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) H[i] = Hll[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) H[i * 5] += lambda;
+  return small_inv<4>(H, D);
 }
 
-// one block per reduced pose pair (a <= b):
-//   S_ab = [a==b](Hpp_a + lambda I) - sum_{landmarks seen by both} Y_e1 Hpl_e2^T,  bs_a = bp_a - sum Y_e bl_l
-__global__ __launch_bounds__(128) void pair_schur_kernel(Problem P, Lin L, Active A, Sys S, double lambda) {
-  __shared__ double red[42][128];
-  const int pr = blockIdx.x, tid = threadIdx.x;
-  const int a = A.pairs[2 * pr], b = A.pairs[2 * pr + 1];
-  const int n = 6 * A.K;
-  double acc[42];
-  for (int i = 0; i < 42; i++) acc[i] = 0;
-  const int b0 = A.ps_off[b], b1 = A.ps_off[b + 1];
-  for (int k = A.ps_off[a] + tid; k < A.ps_off[a + 1]; k += 128) {
-    const int e1 = A.ps_edges[k], g = A.ps_lm[k];
-    const int ld = g < P.nq ? 3 : 4;
-    const double* Y = L.Y + 24 * e1;
-    // lower_bound of g in the (sorted) landmark list of pose b
-    int lo = b0, hi = b1;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (A.ps_lm[mid] < g) lo = mid + 1;
-      else hi = mid;
-    }
-    for (int j = lo; j < b1 && A.ps_lm[j] == g; j++) {
-      const double* B2 = L.Hpl + 24 * A.ps_edges[j];
-      for (int r = 0; r < 6; r++)
-        for (int c = 0; c < 6; c++) {
-          double s = 0;
-          for (int q = 0; q < ld; q++) s += Y[r * 4 + q] * B2[c * 4 + q];
-          acc[r * 6 + c] += s;
-        }
-    }
-    if (a == b) {
-      const double* bl = S.bl + 4 * g;
-      for (int r = 0; r < 6; r++) {
-        double s = 0;
-        for (int q = 0; q < ld; q++) s += Y[r * 4 + q] * bl[q];
-        acc[36 + r] += s;
+// Schur complement, stage 1: one wave per chunk of <= kChunk edge pairs of one pose pair.
+// Each lane forms Y = Hpl_e1 Dinv_g on the fly and accumulates
+//   [0,36)  [e1==e2] Hpp_e1 - Y Hpl_e2^T,   [36,42) [e1==e2] bp_e1,   [42,48) [e1==e2] Y bl_g
+// then the wave sums its 64 lanes in lane order (LDS transpose).
+__global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active A, Sys S, double lambda) {
+  __shared__ double red[64 * 49];
+  const int c = blockIdx.x, lane = threadIdx.x;
+  const int beg = A.ch_beg[c], end = A.ch_end[c];
+  double acc[48];
+#pragma unroll
+  for (int v = 0; v < 48; v++) acc[v] = 0.0;
+  bool bad = false;
+  for (int k = beg + lane; k < end; k += 64) {
+    const int e1 = A.pp_e1[k], e2 = A.pp_e2[k];
+    const int g = P.elm[e1];
+    double D[16];
+    bad |= !lm_dinv(S.Hll + 16 * g, g < P.nq, lambda, D);
+    const double* H1 = L.Hpl + 24 * e1;
+    const double* H2 = L.Hpl + 24 * e2;
+    double B[24];
+#pragma unroll
+    for (int q = 0; q < 24; q++) B[q] = H2[q];
+    const bool diag = e1 == e2;
+#pragma unroll
+    for (int r = 0; r < 6; r++) {
+      const double h0 = H1[r * 4], h1 = H1[r * 4 + 1], h2 = H1[r * 4 + 2], h3 = H1[r * 4 + 3];
+      double y[4];
+#pragma unroll
+      for (int q = 0; q < 4; q++) y[q] = h0 * D[q] + h1 * D[4 + q] + h2 * D[8 + q] + h3 * D[12 + q];
+#pragma unroll
+      for (int cc = 0; cc < 6; cc++)
+        acc[r * 6 + cc] -= y[0] * B[cc * 4] + y[1] * B[cc * 4 + 1] + y[2] * B[cc * 4 + 2] + y[3] * B[cc * 4 + 3];
+      if (diag) {
+        const double* Hp = L.Hpp + 36 * e1;
+        const double* bl = S.bl + 4 * g;
+#pragma unroll
+        for (int cc = 0; cc < 6; cc++) acc[r * 6 + cc] += Hp[r * 6 + cc];
+        acc[36 + r] += L.bp[6 * e1 + r];
+        acc[42 + r] += y[0] * bl[0] + y[1] * bl[1] + y[2] * bl[2] + y[3] * bl[3];
       }
     }
   }
-  for (int i = 0; i < 42; i++) red[i][tid] = acc[i];
+  if (bad) atomicOr(S.fail, 1);
+#pragma unroll
+  for (int v = 0; v < 48; v++) red[lane * 49 + v] = acc[v];
   __syncthreads();
-  for (int s = 64; s > 0; s >>= 1) {
-    if (tid < s)
-      for (int i = 0; i < 42; i++) red[i][tid] += red[i][tid + s];
+  if (lane < 48) {
+    double s = 0;
+    for (int l = 0; l < 64; l++) s += red[l * 49 + lane];
+    S.chunk[48 * c + lane] = s;
+  }
+}
+
+// Schur complement, stage 2: one thread per (pose pair, entry); chunks summed in order.
+//   S_ab = [a==b] lambda I + sum chunks,  bp_a,  bs_a = bp_a - sum Y bl  (solved in place in x)
+__global__ __launch_bounds__(256) void pair_final_kernel(Active A, Sys S, double lambda) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= A.npairs * 42) return;
+  const int pr = idx / 42, v = idx - 42 * pr;
+  const int a = A.pairs[2 * pr], b = A.pairs[2 * pr + 1], n = 6 * A.K;
+  const int c0 = A.pair_choff[pr], c1 = A.pair_choff[pr + 1];
+  double s = 0, s2 = 0;
+#pragma unroll 8
+  for (int c = c0; c < c1; c++) {
+    s += S.chunk[48 * c + v];
+    if (v >= 36) s2 += S.chunk[48 * c + v + 6];
+  }
+  if (v < 36) {
+    const int r = v / 6, cc = v - 6 * r;
+    const double val = s + ((a == b && r == cc) ? lambda : 0.0);
+    S.S[(size_t)(6 * a + r) * n + 6 * b + cc] = val;
+    if (a != b) S.S[(size_t)(6 * b + cc) * n + 6 * a + r] = val;
+  } else if (a == b) {
+    const int r = v - 36;
+    S.bp[6 * a + r] = s;
+    S.x[6 * a + r] = s - s2;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Dense Cholesky of the reduced camera system (n = 6K), matrix in LDS (odd row stride),
+// blocked by the 6x6 pose blocks: K sequential steps, each
+//   (1) factor the 6x6 diagonal block (one thread, fully unrolled registers),
+//   (2) panel: every row below solves x L_dd^T = a (one thread per row),
+//   (3) rank-6 update of the trailing lower triangle (16x16 thread grid),
+// then blocked forward / backward substitution on the right-hand side in LDS.
+// ---------------------------------------------------------------------------
+constexpr int kCholLdsMax = 138;  // n (n|1) + 2n doubles <= 160 KB of LDS
+
+__global__ __launch_bounds__(256) void cholesky_lds_kernel(Sys S, int n) {
+  extern __shared__ double Al[];
+  __shared__ int bad;
+  const int ld = n | 1;
+  double* rdg = Al + (size_t)n * ld;  // [n] reciprocal diagonal of L
+  double* xs = rdg + n;               // [n] right-hand side -> solution
+  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  if (*S.fail) return;
+  for (int i = ty; i < n; i += 16)
+    for (int k = tx; k <= i; k += 16) Al[i * ld + k] = S.S[(size_t)i * n + k];
+  for (int i = tid; i < n; i += 256) xs[i] = S.x[i];
+  if (tid == 0) bad = 0;
+  __syncthreads();
+  const int K = n / 6;
+  for (int s = 0; s < K; s++) {
+    const int c0 = 6 * s;
+    double* Ld = Al + c0 * ld + c0;
+    if (tid == 0) {  // (1)
+      double a[6][6];
+#pragma unroll
+      for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int k = 0; k <= i; k++) a[i][k] = Ld[i * ld + k];
+      bool ok = true;
+#pragma unroll
+      for (int j = 0; j < 6; j++) {
+        const double v = a[j][j];
+        ok = ok && v > 0;
+        const double d = sqrt(v), r = 1.0 / d;
+        a[j][j] = d;
+        rdg[c0 + j] = r;
+#pragma unroll
+        for (int i = j + 1; i < 6; i++) a[i][j] *= r;
+#pragma unroll
+        for (int i = j + 1; i < 6; i++)
+#pragma unroll
+          for (int k = j + 1; k <= i; k++) a[i][k] -= a[i][j] * a[k][j];
+      }
+#pragma unroll
+      for (int i = 0; i < 6; i++)
+#pragma unroll
+        for (int k = 0; k <= i; k++) Ld[i * ld + k] = a[i][k];
+      if (!ok) bad = 1;
+    }
+    __syncthreads();
+    if (bad) {  // LDS flag after the barrier: uniform
+      if (tid == 0) atomicOr(S.fail, 1);
+      return;
+    }
+    double L6[21], r6[6];  // the factored diagonal block, broadcast to every thread
+#pragma unroll
+    for (int i = 0, q = 0; i < 6; i++)
+#pragma unroll
+      for (int k = 0; k < i; k++, q++) L6[q] = Ld[i * ld + k];
+#pragma unroll
+    for (int k = 0; k < 6; k++) r6[k] = rdg[c0 + k];
+    for (int i = c0 + 6 + tid; i < n; i += 256) {  // (2)
+      double* row = Al + i * ld + c0;
+      double x[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) x[k] = row[k];
+#pragma unroll
+      for (int k = 0, q = 0; k < 6; k++) {
+        double v = x[k];
+#pragma unroll
+        for (int l = 0; l < k; l++, q++) v -= x[l] * L6[q];
+        x[k] = v * r6[k];
+      }
+#pragma unroll
+      for (int k = 0; k < 6; k++) row[k] = x[k];
+    }
+    __syncthreads();
+    const int r0 = c0 + 6;  // (3)
+    for (int i = r0 + ty; i < n; i += 16) {
+      double li[6];
+#pragma unroll
+      for (int l = 0; l < 6; l++) li[l] = Al[i * ld + c0 + l];
+      for (int k = r0 + tx; k <= i; k += 16) {
+        const double* lk = Al + k * ld + c0;
+        double t = Al[i * ld + k];
+#pragma unroll
+        for (int l = 0; l < 6; l++) t -= li[l] * lk[l];
+        Al[i * ld + k] = t;
+      }
+    }
     __syncthreads();
   }
-  if (tid < 36) {
-    const int r = tid / 6, c = tid % 6;
-    double v = -red[tid][0];
-    if (a == b) v += S.Hpp[36 * a + tid] + (r == c ? lambda : 0.0);
-    S.S[(size_t)(6 * a + r) * n + 6 * b + c] = v;
-    if (a != b) S.S[(size_t)(6 * b + c) * n + 6 * a + r] = v;
+  for (int s = 0; s < K; s++) {  // L y = b
+    const int c0 = 6 * s;
+    if (tid == 0) {
+      double y[6];
+#pragma unroll
+      for (int k = 0; k < 6; k++) {
+        double v = xs[c0 + k];
+#pragma unroll
+        for (int l = 0; l < k; l++) v -= y[l] * Al[(c0 + k) * ld + c0 + l];
+        y[k] = v * rdg[c0 + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 6; k++) xs[c0 + k] = y[k];
+    }
+    __syncthreads();
+    for (int i = c0 + 6 + tid; i < n; i += 256) {
+      const double* row = Al + i * ld + c0;
+      double v = xs[i];
+#pragma unroll
+      for (int l = 0; l < 6; l++) v -= row[l] * xs[c0 + l];
+      xs[i] = v;
+    }
+    __syncthreads();
   }
-  if (a == b && tid < 6) S.x[6 * a + tid] = S.bp[6 * a + tid] - red[36 + tid][0];  // bs into x (solved in place)
+  for (int s = K - 1; s >= 0; s--) {  // L^T x = y
+    const int c0 = 6 * s;
+    if (tid == 0) {
+      double z[6];
+#pragma unroll
+      for (int k = 5; k >= 0; k--) {
+        double v = xs[c0 + k];
+#pragma unroll
+        for (int l = k + 1; l < 6; l++) v -= z[l] * Al[(c0 + l) * ld + c0 + k];
+        z[k] = v * rdg[c0 + k];
+      }
+#pragma unroll
+      for (int k = 0; k < 6; k++) xs[c0 + k] = z[k];
+    }
+    __syncthreads();
+    for (int i = tid; i < c0; i += 256) {
+      double v = xs[i];
+#pragma unroll
+      for (int l = 0; l < 6; l++) v -= Al[(c0 + l) * ld + i] * xs[c0 + l];
+      xs[i] = v;
+    }
+    __syncthreads();
+  }
+  for (int i = tid; i < n; i += 256) S.x[i] = xs[i];
 }
 
-// ---------------------------------------------------------------------------
-// Dense Cholesky of the reduced camera system, one workgroup (n = 6K <= 384).
-// Right-looking, lower triangle in place; rhs in x[0:n) overwritten by the solution.
-// ---------------------------------------------------------------------------
+// larger systems: one workgroup on global memory
+
 __global__ __launch_bounds__(256) void cholesky_kernel(Sys S, int n) {
   __shared__ double red[256];
   __shared__ int bad;
@@ -568,7 +911,6 @@ __global__ __launch_bounds__(256) void cholesky_kernel(Sys S, int n) {
     }
     __syncthreads();
   }
-  // L y = b
   for (int i = 0; i < n; i++) {
     double s = 0;
     for (int k = tid; k < i; k += 256) s += A[(size_t)i * n + k] * x[k];
@@ -581,7 +923,6 @@ __global__ __launch_bounds__(256) void cholesky_kernel(Sys S, int n) {
     if (tid == 0) x[i] = (x[i] - red[0]) / A[(size_t)i * n + i];
     __syncthreads();
   }
-  // L^T x = y
   for (int i = n - 1; i >= 0; i--) {
     double s = 0;
     for (int k = i + 1 + tid; k < n; k += 256) s += A[(size_t)k * n + i] * x[k];
@@ -596,96 +937,77 @@ __global__ __launch_bounds__(256) void cholesky_kernel(Sys S, int n) {
   }
 }
 
-// xl = Dinv (bl - sum_e Hpl_e^T xp)
-__global__ __launch_bounds__(256) void backsub_kernel(Problem P, Lin L, Active A, Sys S) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= A.nL) return;
-  double* xl = S.x + 6 * A.K + 4 * g;
-  if (!A.lm_act[g] || *S.fail) {
-    for (int i = 0; i < 4; i++) xl[i] = 0;
-    return;
-  }
-  const int ld = g < P.nq ? 3 : 4;
-  double c[4];
-  for (int i = 0; i < ld; i++) c[i] = S.bl[4 * g + i];
-  for (int k = A.lm_off[g]; k < A.lm_off[g + 1]; k++) {
-    const int e = A.lm_edges[k];
-    const int a = A.pidx[P.epose[e]];
-    if (a < 0) continue;
-    const double* B = L.Hpl + 24 * e;
-    for (int j = 0; j < ld; j++) {
-      double s = 0;
-      for (int i = 0; i < 6; i++) s += B[i * 4 + j] * S.x[6 * a + i];
-      c[j] -= s;
-    }
-  }
-  const double* D = S.Dinv + 16 * g;
-  for (int i = 0; i < ld; i++) {
-    double s = 0;
-    for (int j = 0; j < ld; j++) s += D[i * ld + j] * c[j];
-    xl[i] = s;
-  }
-  for (int i = ld; i < 4; i++) xl[i] = 0;
-}
-
-// oplus: poses T <- exp(x) T, points += x, lines oplus(x)
-__global__ __launch_bounds__(256) void apply_kernel(Problem P, Active A, Sys S) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (*S.fail) return;
-  if (i < A.K) {
-    double* Tp = P.T + 8 * A.pose_of[i];
-    const SE3 T = load_T(Tp);
-    const SE3 r = se3_mul(se3_exp(S.x + 6 * i), T);
-    for (int k = 0; k < 4; k++) Tp[k] = r.q[k];
-    for (int k = 0; k < 3; k++) Tp[4 + k] = r.t[k];
-  } else if (i < A.K + A.nL) {
-    const int g = i - A.K;
-    if (!A.lm_act[g]) return;
-    const double* xl = S.x + 6 * A.K + 4 * g;
-    if (g < P.nq) {
-      for (int k = 0; k < 3; k++) P.X[3 * g + k] += xl[k];
-    } else {
-      line_oplus(P.L + 6 * (g - P.nq), xl);
-    }
-  }
-}
-
-// chi2 = sum of block partials (fixed order); scale = x.(lambda x + b) over active vertices
-__global__ __launch_bounds__(256) void finish_kernel(Problem P, Active A, Sys S, int nblocks, int with_scale,
-                                                     double lambda) {
+// Back-substitution xl = Dinv (bl - sum_e Hpl_e^T xp) fused with the candidate state
+// (poses T <- exp(xp) T, points += xl, lines oplus(xl); inactive vertices copied: ping-pong
+// buffers) and the LM scale x.(lambda x + b) per block.
+__global__ __launch_bounds__(256) void update_kernel(Problem P, Lin L, Active A, Sys S, double lambda) {
   __shared__ double red[256];
-  const int tid = threadIdx.x;
-  double c = 0;
-  for (int i = tid; i < nblocks; i += 256) c += S.partial[i];
-  red[tid] = c;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (tid < s) red[tid] += red[tid + s];
-    __syncthreads();
-  }
-  if (tid == 0) S.out[0] = red[0];
-  __syncthreads();
-  if (!with_scale) return;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool failed = *S.fail != 0;
   double sc = 0;
-  for (int i = tid; i < 6 * A.K; i += 256) sc += S.x[i] * (lambda * S.x[i] + S.bp[i]);
-  for (int g = tid; g < A.nL; g += 256) {
-    if (!A.lm_act[g]) continue;
-    const int ld = g < P.nq ? 3 : 4;
-    for (int k = 0; k < ld; k++) {
-      const double xv = S.x[6 * A.K + 4 * g + k];
-      sc += xv * (lambda * xv + S.bl[4 * g + k]);
+  if (i < P.np) {
+    const double* Tp = P.T + 8 * i;
+    double* Tq = P.Tn + 8 * i;
+    const int a = A.pidx[i];
+    if (a >= 0 && !failed) {
+      const double* xp = S.x + 6 * a;
+      const SE3 r = se3_mul(se3_exp(xp), load_T(Tp));
+      for (int k = 0; k < 4; k++) Tq[k] = r.q[k];
+      for (int k = 0; k < 3; k++) Tq[4 + k] = r.t[k];
+      Tq[7] = 0;
+      for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + S.bp[6 * a + k]);
+    } else {
+      for (int k = 0; k < 8; k++) Tq[k] = Tp[k];
+    }
+  } else if (i < P.np + P.nq + P.nl) {
+    const int g = i - P.np;
+    const bool point = g < P.nq;
+    const bool upd = A.lm_act[g] && !failed;
+    double xl[4] = {0, 0, 0, 0};
+    if (upd) {
+      double c[4];
+      for (int k = 0; k < 4; k++) c[k] = S.bl[4 * g + k];
+      const int k0 = A.lm_off[g], k1 = A.lm_off[g + 1];
+      for (int kb = k0; kb < k1; kb += 4) {
+        int es[4], as[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const int k = min(kb + u, k1 - 1);
+          es[u] = A.lm_edges[k];
+          as[u] = kb + u < k1 ? A.lm_pose[k] : -1;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+          const double* B = L.Hpl + 24 * es[u];
+          const double* xp = S.x + 6 * max(as[u], 0);
+#pragma unroll
+          for (int j = 0; j < 4; j++) {
+            double s = 0;
+#pragma unroll
+            for (int r = 0; r < 6; r++) s += B[r * 4 + j] * xp[r];
+            c[j] -= as[u] >= 0 ? s : 0.0;
+          }
+        }
+      }
+      double D[16];
+      if (!lm_dinv(S.Hll + 16 * g, point, lambda, D)) atomicOr(S.fail, 1);
+#pragma unroll
+      for (int r = 0; r < 4; r++) xl[r] = D[r * 4] * c[0] + D[r * 4 + 1] * c[1] + D[r * 4 + 2] * c[2] + D[r * 4 + 3] * c[3];
+#pragma unroll
+      for (int k = 0; k < 4; k++) sc += xl[k] * (lambda * xl[k] + S.bl[4 * g + k]);
+    }
+    if (point) {
+      for (int k = 0; k < 3; k++) P.Xn[3 * g + k] = P.X[3 * g + k] + xl[k];
+    } else {
+      const int l = g - P.nq;
+      double Lv[6];
+      for (int k = 0; k < 6; k++) Lv[k] = P.L[6 * l + k];
+      if (upd) line_oplus(Lv, xl);
+      for (int k = 0; k < 6; k++) P.Ln[6 * l + k] = Lv[k];
     }
   }
-  red[tid] = sc;
-  __syncthreads();
-  for (int s = 128; s > 0; s >>= 1) {
-    if (tid < s) red[tid] += red[tid + s];
-    __syncthreads();
-  }
-  if (tid == 0) {
-    S.out[1] = red[0];
-    S.out[3] = (double)*S.fail;
-  }
+  const double s = block_sum256(sc, red);
+  if (threadIdx.x == 0) S.partial2[blockIdx.x] = s;
 }
 
 // outlier levels after the first optimize / final inlier flags (g2o_optimization.cc:176-231)
@@ -713,40 +1035,62 @@ __global__ __launch_bounds__(256) void classify_kernel(Problem P, Lin L, int E, 
 }
 
 // ---------------------------------------------------------------------------
-int errors_blocks(int Ea) { return (Ea + 255) / 256; }
+int errors_blocks(int Ea) { return Ea > 0 ? (Ea + 255) / 256 : 1; }
+int update_blocks(const Problem& P) {
+  const int nv = P.np + P.nq + P.nl;
+  return nv > 0 ? (nv + 255) / 256 : 1;
+}
 
-hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& S, int nblocks, hipStream_t s) {
-  if (nblocks > 0) hipLaunchKernelGGL(errors_kernel, dim3(nblocks), dim3(256), 0, s, P, L, A, S.partial);
-  hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(256), 0, s, P, A, S, nblocks, 0, 0.0);
+hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(errors_kernel, dim3(errors_blocks(A.Ea)), dim3(256), 0, s, P, L, A, S, 0, seq);
   return hipGetLastError();
 }
 
 hipError_t linearize(const Problem& P, const Lin& L, const Active& A, hipStream_t s) {
-  if (A.Ea > 0) hipLaunchKernelGGL(linearize_kernel, dim3((A.Ea + 127) / 128), dim3(128), 0, s, P, L, A);
+  const int npt = A.Ea - A.n_line_edges;
+  if (npt > 0) hipLaunchKernelGGL(linearize_points_kernel, dim3((npt + 255) / 256), dim3(256), 0, s, P, L, A);
+  if (A.n_line_edges > 0)
+    hipLaunchKernelGGL(linearize_lines_kernel, dim3((A.n_line_edges + 3) / 4), dim3(256), 0, s, P, L, A);
   return hipGetLastError();
 }
 
-hipError_t reduce_blocks(const Problem& P, const Lin& L, const Active& A, Sys& S, hipStream_t s) {
+hipError_t reduce_blocks(const Problem& P, const Lin& L, const Active& A, Sys& S, bool with_maxdiag,
+                         hipStream_t s) {
   if (A.nL > 0) hipLaunchKernelGGL(landmark_reduce_kernel, dim3((A.nL + 255) / 256), dim3(256), 0, s, P, L, A, S);
-  if (A.K > 0) hipLaunchKernelGGL(pose_reduce_kernel, dim3(A.K), dim3(128), 0, s, P, L, A, S);
+  if (with_maxdiag && A.K > 0) hipLaunchKernelGGL(pose_diag_kernel, dim3(A.K), dim3(256), 0, s, P, L, A, S);
   return hipGetLastError();
 }
 
-hipError_t schur(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, hipStream_t s) {
-  if (A.nL > 0)
-    hipLaunchKernelGGL(landmark_schur_kernel, dim3((A.nL + 255) / 256), dim3(256), 0, s, P, L, A, S, lambda);
-  if (A.npairs > 0) hipLaunchKernelGGL(pair_schur_kernel, dim3(A.npairs), dim3(128), 0, s, P, L, A, S, lambda);
+hipError_t post(Sys& S, unsigned long long seq, hipStream_t s) {
+  hipLaunchKernelGGL(post_kernel, dim3(1), dim3(64), 0, s, S, seq);
   return hipGetLastError();
 }
 
-hipError_t solve_update(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, hipStream_t s) {
-  if (A.K > 0) hipLaunchKernelGGL(cholesky_kernel, dim3(1), dim3(256), 0, s, S, 6 * A.K);
-  if (A.nL > 0) hipLaunchKernelGGL(backsub_kernel, dim3((A.nL + 255) / 256), dim3(256), 0, s, P, L, A, S);
-  const int n = A.K + A.nL;
-  if (n > 0) hipLaunchKernelGGL(apply_kernel, dim3((n + 255) / 256), dim3(256), 0, s, P, A, S);
-  const int nb = errors_blocks(A.Ea);
-  if (nb > 0) hipLaunchKernelGGL(errors_kernel, dim3(nb), dim3(256), 0, s, P, L, A, S.partial);
-  hipLaunchKernelGGL(finish_kernel, dim3(1), dim3(256), 0, s, P, A, S, nb, 1, lambda);
+hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
+                 hipStream_t s) {
+  if (A.nch > 0) hipLaunchKernelGGL(pair_chunk_kernel, dim3(A.nch), dim3(64), 0, s, P, L, A, S, lambda);
+  if (A.npairs > 0)
+    hipLaunchKernelGGL(pair_final_kernel, dim3((A.npairs * 42 + 255) / 256), dim3(256), 0, s, A, S, lambda);
+  const int n = 6 * A.K;
+  if (n > 0 && n <= kCholLdsMax) {
+    static bool attr = false;
+    if (!attr) {
+      hipError_t e = hipFuncSetAttribute((const void*)cholesky_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)(sizeof(double) * (kCholLdsMax * (kCholLdsMax | 1) + 2 * kCholLdsMax)));
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+    const size_t bytes = sizeof(double) * ((size_t)n * (n | 1) + 2 * n);
+    hipLaunchKernelGGL(cholesky_lds_kernel, dim3(1), dim3(256), bytes, s, S, n);
+  } else if (n > 0) {
+    hipLaunchKernelGGL(cholesky_kernel, dim3(1), dim3(256), 0, s, S, n);
+  }
+  const int nbu = update_blocks(P);
+  hipLaunchKernelGGL(update_kernel, dim3(nbu), dim3(256), 0, s, P, L, A, S, lambda);
+  Problem Pn = P;  // cost of the candidate state
+  Pn.T = P.Tn; Pn.X = P.Xn; Pn.L = P.Ln;
+  hipLaunchKernelGGL(errors_kernel, dim3(errors_blocks(A.Ea)), dim3(256), 0, s, Pn, L, A, S, nbu, seq);
   return hipGetLastError();
 }
 

@@ -10,9 +10,12 @@ namespace ba {
 // 2 mono line, 3 stereo line.  Unified edge arrays, obs padded to 8 doubles.
 struct Problem {
   const double* cams;    // [nc][5] fx fy cx cy bf
-  double* T;             // [np][8] T_cw: q (w x y z), t (x y z), pad
+  double* T;             // [np][8] T_cw: q (w x y z), t (x y z), pad   (current state)
   double* X;             // [nq][3]
   double* L;             // [nl][6]
+  double* Tn;            // candidate state written by the update (ping-pong)
+  double* Xn;
+  double* Ln;
   int np, nq, nl;
   const int8_t* etype;   // [E]
   const int* epose;      // [E]
@@ -30,8 +33,7 @@ struct Lin {             // per-edge linearisation records (indexed by edge id)
   double* bp;            // [E][6]
   double* Hll;           // [E][16]
   double* bl;            // [E][4]
-  double* Hpl;           // [E][24]  6 x 4 (row stride 4)
-  double* Y;             // [E][24]  Hpl * Dinv
+  double* Hpl;           // [E][24]  6 x 4 (row stride 4; column 3 is zero for points)
 };
 
 struct Active {          // active structure of one optimize() phase
@@ -40,37 +42,59 @@ struct Active {          // active structure of one optimize() phase
   const int* pidx;       // [np] reduced pose index or -1
   const int* lm_off;     // [nL+1] CSR over active edges by landmark
   const int* lm_edges;
+  const int* lm_pose;    // [Ea] reduced pose of lm_edges[k] (or -1)
   const uint8_t* lm_act; // [nL]
-  const int* pose_of;    // [K] pose id of reduced index
-  const int* ps_off;     // [K+1] CSR by reduced pose, sorted by landmark
+  const int* ps_off;     // [K+1] CSR of active edges by reduced pose
   const int* ps_edges;
-  const int* ps_lm;      // landmark of ps_edges[i] (sorted key)
-  const int* pairs;      // [npairs][2] reduced (a <= b)
+  const int* pairs;      // [npairs][2] reduced pose pairs (a <= b)
   int npairs;
+  const int* pair_choff; // [npairs+1] CSR of Schur chunks per pose pair
+  const int* ch_beg;     // [nch] edge-pair range [beg, end) of each chunk
+  const int* ch_end;
+  int nch;
+  const int* pp_e1;      // edge pairs (e1 of pose a, e2 of pose b, same landmark), grouped by pose pair
+  const int* pp_e2;
+  int n_line_edges;      // active line edges are edges[Ea - n_line_edges .. Ea) (input order)
   int K, nL;
   int robust;
 };
 
-struct Sys {
-  double* Hll;           // [nL][16]
-  double* bl;            // [nL][4]
-  double* Dinv;          // [nL][16]
-  double* Hpp;           // [K][36]
-  double* bp;            // [K][6]
-  double* S;             // [6K][6K]
-  double* x;             // [6K + 4 nL]  (landmark l at 6K + 4l)
-  double* partial;       // [nblocks] scratch for reductions
-  double* out;           // [8]: 0 chi2, 1 scale, 2 maxdiag, 3 fail flag
-  int* fail;             // [1]
+struct Mail {            // pinned, host-mapped: the per-trial result the host spins on
+  double v[4];           // chi2, scale, maxdiag, fail
+  unsigned long long seq;
+  unsigned long long pad[3];
 };
 
-hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& S, int nblocks, hipStream_t s);
+struct Sys {
+  double* Hll;           // [nL][16]  (points: 3x3 at stride 3)
+  double* bl;            // [nL][4]
+  double* bp;            // [K][6]   pose gradient (undamped), for the LM scale
+  double* S;             // [6K][6K] reduced camera system
+  double* x;             // [6K]     bs on entry of the solve, xp on exit
+  double* chunk;         // [nch][48] Schur chunk partials
+  double* partial;       // [>= error blocks] chi2 partials
+  double* partial2;      // [>= update blocks] scale partials
+  double* out;           // [8]: 0 chi2, 1 scale, 2 maxdiag, 3 fail
+  int* fail;             // [1]
+  unsigned* counter;     // [1] last-block ticket of the error kernel
+  Mail* mail;            // device view of the mailbox
+};
+
+constexpr int kChunk = 128;  // edge pairs per Schur chunk (2 per lane)
+
+// errors (+ fused final reduction and mailbox post with sequence number seq)
+hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq,
+                          hipStream_t s);
 hipError_t linearize(const Problem& P, const Lin& L, const Active& A, hipStream_t s);
-hipError_t reduce_blocks(const Problem& P, const Lin& L, const Active& A, Sys& S, hipStream_t s);
-hipError_t schur(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, hipStream_t s);
-hipError_t solve_update(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, hipStream_t s);
+hipError_t reduce_blocks(const Problem& P, const Lin& L, const Active& A, Sys& S, bool with_maxdiag,
+                         hipStream_t s);
+hipError_t post(Sys& S, unsigned long long seq, hipStream_t s);
+// one LM trial: Schur complement, Cholesky, back-substitution + candidate state, its cost
+hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
+                 hipStream_t s);
 hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8_t* inlier, int final_pass,
                     hipStream_t s);
+int update_blocks(const Problem& P);
 int errors_blocks(int Ea);
 
 }  // namespace ba

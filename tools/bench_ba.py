@@ -1,0 +1,36 @@
+"""Local-BA timing on the GPU (C3-sized synthetic problems): wall time per LocalmapOptimization call."""
+import argparse
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+import rspl_loader  # noqa: E402
+
+pkg = rspl_loader.load()
+pkg.capi.load()
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--poses", type=int, default=10)
+    ap.add_argument("--points", type=int, default=4000)
+    ap.add_argument("--lines", type=int, default=100)
+    ap.add_argument("--iters", type=int, default=10)
+    a = ap.parse_args()
+    ba = pkg.LocalBA(max_poses=max(16, a.poses), max_points=a.points + 100, max_lines=a.lines + 10, max_edges=80000)
+    probs = [pkg.synthetic.ba_problem(n_poses=a.poses, n_points=a.points, n_lines=a.lines, seed=s)[0] for s in range(3)]
+    for p in probs:
+        ba.run(p)
+    t = time.perf_counter()
+    for i in range(a.iters):
+        r = ba.run(probs[i % 3])
+    dt = (time.perf_counter() - t) / a.iters * 1e3
+    e = sum(probs[0].n_edges(k) for k in ("mono", "stereo", "mono_line", "stereo_line"))
+    print(f"BA {a.poses} poses {probs[0].points.shape[0]} pts {probs[0].lines.shape[0]} lines {e} edges: "
+          f"{dt:.2f} ms/call, iters {r.iters_first}+{r.iters_second}")
+
+
+if __name__ == "__main__":
+    main()
