@@ -29,8 +29,10 @@ struct rspl_sg {
   float *wqkv, *bqkv, *wm, *bm, *w1, *b1, *w2, *b2;  // [18] stacked
   float *wf, *bf, *bin;
   // activations
-  float *kin, *h1, *h2, *X, *QKV, *O, *MSG, *HID, *cpl, *Z, *part, *val0;
-  unsigned *ctr, *err;
+  float *kin, *h1, *h2, *X, *QKV, *O, *MSG, *HID, *cpl, *Z, *val0;
+  unsigned long long* part;
+  unsigned* err;
+  unsigned sk_seq = 0;
   int *max0, *max1, *n0, *n1;
   int32_t *idx0, *idx1;
   double *ms0, *ms1, *f0, *f1;
@@ -65,7 +67,7 @@ void carve(F& ar, rspl_sg* s) {
   take(s->kin, T * kKencIn); take(s->h1, T * 256); take(s->h2, T * 256);
   take(s->X, T * 256); take(s->QKV, T * 768); take(s->O, T * 256); take(s->MSG, T * 256); take(s->HID, T * 512);
   take(s->cpl, B * ld * ld); take(s->Z, B * ld * ld); take(s->part, B * 2 * s->G * ld);
-  take(s->ctr, B); take(s->err, B);
+  take(s->err, B);
   take(s->max0, B * s->nmax); take(s->val0, B * s->nmax); take(s->max1, B * s->nmax);
   take(s->idx0, B * s->nmax); take(s->idx1, B * s->nmax); take(s->ms0, B * s->nmax); take(s->ms1, B * s->nmax);
   take(s->n0, B); take(s->n1, B);
@@ -203,7 +205,11 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
   s->B = s->cfg.max_batch;
   s->nmax = cfg->max_keypoints;  // output stride per pair (rspl.h)
   s->ld = s->nmax + 1;
-  s->G = std::min(32, std::max(1, (s->ld + 25) / 26));
+  {  // sinkhorn workgroups per pair: ~26 rows each, a power of two (compile-time fan-in of the exchange)
+    const int g0 = std::max(1, (s->ld + 25) / 26);
+    s->G = 1;
+    while (s->G < g0 && s->G < 32) s->G <<= 1;
+  }
   if (s->B * s->G > 256) {
     set_error("max_batch * sinkhorn workgroups (%d) exceeds the CU count: co-residency required", s->B * s->G);
     delete s;
@@ -213,6 +219,11 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
   carve(sz, s);
   if ((rc = s->arena.reserve(sz.used))) { delete s; return rc; }
   carve(s->arena, s);
+  if (hipMemset(s->part, 0, sizeof(unsigned long long) * 2 * s->B * s->G * s->ld) != hipSuccess) {
+    set_error("sinkhorn exchange buffer init failed");
+    rspl_sg_destroy(s);
+    return RSPL_E_DEVICE;
+  }
   const size_t nm = s->nmax;
   if (s->timer.init(RSPL_SG_STAGES) != RSPL_OK || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
       hipHostMalloc(&s->h_f, sizeof(double) * nm * 259 * 2) != hipSuccess ||
@@ -302,10 +313,9 @@ extern "C" int rspl_sg_infer_device(rspl_sg* s, int B, const double* d_feat0, co
   RSPL_HIP(sg::bins(bn, B, st));
   s->timer.mark(3, st);
   // log_optimal_transport (superglue.py:185-205)
-  RSPL_HIP(hipMemsetAsync(s->ctr, 0, sizeof(unsigned) * B, st));
   RSPL_HIP(hipMemsetAsync(s->err, 0, sizeof(unsigned) * B, st));
   sg::SinkArgs sk{};
-  sk.cpl = s->cpl; sk.Z = s->Z; sk.part = s->part; sk.ctr = s->ctr; sk.err = s->err; sk.n0 = d_n0; sk.n1 = d_n1;
+  sk.cpl = s->cpl; sk.Z = s->Z; sk.part = s->part; sk.seq = s->sk_seq = (s->sk_seq % 0xFFFFFu) + 1; sk.err = s->err; sk.n0 = d_n0; sk.n1 = d_n1;
   sk.nmax = nm; sk.G = s->G; sk.iters = s->cfg.sinkhorn_iterations;
   RSPL_HIP(sg::sinkhorn(sk, B, st));
   s->timer.mark(4, st);

@@ -286,40 +286,46 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
       __hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-template <bool SLAB_IN_LDS>
-__global__ __launch_bounds__(256) void sinkhorn_kernel(SinkArgs a) {
+constexpr int kSinkThreads = 1024;  // 4 waves per SIMD: latency hiding for the LDS/exp chains
+
+template <bool SLAB_IN_LDS, int G>
+__global__ __launch_bounds__(kSinkThreads) void sinkhorn_kernel(SinkArgs a) {
   extern __shared__ float sm[];
-  const int p = blockIdx.y, g = blockIdx.x, G = a.G;
+  const int p = blockIdx.y, g = blockIdx.x;
   const int m = a.n0[p], n = a.n1[p];
   if (m <= 0 || n <= 0) return;
   const int R = m + 1, Cc = n + 1, ld = a.nmax + 1;
   const int rows = (R + G - 1) / G;
   const int r0 = g * rows;
   const int nr = max(0, min(R, r0 + rows) - r0);
+  constexpr int NW = kSinkThreads / 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const float* Cg = a.cpl + (size_t)p * ld * ld + (size_t)r0 * ld;
   float* u = sm;
   float* v = u + rows;
   float* flag = v + ld;     // timeout broadcast
-  float* Cs = flag + 1;     // slab, only used when SLAB_IN_LDS
+  float* cm = flag + 1;     // [2][512] column half-partials: max
+  float* cs = cm + 1024;    //                                sum
+  float* Cs = cs + 1024;    // slab, only used when SLAB_IN_LDS
   const float* Cr = SLAB_IN_LDS ? Cs : Cg;
   if constexpr (SLAB_IN_LDS) {
-    for (int i = tid; i < nr * Cc; i += 256) {
-      const int r = i / Cc, j = i % Cc;
+    for (int i = tid; i < nr * Cc; i += kSinkThreads) {
+      const int r = i / Cc, j = i - r * Cc;
       Cs[r * ld + j] = Cg[(size_t)r * ld + j];
     }
   }
-  for (int j = tid; j < Cc; j += 256) v[j] = 0.f;
+  for (int j = tid; j < Cc; j += kSinkThreads) v[j] = 0.f;
   // log_mu / log_nu (superglue.py:198-200), float arithmetic as the module
   const float fm = (float)m, fn = (float)n;
   const float norm = -logf(fm + fn);
   const float lmu_bin = logf(fn) + norm, lnu_bin = logf(fm) + norm;
-  unsigned* ctr = a.ctr + p;
   if (tid == 0) *flag = 0.f;
   __syncthreads();
+  const int half = tid >> 9, jj = tid & 511;
+  const int rh = (nr + 1) >> 1, ra = half ? rh : 0, rb = half ? nr : rh;
   for (int it = 0; it < a.iters; it++) {
-    // u_i = log_mu_i - LSE_j(C_ij + v_j)
-    for (int r = wv; r < nr; r += 4) {
+    // u_i = log_mu_i - LSE_j(C_ij + v_j): one wave per row
+    for (int r = wv; r < nr; r += NW) {
       const float* row = Cr + (size_t)r * ld;
       float mx = -INFINITY;
       for (int j = lane; j < Cc; j += 64) mx = fmaxf(mx, row[j] + v[j]);
@@ -330,53 +336,83 @@ __global__ __launch_bounds__(256) void sinkhorn_kernel(SinkArgs a) {
       if (lane == 0) u[r] = ((r0 + r) < m ? norm : lmu_bin) - (logf(s) + mx);
     }
     __syncthreads();
-    // column partial LSE over this slab, published write-through
-    float* part = a.part + ((size_t)(p * 2 + (it & 1)) * G) * ld;
-    for (int j = tid; j < Cc; j += 256) {
-      float mx = -INFINITY;
-      for (int r = 0; r < nr; r++) mx = fmaxf(mx, Cr[(size_t)r * ld + j] + u[r]);
-      float s = 0.f;
-      for (int r = 0; r < nr; r++) s += expf(Cr[(size_t)r * ld + j] + u[r] - mx);
-      st_sc1(part + (size_t)g * ld + j, nr ? logf(s) + mx : -INFINITY);
+    // column partial LSE over this slab (two row halves merged in LDS), published as tagged
+    // 8-byte granules (value + tag in one single-copy-atomic write-through store: no flag,
+    // no arrival counter); slots double-buffered by iteration parity
+    unsigned long long* part = a.part + ((size_t)(p * 2 + (it & 1)) * G) * ld;
+    const unsigned tag = (a.seq << 12) | (unsigned)(it + 1);
+    for (int c0 = 0; c0 < Cc; c0 += 512) {
+      const int j = c0 + jj;
+      if (j < Cc) {
+        float mx = -INFINITY;
+#pragma unroll 4
+        for (int r = ra; r < rb; r++) mx = fmaxf(mx, Cr[(size_t)r * ld + j] + u[r]);
+        float s = 0.f;
+#pragma unroll 4
+        for (int r = ra; r < rb; r++) s += expf(Cr[(size_t)r * ld + j] + u[r] - mx);
+        cm[half * 512 + jj] = mx;
+        cs[half * 512 + jj] = s;
+      }
+      __syncthreads();
+      if (half == 0 && j < Cc) {
+        const float m0 = cm[jj], m1 = cm[512 + jj];
+        const float M = fmaxf(m0, m1);
+        float s = 0.f;
+        if (m0 != -INFINITY) s += cs[jj] * expf(m0 - M);
+        if (m1 != -INFINITY) s += cs[512 + jj] * expf(m1 - M);
+        const float lse = M == -INFINITY ? -INFINITY : logf(s) + M;
+        __hip_atomic_store(part + (size_t)g * ld + j,
+                           ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(lse),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      __syncthreads();
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (tid == 0) {
-      __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const unsigned target = (unsigned)G * (unsigned)(it + 1);
+    // v_j = log_nu_j - LSE_g(partial_g,j): poll the G granules of a column (all loads in
+    // flight together; only the stale ones are re-read), bounded
+    bool timed_out = false;
+    for (int j = tid; j < Cc; j += kSinkThreads) {
+      unsigned long long gv[G];
+#pragma unroll
+      for (int gg = 0; gg < G; gg++)
+        gv[gg] = __hip_atomic_load(part + (size_t)gg * ld + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       unsigned spins = 0;
-      while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
-        __builtin_amdgcn_s_sleep(1);
-        if (++spins > (1u << 24)) {
-          __hip_atomic_store(a.err + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          *flag = 1.f;
+      for (;;) {
+        bool ready = true;
+#pragma unroll
+        for (int gg = 0; gg < G; gg++) ready = ready && (unsigned)(gv[gg] >> 32) == tag;
+        if (ready) break;
+        if (++spins > (1u << 22)) {
+          timed_out = true;
           break;
         }
+        __builtin_amdgcn_s_sleep(1);
+#pragma unroll
+        for (int gg = 0; gg < G; gg++)
+          if ((unsigned)(gv[gg] >> 32) != tag)
+            gv[gg] = __hip_atomic_load(part + (size_t)gg * ld + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-    }
-    __syncthreads();
-    if (*flag != 0.f) break;
-    // v_j = log_nu_j - LSE_g(partial_g,j)   (online LSE over the G partials)
-    for (int j = tid; j < Cc; j += 256) {
-      float mx = -INFINITY, s = 0.f;
+      float mx = -INFINITY;
+#pragma unroll
+      for (int gg = 0; gg < G; gg++) mx = fmaxf(mx, __uint_as_float((unsigned)gv[gg]));
+      float s = 0.f;
+#pragma unroll
       for (int gg = 0; gg < G; gg++) {
-        const float pv = ld_sc1(part + (size_t)gg * ld + j);
-        if (pv == -INFINITY) continue;
-        if (pv > mx) {
-          s = s * expf(mx - pv) + 1.f;
-          mx = pv;
-        } else {
-          s += expf(pv - mx);
-        }
+        const float pv = __uint_as_float((unsigned)gv[gg]);
+        s += pv == -INFINITY ? 0.f : expf(pv - mx);
       }
       v[j] = (j < n ? norm : lnu_bin) - (logf(s) + mx);
     }
+    if (timed_out) {
+      __hip_atomic_store(a.err + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = 1.f;
+    }
     __syncthreads();
+    if (*flag != 0.f) break;
   }
   // Z = couplings + u + v - norm
   float* Z = a.Z + (size_t)p * ld * ld + (size_t)r0 * ld;
-  for (int i = tid; i < nr * Cc; i += 256) {
-    const int r = i / Cc, j = i % Cc;
+  for (int i = tid; i < nr * Cc; i += kSinkThreads) {
+    const int r = i / Cc, j = i - r * Cc;
     Z[(size_t)r * ld + j] = ((Cr[(size_t)r * ld + j] + u[r]) + v[j]) - norm;
   }
 }
@@ -389,7 +425,7 @@ __global__ __launch_bounds__(256) void argmax_kernel(DecodeArgs a) {
   const int p = blockIdx.z, ld = a.nmax + 1;
   const int m = a.n0[p], n = a.n1[p];
   const float* Z = a.Z + (size_t)p * ld * ld;
-  if (blockIdx.y == 0) {  // rows: one wave per row
+  {  // rows: one wave per row
     const int i = (blockIdx.x * blockDim.x + threadIdx.x) >> 6, lane = threadIdx.x & 63;
     if (i >= m) return;
     float best = -FLT_MAX;
@@ -408,16 +444,42 @@ __global__ __launch_bounds__(256) void argmax_kernel(DecodeArgs a) {
       a.max0[(size_t)p * a.nmax + i] = idx;
       a.val0[(size_t)p * a.nmax + i] = best;
     }
-  } else {  // columns: one thread per column
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= n) return;
-    float best = -FLT_MAX;
-    int idx = 0;
-    for (int i = 0; i < m; i++) {
+  }
+}
+
+// column argmax: 64 columns x 16 row groups per block; groups combined in LDS with the
+// same strict '<' scan semantics (the smallest row index among equal maxima wins)
+__global__ __launch_bounds__(1024) void col_argmax_kernel(DecodeArgs a) {
+  __shared__ float bv[16][64];
+  __shared__ int bi[16][64];
+  const int p = blockIdx.z, ld = a.nmax + 1;
+  const int m = a.n0[p], n = a.n1[p];
+  const float* Z = a.Z + (size_t)p * ld * ld;
+  const int c = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + c;
+  float best = -FLT_MAX;
+  int idx = 0;
+  if (j < n) {
+    const int per = (m + 15) / 16, i0 = rg * per, i1 = min(m, i0 + per);
+#pragma unroll 8
+    for (int i = i0; i < i1; i++) {
       const float x = Z[(size_t)i * ld + j];
       if (best < x) { best = x; idx = i; }
     }
-    a.max1[(size_t)p * a.nmax + j] = idx;
+    if (i0 >= i1) idx = 0x7fffffff;
+  }
+  bv[rg][c] = best;
+  bi[rg][c] = idx;
+  __syncthreads();
+  if (rg == 0 && j < n) {
+    float b = -FLT_MAX;
+    int id = 0;
+    bool any = false;
+    for (int g = 0; g < 16; g++) {
+      if (bi[g][c] == 0x7fffffff) continue;
+      if (!any || b < bv[g][c]) { b = bv[g][c]; id = bi[g][c]; any = true; }
+    }
+    a.max1[(size_t)p * a.nmax + j] = id;
   }
 }
 
@@ -496,30 +558,44 @@ static size_t slab_rows(int nmax, int G) { return (size_t)(nmax + 1 + G - 1) / G
 
 size_t sinkhorn_lds_bytes(int nmax, int G) {
   const size_t ld = nmax + 1, rows = slab_rows(nmax, G);
-  return sizeof(float) * (rows + ld + 1 + rows * ld);  // u, v, flag, slab
+  return sizeof(float) * (rows + ld + 1 + 2048 + rows * ld);  // u, v, flag, column halves, slab
 }
 
-hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s) {
-  const size_t ld = a.nmax + 1, rows = slab_rows(a.nmax, a.G);
-  const size_t full = sinkhorn_lds_bytes(a.nmax, a.G);
-  dim3 grid(a.G, B);
+template <int G>
+static hipError_t sinkhorn_g(const SinkArgs& a, int B, hipStream_t s) {
+  const size_t ld = a.nmax + 1, rows = slab_rows(a.nmax, G);
+  const size_t full = sinkhorn_lds_bytes(a.nmax, G);
+  dim3 grid(G, B);
   if (full <= 96 * 1024) {
     static size_t attr = 0;
     if (attr < full) {
-      hipError_t e = hipFuncSetAttribute((const void*)sinkhorn_kernel<true>,
+      hipError_t e = hipFuncSetAttribute((const void*)sinkhorn_kernel<true, G>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)full);
       if (e != hipSuccess) return e;
       attr = full;
     }
-    hipLaunchKernelGGL(sinkhorn_kernel<true>, grid, dim3(256), full, s, a);
+    hipLaunchKernelGGL((sinkhorn_kernel<true, G>), grid, dim3(kSinkThreads), full, s, a);
   } else {
-    hipLaunchKernelGGL(sinkhorn_kernel<false>, grid, dim3(256), sizeof(float) * (rows + ld + 1), s, a);
+    hipLaunchKernelGGL((sinkhorn_kernel<false, G>), grid, dim3(kSinkThreads), sizeof(float) * (rows + ld + 1 + 2048), s, a);
   }
   return hipGetLastError();
 }
 
+hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s) {
+  switch (a.G) {
+    case 1: return sinkhorn_g<1>(a, B, s);
+    case 2: return sinkhorn_g<2>(a, B, s);
+    case 4: return sinkhorn_g<4>(a, B, s);
+    case 8: return sinkhorn_g<8>(a, B, s);
+    case 16: return sinkhorn_g<16>(a, B, s);
+    case 32: return sinkhorn_g<32>(a, B, s);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 hipError_t decode(const DecodeArgs& a, int B, hipStream_t s) {
-  hipLaunchKernelGGL(argmax_kernel, dim3((a.nmax * 64 + 255) / 256, 2, B), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(argmax_kernel, dim3((a.nmax * 64 + 255) / 256, 1, B), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(col_argmax_kernel, dim3((a.nmax + 63) / 64, 1, B), dim3(1024), 0, s, a);
   hipLaunchKernelGGL(finalize_kernel, dim3((a.nmax + 255) / 256, 2, B), dim3(256), 0, s, a);
   return hipGetLastError();
 }

@@ -63,8 +63,8 @@ struct BinsArgs {
 struct SinkArgs {
   const float* cpl;   // couplings [B][ld*ld]
   float* Z;           // [B][ld*ld]
-  float* part;        // [B][2][G][ld] column partial LSEs
-  unsigned* ctr;      // [B] arrival counters (zeroed per call)
+  unsigned long long* part;  // [B][2][G][ld] tagged column partial LSEs {f32 bits, tag}
+  unsigned seq;       // per-call tag base (never 0; granules start zeroed)
   unsigned* err;      // [B] timeout flags
   const int* n0;
   const int* n1;
