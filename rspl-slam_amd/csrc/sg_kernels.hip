@@ -26,12 +26,14 @@ __device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
 }
 
 // ---------------------------------------------------------------------------
-// Generic fp32 MFMA GEMM: 64x64 tile, BK = 16, 4 waves (2x2) of 32x32.
+// Generic fp32 MFMA GEMM: 64x64 tile, BK = 32, 4 waves (2x2) of 32x32 each.
+// Double-buffered LDS with a register prefetch of the next K tile issued before
+// the 16 MFMAs of the current one: one barrier per K step, load latency hidden.
 // ---------------------------------------------------------------------------
 template <int EPI, bool BNT>
 __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
-  __shared__ float As[16][64 + 4];
-  __shared__ float Bs[16][64 + 4];
+  __shared__ float As[2][32][64 + 4];
+  __shared__ float Bs[2][32][64 + 4];
   const int z = blockIdx.z;
   int M = a.M, N = a.N;
   if (a.mcount) M = a.mcount[(size_t)z * a.count_stride];
@@ -42,36 +44,66 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
   const float* A2 = a.A2 ? a.A2 + z * a.sA : nullptr;
   const float* B = a.B + z * a.sB;
   float* C = a.C + z * a.sC;
+  const int K = a.K;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, ml = lane & 31, kl = lane >> 5;
   const int wm = wv >> 1, wn = wv & 1;
+  // loader coordinates: A / B^T tiles 64 x 32 (row = tid>>3 (+32), k4 = (tid&7)*4),
+  // B tile 32 x 64 (k = tid>>4 (+16), n4 = (tid&15)*4)
+  const int lr = tid >> 3, lk4 = (tid & 7) * 4;
+  const int bk = tid >> 4, bn4 = (tid & 15) * 4;
+  float4 ra[2], rb[2];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int m = m0 + lr + 32 * h, k = k0 + lk4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (m < M && k < K) {
+        const float* src = (A2 && k >= a.ksplit) ? A2 + (size_t)m * a.lda + (k - a.ksplit) : A + (size_t)m * a.lda + k;
+        v = *reinterpret_cast<const float4*>(src);
+      }
+      ra[h] = v;
+    }
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if constexpr (!BNT) {
+        const int k = k0 + bk + 16 * h;
+        if (k < K && n0 + bn4 < N) v = *reinterpret_cast<const float4*>(B + (size_t)k * a.ldb + n0 + bn4);
+      } else {
+        const int n = n0 + lr + 32 * h, k = k0 + lk4;
+        if (n < N && k < K) v = *reinterpret_cast<const float4*>(B + (size_t)n * a.ldb + k);
+      }
+      rb[h] = v;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      const int r = lr + 32 * h;
+      As[buf][lk4 + 0][r] = ra[h].x; As[buf][lk4 + 1][r] = ra[h].y;
+      As[buf][lk4 + 2][r] = ra[h].z; As[buf][lk4 + 3][r] = ra[h].w;
+      if constexpr (!BNT) {
+        *reinterpret_cast<float4*>(&Bs[buf][bk + 16 * h][bn4]) = rb[h];
+      } else {
+        Bs[buf][lk4 + 0][r] = rb[h].x; Bs[buf][lk4 + 1][r] = rb[h].y;
+        Bs[buf][lk4 + 2][r] = rb[h].z; Bs[buf][lk4 + 3][r] = rb[h].w;
+      }
+    }
+  };
   floatx16 acc;
 #pragma unroll
   for (int r = 0; r < 16; r++) acc[r] = 0.f;
-  for (int k0 = 0; k0 < a.K; k0 += 16) {
-    {
-      const int row = tid >> 2, k4 = (tid & 3) * 4, m = m0 + row;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (m < M) {
-        const float* src = (A2 && k0 >= a.ksplit) ? A2 + (size_t)m * a.lda + (k0 - a.ksplit) + k4
-                                                  : A + (size_t)m * a.lda + k0 + k4;
-        v = *reinterpret_cast<const float4*>(src);
-      }
-      As[k4 + 0][row] = v.x; As[k4 + 1][row] = v.y; As[k4 + 2][row] = v.z; As[k4 + 3][row] = v.w;
-    }
-    if constexpr (!BNT) {
-      const int k = tid >> 4, n4 = (tid & 15) * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (n0 + n4 < N) v = *reinterpret_cast<const float4*>(B + (size_t)(k0 + k) * a.ldb + n0 + n4);
-      *reinterpret_cast<float4*>(&Bs[k][n4]) = v;
-    } else {
-      const int n = tid >> 2, k4 = (tid & 3) * 4;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (n0 + n < N) v = *reinterpret_cast<const float4*>(B + (size_t)(n0 + n) * a.ldb + k0 + k4);
-      Bs[k4 + 0][n] = v.x; Bs[k4 + 1][n] = v.y; Bs[k4 + 2][n] = v.z; Bs[k4 + 3][n] = v.w;
-    }
-    __syncthreads();
+  const int nk = (K + 31) / 32;
+  load(0);
+  store(0);
+  __syncthreads();
+  for (int kt = 0; kt < nk; kt++) {
+    const int buf = kt & 1;
+    if (kt + 1 < nk) load((kt + 1) * 32);
 #pragma unroll
-    for (int kk = 0; kk < 16; kk += 2) acc = mfma32(As[kk + kl][wm * 32 + ml], Bs[kk + kl][wn * 32 + ml], acc);
+    for (int kk = 0; kk < 32; kk += 2)
+      acc = mfma32(As[buf][kk + kl][wm * 32 + ml], Bs[buf][kk + kl][wn * 32 + ml], acc);
+    if (kt + 1 < nk) store(buf ^ 1);
     __syncthreads();
   }
   const int n = n0 + wn * 32 + ml;
@@ -163,57 +195,67 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs a) {
   for (int r = 0; r < 16; r++) { o0[r] = 0.f; o1[r] = 0.f; }
   float m_run = -INFINITY, l_run = 0.f;
   const int ntiles = (nk + 31) / 32;
-  for (int base = 0; base < ntiles; base += 4) {
-    const int t = base + wv;
-    __syncthreads();
-    if (t < ntiles) {
-      for (int i = lane; i < 32 * 16; i += 64) {
-        const int row = i >> 4, c4 = (i & 15) * 4, key = t * 32 + row;
-        float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
-        if (key < nk) {
-          kv = *reinterpret_cast<const float4*>(Kb + (size_t)key * 768 + c4);
-          vv = *reinterpret_cast<const float4*>(Vb + (size_t)key * 768 + c4);
-        }
-        Ks[wv][row][c4 + 0] = kv.x; Ks[wv][row][c4 + 1] = kv.y;
-        Ks[wv][row][c4 + 2] = kv.z; Ks[wv][row][c4 + 3] = kv.w;
-        *reinterpret_cast<float4*>(&Vs[wv][row][c4]) = vv;
+  // each wave owns key tiles wv, wv+4, ... and a private LDS slot: the next tile is
+  // prefetched into registers while the current one is multiplied (no block barriers)
+  float4 pk[8], pv[8];
+  auto fetch = [&](int t) {
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int i = lane + 64 * u, row = i >> 4, c4 = (i & 15) * 4, key = t * 32 + row;
+      float4 kv = make_float4(0.f, 0.f, 0.f, 0.f), vv = kv;
+      if (key < nk) {
+        kv = *reinterpret_cast<const float4*>(Kb + (size_t)key * 768 + c4);
+        vv = *reinterpret_cast<const float4*>(Vb + (size_t)key * 768 + c4);
       }
+      pk[u] = kv;
+      pv[u] = vv;
     }
-    __syncthreads();
-    if (t < ntiles) {
-      floatx16 st;
+  };
+  if (wv < ntiles) fetch(wv);
+  for (int t = wv; t < ntiles; t += 4) {
+    __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int r = 0; r < 16; r++) st[r] = 0.f;
+    for (int u = 0; u < 8; u++) {
+      const int i = lane + 64 * u, row = i >> 4, c4 = (i & 15) * 4;
+      Ks[wv][row][c4 + 0] = pk[u].x; Ks[wv][row][c4 + 1] = pk[u].y;
+      Ks[wv][row][c4 + 2] = pk[u].z; Ks[wv][row][c4 + 3] = pk[u].w;
+      *reinterpret_cast<float4*>(&Vs[wv][row][c4]) = pv[u];
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    if (t + 4 < ntiles) fetch(t + 4);
+    floatx16 st;
 #pragma unroll
-      for (int s = 0; s < 32; s++) st = mfma32(Ks[wv][ml][2 * s + kl], qf[s], st);
-      float x[16];
-      float mx = -INFINITY;
+    for (int r = 0; r < 16; r++) st[r] = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const int key = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
-        x[r] = key < nk ? st[r] * 0.125f : -INFINITY;  // scores / dim**.5 (superglue.py:90)
-        mx = fmaxf(mx, x[r]);
-      }
-      mx = fmaxf(mx, __shfl_xor(mx, 32));
-      const float m_new = fmaxf(m_run, mx);
-      const float alpha = __expf(m_run - m_new);
-      float sum = 0.f;
+    for (int s = 0; s < 32; s++) st = mfma32(Ks[wv][ml][2 * s + kl], qf[s], st);
+    float x[16];
+    float mx = -INFINITY;
 #pragma unroll
-      for (int r = 0; r < 16; r++) {
-        x[r] = expf(x[r] - m_new);
-        sum += x[r];
-      }
-      sum += __shfl_xor(sum, 32);
-      l_run = l_run * alpha + sum;
-      m_run = m_new;
+    for (int r = 0; r < 16; r++) {
+      const int key = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+      x[r] = key < nk ? st[r] * 0.125f : -INFINITY;  // scores / dim**.5 (superglue.py:90)
+      mx = fmaxf(mx, x[r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = __expf(m_run - m_new);
+    float sum = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; r++) { o0[r] *= alpha; o1[r] *= alpha; }
+    for (int r = 0; r < 16; r++) {
+      x[r] = expf(x[r] - m_new);
+      sum += x[r];
+    }
+    sum += __shfl_xor(sum, 32);
+    l_run = l_run * alpha + sum;
+    m_run = m_new;
 #pragma unroll
-      for (int s = 0; s < 16; s++) {
-        const int key = (s & 3) + 8 * (s >> 2) + 4 * kl;
-        o0 = mfma32(Vs[wv][key][ml], x[s], o0);
-        o1 = mfma32(Vs[wv][key][32 + ml], x[s], o1);
-      }
+    for (int r = 0; r < 16; r++) { o0[r] *= alpha; o1[r] *= alpha; }
+#pragma unroll
+    for (int s = 0; s < 16; s++) {
+      const int key = (s & 3) + 8 * (s >> 2) + 4 * kl;
+      o0 = mfma32(Vs[wv][key][ml], x[s], o0);
+      o1 = mfma32(Vs[wv][key][32 + ml], x[s], o1);
     }
   }
   __syncthreads();
