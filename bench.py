@@ -32,7 +32,6 @@ import rspl_loader  # noqa: E402
 
 pkg = rspl_loader.load()
 capi = pkg.capi
-capi.load()  # librspl's HIP runtime first: one runtime per process
 
 H, W, K = 480, 752, 400
 FP32_MFMA_PEAK = 157.3  # TFLOP/s, MI355X_MICROARCH.md (v_mfma_f32_32x32x2_f32, dense)
@@ -74,12 +73,33 @@ def cpu_baseline(sp_w, sg_w, frames, threads):
                       f"through the oracle's C restatement, OMP_NUM_THREADS={threads}, {dt:.1f} s"}
 
 
+def replica_seeds(rank):
+    """Per-rank synthetic sequence (replicas: each GPU runs its own stereo stream)."""
+    return {"images": [1000 * rank + i for i in range(4)], "ba": [1000 * rank + 50 + i for i in range(3)]}
+
+
+def job_time(elapsed, dist=None):
+    """Whole-job wall time = max over ranks of each rank's timed region (gloo all-reduce)."""
+    if dist is None:
+        return elapsed
+    import torch
+    t = torch.tensor([elapsed], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t[0])
+
+
+def job_value(world, steps, elapsed):
+    """frames/s over all ranks: every rank processed `steps` stereo keyframes."""
+    return world * steps / elapsed
+
+
 def main():
+    capi.load()  # librspl's HIP runtime first: one runtime per process
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--cpu-frames", type=int, default=4, help="keyframes in the bounded CPU-baseline sample")
+    ap.add_argument("--cpu-frames", type=int, default=12, help="keyframes in the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -105,11 +125,11 @@ def main():
     syn = pkg.synthetic
     NP = 4
     pool = capi.DeviceBuffer(NP * 2 * H * W)
+    seeds = replica_seeds(rank)
     for i in range(NP):
-        L, R = syn.stereo_pair(H, W, seed=1000 * rank + i)
+        L, R = syn.stereo_pair(H, W, seed=seeds["images"][i])
         pool.upload(np.stack([L, R]), offset=i * 2 * H * W)
-    problems = [syn.ba_problem(n_poses=10, n_points=4000, n_lines=100, seed=1000 * rank + 50 + i)[0]
-                for i in range(3)]
+    problems = [syn.ba_problem(n_poses=10, n_points=4000, n_lines=100, seed=sd)[0] for sd in seeds["ba"]]
     FB = K * 259 * 8
     feats = [capi.DeviceBuffer(2 * FB) for _ in range(2)]
     counts = [capi.DeviceBuffer(8) for _ in range(2)]
@@ -151,19 +171,15 @@ def main():
     for i in range(args.steps):
         step(args.warmup + i)
     capi.synchronize()
-    elapsed = time.perf_counter() - t0
+    elapsed = job_time(time.perf_counter() - t0, dist)
     if dist:
-        import torch
-        t = torch.tensor([elapsed], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t[0])
         dist.barrier()
 
     sp_ms, sp_calls = sp.stage_times()
     sg_ms, sg_calls = sg.stage_times()
     conv1_ms = sp_ms[0] / max(1, sp_calls)
     achieved = 2 * CONV1_GFLOP_PER_IMAGE / conv1_ms  # GFLOP / ms = TFLOP/s
-    value = world * args.steps / elapsed
+    value = job_value(world, args.steps, elapsed)
     if rank != 0:
         return
     out = {

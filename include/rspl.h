@@ -142,7 +142,8 @@ int rspl_sg_infer(rspl_sg* sg, const double* f0, int n0, const double* f1, int n
                   int32_t* indices0, int32_t* indices1, double* mscores0, double* mscores1);
 
 /* Device-resident batched form.  Pair p reads f0 = d_feat0 + p*259*stride_feat,
- * n0 = counts0[p] (HOST ints), likewise image 1; writes d_idx0 + p*max_kp etc.
+ * n0 = n0[p] (DEVICE int32 counts, e.g. rspl_sp_infer_device's d_counts),
+ * likewise image 1; writes d_idx0 + p*max_kp etc.
  * normalize != 0 applies PointMatching::NormalizeKeypoints on device first. */
 int rspl_sg_infer_device(rspl_sg* sg, int batch, const double* d_feat0, const int* n0,
                          const double* d_feat1, const int* n1, int stride_feat, int normalize,
