@@ -73,6 +73,20 @@ def cpu_baseline(sp_w, sg_w, frames, threads):
                       f"through the oracle's C restatement, OMP_NUM_THREADS={threads}, {dt:.1f} s"}
 
 
+def pmc_traffic(kernel_substr):
+    """HBM bytes per launch of a kernel from the newest committed PMC summary
+    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from two rocprofv3
+    --pmc passes, FETCH_SIZE x2 gfx950 correction), or None."""
+    files = sorted((ROOT / "profiles").glob("*_pmc_traffic.json"))
+    if not files:
+        return None, None
+    data = json.loads(files[-1].read_text())
+    for name, v in data.items():
+        if kernel_substr in name:
+            return v["traffic_bytes"], files[-1].name
+    return None, None
+
+
 def replica_seeds(rank):
     """Per-rank synthetic sequence (replicas: each GPU runs its own stereo stream)."""
     return {"images": [1000 * rank + i for i in range(4)], "ba": [1000 * rank + 50 + i for i in range(3)]}
@@ -179,6 +193,7 @@ def main():
     sg_ms, sg_calls = sg.stage_times()
     conv1_ms = sp_ms[0] / max(1, sp_calls)
     achieved = 2 * CONV1_GFLOP_PER_IMAGE / conv1_ms  # GFLOP / ms = TFLOP/s
+    traffic, traffic_src = pmc_traffic("conv3x3_kernel<64, 16, true, true>")
     value = job_value(world, args.steps, elapsed)
     if rank != 0:
         return
@@ -200,7 +215,11 @@ def main():
                    "global_batch": world, "parallelism": f"replicas x{world} (one sequence per GPU)"},
         "roofline": {"kernel": "conv3x3_kernel<64,16,true,true> (conv1a+conv1b+ReLU+pool, fused)",
                      "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP32_MFMA_PEAK, 4), "traffic": None,
+                     "frac": round(achieved / FP32_MFMA_PEAK, 4),
+                     "traffic": round(traffic) if traffic else None,
+                     "traffic_note": (f"HBM bytes per launch, rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE, {traffic_src}; "
+                                      "algorithmic minimum = 46.2 MB pooled output + 0.7 MB images")
+                     if traffic else None,
                      "algorithmic": f"{2 * CONV1_GFLOP_PER_IMAGE:.3f} GFLOP per launch (2 images)",
                      "avg_launch_ms": round(conv1_ms, 4)},
         "stages_ms_per_step": {**{f"sp:{n}": round(v / max(1, sp_calls), 4) for n, v in zip(sp.STAGES, sp_ms)},
