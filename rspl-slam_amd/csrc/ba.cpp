@@ -388,7 +388,12 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
   int rc = b->arena.reserve(sz.used);
   if (rc) { delete b; return rc; }
   carve(b->arena, b);
-  if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess ||
+  // the BA is a host-driven chain of short kernels on the tracking thread's critical path:
+  // give its stream the highest priority so each trial's kernels dispatch ahead of queued
+  // SuperPoint/SuperGlue work instead of waiting behind it
+  int prio_lo = 0, prio_hi = 0;
+  (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
+  if (hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipHostMalloc((void**)&b->mail, sizeof(ba::Mail), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&b->mail_dev, b->mail, 0) != hipSuccess ||
       hipMemset(b->flags, 0, 4 * sizeof(int)) != hipSuccess || hipMemset(b->out, 0, 8 * sizeof(double)) != hipSuccess) {

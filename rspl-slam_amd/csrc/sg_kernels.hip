@@ -123,6 +123,93 @@ __global__ __launch_bounds__(256) void gemm_kernel(GemmArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Split-K fp32 MFMA GEMM for the token-parallel layers (M = tokens ~ 1600 is too
+// short for 64x64 tiles to fill 256 CUs): one 32x32 output tile per workgroup, the
+// 4 waves take interleaved quarters of K (32-wide steps), each with a register
+// prefetch into a wave-private LDS slot (no block barriers in the K loop).  The 4
+// partial tiles are summed in a fixed order (w0+w1+w2+w3): deterministic.
+// ---------------------------------------------------------------------------
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_sk_kernel(GemmArgs a) {
+  __shared__ float As[4][32][33];  // [wave][k][m]
+  __shared__ float Bs[4][32][33];  // [wave][k][n]
+  const int z = blockIdx.z;
+  int M = a.M, N = a.N;
+  if (a.mcount) M = a.mcount[(size_t)z * a.count_stride];
+  if (a.ncount) N = a.ncount[(size_t)z * a.count_stride];
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  if (m0 >= M || n0 >= N) return;
+  const float* A = a.A + z * a.sA;
+  const float* A2 = a.A2 ? a.A2 + z * a.sA : nullptr;
+  const float* B = a.B + z * a.sB;
+  float* C = a.C + z * a.sC;
+  const int K = a.K, nsteps = (K + 31) / 32;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, ml = lane & 31, kl = lane >> 5;
+  float4 ra[4], rb[4];
+  auto load = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = lane + 64 * u, r = i >> 3, c4 = (i & 7) * 4;
+      const int m = m0 + r, ka = k0 + c4, kb = k0 + r, n = n0 + c4;
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f), w = v;
+      if (m < M && ka < K) {
+        const float* src = (A2 && ka >= a.ksplit) ? A2 + (size_t)m * a.lda + (ka - a.ksplit) : A + (size_t)m * a.lda + ka;
+        v = *reinterpret_cast<const float4*>(src);
+      }
+      if (kb < K && n < N) w = *reinterpret_cast<const float4*>(B + (size_t)kb * a.ldb + n);
+      ra[u] = v;
+      rb[u] = w;
+    }
+  };
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; r++) acc[r] = 0.f;
+  int step = wv;
+  if (step < nsteps) load(step * 32);
+  for (; step < nsteps; step += 4) {
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int i = lane + 64 * u, r = i >> 3, c4 = (i & 7) * 4;
+      As[wv][c4 + 0][r] = ra[u].x; As[wv][c4 + 1][r] = ra[u].y;
+      As[wv][c4 + 2][r] = ra[u].z; As[wv][c4 + 3][r] = ra[u].w;
+      Bs[wv][r][c4 + 0] = rb[u].x; Bs[wv][r][c4 + 1] = rb[u].y;
+      Bs[wv][r][c4 + 2] = rb[u].z; Bs[wv][r][c4 + 3] = rb[u].w;
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+    if (step + 4 < nsteps) load((step + 4) * 32);
+#pragma unroll
+    for (int kk = 0; kk < 32; kk += 2) acc = mfma32(As[wv][kk + kl][ml], Bs[wv][kk + kl][ml], acc);
+  }
+  // fixed-order reduction of the 4 K-partials through LDS (reuses As/Bs: 4 x 1056 >= 3 x 16 x 64)
+  __syncthreads();
+  float* red = &As[0][0][0];
+  if (wv > 0) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) red[((wv - 1) * 16 + r) * 64 + lane] = acc[r];
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  const int n = n0 + ml;
+  if (n >= N) return;
+  const float b = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const float s = ((acc[r] + red[(0 * 16 + r) * 64 + lane]) + red[(1 * 16 + r) * 64 + lane]) +
+                    red[(2 * 16 + r) * 64 + lane];
+    const int m = m0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+    if (m < M) {
+      float v = s * a.alpha + b;
+      float* dst = C + (size_t)m * a.ldc + n;
+      if constexpr (EPI == 1) v = v > 0.f ? v : 0.f;
+      if constexpr (EPI == 2) v = *dst + v;
+      *dst = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // process_input + NormalizeKeypoints: one wave per token.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
@@ -567,15 +654,18 @@ __global__ __launch_bounds__(256) void finalize_kernel(DecodeArgs a) {
 // launchers
 // ---------------------------------------------------------------------------
 hipError_t gemm(const GemmArgs& a, int batch, hipStream_t s) {
-  dim3 grid((a.N + 63) / 64, (a.M + 63) / 64, batch);
   if (a.b_nt) {
+    dim3 grid((a.N + 63) / 64, (a.M + 63) / 64, batch);
     hipLaunchKernelGGL((gemm_kernel<0, true>), grid, dim3(256), 0, s, a);
-  } else if (a.epi == 1) {
-    hipLaunchKernelGGL((gemm_kernel<1, false>), grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
+  dim3 grid((a.N + 31) / 32, (a.M + 31) / 32, batch);
+  if (a.epi == 1) {
+    hipLaunchKernelGGL(gemm_sk_kernel<1>, grid, dim3(256), 0, s, a);
   } else if (a.epi == 2) {
-    hipLaunchKernelGGL((gemm_kernel<2, false>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(gemm_sk_kernel<2>, grid, dim3(256), 0, s, a);
   } else {
-    hipLaunchKernelGGL((gemm_kernel<0, false>), grid, dim3(256), 0, s, a);
+    hipLaunchKernelGGL(gemm_sk_kernel<0>, grid, dim3(256), 0, s, a);
   }
   return hipGetLastError();
 }
