@@ -8,8 +8,10 @@ step is one stereo keyframe of a synthetic EuRoC-shaped stream:
   * one local BA (LocalmapOptimization) of a C3-sized problem: 10 keyframes (1 fixed),
     ~4k points / ~10^4 point observations, 100 lines (synthetic, with ground truth).
 Inputs (images) are resident in HBM before timing.  BA is host-driven and runs on its own
-stream, overlapping the frame's SP/SG exactly as the reference's tracking thread overlaps
-its feature thread (src/map_builder.cc:48-49).  The BA problem is handed over as host
+(highest-priority) stream, overlapping the frame's SP/SG exactly as the reference's tracking
+thread overlaps its feature thread (src/map_builder.cc:48-49); SP of frame t+1 runs on its own
+stream beside SG of frame t (event-ordered).  The timed region ends with a device
+synchronisation, so every frame's SP, SG and BA work is inside it.  The BA problem is handed over as host
 arrays (the reference's std::map containers), so its H2D upload is inside the step.
 
 Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU, each
@@ -20,6 +22,8 @@ HIP runtime (librspl's system ROCm) drives each GPU.
 import argparse
 import json
 import os
+import queue
+import threading
 import pathlib
 import sys
 import time
@@ -28,6 +32,11 @@ import numpy as np
 
 ROOT = pathlib.Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT))
+# SP, SG and BA each need their own hardware queue to overlap (HIP maps streams round-robin
+# onto GPU_MAX_HW_QUEUES queues; with the default 4 the SP and SG streams land on one queue
+# and serialise).  Must be set before the HIP runtime initialises.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 import rspl_loader  # noqa: E402
 
 pkg = rspl_loader.load()
@@ -145,36 +154,72 @@ def main():
         pool.upload(np.stack([L, R]), offset=i * 2 * H * W)
     problems = [syn.ba_problem(n_poses=10, n_points=4000, n_lines=100, seed=sd)[0] for sd in seeds["ba"]]
     FB = K * 259 * 8
-    feats = [capi.DeviceBuffer(2 * FB) for _ in range(2)]
-    counts = [capi.DeviceBuffer(8) for _ in range(2)]
+    # SP(t+1) is pipelined beside SG(t): SP and SG on their own streams,
+    # ordered by events; feature slots triple-buffered (SG(t) reads slots t and t-1,
+    # SP(t+1) writes slot t+1 and first waits for SG(t-1), the last reader of that slot)
+    feats = [capi.DeviceBuffer(2 * FB) for _ in range(3)]
+    counts = [capi.DeviceBuffer(8) for _ in range(3)]
+    for c in counts:
+        c.zero()
     f0, f1 = capi.DeviceBuffer(2 * FB), capi.DeviceBuffer(2 * FB)
     n0, n1 = capi.DeviceBuffer(8), capi.DeviceBuffer(8)
     outs = [capi.DeviceBuffer(2 * K * sz) for sz in (4, 4, 8, 8)]
-    st = capi.Stream()
+    st_sp, st_sg = capi.Stream(), capi.Stream()
+    ev_sp = [capi.Event() for _ in range(3)]
+    ev_sg = [capi.Event() for _ in range(3)]
+    capi.synchronize()
     ba_ms = []
+    ba_err = []
+    ba_q = queue.Queue(maxsize=2)
+
+    def tracking_thread():
+        """BA worker: the reference runs LocalmapOptimization on the tracking thread while the
+        feature thread keeps extracting/matching (src/map_builder.cc:48-49, src/map.cc:105-107)."""
+        capi.check(capi.load().rspl_set_device(local), "rspl_set_device")  # HIP device is per thread
+        while True:
+            prob = ba_q.get()
+            if prob is None:
+                ba_q.task_done()
+                return
+            t = time.perf_counter()
+            try:
+                ba.run(prob)
+            except Exception as e:  # surfaced on the main thread
+                ba_err.append(e)
+            ba_ms.append((time.perf_counter() - t) * 1e3)
+            ba_q.task_done()
+
+    worker = threading.Thread(target=tracking_thread, daemon=True)
+    worker.start()
 
     def step(i):
-        cur, prev = feats[i % 2], feats[(i + 1) % 2]
-        ccur, cprev = counts[i % 2], counts[(i + 1) % 2]
-        sp.infer_device(pool.offset((i % NP) * 2 * H * W), 2, H, W, W, H * W, cur.ptr, K, ccur.ptr, st.handle)
+        slot, pslot = i % 3, (i - 1) % 3
+        cur, prev, ccur, cprev = feats[slot], feats[pslot], counts[slot], counts[pslot]
+        if i >= 2:
+            ev_sg[(i - 2) % 3].wait_on(st_sp.handle)
+        sp.infer_device(pool.offset((i % NP) * 2 * H * W), 2, H, W, W, H * W, cur.ptr, K, ccur.ptr, st_sp.handle)
+        ev_sp[slot].record(st_sp.handle)
+        ev_sp[slot].wait_on(st_sg.handle)
         # PointMatching pairs: (L_t, L_kf) and (L_t, R_t)
-        capi.memcpy_d2d(f0.ptr, cur.ptr, FB, st.handle)
-        capi.memcpy_d2d(f0.offset(FB), cur.ptr, FB, st.handle)
-        capi.memcpy_d2d(f1.ptr, prev.ptr, FB, st.handle)
-        capi.memcpy_d2d(f1.offset(FB), cur.offset(FB), FB, st.handle)
-        capi.memcpy_d2d(n0.ptr, ccur.ptr, 4, st.handle)
-        capi.memcpy_d2d(n0.offset(4), ccur.ptr, 4, st.handle)
-        capi.memcpy_d2d(n1.ptr, cprev.ptr, 4, st.handle)
-        capi.memcpy_d2d(n1.offset(4), ccur.offset(4), 4, st.handle)
+        capi.memcpy_d2d(f0.ptr, cur.ptr, FB, st_sg.handle)
+        capi.memcpy_d2d(f0.offset(FB), cur.ptr, FB, st_sg.handle)
+        capi.memcpy_d2d(f1.ptr, prev.ptr, FB, st_sg.handle)
+        capi.memcpy_d2d(f1.offset(FB), cur.offset(FB), FB, st_sg.handle)
+        capi.memcpy_d2d(n0.ptr, ccur.ptr, 4, st_sg.handle)
+        capi.memcpy_d2d(n0.offset(4), ccur.ptr, 4, st_sg.handle)
+        capi.memcpy_d2d(n1.ptr, cprev.ptr, 4, st_sg.handle)
+        capi.memcpy_d2d(n1.offset(4), ccur.offset(4), 4, st_sg.handle)
         sg.infer_device(2, f0.ptr, n0.ptr, f1.ptr, n1.ptr, K, True, outs[0].ptr, outs[1].ptr, outs[2].ptr,
-                        outs[3].ptr, st.handle)
-        t = time.perf_counter()
-        ba.run(problems[i % len(problems)])     # overlaps the SP/SG work queued above
-        ba_ms.append((time.perf_counter() - t) * 1e3)
-        st.synchronize()
+                        outs[3].ptr, st_sg.handle)
+        ev_sg[slot].record(st_sg.handle)
+        # keyframe i's local BA goes to the tracking thread (own high-priority stream) through a
+        # 2-deep buffer, as the reference's feature thread blocks only while
+        # _tracking_data_buffer.size() >= 2 (src/map_builder.cc:176)
+        ba_q.put(problems[i % len(problems)])
 
     for i in range(args.warmup):
         step(i)
+    ba_q.join()
     capi.synchronize()
     if dist:
         dist.barrier()
@@ -184,8 +229,13 @@ def main():
     t0 = time.perf_counter()
     for i in range(args.steps):
         step(args.warmup + i)
+    ba_q.join()
     capi.synchronize()
     elapsed = job_time(time.perf_counter() - t0, dist)
+    ba_q.put(None)
+    worker.join()
+    if ba_err:
+        raise ba_err[0]
     if dist:
         dist.barrier()
 

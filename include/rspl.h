@@ -60,6 +60,13 @@ int rspl_stream_create(void** stream);
 int rspl_stream_destroy(void* stream);
 int rspl_stream_synchronize(void* stream);
 int rspl_device_synchronize(void);
+/* Cross-stream ordering without host synchronisation (pipelining SuperPoint of the
+ * next frame beside SuperGlue of this one): record an event on one stream, make
+ * another stream wait for it. */
+int rspl_event_create(void** event);
+int rspl_event_record(void* event, void* stream);
+int rspl_stream_wait_event(void* stream, void* event);
+int rspl_event_destroy(void* event);
 /* HIP-event timer on a stream: rspl_timer_record(t, 0|1, stream) marks
  * start / stop; rspl_timer_elapsed_ms waits for stop and returns ms. */
 typedef struct rspl_timer rspl_timer;

@@ -19,7 +19,8 @@ EXPORTS = [
     "rspl_last_error", "rspl_version",
     "rspl_device_count", "rspl_set_device", "rspl_malloc", "rspl_free", "rspl_memcpy_h2d", "rspl_memcpy_d2h",
     "rspl_memset", "rspl_memcpy_d2d", "rspl_stream_create", "rspl_stream_destroy", "rspl_stream_synchronize",
-    "rspl_device_synchronize", "rspl_timer_create", "rspl_timer_record", "rspl_timer_elapsed_ms",
+    "rspl_device_synchronize", "rspl_event_create", "rspl_event_record", "rspl_stream_wait_event",
+    "rspl_event_destroy", "rspl_timer_create", "rspl_timer_record", "rspl_timer_elapsed_ms",
     "rspl_timer_destroy",
     "rspl_sp_create", "rspl_sp_infer", "rspl_sp_infer_device", "rspl_sp_debug_maps", "rspl_sp_profile",
     "rspl_sp_stage_times", "rspl_sp_destroy",
@@ -88,6 +89,10 @@ def load(path: pathlib.Path = LIB_PATH):
     lib.rspl_stream_create.argtypes = [C.POINTER(vp)]
     lib.rspl_stream_destroy.argtypes = [vp]
     lib.rspl_stream_synchronize.argtypes = [vp]
+    lib.rspl_event_create.argtypes = [C.POINTER(vp)]
+    lib.rspl_event_record.argtypes = [vp, vp]
+    lib.rspl_stream_wait_event.argtypes = [vp, vp]
+    lib.rspl_event_destroy.argtypes = [vp]
     lib.rspl_timer_create.argtypes = [C.POINTER(vp)]
     lib.rspl_timer_record.argtypes = [vp, ip, vp]
     lib.rspl_timer_elapsed_ms.argtypes = [vp, C.POINTER(C.c_float)]
@@ -169,6 +174,26 @@ def stage_times(fn_profile, fn_times, handle, nstages):
     calls = C.c_int(0)
     check(fn_times(handle, ms, C.byref(calls)), "stage_times")
     return [ms[i] for i in range(nstages)], calls.value
+
+
+class Event:
+    """hipEvent (timing disabled) for cross-stream ordering."""
+
+    def __init__(self):
+        self._e = C.c_void_p()
+        check(load().rspl_event_create(C.byref(self._e)), "rspl_event_create")
+
+    def record(self, stream):
+        check(load().rspl_event_record(self._e, C.c_void_p(stream)), "rspl_event_record")
+
+    def wait_on(self, stream):
+        """make `stream` wait for this event"""
+        check(load().rspl_stream_wait_event(C.c_void_p(stream), self._e), "rspl_stream_wait_event")
+
+    def __del__(self):
+        if self._e.value:
+            load().rspl_event_destroy(self._e)
+            self._e = C.c_void_p()
 
 
 class Stream:

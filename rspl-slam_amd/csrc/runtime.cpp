@@ -62,6 +62,23 @@ int rspl_stream_synchronize(void* stream) {
   RSPL_HIP(hipStreamSynchronize((hipStream_t)stream));
   return RSPL_OK;
 }
+int rspl_event_create(void** event) {
+  RSPL_CHECK_ARG(event, "NULL event");
+  RSPL_HIP(hipEventCreateWithFlags((hipEvent_t*)event, hipEventDisableTiming));
+  return RSPL_OK;
+}
+int rspl_event_record(void* event, void* stream) {
+  RSPL_HIP(hipEventRecord((hipEvent_t)event, (hipStream_t)stream));
+  return RSPL_OK;
+}
+int rspl_stream_wait_event(void* stream, void* event) {
+  RSPL_HIP(hipStreamWaitEvent((hipStream_t)stream, (hipEvent_t)event, 0));
+  return RSPL_OK;
+}
+int rspl_event_destroy(void* event) {
+  RSPL_HIP(hipEventDestroy((hipEvent_t)event));
+  return RSPL_OK;
+}
 int rspl_device_synchronize(void) {
   RSPL_HIP(hipDeviceSynchronize());
   return RSPL_OK;
