@@ -237,10 +237,12 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
                o_lme = place(4 * (size_t)Ea), o_lmp = place(4 * (size_t)Ea), o_lact = place(nL),
                o_psoff = place(4 * (size_t)(K + 1)), o_pse = place(4 * (size_t)nps),
                o_pairs = place(8 * (size_t)npairs), o_choff = place(4 * (size_t)(npairs + 1)),
-               o_chb = place(4 * (size_t)nch), o_che = place(4 * (size_t)nch), o_e1 = place(4 * (size_t)npp),
+               o_chb = place(4 * (size_t)nch), o_che = place(4 * (size_t)nch), o_chp = place(4 * (size_t)nch), o_e1 = place(4 * (size_t)npp),
                o_e2 = place(4 * (size_t)npp);
   const size_t upload = off;
   const size_t o_chunk = place(sizeof(double) * 48 * (size_t)std::max(nch, 1));
+  const size_t o_pfin = place(sizeof(double) * 48 * (size_t)std::max(npairs, 1));
+  const size_t o_pctr = place(sizeof(unsigned) * (size_t)std::max(npairs, 1));
   int rc;
   if ((rc = ensure_phase(b, off))) return rc;
   if ((rc = ensure_stage(b, soff + upload))) return rc;
@@ -260,6 +262,7 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
     int* choff = I(o_choff);
     int* chb = I(o_chb);
     int* che = I(o_che);
+    int* chp = I(o_chp);
     int c = 0;
     for (int a = 0, p = 0; a < K; a++)
       for (int cc = a; cc < K; cc++, p++) {
@@ -269,6 +272,7 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
         for (int s = w.pp_cnt[p]; s < w.pp_cnt[p + 1]; s += ba::kChunk, c++) {
           chb[c] = s;
           che[c] = std::min(s + ba::kChunk, w.pp_cnt[p + 1]);
+          chp[c] = p;
         }
       }
     choff[npairs] = c;
@@ -304,10 +308,14 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
   A.lm_edges = dptr(o_lme); A.lm_pose = dptr(o_lmp);
   A.lm_act = reinterpret_cast<const uint8_t*>(b->phase_buf + o_lact);
   A.ps_off = dptr(o_psoff); A.ps_edges = dptr(o_pse); A.pairs = dptr(o_pairs); A.npairs = npairs;
-  A.pair_choff = dptr(o_choff); A.ch_beg = dptr(o_chb); A.ch_end = dptr(o_che); A.nch = nch;
+  A.pair_choff = dptr(o_choff); A.ch_beg = dptr(o_chb); A.ch_end = dptr(o_che); A.ch_pair = dptr(o_chp);
+  A.nch = nch;
   A.pp_e1 = dptr(o_e1); A.pp_e2 = dptr(o_e2); A.n_line_edges = n_line_edges; A.nL = nL; A.robust = robust;
   A.K = K;
   S.chunk = reinterpret_cast<double*>(b->phase_buf + o_chunk);
+  S.pairfin = reinterpret_cast<double*>(b->phase_buf + o_pfin);
+  S.pair_ctr = reinterpret_cast<unsigned*>(b->phase_buf + o_pctr);
+  RSPL_HIP(hipMemsetAsync(S.pair_ctr, 0, sizeof(unsigned) * (size_t)std::max(npairs, 1), b->stream));
   return RSPL_OK;
 }
 

@@ -377,8 +377,7 @@ __device__ __forceinline__ double edge_weight(const Problem& P, const Lin& L, co
 // point edges: analytic Jacobians (g2o types_sba), one thread per edge.  Mono edges
 // carry a zero third row, so every index below is a compile-time constant
 // (register resident, no scratch).
-__global__ __launch_bounds__(256) void linearize_points_kernel(Problem P, Lin L, Active A) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+__device__ __forceinline__ void lin_points(const Problem& P, const Lin& L, const Active& A, int i) {
   if (i >= A.Ea - A.n_line_edges) return;
   const int e = A.edges[i];
   const int t = P.etype[e];
@@ -443,11 +442,11 @@ __global__ __launch_bounds__(256) void linearize_points_kernel(Problem P, Lin L,
 
 // line edges: g2o's numeric central difference (delta 1e-9), one wave per edge,
 // the 20 perturbed error evaluations (+-delta on 4 line + 6 pose dims) in parallel lanes.
-__global__ __launch_bounds__(256) void linearize_lines_kernel(Problem P, Lin L, Active A) {
+__device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const Active& A, int blk) {
   __shared__ double ev[4][20][4];
   __shared__ double J[4][4 * 6 + 4 * 4];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = blockIdx.x * 4 + wv;
+  const int i = blk * 4 + wv;
   const bool live = i < A.n_line_edges;
   int e = 0, t = 2, rows = 2;
   if (live) {
@@ -496,6 +495,13 @@ __global__ __launch_bounds__(256) void linearize_lines_kernel(Problem P, Lin L, 
   const bool pose_opt = A.pidx[pose] >= 0;
   for (int o = lane; o < 86; o += 64) store_contrib(L, e, o, contrib(o, rows, 4, w, er, &J[wv][0], &J[wv][24]), pose_opt);
 }
+// one launch for both edge families: blocks [0, nbp) points (1 edge per thread),
+// blocks [nbp, ...) lines (1 edge per wave)
+__global__ __launch_bounds__(256) void linearize_kernel(Problem P, Lin L, Active A, int nbp) {
+  if ((int)blockIdx.x < nbp) lin_points(P, L, A, blockIdx.x * 256 + threadIdx.x);
+  else lin_lines(P, L, A, blockIdx.x - nbp);
+}
+
 __device__ __forceinline__ void atomic_max_pos(double* addr, double v) {
   // non-negative doubles order like their bit patterns
   atomicMax(reinterpret_cast<unsigned long long*>(addr), (unsigned long long)__double_as_longlong(v));
@@ -699,10 +705,34 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
 #pragma unroll
   for (int v = 0; v < 48; v++) red[lane * 49 + v] = acc[v];
   __syncthreads();
+  // chunk partial, handed off write-through (sc1) to whichever chunk of this pose pair
+  // finishes last; that one sums the pair's chunks in chunk order (deterministic)
   if (lane < 48) {
     double s = 0;
     for (int l = 0; l < 64; l++) s += red[l * 49 + lane];
-    S.chunk[48 * c + lane] = s;
+    __hip_atomic_store(S.chunk + 48 * c + lane, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int pr = A.ch_pair[c];
+  const int c0 = A.pair_choff[pr], c1 = A.pair_choff[pr + 1];
+  unsigned tk = 0;
+  if (lane == 0) tk = __hip_atomic_fetch_add(S.pair_ctr + pr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  tk = __shfl(tk, 0);
+  if (tk != (unsigned)(c1 - c0 - 1)) return;
+  if (lane == 0) __hip_atomic_store(S.pair_ctr + pr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane < 48) {
+    double s = 0;
+    for (int cb = c0; cb < c1; cb += 8) {  // 8 write-through loads in flight, summed in chunk order
+      double t[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++)
+        t[u] = cb + u < c1 ? __hip_atomic_load(S.chunk + 48 * (cb + u) + lane, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                           : 0.0;
+#pragma unroll
+      for (int u = 0; u < 8; u++) s += t[u];
+    }
+    S.pairfin[48 * pr + lane] = s;
   }
 }
 
@@ -733,151 +763,223 @@ __global__ __launch_bounds__(256) void pair_final_kernel(Active A, Sys S, double
 }
 
 // ---------------------------------------------------------------------------
-// Dense Cholesky of the reduced camera system (n = 6K), matrix in LDS (odd row stride),
-// blocked by the 6x6 pose blocks: K sequential steps, each
-//   (1) factor the 6x6 diagonal block (one thread, fully unrolled registers),
-//   (2) panel: every row below solves x L_dd^T = a (one thread per row),
-//   (3) rank-6 update of the trailing lower triangle (16x16 thread grid),
-// then blocked forward / backward substitution on the right-hand side in LDS.
+// Reduced camera system: Schur assembly + dense LDL^T + solve in one 1024-thread
+// workgroup, matrix in LDS (odd row stride), n = 6K <= kCholLdsMax.
+//   assembly: S_ab = [a==b] lambda I + the pair's chunk sum (reduced by its last chunk),
+//             written straight into the lower triangle; bs_a, bp_a alongside;
+//   factor:   blocked by the 6x6 pose blocks, K steps of
+//   LDL^T (pivots need a reciprocal only: v_rcp_f64 + Newton, no sqrt / divide chains):
+//             (1) wave 0 factors the diagonal block in registers and publishes it in LDS,
+//             (2) panel rows solve x L_dd^T = a (one thread per row),
+//             (3) rank-6 update of the trailing lower triangle (32x32 thread grid);
+//   solves:   blocked forward / backward substitution in wave 0 (rhs in registers).
 // ---------------------------------------------------------------------------
-constexpr int kCholLdsMax = 138;  // n (n|1) + 2n doubles <= 160 KB of LDS
+constexpr int kCholLdsMax = 132;  // n (n|1) + 3n + 15 n/6 doubles <= 160 KB of LDS
 
-__global__ __launch_bounds__(256) void cholesky_lds_kernel(Sys S, int n) {
+// 1/d to full precision: v_rcp_f64 + two Newton steps (no divide sequence on the chain)
+__device__ __forceinline__ double rcp64(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return fma(r, fma(-d, r, 1.0), r);
+}
+
+// LDL^T of a 6x6 SPD block (lower triangle at Ld, stride ld): unit L (strictly-lower,
+// packed row-major into L6), D (d6) and 1/D (r6); false unless every pivot is > 0
+__device__ __forceinline__ bool ldl6(const double* Ld, int ld, double (&L6)[15], double (&d6)[6], double (&r6)[6]) {
+  double a[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; i++)
+#pragma unroll
+    for (int k = 0; k <= i; k++) a[i][k] = Ld[i * ld + k];
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    const double d = a[j][j];
+    ok = ok && d > 0;
+    const double r = rcp64(d);
+    d6[j] = d;
+    r6[j] = r;
+    double u[6];
+#pragma unroll
+    for (int i = j + 1; i < 6; i++) u[i] = a[i][j];
+#pragma unroll
+    for (int i = j + 1; i < 6; i++) {
+      const double l = u[i] * r;
+      a[i][j] = l;
+#pragma unroll
+      for (int k = j + 1; k <= i; k++) a[i][k] -= l * u[k];
+    }
+  }
+#pragma unroll
+  for (int i = 0, q = 0; i < 6; i++)
+#pragma unroll
+    for (int k = 0; k < i; k++, q++) L6[q] = a[i][k];
+  return ok;
+}
+
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), lane);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+
+__global__ __launch_bounds__(1024) void schur_solve_kernel(Active A, Sys S, int n, double lambda) {
   extern __shared__ double Al[];
-  __shared__ int bad;
-  const int ld = n | 1;
-  double* rdg = Al + (size_t)n * ld;  // [n] reciprocal diagonal of L
-  double* xs = rdg + n;               // [n] right-hand side -> solution
-  const int tid = threadIdx.x, ty = tid >> 4, tx = tid & 15;
+  __shared__ int bad[1];
+  const int ld = n | 1, K = n / 6;
+  double* xs = Al + (size_t)n * ld;  // [n] rhs -> forward result -> solution
+  double* rdg = xs + n;              // [n] 1/D
+  double* ddg = rdg + n;             // [n] D
+  double* Ldg = ddg + n;             // [K][15] strictly-lower parts of the (unit) diagonal blocks
+  const int tid = threadIdx.x, ty = tid >> 5, tx = tid & 31;
   if (*S.fail) return;
-  for (int i = ty; i < n; i += 16)
-    for (int k = tx; k <= i; k += 16) Al[i * ld + k] = S.S[(size_t)i * n + k];
-  for (int i = tid; i < n; i += 256) xs[i] = S.x[i];
-  if (tid == 0) bad = 0;
+  for (int idx = tid; idx < A.npairs * 42; idx += 1024) {
+    const int pr = idx / 42, v = idx - 42 * pr;
+    const int a = A.pairs[2 * pr], b = A.pairs[2 * pr + 1];
+    const double s = S.pairfin[48 * pr + v];
+    if (v < 36) {
+      const int r = v / 6, cc = v - 6 * r;
+      if (a == b) {
+        if (cc <= r) Al[(6 * a + r) * ld + 6 * a + cc] = s + (r == cc ? lambda : 0.0);
+      } else {
+        Al[(6 * b + cc) * ld + 6 * a + r] = s;
+      }
+    } else if (a == b) {
+      const int r = v - 36;
+      S.bp[6 * a + r] = s;
+      xs[6 * a + r] = s - S.pairfin[48 * pr + v + 6];
+    }
+  }
+  if (tid == 0) *bad = 0;
   __syncthreads();
-  const int K = n / 6;
+  // factor + solve on 4 waves: fewer waves per barrier, the trailing updates are small
+  // (terminated waves drop out of the workgroup barrier)
+  if (tid >= 256) return;
+  const int wv = tid >> 6, lane = tid & 63, fy = tid >> 4, fx = tid & 15;
   for (int s = 0; s < K; s++) {
     const int c0 = 6 * s;
-    double* Ld = Al + c0 * ld + c0;
-    if (tid == 0) {  // (1)
-      double a[6][6];
+    if (wv == 0) {  // (1) one wave factors the diagonal block (fp64 issue is 4 cycles per wave op)
+      double L6[15], d6[6], r6[6];
+      const bool ok = ldl6(Al + c0 * ld + c0, ld, L6, d6, r6);
+      if (lane == 0) {
 #pragma unroll
-      for (int i = 0; i < 6; i++)
+        for (int q = 0; q < 15; q++) Ldg[15 * s + q] = L6[q];
 #pragma unroll
-        for (int k = 0; k <= i; k++) a[i][k] = Ld[i * ld + k];
-      bool ok = true;
-#pragma unroll
-      for (int j = 0; j < 6; j++) {
-        const double v = a[j][j];
-        ok = ok && v > 0;
-        const double d = sqrt(v), r = 1.0 / d;
-        a[j][j] = d;
-        rdg[c0 + j] = r;
-#pragma unroll
-        for (int i = j + 1; i < 6; i++) a[i][j] *= r;
-#pragma unroll
-        for (int i = j + 1; i < 6; i++)
-#pragma unroll
-          for (int k = j + 1; k <= i; k++) a[i][k] -= a[i][j] * a[k][j];
+        for (int k = 0; k < 6; k++) {
+          rdg[c0 + k] = r6[k];
+          ddg[c0 + k] = d6[k];
+        }
+        if (!ok) *bad = 1;
       }
-#pragma unroll
-      for (int i = 0; i < 6; i++)
-#pragma unroll
-        for (int k = 0; k <= i; k++) Ld[i * ld + k] = a[i][k];
-      if (!ok) bad = 1;
     }
     __syncthreads();
-    if (bad) {  // LDS flag after the barrier: uniform
+    if (*bad) {  // LDS flag after the barrier: uniform
       if (tid == 0) atomicOr(S.fail, 1);
       return;
     }
-    double L6[21], r6[6];  // the factored diagonal block, broadcast to every thread
+    const int r0 = c0 + 6;
+    if (r0 + tid < n) {  // (2) panel row: x = a L_dd^-T D^-1 (unit L: no divides on the chain)
+      double* row = Al + (r0 + tid) * ld + c0;
+      double w[6];
 #pragma unroll
-    for (int i = 0, q = 0; i < 6; i++)
-#pragma unroll
-      for (int k = 0; k < i; k++, q++) L6[q] = Ld[i * ld + k];
-#pragma unroll
-    for (int k = 0; k < 6; k++) r6[k] = rdg[c0 + k];
-    for (int i = c0 + 6 + tid; i < n; i += 256) {  // (2)
-      double* row = Al + i * ld + c0;
-      double x[6];
-#pragma unroll
-      for (int k = 0; k < 6; k++) x[k] = row[k];
+      for (int k = 0; k < 6; k++) w[k] = row[k];
 #pragma unroll
       for (int k = 0, q = 0; k < 6; k++) {
-        double v = x[k];
 #pragma unroll
-        for (int l = 0; l < k; l++, q++) v -= x[l] * L6[q];
-        x[k] = v * r6[k];
+        for (int l = 0; l < k; l++, q++) w[k] -= w[l] * Ldg[15 * s + q];
       }
 #pragma unroll
-      for (int k = 0; k < 6; k++) row[k] = x[k];
+      for (int k = 0; k < 6; k++) row[k] = w[k] * rdg[c0 + k];
     }
     __syncthreads();
-    const int r0 = c0 + 6;  // (3)
-    for (int i = r0 + ty; i < n; i += 16) {
-      double li[6];
+    for (int i = r0 + fy; i < n; i += 16) {  // (3) trailing update A22 -= X D X^T
+      double wi[6];
 #pragma unroll
-      for (int l = 0; l < 6; l++) li[l] = Al[i * ld + c0 + l];
-      for (int k = r0 + tx; k <= i; k += 16) {
-        const double* lk = Al + k * ld + c0;
+      for (int l = 0; l < 6; l++) wi[l] = Al[i * ld + c0 + l] * ddg[c0 + l];
+      for (int k = r0 + fx; k <= i; k += 16) {
+        const double* xk = Al + k * ld + c0;
         double t = Al[i * ld + k];
 #pragma unroll
-        for (int l = 0; l < 6; l++) t -= li[l] * lk[l];
+        for (int l = 0; l < 6; l++) t -= wi[l] * xk[l];
         Al[i * ld + k] = t;
       }
     }
     __syncthreads();
   }
-  for (int s = 0; s < K; s++) {  // L y = b
+  // solves in wave 0 alone: rows lane, lane+64, lane+128 in registers, block values
+  // broadcast by readlane, no barriers
+  if (wv != 0) return;
+  double x0 = lane < n ? xs[lane] : 0.0, x1 = lane + 64 < n ? xs[lane + 64] : 0.0,
+         x2 = lane + 128 < n ? xs[lane + 128] : 0.0;
+#define RSPL_GET(j) readlane_f64(((j) >> 6) == 0 ? x0 : (((j) >> 6) == 1 ? x1 : x2), (j) & 63)
+#define RSPL_PUT(j, v)                                   \
+  do {                                                   \
+    const bool me = lane == ((j) & 63);                  \
+    const int sl = (j) >> 6;                             \
+    x0 = (me && sl == 0) ? (v) : x0;                     \
+    x1 = (me && sl == 1) ? (v) : x1;                     \
+    x2 = (me && sl == 2) ? (v) : x2;                     \
+  } while (0)
+  for (int s = 0; s < K; s++) {  // L y = b (unit diagonal)
     const int c0 = 6 * s;
-    if (tid == 0) {
-      double y[6];
+    double y[6];
 #pragma unroll
-      for (int k = 0; k < 6; k++) {
-        double v = xs[c0 + k];
+    for (int k = 0, q = 0; k < 6; k++) {
+      double v = RSPL_GET(c0 + k);
 #pragma unroll
-        for (int l = 0; l < k; l++) v -= y[l] * Al[(c0 + k) * ld + c0 + l];
-        y[k] = v * rdg[c0 + k];
-      }
-#pragma unroll
-      for (int k = 0; k < 6; k++) xs[c0 + k] = y[k];
+      for (int l = 0; l < k; l++, q++) v -= y[l] * Ldg[15 * s + q];
+      y[k] = v;
     }
-    __syncthreads();
-    for (int i = c0 + 6 + tid; i < n; i += 256) {
-      const double* row = Al + i * ld + c0;
-      double v = xs[i];
 #pragma unroll
-      for (int l = 0; l < 6; l++) v -= row[l] * xs[c0 + l];
-      xs[i] = v;
+    for (int k = 0; k < 6; k++) RSPL_PUT(c0 + k, y[k]);
+    const int lo = c0 + 6;
+#define RSPL_FWD(xv, i)                                          \
+    if ((i) >= lo && (i) < n) {                                  \
+      const double* row = Al + (i) * ld + c0;                    \
+      double v = xv;                                             \
+      for (int l = 0; l < 6; l++) v -= row[l] * y[l];            \
+      xv = v;                                                    \
     }
-    __syncthreads();
+    RSPL_FWD(x0, lane)
+    RSPL_FWD(x1, lane + 64)
+    RSPL_FWD(x2, lane + 128)
+#undef RSPL_FWD
   }
-  for (int s = K - 1; s >= 0; s--) {  // L^T x = y
+  // z = D^-1 y
+  if (lane < n) x0 *= rdg[lane];
+  if (lane + 64 < n) x1 *= rdg[lane + 64];
+  if (lane + 128 < n) x2 *= rdg[lane + 128];
+  for (int s = K - 1; s >= 0; s--) {  // L^T x = z (unit diagonal)
     const int c0 = 6 * s;
-    if (tid == 0) {
-      double z[6];
+    double z[6];
 #pragma unroll
-      for (int k = 5; k >= 0; k--) {
-        double v = xs[c0 + k];
+    for (int k = 5; k >= 0; k--) {
+      double v = RSPL_GET(c0 + k);
 #pragma unroll
-        for (int l = k + 1; l < 6; l++) v -= z[l] * Al[(c0 + l) * ld + c0 + k];
-        z[k] = v * rdg[c0 + k];
-      }
-#pragma unroll
-      for (int k = 0; k < 6; k++) xs[c0 + k] = z[k];
+      for (int l = k + 1; l < 6; l++) v -= z[l] * Ldg[15 * s + l * (l - 1) / 2 + k];
+      z[k] = v;
     }
-    __syncthreads();
-    for (int i = tid; i < c0; i += 256) {
-      double v = xs[i];
 #pragma unroll
-      for (int l = 0; l < 6; l++) v -= Al[(c0 + l) * ld + i] * xs[c0 + l];
-      xs[i] = v;
+    for (int k = 0; k < 6; k++) RSPL_PUT(c0 + k, z[k]);
+#define RSPL_BWD(xv, i)                                          \
+    if ((i) < c0) {                                              \
+      double v = xv;                                             \
+      for (int l = 0; l < 6; l++) v -= Al[(c0 + l) * ld + (i)] * z[l]; \
+      xv = v;                                                    \
     }
-    __syncthreads();
+    RSPL_BWD(x0, lane)
+    RSPL_BWD(x1, lane + 64)
+    RSPL_BWD(x2, lane + 128)
+#undef RSPL_BWD
   }
-  for (int i = tid; i < n; i += 256) S.x[i] = xs[i];
+#undef RSPL_GET
+#undef RSPL_PUT
+  if (lane < n) S.x[lane] = x0;
+  if (lane + 64 < n) S.x[lane + 64] = x1;
+  if (lane + 128 < n) S.x[lane + 128] = x2;
 }
+
 
 // larger systems: one workgroup on global memory
 
@@ -1049,9 +1151,8 @@ hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& 
 
 hipError_t linearize(const Problem& P, const Lin& L, const Active& A, hipStream_t s) {
   const int npt = A.Ea - A.n_line_edges;
-  if (npt > 0) hipLaunchKernelGGL(linearize_points_kernel, dim3((npt + 255) / 256), dim3(256), 0, s, P, L, A);
-  if (A.n_line_edges > 0)
-    hipLaunchKernelGGL(linearize_lines_kernel, dim3((A.n_line_edges + 3) / 4), dim3(256), 0, s, P, L, A);
+  const int nbp = (npt + 255) / 256, nbl = (A.n_line_edges + 3) / 4;
+  if (nbp + nbl > 0) hipLaunchKernelGGL(linearize_kernel, dim3(nbp + nbl), dim3(256), 0, s, P, L, A, nbp);
   return hipGetLastError();
 }
 
@@ -1070,20 +1171,21 @@ hipError_t post(Sys& S, unsigned long long seq, hipStream_t s) {
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
                  hipStream_t s) {
   if (A.nch > 0) hipLaunchKernelGGL(pair_chunk_kernel, dim3(A.nch), dim3(64), 0, s, P, L, A, S, lambda);
-  if (A.npairs > 0)
-    hipLaunchKernelGGL(pair_final_kernel, dim3((A.npairs * 42 + 255) / 256), dim3(256), 0, s, A, S, lambda);
   const int n = 6 * A.K;
   if (n > 0 && n <= kCholLdsMax) {
     static bool attr = false;
+    const int nm = kCholLdsMax;
+    const size_t max_bytes = sizeof(double) * ((size_t)nm * (nm | 1) + 3 * nm + 15 * (nm / 6));
     if (!attr) {
-      hipError_t e = hipFuncSetAttribute((const void*)cholesky_lds_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)(sizeof(double) * (kCholLdsMax * (kCholLdsMax | 1) + 2 * kCholLdsMax)));
+      hipError_t e = hipFuncSetAttribute((const void*)schur_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)max_bytes);
       if (e != hipSuccess) return e;
       attr = true;
     }
-    const size_t bytes = sizeof(double) * ((size_t)n * (n | 1) + 2 * n);
-    hipLaunchKernelGGL(cholesky_lds_kernel, dim3(1), dim3(256), bytes, s, S, n);
+    const size_t bytes = sizeof(double) * ((size_t)n * (n | 1) + 3 * n + 15 * (n / 6));
+    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(1024), bytes, s, A, S, n, lambda);
   } else if (n > 0) {
+    hipLaunchKernelGGL(pair_final_kernel, dim3((A.npairs * 42 + 255) / 256), dim3(256), 0, s, A, S, lambda);
     hipLaunchKernelGGL(cholesky_kernel, dim3(1), dim3(256), 0, s, S, n);
   }
   const int nbu = update_blocks(P);

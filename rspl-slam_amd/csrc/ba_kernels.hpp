@@ -50,6 +50,7 @@ struct Active {          // active structure of one optimize() phase
   int npairs;
   const int* pair_choff; // [npairs+1] CSR of Schur chunks per pose pair
   const int* ch_beg;     // [nch] edge-pair range [beg, end) of each chunk
+  const int* ch_pair;    // [nch] pose pair of each chunk
   const int* ch_end;
   int nch;
   const int* pp_e1;      // edge pairs (e1 of pose a, e2 of pose b, same landmark), grouped by pose pair
@@ -72,6 +73,8 @@ struct Sys {
   double* S;             // [6K][6K] reduced camera system
   double* x;             // [6K]     bs on entry of the solve, xp on exit
   double* chunk;         // [nch][48] Schur chunk partials
+  double* pairfin;       // [npairs][48] per-pose-pair sums of the chunk partials
+  unsigned* pair_ctr;    // [npairs] chunk tickets (re-armed to 0 by the last chunk)
   double* partial;       // [>= error blocks] chi2 partials
   double* partial2;      // [>= update blocks] scale partials
   double* out;           // [8]: 0 chi2, 1 scale, 2 maxdiag, 3 fail

@@ -101,3 +101,12 @@ def test_localmap_optimization_mirror(weight_blobs):
     np.testing.assert_allclose(np.array([points[k].p for k in qid]), ref.points, atol=1e-6)
     np.testing.assert_array_equal(np.array([c.inlier for c in mono]), ref.inlier["mono"].astype(bool))
     np.testing.assert_array_equal(np.array([c.inlier for c in stereo]), ref.inlier["stereo"].astype(bool))
+
+
+@pytest.mark.parametrize("n_poses", [23, 27])
+def test_ba_many_poses(ba, n_poses):
+    # K = 22 optimised poses is the largest reduced system the LDS Schur/Cholesky path holds
+    # (n = 132); K = 26 takes the global-memory fallback (pair_final + cholesky_kernel)
+    prob, gt = SY.ba_problem(n_poses=n_poses, n_points=1500, n_lines=20, seed=40 + n_poses, pixel_sigma=0.8,
+                             outlier_frac=0.05)
+    _compare(ba.run(prob), oracle.ba_local(prob), tol_pose=1e-6, tol_pt=1e-5)
