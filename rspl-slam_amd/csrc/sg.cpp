@@ -3,6 +3,7 @@
 // PointMatching::MatchingPoints (src/point_matching.cc:34-70).
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -240,6 +241,7 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
 
 extern "C" void rspl_sg_destroy(rspl_sg* s) {
   if (!s) return;
+
   if (s->stream) (void)hipStreamSynchronize(s->stream);
   s->arena.release();
   s->timer.destroy();
@@ -314,10 +316,25 @@ extern "C" int rspl_sg_infer_device(rspl_sg* s, int B, const double* d_feat0, co
   s->timer.mark(3, st);
   // log_optimal_transport (superglue.py:185-205)
   RSPL_HIP(hipMemsetAsync(s->err, 0, sizeof(unsigned) * B, st));
+  static unsigned long long* probe = nullptr;  // debug only (RSPL_SG_PROBE)
+  static const bool probing = getenv("RSPL_SG_PROBE") != nullptr;
+  if (probing && !probe) {
+    RSPL_HIP(hipMalloc(&probe, 4 * sizeof(unsigned long long)));
+    RSPL_HIP(hipMemset(probe, 0, 4 * sizeof(unsigned long long)));
+  }
   sg::SinkArgs sk{};
+  sk.probe = probe;
   sk.cpl = s->cpl; sk.Z = s->Z; sk.part = s->part; sk.seq = s->sk_seq = (s->sk_seq % 0xFFFFFu) + 1; sk.err = s->err; sk.n0 = d_n0; sk.n1 = d_n1;
   sk.nmax = nm; sk.G = s->G; sk.iters = s->cfg.sinkhorn_iterations;
   RSPL_HIP(sg::sinkhorn(sk, B, st));
+  if (probing) {  // debug: Sinkhorn cycles per workgroup-iteration by phase
+    unsigned long long h[4];
+    RSPL_HIP(hipStreamSynchronize(st));
+    RSPL_HIP(hipMemcpy(h, probe, sizeof(h), hipMemcpyDeviceToHost));
+    RSPL_HIP(hipMemset(probe, 0, sizeof(h)));
+    if (h[3]) fprintf(stderr, "sinkhorn cycles/iter: row %.0f col %.0f exchange %.0f\n", (double)h[0] / h[3],
+                      (double)h[1] / h[3], (double)h[2] / h[3]);
+  }
   s->timer.mark(4, st);
   // decode (super_glue.cpp:339-367), threshold 0.2 hard-coded as in the reference (:355)
   sg::DecodeArgs dc{};

@@ -407,6 +407,28 @@ __device__ __forceinline__ float wave_sum(float v) {
   for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
   return v;
 }
+// DPP all-reduce over a wave64: quad swaps + half-row/row mirrors (in-row), then the
+// four row results combined through readlane (uniform).  Fixed structure: deterministic.
+template <int CTRL>
+__device__ __forceinline__ float dppf(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float rdlane(float v, int l) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l)); }
+__device__ __forceinline__ float wave_max_dpp(float v) {
+  v = fmaxf(v, dppf<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = fmaxf(v, dppf<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = fmaxf(v, dppf<0x141>(v));  // row_half_mirror
+  v = fmaxf(v, dppf<0x140>(v));  // row_mirror
+  return fmaxf(fmaxf(rdlane(v, 0), rdlane(v, 16)), fmaxf(rdlane(v, 32), rdlane(v, 48)));
+}
+__device__ __forceinline__ float wave_sum_dpp(float v) {
+  v += dppf<0xB1>(v);
+  v += dppf<0x4E>(v);
+  v += dppf<0x141>(v);
+  v += dppf<0x140>(v);
+  return (rdlane(v, 0) + rdlane(v, 16)) + (rdlane(v, 32) + rdlane(v, 48));
+}
+
 __device__ __forceinline__ void st_sc1(float* p, float v) {
   __hip_atomic_store(reinterpret_cast<unsigned*>(p), __float_as_uint(v), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -452,19 +474,41 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_kernel(SinkArgs a) {
   __syncthreads();
   const int half = tid >> 9, jj = tid & 511;
   const int rh = (nr + 1) >> 1, ra = half ? rh : 0, rb = half ? nr : rh;
+  long long pr_row = 0, pr_col = 0, pr_ex = 0;
   for (int it = 0; it < a.iters; it++) {
-    // u_i = log_mu_i - LSE_j(C_ij + v_j): one wave per row
+    const long long q0 = __builtin_amdgcn_s_memtime();
+    // u_i = log_mu_i - LSE_j(C_ij + v_j): one wave per row; each lane's 8-column chunk is
+    // loaded into registers first (all loads in flight), then max, then independent exps
     for (int r = wv; r < nr; r += NW) {
       const float* row = Cr + (size_t)r * ld;
       float mx = -INFINITY;
-      for (int j = lane; j < Cc; j += 64) mx = fmaxf(mx, row[j] + v[j]);
-      mx = wave_max(mx);
+      for (int j0 = 0; j0 < Cc; j0 += 512) {
+        float x[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+          const int j = j0 + lane + 64 * t;
+          x[t] = j < Cc ? row[j] + v[j] : -INFINITY;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; t++) mx = fmaxf(mx, x[t]);
+      }
+      mx = wave_max_dpp(mx);
       float s = 0.f;
-      for (int j = lane; j < Cc; j += 64) s += expf(row[j] + v[j] - mx);
-      s = wave_sum(s);
+      for (int j0 = 0; j0 < Cc; j0 += 512) {
+        float e[8];
+#pragma unroll
+        for (int t = 0; t < 8; t++) {
+          const int j = j0 + lane + 64 * t;
+          e[t] = j < Cc ? expf(row[j] + v[j] - mx) : 0.f;
+        }
+#pragma unroll
+        for (int t = 0; t < 8; t++) s += e[t];
+      }
+      s = wave_sum_dpp(s);
       if (lane == 0) u[r] = ((r0 + r) < m ? norm : lmu_bin) - (logf(s) + mx);
     }
     __syncthreads();
+    const long long q1 = __builtin_amdgcn_s_memtime();
     // column partial LSE over this slab (two row halves merged in LDS), published as tagged
     // 8-byte granules (value + tag in one single-copy-atomic write-through store: no flag,
     // no arrival counter); slots double-buffered by iteration parity
@@ -472,13 +516,25 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_kernel(SinkArgs a) {
     const unsigned tag = (a.seq << 12) | (unsigned)(it + 1);
     for (int c0 = 0; c0 < Cc; c0 += 512) {
       const int j = c0 + jj;
-      if (j < Cc) {
-        float mx = -INFINITY;
-#pragma unroll 4
-        for (int r = ra; r < rb; r++) mx = fmaxf(mx, Cr[(size_t)r * ld + j] + u[r]);
-        float s = 0.f;
-#pragma unroll 4
-        for (int r = ra; r < rb; r++) s += expf(Cr[(size_t)r * ld + j] + u[r] - mx);
+      if (j < Cc) {  // rows in register batches of 16: loads in flight together, independent exps
+        float mx = -INFINITY, s = 0.f;
+        for (int rb0 = ra; rb0 < rb; rb0 += 16) {
+          float x[16];
+#pragma unroll
+          for (int t = 0; t < 16; t++) {
+            const int r = rb0 + t;
+            x[t] = r < rb ? Cr[(size_t)r * ld + j] + u[r] : -INFINITY;
+          }
+          float bm = -INFINITY;
+#pragma unroll
+          for (int t = 0; t < 16; t++) bm = fmaxf(bm, x[t]);
+          const float nm = fmaxf(mx, bm);
+          float bs = 0.f;
+#pragma unroll
+          for (int t = 0; t < 16; t++) bs += x[t] == -INFINITY ? 0.f : expf(x[t] - nm);
+          s = (mx == -INFINITY ? 0.f : s * expf(mx - nm)) + bs;
+          mx = nm;
+        }
         cm[half * 512 + jj] = mx;
         cs[half * 512 + jj] = s;
       }
@@ -496,6 +552,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_kernel(SinkArgs a) {
       }
       __syncthreads();
     }
+    const long long q2 = __builtin_amdgcn_s_memtime();
     // v_j = log_nu_j - LSE_g(partial_g,j): poll the G granules of a column (all loads in
     // flight together; only the stale ones are re-read), bounded
     bool timed_out = false;
@@ -536,7 +593,17 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_kernel(SinkArgs a) {
       *flag = 1.f;
     }
     __syncthreads();
+    const long long q3 = __builtin_amdgcn_s_memtime();
+    pr_row += q1 - q0;
+    pr_col += q2 - q1;
+    pr_ex += q3 - q2;
     if (*flag != 0.f) break;
+  }
+  if (a.probe && tid == 0) {
+    atomicAdd(a.probe + 0, (unsigned long long)pr_row);
+    atomicAdd(a.probe + 1, (unsigned long long)pr_col);
+    atomicAdd(a.probe + 2, (unsigned long long)pr_ex);
+    atomicAdd(a.probe + 3, (unsigned long long)a.iters);
   }
   // Z = couplings + u + v - norm
   float* Z = a.Z + (size_t)p * ld * ld + (size_t)r0 * ld;

@@ -65,6 +65,7 @@ struct SinkArgs {
   float* Z;           // [B][ld*ld]
   unsigned long long* part;  // [B][2][G][ld] tagged column partial LSEs {f32 bits, tag}
   unsigned seq;       // per-call tag base (never 0; granules start zeroed)
+  unsigned long long* probe;  // optional [4] cycle counters (RSPL_SG_PROBE): row, col, exchange, iters
   unsigned* err;      // [B] timeout flags
   const int* n0;
   const int* n1;
