@@ -35,7 +35,7 @@ struct rspl_ba {
   int *epose, *elm, *ecam;
   // per-edge linearisation records
   double *err, *rho0, *Hpp_e, *bp_e, *Hll_e, *bl_e, *Hpl_e;
-  uint8_t *level, *inlier;
+  uint8_t *level, *inlier, *lm_act2;
   // system
   double *Hll, *bl, *bp, *S, *x, *partial, *partial2, *out;
   int* flags;  // [0] fail, [1] error-kernel ticket counter
@@ -76,7 +76,7 @@ void carve(F& ar, rspl_ba* b) {
   take(b->eobs, E * 8); take(b->etype, E); take(b->epose, E); take(b->elm, E); take(b->ecam, E);
   take(b->err, E * 4); take(b->rho0, E); take(b->Hpp_e, E * 36); take(b->bp_e, E * 6); take(b->Hll_e, E * 16);
   take(b->bl_e, E * 4); take(b->Hpl_e, E * 24);
-  take(b->level, E); take(b->inlier, E);
+  take(b->level, E); take(b->inlier, E); take(b->lm_act2, NL);
   take(b->Hll, NL * 16); take(b->bl, NL * 4); take(b->bp, K * 6);
   take(b->S, 36 * K * K); take(b->x, 6 * K); take(b->partial, E / 256 + 2);
   take(b->partial2, (size_t)b->maxV / 256 + 2); take(b->out, 8); take(b->flags, 4);
@@ -178,6 +178,13 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
                  ba::Active& A, ba::Sys& S) {
   auto& w = b->ws;
   const int Ea = (int)act.size();
+  static const bool btiming = getenv("RSPL_BA_TIMING") != nullptr;
+  std::chrono::steady_clock::time_point bt[5];
+  int nbt = 0;
+  auto bmark = [&]() {
+    if (btiming) bt[nbt++] = std::chrono::steady_clock::now();
+  };
+  bmark();
   w.pidx.assign(np, -1);
   w.lact.assign(nL, 0);
   {
@@ -204,6 +211,7 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
       w.lm_pose[k] = w.pidx[epose[e]];
     }
   }
+  bmark();
   // counts: edges per reduced pose, edge pairs per pose pair (a <= c)
   const int npairs = K * (K + 1) / 2;
   auto pid = [K](int a, int c) { return a * K - a * (a - 1) / 2 + (c - a); };
@@ -226,6 +234,7 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
   for (int p = 0; p < npairs; p++) nch += (w.pp_cnt[p + 1] + ba::kChunk - 1) / ba::kChunk;
   for (int p = 0; p < npairs; p++) w.pp_cnt[p + 1] += w.pp_cnt[p];
   const int npp = w.pp_cnt[npairs], nps = w.ps_cnt[K];
+  bmark();
   // layout (identical in staging and device buffer)
   size_t off = 0;
   auto place = [&](size_t bytes) {
@@ -277,6 +286,7 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
       }
     choff[npairs] = c;
   }
+  bmark();
   {  // fills in landmark order: per-pose edge lists and per-pair edge pairs come out landmark-sorted
     int* pse = I(o_pse);
     int* e1 = I(o_e1);
@@ -303,6 +313,12 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
   for (int e : act)
     if (etype[e] >= 2) n_line_edges++;
   RSPL_HIP(hipMemcpyAsync(b->phase_buf, st, upload, hipMemcpyHostToDevice, b->stream));
+  bmark();
+  if (btiming && nbt == 5) {
+    auto us = [&](int i) { return std::chrono::duration<double, std::micro>(bt[i + 1] - bt[i]).count(); };
+    fprintf(stderr, "build_active us: csr %.0f counts %.0f layout+copies %.0f fill+upload %.0f (Ea %d pairs %d npp %d)\n",
+            us(0), us(1), us(2), us(3), Ea, npairs, npp);
+  }
   auto dptr = [&](size_t o) { return reinterpret_cast<const int*>(b->phase_buf + o); };
   A.edges = dptr(o_act); A.Ea = Ea; A.pidx = dptr(o_pidx); A.lm_off = dptr(o_lmoff);
   A.lm_edges = dptr(o_lme); A.lm_pose = dptr(o_lmp);
@@ -542,10 +558,10 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   S.mail = b->mail_dev;
   const size_t phase_soff = al256(call_bytes);
   // ---- phase 1: all edges, Huber ----
+  ba::Active A{};
   {
     std::vector<int> act(E);
     std::iota(act.begin(), act.end(), 0);
-    ba::Active A{};
     mark();
     if ((rc = build_active(b, act, epose, elm, etype, pr->pose_fixed, np, nL, 1, phase_soff, A, S))) return rc;
     mark();
@@ -554,19 +570,15 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
     mark();
   }
   RSPL_HIP(ba::classify(P, Lr, E, b->level, nullptr, 0, st));
-  if (E) RSPL_HIP(hipMemcpyAsync(b->stage, b->level, E, hipMemcpyDeviceToHost, st));
-  unsigned long long q = ++b->seq;
-  RSPL_HIP(ba::post(S, q, st));
-  if ((rc = wait_mail(b, q, nullptr))) return rc;
-  // ---- phase 2: level-0 edges, no kernel ----
+  mark();
+  // ---- phase 2: level-0 edges, no kernel (initializeOptimization(0), :176-213) ----
+  // Same active structure with the level-1 edges masked (exact-zero records, no cost, errors
+  // kept as g2o keeps them), landmark activity recomputed from the levels on the device.
   {
-    std::vector<int> act;
-    act.reserve(E);
-    for (int i = 0; i < E; i++)
-      if (!b->stage[i]) act.push_back(i);
-    ba::Active A{};
-    mark();
-    if ((rc = build_active(b, act, epose, elm, etype, pr->pose_fixed, np, nL, 0, phase_soff, A, S))) return rc;
+    A.robust = 0;
+    A.elevel = b->level;
+    RSPL_HIP(ba::landmark_active(A, b->level, b->lm_act2, st));
+    A.lm_act = b->lm_act2;
     mark();
     if ((rc = optimize(b, P, Lr, S, A, pr->iterations_second, &res->chi2_second, &res->iterations_done_second)))
       return rc;
@@ -578,7 +590,7 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   if (np) RSPL_HIP(hipMemcpyAsync(b->stage + d_T, P.T, sizeof(double) * 8 * np, hipMemcpyDeviceToHost, st));
   if (nq) RSPL_HIP(hipMemcpyAsync(b->stage + d_X, P.X, sizeof(double) * 3 * nq, hipMemcpyDeviceToHost, st));
   if (nl) RSPL_HIP(hipMemcpyAsync(b->stage + d_L, P.L, sizeof(double) * 6 * nl, hipMemcpyDeviceToHost, st));
-  q = ++b->seq;
+  const unsigned long long q = ++b->seq;
   RSPL_HIP(ba::post(S, q, st));
   if ((rc = wait_mail(b, q, nullptr))) return rc;
   if (nq) memcpy(res->points, b->stage + d_X, sizeof(double) * 3 * nq);

@@ -254,7 +254,7 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
   __shared__ int last;
   const int i = blockIdx.x * 256 + threadIdx.x;
   double c = 0.0;
-  if (i < A.Ea) {
+  if (i < A.Ea && (!A.elevel || !A.elevel[A.edges[i]])) {
     const int e = A.edges[i];
     const int t = P.etype[e];
     const SE3 T = load_T(P.T + 8 * P.epose[e]);
@@ -380,6 +380,21 @@ __device__ __forceinline__ double edge_weight(const Problem& P, const Lin& L, co
 __device__ __forceinline__ void lin_points(const Problem& P, const Lin& L, const Active& A, int i) {
   if (i >= A.Ea - A.n_line_edges) return;
   const int e = A.edges[i];
+  if (A.elevel && A.elevel[e]) {  // outside this phase: exact-zero records
+#pragma unroll
+    for (int k = 0; k < 16; k++) L.Hll[16 * e + k] = 0.0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) L.bl[4 * e + k] = 0.0;
+    if (A.pidx[P.epose[e]] >= 0) {
+#pragma unroll
+      for (int k = 0; k < 36; k++) L.Hpp[36 * e + k] = 0.0;
+#pragma unroll
+      for (int k = 0; k < 6; k++) L.bp[6 * e + k] = 0.0;
+#pragma unroll
+      for (int k = 0; k < 24; k++) L.Hpl[24 * e + k] = 0.0;
+    }
+    return;
+  }
   const int t = P.etype[e];
   const int pose = P.epose[e], g = P.elm[e];
   const double* cam = P.cams + 5 * P.ecam[e];
@@ -447,12 +462,17 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
   __shared__ double J[4][4 * 6 + 4 * 4];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = blk * 4 + wv;
-  const bool live = i < A.n_line_edges;
+  bool live = i < A.n_line_edges;
   int e = 0, t = 2, rows = 2;
   if (live) {
     e = A.edges[A.Ea - A.n_line_edges + i];
     t = P.etype[e];
     rows = edim(t);
+    if (A.elevel && A.elevel[e]) {  // outside this phase: exact-zero records (wave-uniform)
+      const bool po = A.pidx[P.epose[e]] >= 0;
+      for (int o = lane; o < 86; o += 64) store_contrib(L, e, o, 0.0, po);
+      live = false;
+    }
   }
   const int pose = live ? P.epose[e] : 0, g = live ? P.elm[e] : P.nq;
   const double* cam = P.cams + 5 * (live ? P.ecam[e] : 0);
@@ -1112,6 +1132,14 @@ __global__ __launch_bounds__(256) void update_kernel(Problem P, Lin L, Active A,
   if (threadIdx.x == 0) S.partial2[blockIdx.x] = s;
 }
 
+__global__ __launch_bounds__(256) void landmark_active_kernel(Active A, const uint8_t* level, uint8_t* lm_act) {
+  const int g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= A.nL) return;
+  uint8_t on = 0;
+  for (int k = A.lm_off[g]; k < A.lm_off[g + 1]; k++) on |= level[A.lm_edges[k]] == 0;
+  lm_act[g] = on;
+}
+
 // outlier levels after the first optimize / final inlier flags (g2o_optimization.cc:176-231)
 __global__ __launch_bounds__(256) void classify_kernel(Problem P, Lin L, int E, uint8_t* level, uint8_t* inlier,
                                                        int final_pass) {
@@ -1193,6 +1221,11 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
   Problem Pn = P;  // cost of the candidate state
   Pn.T = P.Tn; Pn.X = P.Xn; Pn.L = P.Ln;
   hipLaunchKernelGGL(errors_kernel, dim3(errors_blocks(A.Ea)), dim3(256), 0, s, Pn, L, A, S, nbu, seq);
+  return hipGetLastError();
+}
+
+hipError_t landmark_active(const Active& A, const uint8_t* level, uint8_t* lm_act, hipStream_t s) {
+  if (A.nL > 0) hipLaunchKernelGGL(landmark_active_kernel, dim3((A.nL + 255) / 256), dim3(256), 0, s, A, level, lm_act);
   return hipGetLastError();
 }
 

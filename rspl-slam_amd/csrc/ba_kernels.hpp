@@ -56,6 +56,8 @@ struct Active {          // active structure of one optimize() phase
   const int* pp_e1;      // edge pairs (e1 of pose a, e2 of pose b, same landmark), grouped by pose pair
   const int* pp_e2;
   int n_line_edges;      // active line edges are edges[Ea - n_line_edges .. Ea) (input order)
+  const uint8_t* elevel; // [E] or null: edge level (!= 0: outside this phase -- level 1 in the
+                         // second optimize): zero linearisation records, no cost, error kept
   int K, nL;
   int robust;
 };
@@ -95,6 +97,8 @@ hipError_t post(Sys& S, unsigned long long seq, hipStream_t s);
 // one LM trial: Schur complement, Cholesky, back-substitution + candidate state, its cost
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
                  hipStream_t s);
+// lm_act[g] = landmark g has an edge of level 0 (the second optimize's active landmarks)
+hipError_t landmark_active(const Active& A, const uint8_t* level, uint8_t* lm_act, hipStream_t s);
 hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8_t* inlier, int final_pass,
                     hipStream_t s);
 int update_blocks(const Problem& P);
