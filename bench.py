@@ -164,7 +164,8 @@ def main():
     f0, f1 = capi.DeviceBuffer(2 * FB), capi.DeviceBuffer(2 * FB)
     n0, n1 = capi.DeviceBuffer(8), capi.DeviceBuffer(8)
     outs = [capi.DeviceBuffer(2 * K * sz) for sz in (4, 4, 8, 8)]
-    st_sp, st_sg = capi.Stream(), capi.Stream()
+    # SG is the frame's critical chain (SP has slack): SG and the BA run at high priority
+    st_sp, st_sg = capi.Stream(), capi.Stream(high_priority=True)
     ev_sp = [capi.Event() for _ in range(3)]
     ev_sg = [capi.Event() for _ in range(3)]
     capi.synchronize()

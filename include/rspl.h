@@ -57,6 +57,8 @@ int rspl_memcpy_d2h(void* dst, const void* src, size_t bytes, void* stream);
 int rspl_memset(void* dst, int value, size_t bytes, void* stream);
 int rspl_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 int rspl_stream_create(void** stream);
+/* high != 0: the device's highest stream priority (latency-critical chains) */
+int rspl_stream_create_priority(void** stream, int high);
 int rspl_stream_destroy(void* stream);
 int rspl_stream_synchronize(void* stream);
 int rspl_device_synchronize(void);

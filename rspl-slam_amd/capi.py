@@ -18,7 +18,7 @@ RSPL_PREC_FP16 = 1
 EXPORTS = [
     "rspl_last_error", "rspl_version",
     "rspl_device_count", "rspl_set_device", "rspl_malloc", "rspl_free", "rspl_memcpy_h2d", "rspl_memcpy_d2h",
-    "rspl_memset", "rspl_memcpy_d2d", "rspl_stream_create", "rspl_stream_destroy", "rspl_stream_synchronize",
+    "rspl_memset", "rspl_memcpy_d2d", "rspl_stream_create", "rspl_stream_create_priority", "rspl_stream_destroy", "rspl_stream_synchronize",
     "rspl_device_synchronize", "rspl_event_create", "rspl_event_record", "rspl_stream_wait_event",
     "rspl_event_destroy", "rspl_timer_create", "rspl_timer_record", "rspl_timer_elapsed_ms",
     "rspl_timer_destroy",
@@ -87,6 +87,7 @@ def load(path: pathlib.Path = LIB_PATH):
     lib.rspl_sp_profile.argtypes = [vp, ip]
     lib.rspl_sp_stage_times.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(ip)]
     lib.rspl_stream_create.argtypes = [C.POINTER(vp)]
+    lib.rspl_stream_create_priority.argtypes = [C.POINTER(vp), ip]
     lib.rspl_stream_destroy.argtypes = [vp]
     lib.rspl_stream_synchronize.argtypes = [vp]
     lib.rspl_event_create.argtypes = [C.POINTER(vp)]
@@ -197,9 +198,12 @@ class Event:
 
 
 class Stream:
-    def __init__(self):
+    def __init__(self, high_priority: bool = False):
         self._s = C.c_void_p()
-        check(load().rspl_stream_create(C.byref(self._s)), "rspl_stream_create")
+        if high_priority:
+            check(load().rspl_stream_create_priority(C.byref(self._s), 1), "rspl_stream_create_priority")
+        else:
+            check(load().rspl_stream_create(C.byref(self._s)), "rspl_stream_create")
 
     @property
     def handle(self) -> int:

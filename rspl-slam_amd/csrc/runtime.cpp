@@ -54,6 +54,13 @@ int rspl_stream_create(void** stream) {
   RSPL_HIP(hipStreamCreateWithFlags((hipStream_t*)stream, hipStreamNonBlocking));
   return RSPL_OK;
 }
+int rspl_stream_create_priority(void** stream, int high) {
+  RSPL_CHECK_ARG(stream, "NULL stream");
+  int lo = 0, hi = 0;
+  RSPL_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+  RSPL_HIP(hipStreamCreateWithPriority((hipStream_t*)stream, hipStreamNonBlocking, high ? hi : lo));
+  return RSPL_OK;
+}
 int rspl_stream_destroy(void* stream) {
   RSPL_HIP(hipStreamDestroy((hipStream_t)stream));
   return RSPL_OK;
