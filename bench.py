@@ -124,6 +124,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-frames", type=int, default=12, help="keyframes in the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp32",
+                    help="SP/SG MFMA precision: fp32 (parity path) or fp16 (the reference's TensorRT kFP16 engines)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -137,8 +139,9 @@ def main():
     capi.check(capi.load().rspl_set_device(local), "rspl_set_device")
 
     sp_w, sg_w = pkg.weights.ensure_blobs(str(ROOT / "weights"))
+    prec = capi.RSPL_PREC_FP16 if args.precision == "fp16" else capi.RSPL_PREC_FP32
     sp = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=K, weights=sp_w, max_height=H, max_width=W,
-                                             max_batch=2, device=local))
+                                             max_batch=2, precision=prec, device=local))
     assert sp.build(), sp.error
     sg = pkg.SuperGlue(pkg.SuperGlueConfig(image_width=W, image_height=H, weights=sg_w, max_keypoints=K,
                                            max_batch=2, device=local))

@@ -19,6 +19,8 @@ struct rspl_sp {
   // weights (device)
   float *lut, *w1a, *b1a, *w1b, *b1b, *w2a, *b2a, *w2b, *b2b, *w3a, *b3a, *w3b, *b3b, *w4a, *b4a, *w4b, *b4b;
   float *wPD, *bPD, *wPb, *bPb, *wDb, *bDb;
+  // RSPL_PREC_FP16: the 3x3 conv weights as fp16 [9][Cout][Cin]
+  _Float16 *hw1b, *hw2a, *hw2b, *hw3a, *hw3b, *hw4a, *hw4b, *hwPD;
   // activations
   float *actA, *actB, *cells, *scores, *nms, *desc;
   unsigned long long* cand;
@@ -40,6 +42,14 @@ struct rspl_sp {
 namespace {
 
 // torch conv weight [co][ci][3][3] -> [ky][kx][ci][co_total] at column offset co_off
+// fp16 layout [9][Cout][Cin] (input channels contiguous: one 16-byte MFMA operand read)
+void relayout3x3_h(const Tensor& t, int cin, int cout, std::vector<_Float16>& dst, int co_total, int co_off) {
+  for (int co = 0; co < cout; co++)
+    for (int ci = 0; ci < cin; ci++)
+      for (int k = 0; k < 9; k++)
+        dst[((size_t)k * co_total + co_off + co) * cin + ci] = (_Float16)t.data[((size_t)co * cin + ci) * 9 + k];
+}
+
 void relayout3x3(const Tensor& t, int cin, int cout, std::vector<float>& dst, int co_total, int co_off) {
   for (int co = 0; co < cout; co++)
     for (int ci = 0; ci < cin; ci++)
@@ -64,6 +74,9 @@ void carve(F& ar, rspl_sp* s, int B, int H, int W, int cap) {
   take(s->w4a, 9 * 128 * 128); take(s->b4a, 128);
   take(s->w4b, 9 * 128 * 128); take(s->b4b, 128);
   take(s->wPD, 9 * 128 * 512); take(s->bPD, 512);
+  take(s->hw1b, 9 * 64 * 64); take(s->hw2a, 9 * 64 * 64); take(s->hw2b, 9 * 64 * 64); take(s->hw3a, 9 * 64 * 128);
+  take(s->hw3b, 9 * 128 * 128); take(s->hw4a, 9 * 128 * 128); take(s->hw4b, 9 * 128 * 128);
+  take(s->hwPD, 9 * 128 * 512);
   take(s->wPb, 256 * 96); take(s->bPb, 96);
   take(s->wDb, 256 * 256); take(s->bDb, 256);
   take(s->actA, B * HW * 16);
@@ -87,7 +100,8 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
   RSPL_CHECK_ARG(cfg && out, "rspl_sp_create: NULL argument");
   RSPL_CHECK_ARG(cfg->max_height > 0 && cfg->max_width > 0 && cfg->max_height % 8 == 0 && cfg->max_width % 8 == 0,
                  "max_height/max_width must be positive multiples of 8");
-  RSPL_CHECK_ARG(cfg->precision == RSPL_PREC_FP32, "only RSPL_PREC_FP32 is implemented");
+  RSPL_CHECK_ARG(cfg->precision == RSPL_PREC_FP32 || cfg->precision == RSPL_PREC_FP16,
+                 "precision must be RSPL_PREC_FP32 or RSPL_PREC_FP16");
   RSPL_CHECK_ARG(cfg->remove_borders >= 0, "remove_borders must be >= 0");
   *out = nullptr;
   std::vector<Tensor> ts;
@@ -113,11 +127,14 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
   }
 
   // ---- weights: relayout once (convert2onnx/superpoint.py:88-105) ----
-  struct C3 { const char* name; int cin, cout; float *w, *b; };
-  const C3 convs[] = {{"conv1b", 64, 64, s->w1b, s->b1b}, {"conv2a", 64, 64, s->w2a, s->b2a},
-                      {"conv2b", 64, 64, s->w2b, s->b2b}, {"conv3a", 64, 128, s->w3a, s->b3a},
-                      {"conv3b", 128, 128, s->w3b, s->b3b}, {"conv4a", 128, 128, s->w4a, s->b4a},
-                      {"conv4b", 128, 128, s->w4b, s->b4b}};
+  struct C3 { const char* name; int cin, cout; float *w, *b; _Float16* hw; };
+  const C3 convs[] = {{"conv1b", 64, 64, s->w1b, s->b1b, s->hw1b}, {"conv2a", 64, 64, s->w2a, s->b2a, s->hw2a},
+                      {"conv2b", 64, 64, s->w2b, s->b2b, s->hw2b}, {"conv3a", 64, 128, s->w3a, s->b3a, s->hw3a},
+                      {"conv3b", 128, 128, s->w3b, s->b3b, s->hw3b}, {"conv4a", 128, 128, s->w4a, s->b4a, s->hw4a},
+                      {"conv4b", 128, 128, s->w4b, s->b4b, s->hw4b}};
+  auto uph = [&](_Float16* dst, const std::vector<_Float16>& src) {
+    return hipMemcpy(dst, src.data(), src.size() * sizeof(_Float16), hipMemcpyHostToDevice) == hipSuccess;
+  };
   auto up = [&](float* dst, const std::vector<float>& src) {
     return hipMemcpy(dst, src.data(), src.size() * sizeof(float), hipMemcpyHostToDevice) == hipSuccess;
   };
@@ -128,7 +145,9 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
     if (!w || !b) { rspl_sp_destroy(s); return RSPL_E_WEIGHTS; }
     std::vector<float> r((size_t)9 * c.cin * c.cout);
     relayout3x3(*w, c.cin, c.cout, r, c.cout, 0);
-    ok &= up(c.w, r) && up(c.b, b->data);
+    std::vector<_Float16> rh((size_t)9 * c.cin * c.cout);
+    relayout3x3_h(*w, c.cin, c.cout, rh, c.cout, 0);
+    ok &= up(c.w, r) && up(c.b, b->data) && uph(c.hw, rh);
   }
   const Tensor *w1a = find(ts, "conv1a.weight", 64 * 9), *b1a = find(ts, "conv1a.bias", 64);
   const Tensor *wPa = find(ts, "convPa.weight", 256 * 128 * 9), *bPa = find(ts, "convPa.bias", 256);
@@ -144,6 +163,10 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
     std::vector<float> r((size_t)9 * 128 * 512), b(512);
     relayout3x3(*wPa, 128, 256, r, 512, 0);
     relayout3x3(*wDa, 128, 256, r, 512, 256);
+    std::vector<_Float16> rh((size_t)9 * 128 * 512);
+    relayout3x3_h(*wPa, 128, 256, rh, 512, 0);
+    relayout3x3_h(*wDa, 128, 256, rh, 512, 256);
+    ok &= uph(s->hwPD, rh);
     for (int i = 0; i < 256; i++) { b[i] = bPa->data[i]; b[256 + i] = bDa->data[i]; }
     ok &= up(s->wPD, r) && up(s->bPD, b);
   }
@@ -205,25 +228,50 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
   c.w1a = s->w1a;
   c.b1a = s->b1a;
   // encoder (superpoint.py:117-127)
-  s->timer.mark(0, st);
-  c.H = H; c.W = W; c.cout = 64; c.w = s->w1b; c.bias = s->b1b; c.out = s->actA;
-  RSPL_HIP(conv3x3(c, 64, true, true, B, st));                               // conv1a+1b+pool
-  s->timer.mark(1, st);
-  c.H = H2; c.W = W2; c.cout = 64; c.in = s->actA; c.w = s->w2a; c.bias = s->b2a; c.out = s->actB;
-  RSPL_HIP(conv3x3(c, 64, false, false, B, st));                             // conv2a
-  c.in = s->actB; c.w = s->w2b; c.bias = s->b2b; c.out = s->actA;
-  RSPL_HIP(conv3x3(c, 64, true, false, B, st));                              // conv2b+pool
-  c.H = H4; c.W = W4; c.cout = 128; c.in = s->actA; c.w = s->w3a; c.bias = s->b3a; c.out = s->actB;
-  RSPL_HIP(conv3x3(c, 64, false, false, B, st));                             // conv3a
-  c.in = s->actB; c.w = s->w3b; c.bias = s->b3b; c.out = s->actA;
-  RSPL_HIP(conv3x3(c, 128, true, false, B, st));                             // conv3b+pool
-  c.H = H8; c.W = W8; c.in = s->actA; c.w = s->w4a; c.bias = s->b4a; c.out = s->actB;
-  RSPL_HIP(conv3x3(c, 128, false, false, B, st));                            // conv4a
-  c.in = s->actB; c.w = s->w4b; c.bias = s->b4b; c.out = s->actA;
-  RSPL_HIP(conv3x3(c, 128, false, false, B, st));                            // conv4b
-  s->timer.mark(2, st);
-  c.cout = 512; c.in = s->actA; c.w = s->wPD; c.bias = s->bPD; c.out = s->cells;
-  RSPL_HIP(conv3x3(c, 128, false, false, B, st));                            // convPa | convDa
+  if (s->cfg.precision == RSPL_PREC_FP16) {  // the reference's TensorRT kFP16 engine (super_point.cpp:98)
+    _Float16* hA = reinterpret_cast<_Float16*>(s->actA);
+    _Float16* hB = reinterpret_cast<_Float16*>(s->actB);
+    s->timer.mark(0, st);
+    c.H = H; c.W = W; c.cout = 64; c.hw = s->hw1b; c.bias = s->b1b; c.hout = hA;
+    RSPL_HIP(conv3x3_h(c, 64, true, true, false, B, st));                     // conv1a+1b+pool
+    s->timer.mark(1, st);
+    c.H = H2; c.W = W2; c.cout = 64; c.hin = hA; c.hw = s->hw2a; c.bias = s->b2a; c.hout = hB;
+    RSPL_HIP(conv3x3_h(c, 64, false, false, false, B, st));                   // conv2a
+    c.hin = hB; c.hw = s->hw2b; c.bias = s->b2b; c.hout = hA;
+    RSPL_HIP(conv3x3_h(c, 64, true, false, false, B, st));                    // conv2b+pool
+    c.H = H4; c.W = W4; c.cout = 128; c.hin = hA; c.hw = s->hw3a; c.bias = s->b3a; c.hout = hB;
+    RSPL_HIP(conv3x3_h(c, 64, false, false, false, B, st));                   // conv3a
+    c.hin = hB; c.hw = s->hw3b; c.bias = s->b3b; c.hout = hA;
+    RSPL_HIP(conv3x3_h(c, 128, true, false, false, B, st));                   // conv3b+pool
+    c.H = H8; c.W = W8; c.hin = hA; c.hw = s->hw4a; c.bias = s->b4a; c.hout = hB;
+    RSPL_HIP(conv3x3_h(c, 128, false, false, false, B, st));                  // conv4a
+    c.hin = hB; c.hw = s->hw4b; c.bias = s->b4b; c.hout = hA;
+    RSPL_HIP(conv3x3_h(c, 128, false, false, false, B, st));                  // conv4b
+    s->timer.mark(2, st);
+    c.cout = 512; c.hin = hA; c.hw = s->hwPD; c.bias = s->bPD; c.out = s->cells;
+    RSPL_HIP(conv3x3_h(c, 128, false, false, true, B, st));                   // convPa | convDa (fp32 out)
+  } else {
+    // encoder (superpoint.py:117-127)
+    s->timer.mark(0, st);
+    c.H = H; c.W = W; c.cout = 64; c.w = s->w1b; c.bias = s->b1b; c.out = s->actA;
+    RSPL_HIP(conv3x3(c, 64, true, true, B, st));                               // conv1a+1b+pool
+    s->timer.mark(1, st);
+    c.H = H2; c.W = W2; c.cout = 64; c.in = s->actA; c.w = s->w2a; c.bias = s->b2a; c.out = s->actB;
+    RSPL_HIP(conv3x3(c, 64, false, false, B, st));                             // conv2a
+    c.in = s->actB; c.w = s->w2b; c.bias = s->b2b; c.out = s->actA;
+    RSPL_HIP(conv3x3(c, 64, true, false, B, st));                              // conv2b+pool
+    c.H = H4; c.W = W4; c.cout = 128; c.in = s->actA; c.w = s->w3a; c.bias = s->b3a; c.out = s->actB;
+    RSPL_HIP(conv3x3(c, 64, false, false, B, st));                             // conv3a
+    c.in = s->actB; c.w = s->w3b; c.bias = s->b3b; c.out = s->actA;
+    RSPL_HIP(conv3x3(c, 128, true, false, B, st));                             // conv3b+pool
+    c.H = H8; c.W = W8; c.in = s->actA; c.w = s->w4a; c.bias = s->b4a; c.out = s->actB;
+    RSPL_HIP(conv3x3(c, 128, false, false, B, st));                            // conv4a
+    c.in = s->actB; c.w = s->w4b; c.bias = s->b4b; c.out = s->actA;
+    RSPL_HIP(conv3x3(c, 128, false, false, B, st));                            // conv4b
+    s->timer.mark(2, st);
+    c.cout = 512; c.in = s->actA; c.w = s->wPD; c.bias = s->bPD; c.out = s->cells;
+    RSPL_HIP(conv3x3(c, 128, false, false, B, st));                            // convPa | convDa
+  }
   s->timer.mark(3, st);
   // heads (superpoint.py:130-135, 159-161)
   HeadArgs h{};

@@ -176,6 +176,160 @@ __global__ __launch_bounds__(256) void conv3x3_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// fp16 variant of the 3x3 conv (RSPL_PREC_FP16 = the reference's TensorRT kFP16
+// engines): same tiling, v_mfma_f32_32x32x16_f16 (lane (r, h) holds A[r][8h..8h+7] and
+// B[8h..8h+7][r]: one 16-byte LDS read each), 32 input channels per stage, LDS rows of
+// 40 halves (80 B: conflict-free ds_read_b128), fp32 accumulation, bias/ReLU/pool epilogue.
+// ---------------------------------------------------------------------------
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ floatx16 mfma16(half8 a, half8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+constexpr int HCK = 32;       // input channels per stage
+constexpr int HCS = HCK + 8;  // LDS row stride in halves
+
+template <int CIN, int TH, bool POOL, bool FUSE1A, bool OUT_F32>
+__global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
+  static_assert(CIN % HCK == 0, "Cin must be a multiple of 32");
+  constexpr int HX = TW + 2, HY = TH + 2;
+  constexpr int MT = TH / 8;
+  __shared__ __attribute__((aligned(16))) _Float16 halo[HY * HX * HCS];
+  __shared__ __attribute__((aligned(16))) _Float16 wts[9 * 64 * HCS];
+  __shared__ float patch[FUSE1A ? (TH + 4) * (TW + 4) : 1];
+  __shared__ float w1a[FUSE1A ? 64 * 10 : 1];
+
+  const int H = a.H, W = a.W, COUT = a.cout;
+  const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
+  const int per_img = tiles_x * tiles_y;
+  const int bi = blockIdx.x / per_img;
+  const int t = blockIdx.x % per_img;
+  const int y0 = (t / tiles_x) * TH, x0 = (t % tiles_x) * TW;
+  const int co0 = blockIdx.y * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ml = lane & 31, kl = lane >> 5;
+
+  if constexpr (FUSE1A) {
+    const uint8_t* img = a.img + (size_t)bi * a.img_pitch;
+    for (int i = tid; i < (TH + 4) * (TW + 4); i += 256) {
+      const int py = i / (TW + 4), px = i % (TW + 4);
+      const int y = y0 - 2 + py, x = x0 - 2 + px;
+      patch[i] = (y >= 0 && y < H && x >= 0 && x < W) ? a.lut[img[(size_t)y * a.img_stride + x]] : 0.f;
+    }
+    for (int i = tid; i < 64 * 10; i += 256) w1a[i] = (i % 10 < 9) ? a.w1a[(i / 10) * 9 + i % 10] : a.b1a[i / 10];
+  }
+
+  floatx16 acc[MT][2];
+#pragma unroll
+  for (int m = 0; m < MT; m++)
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc[m][n][r] = 0.f;
+
+  for (int c0 = 0; c0 < CIN; c0 += HCK) {
+    __syncthreads();
+    if constexpr (FUSE1A) {  // conv1a (fp32, as the module's first layer) -> ReLU -> fp16
+      for (int i = tid; i < HY * HX * HCK; i += 256) {
+        const int c = i % HCK, pix = i / HCK;
+        const int hy = pix / HX, hx = pix % HX;
+        const int y = y0 - 1 + hy, x = x0 - 1 + hx;
+        float v = 0.f;
+        if (y >= 0 && y < H && x >= 0 && x < W) {
+          const float* wc = &w1a[(c0 + c) * 10];
+          float s = wc[9];
+#pragma unroll
+          for (int ky = 0; ky < 3; ky++)
+#pragma unroll
+            for (int kx = 0; kx < 3; kx++) s += wc[ky * 3 + kx] * patch[(hy + ky) * (TW + 4) + hx + kx];
+          v = s > 0.f ? s : 0.f;
+        }
+        halo[pix * HCS + c] = (_Float16)v;
+      }
+    } else {
+      const _Float16* in = a.hin + (size_t)bi * H * W * CIN;
+      for (int i = tid; i < HY * HX * (HCK / 8); i += 256) {
+        const int q = i % (HCK / 8), pix = i / (HCK / 8);
+        const int hy = pix / HX, hx = pix % HX;
+        const int y = y0 - 1 + hy, x = x0 - 1 + hx;
+        half8 v = {};
+        if (y >= 0 && y < H && x >= 0 && x < W)
+          v = *reinterpret_cast<const half8*>(in + ((size_t)y * W + x) * CIN + c0 + 8 * q);
+        *reinterpret_cast<half8*>(&halo[pix * HCS + 8 * q]) = v;
+      }
+    }
+    for (int i = tid; i < 9 * 64 * (HCK / 8); i += 256) {  // weights [9][64 co][32 ci]
+      const int q = i % (HCK / 8), r = i / (HCK / 8);     // r = kk*64 + co
+      const int kk = r / 64, co = r % 64;
+      *reinterpret_cast<half8*>(&wts[r * HCS + 8 * q]) =
+          *reinterpret_cast<const half8*>(a.hw + ((size_t)kk * COUT + co0 + co) * CIN + c0 + 8 * q);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < 9; kk++) {
+      const int ky = kk / 3, kx = kk % 3;
+#pragma unroll
+      for (int ks = 0; ks < HCK; ks += 16) {
+        half8 av[MT], bv[2];
+#pragma unroll
+        for (int m = 0; m < MT; m++) {
+          const int ly = wv * (TH / 4) + 2 * m + (ml >> 4);
+          av[m] = *reinterpret_cast<const half8*>(&halo[((ly + ky) * HX + (ml & 15) + kx) * HCS + ks + 8 * kl]);
+        }
+#pragma unroll
+        for (int n = 0; n < 2; n++)
+          bv[n] = *reinterpret_cast<const half8*>(&wts[(kk * 64 + n * 32 + ml) * HCS + ks + 8 * kl]);
+#pragma unroll
+        for (int m = 0; m < MT; m++)
+#pragma unroll
+          for (int n = 0; n < 2; n++) acc[m][n] = mfma16(av[m], bv[n], acc[m][n]);
+      }
+    }
+  }
+
+#pragma unroll
+  for (int n = 0; n < 2; n++) {
+    const int co = co0 + n * 32 + ml;
+    const float bias = a.bias[co];
+#pragma unroll
+    for (int m = 0; m < MT; m++) {
+      const int ly = wv * (TH / 4) + 2 * m;
+      if constexpr (POOL) {
+        const int H2 = H / 2, W2 = W / 2;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+          const int r0 = (g & 1) * 2 + (g >> 1) * 4;
+          const int pc = (r0 & 3) + 8 * ((r0 >> 2) & 1) + 4 * kl;
+          float v = fmaxf(fmaxf(acc[m][n][r0], acc[m][n][r0 + 1]), fmaxf(acc[m][n][r0 + 8], acc[m][n][r0 + 9]));
+          v += bias;
+          v = v > 0.f ? v : 0.f;
+          const int py = (y0 + ly) >> 1, px = (x0 + pc) >> 1;
+          if (py < H2 && px < W2) {
+            const size_t o = (size_t)bi * H2 * W2 * COUT + ((size_t)py * W2 + px) * COUT + co;
+            if constexpr (OUT_F32) a.out[o] = v;
+            else a.hout[o] = (_Float16)v;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int mm = (r & 3) + 8 * (r >> 2) + 4 * kl;
+          const int y = y0 + ly + (mm >> 4), x = x0 + (mm & 15);
+          float v = acc[m][n][r] + bias;
+          v = v > 0.f ? v : 0.f;
+          if (y < H && x < W) {
+            const size_t o = (size_t)bi * H * W * COUT + ((size_t)y * W + x) * COUT + co;
+            if constexpr (OUT_F32) a.out[o] = v;
+            else a.hout[o] = (_Float16)v;
+          }
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // 1x1 heads on the H/8 x W/8 cell grid.  in = [P][512] (convPa | convDa, ReLU'd).
 //   MODE 0: convPb 256->65, softmax over 65, drop dustbin, depth-to-space ->
 //           scores [H][W]  (superpoint.py:131-135)
@@ -521,6 +675,27 @@ hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hi
   if (cin == 64 && !pool) return small ? launch_conv<64, 8, false, false>(a, B, s) : launch_conv<64, 16, false, false>(a, B, s);
   if (cin == 128 && pool) return launch_conv<128, 16, true, false>(a, B, s);
   if (cin == 128 && !pool) return small ? launch_conv<128, 8, false, false>(a, B, s) : launch_conv<128, 16, false, false>(a, B, s);
+  return hipErrorInvalidValue;
+}
+
+template <int CIN, int TH, bool POOL, bool FUSE1A, bool OUT_F32>
+static hipError_t launch_conv_h(const ConvArgs& a, int B, hipStream_t s) {
+  const int tiles = ((a.W + TW - 1) / TW) * ((a.H + TH - 1) / TH);
+  dim3 grid(B * tiles, a.cout / 64);
+  hipLaunchKernelGGL((conv3x3_h_kernel<CIN, TH, POOL, FUSE1A, OUT_F32>), grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool out_f32, int B, hipStream_t s) {
+  const bool small = (a.H * a.W) <= 128 * 192;
+  if (fuse1a) return launch_conv_h<64, 16, true, true, false>(a, B, s);
+  if (out_f32) return launch_conv_h<128, 8, false, false, true>(a, B, s);
+  if (cin == 64 && pool) return launch_conv_h<64, 16, true, false, false>(a, B, s);
+  if (cin == 64 && !pool) return small ? launch_conv_h<64, 8, false, false, false>(a, B, s)
+                                       : launch_conv_h<64, 16, false, false, false>(a, B, s);
+  if (cin == 128 && pool) return launch_conv_h<128, 16, true, false, false>(a, B, s);
+  if (cin == 128 && !pool) return small ? launch_conv_h<128, 8, false, false, false>(a, B, s)
+                                        : launch_conv_h<128, 16, false, false, false>(a, B, s);
   return hipErrorInvalidValue;
 }
 

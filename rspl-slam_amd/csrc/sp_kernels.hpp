@@ -19,6 +19,11 @@ struct ConvArgs {
   const float* lut;      // [256] (float)(u / 255.0)
   const float* w1a;      // [64][9]
   const float* b1a;      // [64]
+  // RSPL_PREC_FP16 path (the reference's TensorRT kFP16 engines, super_point.cpp:98):
+  // fp16 NHWC activations and weights, fp32 accumulation and epilogue
+  const _Float16* hin;   // NHWC [B][H][W][Cin]
+  const _Float16* hw;    // [9][Cout][Cin]
+  _Float16* hout;        // NHWC [B][H(/2)][W(/2)][Cout] (or `out` in fp32 for the heads)
 };
 
 struct HeadArgs {
@@ -65,6 +70,8 @@ struct SampleArgs {
 };
 
 hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hipStream_t s);
+// fp16 MFMA (v_mfma_f32_32x32x16_f16) variant; out_f32 writes `out` (fp32) instead of `hout`
+hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool out_f32, int B, hipStream_t s);
 hipError_t heads(const HeadArgs& a, int mode, hipStream_t s);
 hipError_t nms(const NmsArgs& a, int B, hipStream_t s);
 hipError_t topk(const TopkArgs& a, int B, hipStream_t s);

@@ -102,3 +102,27 @@ def test_sp_batched_device_path(pkg, weight_blobs):
         s, d = oracle.sp_forward(weight_blobs[0], post.image_to_input(img))
         G = post.sp_postprocess(s, d, 0.004, 4, k)
         compare_features(F[b, :cnt[b]].T, G)
+
+
+def test_sp_fp16_vs_reference(pkg, golden, weight_blobs):
+    """RSPL_PREC_FP16 (the reference's TensorRT kFP16 engine, src/super_point.cpp:98) vs the fp32
+    reference outputs, at SURVEY §8c's fp16 acceptance bar: keypoint-set overlap >= 99 % and
+    descriptor cosine >= 0.999 on the shared keypoints; scores within 2 %."""
+    g = golden("sp_euroc")
+    sp = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=400, weights=weight_blobs[0], max_height=480,
+                                             max_width=752, max_batch=1, precision=pkg.capi.RSPL_PREC_FP16))
+    assert sp.build(), sp.error
+    ok, F = sp.infer(g["image"])
+    assert ok, sp.error
+    G = np.concatenate([g["feat_head"], g["feat_desc"].astype(np.float64)])
+    kf = {(int(x), int(y)): i for i, (x, y) in enumerate(zip(F[1], F[2]))}
+    kg = {(int(x), int(y)): i for i, (x, y) in enumerate(zip(G[1], G[2]))}
+    shared = sorted(set(kf) & set(kg))
+    overlap = len(shared) / max(1, len(kg))
+    fi = np.array([kf[k] for k in shared])
+    gi = np.array([kg[k] for k in shared])
+    cos = (F[3:, fi] * G[3:, gi]).sum(0) / (np.linalg.norm(F[3:, fi], axis=0) * np.linalg.norm(G[3:, gi], axis=0))
+    print(f"fp16 SP: keypoint overlap {overlap:.4f}, min desc cosine {cos.min():.6f}")
+    assert overlap >= 0.99
+    assert cos.min() >= 0.999
+    np.testing.assert_allclose(F[0, fi], G[0, gi], rtol=2e-2, atol=1e-4)
