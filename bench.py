@@ -144,7 +144,7 @@ def main():
                                              max_batch=2, precision=prec, device=local))
     assert sp.build(), sp.error
     sg = pkg.SuperGlue(pkg.SuperGlueConfig(image_width=W, image_height=H, weights=sg_w, max_keypoints=K,
-                                           max_batch=2, device=local))
+                                           max_batch=2, precision=prec, device=local))
     assert sg.build(), sg.error
     ba = pkg.LocalBA(max_poses=16, max_points=6000, max_lines=200, max_edges=40000, device=local)
 

@@ -29,6 +29,9 @@ struct rspl_sg {
   float* kb[5];
   float *wqkv, *bqkv, *wm, *bm, *w1, *b1, *w2, *b2;  // [18] stacked
   float *wf, *bf, *bin;
+  // RSPL_PREC_FP16: transposed fp16 copies [N][K] of every projection / MLP weight
+  _Float16* hkw[5];
+  _Float16 *hwqkv, *hwm, *hw1, *hw2, *hwf;
   // activations
   float *kin, *h1, *h2, *X, *QKV, *O, *MSG, *HID, *cpl, *Z, *val0;
   unsigned long long* part;
@@ -65,6 +68,9 @@ void carve(F& ar, rspl_sg* s) {
   take(s->w1, (size_t)kLayers * 512 * 512); take(s->b1, (size_t)kLayers * 512);
   take(s->w2, (size_t)kLayers * 512 * 256); take(s->b2, (size_t)kLayers * 256);
   take(s->wf, 256 * 256); take(s->bf, 256); take(s->bin, 4);
+  for (int i = 0; i < 5; i++) take(s->hkw[i], (size_t)(i == 0 ? kKencIn : kKencCh[i]) * kKencCh[i + 1]);
+  take(s->hwqkv, (size_t)kLayers * 256 * 768); take(s->hwm, (size_t)kLayers * 256 * 256);
+  take(s->hw1, (size_t)kLayers * 512 * 512); take(s->hw2, (size_t)kLayers * 512 * 256); take(s->hwf, 256 * 256);
   take(s->kin, T * kKencIn); take(s->h1, T * 256); take(s->h2, T * 256);
   take(s->X, T * 256); take(s->QKV, T * 768); take(s->O, T * 256); take(s->MSG, T * 256); take(s->HID, T * 512);
   take(s->cpl, B * ld * ld); take(s->Z, B * ld * ld); take(s->part, B * 2 * s->G * ld);
@@ -180,8 +186,10 @@ int upload_weights(rspl_sg* s, const std::vector<Tensor>& ts) {
 }
 
 sg::GemmArgs G_(const float* A, int lda, const float* B, int ldb, const float* bias, float* C, int ldc, int M, int N,
-                int K, int epi) {
+                int K, int epi, const _Float16* hB = nullptr) {
   sg::GemmArgs g{};
+  g.hB = hB;
+  g.ldbh = K;
   g.A = A; g.lda = lda; g.ksplit = K; g.B = B; g.ldb = ldb; g.bias = bias; g.C = C; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K; g.alpha = 1.f; g.epi = epi;
   return g;
@@ -192,7 +200,8 @@ sg::GemmArgs G_(const float* A, int lda, const float* B, int ldb, const float* b
 extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_path, rspl_sg** out) {
   RSPL_CHECK_ARG(cfg && out, "rspl_sg_create: NULL argument");
   RSPL_CHECK_ARG(cfg->max_keypoints > 0 && cfg->max_keypoints <= 4096, "max_keypoints must be in [1, 4096]");
-  RSPL_CHECK_ARG(cfg->precision == RSPL_PREC_FP32, "only RSPL_PREC_FP32 is implemented");
+  RSPL_CHECK_ARG(cfg->precision == RSPL_PREC_FP32 || cfg->precision == RSPL_PREC_FP16,
+                 "precision must be RSPL_PREC_FP32 or RSPL_PREC_FP16");
   RSPL_CHECK_ARG(cfg->image_width > 0 && cfg->image_height > 0, "image size must be positive");
   *out = nullptr;
   std::vector<Tensor> ts;
@@ -235,6 +244,27 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
     return RSPL_E_DEVICE;
   }
   if ((rc = upload_weights(s, ts))) { rspl_sg_destroy(s); return rc; }
+  {  // fp16 transposed copies for RSPL_PREC_FP16 (made on the device from the fp32 layout)
+    bool okh = true;
+    for (int i = 0; i < 5; i++)
+      okh &= sg::to_half_t(s->kw[i], i == 0 ? kKencIn : kKencCh[i], kKencCh[i + 1], s->hkw[i], s->stream) == hipSuccess;
+    for (int l = 0; l < kLayers; l++) {
+      okh &= sg::to_half_t(s->wqkv + (size_t)l * 256 * 768, 256, 768, s->hwqkv + (size_t)l * 256 * 768, s->stream) ==
+             hipSuccess;
+      okh &= sg::to_half_t(s->wm + (size_t)l * 65536, 256, 256, s->hwm + (size_t)l * 65536, s->stream) == hipSuccess;
+      okh &= sg::to_half_t(s->w1 + (size_t)l * 512 * 512, 512, 512, s->hw1 + (size_t)l * 512 * 512, s->stream) ==
+             hipSuccess;
+      okh &= sg::to_half_t(s->w2 + (size_t)l * 512 * 256, 512, 256, s->hw2 + (size_t)l * 512 * 256, s->stream) ==
+             hipSuccess;
+    }
+    okh &= sg::to_half_t(s->wf, 256, 256, s->hwf, s->stream) == hipSuccess;
+    okh &= hipStreamSynchronize(s->stream) == hipSuccess;
+    if (!okh) {
+      set_error("fp16 weight conversion failed");
+      rspl_sg_destroy(s);
+      return RSPL_E_DEVICE;
+    }
+  }
   *out = s;
   return RSPL_OK;
 }
@@ -269,13 +299,15 @@ extern "C" int rspl_sg_infer_device(rspl_sg* s, int B, const double* d_feat0, co
   pa.nmax = nm; pa.kin = s->kin; pa.X = s->X; pa.B = B;
   RSPL_HIP(sg::prep(pa, st));
   // KeypointEncoder: desc += kenc([x, y, score]) (superglue.py:288-289)
+  const bool h16 = s->cfg.precision == RSPL_PREC_FP16;  // the reference's kFP16 engine (super_glue.cpp:132)
   const float* in = s->kin;
   int cin = kKencIn;
   float* bufs[2] = {s->h1, s->h2};
   for (int i = 0; i < 5; i++) {
     const int co = kKencCh[i + 1];
     float* outp = i == 4 ? s->X : bufs[i & 1];
-    RSPL_HIP(sg::gemm(G_(in, cin, s->kw[i], co, s->kb[i], outp, co, T, co, cin, i == 4 ? 2 : 1), 1, st));
+    RSPL_HIP(sg::gemm(G_(in, cin, s->kw[i], co, s->kb[i], outp, co, T, co, cin, i == 4 ? 2 : 1, h16 ? s->hkw[i] : nullptr),
+                      1, st));
     in = outp;
     cin = co;
   }
@@ -283,24 +315,24 @@ extern "C" int rspl_sg_infer_device(rspl_sg* s, int B, const double* d_feat0, co
   // AttentionalGNN (superglue.py:165-173): ['self', 'cross'] * 9; both images read pre-layer descs
   for (int l = 0; l < kLayers; l++) {
     RSPL_HIP(sg::gemm(G_(s->X, 256, s->wqkv + (size_t)l * 256 * 768, 768, s->bqkv + (size_t)l * 768, s->QKV, 768, T,
-                         768, 256, 0), 1, st));
+                         768, 256, 0, h16 ? s->hwqkv + (size_t)l * 256 * 768 : nullptr), 1, st));
     sg::AttnArgs at{};
     at.qkv = s->QKV; at.O = s->O; at.n0 = d_n0; at.n1 = d_n1; at.nmax = nm; at.cross = l & 1;
     RSPL_HIP(sg::attention(at, B, st));
     RSPL_HIP(sg::gemm(G_(s->O, 256, s->wm + (size_t)l * 65536, 256, s->bm + (size_t)l * 256, s->MSG, 256, T, 256, 256,
-                         0), 1, st));
+                         0, h16 ? s->hwm + (size_t)l * 65536 : nullptr), 1, st));
     sg::GemmArgs g1 = G_(s->X, 256, s->w1 + (size_t)l * 512 * 512, 512, s->b1 + (size_t)l * 512, s->HID, 512, T, 512,
-                         512, 1);
+                         512, 1, h16 ? s->hw1 + (size_t)l * 512 * 512 : nullptr);
     g1.A2 = s->MSG;  // torch.cat([x, message], dim=1)
     g1.ksplit = 256;
     RSPL_HIP(sg::gemm(g1, 1, st));
     RSPL_HIP(sg::gemm(G_(s->HID, 512, s->w2 + (size_t)l * 512 * 256, 256, s->b2 + (size_t)l * 256, s->X, 256, T, 256,
-                         512, 2), 1, st));
+                         512, 2, h16 ? s->hw2 + (size_t)l * 512 * 256 : nullptr), 1, st));
   }
   s->timer.mark(2, st);
   // final_proj + scores / descriptor_dim**.5 (superglue.py:295-300)
   float* MD = s->MSG;
-  RSPL_HIP(sg::gemm(G_(s->X, 256, s->wf, 256, s->bf, MD, 256, T, 256, 256, 0), 1, st));
+  RSPL_HIP(sg::gemm(G_(s->X, 256, s->wf, 256, s->bf, MD, 256, T, 256, 256, 0, h16 ? s->hwf : nullptr), 1, st));
   {
     sg::GemmArgs g = G_(MD, 256, MD + (size_t)nm * 256, 256, nullptr, s->cpl, s->ld, nm, nm, 256, 0);
     g.b_nt = 1;

@@ -210,6 +210,97 @@ __global__ __launch_bounds__(256) void gemm_sk_kernel(GemmArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// RSPL_PREC_FP16 GEMM (the reference's TensorRT kFP16 SuperGlue engine,
+// super_glue.cpp:132): v_mfma_f32_32x32x16_f16, fp32 accumulation and epilogue.
+// Lane (r, h) operand fragments come straight from global memory: A = 8 consecutive
+// fp32 activations of row m0+r converted to fp16, B = 8 consecutive fp16 weights of
+// row n0+r of the transposed weight.  Same 32x32 tile / 4-way K split / fixed-order
+// LDS reduction as gemm_sk_kernel; four 16-wide K steps in flight per wave.
+// ---------------------------------------------------------------------------
+typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ floatx16 mfma16(half8 a, half8 b, floatx16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256) void gemm_h_kernel(GemmArgs a) {
+  __shared__ float red[3 * 16 * 64];
+  const int z = blockIdx.z;
+  int M = a.M, N = a.N;
+  if (a.mcount) M = a.mcount[(size_t)z * a.count_stride];
+  if (a.ncount) N = a.ncount[(size_t)z * a.count_stride];
+  const int m0 = blockIdx.y * 32, n0 = blockIdx.x * 32;
+  if (m0 >= M || n0 >= N) return;
+  const float* A = a.A + z * a.sA;
+  const float* A2 = a.A2 ? a.A2 + z * a.sA : nullptr;
+  float* C = a.C + z * a.sC;
+  const int K = a.K, nsteps = K / 16;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, ml = lane & 31, kl = lane >> 5;
+  const int m = m0 + ml, n = n0 + ml;
+  const bool mok = m < M, nok = n < N;
+  const _Float16* Brow = a.hB + (size_t)(nok ? n : 0) * a.ldbh + 8 * kl;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; r++) acc[r] = 0.f;
+  auto afrag = [&](int k0) {
+    const int k = k0 + 8 * kl;
+    half8 h = {};
+    if (mok) {
+      const float* src = (A2 && k >= a.ksplit) ? A2 + (size_t)m * a.lda + (k - a.ksplit) : A + (size_t)m * a.lda + k;
+      const float4 u = *reinterpret_cast<const float4*>(src), v = *reinterpret_cast<const float4*>(src + 4);
+      h[0] = (_Float16)u.x; h[1] = (_Float16)u.y; h[2] = (_Float16)u.z; h[3] = (_Float16)u.w;
+      h[4] = (_Float16)v.x; h[5] = (_Float16)v.y; h[6] = (_Float16)v.z; h[7] = (_Float16)v.w;
+    }
+    return h;
+  };
+  auto bfrag = [&](int k0) {
+    half8 h = {};
+    if (nok) h = *reinterpret_cast<const half8*>(Brow + k0);
+    return h;
+  };
+  int step = wv;
+  for (; step + 12 < nsteps; step += 16) {  // 4 steps per wave in flight
+    half8 av[4], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      av[u] = afrag((step + 4 * u) * 16);
+      bv[u] = bfrag((step + 4 * u) * 16);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) acc = mfma16(av[u], bv[u], acc);
+  }
+  for (; step < nsteps; step += 4) acc = mfma16(afrag(step * 16), bfrag(step * 16), acc);
+  if (wv > 0) {
+#pragma unroll
+    for (int r = 0; r < 16; r++) red[((wv - 1) * 16 + r) * 64 + lane] = acc[r];
+  }
+  __syncthreads();
+  if (wv != 0 || !nok) return;
+  const float b = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const float s = ((acc[r] + red[(0 * 16 + r) * 64 + lane]) + red[(1 * 16 + r) * 64 + lane]) +
+                    red[(2 * 16 + r) * 64 + lane];
+    const int mm = m0 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+    if (mm < M) {
+      float v = s * a.alpha + b;
+      float* dst = C + (size_t)mm * a.ldc + n;
+      if constexpr (EPI == 1) v = v > 0.f ? v : 0.f;
+      if constexpr (EPI == 2) v = *dst + v;
+      *dst = v;
+    }
+  }
+}
+
+__global__ void to_half_t_kernel(const float* W, int K, int N, _Float16* Wt) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= K * N) return;
+  const int n = i / K, k = i - n * K;
+  Wt[i] = (_Float16)W[(size_t)k * N + n];
+}
+
+// ---------------------------------------------------------------------------
 // process_input + NormalizeKeypoints: one wave per token.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
@@ -720,7 +811,19 @@ __global__ __launch_bounds__(256) void finalize_kernel(DecodeArgs a) {
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+hipError_t to_half_t(const float* W, int K, int N, _Float16* Wt, hipStream_t s) {
+  hipLaunchKernelGGL(to_half_t_kernel, dim3((K * N + 255) / 256), dim3(256), 0, s, W, K, N, Wt);
+  return hipGetLastError();
+}
+
 hipError_t gemm(const GemmArgs& a, int batch, hipStream_t s) {
+  if (a.hB && !a.b_nt) {
+    dim3 grid((a.N + 31) / 32, (a.M + 31) / 32, batch);
+    if (a.epi == 1) hipLaunchKernelGGL(gemm_h_kernel<1>, grid, dim3(256), 0, s, a);
+    else if (a.epi == 2) hipLaunchKernelGGL(gemm_h_kernel<2>, grid, dim3(256), 0, s, a);
+    else hipLaunchKernelGGL(gemm_h_kernel<0>, grid, dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   if (a.b_nt) {
     dim3 grid((a.N + 63) / 64, (a.M + 63) / 64, batch);
     hipLaunchKernelGGL((gemm_kernel<0, true>), grid, dim3(256), 0, s, a);

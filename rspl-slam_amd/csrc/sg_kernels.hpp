@@ -26,6 +26,8 @@ struct GemmArgs {
   long long sA, sB, sC;
   const int* mcount;
   const int* ncount;
+  const _Float16* hB;  // RSPL_PREC_FP16: weights as fp16 [N][K] (k contiguous), row stride ldbh
+  int ldbh;
   int count_stride;  // ints between consecutive batches in mcount/ncount
 };
 
@@ -88,6 +90,8 @@ struct DecodeArgs {
 };
 
 hipError_t gemm(const GemmArgs& a, int batch, hipStream_t s);
+// Wt[n][k] = (fp16) W[k][n] for a [K][N] fp32 weight (one-time, at create)
+hipError_t to_half_t(const float* W, int K, int N, _Float16* Wt, hipStream_t s);
 hipError_t prep(const PrepArgs& a, hipStream_t s);
 hipError_t attention(const AttnArgs& a, int B, hipStream_t s);
 hipError_t bins(const BinsArgs& a, int B, hipStream_t s);

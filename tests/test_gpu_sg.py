@@ -96,3 +96,25 @@ def test_sg_batched_device_path(pkg, weight_blobs):
         d = post.decode(Zo)
         np.testing.assert_array_equal(I0[p, :n0[p]], d[0])
         np.testing.assert_array_equal(I1[p, :n1[p]], d[1])
+
+
+def test_sg_fp16_vs_reference(pkg, golden, weight_blobs):
+    """RSPL_PREC_FP16 (the reference's TensorRT kFP16 engine, src/super_glue.cpp:132) vs the fp32
+    reference at SURVEY §8c's fp16 bar: match-index agreement >= 99 %."""
+    g = golden("sg_400")
+    F0, F1 = g["F0"].astype(np.float64), g["F1"].astype(np.float64)
+    G0, G1 = post.normalize_keypoints(F0, 752, 480), post.normalize_keypoints(F1, 752, 480)
+    sg = pkg.SuperGlue(pkg.SuperGlueConfig(weights=weight_blobs[1], max_keypoints=400, max_batch=1,
+                                           precision=pkg.capi.RSPL_PREC_FP16))
+    assert sg.build(), sg.error
+    ok, i0, i1, m0, m1 = sg.infer(G0, G1)
+    assert ok, sg.error
+    Z = sg.debug_scores(0, F0.shape[1], F1.shape[1])
+    agree0 = (i0 == g["idx0"]).mean()
+    agree1 = (i1 == g["idx1"]).mean()
+    zerr = np.abs(Z - g["Z"]).max()
+    print(f"fp16 SG: idx0 agreement {agree0:.4f}, idx1 {agree1:.4f}, max |dZ| {zerr:.4g}, "
+          f"matches {int((i0 >= 0).sum())} vs {int((g['idx0'] >= 0).sum())}")
+    assert agree0 >= 0.99 and agree1 >= 0.99
+    both = (i0 >= 0) & (g["idx0"] >= 0)
+    np.testing.assert_allclose(m0[both], g["ms0"][both], atol=2e-2)
