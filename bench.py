@@ -44,6 +44,7 @@ capi = pkg.capi
 
 H, W, K = 480, 752, 400
 FP32_MFMA_PEAK = 157.3  # TFLOP/s, MI355X_MICROARCH.md (v_mfma_f32_32x32x2_f32, dense)
+FP16_MFMA_PEAK = 2516.8  # TFLOP/s dense (~2.5 PF, = 16 x the f32 MFMA rate), MI355X_MICROARCH.md
 CONV1_GFLOP_PER_IMAGE = 2 * H * W * 64 * 9 / 1e9 + 2 * H * W * 64 * 576 / 1e9  # conv1a + conv1b
 
 
@@ -86,13 +87,10 @@ def pmc_traffic(kernel_substr):
     """HBM bytes per launch of a kernel from the newest committed PMC summary
     (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from two rocprofv3
     --pmc passes, FETCH_SIZE x2 gfx950 correction), or None."""
-    files = sorted((ROOT / "profiles").glob("*_pmc_traffic.json"))
-    if not files:
-        return None, None
-    data = json.loads(files[-1].read_text())
-    for name, v in data.items():
-        if kernel_substr in name:
-            return v["traffic_bytes"], files[-1].name
+    for f in sorted((ROOT / "profiles").glob("*_pmc_traffic*.json"), reverse=True):  # newest first
+        for name, v in json.loads(f.read_text()).items():
+            if kernel_substr in name:
+                return v["traffic_bytes"], f.name
     return None, None
 
 
@@ -124,8 +122,11 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--cpu-frames", type=int, default=12, help="keyframes in the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp32",
-                    help="SP/SG MFMA precision: fp32 (parity path) or fp16 (the reference's TensorRT kFP16 engines)")
+    ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp16",
+                    help="SP/SG MFMA precision: fp16 = the reference's own TensorRT kFP16 engines "
+                         "(src/super_point.cpp:98, src/super_glue.cpp:132; default), fp32 = the parity path")
+    ap.add_argument("--single-precision", action="store_true",
+                    help="skip the second (other-precision) measurement")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -139,15 +140,19 @@ def main():
     capi.check(capi.load().rspl_set_device(local), "rspl_set_device")
 
     sp_w, sg_w = pkg.weights.ensure_blobs(str(ROOT / "weights"))
-    prec = capi.RSPL_PREC_FP16 if args.precision == "fp16" else capi.RSPL_PREC_FP32
-    sp = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=K, weights=sp_w, max_height=H, max_width=W,
-                                             max_batch=2, precision=prec, device=local))
-    assert sp.build(), sp.error
-    sg = pkg.SuperGlue(pkg.SuperGlueConfig(image_width=W, image_height=H, weights=sg_w, max_keypoints=K,
-                                           max_batch=2, precision=prec, device=local))
-    assert sg.build(), sg.error
+    precs = [args.precision] + (["fp32" if args.precision == "fp16" else "fp16"]
+                                if world == 1 and not args.single_precision else [])
+    handles = {}
+    for pr in precs:  # all handles and streams created once, up front: fixed HW-queue placement
+        code = capi.RSPL_PREC_FP16 if pr == "fp16" else capi.RSPL_PREC_FP32
+        sp_h = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=K, weights=sp_w, max_height=H, max_width=W,
+                                                   max_batch=2, precision=code, device=local))
+        assert sp_h.build(), sp_h.error
+        sg_h = pkg.SuperGlue(pkg.SuperGlueConfig(image_width=W, image_height=H, weights=sg_w, max_keypoints=K,
+                                                 max_batch=2, precision=code, device=local))
+        assert sg_h.build(), sg_h.error
+        handles[pr] = (sp_h, sg_h)
     ba = pkg.LocalBA(max_poses=16, max_points=6000, max_lines=200, max_edges=40000, device=local)
-
     syn = pkg.synthetic
     NP = 4
     pool = capi.DeviceBuffer(NP * 2 * H * W)
@@ -171,86 +176,104 @@ def main():
     st_sp, st_sg = capi.Stream(), capi.Stream(high_priority=True)
     ev_sp = [capi.Event() for _ in range(3)]
     ev_sg = [capi.Event() for _ in range(3)]
-    capi.synchronize()
-    ba_ms = []
-    ba_err = []
-    ba_q = queue.Queue(maxsize=2)
 
-    def tracking_thread():
-        """BA worker: the reference runs LocalmapOptimization on the tracking thread while the
-        feature thread keeps extracting/matching (src/map_builder.cc:48-49, src/map.cc:105-107)."""
-        capi.check(capi.load().rspl_set_device(local), "rspl_set_device")  # HIP device is per thread
-        while True:
-            prob = ba_q.get()
-            if prob is None:
+    def measure(precision):
+        """One full timed run of the pipeline at `precision`; returns its measurements."""
+        sp, sg = handles[precision]
+        for c in counts:
+            c.zero()
+        capi.synchronize()
+        ba_ms = []
+        ba_err = []
+        ba_q = queue.Queue(maxsize=2)
+
+        def tracking_thread():
+            """BA worker: the reference runs LocalmapOptimization on the tracking thread while the
+            feature thread keeps extracting/matching (src/map_builder.cc:48-49, src/map.cc:105-107)."""
+            capi.check(capi.load().rspl_set_device(local), "rspl_set_device")  # HIP device is per thread
+            while True:
+                prob = ba_q.get()
+                if prob is None:
+                    ba_q.task_done()
+                    return
+                t = time.perf_counter()
+                try:
+                    ba.run(prob)
+                except Exception as e:  # surfaced on the main thread
+                    ba_err.append(e)
+                ba_ms.append((time.perf_counter() - t) * 1e3)
                 ba_q.task_done()
-                return
-            t = time.perf_counter()
-            try:
-                ba.run(prob)
-            except Exception as e:  # surfaced on the main thread
-                ba_err.append(e)
-            ba_ms.append((time.perf_counter() - t) * 1e3)
-            ba_q.task_done()
 
-    worker = threading.Thread(target=tracking_thread, daemon=True)
-    worker.start()
+        worker = threading.Thread(target=tracking_thread, daemon=True)
+        worker.start()
 
-    def step(i):
-        slot, pslot = i % 3, (i - 1) % 3
-        cur, prev, ccur, cprev = feats[slot], feats[pslot], counts[slot], counts[pslot]
-        if i >= 2:
-            ev_sg[(i - 2) % 3].wait_on(st_sp.handle)
-        sp.infer_device(pool.offset((i % NP) * 2 * H * W), 2, H, W, W, H * W, cur.ptr, K, ccur.ptr, st_sp.handle)
-        ev_sp[slot].record(st_sp.handle)
-        ev_sp[slot].wait_on(st_sg.handle)
-        # PointMatching pairs: (L_t, L_kf) and (L_t, R_t)
-        capi.memcpy_d2d(f0.ptr, cur.ptr, FB, st_sg.handle)
-        capi.memcpy_d2d(f0.offset(FB), cur.ptr, FB, st_sg.handle)
-        capi.memcpy_d2d(f1.ptr, prev.ptr, FB, st_sg.handle)
-        capi.memcpy_d2d(f1.offset(FB), cur.offset(FB), FB, st_sg.handle)
-        capi.memcpy_d2d(n0.ptr, ccur.ptr, 4, st_sg.handle)
-        capi.memcpy_d2d(n0.offset(4), ccur.ptr, 4, st_sg.handle)
-        capi.memcpy_d2d(n1.ptr, cprev.ptr, 4, st_sg.handle)
-        capi.memcpy_d2d(n1.offset(4), ccur.offset(4), 4, st_sg.handle)
-        sg.infer_device(2, f0.ptr, n0.ptr, f1.ptr, n1.ptr, K, True, outs[0].ptr, outs[1].ptr, outs[2].ptr,
-                        outs[3].ptr, st_sg.handle)
-        ev_sg[slot].record(st_sg.handle)
-        # keyframe i's local BA goes to the tracking thread (own high-priority stream) through a
-        # 2-deep buffer, as the reference's feature thread blocks only while
-        # _tracking_data_buffer.size() >= 2 (src/map_builder.cc:176)
-        ba_q.put(problems[i % len(problems)])
+        def step(i):
+            slot, pslot = i % 3, (i - 1) % 3
+            cur, prev, ccur, cprev = feats[slot], feats[pslot], counts[slot], counts[pslot]
+            if i >= 2:
+                ev_sg[(i - 2) % 3].wait_on(st_sp.handle)
+            sp.infer_device(pool.offset((i % NP) * 2 * H * W), 2, H, W, W, H * W, cur.ptr, K, ccur.ptr, st_sp.handle)
+            ev_sp[slot].record(st_sp.handle)
+            ev_sp[slot].wait_on(st_sg.handle)
+            # PointMatching pairs: (L_t, L_kf) and (L_t, R_t)
+            capi.memcpy_d2d(f0.ptr, cur.ptr, FB, st_sg.handle)
+            capi.memcpy_d2d(f0.offset(FB), cur.ptr, FB, st_sg.handle)
+            capi.memcpy_d2d(f1.ptr, prev.ptr, FB, st_sg.handle)
+            capi.memcpy_d2d(f1.offset(FB), cur.offset(FB), FB, st_sg.handle)
+            capi.memcpy_d2d(n0.ptr, ccur.ptr, 4, st_sg.handle)
+            capi.memcpy_d2d(n0.offset(4), ccur.ptr, 4, st_sg.handle)
+            capi.memcpy_d2d(n1.ptr, cprev.ptr, 4, st_sg.handle)
+            capi.memcpy_d2d(n1.offset(4), ccur.offset(4), 4, st_sg.handle)
+            sg.infer_device(2, f0.ptr, n0.ptr, f1.ptr, n1.ptr, K, True, outs[0].ptr, outs[1].ptr, outs[2].ptr,
+                            outs[3].ptr, st_sg.handle)
+            ev_sg[slot].record(st_sg.handle)
+            # keyframe i's local BA goes to the tracking thread (own high-priority stream) through a
+            # 2-deep buffer, as the reference's feature thread blocks only while
+            # _tracking_data_buffer.size() >= 2 (src/map_builder.cc:176)
+            ba_q.put(problems[i % len(problems)])
 
-    for i in range(args.warmup):
-        step(i)
-    ba_q.join()
-    capi.synchronize()
-    if dist:
-        dist.barrier()
-    sp.profile(True)
-    sg.profile(True)
-    ba_ms.clear()
-    t0 = time.perf_counter()
-    for i in range(args.steps):
-        step(args.warmup + i)
-    ba_q.join()
-    capi.synchronize()
-    elapsed = job_time(time.perf_counter() - t0, dist)
-    ba_q.put(None)
-    worker.join()
-    if ba_err:
-        raise ba_err[0]
-    if dist:
-        dist.barrier()
+        for i in range(args.warmup):
+            step(i)
+        ba_q.join()
+        capi.synchronize()
+        if dist:
+            dist.barrier()
+        sp.profile(True)
+        sg.profile(True)
+        ba_ms.clear()
+        t0 = time.perf_counter()
+        for i in range(args.steps):
+            step(args.warmup + i)
+        ba_q.join()
+        capi.synchronize()
+        elapsed = job_time(time.perf_counter() - t0, dist)
+        ba_q.put(None)
+        worker.join()
+        if ba_err:
+            raise ba_err[0]
+        if dist:
+            dist.barrier()
 
-    sp_ms, sp_calls = sp.stage_times()
-    sg_ms, sg_calls = sg.stage_times()
-    conv1_ms = sp_ms[0] / max(1, sp_calls)
-    achieved = 2 * CONV1_GFLOP_PER_IMAGE / conv1_ms  # GFLOP / ms = TFLOP/s
-    traffic, traffic_src = pmc_traffic("conv3x3_kernel<64, 16, true, true>")
-    value = job_value(world, args.steps, elapsed)
+        sp_ms, sp_calls = sp.stage_times()
+        sg_ms, sg_calls = sg.stage_times()
+        conv1_ms = sp_ms[0] / max(1, sp_calls)
+        achieved = 2 * CONV1_GFLOP_PER_IMAGE / conv1_ms  # GFLOP / ms = TFLOP/s
+        value = job_value(world, args.steps, elapsed)
+        return {"value": value, "elapsed": elapsed, "sp": (sp_ms, sp_calls), "sg": (sg_ms, sg_calls), "stages": (sp, sg),
+                "conv1_ms": conv1_ms, "achieved": achieved, "ba_ms": list(ba_ms)}
+
+    res = measure(args.precision)
+    other = measure(precs[1]) if len(precs) > 1 else None  # the other precision, same run, for the record
+    value, elapsed, conv1_ms, achieved, ba_ms = (res["value"], res["elapsed"], res["conv1_ms"], res["achieved"],
+                                                 res["ba_ms"])
+    sp_ms, sp_calls = res["sp"]
+    sg_ms, sg_calls = res["sg"]
+    sp, sg = res["stages"]
+    traffic, traffic_src = pmc_traffic("conv3x3_kernel<64, 16, true, true>" if args.precision == "fp32"
+                                       else "conv3x3_h_kernel<64, 16, true, true, false>")
     if rank != 0:
         return
+    peak = FP16_MFMA_PEAK if args.precision == "fp16" else FP32_MFMA_PEAK
     out = {
         "metric": "stereo frames/sec SuperPoint+SuperGlue+localBA @752x480 (all-keyframe: 2xSP, 2xSG, 1 BA per frame)",
         "value": round(value, 3),
@@ -262,17 +285,21 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32 (SuperPoint/SuperGlue MFMA), fp64 (BA)",
+        "dtype": ("fp16 MFMA with fp32 accumulation for SuperPoint/SuperGlue (the reference's TensorRT kFP16 "
+                  "engines), fp32 Sinkhorn/decode, fp64 BA") if args.precision == "fp16"
+                 else "fp32 (SuperPoint/SuperGlue MFMA), fp64 (BA)",
         "data": "synthetic (seeded textured stereo 752x480, seeded weights, synthetic C3 local-BA problems)",
         "config": {"workload": "C3 EuRoC 752x480 stereo keyframe stream: SP batch 2 top-400, SG 2 pairs N=400, "
                                "local BA 10 poses / ~4k points / 100 lines",
                    "global_batch": world, "parallelism": f"replicas x{world} (one sequence per GPU)"},
-        "roofline": {"kernel": "conv3x3_kernel<64,16,true,true> (conv1a+conv1b+ReLU+pool, fused)",
-                     "bound": "mfma", "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK, "unit": "TFLOP/s",
-                     "frac": round(achieved / FP32_MFMA_PEAK, 4),
+        "roofline": {"kernel": ("conv3x3_h_kernel<64,16,true,true,false>" if args.precision == "fp16"
+                                else "conv3x3_kernel<64,16,true,true>") + " (conv1a+conv1b+ReLU+pool, fused)",
+                     "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4),
                      "traffic": round(traffic) if traffic else None,
                      "traffic_note": (f"HBM bytes per launch, rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE, {traffic_src}; "
-                                      "algorithmic minimum = 46.2 MB pooled output + 0.7 MB images")
+                                      "algorithmic minimum = pooled 64-ch output (46.2 MB fp32 / 23.1 MB fp16) "
+                                      "+ 0.7 MB images")
                      if traffic else None,
                      "algorithmic": f"{2 * CONV1_GFLOP_PER_IMAGE:.3f} GFLOP per launch (2 images)",
                      "avg_launch_ms": round(conv1_ms, 4)},
@@ -280,6 +307,12 @@ def main():
                                **{f"sg:{n}": round(v / max(1, sg_calls), 4) for n, v in zip(sg.STAGES, sg_ms)},
                                "ba:wall": round(float(np.mean(ba_ms)), 4) if ba_ms else None},
     }
+    if other is not None:
+        oname = "fp32" if args.precision == "fp16" else "fp16"
+        out[f"{oname}_run"] = {"value": round(other["value"], 3),
+                               "ms_per_step": round(1e3 * other["elapsed"] / args.steps, 3),
+                               "note": "same workload and run, SP/SG at " + oname +
+                                       (" (the bit-parity path)" if oname == "fp32" else "")}
     if world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         out["cpu_baseline"] = cpu_baseline(sp_w, sg_w, args.cpu_frames, threads)
