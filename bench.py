@@ -174,6 +174,7 @@ def main():
     outs = [capi.DeviceBuffer(2 * K * sz) for sz in (4, 4, 8, 8)]
     # SG is the frame's critical chain (SP has slack): SG and the BA run at high priority
     st_sp, st_sg = capi.Stream(), capi.Stream(high_priority=True)
+    st_post = capi.Stream(high_priority=True)  # SG's Sinkhorn + decode: overlaps the next frame's GNN
     ev_sp = [capi.Event() for _ in range(3)]
     ev_sg = [capi.Event() for _ in range(3)]
 

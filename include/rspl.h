@@ -159,6 +159,15 @@ int rspl_sg_infer_device(rspl_sg* sg, int batch, const double* d_feat0, const in
                          int32_t* d_idx0, int32_t* d_idx1, double* d_ms0, double* d_ms1,
                          void* stream);
 
+/* As rspl_sg_infer_device, with the log-Sinkhorn and decode enqueued on post_stream (after
+ * an event on stream): the next call's GNN on `stream` overlaps this call's Sinkhorn.
+ * Results are complete when post_stream reaches this point.  The counts are snapshotted,
+ * so the caller may reuse n0/n1 once `stream` has passed the call. */
+int rspl_sg_infer_device2(rspl_sg* sg, int batch, const double* d_feat0, const int* n0,
+                          const double* d_feat1, const int* n1, int stride_feat, int normalize,
+                          int32_t* d_idx0, int32_t* d_idx1, double* d_ms0, double* d_ms1, void* stream,
+                          void* post_stream);
+
 /* Log-assignment Z [(n0+1)*(n1+1)] f32 of the last call, pair p (for tests). */
 int rspl_sg_debug_scores(rspl_sg* sg, int p, float* Z);
 

@@ -137,10 +137,18 @@ class SuperGlue:
         return True, i0, i1, m0, m1
 
     def infer_device(self, batch: int, d_feat0: int, d_n0: int, d_feat1: int, d_n1: int, stride_feat: int,
-                     normalize: bool, d_idx0: int, d_idx1: int, d_ms0: int, d_ms1: int, stream=None) -> None:
-        capi.check(self._lib.rspl_sg_infer_device(self._h, batch, d_feat0, d_n0, d_feat1, d_n1, stride_feat,
-                                                  int(normalize), d_idx0, d_idx1, d_ms0, d_ms1, stream),
-                   "rspl_sg_infer_device")
+                     normalize: bool, d_idx0: int, d_idx1: int, d_ms0: int, d_ms1: int, stream=None,
+                     post_stream=None) -> None:
+        """Device-resident batched SuperGlue; with post_stream, Sinkhorn + decode run there
+        (results complete on post_stream) so the next call's GNN overlaps them."""
+        if post_stream is None:
+            capi.check(self._lib.rspl_sg_infer_device(self._h, batch, d_feat0, d_n0, d_feat1, d_n1, stride_feat,
+                                                      int(normalize), d_idx0, d_idx1, d_ms0, d_ms1, stream),
+                       "rspl_sg_infer_device")
+        else:
+            capi.check(self._lib.rspl_sg_infer_device2(self._h, batch, d_feat0, d_n0, d_feat1, d_n1, stride_feat,
+                                                       int(normalize), d_idx0, d_idx1, d_ms0, d_ms1, stream,
+                                                       post_stream), "rspl_sg_infer_device2")
 
     STAGES = ("prep+kenc", "gnn x18", "final+scores", "sinkhorn", "decode")
 

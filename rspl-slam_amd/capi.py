@@ -24,7 +24,7 @@ EXPORTS = [
     "rspl_timer_destroy",
     "rspl_sp_create", "rspl_sp_infer", "rspl_sp_infer_device", "rspl_sp_debug_maps", "rspl_sp_profile",
     "rspl_sp_stage_times", "rspl_sp_destroy",
-    "rspl_sg_create", "rspl_sg_infer", "rspl_sg_infer_device", "rspl_sg_debug_scores", "rspl_sg_profile",
+    "rspl_sg_create", "rspl_sg_infer", "rspl_sg_infer_device", "rspl_sg_infer_device2", "rspl_sg_debug_scores", "rspl_sg_profile",
     "rspl_sg_stage_times", "rspl_sg_destroy",
     "rspl_pm_match",
     "rspl_ba_create", "rspl_ba_local", "rspl_ba_destroy",
@@ -103,6 +103,7 @@ def load(path: pathlib.Path = LIB_PATH):
         lib.rspl_sg_create.argtypes = [C.POINTER(SgConfig), C.c_char_p, C.POINTER(vp)]
         lib.rspl_sg_infer.argtypes = [vp, vp, ip, vp, ip, vp, vp, vp, vp]
         lib.rspl_sg_infer_device.argtypes = [vp, ip, vp, vp, vp, vp, ip, ip, vp, vp, vp, vp, vp]
+        lib.rspl_sg_infer_device2.argtypes = [vp, ip, vp, vp, vp, vp, ip, ip, vp, vp, vp, vp, vp, vp]
         lib.rspl_sg_debug_scores.argtypes = [vp, ip, vp]
         lib.rspl_sg_profile.argtypes = [vp, ip]
         lib.rspl_sg_stage_times.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(ip)]

@@ -45,6 +45,12 @@ struct rspl_sg {
   int32_t* h_idx = nullptr;
   double* h_ms = nullptr;
   int last_n0 = 0, last_n1 = 0, last_B = 0;
+  // post-stream pipelining: couplings / Z / counts double-buffered by call parity
+  int *cn0, *cn1;                     // [2][B] the call's counts (the caller may reuse its own at once)
+  hipEvent_t ev_ready = nullptr;      // main stream: couplings of this call written
+  hipEvent_t ev_sink[2] = {nullptr, nullptr};  // post stream: Sinkhorn of parity p done with cpl[p]
+  unsigned long long calls = 0;
+  int last_parity = 0;
   StageTimer timer;
 };
 
@@ -73,7 +79,8 @@ void carve(F& ar, rspl_sg* s) {
   take(s->hw1, (size_t)kLayers * 512 * 512); take(s->hw2, (size_t)kLayers * 512 * 256); take(s->hwf, 256 * 256);
   take(s->kin, T * kKencIn); take(s->h1, T * 256); take(s->h2, T * 256);
   take(s->X, T * 256); take(s->QKV, T * 768); take(s->O, T * 256); take(s->MSG, T * 256); take(s->HID, T * 512);
-  take(s->cpl, B * ld * ld); take(s->Z, B * ld * ld); take(s->part, B * 2 * s->G * ld);
+  take(s->cpl, 2 * B * ld * ld); take(s->Z, 2 * B * ld * ld); take(s->part, B * 2 * s->G * ld);
+  take(s->cn0, 2 * B); take(s->cn1, 2 * B);
   take(s->err, B);
   take(s->max0, B * s->nmax); take(s->val0, B * s->nmax); take(s->max1, B * s->nmax);
   take(s->idx0, B * s->nmax); take(s->idx1, B * s->nmax); take(s->ms0, B * s->nmax); take(s->ms1, B * s->nmax);
@@ -236,6 +243,9 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
   }
   const size_t nm = s->nmax;
   if (s->timer.init(RSPL_SG_STAGES) != RSPL_OK || hipStreamCreateWithFlags(&s->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_sink[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_sink[1], hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(&s->h_f, sizeof(double) * nm * 259 * 2) != hipSuccess ||
       hipHostMalloc(&s->h_idx, sizeof(int32_t) * nm * 2 + 16) != hipSuccess ||
       hipHostMalloc(&s->h_ms, sizeof(double) * nm * 2) != hipSuccess) {
@@ -278,6 +288,9 @@ extern "C" void rspl_sg_destroy(rspl_sg* s) {
   if (s->h_f) (void)hipHostFree(s->h_f);
   if (s->h_idx) (void)hipHostFree(s->h_idx);
   if (s->h_ms) (void)hipHostFree(s->h_ms);
+  if (s->ev_ready) (void)hipEventDestroy(s->ev_ready);
+  for (auto& e : s->ev_sink)
+    if (e) (void)hipEventDestroy(e);
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
@@ -285,12 +298,29 @@ extern "C" void rspl_sg_destroy(rspl_sg* s) {
 extern "C" int rspl_sg_infer_device(rspl_sg* s, int B, const double* d_feat0, const int* d_n0, const double* d_feat1,
                                     const int* d_n1, int stride_feat, int normalize, int32_t* d_idx0, int32_t* d_idx1,
                                     double* d_ms0, double* d_ms1, void* stream_) {
+  return rspl_sg_infer_device2(s, B, d_feat0, d_n0, d_feat1, d_n1, stride_feat, normalize, d_idx0, d_idx1, d_ms0, d_ms1,
+                               stream_, stream_);
+}
+
+extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, const int* d_n0,
+                                     const double* d_feat1, const int* d_n1, int stride_feat, int normalize,
+                                     int32_t* d_idx0, int32_t* d_idx1, double* d_ms0, double* d_ms1, void* stream_,
+                                     void* post_stream_) {
   RSPL_CHECK_ARG(s && d_feat0 && d_feat1 && d_n0 && d_n1 && d_idx0 && d_idx1 && d_ms0 && d_ms1,
                  "rspl_sg_infer_device: NULL argument");
   RSPL_CHECK_ARG(B >= 1 && B <= s->B, "batch %d outside [1, %d]", B, s->B);
   RSPL_CHECK_ARG(stride_feat >= 1, "stride_feat must be >= 1");
   hipStream_t st = stream_ ? (hipStream_t)stream_ : s->stream;
+  hipStream_t pst = post_stream_ ? (hipStream_t)post_stream_ : st;
   const int nm = s->nmax, T = B * 2 * nm;
+  const int par = (int)(s->calls++ & 1);
+  float* cpl = s->cpl + (size_t)par * s->B * s->ld * s->ld;
+  float* Zp = s->Z + (size_t)par * s->B * s->ld * s->ld;
+  int* cn0 = s->cn0 + par * s->B;
+  int* cn1 = s->cn1 + par * s->B;
+  // counts snapshot (the post stream still reads them after the caller moved on)
+  RSPL_HIP(hipMemcpyAsync(cn0, d_n0, sizeof(int) * B, hipMemcpyDeviceToDevice, st));
+  RSPL_HIP(hipMemcpyAsync(cn1, d_n1, sizeof(int) * B, hipMemcpyDeviceToDevice, st));
   // process_input (+ NormalizeKeypoints when called as PointMatching)
   s->timer.mark(0, st);
   sg::PrepArgs pa{};
@@ -334,7 +364,8 @@ extern "C" int rspl_sg_infer_device(rspl_sg* s, int B, const double* d_feat0, co
   float* MD = s->MSG;
   RSPL_HIP(sg::gemm(G_(s->X, 256, s->wf, 256, s->bf, MD, 256, T, 256, 256, 0, h16 ? s->hwf : nullptr), 1, st));
   {
-    sg::GemmArgs g = G_(MD, 256, MD + (size_t)nm * 256, 256, nullptr, s->cpl, s->ld, nm, nm, 256, 0);
+    if (pst != st && s->calls > 2) RSPL_HIP(hipStreamWaitEvent(st, s->ev_sink[par], 0));
+    sg::GemmArgs g = G_(MD, 256, MD + (size_t)nm * 256, 256, nullptr, cpl, s->ld, nm, nm, 256, 0);
     g.b_nt = 1;
     g.alpha = 1.f / 16.f;
     g.sA = g.sB = (long long)2 * nm * 256;
@@ -343,11 +374,15 @@ extern "C" int rspl_sg_infer_device(rspl_sg* s, int B, const double* d_feat0, co
     RSPL_HIP(sg::gemm(g, B, st));
   }
   sg::BinsArgs bn{};
-  bn.cpl = s->cpl; bn.n0 = d_n0; bn.n1 = d_n1; bn.alpha = s->bin; bn.nmax = nm;
+  bn.cpl = cpl; bn.n0 = d_n0; bn.n1 = d_n1; bn.alpha = s->bin; bn.nmax = nm;
   RSPL_HIP(sg::bins(bn, B, st));
   s->timer.mark(3, st);
+  if (pst != st) {  // log-Sinkhorn + decode on the post stream: the next call's GNN overlaps them
+    RSPL_HIP(hipEventRecord(s->ev_ready, st));
+    RSPL_HIP(hipStreamWaitEvent(pst, s->ev_ready, 0));
+  }
   // log_optimal_transport (superglue.py:185-205)
-  RSPL_HIP(hipMemsetAsync(s->err, 0, sizeof(unsigned) * B, st));
+  RSPL_HIP(hipMemsetAsync(s->err, 0, sizeof(unsigned) * B, pst));
   static unsigned long long* probe = nullptr;  // debug only (RSPL_SG_PROBE)
   static const bool probing = getenv("RSPL_SG_PROBE") != nullptr;
   if (probing && !probe) {
@@ -356,26 +391,28 @@ extern "C" int rspl_sg_infer_device(rspl_sg* s, int B, const double* d_feat0, co
   }
   sg::SinkArgs sk{};
   sk.probe = probe;
-  sk.cpl = s->cpl; sk.Z = s->Z; sk.part = s->part; sk.seq = s->sk_seq = (s->sk_seq % 0xFFFFFu) + 1; sk.err = s->err; sk.n0 = d_n0; sk.n1 = d_n1;
+  sk.cpl = cpl; sk.Z = Zp; sk.part = s->part; sk.seq = s->sk_seq = (s->sk_seq % 0xFFFFFu) + 1; sk.err = s->err; sk.n0 = cn0; sk.n1 = cn1;
   sk.nmax = nm; sk.G = s->G; sk.iters = s->cfg.sinkhorn_iterations;
-  RSPL_HIP(sg::sinkhorn(sk, B, st));
+  RSPL_HIP(sg::sinkhorn(sk, B, pst));
+  if (pst != st) RSPL_HIP(hipEventRecord(s->ev_sink[par], pst));
   if (probing) {  // debug: Sinkhorn cycles per workgroup-iteration by phase
     unsigned long long h[4];
-    RSPL_HIP(hipStreamSynchronize(st));
+    RSPL_HIP(hipStreamSynchronize(pst));
     RSPL_HIP(hipMemcpy(h, probe, sizeof(h), hipMemcpyDeviceToHost));
     RSPL_HIP(hipMemset(probe, 0, sizeof(h)));
     if (h[3]) fprintf(stderr, "sinkhorn cycles/iter: row %.0f col %.0f exchange %.0f\n", (double)h[0] / h[3],
                       (double)h[1] / h[3], (double)h[2] / h[3]);
   }
-  s->timer.mark(4, st);
+  s->timer.mark(4, pst);
   // decode (super_glue.cpp:339-367), threshold 0.2 hard-coded as in the reference (:355)
   sg::DecodeArgs dc{};
-  dc.Z = s->Z; dc.n0 = d_n0; dc.n1 = d_n1; dc.nmax = nm; dc.max0 = s->max0; dc.val0 = s->val0; dc.max1 = s->max1;
+  dc.Z = Zp; dc.n0 = cn0; dc.n1 = cn1; dc.nmax = nm; dc.max0 = s->max0; dc.val0 = s->val0; dc.max1 = s->max1;
   dc.idx0 = d_idx0; dc.idx1 = d_idx1; dc.ms0 = d_ms0; dc.ms1 = d_ms1; dc.threshold = 0.2f;
-  RSPL_HIP(sg::decode(dc, B, st));
-  s->timer.mark(5, st);
+  RSPL_HIP(sg::decode(dc, B, pst));
+  s->timer.mark(5, pst);
   s->timer.end_call();
   s->last_B = B;
+  s->last_parity = par;
   return RSPL_OK;
 }
 
@@ -463,7 +500,8 @@ extern "C" int rspl_sg_debug_scores(rspl_sg* s, int p, float* Z) {
   RSPL_CHECK_ARG(s && Z && p >= 0 && p < s->last_B, "rspl_sg_debug_scores: bad argument");
   RSPL_HIP(hipStreamSynchronize(s->stream));
   const int R = s->last_n0 + 1, Cc = s->last_n1 + 1;
-  RSPL_HIP(hipMemcpy2D(Z, sizeof(float) * Cc, s->Z + (size_t)p * s->ld * s->ld, sizeof(float) * s->ld,
+  RSPL_HIP(hipMemcpy2D(Z, sizeof(float) * Cc, s->Z + ((size_t)s->last_parity * s->B + p) * s->ld * s->ld,
+                       sizeof(float) * s->ld,
                        sizeof(float) * Cc, R, hipMemcpyDeviceToHost));
   return RSPL_OK;
 }

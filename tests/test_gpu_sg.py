@@ -118,3 +118,45 @@ def test_sg_fp16_vs_reference(pkg, golden, weight_blobs):
     assert agree0 >= 0.99 and agree1 >= 0.99
     both = (i0 >= 0) & (g["idx0"] >= 0)
     np.testing.assert_allclose(m0[both], g["ms0"][both], atol=2e-2)
+
+
+def test_sg_post_stream_pipelined(pkg, weight_blobs):
+    """rspl_sg_infer_device2: Sinkhorn + decode on a second stream, 4 calls back to back with the
+    count buffers overwritten right after each call (parity double-buffering + count snapshot);
+    every call's indices equal the single-stream result of the same inputs."""
+    from rspl_slam_amd import capi
+    from rspl_slam_amd import synthetic as SY
+    nmax, B = 400, 2
+    sg = _sg(pkg, weight_blobs[1], nmax=nmax, B=B)
+    calls = []
+    for c in range(4):
+        probs = [SY.sg_problem(400 - 20 * c, 380, 250, seed=30 + c), SY.sg_problem(300 + 10 * c, 400, 200, seed=40 + c)]
+        f0 = np.zeros((B, nmax, 259)); f1 = np.zeros((B, nmax, 259))
+        n0 = np.zeros(B, np.int32); n1 = np.zeros(B, np.int32)
+        for p, (F0, F1, _) in enumerate(probs):
+            f0[p, :F0.shape[1]] = F0.T; f1[p, :F1.shape[1]] = F1.T
+            n0[p], n1[p] = F0.shape[1], F1.shape[1]
+        calls.append((f0, f1, n0, n1))
+
+    def run(post):
+        st, pst = capi.Stream(), capi.Stream()
+        fb = [capi.DeviceBuffer(calls[0][0].nbytes) for _ in range(2)]
+        cb = [capi.DeviceBuffer(8) for _ in range(2)]
+        outs = [{k: capi.DeviceBuffer(B * nmax * sz) for k, sz in dict(i0=4, i1=4, m0=8, m1=8).items()}
+                for _ in calls]
+        for c, (f0, f1, n0, n1) in enumerate(calls):
+            st.synchronize()
+            fb[0].upload(f0); fb[1].upload(f1); cb[0].upload(n0); cb[1].upload(n1)
+            o = outs[c]
+            sg.infer_device(B, fb[0].ptr, cb[0].ptr, fb[1].ptr, cb[1].ptr, nmax, True, o["i0"].ptr, o["i1"].ptr,
+                            o["m0"].ptr, o["m1"].ptr, st.handle, post_stream=pst.handle if post else None)
+            if post:  # overwrite the counts as soon as the main stream has passed the call
+                st.synchronize()
+                cb[0].upload(np.zeros(B, np.int32)); cb[1].upload(np.zeros(B, np.int32))
+        capi.synchronize()
+        return [(o["i0"].download((B, nmax), np.int32), o["i1"].download((B, nmax), np.int32)) for o in outs]
+
+    ref, got = run(False), run(True)
+    for (a0, a1), (b0, b1) in zip(ref, got):
+        np.testing.assert_array_equal(a0, b0)
+        np.testing.assert_array_equal(a1, b1)
