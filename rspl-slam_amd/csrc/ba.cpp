@@ -4,7 +4,8 @@
 //   initializeOptimization(0) + optimize(5) -> inlier flags -> write back T_wc, points, lines.
 // The Levenberg-Marquardt control (g2o OptimizationAlgorithmLevenberg: tau 1e-5,
 // good-step factor clamp [1/3, 2/3], ni doubling, 10 trials) runs on the host.  Each
-// trial is 5 kernels; the last block of the cost kernel posts {chi2, scale, fail} and a
+// trial is 3 kernels (Schur chunks; LDL^T solve + candidate poses; landmark update + cost,
+// see ba_kernels.hip); the last block of the cost kernel posts {chi2, scale, fail} and a
 // sequence number to a pinned host-mapped mailbox that the host spins on (no stream
 // synchronisation, no D2H copy on the critical path).  Host->device traffic goes through
 // one pinned staging buffer (async copies only).
@@ -39,6 +40,7 @@ struct rspl_ba {
   // system
   double *Hll, *bl, *bp, *S, *x, *partial, *partial2, *out;
   int* flags;  // [0] fail, [1] error-kernel ticket counter
+  unsigned* lm_ctr;  // [max_lines] line-landmark tickets (zeroed at create, re-armed by the kernel)
   // per-phase active structure + Schur chunk partials (growable device buffer)
   char* phase_buf = nullptr;
   size_t phase_cap = 0;
@@ -78,8 +80,11 @@ void carve(F& ar, rspl_ba* b) {
   take(b->bl_e, E * 4); take(b->Hpl_e, E * 24);
   take(b->level, E); take(b->inlier, E); take(b->lm_act2, NL);
   take(b->Hll, NL * 16); take(b->bl, NL * 4); take(b->bp, K * 6);
-  take(b->S, 36 * K * K); take(b->x, 6 * K); take(b->partial, E / 256 + 2);
-  take(b->partial2, (size_t)b->maxV / 256 + 2); take(b->out, 8); take(b->flags, 4);
+  // block partials: edge-per-thread kernels (E / 256) and landmark-group kernels (NL * 8 / 256)
+  const size_t nblk = std::max(E / 256, NL * 8 / 256) + 2;
+  take(b->S, 36 * K * K); take(b->x, 6 * K); take(b->partial, nblk);
+  take(b->partial2, std::max((size_t)b->maxV / 256, nblk) + 2); take(b->out, 8); take(b->flags, 4);
+  take(b->lm_ctr, nl);
 }
 
 int ensure_stage(rspl_ba* b, size_t bytes) {
@@ -348,8 +353,7 @@ int optimize(rspl_ba* b, ba::Problem& P, const ba::Lin& Lr, ba::Sys& S, const ba
   double lambda = 0, ni = 2;
   int done = 0;
   for (int it = 0; it < iters; it++) {
-    RSPL_HIP(ba::linearize(P, Lr, A, st));
-    RSPL_HIP(ba::reduce_blocks(P, Lr, A, S, it == 0, st));
+    RSPL_HIP(ba::linearize(P, Lr, A, S, it == 0, st));
     if (it == 0) {
       q = ++b->seq;
       RSPL_HIP(ba::post(S, q, st));
@@ -420,7 +424,8 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
   if (hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipHostMalloc((void**)&b->mail, sizeof(ba::Mail), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&b->mail_dev, b->mail, 0) != hipSuccess ||
-      hipMemset(b->flags, 0, 4 * sizeof(int)) != hipSuccess || hipMemset(b->out, 0, 8 * sizeof(double)) != hipSuccess) {
+      hipMemset(b->flags, 0, 4 * sizeof(int)) != hipSuccess || hipMemset(b->out, 0, 8 * sizeof(double)) != hipSuccess ||
+      hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess) {
     set_error("BA stream / mailbox allocation failed");
     rspl_ba_destroy(b);
     return RSPL_E_DEVICE;
@@ -555,6 +560,7 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   ba::Sys S{};
   S.Hll = b->Hll; S.bl = b->bl; S.bp = b->bp; S.S = b->S; S.x = b->x; S.partial = b->partial;
   S.partial2 = b->partial2; S.out = b->out; S.fail = b->flags; S.counter = reinterpret_cast<unsigned*>(b->flags + 1);
+  S.lm_ctr = b->lm_ctr;
   S.mail = b->mail_dev;
   const size_t phase_soff = al256(call_bytes);
   // ---- phase 1: all edges, Huber ----

@@ -56,15 +56,20 @@ __device__ __forceinline__ void R_to_q(const double* m, double* q) {
   } else {
     int i = 0;
     if (m[4] > m[0]) i = 1;
-    if (m[8] > m[i * 3 + i]) i = 2;
-    const int j = (i + 1) % 3, k = (j + 1) % 3;
-    double s = sqrt(m[i * 3 + i] - m[j * 3 + j] - m[k * 3 + k] + 1.0);
+    if (m[8] > (i == 0 ? m[0] : m[4])) i = 2;
+    // (i, j, k) cyclic; each case spelled out so every index is a constant (no scratch)
+    auto branch = [&](int ii, int jj, int kk, double* v) {
+      double s = sqrt(m[ii * 3 + ii] - m[jj * 3 + jj] - m[kk * 3 + kk] + 1.0);
+      v[ii] = 0.5 * s;
+      s = 0.5 / s;
+      q[0] = (m[kk * 3 + jj] - m[jj * 3 + kk]) * s;
+      v[jj] = (m[jj * 3 + ii] + m[ii * 3 + jj]) * s;
+      v[kk] = (m[kk * 3 + ii] + m[ii * 3 + kk]) * s;
+    };
     double v[3];
-    v[i] = 0.5 * s;
-    s = 0.5 / s;
-    q[0] = (m[k * 3 + j] - m[j * 3 + k]) * s;
-    v[j] = (m[j * 3 + i] + m[i * 3 + j]) * s;
-    v[k] = (m[k * 3 + i] + m[i * 3 + k]) * s;
+    if (i == 0) branch(0, 1, 2, v);
+    else if (i == 1) branch(1, 2, 0, v);
+    else branch(2, 0, 1, v);
     q[1] = v[0]; q[2] = v[1]; q[3] = v[2];
   }
 }
@@ -374,18 +379,14 @@ __device__ __forceinline__ double edge_weight(const Problem& P, const Lin& L, co
   return w;
 }
 
-// point edges: analytic Jacobians (g2o types_sba), one thread per edge.  Mono edges
-// carry a zero third row, so every index below is a compile-time constant
-// (register resident, no scratch).
-__device__ __forceinline__ void lin_points(const Problem& P, const Lin& L, const Active& A, int i) {
-  if (i >= A.Ea - A.n_line_edges) return;
-  const int e = A.edges[i];
-  if (A.elevel && A.elevel[e]) {  // outside this phase: exact-zero records
-#pragma unroll
-    for (int k = 0; k < 16; k++) L.Hll[16 * e + k] = 0.0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) L.bl[4 * e + k] = 0.0;
-    if (A.pidx[P.epose[e]] >= 0) {
+// point edges: analytic Jacobians (g2o types_sba).  Mono edges carry a zero third
+// row, so every index below is a compile-time constant (register resident, no scratch).
+// Writes the pose-side records of edge e (when its pose is optimised) and accumulates
+// the landmark side (Hll 3x3, bl 3) into hl / bv.
+__device__ __forceinline__ void point_edge(const Problem& P, const Lin& L, const Active& A, int e, bool pose_opt,
+                                           double (&hl)[9], double (&bv)[3]) {
+  if (A.elevel && A.elevel[e]) {  // outside this phase: exact-zero records, no contribution
+    if (pose_opt) {
 #pragma unroll
       for (int k = 0; k < 36; k++) L.Hpp[36 * e + k] = 0.0;
 #pragma unroll
@@ -429,18 +430,13 @@ __device__ __forceinline__ void lin_points(const Problem& P, const Lin& L, const
   const double w = edge_weight(P, L, A, e, t);
   const double* er4 = L.err + 4 * e;
   const double er[3] = {er4[0], er4[1], st ? er4[2] : 0.0};
-  double* Hll = L.Hll + 16 * e;
 #pragma unroll
   for (int a = 0; a < 3; a++)
 #pragma unroll
-    for (int b = 0; b < 3; b++) Hll[a * 3 + b] = w * (Jl[0][a] * Jl[0][b] + Jl[1][a] * Jl[1][b] + Jl[2][a] * Jl[2][b]);
+    for (int b = 0; b < 3; b++) hl[a * 3 + b] += w * (Jl[0][a] * Jl[0][b] + Jl[1][a] * Jl[1][b] + Jl[2][a] * Jl[2][b]);
 #pragma unroll
-  for (int k = 9; k < 16; k++) Hll[k] = 0.0;
-  double* bl = L.bl + 4 * e;
-#pragma unroll
-  for (int a = 0; a < 3; a++) bl[a] = -w * (Jl[0][a] * er[0] + Jl[1][a] * er[1] + Jl[2][a] * er[2]);
-  bl[3] = 0.0;
-  if (A.pidx[pose] < 0) return;
+  for (int a = 0; a < 3; a++) bv[a] += -w * (Jl[0][a] * er[0] + Jl[1][a] * er[1] + Jl[2][a] * er[2]);
+  if (!pose_opt) return;
   double* Hpp = L.Hpp + 36 * e;
   double* bp = L.bp + 6 * e;
   double* Hpl = L.Hpl + 24 * e;
@@ -455,24 +451,66 @@ __device__ __forceinline__ void lin_points(const Problem& P, const Lin& L, const
   }
 }
 
-// line edges: g2o's numeric central difference (delta 1e-9), one wave per edge,
-// the 20 perturbed error evaluations (+-delta on 4 line + 6 pose dims) in parallel lanes.
-__device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const Active& A, int blk) {
+__device__ __forceinline__ void atomic_max_pos(double* addr, double v) {
+  // non-negative doubles order like their bit patterns
+  atomicMax(reinterpret_cast<unsigned long long*>(addr), (unsigned long long)__double_as_longlong(v));
+}
+
+// sum over the kGroup lanes of a landmark group (fixed butterfly: deterministic; every
+// lane of the wave takes part)
+constexpr int kGroup = 8;
+template <int N>
+__device__ __forceinline__ void group_sum(double (&v)[N]) {
+#pragma unroll
+  for (int o = 1; o < kGroup; o <<= 1)
+#pragma unroll
+    for (int i = 0; i < N; i++) v[i] += __shfl_xor(v[i], o);
+}
+
+// point landmarks: a group of kGroup lanes per landmark, lane j linearises edges j, j+8, ...
+// of the landmark's CSR list; the group sums Hll / bl (no per-edge landmark records)
+__device__ __forceinline__ void lin_point_landmarks(const Problem& P, const Lin& L, const Active& A, const Sys& S,
+                                                    int t) {
+  const int g = t / kGroup, j = t % kGroup;
+  double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bv[3] = {0, 0, 0};
+  const bool in = g < P.nq;
+  if (in) {
+    const int k1 = A.lm_off[g + 1];
+    for (int k = A.lm_off[g] + j; k < k1; k += kGroup) point_edge(P, L, A, A.lm_edges[k], A.lm_pose[k] >= 0, hl, bv);
+  }
+  group_sum(hl);
+  group_sum(bv);
+  if (!in || j != 0 || !A.lm_act[g]) return;
+  double* H = S.Hll + 16 * g;
+#pragma unroll
+  for (int i = 0; i < 9; i++) H[i] = hl[i];
+#pragma unroll
+  for (int i = 9; i < 16; i++) H[i] = 0.0;
+#pragma unroll
+  for (int i = 0; i < 3; i++) S.bl[4 * g + i] = bv[i];
+  S.bl[4 * g + 3] = 0.0;
+  atomic_max_pos(S.out + 2, fmax(fabs(hl[0]), fmax(fabs(hl[4]), fabs(hl[8]))));
+}
+
+// line edges: g2o's numeric central difference (delta 1e-9), one wave per edge, the 20
+// perturbed error evaluations (+-delta on 4 line + 6 pose dims) in parallel lanes.  The
+// landmark-side records are written through (sc1); the last edge of a line landmark to
+// finish (ticket) sums them in CSR order into the landmark block.
+__device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const Active& A, const Sys& S, int blk) {
   __shared__ double ev[4][20][4];
   __shared__ double J[4][4 * 6 + 4 * 4];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = blk * 4 + wv;
-  bool live = i < A.n_line_edges;
+  const bool on = i < A.n_line_edges;
+  bool live = on;
   int e = 0, t = 2, rows = 2;
-  if (live) {
+  bool pose_opt = false;
+  if (on) {
     e = A.edges[A.Ea - A.n_line_edges + i];
     t = P.etype[e];
     rows = edim(t);
-    if (A.elevel && A.elevel[e]) {  // outside this phase: exact-zero records (wave-uniform)
-      const bool po = A.pidx[P.epose[e]] >= 0;
-      for (int o = lane; o < 86; o += 64) store_contrib(L, e, o, 0.0, po);
-      live = false;
-    }
+    pose_opt = A.pidx[P.epose[e]] >= 0;
+    live = !(A.elevel && A.elevel[e]);  // outside this phase: exact-zero records (wave-uniform)
   }
   const int pose = live ? P.epose[e] : 0, g = live ? P.elm[e] : P.nq;
   const double* cam = P.cams + 5 * (live ? P.ecam[e] : 0);
@@ -509,59 +547,45 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
     }
   }
   __syncthreads();
-  if (!live) return;
-  const double w = edge_weight(P, L, A, e, t);
+  if (!on) return;
+  const double w = live ? edge_weight(P, L, A, e, t) : 0.0;
   const double* er = L.err + 4 * e;
-  const bool pose_opt = A.pidx[pose] >= 0;
-  for (int o = lane; o < 86; o += 64) store_contrib(L, e, o, contrib(o, rows, 4, w, er, &J[wv][0], &J[wv][24]), pose_opt);
-}
-// one launch for both edge families: blocks [0, nbp) points (1 edge per thread),
-// blocks [nbp, ...) lines (1 edge per wave)
-__global__ __launch_bounds__(256) void linearize_kernel(Problem P, Lin L, Active A, int nbp) {
-  if ((int)blockIdx.x < nbp) lin_points(P, L, A, blockIdx.x * 256 + threadIdx.x);
-  else lin_lines(P, L, A, blockIdx.x - nbp);
-}
-
-__device__ __forceinline__ void atomic_max_pos(double* addr, double v) {
-  // non-negative doubles order like their bit patterns
-  atomicMax(reinterpret_cast<unsigned long long*>(addr), (unsigned long long)__double_as_longlong(v));
-}
-
-// landmark blocks: Hll = sum_e Hll_e, bl = sum_e bl_e (edge order of the CSR list).
-// Edge ids are fetched 8 at a time (clamped, unconditional) so the record loads of a
-// batch are in flight together instead of one dependent chain per edge.
-__global__ __launch_bounds__(256) void landmark_reduce_kernel(Problem P, Lin L, Active A, Sys S) {
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= A.nL || !A.lm_act[g]) return;
-  const int ld = g < P.nq ? 3 : 4;
-  double H[16] = {0}, b[4] = {0};
-  const int k0 = A.lm_off[g], k1 = A.lm_off[g + 1];
-  for (int kb = k0; kb < k1; kb += 8) {
-    int es[8];
-#pragma unroll
-    for (int u = 0; u < 8; u++) es[u] = A.lm_edges[min(kb + u, k1 - 1)];
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const bool on = kb + u < k1;
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const double v = L.Hll[16 * es[u] + i];
-        H[i] += on ? v : 0.0;
-      }
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        const double v = L.bl[4 * es[u] + i];
-        b[i] += on ? v : 0.0;
-      }
-    }
+  for (int o = lane; o < 86; o += 64) {
+    const double v = live ? contrib(o, rows, 4, w, er, &J[wv][0], &J[wv][24]) : 0.0;
+    if (o < 20)
+      __hip_atomic_store(o < 16 ? L.Hll + 16 * e + o : L.bl + 4 * e + o - 16, v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    else
+      store_contrib(L, e, o, v, pose_opt);
   }
-  double mx = 0;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int gl = P.elm[e], l = gl - P.nq;
+  const int k0 = A.lm_off[gl], k1 = A.lm_off[gl + 1];
+  unsigned tk = 0;
+  if (lane == 0) tk = __hip_atomic_fetch_add(S.lm_ctr + l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  tk = __shfl(tk, 0);
+  if (tk != (unsigned)(k1 - k0 - 1)) return;
+  if (lane == 0) __hip_atomic_store(S.lm_ctr + l, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  double s = 0;
+  if (lane < 20) {
+    const double* base = lane < 16 ? L.Hll + lane : L.bl + (lane - 16);
+    const int str = lane < 16 ? 16 : 4;
+    for (int k = k0; k < k1; k++)
+      s += __hip_atomic_load(base + (size_t)str * A.lm_edges[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (lane < 16) S.Hll[16 * gl + lane] = s;
+    else S.bl[4 * gl + lane - 16] = s;
+  }
+  double m = (lane < 16 && lane % 5 == 0) ? fabs(s) : 0.0;
 #pragma unroll
-  for (int i = 0; i < 16; i++) S.Hll[16 * g + i] = H[i];
-#pragma unroll
-  for (int i = 0; i < 4; i++) S.bl[4 * g + i] = b[i];
-  for (int i = 0; i < ld; i++) mx = fmax(mx, fabs(H[i * ld + i]));
-  atomic_max_pos(S.out + 2, mx);
+  for (int o = 8; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o));
+  if (lane == 0 && A.lm_act[gl]) atomic_max_pos(S.out + 2, m);
+}
+
+// one launch for both landmark families: blocks [0, nbq) point landmarks (kGroup lanes
+// each), blocks [nbq, ...) line edges (one wave each)
+__global__ __launch_bounds__(256) void linearize_kernel(Problem P, Lin L, Active A, Sys S, int nbq) {
+  if ((int)blockIdx.x < nbq) lin_point_landmarks(P, L, A, S, blockIdx.x * 256 + threadIdx.x);
+  else lin_lines(P, L, A, S, blockIdx.x - nbq);
 }
 
 // deterministic block reduction of NV values per thread: wave shuffles, then waves in order
@@ -844,7 +868,7 @@ __device__ __forceinline__ double readlane_f64(double v, int lane) {
   return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
 }
 
-__global__ __launch_bounds__(1024) void schur_solve_kernel(Active A, Sys S, int n, double lambda) {
+__global__ __launch_bounds__(1024) void schur_solve_kernel(Problem P, Active A, Sys S, int n, double lambda) {
   extern __shared__ double Al[];
   __shared__ int bad[1];
   const int ld = n | 1, K = n / 6;
@@ -998,6 +1022,34 @@ __global__ __launch_bounds__(1024) void schur_solve_kernel(Active A, Sys S, int 
   if (lane < n) S.x[lane] = x0;
   if (lane + 64 < n) S.x[lane + 64] = x1;
   if (lane + 128 < n) S.x[lane + 128] = x2;
+  // candidate poses (lane = pose; np <= 64): T <- exp(xp) T, fixed poses copied (ping-pong),
+  // and the pose part of the LM scale x.(lambda x + bp)
+  double sc = 0;
+  const int a = lane < P.np ? A.pidx[lane] : -1;
+  double xp[6];
+#pragma unroll
+  for (int r = 0; r < 6; r++) {  // gather x[6a + r] from the register-resident solution (all lanes shuffle)
+    const int j = 6 * max(a, 0) + r;
+    const double v0 = __shfl(x0, j & 63), v1 = __shfl(x1, j & 63), v2 = __shfl(x2, j & 63);
+    xp[r] = (j >> 6) == 0 ? v0 : ((j >> 6) == 1 ? v1 : v2);
+  }
+  if (lane < P.np) {
+    const double* Tp = P.T + 8 * lane;
+    double* Tq = P.Tn + 8 * lane;
+    if (a >= 0) {
+      const SE3 r = se3_mul(se3_exp(xp), load_T(Tp));
+      for (int k = 0; k < 4; k++) Tq[k] = r.q[k];
+      for (int k = 0; k < 3; k++) Tq[4 + k] = r.t[k];
+      Tq[7] = 0;
+#pragma unroll
+      for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + S.bp[6 * a + k]);
+    } else {
+      for (int k = 0; k < 8; k++) Tq[k] = Tp[k];
+    }
+  }
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
+  if (lane == 0) S.out[4] = sc;
 }
 
 
@@ -1132,6 +1184,133 @@ __global__ __launch_bounds__(256) void update_kernel(Problem P, Lin L, Active A,
   if (threadIdx.x == 0) S.partial2[blockIdx.x] = s;
 }
 
+// Fast-path trial tail (after schur_solve has written the candidate poses and the pose
+// part of the scale): per landmark a group of kGroup lanes does the back-substitution
+// xl = Dinv (bl - sum_e Hpl_e^T xp) (edges split over the lanes, group sum), the candidate
+// landmark (points += xl, lines oplus; copied when inactive: ping-pong), the scale term, and
+// then the robust cost of the landmark's edges against the candidate poses.  The last block
+// (ticket) sums the block partials in order and posts {chi2, scale, maxdiag, fail} + seq.
+__global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Active A, Sys S, double lambda,
+                                                            unsigned long long seq) {
+  __shared__ double red[4 * 2];
+  __shared__ int last;
+  const int t = blockIdx.x * 256 + threadIdx.x, g = t / kGroup, j = t % kGroup;
+  const bool failed = *S.fail != 0;
+  const bool in = g < A.nL;
+  const bool point = g < P.nq;
+  int k0 = 0, k1 = 0;
+  if (in) {
+    k0 = A.lm_off[g];
+    k1 = A.lm_off[g + 1];
+  }
+  const bool upd = in && A.lm_act[g] && !failed;
+  double c[4] = {0, 0, 0, 0};
+  if (upd)
+    for (int k = k0 + j; k < k1; k += kGroup) {
+      const int a = A.lm_pose[k];
+      if (a < 0) continue;
+      const double* B = L.Hpl + 24 * A.lm_edges[k];
+      const double* xp = S.x + 6 * a;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        double s = 0;
+#pragma unroll
+        for (int r = 0; r < 6; r++) s += B[r * 4 + q] * xp[r];
+        c[q] -= s;
+      }
+    }
+  group_sum(c);
+  double xl[4] = {0, 0, 0, 0};
+  double sc = 0, chi = 0;
+  if (upd) {
+    double bl[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      bl[q] = S.bl[4 * g + q];
+      c[q] += bl[q];
+    }
+    double D[16];
+    const bool ok = lm_dinv(S.Hll + 16 * g, point, lambda, D);
+    if (!ok && j == 0) atomicOr(S.fail, 1);
+#pragma unroll
+    for (int r = 0; r < 4; r++) xl[r] = D[r * 4] * c[0] + D[r * 4 + 1] * c[1] + D[r * 4 + 2] * c[2] + D[r * 4 + 3] * c[3];
+    if (j == 0)
+#pragma unroll
+      for (int q = 0; q < 4; q++) sc += xl[q] * (lambda * xl[q] + bl[q]);
+  }
+  if (in) {
+    double lm[6];
+    if (point) {
+#pragma unroll
+      for (int q = 0; q < 3; q++) lm[q] = P.X[3 * g + q] + xl[q];
+      if (j == 0)
+#pragma unroll
+        for (int q = 0; q < 3; q++) P.Xn[3 * g + q] = lm[q];
+    } else {
+      const int l = g - P.nq;
+#pragma unroll
+      for (int q = 0; q < 6; q++) lm[q] = P.L[6 * l + q];
+      if (upd) line_oplus(lm, xl);
+      if (j == 0)
+#pragma unroll
+        for (int q = 0; q < 6; q++) P.Ln[6 * l + q] = lm[q];
+    }
+    for (int k = k0 + j; k < k1; k += kGroup) {
+      const int e = A.lm_edges[k];
+      if (A.elevel && A.elevel[e]) continue;
+      const int te = P.etype[e];
+      const SE3 T = load_T(P.Tn + 8 * P.epose[e]);
+      double er[4] = {0, 0, 0, 0};
+      edge_error(te, P.cams + 5 * P.ecam[e], P.eobs + 8 * e, T, lm, er);
+      double chi2 = 0;
+      for (int q = 0; q < edim(te); q++) chi2 += er[q] * er[q];
+      chi2 *= einfo(te);
+#pragma unroll
+      for (int q = 0; q < 4; q++) L.err[4 * e + q] = er[q];
+      double cst = chi2;
+      if (A.robust) {
+        double r1;
+        huber(chi2, P.delta[te], cst, r1);
+      }
+      L.rho0[e] = cst;
+      chi += cst;
+    }
+  }
+  double acc[2] = {chi, sc};
+  block_reduce<2>(acc, red);
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(S.partial + blockIdx.x, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(S.partial2 + blockIdx.x, red[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned tk = __hip_atomic_fetch_add(S.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = tk == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  double f2[2] = {0, 0};
+  for (int k = threadIdx.x; k < (int)gridDim.x; k += 256) {
+    f2[0] += __hip_atomic_load(S.partial + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    f2[1] += __hip_atomic_load(S.partial2 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  block_reduce<2>(f2, red);
+  if (threadIdx.x == 0) {
+    const double chi2 = red[0], scale = red[1] + S.out[4];
+    const double f = (double)__hip_atomic_load(S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const double mx = S.out[2];
+    S.out[0] = chi2;
+    S.out[1] = scale;
+    S.out[3] = f;
+    Mail* m = S.mail;
+    m->v[0] = chi2;
+    m->v[1] = scale;
+    m->v[2] = mx;
+    m->v[3] = f;
+    __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(S.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    S.out[2] = 0.0;
+    __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 __global__ __launch_bounds__(256) void landmark_active_kernel(Active A, const uint8_t* level, uint8_t* lm_act) {
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= A.nL) return;
@@ -1177,16 +1356,12 @@ hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& 
   return hipGetLastError();
 }
 
-hipError_t linearize(const Problem& P, const Lin& L, const Active& A, hipStream_t s) {
-  const int npt = A.Ea - A.n_line_edges;
-  const int nbp = (npt + 255) / 256, nbl = (A.n_line_edges + 3) / 4;
-  if (nbp + nbl > 0) hipLaunchKernelGGL(linearize_kernel, dim3(nbp + nbl), dim3(256), 0, s, P, L, A, nbp);
-  return hipGetLastError();
-}
+int update_errors_blocks(const Active& A) { return A.nL > 0 ? (A.nL * kGroup + 255) / 256 : 1; }
 
-hipError_t reduce_blocks(const Problem& P, const Lin& L, const Active& A, Sys& S, bool with_maxdiag,
-                         hipStream_t s) {
-  if (A.nL > 0) hipLaunchKernelGGL(landmark_reduce_kernel, dim3((A.nL + 255) / 256), dim3(256), 0, s, P, L, A, S);
+hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool with_maxdiag,
+                     hipStream_t s) {
+  const int nbq = (P.nq * kGroup + 255) / 256, nbl = (A.n_line_edges + 3) / 4;
+  if (nbq + nbl > 0) hipLaunchKernelGGL(linearize_kernel, dim3(nbq + nbl), dim3(256), 0, s, P, L, A, S, nbq);
   if (with_maxdiag && A.K > 0) hipLaunchKernelGGL(pose_diag_kernel, dim3(A.K), dim3(256), 0, s, P, L, A, S);
   return hipGetLastError();
 }
@@ -1211,8 +1386,11 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
       attr = true;
     }
     const size_t bytes = sizeof(double) * ((size_t)n * (n | 1) + 3 * n + 15 * (n / 6));
-    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(1024), bytes, s, A, S, n, lambda);
-  } else if (n > 0) {
+    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(1024), bytes, s, P, A, S, n, lambda);
+    hipLaunchKernelGGL(update_errors_kernel, dim3(update_errors_blocks(A)), dim3(256), 0, s, P, L, A, S, lambda, seq);
+    return hipGetLastError();
+  }
+  if (n > 0) {  // larger systems: Schur sums + global-memory Cholesky
     hipLaunchKernelGGL(pair_final_kernel, dim3((A.npairs * 42 + 255) / 256), dim3(256), 0, s, A, S, lambda);
     hipLaunchKernelGGL(cholesky_kernel, dim3(1), dim3(256), 0, s, S, n);
   }

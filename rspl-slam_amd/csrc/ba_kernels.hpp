@@ -82,6 +82,7 @@ struct Sys {
   double* out;           // [8]: 0 chi2, 1 scale, 2 maxdiag, 3 fail
   int* fail;             // [1]
   unsigned* counter;     // [1] last-block ticket of the error kernel
+  unsigned* lm_ctr;      // [nl] line-landmark tickets of the linearisation (re-armed to 0 by the last edge)
   Mail* mail;            // device view of the mailbox
 };
 
@@ -90,9 +91,9 @@ constexpr int kChunk = 128;  // edge pairs per Schur chunk (2 per lane)
 // errors (+ fused final reduction and mailbox post with sequence number seq)
 hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq,
                           hipStream_t s);
-hipError_t linearize(const Problem& P, const Lin& L, const Active& A, hipStream_t s);
-hipError_t reduce_blocks(const Problem& P, const Lin& L, const Active& A, Sys& S, bool with_maxdiag,
-                         hipStream_t s);
+// edge Jacobians + landmark blocks S.Hll / S.bl (+ max diagonal; pose blocks too when with_maxdiag)
+hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool with_maxdiag,
+                     hipStream_t s);
 hipError_t post(Sys& S, unsigned long long seq, hipStream_t s);
 // one LM trial: Schur complement, Cholesky, back-substitution + candidate state, its cost
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
@@ -103,6 +104,7 @@ hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8
                     hipStream_t s);
 int update_blocks(const Problem& P);
 int errors_blocks(int Ea);
+int update_errors_blocks(const Active& A);
 
 }  // namespace ba
 }  // namespace rspl
