@@ -30,22 +30,26 @@ struct rspl_ba {
   hipStream_t stream = nullptr;
   Arena arena;
   int maxE = 0, maxL = 0, maxK = 0, maxV = 0;
-  // problem (T/X/L current state, Tb/Xb/Lb the candidate: ping-pong)
-  double *cams, *T, *Tb, *X, *Xb, *L, *Lb, *eobs;
-  int8_t* etype;
-  int *epose, *elm, *ecam;
+  // candidate state (ping-pong partners of the call buffer's T / X / L)
+  double *Tb, *Xb, *Lb;
   // per-edge linearisation records
   double *err, *rho0, *Hpp_e, *bp_e, *Hll_e, *bl_e, *Hpl_e;
-  uint8_t *level, *inlier, *lm_act2;
+  uint8_t* lm_act2;
   // system
-  double *Hll, *bl, *bp, *S, *x, *partial, *partial2, *out;
-  int* flags;  // [0] fail, [1] error-kernel ticket counter
+  double *Hll, *bl, *bp, *S, *x, *partial, *partial2;
   unsigned* lm_ctr;  // [max_lines] line-landmark tickets (zeroed at create, re-armed by the kernel)
-  // per-phase active structure + Schur chunk partials (growable device buffer)
+  // per-call inputs (cameras, T / X / L, edges, zeroed level / flags / out), laid out exactly
+  // like the staging buffer's call region: one upload per call (capacity fixed at create)
+  char* cbuf = nullptr;
+  // active structure of a phase: landmark CSR / pose lists (phase_buf), pose pairs + Schur
+  // chunks (pair_buf); growable device buffers
   char* phase_buf = nullptr;
   size_t phase_cap = 0;
-  // pinned host staging for uploads / downloads
+  char* pair_buf = nullptr;
+  size_t pair_cap = 0;
+  // pinned, host-mapped staging for uploads; the final kernel writes results straight into it
   char* stage = nullptr;
+  char* stage_dev = nullptr;
   size_t stage_cap = 0;
   // host-mapped mailbox
   ba::Mail* mail = nullptr;
@@ -63,6 +67,33 @@ constexpr int kMaxCams = 16;
 
 inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
+// per-call upload layout (staging call region == device call buffer)
+struct CallLayout {
+  size_t cams, T, X, L, obs, type, pose, lm, cam, level, flags, out, bytes;
+  CallLayout(int ncam, int np, int nq, int nl, int E) {
+    size_t so = 0;
+    auto place = [&](size_t n) {
+      const size_t o = so;
+      so = al256(so + n);
+      return o;
+    };
+    cams = place(sizeof(double) * 5 * ncam); T = place(sizeof(double) * 8 * np); X = place(sizeof(double) * 3 * nq);
+    L = place(sizeof(double) * 6 * nl); obs = place(sizeof(double) * 8 * (size_t)E); type = place(E);
+    pose = place(4 * (size_t)E); lm = place(4 * (size_t)E); cam = place(4 * (size_t)E); level = place(E);
+    flags = place(4 * sizeof(int)); out = place(8 * sizeof(double));
+    bytes = so;
+  }
+};
+
+// result layout written by the final kernel into the mapped staging buffer
+struct DownLayout {
+  size_t inl, T, X, L, bytes;
+  DownLayout(int np, int nq, int nl, int E) {
+    inl = 0; T = al256(E); X = T + al256(sizeof(double) * 8 * np); L = X + al256(sizeof(double) * 3 * nq);
+    bytes = L + al256(sizeof(double) * 6 * nl);
+  }
+};
+
 template <typename F>
 void carve(F& ar, rspl_ba* b) {
   const size_t E = b->maxE, NL = b->maxL, K = b->maxK, nq = b->cfg.max_points, nl = b->cfg.max_lines;
@@ -71,19 +102,15 @@ void carve(F& ar, rspl_ba* b) {
     if constexpr (std::is_same_v<F, Arena>) p = ar.template take<Tp>(n ? n : 1);
     else ar.template take<Tp>(n ? n : 1);
   };
-  take(b->cams, kMaxCams * 5);
-  take(b->T, K * 8); take(b->Tb, K * 8);
-  take(b->X, nq * 3); take(b->Xb, nq * 3);
-  take(b->L, nl * 6); take(b->Lb, nl * 6);
-  take(b->eobs, E * 8); take(b->etype, E); take(b->epose, E); take(b->elm, E); take(b->ecam, E);
+  take(b->Tb, K * 8); take(b->Xb, nq * 3); take(b->Lb, nl * 6);
   take(b->err, E * 4); take(b->rho0, E); take(b->Hpp_e, E * 36); take(b->bp_e, E * 6); take(b->Hll_e, E * 16);
   take(b->bl_e, E * 4); take(b->Hpl_e, E * 24);
-  take(b->level, E); take(b->inlier, E); take(b->lm_act2, NL);
+  take(b->lm_act2, NL);
   take(b->Hll, NL * 16); take(b->bl, NL * 4); take(b->bp, K * 6);
   // block partials: edge-per-thread kernels (E / 256) and landmark-group kernels (NL * 8 / 256)
   const size_t nblk = std::max(E / 256, NL * 8 / 256) + 2;
   take(b->S, 36 * K * K); take(b->x, 6 * K); take(b->partial, nblk);
-  take(b->partial2, std::max((size_t)b->maxV / 256, nblk) + 2); take(b->out, 8); take(b->flags, 4);
+  take(b->partial2, std::max((size_t)b->maxV / 256, nblk) + 2);
   take(b->lm_ctr, nl);
 }
 
@@ -95,20 +122,21 @@ int ensure_stage(rspl_ba* b, size_t bytes) {
   b->stage = nullptr;
   const size_t cap = std::max(bytes, b->stage_cap * 2);
   b->stage_cap = 0;
-  RSPL_HIP(hipHostMalloc((void**)&b->stage, cap, hipHostMallocDefault));
+  RSPL_HIP(hipHostMalloc((void**)&b->stage, cap, hipHostMallocMapped | hipHostMallocCoherent));
+  RSPL_HIP(hipHostGetDevicePointer((void**)&b->stage_dev, b->stage, 0));
   b->stage_cap = cap;
   return RSPL_OK;
 }
 
-int ensure_phase(rspl_ba* b, size_t bytes) {
-  if (bytes <= b->phase_cap) return RSPL_OK;
-  RSPL_HIP(hipStreamSynchronize(b->stream));
-  if (b->phase_buf) (void)hipFree(b->phase_buf);
-  b->phase_buf = nullptr;
-  const size_t cap = std::max(bytes, b->phase_cap * 2);
-  b->phase_cap = 0;
-  RSPL_HIP(hipMalloc((void**)&b->phase_buf, cap));
-  b->phase_cap = cap;
+int ensure_dev(rspl_ba* b, char*& buf, size_t& cap, size_t bytes) {
+  if (bytes <= cap) return RSPL_OK;
+  RSPL_HIP(hipStreamSynchronize(b->stream));  // kernels may still read the old buffer
+  if (buf) (void)hipFree(buf);
+  buf = nullptr;
+  const size_t nc = std::max(bytes, cap * 2);
+  cap = 0;
+  RSPL_HIP(hipMalloc((void**)&buf, nc));
+  cap = nc;
   return RSPL_OK;
 }
 
@@ -175,72 +203,51 @@ Se3h inverse(const Se3h& T) {  // SE3Quat::inverse
   return r;
 }
 
-// Host-side construction of one phase's active structure (CSR lists, pose pairs, Schur
-// chunks): counting sorts over the landmark CSR, written straight into the pinned staging
-// buffer at `soff` and uploaded with one async copy.
-int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>& epose, const std::vector<int>& elm,
-                 const std::vector<int8_t>& etype, const uint8_t* fixed, int np, int nL, int robust, size_t soff,
-                 ba::Active& A, ba::Sys& S) {
+// Host-side construction of one phase's active structure, in two parts so the second
+// overlaps the GPU's first cost evaluation + linearisation:
+//   build_csr:   reduced pose ids, landmark CSR (edges in input order within a landmark),
+//                per-pose edge lists -- everything the cost / linearisation kernels read;
+//   build_pairs: pose pairs, per-pair edge pairs (landmark order), Schur chunks -- read only
+//                by the trials.
+// Each part is written straight into the pinned staging buffer at `soff` and uploaded
+// with one async copy.  Returns the staging bytes used in *sbytes.
+// staging bytes build_csr can need (so the call region it reads is never reallocated under it)
+size_t csr_bytes_bound(int E, int np, int nL) {
+  return 4 * (size_t)E * 4 + 4 * (size_t)np * 2 + 5 * (size_t)(nL + 1) + 8 + 8 * 256;
+}
+
+int build_csr(rspl_ba* b, const std::vector<int>& act, const int* epose, const int* elm, const int8_t* etype,
+              const uint8_t* fixed, int np, int nL, int robust, size_t soff, size_t* sbytes, ba::Active& A) {
   auto& w = b->ws;
   const int Ea = (int)act.size();
-  static const bool btiming = getenv("RSPL_BA_TIMING") != nullptr;
-  std::chrono::steady_clock::time_point bt[5];
-  int nbt = 0;
-  auto bmark = [&]() {
-    if (btiming) bt[nbt++] = std::chrono::steady_clock::now();
-  };
-  bmark();
   w.pidx.assign(np, -1);
   w.lact.assign(nL, 0);
-  {
-    w.pact.assign(np, 0);
-    for (int e : act) {
-      w.pact[epose[e]] = 1;
-      w.lact[elm[e]] = 1;
-    }
+  w.pact.assign(np, 0);
+  for (int e : act) {
+    w.pact[epose[e]] = 1;
+    w.lact[elm[e]] = 1;
   }
   int K = 0;
   for (int p = 0; p < np; p++)
     if (w.pact[p] && !fixed[p]) w.pidx[p] = K++;
-  // landmark CSR (edges in input order within a landmark)
   w.lm_off.assign(nL + 1, 0);
   for (int e : act) w.lm_off[elm[e] + 1]++;
   for (int g = 0; g < nL; g++) w.lm_off[g + 1] += w.lm_off[g];
   w.lm_edges.resize(Ea);
   w.lm_pose.resize(Ea);
-  {
-    w.fill.assign(w.lm_off.begin(), w.lm_off.end() - 1);
-    for (int e : act) {
-      const int k = w.fill[elm[e]]++;
-      w.lm_edges[k] = e;
-      w.lm_pose[k] = w.pidx[epose[e]];
-    }
-  }
-  bmark();
-  // counts: edges per reduced pose, edge pairs per pose pair (a <= c)
-  const int npairs = K * (K + 1) / 2;
-  auto pid = [K](int a, int c) { return a * K - a * (a - 1) / 2 + (c - a); };
+  w.fill.assign(w.lm_off.begin(), w.lm_off.end() - 1);
   w.ps_cnt.assign(K + 1, 0);
-  w.pp_cnt.assign(npairs + 1, 0);
-  for (int g = 0; g < nL; g++) {
-    const int k0 = w.lm_off[g], k1 = w.lm_off[g + 1];
-    for (int i = k0; i < k1; i++) {
-      const int ai = w.lm_pose[i];
-      if (ai < 0) continue;
-      w.ps_cnt[ai + 1]++;
-      for (int j = k0; j < k1; j++) {
-        const int aj = w.lm_pose[j];
-        if (aj >= ai) w.pp_cnt[pid(ai, aj) + 1]++;
-      }
-    }
+  int n_line_edges = 0;
+  for (int e : act) {
+    const int k = w.fill[elm[e]]++;
+    const int a = w.pidx[epose[e]];
+    w.lm_edges[k] = e;
+    w.lm_pose[k] = a;
+    if (a >= 0) w.ps_cnt[a + 1]++;
+    n_line_edges += etype[e] >= 2;
   }
   for (int a = 0; a < K; a++) w.ps_cnt[a + 1] += w.ps_cnt[a];
-  int nch = 0;
-  for (int p = 0; p < npairs; p++) nch += (w.pp_cnt[p + 1] + ba::kChunk - 1) / ba::kChunk;
-  for (int p = 0; p < npairs; p++) w.pp_cnt[p + 1] += w.pp_cnt[p];
-  const int npp = w.pp_cnt[npairs], nps = w.ps_cnt[K];
-  bmark();
-  // layout (identical in staging and device buffer)
+  const int nps = w.ps_cnt[K];
   size_t off = 0;
   auto place = [&](size_t bytes) {
     const size_t o = off;
@@ -249,19 +256,11 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
   };
   const size_t o_act = place(4 * (size_t)Ea), o_pidx = place(4 * (size_t)np), o_lmoff = place(4 * (size_t)(nL + 1)),
                o_lme = place(4 * (size_t)Ea), o_lmp = place(4 * (size_t)Ea), o_lact = place(nL),
-               o_psoff = place(4 * (size_t)(K + 1)), o_pse = place(4 * (size_t)nps),
-               o_pairs = place(8 * (size_t)npairs), o_choff = place(4 * (size_t)(npairs + 1)),
-               o_chb = place(4 * (size_t)nch), o_che = place(4 * (size_t)nch), o_chp = place(4 * (size_t)nch), o_e1 = place(4 * (size_t)npp),
-               o_e2 = place(4 * (size_t)npp);
-  const size_t upload = off;
-  const size_t o_chunk = place(sizeof(double) * 48 * (size_t)std::max(nch, 1));
-  const size_t o_pfin = place(sizeof(double) * 48 * (size_t)std::max(npairs, 1));
-  const size_t o_pctr = place(sizeof(unsigned) * (size_t)std::max(npairs, 1));
+               o_psoff = place(4 * (size_t)(K + 1)), o_pse = place(4 * (size_t)nps);
   int rc;
-  if ((rc = ensure_phase(b, off))) return rc;
-  if ((rc = ensure_stage(b, soff + upload))) return rc;
+  if ((rc = ensure_dev(b, b->phase_buf, b->phase_cap, off))) return rc;
+  if ((rc = ensure_stage(b, soff + off))) return rc;
   char* st = b->stage + soff;
-  auto I = [&](size_t o) { return reinterpret_cast<int*>(st + o); };
   if (Ea) memcpy(st + o_act, act.data(), 4 * (size_t)Ea);
   if (np) memcpy(st + o_pidx, w.pidx.data(), 4 * (size_t)np);
   memcpy(st + o_lmoff, w.lm_off.data(), 4 * (size_t)(nL + 1));
@@ -271,6 +270,64 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
   }
   if (nL) memcpy(st + o_lact, w.lact.data(), nL);
   memcpy(st + o_psoff, w.ps_cnt.data(), 4 * (size_t)(K + 1));
+  {  // per-pose edge lists in landmark order
+    int* pse = reinterpret_cast<int*>(st + o_pse);
+    w.fill.assign(w.ps_cnt.begin(), w.ps_cnt.end() - 1);
+    for (int k = 0; k < Ea; k++)
+      if (w.lm_pose[k] >= 0) pse[w.fill[w.lm_pose[k]]++] = w.lm_edges[k];
+  }
+  RSPL_HIP(hipMemcpyAsync(b->phase_buf, st, off, hipMemcpyHostToDevice, b->stream));
+  auto dptr = [&](size_t o) { return reinterpret_cast<const int*>(b->phase_buf + o); };
+  A.edges = dptr(o_act); A.Ea = Ea; A.pidx = dptr(o_pidx); A.lm_off = dptr(o_lmoff);
+  A.lm_edges = dptr(o_lme); A.lm_pose = dptr(o_lmp);
+  A.lm_act = reinterpret_cast<const uint8_t*>(b->phase_buf + o_lact);
+  A.ps_off = dptr(o_psoff); A.ps_edges = dptr(o_pse);
+  A.n_line_edges = n_line_edges; A.nL = nL; A.robust = robust; A.K = K;
+  A.npairs = 0; A.nch = 0;
+  *sbytes = off;
+  return RSPL_OK;
+}
+
+int build_pairs(rspl_ba* b, int nL, size_t soff, ba::Active& A, ba::Sys& S) {
+  auto& w = b->ws;
+  const int K = A.K;
+  const int npairs = K * (K + 1) / 2;
+  auto pid = [K](int a, int c) { return a * K - a * (a - 1) / 2 + (c - a); };
+  // edge pairs per pose pair (a <= c)
+  w.pp_cnt.assign(npairs + 1, 0);
+  for (int g = 0; g < nL; g++) {
+    const int k0 = w.lm_off[g], k1 = w.lm_off[g + 1];
+    for (int i = k0; i < k1; i++) {
+      const int ai = w.lm_pose[i];
+      if (ai < 0) continue;
+      for (int j = k0; j < k1; j++) {
+        const int aj = w.lm_pose[j];
+        if (aj >= ai) w.pp_cnt[pid(ai, aj) + 1]++;
+      }
+    }
+  }
+  int nch = 0;
+  for (int p = 0; p < npairs; p++) nch += (w.pp_cnt[p + 1] + ba::kChunk - 1) / ba::kChunk;
+  for (int p = 0; p < npairs; p++) w.pp_cnt[p + 1] += w.pp_cnt[p];
+  const int npp = w.pp_cnt[npairs];
+  size_t off = 0;
+  auto place = [&](size_t bytes) {
+    const size_t o = off;
+    off = al256(off + bytes);
+    return o;
+  };
+  const size_t o_pairs = place(8 * (size_t)npairs), o_choff = place(4 * (size_t)(npairs + 1)),
+               o_chb = place(4 * (size_t)nch), o_che = place(4 * (size_t)nch), o_chp = place(4 * (size_t)nch),
+               o_e1 = place(4 * (size_t)npp), o_e2 = place(4 * (size_t)npp),
+               o_pctr = place(sizeof(unsigned) * (size_t)std::max(npairs, 1));  // uploaded as zeros
+  const size_t upload = off;
+  const size_t o_chunk = place(sizeof(double) * 48 * (size_t)std::max(nch, 1));
+  const size_t o_pfin = place(sizeof(double) * 48 * (size_t)std::max(npairs, 1));
+  int rc;
+  if ((rc = ensure_dev(b, b->pair_buf, b->pair_cap, off))) return rc;
+  if ((rc = ensure_stage(b, soff + upload))) return rc;
+  char* st = b->stage + soff;
+  auto I = [&](size_t o) { return reinterpret_cast<int*>(st + o); };
   {
     int* pairs = I(o_pairs);
     int* choff = I(o_choff);
@@ -283,27 +340,24 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
         pairs[2 * p] = a;
         pairs[2 * p + 1] = cc;
         choff[p] = c;
-        for (int s = w.pp_cnt[p]; s < w.pp_cnt[p + 1]; s += ba::kChunk, c++) {
-          chb[c] = s;
-          che[c] = std::min(s + ba::kChunk, w.pp_cnt[p + 1]);
+        for (int s2 = w.pp_cnt[p]; s2 < w.pp_cnt[p + 1]; s2 += ba::kChunk, c++) {
+          chb[c] = s2;
+          che[c] = std::min(s2 + ba::kChunk, w.pp_cnt[p + 1]);
           chp[c] = p;
         }
       }
     choff[npairs] = c;
+    memset(st + o_pctr, 0, sizeof(unsigned) * (size_t)std::max(npairs, 1));
   }
-  bmark();
-  {  // fills in landmark order: per-pose edge lists and per-pair edge pairs come out landmark-sorted
-    int* pse = I(o_pse);
+  {  // fills in landmark order: per-pair edge pairs come out landmark-sorted
     int* e1 = I(o_e1);
     int* e2 = I(o_e2);
-    w.fill.assign(w.ps_cnt.begin(), w.ps_cnt.end() - 1);
     w.fill2.assign(w.pp_cnt.begin(), w.pp_cnt.end() - 1);
     for (int g = 0; g < nL; g++) {
       const int k0 = w.lm_off[g], k1 = w.lm_off[g + 1];
       for (int i = k0; i < k1; i++) {
         const int ai = w.lm_pose[i];
         if (ai < 0) continue;
-        pse[w.fill[ai]++] = w.lm_edges[i];
         for (int j = k0; j < k1; j++) {
           const int aj = w.lm_pose[j];
           if (aj < ai) continue;
@@ -314,53 +368,41 @@ int build_active(rspl_ba* b, const std::vector<int>& act, const std::vector<int>
       }
     }
   }
-  int n_line_edges = 0;
-  for (int e : act)
-    if (etype[e] >= 2) n_line_edges++;
-  RSPL_HIP(hipMemcpyAsync(b->phase_buf, st, upload, hipMemcpyHostToDevice, b->stream));
-  bmark();
-  if (btiming && nbt == 5) {
-    auto us = [&](int i) { return std::chrono::duration<double, std::micro>(bt[i + 1] - bt[i]).count(); };
-    fprintf(stderr, "build_active us: csr %.0f counts %.0f layout+copies %.0f fill+upload %.0f (Ea %d pairs %d npp %d)\n",
-            us(0), us(1), us(2), us(3), Ea, npairs, npp);
-  }
-  auto dptr = [&](size_t o) { return reinterpret_cast<const int*>(b->phase_buf + o); };
-  A.edges = dptr(o_act); A.Ea = Ea; A.pidx = dptr(o_pidx); A.lm_off = dptr(o_lmoff);
-  A.lm_edges = dptr(o_lme); A.lm_pose = dptr(o_lmp);
-  A.lm_act = reinterpret_cast<const uint8_t*>(b->phase_buf + o_lact);
-  A.ps_off = dptr(o_psoff); A.ps_edges = dptr(o_pse); A.pairs = dptr(o_pairs); A.npairs = npairs;
+  RSPL_HIP(hipMemcpyAsync(b->pair_buf, st, upload, hipMemcpyHostToDevice, b->stream));
+  auto dptr = [&](size_t o) { return reinterpret_cast<const int*>(b->pair_buf + o); };
+  A.pairs = dptr(o_pairs); A.npairs = npairs;
   A.pair_choff = dptr(o_choff); A.ch_beg = dptr(o_chb); A.ch_end = dptr(o_che); A.ch_pair = dptr(o_chp);
   A.nch = nch;
-  A.pp_e1 = dptr(o_e1); A.pp_e2 = dptr(o_e2); A.n_line_edges = n_line_edges; A.nL = nL; A.robust = robust;
-  A.K = K;
-  S.chunk = reinterpret_cast<double*>(b->phase_buf + o_chunk);
-  S.pairfin = reinterpret_cast<double*>(b->phase_buf + o_pfin);
-  S.pair_ctr = reinterpret_cast<unsigned*>(b->phase_buf + o_pctr);
-  RSPL_HIP(hipMemsetAsync(S.pair_ctr, 0, sizeof(unsigned) * (size_t)std::max(npairs, 1), b->stream));
+  A.pp_e1 = dptr(o_e1); A.pp_e2 = dptr(o_e2);
+  S.chunk = reinterpret_cast<double*>(b->pair_buf + o_chunk);
+  S.pairfin = reinterpret_cast<double*>(b->pair_buf + o_pfin);
+  S.pair_ctr = reinterpret_cast<unsigned*>(b->pair_buf + o_pctr);
   return RSPL_OK;
 }
 
 // one g2o SparseOptimizer::optimize(iters) with OptimizationAlgorithmLevenberg
+// `overlap` (optional) runs on the host while the GPU evaluates the initial cost and the
+// first linearisation; it must be done before the first trial (it builds the pair lists).
+template <typename F>
 int optimize(rspl_ba* b, ba::Problem& P, const ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
-             double* chi2_out, int* done_out) {
+             double* chi2_out, int* done_out, F&& overlap) {
   hipStream_t st = b->stream;
   double v[4];
   int rc;
   unsigned long long q = ++b->seq;
   RSPL_HIP(ba::compute_errors(P, Lr, A, S, q, st));
+  if (iters > 0) {  // the first linearisation does not depend on the cost: queue it right behind
+    RSPL_HIP(ba::linearize(P, Lr, A, S, true, st));
+    q = ++b->seq;
+    RSPL_HIP(ba::post(S, q, st));  // posts chi2 (S.out[0]) and the max diagonal (S.out[2])
+  }
+  if ((rc = overlap())) return rc;
   if ((rc = wait_mail(b, q, v))) return rc;
   double currentChi = v[0];
-  double lambda = 0, ni = 2;
+  double lambda = 1e-5 * v[2], ni = 2;  // computeLambdaInit: tau * max diagonal
   int done = 0;
   for (int it = 0; it < iters; it++) {
-    RSPL_HIP(ba::linearize(P, Lr, A, S, it == 0, st));
-    if (it == 0) {
-      q = ++b->seq;
-      RSPL_HIP(ba::post(S, q, st));
-      if ((rc = wait_mail(b, q, v))) return rc;
-      lambda = 1e-5 * v[2];  // computeLambdaInit: tau * max diagonal
-      ni = 2;
-    }
+    if (it > 0) RSPL_HIP(ba::linearize(P, Lr, A, S, false, st));
     double rho = 0;
     int qmax = 0;
     do {
@@ -424,7 +466,8 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
   if (hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipHostMalloc((void**)&b->mail, sizeof(ba::Mail), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&b->mail_dev, b->mail, 0) != hipSuccess ||
-      hipMemset(b->flags, 0, 4 * sizeof(int)) != hipSuccess || hipMemset(b->out, 0, 8 * sizeof(double)) != hipSuccess ||
+      hipMalloc((void**)&b->cbuf, CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE).bytes) !=
+          hipSuccess ||
       hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess) {
     set_error("BA stream / mailbox allocation failed");
     rspl_ba_destroy(b);
@@ -440,6 +483,8 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
   if (b->stream) (void)hipStreamSynchronize(b->stream);
   b->arena.release();
   if (b->phase_buf) (void)hipFree(b->phase_buf);
+  if (b->pair_buf) (void)hipFree(b->pair_buf);
+  if (b->cbuf) (void)hipFree(b->cbuf);
   if (b->stage) (void)hipHostFree(b->stage);
   if (b->mail) (void)hipHostFree(b->mail);
   if (b->stream) (void)hipStreamDestroy(b->stream);
@@ -468,8 +513,15 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
     if (timing) tmark[ntm++] = clk::now();
   };
   mark();
-  // ---- vertices: VertexSE3Expmap estimate = SE3Quat(q, p).inverse() (g2o_optimization.cc:42) ----
-  std::vector<double> T(8 * (size_t)np);
+  // ---- one staging region for the whole call, mirrored by the device call buffer ----
+  const CallLayout cl(pr->n_cameras, np, nq, nl, E);
+  const DownLayout dl(np, nq, nl, E);
+  int rc;
+  const size_t soff1 = al256(std::max(cl.bytes, dl.bytes));
+  if ((rc = ensure_stage(b, soff1 + csr_bytes_bound(E, np, nL)))) return rc;
+  char* sg = b->stage;
+  // vertices: VertexSE3Expmap estimate = SE3Quat(q, p).inverse() (g2o_optimization.cc:42)
+  double* T = reinterpret_cast<double*>(sg + cl.T);
   for (int p = 0; p < np; p++) {
     Se3h Twc;
     Twc.q[0] = pr->pose_q[4 * p + 3];
@@ -483,35 +535,21 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
     for (int k = 0; k < 3; k++) T[8 * p + 4 + k] = Tcw.t[k];
     T[8 * p + 7] = 0;
   }
-  // ---- edges (unified, input order) ----
-  std::vector<int8_t> etype(E);
-  std::vector<int> epose(E), elm(E), ecam(E);
+  // edges (unified, input order), written straight into the staging region
   const int32_t* poses[4] = {pr->mono_pose, pr->stereo_pose, pr->mono_line_pose, pr->stereo_line_pose};
   const int32_t* lms[4] = {pr->mono_point, pr->stereo_point, pr->mono_line_line, pr->stereo_line_line};
   const int32_t* cams[4] = {pr->mono_camera, pr->stereo_camera, pr->mono_line_camera, pr->stereo_line_camera};
   const double* obs[4] = {pr->mono_obs, pr->stereo_obs, pr->mono_line_obs, pr->stereo_line_obs};
   const int od[4] = {2, 3, 4, 8};
-  // staging layout of the call's uploads
-  size_t so = 0;
-  auto place = [&](size_t bytes) {
-    const size_t o = so;
-    so = al256(so + bytes);
-    return o;
-  };
-  const size_t o_cams = place(sizeof(double) * 5 * pr->n_cameras), o_T = place(sizeof(double) * 8 * np),
-               o_X = place(sizeof(double) * 3 * nq), o_L = place(sizeof(double) * 6 * nl),
-               o_obs = place(sizeof(double) * 8 * E), o_type = place(E), o_pose = place(4 * (size_t)E),
-               o_lm = place(4 * (size_t)E), o_cam = place(4 * (size_t)E);
-  const size_t call_bytes = so;
-  const size_t down_bytes = al256(E) + al256(sizeof(double) * 8 * np) + al256(sizeof(double) * 3 * nq) +
-                            al256(sizeof(double) * 6 * nl);
-  int rc;
-  if ((rc = ensure_stage(b, std::max(call_bytes, down_bytes)))) return rc;
-  double* eobs = reinterpret_cast<double*>(b->stage + o_obs);
+  double* eobs = reinterpret_cast<double*>(sg + cl.obs);
+  int8_t* etype = reinterpret_cast<int8_t*>(sg + cl.type);
+  int* epose = reinterpret_cast<int*>(sg + cl.pose);
+  int* elm = reinterpret_cast<int*>(sg + cl.lm);
+  int* ecam = reinterpret_cast<int*>(sg + cl.cam);
   int e = 0;
-  for (int t = 0; t < 4; t++)
+  for (int t = 0; t < 4; t++) {
+    RSPL_CHECK_ARG(ne[t] == 0 || (poses[t] && lms[t] && obs[t]), "NULL edge arrays");
     for (int i = 0; i < ne[t]; i++, e++) {
-      RSPL_CHECK_ARG(poses[t] && lms[t] && obs[t], "NULL edge arrays");
       const int p = poses[t][i], l = lms[t][i], c = cams[t] ? cams[t][i] : 0;
       RSPL_CHECK_ARG(p >= 0 && p < np && l >= 0 && l < (t < 2 ? nq : nl) && c >= 0 && c < pr->n_cameras,
                      "edge %d of type %d references a missing vertex/camera", i, t);
@@ -520,35 +558,29 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
       elm[e] = t < 2 ? l : nq + l;
       ecam[e] = c;
       double* o = eobs + 8 * (size_t)e;
-      for (int k = 0; k < 8; k++) o[k] = k < od[t] ? obs[t][(size_t)od[t] * i + k] : 0.0;
+      const double* src = obs[t] + (size_t)od[t] * i;
+      for (int k = 0; k < 8; k++) o[k] = k < od[t] ? src[k] : 0.0;
     }
-  memcpy(b->stage + o_cams, pr->cameras, sizeof(double) * 5 * pr->n_cameras);
-  if (np) memcpy(b->stage + o_T, T.data(), sizeof(double) * 8 * np);
-  if (nq) memcpy(b->stage + o_X, pr->points, sizeof(double) * 3 * nq);
-  if (nl) memcpy(b->stage + o_L, pr->lines, sizeof(double) * 6 * nl);
-  if (E) {
-    memcpy(b->stage + o_type, etype.data(), E);
-    memcpy(b->stage + o_pose, epose.data(), 4 * (size_t)E);
-    memcpy(b->stage + o_lm, elm.data(), 4 * (size_t)E);
-    memcpy(b->stage + o_cam, ecam.data(), 4 * (size_t)E);
   }
-  auto up = [&](void* dst, size_t o, size_t bytes) {
-    return bytes == 0 || hipMemcpyAsync(dst, b->stage + o, bytes, hipMemcpyHostToDevice, st) == hipSuccess;
-  };
-  if (!(up(b->cams, o_cams, sizeof(double) * 5 * pr->n_cameras) && up(b->T, o_T, sizeof(double) * 8 * np) &&
-        up(b->X, o_X, sizeof(double) * 3 * nq) && up(b->L, o_L, sizeof(double) * 6 * nl) &&
-        up(b->eobs, o_obs, sizeof(double) * 8 * E) && up(b->etype, o_type, E) &&
-        up(b->epose, o_pose, 4 * (size_t)E) && up(b->elm, o_lm, 4 * (size_t)E) && up(b->ecam, o_cam, 4 * (size_t)E))) {
-    set_error("BA upload failed");
-    return RSPL_E_DEVICE;
-  }
-  if (E) RSPL_HIP(hipMemsetAsync(b->level, 0, E, st));
-  RSPL_HIP(hipMemsetAsync(b->flags, 0, 4 * sizeof(int), st));
-  RSPL_HIP(hipMemsetAsync(b->out, 0, 8 * sizeof(double), st));
+  memcpy(sg + cl.cams, pr->cameras, sizeof(double) * 5 * pr->n_cameras);
+  if (nq) memcpy(sg + cl.X, pr->points, sizeof(double) * 3 * nq);
+  if (nl) memcpy(sg + cl.L, pr->lines, sizeof(double) * 6 * nl);
+  memset(sg + cl.level, 0, cl.bytes - cl.level);  // level, flags, out start at zero
+  RSPL_HIP(hipMemcpyAsync(b->cbuf, sg, cl.bytes, hipMemcpyHostToDevice, st));
+  char* cb = b->cbuf;
+  uint8_t* level = reinterpret_cast<uint8_t*>(cb + cl.level);
   ba::Problem P{};
-  P.cams = b->cams; P.T = b->T; P.X = b->X; P.L = b->L; P.np = np; P.nq = nq; P.nl = nl;
+  P.cams = reinterpret_cast<double*>(cb + cl.cams);
+  P.T = reinterpret_cast<double*>(cb + cl.T);
+  P.X = reinterpret_cast<double*>(cb + cl.X);
+  P.L = reinterpret_cast<double*>(cb + cl.L);
+  P.np = np; P.nq = nq; P.nl = nl;
   P.Tn = b->Tb; P.Xn = b->Xb; P.Ln = b->Lb;
-  P.etype = b->etype; P.epose = b->epose; P.elm = b->elm; P.ecam = b->ecam; P.eobs = b->eobs;
+  P.etype = reinterpret_cast<const int8_t*>(cb + cl.type);
+  P.epose = reinterpret_cast<const int*>(cb + cl.pose);
+  P.elm = reinterpret_cast<const int*>(cb + cl.lm);
+  P.ecam = reinterpret_cast<const int*>(cb + cl.cam);
+  P.eobs = reinterpret_cast<const double*>(cb + cl.obs);
   const double th[4] = {pr->th_mono_point, pr->th_stereo_point, pr->th_mono_line, pr->th_stereo_line};
   for (int t = 0; t < 4; t++) {
     P.th[t] = th[t];
@@ -559,54 +591,62 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   Lr.Hpl = b->Hpl_e;
   ba::Sys S{};
   S.Hll = b->Hll; S.bl = b->bl; S.bp = b->bp; S.S = b->S; S.x = b->x; S.partial = b->partial;
-  S.partial2 = b->partial2; S.out = b->out; S.fail = b->flags; S.counter = reinterpret_cast<unsigned*>(b->flags + 1);
+  S.partial2 = b->partial2;
+  S.out = reinterpret_cast<double*>(cb + cl.out);
+  S.fail = reinterpret_cast<int*>(cb + cl.flags);
+  S.counter = reinterpret_cast<unsigned*>(cb + cl.flags + sizeof(int));
   S.lm_ctr = b->lm_ctr;
   S.mail = b->mail_dev;
-  const size_t phase_soff = al256(call_bytes);
   // ---- phase 1: all edges, Huber ----
+  // (the staging regions of the active structure follow the call region; the second part
+  // is built on the host while the GPU runs the initial cost + first linearisation)
   ba::Active A{};
   {
-    std::vector<int> act(E);
+    std::vector<int>& act = b->ws.act;
+    act.resize(E);
     std::iota(act.begin(), act.end(), 0);
     mark();
-    if ((rc = build_active(b, act, epose, elm, etype, pr->pose_fixed, np, nL, 1, phase_soff, A, S))) return rc;
+    size_t s1 = 0;
+    if ((rc = build_csr(b, act, epose, elm, etype, pr->pose_fixed, np, nL, 1, soff1, &s1, A))) return rc;
     mark();
-    if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first)))
+    const size_t soff2 = soff1 + al256(s1);
+    auto pairs = [&]() { return build_pairs(b, nL, soff2, A, S); };
+    if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first, pairs)))
       return rc;
     mark();
   }
-  RSPL_HIP(ba::classify(P, Lr, E, b->level, nullptr, 0, st));
+  RSPL_HIP(ba::classify(P, Lr, E, level, nullptr, 0, st));
   mark();
   // ---- phase 2: level-0 edges, no kernel (initializeOptimization(0), :176-213) ----
   // Same active structure with the level-1 edges masked (exact-zero records, no cost, errors
   // kept as g2o keeps them), landmark activity recomputed from the levels on the device.
   {
     A.robust = 0;
-    A.elevel = b->level;
-    RSPL_HIP(ba::landmark_active(A, b->level, b->lm_act2, st));
+    A.elevel = level;
+    RSPL_HIP(ba::landmark_active(A, level, b->lm_act2, st));
     A.lm_act = b->lm_act2;
     mark();
-    if ((rc = optimize(b, P, Lr, S, A, pr->iterations_second, &res->chi2_second, &res->iterations_done_second)))
+    if ((rc = optimize(b, P, Lr, S, A, pr->iterations_second, &res->chi2_second, &res->iterations_done_second,
+                       [] { return RSPL_OK; })))
       return rc;
     mark();
   }
-  RSPL_HIP(ba::classify(P, Lr, E, nullptr, b->inlier, 1, st));
-  const size_t d_T = al256(E), d_X = d_T + al256(sizeof(double) * 8 * np), d_L = d_X + al256(sizeof(double) * 3 * nq);
-  if (E) RSPL_HIP(hipMemcpyAsync(b->stage, b->inlier, E, hipMemcpyDeviceToHost, st));
-  if (np) RSPL_HIP(hipMemcpyAsync(b->stage + d_T, P.T, sizeof(double) * 8 * np, hipMemcpyDeviceToHost, st));
-  if (nq) RSPL_HIP(hipMemcpyAsync(b->stage + d_X, P.X, sizeof(double) * 3 * nq, hipMemcpyDeviceToHost, st));
-  if (nl) RSPL_HIP(hipMemcpyAsync(b->stage + d_L, P.L, sizeof(double) * 6 * nl, hipMemcpyDeviceToHost, st));
+  // ---- inlier flags + final state written by the GPU into the mapped staging buffer ----
+  // (the staging call region was consumed by the upload long before: the stream is in order)
   const unsigned long long q = ++b->seq;
-  RSPL_HIP(ba::post(S, q, st));
+  RSPL_HIP(ba::finish(P, Lr, E, reinterpret_cast<uint8_t*>(b->stage_dev + dl.inl), reinterpret_cast<double*>(b->stage_dev + dl.T),
+                      reinterpret_cast<double*>(b->stage_dev + dl.X), reinterpret_cast<double*>(b->stage_dev + dl.L),
+                      S, q, st));
   if ((rc = wait_mail(b, q, nullptr))) return rc;
-  if (nq) memcpy(res->points, b->stage + d_X, sizeof(double) * 3 * nq);
-  if (nl) memcpy(res->lines, b->stage + d_L, sizeof(double) * 6 * nl);
-  const double* Tout = reinterpret_cast<const double*>(b->stage + d_T);
+  if (nq) memcpy(res->points, b->stage + dl.X, sizeof(double) * 3 * nq);
+  if (nl) memcpy(res->lines, b->stage + dl.L, sizeof(double) * 6 * nl);
+  const double* Tout = reinterpret_cast<const double*>(b->stage + dl.T);
   uint8_t* outs[4] = {res->mono_inlier, res->stereo_inlier, res->mono_line_inlier, res->stereo_line_inlier};
   e = 0;
-  for (int t = 0; t < 4; t++)
-    for (int i = 0; i < ne[t]; i++, e++)
-      if (outs[t]) outs[t][i] = (uint8_t)b->stage[e];
+  for (int t = 0; t < 4; t++) {
+    if (outs[t]) memcpy(outs[t], b->stage + dl.inl + e, ne[t]);
+    e += ne[t];
+  }
   // write back T_wc = estimate().inverse() (:235-240)
   for (int p = 0; p < np; p++) {
     Se3h Tcw;
@@ -622,7 +662,7 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   mark();
   if (timing && ntm == 8) {
     auto us = [&](int i) { return std::chrono::duration<double, std::micro>(tmark[i + 1] - tmark[i]).count(); };
-    fprintf(stderr, "rspl_ba_local us: prep %.0f build1 %.0f opt1 %.0f classify %.0f build2 %.0f opt2 %.0f final %.0f\n",
+    fprintf(stderr, "rspl_ba_local us: prep %.0f csr1 %.0f opt1 %.0f classify %.0f active2 %.0f opt2 %.0f final %.0f\n",
             us(0), us(1), us(2), us(3), us(4), us(5), us(6));
   }
   return RSPL_OK;

@@ -7,6 +7,7 @@
 // a call is bitwise reproducible.  Not a dense contraction: no MFMA; HBM/latency bound.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cfloat>
 #include <cstdint>
 
@@ -1320,10 +1321,8 @@ __global__ __launch_bounds__(256) void landmark_active_kernel(Active A, const ui
 }
 
 // outlier levels after the first optimize / final inlier flags (g2o_optimization.cc:176-231)
-__global__ __launch_bounds__(256) void classify_kernel(Problem P, Lin L, int E, uint8_t* level, uint8_t* inlier,
-                                                       int final_pass) {
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= E) return;
+__device__ __forceinline__ void classify_edge(const Problem& P, const Lin& L, int e, uint8_t* level, uint8_t* inlier,
+                                              int final_pass) {
   const int t = P.etype[e];
   double chi2 = 0;
   for (int k = 0; k < edim(t); k++) chi2 += L.err[4 * e + k] * L.err[4 * e + k];
@@ -1341,6 +1340,34 @@ __global__ __launch_bounds__(256) void classify_kernel(Problem P, Lin L, int E, 
   } else {
     inlier[e] = (chi2 <= P.th[t] && depth_ok) ? 1 : 0;
   }
+}
+
+__global__ __launch_bounds__(256) void classify_kernel(Problem P, Lin L, int E, uint8_t* level, uint8_t* inlier,
+                                                       int final_pass) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e < E) classify_edge(P, L, e, level, inlier, final_pass);
+}
+
+// end of a call: final inlier flags + the final T / X / L written straight into host-mapped
+// memory; the last block (ticket) posts the mailbox once every block's writes are out
+__global__ __launch_bounds__(256) void finish_kernel(Problem P, Lin L, int E, uint8_t* inl, double* Th, double* Xh,
+                                                     double* Lh, Sys S, unsigned long long seq) {
+  __shared__ int last;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < E) classify_edge(P, L, i, nullptr, inl, 1);
+  if (i < 8 * P.np) Th[i] = P.T[i];
+  if (i < 3 * P.nq) Xh[i] = P.X[i];
+  if (i < 6 * P.nl) Lh[i] = P.L[i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned tk = __hip_atomic_fetch_add(S.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = tk == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&S.mail->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 // ---------------------------------------------------------------------------
@@ -1399,6 +1426,14 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
   Problem Pn = P;  // cost of the candidate state
   Pn.T = P.Tn; Pn.X = P.Xn; Pn.L = P.Ln;
   hipLaunchKernelGGL(errors_kernel, dim3(errors_blocks(A.Ea)), dim3(256), 0, s, Pn, L, A, S, nbu, seq);
+  return hipGetLastError();
+}
+
+hipError_t finish(const Problem& P, const Lin& L, int E, uint8_t* inl, double* Th, double* Xh, double* Lh, Sys& S,
+                  unsigned long long seq, hipStream_t s) {
+  const int n = std::max(std::max(E, 8 * P.np), std::max(3 * P.nq, 6 * P.nl));
+  hipLaunchKernelGGL(finish_kernel, dim3(std::max((n + 255) / 256, 1)), dim3(256), 0, s, P, L, E, inl, Th, Xh, Lh, S,
+                     seq);
   return hipGetLastError();
 }
 

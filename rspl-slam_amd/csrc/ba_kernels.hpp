@@ -102,6 +102,9 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
 hipError_t landmark_active(const Active& A, const uint8_t* level, uint8_t* lm_act, hipStream_t s);
 hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8_t* inlier, int final_pass,
                     hipStream_t s);
+// final inlier flags + T / X / L into host-mapped memory, then the mailbox post of seq
+hipError_t finish(const Problem& P, const Lin& L, int E, uint8_t* inl, double* Th, double* Xh, double* Lh, Sys& S,
+                  unsigned long long seq, hipStream_t s);
 int update_blocks(const Problem& P);
 int errors_blocks(int Ea);
 int update_errors_blocks(const Active& A);
