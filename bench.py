@@ -226,8 +226,8 @@ def main():
             capi.memcpy_d2d(n1.ptr, cprev.ptr, 4, st_sg.handle)
             capi.memcpy_d2d(n1.offset(4), ccur.offset(4), 4, st_sg.handle)
             sg.infer_device(2, f0.ptr, n0.ptr, f1.ptr, n1.ptr, K, True, outs[0].ptr, outs[1].ptr, outs[2].ptr,
-                            outs[3].ptr, st_sg.handle)
-            ev_sg[slot].record(st_sg.handle)
+                            outs[3].ptr, st_sg.handle, post_stream=st_post.handle)
+            ev_sg[slot].record(st_post.handle)  # matches complete on the post stream
             # keyframe i's local BA goes to the tracking thread (own high-priority stream) through a
             # 2-deep buffer, as the reference's feature thread blocks only while
             # _tracking_data_buffer.size() >= 2 (src/map_builder.cc:176)

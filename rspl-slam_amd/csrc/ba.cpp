@@ -38,15 +38,17 @@ struct rspl_ba {
   // system
   double *Hll, *bl, *bp, *S, *x, *partial, *partial2;
   unsigned* lm_ctr;  // [max_lines] line-landmark tickets (zeroed at create, re-armed by the kernel)
-  // per-call inputs (cameras, T / X / L, edges, zeroed level / flags / out), laid out exactly
-  // like the staging buffer's call region: one upload per call (capacity fixed at create)
+  // landmark CSR (filled on the device) and the Schur chunk / pose-pair sums
+  int *lm_edges, *lm_pose;
+  double *chunk, *pairfin;
+  unsigned* pair_ctr;  // [npairs] chunk tickets (zeroed at create, re-armed by the kernel)
+  int *pp_cnt, *pp_off;  // [npairs * nchk (+1)] edge pairs per Schur chunk, segment offsets
+  int* pp_buf = nullptr;  // edge-pair lists (e1s | e2s), growable
+  size_t pp_cap = 0;      // capacity in pairs
+  // per-call inputs (cameras, T / X / L, edges, reduced pose ids, landmark offsets, pose pairs,
+  // zeroed level / fill / flags / out), laid out exactly like the staging buffer's call
+  // region: one upload per call (capacity fixed at create)
   char* cbuf = nullptr;
-  // active structure of a phase: landmark CSR / pose lists (phase_buf), pose pairs + Schur
-  // chunks (pair_buf); growable device buffers
-  char* phase_buf = nullptr;
-  size_t phase_cap = 0;
-  char* pair_buf = nullptr;
-  size_t pair_cap = 0;
   // pinned, host-mapped staging for uploads; the final kernel writes results straight into it
   char* stage = nullptr;
   char* stage_dev = nullptr;
@@ -55,10 +57,7 @@ struct rspl_ba {
   ba::Mail* mail = nullptr;
   ba::Mail* mail_dev = nullptr;
   unsigned long long seq = 0;
-  struct Workspace {  // host scratch reused across calls (capacity persists)
-    std::vector<int> pidx, lm_off, lm_edges, lm_pose, ps_cnt, pp_cnt, fill, fill2, act;
-    std::vector<uint8_t> pact, lact;
-  } ws;
+  std::vector<uint8_t> pact;  // host scratch reused across calls
 };
 
 namespace {
@@ -69,8 +68,9 @@ inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // per-call upload layout (staging call region == device call buffer)
 struct CallLayout {
-  size_t cams, T, X, L, obs, type, pose, lm, cam, level, flags, out, bytes;
+  size_t cams, T, X, L, obs, type, pose, lm, cam, pidx, lm_off, lm_act, pairs, level, fill, flags, out, bytes;
   CallLayout(int ncam, int np, int nq, int nl, int E) {
+    const size_t nL = (size_t)nq + nl;
     size_t so = 0;
     auto place = [&](size_t n) {
       const size_t o = so;
@@ -79,8 +79,10 @@ struct CallLayout {
     };
     cams = place(sizeof(double) * 5 * ncam); T = place(sizeof(double) * 8 * np); X = place(sizeof(double) * 3 * nq);
     L = place(sizeof(double) * 6 * nl); obs = place(sizeof(double) * 8 * (size_t)E); type = place(E);
-    pose = place(4 * (size_t)E); lm = place(4 * (size_t)E); cam = place(4 * (size_t)E); level = place(E);
-    flags = place(4 * sizeof(int)); out = place(8 * sizeof(double));
+    pose = place(4 * (size_t)E); lm = place(4 * (size_t)E); cam = place(4 * (size_t)E);
+    pidx = place(4 * (size_t)np); lm_off = place(4 * (nL + 1)); lm_act = place(nL);
+    pairs = place(8 * (size_t)np * (np + 1) / 2);
+    level = place(E); fill = place(4 * nL); flags = place(4 * sizeof(int)); out = place(8 * sizeof(double));  // zeros
     bytes = so;
   }
 };
@@ -110,8 +112,13 @@ void carve(F& ar, rspl_ba* b) {
   // block partials: edge-per-thread kernels (E / 256) and landmark-group kernels (NL * 8 / 256)
   const size_t nblk = std::max(E / 256, NL * 8 / 256) + 2;
   take(b->S, 36 * K * K); take(b->x, 6 * K); take(b->partial, nblk);
-  take(b->partial2, std::max((size_t)b->maxV / 256, nblk) + 2);
+  // partial2: scale partials, and the pose-diagonal partials (K x E/256 x 6) of the lambda init
+  take(b->partial2, std::max(std::max((size_t)b->maxV / 256, nblk) + 2, K * (E / 256 + 1) * 6));
   take(b->lm_ctr, nl);
+  const size_t npairs = K * (K + 1) / 2, nchk = std::max<size_t>((NL + ba::kLmChunk - 1) / ba::kLmChunk, 1);
+  take(b->lm_edges, E); take(b->lm_pose, E);
+  take(b->chunk, npairs * nchk * 48); take(b->pairfin, npairs * 48); take(b->pair_ctr, npairs);
+  take(b->pp_cnt, npairs * nchk); take(b->pp_off, npairs * nchk + 1);
 }
 
 int ensure_stage(rspl_ba* b, size_t bytes) {
@@ -125,18 +132,6 @@ int ensure_stage(rspl_ba* b, size_t bytes) {
   RSPL_HIP(hipHostMalloc((void**)&b->stage, cap, hipHostMallocMapped | hipHostMallocCoherent));
   RSPL_HIP(hipHostGetDevicePointer((void**)&b->stage_dev, b->stage, 0));
   b->stage_cap = cap;
-  return RSPL_OK;
-}
-
-int ensure_dev(rspl_ba* b, char*& buf, size_t& cap, size_t bytes) {
-  if (bytes <= cap) return RSPL_OK;
-  RSPL_HIP(hipStreamSynchronize(b->stream));  // kernels may still read the old buffer
-  if (buf) (void)hipFree(buf);
-  buf = nullptr;
-  const size_t nc = std::max(bytes, cap * 2);
-  cap = 0;
-  RSPL_HIP(hipMalloc((void**)&buf, nc));
-  cap = nc;
   return RSPL_OK;
 }
 
@@ -203,189 +198,9 @@ Se3h inverse(const Se3h& T) {  // SE3Quat::inverse
   return r;
 }
 
-// Host-side construction of one phase's active structure, in two parts so the second
-// overlaps the GPU's first cost evaluation + linearisation:
-//   build_csr:   reduced pose ids, landmark CSR (edges in input order within a landmark),
-//                per-pose edge lists -- everything the cost / linearisation kernels read;
-//   build_pairs: pose pairs, per-pair edge pairs (landmark order), Schur chunks -- read only
-//                by the trials.
-// Each part is written straight into the pinned staging buffer at `soff` and uploaded
-// with one async copy.  Returns the staging bytes used in *sbytes.
-// staging bytes build_csr can need (so the call region it reads is never reallocated under it)
-size_t csr_bytes_bound(int E, int np, int nL) {
-  return 4 * (size_t)E * 4 + 4 * (size_t)np * 2 + 5 * (size_t)(nL + 1) + 8 + 8 * 256;
-}
-
-int build_csr(rspl_ba* b, const std::vector<int>& act, const int* epose, const int* elm, const int8_t* etype,
-              const uint8_t* fixed, int np, int nL, int robust, size_t soff, size_t* sbytes, ba::Active& A) {
-  auto& w = b->ws;
-  const int Ea = (int)act.size();
-  w.pidx.assign(np, -1);
-  w.lact.assign(nL, 0);
-  w.pact.assign(np, 0);
-  for (int e : act) {
-    w.pact[epose[e]] = 1;
-    w.lact[elm[e]] = 1;
-  }
-  int K = 0;
-  for (int p = 0; p < np; p++)
-    if (w.pact[p] && !fixed[p]) w.pidx[p] = K++;
-  w.lm_off.assign(nL + 1, 0);
-  for (int e : act) w.lm_off[elm[e] + 1]++;
-  for (int g = 0; g < nL; g++) w.lm_off[g + 1] += w.lm_off[g];
-  w.lm_edges.resize(Ea);
-  w.lm_pose.resize(Ea);
-  w.fill.assign(w.lm_off.begin(), w.lm_off.end() - 1);
-  w.ps_cnt.assign(K + 1, 0);
-  int n_line_edges = 0;
-  for (int e : act) {
-    const int k = w.fill[elm[e]]++;
-    const int a = w.pidx[epose[e]];
-    w.lm_edges[k] = e;
-    w.lm_pose[k] = a;
-    if (a >= 0) w.ps_cnt[a + 1]++;
-    n_line_edges += etype[e] >= 2;
-  }
-  for (int a = 0; a < K; a++) w.ps_cnt[a + 1] += w.ps_cnt[a];
-  const int nps = w.ps_cnt[K];
-  size_t off = 0;
-  auto place = [&](size_t bytes) {
-    const size_t o = off;
-    off = al256(off + bytes);
-    return o;
-  };
-  const size_t o_act = place(4 * (size_t)Ea), o_pidx = place(4 * (size_t)np), o_lmoff = place(4 * (size_t)(nL + 1)),
-               o_lme = place(4 * (size_t)Ea), o_lmp = place(4 * (size_t)Ea), o_lact = place(nL),
-               o_psoff = place(4 * (size_t)(K + 1)), o_pse = place(4 * (size_t)nps);
-  int rc;
-  if ((rc = ensure_dev(b, b->phase_buf, b->phase_cap, off))) return rc;
-  if ((rc = ensure_stage(b, soff + off))) return rc;
-  char* st = b->stage + soff;
-  if (Ea) memcpy(st + o_act, act.data(), 4 * (size_t)Ea);
-  if (np) memcpy(st + o_pidx, w.pidx.data(), 4 * (size_t)np);
-  memcpy(st + o_lmoff, w.lm_off.data(), 4 * (size_t)(nL + 1));
-  if (Ea) {
-    memcpy(st + o_lme, w.lm_edges.data(), 4 * (size_t)Ea);
-    memcpy(st + o_lmp, w.lm_pose.data(), 4 * (size_t)Ea);
-  }
-  if (nL) memcpy(st + o_lact, w.lact.data(), nL);
-  memcpy(st + o_psoff, w.ps_cnt.data(), 4 * (size_t)(K + 1));
-  {  // per-pose edge lists in landmark order
-    int* pse = reinterpret_cast<int*>(st + o_pse);
-    w.fill.assign(w.ps_cnt.begin(), w.ps_cnt.end() - 1);
-    for (int k = 0; k < Ea; k++)
-      if (w.lm_pose[k] >= 0) pse[w.fill[w.lm_pose[k]]++] = w.lm_edges[k];
-  }
-  RSPL_HIP(hipMemcpyAsync(b->phase_buf, st, off, hipMemcpyHostToDevice, b->stream));
-  auto dptr = [&](size_t o) { return reinterpret_cast<const int*>(b->phase_buf + o); };
-  A.edges = dptr(o_act); A.Ea = Ea; A.pidx = dptr(o_pidx); A.lm_off = dptr(o_lmoff);
-  A.lm_edges = dptr(o_lme); A.lm_pose = dptr(o_lmp);
-  A.lm_act = reinterpret_cast<const uint8_t*>(b->phase_buf + o_lact);
-  A.ps_off = dptr(o_psoff); A.ps_edges = dptr(o_pse);
-  A.n_line_edges = n_line_edges; A.nL = nL; A.robust = robust; A.K = K;
-  A.npairs = 0; A.nch = 0;
-  *sbytes = off;
-  return RSPL_OK;
-}
-
-int build_pairs(rspl_ba* b, int nL, size_t soff, ba::Active& A, ba::Sys& S) {
-  auto& w = b->ws;
-  const int K = A.K;
-  const int npairs = K * (K + 1) / 2;
-  auto pid = [K](int a, int c) { return a * K - a * (a - 1) / 2 + (c - a); };
-  // edge pairs per pose pair (a <= c)
-  w.pp_cnt.assign(npairs + 1, 0);
-  for (int g = 0; g < nL; g++) {
-    const int k0 = w.lm_off[g], k1 = w.lm_off[g + 1];
-    for (int i = k0; i < k1; i++) {
-      const int ai = w.lm_pose[i];
-      if (ai < 0) continue;
-      for (int j = k0; j < k1; j++) {
-        const int aj = w.lm_pose[j];
-        if (aj >= ai) w.pp_cnt[pid(ai, aj) + 1]++;
-      }
-    }
-  }
-  int nch = 0;
-  for (int p = 0; p < npairs; p++) nch += (w.pp_cnt[p + 1] + ba::kChunk - 1) / ba::kChunk;
-  for (int p = 0; p < npairs; p++) w.pp_cnt[p + 1] += w.pp_cnt[p];
-  const int npp = w.pp_cnt[npairs];
-  size_t off = 0;
-  auto place = [&](size_t bytes) {
-    const size_t o = off;
-    off = al256(off + bytes);
-    return o;
-  };
-  const size_t o_pairs = place(8 * (size_t)npairs), o_choff = place(4 * (size_t)(npairs + 1)),
-               o_chb = place(4 * (size_t)nch), o_che = place(4 * (size_t)nch), o_chp = place(4 * (size_t)nch),
-               o_e1 = place(4 * (size_t)npp), o_e2 = place(4 * (size_t)npp),
-               o_pctr = place(sizeof(unsigned) * (size_t)std::max(npairs, 1));  // uploaded as zeros
-  const size_t upload = off;
-  const size_t o_chunk = place(sizeof(double) * 48 * (size_t)std::max(nch, 1));
-  const size_t o_pfin = place(sizeof(double) * 48 * (size_t)std::max(npairs, 1));
-  int rc;
-  if ((rc = ensure_dev(b, b->pair_buf, b->pair_cap, off))) return rc;
-  if ((rc = ensure_stage(b, soff + upload))) return rc;
-  char* st = b->stage + soff;
-  auto I = [&](size_t o) { return reinterpret_cast<int*>(st + o); };
-  {
-    int* pairs = I(o_pairs);
-    int* choff = I(o_choff);
-    int* chb = I(o_chb);
-    int* che = I(o_che);
-    int* chp = I(o_chp);
-    int c = 0;
-    for (int a = 0, p = 0; a < K; a++)
-      for (int cc = a; cc < K; cc++, p++) {
-        pairs[2 * p] = a;
-        pairs[2 * p + 1] = cc;
-        choff[p] = c;
-        for (int s2 = w.pp_cnt[p]; s2 < w.pp_cnt[p + 1]; s2 += ba::kChunk, c++) {
-          chb[c] = s2;
-          che[c] = std::min(s2 + ba::kChunk, w.pp_cnt[p + 1]);
-          chp[c] = p;
-        }
-      }
-    choff[npairs] = c;
-    memset(st + o_pctr, 0, sizeof(unsigned) * (size_t)std::max(npairs, 1));
-  }
-  {  // fills in landmark order: per-pair edge pairs come out landmark-sorted
-    int* e1 = I(o_e1);
-    int* e2 = I(o_e2);
-    w.fill2.assign(w.pp_cnt.begin(), w.pp_cnt.end() - 1);
-    for (int g = 0; g < nL; g++) {
-      const int k0 = w.lm_off[g], k1 = w.lm_off[g + 1];
-      for (int i = k0; i < k1; i++) {
-        const int ai = w.lm_pose[i];
-        if (ai < 0) continue;
-        for (int j = k0; j < k1; j++) {
-          const int aj = w.lm_pose[j];
-          if (aj < ai) continue;
-          const int q = w.fill2[pid(ai, aj)]++;
-          e1[q] = w.lm_edges[i];
-          e2[q] = w.lm_edges[j];
-        }
-      }
-    }
-  }
-  RSPL_HIP(hipMemcpyAsync(b->pair_buf, st, upload, hipMemcpyHostToDevice, b->stream));
-  auto dptr = [&](size_t o) { return reinterpret_cast<const int*>(b->pair_buf + o); };
-  A.pairs = dptr(o_pairs); A.npairs = npairs;
-  A.pair_choff = dptr(o_choff); A.ch_beg = dptr(o_chb); A.ch_end = dptr(o_che); A.ch_pair = dptr(o_chp);
-  A.nch = nch;
-  A.pp_e1 = dptr(o_e1); A.pp_e2 = dptr(o_e2);
-  S.chunk = reinterpret_cast<double*>(b->pair_buf + o_chunk);
-  S.pairfin = reinterpret_cast<double*>(b->pair_buf + o_pfin);
-  S.pair_ctr = reinterpret_cast<unsigned*>(b->pair_buf + o_pctr);
-  return RSPL_OK;
-}
-
 // one g2o SparseOptimizer::optimize(iters) with OptimizationAlgorithmLevenberg
-// `overlap` (optional) runs on the host while the GPU evaluates the initial cost and the
-// first linearisation; it must be done before the first trial (it builds the pair lists).
-template <typename F>
 int optimize(rspl_ba* b, ba::Problem& P, const ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
-             double* chi2_out, int* done_out, F&& overlap) {
+             double* chi2_out, int* done_out) {
   hipStream_t st = b->stream;
   double v[4];
   int rc;
@@ -394,9 +209,8 @@ int optimize(rspl_ba* b, ba::Problem& P, const ba::Lin& Lr, ba::Sys& S, const ba
   if (iters > 0) {  // the first linearisation does not depend on the cost: queue it right behind
     RSPL_HIP(ba::linearize(P, Lr, A, S, true, st));
     q = ++b->seq;
-    RSPL_HIP(ba::post(S, q, st));  // posts chi2 (S.out[0]) and the max diagonal (S.out[2])
+    RSPL_HIP(ba::post(S, q, st, &A));  // posts chi2 (S.out[0]) and the max diagonal (S.out[2])
   }
-  if ((rc = overlap())) return rc;
   if ((rc = wait_mail(b, q, v))) return rc;
   double currentChi = v[0];
   double lambda = 1e-5 * v[2], ni = 2;  // computeLambdaInit: tau * max diagonal
@@ -468,7 +282,8 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
       hipHostGetDevicePointer((void**)&b->mail_dev, b->mail, 0) != hipSuccess ||
       hipMalloc((void**)&b->cbuf, CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE).bytes) !=
           hipSuccess ||
-      hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess) {
+      hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
+      hipMemset(b->pair_ctr, 0, sizeof(unsigned) * std::max(b->maxK * (b->maxK + 1) / 2, 1)) != hipSuccess) {
     set_error("BA stream / mailbox allocation failed");
     rspl_ba_destroy(b);
     return RSPL_E_DEVICE;
@@ -482,9 +297,8 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
   if (!b) return;
   if (b->stream) (void)hipStreamSynchronize(b->stream);
   b->arena.release();
-  if (b->phase_buf) (void)hipFree(b->phase_buf);
-  if (b->pair_buf) (void)hipFree(b->pair_buf);
   if (b->cbuf) (void)hipFree(b->cbuf);
+  if (b->pp_buf) (void)hipFree(b->pp_buf);
   if (b->stage) (void)hipHostFree(b->stage);
   if (b->mail) (void)hipHostFree(b->mail);
   if (b->stream) (void)hipStreamDestroy(b->stream);
@@ -517,8 +331,7 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   const CallLayout cl(pr->n_cameras, np, nq, nl, E);
   const DownLayout dl(np, nq, nl, E);
   int rc;
-  const size_t soff1 = al256(std::max(cl.bytes, dl.bytes));
-  if ((rc = ensure_stage(b, soff1 + csr_bytes_bound(E, np, nL)))) return rc;
+  if ((rc = ensure_stage(b, std::max(cl.bytes, dl.bytes)))) return rc;
   char* sg = b->stage;
   // vertices: VertexSE3Expmap estimate = SE3Quat(q, p).inverse() (g2o_optimization.cc:42)
   double* T = reinterpret_cast<double*>(sg + cl.T);
@@ -546,6 +359,11 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   int* epose = reinterpret_cast<int*>(sg + cl.pose);
   int* elm = reinterpret_cast<int*>(sg + cl.lm);
   int* ecam = reinterpret_cast<int*>(sg + cl.cam);
+  // per-landmark edge counts -> CSR offsets, poses with edges -> reduced pose ids (the
+  // device fills the CSR lists from these)
+  int* lm_off = reinterpret_cast<int*>(sg + cl.lm_off);
+  memset(lm_off, 0, sizeof(int) * (nL + 1));
+  b->pact.assign(np, 0);
   int e = 0;
   for (int t = 0; t < 4; t++) {
     RSPL_CHECK_ARG(ne[t] == 0 || (poses[t] && lms[t] && obs[t]), "NULL edge arrays");
@@ -557,11 +375,39 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
       epose[e] = p;
       elm[e] = t < 2 ? l : nq + l;
       ecam[e] = c;
+      lm_off[elm[e] + 1]++;
+      b->pact[p] = 1;
       double* o = eobs + 8 * (size_t)e;
       const double* src = obs[t] + (size_t)od[t] * i;
       for (int k = 0; k < 8; k++) o[k] = k < od[t] ? src[k] : 0.0;
     }
   }
+  uint8_t* lm_act = reinterpret_cast<uint8_t*>(sg + cl.lm_act);
+  size_t pair_bound = 0;  // sum_g k_g^2 >= edge pairs of any pose pair
+  for (int g = 0; g < nL; g++) {
+    const size_t k = lm_off[g + 1];
+    pair_bound += k * k;
+    lm_act[g] = k > 0;
+    lm_off[g + 1] += lm_off[g];
+  }
+  if (pair_bound > b->pp_cap) {  // grow the edge-pair lists (the stream is idle between calls)
+    RSPL_HIP(hipStreamSynchronize(st));
+    if (b->pp_buf) (void)hipFree(b->pp_buf);
+    b->pp_buf = nullptr;
+    b->pp_cap = 0;
+    const size_t cap = std::max(pair_bound, (size_t)1 << 16);
+    RSPL_HIP(hipMalloc((void**)&b->pp_buf, 2 * sizeof(int) * cap));
+    b->pp_cap = cap;
+  }
+  int* pidx = reinterpret_cast<int*>(sg + cl.pidx);
+  int K = 0;
+  for (int p = 0; p < np; p++) pidx[p] = (b->pact[p] && !pr->pose_fixed[p]) ? K++ : -1;
+  int* pairs = reinterpret_cast<int*>(sg + cl.pairs);
+  for (int a = 0, q = 0; a < K; a++)
+    for (int c = a; c < K; c++, q++) {
+      pairs[2 * q] = a;
+      pairs[2 * q + 1] = c;
+    }
   memcpy(sg + cl.cams, pr->cameras, sizeof(double) * 5 * pr->n_cameras);
   if (nq) memcpy(sg + cl.X, pr->points, sizeof(double) * 3 * nq);
   if (nl) memcpy(sg + cl.L, pr->lines, sizeof(double) * 6 * nl);
@@ -597,24 +443,34 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   S.counter = reinterpret_cast<unsigned*>(cb + cl.flags + sizeof(int));
   S.lm_ctr = b->lm_ctr;
   S.mail = b->mail_dev;
+  S.chunk = b->chunk;
+  S.pairfin = b->pairfin;
+  S.pair_ctr = b->pair_ctr;
   // ---- phase 1: all edges, Huber ----
-  // (the staging regions of the active structure follow the call region; the second part
-  // is built on the host while the GPU runs the initial cost + first linearisation)
   ba::Active A{};
-  {
-    std::vector<int>& act = b->ws.act;
-    act.resize(E);
-    std::iota(act.begin(), act.end(), 0);
-    mark();
-    size_t s1 = 0;
-    if ((rc = build_csr(b, act, epose, elm, etype, pr->pose_fixed, np, nL, 1, soff1, &s1, A))) return rc;
-    mark();
-    const size_t soff2 = soff1 + al256(s1);
-    auto pairs = [&]() { return build_pairs(b, nL, soff2, A, S); };
-    if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first, pairs)))
-      return rc;
-    mark();
-  }
+  A.Ea = E;
+  A.pidx = reinterpret_cast<const int*>(cb + cl.pidx);
+  A.lm_off = reinterpret_cast<const int*>(cb + cl.lm_off);
+  A.lm_edges = b->lm_edges;
+  A.lm_pose = b->lm_pose;
+  A.lm_act = reinterpret_cast<const uint8_t*>(cb + cl.lm_act);
+  A.pairs = reinterpret_cast<const int*>(cb + cl.pairs);
+  A.npairs = K * (K + 1) / 2;
+  A.nchk = std::max((nL + ba::kLmChunk - 1) / ba::kLmChunk, 1);
+  A.n_line_edges = ne[2] + ne[3];
+  A.K = K;
+  A.nL = nL;
+  A.robust = 1;
+  mark();
+  A.pp_off = b->pp_off;
+  A.pp_e1 = b->pp_buf;
+  A.pp_e2 = b->pp_buf + b->pp_cap;
+  RSPL_HIP(ba::build_csr(P, A, reinterpret_cast<int*>(cb + cl.fill), b->lm_edges, b->lm_pose, st));
+  RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, b->pp_buf + b->pp_cap, st));
+  mark();
+  if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first)))
+    return rc;
+  mark();
   RSPL_HIP(ba::classify(P, Lr, E, level, nullptr, 0, st));
   mark();
   // ---- phase 2: level-0 edges, no kernel (initializeOptimization(0), :176-213) ----
@@ -626,8 +482,7 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
     RSPL_HIP(ba::landmark_active(A, level, b->lm_act2, st));
     A.lm_act = b->lm_act2;
     mark();
-    if ((rc = optimize(b, P, Lr, S, A, pr->iterations_second, &res->chi2_second, &res->iterations_done_second,
-                       [] { return RSPL_OK; })))
+    if ((rc = optimize(b, P, Lr, S, A, pr->iterations_second, &res->chi2_second, &res->iterations_done_second)))
       return rc;
     mark();
   }
@@ -662,7 +517,7 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   mark();
   if (timing && ntm == 8) {
     auto us = [&](int i) { return std::chrono::duration<double, std::micro>(tmark[i + 1] - tmark[i]).count(); };
-    fprintf(stderr, "rspl_ba_local us: prep %.0f csr1 %.0f opt1 %.0f classify %.0f active2 %.0f opt2 %.0f final %.0f\n",
+    fprintf(stderr, "rspl_ba_local us: prep %.0f csr %.0f opt1 %.0f classify %.0f active2 %.0f opt2 %.0f final %.0f\n",
             us(0), us(1), us(2), us(3), us(4), us(5), us(6));
   }
   return RSPL_OK;

@@ -260,8 +260,8 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
   __shared__ int last;
   const int i = blockIdx.x * 256 + threadIdx.x;
   double c = 0.0;
-  if (i < A.Ea && (!A.elevel || !A.elevel[A.edges[i]])) {
-    const int e = A.edges[i];
+  if (i < A.Ea && (!A.elevel || !A.elevel[i])) {
+    const int e = i;
     const int t = P.etype[e];
     const SE3 T = load_T(P.T + 8 * P.epose[e]);
     double er[4] = {0, 0, 0, 0};
@@ -310,8 +310,22 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
   }
 }
 
-// mailbox post of the lambda-init statistic (max Hessian diagonal) after the first linearisation
-__global__ void post_kernel(Sys S, unsigned long long seq) {
+// mailbox post of the lambda-init statistic (max Hessian diagonal) after the first linearisation;
+// with npd > 0 it first folds in the pose blocks: per pose, the npd block partials of
+// pose_diag_kernel summed in order
+__global__ void post_kernel(Sys S, int K, int npd, unsigned long long seq) {
+  if (npd > 0) {
+    double mx = 0;
+    for (int q = threadIdx.x; q < 6 * K; q += blockDim.x) {  // q = 6 pose + diagonal entry
+      const int pa = q / 6, i = q - 6 * pa;
+      double s = 0;
+      for (int b = 0; b < npd; b++) s += S.partial2[((size_t)pa * npd + b) * 6 + i];
+      mx = fmax(mx, fabs(s));
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+    if (threadIdx.x == 0) S.out[2] = fmax(S.out[2], mx);
+  }
   if (threadIdx.x != 0) return;
   Mail* m = S.mail;
   m->v[0] = S.out[0];
@@ -507,7 +521,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
   int e = 0, t = 2, rows = 2;
   bool pose_opt = false;
   if (on) {
-    e = A.edges[A.Ea - A.n_line_edges + i];
+    e = A.Ea - A.n_line_edges + i;
     t = P.etype[e];
     rows = edim(t);
     pose_opt = A.pidx[P.epose[e]] >= 0;
@@ -612,22 +626,56 @@ __device__ __forceinline__ void block_reduce(double (&acc)[NV], double* lds /* [
   __syncthreads();
 }
 
-// max diagonal of the pose blocks (computeLambdaInit), first iteration only
+// max diagonal of the pose blocks (computeLambdaInit), first iteration only.  Block b sums
+// the Hpp diagonals of its 256 edges per reduced pose (fixed tree) into partial[a][b]; the
+// post kernel sums each pose's partials in block order and takes the max.
 __global__ __launch_bounds__(256) void pose_diag_kernel(Problem P, Lin L, Active A, Sys S) {
   __shared__ double red[4 * 6];
-  const int a = blockIdx.x, tid = threadIdx.x;
-  double acc[6] = {0, 0, 0, 0, 0, 0};
-  for (int k = A.ps_off[a] + tid; k < A.ps_off[a + 1]; k += 256) {
-    const double* H = L.Hpp + 36 * A.ps_edges[k];
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  int a = -1;
+  double d[6] = {0, 0, 0, 0, 0, 0};
+  if (e < A.Ea) {
+    a = A.pidx[P.epose[e]];
+    if (a >= 0) {
+      const double* H = L.Hpp + 36 * e;
 #pragma unroll
-    for (int i = 0; i < 6; i++) acc[i] += H[i * 7];
+      for (int i = 0; i < 6; i++) d[i] = H[i * 7];
+    }
   }
-  block_reduce<6>(acc, red);
-  if (tid == 0) {
-    double mx = 0;
-    for (int i = 0; i < 6; i++) mx = fmax(mx, fabs(red[i]));
-    atomic_max_pos(S.out + 2, mx);
+  for (int pa = 0; pa < A.K; pa++) {
+    double acc[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) acc[i] = a == pa ? d[i] : 0.0;
+    block_reduce<6>(acc, red);
+    if (threadIdx.x < 6) S.partial2[((size_t)pa * gridDim.x + blockIdx.x) * 6 + threadIdx.x] = red[threadIdx.x];
+    __syncthreads();
   }
+}
+
+// Landmark CSR, step 1: each edge takes a slot of its landmark's range (order arbitrary)
+__global__ __launch_bounds__(256) void csr_fill_kernel(Problem P, Active A, int* fill, int* lm_edges) {
+  const int e = blockIdx.x * 256 + threadIdx.x;
+  if (e >= A.Ea) return;
+  const int g = P.elm[e];
+  lm_edges[A.lm_off[g] + atomicAdd(fill + g, 1)] = e;
+}
+
+// step 2: one thread per landmark sorts its (short) list by edge id -- the order every
+// per-landmark reduction then follows -- and records the reduced pose of each entry
+__global__ __launch_bounds__(256) void csr_sort_kernel(Problem P, Active A, int* lm_edges, int* lm_pose) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g >= A.nL) return;
+  const int k0 = A.lm_off[g], k1 = A.lm_off[g + 1];
+  for (int i = k0 + 1; i < k1; i++) {
+    const int v = lm_edges[i];
+    int j = i - 1;
+    while (j >= k0 && lm_edges[j] > v) {
+      lm_edges[j + 1] = lm_edges[j];
+      j--;
+    }
+    lm_edges[j + 1] = v;
+  }
+  for (int k = k0; k < k1; k++) lm_pose[k] = A.pidx[P.epose[lm_edges[k]]];
 }
 
 // ---------------------------------------------------------------------------
@@ -704,47 +752,147 @@ __device__ __forceinline__ bool lm_dinv(const double* Hll, bool point, double la
   return small_inv<4>(H, D);
 }
 
-// Schur complement, stage 1: one wave per chunk of <= kChunk edge pairs of one pose pair.
-// Each lane forms Y = Hpl_e1 Dinv_g on the fly and accumulates
+// one edge pair's Schur terms (Y = Hpl_e1 Dinv_g formed on the fly) added into acc[48]
+__device__ __forceinline__ void schur_pair(const Lin& L, const Sys& S, int g, int e1, int e2, const double (&D)[16],
+                                           double (&acc)[48]) {
+  const double* H1 = L.Hpl + 24 * e1;
+  const double* H2 = L.Hpl + 24 * e2;
+  double B[24];
+#pragma unroll
+  for (int q = 0; q < 24; q++) B[q] = H2[q];
+  const bool diag = e1 == e2;
+#pragma unroll
+  for (int r = 0; r < 6; r++) {
+    const double h0 = H1[r * 4], h1 = H1[r * 4 + 1], h2 = H1[r * 4 + 2], h3 = H1[r * 4 + 3];
+    double y[4];
+#pragma unroll
+    for (int q = 0; q < 4; q++) y[q] = h0 * D[q] + h1 * D[4 + q] + h2 * D[8 + q] + h3 * D[12 + q];
+#pragma unroll
+    for (int cc = 0; cc < 6; cc++)
+      acc[r * 6 + cc] -= y[0] * B[cc * 4] + y[1] * B[cc * 4 + 1] + y[2] * B[cc * 4 + 2] + y[3] * B[cc * 4 + 3];
+    if (diag) {
+      const double* Hp = L.Hpp + 36 * e1;
+      const double* bl = S.bl + 4 * g;
+#pragma unroll
+      for (int cc = 0; cc < 6; cc++) acc[r * 6 + cc] += Hp[r * 6 + cc];
+      acc[36 + r] += L.bp[6 * e1 + r];
+      acc[42 + r] += y[0] * bl[0] + y[1] * bl[1] + y[2] * bl[2] + y[3] * bl[3];
+    }
+  }
+}
+
+// Edge-pair lists, built once per call on the device.  Chunk c = (pose pair pr, landmark
+// range lb) owns the segment [pp_off[c], pp_off[c+1]) of the (e1, e2) lists; within it the
+// pairs follow landmark order, then i, then j (deterministic).  Lane l of round r handles
+// landmark lb * kLmChunk + 64 r + l; its matches are found from bit masks over batches of 8
+// CSR entries (independent loads) and placed by a wave prefix sum in lane order.
+template <bool FILL>
+__device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, const int* pp_off, int* e1s, int* e2s) {
+  const int lane = threadIdx.x;
+  const int pr = c / A.nchk, lb = c - pr * A.nchk;
+  const int pa = A.pairs[2 * pr], pb = A.pairs[2 * pr + 1];
+  int base = FILL ? pp_off[c] : 0;
+  for (int r = 0; r < kLmChunk / 64; r++) {
+    const int g = lb * kLmChunk + 64 * r + lane;
+    int k0 = 0, k1 = 0;
+    if (g < A.nL && A.lm_act[g]) {
+      k0 = A.lm_off[g];
+      k1 = A.lm_off[g + 1];
+    }
+    int cnt = 0;
+    for (int ib = k0; ib < k1; ib += 8) {  // i blocks
+      unsigned ma = 0;
+      int pi[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) pi[u] = A.lm_pose[min(ib + u, k1 - 1)];
+#pragma unroll
+      for (int u = 0; u < 8; u++) ma |= (ib + u < k1 && pi[u] == pa) ? 1u << u : 0u;
+      if (!ma) continue;
+      for (int jb = k0; jb < k1; jb += 8) {  // j blocks
+        unsigned mb = 0;
+        int pj[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) pj[u] = A.lm_pose[min(jb + u, k1 - 1)];
+#pragma unroll
+        for (int u = 0; u < 8; u++) mb |= (jb + u < k1 && pj[u] == pb) ? 1u << u : 0u;
+        cnt += __popc(ma) * __popc(mb);
+      }
+    }
+    // wave exclusive prefix of the per-lane counts (lane order)
+    int pre = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(pre, o);
+      if (lane >= o) pre += t;
+    }
+    const int total = __shfl(pre, 63);
+    if (FILL && cnt) {
+      int q = base + pre - cnt;
+      for (int ib = k0; ib < k1; ib++) {
+        if (A.lm_pose[ib] != pa) continue;
+        const int e1 = A.lm_edges[ib];
+        for (int jb = k0; jb < k1; jb++) {
+          if (A.lm_pose[jb] != pb) continue;
+          e1s[q] = e1;
+          e2s[q] = A.lm_edges[jb];
+          q++;
+        }
+      }
+    }
+    base += total;
+  }
+  if (!FILL && lane == 0) pp_cnt[c] = base;
+}
+
+__global__ __launch_bounds__(64) void pair_count_kernel(Active A, int* pp_cnt) {
+  pair_scan<false>(A, blockIdx.x, pp_cnt, nullptr, nullptr, nullptr);
+}
+__global__ __launch_bounds__(64) void pair_fill_kernel(Active A, const int* pp_off, int* e1s, int* e2s) {
+  pair_scan<true>(A, blockIdx.x, nullptr, pp_off, e1s, e2s);
+}
+// exclusive scan of the chunk counts (one workgroup; n = npairs * nchk + 1 offsets)
+__global__ __launch_bounds__(1024) void pair_offsets_kernel(const int* cnt, int* off, int n) {
+  __shared__ int part[1024];
+  const int tid = threadIdx.x;
+  const int per = (n + 1023) / 1024, b0 = min(tid * per, n), b1 = min(b0 + per, n);
+  int s = 0;
+  for (int i = b0; i < b1; i++) s += cnt[i];
+  part[tid] = s;
+  __syncthreads();
+  for (int o = 1; o < 1024; o <<= 1) {  // Hillis-Steele inclusive scan of the partials
+    const int t = tid >= o ? part[tid - o] : 0;
+    __syncthreads();
+    part[tid] += t;
+    __syncthreads();
+  }
+  int run = part[tid] - s;
+  for (int i = b0; i < b1; i++) {
+    off[i] = run;
+    run += cnt[i];
+  }
+  if (tid == 1023) off[n] = part[1023];
+}
+
+// Schur complement, stage 1: one wave per chunk (pose pair, landmark range) walks its
+// segment of the edge-pair lists, forming Y = Hpl_e1 Dinv_g on the fly:
 //   [0,36)  [e1==e2] Hpp_e1 - Y Hpl_e2^T,   [36,42) [e1==e2] bp_e1,   [42,48) [e1==e2] Y bl_g
 // then the wave sums its 64 lanes in lane order (LDS transpose).
 __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active A, Sys S, double lambda) {
   __shared__ double red[64 * 49];
   const int c = blockIdx.x, lane = threadIdx.x;
-  const int beg = A.ch_beg[c], end = A.ch_end[c];
+  const int pr = c / A.nchk;
+  const int beg = A.pp_off[c], end = A.pp_off[c + 1];
   double acc[48];
 #pragma unroll
   for (int v = 0; v < 48; v++) acc[v] = 0.0;
   bool bad = false;
   for (int k = beg + lane; k < end; k += 64) {
     const int e1 = A.pp_e1[k], e2 = A.pp_e2[k];
+    if (A.elevel && (A.elevel[e1] | A.elevel[e2])) continue;  // zero records: no contribution
     const int g = P.elm[e1];
     double D[16];
     bad |= !lm_dinv(S.Hll + 16 * g, g < P.nq, lambda, D);
-    const double* H1 = L.Hpl + 24 * e1;
-    const double* H2 = L.Hpl + 24 * e2;
-    double B[24];
-#pragma unroll
-    for (int q = 0; q < 24; q++) B[q] = H2[q];
-    const bool diag = e1 == e2;
-#pragma unroll
-    for (int r = 0; r < 6; r++) {
-      const double h0 = H1[r * 4], h1 = H1[r * 4 + 1], h2 = H1[r * 4 + 2], h3 = H1[r * 4 + 3];
-      double y[4];
-#pragma unroll
-      for (int q = 0; q < 4; q++) y[q] = h0 * D[q] + h1 * D[4 + q] + h2 * D[8 + q] + h3 * D[12 + q];
-#pragma unroll
-      for (int cc = 0; cc < 6; cc++)
-        acc[r * 6 + cc] -= y[0] * B[cc * 4] + y[1] * B[cc * 4 + 1] + y[2] * B[cc * 4 + 2] + y[3] * B[cc * 4 + 3];
-      if (diag) {
-        const double* Hp = L.Hpp + 36 * e1;
-        const double* bl = S.bl + 4 * g;
-#pragma unroll
-        for (int cc = 0; cc < 6; cc++) acc[r * 6 + cc] += Hp[r * 6 + cc];
-        acc[36 + r] += L.bp[6 * e1 + r];
-        acc[42 + r] += y[0] * bl[0] + y[1] * bl[1] + y[2] * bl[2] + y[3] * bl[3];
-      }
-    }
+    schur_pair(L, S, g, e1, e2, D, acc);
   }
   if (bad) atomicOr(S.fail, 1);
 #pragma unroll
@@ -752,14 +900,15 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
   __syncthreads();
   // chunk partial, handed off write-through (sc1) to whichever chunk of this pose pair
   // finishes last; that one sums the pair's chunks in chunk order (deterministic)
-  if (lane < 48) {
-    double s = 0;
-    for (int l = 0; l < 64; l++) s += red[l * 49 + lane];
+  if (lane < 48) {  // 8 independent partial sums, combined in a fixed order
+    double p8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int l = 0; l < 64; l++) p8[l & 7] += red[l * 49 + lane];
+    const double s = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
     __hip_atomic_store(S.chunk + 48 * c + lane, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int pr = A.ch_pair[c];
-  const int c0 = A.pair_choff[pr], c1 = A.pair_choff[pr + 1];
+  const int c0 = pr * A.nchk, c1 = c0 + A.nchk;
   unsigned tk = 0;
   if (lane == 0) tk = __hip_atomic_fetch_add(S.pair_ctr + pr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   tk = __shfl(tk, 0);
@@ -781,20 +930,14 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
   }
 }
 
-// Schur complement, stage 2: one thread per (pose pair, entry); chunks summed in order.
-//   S_ab = [a==b] lambda I + sum chunks,  bp_a,  bs_a = bp_a - sum Y bl  (solved in place in x)
+// larger systems, stage 2: one thread per (pose pair, entry) scatters the pair sums.
+//   S_ab = [a==b] lambda I + pair sum,  bp_a,  bs_a = bp_a - sum Y bl  (solved in place in x)
 __global__ __launch_bounds__(256) void pair_final_kernel(Active A, Sys S, double lambda) {
   const int idx = blockIdx.x * 256 + threadIdx.x;
   if (idx >= A.npairs * 42) return;
   const int pr = idx / 42, v = idx - 42 * pr;
   const int a = A.pairs[2 * pr], b = A.pairs[2 * pr + 1], n = 6 * A.K;
-  const int c0 = A.pair_choff[pr], c1 = A.pair_choff[pr + 1];
-  double s = 0, s2 = 0;
-#pragma unroll 8
-  for (int c = c0; c < c1; c++) {
-    s += S.chunk[48 * c + v];
-    if (v >= 36) s2 += S.chunk[48 * c + v + 6];
-  }
+  const double s = S.pairfin[48 * pr + v];
   if (v < 36) {
     const int r = v / 6, cc = v - 6 * r;
     const double val = s + ((a == b && r == cc) ? lambda : 0.0);
@@ -803,7 +946,7 @@ __global__ __launch_bounds__(256) void pair_final_kernel(Active A, Sys S, double
   } else if (a == b) {
     const int r = v - 36;
     S.bp[6 * a + r] = s;
-    S.x[6 * a + r] = s - s2;
+    S.x[6 * a + r] = s - S.pairfin[48 * pr + v + 6];
   }
 }
 
@@ -1389,18 +1532,21 @@ hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys&
                      hipStream_t s) {
   const int nbq = (P.nq * kGroup + 255) / 256, nbl = (A.n_line_edges + 3) / 4;
   if (nbq + nbl > 0) hipLaunchKernelGGL(linearize_kernel, dim3(nbq + nbl), dim3(256), 0, s, P, L, A, S, nbq);
-  if (with_maxdiag && A.K > 0) hipLaunchKernelGGL(pose_diag_kernel, dim3(A.K), dim3(256), 0, s, P, L, A, S);
+  if (with_maxdiag && A.K > 0 && A.Ea > 0)
+    hipLaunchKernelGGL(pose_diag_kernel, dim3((A.Ea + 255) / 256), dim3(256), 0, s, P, L, A, S);
   return hipGetLastError();
 }
 
-hipError_t post(Sys& S, unsigned long long seq, hipStream_t s) {
-  hipLaunchKernelGGL(post_kernel, dim3(1), dim3(64), 0, s, S, seq);
+hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A) {
+  const int npd = (A && A->K > 0 && A->Ea > 0) ? (A->Ea + 255) / 256 : 0;
+  hipLaunchKernelGGL(post_kernel, dim3(1), dim3(64), 0, s, S, A ? A->K : 0, npd, seq);
   return hipGetLastError();
 }
 
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
                  hipStream_t s) {
-  if (A.nch > 0) hipLaunchKernelGGL(pair_chunk_kernel, dim3(A.nch), dim3(64), 0, s, P, L, A, S, lambda);
+  if (A.npairs * A.nchk > 0)
+    hipLaunchKernelGGL(pair_chunk_kernel, dim3(A.npairs * A.nchk), dim3(64), 0, s, P, L, A, S, lambda);
   const int n = 6 * A.K;
   if (n > 0 && n <= kCholLdsMax) {
     static bool attr = false;
@@ -1434,6 +1580,21 @@ hipError_t finish(const Problem& P, const Lin& L, int E, uint8_t* inl, double* T
   const int n = std::max(std::max(E, 8 * P.np), std::max(3 * P.nq, 6 * P.nl));
   hipLaunchKernelGGL(finish_kernel, dim3(std::max((n + 255) / 256, 1)), dim3(256), 0, s, P, L, E, inl, Th, Xh, Lh, S,
                      seq);
+  return hipGetLastError();
+}
+
+hipError_t build_csr(const Problem& P, const Active& A, int* fill, int* lm_edges, int* lm_pose, hipStream_t s) {
+  if (A.Ea > 0) hipLaunchKernelGGL(csr_fill_kernel, dim3((A.Ea + 255) / 256), dim3(256), 0, s, P, A, fill, lm_edges);
+  if (A.nL > 0) hipLaunchKernelGGL(csr_sort_kernel, dim3((A.nL + 255) / 256), dim3(256), 0, s, P, A, lm_edges, lm_pose);
+  return hipGetLastError();
+}
+
+hipError_t build_pairs(const Active& A, int* pp_cnt, int* pp_off, int* e1s, int* e2s, hipStream_t s) {
+  const int nc = A.npairs * A.nchk;
+  if (nc == 0) return hipSuccess;
+  hipLaunchKernelGGL(pair_count_kernel, dim3(nc), dim3(64), 0, s, A, pp_cnt);
+  hipLaunchKernelGGL(pair_offsets_kernel, dim3(1), dim3(1024), 0, s, pp_cnt, pp_off, nc);
+  hipLaunchKernelGGL(pair_fill_kernel, dim3(nc), dim3(64), 0, s, A, pp_off, e1s, e2s);
   return hipGetLastError();
 }
 

@@ -37,25 +37,19 @@ struct Lin {             // per-edge linearisation records (indexed by edge id)
 };
 
 struct Active {          // active structure of one optimize() phase
-  const int* edges;      // [Ea] active edge ids
-  int Ea;
+  int Ea;                // active edges: every edge id in [0, Ea) (input order: points, then lines)
   const int* pidx;       // [np] reduced pose index or -1
-  const int* lm_off;     // [nL+1] CSR over active edges by landmark
+  const int* lm_off;     // [nL+1] CSR of the edges by landmark (edge ids ascending within a landmark)
   const int* lm_edges;
   const int* lm_pose;    // [Ea] reduced pose of lm_edges[k] (or -1)
   const uint8_t* lm_act; // [nL]
-  const int* ps_off;     // [K+1] CSR of active edges by reduced pose
-  const int* ps_edges;
   const int* pairs;      // [npairs][2] reduced pose pairs (a <= b)
   int npairs;
-  const int* pair_choff; // [npairs+1] CSR of Schur chunks per pose pair
-  const int* ch_beg;     // [nch] edge-pair range [beg, end) of each chunk
-  const int* ch_pair;    // [nch] pose pair of each chunk
-  const int* ch_end;
-  int nch;
-  const int* pp_e1;      // edge pairs (e1 of pose a, e2 of pose b, same landmark), grouped by pose pair
-  const int* pp_e2;
-  int n_line_edges;      // active line edges are edges[Ea - n_line_edges .. Ea) (input order)
+  int nchk;              // Schur chunks per pose pair: landmark ranges of kLmChunk
+  const int* pp_off;     // [npairs * nchk + 1] segment of each chunk in the edge-pair lists
+  const int* pp_e1;      // edge pairs (e1 of pose a, e2 of pose b, same landmark), chunk-major,
+  const int* pp_e2;      //   landmark order within a chunk
+  int n_line_edges;      // line edges are [Ea - n_line_edges, Ea)
   const uint8_t* elevel; // [E] or null: edge level (!= 0: outside this phase -- level 1 in the
                          // second optimize): zero linearisation records, no cost, error kept
   int K, nL;
@@ -74,7 +68,7 @@ struct Sys {
   double* bp;            // [K][6]   pose gradient (undamped), for the LM scale
   double* S;             // [6K][6K] reduced camera system
   double* x;             // [6K]     bs on entry of the solve, xp on exit
-  double* chunk;         // [nch][48] Schur chunk partials
+  double* chunk;         // [npairs * nchk][48] Schur chunk partials
   double* pairfin;       // [npairs][48] per-pose-pair sums of the chunk partials
   unsigned* pair_ctr;    // [npairs] chunk tickets (re-armed to 0 by the last chunk)
   double* partial;       // [>= error blocks] chi2 partials
@@ -86,7 +80,7 @@ struct Sys {
   Mail* mail;            // device view of the mailbox
 };
 
-constexpr int kChunk = 128;  // edge pairs per Schur chunk (2 per lane)
+constexpr int kLmChunk = 256;  // landmarks per Schur chunk (4 per lane)
 
 // errors (+ fused final reduction and mailbox post with sequence number seq)
 hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq,
@@ -94,10 +88,16 @@ hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& 
 // edge Jacobians + landmark blocks S.Hll / S.bl (+ max diagonal; pose blocks too when with_maxdiag)
 hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool with_maxdiag,
                      hipStream_t s);
-hipError_t post(Sys& S, unsigned long long seq, hipStream_t s);
+// mailbox post; with A, after linearize(with_maxdiag) it first folds the pose-block maxima in
+hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A = nullptr);
 // one LM trial: Schur complement, Cholesky, back-substitution + candidate state, its cost
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
                  hipStream_t s);
+// landmark CSR from the per-landmark offsets: atomic slots, then each landmark's list sorted by
+// edge id (deterministic) with its reduced poses; fill[] must be zero on entry
+hipError_t build_csr(const Problem& P, const Active& A, int* fill, int* lm_edges, int* lm_pose, hipStream_t s);
+// edge-pair lists of the pose pairs (count, offsets, fill; A.pp_* are not read)
+hipError_t build_pairs(const Active& A, int* pp_cnt, int* pp_off, int* e1s, int* e2s, hipStream_t s);
 // lm_act[g] = landmark g has an edge of level 0 (the second optimize's active landmarks)
 hipError_t landmark_active(const Active& A, const uint8_t* level, uint8_t* lm_act, hipStream_t s);
 hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8_t* inlier, int final_pass,

@@ -8,7 +8,8 @@ db = sqlite3.connect(sys.argv[1])
 rows = list(db.execute("select name,start,end from kernels order by start"))
 print(f"{len(rows)} dispatches, span {(rows[-1][2] - rows[0][1]) / 1e6:.2f} ms")
 for r in db.execute("select name,total_calls,total_duration,average,percentage from top_kernels limit 25"):
-    print(f"{r[0][:70]:70s} {r[1]:6d} {r[2] / 1e3:9.1f}us avg {r[3] / 1e3:8.2f}us {r[4]:5.1f}%")
+    # the rocpd top_kernels view reports durations in microseconds
+    print(f"{r[0][:70]:70s} {r[1]:6d} total {r[2] / 1e3:9.2f}ms avg {r[3]:8.2f}us {r[4]:5.1f}%")
 if len(sys.argv) > 2:
     n = int(sys.argv[2])
     t0, prev = rows[-n][1], None
