@@ -313,18 +313,29 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
 // mailbox post of the lambda-init statistic (max Hessian diagonal) after the first linearisation;
 // with npd > 0 it first folds in the pose blocks: per pose, the npd block partials of
 // pose_diag_kernel summed in order
-__global__ void post_kernel(Sys S, int K, int npd, unsigned long long seq) {
-  if (npd > 0) {
+__global__ __launch_bounds__(256) void post_kernel(Sys S, int K, int npd, unsigned long long seq) {
+  __shared__ double part[4][64];
+  if (npd > 0) {  // entry q = 6 pose + diagonal index: 4 waves each sum every 4th block partial
+    const int lane = threadIdx.x & 63, pt = threadIdx.x >> 6, nq6 = 6 * K;
     double mx = 0;
-    for (int q = threadIdx.x; q < 6 * K; q += blockDim.x) {  // q = 6 pose + diagonal entry
-      const int pa = q / 6, i = q - 6 * pa;
-      double s = 0;
-      for (int b = 0; b < npd; b++) s += S.partial2[((size_t)pa * npd + b) * 6 + i];
-      mx = fmax(mx, fabs(s));
+    for (int q0 = 0; q0 < nq6; q0 += 64) {
+      const int q = q0 + lane;
+      double sacc = 0;
+      if (q < nq6) {
+        const int pa = q / 6, i = q - 6 * pa;
+        const double* src = S.partial2 + (size_t)pa * npd * 6 + i;
+        for (int b = pt; b < npd; b += 4) sacc += src[(size_t)b * 6];
+      }
+      part[pt][lane] = sacc;
+      __syncthreads();
+      if (pt == 0 && q < nq6) mx = fmax(mx, fabs(((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]));
+      __syncthreads();
     }
+    if (pt == 0) {
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
-    if (threadIdx.x == 0) S.out[2] = fmax(S.out[2], mx);
+      for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+      if (lane == 0) S.out[2] = fmax(S.out[2], mx);
+    }
   }
   if (threadIdx.x != 0) return;
   Mail* m = S.mail;
@@ -951,18 +962,21 @@ __global__ __launch_bounds__(256) void pair_final_kernel(Active A, Sys S, double
 }
 
 // ---------------------------------------------------------------------------
-// Reduced camera system: Schur assembly + dense LDL^T + solve in one 1024-thread
-// workgroup, matrix in LDS (odd row stride), n = 6K <= kCholLdsMax.
+// Reduced camera system: Schur assembly + dense LDL^T + solve in one 256-thread workgroup,
+// matrix in LDS (odd row stride), n = 6K <= kCholLdsMax.
 //   assembly: S_ab = [a==b] lambda I + the pair's chunk sum (reduced by its last chunk),
-//             written straight into the lower triangle; bs_a, bp_a alongside;
-//   factor:   blocked by the 6x6 pose blocks, K steps of
-//   LDL^T (pivots need a reciprocal only: v_rcp_f64 + Newton, no sqrt / divide chains):
-//             (1) wave 0 factors the diagonal block in registers and publishes it in LDS,
-//             (2) panel rows solve x L_dd^T = a (one thread per row),
-//             (3) rank-6 update of the trailing lower triangle (32x32 thread grid);
-//   solves:   blocked forward / backward substitution in wave 0 (rhs in registers).
+//             written straight into the lower triangle; bp_a alongside, and bs as an extra
+//             bordered row n;
+//   factor:   blocked by the 6x6 pose blocks, K steps of LDL^T (pivots need a reciprocal
+//             only: v_rcp_f64 + Newton, no sqrt / divide chains):
+//             (1) wave 0 factors the diagonal block in registers (every lane, uniform),
+//             (2) panel rows solve x L_dd^T = a (one lane per row, the rhs row included:
+//                 it ends as z = D^-1 L^-1 bs, so there is no forward substitution),
+//             (3) rank-6 update of the trailing lower triangle (16x16 thread grid);
+//   solve:    backward substitution L^T x = z in wave 0, LDS-resident;
+//   poses:    the candidate T <- exp(xp) T and the pose part of the LM scale.
 // ---------------------------------------------------------------------------
-constexpr int kCholLdsMax = 132;  // n (n|1) + 3n + 15 n/6 doubles <= 160 KB of LDS
+constexpr int kCholLdsMax = 132;  // (n+1) ((n+1)|1) + 2n + 15 n/6 doubles <= 160 KB of LDS
 
 // 1/d to full precision: v_rcp_f64 + two Newton steps (no divide sequence on the chain)
 __device__ __forceinline__ double rcp64(double d) {
@@ -1005,49 +1019,69 @@ __device__ __forceinline__ bool ldl6(const double* Ld, int ld, double (&L6)[15],
   return ok;
 }
 
-__device__ __forceinline__ double readlane_f64(double v, int lane) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), lane);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+
+// pose pair index -> (a, b), a <= b, row-major upper triangle of K poses
+__device__ __forceinline__ void pair_of(int pr, int K, int& a, int& b) {
+  int base = 0;
+  a = 0;
+  while (pr >= base + (K - a)) {
+    base += K - a;
+    a++;
+  }
+  b = a + (pr - base);
 }
 
-__global__ __launch_bounds__(1024) void schur_solve_kernel(Problem P, Active A, Sys S, int n, double lambda) {
-  extern __shared__ double Al[];
-  __shared__ int bad[1];
-  const int ld = n | 1, K = n / 6;
-  double* xs = Al + (size_t)n * ld;  // [n] rhs -> forward result -> solution
-  double* rdg = xs + n;              // [n] 1/D
-  double* ddg = rdg + n;             // [n] D
-  double* Ldg = ddg + n;             // [K][15] strictly-lower parts of the (unit) diagonal blocks
-  const int tid = threadIdx.x, ty = tid >> 5, tx = tid & 31;
-  if (*S.fail) return;
-  for (int idx = tid; idx < A.npairs * 42; idx += 1024) {
-    const int pr = idx / 42, v = idx - 42 * pr;
-    const int a = A.pairs[2 * pr], b = A.pairs[2 * pr + 1];
-    const double s = S.pairfin[48 * pr + v];
-    if (v < 36) {
-      const int r = v / 6, cc = v - 6 * r;
-      if (a == b) {
-        if (cc <= r) Al[(6 * a + r) * ld + 6 * a + cc] = s + (r == cc ? lambda : 0.0);
-      } else {
-        Al[(6 * b + cc) * ld + 6 * a + r] = s;
+__global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, Sys S, int n, double lambda) {
+  extern __shared__ double Al[];     // rows 0..n: the matrix (lower triangle) + the bordered rhs row n
+  __shared__ int bad;
+  const int ld = (n + 1) | 1, K = n / 6;
+  double* z = Al + (size_t)n * ld;   // row n: bs -> z = D^-1 L^-1 bs -> solution x
+  double* rdg = Al + (size_t)(n + 1) * ld;  // [n] 1/D
+  double* ddg = rdg + n;                    // [n] D
+  double* Ldg = ddg + n;                    // [K][15] strictly-lower parts of the (unit) diagonal blocks
+  const int tid = threadIdx.x;
+  if (tid == 0) bad = 0;
+  // assembly: every thread issues its pairfin loads (8 at a time) before writing LDS; the
+  // fail flag is checked after them (it would otherwise gate every load)
+  const int nent = A.npairs * 42;
+  for (int q0 = tid; q0 < nent; q0 += 8 * 256) {
+    double v1[8], v2[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int idx = q0 + u * 256;
+      const int pr = idx / 42, v = idx - 42 * pr;
+      v1[u] = idx < nent ? S.pairfin[48 * pr + v] : 0.0;
+      v2[u] = (idx < nent && v >= 36) ? S.pairfin[48 * pr + v + 6] : 0.0;
+    }
+    if (*S.fail) return;  // uniform: a landmark block failed to invert
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int idx = q0 + u * 256;
+      if (idx >= nent) break;
+      const int pr = idx / 42, v = idx - 42 * pr;
+      int pa, pb;
+      pair_of(pr, K, pa, pb);
+      if (v < 36) {
+        const int r = v / 6, cc = v - 6 * r;
+        if (pa == pb) {
+          if (cc <= r) Al[(6 * pa + r) * ld + 6 * pa + cc] = v1[u] + (r == cc ? lambda : 0.0);
+        } else {
+          Al[(6 * pb + cc) * ld + 6 * pa + r] = v1[u];
+        }
+      } else if (pa == pb) {
+        const int r = v - 36;
+        S.bp[6 * pa + r] = v1[u];
+        z[6 * pa + r] = v1[u] - v2[u];
       }
-    } else if (a == b) {
-      const int r = v - 36;
-      S.bp[6 * a + r] = s;
-      xs[6 * a + r] = s - S.pairfin[48 * pr + v + 6];
     }
   }
-  if (tid == 0) *bad = 0;
   __syncthreads();
-  // factor + solve on 4 waves: fewer waves per barrier, the trailing updates are small
-  // (terminated waves drop out of the workgroup barrier)
-  if (tid >= 256) return;
+  // factor: blocked by the 6x6 pose blocks; the rhs row n is factored along (its panel rows
+  // become z = D^-1 L^-1 bs: no separate forward substitution)
   const int wv = tid >> 6, lane = tid & 63, fy = tid >> 4, fx = tid & 15;
   for (int s = 0; s < K; s++) {
-    const int c0 = 6 * s;
-    if (wv == 0) {  // (1) one wave factors the diagonal block (fp64 issue is 4 cycles per wave op)
+    const int c0 = 6 * s, r0 = c0 + 6;
+    if (wv == 0) {  // (1) diagonal block (every lane, uniform) + (2) panel rows, one per lane
       double L6[15], d6[6], r6[6];
       const bool ok = ldl6(Al + c0 * ld + c0, ld, L6, d6, r6);
       if (lane == 0) {
@@ -1058,34 +1092,33 @@ __global__ __launch_bounds__(1024) void schur_solve_kernel(Problem P, Active A, 
           rdg[c0 + k] = r6[k];
           ddg[c0 + k] = d6[k];
         }
-        if (!ok) *bad = 1;
+        if (!ok) bad = 1;
+      }
+      for (int i = r0 + lane; i <= n; i += 64) {  // x = a L_dd^-T D^-1 (unit L: no divides)
+        double* row = Al + i * ld + c0;
+        double w[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) w[k] = row[k];
+#pragma unroll
+        for (int k = 0, q = 0; k < 6; k++) {
+#pragma unroll
+          for (int l = 0; l < k; l++, q++) w[k] -= w[l] * L6[q];
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) row[k] = w[k] * r6[k];
       }
     }
     __syncthreads();
-    if (*bad) {  // LDS flag after the barrier: uniform
+    if (bad) {  // LDS flag after the barrier: uniform
       if (tid == 0) atomicOr(S.fail, 1);
       return;
     }
-    const int r0 = c0 + 6;
-    if (r0 + tid < n) {  // (2) panel row: x = a L_dd^-T D^-1 (unit L: no divides on the chain)
-      double* row = Al + (r0 + tid) * ld + c0;
-      double w[6];
-#pragma unroll
-      for (int k = 0; k < 6; k++) w[k] = row[k];
-#pragma unroll
-      for (int k = 0, q = 0; k < 6; k++) {
-#pragma unroll
-        for (int l = 0; l < k; l++, q++) w[k] -= w[l] * Ldg[15 * s + q];
-      }
-#pragma unroll
-      for (int k = 0; k < 6; k++) row[k] = w[k] * rdg[c0 + k];
-    }
-    __syncthreads();
-    for (int i = r0 + fy; i < n; i += 16) {  // (3) trailing update A22 -= X D X^T
+    for (int i = r0 + fy; i <= n; i += 16) {  // (3) trailing update A22 -= X D X^T (+ the rhs row)
       double wi[6];
 #pragma unroll
       for (int l = 0; l < 6; l++) wi[l] = Al[i * ld + c0 + l] * ddg[c0 + l];
-      for (int k = r0 + fx; k <= i; k += 16) {
+      const int kmax = min(i, n - 1);
+      for (int k = r0 + fx; k <= kmax; k += 16) {
         const double* xk = Al + k * ld + c0;
         double t = Al[i * ld + k];
 #pragma unroll
@@ -1095,92 +1128,40 @@ __global__ __launch_bounds__(1024) void schur_solve_kernel(Problem P, Active A, 
     }
     __syncthreads();
   }
-  // solves in wave 0 alone: rows lane, lane+64, lane+128 in registers, block values
-  // broadcast by readlane, no barriers
   if (wv != 0) return;
-  double x0 = lane < n ? xs[lane] : 0.0, x1 = lane + 64 < n ? xs[lane + 64] : 0.0,
-         x2 = lane + 128 < n ? xs[lane + 128] : 0.0;
-#define RSPL_GET(j) readlane_f64(((j) >> 6) == 0 ? x0 : (((j) >> 6) == 1 ? x1 : x2), (j) & 63)
-#define RSPL_PUT(j, v)                                   \
-  do {                                                   \
-    const bool me = lane == ((j) & 63);                  \
-    const int sl = (j) >> 6;                             \
-    x0 = (me && sl == 0) ? (v) : x0;                     \
-    x1 = (me && sl == 1) ? (v) : x1;                     \
-    x2 = (me && sl == 2) ? (v) : x2;                     \
-  } while (0)
-  for (int s = 0; s < K; s++) {  // L y = b (unit diagonal)
+  // backward substitution L^T x = z in wave 0 (LDS in program order within the wave)
+  for (int s = K - 1; s >= 0; s--) {
     const int c0 = 6 * s;
-    double y[6];
-#pragma unroll
-    for (int k = 0, q = 0; k < 6; k++) {
-      double v = RSPL_GET(c0 + k);
-#pragma unroll
-      for (int l = 0; l < k; l++, q++) v -= y[l] * Ldg[15 * s + q];
-      y[k] = v;
-    }
-#pragma unroll
-    for (int k = 0; k < 6; k++) RSPL_PUT(c0 + k, y[k]);
-    const int lo = c0 + 6;
-#define RSPL_FWD(xv, i)                                          \
-    if ((i) >= lo && (i) < n) {                                  \
-      const double* row = Al + (i) * ld + c0;                    \
-      double v = xv;                                             \
-      for (int l = 0; l < 6; l++) v -= row[l] * y[l];            \
-      xv = v;                                                    \
-    }
-    RSPL_FWD(x0, lane)
-    RSPL_FWD(x1, lane + 64)
-    RSPL_FWD(x2, lane + 128)
-#undef RSPL_FWD
-  }
-  // z = D^-1 y
-  if (lane < n) x0 *= rdg[lane];
-  if (lane + 64 < n) x1 *= rdg[lane + 64];
-  if (lane + 128 < n) x2 *= rdg[lane + 128];
-  for (int s = K - 1; s >= 0; s--) {  // L^T x = z (unit diagonal)
-    const int c0 = 6 * s;
-    double z[6];
+    double xb[6];
 #pragma unroll
     for (int k = 5; k >= 0; k--) {
-      double v = RSPL_GET(c0 + k);
+      double v = z[c0 + k];
 #pragma unroll
-      for (int l = k + 1; l < 6; l++) v -= z[l] * Ldg[15 * s + l * (l - 1) / 2 + k];
-      z[k] = v;
+      for (int l = k + 1; l < 6; l++) v -= Ldg[15 * s + l * (l - 1) / 2 + k] * xb[l];
+      xb[k] = v;
     }
+    for (int i = lane; i < c0; i += 64) {
+      double v = z[i];
 #pragma unroll
-    for (int k = 0; k < 6; k++) RSPL_PUT(c0 + k, z[k]);
-#define RSPL_BWD(xv, i)                                          \
-    if ((i) < c0) {                                              \
-      double v = xv;                                             \
-      for (int l = 0; l < 6; l++) v -= Al[(c0 + l) * ld + (i)] * z[l]; \
-      xv = v;                                                    \
+      for (int l = 0; l < 6; l++) v -= Al[(c0 + l) * ld + i] * xb[l];
+      z[i] = v;
     }
-    RSPL_BWD(x0, lane)
-    RSPL_BWD(x1, lane + 64)
-    RSPL_BWD(x2, lane + 128)
-#undef RSPL_BWD
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < 6; k++) z[c0 + k] = xb[k];
   }
-#undef RSPL_GET
-#undef RSPL_PUT
-  if (lane < n) S.x[lane] = x0;
-  if (lane + 64 < n) S.x[lane + 64] = x1;
-  if (lane + 128 < n) S.x[lane + 128] = x2;
+  for (int i = lane; i < n; i += 64) S.x[i] = z[i];
   // candidate poses (lane = pose; np <= 64): T <- exp(xp) T, fixed poses copied (ping-pong),
   // and the pose part of the LM scale x.(lambda x + bp)
   double sc = 0;
-  const int a = lane < P.np ? A.pidx[lane] : -1;
-  double xp[6];
-#pragma unroll
-  for (int r = 0; r < 6; r++) {  // gather x[6a + r] from the register-resident solution (all lanes shuffle)
-    const int j = 6 * max(a, 0) + r;
-    const double v0 = __shfl(x0, j & 63), v1 = __shfl(x1, j & 63), v2 = __shfl(x2, j & 63);
-    xp[r] = (j >> 6) == 0 ? v0 : ((j >> 6) == 1 ? v1 : v2);
-  }
   if (lane < P.np) {
+    const int a = A.pidx[lane];
     const double* Tp = P.T + 8 * lane;
     double* Tq = P.Tn + 8 * lane;
     if (a >= 0) {
+      double xp[6];
+#pragma unroll
+      for (int r = 0; r < 6; r++) xp[r] = z[6 * a + r];
       const SE3 r = se3_mul(se3_exp(xp), load_T(Tp));
       for (int k = 0; k < 4; k++) Tq[k] = r.q[k];
       for (int k = 0; k < 3; k++) Tq[4 + k] = r.t[k];
@@ -1539,7 +1520,7 @@ hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys&
 
 hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A) {
   const int npd = (A && A->K > 0 && A->Ea > 0) ? (A->Ea + 255) / 256 : 0;
-  hipLaunchKernelGGL(post_kernel, dim3(1), dim3(64), 0, s, S, A ? A->K : 0, npd, seq);
+  hipLaunchKernelGGL(post_kernel, dim3(1), dim3(256), 0, s, S, A ? A->K : 0, npd, seq);
   return hipGetLastError();
 }
 
@@ -1551,15 +1532,15 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
   if (n > 0 && n <= kCholLdsMax) {
     static bool attr = false;
     const int nm = kCholLdsMax;
-    const size_t max_bytes = sizeof(double) * ((size_t)nm * (nm | 1) + 3 * nm + 15 * (nm / 6));
+    const size_t max_bytes = sizeof(double) * ((size_t)(nm + 1) * ((nm + 1) | 1) + 2 * nm + 15 * (nm / 6));
     if (!attr) {
       hipError_t e = hipFuncSetAttribute((const void*)schur_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                          (int)max_bytes);
       if (e != hipSuccess) return e;
       attr = true;
     }
-    const size_t bytes = sizeof(double) * ((size_t)n * (n | 1) + 3 * n + 15 * (n / 6));
-    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(1024), bytes, s, P, A, S, n, lambda);
+    const size_t bytes = sizeof(double) * ((size_t)(n + 1) * ((n + 1) | 1) + 2 * n + 15 * (n / 6));
+    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), bytes, s, P, A, S, n, lambda);
     hipLaunchKernelGGL(update_errors_kernel, dim3(update_errors_blocks(A)), dim3(256), 0, s, P, L, A, S, lambda, seq);
     return hipGetLastError();
   }
