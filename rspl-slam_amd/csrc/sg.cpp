@@ -34,6 +34,9 @@ struct rspl_sg {
   _Float16 *hwqkv, *hwm, *hw1, *hw2, *hwf;
   // activations
   float *kin, *h1, *h2, *X, *QKV, *O, *MSG, *HID, *cpl, *Z, *val0;
+  // RSPL_PREC_FP16 GNN activations: fp16 shadow of X, Q | K, V^T per head, messages, hidden
+  _Float16 *Xh, *QKh, *Vth, *Oh, *MSGh, *HIDh;
+  int ldv = 0;  // token stride of Vth (nmax rounded up to the 32-key attention tile; zero padded)
   unsigned long long* part;
   unsigned* err;
   unsigned sk_seq = 0;
@@ -79,6 +82,8 @@ void carve(F& ar, rspl_sg* s) {
   take(s->hw1, (size_t)kLayers * 512 * 512); take(s->hw2, (size_t)kLayers * 512 * 256); take(s->hwf, 256 * 256);
   take(s->kin, T * kKencIn); take(s->h1, T * 256); take(s->h2, T * 256);
   take(s->X, T * 256); take(s->QKV, T * 768); take(s->O, T * 256); take(s->MSG, T * 256); take(s->HID, T * 512);
+  take(s->Xh, T * 256); take(s->QKh, T * 512); take(s->Vth, (size_t)B * 2 * 256 * s->ldv); take(s->Oh, T * 256);
+  take(s->MSGh, T * 256); take(s->HIDh, T * 512);
   take(s->cpl, 2 * B * ld * ld); take(s->Z, 2 * B * ld * ld); take(s->part, B * 2 * s->G * ld);
   take(s->cn0, 2 * B); take(s->cn1, 2 * B);
   take(s->err, B);
@@ -222,6 +227,7 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
   s->B = s->cfg.max_batch;
   s->nmax = cfg->max_keypoints;  // output stride per pair (rspl.h)
   s->ld = s->nmax + 1;
+  s->ldv = (s->nmax + 31) / 32 * 32;
   {  // sinkhorn workgroups per pair: ~26 rows each, a power of two (compile-time fan-in of the exchange)
     const int g0 = std::max(1, (s->ld + 25) / 26);
     s->G = 1;
@@ -236,7 +242,8 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
   carve(sz, s);
   if ((rc = s->arena.reserve(sz.used))) { delete s; return rc; }
   carve(s->arena, s);
-  if (hipMemset(s->part, 0, sizeof(unsigned long long) * 2 * s->B * s->G * s->ld) != hipSuccess) {
+  if (hipMemset(s->part, 0, sizeof(unsigned long long) * 2 * s->B * s->G * s->ld) != hipSuccess ||
+      hipMemset(s->Vth, 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess) {
     set_error("sinkhorn exchange buffer init failed");
     rspl_sg_destroy(s);
     return RSPL_E_DEVICE;
@@ -343,7 +350,35 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
   }
   s->timer.mark(1, st);
   // AttentionalGNN (superglue.py:165-173): ['self', 'cross'] * 9; both images read pre-layer descs
-  for (int l = 0; l < kLayers; l++) {
+  if (h16) {  // fp16 activations end to end (X itself stays fp32: the residual stream)
+    RSPL_HIP(sg::to_half(s->X, s->Xh, (size_t)T * 256, st));
+    auto gh = [&](const _Float16* A, int lda, const _Float16* W, int N, int K, const float* bias) {
+      sg::GemmHArgs g{};
+      g.A = A; g.lda = lda; g.ksplit = K; g.B = W; g.ldb = K; g.bias = bias; g.M = T; g.N = N; g.K = K;
+      g.nmax = nm; g.ldv = s->ldv;
+      return g;
+    };
+    for (int l = 0; l < kLayers; l++) {
+      sg::GemmHArgs q = gh(s->Xh, 256, s->hwqkv + (size_t)l * 256 * 768, 768, 256, s->bqkv + (size_t)l * 768);
+      q.C16 = s->QKh; q.ldc16 = 512; q.Vt = s->Vth;
+      RSPL_HIP(sg::gemm_h(q, 4, st));
+      sg::AttnHArgs at{};
+      at.QK = s->QKh; at.Vt = s->Vth; at.O = s->Oh; at.n0 = d_n0; at.n1 = d_n1; at.nmax = nm; at.ldv = s->ldv;
+      at.cross = l & 1;
+      RSPL_HIP(sg::attention_h(at, B, st));
+      sg::GemmHArgs mg = gh(s->Oh, 256, s->hwm + (size_t)l * 65536, 256, 256, s->bm + (size_t)l * 256);
+      mg.C16 = s->MSGh; mg.ldc16 = 256;
+      RSPL_HIP(sg::gemm_h(mg, 1, st));
+      sg::GemmHArgs m1 = gh(s->Xh, 256, s->hw1 + (size_t)l * 512 * 512, 512, 512, s->b1 + (size_t)l * 512);
+      m1.A2 = s->MSGh; m1.lda2 = 256; m1.ksplit = 256;  // torch.cat([x, message], dim=1)
+      m1.C16 = s->HIDh; m1.ldc16 = 512;
+      RSPL_HIP(sg::gemm_h(m1, 2, st));
+      sg::GemmHArgs m2 = gh(s->HIDh, 512, s->hw2 + (size_t)l * 512 * 256, 256, 512, s->b2 + (size_t)l * 256);
+      m2.C32 = s->X; m2.ldc32 = 256; m2.C16 = s->Xh; m2.ldc16 = 256;
+      RSPL_HIP(sg::gemm_h(m2, 3, st));
+    }
+  }
+  for (int l = 0; l < kLayers && !h16; l++) {
     RSPL_HIP(sg::gemm(G_(s->X, 256, s->wqkv + (size_t)l * 256 * 768, 768, s->bqkv + (size_t)l * 768, s->QKV, 768, T,
                          768, 256, 0, h16 ? s->hwqkv + (size_t)l * 256 * 768 : nullptr), 1, st));
     sg::AttnArgs at{};
@@ -362,7 +397,14 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
   s->timer.mark(2, st);
   // final_proj + scores / descriptor_dim**.5 (superglue.py:295-300)
   float* MD = s->MSG;
-  RSPL_HIP(sg::gemm(G_(s->X, 256, s->wf, 256, s->bf, MD, 256, T, 256, 256, 0, h16 ? s->hwf : nullptr), 1, st));
+  if (h16) {
+    sg::GemmHArgs g{};
+    g.A = s->Xh; g.lda = 256; g.ksplit = 256; g.B = s->hwf; g.ldb = 256; g.bias = s->bf; g.M = T; g.N = 256; g.K = 256;
+    g.C32 = MD; g.ldc32 = 256;
+    RSPL_HIP(sg::gemm_h(g, 0, st));
+  } else {
+    RSPL_HIP(sg::gemm(G_(s->X, 256, s->wf, 256, s->bf, MD, 256, T, 256, 256, 0, nullptr), 1, st));
+  }
   {
     if (pst != st && s->calls > 2) RSPL_HIP(hipStreamWaitEvent(st, s->ev_sink[par], 0));
     sg::GemmArgs g = G_(MD, 256, MD + (size_t)nm * 256, 256, nullptr, cpl, s->ld, nm, nm, 256, 0);

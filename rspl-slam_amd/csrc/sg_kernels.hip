@@ -301,6 +301,238 @@ __global__ void to_half_t_kernel(const float* W, int K, int N, _Float16* Wt) {
 }
 
 // ---------------------------------------------------------------------------
+// fp16 GNN GEMM: one 64x64 tile per 256-thread workgroup (4 waves, 32x32 each on
+// v_mfma_f32_32x32x16_f16).  The whole K panel of A and B (K <= 512) is staged in LDS
+// (rows padded by 16 B against bank conflicts) with every global load issued before the
+// first LDS write: one memory round trip per tile, then back-to-back MFMAs.
+// ---------------------------------------------------------------------------
+constexpr int kGhMaxK = 512;
+
+template <int MODE>
+__global__ __launch_bounds__(256) void gemm_hh_kernel(GemmHArgs a) {
+  extern __shared__ _Float16 lds_h[];
+  const int K = a.K, ldk = K + 8, kc = K / 8, nch = 64 * kc;
+  _Float16* As = lds_h;
+  _Float16* Bs = lds_h + 64 * ldk;
+  const int m0 = blockIdx.y * 64, n0 = blockIdx.x * 64;
+  const int tid = threadIdx.x;
+  constexpr int kMaxCh = 64 * kGhMaxK / 8 / 256;  // 16-byte chunks per thread per operand
+  uint4 ra[kMaxCh], rb[kMaxCh];
+#pragma unroll
+  for (int u = 0; u < kMaxCh; u++) {
+    const int c = tid + 256 * u;
+    uint4 va = make_uint4(0, 0, 0, 0), vb = va;
+    if (c < nch) {
+      const int row = c / kc, k8 = (c - row * kc) * 8;
+      const int m = m0 + row, n = n0 + row;
+      if (m < a.M) {
+        const _Float16* src = (a.A2 && k8 >= a.ksplit) ? a.A2 + (size_t)m * a.lda2 + (k8 - a.ksplit)
+                                                        : a.A + (size_t)m * a.lda + k8;
+        va = *reinterpret_cast<const uint4*>(src);
+      }
+      if (n < a.N) vb = *reinterpret_cast<const uint4*>(a.B + (size_t)n * a.ldb + k8);
+    }
+    ra[u] = va;
+    rb[u] = vb;
+  }
+#pragma unroll
+  for (int u = 0; u < kMaxCh; u++) {
+    const int c = tid + 256 * u;
+    if (c < nch) {
+      const int row = c / kc, k8 = (c - row * kc) * 8;
+      *reinterpret_cast<uint4*>(As + row * ldk + k8) = ra[u];
+      *reinterpret_cast<uint4*>(Bs + row * ldk + k8) = rb[u];
+    }
+  }
+  __syncthreads();
+  const int lane = tid & 63, wv = tid >> 6, r32 = lane & 31, kh = lane >> 5;
+  const int wm = 32 * (wv >> 1), wn = 32 * (wv & 1);
+  const _Float16* ap = As + (wm + r32) * ldk + 8 * kh;
+  const _Float16* bp = Bs + (wn + r32) * ldk + 8 * kh;
+  floatx16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; r++) acc[r] = 0.f;
+  const int ns = K / 16;
+  int st = 0;
+  for (; st + 4 <= ns; st += 4) {
+    half8 av[4], bv[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      av[u] = *reinterpret_cast<const half8*>(ap + 16 * (st + u));
+      bv[u] = *reinterpret_cast<const half8*>(bp + 16 * (st + u));
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) acc = mfma16(av[u], bv[u], acc);
+  }
+  for (; st < ns; st++)
+    acc = mfma16(*reinterpret_cast<const half8*>(ap + 16 * st), *reinterpret_cast<const half8*>(bp + 16 * st), acc);
+  const int n = n0 + wn + r32;
+  if (n >= a.N) return;
+  const float bias = a.bias ? a.bias[n] : 0.f;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const int m = m0 + wm + (r & 3) + 8 * (r >> 2) + 4 * kh;
+    if (m >= a.M) continue;
+    const float v = acc[r] + bias;
+    if constexpr (MODE == 0) {
+      a.C32[(size_t)m * a.ldc32 + n] = v;
+    } else if constexpr (MODE == 1) {
+      a.C16[(size_t)m * a.ldc16 + n] = (_Float16)v;
+    } else if constexpr (MODE == 2) {
+      a.C16[(size_t)m * a.ldc16 + n] = (_Float16)(v > 0.f ? v : 0.f);
+    } else if constexpr (MODE == 3) {
+      float* d = a.C32 + (size_t)m * a.ldc32 + n;
+      const float x = *d + v;
+      *d = x;
+      a.C16[(size_t)m * a.ldc16 + n] = (_Float16)x;
+    } else {
+      if (n < 512) {
+        a.C16[(size_t)m * a.ldc16 + n] = (_Float16)v;
+      } else {
+        const int c = n - 512, set = m / a.nmax, tok = m - set * a.nmax;
+        a.Vt[((size_t)(set * 4 + (c >> 6)) * 64 + (c & 63)) * a.ldv + tok] = (_Float16)v;
+      }
+    }
+  }
+}
+
+__global__ void to_half_kernel(const float* x, _Float16* y, size_t n) {
+  const size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) y[i] = (_Float16)x[i];
+}
+
+// ---------------------------------------------------------------------------
+// fp16 multi-head attention (flash, online softmax), one head and 32 queries per
+// workgroup, the 4 waves splitting the key tiles.  Swapped product S^T = K Q^T on
+// v_mfma_f32_32x32x16_f16 (keys on registers, queries on lanes: in-lane softmax + one
+// xor-32); P^T feeds O^T = V^T P^T as the B operand straight from registers: k-step j,
+// lane group kh takes the keys of its registers 8j..8j+7, i.e. runs [16j+4kh, +4) and
+// [16j+8+4kh, +4), and V^T is read with exactly that key order from Vt (two 8-byte loads).
+// K/V fragments come from global memory, the next tile prefetched during the current one.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void attn_h_kernel(AttnHArgs a) {
+  __shared__ float Om[4][64][33];
+  __shared__ float Ml[4][32], Ll[4][32];
+  const int pz = blockIdx.z, p = pz >> 1, img = pz & 1;
+  const int simg = a.cross ? 1 - img : img;
+  const int nq = img ? a.n1[p] : a.n0[p];
+  const int nk = simg ? a.n1[p] : a.n0[p];
+  const int q0 = blockIdx.x * 32;
+  if (q0 >= nq || nk <= 0) return;
+  const int h = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, c = lane & 31, kh = lane >> 5;
+  const int qset = p * 2 + img, kset = p * 2 + simg;
+  const _Float16* Qb = a.QK + (size_t)qset * a.nmax * 512 + h * 64;
+  const _Float16* Kb = a.QK + (size_t)kset * a.nmax * 512 + 256 + h * 64;
+  const _Float16* Vb = a.Vt + (size_t)(kset * 4 + h) * 64 * a.ldv;
+  half8 qf[4];
+  {
+    const _Float16* qr = Qb + (size_t)min(q0 + c, nq - 1) * 512 + 8 * kh;
+#pragma unroll
+    for (int s = 0; s < 4; s++) qf[s] = *reinterpret_cast<const half8*>(qr + 16 * s);
+  }
+  floatx16 o0, o1;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    o0[r] = 0.f;
+    o1[r] = 0.f;
+  }
+  float m_run = -INFINITY, l_run = 0.f;
+  const int ntiles = (nk + 31) / 32;
+  half8 kf[4], vf[2][2];
+  auto fetch = [&](int t) {
+    const _Float16* kr = Kb + (size_t)min(t * 32 + c, nk - 1) * 512 + 8 * kh;
+#pragma unroll
+    for (int s = 0; s < 4; s++) kf[s] = *reinterpret_cast<const half8*>(kr + 16 * s);
+#pragma unroll
+    for (int dt = 0; dt < 2; dt++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        const _Float16* vr = Vb + (size_t)(32 * dt + c) * a.ldv + t * 32 + 16 * j + 4 * kh;
+        const uint2 lo = *reinterpret_cast<const uint2*>(vr), hi = *reinterpret_cast<const uint2*>(vr + 8);
+        uint4 w = make_uint4(lo.x, lo.y, hi.x, hi.y);
+        vf[dt][j] = *reinterpret_cast<const half8*>(&w);
+      }
+  };
+  if (wv < ntiles) fetch(wv);
+  for (int t = wv; t < ntiles; t += 4) {
+    half8 kc_[4], vc[2][2];
+#pragma unroll
+    for (int s = 0; s < 4; s++) kc_[s] = kf[s];
+#pragma unroll
+    for (int dt = 0; dt < 2; dt++)
+#pragma unroll
+      for (int j = 0; j < 2; j++) vc[dt][j] = vf[dt][j];
+    if (t + 4 < ntiles) fetch(t + 4);
+    floatx16 st;
+#pragma unroll
+    for (int r = 0; r < 16; r++) st[r] = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; s++) st = mfma16(kc_[s], qf[s], st);
+    float x[16];
+    float mx = -INFINITY;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      const int key = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+      x[r] = key < nk ? st[r] * 0.125f : -INFINITY;  // scores / dim**.5 (superglue.py:90)
+      mx = fmaxf(mx, x[r]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m_run, mx);
+    const float alpha = __expf(m_run - m_new);
+    float sum = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      x[r] = __expf(x[r] - m_new);
+      sum += x[r];
+    }
+    sum += __shfl_xor(sum, 32);
+    l_run = l_run * alpha + sum;
+    m_run = m_new;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      o0[r] *= alpha;
+      o1[r] *= alpha;
+    }
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+      half8 pf;
+#pragma unroll
+      for (int u = 0; u < 8; u++) pf[u] = (_Float16)x[8 * j + u];
+      o0 = mfma16(vc[0][j], pf, o0);
+      o1 = mfma16(vc[1][j], pf, o1);
+    }
+  }
+  // merge the 4 waves' partial (m, l, O^T) per query
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const int d = (r & 3) + 8 * (r >> 2) + 4 * kh;
+    Om[wv][d][c] = o0[r];
+    Om[wv][32 + d][c] = o1[r];
+  }
+  if (kh == 0) {
+    Ml[wv][c] = m_run;
+    Ll[wv][c] = l_run;
+  }
+  __syncthreads();
+  _Float16* O = a.O + (size_t)qset * a.nmax * 256 + h * 64;
+  for (int idx = tid; idx < 32 * 64; idx += 256) {
+    const int q = idx >> 6, d = idx & 63;
+    float M = -INFINITY;
+#pragma unroll
+    for (int w = 0; w < 4; w++) M = fmaxf(M, Ml[w][q]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int w = 0; w < 4; w++) {
+      const float e = (Ml[w][q] == -INFINITY) ? 0.f : __expf(Ml[w][q] - M);
+      L += e * Ll[w][q];
+      acc += e * Om[w][d][q];
+    }
+    if (q0 + q < nq) O[(size_t)(q0 + q) * 256 + d] = (_Float16)(acc / L);
+  }
+}
+
+// ---------------------------------------------------------------------------
 // process_input + NormalizeKeypoints: one wave per token.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
@@ -837,6 +1069,43 @@ hipError_t gemm(const GemmArgs& a, int batch, hipStream_t s) {
   } else {
     hipLaunchKernelGGL(gemm_sk_kernel<0>, grid, dim3(256), 0, s, a);
   }
+  return hipGetLastError();
+}
+
+template <int MODE>
+static hipError_t gemm_h_launch(const GemmHArgs& a, hipStream_t s) {
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)gemm_hh_kernel<MODE>,
+                                             hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)(2 * 64 * (kGhMaxK + 8) * sizeof(_Float16)));
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  dim3 grid((a.N + 63) / 64, (a.M + 63) / 64);
+  hipLaunchKernelGGL(gemm_hh_kernel<MODE>, grid, dim3(256), 2 * 64 * (a.K + 8) * sizeof(_Float16), s, a);
+  return hipGetLastError();
+}
+
+hipError_t gemm_h(const GemmHArgs& a, int mode, hipStream_t s) {
+  if (a.K > kGhMaxK || a.K % 16 != 0) return hipErrorInvalidValue;
+  switch (mode) {
+    case 0: return gemm_h_launch<0>(a, s);
+    case 1: return gemm_h_launch<1>(a, s);
+    case 2: return gemm_h_launch<2>(a, s);
+    case 3: return gemm_h_launch<3>(a, s);
+    case 4: return gemm_h_launch<4>(a, s);
+  }
+  return hipErrorInvalidValue;
+}
+
+hipError_t attention_h(const AttnHArgs& a, int B, hipStream_t s) {
+  hipLaunchKernelGGL(attn_h_kernel, dim3((a.nmax + 31) / 32, 4, B * 2), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t to_half(const float* x, _Float16* y, size_t n, hipStream_t s) {
+  if (n) hipLaunchKernelGGL(to_half_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, x, y, n);
   return hipGetLastError();
 }
 

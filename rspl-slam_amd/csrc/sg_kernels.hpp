@@ -31,6 +31,41 @@ struct GemmArgs {
   int count_stride;  // ints between consecutive batches in mcount/ncount
 };
 
+// fp16 GNN GEMM (RSPL_PREC_FP16): C = epi(A B^T + bias), A [M][K] fp16 (columns [ksplit, K)
+// from A2), B [N][K] fp16 (the transposed weights), K <= 512 and a multiple of 16.
+//   mode 0: C32 = v          1: C16 = v          2: C16 = relu(v)
+//        3: C32 += v, C16 = fp16(C32)  (the residual stream and its fp16 shadow)
+//        4: QKV: channels [0, 512) -> C16 (Q | K, row stride ldc16); [512, 768) (V) ->
+//           Vt[set][head][dim][token] (token = m % nmax, row stride ldv), so attention can
+//           feed V^T to the MFMA straight from memory
+struct GemmHArgs {
+  const _Float16* A;
+  const _Float16* A2;
+  int lda, lda2, ksplit;
+  const _Float16* B;
+  int ldb;
+  const float* bias;
+  int M, N, K;
+  float* C32;
+  int ldc32;
+  _Float16* C16;
+  int ldc16;
+  _Float16* Vt;
+  int nmax, ldv;
+};
+
+// fp16 multi-head attention: QK [set][nmax][512] (Q | K, head-contiguous), Vt as above,
+// O [set][nmax][256] fp16
+struct AttnHArgs {
+  const _Float16* QK;
+  const _Float16* Vt;
+  _Float16* O;
+  const int* n0;
+  const int* n1;
+  int nmax, ldv;
+  int cross;
+};
+
 struct PrepArgs {
   const double* f0;   // [B][stride][259]
   const double* f1;
@@ -92,6 +127,10 @@ struct DecodeArgs {
 hipError_t gemm(const GemmArgs& a, int batch, hipStream_t s);
 // Wt[n][k] = (fp16) W[k][n] for a [K][N] fp32 weight (one-time, at create)
 hipError_t to_half_t(const float* W, int K, int N, _Float16* Wt, hipStream_t s);
+hipError_t gemm_h(const GemmHArgs& a, int mode, hipStream_t s);
+hipError_t attention_h(const AttnHArgs& a, int B, hipStream_t s);
+// fp32 -> fp16, n elements
+hipError_t to_half(const float* x, _Float16* y, size_t n, hipStream_t s);
 hipError_t prep(const PrepArgs& a, hipStream_t s);
 hipError_t attention(const AttnArgs& a, int B, hipStream_t s);
 hipError_t bins(const BinsArgs& a, int B, hipStream_t s);
