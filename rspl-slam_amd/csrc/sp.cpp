@@ -2,6 +2,7 @@
 // Mirrors SuperPoint::build / infer / process_output (src/super_point.cpp:89-389):
 // weights are loaded and re-laid-out once at create; every buffer is carved from
 // one arena sized for max_batch x max_height x max_width.
+#include <algorithm>
 #include <cstring>
 #include <vector>
 
@@ -10,7 +11,8 @@
 
 using namespace rspl;
 
-static constexpr int kCandCap = 16384;  // NMS survivors above threshold per image (LDS bitonic top-k)
+static constexpr int kCandCap = 16384;  // candidates sorted whole in LDS (bitonic top-k); also the keep-all and
+                                        // max_keypoints limits.  More candidates (large images) are radix-selected.
 
 struct rspl_sp {
   rspl_sp_config cfg{};
@@ -25,6 +27,7 @@ struct rspl_sp {
   float *actA, *actB, *cells, *scores, *nms, *desc;
   unsigned long long* cand;
   int* cand_count;
+  int cand_cap = 0;  // candidate buffer per image: NMS survivors of the largest configured image
   unsigned* sel;
   int* sel_count;
   int32_t* counts;
@@ -85,7 +88,7 @@ void carve(F& ar, rspl_sp* s, int B, int H, int W, int cap) {
   take(s->scores, B * HW);
   take(s->nms, B * HW);
   take(s->desc, B * P * 256);
-  take(s->cand, (size_t)B * kCandCap);
+  take(s->cand, (size_t)B * s->cand_cap);
   take(s->cand_count, B);
   take(s->sel, (size_t)B * kCandCap);
   take(s->sel_count, B);
@@ -112,7 +115,10 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
   s->cfg = *cfg;
   if (s->cfg.max_batch < 1) s->cfg.max_batch = 1;
   const int B = s->cfg.max_batch, H = cfg->max_height, W = cfg->max_width;
+  RSPL_CHECK_ARG(cfg->max_keypoints <= kCandCap, "max_keypoints must be <= %d", kCandCap);
   s->feat_cap = cfg->max_keypoints > 0 ? cfg->max_keypoints : kCandCap;
+  // simple_nms keeps 9x9 local maxima: one survivor per 4x4 pixels is a generous bound (plateaus)
+  s->cand_cap = std::max(kCandCap, H * W / 16);
   Sizer sz;
   carve(sz, s, B, H, W, s->feat_cap);
   if ((rc = s->arena.reserve(sz.used))) { delete s; return rc; }
@@ -284,13 +290,13 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
   s->timer.mark(4, st);
   RSPL_HIP(hipMemsetAsync(s->cand_count, 0, sizeof(int) * B, st));
   NmsArgs n{};
-  n.scores = s->scores; n.nms_out = s->nms; n.cand = s->cand; n.cand_count = s->cand_count; n.cand_cap = kCandCap;
+  n.scores = s->scores; n.nms_out = s->nms; n.cand = s->cand; n.cand_count = s->cand_count; n.cand_cap = s->cand_cap;
   n.H = H; n.W = W; n.threshold = s->cfg.keypoint_threshold; n.border = s->cfg.remove_borders;
   RSPL_HIP(nms(n, B, st));
   // top-k (super_point.cpp:255-274)
   s->timer.mark(5, st);
   TopkArgs t{};
-  t.cand = s->cand; t.cand_count = s->cand_count; t.cand_cap = kCandCap; t.k = k;
+  t.cand = s->cand; t.cand_count = s->cand_count; t.cand_cap = s->cand_cap; t.lds_cap = kCandCap; t.k = k;
   t.sel = s->sel; t.sel_count = s->sel_count; t.sel_cap = kCandCap;
   RSPL_HIP(topk(t, B, st));
   // descriptor sampling + packing (super_point.cpp:276-387)
@@ -320,8 +326,12 @@ extern "C" int rspl_sp_infer(rspl_sp* s, const uint8_t* image, int H, int W, int
   RSPL_HIP(hipStreamSynchronize(s->stream));
   int cand = 0;
   RSPL_HIP(hipMemcpy(&cand, s->cand_count, sizeof(int), hipMemcpyDeviceToHost));
-  if (cand > kCandCap) {
-    set_error("%d candidates above threshold exceed the top-k capacity %d", cand, kCandCap);
+  if (cand > s->cand_cap) {
+    set_error("%d candidates above threshold exceed the candidate buffer %d", cand, s->cand_cap);
+    return RSPL_E_CAPACITY;
+  }
+  if (s->cfg.max_keypoints <= 0 && cand > kCandCap) {
+    set_error("keep-all (max_keypoints <= 0): %d candidates exceed %d", cand, kCandCap);
     return RSPL_E_CAPACITY;
   }
   const int n = s->h_counts[0];

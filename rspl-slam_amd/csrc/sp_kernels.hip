@@ -565,23 +565,66 @@ __global__ __launch_bounds__(256) void nms_kernel(NmsArgs a) {
 // std::sort, src/super_point.cpp:255-260).  If n <= k the reference does not
 // sort: keypoints stay in row-major scan order (flat index asc).
 // ---------------------------------------------------------------------------
+// Keys are (~score bits) << 32 | flat index: ascending key = descending score, ties by flat
+// index.  Up to lds_cap candidates are sorted whole in LDS (bitonic).  With more (large images)
+// and k > 0, an MSB-first 8-bit radix select over the 64-bit keys (LDS histograms) finds the
+// exact k-th key first; the k keys at or below it are compacted into LDS and sorted there.
 __global__ __launch_bounds__(1024) void topk_kernel(TopkArgs a) {
   extern __shared__ unsigned long long keys[];
+  __shared__ unsigned hist[256];
+  __shared__ unsigned long long sel_prefix, sel_mask;
+  __shared__ unsigned sel_want, sel_n;
   const int bi = blockIdx.x;
   int n = a.cand_count[bi];
   if (n > a.cand_cap) n = a.cand_cap;
   const bool sorted_by_score = (a.k != -1 && a.k < n);
+  const unsigned long long* src = a.cand + (size_t)bi * a.cand_cap;
+  if (n > a.lds_cap && !sorted_by_score) {  // keep-all beyond the LDS sort: reported by the host
+    if (threadIdx.x == 0) a.sel_count[bi] = 0;
+    return;
+  }
+  if (n > a.lds_cap) {
+    if (threadIdx.x == 0) {
+      sel_prefix = 0;
+      sel_mask = 0;
+      sel_want = (unsigned)a.k;
+      sel_n = 0;
+    }
+    for (int shift = 56; shift >= 0; shift -= 8) {
+      for (int i = threadIdx.x; i < 256; i += blockDim.x) hist[i] = 0;
+      __syncthreads();
+      const unsigned long long pre = sel_prefix, msk = sel_mask;
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        const unsigned long long key = src[i];
+        if ((key & msk) == pre) atomicAdd(&hist[(key >> shift) & 255], 1u);
+      }
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        unsigned below = 0, d = 0;
+        while (d < 255 && below + hist[d] < sel_want) below += hist[d++];
+        sel_want -= below;
+        sel_prefix |= (unsigned long long)d << shift;
+        sel_mask |= 0xFFull << shift;
+      }
+      __syncthreads();
+    }
+    const unsigned long long kth = sel_prefix;  // keys are unique: exactly k keys are <= kth
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const unsigned long long key = src[i];
+      if (key <= kth) keys[atomicAdd(&sel_n, 1u)] = key;
+    }
+    __syncthreads();
+    n = a.k;
+  } else {
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      unsigned long long key = src[i];
+      if (!sorted_by_score) key &= 0xFFFFFFFFull;  // flat index only
+      keys[i] = key;
+    }
+  }
   int L = 1;
   while (L < n) L <<= 1;
-  const unsigned long long* src = a.cand + (size_t)bi * a.cand_cap;
-  for (int i = threadIdx.x; i < L; i += blockDim.x) {
-    unsigned long long key = ~0ull;
-    if (i < n) {
-      key = src[i];
-      if (!sorted_by_score) key &= 0xFFFFFFFFull;  // flat index only
-    }
-    keys[i] = key;
-  }
+  for (int i = n + threadIdx.x; i < L; i += blockDim.x) keys[i] = ~0ull;
   __syncthreads();
   for (int size = 2; size <= L; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
@@ -716,7 +759,7 @@ hipError_t nms(const NmsArgs& a, int B, hipStream_t s) {
 
 hipError_t topk(const TopkArgs& a, int B, hipStream_t s) {
   int L = 1;
-  while (L < a.cand_cap) L <<= 1;
+  while (L < a.lds_cap) L <<= 1;
   static bool attr_set = false;
   if (!attr_set) {
     hipError_t e = hipFuncSetAttribute((const void*)topk_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -49,7 +49,8 @@ struct NmsArgs {
 struct TopkArgs {
   const unsigned long long* cand;
   const int* cand_count;
-  int cand_cap;
+  int cand_cap;          // candidate buffer stride per image
+  int lds_cap;           // candidates sorted whole in LDS; beyond it (k > 0) radix select first
   int k;                 // -1 = keep all
   unsigned* sel;         // [B][sel_cap] flat indices
   int* sel_count;        // [B]
