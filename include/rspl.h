@@ -273,6 +273,63 @@ int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out);
 int rspl_ba_local(rspl_ba* ba, const rspl_ba_problem* problem, rspl_ba_result* result);
 void rspl_ba_destroy(rspl_ba* ba);
 
+/* ------------------------------------------------------------------------ */
+/* Tracking pose optimisation: FrameOptimization                            */
+/* (src/g2o_optimization/g2o_optimization.cc:256-398, declared at           */
+/* include/g2o_optimization/g2o_optimization.h:20-22; called per frame by   */
+/* MapBuilder::FramePoseOptimization, src/map_builder.cc:583).  One pose     */
+/* vertex, fixed world points, unary EdgeSE3ProjectXYZOnlyPose /            */
+/* EdgeStereoSE3ProjectXYZOnlyPose edges with Huber kernels; 4 rounds of    */
+/* optimize(10) from the initial pose with chi2 re-classification, kernels  */
+/* dropped for the last round.  A batch of independent frames (one sequence */
+/* each, or many sequences per GPU) runs in ONE kernel launch, one wavefront */
+/* per frame.                                                               */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int n_cameras;
+  const double* cameras;        /* [n][5] fx, fy, cx, cy, bf */
+  double pose_q[4];             /* initial T_wc rotation (x, y, z, w) */
+  double pose_p[3];             /* initial T_wc translation */
+  int n_points;
+  const double* points;         /* [n][3] world positions (Position3d, fixed) */
+  int n_mono;                   /* MonoPointConstraint: id_point, id_camera, keypoint */
+  const int32_t* mono_point;
+  const int32_t* mono_camera;   /* may be NULL -> camera 0 */
+  const double* mono_obs;       /* [n][2] */
+  const uint8_t* mono_inlier_in;   /* Constraint::inlier on entry; NULL = all true (map_builder.cc:560) */
+  int n_stereo;                 /* StereoPointConstraint */
+  const int32_t* stereo_point;
+  const int32_t* stereo_camera;
+  const double* stereo_obs;     /* [n][3] u, v, u_right */
+  const uint8_t* stereo_inlier_in;
+  double th_mono_point, th_stereo_point;  /* OptimizationConfig (tracking) */
+} rspl_frame_problem;
+
+typedef struct {
+  double pose_q[4];             /* optimised T_wc (x, y, z, w) */
+  double pose_p[3];
+  uint8_t* mono_inlier;         /* [n_mono] Constraint::inlier on exit (may be NULL) */
+  uint8_t* stereo_inlier;
+  int n_inliers;                /* FrameOptimization's return value */
+  int rounds;                   /* optimize() rounds run (4, or 1 when < 10 edges) */
+  int iterations[4];            /* LM iterations done per round */
+  double chi2[4];               /* final (robust) chi2 per round */
+} rspl_frame_result;
+
+typedef struct {
+  int max_batch;                /* frames per call */
+  int max_edges;                /* total edges (mono + stereo) over a whole batch */
+  int max_points;               /* total points over a whole batch */
+  int device;
+} rspl_frame_config;
+
+typedef struct rspl_frame rspl_frame;
+
+int rspl_frame_create(const rspl_frame_config* cfg, rspl_frame** out);
+/* batch independent FrameOptimization calls; results[b] receives frame b */
+int rspl_frame_optimize(rspl_frame* h, const rspl_frame_problem* problems, int batch, rspl_frame_result* results);
+void rspl_frame_destroy(rspl_frame* h);
+
 #ifdef __cplusplus
 }
 #endif

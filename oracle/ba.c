@@ -842,3 +842,230 @@ int orc_ba_local(const rspl_ba_problem* P, rspl_ba_result* R) {
 
 /* exported helpers for tests: single-edge residual / line oplus */
 void orc_line_oplus(double* L, const double* v) { line_oplus(L, v); }
+
+/* ====================================================================== */
+/* FrameOptimization (src/g2o_optimization/g2o_optimization.cc:256-398):   */
+/* one VertexSE3Expmap (T_cw = SE3Quat(q,p).inverse(), :265), unary        */
+/* EdgeSE3ProjectXYZOnlyPose (I2) / EdgeStereoSE3ProjectXYZOnlyPose (I3)   */
+/* with Huber delta (float)sqrt(th) (:279-282); 4 rounds (:336-392): reset */
+/* the estimate to the input pose, initializeOptimization(0), optimize(10);*/
+/* then chi2 per edge -- re-computed at the current estimate only for      */
+/* edges whose inlier flag is false (:345-347), otherwise the last error   */
+/* the optimizer computed -- cast to float and compared with the threshold */
+/* (:350-351) to set inlier / level; kernels dropped after round 2 (:363); */
+/* stop after the first round when the graph holds < 10 edges (:383).      */
+/* ====================================================================== */
+typedef struct {
+  const rspl_frame_problem* P;
+  int n;          /* edges: mono [0, n_mono), stereo [n_mono, n) */
+  double* err;    /* [n][3] last computed error */
+  unsigned char* level;
+  unsigned char* inl;
+} fo_t;
+
+static void fo_edge(const fo_t* f, int e, int* stereo, const double** X, const double** obs, const double** cam) {
+  const rspl_frame_problem* P = f->P;
+  const int s = e >= P->n_mono, i = s ? e - P->n_mono : e;
+  const int32_t* cid = s ? P->stereo_camera : P->mono_camera;
+  *stereo = s;
+  *X = P->points + 3 * (s ? P->stereo_point[i] : P->mono_point[i]);
+  *obs = s ? P->stereo_obs + 3 * i : P->mono_obs + 2 * i;
+  *cam = P->cameras + 5 * (cid ? cid[i] : 0);
+}
+
+static void fo_error(const fo_t* f, const se3* T, int e, double* out) {
+  int s;
+  const double *X, *obs, *cam;
+  fo_edge(f, e, &s, &X, &obs, &cam);
+  double Xc[3];
+  se3_map(T, X, Xc);
+  const double iz = 1.0 / Xc[2];
+  const double u = cam[0] * Xc[0] * iz + cam[2], v = cam[1] * Xc[1] * iz + cam[3];
+  out[0] = obs[0] - u;
+  out[1] = obs[1] - v;
+  out[2] = s ? obs[2] - (u - cam[4] * iz) : 0.0;
+}
+
+static double fo_chi2(const double* e) { return e[0] * e[0] + e[1] * e[1] + e[2] * e[2]; }
+
+static double fo_delta(const fo_t* f, int e) {
+  return (double)(float)sqrt(e >= f->P->n_mono ? f->P->th_stereo_point : f->P->th_mono_point);
+}
+
+/* computeActiveErrors + activeRobustChi2 */
+static double fo_active_chi2(fo_t* f, const se3* T, int robust) {
+  double s = 0;
+  for (int e = 0; e < f->n; e++) {
+    if (f->level[e]) continue;
+    fo_error(f, T, e, f->err + 3 * e);
+    const double c2 = fo_chi2(f->err + 3 * e);
+    if (robust) {
+      double rho[2];
+      huber(c2, fo_delta(f, e), rho);
+      s += rho[0];
+    } else {
+      s += c2;
+    }
+  }
+  return s;
+}
+
+/* H (6x6) and b = -J^T W e over the active edges at T, from the errors in f->err */
+static void fo_build(fo_t* f, const se3* T, int robust, double* H, double* b) {
+  memset(H, 0, sizeof(double) * 36);
+  memset(b, 0, sizeof(double) * 6);
+  for (int e = 0; e < f->n; e++) {
+    if (f->level[e]) continue;
+    int s;
+    const double *X, *obs, *cam;
+    fo_edge(f, e, &s, &X, &obs, &cam);
+    double Xc[3];
+    se3_map(T, X, Xc);
+    const double fx = cam[0], fy = cam[1], bf = cam[4];
+    const double x = Xc[0], y = Xc[1], z = Xc[2], iz = 1.0 / z, iz2 = iz * iz;
+    const double D[3][3] = {{fx * iz, 0, -fx * x * iz2}, {0, fy * iz, -fy * y * iz2}, {fx * iz, 0, -fx * x * iz2 + bf * iz2}};
+    const double SX[9] = {0, -z, y, z, 0, -x, -y, x, 0};
+    double J[3][6];
+    const int rows = s ? 3 : 2;
+    for (int r = 0; r < rows; r++)
+      for (int c = 0; c < 3; c++) {
+        double a = 0;
+        for (int k = 0; k < 3; k++) a += D[r][k] * SX[k * 3 + c];
+        J[r][c] = a;
+        J[r][3 + c] = -D[r][c];
+      }
+    const double* er = f->err + 3 * e;
+    double w = 1.0;
+    if (robust) {
+      double rho[2];
+      huber(fo_chi2(er), fo_delta(f, e), rho);
+      w = rho[1];
+    }
+    for (int i = 0; i < 6; i++) {
+      double g = 0;
+      for (int r = 0; r < rows; r++) g += J[r][i] * er[r];
+      b[i] += -w * g;
+      for (int j = 0; j < 6; j++) {
+        double h = 0;
+        for (int r = 0; r < rows; r++) h += J[r][i] * J[r][j];
+        H[i * 6 + j] += w * h;
+      }
+    }
+  }
+}
+
+/* SparseOptimizer::optimize(iters) with OptimizationAlgorithmLevenberg on the pose vertex */
+static int fo_optimize(fo_t* f, se3* T, int iters, int robust, double* chi2_out) {
+  double H[36], b[36], A[36], x[6];
+  double lambda = 0, ni = 2, currentChi = 0;
+  int done = 0;
+  for (int it = 0; it < iters; it++) {
+    currentChi = fo_active_chi2(f, T, robust);
+    fo_build(f, T, robust, H, b);
+    if (it == 0) {
+      double mx = 0;
+      for (int i = 0; i < 6; i++) mx = fmax(mx, fabs(H[i * 7]));
+      lambda = 1e-5 * mx;
+      ni = 2;
+    }
+    double rho = 0;
+    int qmax = 0;
+    do {
+      memcpy(A, H, sizeof(A));
+      for (int i = 0; i < 6; i++) A[i * 7] += lambda;
+      memcpy(x, b, sizeof(x));
+      const int ok = chol_solve(A, x, 6) == 0;
+      const se3 Tb = *T;
+      if (ok) {
+        se3 dT = se3_exp(x);
+        *T = se3_mul(&dT, &Tb);
+      }
+      double tempChi = fo_active_chi2(f, T, robust);
+      if (!ok) tempChi = DBL_MAX;
+      rho = currentChi - tempChi;
+      double scale = 1.0;
+      if (ok) {
+        scale = 0;
+        for (int i = 0; i < 6; i++) scale += x[i] * (lambda * x[i] + b[i]);
+        scale += 1e-3;
+      }
+      rho /= scale;
+      if (rho > 0 && isfinite(tempChi) && ok) {
+        double alpha = 1. - pow(2 * rho - 1, 3);
+        alpha = fmin(alpha, 2. / 3.);
+        lambda *= fmax(1. / 3., alpha);
+        ni = 2;
+        currentChi = tempChi;
+      } else {
+        lambda *= ni;
+        ni *= 2;
+        *T = Tb;
+        if (!isfinite(lambda)) break;
+      }
+      qmax++;
+    } while (rho < 0 && qmax < 10);
+    done++;
+    if (qmax == 10 || rho == 0 || !isfinite(lambda)) break;
+  }
+  *chi2_out = currentChi;
+  return done;
+}
+
+int orc_frame_opt(const rspl_frame_problem* P, rspl_frame_result* R) {
+  fo_t f;
+  memset(&f, 0, sizeof(f));
+  f.P = P;
+  f.n = P->n_mono + P->n_stereo;
+  f.err = (double*)calloc(3 * (size_t)f.n + 1, sizeof(double));
+  f.level = (unsigned char*)calloc(f.n + 1, 1);
+  f.inl = (unsigned char*)calloc(f.n + 1, 1);
+  for (int e = 0; e < f.n; e++) {
+    const uint8_t* src = e < P->n_mono ? P->mono_inlier_in : P->stereo_inlier_in;
+    f.inl[e] = src ? src[e < P->n_mono ? e : e - P->n_mono] : 1;
+  }
+  se3 Twc;
+  Twc.q[0] = P->pose_q[3]; Twc.q[1] = P->pose_q[0]; Twc.q[2] = P->pose_q[1]; Twc.q[3] = P->pose_q[2];
+  memcpy(Twc.t, P->pose_p, sizeof(Twc.t));
+  se3_normalize(&Twc);
+  const se3 T0 = se3_inverse(&Twc);
+  se3 T = T0;
+  int num_outlier = 0;
+  R->rounds = 0;
+  for (int r = 0; r < 4; r++) {
+    T = T0;
+    const int robust = r < 3;
+    int active = 0;
+    for (int e = 0; e < f.n; e++) active += !f.level[e];
+    R->iterations[r] = 0;
+    R->chi2[r] = 0;
+    if (active) R->iterations[r] = fo_optimize(&f, &T, 10, robust, &R->chi2[r]);
+    num_outlier = 0;
+    for (int e = 0; e < f.n; e++) {
+      double ev[3];
+      if (!f.inl[e]) fo_error(&f, &T, e, f.err + 3 * e);
+      memcpy(ev, f.err + 3 * e, sizeof(ev));
+      const float c2 = (float)fo_chi2(ev);
+      const double th = e < P->n_mono ? P->th_mono_point : P->th_stereo_point;
+      if (c2 > th) {
+        f.inl[e] = 0;
+        f.level[e] = 1;
+        num_outlier++;
+      } else {
+        f.inl[e] = 1;
+        f.level[e] = 0;
+      }
+    }
+    R->rounds = r + 1;
+    if (f.n < 10) break;
+  }
+  const se3 W = se3_inverse(&T);
+  R->pose_q[0] = W.q[1]; R->pose_q[1] = W.q[2]; R->pose_q[2] = W.q[3]; R->pose_q[3] = W.q[0];
+  memcpy(R->pose_p, W.t, sizeof(W.t));
+  for (int e = 0; e < f.n; e++) {
+    uint8_t* dst = e < P->n_mono ? R->mono_inlier : R->stereo_inlier;
+    if (dst) dst[e < P->n_mono ? e : e - P->n_mono] = f.inl[e];
+  }
+  R->n_inliers = f.n - num_outlier;
+  free(f.err); free(f.level); free(f.inl);
+  return 0;
+}

@@ -114,3 +114,17 @@ def line_oplus(L: np.ndarray, v: np.ndarray) -> np.ndarray:
     L = np.ascontiguousarray(L, np.float64).copy()
     lib().orc_line_oplus(L, np.ascontiguousarray(v, np.float64))
     return L
+
+
+def frame_opt(problem):
+    """problem: rspl_slam_amd.ba_types.FrameProblem -> FrameResult (FrameOptimization restatement)."""
+    from rspl_slam_amd.ba_types import FrameResult
+    res = FrameResult.alloc(problem)
+    P, R = problem.to_ctypes(), res.to_ctypes()
+    L = lib()
+    L.orc_frame_opt.argtypes = [C.c_void_p, C.c_void_p]
+    rc = L.orc_frame_opt(C.byref(P), C.byref(R))
+    if rc:
+        raise RuntimeError(f"orc_frame_opt rc={rc}")
+    res.read_back(R)
+    return res

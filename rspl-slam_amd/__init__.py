@@ -9,7 +9,7 @@ import importlib
 from . import capi, weights, synthetic, ba_types  # noqa: F401
 
 _API = ("SuperPoint", "SuperPointConfig", "SuperGlue", "SuperGlueConfig", "PointMatching",
-        "LocalmapOptimization", "LocalBA")
+        "LocalmapOptimization", "LocalBA", "FrameOptimization", "FrameBA")
 
 
 def __getattr__(name):

@@ -4,6 +4,7 @@
   SuperGlue      include/super_glue.h:20-71       (build / infer)
   PointMatching  include/point_matching.h:7-18    (MatchingPoints / NormalizeKeypoints)
   LocalmapOptimization  include/g2o_optimization/g2o_optimization.h:15-19
+  FrameOptimization     include/g2o_optimization/g2o_optimization.h:20-22
 
 Same names and argument meaning as the reference; C++ out-parameters become
 return values ((ok, features) for SuperPoint::infer, etc.).  Everything runs
@@ -257,3 +258,61 @@ def LocalmapOptimization(poses, points, lines, camera_list, mono_point_constrain
 
 
 _default_ba_caps = (0, 0, 0, 0)
+
+
+# ---------------------------------------------------------------------------
+# Tracking pose optimisation: FrameOptimization (include/g2o_optimization/g2o_optimization.h:20-22)
+# ---------------------------------------------------------------------------
+class FrameBA:
+    """Owns one rspl_frame handle; optimises a batch of independent frames in one launch."""
+
+    def __init__(self, max_batch=64, max_edges=65536, max_points=65536, device=0):
+        self._lib = capi.load()
+        self._h = C.c_void_p()
+        cfg = capi.FrameConfig(max_batch, max_edges, max_points, device)
+        capi.check(self._lib.rspl_frame_create(C.byref(cfg), C.byref(self._h)), "rspl_frame_create")
+
+    def run(self, problems):
+        """problems: list of ba_types.FrameProblem -> list of ba_types.FrameResult"""
+        from .ba_types import FrameResult, RsplFrameProblem, RsplFrameResult
+        res = [FrameResult.alloc(p) for p in problems]
+        P = (RsplFrameProblem * len(problems))(*[p.to_ctypes() for p in problems])
+        R = (RsplFrameResult * len(problems))(*[r.to_ctypes() for r in res])
+        capi.check(self._lib.rspl_frame_optimize(self._h, P, len(problems), R), "rspl_frame_optimize")
+        for r, rc in zip(res, R):
+            r.read_back(rc)
+        return res
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._lib.rspl_frame_destroy(self._h)
+            self._h = C.c_void_p()
+
+
+_default_frame = None
+
+
+def FrameOptimization(poses, points, camera_list, mono_point_constraints, stereo_point_constraints, cfg) -> int:
+    """Same signature, in-place semantics and return value as the reference
+    (g2o_optimization.cc:256-398): the single pose in ``poses`` is updated, constraint ``inlier``
+    flags are written, and the number of inlier constraints is returned."""
+    from . import ba_types as BT
+    global _default_frame
+    fp = BT.pack_frame_problem(poses, points, camera_list, mono_point_constraints, stereo_point_constraints, cfg)
+    ne = len(mono_point_constraints) + len(stereo_point_constraints)
+    if _default_frame is None or ne > _default_frame_cap[0] or len(points) > _default_frame_cap[1]:
+        cap = (max(ne, 65536), max(len(points), 65536))
+        _default_frame = FrameBA(max_batch=1, max_edges=cap[0], max_points=cap[1])
+        globals()["_default_frame_cap"] = cap
+    r = _default_frame.run([fp])[0]
+    pose = next(iter(poses.values()))
+    pose.q = r.pose_q.copy()
+    pose.p = r.pose_p.copy()
+    for c, f in zip(mono_point_constraints, r.inlier["mono"]):
+        c.inlier = bool(f)
+    for c, f in zip(stereo_point_constraints, r.inlier["stereo"]):
+        c.inlier = bool(f)
+    return r.n_inliers
+
+
+_default_frame_cap = (0, 0)

@@ -279,3 +279,125 @@ def unpack_result(res: DenseResult, ids, poses, points, lines, mono, stereo, mon
     for cs, name in ((mono, "mono"), (stereo, "stereo"), (mono_line, "mono_line"), (stereo_line, "stereo_line")):
         for c, f in zip(cs, res.inlier[name]):
             c.inlier = bool(f)
+
+
+# ---------------------------------------------------------------------------
+# FrameOptimization (g2o_optimization.cc:256-398): C-ABI rspl_frame_problem / _result
+# ---------------------------------------------------------------------------
+class RsplFrameProblem(C.Structure):
+    _fields_ = [
+        ("n_cameras", C.c_int), ("cameras", C.POINTER(C.c_double)),
+        ("pose_q", C.c_double * 4), ("pose_p", C.c_double * 3),
+        ("n_points", C.c_int), ("points", C.POINTER(C.c_double)),
+        ("n_mono", C.c_int), ("mono_point", C.POINTER(C.c_int32)), ("mono_camera", C.POINTER(C.c_int32)),
+        ("mono_obs", C.POINTER(C.c_double)), ("mono_inlier_in", C.POINTER(C.c_uint8)),
+        ("n_stereo", C.c_int), ("stereo_point", C.POINTER(C.c_int32)), ("stereo_camera", C.POINTER(C.c_int32)),
+        ("stereo_obs", C.POINTER(C.c_double)), ("stereo_inlier_in", C.POINTER(C.c_uint8)),
+        ("th_mono_point", C.c_double), ("th_stereo_point", C.c_double),
+    ]
+
+
+class RsplFrameResult(C.Structure):
+    _fields_ = [
+        ("pose_q", C.c_double * 4), ("pose_p", C.c_double * 3),
+        ("mono_inlier", C.POINTER(C.c_uint8)), ("stereo_inlier", C.POINTER(C.c_uint8)),
+        ("n_inliers", C.c_int), ("rounds", C.c_int), ("iterations", C.c_int * 4), ("chi2", C.c_double * 4),
+    ]
+
+
+@dataclass
+class FrameProblem:
+    """Dense arrays of one FrameOptimization call (one pose, fixed points, unary edges)."""
+    cameras: np.ndarray                          # [nc, 5]
+    pose_q: np.ndarray                           # [4] (x, y, z, w) of the initial T_wc
+    pose_p: np.ndarray                           # [3]
+    points: np.ndarray                           # [nq, 3]
+    mono: Dict[str, np.ndarray] = field(default_factory=dict)     # lm, cam, obs, inlier
+    stereo: Dict[str, np.ndarray] = field(default_factory=dict)
+    cfg: OptimizationConfig = field(default_factory=OptimizationConfig)
+
+    def __post_init__(self):
+        f = lambda a, dt: np.ascontiguousarray(a, dtype=dt)
+        self.cameras = f(self.cameras, np.float64).reshape(-1, 5)
+        self.pose_q = f(self.pose_q, np.float64).reshape(4)
+        self.pose_p = f(self.pose_p, np.float64).reshape(3)
+        self.points = f(self.points, np.float64).reshape(-1, 3)
+        for name, od in (("mono", 2), ("stereo", 3)):
+            d = getattr(self, name)
+            n = len(d.get("lm", []))
+            d["lm"] = f(d.get("lm", np.zeros(0)), np.int32).reshape(-1)
+            d["cam"] = f(d.get("cam", np.zeros(n)), np.int32).reshape(-1)
+            d["obs"] = f(d.get("obs", np.zeros((0, od))), np.float64).reshape(-1, od)
+            d["inlier"] = f(d.get("inlier", np.ones(n)), np.uint8).reshape(-1)
+
+    def n_edges(self, name):
+        return int(getattr(self, name)["lm"].shape[0])
+
+    def to_ctypes(self) -> RsplFrameProblem:
+        P = RsplFrameProblem()
+        P.n_cameras = self.cameras.shape[0]
+        P.cameras = _ptr(self.cameras, C.c_double)
+        P.pose_q[:] = list(self.pose_q)
+        P.pose_p[:] = list(self.pose_p)
+        P.n_points = self.points.shape[0]
+        P.points = _ptr(self.points, C.c_double)
+        for name in ("mono", "stereo"):
+            d = getattr(self, name)
+            setattr(P, f"n_{name}", d["lm"].shape[0])
+            setattr(P, f"{name}_point", _ptr(d["lm"], C.c_int32))
+            setattr(P, f"{name}_camera", _ptr(d["cam"], C.c_int32))
+            setattr(P, f"{name}_obs", _ptr(d["obs"], C.c_double))
+            setattr(P, f"{name}_inlier_in", _ptr(d["inlier"], C.c_uint8))
+        P.th_mono_point = self.cfg.mono_point
+        P.th_stereo_point = self.cfg.stereo_point
+        return P
+
+
+@dataclass
+class FrameResult:
+    pose_q: np.ndarray
+    pose_p: np.ndarray
+    inlier: Dict[str, np.ndarray]
+    n_inliers: int = 0
+    rounds: int = 0
+    iterations: tuple = ()
+    chi2: tuple = ()
+
+    @staticmethod
+    def alloc(p: FrameProblem) -> "FrameResult":
+        return FrameResult(pose_q=np.zeros(4), pose_p=np.zeros(3),
+                           inlier={k: np.zeros(p.n_edges(k), np.uint8) for k in ("mono", "stereo")})
+
+    def to_ctypes(self) -> RsplFrameResult:
+        R = RsplFrameResult()
+        R.mono_inlier = _ptr(self.inlier["mono"], C.c_uint8)
+        R.stereo_inlier = _ptr(self.inlier["stereo"], C.c_uint8)
+        return R
+
+    def read_back(self, R: RsplFrameResult):
+        self.pose_q = np.array(R.pose_q[:])
+        self.pose_p = np.array(R.pose_p[:])
+        self.n_inliers = R.n_inliers
+        self.rounds = R.rounds
+        self.iterations = tuple(R.iterations[:])
+        self.chi2 = tuple(R.chi2[:])
+
+
+def pack_frame_problem(poses: Dict[int, Pose3d], points: Dict[int, Position3d], camera_list: List[Camera],
+                       mono: List[MonoPointConstraint], stereo: List[StereoPointConstraint],
+                       cfg: OptimizationConfig) -> FrameProblem:
+    """FrameOptimization's inputs (one pose, asserted at g2o_optimization.cc:259) -> dense arrays."""
+    assert len(poses) == 1, "FrameOptimization takes exactly one pose (g2o_optimization.cc:259)"
+    pose = next(iter(poses.values()))
+    qid = {k: i for i, k in enumerate(sorted(points))}
+    cams = np.array([[c.fx, c.fy, c.cx, c.cy, c.bf] for c in camera_list], np.float64)
+
+    def edges(cs, od):
+        return dict(lm=np.array([qid[c.id_point] for c in cs], np.int32),
+                    cam=np.array([c.id_camera for c in cs], np.int32),
+                    obs=np.array([c.keypoint for c in cs], np.float64).reshape(-1, od),
+                    inlier=np.array([c.inlier for c in cs], np.uint8))
+
+    return FrameProblem(cameras=cams, pose_q=pose.q, pose_p=pose.p,
+                        points=np.array([points[k].p for k in sorted(points)]).reshape(-1, 3),
+                        mono=edges(mono, 2), stereo=edges(stereo, 3), cfg=cfg)

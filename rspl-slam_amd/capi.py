@@ -28,6 +28,7 @@ EXPORTS = [
     "rspl_sg_stage_times", "rspl_sg_destroy",
     "rspl_pm_match",
     "rspl_ba_create", "rspl_ba_local", "rspl_ba_destroy",
+    "rspl_frame_create", "rspl_frame_optimize", "rspl_frame_destroy",
 ]
 
 
@@ -50,6 +51,10 @@ class DMatch(C.Structure):
 class BaConfig(C.Structure):
     _fields_ = [("max_poses", C.c_int), ("max_points", C.c_int), ("max_lines", C.c_int),
                 ("max_edges", C.c_int), ("device", C.c_int)]
+
+
+class FrameConfig(C.Structure):
+    _fields_ = [("max_batch", C.c_int), ("max_edges", C.c_int), ("max_points", C.c_int), ("device", C.c_int)]
 
 
 class RsplError(RuntimeError):
@@ -115,6 +120,11 @@ def load(path: pathlib.Path = LIB_PATH):
         lib.rspl_ba_local.argtypes = [vp, vp, vp]
         lib.rspl_ba_destroy.argtypes = [vp]
         lib.rspl_ba_destroy.restype = None
+    if hasattr(lib, "rspl_frame_create"):
+        lib.rspl_frame_create.argtypes = [C.POINTER(FrameConfig), C.POINTER(vp)]
+        lib.rspl_frame_optimize.argtypes = [vp, vp, ip, vp]
+        lib.rspl_frame_destroy.argtypes = [vp]
+        lib.rspl_frame_destroy.restype = None
     _lib = lib
     return lib
 

@@ -1,0 +1,438 @@
+// Tracking pose optimisation, FrameOptimization (src/g2o_optimization/g2o_optimization.cc:256-398),
+// as a single-launch fp64 Levenberg-Marquardt on gfx950: ONE wavefront owns one frame for the
+// whole call -- 4 rounds x optimize(10) x trials -- so there is no host round trip, no grid
+// synchronisation and no LDS.  Each lane linearises a strided subset of the frame's unary edges;
+// the 6x6 normal equations (21 + 6 + chi2 values) are all-reduced across the wave with DPP
+// (quad swaps, half-row / row mirrors, then the four row results through readlane: a fixed tree,
+// and because IEEE addition is commutative every lane ends with the bitwise-same sums).  Every
+// lane then factors the same 6x6 system in registers, so the LM control (g2o
+// OptimizationAlgorithmLevenberg: tau 1e-5, good-step scale clamp [1/3, 2/3], ni doubling,
+// 10 trials, stop on qmax == 10 || rho == 0) is wave-uniform and needs no broadcast.
+// Latency bound by construction (a few hundred edges per frame): throughput comes from batching
+// frames -- one wave each -- into one launch.  Same algorithm as the CPU restatement
+// orc_frame_opt (oracle/ba.c).
+#include <hip/hip_runtime.h>
+
+#include <cfloat>
+#include <cstdint>
+
+#include "frame_kernels.hpp"
+#include "se3_device.hpp"
+
+namespace rspl {
+namespace frame {
+
+using ba::SE3;
+
+template <int CTRL>
+__device__ __forceinline__ double dppd(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ __forceinline__ double rdlaned(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+// wave64 all-reduce (sum), identical bits in every lane
+__device__ __forceinline__ double wsum(double v) {
+  v += dppd<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dppd<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dppd<0x141>(v);  // row_half_mirror
+  v += dppd<0x140>(v);  // row_mirror
+  return (rdlaned(v, 0) + rdlaned(v, 16)) + (rdlaned(v, 32) + rdlaned(v, 48));
+}
+__device__ __forceinline__ int wsum_int(int v) {
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ void huber(double e2, double delta, double& r0, double& r1) {
+  const double dsqr = delta * delta;
+  if (e2 <= dsqr) {
+    r0 = e2;
+    r1 = 1.0;
+  } else {
+    const double s = sqrt(e2);
+    r0 = 2 * s * delta - dsqr;
+    r1 = delta / s;
+  }
+}
+
+struct Pose {  // T_cw with its rotation matrix
+  SE3 T;
+  double R[9];
+  __device__ void set(const SE3& t) {
+    T = t;
+    ba::q_to_R(T.q, R);
+  }
+};
+
+// e = obs - proj(T Xw) (+ the right-image u for stereo); returns Xc for the Jacobian
+__device__ __forceinline__ void edge_error(const Edge& E, const Pose& P, double* Xc, double* e) {
+  ba::mat3_vec(P.R, E.X, Xc);
+  for (int i = 0; i < 3; i++) Xc[i] += P.T.t[i];
+  const double iz = 1.0 / Xc[2];
+  const double u = E.cam[0] * Xc[0] * iz + E.cam[2], v = E.cam[1] * Xc[1] * iz + E.cam[3];
+  e[0] = E.obs[0] - u;
+  e[1] = E.obs[1] - v;
+  e[2] = E.stereo != 0.0 ? E.obs[2] - (u - E.cam[4] * iz) : 0.0;
+}
+
+__device__ __forceinline__ double chi2_of(const double* e) { return e[0] * e[0] + e[1] * e[1] + e[2] * e[2]; }
+
+// One frame's per-edge state: the edge records, the last computed error, the level and the
+// inlier flag -- staged in LDS for frames of <= kLdsEdges edges (one copy in, then every LM
+// pass reads LDS instead of chasing L2 latency), in global scratch otherwise.
+struct View {
+  const Edge* E;
+  double* err;   // [n][3]
+  uint8_t* lev;
+  uint8_t* inl;
+  int n;
+  double delta0, delta1;  // Huber deltas (mono, stereo): scalars, never indexed (no scratch)
+};
+
+// robust (Huber) or plain chi2 of an error, for the edge type
+__device__ __forceinline__ double cost_of(const View& V, const double* ev, bool stereo, bool robust) {
+  const double c2 = chi2_of(ev);
+  if (!robust) return c2;
+  double r0, r1;
+  huber(c2, stereo ? V.delta1 : V.delta0, r0, r1);
+  return r0;
+}
+
+// computeActiveErrors + activeRobustChi2 over this lane's edges (errors stored), wave-reduced.
+// Two edges per lane in flight (loads of both issued before either is used): a lone wave per
+// frame has no other wave to hide the LDS / fp64-divide latency behind.
+__device__ __forceinline__ double active_chi2(const View& V, const Pose& P, int lane, bool robust) {
+  double s = 0;
+  for (int e = lane; e < V.n; e += 128) {
+    const int e1 = e + 64 < V.n ? e + 64 : e;
+    const bool a0 = !V.lev[e], a1 = e + 64 < V.n && !V.lev[e1];
+    const Edge E0 = V.E[e], E1 = V.E[e1];
+    double Xc0[3], Xc1[3], ev0[3], ev1[3];
+    edge_error(E0, P, Xc0, ev0);
+    edge_error(E1, P, Xc1, ev1);
+    const double c0 = cost_of(V, ev0, E0.stereo != 0.0, robust);
+    const double c1 = cost_of(V, ev1, E1.stereo != 0.0, robust);
+    if (a0) {
+      double* er = V.err + 3 * e;
+      er[0] = ev0[0]; er[1] = ev0[1]; er[2] = ev0[2];
+      s += c0;
+    }
+    if (a1) {
+      double* er = V.err + 3 * e1;
+      er[0] = ev1[0]; er[1] = ev1[1]; er[2] = ev1[2];
+      s += c1;
+    }
+  }
+  return wsum(s);
+}
+
+constexpr int kNV = 28;  // 21 upper-triangular H entries, 6 b entries, chi2
+
+// All-reduce of the 28 system values across the wave as a reduce-scatter: 5 exchange steps
+// (xor 32, 16, 8, 4, 2) each halve the values a lane keeps (32 -> 1, padded), one xor-1 step
+// completes the sum, then every value is read back from its owner lane with readlane (wave-
+// uniform).  32 double exchanges instead of 28 x 6 for per-value butterflies; each value is
+// summed by one fixed tree (a + b == b + a in the pair), so the result is deterministic.
+__device__ __forceinline__ double shx(double v, int o) { return __shfl_xor(v, o); }
+__device__ __forceinline__ void wave_allreduce28(double (&acc)[kNV], int lane) {
+  double v[32];
+#pragma unroll
+  for (int k = 0; k < 32; k++) v[k] = k < kNV ? acc[k] : 0.0;
+#pragma unroll
+  for (int o = 32, h = 16; o >= 2; o >>= 1, h >>= 1) {
+    const bool up = lane & o;  // keep the upper half of the current h*2 values
+#pragma unroll
+    for (int k = 0; k < h; k++) {
+      const double keep = up ? v[h + k] : v[k];
+      const double send = up ? v[k] : v[h + k];
+      v[k] = keep + shx(send, o);
+    }
+  }
+  v[0] += shx(v[0], 1);
+  // lane L holds value index j(L): bit 5 of L -> bit 4 of j, bit 4 -> bit 3, ..., bit 1 -> bit 0
+#pragma unroll
+  for (int j = 0; j < kNV; j++) {
+    const int owner = ((j >> 4) & 1) << 5 | ((j >> 3) & 1) << 4 | ((j >> 2) & 1) << 3 | ((j >> 1) & 1) << 2 |
+                      (j & 1) << 1;
+    acc[j] = rdlaned(v[0], owner);
+  }
+}
+
+__device__ __forceinline__ int hidx(int i, int j) { return i * 6 - i * (i - 1) / 2 + (j - i); }
+
+// errors at T (stored) + robust chi2 + H / b (Huber IRLS weights), wave-reduced
+__device__ __forceinline__ void linearize(const View& V, const Pose& P, int lane, bool robust, double (&acc)[kNV]) {
+#pragma unroll
+  for (int k = 0; k < kNV; k++) acc[k] = 0.0;
+  for (int e = lane; e < V.n; e += 64) {
+    if (V.lev[e]) continue;
+    const Edge E = V.E[e];
+    double Xc[3], ev[3];
+    edge_error(E, P, Xc, ev);
+    double* er = V.err + 3 * e;
+    er[0] = ev[0]; er[1] = ev[1]; er[2] = ev[2];
+    const double c2 = chi2_of(ev);
+    double w = 1.0;
+    if (robust) {
+      double r0, r1;
+      huber(c2, E.stereo != 0.0 ? V.delta1 : V.delta0, r0, r1);
+      acc[27] += r0;
+      w = r1;
+    } else {
+      acc[27] += c2;
+    }
+    const double fx = E.cam[0], fy = E.cam[1], bf = E.cam[4];
+    const double x = Xc[0], y = Xc[1], z = Xc[2], iz = 1.0 / z, iz2 = iz * iz;
+    const double Dm[3][3] = {{fx * iz, 0, -fx * x * iz2}, {0, fy * iz, -fy * y * iz2},
+                             {fx * iz, 0, -fx * x * iz2 + bf * iz2}};
+    const double SX[9] = {0, -z, y, z, 0, -x, -y, x, 0};
+    double J[3][6];
+#pragma unroll
+    for (int r = 0; r < 3; r++)
+#pragma unroll
+      for (int c = 0; c < 3; c++) {
+        double s = 0;
+#pragma unroll
+        for (int k = 0; k < 3; k++) s += Dm[r][k] * SX[k * 3 + c];
+        J[r][c] = s;
+        J[r][3 + c] = -Dm[r][c];
+      }
+    const int rows = E.stereo != 0.0 ? 3 : 2;
+    if (rows == 2)
+#pragma unroll
+      for (int c = 0; c < 6; c++) J[2][c] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 6; i++) {
+      const double g = J[0][i] * ev[0] + J[1][i] * ev[1] + J[2][i] * ev[2];
+      acc[21 + i] += -w * g;
+#pragma unroll
+      for (int j = i; j < 6; j++) acc[hidx(i, j)] += w * (J[0][i] * J[0][j] + J[1][i] * J[1][j] + J[2][i] * J[2][j]);
+    }
+  }
+  wave_allreduce28(acc, lane);
+}
+
+__device__ __forceinline__ double rcp64(double d) {
+  double r = __builtin_amdgcn_rcp(d);
+  r = fma(r, fma(-d, r, 1.0), r);
+  return fma(r, fma(-d, r, 1.0), r);
+}
+
+// (H + lambda I) x = b by Cholesky, in registers (every lane the same); false if not SPD.
+// The factor keeps 1 / L[j][j] on its diagonal.
+__device__ __forceinline__ bool solve6(const double (&acc)[kNV], double lambda, double (&x)[6]) {
+  double L[6][6];
+#pragma unroll
+  for (int i = 0; i < 6; i++)
+#pragma unroll
+    for (int j = 0; j < 6; j++) L[i][j] = j >= i ? acc[hidx(i, j)] : acc[hidx(j, i)];
+#pragma unroll
+  for (int i = 0; i < 6; i++) L[i][i] += lambda;
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 6; j++) {
+    double s = L[j][j];
+#pragma unroll
+    for (int k = 0; k < j; k++) s -= L[j][k] * L[j][k];
+    ok = ok && s > 0;
+    const double r = rcp64(sqrt(s));  // 1 / pivot: multiplications instead of a divide chain
+    L[j][j] = r;
+#pragma unroll
+    for (int i = j + 1; i < 6; i++) {
+      double t = L[i][j];
+#pragma unroll
+      for (int k = 0; k < j; k++) t -= L[i][k] * L[j][k];
+      L[i][j] = t * r;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 6; i++) {
+    double s = acc[21 + i];
+#pragma unroll
+    for (int k = 0; k < i; k++) s -= L[i][k] * x[k];
+    x[i] = s * L[i][i];
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; i--) {
+    double s = x[i];
+#pragma unroll
+    for (int k = i + 1; k < 6; k++) s -= L[k][i] * x[k];
+    x[i] = s * L[i][i];
+  }
+  return ok;
+}
+
+// SparseOptimizer::optimize(iters) with OptimizationAlgorithmLevenberg on the pose vertex
+__device__ __forceinline__ int optimize_pose(const View& V, Pose& P, int lane, bool robust, int iters,
+                                             double& chi2_out) {
+  double acc[kNV];
+  double lambda = 0, ni = 2, currentChi = 0;
+  int done = 0;
+  for (int it = 0; it < iters; it++) {
+    linearize(V, P, lane, robust, acc);
+    currentChi = acc[27];
+    if (it == 0) {  // computeLambdaInit: tau * max diagonal
+      double mx = 0;
+#pragma unroll
+      for (int i = 0; i < 6; i++) mx = fmax(mx, fabs(acc[hidx(i, i)]));
+      lambda = 1e-5 * mx;
+      ni = 2;
+    }
+    double rho = 0;
+    int qmax = 0;
+    do {
+      double x[6];
+      const bool ok = solve6(acc, lambda, x);
+      Pose C = P;
+      if (ok) C.set(ba::se3_mul(ba::se3_exp(x), P.T));
+      double tempChi = active_chi2(V, C, lane, robust);
+      if (!ok) tempChi = DBL_MAX;
+      rho = currentChi - tempChi;
+      double scale = 1.0;
+      if (ok) {
+        scale = 0;
+#pragma unroll
+        for (int i = 0; i < 6; i++) scale += x[i] * (lambda * x[i] + acc[21 + i]);
+        scale += 1e-3;
+      }
+      rho /= scale;
+      if (rho > 0 && isfinite(tempChi) && ok) {
+        double alpha = 1. - pow(2 * rho - 1, 3);
+        alpha = fmin(alpha, 2. / 3.);
+        lambda *= fmax(1. / 3., alpha);
+        ni = 2;
+        currentChi = tempChi;
+        P = C;
+      } else {
+        lambda *= ni;
+        ni *= 2;
+        if (!isfinite(lambda)) break;
+      }
+      qmax++;
+    } while (rho < 0 && qmax < 10);
+    done++;
+    if (qmax == 10 || rho == 0 || !isfinite(lambda)) break;
+  }
+  chi2_out = currentChi;
+  return done;
+}
+
+// one wavefront per frame; LDS: the frame's edges + errors + flags staged once (kLdsEdges cap)
+template <bool LDS>
+__global__ __launch_bounds__(64) void frame_opt_kernel(Args a, int batch) {
+  extern __shared__ double smem[];
+  const int f = blockIdx.x;
+  const int lane = threadIdx.x;
+  const Desc D = a.frames[f];
+  View V;
+  V.n = D.n;
+  V.delta0 = D.delta[0];
+  V.delta1 = D.delta[1];
+  const double th0 = D.th[0], th1 = D.th[1];
+  if constexpr (LDS) {
+    Edge* Es = reinterpret_cast<Edge*>(smem);
+    const double* src = reinterpret_cast<const double*>(a.edges + D.e0);
+    double* dst = smem;
+    for (int k = lane; k < D.n * (int)(sizeof(Edge) / 8); k += 64) dst[k] = src[k];
+    V.E = Es;
+    V.err = smem + D.n * (sizeof(Edge) / 8);
+    V.lev = reinterpret_cast<uint8_t*>(V.err + 3 * D.n);
+    V.inl = V.lev + D.n;
+  } else {
+    V.E = a.edges + D.e0;
+    V.err = a.err + 4 * (size_t)D.e0;
+    V.lev = a.level + D.e0;
+    V.inl = a.inl + D.e0;
+  }
+  for (int e = lane; e < D.n; e += 64) {
+    V.inl[e] = a.inl_in[D.e0 + e];
+    V.lev[e] = 0;
+  }
+  __syncthreads();  // single-wave block: orders the LDS staging
+  SE3 T0;
+  for (int k = 0; k < 4; k++) T0.q[k] = D.T0[k];
+  for (int k = 0; k < 3; k++) T0.t[k] = D.T0[4 + k];
+  Pose P;
+  P.set(T0);
+  // per-round results in scalars (a loop-indexed array would live in scratch)
+  double c2r[4] = {0, 0, 0, 0};
+  int itr[4] = {0, 0, 0, 0};
+  int rounds = 0;
+  int num_outlier = 0;
+#pragma unroll 1
+  for (int r = 0; r < 4; r++) {
+    P.set(T0);  // setEstimate(SE3Quat(pose).inverse()) every round (:337)
+    const bool robust = r < 3;  // setRobustKernel(0) after round 2's classification (:363)
+    int act = 0;
+    for (int e = lane; e < D.n; e += 64) act += V.lev[e] == 0;
+    act = wsum_int(act);
+    int its = 0;
+    double chi = 0;
+    if (act) its = optimize_pose(V, P, lane, robust, 10, chi);
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+      if (k == r) {
+        itr[k] = its;
+        c2r[k] = chi;
+      }
+    int no = 0;
+    for (int e = lane; e < D.n; e += 64) {
+      double* er = V.err + 3 * e;
+      const Edge E = V.E[e];
+      double ev[3];
+      if (!V.inl[e]) {  // computeError() at the current estimate (:345-347)
+        double Xc[3];
+        edge_error(E, P, Xc, ev);
+      } else {          // the last error the optimizer computed
+        ev[0] = er[0]; ev[1] = er[1]; ev[2] = er[2];
+      }
+      const float c2 = (float)chi2_of(ev);  // const float chi2 = e->chi2() (:349)
+      if (c2 > (E.stereo != 0.0 ? th1 : th0)) {
+        V.inl[e] = 0;
+        V.lev[e] = 1;
+        no++;
+      } else {
+        V.inl[e] = 1;
+        V.lev[e] = 0;
+      }
+    }
+    num_outlier = wsum_int(no);
+    rounds = r + 1;
+    if (D.n < 10) break;  // optimizer.edges().size() < 10 (:383)
+  }
+  for (int e = lane; e < D.n; e += 64) a.inl_out[D.e0 + e] = V.inl[e];
+  if (lane == 0) {
+    Out* o = a.out + f;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      o->T[k] = P.T.q[k];
+      o->chi2[k] = c2r[k];
+      o->iters[k] = itr[k];
+    }
+#pragma unroll
+    for (int k = 0; k < 3; k++) o->T[4 + k] = P.T.t[k];
+    o->T[7] = 0;
+    o->n_inliers = D.n - num_outlier;
+    o->rounds = rounds;
+  }
+}
+
+size_t lds_bytes(int n) { return (size_t)n * (sizeof(Edge) + 3 * sizeof(double) + 2); }
+
+hipError_t optimize(const Args& a, int batch, int max_n, hipStream_t s) {
+  if (batch <= 0) return hipSuccess;
+  if (max_n <= kLdsEdges) frame_opt_kernel<true><<<batch, 64, lds_bytes(max_n), s>>>(a, batch);
+  else frame_opt_kernel<false><<<batch, 64, 0, s>>>(a, batch);
+  return hipGetLastError();
+}
+
+}  // namespace frame
+}  // namespace rspl

@@ -213,3 +213,39 @@ def ba_problem(n_poses: int = 10, n_points: int = 2000, n_lines: int = 50, obs_p
                         mono_line=arr(mline, 4), stereo_line=arr(sline, 8))
     gt = dict(pose_q=q_gt, pose_p=p_gt, points=pts, lines=lines_gt)
     return prob, gt
+
+
+def frame_problem(n_points: int = 300, pixel_sigma: float = 0.8, outlier_frac: float = 0.1, seed: int = 0,
+                  init_rot: float = 0.01, init_trans: float = 0.05, stereo_frac: float = 0.6,
+                  width: int = 752, height: int = 480, cam=(EUROC_FX, EUROC_FY, EUROC_CX, EUROC_CY, EUROC_BF)):
+    """Seeded FrameOptimization problem (MapBuilder::FramePoseOptimization shape, map_builder.cc:536-580):
+    one camera pose, ``n_points`` fixed map points visible in it, a stereo constraint when the right
+    coordinate is valid (``stereo_frac`` of them), else mono; ``outlier_frac`` gross mismatches;
+    the initial pose is the ground truth perturbed as a PnP initialisation would be.
+    Returns (FrameProblem, gt) with gt = dict(pose_q, pose_p)."""
+    from .ba_types import FrameProblem
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = cam
+    Rwc = _rotvec_to_R(rng.normal(0, 0.1, 3))
+    twc = rng.normal(0, 1.0, 3)
+    pts, mono, stereo = [], dict(lm=[], obs=[], out=[]), dict(lm=[], obs=[], out=[])
+    while len(pts) < n_points:
+        u, v, z = rng.uniform(0, width), rng.uniform(0, height), rng.uniform(1.5, 20.0)
+        Xc = np.array([(u - cx) / fx * z, (v - cy) / fy * z, z])
+        X = Rwc @ Xc + twc
+        j = len(pts)
+        pts.append(X)
+        obs = np.array([u, v, u - bf / z]) + rng.normal(0, pixel_sigma, 3)
+        out = rng.uniform() < outlier_frac
+        if out:
+            obs[:2] += rng.uniform(20, 80, 2) * rng.choice([-1, 1], 2)
+        d = stereo if obs[2] > 0 and rng.uniform() < stereo_frac else mono
+        d["lm"].append(j); d["obs"].append(obs if d is stereo else obs[:2]); d["out"].append(out)
+    dR = _rotvec_to_R(rng.normal(0, init_rot, 3))
+    q0 = R_to_quat_xyzw(dR @ Rwc)
+    p0 = twc + rng.normal(0, init_trans, 3)
+    arr = lambda d, od: dict(lm=np.array(d["lm"], np.int32), obs=np.array(d["obs"], np.float64).reshape(-1, od))
+    prob = FrameProblem(cameras=np.array([cam], np.float64), pose_q=q0, pose_p=p0, points=np.array(pts),
+                        mono=arr(mono, 2), stereo=arr(stereo, 3))
+    return prob, dict(pose_q=R_to_quat_xyzw(Rwc), pose_p=twc, outlier_mono=np.array(mono["out"], bool),
+                      outlier_stereo=np.array(stereo["out"], bool))
