@@ -274,6 +274,43 @@ int rspl_ba_local(rspl_ba* ba, const rspl_ba_problem* problem, rspl_ba_result* r
 void rspl_ba_destroy(rspl_ba* ba);
 
 /* ------------------------------------------------------------------------ */
+/* Landmark-sharded local BA: nranks handles -- one per  */
+/* GPU (RCCL over xGMI), or several on one device (in-process group) -- each  */
+/* call rspl_ba_local with the SAME problem.  Rank r keeps only the edges of  */
+/* the landmarks it owns (landmark g owned by rank g % nranks: points first,  */
+/* then lines, as in rspl_ba_problem), computes its Schur contribution       */
+/* S_r = sum (Hpp - Hpl Hll^-1 Hlp) / b_r, and the ranks sum-all-reduce, per  */
+/* LM trial, the reduced camera system (pose-pair blocks + gradients + the    */
+/* landmark-inversion flag) and the trial's {chi2, LM scale, fail}; at        */
+/* lambda-init the pose-block diagonals and each rank's landmark maximum.    */
+/* Every rank factors the same reduced system, so the LM decisions agree.    */
+/* Results are complete on every rank (owned landmarks and edge flags are    */
+/* gathered by a final all-reduce).                                          */
+/* ------------------------------------------------------------------------ */
+/* in-place sum all-reduce of count doubles on a HIP stream (stream-ordered); 0 = ok */
+typedef int (*rspl_allreduce_fn)(void* ctx, double* d_buf, size_t count, void* stream);
+int rspl_ba_set_shard(rspl_ba* ba, int rank, int nranks, rspl_allreduce_fn allreduce, void* ctx);
+
+/* RCCL communicator (librccl is loaded at first use).  Rank 0 makes the id, the
+ * caller broadcasts its RSPL_COMM_ID_BYTES to the other ranks out of band
+ * (e.g. torch.distributed), every rank creates its communicator. */
+#define RSPL_COMM_ID_BYTES 128
+typedef struct rspl_comm rspl_comm;
+int rspl_comm_unique_id(uint8_t* id /* [RSPL_COMM_ID_BYTES] */);
+int rspl_comm_create(const uint8_t* id, int rank, int nranks, int device, rspl_comm** out);
+int rspl_comm_allreduce_sum(void* comm, double* d_buf, size_t count, void* stream);  /* an rspl_allreduce_fn */
+void rspl_comm_destroy(rspl_comm* comm);
+int rspl_ba_set_comm(rspl_ba* ba, rspl_comm* comm);
+
+/* In-process group: nranks BA handles on ONE device, each driven by its own host
+ * thread (a landmark-sharded solve inside one GPU; also how the sharded math is
+ * tested on a single-GPU host).  The sum is formed in rank order on the device. */
+typedef struct rspl_group rspl_group;
+int rspl_group_create(int nranks, rspl_group** out);
+void rspl_group_destroy(rspl_group* group);
+int rspl_ba_set_group(rspl_ba* ba, rspl_group* group, int rank);
+
+/* ------------------------------------------------------------------------ */
 /* Tracking pose optimisation: FrameOptimization                            */
 /* (src/g2o_optimization/g2o_optimization.cc:256-398, declared at           */
 /* include/g2o_optimization/g2o_optimization.h:20-22; called per frame by   */

@@ -9,7 +9,8 @@ import importlib
 from . import capi, weights, synthetic, ba_types  # noqa: F401
 
 _API = ("SuperPoint", "SuperPointConfig", "SuperGlue", "SuperGlueConfig", "PointMatching",
-        "LocalmapOptimization", "LocalBA", "FrameOptimization", "FrameBA")
+        "LocalmapOptimization", "LocalBA", "FrameOptimization", "FrameBA",
+        "ShardGroup", "Comm", "comm_unique_id", "broadcast_comm_id")
 
 
 def __getattr__(name):

@@ -227,10 +227,68 @@ class LocalBA:
         res.read_back(R)
         return res
 
+    def set_group(self, group: "ShardGroup", rank: int):
+        """Landmark-sharded solve: this handle is rank `rank` of an in-process group (one device)."""
+        capi.check(self._lib.rspl_ba_set_group(self._h, group.handle, rank), "rspl_ba_set_group")
+        self._shard = group  # keep the group alive while the handle uses it
+
+    def set_comm(self, comm: "Comm"):
+        """Landmark-sharded solve across processes / GPUs over RCCL (one rank per GPU)."""
+        capi.check(self._lib.rspl_ba_set_comm(self._h, comm.handle), "rspl_ba_set_comm")
+        self._shard = comm
+
     def __del__(self):
         if getattr(self, "_h", None) and self._h.value:
             self._lib.rspl_ba_destroy(self._h)
             self._h = C.c_void_p()
+
+
+class ShardGroup:
+    """rspl_group: nranks LocalBA handles on one device, each driven by its own host thread."""
+
+    def __init__(self, nranks: int):
+        self._lib = capi.load()
+        self.handle = C.c_void_p()
+        self.nranks = nranks
+        capi.check(self._lib.rspl_group_create(nranks, C.byref(self.handle)), "rspl_group_create")
+
+    def __del__(self):
+        if getattr(self, "handle", None) and self.handle.value:
+            self._lib.rspl_group_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id() -> bytes:
+    """RCCL unique id (rank 0 makes it; broadcast it out of band, e.g. with torch.distributed)."""
+    buf = (C.c_uint8 * COMM_ID_BYTES)()
+    capi.check(capi.load().rspl_comm_unique_id(buf), "rspl_comm_unique_id")
+    return bytes(buf)
+
+
+class Comm:
+    """rspl_comm: an RCCL communicator (one rank per GPU, xGMI within the node)."""
+
+    def __init__(self, unique_id: bytes, rank: int, nranks: int, device: int = 0):
+        self._lib = capi.load()
+        self.handle = C.c_void_p()
+        self.rank, self.nranks = rank, nranks
+        uid = (C.c_uint8 * COMM_ID_BYTES).from_buffer_copy(unique_id)
+        capi.check(self._lib.rspl_comm_create(uid, rank, nranks, device, C.byref(self.handle)), "rspl_comm_create")
+
+    def __del__(self):
+        if getattr(self, "handle", None) and self.handle.value:
+            self._lib.rspl_comm_destroy(self.handle)
+            self.handle = C.c_void_p()
+
+
+def broadcast_comm_id(dist, make_id=comm_unique_id) -> bytes:
+    """Rank 0 makes the RCCL id, every rank of the (gloo) process group receives it."""
+    obj = [make_id() if dist.get_rank() == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    return obj[0]
 
 
 _default_ba = None

@@ -29,6 +29,8 @@ EXPORTS = [
     "rspl_pm_match",
     "rspl_ba_create", "rspl_ba_local", "rspl_ba_destroy",
     "rspl_frame_create", "rspl_frame_optimize", "rspl_frame_destroy",
+    "rspl_ba_set_shard", "rspl_comm_unique_id", "rspl_comm_create", "rspl_comm_allreduce_sum", "rspl_comm_destroy",
+    "rspl_ba_set_comm", "rspl_group_create", "rspl_group_destroy", "rspl_ba_set_group",
 ]
 
 
@@ -120,6 +122,18 @@ def load(path: pathlib.Path = LIB_PATH):
         lib.rspl_ba_local.argtypes = [vp, vp, vp]
         lib.rspl_ba_destroy.argtypes = [vp]
         lib.rspl_ba_destroy.restype = None
+    if hasattr(lib, "rspl_ba_set_shard"):
+        lib.rspl_ba_set_shard.argtypes = [vp, ip, ip, vp, vp]
+        lib.rspl_comm_unique_id.argtypes = [vp]
+        lib.rspl_comm_create.argtypes = [vp, ip, ip, ip, C.POINTER(vp)]
+        lib.rspl_comm_allreduce_sum.argtypes = [vp, vp, C.c_size_t, vp]
+        lib.rspl_comm_destroy.argtypes = [vp]
+        lib.rspl_comm_destroy.restype = None
+        lib.rspl_ba_set_comm.argtypes = [vp, vp]
+        lib.rspl_group_create.argtypes = [ip, C.POINTER(vp)]
+        lib.rspl_group_destroy.argtypes = [vp]
+        lib.rspl_group_destroy.restype = None
+        lib.rspl_ba_set_group.argtypes = [vp, vp, ip]
     if hasattr(lib, "rspl_frame_create"):
         lib.rspl_frame_create.argtypes = [C.POINTER(FrameConfig), C.POINTER(vp)]
         lib.rspl_frame_optimize.argtypes = [vp, vp, ip, vp]

@@ -58,17 +58,35 @@ struct rspl_ba {
   ba::Mail* mail_dev = nullptr;
   unsigned long long seq = 0;
   std::vector<uint8_t> pact;  // host scratch reused across calls
+  // landmark sharding (rspl_ba_set_shard): this rank keeps the edges of landmarks g % nranks == rank
+  int rank = 0, nranks = 1;
+  rspl_allreduce_fn allreduce = nullptr;
+  void* ar_ctx = nullptr;
+  double* red = nullptr;       // [6 maxK + kMaxRanks + 3] lambda-init / cost all-reduce buffer
+  double* gbuf = nullptr;      // final gather buffer (grown on demand)
+  size_t gcap = 0;
 };
 
 namespace {
 
 constexpr int kMaxCams = 16;
+constexpr int kMaxRanks = 64;
+
+// the rank's sum all-reduce, stream-ordered on the BA stream
+int allreduce(rspl_ba* b, double* d, size_t n) {
+  const int rc = b->allreduce(b->ar_ctx, d, n, b->stream);
+  if (rc) {
+    set_error("BA shard all-reduce failed (rank %d of %d, %zu doubles, rc %d)", b->rank, b->nranks, n, rc);
+    return RSPL_E_DEVICE;
+  }
+  return RSPL_OK;
+}
 
 inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // per-call upload layout (staging call region == device call buffer)
 struct CallLayout {
-  size_t cams, T, X, L, obs, type, pose, lm, cam, pidx, lm_off, lm_act, pairs, level, fill, flags, out, bytes;
+  size_t cams, T, X, L, obs, type, pose, lm, cam, gmap, pidx, lm_off, lm_act, pairs, level, fill, flags, out, bytes;
   CallLayout(int ncam, int np, int nq, int nl, int E) {
     const size_t nL = (size_t)nq + nl;
     size_t so = 0;
@@ -79,7 +97,7 @@ struct CallLayout {
     };
     cams = place(sizeof(double) * 5 * ncam); T = place(sizeof(double) * 8 * np); X = place(sizeof(double) * 3 * nq);
     L = place(sizeof(double) * 6 * nl); obs = place(sizeof(double) * 8 * (size_t)E); type = place(E);
-    pose = place(4 * (size_t)E); lm = place(4 * (size_t)E); cam = place(4 * (size_t)E);
+    pose = place(4 * (size_t)E); lm = place(4 * (size_t)E); cam = place(4 * (size_t)E); gmap = place(4 * (size_t)E);
     pidx = place(4 * (size_t)np); lm_off = place(4 * (nL + 1)); lm_act = place(nL);
     pairs = place(8 * (size_t)np * (np + 1) / 2);
     level = place(E); fill = place(4 * nL); flags = place(4 * sizeof(int)); out = place(8 * sizeof(double));  // zeros
@@ -117,7 +135,8 @@ void carve(F& ar, rspl_ba* b) {
   take(b->lm_ctr, nl);
   const size_t npairs = K * (K + 1) / 2, nchk = std::max<size_t>((NL + ba::kLmChunk - 1) / ba::kLmChunk, 1);
   take(b->lm_edges, E); take(b->lm_pose, E);
-  take(b->chunk, npairs * nchk * 48); take(b->pairfin, npairs * 48); take(b->pair_ctr, npairs);
+  take(b->chunk, npairs * nchk * 48); take(b->pairfin, npairs * 48 + 8); take(b->pair_ctr, npairs);
+  take(b->red, 6 * K + kMaxRanks + 8);
   take(b->pp_cnt, npairs * nchk); take(b->pp_off, npairs * nchk + 1);
 }
 
@@ -204,9 +223,22 @@ int optimize(rspl_ba* b, ba::Problem& P, const ba::Lin& Lr, ba::Sys& S, const ba
   hipStream_t st = b->stream;
   double v[4];
   int rc;
+  const bool sh = b->allreduce != nullptr;
+  const int n6 = 6 * A.K;
+  double* so = b->red + n6 + b->nranks;  // this rank's {chi2, scale, fail} (S.shard_out)
   unsigned long long q = ++b->seq;
   RSPL_HIP(ba::compute_errors(P, Lr, A, S, q, st));
-  if (iters > 0) {  // the first linearisation does not depend on the cost: queue it right behind
+  if (sh) {  // sum the ranks' costs (and, before the first iteration, the lambda-init diagonals)
+    if (iters > 0) {
+      RSPL_HIP(ba::linearize(P, Lr, A, S, true, st));
+      RSPL_HIP(ba::shard_fold(A, S, b->red, b->rank, b->nranks, st));
+      if ((rc = allreduce(b, b->red, ba::shard_red_len(A.K, b->nranks)))) return rc;
+      RSPL_HIP(ba::shard_post(S, b->red, n6, b->nranks, 0, 0, q, st));
+    } else {
+      if ((rc = allreduce(b, so, 3))) return rc;
+      RSPL_HIP(ba::shard_post(S, b->red, n6, b->nranks, 1, 0, q, st));
+    }
+  } else if (iters > 0) {  // the first linearisation does not depend on the cost: queue it right behind
     RSPL_HIP(ba::linearize(P, Lr, A, S, true, st));
     q = ++b->seq;
     RSPL_HIP(ba::post(S, q, st, &A));  // posts chi2 (S.out[0]) and the max diagonal (S.out[2])
@@ -221,7 +253,15 @@ int optimize(rspl_ba* b, ba::Problem& P, const ba::Lin& Lr, ba::Sys& S, const ba
     int qmax = 0;
     do {
       q = ++b->seq;
-      RSPL_HIP(ba::trial(P, Lr, A, S, lambda, q, st));
+      if (sh) {  // Schur chunks -> sum of the reduced systems -> identical solve on every rank
+        RSPL_HIP(ba::trial_chunks(P, Lr, A, S, lambda, st));
+        if ((rc = allreduce(b, S.pairfin, (size_t)A.npairs * 48 + 1))) return rc;
+        RSPL_HIP(ba::trial_solve(P, Lr, A, S, lambda, st));
+        if ((rc = allreduce(b, so, 3))) return rc;
+        RSPL_HIP(ba::shard_post(S, b->red, n6, b->nranks, 1, ba::fast_path(A.K) ? 1 : 0, q, st));
+      } else {
+        RSPL_HIP(ba::trial(P, Lr, A, S, lambda, q, st));
+      }
       if ((rc = wait_mail(b, q, v))) return rc;
       const bool ok = v[3] == 0.0;
       const double tempChi = ok ? v[0] : std::numeric_limits<double>::max();
@@ -293,9 +333,24 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
   return RSPL_OK;
 }
 
+extern "C" int rspl_ba_set_shard(rspl_ba* b, int rank, int nranks, rspl_allreduce_fn fn, void* ctx) {
+  RSPL_CHECK_ARG(b, "rspl_ba_set_shard: NULL handle");
+  RSPL_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks && rank >= 0 && rank < nranks, "rank %d of %d (1..%d ranks)", rank,
+                 nranks, kMaxRanks);
+  RSPL_CHECK_ARG(nranks == 1 || fn, "an all-reduce function is required for nranks > 1");
+  // with fn the sharded schedule runs even for one rank (every all-reduce an identity): the
+  // collective path can be exercised on a single GPU; fn == NULL with one rank = unsharded
+  b->rank = rank;
+  b->nranks = nranks;
+  b->allreduce = fn;
+  b->ar_ctx = ctx;
+  return RSPL_OK;
+}
+
 extern "C" void rspl_ba_destroy(rspl_ba* b) {
   if (!b) return;
   if (b->stream) (void)hipStreamSynchronize(b->stream);
+  if (b->gbuf) (void)hipFree(b->gbuf);
   b->arena.release();
   if (b->cbuf) (void)hipFree(b->cbuf);
   if (b->pp_buf) (void)hipFree(b->pp_buf);
@@ -317,7 +372,27 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   RSPL_CHECK_ARG(res->pose_q && res->pose_p && (res->points || !nq) && (res->lines || !nl), "NULL result arrays");
   RSPL_CHECK_ARG(np == 0 || pr->pose_fixed, "NULL pose_fixed");
   hipStream_t st = b->stream;
-  const int E = ne[0] + ne[1] + ne[2] + ne[3], nL = nq + nl;
+  const int Eg = ne[0] + ne[1] + ne[2] + ne[3], nL = nq + nl;
+  // landmark sharding: this rank keeps the edges of its landmarks (g % nranks == rank)
+  const bool sh = b->allreduce != nullptr;
+  const int32_t* lms_[4] = {pr->mono_point, pr->stereo_point, pr->mono_line_line, pr->stereo_line_line};
+  auto owned = [&](int t, int i) {
+    const int g = t < 2 ? lms_[t][i] : nq + lms_[t][i];
+    return !sh || g % b->nranks == b->rank;
+  };
+  int E = Eg, n_line_local = ne[2] + ne[3];
+  if (sh) {
+    E = 0;
+    n_line_local = 0;
+    for (int t = 0; t < 4; t++) {
+      RSPL_CHECK_ARG(ne[t] == 0 || lms_[t], "NULL edge arrays");
+      for (int i = 0; i < ne[t]; i++)
+        if (lms_[t][i] >= 0 && lms_[t][i] < (t < 2 ? nq : nl) && owned(t, i)) {
+          E++;
+          n_line_local += t >= 2;
+        }
+    }
+  }
   // optional host-side stage timing (RSPL_BA_TIMING=1): prep, build1, opt1, classify, build2, opt2, final
   static const bool timing = getenv("RSPL_BA_TIMING") != nullptr;
   using clk = std::chrono::steady_clock;
@@ -329,7 +404,7 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   mark();
   // ---- one staging region for the whole call, mirrored by the device call buffer ----
   const CallLayout cl(pr->n_cameras, np, nq, nl, E);
-  const DownLayout dl(np, nq, nl, E);
+  const DownLayout dl(np, nq, nl, Eg);  // inlier flags by global edge id
   int rc;
   if ((rc = ensure_stage(b, std::max(cl.bytes, dl.bytes)))) return rc;
   char* sg = b->stage;
@@ -364,22 +439,26 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   int* lm_off = reinterpret_cast<int*>(sg + cl.lm_off);
   memset(lm_off, 0, sizeof(int) * (nL + 1));
   b->pact.assign(np, 0);
-  int e = 0;
+  int* gmap = reinterpret_cast<int*>(sg + cl.gmap);
+  int e = 0, eg = 0;
   for (int t = 0; t < 4; t++) {
     RSPL_CHECK_ARG(ne[t] == 0 || (poses[t] && lms[t] && obs[t]), "NULL edge arrays");
-    for (int i = 0; i < ne[t]; i++, e++) {
+    for (int i = 0; i < ne[t]; i++, eg++) {
       const int p = poses[t][i], l = lms[t][i], c = cams[t] ? cams[t][i] : 0;
       RSPL_CHECK_ARG(p >= 0 && p < np && l >= 0 && l < (t < 2 ? nq : nl) && c >= 0 && c < pr->n_cameras,
                      "edge %d of type %d references a missing vertex/camera", i, t);
+      b->pact[p] = 1;  // a pose is optimised when it has an edge on ANY rank: K agrees across ranks
+      if (!owned(t, i)) continue;
       etype[e] = (int8_t)t;
       epose[e] = p;
       elm[e] = t < 2 ? l : nq + l;
       ecam[e] = c;
+      gmap[e] = eg;
       lm_off[elm[e] + 1]++;
-      b->pact[p] = 1;
       double* o = eobs + 8 * (size_t)e;
       const double* src = obs[t] + (size_t)od[t] * i;
       for (int k = 0; k < 8; k++) o[k] = k < od[t] ? src[k] : 0.0;
+      e++;
     }
   }
   uint8_t* lm_act = reinterpret_cast<uint8_t*>(sg + cl.lm_act);
@@ -446,6 +525,8 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   S.chunk = b->chunk;
   S.pairfin = b->pairfin;
   S.pair_ctr = b->pair_ctr;
+  S.shard_out = sh ? b->red + 6 * K + b->nranks : nullptr;
+  S.pose_scale = !sh || b->rank == 0;
   // ---- phase 1: all edges, Huber ----
   ba::Active A{};
   A.Ea = E;
@@ -457,7 +538,7 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   A.pairs = reinterpret_cast<const int*>(cb + cl.pairs);
   A.npairs = K * (K + 1) / 2;
   A.nchk = std::max((nL + ba::kLmChunk - 1) / ba::kLmChunk, 1);
-  A.n_line_edges = ne[2] + ne[3];
+  A.n_line_edges = n_line_local;
   A.K = K;
   A.nL = nL;
   A.robust = 1;
@@ -489,9 +570,27 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   // ---- inlier flags + final state written by the GPU into the mapped staging buffer ----
   // (the staging call region was consumed by the upload long before: the stream is in order)
   const unsigned long long q = ++b->seq;
-  RSPL_HIP(ba::finish(P, Lr, E, reinterpret_cast<uint8_t*>(b->stage_dev + dl.inl), reinterpret_cast<double*>(b->stage_dev + dl.T),
-                      reinterpret_cast<double*>(b->stage_dev + dl.X), reinterpret_cast<double*>(b->stage_dev + dl.L),
-                      S, q, st));
+  uint8_t* inl_h = reinterpret_cast<uint8_t*>(b->stage_dev + dl.inl);
+  double* T_h = reinterpret_cast<double*>(b->stage_dev + dl.T);
+  double* X_h = reinterpret_cast<double*>(b->stage_dev + dl.X);
+  double* L_h = reinterpret_cast<double*>(b->stage_dev + dl.L);
+  if (sh) {  // owned landmarks + local edge flags gathered by one more all-reduce: complete on every rank
+    const size_t glen = 3 * (size_t)nq + 6 * (size_t)nl + Eg;
+    if (glen > b->gcap) {
+      RSPL_HIP(hipStreamSynchronize(st));
+      if (b->gbuf) (void)hipFree(b->gbuf);
+      b->gbuf = nullptr;
+      b->gcap = 0;
+      RSPL_HIP(hipMalloc((void**)&b->gbuf, sizeof(double) * std::max<size_t>(glen, 1024)));
+      b->gcap = std::max<size_t>(glen, 1024);
+    }
+    RSPL_HIP(hipMemsetAsync(b->gbuf, 0, sizeof(double) * glen, st));
+    RSPL_HIP(ba::shard_gather(P, Lr, E, reinterpret_cast<const int*>(cb + cl.gmap), b->rank, b->nranks, b->gbuf, st));
+    if (glen && (rc = allreduce(b, b->gbuf, glen))) return rc;
+    RSPL_HIP(ba::shard_finish(P, Eg, b->gbuf, inl_h, T_h, X_h, L_h, S, q, st));
+  } else {
+    RSPL_HIP(ba::finish(P, Lr, E, inl_h, T_h, X_h, L_h, S, q, st));
+  }
   if ((rc = wait_mail(b, q, nullptr))) return rc;
   if (nq) memcpy(res->points, b->stage + dl.X, sizeof(double) * 3 * nq);
   if (nl) memcpy(res->lines, b->stage + dl.L, sizeof(double) * 6 * nl);

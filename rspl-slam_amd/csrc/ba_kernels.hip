@@ -193,6 +193,15 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
     S.out[0] = chi2;
     S.out[1] = scale;
     S.out[3] = f;
+    if (S.shard_out) {  // sharded: this rank's share goes to the all-reduce, shard_post posts
+      S.shard_out[0] = chi2;
+      S.shard_out[1] = scale;
+      S.shard_out[2] = f;
+      __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(S.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      S.out[2] = 0.0;
+      return;
+    }
     Mail* m = S.mail;
     m->v[0] = chi2;
     m->v[1] = scale;
@@ -871,7 +880,10 @@ __global__ __launch_bounds__(256) void pair_final_kernel(Active A, Sys S, double
 //   solve:    backward substitution L^T x = z in wave 0, LDS-resident;
 //   poses:    the candidate T <- exp(xp) T and the pose part of the LM scale.
 // ---------------------------------------------------------------------------
-constexpr int kCholLdsMax = 132;  // (n+1) ((n+1)|1) + 2n + 15 n/6 doubles <= 160 KB of LDS
+constexpr int kCholLdsMax = 192;  // packed lower triangle (n+1)(n+2)/2 + 2n + 15 n/6 doubles <= 160 KB of LDS
+
+// packed row-major lower triangle: element (r, c <= r)
+__device__ __forceinline__ int pk(int r, int c) { return r * (r + 1) / 2 + c; }
 
 // 1/d to full precision: v_rcp_f64 + two Newton steps (no divide sequence on the chain)
 __device__ __forceinline__ double rcp64(double d) {
@@ -880,14 +892,14 @@ __device__ __forceinline__ double rcp64(double d) {
   return fma(r, fma(-d, r, 1.0), r);
 }
 
-// LDL^T of a 6x6 SPD block (lower triangle at Ld, stride ld): unit L (strictly-lower,
-// packed row-major into L6), D (d6) and 1/D (r6); false unless every pivot is > 0
-__device__ __forceinline__ bool ldl6(const double* Ld, int ld, double (&L6)[15], double (&d6)[6], double (&r6)[6]) {
+// LDL^T of the 6x6 SPD diagonal block at (c0, c0) of the packed lower triangle Al: unit L
+// (strictly-lower, packed row-major into L6), D (d6) and 1/D (r6); false unless every pivot is > 0
+__device__ __forceinline__ bool ldl6(const double* Al, int c0, double (&L6)[15], double (&d6)[6], double (&r6)[6]) {
   double a[6][6];
 #pragma unroll
   for (int i = 0; i < 6; i++)
 #pragma unroll
-    for (int k = 0; k <= i; k++) a[i][k] = Ld[i * ld + k];
+    for (int k = 0; k <= i; k++) a[i][k] = Al[pk(c0 + i, c0 + k)];
   bool ok = true;
 #pragma unroll
   for (int j = 0; j < 6; j++) {
@@ -927,11 +939,11 @@ __device__ __forceinline__ void pair_of(int pr, int K, int& a, int& b) {
 }
 
 __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, Sys S, int n, double lambda) {
-  extern __shared__ double Al[];     // rows 0..n: the matrix (lower triangle) + the bordered rhs row n
+  extern __shared__ double Al[];     // rows 0..n, packed lower triangle: the matrix + the bordered rhs row n
   __shared__ int bad;
-  const int ld = (n + 1) | 1, K = n / 6;
-  double* z = Al + (size_t)n * ld;   // row n: bs -> z = D^-1 L^-1 bs -> solution x
-  double* rdg = Al + (size_t)(n + 1) * ld;  // [n] 1/D
+  const int K = n / 6;
+  double* z = Al + pk(n, 0);         // row n: bs -> z = D^-1 L^-1 bs -> solution x
+  double* rdg = Al + pk(n + 1, 0);   // [n] 1/D
   double* ddg = rdg + n;                    // [n] D
   double* Ldg = ddg + n;                    // [K][15] strictly-lower parts of the (unit) diagonal blocks
   const int tid = threadIdx.x;
@@ -959,9 +971,9 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
       if (v < 36) {
         const int r = v / 6, cc = v - 6 * r;
         if (pa == pb) {
-          if (cc <= r) Al[(6 * pa + r) * ld + 6 * pa + cc] = v1[u] + (r == cc ? lambda : 0.0);
+          if (cc <= r) Al[pk(6 * pa + r, 6 * pa + cc)] = v1[u] + (r == cc ? lambda : 0.0);
         } else {
-          Al[(6 * pb + cc) * ld + 6 * pa + r] = v1[u];
+          Al[pk(6 * pb + cc, 6 * pa + r)] = v1[u];
         }
       } else if (pa == pb) {
         const int r = v - 36;
@@ -978,7 +990,7 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
     const int c0 = 6 * s, r0 = c0 + 6;
     if (wv == 0) {  // (1) diagonal block (every lane, uniform) + (2) panel rows, one per lane
       double L6[15], d6[6], r6[6];
-      const bool ok = ldl6(Al + c0 * ld + c0, ld, L6, d6, r6);
+      const bool ok = ldl6(Al, c0, L6, d6, r6);
       if (lane == 0) {
 #pragma unroll
         for (int q = 0; q < 15; q++) Ldg[15 * s + q] = L6[q];
@@ -990,7 +1002,7 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
         if (!ok) bad = 1;
       }
       for (int i = r0 + lane; i <= n; i += 64) {  // x = a L_dd^-T D^-1 (unit L: no divides)
-        double* row = Al + i * ld + c0;
+        double* row = Al + pk(i, c0);
         double w[6];
 #pragma unroll
         for (int k = 0; k < 6; k++) w[k] = row[k];
@@ -1011,14 +1023,14 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
     for (int i = r0 + fy; i <= n; i += 16) {  // (3) trailing update A22 -= X D X^T (+ the rhs row)
       double wi[6];
 #pragma unroll
-      for (int l = 0; l < 6; l++) wi[l] = Al[i * ld + c0 + l] * ddg[c0 + l];
+      for (int l = 0; l < 6; l++) wi[l] = Al[pk(i, c0 + l)] * ddg[c0 + l];
       const int kmax = min(i, n - 1);
       for (int k = r0 + fx; k <= kmax; k += 16) {
-        const double* xk = Al + k * ld + c0;
-        double t = Al[i * ld + k];
+        const double* xk = Al + pk(k, c0);
+        double t = Al[pk(i, k)];
 #pragma unroll
         for (int l = 0; l < 6; l++) t -= wi[l] * xk[l];
-        Al[i * ld + k] = t;
+        Al[pk(i, k)] = t;
       }
     }
     __syncthreads();
@@ -1038,7 +1050,7 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
     for (int i = lane; i < c0; i += 64) {
       double v = z[i];
 #pragma unroll
-      for (int l = 0; l < 6; l++) v -= Al[(c0 + l) * ld + i] * xb[l];
+      for (int l = 0; l < 6; l++) v -= Al[pk(c0 + l, i)] * xb[l];
       z[i] = v;
     }
     if (lane == 0)
@@ -1149,7 +1161,8 @@ __global__ __launch_bounds__(256) void update_kernel(Problem P, Lin L, Active A,
       for (int k = 0; k < 4; k++) Tq[k] = r.q[k];
       for (int k = 0; k < 3; k++) Tq[4 + k] = r.t[k];
       Tq[7] = 0;
-      for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + S.bp[6 * a + k]);
+      if (S.pose_scale)
+        for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + S.bp[6 * a + k]);
     } else {
       for (int k = 0; k < 8; k++) Tq[k] = Tp[k];
     }
@@ -1319,6 +1332,15 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     S.out[0] = chi2;
     S.out[1] = scale;
     S.out[3] = f;
+    if (S.shard_out) {  // sharded: landmark part only; shard_post adds the pose part S.out[4] once
+      S.shard_out[0] = chi2;
+      S.shard_out[1] = red[1];
+      S.shard_out[2] = f;
+      __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(S.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      S.out[2] = 0.0;
+      return;
+    }
     Mail* m = S.mail;
     m->v[0] = chi2;
     m->v[1] = scale;
@@ -1340,13 +1362,12 @@ __global__ __launch_bounds__(256) void landmark_active_kernel(Active A, const ui
 }
 
 // outlier levels after the first optimize / final inlier flags (g2o_optimization.cc:176-231)
-__device__ __forceinline__ void classify_edge(const Problem& P, const Lin& L, int e, uint8_t* level, uint8_t* inlier,
-                                              int final_pass) {
+__device__ __forceinline__ void edge_status(const Problem& P, const Lin& L, int e, double& chi2, bool& depth_ok) {
   const int t = P.etype[e];
-  double chi2 = 0;
+  chi2 = 0;
   for (int k = 0; k < edim(t); k++) chi2 += L.err[4 * e + k] * L.err[4 * e + k];
   chi2 *= einfo(t);
-  bool depth_ok = true;
+  depth_ok = true;
   if (t < 2) {
     const SE3 T = load_T(P.T + 8 * P.epose[e]);
     double R[9], Xc[3];
@@ -1354,11 +1375,23 @@ __device__ __forceinline__ void classify_edge(const Problem& P, const Lin& L, in
     mat3_vec(R, P.X + 3 * P.elm[e], Xc);
     depth_ok = Xc[2] + T.t[2] > 0.0;
   }
-  if (!final_pass) {
-    if (chi2 > P.th[t] || !depth_ok) level[e] = 1;
-  } else {
-    inlier[e] = (chi2 <= P.th[t] && depth_ok) ? 1 : 0;
+}
+__device__ __forceinline__ bool edge_inlier(const Problem& P, const Lin& L, int e) {
+  double chi2;
+  bool depth_ok;
+  edge_status(P, L, e, chi2, depth_ok);
+  return chi2 <= P.th[P.etype[e]] && depth_ok;
+}
+__device__ __forceinline__ void classify_edge(const Problem& P, const Lin& L, int e, uint8_t* level, uint8_t* inlier,
+                                              int final_pass) {
+  if (final_pass) {
+    inlier[e] = edge_inlier(P, L, e) ? 1 : 0;
+    return;
   }
+  double chi2;
+  bool depth_ok;
+  edge_status(P, L, e, chi2, depth_ok);
+  if (chi2 > P.th[P.etype[e]] || !depth_ok) level[e] = 1;
 }
 
 __global__ __launch_bounds__(256) void classify_kernel(Problem P, Lin L, int E, uint8_t* level, uint8_t* inlier,
@@ -1390,6 +1423,95 @@ __global__ __launch_bounds__(256) void finish_kernel(Problem P, Lin L, int E, ui
 }
 
 // ---------------------------------------------------------------------------
+// landmark sharding (rspl_ba_set_shard): the pieces between the host's all-reduces
+// ---------------------------------------------------------------------------
+__global__ void shard_fail_stage_kernel(Sys S, double* slot) {
+  *slot = (double)__hip_atomic_load(S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__global__ void shard_fail_adopt_kernel(Sys S, const double* slot) {
+  __hip_atomic_store(S.fail, *slot != 0.0 ? 1 : 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// this rank's pose-diagonal sums (block partials of pose_diag_kernel in block order) and its
+// landmark maximum, laid out for the sum all-reduce
+__global__ __launch_bounds__(256) void shard_fold_kernel(Sys S, double* red, int K, int npd, int rank, int nranks) {
+  const int n6 = 6 * K;
+  for (int q = threadIdx.x; q < n6; q += 256) {
+    double acc = 0;
+    if (npd > 0) {
+      const int pa = q / 6, i = q - 6 * pa;
+      const double* src = S.partial2 + (size_t)pa * npd * 6 + i;
+      for (int b = 0; b < npd; b++) acc += src[(size_t)b * 6];
+    }
+    red[q] = acc;
+  }
+  for (int r = threadIdx.x; r < nranks; r += 256) red[n6 + r] = r == rank ? S.out[2] : 0.0;
+}
+
+__global__ void shard_post_kernel(Sys S, const double* red, int n6, int nranks, int mode, int add_pose_scale,
+                                  unsigned long long seq) {
+  __shared__ double mxs[64];
+  const double* so = red + n6 + nranks;  // summed {chi2, scale, fail}
+  double mx = 0;
+  if (mode == 0) {
+    for (int q = threadIdx.x; q < n6; q += 64) mx = fmax(mx, fabs(red[q]));
+    for (int r = threadIdx.x; r < nranks; r += 64) mx = fmax(mx, red[n6 + r]);
+  }
+  mxs[threadIdx.x] = mx;
+  __syncthreads();
+  if (threadIdx.x != 0) return;
+  for (int k = 1; k < 64; k++) mx = fmax(mx, mxs[k]);
+  const double chi2 = so[0], scale = so[1] + (add_pose_scale ? S.out[4] : 0.0), f = so[2] != 0.0 ? 1.0 : 0.0;
+  if (mode == 0) S.out[2] = mx;
+  S.out[0] = chi2;
+  S.out[1] = scale;
+  S.out[3] = f;
+  Mail* m = S.mail;
+  m->v[0] = chi2;
+  m->v[1] = scale;
+  m->v[2] = mode == 0 ? mx : S.out[2];
+  m->v[3] = f;
+  __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// G = [X (owned points) | L (owned lines) | inlier flag at the global edge id of each local edge]
+__global__ __launch_bounds__(256) void shard_gather_kernel(Problem P, Lin L, int E, const int* gmap, int rank,
+                                                           int nranks, double* G) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nq3 = 3 * P.nq, nl6 = 6 * P.nl;
+  if (i < E) {
+    G[nq3 + nl6 + gmap[i]] = edge_inlier(P, L, i) ? 1.0 : 0.0;
+  }
+  if (i < nq3 && (i / 3) % nranks == rank) G[i] = P.X[i];
+  if (i < nl6 && (P.nq + i / 6) % nranks == rank) G[nq3 + i] = P.L[i];
+}
+
+__global__ __launch_bounds__(256) void shard_finish_kernel(Problem P, int E, const double* G, uint8_t* inl,
+                                                           double* Th, double* Xh, double* Lh, Sys S,
+                                                           unsigned long long seq) {
+  __shared__ int last;
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  const int nq3 = 3 * P.nq, nl6 = 6 * P.nl;
+  if (i < E) inl[i] = G[nq3 + nl6 + i] != 0.0;
+  if (i < 8 * P.np) Th[i] = P.T[i];
+  if (i < nq3) Xh[i] = G[i];
+  if (i < nl6) Lh[i] = G[nq3 + i];
+  __threadfence_system();
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned tk = __hip_atomic_fetch_add(S.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    last = tk == gridDim.x - 1;
+  }
+  __syncthreads();
+  if (!last || threadIdx.x != 0) return;
+  __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(&S.mail->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+int shard_red_len(int K, int nranks) { return 6 * K + nranks + 3; }
+bool fast_path(int K) { return 6 * K > 0 && 6 * K <= kCholLdsMax; }
+
+// ---------------------------------------------------------------------------
 int errors_blocks(int Ea) { return Ea > 0 ? (Ea + 255) / 256 : 1; }
 int update_blocks(const Problem& P) {
   const int nv = P.np + P.nq + P.nl;
@@ -1419,23 +1541,26 @@ hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A) 
   return hipGetLastError();
 }
 
+size_t schur_lds_bytes(int n) { return sizeof(double) * ((size_t)(n + 1) * (n + 2) / 2 + 2 * n + 15 * (n / 6)); }
+
+hipError_t ensure_schur_attr() {
+  static bool attr = false;
+  if (attr) return hipSuccess;
+  hipError_t e = hipFuncSetAttribute((const void*)schur_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                     (int)schur_lds_bytes(kCholLdsMax));
+  if (e == hipSuccess) attr = true;
+  return e;
+}
+
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
                  hipStream_t s) {
   if (A.npairs * A.nchk > 0)
     hipLaunchKernelGGL(pair_chunk_kernel, dim3(A.npairs * A.nchk), dim3(64), 0, s, P, L, A, S, lambda);
   const int n = 6 * A.K;
-  if (n > 0 && n <= kCholLdsMax) {
-    static bool attr = false;
-    const int nm = kCholLdsMax;
-    const size_t max_bytes = sizeof(double) * ((size_t)(nm + 1) * ((nm + 1) | 1) + 2 * nm + 15 * (nm / 6));
-    if (!attr) {
-      hipError_t e = hipFuncSetAttribute((const void*)schur_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)max_bytes);
-      if (e != hipSuccess) return e;
-      attr = true;
-    }
-    const size_t bytes = sizeof(double) * ((size_t)(n + 1) * ((n + 1) | 1) + 2 * n + 15 * (n / 6));
-    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), bytes, s, P, A, S, n, lambda);
+  if (fast_path(A.K)) {
+    hipError_t e = ensure_schur_attr();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
     hipLaunchKernelGGL(update_errors_kernel, dim3(update_errors_blocks(A)), dim3(256), 0, s, P, L, A, S, lambda, seq);
     return hipGetLastError();
   }
@@ -1483,6 +1608,63 @@ hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8
                     hipStream_t s) {
   if (E > 0) hipLaunchKernelGGL(classify_kernel, dim3((E + 255) / 256), dim3(256), 0, s, P, L, E, level, inlier,
                                 final_pass);
+  return hipGetLastError();
+}
+
+hipError_t trial_chunks(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, hipStream_t s) {
+  if (A.npairs * A.nchk > 0)
+    hipLaunchKernelGGL(pair_chunk_kernel, dim3(A.npairs * A.nchk), dim3(64), 0, s, P, L, A, S, lambda);
+  hipLaunchKernelGGL(shard_fail_stage_kernel, dim3(1), dim3(1), 0, s, S, S.pairfin + (size_t)A.npairs * 48);
+  return hipGetLastError();
+}
+
+hipError_t trial_solve(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, hipStream_t s) {
+  hipLaunchKernelGGL(shard_fail_adopt_kernel, dim3(1), dim3(1), 0, s, S, S.pairfin + (size_t)A.npairs * 48);
+  const int n = 6 * A.K;
+  if (fast_path(A.K)) {
+    hipError_t e = ensure_schur_attr();
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
+    hipLaunchKernelGGL(update_errors_kernel, dim3(update_errors_blocks(A)), dim3(256), 0, s, P, L, A, S, lambda, 0ull);
+    return hipGetLastError();
+  }
+  if (n > 0) {
+    hipLaunchKernelGGL(pair_final_kernel, dim3((A.npairs * 42 + 255) / 256), dim3(256), 0, s, A, S, lambda);
+    hipLaunchKernelGGL(cholesky_kernel, dim3(1), dim3(256), 0, s, S, n);
+  }
+  const int nbu = update_blocks(P);
+  hipLaunchKernelGGL(update_kernel, dim3(nbu), dim3(256), 0, s, P, L, A, S, lambda);
+  Problem Pn = P;
+  Pn.T = P.Tn; Pn.X = P.Xn; Pn.L = P.Ln;
+  hipLaunchKernelGGL(errors_kernel, dim3(errors_blocks(A.Ea)), dim3(256), 0, s, Pn, L, A, S, nbu, 0ull);
+  return hipGetLastError();
+}
+
+hipError_t shard_fold(const Active& A, Sys& S, double* red, int rank, int nranks, hipStream_t s) {
+  const int npd = (A.K > 0 && A.Ea > 0) ? (A.Ea + 255) / 256 : 0;
+  hipLaunchKernelGGL(shard_fold_kernel, dim3(1), dim3(256), 0, s, S, red, A.K, npd, rank, nranks);
+  return hipGetLastError();
+}
+
+hipError_t shard_post(Sys& S, const double* red, int n6, int nranks, int mode, int add_pose_scale,
+                      unsigned long long seq, hipStream_t s) {
+  hipLaunchKernelGGL(shard_post_kernel, dim3(1), dim3(64), 0, s, S, red, n6, nranks, mode, add_pose_scale, seq);
+  return hipGetLastError();
+}
+
+hipError_t shard_gather(const Problem& P, const Lin& L, int E, const int* gmap, int rank, int nranks, double* G,
+                        hipStream_t s) {
+  const int n = std::max(E, std::max(3 * P.nq, 6 * P.nl));
+  if (n > 0)
+    hipLaunchKernelGGL(shard_gather_kernel, dim3((n + 255) / 256), dim3(256), 0, s, P, L, E, gmap, rank, nranks, G);
+  return hipGetLastError();
+}
+
+hipError_t shard_finish(const Problem& P, int E_global, const double* G, uint8_t* inl, double* Th, double* Xh,
+                        double* Lh, Sys& S, unsigned long long seq, hipStream_t s) {
+  const int n = std::max(std::max(E_global, 8 * P.np), std::max(3 * P.nq, 6 * P.nl));
+  hipLaunchKernelGGL(shard_finish_kernel, dim3(std::max((n + 255) / 256, 1)), dim3(256), 0, s, P, E_global, G, inl,
+                     Th, Xh, Lh, S, seq);
   return hipGetLastError();
 }
 

@@ -78,6 +78,10 @@ struct Sys {
   unsigned* counter;     // [1] last-block ticket of the error kernel
   unsigned* lm_ctr;      // [nl] line-landmark tickets of the linearisation (re-armed to 0 by the last edge)
   Mail* mail;            // device view of the mailbox
+  // landmark sharding (null / 1 when the handle is not sharded)
+  double* shard_out;     // [3] this rank's {chi2, LM scale (landmark part), fail} for the all-reduce,
+                         //     written instead of posting the mailbox
+  int pose_scale;        // 1: this rank adds the pose part of the LM scale (rank 0 or unsharded)
 };
 
 constexpr int kLmChunk = 256;  // landmarks per Schur chunk (4 per lane)
@@ -105,6 +109,28 @@ hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8
 // final inlier flags + T / X / L into host-mapped memory, then the mailbox post of seq
 hipError_t finish(const Problem& P, const Lin& L, int E, uint8_t* inl, double* Th, double* Xh, double* Lh, Sys& S,
                   unsigned long long seq, hipStream_t s);
+// ---- landmark-sharded pieces (rspl_ba_set_shard): the host interleaves the all-reduces ----
+// trial, part 1: Schur chunks of this rank's edge pairs -> pairfin; the landmark-inversion flag
+// is staged into pairfin[npairs * 48] so it is summed with the system
+hipError_t trial_chunks(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, hipStream_t s);
+// trial, part 2 (after the pairfin all-reduce): adopt the summed flag, assemble + factor + solve
+// the (now global) reduced system, candidate state and this rank's cost / scale into shard_out
+hipError_t trial_solve(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, hipStream_t s);
+// lambda init: this rank's pose-diagonal sums into red[0, 6K), its landmark max into red[6K + rank]
+// (other rank slots zeroed); red[6K + nranks ...] holds shard_out
+hipError_t shard_fold(const Active& A, Sys& S, double* red, int rank, int nranks, hipStream_t s);
+// after the all-reduce of red: mailbox post.  mode 0: lambda init (max |pose diagonal|, max rank
+// slot); mode 1: cost only; add_pose_scale: S.out[4] (fast path) joins the summed scale
+hipError_t shard_post(Sys& S, const double* red, int n6, int nranks, int mode, int add_pose_scale,
+                      unsigned long long seq, hipStream_t s);
+// final gather: G = [X of owned points | L of owned lines | inlier flag by global edge id] (G zeroed
+// by the caller), summed across ranks, then written out by shard_finish
+hipError_t shard_gather(const Problem& P, const Lin& L, int E, const int* gmap, int rank, int nranks, double* G,
+                        hipStream_t s);
+hipError_t shard_finish(const Problem& P, int E_global, const double* G, uint8_t* inl, double* Th, double* Xh,
+                        double* Lh, Sys& S, unsigned long long seq, hipStream_t s);
+int shard_red_len(int K, int nranks);  // 6K + nranks + 3
+bool fast_path(int K);                 // the packed-LDS Schur/LDL^T path holds 6K
 int update_blocks(const Problem& P);
 int errors_blocks(int Ea);
 int update_errors_blocks(const Active& A);

@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 def ba():
     import rspl_loader
     pkg = rspl_loader.load()
-    return pkg.LocalBA(max_poses=32, max_points=12000, max_lines=400, max_edges=80000)
+    return pkg.LocalBA(max_poses=40, max_points=12000, max_lines=400, max_edges=80000)
 
 
 def _qclose(a, b):
@@ -103,10 +103,12 @@ def test_localmap_optimization_mirror(weight_blobs):
     np.testing.assert_array_equal(np.array([c.inlier for c in stereo]), ref.inlier["stereo"].astype(bool))
 
 
-@pytest.mark.parametrize("n_poses", [23, 27])
+@pytest.mark.parametrize("n_poses", [23, 33, 36])
 def test_ba_many_poses(ba, n_poses):
-    # K = 22 optimised poses is the largest reduced system the LDS Schur/Cholesky path holds
-    # (n = 132); K = 26 takes the global-memory fallback (pair_final + cholesky_kernel)
+    # K = 32 optimised poses is the largest reduced system the LDS Schur/Cholesky path holds
+    # (n = 192, packed lower triangle); K = 35 takes the global-memory fallback
+    # (pair_final + cholesky_kernel)
     prob, gt = SY.ba_problem(n_poses=n_poses, n_points=1500, n_lines=20, seed=40 + n_poses, pixel_sigma=0.8,
                              outlier_frac=0.05)
-    _compare(ba.run(prob), oracle.ba_local(prob), tol_pose=1e-6, tol_pt=1e-5)
+    # larger systems with line landmarks: numeric-Jacobian noise reaches ~1e-8 of the cost
+    _compare(ba.run(prob), oracle.ba_local(prob), tol_pose=1e-6, tol_pt=1e-5, chi2_rtol=5e-8)

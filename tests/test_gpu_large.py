@@ -130,7 +130,7 @@ def test_sg_large_vs_oracle(pkg, weight_blobs, N, M):
 
 def test_ba_c5_vs_oracle():
     """C5 local BA: 30 poses (1 fixed), 10k points each seen by 6 poses, stereo/mono mix, 5 % gross
-    outliers -- 6K = 174 > kCholLdsMax, so this runs the global-memory reduced-system path."""
+    outliers -- 6K = 174 <= kCholLdsMax = 192: the packed-LDS Schur/LDL^T path."""
     import rspl_loader
     pkg = rspl_loader.load()
     ba = pkg.LocalBA(max_poses=32, max_points=10000, max_lines=16, max_edges=70000)

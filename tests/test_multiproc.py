@@ -61,3 +61,43 @@ def test_single_rank_is_identity():
     import bench
     assert bench.job_time(2.0, None) == 2.0
     assert bench.job_value(1, 10, 2.0) == 5.0
+
+
+def _id_main(rank, world, port, out):
+    sys.path.insert(0, str(ROOT))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch.distributed as dist
+    import rspl_loader
+    pkg = rspl_loader.load()
+    from rspl_slam_amd import api
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        calls = []
+
+        def make_id():  # stands in for rspl_comm_unique_id (RCCL needs a GPU)
+            calls.append(rank)
+            return bytes(range(128))
+
+        uid = api.broadcast_comm_id(dist, make_id)
+        out.put((rank, uid, calls))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_rccl_id_broadcast_two_ranks():
+    """The sharded BA's RCCL bootstrap (api.broadcast_comm_id): only rank 0 makes the id, every
+    rank of the gloo group receives the same 128 bytes."""
+    import torch.multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_id_main, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (r0, u0, c0), (r1, u1, c1) = res
+    assert u0 == u1 == bytes(range(128))
+    assert c0 == [0] and c1 == []
