@@ -7,6 +7,9 @@
  *   PointMatching   include/point_matching.h:7-18   -> rspl_pm_*
  *   LocalmapOptimization
  *                   include/g2o_optimization/g2o_optimization.h:15-19 -> rspl_ba_*
+ *   FrameOptimization
+ *                   include/g2o_optimization/g2o_optimization.h:20-22 -> rspl_frame_*
+ *   SolvePnPWithCV  include/g2o_optimization/g2o_optimization.h:24    -> rspl_pnp_*
  * Plain pointers and sizes only; no Eigen / OpenCV / torch types.  Every call
  * returns RSPL_OK (0) or a negative RSPL_E_* code (rspl_last_error() has the
  * text).  Handles are NOT thread-safe: callers serialise, exactly as the
@@ -366,6 +369,47 @@ int rspl_frame_create(const rspl_frame_config* cfg, rspl_frame** out);
 /* batch independent FrameOptimization calls; results[b] receives frame b */
 int rspl_frame_optimize(rspl_frame* h, const rspl_frame_problem* problems, int batch, rspl_frame_result* results);
 void rspl_frame_destroy(rspl_frame* h);
+
+/* ------------------------------------------------------------------------ */
+/* SolvePnPWithCV (src/g2o_optimization/g2o_optimization.cc:402-461; declared at */
+/* include/g2o_optimization/g2o_optimization.h:24, called per frame by          */
+/* MapBuilder::FramePoseOptimization, src/map_builder.cc:515): the RANSAC of    */
+/* cv::solvePnPRansac (5-point EPnP hypotheses, 100 iterations, 20 px, 0.99,    */
+/* SOLVEPNP_ITERATIVE refinement on the inliers), zero distortion               */
+/* (camera.cc:145-147).  The correspondences are the caller's already-filtered  */
+/* (map point, keypoint) pairs (:417-431); the caller maps inlier slots back to  */
+/* map-point ids (:452-457).  A batch of frames is one launch, one workgroup per */
+/* frame, the hypotheses of a frame solved side by side.                        */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  double fx, fy, cx, cy;        /* Camera::GetCamerMatrix */
+  int n;                        /* correspondences; < 8 -> 0 inliers (:433) */
+  const double* points;         /* [n][3] map points (world), rounded to float like cv::Point3f */
+  const double* keypoints;      /* [n][2] pixels, rounded to float like cv::Point2f */
+  int iterations;               /* 100 (:439); at most 128 */
+  double reprojection_error;    /* 20.0 px */
+  double confidence;            /* 0.99 */
+} rspl_pnp_problem;
+
+typedef struct {
+  double Rwc[9];                /* row-major Rwc = Rcw^T (:447-449); valid when n_inliers > 0 */
+  double twc[3];                /* -Rwc tcw */
+  uint8_t* inlier;              /* [n] inlier mask of the RANSAC model (may be NULL) */
+  int n_inliers;                /* SolvePnPWithCV's return value (cv_inliers.rows) */
+  int hypotheses;               /* RANSAC iterations evaluated (adaptive) */
+} rspl_pnp_result;
+
+typedef struct {
+  int max_batch;
+  int max_points;               /* correspondences over a whole batch */
+  int device;
+} rspl_pnp_config;
+
+typedef struct rspl_pnp rspl_pnp;
+
+int rspl_pnp_create(const rspl_pnp_config* cfg, rspl_pnp** out);
+int rspl_pnp_solve(rspl_pnp* h, const rspl_pnp_problem* problems, int batch, rspl_pnp_result* results);
+void rspl_pnp_destroy(rspl_pnp* h);
 
 #ifdef __cplusplus
 }

@@ -128,3 +128,31 @@ def frame_opt(problem):
         raise RuntimeError(f"orc_frame_opt rc={rc}")
     res.read_back(R)
     return res
+
+
+def pnp(K4, pts3, pts2, iterations=100, reproj_err=20.0, confidence=0.99):
+    """SolvePnPWithCV restatement (oracle/pnp.c): returns (n_inliers, Rwc [3,3], twc [3],
+    inlier mask [n] uint8, hypotheses evaluated)."""
+    L = lib()
+    f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+    u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
+    L.orc_pnp.argtypes = [f64p, C.c_int, f64p, f64p, C.c_int, C.c_double, C.c_double, f64p, f64p, u8p,
+                          C.POINTER(C.c_int)]
+    L.orc_pnp.restype = C.c_int
+    p3 = np.ascontiguousarray(pts3, np.float64).reshape(-1, 3)
+    p2 = np.ascontiguousarray(pts2, np.float64).reshape(-1, 2)
+    n = p3.shape[0]
+    R, t = np.zeros(9), np.zeros(3)
+    inl = np.zeros(max(n, 1), np.uint8)
+    used = C.c_int(0)
+    k = L.orc_pnp(np.ascontiguousarray(K4, np.float64), n, p3 if n else np.zeros(3), p2 if n else np.zeros(2),
+                  iterations, reproj_err, confidence, R, t, inl, C.byref(used))
+    return k, R.reshape(3, 3), t, inl[:n], used.value
+
+
+def pnp_subsets(count, iterations):
+    L = lib()
+    L.orc_pnp_subsets.argtypes = [C.c_int, C.c_int, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")]
+    out = np.zeros((iterations, 5), np.int32)
+    L.orc_pnp_subsets(count, iterations, out)
+    return out

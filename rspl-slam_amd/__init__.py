@@ -10,7 +10,7 @@ from . import capi, weights, synthetic, ba_types  # noqa: F401
 
 _API = ("SuperPoint", "SuperPointConfig", "SuperGlue", "SuperGlueConfig", "PointMatching",
         "LocalmapOptimization", "LocalBA", "FrameOptimization", "FrameBA",
-        "ShardGroup", "Comm", "comm_unique_id", "broadcast_comm_id")
+        "ShardGroup", "Comm", "comm_unique_id", "broadcast_comm_id", "PnP", "SolvePnPWithCV")
 
 
 def __getattr__(name):

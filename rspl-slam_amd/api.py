@@ -5,6 +5,7 @@
   PointMatching  include/point_matching.h:7-18    (MatchingPoints / NormalizeKeypoints)
   LocalmapOptimization  include/g2o_optimization/g2o_optimization.h:15-19
   FrameOptimization     include/g2o_optimization/g2o_optimization.h:20-22
+  SolvePnPWithCV        include/g2o_optimization/g2o_optimization.h:24
 
 Same names and argument meaning as the reference; C++ out-parameters become
 return values ((ok, features) for SuperPoint::infer, etc.).  Everything runs
@@ -374,3 +375,69 @@ def FrameOptimization(poses, points, camera_list, mono_point_constraints, stereo
 
 
 _default_frame_cap = (0, 0)
+
+
+# ---------------------------------------------------------------------------
+# SolvePnPWithCV (include/g2o_optimization/g2o_optimization.h:24, g2o_optimization.cc:402-461)
+# ---------------------------------------------------------------------------
+class PnP:
+    """Owns one rspl_pnp handle: cv::solvePnPRansac's RANSAC (5-point EPnP hypotheses side by
+    side) + refinement, for a batch of frames in one launch."""
+
+    def __init__(self, max_batch=64, max_points=65536, device=0):
+        self._lib = capi.load()
+        self._h = C.c_void_p()
+        cfg = capi.PnpConfig(max_batch, max_points, device)
+        capi.check(self._lib.rspl_pnp_create(C.byref(cfg), C.byref(self._h)), "rspl_pnp_create")
+
+    def solve(self, frames, iterations=100, reprojection_error=20.0, confidence=0.99):
+        """frames: list of (K4 = (fx, fy, cx, cy), points [n, 3], keypoints [n, 2]).
+        Returns a list of (n_inliers, Rwc [3, 3], twc [3], inlier mask [n] uint8, hypotheses)."""
+        keep, P, R = [], [], []
+        for K4, pts, kps in frames:
+            p3 = np.ascontiguousarray(pts, np.float64).reshape(-1, 3)
+            p2 = np.ascontiguousarray(kps, np.float64).reshape(-1, 2)
+            inl = np.zeros(max(p3.shape[0], 1), np.uint8)
+            keep.append((p3, p2, inl))
+            P.append(capi.PnpProblem(K4[0], K4[1], K4[2], K4[3], p3.shape[0],
+                                     p3.ctypes.data_as(C.POINTER(C.c_double)),
+                                     p2.ctypes.data_as(C.POINTER(C.c_double)), iterations, reprojection_error,
+                                     confidence))
+            r = capi.PnpResult()
+            r.inlier = inl.ctypes.data_as(C.POINTER(C.c_uint8))
+            R.append(r)
+        Pa = (capi.PnpProblem * len(P))(*P)
+        Ra = (capi.PnpResult * len(R))(*R)
+        capi.check(self._lib.rspl_pnp_solve(self._h, Pa, len(P), Ra), "rspl_pnp_solve")
+        return [(r.n_inliers, np.array(r.Rwc[:]).reshape(3, 3), np.array(r.twc[:]), k[2][:k[0].shape[0]].copy(),
+                 r.hypotheses) for r, k in zip(Ra, keep)]
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._lib.rspl_pnp_destroy(self._h)
+            self._h = C.c_void_p()
+
+
+_default_pnp = None
+
+
+def SolvePnPWithCV(K4, points, keypoints, point_ids=None):
+    """The reference's SolvePnPWithCV over already-filtered correspondences (:417-431): returns
+    (n_inliers, pose Twc 4x4, inliers) where inliers[i] = point_ids[i] for RANSAC inliers, else -1
+    (:452-457; point_ids defaults to the correspondence index)."""
+    global _default_pnp
+    n = len(points)
+    if _default_pnp is None or n > _default_pnp_cap[0]:
+        cap = max(n, 65536)
+        _default_pnp = PnP(max_batch=1, max_points=cap)
+        globals()["_default_pnp_cap"] = (cap,)
+    k, Rwc, twc, inl, _ = _default_pnp.solve([(K4, points, keypoints)])[0]
+    T = np.eye(4)
+    if k > 0:
+        T[:3, :3] = Rwc
+        T[:3, 3] = twc
+    ids = np.arange(n) if point_ids is None else np.asarray(point_ids)
+    return k, T, np.where(inl.astype(bool), ids, -1)
+
+
+_default_pnp_cap = (0,)

@@ -31,6 +31,7 @@ EXPORTS = [
     "rspl_frame_create", "rspl_frame_optimize", "rspl_frame_destroy",
     "rspl_ba_set_shard", "rspl_comm_unique_id", "rspl_comm_create", "rspl_comm_allreduce_sum", "rspl_comm_destroy",
     "rspl_ba_set_comm", "rspl_group_create", "rspl_group_destroy", "rspl_ba_set_group",
+    "rspl_pnp_create", "rspl_pnp_solve", "rspl_pnp_destroy",
 ]
 
 
@@ -57,6 +58,21 @@ class BaConfig(C.Structure):
 
 class FrameConfig(C.Structure):
     _fields_ = [("max_batch", C.c_int), ("max_edges", C.c_int), ("max_points", C.c_int), ("device", C.c_int)]
+
+
+class PnpConfig(C.Structure):
+    _fields_ = [("max_batch", C.c_int), ("max_points", C.c_int), ("device", C.c_int)]
+
+
+class PnpProblem(C.Structure):
+    _fields_ = [("fx", C.c_double), ("fy", C.c_double), ("cx", C.c_double), ("cy", C.c_double), ("n", C.c_int),
+                ("points", C.POINTER(C.c_double)), ("keypoints", C.POINTER(C.c_double)),
+                ("iterations", C.c_int), ("reprojection_error", C.c_double), ("confidence", C.c_double)]
+
+
+class PnpResult(C.Structure):
+    _fields_ = [("Rwc", C.c_double * 9), ("twc", C.c_double * 3), ("inlier", C.POINTER(C.c_uint8)),
+                ("n_inliers", C.c_int), ("hypotheses", C.c_int)]
 
 
 class RsplError(RuntimeError):
@@ -134,6 +150,11 @@ def load(path: pathlib.Path = LIB_PATH):
         lib.rspl_group_destroy.argtypes = [vp]
         lib.rspl_group_destroy.restype = None
         lib.rspl_ba_set_group.argtypes = [vp, vp, ip]
+    if hasattr(lib, "rspl_pnp_create"):
+        lib.rspl_pnp_create.argtypes = [C.POINTER(PnpConfig), C.POINTER(vp)]
+        lib.rspl_pnp_solve.argtypes = [vp, vp, ip, vp]
+        lib.rspl_pnp_destroy.argtypes = [vp]
+        lib.rspl_pnp_destroy.restype = None
     if hasattr(lib, "rspl_frame_create"):
         lib.rspl_frame_create.argtypes = [C.POINTER(FrameConfig), C.POINTER(vp)]
         lib.rspl_frame_optimize.argtypes = [vp, vp, ip, vp]

@@ -18,38 +18,17 @@
 
 #include "frame_kernels.hpp"
 #include "se3_device.hpp"
+#include "wave_reduce.hpp"
 
 namespace rspl {
 namespace frame {
 
 using ba::SE3;
-
-template <int CTRL>
-__device__ __forceinline__ double dppd(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffff), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ __forceinline__ double rdlaned(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffff), l);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-// wave64 all-reduce (sum), identical bits in every lane
-__device__ __forceinline__ double wsum(double v) {
-  v += dppd<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dppd<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dppd<0x141>(v);  // row_half_mirror
-  v += dppd<0x140>(v);  // row_mirror
-  return (rdlaned(v, 0) + rdlaned(v, 16)) + (rdlaned(v, 32) + rdlaned(v, 48));
-}
-__device__ __forceinline__ int wsum_int(int v) {
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-  return v;
-}
+using wave::kNV;
+using wave::rcp64;
+using wave::wave_allreduce28;
+using wave::wsum;
+using wave::wsum_int;
 
 __device__ __forceinline__ void huber(double e2, double delta, double& r0, double& r1) {
   const double dsqr = delta * delta;
@@ -134,37 +113,6 @@ __device__ __forceinline__ double active_chi2(const View& V, const Pose& P, int 
   return wsum(s);
 }
 
-constexpr int kNV = 28;  // 21 upper-triangular H entries, 6 b entries, chi2
-
-// All-reduce of the 28 system values across the wave as a reduce-scatter: 5 exchange steps
-// (xor 32, 16, 8, 4, 2) each halve the values a lane keeps (32 -> 1, padded), one xor-1 step
-// completes the sum, then every value is read back from its owner lane with readlane (wave-
-// uniform).  32 double exchanges instead of 28 x 6 for per-value butterflies; each value is
-// summed by one fixed tree (a + b == b + a in the pair), so the result is deterministic.
-__device__ __forceinline__ double shx(double v, int o) { return __shfl_xor(v, o); }
-__device__ __forceinline__ void wave_allreduce28(double (&acc)[kNV], int lane) {
-  double v[32];
-#pragma unroll
-  for (int k = 0; k < 32; k++) v[k] = k < kNV ? acc[k] : 0.0;
-#pragma unroll
-  for (int o = 32, h = 16; o >= 2; o >>= 1, h >>= 1) {
-    const bool up = lane & o;  // keep the upper half of the current h*2 values
-#pragma unroll
-    for (int k = 0; k < h; k++) {
-      const double keep = up ? v[h + k] : v[k];
-      const double send = up ? v[k] : v[h + k];
-      v[k] = keep + shx(send, o);
-    }
-  }
-  v[0] += shx(v[0], 1);
-  // lane L holds value index j(L): bit 5 of L -> bit 4 of j, bit 4 -> bit 3, ..., bit 1 -> bit 0
-#pragma unroll
-  for (int j = 0; j < kNV; j++) {
-    const int owner = ((j >> 4) & 1) << 5 | ((j >> 3) & 1) << 4 | ((j >> 2) & 1) << 3 | ((j >> 1) & 1) << 2 |
-                      (j & 1) << 1;
-    acc[j] = rdlaned(v[0], owner);
-  }
-}
 
 __device__ __forceinline__ int hidx(int i, int j) { return i * 6 - i * (i - 1) / 2 + (j - i); }
 
@@ -218,12 +166,6 @@ __device__ __forceinline__ void linearize(const View& V, const Pose& P, int lane
     }
   }
   wave_allreduce28(acc, lane);
-}
-
-__device__ __forceinline__ double rcp64(double d) {
-  double r = __builtin_amdgcn_rcp(d);
-  r = fma(r, fma(-d, r, 1.0), r);
-  return fma(r, fma(-d, r, 1.0), r);
 }
 
 // (H + lambda I) x = b by Cholesky, in registers (every lane the same); false if not SPD.

@@ -1,0 +1,37 @@
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace rspl {
+namespace pnp {
+
+constexpr int kThreads = 128;  // hypotheses per frame: RANSAC iterations <= 128
+
+struct Desc {      // one frame of the batch
+  int p0, n;       // correspondences [p0, p0 + n)
+  int s0, iters;   // subsets [s0, s0 + iters) of 5 indices
+  double K[4];     // fx fy cx cy
+  double thr2;     // reprojection_error^2
+  double confidence;
+};
+
+struct Out {       // per-frame result (host-mapped)
+  double Rwc[9];
+  double twc[3];
+  int n_inliers, hyps;
+};
+
+struct Args {
+  const Desc* frames;
+  const double* pts;      // [P][3], float-rounded like cv::Point3f
+  const double* kps;      // [P][2], float-rounded like cv::Point2f
+  const int32_t* subsets; // [S][5]
+  uint8_t* inl;           // [P] host-mapped
+  Out* out;               // [B] host-mapped
+};
+
+hipError_t solve(const Args& a, int batch, hipStream_t s);
+
+}  // namespace pnp
+}  // namespace rspl

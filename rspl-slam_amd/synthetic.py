@@ -249,3 +249,22 @@ def frame_problem(n_points: int = 300, pixel_sigma: float = 0.8, outlier_frac: f
                         mono=arr(mono, 2), stereo=arr(stereo, 3))
     return prob, dict(pose_q=R_to_quat_xyzw(Rwc), pose_p=twc, outlier_mono=np.array(mono["out"], bool),
                       outlier_stereo=np.array(stereo["out"], bool))
+
+
+def pnp_problem(n_points: int = 300, pixel_sigma: float = 0.8, outlier_frac: float = 0.2, seed: int = 0,
+                width: int = 752, height: int = 480, cam=(EUROC_FX, EUROC_FY, EUROC_CX, EUROC_CY)):
+    """Seeded SolvePnPWithCV input (g2o_optimization.cc:409-431): map points of the last frame
+    matched into the current one, ``outlier_frac`` of them mismatched.  Returns
+    (K4 = (fx, fy, cx, cy), points [n, 3], keypoints [n, 2], gt) with gt = dict(Rwc, twc, outlier)."""
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy = cam
+    Rwc = _rotvec_to_R(rng.normal(0, 0.2, 3))
+    twc = rng.normal(0, 1.0, 3)
+    u, v = rng.uniform(0, width, n_points), rng.uniform(0, height, n_points)
+    z = rng.uniform(1.5, 20.0, n_points)
+    Xc = np.stack([(u - cx) / fx * z, (v - cy) / fy * z, z], 1)
+    X = Xc @ Rwc.T + twc
+    kp = np.stack([u, v], 1) + rng.normal(0, pixel_sigma, (n_points, 2))
+    out = rng.uniform(size=n_points) < outlier_frac
+    kp[out] = np.stack([rng.uniform(0, width, out.sum()), rng.uniform(0, height, out.sum())], 1)
+    return np.array(cam, np.float64), X, kp, dict(Rwc=Rwc, twc=twc, outlier=out)

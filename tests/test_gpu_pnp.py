@@ -1,0 +1,62 @@
+"""GPU SolvePnPWithCV (rspl_pnp_solve) vs the fp64 CPU restatement (oracle/pnp.c) on the same
+inputs: identical RANSAC decisions (inlier counts, inlier masks, hypotheses evaluated) and the
+refined pose within 1e-9 (rotation) / 1e-8 m.  Parity at the OpenCV boundary is unpinned
+(OpenCV is not vendored in the reference)."""
+import numpy as np
+import pytest
+
+import oracle
+from rspl_slam_amd import synthetic as SY
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pnp():
+    import rspl_loader
+    return rspl_loader.load().PnP(max_batch=256, max_points=1 << 18)
+
+
+def _compare(g, ref):
+    n, R, t, inl, used = g
+    rn, rR, rt, rinl, rused = ref
+    assert (n, used) == (rn, rused)
+    np.testing.assert_array_equal(inl, rinl)
+    if n > 0:
+        assert np.abs(R - rR).max() < 1e-9
+        assert np.abs(t - rt).max() < 1e-8
+
+
+@pytest.mark.parametrize("seed,n,outl,sig", [(0, 300, 0.2, 0.8), (1, 200, 0.0, 0.0), (2, 300, 0.4, 0.8),
+                                             (3, 2048, 0.3, 1.0), (4, 8, 0.0, 0.5), (5, 60, 0.5, 0.8)])
+def test_pnp_matches_oracle(pnp, seed, n, outl, sig):
+    K, X, kp, gt = SY.pnp_problem(n_points=n, outlier_frac=outl, pixel_sigma=sig, seed=seed)
+    _compare(pnp.solve([(K, X, kp)])[0], oracle.pnp(K, X, kp))
+
+
+def test_pnp_batch_and_edge_cases(pnp):
+    frames = [SY.pnp_problem(n_points=n, outlier_frac=o, seed=100 + i)[:3]
+              for i, (n, o) in enumerate([(7, 0.0), (400, 0.1), (9, 0.0), (1000, 0.35), (0, 0.0), (150, 0.25)])]
+    res = pnp.solve(frames)
+    for (K, X, kp), g in zip(frames, res):
+        _compare(g, oracle.pnp(K, X, kp))
+    assert res[0][0] == 0 and res[4][0] == 0  # < 8 correspondences -> 0 (:433)
+
+
+def test_pnp_large_batch(pnp):
+    frames = [SY.pnp_problem(n_points=400, outlier_frac=0.25, seed=1000 + i)[:3] for i in range(128)]
+    res = pnp.solve(frames)
+    for i in range(0, 128, 17):
+        _compare(res[i], oracle.pnp(*frames[i]))
+
+
+def test_reference_signature():
+    import rspl_loader
+    pkg = rspl_loader.load()
+    K, X, kp, gt = SY.pnp_problem(n_points=120, outlier_frac=0.2, seed=9)
+    ids = np.arange(120) * 3 + 1000
+    n, T, inliers = pkg.SolvePnPWithCV(K, X, kp, ids)
+    rn, rR, rt, rinl, _ = oracle.pnp(K, X, kp)
+    assert n == rn
+    np.testing.assert_array_equal(inliers, np.where(rinl.astype(bool), ids, -1))
+    assert np.abs(T[:3, 3] - rt).max() < 1e-8

@@ -46,6 +46,23 @@ def main():
         oracle.frame_opt(probs[n % a.batch])
         n += 1
     out["cpu_oracle_1core_frames_per_s"] = round(n / (time.perf_counter() - t), 1)
+    # SolvePnPWithCV (the per-frame initial pose before FrameOptimization, map_builder.cc:515)
+    frames = [pkg.synthetic.pnp_problem(n_points=a.points, outlier_frac=0.2, seed=s)[:3] for s in range(128)]
+    pnp = pkg.PnP(max_batch=128, max_points=128 * a.points)
+    for b in (1, 128):
+        pnp.solve(frames[:b])
+        t = time.perf_counter()
+        for _ in range(a.iters):
+            pnp.solve(frames[:b])
+        dt = (time.perf_counter() - t) / a.iters
+        out[f"pnp_batch{b}_ms_per_call"] = round(dt * 1e3, 3)
+        out[f"pnp_batch{b}_frames_per_s"] = round(b / dt, 1)
+    t = time.perf_counter()
+    n = 0
+    while time.perf_counter() - t < 2.0:
+        oracle.pnp(*frames[n % 128])
+        n += 1
+    out["pnp_cpu_oracle_1core_frames_per_s"] = round(n / (time.perf_counter() - t), 1)
     print(json.dumps(out))
 
 
