@@ -34,6 +34,9 @@ struct rspl_ba {
   double *Tb, *Xb, *Lb;
   // per-edge linearisation records
   double *err, *rho0, *Hpp_e, *bp_e, *Hll_e, *bl_e, *Hpl_e;
+  // spare linearisation set (per-edge records + landmark blocks): each trial's candidate is
+  // linearised speculatively into it, and becomes current by a pointer swap when accepted
+  double *Hpp_s, *bp_s, *Hll_es, *bl_es, *Hpl_s, *Hll_s, *bl_s;
   uint8_t* lm_act2;
   // system
   double *Hll, *bl, *bp, *S, *x, *partial, *partial2;
@@ -125,6 +128,8 @@ void carve(F& ar, rspl_ba* b) {
   take(b->Tb, K * 8); take(b->Xb, nq * 3); take(b->Lb, nl * 6);
   take(b->err, E * 4); take(b->rho0, E); take(b->Hpp_e, E * 36); take(b->bp_e, E * 6); take(b->Hll_e, E * 16);
   take(b->bl_e, E * 4); take(b->Hpl_e, E * 24);
+  take(b->Hpp_s, E * 36); take(b->bp_s, E * 6); take(b->Hll_es, E * 16); take(b->bl_es, E * 4); take(b->Hpl_s, E * 24);
+  take(b->Hll_s, NL * 16); take(b->bl_s, NL * 4);
   take(b->lm_act2, NL);
   take(b->Hll, NL * 16); take(b->bl, NL * 4); take(b->bp, K * 6);
   // block partials: edge-per-thread kernels (E / 256) and landmark-group kernels (NL * 8 / 256)
@@ -218,7 +223,7 @@ Se3h inverse(const Se3h& T) {  // SE3Quat::inverse
 }
 
 // one g2o SparseOptimizer::optimize(iters) with OptimizationAlgorithmLevenberg
-int optimize(rspl_ba* b, ba::Problem& P, const ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
+int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
              double* chi2_out, int* done_out) {
   hipStream_t st = b->stream;
   double v[4];
@@ -248,7 +253,8 @@ int optimize(rspl_ba* b, ba::Problem& P, const ba::Lin& Lr, ba::Sys& S, const ba
   double lambda = 1e-5 * v[2], ni = 2;  // computeLambdaInit: tau * max diagonal
   int done = 0;
   for (int it = 0; it < iters; it++) {
-    if (it > 0) RSPL_HIP(ba::linearize(P, Lr, A, S, false, st));
+    // iterations after the first start from an accepted candidate, whose linearisation the
+    // speculative pass of that trial already produced (now current after the swap)
     double rho = 0;
     int qmax = 0;
     do {
@@ -262,6 +268,16 @@ int optimize(rspl_ba* b, ba::Problem& P, const ba::Lin& Lr, ba::Sys& S, const ba
       } else {
         RSPL_HIP(ba::trial(P, Lr, A, S, lambda, q, st));
       }
+      // speculative linearisation of the candidate into the spare set, queued behind the trial:
+      // the GPU runs it while the host reads the mailbox, so the next iteration's first kernel is
+      // already queued when the host decides (a rejected trial wastes it; the current set stays)
+      ba::Problem Pc = P;
+      Pc.T = P.Tn; Pc.X = P.Xn; Pc.L = P.Ln;
+      ba::Lin Ls = Lr;
+      Ls.Hpp = b->Hpp_s; Ls.bp = b->bp_s; Ls.Hll = b->Hll_es; Ls.bl = b->bl_es; Ls.Hpl = b->Hpl_s;
+      ba::Sys Ss = S;
+      Ss.Hll = b->Hll_s; Ss.bl = b->bl_s;
+      if (it + 1 < iters) RSPL_HIP(ba::linearize(Pc, Ls, A, Ss, false, st));
       if ((rc = wait_mail(b, q, v))) return rc;
       const bool ok = v[3] == 0.0;
       const double tempChi = ok ? v[0] : std::numeric_limits<double>::max();
@@ -277,6 +293,13 @@ int optimize(rspl_ba* b, ba::Problem& P, const ba::Lin& Lr, ba::Sys& S, const ba
         std::swap(P.T, P.Tn);  // accept: the candidate becomes the current state
         std::swap(P.X, P.Xn);
         std::swap(P.L, P.Ln);
+        if (it + 1 < iters) {  // ... and its speculative linearisation the current one
+          std::swap(b->Hpp_e, b->Hpp_s); std::swap(b->bp_e, b->bp_s); std::swap(b->Hll_e, b->Hll_es);
+          std::swap(b->bl_e, b->bl_es); std::swap(b->Hpl_e, b->Hpl_s);
+          std::swap(b->Hll, b->Hll_s); std::swap(b->bl, b->bl_s);
+          Lr.Hpp = b->Hpp_e; Lr.bp = b->bp_e; Lr.Hll = b->Hll_e; Lr.bl = b->bl_e; Lr.Hpl = b->Hpl_e;
+          S.Hll = b->Hll; S.bl = b->bl;
+        }
       } else {
         lambda *= ni;  // reject: the current state was never modified (no restore needed)
         ni *= 2;

@@ -137,6 +137,27 @@ __device__ __forceinline__ void huber(double e2, double delta, double& r0, doubl
 // order, posts {chi2, scale, maxdiag, fail} + seq to the host-mapped mailbox and
 // re-arms the device state (counter, fail flag, maxdiag) for the next trial.
 // ---------------------------------------------------------------------------
+// Mailbox post into fine-grained (uncached) host memory: the four values, then -- once they
+// have completed (vmcnt) -- the sequence number the host spins on.  No release fence: a
+// system/agent-scope release writes back the whole L2 (~3.5 us, MI355X_MICROARCH.md), once per
+// LM trial on the critical path; the host reads only these uncached words.
+__device__ __forceinline__ void post_mail(Mail* m, double v0, double v1, double v2, double v3, unsigned long long seq) {
+  __hip_atomic_store(&m->v[0], v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&m->v[1], v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&m->v[2], v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __hip_atomic_store(&m->v[3], v3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __hip_atomic_store(&m->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Last-block ticket: this block's partials were stored device-coherent (relaxed agent-scope
+// atomics, written through), so completing them (vmcnt) before a relaxed ticket increment is
+// enough -- an acq_rel ticket would write back and invalidate the L2 in every block.
+__device__ __forceinline__ unsigned ticket(unsigned* counter) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  return __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 __device__ __forceinline__ double block_sum256(double v, double* red) {
   red[threadIdx.x] = v;
   __syncthreads();
@@ -176,7 +197,7 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
   const double bsum = block_sum256(c, red);
   if (threadIdx.x == 0) {
     __hip_atomic_store(S.partial + blockIdx.x, bsum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned tk = __hip_atomic_fetch_add(S.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned tk = ticket(S.counter);
     last = tk == gridDim.x - 1;
   }
   __syncthreads();
@@ -202,15 +223,10 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
       S.out[2] = 0.0;
       return;
     }
-    Mail* m = S.mail;
-    m->v[0] = chi2;
-    m->v[1] = scale;
-    m->v[2] = mx;
-    m->v[3] = f;
     __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(S.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     S.out[2] = 0.0;
-    __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    post_mail(S.mail, chi2, scale, mx, f, seq);
   }
 }
 
@@ -242,12 +258,8 @@ __global__ __launch_bounds__(256) void post_kernel(Sys S, int K, int npd, unsign
     }
   }
   if (threadIdx.x != 0) return;
-  Mail* m = S.mail;
-  m->v[0] = S.out[0];
-  m->v[1] = S.out[1];
-  m->v[2] = S.out[2];
-  m->v[3] = (double)__hip_atomic_load(S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  post_mail(S.mail, S.out[0], S.out[1], S.out[2],
+            (double)__hip_atomic_load(S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), seq);
 }
 
 // ---------------------------------------------------------------------------
@@ -1314,7 +1326,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
   if (threadIdx.x == 0) {
     __hip_atomic_store(S.partial + blockIdx.x, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(S.partial2 + blockIdx.x, red[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const unsigned tk = __hip_atomic_fetch_add(S.counter, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned tk = ticket(S.counter);
     last = tk == gridDim.x - 1;
   }
   __syncthreads();
@@ -1341,15 +1353,10 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
       S.out[2] = 0.0;
       return;
     }
-    Mail* m = S.mail;
-    m->v[0] = chi2;
-    m->v[1] = scale;
-    m->v[2] = mx;
-    m->v[3] = f;
     __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(S.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     S.out[2] = 0.0;
-    __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    post_mail(S.mail, chi2, scale, mx, f, seq);
   }
 }
 
@@ -1466,12 +1473,7 @@ __global__ void shard_post_kernel(Sys S, const double* red, int n6, int nranks, 
   S.out[0] = chi2;
   S.out[1] = scale;
   S.out[3] = f;
-  Mail* m = S.mail;
-  m->v[0] = chi2;
-  m->v[1] = scale;
-  m->v[2] = mode == 0 ? mx : S.out[2];
-  m->v[3] = f;
-  __hip_atomic_store(&m->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  post_mail(S.mail, chi2, scale, mode == 0 ? mx : S.out[2], f, seq);
 }
 
 // G = [X (owned points) | L (owned lines) | inlier flag at the global edge id of each local edge]

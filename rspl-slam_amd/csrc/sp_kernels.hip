@@ -230,22 +230,42 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
 
   for (int c0 = 0; c0 < CIN; c0 += HCK) {
     __syncthreads();
-    if constexpr (FUSE1A) {  // conv1a (fp32, as the module's first layer) -> ReLU -> fp16
-      for (int i = tid; i < HY * HX * HCK; i += 256) {
-        const int c = i % HCK, pix = i / HCK;
+    if constexpr (FUSE1A) {
+      // conv1a -> ReLU -> fp16 halo, itself on MFMA: D[pix][c] = A[pix][k] B[k][c] with
+      // k = the 9 taps of the image patch, k = 9 the bias (A = 1), k > 9 zero -- one
+      // v_mfma_f32_32x32x16_f16 per 32 halo pixels x 32 channels (11 per stage) instead of
+      // 9 scalar FMAs and 19 LDS reads per halo value
+      constexpr int NPIX = HY * HX, NMT = (NPIX + 31) / 32;
+      half8 bw;
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int k = 8 * kl + j;
+        bw[j] = (_Float16)(k <= 9 ? w1a[(c0 + ml) * 10 + k] : 0.f);
+      }
+      for (int mt = wv; mt < NMT; mt += 4) {
+        const int pix = mt * 32 + ml;
         const int hy = pix / HX, hx = pix % HX;
-        const int y = y0 - 1 + hy, x = x0 - 1 + hx;
-        float v = 0.f;
-        if (y >= 0 && y < H && x >= 0 && x < W) {
-          const float* wc = &w1a[(c0 + c) * 10];
-          float s = wc[9];
+        half8 av;
 #pragma unroll
-          for (int ky = 0; ky < 3; ky++)
-#pragma unroll
-            for (int kx = 0; kx < 3; kx++) s += wc[ky * 3 + kx] * patch[(hy + ky) * (TW + 4) + hx + kx];
-          v = s > 0.f ? s : 0.f;
+        for (int j = 0; j < 8; j++) {
+          const int k = 8 * kl + j;
+          float v = 0.f;
+          if (pix < NPIX) v = k < 9 ? patch[(hy + k / 3) * (TW + 4) + hx + k % 3] : (k == 9 ? 1.f : 0.f);
+          av[j] = (_Float16)v;
         }
-        halo[pix * HCS + c] = (_Float16)v;
+        floatx16 d;
+#pragma unroll
+        for (int r = 0; r < 16; r++) d[r] = 0.f;
+        d = mfma16(av, bw, d);
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int pp = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
+          if (pp < NPIX) {
+            const int y = y0 - 1 + pp / HX, x = x0 - 1 + pp % HX;
+            const float v = (y >= 0 && y < H && x >= 0 && x < W) ? fmaxf(d[r], 0.f) : 0.f;
+            halo[pp * HCS + ml] = (_Float16)v;
+          }
+        }
       }
     } else {
       const _Float16* in = a.hin + (size_t)bi * H * W * CIN;
