@@ -125,6 +125,10 @@ def main():
     ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp16",
                     help="SP/SG MFMA precision: fp16 = the reference's own TensorRT kFP16 engines "
                          "(src/super_point.cpp:98, src/super_glue.cpp:132; default), fp32 = the parity path")
+    ap.add_argument("--reserve-cus", type=int, default=int(os.environ.get("RSPL_RESERVE_CUS", "0")),
+                    help="CUs the SuperPoint/SuperGlue streams leave free for the BA chain (CU-masked streams)")
+    ap.add_argument("--ba-own-cus", type=int, default=int(os.environ.get("RSPL_BA_OWN_CUS", "1")),
+                    help="1: the BA runs only on the reserved CUs (disjoint from SP/SG)")
     ap.add_argument("--single-precision", action="store_true",
                     help="skip the second (other-precision) measurement")
     args = ap.parse_args()
@@ -153,6 +157,8 @@ def main():
         assert sg_h.build(), sg_h.error
         handles[pr] = (sp_h, sg_h)
     ba = pkg.LocalBA(max_poses=16, max_points=6000, max_lines=200, max_edges=40000, device=local)
+    if args.ba_own_cus and args.reserve_cus > 0:
+        ba.use_reserved_cus(args.reserve_cus)
     syn = pkg.synthetic
     NP = 4
     pool = capi.DeviceBuffer(NP * 2 * H * W)
@@ -172,9 +178,14 @@ def main():
     f0, f1 = capi.DeviceBuffer(2 * FB), capi.DeviceBuffer(2 * FB)
     n0, n1 = capi.DeviceBuffer(8), capi.DeviceBuffer(8)
     outs = [capi.DeviceBuffer(2 * K * sz) for sz in (4, 4, 8, 8)]
-    # SG is the frame's critical chain (SP has slack): SG and the BA run at high priority
-    st_sp, st_sg = capi.Stream(), capi.Stream(high_priority=True)
-    st_post = capi.Stream(high_priority=True)  # SG's Sinkhorn + decode: overlaps the next frame's GNN
+    # SG is the frame's critical chain (SP has slack): SG and the BA run at high priority.  With
+    # --reserve-cus the SP / SG / post streams are CU-masked off a few CUs spread over the chip
+    # (and, with --ba-own-cus, the BA confined to them).  Measured: no gain -- the BA's slowdown
+    # under load (1.62 -> 1.90 ms of GPU work) is memory-latency contention, not CU slots -- so the
+    # default is 0 (unmasked)
+    rc = args.reserve_cus
+    st_sp, st_sg = capi.Stream(reserve_cus=rc), capi.Stream(high_priority=True, reserve_cus=rc)
+    st_post = capi.Stream(high_priority=True, reserve_cus=rc)  # SG's Sinkhorn + decode: overlaps the next GNN
     ev_sp = [capi.Event() for _ in range(3)]
     ev_sg = [capi.Event() for _ in range(3)]
 

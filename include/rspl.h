@@ -62,6 +62,10 @@ int rspl_memcpy_d2d(void* dst, const void* src, size_t bytes, void* stream);
 int rspl_stream_create(void** stream);
 /* high != 0: the device's highest stream priority (latency-critical chains) */
 int rspl_stream_create_priority(void** stream, int high);
+/* A stream whose kernels stay off reserve_cus CUs spread over the chip (HIP CU mask): the
+ * throughput streams (SuperPoint / SuperGlue) leave those CUs free, so the latency-bound BA
+ * chain never waits behind them for a CU slot. */
+int rspl_stream_create_reserving(void** stream, int reserve_cus);
 int rspl_stream_destroy(void* stream);
 int rspl_stream_synchronize(void* stream);
 int rspl_device_synchronize(void);
@@ -275,6 +279,9 @@ typedef struct rspl_ba rspl_ba;
 int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out);
 int rspl_ba_local(rspl_ba* ba, const rspl_ba_problem* problem, rspl_ba_result* result);
 void rspl_ba_destroy(rspl_ba* ba);
+/* Run this handle's kernels only on the reserve_cus CUs that rspl_stream_create_reserving
+ * streams leave free (0 = all CUs, highest stream priority: the default). */
+int rspl_ba_use_reserved_cus(rspl_ba* ba, int reserve_cus);
 
 /* ------------------------------------------------------------------------ */
 /* Landmark-sharded local BA: nranks handles -- one per  */

@@ -228,6 +228,10 @@ class LocalBA:
         res.read_back(R)
         return res
 
+    def use_reserved_cus(self, reserve_cus: int):
+        """Confine this handle's kernels to the CUs reserving streams leave free (0 = all CUs)."""
+        capi.check(self._lib.rspl_ba_use_reserved_cus(self._h, reserve_cus), "rspl_ba_use_reserved_cus")
+
     def set_group(self, group: "ShardGroup", rank: int):
         """Landmark-sharded solve: this handle is rank `rank` of an in-process group (one device)."""
         capi.check(self._lib.rspl_ba_set_group(self._h, group.handle, rank), "rspl_ba_set_group")

@@ -18,7 +18,7 @@ RSPL_PREC_FP16 = 1
 EXPORTS = [
     "rspl_last_error", "rspl_version",
     "rspl_device_count", "rspl_set_device", "rspl_malloc", "rspl_free", "rspl_memcpy_h2d", "rspl_memcpy_d2h",
-    "rspl_memset", "rspl_memcpy_d2d", "rspl_stream_create", "rspl_stream_create_priority", "rspl_stream_destroy", "rspl_stream_synchronize",
+    "rspl_memset", "rspl_memcpy_d2d", "rspl_stream_create", "rspl_stream_create_priority", "rspl_stream_create_reserving", "rspl_stream_destroy", "rspl_stream_synchronize",
     "rspl_device_synchronize", "rspl_event_create", "rspl_event_record", "rspl_stream_wait_event",
     "rspl_event_destroy", "rspl_timer_create", "rspl_timer_record", "rspl_timer_elapsed_ms",
     "rspl_timer_destroy",
@@ -27,7 +27,7 @@ EXPORTS = [
     "rspl_sg_create", "rspl_sg_infer", "rspl_sg_infer_device", "rspl_sg_infer_device2", "rspl_sg_debug_scores", "rspl_sg_profile",
     "rspl_sg_stage_times", "rspl_sg_destroy",
     "rspl_pm_match",
-    "rspl_ba_create", "rspl_ba_local", "rspl_ba_destroy",
+    "rspl_ba_create", "rspl_ba_local", "rspl_ba_destroy", "rspl_ba_use_reserved_cus",
     "rspl_frame_create", "rspl_frame_optimize", "rspl_frame_destroy",
     "rspl_ba_set_shard", "rspl_comm_unique_id", "rspl_comm_create", "rspl_comm_allreduce_sum", "rspl_comm_destroy",
     "rspl_ba_set_comm", "rspl_group_create", "rspl_group_destroy", "rspl_ba_set_group",
@@ -111,6 +111,7 @@ def load(path: pathlib.Path = LIB_PATH):
     lib.rspl_sp_stage_times.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(ip)]
     lib.rspl_stream_create.argtypes = [C.POINTER(vp)]
     lib.rspl_stream_create_priority.argtypes = [C.POINTER(vp), ip]
+    lib.rspl_stream_create_reserving.argtypes = [C.POINTER(vp), ip]
     lib.rspl_stream_destroy.argtypes = [vp]
     lib.rspl_stream_synchronize.argtypes = [vp]
     lib.rspl_event_create.argtypes = [C.POINTER(vp)]
@@ -136,6 +137,7 @@ def load(path: pathlib.Path = LIB_PATH):
     if hasattr(lib, "rspl_ba_create"):
         lib.rspl_ba_create.argtypes = [C.POINTER(BaConfig), C.POINTER(vp)]
         lib.rspl_ba_local.argtypes = [vp, vp, vp]
+        lib.rspl_ba_use_reserved_cus.argtypes = [vp, ip]
         lib.rspl_ba_destroy.argtypes = [vp]
         lib.rspl_ba_destroy.restype = None
     if hasattr(lib, "rspl_ba_set_shard"):
@@ -244,9 +246,11 @@ class Event:
 
 
 class Stream:
-    def __init__(self, high_priority: bool = False):
+    def __init__(self, high_priority: bool = False, reserve_cus: int = 0):
         self._s = C.c_void_p()
-        if high_priority:
+        if reserve_cus > 0:  # CU-masked: leaves reserve_cus CUs to other (latency-bound) streams
+            check(load().rspl_stream_create_reserving(C.byref(self._s), reserve_cus), "rspl_stream_create_reserving")
+        elif high_priority:
             check(load().rspl_stream_create_priority(C.byref(self._s), 1), "rspl_stream_create_priority")
         else:
             check(load().rspl_stream_create(C.byref(self._s)), "rspl_stream_create")

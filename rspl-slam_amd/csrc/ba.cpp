@@ -356,6 +356,25 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
   return RSPL_OK;
 }
 
+extern "C" int rspl_ba_use_reserved_cus(rspl_ba* b, int reserve_cus) {
+  RSPL_CHECK_ARG(b, "rspl_ba_use_reserved_cus: NULL handle");
+  hipStream_t ns = nullptr;
+  if (reserve_cus > 0) {
+    std::vector<uint32_t> mask;
+    int rc = cu_mask(reserve_cus, true, mask);
+    if (rc) return rc;
+    RSPL_HIP(hipExtStreamCreateWithCUMask(&ns, (uint32_t)mask.size(), mask.data()));
+  } else {
+    int lo = 0, hi = 0;
+    RSPL_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    RSPL_HIP(hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, hi));
+  }
+  RSPL_HIP(hipStreamSynchronize(b->stream));
+  RSPL_HIP(hipStreamDestroy(b->stream));
+  b->stream = ns;
+  return RSPL_OK;
+}
+
 extern "C" int rspl_ba_set_shard(rspl_ba* b, int rank, int nranks, rspl_allreduce_fn fn, void* ctx) {
   RSPL_CHECK_ARG(b, "rspl_ba_set_shard: NULL handle");
   RSPL_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks && rank >= 0 && rank < nranks, "rank %d of %d (1..%d ranks)", rank,

@@ -16,6 +16,8 @@
 namespace rspl {
 
 void set_error(const char* fmt, ...);
+// CU mask of the reserved CUs (every ncu/reserve_cus-th CU) or of all the others
+int cu_mask(int reserve_cus, bool reserved_only, std::vector<uint32_t>& mask);
 
 #define RSPL_HIP(expr)                                                                   \
   do {                                                                                   \

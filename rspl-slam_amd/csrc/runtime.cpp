@@ -1,5 +1,7 @@
 // Runtime helpers of the C ABI (include/rspl.h): device memory, streams,
 // HIP-event timers -- all on the system ROCm runtime librspl links against.
+#include <vector>
+
 #include "common.hpp"
 
 using namespace rspl;
@@ -7,6 +9,26 @@ using namespace rspl;
 struct rspl_timer {
   hipEvent_t ev[2] = {nullptr, nullptr};
 };
+
+namespace rspl {
+// CU mask over the device's CUs: every (ncu / reserve)-th CU is "reserved"; the mask enables
+// either everything but the reserved CUs, or only them
+int cu_mask(int reserve_cus, bool reserved_only, std::vector<uint32_t>& mask) {
+  int dev = 0, ncu = 0;
+  RSPL_HIP(hipGetDevice(&dev));
+  RSPL_HIP(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
+  RSPL_CHECK_ARG(reserve_cus > 0 && reserve_cus < ncu, "cannot reserve %d of %d CUs", reserve_cus, ncu);
+  mask.assign((ncu + 31) / 32, 0u);
+  const int step = ncu / reserve_cus;
+  int left = reserve_cus;
+  for (int c = 0; c < ncu; c++) {
+    const bool reserved = left > 0 && c % step == step - 1;
+    if (reserved) left--;
+    if (reserved == reserved_only) mask[c / 32] |= 1u << (c % 32);
+  }
+  return RSPL_OK;
+}
+}  // namespace rspl
 
 extern "C" {
 
@@ -59,6 +81,19 @@ int rspl_stream_create_priority(void** stream, int high) {
   int lo = 0, hi = 0;
   RSPL_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
   RSPL_HIP(hipStreamCreateWithPriority((hipStream_t*)stream, hipStreamNonBlocking, high ? hi : lo));
+  return RSPL_OK;
+}
+
+int rspl_stream_create_reserving(void** stream, int reserve_cus) {
+  RSPL_CHECK_ARG(stream && reserve_cus >= 0, "rspl_stream_create_reserving: bad arguments");
+  if (reserve_cus == 0) {
+    RSPL_HIP(hipStreamCreateWithFlags((hipStream_t*)stream, hipStreamNonBlocking));
+    return RSPL_OK;
+  }
+  std::vector<uint32_t> mask;
+  int rc = rspl::cu_mask(reserve_cus, false, mask);
+  if (rc) return rc;
+  RSPL_HIP(hipExtStreamCreateWithCUMask((hipStream_t*)stream, (uint32_t)mask.size(), mask.data()));
   return RSPL_OK;
 }
 int rspl_stream_destroy(void* stream) {
