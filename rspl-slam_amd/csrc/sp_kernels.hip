@@ -10,6 +10,8 @@
 // on v_mfma_f32_32x32x2_f32 (exact fp32: one rounding per product, like fmaf).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include <cstdint>
 
 #include "sp_kernels.hpp"
@@ -235,35 +237,36 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
       // k = the 9 taps of the image patch, k = 9 the bias (A = 1), k > 9 zero -- one
       // v_mfma_f32_32x32x16_f16 per 32 halo pixels x 32 channels (11 per stage) instead of
       // 9 scalar FMAs and 19 LDS reads per halo value
-      constexpr int NPIX = HY * HX, NMT = (NPIX + 31) / 32;
+      // one M-tile per halo row (32 columns, HX of them real): every output's halo position
+      // is a compile-time function of the accumulator register, no per-element division
       half8 bw;
 #pragma unroll
       for (int j = 0; j < 8; j++) {
         const int k = 8 * kl + j;
         bw[j] = (_Float16)(k <= 9 ? w1a[(c0 + ml) * 10 + k] : 0.f);
       }
-      for (int mt = wv; mt < NMT; mt += 4) {
-        const int pix = mt * 32 + ml;
-        const int hy = pix / HX, hx = pix % HX;
+      for (int hy = wv; hy < HY; hy += 4) {
+        const int y = y0 - 1 + hy;
         half8 av;
 #pragma unroll
         for (int j = 0; j < 8; j++) {
           const int k = 8 * kl + j;
           float v = 0.f;
-          if (pix < NPIX) v = k < 9 ? patch[(hy + k / 3) * (TW + 4) + hx + k % 3] : (k == 9 ? 1.f : 0.f);
+          if (ml < HX) v = k < 9 ? patch[(hy + k / 3) * (TW + 4) + ml + k % 3] : (k == 9 ? 1.f : 0.f);
           av[j] = (_Float16)v;
         }
         floatx16 d;
 #pragma unroll
         for (int r = 0; r < 16; r++) d[r] = 0.f;
         d = mfma16(av, bw, d);
+        const bool yin = y >= 0 && y < H;
 #pragma unroll
         for (int r = 0; r < 16; r++) {
-          const int pp = mt * 32 + (r & 3) + 8 * (r >> 2) + 4 * kl;
-          if (pp < NPIX) {
-            const int y = y0 - 1 + pp / HX, x = x0 - 1 + pp % HX;
-            const float v = (y >= 0 && y < H && x >= 0 && x < W) ? fmaxf(d[r], 0.f) : 0.f;
-            halo[pp * HCS + ml] = (_Float16)v;
+          const int hx = (r & 3) + 8 * (r >> 2) + 4 * kl;  // halo column of accumulator row r
+          if (hx < HX) {
+            const int x = x0 - 1 + hx;
+            const float v = (yin && x >= 0 && x < W) ? fmaxf(d[r], 0.f) : 0.f;
+            halo[(hy * HX + hx) * HCS + ml] = (_Float16)v;
           }
         }
       }
