@@ -129,6 +129,7 @@ def main():
                     help="CUs the SuperPoint/SuperGlue streams leave free for the BA chain (CU-masked streams)")
     ap.add_argument("--ba-own-cus", type=int, default=int(os.environ.get("RSPL_BA_OWN_CUS", "1")),
                     help="1: the BA runs only on the reserved CUs (disjoint from SP/SG)")
+    ap.add_argument("--skip", default="", help="diagnostics only: comma list of stages to leave out (sp,sg,ba)")
     ap.add_argument("--single-precision", action="store_true",
                     help="skip the second (other-precision) measurement")
     args = ap.parse_args()
@@ -222,6 +223,17 @@ def main():
         def step(i):
             slot, pslot = i % 3, (i - 1) % 3
             cur, prev, ccur, cprev = feats[slot], feats[pslot], counts[slot], counts[pslot]
+            skip = args.skip.split(",")
+            if "sp" in skip or "sg" in skip:  # diagnostics: stages left out (not a benchmark line)
+                if "sp" not in skip:
+                    sp.infer_device(pool.offset((i % NP) * 2 * H * W), 2, H, W, W, H * W, cur.ptr, K, ccur.ptr,
+                                    st_sp.handle)
+                if "sg" not in skip:
+                    sg.infer_device(2, f0.ptr, n0.ptr, f1.ptr, n1.ptr, K, True, outs[0].ptr, outs[1].ptr,
+                                    outs[2].ptr, outs[3].ptr, st_sg.handle, post_stream=st_post.handle)
+                if "ba" not in skip:
+                    ba_q.put(problems[i % len(problems)])
+                return
             if i >= 2:
                 ev_sg[(i - 2) % 3].wait_on(st_sp.handle)
             sp.infer_device(pool.offset((i % NP) * 2 * H * W), 2, H, W, W, H * W, cur.ptr, K, ccur.ptr, st_sp.handle)
