@@ -45,6 +45,7 @@ capi = pkg.capi
 H, W, K = 480, 752, 400
 FP32_MFMA_PEAK = 157.3  # TFLOP/s, MI355X_MICROARCH.md (v_mfma_f32_32x32x2_f32, dense)
 FP16_MFMA_PEAK = 2516.8  # TFLOP/s dense (~2.5 PF, = 16 x the f32 MFMA rate), MI355X_MICROARCH.md
+HBM_PEAK_GBS = 8000.0  # HBM3E, MI355X_MICROARCH.md
 CONV1_GFLOP_PER_IMAGE = 2 * H * W * 64 * 9 / 1e9 + 2 * H * W * 64 * 576 / 1e9  # conv1a + conv1b
 
 
@@ -92,6 +93,30 @@ def pmc_traffic(kernel_substr):
             if kernel_substr in name:
                 return v["traffic_bytes"], f.name
     return None, None
+
+
+def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
+    """Achieved rate vs the bounding peak for the other big stages (HIP-event stage times, per
+    step: 2 SuperPoint images, 2 SuperGlue pairs of N = M = 400).  Algorithmic work as SURVEY.md
+    8(d): GNN 2*(655,360 N + 512 N M) per image per layer; Sinkhorn streamed model
+    2*iters*4*(N+1)(M+1) bytes per pair; NMS 2*4*H*W bytes per image."""
+    t = {**{f"sp:{n}": v / max(1, sp_calls) for n, v in zip(sp.STAGES, sp_ms)},
+         **{f"sg:{n}": v / max(1, sg_calls) for n, v in zip(sg.STAGES, sg_ms)}}
+    N = M = K
+    mfma_peak = FP16_MFMA_PEAK if precision == "fp16" else FP32_MFMA_PEAK
+    gnn_gflop = 2 * 2 * 18 * 2 * (655360 * N + 512 * N * M) / 1e9
+    sink_gb = 2 * 2 * 100 * 4 * (N + 1) * (M + 1) / 1e9
+    nms_gb = 2 * 2 * 4 * H * W / 1e9
+    out = {}
+    for key, work, unit, peak, bound in (("sg:gnn x18", gnn_gflop, "TFLOP/s", mfma_peak, "mfma"),
+                                         ("sg:sinkhorn", sink_gb, "GB/s", HBM_PEAK_GBS, "hbm (latency)"),
+                                         ("sp:nms", nms_gb, "GB/s", HBM_PEAK_GBS, "hbm (latency)")):
+        ms = t.get(key)
+        if ms:
+            ach = work / ms if unit == "TFLOP/s" else work / ms * 1e3
+            out[key] = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
+                        "frac": round(ach / peak, 4), "ms": round(ms, 4)}
+    return out
 
 
 def replica_seeds(rank):
@@ -327,6 +352,7 @@ def main():
                      if traffic else None,
                      "algorithmic": f"{2 * CONV1_GFLOP_PER_IMAGE:.3f} GFLOP per launch (2 images)",
                      "avg_launch_ms": round(conv1_ms, 4)},
+        "stages_roofline": stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, args.precision),
         "stages_ms_per_step": {**{f"sp:{n}": round(v / max(1, sp_calls), 4) for n, v in zip(sp.STAGES, sp_ms)},
                                **{f"sg:{n}": round(v / max(1, sg_calls), 4) for n, v in zip(sg.STAGES, sg_ms)},
                                "ba:wall": round(float(np.mean(ba_ms)), 4) if ba_ms else None},
