@@ -41,6 +41,8 @@ struct rspl_ba {
   // system
   double *Hll, *bl, *bp, *S, *x, *partial, *partial2;
   unsigned* lm_ctr;  // [max_lines] line-landmark tickets (zeroed at create, re-armed by the kernel)
+  unsigned* lflag;   // [max_lines] release flags of the fused speculative linearisation (zeroed at create)
+  unsigned tag = 0;  // last flag value used
   // landmark CSR (filled on the device) and the Schur chunk / pose-pair sums
   int *lm_edges, *lm_pose;
   double *chunk, *pairfin;
@@ -138,6 +140,7 @@ void carve(F& ar, rspl_ba* b) {
   // partial2: scale partials, and the pose-diagonal partials (K x E/256 x 6) of the lambda init
   take(b->partial2, std::max(std::max((size_t)b->maxV / 256, nblk) + 2, K * (E / 256 + 1) * 6));
   take(b->lm_ctr, nl);
+  take(b->lflag, nl);
   const size_t npairs = K * (K + 1) / 2, nchk = std::max<size_t>((NL + ba::kLmChunk - 1) / ba::kLmChunk, 1);
   take(b->lm_edges, E); take(b->lm_pose, E);
   take(b->chunk, npairs * nchk * 48); take(b->pairfin, npairs * 48 + 8); take(b->pair_ctr, npairs);
@@ -265,19 +268,26 @@ int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Acti
         RSPL_HIP(ba::trial_solve(P, Lr, A, S, lambda, st));
         if ((rc = allreduce(b, so, 3))) return rc;
         RSPL_HIP(ba::shard_post(S, b->red, n6, b->nranks, 1, ba::fast_path(A.K) ? 1 : 0, q, st));
-      } else {
-        RSPL_HIP(ba::trial(P, Lr, A, S, lambda, q, st));
       }
-      // speculative linearisation of the candidate into the spare set, queued behind the trial:
-      // the GPU runs it while the host reads the mailbox, so the next iteration's first kernel is
-      // already queued when the host decides (a rejected trial wastes it; the current set stays)
-      ba::Problem Pc = P;
-      Pc.T = P.Tn; Pc.X = P.Xn; Pc.L = P.Ln;
+      // speculative linearisation of the candidate into the spare set: the GPU runs it while the
+      // host reads the mailbox, so the next iteration's first kernel is already queued when the
+      // host decides (a rejected trial wastes it; the current set stays).  On the fast path it
+      // is fused into the trial's last kernel, otherwise queued behind the trial.
       ba::Lin Ls = Lr;
       Ls.Hpp = b->Hpp_s; Ls.bp = b->bp_s; Ls.Hll = b->Hll_es; Ls.bl = b->bl_es; Ls.Hpl = b->Hpl_s;
       ba::Sys Ss = S;
       Ss.Hll = b->Hll_s; Ss.bl = b->bl_s;
-      if (it + 1 < iters) RSPL_HIP(ba::linearize(Pc, Ls, A, Ss, false, st));
+      bool fused = false;
+      if (!sh) {
+        if (++b->tag == 0) b->tag = 1;  // 0 is the flags' initial value
+        ba::Spec sp{Ls, Ss, b->lflag, b->tag};
+        RSPL_HIP(ba::trial(P, Lr, A, S, lambda, q, st, it + 1 < iters ? &sp : nullptr, &fused));
+      }
+      if (it + 1 < iters && !fused) {
+        ba::Problem Pc = P;
+        Pc.T = P.Tn; Pc.X = P.Xn; Pc.L = P.Ln;
+        RSPL_HIP(ba::linearize(Pc, Ls, A, Ss, false, st));
+      }
       if ((rc = wait_mail(b, q, v))) return rc;
       const bool ok = v[3] == 0.0;
       const double tempChi = ok ? v[0] : std::numeric_limits<double>::max();
@@ -346,6 +356,7 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
       hipMalloc((void**)&b->cbuf, CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE).bytes) !=
           hipSuccess ||
       hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
+      hipMemset(b->lflag, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
       hipMemset(b->pair_ctr, 0, sizeof(unsigned) * std::max(b->maxK * (b->maxK + 1) / 2, 1)) != hipSuccess) {
     set_error("BA stream / mailbox allocation failed");
     rspl_ba_destroy(b);

@@ -307,10 +307,9 @@ __device__ __forceinline__ void store_contrib(const Lin& L, int e, int o, double
   else L.Hpl[24 * e + o - 62] = v;
 }
 
-__device__ __forceinline__ double edge_weight(const Problem& P, const Lin& L, const Active& A, int e, int t) {
+__device__ __forceinline__ double edge_weight_of(const Problem& P, const Active& A, const double* er, int t) {
   double w = einfo(t);
   if (A.robust) {
-    const double* er = L.err + 4 * e;
     double chi2 = 0;
     for (int k = 0; k < edim(t); k++) chi2 += er[k] * er[k];
     chi2 *= einfo(t);
@@ -321,12 +320,16 @@ __device__ __forceinline__ double edge_weight(const Problem& P, const Lin& L, co
   return w;
 }
 
+__device__ __forceinline__ double edge_weight(const Problem& P, const Lin& L, const Active& A, int e, int t) {
+  return edge_weight_of(P, A, L.err + 4 * e, t);
+}
+
 // point edges: analytic Jacobians (g2o types_sba).  Mono edges carry a zero third
 // row, so every index below is a compile-time constant (register resident, no scratch).
 // Writes the pose-side records of edge e (when its pose is optimised) and accumulates
 // the landmark side (Hll 3x3, bl 3) into hl / bv.
 __device__ __forceinline__ void point_edge(const Problem& P, const Lin& L, const Active& A, int e, bool pose_opt,
-                                           double (&hl)[9], double (&bv)[3]) {
+                                           const double* Tb, const double* Xg, double (&hl)[9], double (&bv)[3]) {
   if (A.elevel && A.elevel[e]) {  // outside this phase: exact-zero records, no contribution
     if (pose_opt) {
 #pragma unroll
@@ -339,13 +342,13 @@ __device__ __forceinline__ void point_edge(const Problem& P, const Lin& L, const
     return;
   }
   const int t = P.etype[e];
-  const int pose = P.epose[e], g = P.elm[e];
+  const int pose = P.epose[e];
   const double* cam = P.cams + 5 * P.ecam[e];
-  const SE3 T = load_T(P.T + 8 * pose);
+  const SE3 T = load_T(Tb + 8 * pose);
   const double fx = cam[0], fy = cam[1], bf = cam[4];
   double R[9], Xc[3];
   q_to_R(T.q, R);
-  mat3_vec(R, P.X + 3 * g, Xc);
+  mat3_vec(R, Xg, Xc);
 #pragma unroll
   for (int k = 0; k < 3; k++) Xc[k] += T.t[k];
   const double x = Xc[0], y = Xc[1], z = Xc[2], iz = 1.0 / z, iz2 = iz * iz;
@@ -412,13 +415,14 @@ __device__ __forceinline__ void group_sum(double (&v)[N]) {
 // point landmarks: a group of kGroup lanes per landmark, lane j linearises edges j, j+8, ...
 // of the landmark's CSR list; the group sums Hll / bl (no per-edge landmark records)
 __device__ __forceinline__ void lin_point_landmarks(const Problem& P, const Lin& L, const Active& A, const Sys& S,
-                                                    int t) {
+                                                    int t, bool maxd) {
   const int g = t / kGroup, j = t % kGroup;
   double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bv[3] = {0, 0, 0};
   const bool in = g < P.nq;
   if (in) {
     const int k1 = A.lm_off[g + 1];
-    for (int k = A.lm_off[g] + j; k < k1; k += kGroup) point_edge(P, L, A, A.lm_edges[k], A.lm_pose[k] >= 0, hl, bv);
+    for (int k = A.lm_off[g] + j; k < k1; k += kGroup)
+      point_edge(P, L, A, A.lm_edges[k], A.lm_pose[k] >= 0, P.T, P.X + 3 * g, hl, bv);
   }
   group_sum(hl);
   group_sum(bv);
@@ -431,16 +435,24 @@ __device__ __forceinline__ void lin_point_landmarks(const Problem& P, const Lin&
 #pragma unroll
   for (int i = 0; i < 3; i++) S.bl[4 * g + i] = bv[i];
   S.bl[4 * g + 3] = 0.0;
-  atomic_max_pos(S.out + 2, fmax(fabs(hl[0]), fmax(fabs(hl[4]), fabs(hl[8]))));
+  if (maxd) atomic_max_pos(S.out + 2, fmax(fabs(hl[0]), fmax(fabs(hl[4]), fabs(hl[8]))));
 }
 
 // line edges: g2o's numeric central difference (delta 1e-9), one wave per edge, the 20
 // perturbed error evaluations (+-delta on 4 line + 6 pose dims) in parallel lanes.  The
 // landmark-side records are written through (sc1); the last edge of a line landmark to
 // finish (ticket) sums them in CSR order into the landmark block.
-__device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const Active& A, const Sys& S, int blk) {
+// SPEC: the speculative linearisation (at the candidate P.Tn / P.Ln) inside
+// update_errors_kernel.  The wave waits for the
+// group that updates its line landmark (lflag[l] == tag; the groups run in lower-numbered
+// blocks, which are dispatched first) and takes the candidate line and the edge's error from
+// it through coherent loads, so the records are bitwise those of a separate pass.
+template <bool SPEC>
+__device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const Active& A, const Sys& S, int blk,
+                                          bool maxd, const unsigned* lflag, unsigned tag) {
   __shared__ double ev[4][20][4];
   __shared__ double J[4][4 * 6 + 4 * 4];
+  __shared__ double es[4][4];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int i = blk * 4 + wv;
   const bool on = i < A.n_line_edges;
@@ -458,13 +470,26 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
   const double* cam = P.cams + 5 * (live ? P.ecam[e] : 0);
   const double* obs = P.eobs + 8 * e;
   const double delta = 1e-9, scal = 1.0 / (2 * delta);
+  double lv = 0;  // SPEC: lanes 0-5 the candidate line, lanes 6-9 the edge's error
+  if (SPEC && live) {
+    const int l = g - P.nq;
+    if (lane == 0)
+      while (__hip_atomic_load(lflag + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag) __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+    if (lane < 6) lv = __hip_atomic_load(P.Ln + 6 * l + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else if (lane < 10) lv = __hip_atomic_load(L.err + 4 * e + lane - 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  double Lc[6];  // SPEC only
+#pragma unroll
+  for (int k = 0; k < 6; k++) Lc[k] = __shfl(lv, k);
+  if (SPEC && lane >= 6 && lane < 10) es[wv][lane - 6] = lv;
   if (live && lane < 20) {
     const int d = lane >> 1;
     const double sgn = (lane & 1) ? -delta : delta;
-    const SE3 T = load_T(P.T + 8 * pose);
+    const SE3 T = load_T((SPEC ? P.Tn : P.T) + 8 * pose);
     double Lp[6];
     const double* L0 = P.L + 6 * (g - P.nq);
-    for (int k = 0; k < 6; k++) Lp[k] = L0[k];
+    for (int k = 0; k < 6; k++) Lp[k] = SPEC ? Lc[k] : L0[k];
     double er[4] = {0, 0, 0, 0};
     if (d < 4) {
       double v[4] = {0, 0, 0, 0};
@@ -490,8 +515,8 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
   }
   __syncthreads();
   if (!on) return;
-  const double w = live ? edge_weight(P, L, A, e, t) : 0.0;
-  const double* er = L.err + 4 * e;
+  const double* er = SPEC ? &es[wv][0] : L.err + 4 * e;
+  const double w = live ? edge_weight_of(P, A, er, t) : 0.0;
   for (int o = lane; o < 86; o += 64) {
     const double v = live ? contrib(o, rows, 4, w, er, &J[wv][0], &J[wv][24]) : 0.0;
     if (o < 20)
@@ -520,14 +545,15 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
   double m = (lane < 16 && lane % 5 == 0) ? fabs(s) : 0.0;
 #pragma unroll
   for (int o = 8; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o));
-  if (lane == 0 && A.lm_act[gl]) atomic_max_pos(S.out + 2, m);
+  if (maxd && lane == 0 && A.lm_act[gl]) atomic_max_pos(S.out + 2, m);
 }
 
 // one launch for both landmark families: blocks [0, nbq) point landmarks (kGroup lanes
-// each), blocks [nbq, ...) line edges (one wave each)
-__global__ __launch_bounds__(256) void linearize_kernel(Problem P, Lin L, Active A, Sys S, int nbq) {
-  if ((int)blockIdx.x < nbq) lin_point_landmarks(P, L, A, S, blockIdx.x * 256 + threadIdx.x);
-  else lin_lines(P, L, A, S, blockIdx.x - nbq);
+// each), blocks [nbq, ...) line edges (one wave each).  maxd: contribute the landmark
+// diagonals to S.out[2] (computeLambdaInit); speculative passes leave it alone.
+__global__ __launch_bounds__(256) void linearize_kernel(Problem P, Lin L, Active A, Sys S, int nbq, int maxd) {
+  if ((int)blockIdx.x < nbq) lin_point_landmarks(P, L, A, S, blockIdx.x * 256 + threadIdx.x, maxd != 0);
+  else lin_lines<false>(P, L, A, S, blockIdx.x - nbq, maxd != 0, nullptr, 0u);
 }
 
 // deterministic block reduction of NV values per thread: wave shuffles, then waves in order
@@ -1235,10 +1261,24 @@ __global__ __launch_bounds__(256) void update_kernel(Problem P, Lin L, Active A,
 // landmark (points += xl, lines oplus; copied when inactive: ping-pong), the scale term, and
 // then the robust cost of the landmark's edges against the candidate poses.  The last block
 // (ticket) sums the block partials in order and posts {chi2, scale, maxdiag, fail} + seq.
+// Spec: the speculative linearisation of the candidate fused into update_errors_kernel
+// (records into the spare set Ls / Ss).  Blocks [0, nbu) are the landmark groups: besides the
+// update and the errors, a point group linearises its landmark's edges at the candidate
+// (each lane re-reading only the errors it wrote itself) and a line group publishes the
+// candidate line and its edges' errors (coherent stores, then lflag[l] = tag).  Blocks
+// [nbu, ...) are line-edge waves (lin_lines<true>).  The mailbox ticket counts only the
+// group blocks, so the host decides while the line waves still run.
+template <bool SPEC>
 __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Active A, Sys S, double lambda,
-                                                            unsigned long long seq) {
+                                                            unsigned long long seq, Lin Ls, Sys Ss, int nbu,
+                                                            unsigned* lflag, unsigned tag) {
   __shared__ double red[4 * 2];
   __shared__ int last;
+  if (SPEC && (int)blockIdx.x >= nbu) {
+    lin_lines<true>(P, Ls, A, Ss, blockIdx.x - nbu, false, lflag, tag);
+    return;
+  }
+  if (!SPEC) nbu = gridDim.x;
   const int t = blockIdx.x * 256 + threadIdx.x, g = t / kGroup, j = t % kGroup;
   const bool failed = *S.fail != 0;
   const bool in = g < A.nL;
@@ -1283,8 +1323,8 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
 #pragma unroll
       for (int q = 0; q < 4; q++) sc += xl[q] * (lambda * xl[q] + bl[q]);
   }
+  double lm[6] = {0, 0, 0, 0, 0, 0};
   if (in) {
-    double lm[6];
     if (point) {
 #pragma unroll
       for (int q = 0; q < 3; q++) lm[q] = P.X[3 * g + q] + xl[q];
@@ -1298,7 +1338,10 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
       if (upd) line_oplus(lm, xl);
       if (j == 0)
 #pragma unroll
-        for (int q = 0; q < 6; q++) P.Ln[6 * l + q] = lm[q];
+        for (int q = 0; q < 6; q++) {
+          if (SPEC) __hip_atomic_store(P.Ln + 6 * l + q, lm[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else P.Ln[6 * l + q] = lm[q];
+        }
     }
     for (int k = k0 + j; k < k1; k += kGroup) {
       const int e = A.lm_edges[k];
@@ -1311,7 +1354,10 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
       for (int q = 0; q < edim(te); q++) chi2 += er[q] * er[q];
       chi2 *= einfo(te);
 #pragma unroll
-      for (int q = 0; q < 4; q++) L.err[4 * e + q] = er[q];
+      for (int q = 0; q < 4; q++) {
+        if (SPEC && !point) __hip_atomic_store(L.err + 4 * e + q, er[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else L.err[4 * e + q] = er[q];
+      }
       double cst = chi2;
       if (A.robust) {
         double r1;
@@ -1320,6 +1366,28 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
       L.rho0[e] = cst;
       chi += cst;
     }
+    if (SPEC && !point) {  // the line and its edges' errors are out: release the line-edge waves
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (j == 0) __hip_atomic_store(lflag + (g - P.nq), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  if (SPEC) {  // point landmarks: linearise at the candidate (the errors just written by this lane)
+    double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bv[3] = {0, 0, 0};
+    if (in && point)
+      for (int k = k0 + j; k < k1; k += kGroup)
+        point_edge(P, Ls, A, A.lm_edges[k], A.lm_pose[k] >= 0, P.Tn, lm, hl, bv);
+    group_sum(hl);
+    group_sum(bv);
+    if (in && point && j == 0 && A.lm_act[g]) {
+      double* H = Ss.Hll + 16 * g;
+#pragma unroll
+      for (int i = 0; i < 9; i++) H[i] = hl[i];
+#pragma unroll
+      for (int i = 9; i < 16; i++) H[i] = 0.0;
+#pragma unroll
+      for (int i = 0; i < 3; i++) Ss.bl[4 * g + i] = bv[i];
+      Ss.bl[4 * g + 3] = 0.0;
+    }
   }
   double acc[2] = {chi, sc};
   block_reduce<2>(acc, red);
@@ -1327,12 +1395,12 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     __hip_atomic_store(S.partial + blockIdx.x, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(S.partial2 + blockIdx.x, red[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned tk = ticket(S.counter);
-    last = tk == gridDim.x - 1;
+    last = tk == (unsigned)nbu - 1;
   }
   __syncthreads();
   if (!last) return;
   double f2[2] = {0, 0};
-  for (int k = threadIdx.x; k < (int)gridDim.x; k += 256) {
+  for (int k = threadIdx.x; k < nbu; k += 256) {
     f2[0] += __hip_atomic_load(S.partial + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     f2[1] += __hip_atomic_load(S.partial2 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1531,7 +1599,8 @@ int update_errors_blocks(const Active& A) { return A.nL > 0 ? (A.nL * kGroup + 2
 hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool with_maxdiag,
                      hipStream_t s) {
   const int nbq = (P.nq * kGroup + 255) / 256, nbl = (A.n_line_edges + 3) / 4;
-  if (nbq + nbl > 0) hipLaunchKernelGGL(linearize_kernel, dim3(nbq + nbl), dim3(256), 0, s, P, L, A, S, nbq);
+  if (nbq + nbl > 0)
+    hipLaunchKernelGGL(linearize_kernel, dim3(nbq + nbl), dim3(256), 0, s, P, L, A, S, nbq, with_maxdiag ? 1 : 0);
   if (with_maxdiag && A.K > 0 && A.Ea > 0)
     hipLaunchKernelGGL(pose_diag_kernel, dim3((A.Ea + 255) / 256), dim3(256), 0, s, P, L, A, S);
   return hipGetLastError();
@@ -1555,7 +1624,8 @@ hipError_t ensure_schur_attr() {
 }
 
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
-                 hipStream_t s) {
+                 hipStream_t s, const Spec* spec, bool* fused) {
+  *fused = false;
   if (A.npairs * A.nchk > 0)
     hipLaunchKernelGGL(pair_chunk_kernel, dim3(A.npairs * A.nchk), dim3(64), 0, s, P, L, A, S, lambda);
   const int n = 6 * A.K;
@@ -1563,7 +1633,16 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
     hipError_t e = ensure_schur_attr();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
-    hipLaunchKernelGGL(update_errors_kernel, dim3(update_errors_blocks(A)), dim3(256), 0, s, P, L, A, S, lambda, seq);
+    const int nbu = update_errors_blocks(A);
+    if (spec) {
+      const int nbl = (A.n_line_edges + 3) / 4;
+      hipLaunchKernelGGL(update_errors_kernel<true>, dim3(nbu + nbl), dim3(256), 0, s, P, L, A, S, lambda, seq,
+                         spec->Ls, spec->Ss, nbu, spec->lflag, spec->tag);
+      *fused = true;
+    } else {
+      hipLaunchKernelGGL(update_errors_kernel<false>, dim3(nbu), dim3(256), 0, s, P, L, A, S, lambda, seq, L, S, 0,
+                         nullptr, 0u);
+    }
     return hipGetLastError();
   }
   if (n > 0) {  // larger systems: Schur sums + global-memory Cholesky
@@ -1627,7 +1706,8 @@ hipError_t trial_solve(const Problem& P, const Lin& L, const Active& A, Sys& S, 
     hipError_t e = ensure_schur_attr();
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
-    hipLaunchKernelGGL(update_errors_kernel, dim3(update_errors_blocks(A)), dim3(256), 0, s, P, L, A, S, lambda, 0ull);
+    hipLaunchKernelGGL(update_errors_kernel<false>, dim3(update_errors_blocks(A)), dim3(256), 0, s, P, L, A, S, lambda,
+                       0ull, L, S, 0, nullptr, 0u);
     return hipGetLastError();
   }
   if (n > 0) {

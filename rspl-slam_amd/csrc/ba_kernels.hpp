@@ -89,14 +89,24 @@ constexpr int kLmChunk = 256;  // landmarks per Schur chunk (4 per lane)
 // errors (+ fused final reduction and mailbox post with sequence number seq)
 hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq,
                           hipStream_t s);
-// edge Jacobians + landmark blocks S.Hll / S.bl (+ max diagonal; pose blocks too when with_maxdiag)
+// edge Jacobians + landmark blocks S.Hll / S.bl (+ with_maxdiag: the max diagonal of pose and
+// landmark blocks into S.out[2], computeLambdaInit)
 hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool with_maxdiag,
                      hipStream_t s);
 // mailbox post; with A, after linearize(with_maxdiag) it first folds the pose-block maxima in
 hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A = nullptr);
-// one LM trial: Schur complement, Cholesky, back-substitution + candidate state, its cost
+// speculative linearisation of a trial's candidate into a spare record set, fused into the
+// trial's last kernel (fast path only)
+struct Spec {
+  Lin Ls;            // spare edge records (err / rho0 shared with the current set)
+  Sys Ss;            // spare landmark blocks Hll / bl
+  unsigned* lflag;   // [max_lines] line-landmark release flags (zeroed at create)
+  unsigned tag;      // this trial's flag value (distinct per launch)
+};
+// one LM trial: Schur complement, Cholesky, back-substitution + candidate state, its cost;
+// with spec on the fast path also the candidate's linearisation (*fused = true)
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
-                 hipStream_t s);
+                 hipStream_t s, const Spec* spec, bool* fused);
 // landmark CSR from the per-landmark offsets: atomic slots, then each landmark's list sorted by
 // edge id (deterministic) with its reduced poses; fill[] must be zero on entry
 hipError_t build_csr(const Problem& P, const Active& A, int* fill, int* lm_edges, int* lm_pose, hipStream_t s);
