@@ -43,12 +43,14 @@ struct rspl_ba {
   unsigned* lm_ctr;  // [max_lines] line-landmark tickets (zeroed at create, re-armed by the kernel)
   unsigned* lflag;   // [max_lines] release flags of the fused speculative linearisation (zeroed at create)
   unsigned tag = 0;  // last flag value used
+  unsigned long long* prof = nullptr;  // RSPL_BA_PROF: timing trace of one trial per call
+  int prof_nb[3] = {0, 0, 0};          // its pair_chunk / update_errors grid sizes, group blocks
   // landmark CSR (filled on the device) and the Schur chunk / pose-pair sums
   int *lm_edges, *lm_pose;
   double *chunk, *pairfin;
   unsigned* pair_ctr;  // [npairs] chunk tickets (zeroed at create, re-armed by the kernel)
   int *pp_cnt, *pp_off;  // [npairs * nchk (+1)] edge pairs per Schur chunk, segment offsets
-  int* pp_buf = nullptr;  // edge-pair lists (e1s | e2s), growable
+  int4* pp_buf = nullptr;  // edge-pair list {e1, e2, landmark, 0}, growable
   size_t pp_cap = 0;      // capacity in pairs
   // per-call inputs (cameras, T / X / L, edges, reduced pose ids, landmark offsets, pose pairs,
   // zeroed level / fill / flags / out), laid out exactly like the staging buffer's call
@@ -225,6 +227,42 @@ Se3h inverse(const Se3h& T) {  // SE3Quat::inverse
   return r;
 }
 
+// RSPL_BA_PROF: one traced trial per call -> one stderr line of in-kernel spans (us, from the
+// device's 100 MHz wall clock): pair_chunk first..last block start, span; gap to the solve;
+// solve phases (assembly, factor, back-substitution, poses); gap; update_errors span
+void report_prof(rspl_ba* b) {
+  std::vector<unsigned long long> h(ba::kProfLen);
+  if (hipStreamSynchronize(b->stream) != hipSuccess ||
+      hipMemcpy(h.data(), b->prof, sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost) != hipSuccess)
+    return;
+  // per kernel: first block start, then over blocks [b0, b1) the latest stamp of each slot
+  auto us = [](unsigned long long a, unsigned long long c) { return c && a ? ((double)c - (double)a) / 100.0 : -1.0; };
+  auto first = [&](int off, int b0, int b1) {
+    unsigned long long t = ~0ull;
+    for (int i = b0; i < std::min(b1, 4096); i++)
+      if (h[off + 4 * i]) t = std::min(t, h[off + 4 * i]);
+    return t;
+  };
+  auto last = [&](int off, int b0, int b1, int slot) {
+    unsigned long long t = 0;
+    for (int i = b0; i < std::min(b1, 4096); i++) t = std::max(t, h[off + 4 * i + slot]);
+    return t;
+  };
+  const int npc = b->prof_nb[0], nue = b->prof_nb[1], nbu = b->prof_nb[2];
+  const unsigned long long p0 = first(ba::kProfPc, 0, npc), u0 = first(ba::kProfUe, 0, nue);
+  fprintf(stderr,
+          "ba_prof us: pcstarts %.1f pcloop %.1f pcticket %.1f pcend %.1f gap %.1f asm %.1f factor %.1f back %.1f"
+          " poses %.1f gap %.1f uestarts %.1f upd %.1f pointlin %.1f groupsend %.1f lineswait %.1f linesend %.1f\n",
+          us(p0, last(ba::kProfPc, 0, npc, 0)), us(p0, last(ba::kProfPc, 0, npc, 1)),
+          us(p0, last(ba::kProfPc, 0, npc, 2)), us(p0, last(ba::kProfPc, 0, npc, 3)),
+          us(last(ba::kProfPc, 0, npc, 3), h[0]), us(h[0], h[1]), us(h[1], h[2]), us(h[2], h[3]), us(h[3], h[4]),
+          us(h[4], u0), us(u0, last(ba::kProfUe, 0, nue, 0)), us(u0, last(ba::kProfUe, 0, nbu, 1)),
+          us(u0, last(ba::kProfUe, 0, nbu, 2)), us(u0, last(ba::kProfUe, 0, nbu, 3)),
+          us(u0, last(ba::kProfUe, nbu, nue, 1)), us(u0, last(ba::kProfUe, nbu, nue, 3)));
+  b->prof_nb[0] = 0;
+  (void)hipMemset(b->prof, 0, sizeof(unsigned long long) * ba::kProfLen);
+}
+
 // one g2o SparseOptimizer::optimize(iters) with OptimizationAlgorithmLevenberg
 int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
              double* chi2_out, int* done_out) {
@@ -281,7 +319,15 @@ int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Acti
       if (!sh) {
         if (++b->tag == 0) b->tag = 1;  // 0 is the flags' initial value
         ba::Spec sp{Ls, Ss, b->lflag, b->tag};
+        const bool traced = b->prof && it == 3 && qmax == 0 && !b->prof_nb[0];
+        if (traced) {
+          S.prof = sp.Ss.prof = b->prof;
+          b->prof_nb[0] = A.npairs * A.nchk;
+          b->prof_nb[1] = ba::update_errors_blocks(A) + (A.n_line_edges + 3) / 4;
+          b->prof_nb[2] = ba::update_errors_blocks(A);
+        }
         RSPL_HIP(ba::trial(P, Lr, A, S, lambda, q, st, it + 1 < iters ? &sp : nullptr, &fused));
+        S.prof = nullptr;
       }
       if (it + 1 < iters && !fused) {
         ba::Problem Pc = P;
@@ -363,6 +409,13 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
     return RSPL_E_DEVICE;
   }
   memset(b->mail, 0, sizeof(ba::Mail));
+  if (getenv("RSPL_BA_PROF") &&
+      (hipMalloc((void**)&b->prof, sizeof(unsigned long long) * ba::kProfLen) != hipSuccess ||
+       hipMemset(b->prof, 0, sizeof(unsigned long long) * ba::kProfLen) != hipSuccess)) {
+    set_error("BA trace allocation failed");
+    rspl_ba_destroy(b);
+    return RSPL_E_DEVICE;
+  }
   *out = b;
   return RSPL_OK;
 }
@@ -407,6 +460,7 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
   b->arena.release();
   if (b->cbuf) (void)hipFree(b->cbuf);
   if (b->pp_buf) (void)hipFree(b->pp_buf);
+  if (b->prof) (void)hipFree(b->prof);
   if (b->stage) (void)hipHostFree(b->stage);
   if (b->mail) (void)hipHostFree(b->mail);
   if (b->stream) (void)hipStreamDestroy(b->stream);
@@ -528,7 +582,7 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
     b->pp_buf = nullptr;
     b->pp_cap = 0;
     const size_t cap = std::max(pair_bound, (size_t)1 << 16);
-    RSPL_HIP(hipMalloc((void**)&b->pp_buf, 2 * sizeof(int) * cap));
+    RSPL_HIP(hipMalloc((void**)&b->pp_buf, sizeof(int4) * cap));
     b->pp_cap = cap;
   }
   int* pidx = reinterpret_cast<int*>(sg + cl.pidx);
@@ -597,10 +651,9 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   A.robust = 1;
   mark();
   A.pp_off = b->pp_off;
-  A.pp_e1 = b->pp_buf;
-  A.pp_e2 = b->pp_buf + b->pp_cap;
+  A.pp = b->pp_buf;
   RSPL_HIP(ba::build_csr(P, A, reinterpret_cast<int*>(cb + cl.fill), b->lm_edges, b->lm_pose, st));
-  RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, b->pp_buf + b->pp_cap, st));
+  RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, st));
   mark();
   if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first)))
     return rc;
@@ -645,6 +698,7 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
     RSPL_HIP(ba::finish(P, Lr, E, inl_h, T_h, X_h, L_h, S, q, st));
   }
   if ((rc = wait_mail(b, q, nullptr))) return rc;
+  if (b->prof && b->prof_nb[0]) report_prof(b);
   if (nq) memcpy(res->points, b->stage + dl.X, sizeof(double) * 3 * nq);
   if (nl) memcpy(res->lines, b->stage + dl.L, sizeof(double) * 6 * nl);
   const double* Tout = reinterpret_cast<const double*>(b->stage + dl.T);

@@ -449,7 +449,8 @@ __device__ __forceinline__ void lin_point_landmarks(const Problem& P, const Lin&
 // it through coherent loads, so the records are bitwise those of a separate pass.
 template <bool SPEC>
 __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const Active& A, const Sys& S, int blk,
-                                          bool maxd, const unsigned* lflag, unsigned tag) {
+                                          bool maxd, const unsigned* lflag, unsigned tag,
+                                          unsigned long long* stamp = nullptr) {
   __shared__ double ev[4][20][4];
   __shared__ double J[4][4 * 6 + 4 * 4];
   __shared__ double es[4][4];
@@ -476,6 +477,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
     if (lane == 0)
       while (__hip_atomic_load(lflag + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag) __builtin_amdgcn_s_sleep(1);
     asm volatile("" ::: "memory");
+    if (stamp && lane == 0 && wv == 0) *stamp = wall_clock64();
     if (lane < 6) lv = __hip_atomic_load(P.Ln + 6 * l + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else if (lane < 10) lv = __hip_atomic_load(L.err + 4 * e + lane - 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -705,15 +707,11 @@ __device__ __forceinline__ bool lm_dinv(const double* Hll, bool point, double la
   return small_inv<4>(H, D);
 }
 
-// one edge pair's Schur terms (Y = Hpl_e1 Dinv_g formed on the fly) added into acc[48]
-__device__ __forceinline__ void schur_pair(const Lin& L, const Sys& S, int g, int e1, int e2, const double (&D)[16],
-                                           double (&acc)[48]) {
-  const double* H1 = L.Hpl + 24 * e1;
-  const double* H2 = L.Hpl + 24 * e2;
-  double B[24];
-#pragma unroll
-  for (int q = 0; q < 24; q++) B[q] = H2[q];
-  const bool diag = e1 == e2;
+// one edge pair's Schur terms (Y = Hpl_e1 Dinv_g formed on the fly) added into acc[48];
+// H1 / H2 / Hp / bpv / blv already in registers (diag: e1 == e2, H2 == H1)
+__device__ __forceinline__ void schur_pair(const double (&H1)[24], const double (&B)[24], bool diag,
+                                           const double (&Hp)[36], const double (&bpv)[6], const double (&blv)[4],
+                                           const double (&D)[16], double (&acc)[48]) {
 #pragma unroll
   for (int r = 0; r < 6; r++) {
     const double h0 = H1[r * 4], h1 = H1[r * 4 + 1], h2 = H1[r * 4 + 2], h3 = H1[r * 4 + 3];
@@ -724,12 +722,10 @@ __device__ __forceinline__ void schur_pair(const Lin& L, const Sys& S, int g, in
     for (int cc = 0; cc < 6; cc++)
       acc[r * 6 + cc] -= y[0] * B[cc * 4] + y[1] * B[cc * 4 + 1] + y[2] * B[cc * 4 + 2] + y[3] * B[cc * 4 + 3];
     if (diag) {
-      const double* Hp = L.Hpp + 36 * e1;
-      const double* bl = S.bl + 4 * g;
 #pragma unroll
       for (int cc = 0; cc < 6; cc++) acc[r * 6 + cc] += Hp[r * 6 + cc];
-      acc[36 + r] += L.bp[6 * e1 + r];
-      acc[42 + r] += y[0] * bl[0] + y[1] * bl[1] + y[2] * bl[2] + y[3] * bl[3];
+      acc[36 + r] += bpv[r];
+      acc[42 + r] += y[0] * blv[0] + y[1] * blv[1] + y[2] * blv[2] + y[3] * blv[3];
     }
   }
 }
@@ -740,7 +736,7 @@ __device__ __forceinline__ void schur_pair(const Lin& L, const Sys& S, int g, in
 // landmark lb * kLmChunk + 64 r + l; its matches are found from bit masks over batches of 8
 // CSR entries (independent loads) and placed by a wave prefix sum in lane order.
 template <bool FILL>
-__device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, const int* pp_off, int* e1s, int* e2s) {
+__device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, const int* pp_off, int4* pp) {
   const int lane = threadIdx.x;
   const int pr = c / A.nchk, lb = c - pr * A.nchk;
   const int pa = A.pairs[2 * pr], pb = A.pairs[2 * pr + 1];
@@ -786,8 +782,7 @@ __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, c
         const int e1 = A.lm_edges[ib];
         for (int jb = k0; jb < k1; jb++) {
           if (A.lm_pose[jb] != pb) continue;
-          e1s[q] = e1;
-          e2s[q] = A.lm_edges[jb];
+          pp[q] = make_int4(e1, A.lm_edges[jb], g, 0);
           q++;
         }
       }
@@ -798,10 +793,10 @@ __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, c
 }
 
 __global__ __launch_bounds__(64) void pair_count_kernel(Active A, int* pp_cnt) {
-  pair_scan<false>(A, blockIdx.x, pp_cnt, nullptr, nullptr, nullptr);
+  pair_scan<false>(A, blockIdx.x, pp_cnt, nullptr, nullptr);
 }
-__global__ __launch_bounds__(64) void pair_fill_kernel(Active A, const int* pp_off, int* e1s, int* e2s) {
-  pair_scan<true>(A, blockIdx.x, nullptr, pp_off, e1s, e2s);
+__global__ __launch_bounds__(64) void pair_fill_kernel(Active A, const int* pp_off, int4* pp) {
+  pair_scan<true>(A, blockIdx.x, nullptr, pp_off, pp);
 }
 // exclusive scan of the chunk counts (one workgroup; n = npairs * nchk + 1 offsets)
 __global__ __launch_bounds__(1024) void pair_offsets_kernel(const int* cnt, int* off, int n) {
@@ -830,9 +825,14 @@ __global__ __launch_bounds__(1024) void pair_offsets_kernel(const int* cnt, int*
 // segment of the edge-pair lists, forming Y = Hpl_e1 Dinv_g on the fly:
 //   [0,36)  [e1==e2] Hpp_e1 - Y Hpl_e2^T,   [36,42) [e1==e2] bp_e1,   [42,48) [e1==e2] Y bl_g
 // then the wave sums its 64 lanes in lane order (LDS transpose).
+__device__ __forceinline__ void prof_stamp(const Sys& S, int slot) {
+  if (S.prof) S.prof[slot] = wall_clock64();
+}
+
 __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active A, Sys S, double lambda) {
   __shared__ double red[64 * 49];
   const int c = blockIdx.x, lane = threadIdx.x;
+  if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c);
   const int pr = c / A.nchk;
   const int beg = A.pp_off[c], end = A.pp_off[c + 1];
   double acc[48];
@@ -840,13 +840,36 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
   for (int v = 0; v < 48; v++) acc[v] = 0.0;
   bool bad = false;
   for (int k = beg + lane; k < end; k += 64) {
-    const int e1 = A.pp_e1[k], e2 = A.pp_e2[k];
-    if (A.elevel && (A.elevel[e1] | A.elevel[e2])) continue;  // zero records: no contribution
-    const int g = P.elm[e1];
+    // every operand of the pair is requested before any arithmetic: one memory round trip
+    const int4 q = A.pp[k];
+    const int e1 = q.x, e2 = q.y, g = q.z;
+    const bool diag = e1 == e2;
+    const bool live = !(A.elevel && (A.elevel[e1] | A.elevel[e2]));  // else zero records: no contribution
+    double Hl[16], H1[24], H2[24], Hp[36], bpv[6], blv[4];
+    const double* hl = S.Hll + 16 * g;
+#pragma unroll
+    for (int i = 0; i < 16; i++) Hl[i] = hl[i];
+#pragma unroll
+    for (int i = 0; i < 24; i++) H1[i] = L.Hpl[24 * e1 + i];
+    if (diag) {
+#pragma unroll
+      for (int i = 0; i < 36; i++) Hp[i] = L.Hpp[36 * e1 + i];
+#pragma unroll
+      for (int i = 0; i < 6; i++) bpv[i] = L.bp[6 * e1 + i];
+#pragma unroll
+      for (int i = 0; i < 4; i++) blv[i] = S.bl[4 * g + i];
+#pragma unroll
+      for (int i = 0; i < 24; i++) H2[i] = H1[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 24; i++) H2[i] = L.Hpl[24 * e2 + i];
+    }
+    if (!live) continue;
     double D[16];
-    bad |= !lm_dinv(S.Hll + 16 * g, g < P.nq, lambda, D);
-    schur_pair(L, S, g, e1, e2, D, acc);
+    bad |= !lm_dinv(Hl, g < P.nq, lambda, D);
+    schur_pair(H1, H2, diag, Hp, bpv, blv, D, acc);
   }
+  if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 1);
   if (bad) atomicOr(S.fail, 1);
 #pragma unroll
   for (int v = 0; v < 48; v++) red[lane * 49 + v] = acc[v];
@@ -865,22 +888,26 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
   unsigned tk = 0;
   if (lane == 0) tk = __hip_atomic_fetch_add(S.pair_ctr + pr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   tk = __shfl(tk, 0);
-  if (tk != (unsigned)(c1 - c0 - 1)) return;
+  if (tk != (unsigned)(c1 - c0 - 1)) {
+    if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 2);
+    return;
+  }
   if (lane == 0) __hip_atomic_store(S.pair_ctr + pr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (lane < 48) {
     double s = 0;
-    for (int cb = c0; cb < c1; cb += 8) {  // 8 write-through loads in flight, summed in chunk order
-      double t[8];
+    for (int cb = c0; cb < c1; cb += 16) {  // 16 write-through loads in flight, summed in chunk order
+      double t[16];
 #pragma unroll
-      for (int u = 0; u < 8; u++)
+      for (int u = 0; u < 16; u++)
         t[u] = cb + u < c1 ? __hip_atomic_load(S.chunk + 48 * (cb + u) + lane, __ATOMIC_RELAXED,
                                                __HIP_MEMORY_SCOPE_AGENT)
                            : 0.0;
 #pragma unroll
-      for (int u = 0; u < 8; u++) s += t[u];
+      for (int u = 0; u < 16; u++) s += t[u];
     }
     S.pairfin[48 * pr + lane] = s;
   }
+  if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 3);
 }
 
 // larger systems, stage 2: one thread per (pose pair, entry) scatters the pair sums.
@@ -918,7 +945,7 @@ __global__ __launch_bounds__(256) void pair_final_kernel(Active A, Sys S, double
 //   solve:    backward substitution L^T x = z in wave 0, LDS-resident;
 //   poses:    the candidate T <- exp(xp) T and the pose part of the LM scale.
 // ---------------------------------------------------------------------------
-constexpr int kCholLdsMax = 192;  // packed lower triangle (n+1)(n+2)/2 + 2n + 15 n/6 doubles <= 160 KB of LDS
+constexpr int kCholLdsMax = 192;  // packed lower triangle (n+1)(n+2)/2 + 3n + 15 n/6 doubles <= 160 KB of LDS
 
 // packed row-major lower triangle: element (r, c <= r)
 __device__ __forceinline__ int pk(int r, int c) { return r * (r + 1) / 2 + c; }
@@ -984,8 +1011,18 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
   double* rdg = Al + pk(n + 1, 0);   // [n] 1/D
   double* ddg = rdg + n;                    // [n] D
   double* Ldg = ddg + n;                    // [K][15] strictly-lower parts of the (unit) diagonal blocks
+  double* bpl = Ldg + 15 * K;               // [n] pose gradient bp (for the LM scale)
   const int tid = threadIdx.x;
   if (tid == 0) bad = 0;
+  // the candidate-pose step's operands, fetched before the factorisation (lane = pose)
+  int pose_a = -1;
+  double Tp0[8];
+  if (tid < P.np) {
+    pose_a = A.pidx[tid];
+#pragma unroll
+    for (int k = 0; k < 8; k++) Tp0[k] = P.T[8 * tid + k];
+  }
+  if (tid == 0) prof_stamp(S, 0);
   // assembly: every thread issues its pairfin loads (8 at a time) before writing LDS; the
   // fail flag is checked after them (it would otherwise gate every load)
   const int nent = A.npairs * 42;
@@ -1015,12 +1052,13 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
         }
       } else if (pa == pb) {
         const int r = v - 36;
-        S.bp[6 * pa + r] = v1[u];
+        bpl[6 * pa + r] = v1[u];
         z[6 * pa + r] = v1[u] - v2[u];
       }
     }
   }
   __syncthreads();
+  if (tid == 0) prof_stamp(S, 1);
   // factor: blocked by the 6x6 pose blocks; the rhs row n is factored along (its panel rows
   // become z = D^-1 L^-1 bs: no separate forward substitution)
   const int wv = tid >> 6, lane = tid & 63, fy = tid >> 4, fx = tid & 15;
@@ -1074,6 +1112,7 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
     __syncthreads();
   }
   if (wv != 0) return;
+  if (tid == 0) prof_stamp(S, 2);
   // backward substitution L^T x = z in wave 0 (LDS in program order within the wave)
   for (int s = K - 1; s >= 0; s--) {
     const int c0 = 6 * s;
@@ -1096,30 +1135,32 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
       for (int k = 0; k < 6; k++) z[c0 + k] = xb[k];
   }
   for (int i = lane; i < n; i += 64) S.x[i] = z[i];
+  if (tid == 0) prof_stamp(S, 3);
   // candidate poses (lane = pose; np <= 64): T <- exp(xp) T, fixed poses copied (ping-pong),
   // and the pose part of the LM scale x.(lambda x + bp)
   double sc = 0;
   if (lane < P.np) {
-    const int a = A.pidx[lane];
-    const double* Tp = P.T + 8 * lane;
+    const int a = pose_a;
     double* Tq = P.Tn + 8 * lane;
     if (a >= 0) {
       double xp[6];
 #pragma unroll
       for (int r = 0; r < 6; r++) xp[r] = z[6 * a + r];
-      const SE3 r = se3_mul(se3_exp(xp), load_T(Tp));
+      const SE3 r = se3_mul(se3_exp(xp), load_T(Tp0));
       for (int k = 0; k < 4; k++) Tq[k] = r.q[k];
       for (int k = 0; k < 3; k++) Tq[4 + k] = r.t[k];
       Tq[7] = 0;
 #pragma unroll
-      for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + S.bp[6 * a + k]);
+      for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + bpl[6 * a + k]);
     } else {
-      for (int k = 0; k < 8; k++) Tq[k] = Tp[k];
+#pragma unroll
+      for (int k = 0; k < 8; k++) Tq[k] = Tp0[k];
     }
   }
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
   if (lane == 0) S.out[4] = sc;
+  if (tid == 0) prof_stamp(S, 4);
 }
 
 
@@ -1274,8 +1315,12 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
                                                             unsigned* lflag, unsigned tag) {
   __shared__ double red[4 * 2];
   __shared__ int last;
+  const bool stamp = threadIdx.x == 0 && blockIdx.x < 4096;
+  if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x);
   if (SPEC && (int)blockIdx.x >= nbu) {
-    lin_lines<true>(P, Ls, A, Ss, blockIdx.x - nbu, false, lflag, tag);
+    lin_lines<true>(P, Ls, A, Ss, blockIdx.x - nbu, false, lflag, tag,
+                    S.prof ? S.prof + kProfUe + 4 * blockIdx.x + 1 : nullptr);
+    if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 3);
     return;
   }
   if (!SPEC) nbu = gridDim.x;
@@ -1371,6 +1416,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
       if (j == 0) __hip_atomic_store(lflag + (g - P.nq), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
+  if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 1);
   if (SPEC) {  // point landmarks: linearise at the candidate (the errors just written by this lane)
     double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bv[3] = {0, 0, 0};
     if (in && point)
@@ -1389,6 +1435,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
       Ss.bl[4 * g + 3] = 0.0;
     }
   }
+  if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 2);
   double acc[2] = {chi, sc};
   block_reduce<2>(acc, red);
   if (threadIdx.x == 0) {
@@ -1398,6 +1445,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     last = tk == (unsigned)nbu - 1;
   }
   __syncthreads();
+  if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 3);
   if (!last) return;
   double f2[2] = {0, 0};
   for (int k = threadIdx.x; k < nbu; k += 256) {
@@ -1612,7 +1660,7 @@ hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A) 
   return hipGetLastError();
 }
 
-size_t schur_lds_bytes(int n) { return sizeof(double) * ((size_t)(n + 1) * (n + 2) / 2 + 2 * n + 15 * (n / 6)); }
+size_t schur_lds_bytes(int n) { return sizeof(double) * ((size_t)(n + 1) * (n + 2) / 2 + 3 * n + 15 * (n / 6)); }
 
 hipError_t ensure_schur_attr() {
   static bool attr = false;
@@ -1671,12 +1719,12 @@ hipError_t build_csr(const Problem& P, const Active& A, int* fill, int* lm_edges
   return hipGetLastError();
 }
 
-hipError_t build_pairs(const Active& A, int* pp_cnt, int* pp_off, int* e1s, int* e2s, hipStream_t s) {
+hipError_t build_pairs(const Active& A, int* pp_cnt, int* pp_off, int4* pp, hipStream_t s) {
   const int nc = A.npairs * A.nchk;
   if (nc == 0) return hipSuccess;
   hipLaunchKernelGGL(pair_count_kernel, dim3(nc), dim3(64), 0, s, A, pp_cnt);
   hipLaunchKernelGGL(pair_offsets_kernel, dim3(1), dim3(1024), 0, s, pp_cnt, pp_off, nc);
-  hipLaunchKernelGGL(pair_fill_kernel, dim3(nc), dim3(64), 0, s, A, pp_off, e1s, e2s);
+  hipLaunchKernelGGL(pair_fill_kernel, dim3(nc), dim3(64), 0, s, A, pp_off, pp);
   return hipGetLastError();
 }
 

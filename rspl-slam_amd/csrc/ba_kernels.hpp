@@ -47,8 +47,8 @@ struct Active {          // active structure of one optimize() phase
   int npairs;
   int nchk;              // Schur chunks per pose pair: landmark ranges of kLmChunk
   const int* pp_off;     // [npairs * nchk + 1] segment of each chunk in the edge-pair lists
-  const int* pp_e1;      // edge pairs (e1 of pose a, e2 of pose b, same landmark), chunk-major,
-  const int* pp_e2;      //   landmark order within a chunk
+  const int4* pp;        // edge pairs {e1 of pose a, e2 of pose b, their landmark, 0}, chunk-major,
+                         //   landmark order within a chunk
   int n_line_edges;      // line edges are [Ea - n_line_edges, Ea)
   const uint8_t* elevel; // [E] or null: edge level (!= 0: outside this phase -- level 1 in the
                          // second optimize): zero linearisation records, no cost, error kept
@@ -82,7 +82,13 @@ struct Sys {
   double* shard_out;     // [3] this rank's {chi2, LM scale (landmark part), fail} for the all-reduce,
                          //     written instead of posting the mailbox
   int pose_scale;        // 1: this rank adds the pose part of the LM scale (rank 0 or unsharded)
+  // timing trace of one trial (RSPL_BA_PROF; null otherwise): wall_clock64 stamps
+  //   [0, 8) schur_solve phases, [kProfPc + 4b + i] pair_chunk block b stamps (start, loop
+  //   done, ticket, end), [kProfUe + 4b + i] update_errors block b stamps (start, update /
+  //   flag wait done, before ticket, end)
+  unsigned long long* prof;
 };
+constexpr int kProfPc = 16, kProfUe = kProfPc + 4 * 4096, kProfLen = kProfUe + 4 * 4096;
 
 constexpr int kLmChunk = 256;  // landmarks per Schur chunk (4 per lane)
 
@@ -111,7 +117,7 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
 // edge id (deterministic) with its reduced poses; fill[] must be zero on entry
 hipError_t build_csr(const Problem& P, const Active& A, int* fill, int* lm_edges, int* lm_pose, hipStream_t s);
 // edge-pair lists of the pose pairs (count, offsets, fill; A.pp_* are not read)
-hipError_t build_pairs(const Active& A, int* pp_cnt, int* pp_off, int* e1s, int* e2s, hipStream_t s);
+hipError_t build_pairs(const Active& A, int* pp_cnt, int* pp_off, int4* pp, hipStream_t s);
 // lm_act[g] = landmark g has an edge of level 0 (the second optimize's active landmarks)
 hipError_t landmark_active(const Active& A, const uint8_t* level, uint8_t* lm_act, hipStream_t s);
 hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8_t* inlier, int final_pass,

@@ -28,6 +28,8 @@ struct rspl_sg {
   float* kw[5];
   float* kb[5];
   float *wqkv, *bqkv, *wm, *bm, *w1, *b1, *w2, *b2;  // [18] stacked
+  // RSPL_PREC_FP16: mlp.0 with attn.merge folded into its message half (fp32 source of hw1, bias)
+  float *w1m, *b1m;
   float *wf, *bf, *bin;
   // RSPL_PREC_FP16: transposed fp16 copies [N][K] of every projection / MLP weight
   _Float16* hkw[5];
@@ -75,6 +77,7 @@ void carve(F& ar, rspl_sg* s) {
   take(s->wqkv, (size_t)kLayers * 256 * 768); take(s->bqkv, (size_t)kLayers * 768);
   take(s->wm, (size_t)kLayers * 256 * 256); take(s->bm, (size_t)kLayers * 256);
   take(s->w1, (size_t)kLayers * 512 * 512); take(s->b1, (size_t)kLayers * 512);
+  take(s->w1m, (size_t)kLayers * 512 * 512); take(s->b1m, (size_t)kLayers * 512);
   take(s->w2, (size_t)kLayers * 512 * 256); take(s->b2, (size_t)kLayers * 256);
   take(s->wf, 256 * 256); take(s->bf, 256); take(s->bin, 4);
   for (int i = 0; i < 5; i++) take(s->hkw[i], (size_t)(i == 0 ? kKencIn : kKencCh[i]) * kKencCh[i + 1]);
@@ -174,6 +177,31 @@ int upload_weights(rspl_sg* s, const std::vector<Tensor>& ts) {
     }
     up(s->w1 + (size_t)l * 512 * 512, w1t);
     up(s->b1 + (size_t)l * 512, b1t);
+    {  // fp16 engine: attn.merge is linear and feeds only mlp.0's message half, so
+       // W1 [x; Wm o + bm] + b1 = [W1x | W1m Wm] [x; o] + (b1 + W1m bm): one GEMM fewer per layer
+      std::vector<double> acc((size_t)256 * 512, 0.0), bacc(512);
+      for (int o = 0; o < 512; o++) {
+        double sb = sc[o] * b0->data[o] + sh[o];
+        for (int m = 0; m < 256; m++) sb += sc[o] * w0->data[(size_t)o * 512 + 256 + m] * bm->data[m];
+        bacc[o] = sb;
+      }
+      std::vector<double> w1d((size_t)256 * 512);  // message half, [m][o]
+      for (int o = 0; o < 512; o++)
+        for (int m = 0; m < 256; m++) w1d[(size_t)m * 512 + o] = sc[o] * w0->data[(size_t)o * 512 + 256 + m];
+      for (int c = 0; c < 256; c++) {
+        double* ac = acc.data() + (size_t)c * 512;
+        for (int m = 0; m < 256; m++) {
+          const double a = wmt[(size_t)c * 256 + m];
+          const double* row = w1d.data() + (size_t)m * 512;
+          for (int o = 0; o < 512; o++) ac[o] += a * row[o];
+        }
+      }
+      std::vector<float> w1f(w1t), b1f(512);
+      for (size_t i = 0; i < acc.size(); i++) w1f[(size_t)256 * 512 + i] = (float)acc[i];
+      for (int o = 0; o < 512; o++) b1f[o] = (float)bacc[o];
+      up(s->w1m + (size_t)l * 512 * 512, w1f);
+      up(s->b1m + (size_t)l * 512, b1f);
+    }
     std::vector<float> w2t((size_t)512 * 256);
     for (int o = 0; o < 256; o++)
       for (int k = 0; k < 512; k++) w2t[(size_t)k * 256 + o] = w3->data[(size_t)o * 512 + k];
@@ -269,7 +297,7 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
       okh &= sg::to_half_t(s->wqkv + (size_t)l * 256 * 768, 256, 768, s->hwqkv + (size_t)l * 256 * 768, s->stream) ==
              hipSuccess;
       okh &= sg::to_half_t(s->wm + (size_t)l * 65536, 256, 256, s->hwm + (size_t)l * 65536, s->stream) == hipSuccess;
-      okh &= sg::to_half_t(s->w1 + (size_t)l * 512 * 512, 512, 512, s->hw1 + (size_t)l * 512 * 512, s->stream) ==
+      okh &= sg::to_half_t(s->w1m + (size_t)l * 512 * 512, 512, 512, s->hw1 + (size_t)l * 512 * 512, s->stream) ==
              hipSuccess;
       okh &= sg::to_half_t(s->w2 + (size_t)l * 512 * 256, 512, 256, s->hw2 + (size_t)l * 512 * 256, s->stream) ==
              hipSuccess;
@@ -366,11 +394,9 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
       at.QK = s->QKh; at.Vt = s->Vth; at.O = s->Oh; at.n0 = d_n0; at.n1 = d_n1; at.nmax = nm; at.ldv = s->ldv;
       at.cross = l & 1;
       RSPL_HIP(sg::attention_h(at, B, st));
-      sg::GemmHArgs mg = gh(s->Oh, 256, s->hwm + (size_t)l * 65536, 256, 256, s->bm + (size_t)l * 256);
-      mg.C16 = s->MSGh; mg.ldc16 = 256;
-      RSPL_HIP(sg::gemm_h(mg, 1, st));
-      sg::GemmHArgs m1 = gh(s->Xh, 256, s->hw1 + (size_t)l * 512 * 512, 512, 512, s->b1 + (size_t)l * 512);
-      m1.A2 = s->MSGh; m1.lda2 = 256; m1.ksplit = 256;  // torch.cat([x, message], dim=1)
+      // torch.cat([x, merge(o)], dim=1) through mlp.0, the merge folded into hw1 (upload_weights)
+      sg::GemmHArgs m1 = gh(s->Xh, 256, s->hw1 + (size_t)l * 512 * 512, 512, 512, s->b1m + (size_t)l * 512);
+      m1.A2 = s->Oh; m1.lda2 = 256; m1.ksplit = 256;
       m1.C16 = s->HIDh; m1.ldc16 = 512;
       RSPL_HIP(sg::gemm_h(m1, 2, st));
       sg::GemmHArgs m2 = gh(s->HIDh, 512, s->hw2 + (size_t)l * 512 * 256, 256, 512, s->b2 + (size_t)l * 256);

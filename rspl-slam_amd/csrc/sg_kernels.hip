@@ -9,6 +9,8 @@
 // Layout: token-major.  Token t = (pair*2 + image)*nmax + i; descriptors X[t][256].
 // Q/K/V channels are stored head-contiguous (h*64 + d); the weight rows are
 // permuted once on the host so this equals the reference's d*4 + h interleave.
+#include <cstdlib>
+#include <string>
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
@@ -393,6 +395,97 @@ __global__ __launch_bounds__(256) void gemm_hh_kernel(GemmHArgs a) {
         a.Vt[((size_t)(set * 4 + (c >> 6)) * 64 + (c & 63)) * a.ldv + tok] = (_Float16)v;
       }
     }
+  }
+}
+
+// fp16 GEMM epilogue of one output element (MODE as gemm_hh_kernel)
+template <int MODE>
+__device__ __forceinline__ void gemm_h_store(const GemmHArgs& a, int m, int n, float v) {
+  if constexpr (MODE == 0) {
+    a.C32[(size_t)m * a.ldc32 + n] = v;
+  } else if constexpr (MODE == 1) {
+    a.C16[(size_t)m * a.ldc16 + n] = (_Float16)v;
+  } else if constexpr (MODE == 2) {
+    a.C16[(size_t)m * a.ldc16 + n] = (_Float16)(v > 0.f ? v : 0.f);
+  } else if constexpr (MODE == 3) {
+    float* d = a.C32 + (size_t)m * a.ldc32 + n;
+    const float x = *d + v;
+    *d = x;
+    a.C16[(size_t)m * a.ldc16 + n] = (_Float16)x;
+  } else {
+    if (n < 512) {
+      a.C16[(size_t)m * a.ldc16 + n] = (_Float16)v;
+    } else {
+      const int c = n - 512, set = m / a.nmax, tok = m - set * a.nmax;
+      a.Vt[((size_t)(set * 4 + (c >> 6)) * 64 + (c & 63)) * a.ldv + tok] = (_Float16)v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// fp16 GEMM for the GNN's small-M projections (M = 2B x nmax tokens, K = 256 / 512): one
+// workgroup per 32 x (32 TN) output tile, K split four ways (wave w takes the w-th quarter,
+// K / 64 <= 8 MFMA steps with every load in flight at once: a single memory round trip).
+// Lane (r, h) loads its fragments straight from global memory (16 bytes of row r at
+// k = 16 s + 8 h, the 32x32x16 operand layout); the four partial tiles are summed in wave
+// order through LDS (16 KB) and stored coalesced.  Small LDS / VGPR footprint, so the BA's
+// latency-bound kernels still find room on the CUs while the GNN runs.
+// ---------------------------------------------------------------------------
+constexpr int kRdU = 8;  // max K steps (16 each) per wave: K <= 512
+template <int MODE, int TN>
+__global__ __launch_bounds__(256) void gemm_rk_kernel(GemmHArgs a, int ntn) {
+  __shared__ float red[4][TN * 16][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int tm = blockIdx.x / ntn, tn = blockIdx.x - tm * ntn;
+  const int m0 = 32 * tm, n0 = 32 * TN * tn;
+  const int r = lane & 31, h = lane >> 5;
+  const int m = m0 + r;
+  const bool mok = m < a.M;
+  const int nsw = a.K / 64, k0 = wv * nsw * 16;
+  const _Float16* Ap = a.A + (size_t)(mok ? m : 0) * a.lda + 8 * h;
+  const _Float16* A2p = a.A2 ? a.A2 + (size_t)(mok ? m : 0) * a.lda2 + 8 * h - a.ksplit : nullptr;
+  const _Float16* Bp[TN];
+  bool nok[TN];
+#pragma unroll
+  for (int t = 0; t < TN; t++) {
+    const int n = n0 + 32 * t + r;
+    nok[t] = n < a.N;
+    Bp[t] = a.B + (size_t)(nok[t] ? n : 0) * a.ldb + 8 * h;
+  }
+  half8 av[kRdU], bv[kRdU][TN];
+  const half8 z = {};
+#pragma unroll
+  for (int u = 0; u < kRdU; u++) {
+    const int k = k0 + 16 * u;
+    const bool in = u < nsw;
+    const _Float16* src = (A2p && k >= a.ksplit) ? A2p + k : Ap + k;
+    av[u] = (in && mok) ? *reinterpret_cast<const half8*>(src) : z;
+#pragma unroll
+    for (int t = 0; t < TN; t++) bv[u][t] = (in && nok[t]) ? *reinterpret_cast<const half8*>(Bp[t] + k) : z;
+  }
+  floatx16 acc[TN];
+#pragma unroll
+  for (int t = 0; t < TN; t++)
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[t][i] = 0.f;
+#pragma unroll
+  for (int u = 0; u < kRdU; u++)
+    if (u < nsw)
+#pragma unroll
+      for (int t = 0; t < TN; t++) acc[t] = mfma16(av[u], bv[u][t], acc[t]);
+#pragma unroll
+  for (int t = 0; t < TN; t++)
+#pragma unroll
+    for (int i = 0; i < 16; i++) red[wv][16 * t + i][lane] = acc[t][i];
+  __syncthreads();
+#pragma unroll
+  for (int e = threadIdx.x; e < TN * 16 * 64; e += 256) {
+    const int i16 = e >> 6, ln = e & 63;
+    const float v = (red[0][i16][ln] + red[1][i16][ln]) + (red[2][i16][ln] + red[3][i16][ln]);
+    const int t = i16 >> 4, i = i16 & 15;
+    const int n = n0 + 32 * t + (ln & 31);
+    const int mm = m0 + (i & 3) + 8 * (i >> 2) + 4 * (ln >> 5);
+    if (n < a.N && mm < a.M) gemm_h_store<MODE>(a, mm, n, v + (a.bias ? a.bias[n] : 0.f));
   }
 }
 
@@ -1087,8 +1180,32 @@ static hipError_t gemm_h_launch(const GemmHArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int MODE, int TN>
+static hipError_t gemm_rk_launch(const GemmHArgs& a, hipStream_t s) {
+  const int ntn = (a.N + 32 * TN - 1) / (32 * TN), tiles = (a.M + 31) / 32 * ntn;
+  hipLaunchKernelGGL((gemm_rk_kernel<MODE, TN>), dim3(tiles), dim3(256), 0, s, a, ntn);
+  return hipGetLastError();
+}
+
+// RSPL_SG_GEMM=lds: the LDS-staged 64x64 kernel (timing comparisons); default the K-split one
+static bool gemm_lds() {
+  const char* v = getenv("RSPL_SG_GEMM");
+  return v && std::string(v) == "lds";
+}
+
 hipError_t gemm_h(const GemmHArgs& a, int mode, hipStream_t s) {
   if (a.K > kGhMaxK || a.K % 16 != 0) return hipErrorInvalidValue;
+  static const bool lds = gemm_lds();
+  if (!lds && a.K % 64 == 0 && a.K <= 64 * kRdU && (!a.A2 || a.ksplit % 16 == 0)) {
+    switch (mode) {
+      case 0: return gemm_rk_launch<0, 1>(a, s);
+      case 1: return gemm_rk_launch<1, 1>(a, s);
+      case 2: return gemm_rk_launch<2, 1>(a, s);
+      case 3: return gemm_rk_launch<3, 1>(a, s);
+      case 4: return gemm_rk_launch<4, 1>(a, s);
+    }
+    return hipErrorInvalidValue;
+  }
   switch (mode) {
     case 0: return gemm_h_launch<0>(a, s);
     case 1: return gemm_h_launch<1>(a, s);
