@@ -401,6 +401,12 @@ __device__ __forceinline__ void atomic_max_pos(double* addr, double v) {
   atomicMax(reinterpret_cast<unsigned long long*>(addr), (unsigned long long)__double_as_longlong(v));
 }
 
+// orders this wave's LDS writes before its later LDS reads (lanes exchange through LDS)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // sum over the kGroup lanes of a landmark group (fixed butterfly: deterministic; every
 // lane of the wave takes part)
 constexpr int kGroup = 8;
@@ -438,116 +444,172 @@ __device__ __forceinline__ void lin_point_landmarks(const Problem& P, const Lin&
   if (maxd) atomic_max_pos(S.out + 2, fmax(fabs(hl[0]), fmax(fabs(hl[4]), fabs(hl[8]))));
 }
 
-// line edges: g2o's numeric central difference (delta 1e-9), one wave per edge, the 20
-// perturbed error evaluations (+-delta on 4 line + 6 pose dims) in parallel lanes.  The
-// landmark-side records are written through (sc1); the last edge of a line landmark to
-// finish (ticket) sums them in CSR order into the landmark block.
+// line edges: g2o's numeric central difference (delta 1e-9).  A workgroup takes
+// kLineBlk = 8 edges and splits the 20 perturbed error evaluations of each by kind, so no
+// wave diverges between the two transcendental paths: wave 0 evaluates the +-delta line
+// perturbations of all 8 edges (Line3D::oplus, 8 lanes per edge), waves 1-2 the +-delta pose
+// perturbations (SE3 exp, 12 lanes per edge).  The landmark-side records are written through
+// (sc1); the last edge of a line landmark to finish (ticket) sums them in CSR order into the
+// landmark block.
 // SPEC: the speculative linearisation (at the candidate P.Tn / P.Ln) inside
-// update_errors_kernel.  The wave waits for the
-// group that updates its line landmark (lflag[l] == tag; the groups run in lower-numbered
-// blocks, which are dispatched first) and takes the candidate line and the edge's error from
-// it through coherent loads, so the records are bitwise those of a separate pass.
+// update_errors_kernel.  The block waits for the groups that update its edges' line landmarks
+// (lflag[l] == tag; the groups run in lower-numbered blocks, which are dispatched first),
+// takes the candidate lines from them through coherent loads and evaluates each edge's own
+// error there in wave 3.
 template <bool SPEC>
 __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const Active& A, const Sys& S, int blk,
                                           bool maxd, const unsigned* lflag, unsigned tag,
                                           unsigned long long* stamp = nullptr) {
-  __shared__ double ev[4][20][4];
-  __shared__ double J[4][4 * 6 + 4 * 4];
-  __shared__ double es[4][4];
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i = blk * 4 + wv;
-  const bool on = i < A.n_line_edges;
-  bool live = on;
-  int e = 0, t = 2, rows = 2;
-  bool pose_opt = false;
-  if (on) {
-    e = A.Ea - A.n_line_edges + i;
-    t = P.etype[e];
-    rows = edim(t);
-    pose_opt = A.pidx[P.epose[e]] >= 0;
-    live = !(A.elevel && A.elevel[e]);  // outside this phase: exact-zero records (wave-uniform)
+  __shared__ double ev[kLineBlk][20][4];
+  __shared__ double J[kLineBlk][4 * 6 + 4 * 4];
+  __shared__ double Lsh[kLineBlk][6];
+  __shared__ double es[kLineBlk][4];
+  __shared__ int einfo_s[kLineBlk][4];  // edge id, type, flags (1 on, 2 live, 4 pose optimised), landmark
+  const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
+  const int n_le = A.n_line_edges, e_base = A.Ea - n_le, i0 = blk * kLineBlk;
+  auto edge = [&](int slot, int& e, int& t, bool& on, bool& live) {
+    e = einfo_s[slot][0];
+    t = einfo_s[slot][1];
+    on = einfo_s[slot][2] & 1;
+    live = einfo_s[slot][2] & 2;
+  };
+  // per edge: its attributes and the current (or candidate) line, into LDS
+  if (tid < kLineBlk) {
+    const int i = i0 + tid;
+    const bool on = i < n_le;
+    const int e = on ? e_base + i : 0;
+    const int t = on ? P.etype[e] : 2;
+    const bool live = on && !(A.elevel && A.elevel[e]);  // outside this phase: exact-zero records
+    const bool popt = on && A.pidx[P.epose[e]] >= 0;
+    einfo_s[tid][0] = e;
+    einfo_s[tid][1] = t;
+    einfo_s[tid][2] = (on ? 1 : 0) | (live ? 2 : 0) | (popt ? 4 : 0);
+    einfo_s[tid][3] = on ? P.elm[e] : 0;
+    if (live) {
+      const int l = P.elm[e] - P.nq;
+      if (SPEC) {
+        while (__hip_atomic_load(lflag + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag)
+          __builtin_amdgcn_s_sleep(1);
+        asm volatile("" ::: "memory");
+        for (int k = 0; k < 6; k++) Lsh[tid][k] = __hip_atomic_load(P.Ln + 6 * l + k, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT);
+      } else {
+        for (int k = 0; k < 6; k++) Lsh[tid][k] = P.L[6 * l + k];
+      }
+    }
   }
-  const int pose = live ? P.epose[e] : 0, g = live ? P.elm[e] : P.nq;
-  const double* cam = P.cams + 5 * (live ? P.ecam[e] : 0);
-  const double* obs = P.eobs + 8 * e;
+  __syncthreads();
+  if (stamp && tid == 0) stamp[0] = wall_clock64();
   const double delta = 1e-9, scal = 1.0 / (2 * delta);
-  double lv = 0;  // SPEC: lanes 0-5 the candidate line, lanes 6-9 the edge's error
-  if (SPEC && live) {
-    const int l = g - P.nq;
-    if (lane == 0)
-      while (__hip_atomic_load(lflag + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag) __builtin_amdgcn_s_sleep(1);
-    asm volatile("" ::: "memory");
-    if (stamp && lane == 0 && wv == 0) *stamp = wall_clock64();
-    if (lane < 6) lv = __hip_atomic_load(P.Ln + 6 * l + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    else if (lane < 10) lv = __hip_atomic_load(L.err + 4 * e + lane - 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  double Lc[6];  // SPEC only
-#pragma unroll
-  for (int k = 0; k < 6; k++) Lc[k] = __shfl(lv, k);
-  if (SPEC && lane >= 6 && lane < 10) es[wv][lane - 6] = lv;
-  if (live && lane < 20) {
-    const int d = lane >> 1;
-    const double sgn = (lane & 1) ? -delta : delta;
-    const SE3 T = load_T((SPEC ? P.Tn : P.T) + 8 * pose);
-    double Lp[6];
-    const double* L0 = P.L + 6 * (g - P.nq);
-    for (int k = 0; k < 6; k++) Lp[k] = SPEC ? Lc[k] : L0[k];
-    double er[4] = {0, 0, 0, 0};
-    if (d < 4) {
-      double v[4] = {0, 0, 0, 0};
-      v[d] = sgn;
-      line_oplus(Lp, v);
-      edge_error(t, cam, obs, T, Lp, er);
-    } else {
-      double u[6] = {0, 0, 0, 0, 0, 0};
-      u[d - 4] = sgn;
-      edge_error(t, cam, obs, se3_mul(se3_exp(u), T), Lp, er);
+  {
+    // this thread's evaluation: wave 0 line perturbations, waves 1-2 pose perturbations,
+    // wave 3 (SPEC) the unperturbed error
+    int slot = -1, m = 0;
+    if (wv == 0) {
+      slot = lane >> 3;
+      m = lane & 7;  // ev row 2d + sign, d < 4
+    } else if (wv < 3) {
+      const int idx = (wv - 1) * 64 + lane;
+      if (idx < 12 * kLineBlk) {
+        slot = idx / 12;
+        m = 8 + idx % 12;  // ev row 2d + sign, d = 4..9
+      }
+    } else if (SPEC && lane < kLineBlk) {
+      slot = lane;
+      m = 20;
     }
-    for (int k = 0; k < 4; k++) ev[wv][lane][k] = er[k];
+    int e = 0, t = 2;
+    bool on = false, live = false;
+    if (slot >= 0) edge(slot, e, t, on, live);
+    if (live) {
+      const int d = m >> 1;
+      const double sgn = (m & 1) ? -delta : delta;
+      const SE3 T = load_T((SPEC ? P.Tn : P.T) + 8 * P.epose[e]);
+      const double* cam = P.cams + 5 * P.ecam[e];
+      const double* obs = P.eobs + 8 * e;
+      double Lp[6];
+      for (int k = 0; k < 6; k++) Lp[k] = Lsh[slot][k];
+      double er[4] = {0, 0, 0, 0};
+      if (wv == 0) {
+        double v[4] = {0, 0, 0, 0};
+        v[d] = sgn;
+        line_oplus(Lp, v);
+        edge_error(t, cam, obs, T, Lp, er);
+      } else if (wv < 3) {
+        double u[6] = {0, 0, 0, 0, 0, 0};
+        u[d - 4] = sgn;
+        edge_error(t, cam, obs, se3_mul(se3_exp(u), T), Lp, er);
+      } else {
+        edge_error(t, cam, obs, T, Lp, er);
+      }
+      if (m < 20)
+        for (int k = 0; k < 4; k++) ev[slot][m][k] = er[k];
+      else
+        for (int k = 0; k < 4; k++) es[slot][k] = er[k];
+    }
   }
   __syncthreads();
-  // J layout: Jp [4][6] at 0, Jl [4][4] at 24
-  if (live && lane < 40) {
-    const int r = lane / 10, d = lane % 10;
-    if (r < rows) {
-      const double v = scal * (ev[wv][2 * d][r] - ev[wv][2 * d + 1][r]);
-      if (d < 4) J[wv][24 + r * 4 + d] = v;
-      else J[wv][r * 6 + (d - 4)] = v;
+  if (stamp && tid == 0) stamp[1] = wall_clock64();
+  // J layout per edge: Jp [4][6] at 0, Jl [4][4] at 24
+  for (int idx = tid; idx < 40 * kLineBlk; idx += 256) {
+    const int slot = idx / 40, rd = idx - 40 * slot, r = rd / 10, d = rd % 10;
+    int e, t;
+    bool on, live;
+    edge(slot, e, t, on, live);
+    if (live && r < edim(t)) {
+      const double v = scal * (ev[slot][2 * d][r] - ev[slot][2 * d + 1][r]);
+      if (d < 4) J[slot][24 + r * 4 + d] = v;
+      else J[slot][r * 6 + (d - 4)] = v;
     }
   }
   __syncthreads();
-  if (!on) return;
-  const double* er = SPEC ? &es[wv][0] : L.err + 4 * e;
-  const double w = live ? edge_weight_of(P, A, er, t) : 0.0;
-  for (int o = lane; o < 86; o += 64) {
-    const double v = live ? contrib(o, rows, 4, w, er, &J[wv][0], &J[wv][24]) : 0.0;
+  for (int idx = tid; idx < 86 * kLineBlk; idx += 256) {
+    const int slot = idx / 86, o = idx - 86 * slot;
+    int e, t;
+    bool on, live;
+    edge(slot, e, t, on, live);
+    if (!on) continue;
+    const double* er = SPEC ? &es[slot][0] : L.err + 4 * e;
+    const double w = live ? edge_weight_of(P, A, er, t) : 0.0;
+    const double v = live ? contrib(o, edim(t), 4, w, er, &J[slot][0], &J[slot][24]) : 0.0;
     if (o < 20)
       __hip_atomic_store(o < 16 ? L.Hll + 16 * e + o : L.bl + 4 * e + o - 16, v, __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     else
-      store_contrib(L, e, o, v, pose_opt);
+      store_contrib(L, e, o, v, (einfo_s[slot][2] & 4) != 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int gl = P.elm[e], l = gl - P.nq;
-  const int k0 = A.lm_off[gl], k1 = A.lm_off[gl + 1];
-  unsigned tk = 0;
-  if (lane == 0) tk = __hip_atomic_fetch_add(S.lm_ctr + l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  tk = __shfl(tk, 0);
-  if (tk != (unsigned)(k1 - k0 - 1)) return;
-  if (lane == 0) __hip_atomic_store(S.lm_ctr + l, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  double s = 0;
-  if (lane < 20) {
-    const double* base = lane < 16 ? L.Hll + lane : L.bl + (lane - 16);
-    const int str = lane < 16 ? 16 : 4;
-    for (int k = k0; k < k1; k++)
-      s += __hip_atomic_load(base + (size_t)str * A.lm_edges[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (lane < 16) S.Hll[16 * gl + lane] = s;
-    else S.bl[4 * gl + lane - 16] = s;
-  }
-  double m = (lane < 16 && lane % 5 == 0) ? fabs(s) : 0.0;
+  __syncthreads();
+  // per edge (32 lanes each): landmark ticket; the last edge of its landmark sums the records
+  {
+    const int slot = 2 * wv + (lane >> 5), ln = lane & 31;
+    int e, t;
+    bool on, live;
+    edge(slot, e, t, on, live);
+    if (on) {
+      const int gl = einfo_s[slot][3], l = gl - P.nq;
+      const int k0 = A.lm_off[gl], k1 = A.lm_off[gl + 1];
+      unsigned tk = 0;
+      if (ln == 0) tk = __hip_atomic_fetch_add(S.lm_ctr + l, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      tk = __shfl(tk, lane & 32);
+      if (tk == (unsigned)(k1 - k0 - 1)) {
+        if (ln == 0) __hip_atomic_store(S.lm_ctr + l, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        double sm = 0;
+        if (ln < 20) {
+          const double* base = ln < 16 ? L.Hll + ln : L.bl + (ln - 16);
+          const int str = ln < 16 ? 16 : 4;
+          for (int k = k0; k < k1; k++)
+            sm += __hip_atomic_load(base + (size_t)str * A.lm_edges[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          if (ln < 16) S.Hll[16 * gl + ln] = sm;
+          else S.bl[4 * gl + ln - 16] = sm;
+        }
+        double mx = (ln < 16 && ln % 5 == 0) ? fabs(sm) : 0.0;
 #pragma unroll
-  for (int o = 8; o >= 1; o >>= 1) m = fmax(m, __shfl_xor(m, o));
-  if (maxd && lane == 0 && A.lm_act[gl]) atomic_max_pos(S.out + 2, m);
+        for (int o = 8; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+        if (maxd && ln == 0 && A.lm_act[gl]) atomic_max_pos(S.out + 2, mx);
+      }
+    }
+  }
 }
 
 // one launch for both landmark families: blocks [0, nbq) point landmarks (kGroup lanes
@@ -1306,7 +1368,7 @@ __global__ __launch_bounds__(256) void update_kernel(Problem P, Lin L, Active A,
 // (records into the spare set Ls / Ss).  Blocks [0, nbu) are the landmark groups: besides the
 // update and the errors, a point group linearises its landmark's edges at the candidate
 // (each lane re-reading only the errors it wrote itself) and a line group publishes the
-// candidate line and its edges' errors (coherent stores, then lflag[l] = tag).  Blocks
+// candidate line as soon as it has it (coherent stores, then lflag[l] = tag).  Blocks
 // [nbu, ...) are line-edge waves (lin_lines<true>).  The mailbox ticket counts only the
 // group blocks, so the host decides while the line waves still run.
 template <bool SPEC>
@@ -1387,6 +1449,10 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
           if (SPEC) __hip_atomic_store(P.Ln + 6 * l + q, lm[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           else P.Ln[6 * l + q] = lm[q];
         }
+      if (SPEC) {  // the candidate line is out: release its line-edge waves
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (j == 0) __hip_atomic_store(lflag + l, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     for (int k = k0 + j; k < k1; k += kGroup) {
       const int e = A.lm_edges[k];
@@ -1399,10 +1465,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
       for (int q = 0; q < edim(te); q++) chi2 += er[q] * er[q];
       chi2 *= einfo(te);
 #pragma unroll
-      for (int q = 0; q < 4; q++) {
-        if (SPEC && !point) __hip_atomic_store(L.err + 4 * e + q, er[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        else L.err[4 * e + q] = er[q];
-      }
+      for (int q = 0; q < 4; q++) L.err[4 * e + q] = er[q];
       double cst = chi2;
       if (A.robust) {
         double r1;
@@ -1410,10 +1473,6 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
       }
       L.rho0[e] = cst;
       chi += cst;
-    }
-    if (SPEC && !point) {  // the line and its edges' errors are out: release the line-edge waves
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (j == 0) __hip_atomic_store(lflag + (g - P.nq), tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
   if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 1);
@@ -1646,7 +1705,7 @@ int update_errors_blocks(const Active& A) { return A.nL > 0 ? (A.nL * kGroup + 2
 
 hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool with_maxdiag,
                      hipStream_t s) {
-  const int nbq = (P.nq * kGroup + 255) / 256, nbl = (A.n_line_edges + 3) / 4;
+  const int nbq = (P.nq * kGroup + 255) / 256, nbl = (A.n_line_edges + kLineBlk - 1) / kLineBlk;
   if (nbq + nbl > 0)
     hipLaunchKernelGGL(linearize_kernel, dim3(nbq + nbl), dim3(256), 0, s, P, L, A, S, nbq, with_maxdiag ? 1 : 0);
   if (with_maxdiag && A.K > 0 && A.Ea > 0)
@@ -1683,7 +1742,7 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
     hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
     const int nbu = update_errors_blocks(A);
     if (spec) {
-      const int nbl = (A.n_line_edges + 3) / 4;
+      const int nbl = (A.n_line_edges + kLineBlk - 1) / kLineBlk;
       hipLaunchKernelGGL(update_errors_kernel<true>, dim3(nbu + nbl), dim3(256), 0, s, P, L, A, S, lambda, seq,
                          spec->Ls, spec->Ss, nbu, spec->lflag, spec->tag);
       *fused = true;

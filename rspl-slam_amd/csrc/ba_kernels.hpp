@@ -91,6 +91,7 @@ struct Sys {
 constexpr int kProfPc = 16, kProfUe = kProfPc + 4 * 4096, kProfLen = kProfUe + 4 * 4096;
 
 constexpr int kLmChunk = 256;  // landmarks per Schur chunk (4 per lane)
+constexpr int kLineBlk = 8;    // line edges per linearisation workgroup
 
 // errors (+ fused final reduction and mailbox post with sequence number seq)
 hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq,
