@@ -93,7 +93,8 @@ inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // per-call upload layout (staging call region == device call buffer)
 struct CallLayout {
-  size_t cams, T, X, L, obs, type, pose, lm, cam, gmap, pidx, lm_off, lm_act, pairs, level, fill, flags, out, bytes;
+  size_t cams, T, X, L, obs, type, pose, lm, cam, gmap, pidx, lm_off, lm_act, pairs, ltab, level, fill, flags, out,
+      bytes;
   CallLayout(int ncam, int np, int nq, int nl, int E) {
     const size_t nL = (size_t)nq + nl;
     size_t so = 0;
@@ -107,6 +108,7 @@ struct CallLayout {
     pose = place(4 * (size_t)E); lm = place(4 * (size_t)E); cam = place(4 * (size_t)E); gmap = place(4 * (size_t)E);
     pidx = place(4 * (size_t)np); lm_off = place(4 * (nL + 1)); lm_act = place(nL);
     pairs = place(8 * (size_t)np * (np + 1) / 2);
+    ltab = place(16 * ((size_t)E + nl + 1));
     level = place(E); fill = place(4 * nL); flags = place(4 * sizeof(int)); out = place(8 * sizeof(double));  // zeros
     bytes = so;
   }
@@ -325,7 +327,7 @@ int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Acti
         if (traced) {
           S.prof = sp.Ss.prof = b->prof;
           b->prof_nb[0] = A.npairs * A.nchk;
-          b->prof_nb[1] = ba::update_errors_blocks(A) + (A.n_line_edges + ba::kLineBlk - 1) / ba::kLineBlk;
+          b->prof_nb[1] = ba::update_errors_blocks(A) + A.n_lblk;
           b->prof_nb[2] = ba::update_errors_blocks(A);
         }
         RSPL_HIP(ba::trial(P, Lr, A, S, lambda, q, st, it + 1 < iters ? &sp : nullptr, &fused));
@@ -587,6 +589,36 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
     RSPL_HIP(hipMalloc((void**)&b->pp_buf, sizeof(int4) * cap));
     b->pp_cap = cap;
   }
+  // line workgroups: consecutive line landmarks packed whole into <= kLineBlk edges (and <=
+  // kLineBlk landmarks), so a workgroup sums their blocks itself; a landmark with more edges
+  // gets workgroups of its own, flagged split (per-edge records + last-edge ticket)
+  int4* ltab = reinterpret_cast<int4*>(sg + cl.ltab);
+  int n_lblk = 0;
+  {
+    constexpr int kB = ba::kLineBlk;
+    int p0 = 0, cnt = 0, gb = -1, ge = 0;
+    auto flush = [&]() {
+      if (gb >= 0 && cnt > 0) ltab[n_lblk++] = make_int4(p0, cnt, gb, ge);
+      gb = -1;
+      cnt = 0;
+    };
+    for (int g = nq; g < nL; g++) {
+      const int k = lm_off[g + 1] - lm_off[g];
+      if (k > kB) {
+        flush();
+        for (int o = 0; o < k; o += kB) ltab[n_lblk++] = make_int4(lm_off[g] + o, std::min(kB, k - o) | (1 << 8), g, g + 1);
+        continue;
+      }
+      if (gb >= 0 && (cnt + k > kB || g - gb >= kB)) flush();
+      if (gb < 0) {
+        p0 = lm_off[g];
+        gb = g;
+      }
+      cnt += k;
+      ge = g + 1;
+    }
+    flush();
+  }
   int* pidx = reinterpret_cast<int*>(sg + cl.pidx);
   int K = 0;
   for (int p = 0; p < np; p++) pidx[p] = (b->pact[p] && !pr->pose_fixed[p]) ? K++ : -1;
@@ -648,6 +680,8 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   A.npairs = K * (K + 1) / 2;
   A.nchk = std::max((nL + ba::kLmChunk - 1) / ba::kLmChunk, 1);
   A.n_line_edges = n_line_local;
+  A.ltab = reinterpret_cast<const int4*>(cb + cl.ltab);
+  A.n_lblk = n_lblk;
   A.K = K;
   A.nL = nL;
   A.robust = 1;

@@ -444,13 +444,15 @@ __device__ __forceinline__ void lin_point_landmarks(const Problem& P, const Lin&
   if (maxd) atomic_max_pos(S.out + 2, fmax(fabs(hl[0]), fmax(fabs(hl[4]), fabs(hl[8]))));
 }
 
-// line edges: g2o's numeric central difference (delta 1e-9).  A workgroup takes
-// kLineBlk = 8 edges and splits the 20 perturbed error evaluations of each by kind, so no
+// line edges: g2o's numeric central difference (delta 1e-9).  A workgroup takes the
+// <= kLineBlk = 8 edges of a run of whole line landmarks (A.ltab, CSR order) and splits the 20
+// perturbed error evaluations of each by kind, so no
 // wave diverges between the two transcendental paths: wave 0 evaluates the +-delta line
 // perturbations of all 8 edges (Line3D::oplus, 8 lanes per edge), waves 1-2 the +-delta pose
-// perturbations (SE3 exp, 12 lanes per edge).  The landmark-side records are written through
-// (sc1); the last edge of a line landmark to finish (ticket) sums them in CSR order into the
-// landmark block.
+// perturbations (SE3 exp, 12 lanes per edge).  The workgroup sums each landmark's edge
+// records in CSR order into the landmark block itself; only a landmark with more than
+// kLineBlk edges (split over workgroups) goes through per-edge records written through (sc1)
+// and a last-edge ticket.
 // SPEC: the speculative linearisation (at the candidate P.Tn / P.Ln) inside
 // update_errors_kernel.  The block waits for the groups that update its edges' line landmarks
 // (lflag[l] == tag; the groups run in lower-numbered blocks, which are dispatched first),
@@ -465,8 +467,11 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
   __shared__ double Lsh[kLineBlk][6];
   __shared__ double es[kLineBlk][4];
   __shared__ int einfo_s[kLineBlk][4];  // edge id, type, flags (1 on, 2 live, 4 pose optimised), landmark
+  __shared__ double cv[kLineBlk][20];   // landmark-side records (Hll 16, bl 4) of each edge
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
-  const int n_le = A.n_line_edges, e_base = A.Ea - n_le, i0 = blk * kLineBlk;
+  const int4 tb = A.ltab[blk];
+  const int p0 = tb.x, cnt = tb.y & 0xff, gb = tb.z, ge = tb.w;
+  const bool split = (tb.y >> 8) != 0;
   auto edge = [&](int slot, int& e, int& t, bool& on, bool& live) {
     e = einfo_s[slot][0];
     t = einfo_s[slot][1];
@@ -475,16 +480,15 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
   };
   // per edge: its attributes and the current (or candidate) line, into LDS
   if (tid < kLineBlk) {
-    const int i = i0 + tid;
-    const bool on = i < n_le;
-    const int e = on ? e_base + i : 0;
+    const bool on = tid < cnt;
+    const int e = on ? A.lm_edges[p0 + tid] : 0;
     const int t = on ? P.etype[e] : 2;
     const bool live = on && !(A.elevel && A.elevel[e]);  // outside this phase: exact-zero records
     const bool popt = on && A.pidx[P.epose[e]] >= 0;
     einfo_s[tid][0] = e;
     einfo_s[tid][1] = t;
     einfo_s[tid][2] = (on ? 1 : 0) | (live ? 2 : 0) | (popt ? 4 : 0);
-    einfo_s[tid][3] = on ? P.elm[e] : 0;
+    einfo_s[tid][3] = on ? P.elm[e] : gb;
     if (live) {
       const int l = P.elm[e] - P.nq;
       if (SPEC) {
@@ -572,15 +576,41 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
     const double* er = SPEC ? &es[slot][0] : L.err + 4 * e;
     const double w = live ? edge_weight_of(P, A, er, t) : 0.0;
     const double v = live ? contrib(o, edim(t), 4, w, er, &J[slot][0], &J[slot][24]) : 0.0;
-    if (o < 20)
-      __hip_atomic_store(o < 16 ? L.Hll + 16 * e + o : L.bl + 4 * e + o - 16, v, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    else
+    if (o < 20) {
+      cv[slot][o] = v;
+      if (split)
+        __hip_atomic_store(o < 16 ? L.Hll + 16 * e + o : L.bl + 4 * e + o - 16, v, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    } else {
       store_contrib(L, e, o, v, (einfo_s[slot][2] & 4) != 0);
+    }
+  }
+  if (!split) {  // whole landmarks: their blocks from this workgroup's records, CSR (slot) order
+    __syncthreads();
+    if (tid < 20 * (ge - gb)) {
+      const int g = gb + tid / 20, o = tid % 20;
+      const int s0 = A.lm_off[g] - p0, s1 = A.lm_off[g + 1] - p0;
+      if (s1 > s0) {
+        double sm = 0;
+        for (int q = s0; q < s1; q++) sm += cv[q][o];
+        if (o < 16) S.Hll[16 * g + o] = sm;
+        else S.bl[4 * g + o - 16] = sm;
+        if (maxd && o == 0 && A.lm_act[g]) {  // max |diagonal| of the block, as the ticket path
+          double mx = 0;
+          for (int dgi = 0; dgi < 16; dgi += 5) {
+            double sd = 0;
+            for (int q = s0; q < s1; q++) sd += cv[q][dgi];
+            mx = fmax(mx, fabs(sd));
+          }
+          atomic_max_pos(S.out + 2, mx);
+        }
+      }
+    }
+    return;
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  // per edge (32 lanes each): landmark ticket; the last edge of its landmark sums the records
+  // split landmark, per edge (32 lanes each): ticket; the last edge sums the landmark's records
   {
     const int slot = 2 * wv + (lane >> 5), ln = lane & 31;
     int e, t;
@@ -1705,7 +1735,7 @@ int update_errors_blocks(const Active& A) { return A.nL > 0 ? (A.nL * kGroup + 2
 
 hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool with_maxdiag,
                      hipStream_t s) {
-  const int nbq = (P.nq * kGroup + 255) / 256, nbl = (A.n_line_edges + kLineBlk - 1) / kLineBlk;
+  const int nbq = (P.nq * kGroup + 255) / 256, nbl = A.n_lblk;
   if (nbq + nbl > 0)
     hipLaunchKernelGGL(linearize_kernel, dim3(nbq + nbl), dim3(256), 0, s, P, L, A, S, nbq, with_maxdiag ? 1 : 0);
   if (with_maxdiag && A.K > 0 && A.Ea > 0)
@@ -1742,7 +1772,7 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
     hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
     const int nbu = update_errors_blocks(A);
     if (spec) {
-      const int nbl = (A.n_line_edges + kLineBlk - 1) / kLineBlk;
+      const int nbl = A.n_lblk;
       hipLaunchKernelGGL(update_errors_kernel<true>, dim3(nbu + nbl), dim3(256), 0, s, P, L, A, S, lambda, seq,
                          spec->Ls, spec->Ss, nbu, spec->lflag, spec->tag);
       *fused = true;

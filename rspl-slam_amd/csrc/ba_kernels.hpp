@@ -50,6 +50,9 @@ struct Active {          // active structure of one optimize() phase
   const int4* pp;        // edge pairs {e1 of pose a, e2 of pose b, their landmark, 0}, chunk-major,
                          //   landmark order within a chunk
   int n_line_edges;      // line edges are [Ea - n_line_edges, Ea)
+  const int4* ltab;      // [n_lblk] line workgroups {first CSR position, edges | split << 8, first
+  int n_lblk;            //   landmark, end landmark}: whole line landmarks of <= kLineBlk edges
+                         //   (summed in the workgroup), or one slice of a larger landmark (split)
   const uint8_t* elevel; // [E] or null: edge level (!= 0: outside this phase -- level 1 in the
                          // second optimize): zero linearisation records, no cost, error kept
   int K, nL;
