@@ -923,7 +923,14 @@ __device__ __forceinline__ void prof_stamp(const Sys& S, int slot) {
 
 __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active A, Sys S, double lambda) {
   __shared__ double red[64 * 49];
-  const int c = blockIdx.x, lane = threadIdx.x;
+  // XCD-aware chunk order: workgroups go round-robin over the 8 XCDs (blockIdx % 8), so
+  // landmark range lb runs on XCD lb % 8 for every pose pair -- each XCD's L2 then holds only
+  // its ranges' records (~1/8 of them), which its ~k_g pose pairs per landmark re-read
+  const int lane = threadIdx.x;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, rpx = (A.nchk + 7) >> 3;
+  const int lb = (slot % rpx) * 8 + xcd, pr0 = slot / rpx;
+  if (lb >= A.nchk || pr0 >= A.npairs) return;
+  const int c = pr0 * A.nchk + lb;
   if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c);
   const int pr = c / A.nchk;
   const int beg = A.pp_off[c], end = A.pp_off[c + 1];
@@ -1760,11 +1767,14 @@ hipError_t ensure_schur_attr() {
   return e;
 }
 
+// pair_chunk grid: 8 XCD lanes x (landmark ranges per XCD) x pose pairs (idle slots exit)
+static int pair_chunk_blocks(const Active& A) { return 8 * ((A.nchk + 7) / 8) * A.npairs; }
+
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
                  hipStream_t s, const Spec* spec, bool* fused) {
   *fused = false;
   if (A.npairs * A.nchk > 0)
-    hipLaunchKernelGGL(pair_chunk_kernel, dim3(A.npairs * A.nchk), dim3(64), 0, s, P, L, A, S, lambda);
+    hipLaunchKernelGGL(pair_chunk_kernel, dim3(pair_chunk_blocks(A)), dim3(64), 0, s, P, L, A, S, lambda);
   const int n = 6 * A.K;
   if (fast_path(A.K)) {
     hipError_t e = ensure_schur_attr();
@@ -1831,7 +1841,7 @@ hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8
 
 hipError_t trial_chunks(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, hipStream_t s) {
   if (A.npairs * A.nchk > 0)
-    hipLaunchKernelGGL(pair_chunk_kernel, dim3(A.npairs * A.nchk), dim3(64), 0, s, P, L, A, S, lambda);
+    hipLaunchKernelGGL(pair_chunk_kernel, dim3(pair_chunk_blocks(A)), dim3(64), 0, s, P, L, A, S, lambda);
   hipLaunchKernelGGL(shard_fail_stage_kernel, dim3(1), dim3(1), 0, s, S, S.pairfin + (size_t)A.npairs * 48);
   return hipGetLastError();
 }
