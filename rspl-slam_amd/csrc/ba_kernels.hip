@@ -841,6 +841,7 @@ __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, c
       k1 = A.lm_off[g + 1];
     }
     int cnt = 0;
+    unsigned ma1 = 0, mb1 = 0;  // the masks when the landmark has <= 8 edges (one block each)
     for (int ib = k0; ib < k1; ib += 8) {  // i blocks
       unsigned ma = 0;
       int pi[8];
@@ -857,6 +858,8 @@ __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, c
 #pragma unroll
         for (int u = 0; u < 8; u++) mb |= (jb + u < k1 && pj[u] == pb) ? 1u << u : 0u;
         cnt += __popc(ma) * __popc(mb);
+        ma1 = ma;
+        mb1 = mb;
       }
     }
     // wave exclusive prefix of the per-lane counts (lane order)
@@ -867,7 +870,13 @@ __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, c
       if (lane >= o) pre += t;
     }
     const int total = __shfl(pre, 63);
-    if (FILL && cnt) {
+    if (FILL && cnt && k1 - k0 <= 8) {  // emit from the masks: i ascending, then j ascending
+      int q = base + pre - cnt;
+      for (unsigned ma = ma1; ma; ma &= ma - 1) {
+        const int e1 = A.lm_edges[k0 + __ffs(ma) - 1];
+        for (unsigned mb = mb1; mb; mb &= mb - 1) pp[q++] = make_int4(e1, A.lm_edges[k0 + __ffs(mb) - 1], g, 0);
+      }
+    } else if (FILL && cnt) {
       int q = base + pre - cnt;
       for (int ib = k0; ib < k1; ib++) {
         if (A.lm_pose[ib] != pa) continue;
