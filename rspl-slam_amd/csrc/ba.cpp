@@ -95,7 +95,7 @@ inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 struct CallLayout {
   size_t cams, T, X, L, obs, type, pose, lm, cam, gmap, pidx, lm_off, lm_act, pairs, ltab, level, fill, flags, out,
       bytes;
-  CallLayout(int ncam, int np, int nq, int nl, int E) {
+  CallLayout(int ncam, int np, int nq, int nl, int E, size_t nobs) {  // nobs: packed observation doubles
     const size_t nL = (size_t)nq + nl;
     size_t so = 0;
     auto place = [&](size_t n) {
@@ -104,7 +104,7 @@ struct CallLayout {
       return o;
     };
     cams = place(sizeof(double) * 5 * ncam); T = place(sizeof(double) * 8 * np); X = place(sizeof(double) * 3 * nq);
-    L = place(sizeof(double) * 6 * nl); obs = place(sizeof(double) * 8 * (size_t)E); type = place(E);
+    L = place(sizeof(double) * 6 * nl); obs = place(sizeof(double) * nobs); type = place(E);
     pose = place(4 * (size_t)E); lm = place(4 * (size_t)E); cam = place(4 * (size_t)E); gmap = place(4 * (size_t)E);
     pidx = place(4 * (size_t)np); lm_off = place(4 * (nL + 1)); lm_act = place(nL);
     pairs = place(8 * (size_t)np * (np + 1) / 2);
@@ -403,7 +403,7 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
   if (hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
       hipHostMalloc((void**)&b->mail, sizeof(ba::Mail), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&b->mail_dev, b->mail, 0) != hipSuccess ||
-      hipMalloc((void**)&b->cbuf, CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE).bytes) !=
+      hipMalloc((void**)&b->cbuf, CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE, 8 * (size_t)b->maxE).bytes) !=
           hipSuccess ||
       hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
       hipMemset(b->lflag, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
@@ -514,7 +514,12 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   };
   mark();
   // ---- one staging region for the whole call, mirrored by the device call buffer ----
-  const CallLayout cl(pr->n_cameras, np, nq, nl, E);
+  size_t nobs = 0;  // packed observation doubles (all edges: an upper bound when sharded)
+  {
+    const int odt[4] = {2, 3, 4, 8};
+    for (int t = 0; t < 4; t++) nobs += (size_t)odt[t] * ne[t];
+  }
+  const CallLayout cl(pr->n_cameras, np, nq, nl, E, nobs);
   const DownLayout dl(np, nq, nl, Eg);  // inlier flags by global edge id
   int rc;
   if ((rc = ensure_stage(b, std::max(cl.bytes, dl.bytes)))) return rc;
@@ -552,26 +557,51 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   b->pact.assign(np, 0);
   int* gmap = reinterpret_cast<int*>(sg + cl.gmap);
   int e = 0, eg = 0;
+  size_t opos = 0;
+  int lstart[5], obase[4];
   for (int t = 0; t < 4; t++) {
     RSPL_CHECK_ARG(ne[t] == 0 || (poses[t] && lms[t] && obs[t]), "NULL edge arrays");
-    for (int i = 0; i < ne[t]; i++, eg++) {
-      const int p = poses[t][i], l = lms[t][i], c = cams[t] ? cams[t][i] : 0;
-      RSPL_CHECK_ARG(p >= 0 && p < np && l >= 0 && l < (t < 2 ? nq : nl) && c >= 0 && c < pr->n_cameras,
+    lstart[t] = e;
+    obase[t] = (int)opos;
+    const int n = ne[t], lmax = t < 2 ? nq : nl, loff = t < 2 ? 0 : nq;
+    const int32_t *pt = poses[t], *lt = lms[t], *ct = cams[t];
+    if (!sh) {  // every edge is local: bulk copies, one validation pass
+      for (int i = 0; i < n; i++) {
+        const int p = pt[i], l = lt[i], c = ct ? ct[i] : 0;
+        RSPL_CHECK_ARG(p >= 0 && p < np && l >= 0 && l < lmax && c >= 0 && c < pr->n_cameras,
+                       "edge %d of type %d references a missing vertex/camera", i, t);
+        b->pact[p] = 1;
+        elm[e + i] = loff + l;
+        lm_off[loff + l + 1]++;
+      }
+      memset(etype + e, t, n);
+      memcpy(epose + e, pt, sizeof(int) * n);
+      if (ct) memcpy(ecam + e, ct, sizeof(int) * n);
+      else memset(ecam + e, 0, sizeof(int) * n);
+      memcpy(eobs + opos, obs[t], sizeof(double) * od[t] * n);
+      opos += (size_t)od[t] * n;
+      e += n;
+      eg += n;
+      continue;
+    }
+    for (int i = 0; i < n; i++, eg++) {
+      const int p = pt[i], l = lt[i], c = ct ? ct[i] : 0;
+      RSPL_CHECK_ARG(p >= 0 && p < np && l >= 0 && l < lmax && c >= 0 && c < pr->n_cameras,
                      "edge %d of type %d references a missing vertex/camera", i, t);
       b->pact[p] = 1;  // a pose is optimised when it has an edge on ANY rank: K agrees across ranks
       if (!owned(t, i)) continue;
       etype[e] = (int8_t)t;
       epose[e] = p;
-      elm[e] = t < 2 ? l : nq + l;
+      elm[e] = loff + l;
       ecam[e] = c;
-      gmap[e] = eg;
+      gmap[e] = eg;  // global edge id (sharded runs only)
       lm_off[elm[e] + 1]++;
-      double* o = eobs + 8 * (size_t)e;
-      const double* src = obs[t] + (size_t)od[t] * i;
-      for (int k = 0; k < 8; k++) o[k] = k < od[t] ? src[k] : 0.0;
+      memcpy(eobs + opos, obs[t] + (size_t)od[t] * i, sizeof(double) * od[t]);
+      opos += od[t];
       e++;
     }
   }
+  lstart[4] = e;
   uint8_t* lm_act = reinterpret_cast<uint8_t*>(sg + cl.lm_act);
   size_t pair_bound = 0;  // sum_g k_g^2 >= edge pairs of any pose pair
   for (int g = 0; g < nL; g++) {
@@ -647,6 +677,11 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   P.elm = reinterpret_cast<const int*>(cb + cl.lm);
   P.ecam = reinterpret_cast<const int*>(cb + cl.cam);
   P.eobs = reinterpret_cast<const double*>(cb + cl.obs);
+  for (int t = 0; t < 4; t++) {
+    P.lstart[t] = lstart[t];
+    P.obase[t] = obase[t];
+  }
+  P.lstart[4] = lstart[4];
   const double th[4] = {pr->th_mono_point, pr->th_stereo_point, pr->th_mono_line, pr->th_stereo_line};
   for (int t = 0; t < 4; t++) {
     P.th[t] = th[t];

@@ -110,6 +110,12 @@ __device__ void edge_error(int type, const double* cam, const double* obs, const
 }
 
 __device__ __forceinline__ int edim(int t) { return t == 0 ? 2 : t == 1 ? 3 : t == 2 ? 2 : 4; }
+
+// edge e's observation (type t): packed per type
+__device__ __forceinline__ const double* obs_of(const Problem& P, int e, int t) {
+  const int od = t == 0 ? 2 : t == 1 ? 3 : t == 2 ? 4 : 8;
+  return P.eobs + P.obase[t] + od * (e - P.lstart[t]);
+}
 __device__ __forceinline__ int ldim(int t) { return t < 2 ? 3 : 4; }
 __device__ __forceinline__ double einfo(int t) { return t < 2 ? 1.0 : 0.1; }
 
@@ -181,7 +187,7 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
     const int t = P.etype[e];
     const SE3 T = load_T(P.T + 8 * P.epose[e]);
     double er[4] = {0, 0, 0, 0};
-    edge_error(t, P.cams + 5 * P.ecam[e], P.eobs + 8 * e, T, lm_ptr(P, P.elm[e]), er);
+    edge_error(t, P.cams + 5 * P.ecam[e], obs_of(P, e, t), T, lm_ptr(P, P.elm[e]), er);
     double chi2 = 0;
     for (int k = 0; k < edim(t); k++) chi2 += er[k] * er[k];
     chi2 *= einfo(t);
@@ -530,7 +536,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
       const double sgn = (m & 1) ? -delta : delta;
       const SE3 T = load_T((SPEC ? P.Tn : P.T) + 8 * P.epose[e]);
       const double* cam = P.cams + 5 * P.ecam[e];
-      const double* obs = P.eobs + 8 * e;
+      const double* obs = obs_of(P, e, t);
       double Lp[6];
       for (int k = 0; k < 6; k++) Lp[k] = Lsh[slot][k];
       double er[4] = {0, 0, 0, 0};
@@ -1506,7 +1512,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
       const int te = P.etype[e];
       const SE3 T = load_T(P.Tn + 8 * P.epose[e]);
       double er[4] = {0, 0, 0, 0};
-      edge_error(te, P.cams + 5 * P.ecam[e], P.eobs + 8 * e, T, lm, er);
+      edge_error(te, P.cams + 5 * P.ecam[e], obs_of(P, e, te), T, lm, er);
       double chi2 = 0;
       for (int q = 0; q < edim(te); q++) chi2 += er[q] * er[q];
       chi2 *= einfo(te);

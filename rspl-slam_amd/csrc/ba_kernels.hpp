@@ -7,7 +7,8 @@ namespace rspl {
 namespace ba {
 
 // Edge types (same order as rspl_ba_problem): 0 mono point, 1 stereo point,
-// 2 mono line, 3 stereo line.  Unified edge arrays, obs padded to 8 doubles.
+// 2 mono line, 3 stereo line.  Unified edge arrays in type order; observations packed per type
+// (2 / 3 / 4 / 8 doubles per edge): edge e of type t at eobs + obase[t] + od(t) (e - lstart[t]).
 struct Problem {
   const double* cams;    // [nc][5] fx fy cx cy bf
   double* T;             // [np][8] T_cw: q (w x y z), t (x y z), pad   (current state)
@@ -21,7 +22,9 @@ struct Problem {
   const int* epose;      // [E]
   const int* elm;        // [E] landmark index: point id, or nq + line id
   const int* ecam;       // [E]
-  const double* eobs;    // [E][8]
+  const double* eobs;    // packed observations (see above)
+  int lstart[5];         // first edge of each type (lstart[4] = E)
+  int obase[4];          // offset of each type's observations in eobs
   double delta[4];       // Huber deltas per type
   double th[4];          // chi2 thresholds per type
 };
