@@ -115,12 +115,12 @@ class RsplBaProblem(C.Structure):
     ]
 
 
-class RsplBaResult(C.Structure):
+class RsplBaResult(C.Structure):  # output pointers as plain addresses (set from one result buffer)
     _fields_ = [
-        ("pose_q", C.POINTER(C.c_double)), ("pose_p", C.POINTER(C.c_double)),
-        ("points", C.POINTER(C.c_double)), ("lines", C.POINTER(C.c_double)),
-        ("mono_inlier", C.POINTER(C.c_uint8)), ("stereo_inlier", C.POINTER(C.c_uint8)),
-        ("mono_line_inlier", C.POINTER(C.c_uint8)), ("stereo_line_inlier", C.POINTER(C.c_uint8)),
+        ("pose_q", C.c_void_p), ("pose_p", C.c_void_p),
+        ("points", C.c_void_p), ("lines", C.c_void_p),
+        ("mono_inlier", C.c_void_p), ("stereo_inlier", C.c_void_p),
+        ("mono_line_inlier", C.c_void_p), ("stereo_line_inlier", C.c_void_p),
         ("chi2_first", C.c_double), ("chi2_second", C.c_double),
         ("iterations_done_first", C.c_int), ("iterations_done_second", C.c_int),
     ]
@@ -168,26 +168,40 @@ class DenseProblem:
     def n_edges(self, name):
         return int(getattr(self, name)["pose"].shape[0])
 
+    _EDGE_SETS = (("mono", "mono", "point"), ("stereo", "stereo", "point"),
+                  ("mono_line", "mono_line", "line"), ("stereo_line", "stereo_line", "line"))
+
+    def _arrays(self):
+        return (self.cameras, self.pose_q, self.pose_p, self.pose_fixed, self.points, self.lines) + tuple(
+            getattr(self, name)[k] for name, _, _ in self._EDGE_SETS for k in ("pose", "lm", "cam", "obs"))
+
     def to_ctypes(self) -> RsplBaProblem:
-        P = RsplBaProblem()
+        # the pointer struct is rebuilt only when an array object changed (the cache holds the
+        # arrays it points into, so they stay alive); counts and scalars are set on every call
+        arrays = self._arrays()
+        cache = self.__dict__.get("_ct_cache")
+        if cache is None or any(a is not b for a, b in zip(cache[0], arrays)):
+            P = RsplBaProblem()
+            P.cameras = _ptr(self.cameras, C.c_double)
+            P.pose_q = _ptr(self.pose_q, C.c_double)
+            P.pose_p = _ptr(self.pose_p, C.c_double)
+            P.pose_fixed = _ptr(self.pose_fixed, C.c_uint8)
+            P.points = _ptr(self.points, C.c_double)
+            P.lines = _ptr(self.lines, C.c_double)
+            for name, pre, lmname in self._EDGE_SETS:
+                d = getattr(self, name)
+                setattr(P, f"{pre}_pose", _ptr(d["pose"], C.c_int32))
+                setattr(P, f"{pre}_{lmname}", _ptr(d["lm"], C.c_int32))
+                setattr(P, f"{pre}_camera", _ptr(d["cam"], C.c_int32))
+                setattr(P, f"{pre}_obs", _ptr(d["obs"], C.c_double))
+            self.__dict__["_ct_cache"] = cache = (arrays, P)
+        P = cache[1]
         P.n_cameras = self.cameras.shape[0]
-        P.cameras = _ptr(self.cameras, C.c_double)
         P.n_poses = self.pose_q.shape[0]
-        P.pose_q = _ptr(self.pose_q, C.c_double)
-        P.pose_p = _ptr(self.pose_p, C.c_double)
-        P.pose_fixed = _ptr(self.pose_fixed, C.c_uint8)
         P.n_points = self.points.shape[0]
-        P.points = _ptr(self.points, C.c_double)
         P.n_lines = self.lines.shape[0]
-        P.lines = _ptr(self.lines, C.c_double)
-        for name, pre, lmname in (("mono", "mono", "point"), ("stereo", "stereo", "point"),
-                                  ("mono_line", "mono_line", "line"), ("stereo_line", "stereo_line", "line")):
-            d = getattr(self, name)
-            setattr(P, f"n_{pre}", d["pose"].shape[0])
-            setattr(P, f"{pre}_pose", _ptr(d["pose"], C.c_int32))
-            setattr(P, f"{pre}_{lmname}", _ptr(d["lm"], C.c_int32))
-            setattr(P, f"{pre}_camera", _ptr(d["cam"], C.c_int32))
-            setattr(P, f"{pre}_obs", _ptr(d["obs"], C.c_double))
+        for name, pre, _ in self._EDGE_SETS:
+            setattr(P, f"n_{pre}", getattr(self, name)["pose"].shape[0])
         P.th_mono_point = self.cfg.mono_point
         P.th_stereo_point = self.cfg.stereo_point
         P.th_mono_line = self.cfg.mono_line
@@ -209,23 +223,43 @@ class DenseResult:
     iters_first: int = 0
     iters_second: int = 0
 
+    _KINDS = ("mono", "stereo", "mono_line", "stereo_line")
+
     @staticmethod
     def alloc(p: DenseProblem) -> "DenseResult":
-        return DenseResult(
-            pose_q=np.zeros_like(p.pose_q), pose_p=np.zeros_like(p.pose_p),
-            points=np.zeros_like(p.points), lines=np.zeros_like(p.lines),
-            inlier={k: np.zeros(p.n_edges(k), np.uint8) for k in ("mono", "stereo", "mono_line", "stereo_line")})
+        # one buffer for every output (all entries are written by rspl_ba_local): doubles first,
+        # then the inlier flags; the arrays are views, their addresses base + offset
+        shapes = [p.pose_q.shape, p.pose_p.shape, p.points.shape, p.lines.shape]
+        nd = [int(np.prod(sh)) for sh in shapes]
+        ni = [p.n_edges(k) for k in DenseResult._KINDS]
+        buf = np.empty(8 * sum(nd) + sum(ni), np.uint8)
+        dbl = buf[:8 * sum(nd)].view(np.float64)
+        views, offs, o = [], [], 0
+        for sh, n in zip(shapes, nd):
+            views.append(dbl[o:o + n].reshape(sh))
+            offs.append(8 * o)
+            o += n
+        o8 = 8 * o
+        inl = {}
+        for k, n in zip(DenseResult._KINDS, ni):
+            inl[k] = buf[o8:o8 + n]
+            offs.append(o8)
+            o8 += n
+        r = DenseResult(pose_q=views[0], pose_p=views[1], points=views[2], lines=views[3], inlier=inl)
+        r._buf, r._offs = buf, offs
+        return r
 
     def to_ctypes(self) -> RsplBaResult:
         R = RsplBaResult()
-        R.pose_q = _ptr(self.pose_q, C.c_double)
-        R.pose_p = _ptr(self.pose_p, C.c_double)
-        R.points = _ptr(self.points, C.c_double)
-        R.lines = _ptr(self.lines, C.c_double)
-        R.mono_inlier = _ptr(self.inlier["mono"], C.c_uint8)
-        R.stereo_inlier = _ptr(self.inlier["stereo"], C.c_uint8)
-        R.mono_line_inlier = _ptr(self.inlier["mono_line"], C.c_uint8)
-        R.stereo_line_inlier = _ptr(self.inlier["stereo_line"], C.c_uint8)
+        buf = getattr(self, "_buf", None)
+        if buf is not None:
+            base = buf.ctypes.data
+            (R.pose_q, R.pose_p, R.points, R.lines, R.mono_inlier, R.stereo_inlier, R.mono_line_inlier,
+             R.stereo_line_inlier) = (base + o for o in self._offs)
+            return R
+        arrs = [self.pose_q, self.pose_p, self.points, self.lines] + [self.inlier[k] for k in self._KINDS]
+        (R.pose_q, R.pose_p, R.points, R.lines, R.mono_inlier, R.stereo_inlier, R.mono_line_inlier,
+         R.stereo_line_inlier) = (np.ascontiguousarray(a).ctypes.data for a in arrs)
         return R
 
     def read_back(self, R: RsplBaResult):
