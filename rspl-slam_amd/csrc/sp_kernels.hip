@@ -473,30 +473,32 @@ constexpr int NT_ = 32, NH = 20, NR = NT_ + 2 * NH;  // 72
 
 // dst[y][x] = max_{|k|<=4} src[y][x+k]  over the rectangle [y0,y1) x [x0,x1)
 __device__ __forceinline__ void rowpass(const float* src, float* dst, int y0, int y1, int x0, int x1) {
-  const int w = x1 - x0, n = (y1 - y0) * w;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int y = y0 + i / w, x = x0 + i % w;
-    const float* s = src + y * NR + x - 4;
-    float m = s[0];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = y0 + ty; y < y1; y += 32)
+    for (int x = x0 + tx; x < x1; x += 32) {
+      const float* s = src + y * NR + x - 4;
+      float m = s[0];
 #pragma unroll
-    for (int k = 1; k < 9; k++) m = fmaxf(m, s[k]);
-    dst[y * NR + x] = m;
-  }
+      for (int k = 1; k < 9; k++) m = fmaxf(m, s[k]);
+      dst[y * NR + x] = m;
+    }
 }
 // dst[y][x] = max_{|k|<=4} src[y+k][x]
 __device__ __forceinline__ void colpass(const float* src, float* dst, int y0, int y1, int x0, int x1) {
-  const int w = x1 - x0, n = (y1 - y0) * w;
-  for (int i = threadIdx.x; i < n; i += blockDim.x) {
-    const int y = y0 + i / w, x = x0 + i % w;
-    const float* s = src + (y - 4) * NR + x;
-    float m = s[0];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int y = y0 + ty; y < y1; y += 32)
+    for (int x = x0 + tx; x < x1; x += 32) {
+      const float* s = src + (y - 4) * NR + x;
+      float m = s[0];
 #pragma unroll
-    for (int k = 1; k < 9; k++) m = fmaxf(m, s[k * NR]);
-    dst[y * NR + x] = m;
-  }
+      for (int k = 1; k < 9; k++) m = fmaxf(m, s[k * NR]);
+      dst[y * NR + x] = m;
+    }
 }
 
-__global__ __launch_bounds__(256) void nms_kernel(NmsArgs a) {
+static_assert(NT_ == 32, "the output pass maps the 32 x 32 tile one element per thread");
+// 1024 threads as 32 x 32 (2D loops over the tile: no index divisions), one 72 x 72 tile
+__global__ __launch_bounds__(1024) void nms_kernel(NmsArgs a) {
   __shared__ float S[NR * NR];          // scores (0 outside the image)
   __shared__ float T[NR * NR];          // row-pass scratch
   __shared__ float M[NR * NR];          // max-pool result / supp flag
@@ -508,25 +510,29 @@ __global__ __launch_bounds__(256) void nms_kernel(NmsArgs a) {
   const int bi = blockIdx.x / per, t = blockIdx.x % per;
   const int y0 = (t / tiles_x) * NT_ - NH, x0 = (t % tiles_x) * NT_ - NH;
   const float* sc = a.scores + (size_t)bi * H * W;
-  for (int i = threadIdx.x; i < NR * NR; i += blockDim.x) {
-    const int y = y0 + i / NR, x = x0 + i % NR;
-    S[i] = (y >= 0 && y < H && x >= 0 && x < W) ? sc[(size_t)y * W + x] : 0.f;
-  }
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int ly = ty; ly < NR; ly += 32)
+    for (int lx = tx; lx < NR; lx += 32) {
+      const int y = y0 + ly, x = x0 + lx;
+      S[ly * NR + lx] = (y >= 0 && y < H && x >= 0 && x < W) ? sc[(size_t)y * W + x] : 0.f;
+    }
   __syncthreads();
   // max_mask = scores == max_pool(scores), valid on [4, NR-4)^2
   rowpass(S, T, 0, NR, 4, NR - 4);
   __syncthreads();
   colpass(T, M, 4, NR - 4, 4, NR - 4);
   __syncthreads();
-  for (int i = threadIdx.x; i < NR * NR; i += blockDim.x) {
-    const int y = i / NR, x = i % NR;
-    K[i] = (y >= 4 && y < NR - 4 && x >= 4 && x < NR - 4) ? (S[i] == M[i]) : 0;
-  }
+  for (int y = ty; y < NR; y += 32)
+    for (int x = tx; x < NR; x += 32) {
+      const int i = y * NR + x;
+      K[i] = (y >= 4 && y < NR - 4 && x >= 4 && x < NR - 4) ? (S[i] == M[i]) : 0;
+    }
   __syncthreads();
   for (int it = 0; it < 2; it++) {
     const int lo = 4 + 8 * it;  // K valid on [lo, NR-lo)^2
     const int l1 = lo + 4, l2 = lo + 8;
-    for (int i = threadIdx.x; i < NR * NR; i += blockDim.x) F[i] = K[i] ? 1.f : 0.f;
+    for (int y = ty; y < NR; y += 32)
+      for (int x = tx; x < NR; x += 32) F[y * NR + x] = K[y * NR + x] ? 1.f : 0.f;
     __syncthreads();
     // supp_mask = max_pool(max_mask) > 0, valid on [l1, NR-l1)^2
     rowpass(F, T, lo, NR - lo, l1, NR - l1);
@@ -534,48 +540,49 @@ __global__ __launch_bounds__(256) void nms_kernel(NmsArgs a) {
     colpass(T, M, l1, NR - l1, l1, NR - l1);
     __syncthreads();
     // supp_scores = where(supp_mask, 0, scores)
-    for (int i = threadIdx.x; i < NR * NR; i += blockDim.x) {
-      const int y = i / NR, x = i % NR;
-      if (y >= l1 && y < NR - l1 && x >= l1 && x < NR - l1) {
+    for (int y = l1 + ty; y < NR - l1; y += 32)
+      for (int x = l1 + tx; x < NR - l1; x += 32) {
+        const int i = y * NR + x;
         const bool supp = M[i] > 0.f;
         M[i] = supp ? 1.f : 0.f;
         F[i] = supp ? 0.f : S[i];
       }
-    }
     __syncthreads();
     // new_max_mask = supp_scores == max_pool(supp_scores), valid on [l2, NR-l2)^2
     rowpass(F, T, l1, NR - l1, l2, NR - l2);
     __syncthreads();
-    for (int i = threadIdx.x; i < NR * NR; i += blockDim.x) {
-      const int y = i / NR, x = i % NR;
-      if (y >= l2 && y < NR - l2 && x >= l2 && x < NR - l2) {
-        const float* s = T + (y - 4) * NR + x;
-        float m = s[0];
+    for (int y = ty; y < NR; y += 32)
+      for (int x = tx; x < NR; x += 32) {
+        const int i = y * NR + x;
+        if (y >= l2 && y < NR - l2 && x >= l2 && x < NR - l2) {
+          const float* s = T + (y - 4) * NR + x;
+          float m = s[0];
 #pragma unroll
-        for (int k = 1; k < 9; k++) m = fmaxf(m, s[k * NR]);
-        // max_mask | (new_max_mask & ~supp_mask)
-        K[i] = K[i] | ((F[i] == m) && !(M[i] > 0.f));
-      } else {
-        K[i] = 0;
+          for (int k = 1; k < 9; k++) m = fmaxf(m, s[k * NR]);
+          // max_mask | (new_max_mask & ~supp_mask)
+          K[i] = K[i] | ((F[i] == m) && !(M[i] > 0.f));
+        } else {
+          K[i] = 0;
+        }
       }
-    }
     __syncthreads();
   }
-  // output region [NH, NH+NT_)^2: NMS'd map + candidates
-  for (int i = threadIdx.x; i < NT_ * NT_; i += blockDim.x) {
-    const int ly = NH + i / NT_, lx = NH + i % NT_;
+  // output region [NH, NH+NT_)^2 (one element per thread): NMS'd map + candidates
+  {
+    const int ly = NH + ty, lx = NH + tx;
     const int y = y0 + ly, x = x0 + lx;
-    if (y >= H || x >= W) continue;
-    const float v = K[ly * NR + lx] ? S[ly * NR + lx] : 0.f;
-    if (a.nms_out) a.nms_out[(size_t)bi * H * W + (size_t)y * W + x] = v;
-    // find_high_score_index: float score > double threshold (src/super_point.cpp:228);
-    // remove_borders: border <= y < H-border, border <= x < W-border (:244-245)
-    if ((double)v > a.threshold && y >= a.border && y < H - a.border && x >= a.border && x < W - a.border) {
-      const int slot = atomicAdd(&a.cand_count[bi], 1);
-      if (slot < a.cand_cap) {
-        const unsigned long long key =
-            ((unsigned long long)(0xFFFFFFFFu - __float_as_uint(v)) << 32) | (unsigned)(y * W + x);
-        a.cand[(size_t)bi * a.cand_cap + slot] = key;
+    if (y < H && x < W) {
+      const float v = K[ly * NR + lx] ? S[ly * NR + lx] : 0.f;
+      if (a.nms_out) a.nms_out[(size_t)bi * H * W + (size_t)y * W + x] = v;
+      // find_high_score_index: float score > double threshold (src/super_point.cpp:228);
+      // remove_borders: border <= y < H-border, border <= x < W-border (:244-245)
+      if ((double)v > a.threshold && y >= a.border && y < H - a.border && x >= a.border && x < W - a.border) {
+        const int slot = atomicAdd(&a.cand_count[bi], 1);
+        if (slot < a.cand_cap) {
+          const unsigned long long key =
+              ((unsigned long long)(0xFFFFFFFFu - __float_as_uint(v)) << 32) | (unsigned)(y * W + x);
+          a.cand[(size_t)bi * a.cand_cap + slot] = key;
+        }
       }
     }
   }
@@ -776,7 +783,7 @@ hipError_t heads(const HeadArgs& a, int mode, hipStream_t s) {
 
 hipError_t nms(const NmsArgs& a, int B, hipStream_t s) {
   const int tiles = ((a.W + NT_ - 1) / NT_) * ((a.H + NT_ - 1) / NT_);
-  hipLaunchKernelGGL(nms_kernel, dim3(B * tiles), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(nms_kernel, dim3(B * tiles), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
 
