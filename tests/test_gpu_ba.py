@@ -112,3 +112,13 @@ def test_ba_many_poses(ba, n_poses):
                              outlier_frac=0.05)
     # larger systems with line landmarks: numeric-Jacobian noise reaches ~1e-8 of the cost
     _compare(ba.run(prob), oracle.ba_local(prob), tol_pose=1e-6, tol_pt=1e-5, chi2_rtol=5e-8)
+
+
+def test_ba_long_lines(ba):
+    """Line landmarks seen by more than 8 poses: their linearisation is split over several line
+    workgroups (per-edge records + last-edge ticket) instead of being summed in one."""
+    prob, gt = SY.ba_problem(n_poses=14, n_points=300, n_lines=30, obs_per_point=12, seed=21, pixel_sigma=0.8,
+                             outlier_frac=0.05)
+    lm = np.concatenate([prob.mono_line["lm"], prob.stereo_line["lm"]])
+    assert np.bincount(lm).max() > 8  # the split path is exercised
+    _compare(ba.run(prob), oracle.ba_local(prob), tol_pose=1e-6, tol_pt=1e-5, chi2_rtol=5e-8)
