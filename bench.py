@@ -233,8 +233,12 @@ def main():
     # under load (1.62 -> 1.90 ms of GPU work) is memory-latency contention, not CU slots -- so the
     # default is 0 (unmasked)
     rc = args.reserve_cus
-    st_sp, st_sg = capi.Stream(reserve_cus=rc), capi.Stream(high_priority=True, reserve_cus=rc)
-    st_post = capi.Stream(high_priority=True, reserve_cus=rc)  # SG's Sinkhorn + decode: overlaps the next GNN
+    # stream priorities (RSPL_STREAM_PRIO="sp=normal,sg=high,post=high", the defaults): the BA's
+    # own stream is always high
+    prio = dict(sp="normal", sg="high", post="high")
+    prio.update(kv.split("=") for kv in os.environ.get("RSPL_STREAM_PRIO", "").split(",") if "=" in kv)
+    st_sp, st_sg = capi.Stream(reserve_cus=rc, priority=prio["sp"]), capi.Stream(reserve_cus=rc, priority=prio["sg"])
+    st_post = capi.Stream(reserve_cus=rc, priority=prio["post"])  # SG's Sinkhorn + decode: overlaps the next GNN
     ev_sp = [capi.Event() for _ in range(3)]
     ev_sg = [capi.Event() for _ in range(3)]
 

@@ -246,12 +246,16 @@ class Event:
 
 
 class Stream:
-    def __init__(self, high_priority: bool = False, reserve_cus: int = 0):
+    def __init__(self, high_priority: bool = False, reserve_cus: int = 0, priority: str = ""):
+        """priority: "" (from high_priority), "high", "normal" or "low" (HIP stream priorities)."""
         self._s = C.c_void_p()
+        if not priority:
+            priority = "high" if high_priority else "normal"
         if reserve_cus > 0:  # CU-masked: leaves reserve_cus CUs to other (latency-bound) streams
             check(load().rspl_stream_create_reserving(C.byref(self._s), reserve_cus), "rspl_stream_create_reserving")
-        elif high_priority:
-            check(load().rspl_stream_create_priority(C.byref(self._s), 1), "rspl_stream_create_priority")
+        elif priority in ("high", "low"):
+            check(load().rspl_stream_create_priority(C.byref(self._s), 1 if priority == "high" else 0),
+                  "rspl_stream_create_priority")
         else:
             check(load().rspl_stream_create(C.byref(self._s)), "rspl_stream_create")
 
