@@ -19,7 +19,7 @@
  *
  * Feature layout (SuperPoint output / SuperGlue input) is the reference's
  * Eigen::Matrix<double,259,Dynamic> column-major storage
- * (src/super_point.cpp:368-387): feature i occupies doubles [259*i, 259*i+259):
+ * (SuperPoint::process_output, src/super_point.cpp:285-319; resized at :298): feature i occupies doubles [259*i, 259*i+259):
  *   [0] score, [1] x, [2] y, [3..258] L2-normalised descriptor.
  */
 #ifndef RSPL_H_
@@ -87,12 +87,12 @@ void rspl_timer_destroy(rspl_timer* t);
 /* ------------------------------------------------------------------------ */
 /* SuperPoint: SuperPointConfig (include/read_configs.h:9-18) minus TRT-only */
 /* fields; max_height/max_width size the device arena like the TRT profile   */
-/* kMAX does (src/super_point.cpp:113-123).                                 */
+/* kMAX does (src/super_point.cpp:46-53).                                 */
 /* ------------------------------------------------------------------------ */
 typedef struct {
-  int max_keypoints;         /* top-k; -1 keeps all (src/super_point.cpp:263) */
-  double keypoint_threshold; /* scores > threshold (src/super_point.cpp:228) */
-  int remove_borders;        /* border in pixels (src/super_point.cpp:244-245) */
+  int max_keypoints;         /* top-k; -1 keeps all (top_k_keypoints, src/super_point.cpp:192-204) */
+  double keypoint_threshold; /* scores > threshold (src/super_point.cpp:154-165) */
+  int remove_borders;        /* border in pixels (src/super_point.cpp:168-183) */
   int max_height;            /* arena sizing; H, W must be multiples of 8 */
   int max_width;
   int max_batch;             /* images per batched device call (>= 1) */
@@ -102,12 +102,12 @@ typedef struct {
 
 typedef struct rspl_sp rspl_sp;
 
-/* SuperPoint::SuperPoint + build() (src/super_point.cpp:83-156).
+/* SuperPoint::SuperPoint + build() (src/super_point.cpp:13-86).
  * weights_path: RSPLWT01 blob holding the reference state_dict
  * (convert2onnx/superpoint.py:86-105). */
 int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_path, rspl_sp** out);
 
-/* SuperPoint::infer (src/super_point.cpp:174-205): rectified u8 image
+/* SuperPoint::infer (src/super_point.cpp:104-135): rectified u8 image
  * (row stride in bytes) -> features[259 * capacity]; *n_out = keypoints. */
 int rspl_sp_infer(rspl_sp* sp, const uint8_t* image, int height, int width, int stride,
                   double* features, int capacity, int* n_out);

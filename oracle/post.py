@@ -14,13 +14,13 @@ FLT_MAX = np.float32(3.4028234663852886e38)
 
 
 def image_to_input(img_u8: np.ndarray) -> np.ndarray:
-    """src/super_point.cpp:216-220: float(u8) / 255.0 (double division, stored as float)."""
+    """src/super_point.cpp:146-150: float(u8) / 255.0 (double division, stored as float)."""
     return (img_u8.astype(np.float64) / 255.0).astype(np.float32)
 
 
 def sp_postprocess(scores: np.ndarray, desc: np.ndarray, threshold: float = 0.004,
                    border: int = 4, k: int = 400) -> np.ndarray:
-    """SuperPoint::process_output (src/super_point.cpp:355-389) -> 259 x n float64 (column per keypoint).
+    """SuperPoint::process_output (src/super_point.cpp:285-319) -> 259 x n float64 (column per keypoint).
 
     scores: [H, W] float32 NMS'd score map; desc: [256, H/8, W/8] float32 (L2-normalised).
     Returns F with F[:, i] = (score, x, y, desc[256]) exactly as the Eigen matrix columns.
@@ -50,7 +50,7 @@ def sp_postprocess(scores: np.ndarray, desc: np.ndarray, threshold: float = 0.00
 
 
 def sample_descriptors(xs: np.ndarray, ys: np.ndarray, desc: np.ndarray, s: int = 8) -> np.ndarray:
-    """normalize_keypoints + grid_sample + normalize_descriptors (src/super_point.cpp:276-353).
+    """normalize_keypoints + grid_sample + normalize_descriptors (src/super_point.cpp:206-283).
 
     Bilinear with align_corners=True semantics, computed in float64 over the float32 map.
     Returns [n, 256] float64.
@@ -90,7 +90,7 @@ def sample_descriptors(xs: np.ndarray, ys: np.ndarray, desc: np.ndarray, s: int 
 
 
 def normalize_keypoints(F: np.ndarray, width: int, height: int) -> np.ndarray:
-    """PointMatching::NormalizeKeypoints (src/point_matching.cc:72-84); width/2 is integer division."""
+    """PointMatching::NormalizeKeypoints (src/point_matching.cc:50-62); width/2 is integer division."""
     G = F.copy()
     scale = max(width, height) * 0.7
     G[1] = (F[1] - width // 2) / scale
@@ -142,7 +142,7 @@ def decode(Z: np.ndarray, threshold: float = 0.2):
 
 
 def match_points(idx0, idx1, ms0, ms1):
-    """PointMatching::MatchingPoints mutual re-check + DMatch (src/point_matching.cc:43-54).
+    """PointMatching::MatchingPoints mutual re-check + DMatch (src/point_matching.cc:24-31).
 
     Returns int32 [K,2] (query, train) and float32 [K] distances (cv::DMatch stores float).
     """

@@ -55,7 +55,7 @@ class SuperPoint:
         return self.config.max_keypoints if self.config.max_keypoints > 0 else 16384
 
     def infer(self, image: np.ndarray) -> Tuple[bool, np.ndarray]:
-        """SuperPoint::infer (src/super_point.cpp:174-205): u8 [H, W] -> (ok, features [259, N])."""
+        """SuperPoint::infer (src/super_point.cpp:104-135): u8 [H, W] -> (ok, features [259, N])."""
         img = np.ascontiguousarray(image, dtype=np.uint8)
         H, W = img.shape
         cap = self._cap()
@@ -199,7 +199,7 @@ class PointMatching:
 
     @staticmethod
     def NormalizeKeypoints(features: np.ndarray, width: int, height: int) -> np.ndarray:
-        """src/point_matching.cc:72-84 (host helper; the device path normalises in-kernel)."""
+        """src/point_matching.cc:50-62 (host helper; the device path normalises in-kernel)."""
         g = np.array(features, np.float64, copy=True)
         scale = max(width, height) * 0.7
         g[1] = (features[1] - width // 2) / scale

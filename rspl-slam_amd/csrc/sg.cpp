@@ -1,6 +1,6 @@
 // SuperGlue + PointMatching handle: C ABI (include/rspl.h) over sg_kernels.hip.
 // Mirrors SuperGlue::build / infer / process_output (src/super_glue.cpp:21-472) and
-// PointMatching::MatchingPoints (src/point_matching.cc:34-70).
+// PointMatching::MatchingPoints (src/point_matching.cc:12-62).
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
@@ -546,7 +546,7 @@ extern "C" int rspl_pm_match(rspl_sg* s, const double* f0, int n0, const double*
   const double* m0 = s->h_ms;
   const double* m1 = s->h_ms + nm;
   int k = 0;
-  for (int i = 0; i < n0; i++) {  // src/point_matching.cc:46-54
+  for (int i = 0; i < n0; i++) {  // src/point_matching.cc:24-31
     const int j = i0[i];
     if (j < n1 && j >= 0 && i1[j] == i) {
       if (k >= capacity) {

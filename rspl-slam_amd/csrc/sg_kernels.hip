@@ -5,7 +5,7 @@
 //   final_proj + scores/16 :295-300, log_optimal_transport :176-205,
 //   decode (argmax / mutual / exp / 0.2) super_glue.cpp:258-367,
 //   process_input (double -> float packing) super_glue.cpp:199-246,
-//   PointMatching::NormalizeKeypoints point_matching.cc:72-84.
+//   PointMatching::NormalizeKeypoints point_matching.cc:50-62.
 // Layout: token-major.  Token t = (pair*2 + image)*nmax + i; descriptors X[t][256].
 // Q/K/V channels are stored head-contiguous (h*64 + d); the weight rows are
 // permuted once on the host so this equals the reference's d*4 + h interleave.
@@ -647,7 +647,7 @@ __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
     if (lane == 0 || lane == 1) {
       double c = f[1 + lane];
       if (a.normalize) {
-        const int half = (lane == 0 ? a.width : a.height) / 2;  // integer division (point_matching.cc:79-81)
+        const int half = (lane == 0 ? a.width : a.height) / 2;  // integer division (point_matching.cc:56-59)
         c = (c - half) / ((a.width > a.height ? a.width : a.height) * 0.7);
       }
       v = (float)c;

@@ -1,5 +1,5 @@
 // SuperPoint handle: C ABI (include/rspl.h) over the HIP kernels in sp_kernels.hip.
-// Mirrors SuperPoint::build / infer / process_output (src/super_point.cpp:89-389):
+// Mirrors SuperPoint::build / infer / process_output (src/super_point.cpp:19-319):
 // weights are loaded and re-laid-out once at create; every buffer is carved from
 // one arena sized for max_batch x max_height x max_width.
 #include <algorithm>
@@ -186,7 +186,7 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
       for (int ci = 0; ci < 256; ci++) d[ci * 256 + co] = wDb->data[co * 256 + ci];
     ok &= up(s->wPb, r) && up(s->bPb, b) && up(s->wDb, d) && up(s->bDb, bDb->data);
   }
-  {  // src/super_point.cpp:218: float(u8) / 255.0 computed in double, stored as float
+  {  // src/super_point.cpp:148: float(u8) / 255.0 computed in double, stored as float
     std::vector<float> lut(256);
     for (int u = 0; u < 256; u++) lut[u] = (float)(double(u) / 255.0);
     ok &= up(s->lut, lut);
@@ -286,20 +286,20 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
   RSPL_HIP(heads(h, 0, st));
   h.w = s->wDb; h.bias = s->bDb; h.desc = s->desc;
   RSPL_HIP(heads(h, 1, st));
-  // NMS + threshold + borders (superpoint.py:16-33, super_point.cpp:224-253)
+  // NMS + threshold + borders (superpoint.py:16-33, super_point.cpp:154-183)
   s->timer.mark(4, st);
   RSPL_HIP(hipMemsetAsync(s->cand_count, 0, sizeof(int) * B, st));
   NmsArgs n{};
   n.scores = s->scores; n.nms_out = s->nms; n.cand = s->cand; n.cand_count = s->cand_count; n.cand_cap = s->cand_cap;
   n.H = H; n.W = W; n.threshold = s->cfg.keypoint_threshold; n.border = s->cfg.remove_borders;
   RSPL_HIP(nms(n, B, st));
-  // top-k (super_point.cpp:255-274)
+  // top-k (super_point.cpp:185-204)
   s->timer.mark(5, st);
   TopkArgs t{};
   t.cand = s->cand; t.cand_count = s->cand_count; t.cand_cap = s->cand_cap; t.lds_cap = kCandCap; t.k = k;
   t.sel = s->sel; t.sel_count = s->sel_count; t.sel_cap = kCandCap;
   RSPL_HIP(topk(t, B, st));
-  // descriptor sampling + packing (super_point.cpp:276-387)
+  // descriptor sampling + packing (super_point.cpp:206-319)
   s->timer.mark(6, st);
   SampleArgs sa{};
   sa.sel = s->sel; sa.sel_count = s->sel_count; sa.sel_stride = kCandCap; sa.per_image = (k > 0 ? k : kCandCap);

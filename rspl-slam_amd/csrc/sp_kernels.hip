@@ -3,7 +3,7 @@
 // Reference semantics:
 //   network  convert2onnx/superpoint.py:114-161  (encoder, detector & descriptor heads)
 //   NMS      convert2onnx/superpoint.py:16-33    (simple_nms, radius 4)
-//   host     src/super_point.cpp:207-389         (u8/255, threshold, borders, top-k,
+//   host     src/super_point.cpp:137-319         (u8/255, threshold, borders, top-k,
 //                                                 bilinear sampling in double, packing)
 // Layout: activations NHWC fp32 (channels contiguous), one batch of B images.
 // Convolutions are implicit GEMMs (M = pixels, N = output channels, K = 9*Cin)
@@ -32,7 +32,7 @@ __device__ __forceinline__ floatx16 mfma32(float a, float b, floatx16 c) {
 //   K loop = Cin in chunks of CK=16, staged in LDS with the 1-pixel halo;
 //            weights staged as [9][CK][64].
 // FUSE1A: the input tile is conv1a(relu) computed on the fly from the u8
-// image (src/super_point.cpp:216-220 normalisation via LUT), so the 64-channel
+// image (src/super_point.cpp:146-150 normalisation via LUT), so the 64-channel
 // full-resolution conv1a map never touches HBM.
 // ---------------------------------------------------------------------------
 constexpr int CK = 16;
@@ -574,7 +574,7 @@ __global__ __launch_bounds__(1024) void nms_kernel(NmsArgs a) {
     if (y < H && x < W) {
       const float v = K[ly * NR + lx] ? S[ly * NR + lx] : 0.f;
       if (a.nms_out) a.nms_out[(size_t)bi * H * W + (size_t)y * W + x] = v;
-      // find_high_score_index: float score > double threshold (src/super_point.cpp:228);
+      // find_high_score_index: float score > double threshold (src/super_point.cpp:158);
       // remove_borders: border <= y < H-border, border <= x < W-border (:244-245)
       if ((double)v > a.threshold && y >= a.border && y < H - a.border && x >= a.border && x < W - a.border) {
         const int slot = atomicAdd(&a.cand_count[bi], 1);
@@ -592,7 +592,7 @@ __global__ __launch_bounds__(1024) void nms_kernel(NmsArgs a) {
 // Top-k selection: one workgroup per image, bitonic sort in LDS.
 // Key = (~score_bits << 32) | flat_index: ascending key order = score desc,
 // then flat index asc (documented tie-break for the reference's non-stable
-// std::sort, src/super_point.cpp:255-260).  If n <= k the reference does not
+// std::sort, src/super_point.cpp:185-190).  If n <= k the reference does not
 // sort: keypoints stay in row-major scan order (flat index asc).
 // ---------------------------------------------------------------------------
 // Keys are (~score bits) << 32 | flat index: ascending key = descending score, ties by flat
@@ -677,7 +677,7 @@ __global__ __launch_bounds__(1024) void topk_kernel(TopkArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Descriptor sampling + packing (src/super_point.cpp:276-387), fp64.
+// Descriptor sampling + packing (src/super_point.cpp:206-319), fp64.
 // One wave per keypoint, 4 channels per lane.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void sample_kernel(SampleArgs a) {

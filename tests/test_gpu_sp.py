@@ -51,7 +51,7 @@ def test_sp_keep_all_and_empty(pkg, weight_blobs):
     from rspl_slam_amd import synthetic as SY
     img = SY.textured_image(96, 128, seed=11, n_blobs=10)
     s, d = oracle.sp_forward(weight_blobs[0], post.image_to_input(img))
-    # k = -1: no sort, keypoints in row-major scan order (src/super_point.cpp:263)
+    # k = -1: no sort, keypoints in row-major scan order (src/super_point.cpp:193)
     sp = _sp(pkg, weight_blobs[0], -1, 96, 128)
     ok, F = sp.infer(img)
     assert ok, sp.error
