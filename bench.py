@@ -14,10 +14,16 @@ stream beside SG of frame t (event-ordered).  The timed region ends
 synchronisation, so every frame's SP, SG and BA work is inside it.  The BA problem is handed over as host
 arrays (the reference's std::map containers), so its H2D upload is inside the step.
 
-Multi-GPU (python -m torch.distributed.run ... bench.py --gpus N): one process per GPU, each
-rank runs its own stereo sequence (replicas, weak scaling, no data-path collective); the
-gloo process group only provides the barrier and the max-over-ranks timing, so a single
-HIP runtime (librspl's system ROCm) drives each GPU.
+Multi-GPU: `bench.py --gpus N` spawns N rank processes itself (before anything touches the GPU),
+or runs as one rank under `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`
+(then WORLD_SIZE must equal N).  One process per GPU; each rank runs its own stereo sequence
+(replicas, weak scaling); the gloo group provides the barrier, the max-over-ranks timing and the
+rank census (fails loudly if fewer than N distinct GPUs come up).  `--ba-mode shard` instead
+solves every step's N local BAs (one per rank's sequence) jointly, landmark-sharded over all
+ranks with an RCCL all-reduce of the reduced camera system per LM trial.
+
+Workloads: `--workload c3` (default, BASELINE configs[2]) or `c5` (configs[4]: synthetic
+1920x1080 stereo, 2048 keypoints, SG N=2048, 30-keyframe / 10k-landmark BA).
 """
 import argparse
 import json
@@ -42,25 +48,48 @@ import rspl_loader  # noqa: E402
 pkg = rspl_loader.load()
 capi = pkg.capi
 
-H, W, K = 480, 752, 400
+WORKLOADS = {
+    "c3": dict(H=480, W=752, K=400, ba=dict(n_poses=10, n_points=4000, n_lines=100), ba_caps=(16, 6000, 200, 40000),
+               desc="C3 EuRoC 752x480 stereo keyframe stream: SP batch 2 top-400, SG 2 pairs N=400, "
+                    "local BA 10 poses / ~4k points / 100 lines"),
+    "c5": dict(H=1080, W=1920, K=2048, ba=dict(n_poses=30, n_points=10000, n_lines=0, pixel_sigma=0.8,
+                                               outlier_frac=0.05), ba_caps=(32, 10000, 16, 70000),
+               desc="C5 synthetic 1920x1080 stereo stream: SP batch 2 top-2048, SG 2 pairs N=2048, "
+                    "local BA 30 keyframes / 10k landmarks (5 % outliers)"),
+}
+H, W, K = 480, 752, 400  # set from the workload in main()
 FP32_MFMA_PEAK = 157.3  # TFLOP/s, MI355X_MICROARCH.md (v_mfma_f32_32x32x2_f32, dense)
 FP16_MFMA_PEAK = 2516.8  # TFLOP/s dense (~2.5 PF, = 16 x the f32 MFMA rate), MI355X_MICROARCH.md
 HBM_PEAK_GBS = 8000.0  # HBM3E, MI355X_MICROARCH.md
-CONV1_GFLOP_PER_IMAGE = 2 * H * W * 64 * 9 / 1e9 + 2 * H * W * 64 * 576 / 1e9  # conv1a + conv1b
+
+
+def conv1_gflop_per_image():
+    return 2 * H * W * 64 * 9 / 1e9 + 2 * H * W * 64 * 576 / 1e9  # conv1a + conv1b
+
+
+def ba_bytes_per_iteration(prob):
+    """algorithmic bytes of one LM iteration = N_obs (4 d + 8) (measurements + ids)
+    + 12 N_pt + 24 N_line + 28 K + 8 ((6K)^2 + 6K) (parameters, reduced-system write)."""
+    sets = (("mono", 2), ("stereo", 3), ("mono_line", 4), ("stereo_line", 8))
+    nobs = sum(d * prob.n_edges(n) for n, d in sets)
+    nedges = sum(prob.n_edges(n) for n, _ in sets)
+    Kp = int((prob.pose_fixed == 0).sum())
+    return 4 * nobs + 8 * nedges + 12 * len(prob.points) + 24 * len(prob.lines) + 28 * Kp + \
+        8 * ((6 * Kp) ** 2 + 6 * Kp)
 
 
 def log(msg):
     print(msg, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(sp_w, sg_w, frames, threads):
+def cpu_baseline(sp_w, sg_w, frames, threads, wl):
     """The oracle's C restatement (oracle/*.c) of the same per-keyframe work on host cores."""
     sys.path.insert(0, str(ROOT / "oracle"))
     import oracle  # checker/baseline only
     import post
     oracle.set_threads(threads)
     syn = pkg.synthetic
-    probs = [syn.ba_problem(n_poses=10, n_points=4000, n_lines=100, seed=100 + i)[0] for i in range(frames)]
+    probs = [syn.ba_problem(seed=100 + i, **wl["ba"])[0] for i in range(frames)]
     pairs = [syn.stereo_pair(H, W, seed=200 + i) for i in range(frames + 1)]
     prev = None
     t0 = time.perf_counter()
@@ -96,26 +125,34 @@ def pmc_traffic(kernel_substr):
 
 
 def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
-    """Achieved rate vs the bounding peak for the other big stages (HIP-event stage times, per
-    step: 2 SuperPoint images, 2 SuperGlue pairs of N = M = 400).  Algorithmic work as SURVEY.md
-    8(d): GNN 2*(655,360 N + 512 N M) per image per layer; Sinkhorn streamed model
-    2*iters*4*(N+1)(M+1) bytes per pair; NMS 2*4*H*W bytes per image."""
+    """Achieved rate vs the bounding peak for the big stages (HIP-event stage times on the stage's
+    launch stream, per step: 2 SuperPoint images, 2 SuperGlue pairs of N = M = K).  Algorithmic work
+    as SURVEY.md 8(d): conv1a+conv1b 2*H*W*64*(9 + 576) FLOP per image; GNN 2*(655,360 N + 512 N M)
+    per image per layer; Sinkhorn streamed model 2*iters*4*(N+1)(M+1) bytes per pair; NMS 2*4*H*W
+    bytes per image.  Single-kernel stages carry the kernel name (pmc_kernel) whose PMC traffic
+    summary under profiles/ gives `traffic`; the GNN is a 72-launch family (single_kernel false)."""
     t = {**{f"sp:{n}": v / max(1, sp_calls) for n, v in zip(sp.STAGES, sp_ms)},
          **{f"sg:{n}": v / max(1, sg_calls) for n, v in zip(sg.STAGES, sg_ms)}}
     N = M = K
     mfma_peak = FP16_MFMA_PEAK if precision == "fp16" else FP32_MFMA_PEAK
-    gnn_gflop = 2 * 2 * 18 * 2 * (655360 * N + 512 * N * M) / 1e9
-    sink_gb = 2 * 2 * 100 * 4 * (N + 1) * (M + 1) / 1e9
-    nms_gb = 2 * 2 * 4 * H * W / 1e9
+    conv1_k = ("conv3x3_h_kernel<64, 16, true, true, false>" if precision == "fp16"
+               else "conv3x3_kernel<64, 16, true, true>")
+    rows = (("sp:conv1a+1b+pool", 2 * conv1_gflop_per_image(), "TFLOP/s", mfma_peak, "mfma", conv1_k, True,
+             "GFLOP per launch (2 images, conv1a+conv1b)"),
+            ("sg:gnn x18", 2 * 2 * 18 * 2 * (655360 * N + 512 * N * M) / 1e9, "TFLOP/s", mfma_peak, "mfma",
+             "gemm_rk_kernel", False, "GFLOP per step (2 pairs x 2 images x 18 layers, 72 launches)"),
+            ("sg:sinkhorn", 2 * 2 * 100 * 4 * (N + 1) * (M + 1) / 1e9, "GB/s", HBM_PEAK_GBS, "hbm", "sinkhorn_kernel",
+             True, "GB per launch (2 pairs, streamed model 2*iters*4*(N+1)(M+1))"),
+            ("sp:nms", 2 * 2 * 4 * H * W / 1e9, "GB/s", HBM_PEAK_GBS, "hbm", "nms_kernel", True,
+             "GB per launch (2 images, 2*4*H*W)"))
     out = {}
-    for key, work, unit, peak, bound in (("sg:gnn x18", gnn_gflop, "TFLOP/s", mfma_peak, "mfma"),
-                                         ("sg:sinkhorn", sink_gb, "GB/s", HBM_PEAK_GBS, "hbm (latency)"),
-                                         ("sp:nms", nms_gb, "GB/s", HBM_PEAK_GBS, "hbm (latency)")):
+    for key, work, unit, peak, bound, kern, single, what in rows:
         ms = t.get(key)
         if ms:
             ach = work / ms if unit == "TFLOP/s" else work / ms * 1e3
             out[key] = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
-                        "frac": round(ach / peak, 4), "ms": round(ms, 4)}
+                        "frac": round(ach / peak, 4), "ms": round(ms, 4), "avg_launch_ms": round(ms, 4),
+                        "algorithmic": f"{work:.4g} {what}", "pmc_kernel": kern, "single_kernel": single}
     return out
 
 
@@ -161,13 +198,55 @@ def job_value(world, steps, elapsed):
     return world * steps / elapsed
 
 
+def spawn_ranks(n, argv):
+    """bench.py --gpus N without a launcher: start N rank processes (one per GPU) before this
+    process touches the GPU, wait for all of them, exit with the first failure's code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, str(pathlib.Path(__file__).resolve())] + argv, env=env))
+    rc = 0
+    for pr in procs:
+        c = pr.wait()
+        if c != 0 and rc == 0:
+            rc = c
+            for q in procs:  # one rank failed: the others would wait on it forever
+                if q.poll() is None:
+                    q.kill()
+    if rc:
+        log(f"bench: a rank exited with {rc}")
+    return rc
+
+
+def rank_census(dist, world, want, local):
+    """Every rank reports (rank, device, visible devices, host); fail loudly unless exactly `want`
+    ranks came up on distinct GPUs."""
+    n = C_int = None  # noqa: F841
+    cnt = pkg.capi.device_count()
+    rows = [None] * world
+    dist.all_gather_object(rows, (int(os.environ.get("RANK", 0)), local, cnt, os.uname().nodename))
+    devs = {(h, d) for _, d, _, h in rows}
+    if world != want or len(devs) != world:
+        raise SystemExit(f"bench: --gpus {want} but {world} ranks on {len(devs)} distinct GPUs came up: {rows}")
+    return rows
+
+
 def main():
-    capi.load()  # librspl's HIP runtime first: one runtime per process
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=30)
-    ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--cpu-frames", type=int, default=12, help="keyframes in the bounded CPU-baseline sample")
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
+    ap.add_argument("--ba-mode", choices=["replica", "shard"], default="replica",
+                    help="replica: each rank solves its own sequence's BA; shard: every step's N BAs are solved "
+                         "jointly, landmark-sharded over all ranks (RCCL all-reduce of the reduced camera system)")
+    ap.add_argument("--cpu-frames", type=int, default=None, help="keyframes in the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp16",
                     help="SP/SG MFMA precision: fp16 = the reference's own TensorRT kFP16 engines "
@@ -181,14 +260,24 @@ def main():
                     help="skip the second (other-precision) measurement")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE={world}")
+    global H, W, K
+    wl = WORKLOADS[args.workload]
+    H, W, K = wl["H"], wl["W"], wl["K"]
+    capi.load()  # librspl's HIP runtime first: one runtime per process
     dist = None
     if world > 1:
+        import datetime
         import torch
         import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=300))
+        rank_census(dist, world, args.gpus, local)
     capi.check(capi.load().rspl_set_device(local), "rspl_set_device")
 
     sp_w, sg_w = pkg.weights.ensure_blobs(str(ROOT / "weights"))
@@ -204,9 +293,16 @@ def main():
                                                  max_batch=2, precision=code, device=local))
         assert sg_h.build(), sg_h.error
         handles[pr] = (sp_h, sg_h)
-    ba = pkg.LocalBA(max_poses=16, max_points=6000, max_lines=200, max_edges=40000, device=local)
+    ba = pkg.LocalBA(*wl["ba_caps"], device=local)
     if args.ba_own_cus and args.reserve_cus > 0:
         ba.use_reserved_cus(args.reserve_cus)
+    shard = args.ba_mode == "shard"
+    if shard:  # landmark-sharded BA over RCCL: one communicator across all ranks (also valid at N = 1)
+        if dist is not None:
+            comm = pkg.Comm(pkg.broadcast_comm_id(dist), rank, world, local)
+        else:
+            comm = pkg.Comm(pkg.comm_unique_id(), 0, 1, local)
+        ba.set_comm(comm)
     syn = pkg.synthetic
     NP = 4
     pool = capi.DeviceBuffer(NP * 2 * H * W)
@@ -214,7 +310,10 @@ def main():
     for i in range(NP):
         L, R = syn.stereo_pair(H, W, seed=seeds["images"][i])
         pool.upload(np.stack([L, R]), offset=i * 2 * H * W)
-    ba_sets = [syn.ba_problem(n_poses=10, n_points=4000, n_lines=100, seed=sd) for sd in seeds["ba"]]
+    if shard:  # every rank holds every rank's problems: step i solves all N of them jointly
+        ba_sets = [syn.ba_problem(seed=sd, **wl["ba"]) for r in range(world) for sd in replica_seeds(r)["ba"]]
+    else:
+        ba_sets = [syn.ba_problem(seed=sd, **wl["ba"]) for sd in seeds["ba"]]
     problems = [p for p, _ in ba_sets]
     FB = K * 259 * 8
     # SP(t+1) is pipelined beside SG(t): SP and SG on their own streams,
@@ -230,8 +329,7 @@ def main():
     # SG is the frame's critical chain (SP has slack): SG and the BA run at high priority.  With
     # --reserve-cus the SP / SG / post streams are CU-masked off a few CUs spread over the chip
     # (and, with --ba-own-cus, the BA confined to them).  Measured: no gain -- the BA's slowdown
-    # under load (1.62 -> 1.90 ms of GPU work) is memory-latency contention, not CU slots -- so the
-    # default is 0 (unmasked)
+    # under load is memory-latency contention, not CU slots -- so the default is 0 (unmasked)
     rc = args.reserve_cus
     # stream priorities (RSPL_STREAM_PRIO="sp=normal,sg=high,post=high", the defaults): the BA's
     # own stream is always high
@@ -249,6 +347,7 @@ def main():
             c.zero()
         capi.synchronize()
         ba_ms = []
+        ba_iters = []
         ba_err = []
         ba_q = queue.Queue(maxsize=2)
 
@@ -257,20 +356,27 @@ def main():
             feature thread keeps extracting/matching (src/map_builder.cc:48-49, src/map.cc:105-107)."""
             capi.check(capi.load().rspl_set_device(local), "rspl_set_device")  # HIP device is per thread
             while True:
-                prob = ba_q.get()
-                if prob is None:
+                item = ba_q.get()
+                if item is None:
                     ba_q.task_done()
                     return
                 t = time.perf_counter()
                 try:
-                    ba.run(prob)
+                    for prob in item:
+                        r = ba.run(prob)
+                        ba_iters.append(r.iters_first + r.iters_second)
                 except Exception as e:  # surfaced on the main thread
                     ba_err.append(e)
-                ba_ms.append((time.perf_counter() - t) * 1e3)
+                ba_ms.append((time.perf_counter() - t) * 1e3 / len(item))
                 ba_q.task_done()
 
         worker = threading.Thread(target=tracking_thread, daemon=True)
         worker.start()
+
+        def ba_item(i):
+            if shard:  # all ranks' BAs of step i, each solved jointly by every rank
+                return [problems[(i % len(seeds["ba"])) + len(seeds["ba"]) * r] for r in range(world)]
+            return [problems[i % len(problems)]]
 
         def step(i):
             slot, pslot = i % 3, (i - 1) % 3
@@ -284,7 +390,7 @@ def main():
                     sg.infer_device(2, f0.ptr, n0.ptr, f1.ptr, n1.ptr, K, True, outs[0].ptr, outs[1].ptr,
                                     outs[2].ptr, outs[3].ptr, st_sg.handle, post_stream=st_post.handle)
                 if "ba" not in skip:
-                    ba_q.put(problems[i % len(problems)])
+                    ba_q.put(ba_item(i))
                 return
             if i >= 2:
                 ev_sg[(i - 2) % 3].wait_on(st_sp.handle)
@@ -306,17 +412,20 @@ def main():
             # keyframe i's local BA goes to the tracking thread (own high-priority stream) through a
             # 2-deep buffer, as the reference's feature thread blocks only while
             # _tracking_data_buffer.size() >= 2 (src/map_builder.cc:176)
-            ba_q.put(problems[i % len(problems)])
+            ba_q.put(ba_item(i))
 
         for i in range(args.warmup):
             step(i)
         ba_q.join()
         capi.synchronize()
+        if not sg.status()[0]:
+            raise SystemExit(f"bench: SuperGlue device path failed during warmup: {sg.error}")
         if dist:
             dist.barrier()
         sp.profile(True)
         sg.profile(True)
         ba_ms.clear()
+        ba_iters.clear()
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(args.warmup + i)
@@ -327,31 +436,41 @@ def main():
         worker.join()
         if ba_err:
             raise ba_err[0]
+        ok, mask = sg.status()  # Sinkhorn exchange health of every call in the timed region
+        if not ok:
+            raise SystemExit(f"bench: SuperGlue device path failed in the timed region (pairs 0x{mask:x}): {sg.error}")
         if dist:
             dist.barrier()
 
         sp_ms, sp_calls = sp.stage_times()
         sg_ms, sg_calls = sg.stage_times()
-        conv1_ms = sp_ms[0] / max(1, sp_calls)
-        achieved = 2 * CONV1_GFLOP_PER_IMAGE / conv1_ms  # GFLOP / ms = TFLOP/s
         value = job_value(world, args.steps, elapsed)
-        return {"value": value, "elapsed": elapsed, "sp": (sp_ms, sp_calls), "sg": (sg_ms, sg_calls), "stages": (sp, sg),
-                "conv1_ms": conv1_ms, "achieved": achieved, "ba_ms": list(ba_ms)}
+        return {"value": value, "elapsed": elapsed, "sp": (sp_ms, sp_calls), "sg": (sg_ms, sg_calls),
+                "stages": (sp, sg), "ba_ms": list(ba_ms), "ba_iters": list(ba_iters)}
 
     res = measure(args.precision)
     other = measure(precs[1]) if len(precs) > 1 else None  # the other precision, same run, for the record
-    value, elapsed, conv1_ms, achieved, ba_ms = (res["value"], res["elapsed"], res["conv1_ms"], res["achieved"],
-                                                 res["ba_ms"])
+    value, elapsed, ba_ms = res["value"], res["elapsed"], res["ba_ms"]
     sp_ms, sp_calls = res["sp"]
     sg_ms, sg_calls = res["sg"]
     sp, sg = res["stages"]
-    traffic, traffic_src = pmc_traffic("conv3x3_kernel<64, 16, true, true>" if args.precision == "fp32"
-                                       else "conv3x3_h_kernel<64, 16, true, true, false>")
     if rank != 0:
         return
-    peak = FP16_MFMA_PEAK if args.precision == "fp16" else FP32_MFMA_PEAK
+    stages = stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, args.precision)
+    # the dominant single kernel by device time per step
+    dom_key = max((k for k in stages if stages[k]["single_kernel"]), key=lambda k: stages[k]["ms"])
+    dom = {k: v for k, v in stages[dom_key].items() if k not in ("single_kernel", "ms")}
+    traffic, traffic_src = pmc_traffic(dom["pmc_kernel"])
+    dom["traffic"] = round(traffic) if traffic else None
+    dom["traffic_note"] = (f"HBM bytes per launch, rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE, profiles/{traffic_src}"
+                           if traffic else "no PMC summary for this kernel under profiles/")
+    ba_wall = float(np.mean(ba_ms)) if ba_ms else None
+    ba_it = float(np.mean(res["ba_iters"])) if res["ba_iters"] else None
+    ba_bytes = float(np.mean([ba_bytes_per_iteration(p) for p in problems]))
     out = {
-        "metric": "stereo frames/sec SuperPoint+SuperGlue+localBA @752x480 (all-keyframe: 2xSP, 2xSG, 1 BA per frame)",
+        "metric": "stereo frames/sec SuperPoint+SuperGlue+localBA @752x480 (all-keyframe: 2xSP, 2xSG, 1 BA per frame)"
+                  if args.workload == "c3" else
+                  "stereo frames/sec SuperPoint+SuperGlue+localBA @1920x1080 (C5, all-keyframe: 2xSP, 2xSG, 1 BA per frame)",
         "value": round(value, 3),
         "unit": "frames/s",
         "n_gpus": world,
@@ -364,25 +483,24 @@ def main():
         "dtype": ("fp16 MFMA with fp32 accumulation for SuperPoint/SuperGlue (the reference's TensorRT kFP16 "
                   "engines), fp32 Sinkhorn/decode, fp64 BA") if args.precision == "fp16"
                  else "fp32 (SuperPoint/SuperGlue MFMA), fp64 (BA)",
-        "data": "synthetic (seeded textured stereo 752x480, seeded weights, synthetic C3 local-BA problems)",
-        "config": {"workload": "C3 EuRoC 752x480 stereo keyframe stream: SP batch 2 top-400, SG 2 pairs N=400, "
-                               "local BA 10 poses / ~4k points / 100 lines",
-                   "global_batch": world, "parallelism": f"replicas x{world} (one sequence per GPU)"},
-        "roofline": {"kernel": ("conv3x3_h_kernel<64,16,true,true,false>" if args.precision == "fp16"
-                                else "conv3x3_kernel<64,16,true,true>") + " (conv1a+conv1b+ReLU+pool, fused)",
-                     "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                     "frac": round(achieved / peak, 4),
-                     "traffic": round(traffic) if traffic else None,
-                     "traffic_note": (f"HBM bytes per launch, rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE, {traffic_src}; "
-                                      "algorithmic minimum = pooled 64-ch output (46.2 MB fp32 / 23.1 MB fp16) "
-                                      "+ 0.7 MB images")
-                     if traffic else None,
-                     "algorithmic": f"{2 * CONV1_GFLOP_PER_IMAGE:.3f} GFLOP per launch (2 images)",
-                     "avg_launch_ms": round(conv1_ms, 4)},
-        "stages_roofline": stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, args.precision),
+        "data": f"synthetic (seeded textured stereo {W}x{H}, seeded weights, synthetic local-BA problems)",
+        "config": {"workload": wl["desc"], "global_batch": world,
+                   "parallelism": (f"replicas x{world} (one sequence per GPU)" if not shard else
+                                   f"replicas x{world} front end; every step's {world} local BAs landmark-sharded "
+                                   f"over {world} ranks (RCCL all-reduce per LM trial)")},
+        "roofline": {"kernel": dom_key, **dom},
+        "stages_roofline": stages,
         "stages_ms_per_step": {**{f"sp:{n}": round(v / max(1, sp_calls), 4) for n, v in zip(sp.STAGES, sp_ms)},
                                **{f"sg:{n}": round(v / max(1, sg_calls), 4) for n, v in zip(sg.STAGES, sg_ms)},
-                               "ba:wall": round(float(np.mean(ba_ms)), 4) if ba_ms else None},
+                               "ba:wall": round(ba_wall, 4) if ba_wall else None},
+        "ba": {"ms_per_call": round(ba_wall, 4) if ba_wall else None,
+               "lm_iterations_per_call": ba_it,
+               "us_per_lm_iteration": round(1e3 * ba_wall / ba_it, 2) if ba_wall and ba_it else None,
+               "algorithmic_bytes_per_iteration": round(ba_bytes),
+               "achieved_GBps": round(ba_bytes / (ba_wall / ba_it) / 1e6, 3) if ba_wall and ba_it else None,
+               "frac_hbm": round(ba_bytes / (ba_wall / ba_it) / 1e6 / HBM_PEAK_GBS, 6) if ba_wall and ba_it else None,
+               "note": "SURVEY 8(d) bytes per LM iteration; the BA is launch/latency-bound, wall time under the "
+                       "pipeline's contention, host-array hand-over included"},
     }
     if other is not None:
         oname = "fp32" if args.precision == "fp16" else "fp16"
@@ -391,9 +509,16 @@ def main():
                                "note": "same workload and run, SP/SG at " + oname +
                                        (" (the bit-parity path)" if oname == "fp32" else "")}
     if world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
-        out["cpu_baseline"] = cpu_baseline(sp_w, sg_w, args.cpu_frames, threads)
-        out["ate"] = ate_report(ba, ba_sets)
+        nproc = os.cpu_count() or 1
+        threads = min(16, nproc)  # the GPU box's CPU share is 16 cores per GPU
+        frames = args.cpu_frames or (12 if args.workload == "c3" else 1)
+        cb = cpu_baseline(sp_w, sg_w, frames, threads, wl)
+        cb1 = cpu_baseline(sp_w, sg_w, max(1, frames // 6), 1, wl)
+        cb["nproc"] = nproc
+        cb["one_core"] = {"value": cb1["value"], "cores": 1, "sample": cb1["sample"]}
+        out["cpu_baseline"] = cb
+        if args.workload == "c3":
+            out["ate"] = ate_report(ba, ba_sets)
     print(json.dumps(out), flush=True)
 
 

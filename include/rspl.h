@@ -123,6 +123,10 @@ int rspl_sp_infer_device(rspl_sp* sp, const uint8_t* d_images, int batch, int he
  * scores [H*W] f32 after NMS, desc [256*(H/8)*(W/8)] f32 channel-major. */
 int rspl_sp_debug_maps(rspl_sp* sp, int b, float* scores, float* desc);
 
+/* Test hook: the device simple_nms (convert2onnx/superpoint.py:6-33, radius 4) of a host
+ * score map [H][W] (any H, W within the arena) -> out [H][W]. */
+int rspl_sp_debug_nms(rspl_sp* sp, const float* scores, int height, int width, float* out);
+
 /* Per-stage device time (HIP events on the launch stream) summed over the calls
  * made since rspl_sp_profile(sp, 1).  Stages: 0 conv1a+conv1b+pool (fused),
  * 1 conv2a..conv4b, 2 convPa|convDa, 3 1x1 heads (softmax/d2s, L2 norm),
@@ -178,9 +182,28 @@ int rspl_sg_infer_device2(rspl_sg* sg, int batch, const double* d_feat0, const i
 /* Log-assignment Z [(n0+1)*(n1+1)] f32 of the last call, pair p (for tests). */
 int rspl_sg_debug_scores(rspl_sg* sg, int p, float* Z);
 
+/* Sinkhorn health of the device paths.  The persistent log-Sinkhorn exchanges u / v between
+ * co-resident workgroups with bounded spins; a pair whose exchange timed out sets a sticky
+ * flag (its indices / scores are then invalid).  After synchronising the stream the results
+ * were produced on, rspl_sg_status returns RSPL_OK, or RSPL_E_DEVICE with *pair_flags = the
+ * bitmask of the failed pairs (bit 31 = any pair >= 31), and clears the flags.  rspl_sg_infer
+ * and rspl_pm_match check it themselves. */
+int rspl_sg_status(rspl_sg* sg, uint32_t* pair_flags);
+
+/* Test hooks.  rspl_sg_debug_inject(sg, 1, limit): workgroup 0 of pair 0 reports an exchange
+ * timeout at iteration 0 and every spin is bounded by `limit` polls (0 = the default), to
+ * prove the failure reaches the caller.  rspl_sg_debug_sinkhorn: bins (alpha) + log_optimal_transport
+ * (convert2onnx/superglue.py:185-205) of a host score matrix [n0][n1] -> Z [(n0+1)][(n1+1)].
+ * rspl_sg_debug_decode: the device decode (src/super_glue.cpp:258-367) of a host Z. */
+int rspl_sg_debug_inject(rspl_sg* sg, int inject, unsigned spin_limit);
+int rspl_sg_debug_sinkhorn(rspl_sg* sg, const float* scores, int n0, int n1, float alpha, int iters, float* Z);
+int rspl_sg_debug_decode(rspl_sg* sg, const float* Z, int n0, int n1, int32_t* indices0, int32_t* indices1,
+                         double* mscores0, double* mscores1);
+
 /* Stages: 0 prep + keypoint encoder, 1 18 GNN layers, 2 final_proj + scores + bins,
- * 3 log-Sinkhorn, 4 decode. */
-#define RSPL_SG_STAGES 5
+ * 3 hand-over to the post stream (queueing behind the previous call's post work; no kernel),
+ * 4 log-Sinkhorn (one kernel), 5 decode. */
+#define RSPL_SG_STAGES 6
 int rspl_sg_profile(rspl_sg* sg, int enable);
 int rspl_sg_stage_times(rspl_sg* sg, float* ms, int* calls);
 

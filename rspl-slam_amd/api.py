@@ -82,6 +82,14 @@ class SuperPoint:
         """(per-stage summed ms, calls) since profile(True)"""
         return capi.stage_times(None, self._lib.rspl_sp_stage_times, self._h, len(self.STAGES))
 
+    def debug_nms(self, scores: np.ndarray) -> np.ndarray:
+        """The device simple_nms (superpoint.py:6-33) of a host score map."""
+        sc = np.ascontiguousarray(scores, np.float32)
+        out = np.empty_like(sc)
+        capi.check(self._lib.rspl_sp_debug_nms(self._h, sc.ctypes.data, sc.shape[0], sc.shape[1], out.ctypes.data),
+                   "rspl_sp_debug_nms")
+        return out
+
     def debug_maps(self, b: int, height: int, width: int):
         s = np.empty((height, width), np.float32)
         d = np.empty((256, height // 8, width // 8), np.float32)
@@ -152,7 +160,7 @@ class SuperGlue:
                                                        int(normalize), d_idx0, d_idx1, d_ms0, d_ms1, stream,
                                                        post_stream), "rspl_sg_infer_device2")
 
-    STAGES = ("prep+kenc", "gnn x18", "final+scores", "sinkhorn", "decode")
+    STAGES = ("prep+kenc", "gnn x18", "final+scores", "post hand-over", "sinkhorn", "decode")
 
     def profile(self, enable: bool = True):
         capi.check(self._lib.rspl_sg_profile(self._h, int(enable)), "rspl_sg_profile")
@@ -164,6 +172,39 @@ class SuperGlue:
         Z = np.empty((n0 + 1, n1 + 1), np.float32)
         capi.check(self._lib.rspl_sg_debug_scores(self._h, p, Z.ctypes.data), "rspl_sg_debug_scores")
         return Z
+
+    def status(self):
+        """rspl_sg_status: (ok, failed-pair bitmask) of the device paths since the last check
+        (call after synchronising the stream the results were produced on)."""
+        f = C.c_uint32(0)
+        rc = self._lib.rspl_sg_status(self._h, C.byref(f))
+        if rc != 0:
+            self.error = self._lib.rspl_last_error().decode()
+        return rc == 0, f.value
+
+    def debug_inject(self, inject: bool, spin_limit: int = 0):
+        capi.check(self._lib.rspl_sg_debug_inject(self._h, int(inject), spin_limit), "rspl_sg_debug_inject")
+
+    def debug_sinkhorn(self, scores: np.ndarray, alpha: float, iters: int = 100):
+        """bins + log_optimal_transport (superglue.py:185-205) of a host score matrix on the device.
+        Returns (ok, Z)."""
+        sc = np.ascontiguousarray(scores, np.float32)
+        n0, n1 = sc.shape
+        Z = np.empty((n0 + 1, n1 + 1), np.float32)
+        rc = self._lib.rspl_sg_debug_sinkhorn(self._h, sc.ctypes.data, n0, n1, float(alpha), iters, Z.ctypes.data)
+        if rc != 0:
+            self.error = self._lib.rspl_last_error().decode()
+        return rc == 0, Z
+
+    def debug_decode(self, Z: np.ndarray):
+        """The device decode (src/super_glue.cpp:258-367) of a host log-assignment matrix."""
+        z = np.ascontiguousarray(Z, np.float32)
+        n0, n1 = z.shape[0] - 1, z.shape[1] - 1
+        i0, i1 = np.empty(n0, np.int32), np.empty(n1, np.int32)
+        m0, m1 = np.empty(n0, np.float64), np.empty(n1, np.float64)
+        capi.check(self._lib.rspl_sg_debug_decode(self._h, z.ctypes.data, n0, n1, i0.ctypes.data, i1.ctypes.data,
+                                                  m0.ctypes.data, m1.ctypes.data), "rspl_sg_debug_decode")
+        return i0, i1, m0, m1
 
     @property
     def handle(self):

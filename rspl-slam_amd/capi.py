@@ -22,9 +22,10 @@ EXPORTS = [
     "rspl_device_synchronize", "rspl_event_create", "rspl_event_record", "rspl_stream_wait_event",
     "rspl_event_destroy", "rspl_timer_create", "rspl_timer_record", "rspl_timer_elapsed_ms",
     "rspl_timer_destroy",
-    "rspl_sp_create", "rspl_sp_infer", "rspl_sp_infer_device", "rspl_sp_debug_maps", "rspl_sp_profile",
+    "rspl_sp_create", "rspl_sp_infer", "rspl_sp_infer_device", "rspl_sp_debug_maps", "rspl_sp_debug_nms", "rspl_sp_profile",
     "rspl_sp_stage_times", "rspl_sp_destroy",
     "rspl_sg_create", "rspl_sg_infer", "rspl_sg_infer_device", "rspl_sg_infer_device2", "rspl_sg_debug_scores", "rspl_sg_profile",
+    "rspl_sg_status", "rspl_sg_debug_inject", "rspl_sg_debug_sinkhorn", "rspl_sg_debug_decode",
     "rspl_sg_stage_times", "rspl_sg_destroy",
     "rspl_pm_match",
     "rspl_ba_create", "rspl_ba_local", "rspl_ba_destroy", "rspl_ba_use_reserved_cus",
@@ -97,6 +98,7 @@ def load(path: pathlib.Path = LIB_PATH):
     lib.rspl_sp_infer.argtypes = [vp, vp, ip, ip, ip, vp, ip, C.POINTER(ip)]
     lib.rspl_sp_infer_device.argtypes = [vp, vp, ip, ip, ip, ip, C.c_size_t, vp, ip, vp, vp]
     lib.rspl_sp_debug_maps.argtypes = [vp, ip, vp, vp]
+    lib.rspl_sp_debug_nms.argtypes = [vp, vp, ip, ip, vp]
     lib.rspl_sp_destroy.argtypes = [vp]
     lib.rspl_sp_destroy.restype = None
     lib.rspl_device_count.argtypes = [C.POINTER(ip)]
@@ -129,6 +131,10 @@ def load(path: pathlib.Path = LIB_PATH):
         lib.rspl_sg_infer_device.argtypes = [vp, ip, vp, vp, vp, vp, ip, ip, vp, vp, vp, vp, vp]
         lib.rspl_sg_infer_device2.argtypes = [vp, ip, vp, vp, vp, vp, ip, ip, vp, vp, vp, vp, vp, vp]
         lib.rspl_sg_debug_scores.argtypes = [vp, ip, vp]
+        lib.rspl_sg_status.argtypes = [vp, C.POINTER(C.c_uint32)]
+        lib.rspl_sg_debug_inject.argtypes = [vp, ip, C.c_uint]
+        lib.rspl_sg_debug_sinkhorn.argtypes = [vp, vp, ip, ip, C.c_float, ip, vp]
+        lib.rspl_sg_debug_decode.argtypes = [vp, vp, ip, ip, vp, vp, vp, vp]
         lib.rspl_sg_profile.argtypes = [vp, ip]
         lib.rspl_sg_stage_times.argtypes = [vp, C.POINTER(C.c_float), C.POINTER(ip)]
         lib.rspl_sg_destroy.argtypes = [vp]

@@ -39,9 +39,15 @@ struct rspl_sg {
   // RSPL_PREC_FP16 GNN activations: fp16 shadow of X, Q | K, V^T per head, messages, hidden
   _Float16 *Xh, *QKh, *Vth, *Oh, *MSGh, *HIDh;
   int ldv = 0;  // token stride of Vth (nmax rounded up to the 32-key attention tile; zero padded)
-  unsigned long long* part;
-  unsigned* err;
+  unsigned long long *ug, *vg;  // Sinkhorn u / v exchange granules [B][ld]
+  float* cplT = nullptr;        // transposed column slabs when they exceed LDS [B][ld*ld]
+  bool sink_scratch = false;
+  unsigned* err = nullptr;      // [B] sticky Sinkhorn timeout flags, host-mapped (rspl_sg_status)
+  unsigned* d_err = nullptr;    // device alias of err
   unsigned sk_seq = 0;
+  unsigned spin_limit = 1u << 22;
+  int inject = 0;
+  float* dbg_alpha;             // rspl_sg_debug_sinkhorn's bin score
   int *max0, *max1, *n0, *n1;
   int32_t *idx0, *idx1;
   double *ms0, *ms1, *f0, *f1;
@@ -87,9 +93,10 @@ void carve(F& ar, rspl_sg* s) {
   take(s->X, T * 256); take(s->QKV, T * 768); take(s->O, T * 256); take(s->MSG, T * 256); take(s->HID, T * 512);
   take(s->Xh, T * 256); take(s->QKh, T * 512); take(s->Vth, (size_t)B * 2 * 256 * s->ldv); take(s->Oh, T * 256);
   take(s->MSGh, T * 256); take(s->HIDh, T * 512);
-  take(s->cpl, 2 * B * ld * ld); take(s->Z, 2 * B * ld * ld); take(s->part, B * 2 * s->G * ld);
+  take(s->cpl, 2 * B * ld * ld); take(s->Z, 2 * B * ld * ld); take(s->ug, B * ld); take(s->vg, B * ld);
+  if (s->sink_scratch) take(s->cplT, B * ld * ld);
+  take(s->dbg_alpha, 4);
   take(s->cn0, 2 * B); take(s->cn1, 2 * B);
-  take(s->err, B);
   take(s->max0, B * s->nmax); take(s->val0, B * s->nmax); take(s->max1, B * s->nmax);
   take(s->idx0, B * s->nmax); take(s->idx1, B * s->nmax); take(s->ms0, B * s->nmax); take(s->ms1, B * s->nmax);
   take(s->n0, B); take(s->n1, B);
@@ -237,6 +244,35 @@ sg::GemmArgs G_(const float* A, int lda, const float* B, int ldb, const float* b
 
 }  // namespace
 
+// log_optimal_transport (superglue.py:185-205) on the couplings of B pairs, on stream st
+static hipError_t run_sinkhorn(rspl_sg* s, const float* cpl, float* Zp, const int* cn0, const int* cn1, int B,
+                               int iters, hipStream_t st) {
+  static unsigned long long* probe = nullptr;  // debug only (RSPL_SG_PROBE)
+  static const bool probing = getenv("RSPL_SG_PROBE") != nullptr;
+  hipError_t e;
+  if (probing && !probe) {
+    if ((e = hipMalloc(&probe, 5 * sizeof(unsigned long long))) != hipSuccess) return e;
+    if ((e = hipMemset(probe, 0, 5 * sizeof(unsigned long long))) != hipSuccess) return e;
+  }
+  sg::SinkArgs sk{};
+  sk.probe = probe;
+  sk.cpl = cpl; sk.Z = Zp; sk.cplT = s->cplT; sk.ug = s->ug; sk.vg = s->vg;
+  sk.seq = s->sk_seq = (s->sk_seq % 0xFFFFFu) + 1;
+  sk.spin_limit = s->spin_limit; sk.inject = s->inject;
+  sk.err = s->d_err; sk.n0 = cn0; sk.n1 = cn1;
+  sk.nmax = s->nmax; sk.G = s->G; sk.iters = iters;
+  if ((e = sg::sinkhorn(sk, B, st)) != hipSuccess) return e;
+  if (probing) {  // debug: Sinkhorn cycles per workgroup-iteration by phase
+    unsigned long long h[5];
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+    if ((e = hipMemcpy(h, probe, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess) return e;
+    if ((e = hipMemset(probe, 0, sizeof(h))) != hipSuccess) return e;
+    if (h[4]) fprintf(stderr, "sinkhorn cycles/iter (G=%d): row %.0f gather-u %.0f col %.0f gather-v %.0f\n", s->G,
+                      (double)h[0] / h[4], (double)h[1] / h[4], (double)h[2] / h[4], (double)h[3] / h[4]);
+  }
+  return hipSuccess;
+}
+
 extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_path, rspl_sg** out) {
   RSPL_CHECK_ARG(cfg && out, "rspl_sg_create: NULL argument");
   RSPL_CHECK_ARG(cfg->max_keypoints > 0 && cfg->max_keypoints <= 4096, "max_keypoints must be in [1, 4096]");
@@ -256,21 +292,33 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
   s->nmax = cfg->max_keypoints;  // output stride per pair (rspl.h)
   s->ld = s->nmax + 1;
   s->ldv = (s->nmax + 31) / 32 * 32;
-  {  // sinkhorn workgroups per pair: ~26 rows each, a power of two (compile-time fan-in of the exchange)
-    const int g0 = std::max(1, (s->ld + 25) / 26);
-    s->G = 1;
-    while (s->G < g0 && s->G < 32) s->G <<= 1;
-  }
-  if (s->B * s->G > 256) {
-    set_error("max_batch * sinkhorn workgroups (%d) exceeds the CU count: co-residency required", s->B * s->G);
-    delete s;
-    return RSPL_E_ARG;
+  {  // Sinkhorn workgroups per pair: ~kRows rows + columns each, and at least enough that both
+     // slabs fit one workgroup's LDS; all B*G workgroups must be co-resident (one per CU)
+    int ncu = 0;
+    if (hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess || ncu < 1) {
+      set_error("hipDeviceGetAttribute(MultiprocessorCount) failed");
+      delete s;
+      return RSPL_E_DEVICE;
+    }
+    constexpr int kRows = 26;
+    int G = std::max(1, (s->ld + kRows - 1) / kRows);
+    while (G < s->ld && sg::sinkhorn_lds_bytes(s->nmax, G, true) > sg::kSinkLdsMax) G++;
+    if (const char* e = getenv("RSPL_SG_SINK_G")) G = std::max(1, atoi(e));  // tuning knob
+    G = std::min(G, std::max(1, ncu / s->B));
+    s->G = G;
+    s->sink_scratch = sg::sinkhorn_lds_bytes(s->nmax, G, true) > sg::kSinkLdsMax;
+    if (s->B * s->G > ncu) {
+      set_error("max_batch (%d) exceeds the CU count (%d): the Sinkhorn workgroups must be co-resident", s->B, ncu);
+      delete s;
+      return RSPL_E_ARG;
+    }
   }
   Sizer sz;
   carve(sz, s);
   if ((rc = s->arena.reserve(sz.used))) { delete s; return rc; }
   carve(s->arena, s);
-  if (hipMemset(s->part, 0, sizeof(unsigned long long) * 2 * s->B * s->G * s->ld) != hipSuccess ||
+  if (hipMemset(s->ug, 0, sizeof(unsigned long long) * s->B * s->ld) != hipSuccess ||
+      hipMemset(s->vg, 0, sizeof(unsigned long long) * s->B * s->ld) != hipSuccess ||
       hipMemset(s->Vth, 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess) {
     set_error("sinkhorn exchange buffer init failed");
     rspl_sg_destroy(s);
@@ -283,11 +331,14 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
       hipEventCreateWithFlags(&s->ev_sink[1], hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(&s->h_f, sizeof(double) * nm * 259 * 2) != hipSuccess ||
       hipHostMalloc(&s->h_idx, sizeof(int32_t) * nm * 2 + 16) != hipSuccess ||
-      hipHostMalloc(&s->h_ms, sizeof(double) * nm * 2) != hipSuccess) {
+      hipHostMalloc(&s->h_ms, sizeof(double) * nm * 2) != hipSuccess ||
+      hipHostMalloc(&s->err, sizeof(unsigned) * s->B, hipHostMallocMapped) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&s->d_err, s->err, 0) != hipSuccess) {
     set_error("stream / pinned allocation failed");
     rspl_sg_destroy(s);
     return RSPL_E_DEVICE;
   }
+  memset(s->err, 0, sizeof(unsigned) * s->B);
   if ((rc = upload_weights(s, ts))) { rspl_sg_destroy(s); return rc; }
   {  // fp16 transposed copies for RSPL_PREC_FP16 (made on the device from the fp32 layout)
     bool okh = true;
@@ -323,6 +374,7 @@ extern "C" void rspl_sg_destroy(rspl_sg* s) {
   if (s->h_f) (void)hipHostFree(s->h_f);
   if (s->h_idx) (void)hipHostFree(s->h_idx);
   if (s->h_ms) (void)hipHostFree(s->h_ms);
+  if (s->err) (void)hipHostFree(s->err);
   if (s->ev_ready) (void)hipEventDestroy(s->ev_ready);
   for (auto& e : s->ev_sink)
     if (e) (void)hipEventDestroy(e);
@@ -450,34 +502,16 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
     RSPL_HIP(hipStreamWaitEvent(pst, s->ev_ready, 0));
   }
   // log_optimal_transport (superglue.py:185-205)
-  RSPL_HIP(hipMemsetAsync(s->err, 0, sizeof(unsigned) * B, pst));
-  static unsigned long long* probe = nullptr;  // debug only (RSPL_SG_PROBE)
-  static const bool probing = getenv("RSPL_SG_PROBE") != nullptr;
-  if (probing && !probe) {
-    RSPL_HIP(hipMalloc(&probe, 4 * sizeof(unsigned long long)));
-    RSPL_HIP(hipMemset(probe, 0, 4 * sizeof(unsigned long long)));
-  }
-  sg::SinkArgs sk{};
-  sk.probe = probe;
-  sk.cpl = cpl; sk.Z = Zp; sk.part = s->part; sk.seq = s->sk_seq = (s->sk_seq % 0xFFFFFu) + 1; sk.err = s->err; sk.n0 = cn0; sk.n1 = cn1;
-  sk.nmax = nm; sk.G = s->G; sk.iters = s->cfg.sinkhorn_iterations;
-  RSPL_HIP(sg::sinkhorn(sk, B, pst));
+  s->timer.mark(4, pst);  // the Sinkhorn starts here: stage 3 is the post stream's hand-over wait
+  RSPL_HIP(run_sinkhorn(s, cpl, Zp, cn0, cn1, B, s->cfg.sinkhorn_iterations, pst));
   if (pst != st) RSPL_HIP(hipEventRecord(s->ev_sink[par], pst));
-  if (probing) {  // debug: Sinkhorn cycles per workgroup-iteration by phase
-    unsigned long long h[4];
-    RSPL_HIP(hipStreamSynchronize(pst));
-    RSPL_HIP(hipMemcpy(h, probe, sizeof(h), hipMemcpyDeviceToHost));
-    RSPL_HIP(hipMemset(probe, 0, sizeof(h)));
-    if (h[3]) fprintf(stderr, "sinkhorn cycles/iter: row %.0f col %.0f exchange %.0f\n", (double)h[0] / h[3],
-                      (double)h[1] / h[3], (double)h[2] / h[3]);
-  }
-  s->timer.mark(4, pst);
+  s->timer.mark(5, pst);
   // decode (super_glue.cpp:339-367), threshold 0.2 hard-coded as in the reference (:355)
   sg::DecodeArgs dc{};
   dc.Z = Zp; dc.n0 = cn0; dc.n1 = cn1; dc.nmax = nm; dc.max0 = s->max0; dc.val0 = s->val0; dc.max1 = s->max1;
   dc.idx0 = d_idx0; dc.idx1 = d_idx1; dc.ms0 = d_ms0; dc.ms1 = d_ms1; dc.threshold = 0.2f;
   RSPL_HIP(sg::decode(dc, B, pst));
-  s->timer.mark(5, pst);
+  s->timer.mark(6, pst);
   s->timer.end_call();
   s->last_B = B;
   s->last_parity = par;
@@ -503,14 +537,9 @@ static int sg_host_run(rspl_sg* s, const double* f0, int n0, const double* f1, i
   RSPL_HIP(hipMemcpyAsync(s->h_idx + nm, s->idx1, sizeof(int32_t) * n1, hipMemcpyDeviceToHost, s->stream));
   RSPL_HIP(hipMemcpyAsync(s->h_ms, s->ms0, sizeof(double) * n0, hipMemcpyDeviceToHost, s->stream));
   RSPL_HIP(hipMemcpyAsync(s->h_ms + nm, s->ms1, sizeof(double) * n1, hipMemcpyDeviceToHost, s->stream));
-  unsigned err = 0;
-  RSPL_HIP(hipMemcpyAsync(s->h_idx + 2 * nm, s->err, sizeof(unsigned), hipMemcpyDeviceToHost, s->stream));
   RSPL_HIP(hipStreamSynchronize(s->stream));
-  memcpy(&err, s->h_idx + 2 * nm, sizeof(unsigned));
-  if (err) {
-    set_error("sinkhorn: cross-workgroup exchange timed out");
-    return RSPL_E_DEVICE;
-  }
+  unsigned flags = 0;
+  if (int rc2 = rspl_sg_status(s, &flags)) return rc2;
   s->last_n0 = n0;
   s->last_n1 = n1;
   if (n0 == 0 || n1 == 0) {  // no couplings: every keypoint unmatched
@@ -583,4 +612,77 @@ extern "C" int rspl_sg_profile(rspl_sg* s, int enable) {
 extern "C" int rspl_sg_stage_times(rspl_sg* s, float* ms, int* calls) {
   RSPL_CHECK_ARG(s && ms, "NULL argument");
   return s->timer.query(ms, calls);
+}
+
+extern "C" int rspl_sg_status(rspl_sg* s, uint32_t* pair_flags) {
+  RSPL_CHECK_ARG(s, "rspl_sg_status: NULL handle");
+  uint32_t f = 0;
+  for (int p = 0; p < s->B; p++) {
+    volatile unsigned* e = s->err + p;
+    if (*e) f |= p < 32 ? (1u << p) : 0x80000000u;
+    *e = 0;
+  }
+  if (pair_flags) *pair_flags = f;
+  if (f) {
+    set_error("sinkhorn: cross-workgroup exchange timed out (pair mask 0x%x); results of those pairs are invalid", f);
+    return RSPL_E_DEVICE;
+  }
+  return RSPL_OK;
+}
+
+extern "C" int rspl_sg_debug_inject(rspl_sg* s, int inject, unsigned spin_limit) {
+  RSPL_CHECK_ARG(s, "NULL handle");
+  s->inject = inject != 0;
+  s->spin_limit = spin_limit ? spin_limit : (1u << 22);
+  return RSPL_OK;
+}
+
+extern "C" int rspl_sg_debug_sinkhorn(rspl_sg* s, const float* scores, int n0, int n1, float alpha, int iters,
+                                      float* Z) {
+  RSPL_CHECK_ARG(s && scores && Z, "rspl_sg_debug_sinkhorn: NULL argument");
+  RSPL_CHECK_ARG(n0 >= 1 && n1 >= 1 && n0 <= s->nmax && n1 <= s->nmax && iters >= 0, "bad shape");
+  const size_t ld = s->ld;
+  hipStream_t st = s->stream;
+  RSPL_HIP(hipStreamSynchronize(st));
+  int cnt[2] = {n0, n1};
+  const float al[4] = {alpha, 0.f, 0.f, 0.f};
+  RSPL_HIP(hipMemcpy2DAsync(s->cpl, sizeof(float) * ld, scores, sizeof(float) * n1, sizeof(float) * n1, n0,
+                            hipMemcpyHostToDevice, st));
+  RSPL_HIP(hipMemcpyAsync(s->cn0, &cnt[0], sizeof(int), hipMemcpyHostToDevice, st));
+  RSPL_HIP(hipMemcpyAsync(s->cn1, &cnt[1], sizeof(int), hipMemcpyHostToDevice, st));
+  RSPL_HIP(hipMemcpyAsync(s->dbg_alpha, al, sizeof(al), hipMemcpyHostToDevice, st));
+  sg::BinsArgs bn{};
+  bn.cpl = s->cpl; bn.n0 = s->cn0; bn.n1 = s->cn1; bn.alpha = s->dbg_alpha; bn.nmax = s->nmax;
+  RSPL_HIP(sg::bins(bn, 1, st));
+  RSPL_HIP(run_sinkhorn(s, s->cpl, s->Z, s->cn0, s->cn1, 1, iters, st));
+  RSPL_HIP(hipMemcpy2DAsync(Z, sizeof(float) * (n1 + 1), s->Z, sizeof(float) * ld, sizeof(float) * (n1 + 1), n0 + 1,
+                            hipMemcpyDeviceToHost, st));
+  RSPL_HIP(hipStreamSynchronize(st));
+  s->last_B = 0;  // the debug call reused pair 0's buffers
+  return rspl_sg_status(s, nullptr);
+}
+
+extern "C" int rspl_sg_debug_decode(rspl_sg* s, const float* Z, int n0, int n1, int32_t* indices0, int32_t* indices1,
+                                    double* mscores0, double* mscores1) {
+  RSPL_CHECK_ARG(s && Z && indices0 && indices1 && mscores0 && mscores1, "rspl_sg_debug_decode: NULL argument");
+  RSPL_CHECK_ARG(n0 >= 1 && n1 >= 1 && n0 <= s->nmax && n1 <= s->nmax, "bad shape");
+  const size_t ld = s->ld;
+  hipStream_t st = s->stream;
+  RSPL_HIP(hipStreamSynchronize(st));
+  int cnt[2] = {n0, n1};
+  RSPL_HIP(hipMemcpy2DAsync(s->Z, sizeof(float) * ld, Z, sizeof(float) * (n1 + 1), sizeof(float) * (n1 + 1), n0 + 1,
+                            hipMemcpyHostToDevice, st));
+  RSPL_HIP(hipMemcpyAsync(s->cn0, &cnt[0], sizeof(int), hipMemcpyHostToDevice, st));
+  RSPL_HIP(hipMemcpyAsync(s->cn1, &cnt[1], sizeof(int), hipMemcpyHostToDevice, st));
+  sg::DecodeArgs dc{};
+  dc.Z = s->Z; dc.n0 = s->cn0; dc.n1 = s->cn1; dc.nmax = s->nmax; dc.max0 = s->max0; dc.val0 = s->val0;
+  dc.max1 = s->max1; dc.idx0 = s->idx0; dc.idx1 = s->idx1; dc.ms0 = s->ms0; dc.ms1 = s->ms1; dc.threshold = 0.2f;
+  RSPL_HIP(sg::decode(dc, 1, st));
+  RSPL_HIP(hipMemcpyAsync(indices0, s->idx0, sizeof(int32_t) * n0, hipMemcpyDeviceToHost, st));
+  RSPL_HIP(hipMemcpyAsync(indices1, s->idx1, sizeof(int32_t) * n1, hipMemcpyDeviceToHost, st));
+  RSPL_HIP(hipMemcpyAsync(mscores0, s->ms0, sizeof(double) * n0, hipMemcpyDeviceToHost, st));
+  RSPL_HIP(hipMemcpyAsync(mscores1, s->ms1, sizeof(double) * n1, hipMemcpyDeviceToHost, st));
+  RSPL_HIP(hipStreamSynchronize(st));
+  s->last_B = 0;
+  return RSPL_OK;
 }

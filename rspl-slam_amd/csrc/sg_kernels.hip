@@ -807,11 +807,18 @@ __global__ void bins_kernel(BinsArgs a) {
 
 // ---------------------------------------------------------------------------
 // Persistent log-domain Sinkhorn (superglue.py:176-205).
-// G workgroups per pair; workgroup g owns a slab of rows (held in LDS when it
-// fits).  Per iteration: u for own rows (row LSE) -> per-slab column LSE
-// partials published write-through (sc1) -> one arrival counter -> every
-// workgroup combines the G partials into v.  One cross-workgroup exchange per
-// iteration; spins are bounded (timeout flag, no hang).
+// G workgroups per pair (one per CU, co-resident); workgroup g owns a slab of
+// rows AND a slab of columns of the couplings, both held in LDS when they fit
+// (the column slab transposed, so both passes read contiguous LDS rows).
+// Per iteration (u = log_mu - LSE_row(C + v); v = log_nu - LSE_col(C + u)):
+//   row pass over the own rows -> publish own u as tagged granules -> all-gather u
+//   column pass over the own columns -> publish own v -> all-gather v.
+// Two hand-offs of (N+1) 8-byte granules {f32 bits, tag} per workgroup and
+// iteration (a single write-through store each; no flags, no counters).  One
+// buffer per vector suffices: a workgroup can only publish u(it+1) after every
+// workgroup has published v(it), i.e. finished reading u(it).  Spins are bounded:
+// a timed-out workgroup raises the pair's sticky error flag (host-mapped, read by
+// rspl_sg_status) and leaves the loop, so every wave reaches the kernel end.
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ float wave_max(float v) {
 #pragma unroll
@@ -853,179 +860,213 @@ __device__ __forceinline__ float ld_sc1(const float* p) {
       __hip_atomic_load(reinterpret_cast<const unsigned*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
 }
 
-constexpr int kSinkThreads = 1024;  // 4 waves per SIMD: latency hiding for the LDS/exp chains
+constexpr int kSinkThreads = 1024;  // 16 waves: one wave per slab row / column in flight
 
-template <bool SLAB_IN_LDS, int G>
+__device__ __forceinline__ unsigned long long sk_granule(float v, unsigned tag) {
+  return ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(v);
+}
+
+// LSE over len values x[k] + w[k] (x, w in LDS, or x global) of NR rows at once by one wave
+// (independent chains interleaved: the DPP reductions and exps of the rows overlap); rows of
+// up to 512 values stay in registers between the max and the exp pass.  Lane-uniform results.
+template <int NR>
+__device__ __forceinline__ void wave_lse(const float* const (&x)[NR], const float* w, int len, int lane,
+                                         float (&out)[NR]) {
+  float mx[NR], s[NR];
+  if (len <= 512) {
+    float t[NR][8];
+#pragma unroll
+    for (int r = 0; r < NR; r++)
+#pragma unroll
+      for (int q = 0; q < 8; q++) {
+        const int j = lane + 64 * q;
+        t[r][q] = j < len ? x[r][j] + w[j] : -INFINITY;
+      }
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      mx[r] = t[r][0];
+#pragma unroll
+      for (int q = 1; q < 8; q++) mx[r] = fmaxf(mx[r], t[r][q]);
+    }
+#pragma unroll
+    for (int r = 0; r < NR; r++) mx[r] = wave_max_dpp(mx[r]);
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      s[r] = 0.f;
+#pragma unroll
+      for (int q = 0; q < 8; q++) s[r] += (lane + 64 * q) < len ? expf(t[r][q] - mx[r]) : 0.f;
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < NR; r++) mx[r] = -INFINITY;
+    for (int j0 = 0; j0 < len; j0 += 512)
+#pragma unroll
+      for (int r = 0; r < NR; r++)
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const int j = j0 + lane + 64 * q;
+          if (j < len) mx[r] = fmaxf(mx[r], x[r][j] + w[j]);
+        }
+#pragma unroll
+    for (int r = 0; r < NR; r++) {
+      mx[r] = wave_max_dpp(mx[r]);
+      s[r] = 0.f;
+    }
+    for (int j0 = 0; j0 < len; j0 += 512)
+#pragma unroll
+      for (int r = 0; r < NR; r++)
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+          const int j = j0 + lane + 64 * q;
+          if (j < len) s[r] += expf(x[r][j] + w[j] - mx[r]);
+        }
+  }
+#pragma unroll
+  for (int r = 0; r < NR; r++) s[r] = wave_sum_dpp(s[r]);
+#pragma unroll
+  for (int r = 0; r < NR; r++) out[r] = logf(s[r]) + mx[r];
+}
+
+// One LSE pass over the n rows of a slab (stride ld) by the workgroup's waves: wave wv takes rows
+// wv and wv + NW together.  Lane 0 of the owning wave gets each row's LSE in fn(row, lse).
+template <typename F>
+__device__ __forceinline__ void slab_lse(const float* slab, int ld, const float* w, int len, int n, int wv, int lane,
+                                         F&& fn) {
+  constexpr int NW = kSinkThreads / 64;
+  for (int r = wv; r < n; r += 2 * NW) {
+    if (r + NW < n) {
+      const float* const xs[2] = {slab + (size_t)r * ld, slab + (size_t)(r + NW) * ld};
+      float o[2];
+      wave_lse<2>(xs, w, len, lane, o);
+      fn(r, o[0]);
+      fn(r + NW, o[1]);
+    } else {
+      const float* const xs[1] = {slab + (size_t)r * ld};
+      float o[1];
+      wave_lse<1>(xs, w, len, lane, o);
+      fn(r, o[0]);
+    }
+  }
+}
+
+// All-gather of a vector published as tagged granules: dst[j] for j in [0, len) outside the
+// caller's own range [o0, o1).  Every thread polls its granules (all loads in flight, only
+// the stale ones re-read), bounded by spin_limit.  Returns true on timeout.
+__device__ __forceinline__ bool sk_gather(const unsigned long long* src, float* dst, int len, int o0, int o1,
+                                          unsigned tag, unsigned spin_limit) {
+  bool timed_out = false;
+  for (int j = threadIdx.x; j < len; j += kSinkThreads) {
+    if (j >= o0 && j < o1) continue;
+    unsigned long long gv = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    unsigned spins = 0;
+    while ((unsigned)(gv >> 32) != tag) {
+      if (++spins > spin_limit) {
+        timed_out = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      gv = __hip_atomic_load(src + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    dst[j] = __uint_as_float((unsigned)gv);
+  }
+  return timed_out;
+}
+
+template <bool SLAB_IN_LDS>
 __global__ __launch_bounds__(kSinkThreads) void sinkhorn_kernel(SinkArgs a) {
   extern __shared__ float sm[];
-  const int p = blockIdx.y, g = blockIdx.x;
+  const int p = blockIdx.y, g = blockIdx.x, G = gridDim.x;
   const int m = a.n0[p], n = a.n1[p];
   if (m <= 0 || n <= 0) return;
-  const int R = m + 1, Cc = n + 1, ld = a.nmax + 1;
-  const int rows = (R + G - 1) / G;
-  const int r0 = g * rows;
-  const int nr = max(0, min(R, r0 + rows) - r0);
-  constexpr int NW = kSinkThreads / 64;
+  const int R = m + 1, Cc = n + 1, ld = a.nmax + 1, ldp = (ld + 3) & ~3;
+  const int rs = (R + G - 1) / G, cs = (Cc + G - 1) / G;
+  const int r0 = min(R, g * rs), nr = min(R, r0 + rs) - r0;
+  const int c0 = min(Cc, g * cs), nc = min(Cc, c0 + cs) - c0;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const float* Cg = a.cpl + (size_t)p * ld * ld + (size_t)r0 * ld;
-  float* u = sm;
-  float* v = u + rows;
-  float* flag = v + ld;     // timeout broadcast
-  float* cm = flag + 1;     // [2][512] column half-partials: max
-  float* cs = cm + 1024;    //                                sum
-  float* Cs = cs + 1024;    // slab, only used when SLAB_IN_LDS
-  const float* Cr = SLAB_IN_LDS ? Cs : Cg;
+  const float* Cg = a.cpl + (size_t)p * ld * ld;
+  float* u = sm;                                   // [ld] full u
+  float* v = u + ldp;                              // [ld] full v
+  int* flag = reinterpret_cast<int*>(v + ldp);     // [2] timeout broadcast: u exchange, v exchange
+  float* Rs;                                       // [nr][ld] own rows
+  float* Cs;                                       // [nc][ld] own columns, transposed
+  if constexpr (SLAB_IN_LDS) {
+    Rs = v + ldp + 4;
+    Cs = Rs + (size_t)rs * ld;
+  } else {  // slabs too large for LDS: rows read in place, columns from a transposed scratch copy
+    Rs = const_cast<float*>(Cg) + (size_t)r0 * ld;
+    Cs = a.cplT + (size_t)p * ld * ld + (size_t)c0 * ld;
+  }
   if constexpr (SLAB_IN_LDS) {
     for (int i = tid; i < nr * Cc; i += kSinkThreads) {
       const int r = i / Cc, j = i - r * Cc;
-      Cs[r * ld + j] = Cg[(size_t)r * ld + j];
+      Rs[r * ld + j] = Cg[(size_t)(r0 + r) * ld + j];
     }
   }
+  if (nc > 0)
+    for (int i = tid; i < R * nc; i += kSinkThreads) {  // consecutive threads: consecutive columns of a row
+      const int r = i / nc, c = i - r * nc;
+      Cs[(size_t)c * ld + r] = Cg[(size_t)r * ld + c0 + c];
+    }
   for (int j = tid; j < Cc; j += kSinkThreads) v[j] = 0.f;
   // log_mu / log_nu (superglue.py:198-200), float arithmetic as the module
   const float fm = (float)m, fn = (float)n;
   const float norm = -logf(fm + fn);
   const float lmu_bin = logf(fn) + norm, lnu_bin = logf(fm) + norm;
-  if (tid == 0) *flag = 0.f;
-  __syncthreads();
-  const int half = tid >> 9, jj = tid & 511;
-  const int rh = (nr + 1) >> 1, ra = half ? rh : 0, rb = half ? nr : rh;
-  long long pr_row = 0, pr_col = 0, pr_ex = 0;
+  if (tid < 2) flag[tid] = 0;
+  __syncthreads();  // also orders the transposed scratch copy (workgroup-private) before its reads
+  unsigned long long* ug = a.ug + (size_t)p * ld;
+  unsigned long long* vg = a.vg + (size_t)p * ld;
+  long long pr[4] = {0, 0, 0, 0};
+  // one flag slot per exchange: a slot is rewritten only after a barrier every thread passes
+  // after reading it, so all threads take the same branch
+  bool failed = false;
   for (int it = 0; it < a.iters; it++) {
-    const long long q0 = __builtin_amdgcn_s_memtime();
-    // u_i = log_mu_i - LSE_j(C_ij + v_j): one wave per row; each lane's 8-column chunk is
-    // loaded into registers first (all loads in flight), then max, then independent exps
-    for (int r = wv; r < nr; r += NW) {
-      const float* row = Cr + (size_t)r * ld;
-      float mx = -INFINITY;
-      for (int j0 = 0; j0 < Cc; j0 += 512) {
-        float x[8];
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-          const int j = j0 + lane + 64 * t;
-          x[t] = j < Cc ? row[j] + v[j] : -INFINITY;
-        }
-#pragma unroll
-        for (int t = 0; t < 8; t++) mx = fmaxf(mx, x[t]);
-      }
-      mx = wave_max_dpp(mx);
-      float s = 0.f;
-      for (int j0 = 0; j0 < Cc; j0 += 512) {
-        float e[8];
-#pragma unroll
-        for (int t = 0; t < 8; t++) {
-          const int j = j0 + lane + 64 * t;
-          e[t] = j < Cc ? expf(row[j] + v[j] - mx) : 0.f;
-        }
-#pragma unroll
-        for (int t = 0; t < 8; t++) s += e[t];
-      }
-      s = wave_sum_dpp(s);
-      if (lane == 0) u[r] = ((r0 + r) < m ? norm : lmu_bin) - (logf(s) + mx);
-    }
-    __syncthreads();
-    const long long q1 = __builtin_amdgcn_s_memtime();
-    // column partial LSE over this slab (two row halves merged in LDS), published as tagged
-    // 8-byte granules (value + tag in one single-copy-atomic write-through store: no flag,
-    // no arrival counter); slots double-buffered by iteration parity
-    unsigned long long* part = a.part + ((size_t)(p * 2 + (it & 1)) * G) * ld;
     const unsigned tag = (a.seq << 12) | (unsigned)(it + 1);
-    for (int c0 = 0; c0 < Cc; c0 += 512) {
-      const int j = c0 + jj;
-      if (j < Cc) {  // rows in register batches of 16: loads in flight together, independent exps
-        float mx = -INFINITY, s = 0.f;
-        for (int rb0 = ra; rb0 < rb; rb0 += 16) {
-          float x[16];
-#pragma unroll
-          for (int t = 0; t < 16; t++) {
-            const int r = rb0 + t;
-            x[t] = r < rb ? Cr[(size_t)r * ld + j] + u[r] : -INFINITY;
-          }
-          float bm = -INFINITY;
-#pragma unroll
-          for (int t = 0; t < 16; t++) bm = fmaxf(bm, x[t]);
-          const float nm = fmaxf(mx, bm);
-          float bs = 0.f;
-#pragma unroll
-          for (int t = 0; t < 16; t++) bs += x[t] == -INFINITY ? 0.f : expf(x[t] - nm);
-          s = (mx == -INFINITY ? 0.f : s * expf(mx - nm)) + bs;
-          mx = nm;
-        }
-        cm[half * 512 + jj] = mx;
-        cs[half * 512 + jj] = s;
+    const long long q0 = __builtin_amdgcn_s_memtime();
+    // u_i = log_mu_i - LSE_j(C_ij + v_j), own rows, one wave per row
+    slab_lse(Rs, ld, v, Cc, nr, wv, lane, [&](int r, float lse) {
+      if (lane == 0) {
+        const float ui = ((r0 + r) < m ? norm : lmu_bin) - lse;
+        u[r0 + r] = ui;
+        __hip_atomic_store(ug + r0 + r, sk_granule(ui, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      __syncthreads();
-      if (half == 0 && j < Cc) {
-        const float m0 = cm[jj], m1 = cm[512 + jj];
-        const float M = fmaxf(m0, m1);
-        float s = 0.f;
-        if (m0 != -INFINITY) s += cs[jj] * expf(m0 - M);
-        if (m1 != -INFINITY) s += cs[512 + jj] * expf(m1 - M);
-        const float lse = M == -INFINITY ? -INFINITY : logf(s) + M;
-        __hip_atomic_store(part + (size_t)g * ld + j,
-                           ((unsigned long long)tag << 32) | (unsigned long long)__float_as_uint(lse),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      __syncthreads();
-    }
-    const long long q2 = __builtin_amdgcn_s_memtime();
-    // v_j = log_nu_j - LSE_g(partial_g,j): poll the G granules of a column (all loads in
-    // flight together; only the stale ones are re-read), bounded
-    bool timed_out = false;
-    for (int j = tid; j < Cc; j += kSinkThreads) {
-      unsigned long long gv[G];
-#pragma unroll
-      for (int gg = 0; gg < G; gg++)
-        gv[gg] = __hip_atomic_load(part + (size_t)gg * ld + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      unsigned spins = 0;
-      for (;;) {
-        bool ready = true;
-#pragma unroll
-        for (int gg = 0; gg < G; gg++) ready = ready && (unsigned)(gv[gg] >> 32) == tag;
-        if (ready) break;
-        if (++spins > (1u << 22)) {
-          timed_out = true;
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-#pragma unroll
-        for (int gg = 0; gg < G; gg++)
-          if ((unsigned)(gv[gg] >> 32) != tag)
-            gv[gg] = __hip_atomic_load(part + (size_t)gg * ld + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      float mx = -INFINITY;
-#pragma unroll
-      for (int gg = 0; gg < G; gg++) mx = fmaxf(mx, __uint_as_float((unsigned)gv[gg]));
-      float s = 0.f;
-#pragma unroll
-      for (int gg = 0; gg < G; gg++) {
-        const float pv = __uint_as_float((unsigned)gv[gg]);
-        s += pv == -INFINITY ? 0.f : expf(pv - mx);
-      }
-      v[j] = (j < n ? norm : lnu_bin) - (logf(s) + mx);
-    }
-    if (timed_out) {
-      __hip_atomic_store(a.err + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = 1.f;
-    }
+    });
+    const long long q1 = __builtin_amdgcn_s_memtime();
+    bool to = sk_gather(ug, u, R, r0, r0 + nr, tag, a.spin_limit);
+    if (a.inject && p == 0 && g == 0 && it == 0) to = true;  // fault injection (rspl_sg_debug_inject)
+    if (to) flag[0] = 1;
     __syncthreads();
+    if (flag[0]) { failed = true; break; }
+    const long long q2 = __builtin_amdgcn_s_memtime();
+    // v_j = log_nu_j - LSE_i(C_ij + u_i), own columns, one wave per column
+    slab_lse(Cs, ld, u, R, nc, wv, lane, [&](int c, float lse) {
+      if (lane == 0) {
+        const float vj = ((c0 + c) < n ? norm : lnu_bin) - lse;
+        v[c0 + c] = vj;
+        __hip_atomic_store(vg + c0 + c, sk_granule(vj, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    });
     const long long q3 = __builtin_amdgcn_s_memtime();
-    pr_row += q1 - q0;
-    pr_col += q2 - q1;
-    pr_ex += q3 - q2;
-    if (*flag != 0.f) break;
+    if (sk_gather(vg, v, Cc, c0, c0 + nc, tag, a.spin_limit)) flag[1] = 1;
+    __syncthreads();
+    const long long q4 = __builtin_amdgcn_s_memtime();
+    pr[0] += q1 - q0; pr[1] += q2 - q1; pr[2] += q3 - q2; pr[3] += q4 - q3;
+    if (flag[1]) { failed = true; break; }
+  }
+  if (failed) {
+    if (tid == 0) __hip_atomic_store(a.err + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
   }
   if (a.probe && tid == 0) {
-    atomicAdd(a.probe + 0, (unsigned long long)pr_row);
-    atomicAdd(a.probe + 1, (unsigned long long)pr_col);
-    atomicAdd(a.probe + 2, (unsigned long long)pr_ex);
-    atomicAdd(a.probe + 3, (unsigned long long)a.iters);
+#pragma unroll
+    for (int k = 0; k < 4; k++) atomicAdd(a.probe + k, (unsigned long long)pr[k]);
+    atomicAdd(a.probe + 4, (unsigned long long)a.iters);
   }
-  // Z = couplings + u + v - norm
-  float* Z = a.Z + (size_t)p * ld * ld + (size_t)r0 * ld;
+  // Z = ((couplings + u) + v) - norm (superglue.py:203, :219), own rows
+  float* Z = a.Z + (size_t)p * ld * ld;
   for (int i = tid; i < nr * Cc; i += kSinkThreads) {
     const int r = i / Cc, j = i - r * Cc;
-    Z[(size_t)r * ld + j] = ((Cr[(size_t)r * ld + j] + u[r]) + v[j]) - norm;
+    Z[(size_t)(r0 + r) * ld + j] = ((Rs[(size_t)r * ld + j] + u[r0 + r]) + v[j]) - norm;
   }
 }
 
@@ -1242,43 +1283,29 @@ hipError_t bins(const BinsArgs& a, int B, hipStream_t s) {
   return hipGetLastError();
 }
 
-static size_t slab_rows(int nmax, int G) { return (size_t)(nmax + 1 + G - 1) / G; }
-
-size_t sinkhorn_lds_bytes(int nmax, int G) {
-  const size_t ld = nmax + 1, rows = slab_rows(nmax, G);
-  return sizeof(float) * (rows + ld + 1 + 2048 + rows * ld);  // u, v, flag, column halves, slab
+size_t sinkhorn_lds_bytes(int nmax, int G, bool slabs) {
+  const size_t ld = nmax + 1, ldp = (ld + 3) & ~size_t(3), per = (ld + G - 1) / G;
+  return sizeof(float) * (2 * ldp + 4 + (slabs ? 2 * per * ld : 0));
 }
 
-template <int G>
-static hipError_t sinkhorn_g(const SinkArgs& a, int B, hipStream_t s) {
-  const size_t ld = a.nmax + 1, rows = slab_rows(a.nmax, G);
-  const size_t full = sinkhorn_lds_bytes(a.nmax, G);
-  dim3 grid(G, B);
-  if (full <= 96 * 1024) {
+hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s) {
+  if (a.G < 1 || a.G > 1024) return hipErrorInvalidValue;
+  dim3 grid(a.G, B);
+  const size_t full = sinkhorn_lds_bytes(a.nmax, a.G, true);
+  if (full <= kSinkLdsMax) {
     static size_t attr = 0;
     if (attr < full) {
-      hipError_t e = hipFuncSetAttribute((const void*)sinkhorn_kernel<true, G>,
+      hipError_t e = hipFuncSetAttribute((const void*)sinkhorn_kernel<true>,
                                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)full);
       if (e != hipSuccess) return e;
       attr = full;
     }
-    hipLaunchKernelGGL((sinkhorn_kernel<true, G>), grid, dim3(kSinkThreads), full, s, a);
+    hipLaunchKernelGGL((sinkhorn_kernel<true>), grid, dim3(kSinkThreads), full, s, a);
   } else {
-    hipLaunchKernelGGL((sinkhorn_kernel<false, G>), grid, dim3(kSinkThreads), sizeof(float) * (rows + ld + 1 + 2048), s, a);
+    if (!a.cplT) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((sinkhorn_kernel<false>), grid, dim3(kSinkThreads), sinkhorn_lds_bytes(a.nmax, a.G, false), s, a);
   }
   return hipGetLastError();
-}
-
-hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s) {
-  switch (a.G) {
-    case 1: return sinkhorn_g<1>(a, B, s);
-    case 2: return sinkhorn_g<2>(a, B, s);
-    case 4: return sinkhorn_g<4>(a, B, s);
-    case 8: return sinkhorn_g<8>(a, B, s);
-    case 16: return sinkhorn_g<16>(a, B, s);
-    case 32: return sinkhorn_g<32>(a, B, s);
-    default: return hipErrorInvalidValue;
-  }
 }
 
 hipError_t decode(const DecodeArgs& a, int B, hipStream_t s) {

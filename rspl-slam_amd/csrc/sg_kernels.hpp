@@ -100,10 +100,14 @@ struct BinsArgs {
 struct SinkArgs {
   const float* cpl;   // couplings [B][ld*ld]
   float* Z;           // [B][ld*ld]
-  unsigned long long* part;  // [B][2][G][ld] tagged column partial LSEs {f32 bits, tag}
+  float* cplT;        // [B][ld*ld] transposed column slabs (scratch; only when the slabs exceed LDS)
+  unsigned long long* ug;  // [B][ld] tagged u granules {f32 bits, tag}
+  unsigned long long* vg;  // [B][ld] tagged v granules
   unsigned seq;       // per-call tag base (never 0; granules start zeroed)
-  unsigned long long* probe;  // optional [4] cycle counters (RSPL_SG_PROBE): row, col, exchange, iters
-  unsigned* err;      // [B] timeout flags
+  unsigned spin_limit;  // bounded polls per granule before the exchange is declared timed out
+  int inject;         // debug: workgroup 0 of pair 0 reports a timeout at iteration 0
+  unsigned long long* probe;  // optional [5] cycle counters (RSPL_SG_PROBE): row, gather u, col, gather v, iters
+  unsigned* err;      // [B] sticky timeout flags (host-mapped)
   const int* n0;
   const int* n1;
   int nmax, G, iters;
@@ -136,7 +140,9 @@ hipError_t attention(const AttnArgs& a, int B, hipStream_t s);
 hipError_t bins(const BinsArgs& a, int B, hipStream_t s);
 hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s);
 hipError_t decode(const DecodeArgs& a, int B, hipStream_t s);
-size_t sinkhorn_lds_bytes(int nmax, int G);
+// LDS bytes of one Sinkhorn workgroup (with or without the row / column slabs)
+size_t sinkhorn_lds_bytes(int nmax, int G, bool slabs);
+constexpr size_t kSinkLdsMax = 150 * 1024;  // slab budget per workgroup (160 KB LDS per CU)
 
 }  // namespace sg
 }  // namespace rspl

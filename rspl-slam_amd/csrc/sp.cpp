@@ -117,8 +117,9 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
   const int B = s->cfg.max_batch, H = cfg->max_height, W = cfg->max_width;
   RSPL_CHECK_ARG(cfg->max_keypoints <= kCandCap, "max_keypoints must be <= %d", kCandCap);
   s->feat_cap = cfg->max_keypoints > 0 ? cfg->max_keypoints : kCandCap;
-  // simple_nms keeps 9x9 local maxima: one survivor per 4x4 pixels is a generous bound (plateaus)
-  s->cand_cap = std::max(kCandCap, H * W / 16);
+  // one slot per pixel: the candidate buffer cannot overflow whatever survives simple_nms
+  // (flat plateaus keep every tied pixel), so no device path ever truncates it
+  s->cand_cap = std::max(kCandCap, H * W);
   Sizer sz;
   carve(sz, s, B, H, W, s->feat_cap);
   if ((rc = s->arena.reserve(sz.used))) { delete s; return rc; }
@@ -373,4 +374,22 @@ extern "C" int rspl_sp_profile(rspl_sp* s, int enable) {
 extern "C" int rspl_sp_stage_times(rspl_sp* s, float* ms, int* calls) {
   RSPL_CHECK_ARG(s && ms, "NULL argument");
   return s->timer.query(ms, calls);
+}
+
+extern "C" int rspl_sp_debug_nms(rspl_sp* s, const float* scores, int H, int W, float* out) {
+  RSPL_CHECK_ARG(s && scores && out, "rspl_sp_debug_nms: NULL argument");
+  RSPL_CHECK_ARG(H > 0 && W > 0 && H <= s->cfg.max_height && W <= s->cfg.max_width, "map %dx%d outside %dx%d", H, W,
+                 s->cfg.max_height, s->cfg.max_width);
+  hipStream_t st = s->stream;
+  RSPL_HIP(hipStreamSynchronize(st));
+  RSPL_HIP(hipMemcpyAsync(s->scores, scores, sizeof(float) * H * W, hipMemcpyHostToDevice, st));
+  RSPL_HIP(hipMemsetAsync(s->cand_count, 0, sizeof(int), st));
+  sp::NmsArgs n{};
+  n.scores = s->scores; n.nms_out = s->nms; n.cand = s->cand; n.cand_count = s->cand_count; n.cand_cap = s->cand_cap;
+  n.H = H; n.W = W; n.threshold = s->cfg.keypoint_threshold; n.border = s->cfg.remove_borders;
+  RSPL_HIP(sp::nms(n, 1, st));
+  RSPL_HIP(hipMemcpyAsync(out, s->nms, sizeof(float) * H * W, hipMemcpyDeviceToHost, st));
+  RSPL_HIP(hipStreamSynchronize(st));
+  s->last_B = 0;
+  return RSPL_OK;
 }

@@ -23,3 +23,37 @@ def compare_features(F, G, score_atol=1e-5, desc_atol=1e-5, desc_rtol=1e-3, orde
     moved = np.nonzero(perm != np.arange(len(perm)))[0]
     for i in moved:
         assert abs(G[0, i] - G[0, perm[i]]) < order_atol, f"order differs beyond score tolerance at column {i}"
+
+
+def unexplained_match_disagreements(Zo, i0, i1, i0r, i1r, tol):
+    """Rows / columns whose match index differs from the oracle's and that the oracle's own Z does
+    NOT show as a near-tie (indices identical except at ties within the Z tolerance).
+
+    Z is the (N+1) x (M+1) log-assignment of the oracle; decode (src/super_glue.cpp:258-367) can only
+    flip where (a) a row or column argmax has a runner-up within tol, or (b) the kept score sits
+    within tol of the 0.2 threshold (log space).  Returns the unexplained (kind, index) list."""
+    Z = np.asarray(Zo, np.float64)[:-1, :-1]
+    N, M = Z.shape
+    lthr = np.log(0.2)
+
+    def gap(v):
+        if v.size < 2:
+            return np.inf
+        t = np.partition(v, -2)[-2:]
+        return t[1] - t[0]
+    rowgap = np.array([gap(Z[i]) for i in range(N)])
+    colgap = np.array([gap(Z[:, j]) for j in range(M)])
+    amax0, amax1 = Z.argmax(1), Z.argmax(0)
+
+    def row_near(i):
+        j = amax0[i]
+        return rowgap[i] < tol or colgap[j] < tol or abs(Z[i, j] - lthr) < tol or \
+            (i0[i] >= 0 and colgap[i0[i]] < tol) or (i0r[i] >= 0 and colgap[i0r[i]] < tol)
+
+    def col_near(j):
+        i = amax1[j]
+        return colgap[j] < tol or rowgap[i] < tol or abs(Z[i, j] - lthr) < tol or \
+            (i1[j] >= 0 and rowgap[i1[j]] < tol) or (i1r[j] >= 0 and rowgap[i1r[j]] < tol)
+    bad = [("row", int(i)) for i in np.nonzero(i0 != i0r)[0] if not row_near(i)]
+    bad += [("col", int(j)) for j in np.nonzero(i1 != i1r)[0] if not col_near(j)]
+    return bad

@@ -7,7 +7,7 @@ import pytest
 
 import oracle
 import post
-from helpers import compare_features
+from helpers import compare_features, unexplained_match_disagreements
 from rspl_slam_amd import synthetic as SY
 
 pytestmark = pytest.mark.gpu
@@ -117,8 +117,12 @@ def test_sg_large_vs_oracle(pkg, weight_blobs, N, M):
         assert ok, sg.error
         res[name] = (i0, i1, m0, m1, sg.debug_scores(0, N, M))
     i0, i1, m0, m1, Zg = res["fp32"]
-    np.testing.assert_allclose(Zg, Z, atol=2e-3)
-    assert (i0 == i0r).mean() >= 0.999 and (i1 == i1r).mean() >= 0.999
+    dz = np.abs(Zg - Z).max()
+    print(f"SG N={N}: fp32 max |dZ| vs oracle {dz:.3g}")
+    np.testing.assert_allclose(Zg, Z, atol=1e-4, rtol=1e-5)         # Z atol 1e-4
+    # indices identical except where the oracle's own Z shows a near-tie within the Z tolerance
+    bad = unexplained_match_disagreements(Z, i0, i1, i0r, i1r, tol=2e-4)
+    assert not bad, f"{len(bad)} index disagreements not explained by near-ties: {bad[:10]}"
     both = (i0 >= 0) & (i0r >= 0)
     np.testing.assert_allclose(m0[both], m0r[both], atol=1e-3)
     h0, h1 = res["fp16"][0], res["fp16"][1]

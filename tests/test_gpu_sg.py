@@ -20,7 +20,7 @@ def _sg(pkg, w, nmax=400, B=1):
     return sg
 
 
-@pytest.mark.parametrize("name,atol", [("sg_small", 1e-4), ("sg_400", 1e-3)])
+@pytest.mark.parametrize("name,atol", [("sg_small", 1e-4), ("sg_400", 1e-4)])   # Z atol 1e-4
 def test_sg_vs_reference(pkg, golden, weight_blobs, name, atol):
     g = golden(name)
     F0, F1 = g["F0"].astype(np.float64), g["F1"].astype(np.float64)
@@ -29,6 +29,7 @@ def test_sg_vs_reference(pkg, golden, weight_blobs, name, atol):
     ok, i0, i1, m0, m1 = sg.infer(G0, G1)
     assert ok, sg.error
     Z = sg.debug_scores(0, F0.shape[1], F1.shape[1])
+    print(f"{name}: max |dZ| vs the reference module {np.abs(Z - g['Z']).max():.3g}")
     np.testing.assert_allclose(Z, g["Z"], atol=atol, rtol=1e-5)
     np.testing.assert_array_equal(i0, g["idx0"])
     np.testing.assert_array_equal(i1, g["idx1"])
@@ -60,7 +61,7 @@ def test_sg_ragged_and_empty(pkg, weight_blobs):
         assert ok, sg.error
         Zo = oracle.sg_forward(weight_blobs[1], *post.sg_inputs(G0), *post.sg_inputs(G1))
         Z = sg.debug_scores(0, n0, n1)
-        np.testing.assert_allclose(Z, Zo, atol=1e-3, rtol=1e-5, err_msg=f"{n0}x{n1}")
+        np.testing.assert_allclose(Z, Zo, atol=1e-4, rtol=1e-5, err_msg=f"{n0}x{n1}")
         d = post.decode(Z)
         np.testing.assert_array_equal(i0, d[0])
         np.testing.assert_array_equal(i1, d[1])
@@ -160,3 +161,68 @@ def test_sg_post_stream_pipelined(pkg, weight_blobs):
     for (a0, a1), (b0, b1) in zip(ref, got):
         np.testing.assert_array_equal(a0, b0)
         np.testing.assert_array_equal(a1, b1)
+
+
+def test_sinkhorn_unit_vs_reference(pkg, golden, weight_blobs):
+    """The device log-Sinkhorn on the reference module's own fixture (superglue.log_optimal_transport,
+    convert2onnx/superglue.py:185-205: random 64x56 scores, bin score alpha, 100 iterations)."""
+    g = golden("sinkhorn_unit")
+    sg = _sg(pkg, weight_blobs[1], nmax=64)
+    ok, Z = sg.debug_sinkhorn(g["scores"], float(g["alpha"]), int(g["iters"]))
+    assert ok, sg.error
+    print(f"sinkhorn_unit: max |dZ| {np.abs(Z - g['Z']).max():.3g}")
+    np.testing.assert_allclose(Z, g["Z"], atol=1e-4, rtol=0)
+    i0, i1, m0, m1 = sg.debug_decode(Z)
+    np.testing.assert_array_equal(i0, g["idx0"])
+    np.testing.assert_array_equal(i1, g["idx1"])
+    np.testing.assert_allclose(m0, g["ms0"], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("which", ["Z", "Z_ties"])
+def test_decode_unit_vs_reference(pkg, golden, weight_blobs, which):
+    """The device decode (argmax / col_argmax / finalize) on the reference's decode fixtures, including
+    Z_ties (duplicated row / column maxima: first maximum wins, src/super_glue.cpp:258-337)."""
+    g = golden("sinkhorn_unit")
+    sg = _sg(pkg, weight_blobs[1], nmax=64)
+    i0, i1, m0, m1 = sg.debug_decode(g[which])
+    p = "" if which == "Z" else "t_"
+    np.testing.assert_array_equal(i0, g[p + "idx0"])
+    np.testing.assert_array_equal(i1, g[p + "idx1"])
+    # std::exp(float) widened to double: the device expf and the fixture's exp agree to 1 float ulp
+    np.testing.assert_allclose(m0, g[p + "ms0"], rtol=2.4e-7, atol=0)
+    np.testing.assert_allclose(m1, g[p + "ms1"], rtol=2.4e-7, atol=0)
+
+
+def test_sinkhorn_timeout_reaches_caller(pkg, weight_blobs):
+    """A Sinkhorn exchange timeout (injected) is reported on the device path through rspl_sg_status and
+    fails rspl_sg_infer; clearing the injection restores correct results on the same handle."""
+    from rspl_slam_amd import capi
+    from rspl_slam_amd import synthetic as SY
+    sg = _sg(pkg, weight_blobs[1], nmax=96, B=2)
+    F0, F1, _ = SY.sg_problem(90, 80, 40, seed=3)
+    G0, G1 = post.normalize_keypoints(F0, 752, 480), post.normalize_keypoints(F1, 752, 480)
+    ok, r0, r1, _, _ = sg.infer(G0, G1)
+    assert ok, sg.error
+    sg.debug_inject(True, spin_limit=1 << 12)
+    ok, *_ = sg.infer(G0, G1)
+    assert not ok and "timed out" in sg.error
+    # device path: the flag is sticky until rspl_sg_status reads it
+    nmax, B = 96, 2
+    f0 = np.zeros((B, nmax, 259)); f1 = np.zeros((B, nmax, 259))
+    f0[:, :90] = G0.T; f1[:, :80] = G1.T
+    st = capi.Stream()
+    bufs = {k: capi.DeviceBuffer(v.nbytes).upload(v) for k, v in
+            dict(f0=f0, f1=f1, n0=np.array([90, 90], np.int32), n1=np.array([80, 80], np.int32)).items()}
+    out = {k: capi.DeviceBuffer(B * nmax * sz) for k, sz in dict(i0=4, i1=4, m0=8, m1=8).items()}
+    sg.infer_device(B, bufs["f0"].ptr, bufs["n0"].ptr, bufs["f1"].ptr, bufs["n1"].ptr, nmax, False,
+                    out["i0"].ptr, out["i1"].ptr, out["m0"].ptr, out["m1"].ptr, st.handle)
+    st.synchronize()
+    ok, mask = sg.status()
+    assert not ok and mask & 1, (ok, mask)
+    assert sg.status() == (True, 0)          # cleared by the read
+    sg.debug_inject(False)
+    ok, i0, i1, _, _ = sg.infer(G0, G1)
+    assert ok, sg.error
+    np.testing.assert_array_equal(i0, r0)
+    np.testing.assert_array_equal(i1, r1)
+    assert sg.status() == (True, 0)

@@ -126,3 +126,13 @@ def test_sp_fp16_vs_reference(pkg, golden, weight_blobs):
     assert overlap >= 0.99
     assert cos.min() >= 0.999
     np.testing.assert_allclose(F[0, fi], G[0, gi], rtol=2e-2, atol=1e-4)
+
+
+def test_nms_unit_vs_reference(pkg, golden, weight_blobs):
+    """The device simple_nms on the reference module's fixture (superpoint.simple_nms, radius 4,
+    convert2onnx/superpoint.py:6-33): a random map and two plateau maps with exact ties."""
+    g = golden("nms_unit")
+    sp = _sp(pkg, weight_blobs[0], 32, 64, 96)
+    for k in range(3):
+        out = sp.debug_nms(g[f"in{k}"])
+        np.testing.assert_array_equal(out, g[f"out{k}"], err_msg=f"map {k}")
