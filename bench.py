@@ -17,8 +17,8 @@ arrays (the reference's std::map containers), so its H2D upload is inside the st
 Multi-GPU: `bench.py --gpus N` spawns N rank processes itself (before anything touches the GPU),
 or runs as one rank under `python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N`
 (then WORLD_SIZE must equal N).  One process per GPU; each rank runs its own stereo sequence
-(replicas, weak scaling); the gloo group provides the barrier, the max-over-ranks timing and the
-rank census (fails loudly if fewer than N distinct GPUs come up).  `--ba-mode shard` instead
+(replicas, weak scaling); a torch-free TCP host group (rspl-slam_amd/hostgroup.py) provides the barrier, the
+max-over-ranks timing and the rank census (fails loudly if fewer than N distinct GPUs come up).  `--ba-mode shard` instead
 solves every step's N local BAs (one per rank's sequence) jointly, landmark-sharded over all
 ranks with an RCCL all-reduce of the reduced camera system per LM trial.
 
@@ -183,14 +183,11 @@ def replica_seeds(rank):
     return {"images": [1000 * rank + i for i in range(4)], "ba": [1000 * rank + 50 + i for i in range(3)]}
 
 
-def job_time(elapsed, dist=None):
-    """Whole-job wall time = max over ranks of each rank's timed region (gloo all-reduce)."""
-    if dist is None:
+def job_time(elapsed, group=None):
+    """Whole-job wall time = max over ranks of each rank's timed region (host-group all-reduce)."""
+    if group is None:
         return elapsed
-    import torch
-    t = torch.tensor([elapsed], dtype=torch.float64)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t[0])
+    return group.allreduce_max(elapsed)
 
 
 def job_value(world, steps, elapsed):
@@ -198,7 +195,7 @@ def job_value(world, steps, elapsed):
     return world * steps / elapsed
 
 
-def spawn_ranks(n, argv):
+def spawn_ranks(n, argv, script=None):
     """bench.py --gpus N without a launcher: start N rank processes (one per GPU) before this
     process touches the GPU, wait for all of them, exit with the first failure's code."""
     import socket
@@ -210,27 +207,33 @@ def spawn_ranks(n, argv):
     for r in range(n):
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, str(pathlib.Path(__file__).resolve())] + argv, env=env))
+        procs.append(subprocess.Popen([sys.executable, str(script or pathlib.Path(__file__).resolve())] + argv, env=env))
     rc = 0
-    for pr in procs:
-        c = pr.wait()
-        if c != 0 and rc == 0:
-            rc = c
-            for q in procs:  # one rank failed: the others would wait on it forever
+    while [pr.poll() for pr in procs].count(None):  # poll every rank each round
+        bad = [pr.returncode for pr in procs if pr.returncode not in (None, 0)]
+        if bad:  # one rank failed: the others would wait on it forever
+            rc = bad[0]
+            for q in procs:
                 if q.poll() is None:
                     q.kill()
+            break
+        time.sleep(0.2)
+    for pr in procs:
+        pr.wait()
+        if pr.returncode and not rc:
+            rc = pr.returncode
     if rc:
         log(f"bench: a rank exited with {rc}")
     return rc
 
 
-def rank_census(dist, world, want, local):
+def rank_census(group, world, want, local, cnt):
     """Every rank reports (rank, device, visible devices, host); fail loudly unless exactly `want`
     ranks came up on distinct GPUs."""
-    n = C_int = None  # noqa: F841
-    cnt = pkg.capi.device_count()
-    rows = [None] * world
-    dist.all_gather_object(rows, (int(os.environ.get("RANK", 0)), local, cnt, os.uname().nodename))
+    rows = group.all_gather([group.rank, local, cnt, os.uname().nodename])
+    bad = [r for r in rows if r[1] >= r[2]]
+    if bad:
+        raise SystemExit(f"bench: ranks want GPUs that are not visible (rank, device, visible, host): {bad}")
     devs = {(h, d) for _, d, _, h in rows}
     if world != want or len(devs) != world:
         raise SystemExit(f"bench: --gpus {want} but {world} ranks on {len(devs)} distinct GPUs came up: {rows}")
@@ -271,13 +274,10 @@ def main():
     wl = WORKLOADS[args.workload]
     H, W, K = wl["H"], wl["W"], wl["K"]
     capi.load()  # librspl's HIP runtime first: one runtime per process
-    dist = None
+    dist = None  # host group (barrier, max-over-ranks time, census, RCCL id): no torch in this process
     if world > 1:
-        import datetime
-        import torch
-        import torch.distributed as dist
-        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=300))
-        rank_census(dist, world, args.gpus, local)
+        dist = pkg.hostgroup.HostGroup(rank, world, timeout=300.0)
+        rank_census(dist, world, args.gpus, local, capi.device_count())
     capi.check(capi.load().rspl_set_device(local), "rspl_set_device")
 
     sp_w, sg_w = pkg.weights.ensure_blobs(str(ROOT / "weights"))
@@ -298,10 +298,16 @@ def main():
         ba.use_reserved_cus(args.reserve_cus)
     shard = args.ba_mode == "shard"
     if shard:  # landmark-sharded BA over RCCL: one communicator across all ranks (also valid at N = 1)
-        if dist is not None:
-            comm = pkg.Comm(pkg.broadcast_comm_id(dist), rank, world, local)
-        else:
-            comm = pkg.Comm(pkg.comm_unique_id(), 0, 1, local)
+        # librccl prints its version banner on stdout: keep stdout for the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            uid = pkg.broadcast_comm_id(dist) if dist is not None else pkg.comm_unique_id()
+            comm = pkg.Comm(uid, rank, world, local)
+        finally:
+            os.dup2(saved, 1)
+            os.close(saved)
         ba.set_comm(comm)
     syn = pkg.synthetic
     NP = 4

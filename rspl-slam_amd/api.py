@@ -278,6 +278,25 @@ class LocalBA:
         capi.check(self._lib.rspl_ba_set_group(self._h, group.handle, rank), "rspl_ba_set_group")
         self._shard = group  # keep the group alive while the handle uses it
 
+    def set_shard(self, rank: int, nranks: int, host_allreduce):
+        """Landmark-sharded solve over any host transport: host_allreduce(x) sums the float64 numpy
+        array x in place across the ranks (e.g. a gloo / MPI all-reduce).  The device buffer of each
+        per-trial all-reduce is staged through host memory (rspl_allreduce_fn, stream-ordered)."""
+        lib = self._lib
+        AR = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p)
+
+        def cb(ctx, d_buf, count, stream):
+            try:
+                h = np.empty(count, np.float64)
+                if lib.rspl_memcpy_d2h(h.ctypes.data, d_buf, count * 8, stream):
+                    return -1
+                host_allreduce(h)
+                return 1 if lib.rspl_memcpy_h2d(d_buf, h.ctypes.data, count * 8, stream) else 0
+            except Exception:  # the C side turns a non-zero return into RSPL_E_DEVICE
+                return -1
+        self._ar_cb = AR(cb)  # keep the trampoline alive as long as the handle
+        capi.check(lib.rspl_ba_set_shard(self._h, rank, nranks, self._ar_cb, None), "rspl_ba_set_shard")
+
     def set_comm(self, comm: "Comm"):
         """Landmark-sharded solve across processes / GPUs over RCCL (one rank per GPU)."""
         capi.check(self._lib.rspl_ba_set_comm(self._h, comm.handle), "rspl_ba_set_comm")
@@ -330,11 +349,9 @@ class Comm:
             self.handle = C.c_void_p()
 
 
-def broadcast_comm_id(dist, make_id=comm_unique_id) -> bytes:
-    """Rank 0 makes the RCCL id, every rank of the (gloo) process group receives it."""
-    obj = [make_id() if dist.get_rank() == 0 else None]
-    dist.broadcast_object_list(obj, src=0)
-    return obj[0]
+def broadcast_comm_id(group, make_id=comm_unique_id) -> bytes:
+    """Rank 0 makes the RCCL id, every rank of the host group (hostgroup.HostGroup) receives it."""
+    return group.broadcast_bytes(make_id() if group.rank == 0 else b"")
 
 
 _default_ba = None

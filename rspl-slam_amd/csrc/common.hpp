@@ -99,6 +99,9 @@ struct StageTimer {
   void mark(int i, hipStream_t s) {
     if (enabled) (void)hipEventRecord(ev[head][i], s);
   }
+  // event i of the current call, to be stamped by a kernel launch itself (hipExtLaunchKernelGGL);
+  // null when profiling is off
+  hipEvent_t slot(int i) const { return enabled ? ev[head][i] : nullptr; }
   void harvest(int r) {
     if (!pending[r]) return;
     (void)hipEventSynchronize(ev[r][n]);

@@ -246,7 +246,7 @@ sg::GemmArgs G_(const float* A, int lda, const float* B, int ldb, const float* b
 
 // log_optimal_transport (superglue.py:185-205) on the couplings of B pairs, on stream st
 static hipError_t run_sinkhorn(rspl_sg* s, const float* cpl, float* Zp, const int* cn0, const int* cn1, int B,
-                               int iters, hipStream_t st) {
+                               int iters, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr) {
   static unsigned long long* probe = nullptr;  // debug only (RSPL_SG_PROBE)
   static const bool probing = getenv("RSPL_SG_PROBE") != nullptr;
   hipError_t e;
@@ -261,7 +261,7 @@ static hipError_t run_sinkhorn(rspl_sg* s, const float* cpl, float* Zp, const in
   sk.spin_limit = s->spin_limit; sk.inject = s->inject;
   sk.err = s->d_err; sk.n0 = cn0; sk.n1 = cn1;
   sk.nmax = s->nmax; sk.G = s->G; sk.iters = iters;
-  if ((e = sg::sinkhorn(sk, B, st)) != hipSuccess) return e;
+  if ((e = sg::sinkhorn(sk, B, st, t0, t1)) != hipSuccess) return e;
   if (probing) {  // debug: Sinkhorn cycles per workgroup-iteration by phase
     unsigned long long h[5];
     if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
@@ -502,10 +502,11 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
     RSPL_HIP(hipStreamWaitEvent(pst, s->ev_ready, 0));
   }
   // log_optimal_transport (superglue.py:185-205)
-  s->timer.mark(4, pst);  // the Sinkhorn starts here: stage 3 is the post stream's hand-over wait
-  RSPL_HIP(run_sinkhorn(s, cpl, Zp, cn0, cn1, B, s->cfg.sinkhorn_iterations, pst));
+  // events 4 / 5 are stamped by the Sinkhorn launch itself (its own start / end): stage 3 is the
+  // post stream's hand-over wait, stage 4 exactly the Sinkhorn kernel
+  RSPL_HIP(run_sinkhorn(s, cpl, Zp, cn0, cn1, B, s->cfg.sinkhorn_iterations, pst, s->timer.slot(4),
+                        s->timer.slot(5)));
   if (pst != st) RSPL_HIP(hipEventRecord(s->ev_sink[par], pst));
-  s->timer.mark(5, pst);
   // decode (super_glue.cpp:339-367), threshold 0.2 hard-coded as in the reference (:355)
   sg::DecodeArgs dc{};
   dc.Z = Zp; dc.n0 = cn0; dc.n1 = cn1; dc.nmax = nm; dc.max0 = s->max0; dc.val0 = s->val0; dc.max1 = s->max1;

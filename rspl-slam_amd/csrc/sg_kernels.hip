@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <string>
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cfloat>
 #include <cstdint>
@@ -1288,7 +1289,7 @@ size_t sinkhorn_lds_bytes(int nmax, int G, bool slabs) {
   return sizeof(float) * (2 * ldp + 4 + (slabs ? 2 * per * ld : 0));
 }
 
-hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s) {
+hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   if (a.G < 1 || a.G > 1024) return hipErrorInvalidValue;
   dim3 grid(a.G, B);
   const size_t full = sinkhorn_lds_bytes(a.nmax, a.G, true);
@@ -1300,10 +1301,11 @@ hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s) {
       if (e != hipSuccess) return e;
       attr = full;
     }
-    hipLaunchKernelGGL((sinkhorn_kernel<true>), grid, dim3(kSinkThreads), full, s, a);
+    hipExtLaunchKernelGGL((sinkhorn_kernel<true>), grid, dim3(kSinkThreads), (uint32_t)full, s, t0, t1, 0, a);
   } else {
     if (!a.cplT) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((sinkhorn_kernel<false>), grid, dim3(kSinkThreads), sinkhorn_lds_bytes(a.nmax, a.G, false), s, a);
+    hipExtLaunchKernelGGL((sinkhorn_kernel<false>), grid, dim3(kSinkThreads),
+                          (uint32_t)sinkhorn_lds_bytes(a.nmax, a.G, false), s, t0, t1, 0, a);
   }
   return hipGetLastError();
 }

@@ -138,7 +138,8 @@ hipError_t to_half(const float* x, _Float16* y, size_t n, hipStream_t s);
 hipError_t prep(const PrepArgs& a, hipStream_t s);
 hipError_t attention(const AttnArgs& a, int B, hipStream_t s);
 hipError_t bins(const BinsArgs& a, int B, hipStream_t s);
-hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s);
+// t0 / t1 (may be null): events stamped with the kernel's own start / end (hipExtLaunchKernelGGL)
+hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 hipError_t decode(const DecodeArgs& a, int B, hipStream_t s);
 // LDS bytes of one Sinkhorn workgroup (with or without the row / column slabs)
 size_t sinkhorn_lds_bytes(int nmax, int G, bool slabs);

@@ -9,6 +9,7 @@
 // Convolutions are implicit GEMMs (M = pixels, N = output channels, K = 9*Cin)
 // on v_mfma_f32_32x32x2_f32 (exact fp32: one rounding per product, like fmaf).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdlib>
 
@@ -734,16 +735,18 @@ __global__ __launch_bounds__(256) void sample_kernel(SampleArgs a) {
 // launchers
 // ---------------------------------------------------------------------------
 template <int CIN, int TH, bool POOL, bool FUSE1A>
-static hipError_t launch_conv(const ConvArgs& a, int B, hipStream_t s) {
+static hipError_t launch_conv(const ConvArgs& a, int B, hipStream_t s, hipEvent_t t0 = nullptr,
+                              hipEvent_t t1 = nullptr) {
   const int tiles = ((a.W + TW - 1) / TW) * ((a.H + TH - 1) / TH);
   dim3 grid(B * tiles, a.cout / 64);
-  hipLaunchKernelGGL((conv3x3_kernel<CIN, TH, POOL, FUSE1A>), grid, dim3(256), 0, s, a);
+  hipExtLaunchKernelGGL((conv3x3_kernel<CIN, TH, POOL, FUSE1A>), grid, dim3(256), 0, s, t0, t1, 0, a);
   return hipGetLastError();
 }
 
-hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hipStream_t s) {
+hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hipStream_t s, hipEvent_t t0,
+                   hipEvent_t t1) {
   const bool small = (a.H * a.W) <= 128 * 192;  // more, smaller tiles for the low-res layers
-  if (fuse1a) return launch_conv<64, 16, true, true>(a, B, s);
+  if (fuse1a) return launch_conv<64, 16, true, true>(a, B, s, t0, t1);
   if (cin == 64 && pool) return launch_conv<64, 16, true, false>(a, B, s);
   if (cin == 64 && !pool) return small ? launch_conv<64, 8, false, false>(a, B, s) : launch_conv<64, 16, false, false>(a, B, s);
   if (cin == 128 && pool) return launch_conv<128, 16, true, false>(a, B, s);
@@ -752,16 +755,18 @@ hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hi
 }
 
 template <int CIN, int TH, bool POOL, bool FUSE1A, bool OUT_F32>
-static hipError_t launch_conv_h(const ConvArgs& a, int B, hipStream_t s) {
+static hipError_t launch_conv_h(const ConvArgs& a, int B, hipStream_t s, hipEvent_t t0 = nullptr,
+                                hipEvent_t t1 = nullptr) {
   const int tiles = ((a.W + TW - 1) / TW) * ((a.H + TH - 1) / TH);
   dim3 grid(B * tiles, a.cout / 64);
-  hipLaunchKernelGGL((conv3x3_h_kernel<CIN, TH, POOL, FUSE1A, OUT_F32>), grid, dim3(256), 0, s, a);
+  hipExtLaunchKernelGGL((conv3x3_h_kernel<CIN, TH, POOL, FUSE1A, OUT_F32>), grid, dim3(256), 0, s, t0, t1, 0, a);
   return hipGetLastError();
 }
 
-hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool out_f32, int B, hipStream_t s) {
+hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool out_f32, int B, hipStream_t s,
+                     hipEvent_t t0, hipEvent_t t1) {
   const bool small = (a.H * a.W) <= 128 * 192;
-  if (fuse1a) return launch_conv_h<64, 16, true, true, false>(a, B, s);
+  if (fuse1a) return launch_conv_h<64, 16, true, true, false>(a, B, s, t0, t1);
   if (out_f32) return launch_conv_h<128, 8, false, false, true>(a, B, s);
   if (cin == 64 && pool) return launch_conv_h<64, 16, true, false, false>(a, B, s);
   if (cin == 64 && !pool) return small ? launch_conv_h<64, 8, false, false, false>(a, B, s)

@@ -70,9 +70,12 @@ struct SampleArgs {
   int B, H, W;
 };
 
-hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hipStream_t s);
+hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hipStream_t s, hipEvent_t t0 = nullptr,
+                   hipEvent_t t1 = nullptr);
 // fp16 MFMA (v_mfma_f32_32x32x16_f16) variant; out_f32 writes `out` (fp32) instead of `hout`
-hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool out_f32, int B, hipStream_t s);
+// t0 / t1 (may be null): events stamped with the fused conv1 kernel's own start / end
+hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool out_f32, int B, hipStream_t s,
+                     hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 hipError_t heads(const HeadArgs& a, int mode, hipStream_t s);
 hipError_t nms(const NmsArgs& a, int B, hipStream_t s);
 hipError_t topk(const TopkArgs& a, int B, hipStream_t s);

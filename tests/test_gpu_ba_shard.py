@@ -106,3 +106,56 @@ def test_rccl_single_rank():
     _compare(res, oracle.ba_local(prob))
     plain = pkg.LocalBA(16, 2000, 100, 20000).run(prob)  # unsharded schedule on the same GPU
     _compare(res, plain, tol_pose=1e-10, tol_pt=1e-9, chi2_rtol=1e-12)
+
+
+SHARD_PROB = dict(n_poses=8, n_points=1500, n_lines=40, seed=21, pixel_sigma=0.8, outlier_frac=0.05)
+
+
+def test_two_process_shard_host_allreduce():
+    """Two processes, each with its own rspl_ba handle (GPU 0), landmark-sharded over a host-staged
+    all-reduce (rspl_ba_set_shard with the TCP host group's rank-ordered sum; gloo would bring torch's
+    own HIP runtime into the process): results bitwise equal across the ranks and equal to the
+    unsharded oracle."""
+    import multiprocessing as mp
+    import socket
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    import shard_worker
+    procs = [ctx.Process(target=shard_worker.rank_main, args=(r, 2, port, q, SHARD_PROB)) for r in range(2)]
+    for p in procs:
+        p.start()
+    got = []
+    import queue as _q
+    import time
+    t0 = time.time()
+    while len(got) < 2:  # fail fast if a rank dies instead of waiting out the timeout
+        try:
+            got.append(q.get(timeout=5))
+        except _q.Empty:
+            dead = [p.exitcode for p in procs if p.exitcode not in (None, 0)]
+            assert not dead, f"a rank process died: exit codes {dead}"
+            assert time.time() - t0 < 120, "sharded BA ranks did not finish"
+    res = sorted(got, key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0, f"rank process exit code {p.exitcode}"
+    for r in res:
+        assert r[1] != "error", r
+    a, b = res
+    for x, y in zip(a[1:9], b[1:9]):
+        np.testing.assert_array_equal(x, y)
+    for k in a[9]:
+        np.testing.assert_array_equal(a[9][k], b[9][k])
+    prob, _ = SY.ba_problem(**SHARD_PROB)
+    ref = oracle.ba_local(prob)
+    assert (a[1], a[2]) == (ref.iters_first, ref.iters_second)
+    np.testing.assert_allclose(a[3], ref.chi2_first, rtol=1e-8)
+    np.testing.assert_allclose(a[4], ref.chi2_second, rtol=1e-8)
+    assert np.abs(a[6] - ref.pose_p).max() < 1e-7
+    assert np.abs(a[7] - ref.points).max() < 1e-6
+    assert np.abs(a[8] - ref.lines).max() < 5e-3
+    for k in a[9]:
+        np.testing.assert_array_equal(a[9][k], ref.inlier[k], err_msg=k)

@@ -1,15 +1,17 @@
-"""N>1 path on CPU: world_size-2 gloo ranks run bench.py's cross-rank timing and replica seeding.
+"""N>1 path on CPU: host-group ranks run bench.py's cross-rank timing, census data and replica seeding.
 
-bench.py --gpus N is launched by torch.distributed.run, one process per GPU, each running
-its own stereo sequence (replicas, weak scaling).  The only collective is the max-over-ranks
-wall time; this test exercises exactly that code (bench.job_time / job_value / replica_seeds)
-with two real gloo processes on 127.0.0.1.
+bench.py --gpus N spawns (or torch.distributed.run launches) one process per GPU, each running
+its own stereo sequence (replicas, weak scaling).  The host control plane is
+rspl-slam_amd/hostgroup.py (TCP on 127.0.0.1, no torch in the rank processes): max-over-ranks wall
+time, the rank census, the RCCL id broadcast, rank-ordered host sums.  These tests run that code
+(bench.job_time / job_value / replica_seeds / spawn_ranks, api.broadcast_comm_id) in real processes.
 """
 import os
 import pathlib
 import socket
 import sys
 
+import numpy as np
 import pytest
 
 ROOT = pathlib.Path(__file__).resolve().parents[1]
@@ -23,37 +25,44 @@ def _free_port():
 
 def _rank_main(rank, world, port, out):
     sys.path.insert(0, str(ROOT))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    import torch.distributed as dist
+    import rspl_loader
+    pkg = rspl_loader.load()
     import bench
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = pkg.hostgroup.HostGroup(rank, world, "127.0.0.1", port, timeout=60)
     try:
         elapsed = 0.5 + rank  # rank 1 is the slow one
-        t = bench.job_time(elapsed, dist)
-        dist.barrier()
-        out.put((rank, t, bench.job_value(world, 30, t), bench.replica_seeds(rank)))
+        t = bench.job_time(elapsed, g)
+        g.barrier()
+        x = np.full(5, 0.1 * (rank + 1))
+        g.allreduce_sum_(x)
+        rows = g.all_gather([rank, rank % 2, 8, "host"])
+        out.put((rank, t, bench.job_value(world, 30, t), bench.replica_seeds(rank), x.tolist(), rows))
     finally:
-        dist.destroy_process_group()
+        g.close()
 
 
-def test_two_rank_timing_and_replicas():
-    import torch.multiprocessing as mp
+def test_three_rank_host_group_timing_and_replicas():
+    """bench.py's N > 1 control plane (hostgroup.HostGroup, no torch): max-over-ranks time seen by every
+    rank, whole-job frames/s, disjoint replica seeds, rank-ordered sums bitwise equal on all ranks."""
+    import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main, args=(r, 3, port, q)) for r in range(3)]
     for p in procs:
         p.start()
-    res = sorted(q.get(timeout=120) for _ in procs)
+    res = sorted((q.get(timeout=120) for _ in procs), key=lambda t: t[0])
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, t0, v0, s0), (r1, t1, v1, s1) = res
-    assert t0 == t1 == pytest.approx(1.5)           # max over ranks, seen by every rank
-    assert v0 == v1 == pytest.approx(2 * 30 / 1.5)   # whole-job frames/s
-    # replicas: disjoint synthetic sequences per rank
-    assert not set(s0["images"]) & set(s1["images"])
-    assert not set(s0["ba"]) & set(s1["ba"])
+    for r, t, v, seeds, x, rows in res:
+        assert t == pytest.approx(2.5)              # max over ranks, seen by every rank
+        assert v == pytest.approx(3 * 30 / 2.5)     # whole-job frames/s
+        assert rows == [[k, k % 2, 8, "host"] for k in range(3)]
+        assert x == res[0][4]                       # identical bits on every rank
+    assert res[0][4] == [(0.1 + 0.2) + 0.30000000000000004] * 5
+    s = [set(r[3]["images"]) for r in res]
+    assert not (s[0] & s[1]) and not (s[1] & s[2])
 
 
 def test_single_rank_is_identity():
@@ -65,12 +74,10 @@ def test_single_rank_is_identity():
 
 def _id_main(rank, world, port, out):
     sys.path.insert(0, str(ROOT))
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    import torch.distributed as dist
     import rspl_loader
     pkg = rspl_loader.load()
     from rspl_slam_amd import api
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    g = pkg.hostgroup.HostGroup(rank, world, "127.0.0.1", port, timeout=60)
     try:
         calls = []
 
@@ -78,16 +85,16 @@ def _id_main(rank, world, port, out):
             calls.append(rank)
             return bytes(range(128))
 
-        uid = api.broadcast_comm_id(dist, make_id)
+        uid = api.broadcast_comm_id(g, make_id)
         out.put((rank, uid, calls))
     finally:
-        dist.destroy_process_group()
+        g.close()
 
 
 def test_rccl_id_broadcast_two_ranks():
     """The sharded BA's RCCL bootstrap (api.broadcast_comm_id): only rank 0 makes the id, every
     rank of the gloo group receives the same 128 bytes."""
-    import torch.multiprocessing as mp
+    import multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -101,3 +108,31 @@ def test_rccl_id_broadcast_two_ranks():
     (r0, u0, c0), (r1, u1, c1) = res
     assert u0 == u1 == bytes(range(128))
     assert c0 == [0] and c1 == []
+
+
+RANK_SCRIPT = """
+import os, sys, time, pathlib
+out = pathlib.Path(sys.argv[1])
+r, w = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+(out / f"rank{r}").write_text(f"{r} {w} {os.environ['LOCAL_RANK']} {os.environ['MASTER_ADDR']}")
+if len(sys.argv) > 2 and r == int(sys.argv[2]):
+    sys.exit(3)                   # this rank fails
+if len(sys.argv) > 2:
+    time.sleep(600)               # the others would wait for it forever
+"""
+
+
+def test_spawn_ranks(tmp_path):
+    """bench.py --gpus N without a launcher: N rank processes with RANK / WORLD_SIZE / LOCAL_RANK and a
+    127.0.0.1 rendezvous; a failing rank ends the job with its exit code (the others are killed)."""
+    sys.path.insert(0, str(ROOT))
+    import time
+    import bench
+    script = tmp_path / "rank.py"
+    script.write_text(RANK_SCRIPT)
+    assert bench.spawn_ranks(3, [str(tmp_path)], script=script) == 0
+    rows = sorted((tmp_path / f"rank{r}").read_text() for r in range(3))
+    assert rows == [f"{r} 3 {r} 127.0.0.1" for r in range(3)]
+    t = time.time()
+    assert bench.spawn_ranks(2, [str(tmp_path), "1"], script=script) == 3
+    assert time.time() - t < 60
