@@ -70,6 +70,7 @@ struct rspl_ba {
   rspl_allreduce_fn allreduce = nullptr;
   void* ar_ctx = nullptr;
   double* red = nullptr;       // [6 maxK + kMaxRanks + 3] lambda-init / cost all-reduce buffer
+  ba::LmCtrl* lmctl = nullptr;  // device-side LM control (fast path, unsharded)
   double* gbuf = nullptr;      // final gather buffer (grown on demand)
   size_t gcap = 0;
 };
@@ -149,6 +150,7 @@ void carve(F& ar, rspl_ba* b) {
   take(b->lm_edges, E); take(b->lm_pose, E);
   take(b->chunk, npairs * nchk * 48); take(b->pairfin, npairs * 48 + 8); take(b->pair_ctr, npairs);
   take(b->red, 6 * K + kMaxRanks + 8);
+  take(b->lmctl, 1);
   take(b->pp_cnt, npairs * nchk); take(b->pp_off, npairs * nchk + 1);
 }
 
@@ -267,6 +269,110 @@ void report_prof(rspl_ba* b) {
   (void)hipMemset(b->prof, 0, sizeof(unsigned long long) * ba::kProfLen);
 }
 
+// an accepted candidate becomes the current state; with lin also its speculative linearisation
+void accept_swap(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, bool lin) {
+  std::swap(P.T, P.Tn);
+  std::swap(P.X, P.Xn);
+  std::swap(P.L, P.Ln);
+  if (!lin) return;
+  std::swap(b->Hpp_e, b->Hpp_s); std::swap(b->bp_e, b->bp_s); std::swap(b->Hll_e, b->Hll_es);
+  std::swap(b->bl_e, b->bl_es); std::swap(b->Hpl_e, b->Hpl_s);
+  std::swap(b->Hll, b->Hll_s); std::swap(b->bl, b->bl_s);
+  Lr.Hpp = b->Hpp_e; Lr.bp = b->bp_e; Lr.Hll = b->Hll_e; Lr.bl = b->bl_e; Lr.Hpl = b->Hpl_e;
+  S.Hll = b->Hll; S.bl = b->bl;
+}
+
+// RSPL_BA_HOSTLM=1: the host decides every trial (the mailbox round trip per trial)
+bool host_lm() {
+  static const bool v = getenv("RSPL_BA_HOSTLM") != nullptr;
+  return v;
+}
+
+// optimize(iters) with the LM control on the device (fast path, unsharded): the first errors, the
+// first linearisation and the control's initialisation, then `iters` trials queued back to back
+// with no host round trip -- each trial's last kernel takes the accept / reject decision (ba::LmCtrl)
+// and the next trial's kernels read it.  The host waits once, for the trial that stops the
+// optimize(); when rejected trials leave iterations undone it queues more.  At the end the host
+// pointer view follows the device's current bank.
+int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
+                 double* chi2_out, int* done_out) {
+  hipStream_t st = b->stream;
+  S.lm = b->lmctl;
+  unsigned long long q = ++b->seq;
+  RSPL_HIP(ba::compute_errors(P, Lr, A, S, q, st));
+  RSPL_HIP(ba::linearize(P, Lr, A, S, true, st));
+  q = ++b->seq;
+  RSPL_HIP(ba::post(S, q, st, &A, iters));  // + computeLambdaInit into the control
+  const unsigned long long q_first = b->seq + 1;
+  ba::Lin Ls = Lr;
+  Ls.Hpp = b->Hpp_s; Ls.bp = b->bp_s; Ls.Hll = b->Hll_es; Ls.bl = b->bl_es; Ls.Hpl = b->Hpl_s;
+  ba::Sys Ss = S;
+  Ss.Hll = b->Hll_s; Ss.bl = b->bl_s;
+  int queued = 0;
+  auto enqueue = [&](int n) -> int {
+    for (int k = 0; k < n; k++, queued++) {
+      q = ++b->seq;
+      if (++b->tag == 0) b->tag = 1;  // 0 is the flags' initial value
+      ba::Spec sp{Ls, Ss, b->lflag, b->tag};
+      const bool traced = b->prof && queued == 3 && !b->prof_nb[0];
+      if (traced) {
+        S.prof = b->prof;
+        b->prof_nb[0] = A.npairs * A.nchk;
+        b->prof_nb[1] = ba::update_errors_blocks(A) + A.n_lblk;
+        b->prof_nb[2] = ba::update_errors_blocks(A);
+      }
+      const hipError_t e = ba::trial_dev(P, Lr, A, S, q, st, sp);
+      S.prof = nullptr;
+      if (e != hipSuccess) {
+        set_error("BA trial launch failed: %s", hipGetErrorString(e));
+        return RSPL_E_DEVICE;
+      }
+    }
+    return RSPL_OK;
+  };
+  int rc;
+  if ((rc = enqueue(iters))) return rc;
+  double v[4];
+  for (;;) {
+    const unsigned long long q_last = b->seq;
+    // wait for the stopping trial (trials queued after it post nothing) or the last queued one
+    using clk = std::chrono::steady_clock;
+    const auto t0 = clk::now();
+    for (unsigned spin = 1;; spin++) {
+      const unsigned long long s1 = __atomic_load_n(&b->mail->seq, __ATOMIC_ACQUIRE);
+      if (s1 >= q_first && s1 <= q_last) {
+        volatile const double* mv = b->mail->v;
+        for (int k = 0; k < 4; k++) v[k] = mv[k];
+        if (__atomic_load_n(&b->mail->seq, __ATOMIC_ACQUIRE) == s1 && (s1 == q_last || v[3] != 0.0)) break;
+      }
+      if ((spin & 4095) == 0) {
+        const hipError_t e = hipStreamQuery(st);
+        if (e != hipSuccess && e != hipErrorNotReady) {
+          set_error("BA stream failed: %s", hipGetErrorString(e));
+          return RSPL_E_DEVICE;
+        }
+        if (e == hipSuccess && __atomic_load_n(&b->mail->seq, __ATOMIC_ACQUIRE) < q_first) {
+          set_error("BA mailbox: stream idle but no trial posted");
+          return RSPL_E_DEVICE;
+        }
+        if (clk::now() - t0 > std::chrono::seconds(60)) {
+          set_error("BA mailbox: timed out waiting for the LM trials");
+          return RSPL_E_DEVICE;
+        }
+      }
+      _mm_pause();
+    }
+    if (v[3] != 0.0) break;
+    // rejected trials left iterations to do: queue one trial per remaining iteration
+    if ((rc = enqueue(std::max(1, iters - (int)v[1])))) return rc;
+  }
+  S.lm = nullptr;
+  if (v[2] != 0.0) accept_swap(b, P, Lr, S, true);  // the device's current bank is the host's spare one
+  *chi2_out = v[0];
+  *done_out = (int)v[1];
+  return RSPL_OK;
+}
+
 // one g2o SparseOptimizer::optimize(iters) with OptimizationAlgorithmLevenberg
 int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
              double* chi2_out, int* done_out) {
@@ -274,6 +380,7 @@ int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Acti
   double v[4];
   int rc;
   const bool sh = b->allreduce != nullptr;
+  if (!sh && iters > 0 && ba::fast_path(A.K) && !host_lm()) return optimize_dev(b, P, Lr, S, A, iters, chi2_out, done_out);
   const int n6 = 6 * A.K;
   double* so = b->red + n6 + b->nranks;  // this rank's {chi2, scale, fail} (S.shard_out)
   unsigned long long q = ++b->seq;
@@ -350,16 +457,9 @@ int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Acti
         lambda *= std::max(1. / 3., alpha);
         ni = 2;
         currentChi = tempChi;
-        std::swap(P.T, P.Tn);  // accept: the candidate becomes the current state
-        std::swap(P.X, P.Xn);
-        std::swap(P.L, P.Ln);
-        if (it + 1 < iters) {  // ... and its speculative linearisation the current one
-          std::swap(b->Hpp_e, b->Hpp_s); std::swap(b->bp_e, b->bp_s); std::swap(b->Hll_e, b->Hll_es);
-          std::swap(b->bl_e, b->bl_es); std::swap(b->Hpl_e, b->Hpl_s);
-          std::swap(b->Hll, b->Hll_s); std::swap(b->bl, b->bl_s);
-          Lr.Hpp = b->Hpp_e; Lr.bp = b->bp_e; Lr.Hll = b->Hll_e; Lr.bl = b->bl_e; Lr.Hpl = b->Hpl_e;
-          S.Hll = b->Hll; S.bl = b->bl;
-        }
+        // accept: the candidate becomes the current state, and its speculative linearisation
+        // (when one was made) the current one
+        accept_swap(b, P, Lr, S, it + 1 < iters);
       } else {
         lambda *= ni;  // reject: the current state was never modified (no restore needed)
         ni *= 2;

@@ -156,6 +156,85 @@ __device__ __forceinline__ void post_mail(Mail* m, double v0, double v1, double 
   __hip_atomic_store(&m->seq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
+// ---- device-side LM control (Sys::lm) ----
+// Trial entry: false when the optimize() has already stopped (this trial is a no-op); else the
+// damping, the current bank and whether the candidate's speculative linearisation is wanted
+// (not in the last iteration).  Uniform scalar loads; the control was written by the previous
+// trial's last kernel (kernel boundary = visibility).
+struct LmView {
+  double lambda;
+  int cur, spec;
+};
+__device__ __forceinline__ bool lm_view(const Sys& S, LmView& v) {
+  const LmCtrl* c = S.lm;
+  if (c->stop) return false;
+  v.lambda = c->lambda;
+  v.cur = c->cur;
+  v.spec = c->it + 1 < c->iters;
+  return true;
+}
+template <typename T>
+__device__ __forceinline__ void swp(T& a, T& b) {
+  T t = a;
+  a = b;
+  b = t;
+}
+// bank 1 current: the host's candidate state / spare records are the current ones
+__device__ __forceinline__ void bank_state(Problem& P) {
+  swp(P.T, P.Tn);
+  swp(P.X, P.Xn);
+  swp(P.L, P.Ln);
+}
+__device__ __forceinline__ void bank_lin(Lin& L, Lin& Ls, Sys& S, Sys& Ss) {
+  swp(L.Hpp, Ls.Hpp);
+  swp(L.bp, Ls.bp);
+  swp(L.Hll, Ls.Hll);
+  swp(L.bl, Ls.bl);
+  swp(L.Hpl, Ls.Hpl);
+  swp(S.Hll, Ss.Hll);
+  swp(S.bl, Ss.bl);
+}
+// One trial's verdict, g2o OptimizationAlgorithmLevenberg::solve as restated by ba.cpp optimize()
+// (g2o_optimization.cc:172-210 runs optimize(10) / optimize(5)): rho test with the LM scale,
+// damping update (accept: lambda *= max(1/3, min(2/3, 1 - (2 rho - 1)^3)), ni = 2; reject:
+// lambda *= ni, ni *= 2), at most 10 trials per iteration, stop at qmax == 10 or rho == 0.
+// Returns 1 when the optimize() is finished.
+__device__ int lm_decide(LmCtrl* c, double chi2, double scale, double fail) {
+  const bool ok = fail == 0.0;
+  const double tempChi = ok ? chi2 : DBL_MAX;
+  double rho = c->chi - tempChi;
+  rho /= ok ? scale + 1e-3 : 1.0;
+  double lambda = c->lambda, ni = c->ni;
+  int qmax = c->qmax, it = c->it;
+  bool brk = false;
+  if (rho > 0 && isfinite(tempChi) && ok) {
+    double alpha = 1. - pow(2 * rho - 1, 3.0);
+    alpha = fmin(alpha, 2. / 3.);
+    lambda *= fmax(1. / 3., alpha);
+    ni = 2;
+    c->chi = tempChi;
+    c->cur ^= 1;
+  } else {
+    lambda *= ni;
+    ni *= 2;
+    brk = !isfinite(lambda);
+  }
+  if (!brk) qmax++;
+  int stop = 0;
+  if (brk || !(rho < 0 && qmax < 10)) {  // the iteration ends
+    it++;
+    if (qmax == 10 || rho == 0 || !isfinite(lambda) || it >= c->iters) stop = 1;
+    else qmax = 0;
+  }
+  c->lambda = lambda;
+  c->ni = ni;
+  c->qmax = qmax;
+  c->it = it;
+  c->trials++;
+  c->stop = stop;
+  return stop;
+}
+
 // Last-block ticket: this block's partials were stored device-coherent (relaxed agent-scope
 // atomics, written through), so completing them (vmcnt) before a relaxed ticket increment is
 // enough -- an acq_rel ticket would write back and invalidate the L2 in every block.
@@ -232,6 +311,12 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
     __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(S.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     S.out[2] = 0.0;
+    if (S.lm) {  // device-side LM: decide here; the host reads the outcome only at the end
+      LmCtrl* c = S.lm;
+      const int stop = lm_decide(c, chi2, scale, f);
+      post_mail(S.mail, c->chi, (double)c->it, (double)c->cur, (double)stop, seq);
+      return;
+    }
     post_mail(S.mail, chi2, scale, mx, f, seq);
   }
 }
@@ -239,7 +324,7 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
 // mailbox post of the lambda-init statistic (max Hessian diagonal) after the first linearisation;
 // with npd > 0 it first folds in the pose blocks: per pose, the npd block partials of
 // pose_diag_kernel summed in order
-__global__ __launch_bounds__(256) void post_kernel(Sys S, int K, int npd, unsigned long long seq) {
+__global__ __launch_bounds__(256) void post_kernel(Sys S, int K, int npd, unsigned long long seq, int lm_iters) {
   __shared__ double part[4][64];
   if (npd > 0) {  // entry q = 6 pose + diagonal index: 4 waves each sum every 4th block partial
     const int lane = threadIdx.x & 63, pt = threadIdx.x >> 6, nq6 = 6 * K;
@@ -264,6 +349,18 @@ __global__ __launch_bounds__(256) void post_kernel(Sys S, int K, int npd, unsign
     }
   }
   if (threadIdx.x != 0) return;
+  if (S.lm && lm_iters > 0) {  // device-side LM: computeLambdaInit (tau = 1e-5 x max diagonal)
+    LmCtrl* c = S.lm;
+    c->lambda = 1e-5 * S.out[2];
+    c->ni = 2;
+    c->chi = S.out[0];
+    c->cur = 0;
+    c->it = 0;
+    c->qmax = 0;
+    c->stop = 0;
+    c->iters = lm_iters;
+    c->trials = 0;
+  }
   post_mail(S.mail, S.out[0], S.out[1], S.out[2],
             (double)__hip_atomic_load(S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), seq);
 }
@@ -936,8 +1033,15 @@ __device__ __forceinline__ void prof_stamp(const Sys& S, int slot) {
   if (S.prof) S.prof[slot] = wall_clock64();
 }
 
-__global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active A, Sys S, double lambda) {
+__global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active A, Sys S, double lambda, Lin Ls,
+                                                        Sys Ss) {
   __shared__ double red[64 * 49];
+  if (S.lm) {  // device-side LM: damping and bank from the control
+    LmView v;
+    if (!lm_view(S, v)) return;
+    lambda = v.lambda;
+    if (v.cur) bank_lin(L, Ls, S, Ss);
+  }
   // XCD-aware chunk order: workgroups go round-robin over the 8 XCDs (blockIdx % 8), so
   // landmark range lb runs on XCD lb % 8 for every pose pair -- each XCD's L2 then holds only
   // its ranges' records (~1/8 of them), which its ~k_g pose pairs per landmark re-read
@@ -1120,6 +1224,12 @@ __device__ __forceinline__ void pair_of(int pr, int K, int& a, int& b) {
 __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, Sys S, int n, double lambda) {
   extern __shared__ double Al[];     // rows 0..n, packed lower triangle: the matrix + the bordered rhs row n
   __shared__ int bad;
+  if (S.lm) {  // device-side LM: damping and bank from the control
+    LmView v;
+    if (!lm_view(S, v)) return;
+    lambda = v.lambda;
+    if (v.cur) bank_state(P);
+  }
   const int K = n / 6;
   double* z = Al + pk(n, 0);         // row n: bs -> z = D^-1 L^-1 bs -> solution x
   double* rdg = Al + pk(n + 1, 0);   // [n] 1/D
@@ -1431,7 +1541,19 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
   __shared__ int last;
   const bool stamp = threadIdx.x == 0 && blockIdx.x < 4096;
   if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x);
+  bool spec = SPEC;  // the candidate's speculative linearisation (device LM: not in the last iteration)
+  if (S.lm) {
+    LmView v;
+    if (!lm_view(S, v)) return;
+    lambda = v.lambda;
+    spec = SPEC && v.spec;
+    if (v.cur) {
+      bank_state(P);
+      bank_lin(L, Ls, S, Ss);
+    }
+  }
   if (SPEC && (int)blockIdx.x >= nbu) {
+    if (!spec) return;
     lin_lines<true>(P, Ls, A, Ss, blockIdx.x - nbu, false, lflag, tag,
                     S.prof ? S.prof + kProfUe + 4 * blockIdx.x + 1 : nullptr);
     if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 3);
@@ -1528,7 +1650,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     }
   }
   if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 1);
-  if (SPEC) {  // point landmarks: linearise at the candidate (the errors just written by this lane)
+  if (SPEC && spec) {  // point landmarks: linearise at the candidate (the errors just written by this lane)
     double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bv[3] = {0, 0, 0};
     if (in && point)
       for (int k = k0 + j; k < k1; k += kGroup)
@@ -1583,6 +1705,12 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(S.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     S.out[2] = 0.0;
+    if (S.lm) {  // device-side LM: decide here; the host reads the outcome only at the end
+      LmCtrl* c = S.lm;
+      const int stop = lm_decide(c, chi2, scale, f);
+      post_mail(S.mail, c->chi, (double)c->it, (double)c->cur, (double)stop, seq);
+      return;
+    }
     post_mail(S.mail, chi2, scale, mx, f, seq);
   }
 }
@@ -1765,9 +1893,9 @@ hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys&
   return hipGetLastError();
 }
 
-hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A) {
+hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A, int lm_iters) {
   const int npd = (A && A->K > 0 && A->Ea > 0) ? (A->Ea + 255) / 256 : 0;
-  hipLaunchKernelGGL(post_kernel, dim3(1), dim3(256), 0, s, S, A ? A->K : 0, npd, seq);
+  hipLaunchKernelGGL(post_kernel, dim3(1), dim3(256), 0, s, S, A ? A->K : 0, npd, seq, lm_iters);
   return hipGetLastError();
 }
 
@@ -1789,7 +1917,7 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
                  hipStream_t s, const Spec* spec, bool* fused) {
   *fused = false;
   if (A.npairs * A.nchk > 0)
-    hipLaunchKernelGGL(pair_chunk_kernel, dim3(pair_chunk_blocks(A)), dim3(64), 0, s, P, L, A, S, lambda);
+    hipLaunchKernelGGL(pair_chunk_kernel, dim3(pair_chunk_blocks(A)), dim3(64), 0, s, P, L, A, S, lambda, L, S);
   const int n = 6 * A.K;
   if (fast_path(A.K)) {
     hipError_t e = ensure_schur_attr();
@@ -1816,6 +1944,22 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
   Problem Pn = P;  // cost of the candidate state
   Pn.T = P.Tn; Pn.X = P.Xn; Pn.L = P.Ln;
   hipLaunchKernelGGL(errors_kernel, dim3(errors_blocks(A.Ea)), dim3(256), 0, s, Pn, L, A, S, nbu, seq);
+  return hipGetLastError();
+}
+
+hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq, hipStream_t s,
+                     const Spec& spec) {
+  if (!S.lm || !fast_path(A.K)) return hipErrorInvalidValue;
+  if (A.npairs * A.nchk > 0)
+    hipLaunchKernelGGL(pair_chunk_kernel, dim3(pair_chunk_blocks(A)), dim3(64), 0, s, P, L, A, S, 0.0, spec.Ls,
+                       spec.Ss);
+  hipError_t e = ensure_schur_attr();
+  if (e != hipSuccess) return e;
+  const int n = 6 * A.K;
+  hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, 0.0);
+  const int nbu = update_errors_blocks(A), nbl = A.n_lblk;
+  hipLaunchKernelGGL(update_errors_kernel<true>, dim3(nbu + nbl), dim3(256), 0, s, P, L, A, S, 0.0, seq, spec.Ls,
+                     spec.Ss, nbu, spec.lflag, spec.tag);
   return hipGetLastError();
 }
 
@@ -1856,7 +2000,7 @@ hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8
 
 hipError_t trial_chunks(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, hipStream_t s) {
   if (A.npairs * A.nchk > 0)
-    hipLaunchKernelGGL(pair_chunk_kernel, dim3(pair_chunk_blocks(A)), dim3(64), 0, s, P, L, A, S, lambda);
+    hipLaunchKernelGGL(pair_chunk_kernel, dim3(pair_chunk_blocks(A)), dim3(64), 0, s, P, L, A, S, lambda, L, S);
   hipLaunchKernelGGL(shard_fail_stage_kernel, dim3(1), dim3(1), 0, s, S, S.pairfin + (size_t)A.npairs * 48);
   return hipGetLastError();
 }

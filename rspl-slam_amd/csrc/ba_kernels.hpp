@@ -68,6 +68,21 @@ struct Mail {            // pinned, host-mapped: the per-trial result the host s
   unsigned long long pad[3];
 };
 
+// Device-resident Levenberg-Marquardt control (g2o OptimizationAlgorithmLevenberg::solve,
+// restated in ba.cpp's host loop): initialised after the first linearisation, advanced by the last
+// block of every trial's update_errors kernel, read by the next trial's kernels at their start.
+// Two banks of state + linearisation records alternate: `cur` names the current one (the host's
+// pointer view is bank 0 at the start of each optimize()).  A trial queued after `stop` is a no-op.
+struct LmCtrl {
+  double lambda, ni, chi;  // damping, its growth factor, current chi2
+  int cur;                 // current bank (0: the host's current pointers, 1: its spare/candidate ones)
+  int it;                  // iterations done
+  int qmax;                // trials of the running iteration
+  int stop;                // 1: optimize() finished
+  int iters;               // iterations requested
+  int trials;              // trials evaluated (diagnostics)
+};
+
 struct Sys {
   double* Hll;           // [nL][16]  (points: 3x3 at stride 3)
   double* bl;            // [nL][4]
@@ -93,6 +108,7 @@ struct Sys {
   //   done, ticket, end), [kProfUe + 4b + i] update_errors block b stamps (start, update /
   //   flag wait done, before ticket, end)
   unsigned long long* prof;
+  LmCtrl* lm;            // device-side LM control (fast path, unsharded), null: the host decides
 };
 constexpr int kProfPc = 16, kProfUe = kProfPc + 4 * 4096, kProfLen = kProfUe + 4 * 4096;
 
@@ -107,7 +123,7 @@ hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& 
 hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool with_maxdiag,
                      hipStream_t s);
 // mailbox post; with A, after linearize(with_maxdiag) it first folds the pose-block maxima in
-hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A = nullptr);
+hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A = nullptr, int lm_iters = 0);
 // speculative linearisation of a trial's candidate into a spare record set, fused into the
 // trial's last kernel (fast path only)
 struct Spec {
@@ -120,6 +136,12 @@ struct Spec {
 // with spec on the fast path also the candidate's linearisation (*fused = true)
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
                  hipStream_t s, const Spec* spec, bool* fused);
+// one LM trial under device control (S.lm set, fast path): lambda, the current bank and the
+// accept / reject decision live in *S.lm; the trial's last kernel advances it and posts the mailbox
+// {chi2, iterations done, current bank, stop} + seq.  Always fused with the speculative linearisation
+// (skipped on the device when the iteration is the last one).
+hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq, hipStream_t s,
+                     const Spec& spec);
 // landmark CSR from the per-landmark offsets: atomic slots, then each landmark's list sorted by
 // edge id (deterministic) with its reduced poses; fill[] must be zero on entry
 hipError_t build_csr(const Problem& P, const Active& A, int* fill, int* lm_edges, int* lm_pose, hipStream_t s);
