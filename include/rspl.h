@@ -441,6 +441,90 @@ int rspl_pnp_create(const rspl_pnp_config* cfg, rspl_pnp** out);
 int rspl_pnp_solve(rspl_pnp* h, const rspl_pnp_problem* problems, int batch, rspl_pnp_result* results);
 void rspl_pnp_destroy(rspl_pnp* h);
 
+/* ------------------------------------------------------------------------ */
+/* Map-side local BA: the keyframe / map-point / map-line */
+/* graph of the reference's Map (include/map.h:15-52) and                   */
+/* Map::LocalMapOptimization (src/map.cc:537-808) around rspl_ba_local:      */
+/* window selection (SearchNeighborFrames, :471-525; one extra fixed frame,  */
+/* :593-606), the constraints that enter the BA (:608-707), outlier removal  */
+/* (RemoveOutliers / RemoveLineOutliers, :712-757, :818-895), the            */
+/* covisibility update (UpdateFrameConnection, :897-937), write-back and     */
+/* line endpoints (UppdateMapline, :121-177).  Frames, map points and map    */
+/* lines are named by id (shared_ptr -> id; a frame's map-point / map-line   */
+/* slot holds an id or -1).  Equal covisibility weights are ordered by frame */
+/* id (the reference: by FramePtr address, i.e. allocation order).          */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  const double* camera;          /* [5] fx fy cx cy bf (Map::_camera) */
+  /* OptimizationConfig (_backend_optimization_config, configs_euroc.yaml:56-61) */
+  double th_mono_point, th_stereo_point, th_mono_line, th_stereo_line;
+  int iterations_first, iterations_second;
+} rspl_map_config;
+
+typedef struct {
+  int frame_id;
+  double timestamp;
+  const double* Twc;             /* [16] row-major 4x4 pose (Frame::GetPose) */
+  int n_keypoints;
+  const double* keypoints;       /* [n][3] x, y (features rows 1-2), u_right (< 0: mono) */
+  int n_lines;
+  const double* lines_left;      /* [n_lines][4] Frame::_lines */
+  const double* lines_right;     /* [n_lines][4] Frame::_lines_right (may be NULL) */
+  const uint8_t* lines_right_valid; /* [n_lines] (may be NULL: none) */
+  const int32_t* pol_offsets;    /* [n_lines + 1] CSR of Frame::_points_on_lines (may be NULL) */
+  const int32_t* pol_points;     /*   keypoint index */
+  const double* pol_dist;        /*   distance */
+  int parent_id;                 /* Frame::_parent (-1: none) */
+} rspl_map_keyframe;
+
+typedef struct {
+  int n_poses, n_fixed, n_points, n_lines;
+  int n_mono, n_stereo, n_mono_line, n_stereo_line;
+  int n_point_outliers, n_line_outliers;
+  double chi2_first, chi2_second;
+  int iterations_first, iterations_second;
+} rspl_map_report;
+
+enum { RSPL_MAP_UNTRIANGULATED = 0, RSPL_MAP_GOOD = 1, RSPL_MAP_BAD = 2 };  /* Mappoint::Type */
+
+typedef struct rspl_map rspl_map;
+int rspl_map_create(const rspl_map_config* cfg, rspl_map** out);        /* Map::Map */
+void rspl_map_destroy(rspl_map* m);
+/* Map::InsertKeyframe's bookkeeping (_keyframes, _keyframe_ids; map.cc:24-28) */
+int rspl_map_add_keyframe(rspl_map* m, const rspl_map_keyframe* kf);
+int rspl_map_add_mappoint(rspl_map* m, int id, const double* p, int type);       /* Map::InsertMappoint */
+int rspl_map_add_mapline(rspl_map* m, int id, const double* line3d, int type);   /* Map::InsertMapline */
+/* Mappoint::AddObverser + Frame::InsertMappoint; Mapline::AddObverser + Frame::InsertMapline */
+int rspl_map_add_point_observation(rspl_map* m, int point_id, int frame_id, int keypoint_idx);
+int rspl_map_add_line_observation(rspl_map* m, int line_id, int frame_id, int line_idx);
+/* bulk forms: n map points (types may be NULL: Good); n observations of frame_id */
+int rspl_map_add_mappoints(rspl_map* m, int n, const int32_t* ids, const double* p, const int32_t* types);
+int rspl_map_add_point_observations(rspl_map* m, int frame_id, int n, const int32_t* point_ids,
+                                    const int32_t* keypoints);
+int rspl_map_update_connections(rspl_map* m, int frame_id);             /* Map::UpdateFrameConnection */
+/* Map::LocalMapOptimization(new_frame) with the local BA on `ba` (GPU) */
+int rspl_map_local_optimization(rspl_map* m, int frame_id, rspl_ba* ba, rspl_map_report* report);
+/* the same window / constraint selection without the BA (no write-back, no outlier removal) */
+int rspl_map_assemble(rspl_map* m, int frame_id, rspl_map_report* report);
+/* the rest of LocalMapOptimization (outlier removal, covisibility update, write-back, line
+ * endpoints; map.cc:712-802) applied to the last assembled problem with a supplied BA result */
+int rspl_map_finish(rspl_map* m, const rspl_ba_result* result, rspl_map_report* report);
+/* the last assembled problem: ids of the dense poses / points / lines (ascending, the
+ * LocalmapOptimization vertex order), and per constraint type t (mono, stereo, mono line, stereo
+ * line) the dense pose / landmark index and the observation (2 / 3 / 4 / 8 doubles) */
+int rspl_map_last_problem(const rspl_map* m, int32_t* pose_ids, uint8_t* pose_fixed, int32_t* point_ids,
+                          int32_t* line_ids, int32_t* const* c_pose, int32_t* const* c_lm, double* const* c_obs);
+int rspl_map_get_keyframe(const rspl_map* m, int frame_id, double* Twc, int* n_connections);
+/* Frame::GetOrderedConnections(-1): ascending (weight, frame id) */
+int rspl_map_get_connections(const rspl_map* m, int frame_id, int32_t* ids, int32_t* weights, int cap, int* n);
+int rspl_map_get_mappoint(const rspl_map* m, int id, double* p, int* type, int* n_observers, int32_t* frames,
+                          int32_t* keypoints, int cap);
+int rspl_map_get_mapline(const rspl_map* m, int id, double* line3d, int* type, int* n_observers,
+                         double* endpoints, int* endpoints_valid);
+int rspl_map_get_frame_slots(const rspl_map* m, int frame_id, int32_t* mappoints, int32_t* maplines);
+/* Map::SaveKeyframeTrajectory (map.cc:1007-1024): TUM "t tx ty tz qx qy qz qw", %.9f */
+int rspl_map_save_trajectory(const rspl_map* m, const char* path);
+
 #ifdef __cplusplus
 }
 #endif

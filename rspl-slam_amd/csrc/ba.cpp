@@ -150,7 +150,7 @@ void carve(F& ar, rspl_ba* b) {
   take(b->lm_edges, E); take(b->lm_pose, E);
   take(b->chunk, npairs * nchk * 48); take(b->pairfin, npairs * 48 + 8); take(b->pair_ctr, npairs);
   take(b->red, 6 * K + kMaxRanks + 8);
-  take(b->lmctl, 1);
+  take(b->lmctl, 2);
   take(b->pp_cnt, npairs * nchk); take(b->pp_off, npairs * nchk + 1);
 }
 
@@ -302,7 +302,8 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
   RSPL_HIP(ba::compute_errors(P, Lr, A, S, q, st));
   RSPL_HIP(ba::linearize(P, Lr, A, S, true, st));
   q = ++b->seq;
-  RSPL_HIP(ba::post(S, q, st, &A, iters));  // + computeLambdaInit into the control
+  S.lm_slot = 0;
+  RSPL_HIP(ba::post(S, q, st, &A, iters));  // + computeLambdaInit into the control (slot 0)
   const unsigned long long q_first = b->seq + 1;
   ba::Lin Ls = Lr;
   Ls.Hpp = b->Hpp_s; Ls.bp = b->bp_s; Ls.Hll = b->Hll_es; Ls.bl = b->bl_es; Ls.Hpl = b->Hpl_s;
@@ -321,6 +322,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
         b->prof_nb[1] = ba::update_errors_blocks(A) + A.n_lblk;
         b->prof_nb[2] = ba::update_errors_blocks(A);
       }
+      S.lm_slot = queued & 1;
       const hipError_t e = ba::trial_dev(P, Lr, A, S, q, st, sp);
       S.prof = nullptr;
       if (e != hipSuccess) {

@@ -166,7 +166,7 @@ struct LmView {
   int cur, spec;
 };
 __device__ __forceinline__ bool lm_view(const Sys& S, LmView& v) {
-  const LmCtrl* c = S.lm;
+  const LmCtrl* c = S.lm + S.lm_slot;
   if (c->stop) return false;
   v.lambda = c->lambda;
   v.cur = c->cur;
@@ -199,7 +199,7 @@ __device__ __forceinline__ void bank_lin(Lin& L, Lin& Ls, Sys& S, Sys& Ss) {
 // damping update (accept: lambda *= max(1/3, min(2/3, 1 - (2 rho - 1)^3)), ni = 2; reject:
 // lambda *= ni, ni *= 2), at most 10 trials per iteration, stop at qmax == 10 or rho == 0.
 // Returns 1 when the optimize() is finished.
-__device__ int lm_decide(LmCtrl* c, double chi2, double scale, double fail) {
+__device__ int lm_decide(const LmCtrl* c, LmCtrl* n, double chi2, double scale, double fail) {
   const bool ok = fail == 0.0;
   const double tempChi = ok ? chi2 : DBL_MAX;
   double rho = c->chi - tempChi;
@@ -207,13 +207,14 @@ __device__ int lm_decide(LmCtrl* c, double chi2, double scale, double fail) {
   double lambda = c->lambda, ni = c->ni;
   int qmax = c->qmax, it = c->it;
   bool brk = false;
+  *n = *c;
   if (rho > 0 && isfinite(tempChi) && ok) {
     double alpha = 1. - pow(2 * rho - 1, 3.0);
     alpha = fmin(alpha, 2. / 3.);
     lambda *= fmax(1. / 3., alpha);
     ni = 2;
-    c->chi = tempChi;
-    c->cur ^= 1;
+    n->chi = tempChi;
+    n->cur = c->cur ^ 1;
   } else {
     lambda *= ni;
     ni *= 2;
@@ -226,12 +227,12 @@ __device__ int lm_decide(LmCtrl* c, double chi2, double scale, double fail) {
     if (qmax == 10 || rho == 0 || !isfinite(lambda) || it >= c->iters) stop = 1;
     else qmax = 0;
   }
-  c->lambda = lambda;
-  c->ni = ni;
-  c->qmax = qmax;
-  c->it = it;
-  c->trials++;
-  c->stop = stop;
+  n->lambda = lambda;
+  n->ni = ni;
+  n->qmax = qmax;
+  n->it = it;
+  n->trials = c->trials + 1;
+  n->stop = stop;
   return stop;
 }
 
@@ -311,12 +312,6 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
     __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(S.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     S.out[2] = 0.0;
-    if (S.lm) {  // device-side LM: decide here; the host reads the outcome only at the end
-      LmCtrl* c = S.lm;
-      const int stop = lm_decide(c, chi2, scale, f);
-      post_mail(S.mail, c->chi, (double)c->it, (double)c->cur, (double)stop, seq);
-      return;
-    }
     post_mail(S.mail, chi2, scale, mx, f, seq);
   }
 }
@@ -350,7 +345,7 @@ __global__ __launch_bounds__(256) void post_kernel(Sys S, int K, int npd, unsign
   }
   if (threadIdx.x != 0) return;
   if (S.lm && lm_iters > 0) {  // device-side LM: computeLambdaInit (tau = 1e-5 x max diagonal)
-    LmCtrl* c = S.lm;
+    LmCtrl* c = S.lm;  // slot 0: the first trial's
     c->lambda = 1e-5 * S.out[2];
     c->ni = 2;
     c->chi = S.out[0];
@@ -1544,7 +1539,10 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
   bool spec = SPEC;  // the candidate's speculative linearisation (device LM: not in the last iteration)
   if (S.lm) {
     LmView v;
-    if (!lm_view(S, v)) return;
+    if (!lm_view(S, v)) {  // stopped: carry the control over to the next trial's slot
+      if (blockIdx.x == 0 && threadIdx.x == 0) S.lm[S.lm_slot ^ 1] = S.lm[S.lm_slot];
+      return;
+    }
     lambda = v.lambda;
     spec = SPEC && v.spec;
     if (v.cur) {
@@ -1706,8 +1704,8 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     __hip_atomic_store(S.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     S.out[2] = 0.0;
     if (S.lm) {  // device-side LM: decide here; the host reads the outcome only at the end
-      LmCtrl* c = S.lm;
-      const int stop = lm_decide(c, chi2, scale, f);
+      LmCtrl* c = S.lm + (S.lm_slot ^ 1);
+      const int stop = lm_decide(S.lm + S.lm_slot, c, chi2, scale, f);
       post_mail(S.mail, c->chi, (double)c->it, (double)c->cur, (double)stop, seq);
       return;
     }

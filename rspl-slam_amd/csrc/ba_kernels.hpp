@@ -72,7 +72,8 @@ struct Mail {            // pinned, host-mapped: the per-trial result the host s
 // restated in ba.cpp's host loop): initialised after the first linearisation, advanced by the last
 // block of every trial's update_errors kernel, read by the next trial's kernels at their start.
 // Two banks of state + linearisation records alternate: `cur` names the current one (the host's
-// pointer view is bank 0 at the start of each optimize()).  A trial queued after `stop` is a no-op.
+// pointer view is bank 0 at the start of each optimize()).  A trial queued after `stop` is a no-op
+// that only carries the control over to the next slot.
 struct LmCtrl {
   double lambda, ni, chi;  // damping, its growth factor, current chi2
   int cur;                 // current bank (0: the host's current pointers, 1: its spare/candidate ones)
@@ -108,7 +109,9 @@ struct Sys {
   //   done, ticket, end), [kProfUe + 4b + i] update_errors block b stamps (start, update /
   //   flag wait done, before ticket, end)
   unsigned long long* prof;
-  LmCtrl* lm;            // device-side LM control (fast path, unsharded), null: the host decides
+  LmCtrl* lm;            // device-side LM control [2] (fast path, unsharded), null: the host decides
+  int lm_slot;           // trial k reads lm[k & 1] and its last block writes lm[(k + 1) & 1]: the
+                         // control a trial's blocks read never changes under them
 };
 constexpr int kProfPc = 16, kProfUe = kProfPc + 4 * 4096, kProfLen = kProfUe + 4 * 4096;
 

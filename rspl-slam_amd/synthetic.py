@@ -268,3 +268,125 @@ def pnp_problem(n_points: int = 300, pixel_sigma: float = 0.8, outlier_frac: flo
     out = rng.uniform(size=n_points) < outlier_frac
     kp[out] = np.stack([rng.uniform(0, width, out.sum()), rng.uniform(0, height, out.sum())], 1)
     return np.array(cam, np.float64), X, kp, dict(Rwc=Rwc, twc=twc, outlier=out)
+
+
+# ----------------------------------------------------------------------------
+# Synthetic keyframe sequence for the map-side local BA (Map::InsertKeyframe ->
+# Map::LocalMapOptimization, src/map.cc:24-118, :537-808)
+# ----------------------------------------------------------------------------
+def _Twc(R, t):
+    T = np.eye(4)
+    T[:3, :3] = R
+    T[:3, 3] = t
+    return T
+
+
+def map_sequence(n_keyframes: int = 30, n_points: int = 6000, n_lines: int = 80, seed: int = 0,
+                 pixel_sigma: float = 0.8, outlier_frac: float = 0.03, drift: float = 1.0, step: float = 0.25,
+                 points_per_line: int = 4, frames_per_keyframe: int = 5, width: int = 752, height: int = 480,
+                 cam=(EUROC_FX, EUROC_FY, EUROC_CX, EUROC_CY, EUROC_BF)):
+    """What tracking hands the map, keyframe by keyframe, for a forward-moving stereo rig.
+
+    Returns dict(camera, gt_Twc [n][4][4], timestamps [n], keyframes [n]) where keyframe k is a dict:
+      id, timestamp, parent_id, Twc (the tracked pose: ground truth with an accumulated drift),
+      keypoints [m][3] (x, y, u_right; u_right < 0 = mono), lines_left / lines_right [l][4],
+      lines_right_valid [l], points_on_lines [l] {keypoint: distance},
+      new_points [(id, p)] (first seen here; p = ground truth + a depth-scaled triangulation error),
+      new_lines [(id, Pluecker (w, d))], point_obs [(point id, keypoint)], line_obs [(line id, line)].
+    Landmarks are created Good with a position (the reference triangulates them while inserting the
+    keyframe, map.cc:41-60 -- outside this path).  ``outlier_frac`` of the observations carry gross
+    30-80 px errors, so the BA flags outliers and the map removes them.  Points sampled on the lines
+    are associated with them (points_on_lines), so UppdateMapline finds endpoints.
+    """
+    rng = np.random.default_rng(seed)
+    fx, fy, cx, cy, bf = cam
+    n = n_keyframes
+    gt, tracked, ts = [], [], []
+    drift_R, drift_t = np.eye(3), np.zeros(3)
+    for k in range(n):
+        s = k * step
+        R = _rotvec_to_R(np.array([0.03 * np.sin(0.4 * k), 0.08 * np.sin(0.15 * k), 0.02 * np.sin(0.3 * k)]))
+        t = np.array([0.6 * np.sin(0.12 * k), 0.05 * np.sin(0.3 * k), s])
+        gt.append(_Twc(R, t))
+        if k > 0:  # tracking drift: a random walk on the pose
+            drift_R = _rotvec_to_R(rng.normal(0, 0.002 * drift, 3)) @ drift_R
+            drift_t = drift_t + rng.normal(0, 0.006 * drift, 3)
+        tracked.append(_Twc(drift_R @ R, t + drift_t))
+        ts.append(1403636579.0 + 0.05 * frames_per_keyframe * k)
+    zmax = n * step + 14.0
+    pts = np.stack([rng.uniform(-7, 7, n_points), rng.uniform(-3.5, 3.5, n_points), rng.uniform(1.5, zmax, n_points)], 1)
+    segs = []
+    for _ in range(n_lines):
+        p0 = np.array([rng.uniform(-5, 5), rng.uniform(-2.5, 2.5), rng.uniform(3, zmax - 2)])
+        dv = rng.normal(size=3)
+        dv /= np.linalg.norm(dv)
+        segs.append((p0, p0 + dv * rng.uniform(1.0, 2.5)))
+    # points on the lines (associated with them in the frames)
+    on_line = []
+    for li, (a, b) in enumerate(segs):
+        for u in rng.uniform(0.05, 0.95, points_per_line):
+            on_line.append((li, a + u * (b - a)))
+    n_free = len(pts)
+    pts = np.concatenate([pts, np.array([p for _, p in on_line]).reshape(-1, 3)], 0)
+    line_of_point = {n_free + i: li for i, (li, _) in enumerate(on_line)}
+
+    def project(T, X):
+        Xc = T[:3, :3].T @ (X - T[:3, 3])
+        if Xc[2] <= 0.3 or Xc[2] > 30.0:
+            return None
+        u, v = fx * Xc[0] / Xc[2] + cx, fy * Xc[1] / Xc[2] + cy
+        if not (2 <= u < width - 2 and 2 <= v < height - 2):
+            return None
+        return np.array([u, v, u - bf / Xc[2]]), Xc[2]
+
+    created_p, created_l = set(), set()
+    kfs = []
+    for k in range(n):
+        T = gt[k]
+        kps, pobs, newp = [], [], []
+        kp_of_point = {}
+        for j in range(len(pts)):
+            pr = project(T, pts[j])
+            if pr is None or rng.uniform() < 0.1:   # missed detection / not matched
+                continue
+            uvr, z = pr
+            o = uvr + rng.normal(0, pixel_sigma, 3)
+            if rng.uniform() < outlier_frac:
+                o[:2] += rng.uniform(30, 80, 2) * rng.choice([-1, 1], 2)
+            if not (uvr[2] > 0 and z < 12.0 and rng.uniform() < 0.75):
+                o[2] = -1.0                          # no right match: mono
+            kp_of_point[j] = len(kps)
+            kps.append(o)
+            if j not in created_p:
+                created_p.add(j)
+                err = rng.normal(0, 0.01 + 0.004 * z, 3)
+                newp.append((j, pts[j] + err))
+            pobs.append((j, kp_of_point[j]))
+        ll, lr, lv, pol, lobs, newl = [], [], [], [], [], []
+        for li, (a, b) in enumerate(segs):
+            pa, pb = project(T, a), project(T, b)
+            if pa is None or pb is None:
+                continue
+            idx = len(ll)
+            ll.append(np.array([pa[0][0], pa[0][1], pb[0][0], pb[0][1]]) + rng.normal(0, pixel_sigma, 4))
+            stereo = pa[0][2] > 0 and pb[0][2] > 0 and rng.uniform() < 0.6
+            lr.append(np.array([pa[0][2], pa[0][1], pb[0][2], pb[0][1]]) + rng.normal(0, pixel_sigma, 4)
+                      if stereo else np.zeros(4))
+            lv.append(1 if stereo else 0)
+            pol.append({kp_of_point[j]: float(rng.uniform(0.1, 1.5)) for j, l2 in line_of_point.items()
+                        if l2 == li and j in kp_of_point})
+            lobs.append((li, idx))
+            if li not in created_l:
+                created_l.add(li)
+                d = b - a
+                d = d / np.linalg.norm(d)
+                pc = a + rng.normal(0, 0.03, 3)
+                dd = d + rng.normal(0, 0.01, 3)
+                dd /= np.linalg.norm(dd)
+                newl.append((li, np.concatenate([np.cross(pc, dd), dd])))
+        kfs.append(dict(id=k * frames_per_keyframe, timestamp=ts[k], parent_id=(k - 1) * frames_per_keyframe if k else -1,
+                        Twc=tracked[k], keypoints=np.array(kps).reshape(-1, 3),
+                        lines_left=np.array(ll).reshape(-1, 4), lines_right=np.array(lr).reshape(-1, 4),
+                        lines_right_valid=np.array(lv, np.uint8), points_on_lines=pol,
+                        new_points=newp, new_lines=newl, point_obs=pobs, line_obs=lobs))
+    return dict(camera=np.array(cam, np.float64), gt_Twc=np.array(gt), timestamps=np.array(ts), keyframes=kfs)

@@ -68,6 +68,19 @@ static int layout(void) {
   F(rspl_pnp_problem, iterations); F(rspl_pnp_problem, reprojection_error); F(rspl_pnp_problem, confidence); END();
   BEGIN(rspl_pnp_result); F(rspl_pnp_result, Rwc); F(rspl_pnp_result, twc); F(rspl_pnp_result, inlier);
   F(rspl_pnp_result, n_inliers); F(rspl_pnp_result, hypotheses); END();
+  BEGIN(rspl_map_config); F(rspl_map_config, camera); F(rspl_map_config, th_mono_point);
+  F(rspl_map_config, th_stereo_point); F(rspl_map_config, th_mono_line); F(rspl_map_config, th_stereo_line);
+  F(rspl_map_config, iterations_first); F(rspl_map_config, iterations_second); END();
+  BEGIN(rspl_map_keyframe); F(rspl_map_keyframe, frame_id); F(rspl_map_keyframe, timestamp); F(rspl_map_keyframe, Twc);
+  F(rspl_map_keyframe, n_keypoints); F(rspl_map_keyframe, keypoints); F(rspl_map_keyframe, n_lines);
+  F(rspl_map_keyframe, lines_left); F(rspl_map_keyframe, lines_right); F(rspl_map_keyframe, lines_right_valid);
+  F(rspl_map_keyframe, pol_offsets); F(rspl_map_keyframe, pol_points); F(rspl_map_keyframe, pol_dist);
+  F(rspl_map_keyframe, parent_id); END();
+  BEGIN(rspl_map_report); F(rspl_map_report, n_poses); F(rspl_map_report, n_fixed); F(rspl_map_report, n_points);
+  F(rspl_map_report, n_lines); F(rspl_map_report, n_mono); F(rspl_map_report, n_stereo); F(rspl_map_report, n_mono_line);
+  F(rspl_map_report, n_stereo_line); F(rspl_map_report, n_point_outliers); F(rspl_map_report, n_line_outliers);
+  F(rspl_map_report, chi2_first); F(rspl_map_report, chi2_second); F(rspl_map_report, iterations_first);
+  F(rspl_map_report, iterations_second); END();
   printf("}\n");
   return 0;
 }

@@ -31,7 +31,9 @@ def _mirrors():
             "rspl_ba_config": capi.BaConfig, "rspl_ba_problem": BT.RsplBaProblem, "rspl_ba_result": BT.RsplBaResult,
             "rspl_frame_config": capi.FrameConfig, "rspl_frame_problem": BT.RsplFrameProblem,
             "rspl_frame_result": BT.RsplFrameResult, "rspl_pnp_config": capi.PnpConfig,
-            "rspl_pnp_problem": capi.PnpProblem, "rspl_pnp_result": capi.PnpResult}
+            "rspl_pnp_problem": capi.PnpProblem, "rspl_pnp_result": capi.PnpResult,
+            "rspl_map_config": pkg.mapping.MapConfig, "rspl_map_keyframe": pkg.mapping.MapKeyframe,
+            "rspl_map_report": pkg.mapping.MapReport}
 
 
 def test_struct_layout_matches_ctypes():
