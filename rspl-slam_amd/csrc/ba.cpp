@@ -71,6 +71,7 @@ struct rspl_ba {
   void* ar_ctx = nullptr;
   double* red = nullptr;       // [6 maxK + kMaxRanks + 3] lambda-init / cost all-reduce buffer
   ba::LmCtrl* lmctl = nullptr;  // device-side LM control (fast path, unsharded)
+  double* lm_trace = nullptr;   // RSPL_BA_LMTRACE: per-trial decisions (debug)
   double* gbuf = nullptr;      // final gather buffer (grown on demand)
   size_t gcap = 0;
 };
@@ -303,6 +304,12 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
   RSPL_HIP(ba::linearize(P, Lr, A, S, true, st));
   q = ++b->seq;
   S.lm_slot = 0;
+  static const bool trace = getenv("RSPL_BA_LMTRACE") != nullptr, sync = getenv("RSPL_BA_DEVLM_SYNC") != nullptr;
+  if (trace && !b->lm_trace) {
+    RSPL_HIP(hipMalloc((void**)&b->lm_trace, sizeof(double) * 8 * 64));
+    RSPL_HIP(hipMemset(b->lm_trace, 0, sizeof(double) * 8 * 64));
+  }
+  S.lm_trace = trace ? b->lm_trace + (iters == 10 ? 0 : 8 * 32) : nullptr;
   RSPL_HIP(ba::post(S, q, st, &A, iters));  // + computeLambdaInit into the control (slot 0)
   const unsigned long long q_first = b->seq + 1;
   ba::Lin Ls = Lr;
@@ -329,6 +336,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
         set_error("BA trial launch failed: %s", hipGetErrorString(e));
         return RSPL_E_DEVICE;
       }
+      if (sync && hipStreamSynchronize(st) != hipSuccess) return RSPL_E_DEVICE;
     }
     return RSPL_OK;
   };
@@ -341,11 +349,13 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
     for (unsigned spin = 1;; spin++) {
+      // seqlock read: the next trial may be posting while we read; v is s1's iff vseq is still s1
       const unsigned long long s1 = __atomic_load_n(&b->mail->seq, __ATOMIC_ACQUIRE);
       if (s1 >= q_first && s1 <= q_last) {
         volatile const double* mv = b->mail->v;
         for (int k = 0; k < 4; k++) v[k] = mv[k];
-        if (__atomic_load_n(&b->mail->seq, __ATOMIC_ACQUIRE) == s1 && (s1 == q_last || v[3] != 0.0)) break;
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        if (__atomic_load_n(&b->mail->vseq, __ATOMIC_ACQUIRE) == s1 && (s1 == q_last || v[3] != 0.0)) break;
       }
       if ((spin & 4095) == 0) {
         const hipError_t e = hipStreamQuery(st);
@@ -448,6 +458,9 @@ int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Acti
         RSPL_HIP(ba::linearize(Pc, Ls, A, Ss, false, st));
       }
       if ((rc = wait_mail(b, q, v))) return rc;
+      if (getenv("RSPL_BA_LMTRACE"))
+        fprintf(stderr, "lmtrace-host iters=%d it %d q %d chi2 %.17g scale %.6g fail %g lambda %.6g chi0 %.17g\n", iters, it,
+                qmax, v[0], v[1], v[3], lambda, currentChi);
       const bool ok = v[3] == 0.0;
       const double tempChi = ok ? v[0] : std::numeric_limits<double>::max();
       rho = currentChi - tempChi;
@@ -872,6 +885,16 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   }
   if ((rc = wait_mail(b, q, nullptr))) return rc;
   if (b->prof && b->prof_nb[0]) report_prof(b);
+  if (b->lm_trace) {  // RSPL_BA_LMTRACE: the device LM decisions of both optimize() calls
+    std::vector<double> h(8 * 64);
+    if (hipMemcpy(h.data(), b->lm_trace, sizeof(double) * h.size(), hipMemcpyDeviceToHost) == hipSuccess)
+      for (int k = 0; k < 64; k++)
+        if (h[8 * k] != 0.0)
+          fprintf(stderr, "lmtrace phase %d trial %d chi2 %.17g scale %.6g fail %g lambda %.6g chi0 %.17g cur %g it %g q %g\n",
+                  k / 32, k % 32, h[8 * k], h[8 * k + 1], h[8 * k + 2], h[8 * k + 3], h[8 * k + 4], h[8 * k + 5],
+                  h[8 * k + 6], h[8 * k + 7]);
+    (void)hipMemset(b->lm_trace, 0, sizeof(double) * h.size());
+  }
   if (nq) memcpy(res->points, b->stage + dl.X, sizeof(double) * 3 * nq);
   if (nl) memcpy(res->lines, b->stage + dl.L, sizeof(double) * 6 * nl);
   const double* Tout = reinterpret_cast<const double*>(b->stage + dl.T);

@@ -148,6 +148,9 @@ __device__ __forceinline__ void huber(double e2, double delta, double& r0, doubl
 // system/agent-scope release writes back the whole L2 (~3.5 us, MI355X_MICROARCH.md), once per
 // LM trial on the critical path; the host reads only these uncached words.
 __device__ __forceinline__ void post_mail(Mail* m, double v0, double v1, double v2, double v3, unsigned long long seq) {
+  // vseq first (a reader that sees it change knows v is being rewritten), then v, then seq
+  __hip_atomic_store(&m->vseq, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __hip_atomic_store(&m->v[0], v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&m->v[1], v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   __hip_atomic_store(&m->v[2], v2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -1705,7 +1708,12 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     S.out[2] = 0.0;
     if (S.lm) {  // device-side LM: decide here; the host reads the outcome only at the end
       LmCtrl* c = S.lm + (S.lm_slot ^ 1);
+      const double lam0 = S.lm[S.lm_slot].lambda, chi0 = S.lm[S.lm_slot].chi;
       const int stop = lm_decide(S.lm + S.lm_slot, c, chi2, scale, f);
+      if (S.lm_trace && c->trials <= 64) {
+        double* t = S.lm_trace + 8 * (c->trials - 1);
+        t[0] = chi2; t[1] = scale; t[2] = f; t[3] = lam0; t[4] = chi0; t[5] = c->cur; t[6] = c->it; t[7] = c->qmax;
+      }
       post_mail(S.mail, c->chi, (double)c->it, (double)c->cur, (double)stop, seq);
       return;
     }

@@ -65,7 +65,8 @@ struct Active {          // active structure of one optimize() phase
 struct Mail {            // pinned, host-mapped: the per-trial result the host spins on
   double v[4];           // chi2, scale, maxdiag, fail
   unsigned long long seq;
-  unsigned long long pad[3];
+  unsigned long long vseq;  // written before v (seq after it): v belongs to seq iff vseq == seq
+  unsigned long long pad[2];
 };
 
 // Device-resident Levenberg-Marquardt control (g2o OptimizationAlgorithmLevenberg::solve,
@@ -110,6 +111,7 @@ struct Sys {
   //   flag wait done, before ticket, end)
   unsigned long long* prof;
   LmCtrl* lm;            // device-side LM control [2] (fast path, unsharded), null: the host decides
+  double* lm_trace;      // debug (RSPL_BA_LMTRACE): per trial {chi2, scale, fail, lambda, rho, cur, it, qmax}
   int lm_slot;           // trial k reads lm[k & 1] and its last block writes lm[(k + 1) & 1]: the
                          // control a trial's blocks read never changes under them
 };
