@@ -34,10 +34,12 @@ struct rspl_sg {
   // RSPL_PREC_FP16: transposed fp16 copies [N][K] of every projection / MLP weight
   _Float16* hkw[5];
   _Float16 *hwqkv, *hwm, *hw1, *hw2, *hwf;
+  _Float16 *fwqkv, *fw1, *fw2;  // the same in MFMA B-fragment order (fused GNN layers)
   // activations
   float *kin, *h1, *h2, *X, *QKV, *O, *MSG, *HID, *cpl, *Z, *val0;
   // RSPL_PREC_FP16 GNN activations: fp16 shadow of X, Q | K, V^T per head, messages, hidden
   _Float16 *Xh, *QKh, *Vth, *Oh, *MSGh, *HIDh;
+  _Float16 *Qf[2], *Kf[2], *Vf[2];  // fused layers: q (row-major) / k, v (MFMA fragment order), ping-pong
   int ldv = 0;  // token stride of Vth (nmax rounded up to the 32-key attention tile; zero padded)
   unsigned long long *ug, *vg;  // Sinkhorn u / v exchange granules [B][ld]
   float* cplT = nullptr;        // transposed column slabs when they exceed LDS [B][ld*ld]
@@ -89,10 +91,15 @@ void carve(F& ar, rspl_sg* s) {
   for (int i = 0; i < 5; i++) take(s->hkw[i], (size_t)(i == 0 ? kKencIn : kKencCh[i]) * kKencCh[i + 1]);
   take(s->hwqkv, (size_t)kLayers * 256 * 768); take(s->hwm, (size_t)kLayers * 256 * 256);
   take(s->hw1, (size_t)kLayers * 512 * 512); take(s->hw2, (size_t)kLayers * 512 * 256); take(s->hwf, 256 * 256);
+  take(s->fwqkv, (size_t)kLayers * 256 * 768); take(s->fw1, (size_t)kLayers * 512 * 512);
+  take(s->fw2, (size_t)kLayers * 512 * 256);
   take(s->kin, T * kKencIn); take(s->h1, T * 256); take(s->h2, T * 256);
   take(s->X, T * 256); take(s->QKV, T * 768); take(s->O, T * 256); take(s->MSG, T * 256); take(s->HID, T * 512);
   take(s->Xh, T * 256); take(s->QKh, T * 512); take(s->Vth, (size_t)B * 2 * 256 * s->ldv); take(s->Oh, T * 256);
   take(s->MSGh, T * 256); take(s->HIDh, T * 512);
+  for (int i = 0; i < 2; i++) {
+    take(s->Qf[i], T * 256); take(s->Kf[i], (size_t)B * 2 * 256 * s->ldv); take(s->Vf[i], (size_t)B * 2 * 256 * s->ldv);
+  }
   take(s->cpl, 2 * B * ld * ld); take(s->Z, 2 * B * ld * ld); take(s->ug, B * ld); take(s->vg, B * ld);
   if (s->sink_scratch) take(s->cplT, B * ld * ld);
   take(s->dbg_alpha, 4);
@@ -319,7 +326,11 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
   carve(s->arena, s);
   if (hipMemset(s->ug, 0, sizeof(unsigned long long) * s->B * s->ld) != hipSuccess ||
       hipMemset(s->vg, 0, sizeof(unsigned long long) * s->B * s->ld) != hipSuccess ||
-      hipMemset(s->Vth, 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess) {
+      hipMemset(s->Vth, 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess ||
+      hipMemset(s->Kf[0], 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess ||
+      hipMemset(s->Kf[1], 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess ||
+      hipMemset(s->Vf[0], 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess ||
+      hipMemset(s->Vf[1], 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess) {
     set_error("sinkhorn exchange buffer init failed");
     rspl_sg_destroy(s);
     return RSPL_E_DEVICE;
@@ -351,6 +362,12 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
       okh &= sg::to_half_t(s->w1m + (size_t)l * 512 * 512, 512, 512, s->hw1 + (size_t)l * 512 * 512, s->stream) ==
              hipSuccess;
       okh &= sg::to_half_t(s->w2 + (size_t)l * 512 * 256, 512, 256, s->hw2 + (size_t)l * 512 * 256, s->stream) ==
+             hipSuccess;
+      okh &= sg::to_frag(s->hwqkv + (size_t)l * 256 * 768, 768, 256, s->fwqkv + (size_t)l * 256 * 768, s->stream) ==
+             hipSuccess;
+      okh &= sg::to_frag(s->hw1 + (size_t)l * 512 * 512, 512, 512, s->fw1 + (size_t)l * 512 * 512, s->stream) ==
+             hipSuccess;
+      okh &= sg::to_frag(s->hw2 + (size_t)l * 512 * 256, 256, 512, s->fw2 + (size_t)l * 512 * 256, s->stream) ==
              hipSuccess;
     }
     okh &= sg::to_half_t(s->wf, 256, 256, s->hwf, s->stream) == hipSuccess;
@@ -438,7 +455,49 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
       g.nmax = nm; g.ldv = s->ldv;
       return g;
     };
-    for (int l = 0; l < kLayers; l++) {
+    static const bool unfused = [] {
+      const char* v = getenv("RSPL_SG_GNN");  // A/B knob: "unfused" = four launches per layer
+      return v && std::string(v) == "unfused";
+    }();
+    if (!unfused) {  // layer 0's q / k / v (prologue launch), then one fused launch per layer
+      static unsigned long long* lprobe = nullptr;  // debug: RSPL_SG_LPROBE
+      static const bool lprobing = getenv("RSPL_SG_LPROBE") != nullptr;
+      if (lprobing && !lprobe) {
+        RSPL_HIP(hipMalloc(&lprobe, 8 * sizeof(unsigned long long)));
+        RSPL_HIP(hipMemset(lprobe, 0, 8 * sizeof(unsigned long long)));
+      }
+      {
+        sg::LayerArgs la{};
+        la.Qn = s->Qf[0]; la.Kn = s->Kf[0]; la.Vn = s->Vf[0];
+        la.X = s->X; la.Xh = s->Xh;
+        la.Wq = s->fwqkv; la.bq = s->bqkv;
+        la.n0 = d_n0; la.n1 = d_n1; la.nmax = nm; la.nt = s->ldv / 32; la.qkv_only = 1;
+        RSPL_HIP(sg::gnn_layer(la, B, st));
+      }
+      for (int l = 0; l < kLayers; l++) {
+        sg::LayerArgs la{};
+        la.Qc = s->Qf[l & 1]; la.Kc = s->Kf[l & 1]; la.Vc = s->Vf[l & 1];
+        la.Qn = s->Qf[(l + 1) & 1]; la.Kn = s->Kf[(l + 1) & 1]; la.Vn = s->Vf[(l + 1) & 1];
+        la.X = s->X; la.Xh = s->Xh;
+        la.W1 = s->fw1 + (size_t)l * 512 * 512; la.b1 = s->b1m + (size_t)l * 512;
+        la.W2 = s->fw2 + (size_t)l * 512 * 256; la.b2 = s->b2 + (size_t)l * 256;
+        const int ln = std::min(l + 1, kLayers - 1);
+        la.Wq = s->fwqkv + (size_t)ln * 256 * 768; la.bq = s->bqkv + (size_t)ln * 768;
+        la.n0 = d_n0; la.n1 = d_n1; la.nmax = nm; la.nt = s->ldv / 32; la.cross = l & 1; la.last = l == kLayers - 1;
+        la.probe = lprobe;
+        RSPL_HIP(sg::gnn_layer(la, B, st));
+      }
+      if (lprobing) {
+        unsigned long long h[8];
+        RSPL_HIP(hipStreamSynchronize(st));
+        RSPL_HIP(hipMemcpy(h, lprobe, sizeof(h), hipMemcpyDeviceToHost));
+        RSPL_HIP(hipMemset(lprobe, 0, sizeof(h)));
+        if (h[5])  // 100 MHz wall clock: us = ticks / 100 (17 non-last layers counted)
+          fprintf(stderr, "layer us: attention %.2f mlp0 %.2f mlp3 %.2f qkv %.2f\n", (h[1] - h[0]) / 100.0 / h[5],
+                  (h[2] - h[1]) / 100.0 / h[5], (h[3] - h[2]) / 100.0 / h[5], (h[4] - h[3]) / 100.0 / h[5]);
+      }
+    }
+    for (int l = 0; l < kLayers && unfused; l++) {
       sg::GemmHArgs q = gh(s->Xh, 256, s->hwqkv + (size_t)l * 256 * 768, 768, 256, s->bqkv + (size_t)l * 768);
       q.C16 = s->QKh; q.ldc16 = 512; q.Vt = s->Vth;
       RSPL_HIP(sg::gemm_h(q, 4, st));

@@ -627,6 +627,308 @@ __global__ __launch_bounds__(256) void attn_h_kernel(AttnHArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// One AttentionalGNN layer, fused (fp16 engine; superglue.py:88-173): a 512-thread workgroup
+// owns 32 tokens of one image and runs, without leaving the CU,
+//   (1) multi-head attention of its 32 queries against all keys / values of the source image
+//       (self or cross), flash-style as attn_h_kernel: wave w takes head w & 3 and every
+//       other 32-key tile; the two partial softmax states per head merge through LDS;
+//   (2) mlp.0 on [x | message] (merge folded into W1, BN folded) + ReLU -> HID in LDS;
+//   (3) mlp.3 + the residual: x += delta (fp32 stream, fp16 shadow, and the new fp16 x in LDS);
+//   (4) the NEXT layer's q / k / v projections of the same 32 tokens (v stored transposed).
+// The only cross-token dependency of a layer -- attention reads every token's k / v of the
+// layer -- is the kernel boundary: Q/K/V ping-pong between two buffer sets.  All operands of the
+// 32x32x16 f16 MFMAs: activations from LDS (rows padded to 1040 B), weights straight from
+// global (L2-resident: 1.15 MB per layer, read once per workgroup), fp32 accumulation.
+// One launch per layer instead of four (QKV GEMM, attention, mlp.0, mlp.3).
+// ---------------------------------------------------------------------------
+constexpr int kLdA = 520;  // halves per LDS activation row (512 + 8: 16-byte aligned, bank spread)
+
+// acc[t] += A[32 x K] (LDS rows) * W[n0 + 32 t + r][k]^T, t < NT; W in B-fragment order
+// (to_frag): the operand of (n-tile, k-step) is one contiguous 1 KB read per wave
+template <int NT>
+__device__ __forceinline__ void wave_mm(const _Float16* Al, const _Float16* Wf, int n0, int K, floatx16 (&acc)[NT]) {
+  const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, KS = K / 16;
+  const _Float16* ap = Al + r * kLdA + 8 * h;
+  const _Float16* bp[NT];
+#pragma unroll
+  for (int t = 0; t < NT; t++) bp[t] = Wf + ((size_t)(n0 / 32 + t) * KS * 64 + lane) * 8;
+  constexpr int U = 8;  // k-steps per chunk (16 each): the next chunk's weights load during this one
+  half8 bcur[U][NT], bnxt[U][NT];
+#pragma unroll
+  for (int u = 0; u < U; u++)
+#pragma unroll
+    for (int t = 0; t < NT; t++) bcur[u][t] = *reinterpret_cast<const half8*>(bp[t] + 512 * u);
+  for (int k0 = 0; k0 < K; k0 += 16 * U) {
+    const bool more = k0 + 16 * U < K;
+    const int ks0 = k0 / 16;
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int t = 0; t < NT; t++) bnxt[u][t] = *reinterpret_cast<const half8*>(bp[t] + 512 * (ks0 + U + u));
+    }
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+      const half8 a = *reinterpret_cast<const half8*>(ap + k0 + 16 * u);
+#pragma unroll
+      for (int t = 0; t < NT; t++) acc[t] = mfma16(a, bcur[u][t], acc[t]);
+    }
+    if (more) {
+#pragma unroll
+      for (int u = 0; u < U; u++)
+#pragma unroll
+        for (int t = 0; t < NT; t++) bcur[u][t] = bnxt[u][t];
+    }
+  }
+}
+
+__global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
+  extern __shared__ _Float16 lds_l[];
+  _Float16* Ab = lds_l;               // [32][kLdA]: x (0..255) | message (256..511)
+  _Float16* Hb = lds_l + 32 * kLdA;   // [32][kLdA]: HID; before that the attention merge buffer
+  float* Om = reinterpret_cast<float*>(Hb);  // [4 heads][64 d][32 q]
+  __shared__ float Ml[4][32], Ll[4][32];
+  const int set = blockIdx.y, p = set >> 1, img = set & 1;
+  const int simg = a.cross ? 1 - img : img;
+  const int nk = simg ? a.n1[p] : a.n0[p];
+  const int q0 = blockIdx.x * 32;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, c = lane & 31, kh = lane >> 5;
+  const size_t tok0 = (size_t)set * a.nmax + q0;   // first token of the tile
+  const int kset = p * 2 + simg;
+  if (a.probe && !a.last && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) a.probe[0] += wall_clock64();
+  // x tile -> LDS (rows past the set clamp to its last token; never stored back)
+  for (int e = tid; e < 32 * 32; e += 512) {
+    const int row = e >> 5, ch = e & 31;
+    const int q = min(q0 + row, a.nmax - 1);
+    *reinterpret_cast<uint4*>(Ab + row * kLdA + 8 * ch) =
+        *reinterpret_cast<const uint4*>(a.Xh + ((size_t)set * a.nmax + q) * 256 + 8 * ch);
+  }
+  // the fp32 residual values this lane updates in (3), fetched now so the load latency hides
+  // behind attention and mlp.0: X[token row(i)][32 wv + r]
+  float xres[16];
+  if (!a.qkv_only) {
+    const int r_ = lane & 31, h_ = lane >> 5;
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int row = (i & 3) + 8 * (i >> 2) + 4 * h_;
+      const int q = min(q0 + row, a.nmax - 1);
+      xres[i] = a.X[((size_t)set * a.nmax + q) * 256 + 32 * wv + r_];
+    }
+  }
+  if (a.qkv_only) __syncthreads();  // prologue: layer 0's q / k / v from the current x
+  // ---- (1) attention: head h = wv & 3, key tiles part, part + 2, ... (part = wv >> 2) ----
+  if (!a.qkv_only) {
+    const int h = wv & 3, part = wv >> 2;
+    const _Float16* Qb = a.Qc + (size_t)set * a.nmax * 256 + h * 64;
+    // fragment-ordered k / v of (source set, head): 32-key tile t, k-step / (d-half, key-half) blocks
+    // of 64 lanes x 16 B, every operand load one contiguous 1 KB read
+    const _Float16* Kb = a.Kc + ((size_t)(kset * 4 + h) * a.nt) * 4 * 512 + 8 * lane;
+    const _Float16* Vb = a.Vc + ((size_t)(kset * 4 + h) * a.nt) * 4 * 512 + 8 * lane;
+    half8 qf[4];
+    {
+      const _Float16* qr = Qb + (size_t)min(q0 + c, a.nmax - 1) * 256 + 8 * kh;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; s4++) qf[s4] = *reinterpret_cast<const half8*>(qr + 16 * s4);
+    }
+    floatx16 o0, o1;
+#pragma unroll
+    for (int r = 0; r < 16; r++) {
+      o0[r] = 0.f;
+      o1[r] = 0.f;
+    }
+    float m_run = -INFINITY, l_run = 0.f;
+    const int ntiles = (nk + 31) / 32;
+    // operands two tiles ahead: this wave's tiles are t, t + 2, t + 4, ...; A and B alternate as the
+    // operand sets (the loop body is written for a pair of tiles: static register names, no indexing)
+    half8 kA[4], vA[2][2], kB[4], vB[2][2];
+    auto fetch = [&](int t, half8 (&kf)[4], half8 (&vf)[2][2]) {
+#pragma unroll
+      for (int s4 = 0; s4 < 4; s4++) kf[s4] = *reinterpret_cast<const half8*>(Kb + ((size_t)t * 4 + s4) * 512);
+#pragma unroll
+      for (int dt = 0; dt < 2; dt++)
+#pragma unroll
+        for (int j = 0; j < 2; j++)
+          vf[dt][j] = *reinterpret_cast<const half8*>(Vb + ((size_t)t * 4 + 2 * dt + j) * 512);
+    };
+    auto tile = [&](int t, const half8 (&kc_)[4], const half8 (&vc)[2][2]) {
+      floatx16 st;
+#pragma unroll
+      for (int r = 0; r < 16; r++) st[r] = 0.f;
+#pragma unroll
+      for (int s4 = 0; s4 < 4; s4++) st = mfma16(kc_[s4], qf[s4], st);
+      float x[16];
+      float mx = -INFINITY;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int key = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
+        x[r] = key < nk ? st[r] * 0.125f : -INFINITY;  // scores / dim**.5 (superglue.py:90)
+        mx = fmaxf(mx, x[r]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+      const float m_new = fmaxf(m_run, mx);
+      const float alpha = __expf(m_run - m_new);
+      float sum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        x[r] = __expf(x[r] - m_new);
+        sum += x[r];
+      }
+      sum += __shfl_xor(sum, 32);
+      l_run = l_run * alpha + sum;
+      m_run = m_new;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        o0[r] *= alpha;
+        o1[r] *= alpha;
+      }
+#pragma unroll
+      for (int j = 0; j < 2; j++) {
+        half8 pf;
+#pragma unroll
+        for (int u = 0; u < 8; u++) pf[u] = (_Float16)x[8 * j + u];
+        o0 = mfma16(vc[0][j], pf, o0);
+        o1 = mfma16(vc[1][j], pf, o1);
+      }
+    };
+    if (part < ntiles) fetch(part, kA, vA);
+    if (part + 2 < ntiles) fetch(part + 2, kB, vB);
+    for (int t = part; t < ntiles; t += 4) {
+      tile(t, kA, vA);
+      if (t + 4 < ntiles) fetch(t + 4, kA, vA);
+      if (t + 2 >= ntiles) break;
+      tile(t + 2, kB, vB);
+      if (t + 6 < ntiles) fetch(t + 6, kB, vB);
+    }
+    // merge the two partial states of each head (part 1 -> LDS -> part 0), message -> Ab
+    if (part == 1) {
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int d = (r & 3) + 8 * (r >> 2) + 4 * kh;
+        Om[(h * 64 + d) * 32 + c] = o0[r];
+        Om[(h * 64 + 32 + d) * 32 + c] = o1[r];
+      }
+      if (kh == 0) {
+        Ml[h][c] = m_run;
+        Ll[h][c] = l_run;
+      }
+    }
+    __syncthreads();
+    if (part == 0) {
+      const float m1 = Ml[h][c], l1 = Ll[h][c];
+      const float M = fmaxf(m_run, m1);
+      const float e0 = m_run == -INFINITY ? 0.f : __expf(m_run - M);
+      const float e1 = m1 == -INFINITY ? 0.f : __expf(m1 - M);
+      const float L = e0 * l_run + e1 * l1;
+      const float inv = L > 0.f ? 1.f / L : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const int d = (r & 3) + 8 * (r >> 2) + 4 * kh;
+        const float v0 = (e0 * o0[r] + e1 * Om[(h * 64 + d) * 32 + c]) * inv;
+        const float v1 = (e0 * o1[r] + e1 * Om[(h * 64 + 32 + d) * 32 + c]) * inv;
+        Ab[c * kLdA + 256 + h * 64 + d] = (_Float16)v0;
+        Ab[c * kLdA + 256 + h * 64 + 32 + d] = (_Float16)v1;
+      }
+    }
+    __syncthreads();
+  }
+  if (a.probe && !a.last && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) a.probe[1] += wall_clock64();
+  const int r = lane & 31, hh = lane >> 5;
+  if (!a.qkv_only) {
+  // ---- (2) HID = ReLU([x | message] W1^T + b1): wave wv -> columns 64 wv .. 64 wv + 63 ----
+  {
+    floatx16 acc[2];
+#pragma unroll
+    for (int t = 0; t < 2; t++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[t][i] = 0.f;
+    wave_mm<2>(Ab, a.W1, 64 * wv, 512, acc);
+#pragma unroll
+    for (int t = 0; t < 2; t++) {
+      const int n = 64 * wv + 32 * t + r;
+      const float b = a.b1[n];
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
+        const float v = acc[t][i] + b;
+        Hb[row * kLdA + n] = (_Float16)(v > 0.f ? v : 0.f);
+      }
+    }
+  }
+  __syncthreads();
+  if (a.probe && !a.last && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) a.probe[2] += wall_clock64();
+  // ---- (3) x += HID W2^T + b2 (fp32 stream, fp16 shadow, new x into Ab): columns 32 wv .. +31 ----
+  {
+    floatx16 acc[1];
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc[0][i] = 0.f;
+    wave_mm<1>(Hb, a.W2, 32 * wv, 512, acc);
+    const int n = 32 * wv + r;
+    const float b = a.b2[n];
+#pragma unroll
+    for (int i = 0; i < 16; i++) {
+      const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
+      if (q0 + row >= a.nmax) continue;
+      const float x = xres[i] + (acc[0][i] + b);
+      a.X[(tok0 + row) * 256 + n] = x;
+      const _Float16 xh = (_Float16)x;
+      a.Xh[(tok0 + row) * 256 + n] = xh;
+      Ab[row * kLdA + n] = xh;
+    }
+  }
+  if (a.last) return;
+  __syncthreads();
+  }
+  if (a.probe && !a.last && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) a.probe[3] += wall_clock64();
+  // ---- (4) next layer's q | k | v of these tokens: columns 96 wv .. 96 wv + 95 ----
+  {
+    floatx16 acc[3];
+#pragma unroll
+    for (int t = 0; t < 3; t++)
+#pragma unroll
+      for (int i = 0; i < 16; i++) acc[t][i] = 0.f;
+    wave_mm<3>(Ab, a.Wq, 96 * wv, 256, acc);
+    __syncthreads();  // every wave is done with Ab: the q | k | v tile is staged over Ab + Hb
+    _Float16* Tq = lds_l;  // [32 tokens][776]
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+      const int n = 96 * wv + 32 * t + r;
+      const float b = a.bq[n];
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
+        Tq[row * 776 + n] = (_Float16)(acc[t][i] + b);
+      }
+    }
+    __syncthreads();
+    // q rows out (valid tokens), 16-byte stores
+    for (int e = tid; e < 32 * 32; e += 512) {
+      const int row = e >> 5, ch = e & 31;
+      if (q0 + row < a.nmax)
+        *reinterpret_cast<uint4*>(a.Qn + (tok0 + row) * 256 + 8 * ch) = *reinterpret_cast<const uint4*>(Tq + row * 776 + 8 * ch);
+    }
+    // k / v in fragment order: this tile is key tile q0 / 32 of the set; 16 + 16 blocks of 1 KB
+    const int kt = q0 >> 5;
+    for (int e = tid; e < 2 * 16 * 64; e += 512) {
+      const int isv = e >> 10, blk = (e >> 6) & 15, L = e & 63, cl = L & 31, kl = L >> 5, hd = blk >> 2, q4 = blk & 3;
+      _Float16* dst = (isv ? a.Vn : a.Kn) + (((size_t)(set * 4 + hd) * a.nt + kt) * 4 + q4) * 512 + 8 * L;
+      if (!isv) {  // k: key cl, dims 16 q4 + 8 kl .. +7 of head hd
+        *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(Tq + cl * 776 + 256 + 64 * hd + 16 * q4 + 8 * kl);
+      } else {  // v: dim 32 dt + cl, keys 16 j + 4 kl + {0..3, 8..11} (q4 = 2 dt + j)
+        const int dt = q4 >> 1, j = q4 & 1, d = 512 + 64 * hd + 32 * dt + cl, k0 = 16 * j + 4 * kl;
+        half8 v;
+#pragma unroll
+        for (int u = 0; u < 8; u++) v[u] = Tq[(k0 + (u < 4 ? u : u + 4)) * 776 + d];
+        *reinterpret_cast<half8*>(dst) = v;
+      }
+    }
+  }
+  if (a.probe && !a.last && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
+    a.probe[4] += wall_clock64();
+    a.probe[5] += 1;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // process_input + NormalizeKeypoints: one wave per token.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
@@ -1260,6 +1562,39 @@ hipError_t gemm_h(const GemmHArgs& a, int mode, hipStream_t s) {
 
 hipError_t attention_h(const AttnHArgs& a, int B, hipStream_t s) {
   hipLaunchKernelGGL(attn_h_kernel, dim3((a.nmax + 31) / 32, 4, B * 2), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t gnn_layer(const LayerArgs& a, int B, hipStream_t s) {
+  constexpr size_t lds = sizeof(_Float16) * 2 * 32 * kLdA;  // x | message, HID (>= the 32 x 776 q|k|v stage)
+  static_assert(2 * kLdA >= 776, "q | k | v staging tile exceeds the LDS carve");
+  static bool attr = false;
+  if (!attr) {
+    const hipError_t e = hipFuncSetAttribute((const void*)layer_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                             (int)lds);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  hipLaunchKernelGGL(layer_kernel, dim3((a.nmax + 31) / 32, B * 2), dim3(512), lds, s, a);
+  return hipGetLastError();
+}
+
+// n-major fp16 weights Wt [N][K] -> 32x32x16 MFMA B-fragment order: block (nt, ks) = the 64 lanes'
+// 16-byte operands of n-tile nt, k-step ks, lane L = r + 32 h holding Wt[32 nt + r][16 ks + 8 h ..];
+// a wave's operand load is then one contiguous 1 KB read
+__global__ void frag_kernel(const _Float16* Wt, int N, int K, _Float16* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;  // one 8-half operand
+  const int KS = K / 16;
+  if (i >= (N / 32) * KS * 64) return;
+  const int L = i & 63, blk = i >> 6, nt = blk / KS, ks = blk - nt * KS, r = L & 31, h = L >> 5;
+  *reinterpret_cast<uint4*>(out + (size_t)i * 8) =
+      *reinterpret_cast<const uint4*>(Wt + (size_t)(32 * nt + r) * K + 16 * ks + 8 * h);
+}
+
+hipError_t to_frag(const _Float16* Wt, int N, int K, _Float16* out, hipStream_t s) {
+  if (N % 32 || K % 16) return hipErrorInvalidValue;
+  const int n = (N / 32) * (K / 16) * 64;
+  hipLaunchKernelGGL(frag_kernel, dim3((n + 255) / 256), dim3(256), 0, s, Wt, N, K, out);
   return hipGetLastError();
 }
 

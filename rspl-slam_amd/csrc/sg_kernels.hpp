@@ -66,6 +66,33 @@ struct AttnHArgs {
   int cross;
 };
 
+// One fused AttentionalGNN layer (fp16 engine): attention -> [x | message] MLP -> residual ->
+// the next layer's Q / K / V^T, per 32-token tile of one image (layer_kernel).  QK / Vt of the
+// running layer are read (all tokens of the source image), the next layer's are written to the
+// other buffer of the ping-pong pair.
+struct LayerArgs {
+  const _Float16* Qc;    // [T][256] q of this layer (head-contiguous), row-major
+  const _Float16* Kc;    // k of this layer, MFMA-fragment order per (set, head, 32-key tile, k-step)
+  const _Float16* Vc;    // v of this layer, fragment order per (set, head, key tile, d-half, key-half)
+  _Float16* Qn;          // the next layer's (written unless last)
+  _Float16* Kn;
+  _Float16* Vn;
+  float* X;              // [T][256] fp32 residual stream
+  _Float16* Xh;          // [T][256] fp16 shadow
+  const _Float16* W1;    // mlp.0 (merge folded in), [512 n][512 k] in B-fragment order (to_frag)
+  const float* b1;
+  const _Float16* W2;    // mlp.3 [256][512], fragment order
+  const float* b2;
+  const _Float16* Wq;    // next layer's q | k | v [768][256] (head-contiguous rows), fragment order
+  const float* bq;
+  const int* n0;
+  const int* n1;
+  int nmax, nt;          // tokens per image set; 32-key tiles per set in Kc / Vc (ldv / 32)
+  int cross, last;
+  int qkv_only;          // prologue: only phase (4) from the current x (layer 0's q / k / v)
+  unsigned long long* probe;  // debug (RSPL_SG_LPROBE): phase wall clocks of workgroup (0, 0)
+};
+
 struct PrepArgs {
   const double* f0;   // [B][stride][259]
   const double* f1;
@@ -131,8 +158,10 @@ struct DecodeArgs {
 hipError_t gemm(const GemmArgs& a, int batch, hipStream_t s);
 // Wt[n][k] = (fp16) W[k][n] for a [K][N] fp32 weight (one-time, at create)
 hipError_t to_half_t(const float* W, int K, int N, _Float16* Wt, hipStream_t s);
+hipError_t to_frag(const _Float16* Wt, int N, int K, _Float16* out, hipStream_t s);
 hipError_t gemm_h(const GemmHArgs& a, int mode, hipStream_t s);
 hipError_t attention_h(const AttnHArgs& a, int B, hipStream_t s);
+hipError_t gnn_layer(const LayerArgs& a, int B, hipStream_t s);
 // fp32 -> fp16, n elements
 hipError_t to_half(const float* x, _Float16* y, size_t n, hipStream_t s);
 hipError_t prep(const PrepArgs& a, hipStream_t s);
