@@ -6,10 +6,12 @@ fallback -- if librspl.so is missing or no HIP device is visible, calls raise.
 from __future__ import annotations
 
 import ctypes as C
+import os
 import pathlib
 
 PKG = pathlib.Path(__file__).resolve().parent
-LIB_PATH = PKG / "librspl.so"
+# RSPL_LIB: another in-tree build of the same ABI (A/B timing of two builds in one GPU call)
+LIB_PATH = PKG / os.environ.get("RSPL_LIB", "librspl.so")
 
 RSPL_OK = 0
 RSPL_PREC_FP32 = 0

@@ -23,6 +23,7 @@ struct rspl_sp {
   float *wPD, *bPD, *wPb, *bPb, *wDb, *bDb;
   // RSPL_PREC_FP16: the 3x3 conv weights as fp16 [9][Cout][Cin]
   _Float16 *hw1b, *hw2a, *hw2b, *hw3a, *hw3b, *hw4a, *hw4b, *hwPD;
+  _Float16 *fwPb, *fwDb;  // convPb / convDb in MFMA B-fragment order (sp::HeadHArgs / TapArgs)
   // activations
   float *actA, *actB, *cells, *scores, *nms, *desc;
   unsigned long long* cand;
@@ -82,6 +83,7 @@ void carve(F& ar, rspl_sp* s, int B, int H, int W, int cap) {
   take(s->hwPD, 9 * 128 * 512);
   take(s->wPb, 256 * 96); take(s->bPb, 96);
   take(s->wDb, 256 * 256); take(s->bDb, 256);
+  take(s->fwPb, 256 * 96); take(s->fwDb, 256 * 256);
   take(s->actA, B * HW * 16);
   take(s->actB, B * HW * 16);
   take(s->cells, B * P * 512);
@@ -186,6 +188,18 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
     for (int co = 0; co < 256; co++)
       for (int ci = 0; ci < 256; ci++) d[ci * 256 + co] = wDb->data[co * 256 + ci];
     ok &= up(s->wPb, r) && up(s->bPb, b) && up(s->wDb, d) && up(s->bDb, bDb->data);
+    // fp16 fragments: [N-tile][k-step][lane][8], lane (c, h) holding W[16 t + 8 h + j][32 n + c]
+    auto frag = [](const std::vector<float>& wkn, int N) {
+      std::vector<_Float16> f((size_t)256 * N);
+      for (int n = 0; n < N / 32; n++)
+        for (int t = 0; t < 16; t++)
+          for (int lane = 0; lane < 64; lane++)
+            for (int j = 0; j < 8; j++)
+              f[(((size_t)n * 16 + t) * 64 + lane) * 8 + j] =
+                  (_Float16)wkn[(size_t)(16 * t + 8 * (lane >> 5) + j) * N + 32 * n + (lane & 31)];
+      return f;
+    };
+    ok &= uph(s->fwPb, frag(r, 96)) && uph(s->fwDb, frag(d, 256));
   }
   {  // src/super_point.cpp:148: float(u8) / 255.0 computed in double, stored as float
     std::vector<float> lut(256);
@@ -212,6 +226,25 @@ extern "C" void rspl_sp_destroy(rspl_sp* s) {
   if (s->stream) (void)hipStreamDestroy(s->stream);
   delete s;
 }
+
+namespace {
+// NMS + threshold + borders (superpoint.py:16-33, super_point.cpp:154-183), then top-k
+// (super_point.cpp:185-204); stage marks 4 -> 5 -> 6 are the caller's
+int nms_topk(rspl_sp* s, int B, int H, int W, int k, hipStream_t st) {
+  using namespace sp;
+  RSPL_HIP(hipMemsetAsync(s->cand_count, 0, sizeof(int) * B, st));
+  NmsArgs n{};
+  n.scores = s->scores; n.nms_out = s->nms; n.cand = s->cand; n.cand_count = s->cand_count; n.cand_cap = s->cand_cap;
+  n.H = H; n.W = W; n.threshold = s->cfg.keypoint_threshold; n.border = s->cfg.remove_borders;
+  RSPL_HIP(nms(n, B, st));
+  s->timer.mark(5, st);
+  TopkArgs t{};
+  t.cand = s->cand; t.cand_count = s->cand_count; t.cand_cap = s->cand_cap; t.lds_cap = kCandCap; t.k = k;
+  t.sel = s->sel; t.sel_count = s->sel_count; t.sel_cap = kCandCap;
+  RSPL_HIP(topk(t, B, st));
+  return RSPL_OK;
+}
+}  // namespace
 
 extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, int H, int W, int stride,
                                     size_t image_pitch, double* d_features, int capacity, int32_t* d_counts,
@@ -254,8 +287,27 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
     c.hin = hB; c.hw = s->hw4b; c.bias = s->b4b; c.hout = hA;
     RSPL_HIP(conv3x3_h(c, 128, false, false, false, B, st));                  // conv4b
     s->timer.mark(2, st);
-    c.cout = 512; c.hin = hA; c.hw = s->hwPD; c.bias = s->bPD; c.out = s->cells;
-    RSPL_HIP(conv3x3_h(c, 128, false, false, true, B, st));                   // convPa | convDa (fp32 out)
+    c.cout = 512; c.hin = hA; c.hw = s->hwPD; c.bias = s->bPD; c.hout = reinterpret_cast<_Float16*>(s->cells);
+    RSPL_HIP(conv3x3_h(c, 128, false, false, false, B, st));                  // convPa | convDa (fp16 out)
+    s->timer.mark(3, st);
+    // detector head (superpoint.py:130-135) on fp16 MFMA
+    HeadHArgs h{};
+    h.cells = c.hout; h.wPb = s->fwPb; h.bPb = s->bPb; h.scores = s->scores; h.B = B; h.P = P; h.W8 = W8;
+    RSPL_HIP(det_head_h(h, st));
+    s->timer.mark(4, st);
+    if (int rc = nms_topk(s, B, H, W, k, st)) return rc;
+    // descriptor head at the sampled taps + sampling + packing (superpoint.py:159-161,
+    // super_point.cpp:206-319)
+    s->timer.mark(6, st);
+    TapArgs ta{};
+    ta.cells = c.hout; ta.wDb = s->fwDb; ta.bDb = s->bDb;
+    ta.sel = s->sel; ta.sel_count = s->sel_count; ta.sel_stride = kCandCap; ta.per_image = (k > 0 ? k : kCandCap);
+    ta.nms = s->nms; ta.features = d_features; ta.feat_cap = capacity; ta.counts = d_counts; ta.B = B; ta.H = H; ta.W = W;
+    RSPL_HIP(sample_taps_h(ta, st));
+    s->timer.mark(7, st);
+    s->timer.end_call();
+    s->last_B = B; s->last_H = H; s->last_W = W;
+    return RSPL_OK;
   } else {
     // encoder (superpoint.py:117-127)
     c.H = H; c.W = W; c.cout = 64; c.w = s->w1b; c.bias = s->b1b; c.out = s->actA;
@@ -284,19 +336,8 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
   RSPL_HIP(heads(h, 0, st));
   h.w = s->wDb; h.bias = s->bDb; h.desc = s->desc;
   RSPL_HIP(heads(h, 1, st));
-  // NMS + threshold + borders (superpoint.py:16-33, super_point.cpp:154-183)
   s->timer.mark(4, st);
-  RSPL_HIP(hipMemsetAsync(s->cand_count, 0, sizeof(int) * B, st));
-  NmsArgs n{};
-  n.scores = s->scores; n.nms_out = s->nms; n.cand = s->cand; n.cand_count = s->cand_count; n.cand_cap = s->cand_cap;
-  n.H = H; n.W = W; n.threshold = s->cfg.keypoint_threshold; n.border = s->cfg.remove_borders;
-  RSPL_HIP(nms(n, B, st));
-  // top-k (super_point.cpp:185-204)
-  s->timer.mark(5, st);
-  TopkArgs t{};
-  t.cand = s->cand; t.cand_count = s->cand_count; t.cand_cap = s->cand_cap; t.lds_cap = kCandCap; t.k = k;
-  t.sel = s->sel; t.sel_count = s->sel_count; t.sel_cap = kCandCap;
-  RSPL_HIP(topk(t, B, st));
+  if (int rc = nms_topk(s, B, H, W, k, st)) return rc;
   // descriptor sampling + packing (super_point.cpp:206-319)
   s->timer.mark(6, st);
   SampleArgs sa{};
@@ -352,6 +393,8 @@ extern "C" int rspl_sp_debug_maps(rspl_sp* s, int b, float* scores, float* desc)
   RSPL_HIP(hipStreamSynchronize(s->stream));
   if (scores) RSPL_HIP(hipMemcpy(scores, s->nms + (size_t)b * H * W, sizeof(float) * H * W, hipMemcpyDeviceToHost));
   if (desc) {
+    RSPL_CHECK_ARG(s->cfg.precision == RSPL_PREC_FP32,
+                   "RSPL_PREC_FP16 forms descriptors only at the sampled keypoints' taps (no dense map)");
     // device layout [P][256] -> channel-major [256][P] like the reference tensor
     const size_t P = (size_t)H * W / 64;
     std::vector<float> tmp(P * 256);

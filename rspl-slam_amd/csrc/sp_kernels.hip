@@ -465,6 +465,201 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// RSPL_PREC_FP16 heads.  The fp16 convPa | convDa map ([P][512] halves) is read straight into
+// v_mfma_f32_32x32x16_f16 A operands (lane (r, h): cell r, channels 16t + 8h .. +7); the 1x1
+// weights come from L2 in B-fragment order, so neither head stages anything through LDS.
+//   det_head_h:    convPb 256->65, softmax over 65, dustbin dropped, depth-to-space
+//                  (superpoint.py:131-135); one wave per 32 cells.
+//   sample_taps_h: convDb 256->256 + per-cell L2 normalise (superpoint.py:160-161) evaluated
+//                  only at the 4 bilinear taps of each selected keypoint (the dense map is never
+//                  formed: the 1x1 conv and the per-cell normalise are pointwise, so this is the
+//                  same function), then the double-precision bilinear sample and renormalise of
+//                  src/super_point.cpp:206-319.  A workgroup takes 8 keypoints = 32 tap rows
+//                  (one M-tile); wave w owns output channels 64w .. 64w+63.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void det_head_h_kernel(HeadHArgs a) {
+  constexpr int NT = 3;  // 96 columns, 65 real
+  const int total = a.B * a.P;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, ml = lane & 31, kl = lane >> 5;
+  const int base = (blockIdx.x * 4 + wv) * 32;
+  if (base >= total) return;  // per wave: no barriers below
+  const _Float16* row = a.cells + (size_t)min(base + ml, total - 1) * 512 + 8 * kl;
+  half8 av[16];
+#pragma unroll
+  for (int t = 0; t < 16; t++) av[t] = *reinterpret_cast<const half8*>(row + 16 * t);
+  floatx16 acc[NT];
+#pragma unroll
+  for (int n = 0; n < NT; n++)
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[n][r] = 0.f;
+  const half8* wf = reinterpret_cast<const half8*>(a.wPb) + lane;
+#pragma unroll
+  for (int t = 0; t < 16; t++) {
+    half8 bv[NT];
+#pragma unroll
+    for (int n = 0; n < NT; n++) bv[n] = wf[(n * 16 + t) * 64];
+#pragma unroll
+    for (int n = 0; n < NT; n++) acc[n] = mfma16(av[t], bv[n], acc[n]);
+  }
+#pragma unroll
+  for (int n = 0; n < NT; n++) {
+    const float b = a.bPb[n * 32 + ml];
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[n][r] += b;
+  }
+  const int Wf = a.W8 * 8;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    float m = -INFINITY;
+#pragma unroll
+    for (int n = 0; n < NT; n++)
+      if (n * 32 + ml < 65) m = fmaxf(m, acc[n][r]);
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 32));
+    float e[NT], sum = 0.f;
+#pragma unroll
+    for (int n = 0; n < NT; n++) {
+      e[n] = (n * 32 + ml < 65) ? expf(acc[n][r] - m) : 0.f;
+      sum += e[n];
+    }
+#pragma unroll
+    for (int o = 16; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 32);
+    const int cell = base + (r & 3) + 8 * (r >> 2) + 4 * kl;
+    if (cell < total) {
+      const int bi = cell / a.P, p = cell % a.P;
+      const int cy = p / a.W8, cx = p % a.W8;
+      float* sc = a.scores + (size_t)bi * a.P * 64;
+#pragma unroll
+      for (int n = 0; n < 2; n++) {  // channels 0..63 (the dustbin, 64, is dropped)
+        const int c = n * 32 + ml;
+        sc[(size_t)(cy * 8 + (c >> 3)) * Wf + cx * 8 + (c & 7)] = e[n] / sum;
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void sample_taps_h_kernel(TapArgs a) {
+  __shared__ int tcell[32];      // tap row 4 kp + q: cell of tap q (nw, ne, sw, se) of keypoint kp
+  __shared__ double twt[32];     // its bilinear weight
+  __shared__ float part[4][32];  // per-wave partial sums of squares per tap row
+  __shared__ double part2[4][8]; // per-wave partial sums of squares per keypoint
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, ml = lane & 31, kl = lane >> 5;
+  const int bpi = (a.per_image + 7) / 8;
+  const int bi = blockIdx.x / bpi, i0 = (blockIdx.x % bpi) * 8;
+  if (bi >= a.B) return;
+  const int n = a.sel_count[bi];
+  if (tid == 0 && i0 == 0) a.counts[bi] = n;
+  if (i0 >= n) return;  // uniform over the workgroup
+  const int H = a.H, W = a.W, h = H / 8, w = W / 8, P = h * w;
+  if (tid < 8) {
+    const int i = i0 + tid;
+    int c[4] = {0, 0, 0, 0};
+    double wt[4] = {0, 0, 0, 0};
+    if (i < n) {
+      const unsigned flat = a.sel[(size_t)bi * a.sel_stride + i];
+      const int y = flat / W, x = flat % W;
+      // normalize_keypoints (:276-287; s/2 is integer division) and grid_sample (:294-332)
+      const double gx = ((double)x - 8 / 2 + 0.5) / (w * 8 - 8 / 2 - 0.5) * 2 - 1;
+      const double gy = ((double)y - 8 / 2 + 0.5) / (h * 8 - 8 / 2 - 0.5) * 2 - 1;
+      const double ix = ((gx + 1) / 2) * (w - 1), iy = ((gy + 1) / 2) * (h - 1);
+      auto clip = [](int v, int m) { return v < 0 ? 0 : (v < m - 1 ? v : m - 1); };
+      const int ix_nw = clip((int)floor(ix), w), iy_nw = clip((int)floor(iy), h);
+      const int ix_ne = clip(ix_nw + 1, w), iy_ne = clip(iy_nw, h);
+      const int ix_sw = clip(ix_nw, w), iy_sw = clip(iy_nw + 1, h);
+      const int ix_se = clip(ix_nw + 1, w), iy_se = clip(iy_nw + 1, h);
+      wt[0] = (ix_se - ix) * (iy_se - iy);
+      wt[1] = (ix - ix_sw) * (iy_sw - iy);
+      wt[2] = (ix_ne - ix) * (iy - iy_ne);
+      wt[3] = (ix - ix_nw) * (iy - iy_nw);
+      c[0] = iy_nw * w + ix_nw;
+      c[1] = iy_ne * w + ix_ne;
+      c[2] = iy_sw * w + ix_sw;
+      c[3] = iy_se * w + ix_se;
+      double* f = a.features + ((size_t)bi * a.feat_cap + i) * 259;
+      f[0] = (double)a.nms[(size_t)bi * H * W + flat];
+      f[1] = (double)x;
+      f[2] = (double)y;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      tcell[4 * tid + q] = c[q];
+      twt[4 * tid + q] = wt[q];
+    }
+  }
+  __syncthreads();
+  const _Float16* row = a.cells + ((size_t)bi * P + tcell[ml]) * 512 + 256 + 8 * kl;
+  half8 av[16];
+#pragma unroll
+  for (int t = 0; t < 16; t++) av[t] = *reinterpret_cast<const half8*>(row + 16 * t);
+  floatx16 acc[2];
+#pragma unroll
+  for (int j = 0; j < 2; j++)
+#pragma unroll
+    for (int r = 0; r < 16; r++) acc[j][r] = 0.f;
+  const half8* wf = reinterpret_cast<const half8*>(a.wDb) + lane;
+#pragma unroll
+  for (int t = 0; t < 16; t++) {
+    const half8 b0 = wf[((2 * wv) * 16 + t) * 64], b1 = wf[((2 * wv + 1) * 16 + t) * 64];
+    acc[0] = mfma16(av[t], b0, acc[0]);
+    acc[1] = mfma16(av[t], b1, acc[1]);
+  }
+  // bias; per tap row (register r, lane half kl: row (r & 3) + 8 (r >> 2) + 4 kl) the sum of
+  // squares over this wave's 64 channels, then over the 4 waves in a fixed order
+  const float bias0 = a.bDb[64 * wv + ml], bias1 = a.bDb[64 * wv + 32 + ml];
+  float ss[16];
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    acc[0][r] += bias0;
+    acc[1][r] += bias1;
+    ss[r] = acc[0][r] * acc[0][r] + acc[1][r] * acc[1][r];
+  }
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1)
+#pragma unroll
+    for (int r = 0; r < 16; r++) ss[r] += __shfl_xor(ss[r], o, 32);
+  if (ml == 0)
+#pragma unroll
+    for (int r = 0; r < 16; r++) part[wv][(r & 3) + 8 * (r >> 2) + 4 * kl] = ss[r];
+  __syncthreads();
+  // keypoint kp = 2 q + kl holds its taps in registers 4q .. 4q+3 (nw, ne, sw, se)
+  double v[4][2], s2[4];
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int kp = 2 * q + kl;
+    double vv0 = 0, vv1 = 0;
+#pragma unroll
+    for (int tp = 0; tp < 4; tp++) {
+      const int rw = 4 * kp + tp;
+      float nrm = sqrtf(((part[0][rw] + part[1][rw]) + part[2][rw]) + part[3][rw]);
+      nrm = nrm < 1e-12f ? 1e-12f : nrm;
+      const double wt = twt[rw];
+      vv0 += (double)(acc[0][4 * q + tp] / nrm) * wt;
+      vv1 += (double)(acc[1][4 * q + tp] / nrm) * wt;
+    }
+    v[q][0] = vv0;
+    v[q][1] = vv1;
+    s2[q] = vv0 * vv0 + vv1 * vv1;
+  }
+#pragma unroll
+  for (int o = 16; o >= 1; o >>= 1)
+#pragma unroll
+    for (int q = 0; q < 4; q++) s2[q] += __shfl_xor(s2[q], o, 32);
+  if (ml == 0)
+#pragma unroll
+    for (int q = 0; q < 4; q++) part2[wv][2 * q + kl] = s2[q];
+  __syncthreads();
+#pragma unroll
+  for (int q = 0; q < 4; q++) {
+    const int kp = 2 * q + kl, i = i0 + kp;
+    if (i >= n) continue;
+    const double inv = 1.0 / sqrt(((part2[0][kp] + part2[1][kp]) + part2[2][kp]) + part2[3][kp]);
+    double* f = a.features + ((size_t)bi * a.feat_cap + i) * 259 + 3 + 64 * wv + ml;
+    f[0] = inv * v[q][0];
+    f[32] = inv * v[q][1];
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Fused simple_nms (5 x 9x9 max-pools) + threshold / border candidate
 // extraction.  Tile 32x32 outputs, halo 20, separable LDS max.  Scores are
 // softmax outputs (>= 0) and every window contains its centre, so zero padding
@@ -783,6 +978,18 @@ hipError_t heads(const HeadArgs& a, int mode, hipStream_t s) {
     hipLaunchKernelGGL(head_kernel<0>, dim3(blocks), dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL(head_kernel<1>, dim3(blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t det_head_h(const HeadHArgs& a, hipStream_t s) {
+  const int blocks = (a.B * a.P + 127) / 128;
+  hipLaunchKernelGGL(det_head_h_kernel, dim3(blocks), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t sample_taps_h(const TapArgs& a, hipStream_t s) {
+  const int blocks = a.B * ((a.per_image + 7) / 8);
+  hipLaunchKernelGGL(sample_taps_h_kernel, dim3(blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 

@@ -35,6 +35,31 @@ struct HeadArgs {
   int B, P, W8;
 };
 
+// RSPL_PREC_FP16 heads on v_mfma_f32_32x32x16_f16, weights in B-fragment order
+// ([N-tile][k-step][lane][8]: one contiguous 1 KB operand load per wave)
+struct HeadHArgs {
+  const _Float16* cells; // [B*P][512] (convPa | convDa, ReLU'd, fp16)
+  const _Float16* wPb;   // convPb fragments: 3 N-tiles x 16 k-steps (65 real of 96 columns)
+  const float* bPb;      // [96]
+  float* scores;         // [B][H][W]
+  int B, P, W8;
+};
+
+struct TapArgs {         // descriptors at the sampled keypoints' bilinear taps only
+  const _Float16* cells; // [B*P][512]: convDa at channels 256..511
+  const _Float16* wDb;   // convDb fragments: 8 N-tiles x 16 k-steps
+  const float* bDb;      // [256]
+  const unsigned* sel;
+  const int* sel_count;
+  int sel_stride;
+  int per_image;         // keypoint slots per image (>= max selected)
+  const float* nms;      // [B][H][W]
+  double* features;      // [B][feat_cap][259]
+  int feat_cap;
+  int32_t* counts;       // [B]
+  int B, H, W;
+};
+
 struct NmsArgs {
   const float* scores;   // [B][H][W]
   float* nms_out;        // [B][H][W]
@@ -77,6 +102,8 @@ hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hi
 hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool out_f32, int B, hipStream_t s,
                      hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 hipError_t heads(const HeadArgs& a, int mode, hipStream_t s);
+hipError_t det_head_h(const HeadHArgs& a, hipStream_t s);
+hipError_t sample_taps_h(const TapArgs& a, hipStream_t s);
 hipError_t nms(const NmsArgs& a, int B, hipStream_t s);
 hipError_t topk(const TopkArgs& a, int B, hipStream_t s);
 hipError_t sample(const SampleArgs& a, hipStream_t s);
