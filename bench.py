@@ -130,7 +130,7 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
     as SURVEY.md 8(d): conv1a+conv1b 2*H*W*64*(9 + 576) FLOP per image; GNN 2*(655,360 N + 512 N M)
     per image per layer; Sinkhorn streamed model 2*iters*4*(N+1)(M+1) bytes per pair; NMS 2*4*H*W
     bytes per image.  Single-kernel stages carry the kernel name (pmc_kernel) whose PMC traffic
-    summary under profiles/ gives `traffic`; the GNN is a 72-launch family (single_kernel false)."""
+    summary under profiles/ gives `traffic`; the GNN is a launch family (single_kernel false)."""
     t = {**{f"sp:{n}": v / max(1, sp_calls) for n, v in zip(sp.STAGES, sp_ms)},
          **{f"sg:{n}": v / max(1, sg_calls) for n, v in zip(sg.STAGES, sg_ms)}}
     N = M = K
@@ -140,7 +140,9 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
     rows = (("sp:conv1a+1b+pool", 2 * conv1_gflop_per_image(), "TFLOP/s", mfma_peak, "mfma", conv1_k, True,
              "GFLOP per launch (2 images, conv1a+conv1b)"),
             ("sg:gnn x18", 2 * 2 * 18 * 2 * (655360 * N + 512 * N * M) / 1e9, "TFLOP/s", mfma_peak, "mfma",
-             "gemm_rk_kernel", False, "GFLOP per step (2 pairs x 2 images x 18 layers, 72 launches)"),
+             "layer_kernel" if precision == "fp16" else "gemm_kernel", False,
+             "GFLOP per step (2 pairs x 2 images x 18 layers; fp16: 19 launches of the fused layer kernel, "
+             "fp32: 4 GEMM/attention launches per layer)"),
             ("sg:sinkhorn", 2 * 2 * 100 * 4 * (N + 1) * (M + 1) / 1e9, "GB/s", HBM_PEAK_GBS, "hbm", "sinkhorn_kernel",
              True, "GB per launch (2 pairs, streamed model 2*iters*4*(N+1)(M+1))"),
             ("sp:nms", 2 * 2 * 4 * H * W / 1e9, "GB/s", HBM_PEAK_GBS, "hbm", "nms_kernel", True,

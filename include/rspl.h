@@ -525,6 +525,52 @@ int rspl_map_get_frame_slots(const rspl_map* m, int frame_id, int32_t* mappoints
 /* Map::SaveKeyframeTrajectory (map.cc:1007-1024): TUM "t tx ty tz qx qy qz qw", %.9f */
 int rspl_map_save_trajectory(const rspl_map* m, const char* path);
 
+/* ------------------------------------------------------------------------------------------ */
+/* Line front end after the detector.  FLD (cv::ximgproc) and the RCF edge  */
+/* net are not rebuilt: detected segments enter here.                                          */
+/* ------------------------------------------------------------------------------------------ */
+
+/* LineDetector::LineExtractor after fld->detect (src/line_processor.cc:460-490): segments
+ * [n][4] float as FLD returns them on the half-size image -> lines [n_out][4] double at full
+ * size; do_merge runs MergeLines(0.05, 5, 15), FilterShortLines(30), MergeLines(0.03, 3, 50),
+ * FilterShortLines(60) (:492-665, 11-24).  Host code (a sequential clustering); *n_out is set
+ * even when it exceeds capacity (RSPL_E_CAPACITY). */
+int rspl_line_extract(const float* segments, int n, int do_merge, double* lines, int capacity, int* n_out);
+
+typedef struct rspl_lines rspl_lines;
+typedef struct rspl_lines_config {
+  int max_lines;   /* lines per image, <= 1024 */
+  int max_points;  /* keypoints per image, <= 4096 */
+  int max_pairs;   /* point-line pairs per image (the sum of the std::map sizes) */
+  int max_matches; /* point matches per MatchLines call */
+  int device;
+} rspl_lines_config;
+
+int rspl_lines_create(const rspl_lines_config* cfg, rspl_lines** out);
+void rspl_lines_destroy(rspl_lines* h);
+/* AssignPointsToLines(lines, points, relation) (src/line_processor.cc:163-216) on the GPU.
+ * lines [n_lines][4] double; features = the 259 x N column-major keypoint records (x, y = rows
+ * 1, 2).  relation as CSR: line i's points are point_idx[offsets[i] .. offsets[i+1]) in
+ * ascending index order (the std::map<int, double> order) with dist[] = the map values. */
+int rspl_lines_assign(rspl_lines* h, const double* lines, int n_lines, const double* features, int n_points,
+                      int* offsets, int* point_idx, double* dist, int capacity);
+/* MatchLines(points_on_line0, points_on_line1, point_matches, point_num0, point_num1, line_matches)
+ * (src/line_processor.cc:221-283) on the GPU.  The relations as rspl_lines_assign returns them
+ * (the distances are not needed); matches [n_matches][2] = (queryIdx, trainIdx);
+ * line_matches [n_lines0]: the matched line of image 1, or -1. */
+int rspl_lines_match(rspl_lines* h, const int* offsets0, const int* idx0, int n_lines0, const int* offsets1,
+                     const int* idx1, int n_lines1, const int* matches, int n_matches, int n_points0, int n_points1,
+                     int* line_matches);
+/* The line part of Frame::AddLeftFeatures + Frame::AddRightFeatures (src/frame.cc:124-129,
+ * 150-196): the stereo matches inside the disparity window (camera_limits = {MinXDiff,
+ * MaxXDiff, MaxYDiff}, frame.cc:157-167), both images' point-line assignments (one launch),
+ * MatchLines -> per left line the right line and its validity (line_matches[i] > 0, as the
+ * reference tests it).  *n_kept_matches = the filtered stereo matches' count. */
+int rspl_lines_stereo(rspl_lines* h, const double* lines_left, int n_left, const double* features_left,
+                      int n_points_left, const double* lines_right, int n_right, const double* features_right,
+                      int n_points_right, const int* stereo_matches, int n_matches, const double* camera_limits,
+                      double* lines_right_out, uint8_t* lines_right_valid, int* n_kept_matches);
+
 #ifdef __cplusplus
 }
 #endif

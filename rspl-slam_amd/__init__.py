@@ -6,7 +6,7 @@ this package only mirrors the reference's C++ interface over its C ABI.
 """
 import importlib
 
-from . import capi, weights, synthetic, ba_types, hostgroup, mapping, trajectory, sequence  # noqa: F401
+from . import capi, weights, synthetic, ba_types, hostgroup, mapping, trajectory, sequence, lines  # noqa: F401
 
 _API = ("SuperPoint", "SuperPointConfig", "SuperGlue", "SuperGlueConfig", "PointMatching",
         "LocalmapOptimization", "LocalBA", "FrameOptimization", "FrameBA",

@@ -35,6 +35,8 @@ EXPORTS = [
     "rspl_ba_set_shard", "rspl_comm_unique_id", "rspl_comm_create", "rspl_comm_allreduce_sum", "rspl_comm_destroy",
     "rspl_ba_set_comm", "rspl_group_create", "rspl_group_destroy", "rspl_ba_set_group",
     "rspl_pnp_create", "rspl_pnp_solve", "rspl_pnp_destroy",
+    "rspl_line_extract", "rspl_lines_create", "rspl_lines_destroy", "rspl_lines_assign", "rspl_lines_match",
+    "rspl_lines_stereo",
 ]
 
 

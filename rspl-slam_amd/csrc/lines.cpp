@@ -1,0 +1,441 @@
+// Line front end after the detector: the LineDetector merge passes on the
+// host, point-to-line assignment and shared-point line matching on the GPU (line_kernels.hip).
+//
+//   LineDetector::LineExtractor after fld->detect   src/line_processor.cc:460-490
+//   LineDetector::MergeLines, MergeTwoLines,
+//   FilterShortLines, PointLineDistance, AngleDiff   src/line_processor.cc:11-161, 492-665
+//   AssignPointsToLines / MatchLines                 src/line_processor.cc:163-283 (kernels)
+//   Frame::AddRightFeatures (line part)              src/frame.cc:150-203
+//
+// The merge is a sequential clustering over a few hundred segments per image (an angle sort, a
+// neighbour search that breaks early in sorted order, BFS clusters, pairwise merges whose result
+// depends on the order): it stays on the host, in the reference's float / double types.  FLD
+// itself (cv::ximgproc) and the RCF edge net are not rebuilt: segments enter through the API.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <numeric>
+#include <set>
+#include <type_traits>
+#include <unordered_map>
+#include <vector>
+
+#include "common.hpp"
+#include "line_kernels.hpp"
+
+#pragma clang fp contract(off)
+
+using namespace rspl;
+
+namespace {
+
+struct Seg {
+  float v[4];
+};
+
+// line_processor.cc:11-24 (float lines)
+void filter_short(std::vector<Seg>& ls, float thr) {
+  const float t2 = thr * thr;
+  size_t k = 0;
+  for (const Seg& s : ls) {
+    const float dx = s.v[2] - s.v[0], dy = s.v[3] - s.v[1];
+    if (dx * dx + dy * dy > t2) ls[k++] = s;
+  }
+  ls.resize(k);
+}
+
+// line_processor.cc:41-50: float numerator; std::pow(float, int) is a double, so is the root
+float point_line_distance(const Seg& l, float x0, float y0) {
+  const float x1 = l.v[0], y1 = l.v[1], x2 = l.v[2], y2 = l.v[3];
+  const float num = std::fabs((y2 - y1) * x0 + (x1 - x2) * y0 + ((x2 * y1) - (x1 * y2)));
+  const double a = (double)(y2 - y1), b = (double)(x1 - x2);
+  return (float)(num / std::sqrt(a * a + b * b));
+}
+
+// line_processor.cc:92-96
+float angle_diff(float a1, float a2) {
+  const float c1 = std::fabs(a2 - a1);
+  const float c2 = (float)(M_PI + (double)std::min(a1, a2) - (double)std::max(a1, a2));
+  return std::min(c1, c2);
+}
+
+// line_processor.cc:98-161: length-weighted centroid and angle in double; the angle of each
+// segment is atan of the float slope (the float overload, atanf)
+Seg merge_two(const Seg& p, const Seg& q) {
+  const float ax = p.v[0], ay = p.v[1], bx = p.v[2], by = p.v[3];
+  const float cx = q.v[0], cy = q.v[1], dx = q.v[2], dy = q.v[3];
+  const float dlix = bx - ax, dliy = by - ay, dljx = dx - cx, dljy = dy - cy;
+  const double li = std::sqrt((double)(dlix * dlix) + (double)(dliy * dliy));
+  const double lj = std::sqrt((double)(dljx * dljx) + (double)(dljy * dljy));
+  const double xg = (li * (double)(ax + bx) + lj * (double)(cx + dx)) / (2.0 * (li + lj));
+  const double yg = (li * (double)(ay + by) + lj * (double)(cy + dy)) / (2.0 * (li + lj));
+  const double thi = dlix == 0.0f ? M_PI / 2.0 : (double)atanf(dliy / dlix);
+  const double thj = dljx == 0.0f ? M_PI / 2.0 : (double)atanf(dljy / dljx);
+  double thr;
+  if (std::fabs(thi - thj) <= M_PI / 2.0) {
+    thr = (li * thi + lj * thj) / (li + lj);
+  } else {
+    const double tmp = thj - M_PI * (thj / std::fabs(thj));
+    thr = (li * thi + lj * tmp) / (li + lj);
+  }
+  const double s = std::sin(thr), c = std::cos(thr);
+  const double g[4] = {((double)ay - yg) * s + ((double)ax - xg) * c, ((double)by - yg) * s + ((double)bx - xg) * c,
+                       ((double)cy - yg) * s + ((double)cx - xg) * c, ((double)dy - yg) * s + ((double)dx - xg) * c};
+  const double lo = std::min(g[0], std::min(g[1], std::min(g[2], g[3])));
+  const double hi = std::max(g[0], std::max(g[1], std::max(g[2], g[3])));
+  Seg r;
+  r.v[0] = (float)(lo * std::cos(thr) + xg);
+  r.v[1] = (float)(lo * std::sin(thr) + yg);
+  r.v[2] = (float)(hi * std::cos(thr) + xg);
+  r.v[3] = (float)(hi * std::sin(thr) + yg);
+  return r;
+}
+
+// line_processor.cc:492-665
+std::vector<Seg> merge_lines(const std::vector<Seg>& src, float angle_thr, float dist_thr, float ep) {
+  const size_t n = src.size();
+  std::vector<Seg> dst;
+  if (n == 0) return dst;  // the reference maps src[0] of an empty vector (undefined): empty in, empty out
+  std::vector<float> ang(n), len(n);
+  for (size_t i = 0; i < n; i++) {
+    const float dx = src[i].v[2] - src[i].v[0], dy = src[i].v[3] - src[i].v[1];
+    ang[i] = atanf(dy / dx);
+    len[i] = std::sqrt(dx * dx + dy * dy);
+  }
+  std::vector<size_t> order(n);
+  std::iota(order.begin(), order.end(), 0);
+  std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return ang[a] < ang[b]; });
+  const float ep2 = ep * ep, quarter = (float)(M_PI / 4.0);
+  // neighbours in the reference's push_back order: by sorted position of the other line
+  std::vector<std::vector<size_t>> nbr(n);
+  for (size_t i = 0; i < n; i++) {
+    const size_t a = order[i];
+    float x11 = src[a].v[0], y11 = src[a].v[1], x12 = src[a].v[2], y12 = src[a].v[3];
+    const float a1 = ang[a];
+    const bool sx = std::fabs(a1) < quarter;
+    if ((sx && x12 < x11) || (!sx && y12 < y11)) {
+      std::swap(x11, x12);
+      std::swap(y11, y12);
+    }
+    for (size_t j = i + 1; j < n; j++) {
+      const size_t b = order[j];
+      float x21 = src[b].v[0], y21 = src[b].v[1], x22 = src[b].v[2], y22 = src[b].v[3];
+      if ((sx && x22 < x21) || (!sx && y22 < y21)) {
+        std::swap(x21, x22);
+        std::swap(y21, y22);
+      }
+      if (angle_diff(a1, ang[b]) > angle_thr) {
+        if (std::fabs(a1) < (M_PI_2 - (double)angle_thr)) break;  // sorted: no later line is closer
+        continue;
+      }
+      const float m1x = 0.5f * (src[a].v[0] + src[a].v[2]), m1y = 0.5f * (src[a].v[1] + src[a].v[3]);
+      const float m2x = 0.5f * (src[b].v[0] + src[b].v[2]), m2y = 0.5f * (src[b].v[1] + src[b].v[3]);
+      if (point_line_distance(src[b], m1x, m1y) > dist_thr && point_line_distance(src[a], m2x, m2y) > dist_thr)
+        continue;
+      float cx12, cy12, cx21, cy21;
+      if ((sx && x12 > x22) || (!sx && y12 > y22)) {
+        cx12 = x22; cy12 = y22; cx21 = x11; cy21 = y11;
+      } else {
+        cx12 = x12; cy12 = y12; cx21 = x21; cy21 = y21;
+      }
+      bool merge = (sx && cx12 >= cx21) || (!sx && cy12 >= cy21);
+      if (!merge) merge = (cx21 - cx12) * (cx21 - cx12) + (cy21 - cy12) * (cy21 - cy12) < ep2;
+      if (merge) {
+        nbr[a].push_back(b);
+        nbr[b].push_back(a);
+      }
+    }
+  }
+  // connected components (breadth-first, each frontier in ascending line order)
+  std::vector<int> code(n, -1);
+  std::vector<std::vector<size_t>> clusters;
+  for (size_t i = 0; i < n; i++) {
+    if (code[i] >= 0) continue;
+    const int c = (int)clusters.size();
+    code[i] = c;
+    std::vector<size_t> todo = nbr[i], cl{i};
+    while (!todo.empty()) {
+      std::set<size_t> next;
+      for (size_t j : todo) {
+        if (code[j] < 0) {
+          code[j] = c;
+          cl.push_back(j);
+        }
+        for (size_t k : nbr[j])
+          if (code[k] < 0) next.insert(k);
+      }
+      todo.assign(next.begin(), next.end());
+    }
+    clusters.push_back(std::move(cl));
+  }
+  // sub-clusters: longest first, each unclaimed line with its direct neighbours
+  std::vector<std::vector<size_t>> subs;
+  for (auto& cl : clusters) {
+    if (cl.size() <= 2) {
+      subs.push_back(cl);
+      continue;
+    }
+    std::sort(cl.begin(), cl.end(), [&](size_t a, size_t b) { return len[a] > len[b]; });
+    std::unordered_map<size_t, size_t> at;
+    for (size_t k = 0; k < cl.size(); k++) at[cl[k]] = k;
+    std::vector<bool> taken(cl.size(), false);
+    for (size_t k = 0; k < cl.size(); k++) {
+      if (taken[k]) continue;
+      std::vector<size_t> sub{cl[k]};
+      for (size_t m : nbr[cl[k]]) {
+        taken[at[m]] = true;
+        sub.push_back(m);
+      }
+      subs.push_back(std::move(sub));
+    }
+  }
+  dst.reserve(subs.size());
+  for (auto& sub : subs) {
+    Seg l = src[sub[0]];
+    for (size_t k = 1; k < sub.size(); k++) l = merge_two(l, src[sub[k]]);
+    dst.push_back(l);
+  }
+  return dst;
+}
+
+}  // namespace
+
+extern "C" int rspl_line_extract(const float* segments, int n, int do_merge, double* lines, int capacity, int* n_out) {
+  RSPL_CHECK_ARG(n >= 0 && n_out && (n == 0 || segments) && capacity >= 0 && (capacity == 0 || lines),
+                 "rspl_line_extract: bad argument");
+  std::vector<Seg> src((size_t)n);
+  for (int i = 0; i < n; i++)
+    for (int k = 0; k < 4; k++) src[i].v[k] = segments[4 * i + k] * 2;  // detected on the half-size image
+  std::vector<Seg> dst;
+  if (do_merge) {
+    std::vector<Seg> tmp = merge_lines(src, 0.05f, 5.f, 15.f);
+    filter_short(tmp, 30.f);
+    dst = merge_lines(tmp, 0.03f, 3.f, 50.f);
+    filter_short(dst, 60.f);
+  } else {
+    dst = std::move(src);
+  }
+  *n_out = (int)dst.size();
+  if ((int)dst.size() > capacity) {
+    set_error("%zu lines exceed capacity %d", dst.size(), capacity);
+    return RSPL_E_CAPACITY;
+  }
+  for (size_t i = 0; i < dst.size(); i++)
+    for (int k = 0; k < 4; k++) lines[4 * i + k] = (double)dst[i].v[k];
+  return RSPL_OK;
+}
+
+struct rspl_lines {
+  rspl_lines_config cfg{};
+  hipStream_t stream = nullptr;
+  Arena arena;
+  int cap = 0;
+  double *lines, *pts, *dist;
+  int *n_lines, *n_points, *offsets, *idx, *status;
+  int *matches, *n_matches, *M, *inv, *out;
+};
+
+extern "C" int rspl_lines_create(const rspl_lines_config* cfg, rspl_lines** out) {
+  RSPL_CHECK_ARG(cfg && out, "rspl_lines_create: NULL argument");
+  RSPL_CHECK_ARG(cfg->max_lines > 0 && cfg->max_lines <= 1024, "max_lines must be in [1, 1024]");
+  RSPL_CHECK_ARG(cfg->max_points > 0 && cfg->max_points <= lines::kMaxPointsLds, "max_points must be in [1, %d]",
+                 lines::kMaxPointsLds);
+  RSPL_CHECK_ARG(cfg->max_pairs > 0 && cfg->max_matches >= 0, "max_pairs must be > 0, max_matches >= 0");
+  *out = nullptr;
+  RSPL_HIP(hipSetDevice(cfg->device));
+  auto* h = new rspl_lines();
+  h->cfg = *cfg;
+  h->cap = cfg->max_pairs;
+  const size_t L = cfg->max_lines, N = cfg->max_points, C = cfg->max_pairs, Mm = std::max(1, cfg->max_matches);
+  // two assignment sets (left / right, or frame 0 / frame 1) and two matching problems
+  auto carve = [&](auto& ar) {
+    auto take = [&](auto*& p, size_t n) {
+      using T = std::remove_pointer_t<std::remove_reference_t<decltype(p)>>;
+      if constexpr (std::is_same_v<std::remove_reference_t<decltype(ar)>, Arena>) p = ar.template take<T>(n);
+      else ar.template take<T>(n);
+    };
+    take(h->lines, 2 * L * 4); take(h->pts, 2 * N * 2); take(h->dist, 2 * C);
+    take(h->n_lines, 2); take(h->n_points, 2); take(h->offsets, 2 * (L + 1)); take(h->idx, 2 * C);
+    take(h->status, 2); take(h->matches, 2 * Mm * 2); take(h->n_matches, 2); take(h->M, 2 * L * L);
+    take(h->inv, 2 * 2 * C); take(h->out, 2 * L);
+  };
+  Sizer sz;
+  carve(sz);
+  if (int rc = h->arena.reserve(sz.used)) {
+    delete h;
+    return rc;
+  }
+  carve(h->arena);
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+    rspl_lines_destroy(h);
+    set_error("stream creation failed");
+    return RSPL_E_DEVICE;
+  }
+  *out = h;
+  return RSPL_OK;
+}
+
+extern "C" void rspl_lines_destroy(rspl_lines* h) {
+  if (!h) return;
+  if (h->stream) (void)hipStreamSynchronize(h->stream);
+  h->arena.release();
+  if (h->stream) (void)hipStreamDestroy(h->stream);
+  delete h;
+}
+
+namespace {
+
+// one image's lines and keypoint (x, y) into assignment set `set`
+int stage_image(rspl_lines* h, int set, const double* lines, int n_lines, const double* features, int n_points) {
+  RSPL_CHECK_ARG(n_lines >= 0 && n_lines <= h->cfg.max_lines, "n_lines %d outside [0, %d]", n_lines, h->cfg.max_lines);
+  RSPL_CHECK_ARG(n_points >= 0 && n_points <= h->cfg.max_points, "n_points %d outside [0, %d]", n_points,
+                 h->cfg.max_points);
+  RSPL_CHECK_ARG((n_lines == 0 || lines) && (n_points == 0 || features), "NULL lines / features");
+  const size_t L = h->cfg.max_lines, N = h->cfg.max_points;
+  std::vector<double> xy((size_t)2 * n_points);
+  for (int j = 0; j < n_points; j++) {  // rows 1, 2 of the 259 x N column-major features
+    xy[2 * j] = features[(size_t)259 * j + 1];
+    xy[2 * j + 1] = features[(size_t)259 * j + 2];
+  }
+  const int cnt[2] = {n_lines, n_points};
+  RSPL_HIP(hipMemcpyAsync(h->lines + set * L * 4, lines, sizeof(double) * 4 * n_lines, hipMemcpyHostToDevice, h->stream));
+  RSPL_HIP(hipMemcpyAsync(h->pts + set * N * 2, xy.data(), sizeof(double) * xy.size(), hipMemcpyHostToDevice, h->stream));
+  RSPL_HIP(hipMemcpyAsync(h->n_lines + set, &cnt[0], sizeof(int), hipMemcpyHostToDevice, h->stream));
+  RSPL_HIP(hipMemcpyAsync(h->n_points + set, &cnt[1], sizeof(int), hipMemcpyHostToDevice, h->stream));
+  RSPL_HIP(hipStreamSynchronize(h->stream));  // the host vectors above go out of scope
+  return RSPL_OK;
+}
+
+int run_assign(rspl_lines* h, int B) {
+  lines::AssignArgs a{};
+  a.lines = h->lines; a.n_lines = h->n_lines; a.pts = h->pts; a.pt_batch = (size_t)h->cfg.max_points * 2;
+  a.pt_stride = 2; a.pt_xoff = 0; a.n_points = h->n_points; a.offsets = h->offsets; a.idx = h->idx;
+  a.dist = h->dist; a.max_lines = h->cfg.max_lines; a.cap = h->cap; a.status = h->status;
+  RSPL_HIP(lines::assign(a, B, h->stream));
+  int st[2] = {0, 0};
+  RSPL_HIP(hipMemcpyAsync(st, h->status, sizeof(int) * B, hipMemcpyDeviceToHost, h->stream));
+  RSPL_HIP(hipStreamSynchronize(h->stream));
+  for (int b = 0; b < B; b++)
+    if (st[b]) {
+      set_error("point-line pairs exceed max_pairs %d", h->cap);
+      return RSPL_E_CAPACITY;
+    }
+  return RSPL_OK;
+}
+
+int read_assignment(rspl_lines* h, int set, int n_lines, int* offsets, int* point_idx, double* dist, int capacity) {
+  RSPL_HIP(hipMemcpy(offsets, h->offsets + (size_t)set * (h->cfg.max_lines + 1), sizeof(int) * (n_lines + 1),
+                     hipMemcpyDeviceToHost));
+  const int tot = offsets[n_lines];
+  if (tot > capacity) {
+    set_error("%d point-line pairs exceed capacity %d", tot, capacity);
+    return RSPL_E_CAPACITY;
+  }
+  if (tot) {
+    RSPL_HIP(hipMemcpy(point_idx, h->idx + (size_t)set * h->cap, sizeof(int) * tot, hipMemcpyDeviceToHost));
+    RSPL_HIP(hipMemcpy(dist, h->dist + (size_t)set * h->cap, sizeof(double) * tot, hipMemcpyDeviceToHost));
+  }
+  return RSPL_OK;
+}
+
+int stage_assignment(rspl_lines* h, int set, const int* offsets, const int* idx, int n_lines, int n_points) {
+  RSPL_CHECK_ARG(n_lines >= 0 && n_lines <= h->cfg.max_lines && n_points >= 0 && n_points <= h->cfg.max_points,
+                 "assignment sizes outside the handle's limits");
+  RSPL_CHECK_ARG(offsets && offsets[0] == 0, "offsets must start at 0");
+  for (int l = 0; l < n_lines; l++) RSPL_CHECK_ARG(offsets[l + 1] >= offsets[l], "offsets must be non-decreasing");
+  const int tot = offsets[n_lines];
+  RSPL_CHECK_ARG(tot <= h->cap, "%d point-line pairs exceed max_pairs %d", tot, h->cap);
+  for (int e = 0; e < tot; e++) RSPL_CHECK_ARG(idx[e] >= 0 && idx[e] < n_points, "point index %d outside [0, %d)", idx[e], n_points);
+  const int cnt[2] = {n_lines, n_points};
+  RSPL_HIP(hipMemcpy(h->offsets + (size_t)set * (h->cfg.max_lines + 1), offsets, sizeof(int) * (n_lines + 1),
+                     hipMemcpyHostToDevice));
+  if (tot) RSPL_HIP(hipMemcpy(h->idx + (size_t)set * h->cap, idx, sizeof(int) * tot, hipMemcpyHostToDevice));
+  RSPL_HIP(hipMemcpy(h->n_lines + set, &cnt[0], sizeof(int), hipMemcpyHostToDevice));
+  RSPL_HIP(hipMemcpy(h->n_points + set, &cnt[1], sizeof(int), hipMemcpyHostToDevice));
+  return RSPL_OK;
+}
+
+int run_match(rspl_lines* h, int problem, int set0, int set1, const int* matches, int n_matches, int n_points0,
+              int n_points1) {
+  RSPL_CHECK_ARG(n_matches >= 0 && n_matches <= h->cfg.max_matches, "n_matches %d outside [0, %d]", n_matches,
+                 h->cfg.max_matches);
+  for (int m = 0; m < n_matches; m++)
+    RSPL_CHECK_ARG(matches[2 * m] >= 0 && matches[2 * m] < n_points0 && matches[2 * m + 1] >= 0 &&
+                       matches[2 * m + 1] < n_points1,
+                   "match %d (%d, %d) outside the keypoint ranges", m, matches[2 * m], matches[2 * m + 1]);
+  const size_t Mm = std::max(1, h->cfg.max_matches);
+  if (n_matches)
+    RSPL_HIP(hipMemcpy(h->matches + problem * Mm * 2, matches, sizeof(int) * 2 * n_matches, hipMemcpyHostToDevice));
+  RSPL_HIP(hipMemcpy(h->n_matches + problem, &n_matches, sizeof(int), hipMemcpyHostToDevice));
+  lines::MatchArgs a{};
+  a.off0 = a.off1 = h->offsets; a.idx0 = a.idx1 = h->idx; a.n_lines0 = a.n_lines1 = h->n_lines;
+  a.n_points0 = a.n_points1 = h->n_points; a.set0 = set0; a.set1 = set1; a.step0 = a.step1 = 0;
+  a.matches = h->matches + problem * Mm * 2; a.n_matches = h->n_matches + problem; a.max_lines = h->cfg.max_lines;
+  a.cap = h->cap; a.max_matches = (int)Mm; a.M = h->M + (size_t)problem * h->cfg.max_lines * h->cfg.max_lines;
+  a.inv = h->inv + (size_t)problem * 2 * h->cap; a.out = h->out + (size_t)problem * h->cfg.max_lines;
+  RSPL_HIP(lines::match(a, 1, h->stream));
+  RSPL_HIP(hipStreamSynchronize(h->stream));
+  (void)n_points0;
+  (void)n_points1;
+  return RSPL_OK;
+}
+
+}  // namespace
+
+extern "C" int rspl_lines_assign(rspl_lines* h, const double* lines, int n_lines, const double* features, int n_points,
+                                 int* offsets, int* point_idx, double* dist, int capacity) {
+  RSPL_CHECK_ARG(h && offsets && (capacity == 0 || (point_idx && dist)), "rspl_lines_assign: NULL argument");
+  if (int rc = stage_image(h, 0, lines, n_lines, features, n_points)) return rc;
+  if (int rc = run_assign(h, 1)) return rc;
+  return read_assignment(h, 0, n_lines, offsets, point_idx, dist, capacity);
+}
+
+extern "C" int rspl_lines_match(rspl_lines* h, const int* offsets0, const int* idx0, int n_lines0, const int* offsets1,
+                                const int* idx1, int n_lines1, const int* matches, int n_matches, int n_points0,
+                                int n_points1, int* line_matches) {
+  RSPL_CHECK_ARG(h && offsets0 && offsets1 && (n_matches == 0 || matches) && (n_lines0 == 0 || line_matches),
+                 "rspl_lines_match: NULL argument");
+  if (int rc = stage_assignment(h, 0, offsets0, idx0, n_lines0, n_points0)) return rc;
+  if (int rc = stage_assignment(h, 1, offsets1, idx1, n_lines1, n_points1)) return rc;
+  if (int rc = run_match(h, 0, 0, 1, matches, n_matches, n_points0, n_points1)) return rc;
+  if (n_lines0) RSPL_HIP(hipMemcpy(line_matches, h->out, sizeof(int) * n_lines0, hipMemcpyDeviceToHost));
+  return RSPL_OK;
+}
+
+extern "C" int rspl_lines_stereo(rspl_lines* h, const double* lines_left, int n_left, const double* features_left,
+                                 int n_points_left, const double* lines_right, int n_right, const double* features_right,
+                                 int n_points_right, const int* stereo_matches, int n_matches, const double* camera_limits,
+                                 double* lines_right_out, uint8_t* lines_right_valid, int* n_kept_matches) {
+  RSPL_CHECK_ARG(h && camera_limits && n_kept_matches && (n_left == 0 || (lines_right_out && lines_right_valid)),
+                 "rspl_lines_stereo: NULL argument");
+  RSPL_CHECK_ARG(n_matches >= 0 && (n_matches == 0 || stereo_matches), "bad stereo matches");
+  // frame.cc:157-167: keep the stereo matches inside the disparity window
+  const double min_x = camera_limits[0], max_x = camera_limits[1], max_y = camera_limits[2];
+  std::vector<int> kept;
+  kept.reserve((size_t)2 * n_matches);
+  for (int m = 0; m < n_matches; m++) {
+    const int q = stereo_matches[2 * m], t = stereo_matches[2 * m + 1];
+    RSPL_CHECK_ARG(q >= 0 && q < n_points_left && t >= 0 && t < n_points_right, "stereo match %d out of range", m);
+    const double dx = std::fabs(features_left[(size_t)259 * q + 1] - features_right[(size_t)259 * t + 1]);
+    const double dy = std::fabs(features_left[(size_t)259 * q + 2] - features_right[(size_t)259 * t + 2]);
+    if (dx > min_x && dx < max_x && dy <= max_y) {
+      kept.push_back(q);
+      kept.push_back(t);
+    }
+  }
+  *n_kept_matches = (int)kept.size() / 2;
+  // frame.cc:128, 181: both images' assignments in one launch; :188 MatchLines
+  if (int rc = stage_image(h, 0, lines_left, n_left, features_left, n_points_left)) return rc;
+  if (int rc = stage_image(h, 1, lines_right, n_right, features_right, n_points_right)) return rc;
+  if (int rc = run_assign(h, 2)) return rc;
+  if (int rc = run_match(h, 0, 0, 1, kept.data(), (int)kept.size() / 2, n_points_left, n_points_right)) return rc;
+  std::vector<int> lm((size_t)n_left);
+  if (n_left) RSPL_HIP(hipMemcpy(lm.data(), h->out, sizeof(int) * n_left, hipMemcpyDeviceToHost));
+  // frame.cc:189-196 (a match to right line 0 counts as invalid, as in the reference)
+  for (int i = 0; i < n_left; i++) {
+    const bool ok = lm[i] > 0;
+    lines_right_valid[i] = ok ? 1 : 0;
+    for (int k = 0; k < 4; k++) lines_right_out[4 * i + k] = ok ? lines_right[4 * lm[i] + k] : 0.0;
+  }
+  return RSPL_OK;
+}

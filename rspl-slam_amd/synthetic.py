@@ -390,3 +390,80 @@ def map_sequence(n_keyframes: int = 30, n_points: int = 6000, n_lines: int = 80,
                         lines_right_valid=np.array(lv, np.uint8), points_on_lines=pol,
                         new_points=newp, new_lines=newl, point_obs=pobs, line_obs=lobs))
     return dict(camera=np.array(cam, np.float64), gt_Twc=np.array(gt), timestamps=np.array(ts), keyframes=kfs)
+
+
+def line_scene(n_lines: int = 60, n_points: int = 400, seed: int = 0, width: int = 752, height: int = 480,
+               disparity: float = 14.0, frag: int = 3, on_line_frac: float = 0.5, noise: float = 0.4):
+    """A stereo frame of the line front end: long scene segments observed as
+    FLD-like fragments (each split into `frag` pieces with small gaps, endpoint jitter, on the
+    half-size image as fld->detect returns them), keypoints half on / near the segments, half
+    anywhere, as the 259-double records' (x, y) rows, and stereo matches (left i <-> its right
+    counterpart, shifted by the disparity; a few wrong ones).  Returns a dict of
+    seg_left/seg_right [n][4] float32, feat_left/feat_right [N][259], stereo_matches [m][2],
+    lines_left/lines_right [n_lines][4] (the full-size scene segments)."""
+    rng = np.random.default_rng(seed)
+    L = []
+    for _ in range(n_lines):
+        length = rng.uniform(70, 260)
+        a = rng.uniform(-np.pi, np.pi)
+        cx, cy = rng.uniform(40, width - 40), rng.uniform(40, height - 40)
+        d = np.array([np.cos(a), np.sin(a)]) * length / 2
+        p, q = np.clip([cx, cy] - d, 2, [width - 3, height - 3]), np.clip([cx, cy] + d, 2, [width - 3, height - 3])
+        if np.hypot(*(q - p)) < 40:
+            continue
+        L.append(np.concatenate([p, q]))
+    L = np.array(L)
+
+    def fragments(lines, shift):
+        out = []
+        for ln in lines:
+            p, q = ln[:2] - [shift, 0], ln[2:] - [shift, 0]
+            cuts = np.sort(rng.uniform(0.15, 0.85, frag - 1))
+            ts = np.concatenate([[0.0], cuts, [1.0]])
+            for k in range(frag):
+                t0 = ts[k] + (0.01 if k else 0.0)
+                t1 = ts[k + 1] - (0.01 if k < frag - 1 else 0.0)
+                a_, b_ = p + (q - p) * t0, p + (q - p) * t1
+                jit = rng.normal(0, 0.3, 4)
+                seg = (np.concatenate([a_, b_]) + jit) / 2.0
+                if rng.random() < 0.5:
+                    seg = seg[[2, 3, 0, 1]]
+                out.append(seg)
+        return np.array(out, np.float32).reshape(-1, 4)
+
+    def points(lines):
+        P = []
+        n_on = int(n_points * on_line_frac)
+        for _ in range(n_on):
+            ln = lines[rng.integers(len(lines))]
+            t = rng.uniform(-0.03, 1.03)
+            off = rng.normal(0, 2.5)
+            dirv = ln[2:] - ln[:2]
+            nrm = np.array([-dirv[1], dirv[0]]) / np.hypot(*dirv)
+            P.append(ln[:2] + dirv * t + nrm * off)
+        P += list(np.column_stack([rng.uniform(8, width - 8, n_points - n_on),
+                                   rng.uniform(8, height - 8, n_points - n_on)]))
+        return np.round(np.array(P), 0)  # SuperPoint keypoints are integer pixels
+
+    xy_left = points(L)
+    xy_right = xy_left - [disparity, 0] + np.round(rng.normal(0, noise, xy_left.shape))
+    perm = rng.permutation(len(xy_right))
+    xy_right = xy_right[perm]
+    inv = np.argsort(perm)
+    m = np.column_stack([np.arange(len(xy_left)), inv])
+    keep = rng.random(len(m)) < 0.8
+    m = m[keep]
+    wrong = rng.random(len(m)) < 0.05
+    m[wrong, 1] = rng.integers(0, len(xy_right), int(wrong.sum()))
+
+    def feats(xy):
+        F = np.zeros((len(xy), 259))
+        F[:, 0] = rng.uniform(0.01, 1, len(xy))
+        F[:, 1:3] = xy
+        F[:, 3:] = rng.normal(0, 1, (len(xy), 256)) / 16
+        return F
+
+    Lr = L - [disparity, 0, disparity, 0]
+    return {"seg_left": fragments(L, 0.0), "seg_right": fragments(L, disparity),
+            "feat_left": feats(xy_left), "feat_right": feats(xy_right),
+            "stereo_matches": m.astype(np.int32), "lines_left": L, "lines_right": Lr}

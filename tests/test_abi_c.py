@@ -33,7 +33,7 @@ def _mirrors():
             "rspl_frame_result": BT.RsplFrameResult, "rspl_pnp_config": capi.PnpConfig,
             "rspl_pnp_problem": capi.PnpProblem, "rspl_pnp_result": capi.PnpResult,
             "rspl_map_config": pkg.mapping.MapConfig, "rspl_map_keyframe": pkg.mapping.MapKeyframe,
-            "rspl_map_report": pkg.mapping.MapReport}
+            "rspl_map_report": pkg.mapping.MapReport, "rspl_lines_config": pkg.lines.LinesConfig}
 
 
 def test_struct_layout_matches_ctypes():

@@ -1,0 +1,91 @@
+"""Line front end on the GPU: AssignPointsToLines and MatchLines kernels
+(csrc/line_kernels.hip) and the stereo line association (rspl_lines_stereo) against the oracle's
+restatements (oracle/lines_ref.py of src/line_processor.cc:163-283, src/frame.cc:150-203).
+Index work: relations (point sets, order) and line matches identical; distances bit-identical
+(the reference's doubles through a float).  Parity unpinned at the reference C++ (unbuildable here).
+"""
+import numpy as np
+import pytest
+
+from conftest import pkg
+import lines_ref as LR
+from rspl_slam_amd import synthetic as SY
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def lm():
+    return pkg.lines.LineMatcher(max_lines=512, max_points=2048, max_pairs=65536, max_matches=4096)
+
+
+def _rel_equal(got, ref):
+    assert len(got) == len(ref)
+    for i, (g, r) in enumerate(zip(got, ref)):
+        assert list(g) == sorted(r), f"line {i}: points"
+        assert [g[k] for k in g] == [r[k] for k in sorted(r)], f"line {i}: distances"
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2])
+def test_assign_matches_oracle(lm, seed):
+    sc = SY.line_scene(n_lines=80, n_points=500, seed=seed)
+    for side in ("left", "right"):
+        lines = LR.line_extractor(sc[f"seg_{side}"])
+        F = sc[f"feat_{side}"]
+        got = lm.AssignPointsToLines(lines, F)
+        ref = LR.assign_points_to_lines(lines, F[:, 1:3])
+        _rel_equal(got, ref)
+        assert sum(len(r) for r in ref) > 50
+
+
+@pytest.mark.parametrize("seed", [0, 3])
+def test_match_lines_matches_oracle(lm, seed):
+    sc = SY.line_scene(n_lines=80, n_points=600, seed=seed)
+    L0, L1 = LR.line_extractor(sc["seg_left"]), LR.line_extractor(sc["seg_right"])
+    F0, F1 = sc["feat_left"], sc["feat_right"]
+    r0, r1 = LR.assign_points_to_lines(L0, F0[:, 1:3]), LR.assign_points_to_lines(L1, F1[:, 1:3])
+    m = sc["stereo_matches"]
+    got = lm.MatchLines(r0, r1, m, len(F0), len(F1))
+    ref = LR.match_lines(r0, r1, m, len(F0), len(F1))
+    assert got == ref
+    assert sum(v >= 0 for v in ref) > 10  # the scene's lines do match
+
+
+def test_match_lines_edge_cases(lm):
+    r0 = [{0: 0.0, 1: 0.0, 2: 0.0}, {3: 0.0}, {}]
+    r1 = [{0: 0.0}, {1: 0.0, 2: 0.0, 5: 0.0}]
+    m = np.array([[0, 1], [1, 2], [2, 5], [3, 0]])
+    assert lm.MatchLines(r0, r1, m, 6, 6) == LR.match_lines(r0, r1, m, 6, 6)
+    assert lm.MatchLines(r0, r1, np.zeros((0, 2)), 6, 6) == [-1, -1, -1]
+    assert lm.MatchLines(r0, [], m, 6, 6) == [-1, -1, -1]          # no lines in image 1
+    assert lm.MatchLines([], r1, m, 6, 6) == []
+    # ties: two right lines with the same count -> the first column wins the row maximum
+    r1t = [{1: 0.0, 2: 0.0}, {1: 0.0, 2: 0.0}]
+    m2 = np.array([[0, 1], [1, 2]])
+    assert lm.MatchLines(r0, r1t, m2, 6, 6) == LR.match_lines(r0, r1t, m2, 6, 6)
+    with pytest.raises(pkg.capi.RsplError):
+        lm.MatchLines(r0, r1, np.array([[9, 0]]), 6, 6)           # query index out of range
+
+
+def test_assign_edge_cases(lm):
+    F = np.zeros((5, 259))
+    F[:, 1:3] = [[0, 0], [10, 3], [3, 3], [103, 0], [50, 6.0000001]]
+    lines = np.array([[0.0, 0.0, 100.0, 0.0], [5.0, 5.0, 5.0, 5.0001]])
+    _rel_equal(lm.AssignPointsToLines(lines, F), LR.assign_points_to_lines(lines, F[:, 1:3]))
+    assert lm.AssignPointsToLines(np.zeros((0, 4)), F) == []
+    assert lm.AssignPointsToLines(lines, np.zeros((0, 259))) == [{}, {}]
+
+
+def test_stereo_lines_matches_oracle(lm):
+    sc = SY.line_scene(n_lines=80, n_points=600, seed=4)
+    L0, L1 = LR.line_extractor(sc["seg_left"]), LR.line_extractor(sc["seg_right"])
+    F0, F1, m = sc["feat_left"], sc["feat_right"], sc["stereo_matches"]
+    lim = (2.0, 60.0, 2.0)  # MinXDiff, MaxXDiff, MaxYDiff
+    lr, valid, kept = lm.StereoLines(L0, F0, L1, F1, m, lim)
+    km = LR.stereo_filter(F0[:, 1], F1[:, 1], F0[:, 2], F1[:, 2], m, *lim)
+    r0, r1 = LR.assign_points_to_lines(L0, F0[:, 1:3]), LR.assign_points_to_lines(L1, F1[:, 1:3])
+    ref_lr, ref_valid = LR.right_lines(L1, LR.match_lines(r0, r1, km, len(F0), len(F1)), len(L0))
+    assert kept == len(km)
+    np.testing.assert_array_equal(valid, ref_valid)
+    np.testing.assert_array_equal(lr, ref_lr)
+    assert valid.sum() > 10

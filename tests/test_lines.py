@@ -1,0 +1,94 @@
+"""Line front end after the detector, CPU part.
+
+librspl's LineDetector post-processing (rspl_line_extract, host C++: csrc/lines.cpp) against the
+oracle's restatement (oracle/lines_ref.py) of LineDetector::LineExtractor / MergeLines /
+MergeTwoLines / FilterShortLines (src/line_processor.cc:11-161, 460-665): bit-exact lines on
+synthetic FLD-like fragment sets.  The oracle's assignment / matching restatements are checked on
+hand-made cases here; the GPU kernels against them in tests/test_gpu_lines.py.
+Parity unpinned at the reference C++ (needs OpenCV contrib + Eigen: unbuildable here; its tests
+hold no line vectors).
+"""
+import math
+
+import numpy as np
+import pytest
+
+from conftest import pkg
+import lines_ref as LR
+from rspl_slam_amd import synthetic as SY
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 3])
+def test_line_extract_matches_oracle(seed):
+    sc = SY.line_scene(n_lines=70, seed=seed)
+    for segs in (sc["seg_left"], sc["seg_right"]):
+        got = pkg.lines.LineExtractor(segs)
+        ref = LR.line_extractor(segs)
+        assert got.shape == ref.shape and len(got) > 10
+        np.testing.assert_array_equal(got, ref)
+        # the merge joins fragments: fewer lines than fragments, all longer than 60 px
+        assert len(got) < len(segs)
+        assert (np.hypot(got[:, 2] - got[:, 0], got[:, 3] - got[:, 1]) > 60).all()
+
+
+def test_line_extract_without_merge_and_empty():
+    segs = np.array([[10, 10, 50, 12], [100, 100, 100, 160]], np.float32)
+    got = pkg.lines.LineExtractor(segs, do_merge=False)
+    np.testing.assert_array_equal(got, segs.astype(np.float64) * 2)
+    assert pkg.lines.LineExtractor(np.zeros((0, 4), np.float32)).shape == (0, 4)
+
+
+def test_line_extract_edge_cases():
+    # vertical (dx == 0), horizontal, near +-pi/2 pairs that wrap the angle difference, and
+    # collinear fragments with gaps below / above the endpoint thresholds
+    segs = np.array([[100, 20, 100, 80], [100.5, 82, 100.3, 150],          # vertical, merges
+                     [20, 200, 90, 200], [96, 200.4, 160, 200.2],           # horizontal, 6 px gap (< 15)
+                     [300, 200, 360, 200], [400, 200, 460, 200],            # 40 px gap: kept apart in pass 1
+                     [200, 10, 200.8, 70], [201.1, 72, 200.2, 140],        # angles near +pi/2 and -pi/2
+                     [50, 300, 52, 300]], np.float32)                        # too short: filtered
+    got = pkg.lines.LineExtractor(segs)
+    ref = LR.line_extractor(segs)
+    np.testing.assert_array_equal(got, ref)
+    # with capacity too small the call reports the count
+    lib = pkg.lines._declare(pkg.capi.load())
+    import ctypes as C
+    n = C.c_int()
+    rc = lib.rspl_line_extract(segs.ctypes.data_as(C.POINTER(C.c_float)), len(segs), 1, None, 0, C.byref(n))
+    assert rc == -4 and n.value == len(ref)
+
+
+def test_merge_two_lines_known_answer():
+    # two collinear horizontal pieces merge into their hull
+    m = LR.merge_two_lines(np.array([0, 0, 10, 0], np.float32), np.array([12, 0, 30, 0], np.float32))
+    np.testing.assert_allclose(m, [0, 0, 30, 0], atol=1e-5)
+
+
+def test_oracle_assignment_and_matching_known_answers():
+    lines = np.array([[0.0, 0.0, 100.0, 0.0], [50.0, -50.0, 50.0, 50.0]])
+    xy = np.array([[10, 1], [50, 0], [120, 0], [101, 2], [50, 40], [70, 10], [-2.5, 0.5]], np.float64)
+    rel = LR.assign_points_to_lines(lines, xy)
+    # point 2 is beyond the box (x > 103); point 3 is within 3 px of the endpoint; point 6 too
+    assert sorted(rel[0]) == [0, 1, 3, 6]
+    assert sorted(rel[1]) == [1, 4]
+    assert rel[0][0] == pytest.approx(1.0) and rel[1][4] == 0.0
+    # matching: line 0 of image 0 shares 3 matched points with line 1 of image 1
+    rel1 = [{5: 0.0}, {0: 0.0, 1: 0.0, 3: 0.0}]
+    m = np.array([[0, 0], [1, 1], [3, 3], [4, 5]])
+    out = LR.match_lines(rel, rel1, m, len(xy), 6)
+    # v = 3 shared points, score 9 / min(4, 3) = 3 >= 0.8; line 1 (points 1, 4) shares 1: unmatched
+    assert out == [1, -1]
+    assert LR.match_lines(rel, rel1, m, 0, 6) == [-1, -1]
+
+
+def test_oracle_stereo_quirk():
+    # frame.cc:190 tests line_matches[i] > 0: a match to right line 0 is invalid
+    lr, valid = LR.right_lines(np.arange(8.0).reshape(2, 4), [0, 1, -1], 3)
+    assert valid.tolist() == [False, True, False]
+    np.testing.assert_array_equal(lr[1], [4, 5, 6, 7])
+
+
+def test_line_scene_is_reproducible():
+    a, b = SY.line_scene(seed=5), SY.line_scene(seed=5)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+    assert a["feat_left"].shape[1] == 259 and math.isfinite(a["seg_left"].sum())
