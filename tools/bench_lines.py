@@ -1,0 +1,59 @@
+"""Line front end timing: one stereo frame's line association -- both images'
+AssignPointsToLines (one launch) + the stereo filter + MatchLines (rspl_lines_stereo, host
+arrays in / out, the reference's per-frame contract) -- on the GPU, the LineDetector merge passes
+(host C++), and the oracle restatement of the same work on one CPU core for comparison."""
+import argparse
+import json
+import pathlib
+import sys
+import time
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+import rspl_loader  # noqa: E402
+
+pkg = rspl_loader.load()
+pkg.capi.load()
+import lines_ref as LR  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--lines", type=int, default=80)
+    ap.add_argument("--points", type=int, default=400)
+    ap.add_argument("--iters", type=int, default=200)
+    a = ap.parse_args()
+    sc = pkg.synthetic.line_scene(n_lines=a.lines, n_points=a.points, seed=11)
+    lm = pkg.lines.LineMatcher(max_lines=512, max_points=2048)
+    lim = (2.0, 60.0, 2.0)
+    t = time.perf_counter()
+    for _ in range(a.iters):
+        L0 = pkg.lines.LineExtractor(sc["seg_left"])
+        L1 = pkg.lines.LineExtractor(sc["seg_right"])
+    merge_ms = (time.perf_counter() - t) / a.iters * 1e3 / 2
+    args = (L0, sc["feat_left"], L1, sc["feat_right"], sc["stereo_matches"], lim)
+    for _ in range(10):
+        lm.StereoLines(*args)
+    t = time.perf_counter()
+    for _ in range(a.iters):
+        lr, valid, kept = lm.StereoLines(*args)
+    gpu_ms = (time.perf_counter() - t) / a.iters * 1e3
+    t = time.perf_counter()
+    n_cpu = max(3, a.iters // 50)
+    F0, F1, m = sc["feat_left"], sc["feat_right"], sc["stereo_matches"]
+    for _ in range(n_cpu):
+        km = LR.stereo_filter(F0[:, 1], F1[:, 1], F0[:, 2], F1[:, 2], m, *lim)
+        r0 = LR.assign_points_to_lines(L0, F0[:, 1:3])
+        r1 = LR.assign_points_to_lines(L1, F1[:, 1:3])
+        LR.right_lines(L1, LR.match_lines(r0, r1, km, len(F0), len(F1)), len(L0))
+    cpu_ms = (time.perf_counter() - t) / n_cpu * 1e3
+    print(json.dumps({"lines_left": len(L0), "lines_right": len(L1), "points": a.points,
+                      "stereo_matches_kept": kept, "right_lines_valid": int(valid.sum()),
+                      "merge_ms_per_image_host": round(merge_ms, 4),
+                      "stereo_association_ms_gpu_call": round(gpu_ms, 4),
+                      "stereo_association_ms_oracle_python_1core": round(cpu_ms, 3)}))
+
+
+if __name__ == "__main__":
+    main()

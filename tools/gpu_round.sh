@@ -12,6 +12,10 @@ tail -1 gpurun_out/gpu_tests.log
 timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; cat gpurun_out/smoke.log; exit 1; }
 cat gpurun_out/smoke.log
 fi
+timeout -k 10 120 python -u tools/bench_lines.py > gpurun_out/r02_bench_lines.json || { echo "line bench failed"; exit 1; }
+cat gpurun_out/r02_bench_lines.json
+{ timeout -k 10 60 python -u tools/bench_ba.py --iters 50 && timeout -k 10 60 python -u tools/bench_ba.py --iters 10 --poses 30 --points 10000 --lines 0; } > gpurun_out/r02_bench_ba.txt || { echo "ba bench failed"; exit 1; }
+cat gpurun_out/r02_bench_ba.txt
 cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --single-precision --steps 10 --warmup 2 > /dev/null 2>&1 || { echo "pmc fetch failed"; exit 1; }
 timeout -s KILL 120 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run --output-format csv -- python3 $R/bench.py --no-cpu-baseline --single-precision --steps 10 --warmup 2 > /dev/null 2>&1 || { echo "pmc write failed"; exit 1; }
