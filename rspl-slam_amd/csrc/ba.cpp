@@ -258,14 +258,14 @@ void report_prof(rspl_ba* b) {
   fprintf(stderr,
           "ba_prof us: pcstarts %.1f pcloop %.1f pcticket %.1f pcend %.1f gap %.1f asm %.1f factor %.1f back %.1f"
           " poses %.1f gap %.1f uestarts %.1f upd %.1f pointlin %.1f groupsend %.1f lineswait %.1f linescomp %.1f"
-          " linesend %.1f\n",
+          " linesend %.1f sApanel %.1f sAtrail %.1f sBpanel %.1f sBtrail %.1f\n",
           us(p0, last(ba::kProfPc, 0, npc, 0)), us(p0, last(ba::kProfPc, 0, npc, 1)),
           us(p0, last(ba::kProfPc, 0, npc, 2)), us(p0, last(ba::kProfPc, 0, npc, 3)),
           us(last(ba::kProfPc, 0, npc, 3), h[0]), us(h[0], h[1]), us(h[1], h[2]), us(h[2], h[3]), us(h[3], h[4]),
           us(h[4], u0), us(u0, last(ba::kProfUe, 0, nue, 0)), us(u0, last(ba::kProfUe, 0, nbu, 1)),
           us(u0, last(ba::kProfUe, 0, nbu, 2)), us(u0, last(ba::kProfUe, 0, nbu, 3)),
           us(u0, last(ba::kProfUe, nbu, nue, 1)), us(u0, last(ba::kProfUe, nbu, nue, 2)),
-          us(u0, last(ba::kProfUe, nbu, nue, 3)));
+          us(u0, last(ba::kProfUe, nbu, nue, 3)), us(h[1], h[5]), us(h[5], h[6]), us(h[6], h[7]), us(h[7], h[8]));
   b->prof_nb[0] = 0;
   (void)hipMemset(b->prof, 0, sizeof(unsigned long long) * ba::kProfLen);
 }

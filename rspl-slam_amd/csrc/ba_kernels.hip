@@ -1314,6 +1314,7 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
       }
     }
     __syncthreads();
+    if (tid == 0 && s < 2) prof_stamp(S, 5 + 2 * s);  // step s: pivot block + panel done
     if (bad) {  // LDS flag after the barrier: uniform
       if (tid == 0) atomicOr(S.fail, 1);
       return;
@@ -1332,6 +1333,7 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
       }
     }
     __syncthreads();
+    if (tid == 0 && s < 2) prof_stamp(S, 6 + 2 * s);  // step s: trailing update done
   }
   if (wv != 0) return;
   if (tid == 0) prof_stamp(S, 2);
