@@ -231,6 +231,33 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; r++) acc[m][n][r] = 0.f;
 
+  // software pipeline over the input-channel stages: the next stage's weights (and halo, unless
+  // conv1a computes it) are fetched into registers while the current stage's MFMAs run, and
+  // written to LDS after the next barrier
+  constexpr int HALO8 = HY * HX * (HCK / 8), HPT = (HALO8 + 255) / 256;
+  half8 pw[9], ph[FUSE1A ? 1 : HPT];
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int r = 0; r < 9; r++) {  // weights [9][64 co][32 ci]: 2304 half8, 9 per thread
+      const int i = tid + 256 * r, q = i % (HCK / 8), rr = i / (HCK / 8);
+      const int kk = rr / 64, co = rr % 64;
+      pw[r] = *reinterpret_cast<const half8*>(a.hw + ((size_t)kk * COUT + co0 + co) * CIN + c0 + 8 * q);
+    }
+    if constexpr (!FUSE1A) {
+      const _Float16* in = a.hin + (size_t)bi * H * W * CIN;
+#pragma unroll
+      for (int r = 0; r < HPT; r++) {
+        const int i = tid + 256 * r, q = i % (HCK / 8), pix = i / (HCK / 8);
+        const int hy = pix / HX, hx = pix % HX;
+        const int y = y0 - 1 + hy, x = x0 - 1 + hx;
+        half8 v = {};
+        if (i < HALO8 && y >= 0 && y < H && x >= 0 && x < W)
+          v = *reinterpret_cast<const half8*>(in + ((size_t)y * W + x) * CIN + c0 + 8 * q);
+        ph[r] = v;
+      }
+    }
+  };
+  fetch(0);
   for (int c0 = 0; c0 < CIN; c0 += HCK) {
     __syncthreads();
     if constexpr (FUSE1A) {
@@ -272,24 +299,19 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
         }
       }
     } else {
-      const _Float16* in = a.hin + (size_t)bi * H * W * CIN;
-      for (int i = tid; i < HY * HX * (HCK / 8); i += 256) {
-        const int q = i % (HCK / 8), pix = i / (HCK / 8);
-        const int hy = pix / HX, hx = pix % HX;
-        const int y = y0 - 1 + hy, x = x0 - 1 + hx;
-        half8 v = {};
-        if (y >= 0 && y < H && x >= 0 && x < W)
-          v = *reinterpret_cast<const half8*>(in + ((size_t)y * W + x) * CIN + c0 + 8 * q);
-        *reinterpret_cast<half8*>(&halo[pix * HCS + 8 * q]) = v;
+#pragma unroll
+      for (int r = 0; r < HPT; r++) {
+        const int i = tid + 256 * r;
+        if (i < HALO8) *reinterpret_cast<half8*>(&halo[(i / (HCK / 8)) * HCS + 8 * (i % (HCK / 8))]) = ph[r];
       }
     }
-    for (int i = tid; i < 9 * 64 * (HCK / 8); i += 256) {  // weights [9][64 co][32 ci]
-      const int q = i % (HCK / 8), r = i / (HCK / 8);     // r = kk*64 + co
-      const int kk = r / 64, co = r % 64;
-      *reinterpret_cast<half8*>(&wts[r * HCS + 8 * q]) =
-          *reinterpret_cast<const half8*>(a.hw + ((size_t)kk * COUT + co0 + co) * CIN + c0 + 8 * q);
+#pragma unroll
+    for (int r = 0; r < 9; r++) {
+      const int i = tid + 256 * r;
+      *reinterpret_cast<half8*>(&wts[(i / (HCK / 8)) * HCS + 8 * (i % (HCK / 8))]) = pw[r];
     }
     __syncthreads();
+    if (c0 + HCK < CIN) fetch(c0 + HCK);
 #pragma unroll
     for (int kk = 0; kk < 9; kk++) {
       const int ky = kk / 3, kx = kk % 3;
