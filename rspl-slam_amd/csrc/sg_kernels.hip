@@ -645,8 +645,16 @@ constexpr int kLdA = 520;  // halves per LDS activation row (512 + 8: 16-byte al
 
 // acc[t] += A[32 x K] (LDS rows) * W[n0 + 32 t + r][k]^T, t < NT; W in B-fragment order
 // (to_frag): the operand of (n-tile, k-step) is one contiguous 1 KB read per wave
+// one output tile per wave: odd k-steps go to a second accumulator set (two independent MFMA
+// dependency chains per tile instead of one), summed at the end
 template <int NT>
 __device__ __forceinline__ void wave_mm(const _Float16* Al, const _Float16* Wf, int n0, int K, floatx16 (&acc)[NT]) {
+  constexpr bool SPLIT = NT < 2;
+  floatx16 acc2[NT];
+#pragma unroll
+  for (int t = 0; t < NT; t++)
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc2[t][i] = 0.f;
   const int lane = threadIdx.x & 63, r = lane & 31, h = lane >> 5, KS = K / 16;
   const _Float16* ap = Al + r * kLdA + 8 * h;
   const _Float16* bp[NT];
@@ -671,7 +679,10 @@ __device__ __forceinline__ void wave_mm(const _Float16* Al, const _Float16* Wf, 
     for (int u = 0; u < U; u++) {
       const half8 a = *reinterpret_cast<const half8*>(ap + k0 + 16 * u);
 #pragma unroll
-      for (int t = 0; t < NT; t++) acc[t] = mfma16(a, bcur[u][t], acc[t]);
+      for (int t = 0; t < NT; t++) {
+        if (SPLIT && (u & 1)) acc2[t] = mfma16(a, bcur[u][t], acc2[t]);
+        else acc[t] = mfma16(a, bcur[u][t], acc[t]);
+      }
     }
     if (more) {
 #pragma unroll
@@ -680,6 +691,9 @@ __device__ __forceinline__ void wave_mm(const _Float16* Al, const _Float16* Wf, 
         for (int t = 0; t < NT; t++) bcur[u][t] = bnxt[u][t];
     }
   }
+  if (SPLIT)
+#pragma unroll
+    for (int t = 0; t < NT; t++) acc[t] += acc2[t];
 }
 
 __global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
