@@ -586,7 +586,33 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
   delete b;
 }
 
+namespace {
+int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res);
+}
+
+// A device-side failure can return while the call's kernel chain is still queued or running (a
+// mailbox timeout, a failed all-reduce): drain the stream before anything of the handle is reused
+// (the next call restages the mapped buffers the old chain reads) and re-arm the cross-call
+// tickets and release flags the chain may have left half-counted.  If the drain itself fails the
+// device is gone and the handle must be recreated (the error says so).
 extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
+  const int rc = ba_local_impl(b, pr, res);
+  if (rc != RSPL_E_DEVICE || !b) return rc;
+  const std::string msg = rspl_last_error();
+  if (hipStreamSynchronize(b->stream) != hipSuccess ||
+      hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
+      hipMemset(b->lflag, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
+      hipMemset(b->pair_ctr, 0, sizeof(unsigned) * std::max(b->maxK * (b->maxK + 1) / 2, 1)) != hipSuccess) {
+    set_error("%s; the BA stream could not be drained: recreate the handle", msg.c_str());
+    return rc;
+  }
+  b->tag = 0;
+  set_error("%s", msg.c_str());
+  return rc;
+}
+
+namespace {
+int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   RSPL_CHECK_ARG(b && pr && res, "rspl_ba_local: NULL argument");
   const int np = pr->n_poses, nq = pr->n_points, nl = pr->n_lines;
   const int ne[4] = {pr->n_mono, pr->n_stereo, pr->n_mono_line, pr->n_stereo_line};
@@ -924,3 +950,4 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   }
   return RSPL_OK;
 }
+}  // namespace

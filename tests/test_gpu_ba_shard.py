@@ -159,3 +159,26 @@ def test_two_process_shard_host_allreduce():
     assert np.abs(a[8] - ref.lines).max() < 5e-3
     for k in a[9]:
         np.testing.assert_array_equal(a[9][k], ref.inlier[k], err_msg=k)
+
+
+def test_failed_call_leaves_the_handle_usable():
+    """a device-side failure returns while the chain may still run.  rspl_ba_local drains
+    the stream and re-arms the tickets / release flags, so the next call on the same handle is
+    correct: a shard all-reduce that fails mid-optimisation, then a good call vs the oracle."""
+    pkg = _pkg()
+    prob, _ = SY.ba_problem(n_poses=8, n_points=600, n_lines=12, seed=17, pixel_sigma=0.8, outlier_frac=0.05)
+    ref = oracle.ba_local(prob)
+    ba = pkg.LocalBA(max_poses=16, max_points=1000, max_lines=40, max_edges=20000)
+    calls = [0]
+
+    def flaky(x):
+        calls[0] += 1
+        if calls[0] == 5:
+            raise RuntimeError("injected all-reduce failure")
+
+    ba.set_shard(0, 1, flaky)
+    with pytest.raises(pkg.capi.RsplError, match="all-reduce failed"):
+        ba.run(prob)
+    ba.set_shard(0, 1, lambda x: None)
+    for _ in range(2):
+        _compare(ba.run(prob), ref)
