@@ -702,14 +702,26 @@ __global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
   _Float16* Hb = lds_l + 32 * kLdA;   // [32][kLdA]: HID; before that the attention merge buffer
   float* Om = reinterpret_cast<float*>(Hb);  // [4 heads][64 d][32 q]
   __shared__ float Ml[4][32], Ll[4][32];
-  const int set = blockIdx.y, p = set >> 1, img = set & 1;
+  // XCD-aware placement: the tiles of one token set go to the same XCD(s) (block b runs on XCD
+  // b % 8), so each XCD's L2 holds the k / v of one set instead of all of them
+  int bx, set;
+  if (a.xps > 0) {
+    const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+    set = xcd / a.xps;
+    bx = (xcd % a.xps) * a.tpx + slot;
+    if (set >= a.nsets || slot >= a.tpx || bx >= (a.nmax + 31) / 32) return;  // whole workgroup
+  } else {
+    bx = blockIdx.x;
+    set = blockIdx.y;
+  }
+  const int p = set >> 1, img = set & 1;
   const int simg = a.cross ? 1 - img : img;
   const int nk = simg ? a.n1[p] : a.n0[p];
-  const int q0 = blockIdx.x * 32;
+  const int q0 = bx * 32;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, c = lane & 31, kh = lane >> 5;
   const size_t tok0 = (size_t)set * a.nmax + q0;   // first token of the tile
   const int kset = p * 2 + simg;
-  if (a.probe && !a.last && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) a.probe[0] += wall_clock64();
+  if (a.probe && !a.last && tid == 0 && bx == 0 && set == 0) a.probe[0] += wall_clock64();
   // x tile -> LDS (rows past the set clamp to its last token; never stored back)
   for (int e = tid; e < 32 * 32; e += 512) {
     const int row = e >> 5, ch = e & 31;
@@ -845,7 +857,7 @@ __global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
     }
     __syncthreads();
   }
-  if (a.probe && !a.last && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) a.probe[1] += wall_clock64();
+  if (a.probe && !a.last && tid == 0 && bx == 0 && set == 0) a.probe[1] += wall_clock64();
   const int r = lane & 31, hh = lane >> 5;
   if (!a.qkv_only) {
   // ---- (2) HID = ReLU([x | message] W1^T + b1): wave wv -> columns 64 wv .. 64 wv + 63 ----
@@ -869,7 +881,7 @@ __global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
     }
   }
   __syncthreads();
-  if (a.probe && !a.last && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) a.probe[2] += wall_clock64();
+  if (a.probe && !a.last && tid == 0 && bx == 0 && set == 0) a.probe[2] += wall_clock64();
   // ---- (3) x += HID W2^T + b2 (fp32 stream, fp16 shadow, new x into Ab): columns 32 wv .. +31 ----
   {
     floatx16 acc[1];
@@ -892,7 +904,7 @@ __global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
   if (a.last) return;
   __syncthreads();
   }
-  if (a.probe && !a.last && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) a.probe[3] += wall_clock64();
+  if (a.probe && !a.last && tid == 0 && bx == 0 && set == 0) a.probe[3] += wall_clock64();
   // ---- (4) next layer's q | k | v of these tokens: columns 96 wv .. 96 wv + 95 ----
   {
     floatx16 acc[3];
@@ -936,7 +948,7 @@ __global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
       }
     }
   }
-  if (a.probe && !a.last && tid == 0 && blockIdx.x == 0 && blockIdx.y == 0) {
+  if (a.probe && !a.last && tid == 0 && bx == 0 && set == 0) {
     a.probe[4] += wall_clock64();
     a.probe[5] += 1;
   }
@@ -1589,7 +1601,16 @@ hipError_t gnn_layer(const LayerArgs& a, int B, hipStream_t s) {
     if (e != hipSuccess) return e;
     attr = true;
   }
-  hipLaunchKernelGGL(layer_kernel, dim3((a.nmax + 31) / 32, B * 2), dim3(512), lds, s, a);
+  LayerArgs la = a;
+  const int sets = B * 2, tiles = (a.nmax + 31) / 32;
+  la.nsets = sets;
+  static const bool noxcd = getenv("RSPL_SG_NOXCD") != nullptr;  // A/B knob: the plain (tile, set) grid
+  la.xps = sets <= 8 && !noxcd ? 8 / sets : 0;                      // XCDs per token set
+  la.tpx = la.xps ? (tiles + la.xps - 1) / la.xps : 0;            // tiles per XCD
+  if (la.xps)
+    hipLaunchKernelGGL(layer_kernel, dim3(8 * la.tpx), dim3(512), lds, s, la);
+  else
+    hipLaunchKernelGGL(layer_kernel, dim3(tiles, sets), dim3(512), lds, s, la);
   return hipGetLastError();
 }
 

@@ -91,6 +91,7 @@ struct LayerArgs {
   int cross, last;
   int qkv_only;          // prologue: only phase (4) from the current x (layer 0's q / k / v)
   unsigned long long* probe;  // debug (RSPL_SG_LPROBE): phase wall clocks of workgroup (0, 0)
+  int nsets, xps, tpx;   // set by gnn_layer: token sets, XCDs per set (0 = plain grid), tiles per XCD
 };
 
 struct PrepArgs {

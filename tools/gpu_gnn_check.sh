@@ -8,3 +8,6 @@ grep -E "agree|passed|failed" gpurun_out/sg_tests.log | tail -5
 RSPL_SG_LPROBE=1 timeout -k 10 120 python -u tools/bench_sg.py --iters 20 2>&1 | tail -2 || exit 1
 timeout -k 10 300 python -u bench.py --single-precision --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
 python3 -c "import json; d=json.load(open('gpurun_out/bench.json')); print(d['value'], d['ms_per_step'], d['stages_ms_per_step'])"
+RSPL_SG_NOXCD=1 RSPL_SG_LPROBE=1 timeout -k 10 120 python -u tools/bench_sg.py --iters 20 2>&1 | tail -2 | sed 's/^/noxcd: /' || exit 1
+RSPL_SG_NOXCD=1 timeout -k 10 300 python -u bench.py --single-precision --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
+python3 -c "import json; d=json.load(open('gpurun_out/bench.json')); print('noxcd', d['value'], d['ms_per_step'], d['stages_ms_per_step']['sg:gnn x18'], d['stages_ms_per_step']['ba:wall'])"
