@@ -14,12 +14,14 @@
 // allocation order; here ties are ordered by frame id (the same order when keyframes are allocated
 // in id order, which is how MapBuilder creates them).
 #include <algorithm>
+#include <chrono>
 #include <array>
 #include <cfloat>
 #include <cmath>
 #include <cstring>
 #include <map>
 #include <set>
+#include <unordered_map>
 #include <vector>
 
 #include "common.hpp"
@@ -91,6 +93,7 @@ struct MPoint {  // Mappoint
   int type = kUnTriangulated;
   std::map<int, int> obs;  // _obversers: frame id -> keypoint index
   int lmo = -1;
+  int dense = -1;          // index in the last assembled problem
   int observers() const {  // ObverserNum
     int n = 0;
     for (auto& kv : obs) n += kv.second >= 0;
@@ -109,6 +112,7 @@ struct MLine {  // Mapline
   std::map<int, int> obs;   // frame id -> line index
   std::map<int, int> incl;  // _included_endpoints
   int lmo = -1;
+  int dense = -1;            // index in the last assembled problem
   double ep[6] = {};
   bool ep_valid = false, to_update = false;
   int observers() const {
@@ -192,10 +196,11 @@ void line_to_cartesian(const double* L, double* c) {
 struct rspl_map {
   double cam[5] = {};
   rspl_map_config cfg{};
-  std::map<int, MFrame> kf;     // _keyframes
+  std::unordered_map<int, MFrame> kf;  // _keyframes (by id; id order where the reference iterates it)
   std::vector<int> kf_ids;      // _keyframe_ids (insertion order)
-  std::map<int, MPoint> mp;     // _mappoints
-  std::map<int, MLine> ml;      // _maplines
+  // _mappoints / _maplines: looked up by id only, never iterated (node-based: element pointers stay valid)
+  std::unordered_map<int, MPoint> mp;
+  std::unordered_map<int, MLine> ml;
   // the last assembled problem (rspl_map_last_problem)
   std::vector<int> pose_ids, point_ids, line_ids;
   std::vector<uint8_t> pose_fixed;
@@ -255,11 +260,10 @@ struct rspl_map {
     constexpr size_t target = 9;
     const int fid = f.id;
     nb.clear();
-    if (kf.size() <= target) {
-      for (auto& kv : kf) {
-        kv.second.lmo = fid;
-        nb.push_back(&kv.second);
-      }
+    if (kf.size() <= target) {  // every keyframe, in id order (the reference's std::map)
+      for (auto& kv : kf) nb.push_back(&kv.second);
+      std::sort(nb.begin(), nb.end(), [](const MFrame* a, const MFrame* b) { return a->id < b->id; });
+      for (MFrame* k : nb) k->lmo = fid;
       return;
     }
     nb.push_back(&f);
@@ -435,7 +439,16 @@ struct rspl_map {
       set_error("rspl_map_local_optimization: frame %d is not a keyframe", fid);
       return RSPL_E_ARG;
     }
+    static const bool timing = getenv("RSPL_MAP_TIMING") != nullptr;
+    using clk = std::chrono::steady_clock;
+    clk::time_point tm[6];
+    int ntm = 0;
+    auto mark = [&]() {
+      if (timing) tm[ntm++] = clk::now();
+    };
+    mark();
     update_connection(*nf);
+    mark();
     std::map<int, PoseV> poses;
     std::vector<MFrame*> nb;
     search_neighbors(*nf, nb);
@@ -476,15 +489,18 @@ struct rspl_map {
         add_vertex(poses, *o, true);
       }
     }
+    mark();
     auto in_window = [&](const MFrame* o) { return o && (o->lmo == fid || o->lmo_fix == fid); };
     // constraints in the reference's order: landmark by landmark, observers by frame id
     std::vector<Con> cons[4];  // mono, stereo, mono line, stereo line
-    std::map<int, std::array<double, 3>> points;
-    std::map<int, std::array<double, 6>> lines;
+    std::vector<MPoint*> points;  // kept landmarks (dense order = ascending id, set below)
+    std::vector<MLine*> lines;
+    std::vector<Con> mono, stereo;
     for (int pid : mpts) {
       MPoint* m = point(pid);
       if (!m || m->type != kGood) continue;
-      std::vector<Con> mono, stereo;
+      mono.clear();
+      stereo.clear();
       for (auto& kv : m->obs) {
         MFrame* o = frame(kv.first);
         if (!in_window(o)) continue;
@@ -494,7 +510,7 @@ struct rspl_map {
         else mono.push_back({kv.first, pid, {k[0], k[1]}});
       }
       if (!stereo.empty() || mono.size() > 1) {
-        points[pid] = {m->p[0], m->p[1], m->p[2]};
+        points.push_back(m);
         cons[0].insert(cons[0].end(), mono.begin(), mono.end());
         cons[1].insert(cons[1].end(), stereo.begin(), stereo.end());
       }
@@ -502,7 +518,8 @@ struct rspl_map {
     for (int lid : mpls) {
       MLine* l = line(lid);
       if (!l || l->type != kGood) continue;
-      std::vector<Con> mono, stereo;
+      mono.clear();
+      stereo.clear();
       for (auto& kv : l->obs) {
         MFrame* o = frame(kv.first);
         if (!in_window(o)) continue;
@@ -517,16 +534,15 @@ struct rspl_map {
         }
       }
       if (!stereo.empty() || mono.size() > 1) {
-        std::array<double, 6> L;
-        for (int i = 0; i < 6; i++) L[i] = l->L[i];
-        lines[lid] = L;
+        lines.push_back(l);
         cons[2].insert(cons[2].end(), mono.begin(), mono.end());
         cons[3].insert(cons[3].end(), stereo.begin(), stereo.end());
       }
     }
+    mark();
     // dense problem: std::map ids in ascending order (LocalmapOptimization's vertex order)
     pose_ids.clear(); point_ids.clear(); line_ids.clear(); pose_fixed.clear();
-    std::map<int, int> pidx, qidx, lidx;
+    std::map<int, int> pidx;
     std::vector<double> pq, pp, X, Ls;
     for (auto& kv : poses) {
       pidx[kv.first] = (int)pose_ids.size();
@@ -535,22 +551,26 @@ struct rspl_map {
       pq.insert(pq.end(), kv.second.q, kv.second.q + 4);
       pp.insert(pp.end(), kv.second.p, kv.second.p + 3);
     }
-    for (auto& kv : points) {
-      qidx[kv.first] = (int)point_ids.size();
-      point_ids.push_back(kv.first);
-      X.insert(X.end(), kv.second.begin(), kv.second.end());
+    std::sort(points.begin(), points.end(), [](const MPoint* a, const MPoint* b) { return a->id < b->id; });
+    std::sort(lines.begin(), lines.end(), [](const MLine* a, const MLine* b) { return a->id < b->id; });
+    X.reserve(3 * points.size());
+    Ls.reserve(6 * lines.size());
+    for (MPoint* m : points) {
+      m->dense = (int)point_ids.size();
+      point_ids.push_back(m->id);
+      X.insert(X.end(), m->p, m->p + 3);
     }
-    for (auto& kv : lines) {
-      lidx[kv.first] = (int)line_ids.size();
-      line_ids.push_back(kv.first);
-      Ls.insert(Ls.end(), kv.second.begin(), kv.second.end());
+    for (MLine* l : lines) {
+      l->dense = (int)line_ids.size();
+      line_ids.push_back(l->id);
+      Ls.insert(Ls.end(), l->L, l->L + 6);
     }
     static const int od[4] = {2, 3, 4, 8};
     for (int t = 0; t < 4; t++) {
       c_pose[t].clear(); c_lm[t].clear(); c_obs[t].clear();
       for (auto& c : cons[t]) {
         c_pose[t].push_back(pidx.at(c.pose));
-        c_lm[t].push_back(t < 2 ? qidx.at(c.lm) : lidx.at(c.lm));
+        c_lm[t].push_back(t < 2 ? point(c.lm)->dense : line(c.lm)->dense);
         c_obs[t].insert(c_obs[t].end(), c.obs, c.obs + od[t]);
       }
       c_inl[t].assign(cons[t].size(), 1);
@@ -565,6 +585,12 @@ struct rspl_map {
       rep->n_stereo = (int)cons[1].size();
       rep->n_mono_line = (int)cons[2].size();
       rep->n_stereo_line = (int)cons[3].size();
+    }
+    mark();
+    if (timing && ntm == 5) {
+      auto us = [&](int i) { return std::chrono::duration<double, std::micro>(tm[i + 1] - tm[i]).count(); };
+      fprintf(stderr, "rspl_map assembly us: connections %.0f window %.0f constraints %.0f dense %.0f\n", us(0), us(1),
+              us(2), us(3));
     }
     last_fid = fid;
     last_cons_ok = true;
