@@ -682,115 +682,124 @@ __global__ __launch_bounds__(256) void sample_taps_h_kernel(TapArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Fused simple_nms (5 x 9x9 max-pools) + threshold / border candidate
-// extraction.  Tile 32x32 outputs, halo 20, separable LDS max.  Scores are
-// softmax outputs (>= 0) and every window contains its centre, so zero padding
-// outside the image equals MaxPool2d's -inf padding here.
+// Fused simple_nms (5 x 9x9 max-pools) + threshold / border candidate extraction.  Scores are
+// softmax outputs (>= 0) and every window contains its centre, so zero padding outside the image
+// equals MaxPool2d's -inf padding here.  Tile 64 x 32 outputs with the 20-pixel halo the five
+// dependent pools need (104 x 72 in LDS: 3.7x the output area re-read instead of 5.1x with 32 x 32
+// tiles).  Each 1-D pass gives a thread 8 consecutive outputs from 16 register-held inputs
+// (van Herk / Gil-Werman with block 8: suffix maxima of the first 8, prefix maxima of the second,
+// out[i] = max(suffix[i], prefix[i]) = the 9-window [i, i+8]): 2 LDS reads per output instead of
+// 9.  Passes run over the whole region; values near its border are garbage that never reaches the
+// output tile (each pool shrinks the valid region by 4, five pools = the 20-pixel halo).
 // ---------------------------------------------------------------------------
-constexpr int NT_ = 32, NH = 20, NR = NT_ + 2 * NH;  // 72
+constexpr int NTX = 64, NTY = 32, NH = 20, RX = NTX + 2 * NH, RY = NTY + 2 * NH;  // 104 x 72
+static_assert(RX % 8 == 0 && (RX - 8) % 8 == 0 && (RY - 8) % 8 == 0, "8-output chunks tile the passes");
 
-// dst[y][x] = max_{|k|<=4} src[y][x+k]  over the rectangle [y0,y1) x [x0,x1)
-__device__ __forceinline__ void rowpass(const float* src, float* dst, int y0, int y1, int x0, int x1) {
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int y = y0 + ty; y < y1; y += 32)
-    for (int x = x0 + tx; x < x1; x += 32) {
-      const float* s = src + y * NR + x - 4;
-      float m = s[0];
+// 9-window max of 16 register values: out[i] = max(v[i .. i+8]), i < 8
+__device__ __forceinline__ void window9(const float (&v)[16], float (&o)[8]) {
+  float suf[8], pre[8];
+  suf[7] = v[7];
 #pragma unroll
-      for (int k = 1; k < 9; k++) m = fmaxf(m, s[k]);
-      dst[y * NR + x] = m;
-    }
+  for (int i = 6; i >= 0; i--) suf[i] = fmaxf(v[i], suf[i + 1]);
+  pre[0] = v[8];
+#pragma unroll
+  for (int i = 1; i < 8; i++) pre[i] = fmaxf(pre[i - 1], v[8 + i]);
+#pragma unroll
+  for (int i = 0; i < 8; i++) o[i] = fmaxf(suf[i], pre[i]);
 }
-// dst[y][x] = max_{|k|<=4} src[y+k][x]
-__device__ __forceinline__ void colpass(const float* src, float* dst, int y0, int y1, int x0, int x1) {
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int y = y0 + ty; y < y1; y += 32)
-    for (int x = x0 + tx; x < x1; x += 32) {
-      const float* s = src + (y - 4) * NR + x;
-      float m = s[0];
+// dst[y][x] = max_{|k|<=4} src[y][x+k] for every row, x in [4, RX-4): (RX-8)/8 chunks per row
+__device__ __forceinline__ void rowpass9(const float* src, float* dst) {
+  constexpr int CPR = (RX - 8) / 8;
+  for (int c = threadIdx.x; c < CPR * RY; c += blockDim.x) {
+    const int y = c / CPR, x0 = 4 + 8 * (c % CPR);
+    const float4* p = reinterpret_cast<const float4*>(src + y * RX + x0 - 4);
+    float v[16];
 #pragma unroll
-      for (int k = 1; k < 9; k++) m = fmaxf(m, s[k * NR]);
-      dst[y * NR + x] = m;
+    for (int q = 0; q < 4; q++) {
+      const float4 t = p[q];
+      v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
     }
+    float o[8];
+    window9(v, o);
+    float4* d = reinterpret_cast<float4*>(dst + y * RX + x0);
+    d[0] = make_float4(o[0], o[1], o[2], o[3]);
+    d[1] = make_float4(o[4], o[5], o[6], o[7]);
+  }
+}
+// dst[y][x] = max_{|k|<=4} src[y+k][x] for every column, y in [4, RY-4); F(o, x, y0) consumes the
+// 8 outputs of column x from row y0 (a store, or the max_mask update)
+template <typename F>
+__device__ __forceinline__ void colpass9(const float* src, F&& out) {
+  constexpr int CPC = (RY - 8) / 8;
+  for (int c = threadIdx.x; c < CPC * RX; c += blockDim.x) {
+    const int x = c % RX, y0 = 4 + 8 * (c / RX);
+    float v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) v[k] = src[(y0 - 4 + k) * RX + x];
+    float o[8];
+    window9(v, o);
+    out(o, x, y0);
+  }
 }
 
-static_assert(NT_ == 32, "the output pass maps the 32 x 32 tile one element per thread");
-// 1024 threads as 32 x 32 (2D loops over the tile: no index divisions), one 72 x 72 tile
 __global__ __launch_bounds__(1024) void nms_kernel(NmsArgs a) {
-  __shared__ float S[NR * NR];          // scores (0 outside the image)
-  __shared__ float T[NR * NR];          // row-pass scratch
-  __shared__ float M[NR * NR];          // max-pool result / supp flag
-  __shared__ float F[NR * NR];          // mask as float / supp_scores
-  __shared__ unsigned char K[NR * NR];  // max_mask
+  __shared__ __attribute__((aligned(16))) float S[RY * RX];  // scores (0 outside the image)
+  __shared__ __attribute__((aligned(16))) float T[RY * RX];  // row-pass result
+  __shared__ __attribute__((aligned(16))) float M[RY * RX];  // supp flag (1 / 0)
+  __shared__ __attribute__((aligned(16))) float F[RY * RX];  // mask as float / supp_scores
+  __shared__ unsigned char K[RY * RX];                       // max_mask
   const int H = a.H, W = a.W;
-  const int tiles_x = (W + NT_ - 1) / NT_, tiles_y = (H + NT_ - 1) / NT_;
+  const int tiles_x = (W + NTX - 1) / NTX, tiles_y = (H + NTY - 1) / NTY;
   const int per = tiles_x * tiles_y;
   const int bi = blockIdx.x / per, t = blockIdx.x % per;
-  const int y0 = (t / tiles_x) * NT_ - NH, x0 = (t % tiles_x) * NT_ - NH;
+  const int y0 = (t / tiles_x) * NTY - NH, x0 = (t % tiles_x) * NTX - NH;
   const float* sc = a.scores + (size_t)bi * H * W;
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  for (int ly = ty; ly < NR; ly += 32)
-    for (int lx = tx; lx < NR; lx += 32) {
-      const int y = y0 + ly, x = x0 + lx;
-      S[ly * NR + lx] = (y >= 0 && y < H && x >= 0 && x < W) ? sc[(size_t)y * W + x] : 0.f;
-    }
+  for (int i = threadIdx.x; i < RY * RX; i += blockDim.x) {
+    const int ly = i / RX, lx = i - ly * RX;
+    const int y = y0 + ly, x = x0 + lx;
+    S[i] = (y >= 0 && y < H && x >= 0 && x < W) ? sc[(size_t)y * W + x] : 0.f;
+    K[i] = 0;
+  }
   __syncthreads();
-  // max_mask = scores == max_pool(scores), valid on [4, NR-4)^2
-  rowpass(S, T, 0, NR, 4, NR - 4);
+  // max_mask = scores == max_pool(scores)
+  rowpass9(S, T);
   __syncthreads();
-  colpass(T, M, 4, NR - 4, 4, NR - 4);
-  __syncthreads();
-  for (int y = ty; y < NR; y += 32)
-    for (int x = tx; x < NR; x += 32) {
-      const int i = y * NR + x;
-      K[i] = (y >= 4 && y < NR - 4 && x >= 4 && x < NR - 4) ? (S[i] == M[i]) : 0;
-    }
+  colpass9(T, [&](const float (&o)[8], int x, int y) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) K[(y + k) * RX + x] = S[(y + k) * RX + x] == o[k];
+  });
   __syncthreads();
   for (int it = 0; it < 2; it++) {
-    const int lo = 4 + 8 * it;  // K valid on [lo, NR-lo)^2
-    const int l1 = lo + 4, l2 = lo + 8;
-    for (int y = ty; y < NR; y += 32)
-      for (int x = tx; x < NR; x += 32) F[y * NR + x] = K[y * NR + x] ? 1.f : 0.f;
+    for (int i = threadIdx.x; i < RY * RX; i += blockDim.x) F[i] = K[i] ? 1.f : 0.f;
     __syncthreads();
-    // supp_mask = max_pool(max_mask) > 0, valid on [l1, NR-l1)^2
-    rowpass(F, T, lo, NR - lo, l1, NR - l1);
+    // supp_mask = max_pool(max_mask) > 0; supp_scores = where(supp_mask, 0, scores)
+    rowpass9(F, T);
     __syncthreads();
-    colpass(T, M, l1, NR - l1, l1, NR - l1);
-    __syncthreads();
-    // supp_scores = where(supp_mask, 0, scores)
-    for (int y = l1 + ty; y < NR - l1; y += 32)
-      for (int x = l1 + tx; x < NR - l1; x += 32) {
-        const int i = y * NR + x;
-        const bool supp = M[i] > 0.f;
-        M[i] = supp ? 1.f : 0.f;
-        F[i] = supp ? 0.f : S[i];
-      }
-    __syncthreads();
-    // new_max_mask = supp_scores == max_pool(supp_scores), valid on [l2, NR-l2)^2
-    rowpass(F, T, l1, NR - l1, l2, NR - l2);
-    __syncthreads();
-    for (int y = ty; y < NR; y += 32)
-      for (int x = tx; x < NR; x += 32) {
-        const int i = y * NR + x;
-        if (y >= l2 && y < NR - l2 && x >= l2 && x < NR - l2) {
-          const float* s = T + (y - 4) * NR + x;
-          float m = s[0];
+    colpass9(T, [&](const float (&o)[8], int x, int y) {
 #pragma unroll
-          for (int k = 1; k < 9; k++) m = fmaxf(m, s[k * NR]);
-          // max_mask | (new_max_mask & ~supp_mask)
-          K[i] = K[i] | ((F[i] == m) && !(M[i] > 0.f));
-        } else {
-          K[i] = 0;
-        }
+      for (int k = 0; k < 8; k++) M[(y + k) * RX + x] = o[k] > 0.f ? 1.f : 0.f;
+    });
+    __syncthreads();
+    for (int i = threadIdx.x; i < RY * RX; i += blockDim.x) F[i] = M[i] > 0.f ? 0.f : S[i];
+    __syncthreads();
+    // new_max_mask = supp_scores == max_pool(supp_scores); max_mask |= new_max_mask & ~supp_mask
+    rowpass9(F, T);
+    __syncthreads();
+    colpass9(T, [&](const float (&o)[8], int x, int y) {
+#pragma unroll
+      for (int k = 0; k < 8; k++) {
+        const int i = (y + k) * RX + x;
+        K[i] = K[i] | ((F[i] == o[k]) && !(M[i] > 0.f));
       }
+    });
     __syncthreads();
   }
-  // output region [NH, NH+NT_)^2 (one element per thread): NMS'd map + candidates
-  {
-    const int ly = NH + ty, lx = NH + tx;
+  // output region [NH, NH+NTY) x [NH, NH+NTX): NMS'd map + candidates
+  for (int i = threadIdx.x; i < NTX * NTY; i += blockDim.x) {
+    const int ly = NH + i / NTX, lx = NH + i % NTX;
     const int y = y0 + ly, x = x0 + lx;
     if (y < H && x < W) {
-      const float v = K[ly * NR + lx] ? S[ly * NR + lx] : 0.f;
+      const float v = K[ly * RX + lx] ? S[ly * RX + lx] : 0.f;
       if (a.nms_out) a.nms_out[(size_t)bi * H * W + (size_t)y * W + x] = v;
       // find_high_score_index: float score > double threshold (src/super_point.cpp:158);
       // remove_borders: border <= y < H-border, border <= x < W-border (:244-245)
@@ -1016,7 +1025,7 @@ hipError_t sample_taps_h(const TapArgs& a, hipStream_t s) {
 }
 
 hipError_t nms(const NmsArgs& a, int B, hipStream_t s) {
-  const int tiles = ((a.W + NT_ - 1) / NT_) * ((a.H + NT_ - 1) / NT_);
+  const int tiles = ((a.W + NTX - 1) / NTX) * ((a.H + NTY - 1) / NTY);
   hipLaunchKernelGGL(nms_kernel, dim3(B * tiles), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
