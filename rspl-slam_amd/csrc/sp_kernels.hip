@@ -840,7 +840,9 @@ __global__ __launch_bounds__(1024) void topk_kernel(TopkArgs a) {
     if (threadIdx.x == 0) a.sel_count[bi] = 0;
     return;
   }
-  if (n > a.lds_cap) {
+  // k well below the candidate count (or beyond the LDS sort): select the k-th key first, then
+  // sort only the k selected keys (the same k keys in the same order as sorting all of them)
+  if (sorted_by_score && (n > a.lds_cap || n > 2 * a.k)) {
     if (threadIdx.x == 0) {
       sel_prefix = 0;
       sel_mask = 0;
@@ -856,12 +858,31 @@ __global__ __launch_bounds__(1024) void topk_kernel(TopkArgs a) {
         if ((key & msk) == pre) atomicAdd(&hist[(key >> shift) & 255], 1u);
       }
       __syncthreads();
-      if (threadIdx.x == 0) {
-        unsigned below = 0, d = 0;
-        while (d < 255 && below + hist[d] < sel_want) below += hist[d++];
-        sel_want -= below;
-        sel_prefix |= (unsigned long long)d << shift;
-        sel_mask |= 0xFFull << shift;
+      if (threadIdx.x < 64) {  // the first bin whose cumulative count reaches sel_want: wave scan
+        const int l = threadIdx.x;
+        unsigned h[4], sum = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+          h[j] = hist[4 * l + j];
+          sum += h[j];
+        }
+        unsigned incl = sum;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+          const unsigned y = __shfl_up(incl, o);
+          if (l >= o) incl += y;
+        }
+        const unsigned want = sel_want, excl = incl - sum;
+        const bool mine = excl < want && want <= incl;
+        const unsigned long long any = __ballot(mine);
+        if (mine || (any == 0 && l == 63)) {  // (a bin is always found: the total reaches want)
+          unsigned below = excl, d = 4 * l, j = 0;
+          while (j < 3 && below + h[j] < want) below += h[j++];
+          d += j;
+          sel_want = want - below;
+          sel_prefix |= (unsigned long long)d << shift;
+          sel_mask |= 0xFFull << shift;
+        }
       }
       __syncthreads();
     }
