@@ -5,3 +5,5 @@ tail -1 gpurun_out/ba_tests.log
 timeout -k 10 200 python -u tools/ba_repeat.py > gpurun_out/ba_repeat.log 2>&1 || { echo "repeat failed"; tail -20 gpurun_out/ba_repeat.log; exit 1; }
 tail -3 gpurun_out/ba_repeat.log
 bash tools/gpu_baprof.sh
+timeout -k 10 300 python -u bench.py --single-precision --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -30 gpurun_out/bench.err; exit 1; }
+python3 -c "import json; d=json.load(open('gpurun_out/bench.json')); print(d['value'], d['ms_per_step'], d['ba'])"
