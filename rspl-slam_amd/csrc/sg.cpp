@@ -307,7 +307,7 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
       delete s;
       return RSPL_E_DEVICE;
     }
-    constexpr int kRows = 13;
+    constexpr int kRows = 9;  // 45 workgroups per pair at N = 400 (tools/gpu_sink_ab.sh: 32 vs 48)
     int G = std::max(1, (s->ld + kRows - 1) / kRows);
     while (G < s->ld && sg::sinkhorn_lds_bytes(s->nmax, G, true) > sg::kSinkLdsMax) G++;
     if (const char* e = getenv("RSPL_SG_SINK_G")) G = std::max(1, atoi(e));  // tuning knob
