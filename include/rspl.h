@@ -570,6 +570,17 @@ int rspl_lines_stereo(rspl_lines* h, const double* lines_left, int n_left, const
                       int n_points_left, const double* lines_right, int n_right, const double* features_right,
                       int n_points_right, const int* stereo_matches, int n_matches, const double* camera_limits,
                       double* lines_right_out, uint8_t* lines_right_valid, int* n_kept_matches);
+/* Device-resident rspl_lines_stereo for a GPU pipeline: lines (device [n][4] doubles), the
+ * SuperPoint device features [2][feat_cap][259] (image 0 left, 1 right) with their device counts
+ * [2], SuperGlue's device match index of each left keypoint (right keypoint or -1); outputs the
+ * right line and validity per left line in device memory.  Stream-ordered: no host copy, no sync.
+ * A point-line overflow of max_pairs leaves every line unmatched; rspl_lines_status reports it
+ * once the stream has completed. */
+int rspl_lines_stereo_device(rspl_lines* h, const double* d_lines_left, int n_left, const double* d_lines_right,
+                             int n_right, const double* d_features, int feat_cap, const int32_t* d_counts,
+                             const int32_t* d_match_idx, const double* camera_limits, double* d_lines_right_out,
+                             uint8_t* d_lines_right_valid, void* stream);
+int rspl_lines_status(rspl_lines* h, int* overflow);
 
 #ifdef __cplusplus
 }

@@ -176,6 +176,7 @@ __global__ __launch_bounds__(1024) void match_kernel(MatchArgs a) {
   int* out = a.out + (size_t)p * a.max_lines;
   for (int i = tid; i < n0; i += 1024) out[i] = -1;
   if (np0 == 0 || np1 == 0 || n0 == 0 || n1 == 0) return;
+  if (a.status && (a.status[s0] | a.status[s1])) return;  // an assignment overflowed its capacity
   int* M = a.M + (size_t)p * a.max_lines * a.max_lines;
   int* inv0 = a.inv + (size_t)p * 2 * a.cap;
   int* inv1 = inv0 + a.cap;
@@ -205,7 +206,7 @@ __global__ __launch_bounds__(1024) void match_kernel(MatchArgs a) {
       inv1[c1[t] + atomicAdd(&f1[t], 1)] = l;
     }
   __syncthreads();
-  const int nm = a.n_matches[p];
+  const int nm = min(a.n_matches[p], a.max_matches);
   const int* mt = a.matches + (size_t)p * a.max_matches * 2;
   for (int m = tid; m < nm; m += 1024) {
     const int q = mt[2 * m], t = mt[2 * m + 1];
@@ -261,6 +262,60 @@ __global__ __launch_bounds__(1024) void match_kernel(MatchArgs a) {
       out[bi] = j;
     }
   }
+}
+
+__global__ __launch_bounds__(256) void stereo_filter_kernel(StereoArgs a) {
+#pragma clang fp contract(off)
+  const int q = blockIdx.x * 256 + threadIdx.x;
+  if (q >= a.n_points[0]) return;
+  const int t = a.idx[q];
+  if (t < 0 || t >= a.n_points[1]) return;
+  const double* l = a.pts + (size_t)q * a.stride + a.xoff;
+  const double* r = a.pts + a.pt_batch + (size_t)t * a.stride + a.xoff;
+  const double dx = fabs(l[0] - r[0]), dy = fabs(l[1] - r[1]);
+  if (dx > a.min_x && dx < a.max_x && dy <= a.max_y) {
+    const int slot = atomicAdd(a.n_out, 1);
+    if (slot < a.max_matches) {
+      a.matches[2 * slot] = q;
+      a.matches[2 * slot + 1] = t;
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void right_lines_kernel(RightArgs a) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= a.n_lines[0]) return;
+  const int j = a.line_matches[i];
+  const bool ok = j > 0;  // frame.cc:190
+  a.valid[i] = ok ? 1 : 0;
+  for (int k = 0; k < 4; k++) a.out[4 * i + k] = ok ? a.lines_right[4 * j + k] : 0.0;
+}
+
+__global__ void set_counts_kernel(int* n_lines, int nl0, int nl1, int* n_points, const int32_t* counts,
+                                  int* n_matches) {
+  if (threadIdx.x == 0) {
+    n_lines[0] = nl0;
+    n_lines[1] = nl1;
+    n_points[0] = counts[0];
+    n_points[1] = counts[1];
+    n_matches[0] = 0;
+  }
+}
+
+hipError_t set_counts(int* n_lines, int nl0, int nl1, int* n_points, const int32_t* counts, int* n_matches,
+                      hipStream_t s) {
+  hipLaunchKernelGGL(set_counts_kernel, dim3(1), dim3(64), 0, s, n_lines, nl0, nl1, n_points, counts, n_matches);
+  return hipGetLastError();
+}
+
+hipError_t stereo_filter(const StereoArgs& a, int max_left, hipStream_t s) {
+  hipLaunchKernelGGL(stereo_filter_kernel, dim3((max_left + 255) / 256), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t right_lines(const RightArgs& a, int max_lines, hipStream_t s) {
+  hipLaunchKernelGGL(right_lines_kernel, dim3((max_lines + 255) / 256), dim3(256), 0, s, a);
+  return hipGetLastError();
 }
 
 hipError_t assign(const AssignArgs& a, int B, hipStream_t s) {

@@ -44,9 +44,38 @@ struct MatchArgs {
   int* M;
   int* inv;
   int* out;
+  const int* status;     // AssignArgs::status of the sets (nullable): an overflowed set matches nothing
+};
+
+// Frame::AddRightFeatures' stereo filter (frame.cc:157-167) on the device: the SuperGlue match
+// index of each left keypoint (idx[q] = right keypoint or -1) -> (q, t) pairs inside the disparity
+// window, compacted in any order (MatchLines only counts them) into matches, count into *n_out.
+struct StereoArgs {
+  const int32_t* idx;     // [n_left_points]
+  const int* n_points;    // [2] left / right keypoint counts
+  const double* pts;      // left record j at pts + j * stride + xoff, right at + pt_batch
+  size_t pt_batch;
+  int stride, xoff;
+  double min_x, max_x, max_y;
+  int* matches;           // [max_matches][2]
+  int* n_out;
+  int max_matches;
+};
+// right line of each left line from the line matches (frame.cc:189-196, the reference's > 0 test)
+struct RightArgs {
+  const int* line_matches;  // [n_left]
+  const double* lines_right;  // [max_lines][4]
+  const int* n_lines;       // [2]
+  double* out;              // [n_left][4]
+  uint8_t* valid;           // [n_left]
 };
 
 hipError_t assign(const AssignArgs& a, int B, hipStream_t s);
+// device-side counts of a device call: n_lines = {nl0, nl1}, n_points = counts[0..1], zeroed n_matches
+hipError_t set_counts(int* n_lines, int nl0, int nl1, int* n_points, const int32_t* counts, int* n_matches,
+                      hipStream_t s);
+hipError_t stereo_filter(const StereoArgs& a, int max_left, hipStream_t s);
+hipError_t right_lines(const RightArgs& a, int max_lines, hipStream_t s);
 hipError_t match(const MatchArgs& a, int P, hipStream_t s);
 
 }  // namespace lines

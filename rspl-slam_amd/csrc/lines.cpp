@@ -373,6 +373,7 @@ int run_match(rspl_lines* h, int problem, int set0, int set1, const int* matches
   a.matches = h->matches + problem * Mm * 2; a.n_matches = h->n_matches + problem; a.max_lines = h->cfg.max_lines;
   a.cap = h->cap; a.max_matches = (int)Mm; a.M = h->M + (size_t)problem * h->cfg.max_lines * h->cfg.max_lines;
   a.inv = h->inv + (size_t)problem * 2 * h->cap; a.out = h->out + (size_t)problem * h->cfg.max_lines;
+  a.status = nullptr;  // host calls check the assignment status themselves
   RSPL_HIP(lines::match(a, 1, h->stream));
   RSPL_HIP(hipStreamSynchronize(h->stream));
   (void)n_points0;
@@ -439,3 +440,58 @@ extern "C" int rspl_lines_stereo(rspl_lines* h, const double* lines_left, int n_
   }
   return RSPL_OK;
 }
+
+// Device-resident form of rspl_lines_stereo for a GPU pipeline: SuperPoint's device features and
+// counts (image 0 = left, 1 = right) and SuperGlue's device match index of each left keypoint go in,
+// per left line the right line and its validity come out, all stream-ordered (no host copy, no
+// synchronisation).  An assignment that overflows max_pairs leaves every left line unmatched;
+// rspl_lines_status reports it after the stream has completed.
+extern "C" int rspl_lines_stereo_device(rspl_lines* h, const double* d_lines_left, int n_left,
+                                        const double* d_lines_right, int n_right, const double* d_features,
+                                        int feat_cap, const int32_t* d_counts, const int32_t* d_match_idx,
+                                        const double* camera_limits, double* d_lines_right_out,
+                                        uint8_t* d_lines_right_valid, void* stream) {
+  RSPL_CHECK_ARG(h && d_features && d_counts && d_match_idx && camera_limits && (n_left == 0 || d_lines_left) &&
+                     (n_right == 0 || d_lines_right) && (n_left == 0 || (d_lines_right_out && d_lines_right_valid)),
+                 "rspl_lines_stereo_device: NULL argument");
+  RSPL_CHECK_ARG(n_left >= 0 && n_left <= h->cfg.max_lines && n_right >= 0 && n_right <= h->cfg.max_lines,
+                 "line counts outside [0, %d]", h->cfg.max_lines);
+  RSPL_CHECK_ARG(feat_cap > 0 && feat_cap <= h->cfg.max_points, "feat_cap outside [1, %d]", h->cfg.max_points);
+  hipStream_t st = stream ? (hipStream_t)stream : h->stream;
+  const size_t L = h->cfg.max_lines;
+  if (n_left)
+    RSPL_HIP(hipMemcpyAsync(h->lines, d_lines_left, sizeof(double) * 4 * n_left, hipMemcpyDeviceToDevice, st));
+  if (n_right)
+    RSPL_HIP(hipMemcpyAsync(h->lines + L * 4, d_lines_right, sizeof(double) * 4 * n_right, hipMemcpyDeviceToDevice, st));
+  RSPL_HIP(lines::set_counts(h->n_lines, n_left, n_right, h->n_points, d_counts, h->n_matches, st));
+  lines::AssignArgs a{};
+  a.lines = h->lines; a.n_lines = h->n_lines; a.pts = d_features; a.pt_batch = (size_t)feat_cap * 259;
+  a.pt_stride = 259; a.pt_xoff = 1; a.n_points = h->n_points; a.offsets = h->offsets; a.idx = h->idx;
+  a.dist = h->dist; a.max_lines = h->cfg.max_lines; a.cap = h->cap; a.status = h->status;
+  RSPL_HIP(lines::assign(a, 2, st));
+  lines::StereoArgs sa{};
+  sa.idx = d_match_idx; sa.n_points = h->n_points; sa.pts = d_features; sa.pt_batch = (size_t)feat_cap * 259;
+  sa.stride = 259; sa.xoff = 1; sa.min_x = camera_limits[0]; sa.max_x = camera_limits[1]; sa.max_y = camera_limits[2];
+  sa.matches = h->matches; sa.n_out = h->n_matches; sa.max_matches = std::max(1, h->cfg.max_matches);
+  RSPL_HIP(lines::stereo_filter(sa, feat_cap, st));
+  lines::MatchArgs m{};
+  m.off0 = m.off1 = h->offsets; m.idx0 = m.idx1 = h->idx; m.n_lines0 = m.n_lines1 = h->n_lines;
+  m.n_points0 = m.n_points1 = h->n_points; m.set0 = 0; m.set1 = 1; m.step0 = m.step1 = 0;
+  m.matches = h->matches; m.n_matches = h->n_matches; m.max_lines = h->cfg.max_lines; m.cap = h->cap;
+  m.max_matches = std::max(1, h->cfg.max_matches); m.M = h->M; m.inv = h->inv; m.out = h->out; m.status = h->status;
+  RSPL_HIP(lines::match(m, 1, st));
+  lines::RightArgs r{};
+  r.line_matches = h->out; r.lines_right = h->lines + L * 4; r.n_lines = h->n_lines; r.out = d_lines_right_out;
+  r.valid = d_lines_right_valid;
+  RSPL_HIP(lines::right_lines(r, std::max(1, n_left), st));
+  return RSPL_OK;
+}
+
+extern "C" int rspl_lines_status(rspl_lines* h, int* overflow) {
+  RSPL_CHECK_ARG(h && overflow, "rspl_lines_status: NULL argument");
+  int st[2] = {0, 0};
+  RSPL_HIP(hipMemcpy(st, h->status, sizeof(st), hipMemcpyDeviceToHost));
+  *overflow = st[0] | st[1];
+  return RSPL_OK;
+}
+

@@ -8,6 +8,8 @@ Mirrors the reference's free functions and LineDetector (include/line_processor.
   MatchLines                line_processor.cc:221-283 (GPU) -> line_matches (-1 = unmatched)
   StereoLines               the line part of Frame::AddLeftFeatures / AddRightFeatures
                             (frame.cc:124-129, 150-196) in one call
+  stereo_lines_device       the same, device-resident (SuperPoint / SuperGlue device outputs in,
+                            device right lines out, stream-ordered)
 
 FLD (cv::ximgproc::FastLineDetector) and the RCF edge network are not rebuilt: detected segments
 are the input.  There is no CPU path for the GPU functions.
@@ -41,6 +43,8 @@ def _declare(lib):
     lib.rspl_lines_match.argtypes = [vp, _i32p, _i32p, ip, _i32p, _i32p, ip, _i32p, ip, ip, ip, _i32p]
     lib.rspl_lines_stereo.argtypes = [vp, _dp, ip, _dp, ip, _dp, ip, _dp, ip, _i32p, ip, _dp, _dp, _u8p,
                                       C.POINTER(ip)]
+    lib.rspl_lines_stereo_device.argtypes = [vp, vp, ip, vp, ip, vp, ip, vp, vp, _dp, vp, vp, vp]
+    lib.rspl_lines_status.argtypes = [vp, C.POINTER(ip)]
     lib._rspl_lines_declared = True
     return lib
 
@@ -148,3 +152,20 @@ class LineMatcher:
                    "rspl_lines_stereo")
         n = len(Ll)
         return out[:n].copy(), valid[:n].astype(bool), kept.value
+
+    def stereo_lines_device(self, d_lines_left: int, n_left: int, d_lines_right: int, n_right: int,
+                            d_features: int, feat_cap: int, d_counts: int, d_match_idx: int,
+                            camera_limits: Sequence[float], d_lines_right_out: int, d_valid: int, stream=None):
+        """rspl_lines_stereo_device on raw device pointers (see include/rspl.h)."""
+        lim = np.ascontiguousarray(camera_limits, np.float64)
+        capi.check(self._lib.rspl_lines_stereo_device(self._h, d_lines_left, n_left, d_lines_right, n_right,
+                                                      d_features, feat_cap, d_counts, d_match_idx,
+                                                      lim.ctypes.data_as(_dp), d_lines_right_out, d_valid, stream),
+                   "rspl_lines_stereo_device")
+
+    def status(self) -> bool:
+        """True when an assignment of the last device call overflowed max_pairs."""
+        o = C.c_int()
+        capi.check(self._lib.rspl_lines_status(self._h, C.byref(o)), "rspl_lines_status")
+        return bool(o.value)
+

@@ -89,3 +89,33 @@ def test_stereo_lines_matches_oracle(lm):
     np.testing.assert_array_equal(valid, ref_valid)
     np.testing.assert_array_equal(lr, ref_lr)
     assert valid.sum() > 10
+
+
+def test_stereo_lines_device_matches_host(lm):
+    """rspl_lines_stereo_device (SuperPoint-layout device features, a SuperGlue-style device match
+    index per left keypoint) gives the same right lines / validity as the host call and the oracle."""
+    C = pkg.capi
+    sc = SY.line_scene(n_lines=80, n_points=600, seed=6)
+    L0, L1 = LR.line_extractor(sc["seg_left"]), LR.line_extractor(sc["seg_right"])
+    F0, F1, m = sc["feat_left"], sc["feat_right"], sc["stereo_matches"]
+    lim = (2.0, 60.0, 2.0)
+    ref_lr, ref_valid, _ = lm.StereoLines(L0, F0, L1, F1, m, lim)
+    cap = 800
+    feats = np.zeros((2, cap, 259))
+    feats[0, :len(F0)] = F0
+    feats[1, :len(F1)] = F1
+    idx = np.full(cap, -1, np.int32)
+    idx[m[:, 0]] = m[:, 1]  # one right keypoint per left keypoint, as SuperGlue's mutual matches
+    dF = C.DeviceBuffer(feats.nbytes).upload(feats)
+    dC = C.DeviceBuffer(8).upload(np.array([len(F0), len(F1)], np.int32))
+    dI = C.DeviceBuffer(idx.nbytes).upload(idx)
+    dL0 = C.DeviceBuffer(max(8, L0.nbytes)).upload(np.ascontiguousarray(L0))
+    dL1 = C.DeviceBuffer(max(8, L1.nbytes)).upload(np.ascontiguousarray(L1))
+    dO = C.DeviceBuffer(len(L0) * 32)
+    dV = C.DeviceBuffer(max(8, len(L0)))
+    lm.stereo_lines_device(dL0.ptr, len(L0), dL1.ptr, len(L1), dF.ptr, cap, dC.ptr, dI.ptr, lim, dO.ptr, dV.ptr)
+    C.load().rspl_device_synchronize()
+    assert not lm.status()
+    np.testing.assert_array_equal(dV.download(len(L0), np.uint8).astype(bool), ref_valid)
+    np.testing.assert_array_equal(dO.download((len(L0), 4), np.float64), ref_lr)
+    assert ref_valid.sum() > 10

@@ -8,6 +8,8 @@ import pathlib
 import sys
 import time
 
+import numpy as np
+
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "oracle"))
@@ -39,6 +41,31 @@ def main():
     for _ in range(a.iters):
         lr, valid, kept = lm.StereoLines(*args)
     gpu_ms = (time.perf_counter() - t) / a.iters * 1e3
+    # device-resident form: SuperPoint-layout device features, a device match index per left keypoint
+    C = pkg.capi
+    m = sc["stereo_matches"]
+    cap = max(len(sc["feat_left"]), len(sc["feat_right"]))
+    feats = np.zeros((2, cap, 259))
+    feats[0, :len(sc["feat_left"])] = sc["feat_left"]
+    feats[1, :len(sc["feat_right"])] = sc["feat_right"]
+    idx = np.full(cap, -1, np.int32)
+    idx[m[:, 0]] = m[:, 1]
+    dF = C.DeviceBuffer(feats.nbytes).upload(feats)
+    dC = C.DeviceBuffer(8).upload(np.array([len(sc["feat_left"]), len(sc["feat_right"])], np.int32))
+    dI = C.DeviceBuffer(idx.nbytes).upload(idx)
+    dL0, dL1 = C.DeviceBuffer(L0.nbytes).upload(L0), C.DeviceBuffer(L1.nbytes).upload(L1)
+    dO, dV = C.DeviceBuffer(L0.nbytes), C.DeviceBuffer(len(L0))
+    st = C.Stream()
+    dev = lambda: lm.stereo_lines_device(dL0.ptr, len(L0), dL1.ptr, len(L1), dF.ptr, cap, dC.ptr, dI.ptr, lim,
+                                         dO.ptr, dV.ptr, st.handle)
+    for _ in range(10):
+        dev()
+    st.synchronize()
+    t = time.perf_counter()
+    for _ in range(a.iters):
+        dev()
+    st.synchronize()
+    dev_ms = (time.perf_counter() - t) / a.iters * 1e3
     t = time.perf_counter()
     n_cpu = max(3, a.iters // 50)
     F0, F1, m = sc["feat_left"], sc["feat_right"], sc["stereo_matches"]
@@ -52,6 +79,7 @@ def main():
                       "stereo_matches_kept": kept, "right_lines_valid": int(valid.sum()),
                       "merge_ms_per_image_host": round(merge_ms, 4),
                       "stereo_association_ms_gpu_call": round(gpu_ms, 4),
+                      "stereo_association_ms_device_resident": round(dev_ms, 4),
                       "stereo_association_ms_oracle_python_1core": round(cpu_ms, 3)}))
 
 
