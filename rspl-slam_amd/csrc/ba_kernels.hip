@@ -790,14 +790,34 @@ __global__ __launch_bounds__(256) void pose_diag_kernel(Problem P, Lin L, Active
       for (int i = 0; i < 6; i++) d[i] = H[i * 7];
     }
   }
-  for (int pa = 0; pa < A.K; pa++) {
-    double acc[6];
+  // per pose: each wave's butterfly (poses absent from the wave skipped), then the 4 wave sums in
+  // wave order -- no block barrier per pose
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ double wsum[4][32][6];
+  for (int p0 = 0; p0 < A.K; p0 += 32) {
+    const int pn = min(32, A.K - p0);
+    for (int j = 0; j < pn; j++) {
+      const int pa = p0 + j;
+      double acc[6];
 #pragma unroll
-    for (int i = 0; i < 6; i++) acc[i] = a == pa ? d[i] : 0.0;
-    block_reduce<6>(acc, red);
-    if (threadIdx.x < 6) S.partial2[((size_t)pa * gridDim.x + blockIdx.x) * 6 + threadIdx.x] = red[threadIdx.x];
+      for (int i = 0; i < 6; i++) acc[i] = a == pa ? d[i] : 0.0;
+      if (__ballot(a == pa)) {  // wave-uniform
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+          for (int i = 0; i < 6; i++) acc[i] += __shfl_xor(acc[i], o);
+      }
+      if (lane < 6) wsum[wv][j][lane] = acc[lane];
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < 6 * pn; q += 256) {
+      const int j = q / 6, i = q - 6 * j;
+      S.partial2[((size_t)(p0 + j) * gridDim.x + blockIdx.x) * 6 + i] =
+          ((wsum[0][j][i] + wsum[1][j][i]) + wsum[2][j][i]) + wsum[3][j][i];
+    }
     __syncthreads();
   }
+  (void)red;
 }
 
 // Landmark CSR, step 1: each edge takes a slot of its landmark's range (order arbitrary)
