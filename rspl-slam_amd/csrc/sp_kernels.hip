@@ -334,6 +334,36 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
     }
   }
 
+  if constexpr (!POOL && !OUT_F32) {
+    // full-resolution fp16 output staged through LDS (the weight buffer, free after the last
+    // stage) so the global stores are 16-byte rows of 8 channels instead of 2-byte scatters
+    constexpr int OS = 72;  // halves per pixel row in LDS (64 channels + pad)
+    static_assert(TH * 16 * OS <= 9 * 64 * HCS, "output tile exceeds the weight buffer");
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+      const float bias = a.bias[co0 + n * 32 + ml];
+#pragma unroll
+      for (int m = 0; m < MT; m++) {
+        const int ly = wv * (TH / 4) + 2 * m;
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+          const int mm = (r & 3) + 8 * (r >> 2) + 4 * kl;
+          const float v = acc[m][n][r] + bias;
+          wts[((ly + (mm >> 4)) * 16 + (mm & 15)) * OS + n * 32 + ml] = (_Float16)(v > 0.f ? v : 0.f);
+        }
+      }
+    }
+    __syncthreads();
+    for (int i = tid; i < TH * 16 * 8; i += 256) {
+      const int px = i >> 3, q = i & 7;
+      const int y = y0 + (px >> 4), x = x0 + (px & 15);
+      if (y < H && x < W)
+        *reinterpret_cast<half8*>(a.hout + (size_t)bi * H * W * COUT + ((size_t)y * W + x) * COUT + co0 + 8 * q) =
+            *reinterpret_cast<const half8*>(&wts[px * OS + 8 * q]);
+    }
+    return;
+  }
 #pragma unroll
   for (int n = 0; n < 2; n++) {
     const int co = co0 + n * 32 + ml;
