@@ -364,6 +364,38 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
     }
     return;
   }
+  if constexpr (POOL && !OUT_F32) {
+    // 2x2-pooled output tile (TH/2 x 8 pixels x 64 channels) staged through LDS the same way
+    constexpr int OS = 72;
+    static_assert((TH / 2) * 8 * OS <= 9 * 64 * HCS, "pooled tile exceeds the weight buffer");
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+      const float bias = a.bias[co0 + n * 32 + ml];
+#pragma unroll
+      for (int m = 0; m < MT; m++) {
+        const int pyl = wv * (TH / 8) + m;  // (wv * TH/4 + 2m) / 2
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+          const int r0 = (g & 1) * 2 + (g >> 1) * 4;
+          const int pc = (r0 & 3) + 8 * ((r0 >> 2) & 1) + 4 * kl;
+          float v = fmaxf(fmaxf(acc[m][n][r0], acc[m][n][r0 + 1]), fmaxf(acc[m][n][r0 + 8], acc[m][n][r0 + 9]));
+          v += bias;
+          wts[(pyl * 8 + (pc >> 1)) * OS + n * 32 + ml] = (_Float16)(v > 0.f ? v : 0.f);
+        }
+      }
+    }
+    __syncthreads();
+    const int H2 = H / 2, W2 = W / 2;
+    for (int i = tid; i < (TH / 2) * 8 * 8; i += 256) {
+      const int px = i >> 3, q = i & 7;
+      const int py = (y0 >> 1) + (px >> 3), pxx = (x0 >> 1) + (px & 7);
+      if (py < H2 && pxx < W2)
+        *reinterpret_cast<half8*>(a.hout + (size_t)bi * H2 * W2 * COUT + ((size_t)py * W2 + pxx) * COUT + co0 + 8 * q) =
+            *reinterpret_cast<const half8*>(&wts[px * OS + 8 * q]);
+    }
+    return;
+  }
 #pragma unroll
   for (int n = 0; n < 2; n++) {
     const int co = co0 + n * 32 + ml;
