@@ -592,6 +592,11 @@ __global__ __launch_bounds__(256) void det_head_h_kernel(HeadHArgs a) {
     for (int r = 0; r < 16; r++) acc[n][r] += b;
   }
   const int Wf = a.W8 * 8;
+  // the wave's 32 cells x 64 scores go through LDS, then out as rows of the full-resolution map
+  // (lanes = consecutive cells of one pixel row: 32-byte pieces side by side) instead of 4-byte
+  // scatters into 8 rows per cell
+  __shared__ __attribute__((aligned(16))) float stage[4][32][65];
+  float(*sg)[65] = stage[wv];
 #pragma unroll
   for (int r = 0; r < 16; r++) {
     float m = -INFINITY;
@@ -608,17 +613,20 @@ __global__ __launch_bounds__(256) void det_head_h_kernel(HeadHArgs a) {
     }
 #pragma unroll
     for (int o = 16; o >= 1; o >>= 1) sum += __shfl_xor(sum, o, 32);
-    const int cell = base + (r & 3) + 8 * (r >> 2) + 4 * kl;
-    if (cell < total) {
-      const int bi = cell / a.P, p = cell % a.P;
-      const int cy = p / a.W8, cx = p % a.W8;
-      float* sc = a.scores + (size_t)bi * a.P * 64;
+    const int cl = (r & 3) + 8 * (r >> 2) + 4 * kl;
 #pragma unroll
-      for (int n = 0; n < 2; n++) {  // channels 0..63 (the dustbin, 64, is dropped)
-        const int c = n * 32 + ml;
-        sc[(size_t)(cy * 8 + (c >> 3)) * Wf + cx * 8 + (c & 7)] = e[n] / sum;
-      }
-    }
+    for (int n = 0; n < 2; n++) sg[cl][n * 32 + ml] = e[n] / sum;  // channels 0..63 (dustbin dropped)
+  }
+  __builtin_amdgcn_wave_barrier();  // LDS in program order within the wave
+  for (int i = lane; i < 32 * 8 * 2; i += 64) {  // (pixel row pr, cell j, half h): 4 floats each
+    const int pr = i >> 6, j = (i >> 1) & 31, hh = i & 1;
+    const int cell = base + j;
+    if (cell >= total) continue;
+    const int bi = cell / a.P, p = cell % a.P;
+    const int cy = p / a.W8, cx = p % a.W8;
+    const float* src = &sg[j][pr * 8 + 4 * hh];
+    *reinterpret_cast<float4*>(a.scores + (size_t)bi * a.P * 64 + (size_t)(cy * 8 + pr) * Wf + cx * 8 + 4 * hh) =
+        make_float4(src[0], src[1], src[2], src[3]);
   }
 }
 
