@@ -9,7 +9,7 @@ for L in librspl_old.so librspl.so; do
 import sqlite3,sys,glob
 f=glob.glob(f"gpurun_out/pd_{sys.argv[1]}/**/run_results.db", recursive=True)[0]
 c=sqlite3.connect(f)
-for n,cnt,avg in c.execute("select name,count(*),avg(duration) from kernels where name like '%pose_diag%' or name like '%post_kernel%' group by name"):
+for n,cnt,avg in c.execute("select name,count(*),avg(duration) from kernels where name like '%pair_chunk%' or name like '%schur%' group by name"):
     print(sys.argv[1], n[:40], cnt, round(avg/1000,2))
 PY
   rm -rf gpurun_out/pd_$L
