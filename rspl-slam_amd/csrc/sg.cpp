@@ -41,7 +41,8 @@ struct rspl_sg {
   _Float16 *Xh, *QKh, *Vth, *Oh, *MSGh, *HIDh;
   _Float16 *Qf[2], *Kf[2], *Vf[2];  // fused layers: q (row-major) / k, v (MFMA fragment order), ping-pong
   int ldv = 0;  // token stride of Vth (nmax rounded up to the 32-key attention tile; zero padded)
-  unsigned long long *ug, *vg;  // Sinkhorn u / v exchange granules [B][ld]
+  unsigned long long *ug, *vg;  // Sinkhorn u / v exchange granules [B][ld] (row-block: ug = [B][2][rbG][ld])
+  int rbG = 0;                  // row-block Sinkhorn workgroups per pair (0: slab kernel)
   float* cplT = nullptr;        // transposed column slabs when they exceed LDS [B][ld*ld]
   bool sink_scratch = false;
   unsigned* err = nullptr;      // [B] sticky Sinkhorn timeout flags, host-mapped (rspl_sg_status)
@@ -100,7 +101,7 @@ void carve(F& ar, rspl_sg* s) {
   for (int i = 0; i < 2; i++) {
     take(s->Qf[i], T * 256); take(s->Kf[i], (size_t)B * 2 * 256 * s->ldv); take(s->Vf[i], (size_t)B * 2 * 256 * s->ldv);
   }
-  take(s->cpl, 2 * B * ld * ld); take(s->Z, 2 * B * ld * ld); take(s->ug, B * ld); take(s->vg, B * ld);
+  take(s->cpl, 2 * B * ld * ld); take(s->Z, 2 * B * ld * ld); take(s->ug, B * ld * (s->rbG ? 2 * s->rbG : 1)); take(s->vg, B * ld);
   if (s->sink_scratch) take(s->cplT, B * ld * ld);
   take(s->dbg_alpha, 4);
   take(s->cn0, 2 * B); take(s->cn1, 2 * B);
@@ -267,7 +268,9 @@ static hipError_t run_sinkhorn(rspl_sg* s, const float* cpl, float* Zp, const in
   sk.seq = s->sk_seq = (s->sk_seq % 0xFFFFFu) + 1;
   sk.spin_limit = s->spin_limit; sk.inject = s->inject;
   sk.err = s->d_err; sk.n0 = cn0; sk.n1 = cn1;
-  sk.nmax = s->nmax; sk.G = s->G; sk.iters = iters;
+  sk.nmax = s->nmax; sk.G = s->rbG ? s->rbG : s->G; sk.rb = s->rbG > 0; sk.iters = iters;
+  static const bool fx = getenv("RSPL_SG_FEXP") && atoi(getenv("RSPL_SG_FEXP")) != 0;
+  sk.fx = fx;
   if ((e = sg::sinkhorn(sk, B, st, t0, t1)) != hipSuccess) return e;
   if (probing) {  // debug: Sinkhorn cycles per workgroup-iteration by phase
     unsigned long long h[5];
@@ -314,7 +317,17 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
     G = std::min(G, std::max(1, ncu / s->B));
     s->G = G;
     s->sink_scratch = sg::sinkhorn_lds_bytes(s->nmax, G, true) > sg::kSinkLdsMax;
-    if (s->B * s->G > ncu) {
+    // row-block kernel (rows in registers, one exchange per iteration) when nmax + 1 <= 448;
+    // RSPL_SG_SINK=slab keeps the slab kernel, RSPL_SG_RB_G picks its workgroups per pair
+    const char* sk = getenv("RSPL_SG_SINK");
+    if (!(sk && std::string(sk) == "slab")) {
+      int rg = 16;
+      if (const char* e = getenv("RSPL_SG_RB_G")) rg = atoi(e);
+      rg = std::min(rg, std::max(1, ncu / s->B));
+      while (rg <= 32 && rg * s->B <= ncu && !sg::sinkhorn_rb_rpw(s->nmax, rg)) rg++;
+      if (rg * s->B <= ncu && sg::sinkhorn_rb_rpw(s->nmax, rg)) s->rbG = rg;
+    }
+    if (s->B * s->G > ncu && !s->rbG) {
       set_error("max_batch (%d) exceeds the CU count (%d): the Sinkhorn workgroups must be co-resident", s->B, ncu);
       delete s;
       return RSPL_E_ARG;
@@ -324,7 +337,7 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
   carve(sz, s);
   if ((rc = s->arena.reserve(sz.used))) { delete s; return rc; }
   carve(s->arena, s);
-  if (hipMemset(s->ug, 0, sizeof(unsigned long long) * s->B * s->ld) != hipSuccess ||
+  if (hipMemset(s->ug, 0, sizeof(unsigned long long) * s->B * s->ld * (s->rbG ? 2 * s->rbG : 1)) != hipSuccess ||
       hipMemset(s->vg, 0, sizeof(unsigned long long) * s->B * s->ld) != hipSuccess ||
       hipMemset(s->Vth, 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess ||
       hipMemset(s->Kf[0], 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess ||

@@ -1400,6 +1400,221 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_kernel(SinkArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Row-block log-domain Sinkhorn (superglue.py:176-205), one exchange per iteration.
+// G workgroups per pair; workgroup g holds WHOLE rows [r0, r0 + nr) of the couplings in
+// registers: wave w owns rows w + 16 k (k < RPW), lane L columns L + 64 q (q < kRbQ).
+// Since every wave holds full rows and a replicated v, the row pass
+//   u_i = log_mu_i - LSE_j(C_ij + v_j)
+// is wave-local (no barrier, no exchange).  The column pass
+//   v_j = log_nu_j - LSE_i(C_ij + u_i)
+// reduces each lane's columns over its wave's rows in registers, the 16 waves through LDS,
+// and the G workgroups through one all-gather of per-column partial LSEs (tagged 8-byte
+// granules, double-buffered by iteration parity).  Every workgroup merges the G partials
+// in the same order (g = 0 .. G-1), so all hold a bit-identical v.  Parity reuse is safe:
+// workgroup g publishes iteration it + 2 into slot (it & 1) only after every peer has
+// published it + 1, which each peer does only after reading all of iteration it.
+// ---------------------------------------------------------------------------
+constexpr int kRbQ = 7;                 // 7 x 64 = 448 >= nmax + 1 columns per lane set
+// exp for the LSE terms: FX = false -> expf; FX = true -> v_exp_f32 on the split product
+// d*log2(e) = a + e (a rounded, e its fma residual) corrected to first order: 2^a (1 + e ln 2);
+// arguments are <= 0 here (shifted by the max), below -150 the result is 0 as with expf
+template <bool FX>
+__device__ __forceinline__ float sk_exp(float d) {
+  if constexpr (!FX) {
+    return expf(d);
+  } else {
+    d = fmaxf(d, -150.f);  // -inf (masked rows / columns) -> exactly 0 below, not NaN
+    const float a = d * 1.44269504f;
+    const float e = fmaf(d, 1.44269504f, -a) + d * 1.9259630e-8f;
+    const float r = __builtin_amdgcn_exp2f(a);
+    return fmaf(r, e * 0.693147181f, r);
+  }
+}
+
+template <int RPW, int GM, bool FX>  // rows per wave, max workgroups per pair, fast exp
+__global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
+  __shared__ float pm[16][kRbQ * 64];   // per-wave column partial max
+  __shared__ float ps[16][kRbQ * 64];   // per-wave column partial sum
+  __shared__ float vs[kRbQ * 64];       // merged v
+  __shared__ int flag[1];
+  const int p = blockIdx.y, g = blockIdx.x, G = gridDim.x;
+  const int m = a.n0[p], n = a.n1[p];
+  if (m <= 0 || n <= 0) return;
+  const int R = m + 1, Cc = n + 1, ld = a.nmax + 1;
+  const int rs = (R + G - 1) / G;
+  const int r0 = min(R, g * rs), nr = min(R, r0 + rs) - r0;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* Cg = a.cpl + (size_t)p * ld * ld;
+  float x[RPW][kRbQ];
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int r = wv + 16 * k;
+#pragma unroll
+    for (int q = 0; q < kRbQ; q++) {
+      const int j = lane + 64 * q;
+      x[k][q] = (r < nr && j < Cc) ? Cg[(size_t)(r0 + r) * ld + j] : -INFINITY;
+    }
+  }
+  float vr[kRbQ];
+#pragma unroll
+  for (int q = 0; q < kRbQ; q++) vr[q] = 0.f;
+  float ur[RPW];
+  // log_mu / log_nu (superglue.py:198-200), float arithmetic as the module
+  const float fm = (float)m, fn = (float)n;
+  const float norm = -logf(fm + fn);
+  const float lmu_bin = logf(fn) + norm, lnu_bin = logf(fm) + norm;
+  if (tid == 0) flag[0] = 0;
+  __syncthreads();
+  long long pr[4] = {0, 0, 0, 0};
+  bool failed = false;
+  for (int it = 0; it < a.iters; it++) {
+    const unsigned tag = (a.seq << 12) | (unsigned)(it + 1);
+    const long long q0 = __builtin_amdgcn_s_memtime();
+    // row pass: all RPW rows of the wave together (independent DPP chains interleave)
+    {
+      float mx[RPW], sm[RPW];
+#pragma unroll
+      for (int k = 0; k < RPW; k++) {
+        mx[k] = x[k][0] + vr[0];
+#pragma unroll
+        for (int q = 1; q < kRbQ; q++) mx[k] = fmaxf(mx[k], x[k][q] + vr[q]);
+      }
+#pragma unroll
+      for (int k = 0; k < RPW; k++) mx[k] = wave_max_dpp(mx[k]);
+#pragma unroll
+      for (int k = 0; k < RPW; k++) {
+        sm[k] = 0.f;
+#pragma unroll
+        for (int q = 0; q < kRbQ; q++) sm[k] += sk_exp<FX>((x[k][q] + vr[q]) - mx[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < RPW; k++) sm[k] = wave_sum_dpp(sm[k]);
+#pragma unroll
+      for (int k = 0; k < RPW; k++) {
+        const int r = wv + 16 * k;
+        ur[k] = r < nr ? ((r0 + r) < m ? norm : lmu_bin) - (logf(sm[k]) + mx[k]) : 0.f;
+      }
+    }
+    const long long q1 = __builtin_amdgcn_s_memtime();
+    // column partials over the wave's rows, then over the 16 waves
+#pragma unroll
+    for (int q = 0; q < kRbQ; q++) {
+      float t[RPW], cm = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < RPW; k++) {
+        t[k] = x[k][q] + ur[k];
+        cm = fmaxf(cm, t[k]);
+      }
+      float cs = 0.f;
+      if (cm != -INFINITY) {
+#pragma unroll
+        for (int k = 0; k < RPW; k++) cs += sk_exp<FX>(t[k] - cm);
+      }
+      pm[wv][lane + 64 * q] = cm;
+      ps[wv][lane + 64 * q] = cs;
+    }
+    __syncthreads();
+    const long long q2 = __builtin_amdgcn_s_memtime();
+    unsigned long long* slot = a.ug + (size_t)(p * 2 + (it & 1)) * G * ld;
+    // two adjacent lanes per column: lane `half` merges waves 8 half .. 8 half + 7 and polls the
+    // peers h with (h & 1) == half; the pair's results are combined by a lane swap in an order
+    // both lanes (and every workgroup) share
+    if (tid < 2 * Cc) {
+      const int j = tid >> 1, half = tid & 1;
+      float M = -INFINITY;
+#pragma unroll
+      for (int w = 0; w < 8; w++) M = fmaxf(M, pm[8 * half + w][j]);
+      float S = 0.f;
+      if (M != -INFINITY) {
+#pragma unroll
+        for (int w = 0; w < 8; w++) S += ps[8 * half + w][j] * sk_exp<FX>(pm[8 * half + w][j] - M);
+      }
+      const float Mo = __shfl_xor(M, 1), So = __shfl_xor(S, 1);
+      const float MM = fmaxf(M, Mo);
+      float own = -INFINITY;
+      if (MM != -INFINITY) {
+        const float e0 = M == -INFINITY ? 0.f : S * sk_exp<FX>(M - MM), e1 = Mo == -INFINITY ? 0.f : So * sk_exp<FX>(Mo - MM);
+        own = logf(half ? e1 + e0 : e0 + e1) + MM;  // lane 0's term first in both lanes
+      }
+      if (!half)
+        __hip_atomic_store(slot + (size_t)g * ld + j, sk_granule(own, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      // all-gather of the G partials: every stale granule of this lane re-polled together
+      constexpr int GH = GM / 2;
+      float l[GH];
+      unsigned long long gv[GH];
+      unsigned pend = 0;
+#pragma unroll
+      for (int k = 0; k < GH; k++) {
+        const int h = 2 * k + half;
+        l[k] = -INFINITY;
+        if (h < G) {
+          if (h == g) l[k] = own;
+          else pend |= 1u << k;
+        }
+      }
+      bool to = a.inject && p == 0 && g == 0 && it == 0;  // fault injection (rspl_sg_debug_inject)
+      unsigned spins = 0;
+      while (pend && !to) {
+#pragma unroll
+        for (int k = 0; k < GH; k++)
+          if (pend >> k & 1)
+            gv[k] = __hip_atomic_load(slot + (size_t)(2 * k + half) * ld + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < GH; k++)
+          if ((pend >> k & 1) && (unsigned)(gv[k] >> 32) == tag) {
+            l[k] = __uint_as_float((unsigned)gv[k]);
+            pend &= ~(1u << k);
+          }
+        if (!pend) break;
+        if (++spins > a.spin_limit) { to = true; break; }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      if (to) flag[0] = 1;
+      float LM = -INFINITY;
+#pragma unroll
+      for (int k = 0; k < GH; k++) LM = fmaxf(LM, l[k]);
+      LM = fmaxf(LM, __shfl_xor(LM, 1));
+      float LS = 0.f;
+#pragma unroll
+      for (int k = 0; k < GH; k++)
+        if (l[k] != -INFINITY) LS += sk_exp<FX>(l[k] - LM);
+      const float LSo = __shfl_xor(LS, 1);
+      if (!half) vs[j] = (j < n ? norm : lnu_bin) - (logf(LS + LSo) + LM);
+    }
+    __syncthreads();
+    if (flag[0]) { failed = true; break; }
+#pragma unroll
+    for (int q = 0; q < kRbQ; q++) {
+      const int j = lane + 64 * q;
+      vr[q] = j < Cc ? vs[j] : 0.f;
+    }
+    const long long q3 = __builtin_amdgcn_s_memtime();
+    pr[0] += q1 - q0; pr[1] += q2 - q1; pr[2] += q3 - q2;
+  }
+  if (failed) {
+    if (tid == 0) __hip_atomic_store(a.err + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  if (a.probe && tid == 0) {
+#pragma unroll
+    for (int k = 0; k < 4; k++) atomicAdd(a.probe + k, (unsigned long long)pr[k]);
+    atomicAdd(a.probe + 4, (unsigned long long)a.iters);
+  }
+  // Z = ((couplings + u) + v) - norm (superglue.py:203, :219), own rows straight from registers
+  float* Z = a.Z + (size_t)p * ld * ld;
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int r = wv + 16 * k;
+    if (r >= nr) continue;
+#pragma unroll
+    for (int q = 0; q < kRbQ; q++) {
+      const int j = lane + 64 * q;
+      if (j < Cc) Z[(size_t)(r0 + r) * ld + j] = ((x[k][q] + ur[k]) + vr[q]) - norm;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // decode (super_glue.cpp:339-367).  Pass 1: row / column argmax (strict '<'
 // from -FLT_MAX: first maximum wins).  Pass 2: mutual check, exp, threshold.
 // ---------------------------------------------------------------------------
@@ -1659,9 +1874,35 @@ size_t sinkhorn_lds_bytes(int nmax, int G, bool slabs) {
   return sizeof(float) * (2 * ldp + 4 + (slabs ? 2 * per * ld : 0));
 }
 
+int sinkhorn_rb_rpw(int nmax, int G) {
+  const int ld = nmax + 1, rs = (ld + G - 1) / G;
+  if (ld > kRbQ * 64 || G < 1) return 0;
+  if (G <= 4 && rs <= 16 * 8) return 8;
+  if (G <= 8 && rs <= 16 * 4) return 4;
+  if (G <= 16 && rs <= 16 * 2) return 2;
+  if (G <= 32 && rs <= 16) return 1;
+  return 0;
+}
+
 hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   if (a.G < 1 || a.G > 1024) return hipErrorInvalidValue;
   dim3 grid(a.G, B);
+  if (a.rb) {  // row-block kernel: the workgroup count must match an instantiated (RPW, GM)
+    switch (sinkhorn_rb_rpw(a.nmax, a.G)) {
+#define RSPL_SK_RB(R, M)                                                                                      \
+  case R:                                                                                                     \
+    if (a.fx) hipExtLaunchKernelGGL((sinkhorn_rb_kernel<R, M, true>), grid, dim3(kSinkThreads), 0, s, t0, t1, 0, a); \
+    else hipExtLaunchKernelGGL((sinkhorn_rb_kernel<R, M, false>), grid, dim3(kSinkThreads), 0, s, t0, t1, 0, a);    \
+    break;
+      RSPL_SK_RB(8, 4)
+      RSPL_SK_RB(4, 8)
+      RSPL_SK_RB(2, 16)
+      RSPL_SK_RB(1, 32)
+#undef RSPL_SK_RB
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   const size_t full = sinkhorn_lds_bytes(a.nmax, a.G, true);
   if (full <= kSinkLdsMax) {
     static size_t attr = 0;

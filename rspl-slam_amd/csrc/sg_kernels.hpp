@@ -129,7 +129,7 @@ struct SinkArgs {
   const float* cpl;   // couplings [B][ld*ld]
   float* Z;           // [B][ld*ld]
   float* cplT;        // [B][ld*ld] transposed column slabs (scratch; only when the slabs exceed LDS)
-  unsigned long long* ug;  // [B][ld] tagged u granules {f32 bits, tag}
+  unsigned long long* ug;  // [B][ld] tagged u granules {f32 bits, tag}; row-block kernel: [B][2][G][ld] partial LSEs
   unsigned long long* vg;  // [B][ld] tagged v granules
   unsigned seq;       // per-call tag base (never 0; granules start zeroed)
   unsigned spin_limit;  // bounded polls per granule before the exchange is declared timed out
@@ -139,6 +139,8 @@ struct SinkArgs {
   const int* n0;
   const int* n1;
   int nmax, G, iters;
+  int rb;             // 1: row-block kernel (rows in registers, one exchange per iteration)
+  int fx;             // row-block kernel: v_exp_f32-based exp (RSPL_SG_FEXP=1; A/B knob)
 };
 
 struct DecodeArgs {
@@ -173,6 +175,8 @@ hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s, hipEvent_t t0 = nul
 hipError_t decode(const DecodeArgs& a, int B, hipStream_t s);
 // LDS bytes of one Sinkhorn workgroup (with or without the row / column slabs)
 size_t sinkhorn_lds_bytes(int nmax, int G, bool slabs);
+// rows per wave of the row-block Sinkhorn for G workgroups per pair (0: not supported)
+int sinkhorn_rb_rpw(int nmax, int G);
 constexpr size_t kSinkLdsMax = 150 * 1024;  // slab budget per workgroup (160 KB LDS per CU)
 
 }  // namespace sg

@@ -1,0 +1,12 @@
+set -o pipefail
+mkdir -p gpurun_out
+RSPL_SG_RB_G=16 RSPL_SG_FEXP=1 timeout -k 10 400 python -u -m pytest tests/test_gpu_sg.py tests/test_gpu_large.py -m gpu -x -q --timeout 200 --timeout-method thread > gpurun_out/sink_tests_fx.log 2>&1 && echo "fexp G=16 tests ok" || { echo "fexp tests FAILED"; grep -E "^E " gpurun_out/sink_tests_fx.log | head -12; }
+RSPL_SG_RB_G=16 RSPL_SG_FEXP=1 timeout -k 10 60 python -u tools/bench_sg.py --precision fp16 --iters 100 || exit 1
+for rep in 1 2 3; do
+  for V in slab 16 16fx; do
+    unset RSPL_SG_SINK RSPL_SG_RB_G RSPL_SG_FEXP
+    case $V in slab) export RSPL_SG_SINK=slab;; *fx) export RSPL_SG_RB_G=${V%fx} RSPL_SG_FEXP=1;; *) export RSPL_SG_RB_G=$V;; esac
+    timeout -k 10 200 python -u bench.py --no-cpu-baseline --single-precision --steps 200 > gpurun_out/sk_ab.json 2> gpurun_out/sk_ab.err || { echo "bench failed"; tail -20 gpurun_out/sk_ab.err; exit 1; }
+    python3 -c "import json,sys; d=json.load(open('gpurun_out/sk_ab.json')); s=d['stages_ms_per_step']; print(sys.argv[1], d['value'], 'sink', s['sg:sinkhorn'], 'ba', s['ba:wall'], 'roof', d['roofline']['frac'])" $V
+  done
+done
