@@ -271,6 +271,8 @@ static hipError_t run_sinkhorn(rspl_sg* s, const float* cpl, float* Zp, const in
   sk.nmax = s->nmax; sk.G = s->rbG ? s->rbG : s->G; sk.rb = s->rbG > 0; sk.iters = iters;
   static const bool fx = getenv("RSPL_SG_FEXP") && atoi(getenv("RSPL_SG_FEXP")) != 0;
   sk.fx = fx;
+  static const int sleep = getenv("RSPL_SG_SLEEP") ? std::max(0, atoi(getenv("RSPL_SG_SLEEP"))) : 1;
+  sk.sleep = sleep;
   if ((e = sg::sinkhorn(sk, B, st, t0, t1)) != hipSuccess) return e;
   if (probing) {  // debug: Sinkhorn cycles per workgroup-iteration by phase
     unsigned long long h[5];

@@ -1459,6 +1459,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
 #pragma unroll
   for (int q = 0; q < kRbQ; q++) vr[q] = 0.f;
   float ur[RPW];
+  const int nk = min(RPW, max(0, (nr - wv + 15) / 16));  // the wave's rows inside the slab
   // log_mu / log_nu (superglue.py:198-200), float arithmetic as the module
   const float fm = (float)m, fn = (float)n;
   const float norm = -logf(fm + fn);
@@ -1484,8 +1485,9 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
 #pragma unroll
       for (int k = 0; k < RPW; k++) {
         sm[k] = 0.f;
+        if (k < nk)  // wave-uniform: rows past the slab end cost nothing
 #pragma unroll
-        for (int q = 0; q < kRbQ; q++) sm[k] += sk_exp<FX>((x[k][q] + vr[q]) - mx[k]);
+          for (int q = 0; q < kRbQ; q++) sm[k] += sk_exp<FX>((x[k][q] + vr[q]) - mx[k]);
       }
 #pragma unroll
       for (int k = 0; k < RPW; k++) sm[k] = wave_sum_dpp(sm[k]);
@@ -1508,7 +1510,8 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
       float cs = 0.f;
       if (cm != -INFINITY) {
 #pragma unroll
-        for (int k = 0; k < RPW; k++) cs += sk_exp<FX>(t[k] - cm);
+        for (int k = 0; k < RPW; k++)
+          if (k < nk) cs += sk_exp<FX>(t[k] - cm);
       }
       pm[wv][lane + 64 * q] = cm;
       ps[wv][lane + 64 * q] = cs;
@@ -1567,7 +1570,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
           }
         if (!pend) break;
         if (++spins > a.spin_limit) { to = true; break; }
-        __builtin_amdgcn_s_sleep(1);
+        for (int z = 0; z < a.sleep; z++) __builtin_amdgcn_s_sleep(1);  // poll spacing (fabric traffic)
       }
       if (to) flag[0] = 1;
       float LM = -INFINITY;
