@@ -1,6 +1,7 @@
 #!/bin/bash
 # Alternating A/B of Sinkhorn workgroups per pair in the pipeline (frames/s, Sinkhorn, BA wall).
 set -o pipefail
+export RSPL_SG_SINK=slab  # these sweeps are of the slab kernel (RSPL_SG_SINK_G); the row-block kernel is the default
 mkdir -p gpurun_out
 for rep in 1 2 3; do
   for G in 32 48; do

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Sinkhorn workgroups per pair: standalone SuperGlue stage times and the pipeline line per G.
 set -o pipefail
+export RSPL_SG_SINK=slab  # these sweeps are of the slab kernel (RSPL_SG_SINK_G); the row-block kernel is the default
 mkdir -p gpurun_out
 for G in 32 48 64 100; do
   RSPL_SG_SINK_G=$G timeout -k 10 120 python -u tools/bench_sg.py --iters 30 2>&1 | tail -1 | sed "s/^/G=$G /" || exit 1
