@@ -269,7 +269,7 @@ static hipError_t run_sinkhorn(rspl_sg* s, const float* cpl, float* Zp, const in
   sk.spin_limit = s->spin_limit; sk.inject = s->inject;
   sk.err = s->d_err; sk.n0 = cn0; sk.n1 = cn1;
   sk.nmax = s->nmax; sk.G = s->rbG ? s->rbG : s->G; sk.rb = s->rbG > 0; sk.iters = iters;
-  static const bool fx = getenv("RSPL_SG_FEXP") && atoi(getenv("RSPL_SG_FEXP")) != 0;  // RSPL_SG_FEXP=1: v_exp_f32
+  static const bool fx = !getenv("RSPL_SG_FEXP") || atoi(getenv("RSPL_SG_FEXP")) != 0;  // RSPL_SG_FEXP=0: expf
   sk.fx = fx;
   static const int sleep = getenv("RSPL_SG_SLEEP") ? std::max(0, atoi(getenv("RSPL_SG_SLEEP"))) : 1;
   sk.sleep = sleep;
