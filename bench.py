@@ -5,6 +5,11 @@ Workload (BASELINE.json configs[2], "C3", all-keyframe worst case of SURVEY.md Â
 step is one stereo keyframe of a synthetic EuRoC-shaped stream:
   * SuperPoint on the rectified stereo pair (batch 2, 480x752, top-400),
   * SuperGlue/PointMatching on 2 pairs: left(t) vs left(t-1) keyframe, left(t) vs right(t),
+  * the line part of the stereo keyframe (Frame::AddRightFeatures, src/frame.cc:150-203): both
+    images' AssignPointsToLines, the stereo-match disparity filter and MatchLines on the GPU
+    (rspl_lines_stereo_device), fed by SuperPoint's device features and SuperGlue's device match
+    index of the left(t)-right(t) pair; the ~80 segments per image come from the host merge passes
+    (LineDetector after FLD, which runs on the reference's own line thread and is not rebuilt),
   * one local BA (LocalmapOptimization) of a C3-sized problem: 10 keyframes (1 fixed),
     ~4k points / ~10^4 point observations, 100 lines (synthetic, with ground truth).
 Inputs (images) are resident in HBM before timing.  BA is host-driven and runs on its own
@@ -144,7 +149,8 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
              "GFLOP per step (2 pairs x 2 images x 18 layers; fp16: 19 launches of the fused layer kernel, "
              "fp32: 4 GEMM/attention launches per layer)"),
             ("sg:sinkhorn", 2 * 2 * 100 * 4 * (N + 1) * (M + 1) / 1e9, "GB/s", HBM_PEAK_GBS, "hbm",
-             "sinkhorn_kernel<" if os.environ.get("RSPL_SG_SINK") == "slab" else "sinkhorn_rb_kernel",
+             {"slab": "sinkhorn_kernel<", "rb": "sinkhorn_rb_kernel"}.get(os.environ.get("RSPL_SG_SINK", "sc"),
+                                                                         "sinkhorn_sc_kernel"),
              True, "GB per launch (2 pairs, streamed model 2*iters*4*(N+1)(M+1))"),
             ("sp:nms", 2 * 2 * 4 * H * W / 1e9, "GB/s", HBM_PEAK_GBS, "hbm", "nms_kernel", True,
              "GB per launch (2 images, 2*4*H*W)"))
@@ -362,6 +368,22 @@ def main():
     st_post = capi.Stream(reserve_cus=rc, priority=prio["post"])  # SG's Sinkhorn + decode: overlaps the next GNN
     ev_sp = [capi.Event() for _ in range(3)]
     ev_sg = [capi.Event() for _ in range(3)]
+    # line part of each stereo keyframe (frame.cc:150-203): per replica frame a left / right line set
+    # (host LineDetector merge passes over FLD-like fragments, run once: the reference's line thread),
+    # resident in HBM like the images; the association runs on the post stream after the decode
+    lm = pkg.lines.LineMatcher(max_lines=512, max_points=max(K, 512), device=local)
+    line_sets = []
+    for i in range(NP):
+        sc = syn.line_scene(n_lines=80, n_points=16, seed=seeds["images"][i], width=W, height=H)
+        L0, L1 = pkg.lines.LineExtractor(sc["seg_left"]), pkg.lines.LineExtractor(sc["seg_right"])
+        d0, d1 = capi.DeviceBuffer(max(1, L0.nbytes)), capi.DeviceBuffer(max(1, L1.nbytes))
+        d0.upload(L0)
+        d1.upload(L1)
+        line_sets.append((d0, len(L0), d1, len(L1)))
+    n_lines_step = float(np.mean([2 * ls[1] for ls in line_sets]))
+    lines_out, lines_valid = capi.DeviceBuffer(512 * 4 * 8), capi.DeviceBuffer(512)
+    bf = pkg.synthetic.EUROC_BF
+    cam_limits = (bf / 10.0, bf / 0.1, 2.0)  # MinXDiff, MaxXDiff, MaxYDiff (camera.cc:21-22, euroc.yaml)
 
     def measure(precision):
         """One full timed run of the pipeline at `precision`; returns its measurements."""
@@ -395,6 +417,7 @@ def main():
 
         worker = threading.Thread(target=tracking_thread, daemon=True)
         worker.start()
+        line_timers = []  # HIP-event timers around the line association (post stream), timed steps only
 
         def ba_item(i):
             if shard:  # all ranks' BAs of step i, each solved jointly by every rank
@@ -431,12 +454,23 @@ def main():
             capi.memcpy_d2d(n1.offset(4), ccur.offset(4), 4, st_sg.handle)
             sg.infer_device(2, f0.ptr, n0.ptr, f1.ptr, n1.ptr, K, True, outs[0].ptr, outs[1].ptr, outs[2].ptr,
                             outs[3].ptr, st_sg.handle, post_stream=st_post.handle)
-            ev_sg[slot].record(st_post.handle)  # matches complete on the post stream
+            # stereo line association of frame t: SP's device records of (left, right) and SG's match
+            # index of pair 1 (left(t) -> right(t)), stream-ordered behind the decode
+            dl0, nl0, dl1, nl1 = line_sets[i % NP]
+            tm = line_timers[i - line_t0] if line_t0 is not None else None
+            if tm is not None:
+                tm.start(st_post.handle)
+            lm.stereo_lines_device(dl0.ptr, nl0, dl1.ptr, nl1, cur.ptr, K, ccur.ptr, outs[0].offset(K * 4),
+                                   cam_limits, lines_out.ptr, lines_valid.ptr, st_post.handle)
+            if tm is not None:
+                tm.stop(st_post.handle)
+            ev_sg[slot].record(st_post.handle)  # matches and lines complete on the post stream
             # keyframe i's local BA goes to the tracking thread (own high-priority stream) through a
             # 2-deep buffer, as the reference's feature thread blocks only while
             # _tracking_data_buffer.size() >= 2 (src/map_builder.cc:176)
             ba_q.put(ba_item(i))
 
+        line_t0 = None
         for i in range(args.warmup):
             step(i)
         ba_q.join()
@@ -449,6 +483,8 @@ def main():
         sg.profile(True)
         ba_ms.clear()
         ba_iters.clear()
+        line_timers[:] = [capi.Timer() for _ in range(args.steps)]
+        line_t0 = args.warmup
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(args.warmup + i)
@@ -465,11 +501,15 @@ def main():
         if dist:
             dist.barrier()
 
+        if lm.status():
+            raise SystemExit("bench: the stereo line association overflowed its point-line pairs")
+        lines_ms = float(np.mean([tm.elapsed_ms() for tm in line_timers])) if line_timers else None
+        line_t0 = None
         sp_ms, sp_calls = sp.stage_times()
         sg_ms, sg_calls = sg.stage_times()
         value = job_value(world, args.steps, elapsed)
         return {"value": value, "elapsed": elapsed, "sp": (sp_ms, sp_calls), "sg": (sg_ms, sg_calls),
-                "stages": (sp, sg), "ba_ms": list(ba_ms), "ba_iters": list(ba_iters)}
+                "stages": (sp, sg), "ba_ms": list(ba_ms), "ba_iters": list(ba_iters), "lines_ms": lines_ms}
 
     res = measure(args.precision)
     other = measure(precs[1]) if len(precs) > 1 else None  # the other precision, same run, for the record
@@ -515,7 +555,11 @@ def main():
         "stages_roofline": stages,
         "stages_ms_per_step": {**{f"sp:{n}": round(v / max(1, sp_calls), 4) for n, v in zip(sp.STAGES, sp_ms)},
                                **{f"sg:{n}": round(v / max(1, sg_calls), 4) for n, v in zip(sg.STAGES, sg_ms)},
+                               "lines:stereo": round(res["lines_ms"], 4) if res["lines_ms"] else None,
                                "ba:wall": round(ba_wall, 4) if ba_wall else None},
+        "lines": {"segments_per_step": n_lines_step, "keypoints_per_image": K,
+                  "note": "stereo line association per keyframe on the GPU (AssignPointsToLines x2, disparity "
+                          "filter, MatchLines; frame.cc:150-203), post stream, HIP-event time per step"},
         "ba": {"ms_per_call": round(ba_wall, 4) if ba_wall else None,
                "lm_iterations_per_call": ba_it,
                "us_per_lm_iteration": round(1e3 * ba_wall / ba_it, 2) if ba_wall and ba_it else None,

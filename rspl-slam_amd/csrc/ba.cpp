@@ -149,7 +149,7 @@ void carve(F& ar, rspl_ba* b) {
   take(b->lflag, nl);
   const size_t npairs = K * (K + 1) / 2, nchk = std::max<size_t>((NL + ba::kLmChunk - 1) / ba::kLmChunk, 1);
   take(b->lm_edges, E); take(b->lm_pose, E);
-  take(b->chunk, npairs * nchk * 48); take(b->pairfin, npairs * 48 + 8); take(b->pair_ctr, npairs);
+  take(b->chunk, npairs * nchk * 48); take(b->pairfin, npairs * 48 + 8); take(b->pair_ctr, npairs + 1);  // + the solve ticket
   take(b->red, 6 * K + kMaxRanks + 8);
   take(b->lmctl, 2);
   take(b->pp_cnt, npairs * nchk); take(b->pp_off, npairs * nchk + 1);
@@ -522,7 +522,7 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
           hipSuccess ||
       hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
       hipMemset(b->lflag, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
-      hipMemset(b->pair_ctr, 0, sizeof(unsigned) * std::max(b->maxK * (b->maxK + 1) / 2, 1)) != hipSuccess) {
+      hipMemset(b->pair_ctr, 0, sizeof(unsigned) * (b->maxK * (b->maxK + 1) / 2 + 1)) != hipSuccess) {
     set_error("BA stream / mailbox allocation failed");
     rspl_ba_destroy(b);
     return RSPL_E_DEVICE;
@@ -602,7 +602,7 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   if (hipStreamSynchronize(b->stream) != hipSuccess ||
       hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
       hipMemset(b->lflag, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
-      hipMemset(b->pair_ctr, 0, sizeof(unsigned) * std::max(b->maxK * (b->maxK + 1) / 2, 1)) != hipSuccess) {
+      hipMemset(b->pair_ctr, 0, sizeof(unsigned) * (b->maxK * (b->maxK + 1) / 2 + 1)) != hipSuccess) {
     set_error("%s; the BA stream could not be drained: recreate the handle", msg.c_str());
     return rc;
   }
@@ -842,6 +842,7 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   S.chunk = b->chunk;
   S.pairfin = b->pairfin;
   S.pair_ctr = b->pair_ctr;
+  S.solve_ctr = b->pair_ctr + b->maxK * (b->maxK + 1) / 2;
   S.shard_out = sh ? b->red + 6 * K + b->nranks : nullptr;
   S.pose_scale = !sh || b->rank == 0;
   // ---- phase 1: all edges, Huber ----

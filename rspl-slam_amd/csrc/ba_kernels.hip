@@ -1051,101 +1051,6 @@ __device__ __forceinline__ void prof_stamp(const Sys& S, int slot) {
   if (S.prof) S.prof[slot] = wall_clock64();
 }
 
-__global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active A, Sys S, double lambda, Lin Ls,
-                                                        Sys Ss) {
-  __shared__ double red[64 * 49];
-  if (S.lm) {  // device-side LM: damping and bank from the control
-    LmView v;
-    if (!lm_view(S, v)) return;
-    lambda = v.lambda;
-    if (v.cur) bank_lin(L, Ls, S, Ss);
-  }
-  // XCD-aware chunk order: workgroups go round-robin over the 8 XCDs (blockIdx % 8), so
-  // landmark range lb runs on XCD lb % 8 for every pose pair -- each XCD's L2 then holds only
-  // its ranges' records (~1/8 of them), which its ~k_g pose pairs per landmark re-read
-  const int lane = threadIdx.x;
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, rpx = (A.nchk + 7) >> 3;
-  const int lb = (slot % rpx) * 8 + xcd, pr0 = slot / rpx;
-  if (lb >= A.nchk || pr0 >= A.npairs) return;
-  const int c = pr0 * A.nchk + lb;
-  if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c);
-  const int pr = c / A.nchk;
-  const int beg = A.pp_off[c], end = A.pp_off[c + 1];
-  double acc[48];
-#pragma unroll
-  for (int v = 0; v < 48; v++) acc[v] = 0.0;
-  bool bad = false;
-  for (int k = beg + lane; k < end; k += 64) {
-    // every operand of the pair is requested before any arithmetic: one memory round trip
-    const int4 q = A.pp[k];
-    const int e1 = q.x, e2 = q.y, g = q.z;
-    const bool diag = e1 == e2;
-    const bool live = !(A.elevel && (A.elevel[e1] | A.elevel[e2]));  // else zero records: no contribution
-    double Hl[16], H1[24], H2[24], Hp[36], bpv[6], blv[4];
-    const double* hl = S.Hll + 16 * g;
-#pragma unroll
-    for (int i = 0; i < 16; i++) Hl[i] = hl[i];
-#pragma unroll
-    for (int i = 0; i < 24; i++) H1[i] = L.Hpl[24 * e1 + i];
-    if (diag) {
-#pragma unroll
-      for (int i = 0; i < 36; i++) Hp[i] = L.Hpp[36 * e1 + i];
-#pragma unroll
-      for (int i = 0; i < 6; i++) bpv[i] = L.bp[6 * e1 + i];
-#pragma unroll
-      for (int i = 0; i < 4; i++) blv[i] = S.bl[4 * g + i];
-#pragma unroll
-      for (int i = 0; i < 24; i++) H2[i] = H1[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < 24; i++) H2[i] = L.Hpl[24 * e2 + i];
-    }
-    if (!live) continue;
-    double D[16];
-    bad |= !lm_dinv(Hl, g < P.nq, lambda, D);
-    schur_pair(H1, H2, diag, Hp, bpv, blv, D, acc);
-  }
-  if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 1);
-  if (bad) atomicOr(S.fail, 1);
-#pragma unroll
-  for (int v = 0; v < 48; v++) red[lane * 49 + v] = acc[v];
-  __syncthreads();
-  // chunk partial, handed off write-through (sc1) to whichever chunk of this pose pair
-  // finishes last; that one sums the pair's chunks in chunk order (deterministic)
-  if (lane < 48) {  // 8 independent partial sums, combined in a fixed order
-    double p8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-    for (int l = 0; l < 64; l++) p8[l & 7] += red[l * 49 + lane];
-    const double s = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
-    __hip_atomic_store(S.chunk + 48 * c + lane, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int c0 = pr * A.nchk, c1 = c0 + A.nchk;
-  unsigned tk = 0;
-  if (lane == 0) tk = __hip_atomic_fetch_add(S.pair_ctr + pr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  tk = __shfl(tk, 0);
-  if (tk != (unsigned)(c1 - c0 - 1)) {
-    if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 2);
-    return;
-  }
-  if (lane == 0) __hip_atomic_store(S.pair_ctr + pr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  if (lane < 48) {
-    double s = 0;
-    for (int cb = c0; cb < c1; cb += 16) {  // 16 write-through loads in flight, summed in chunk order
-      double t[16];
-#pragma unroll
-      for (int u = 0; u < 16; u++)
-        t[u] = cb + u < c1 ? __hip_atomic_load(S.chunk + 48 * (cb + u) + lane, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT)
-                           : 0.0;
-#pragma unroll
-      for (int u = 0; u < 16; u++) s += t[u];
-    }
-    S.pairfin[48 * pr + lane] = s;
-  }
-  if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 3);
-}
-
 // larger systems, stage 2: one thread per (pose pair, entry) scatters the pair sums.
 //   S_ab = [a==b] lambda I + pair sum,  bp_a,  bs_a = bp_a - sum Y bl  (solved in place in x)
 __global__ __launch_bounds__(256) void pair_final_kernel(Active A, Sys S, double lambda) {
@@ -1407,6 +1312,269 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
   if (tid == 0) prof_stamp(S, 4);
 }
 
+
+// ---------------------------------------------------------------------------
+// Reduced camera system for n = 6K <= 60 (K <= kWaveSolveMaxK optimised poses: the C3 window)
+// in ONE wavefront, no workgroup barrier.  Lane i owns row i of S in registers (a[0, N): only
+// k <= i is meaningful) and the bordered rhs entry z_i.  Right-looking LDL^T column by column:
+//   pivot d_j = a_jj by readlane (every lane, uniform), l_ij = a_ij / d_j (lanes i > j),
+//   column j's unscaled entries w_kj broadcast through LDS, a_ik -= l_ij w_kj for every k > j
+//   (entries above the diagonal are never read), z_i -= l_ij z_j (forward substitution fused);
+// then y = D^-1 z and the backward substitution L^T x = y, column i of L read back from LDS into
+// registers so the dependent chain is readlane + fma per row.  Assembly reads the pose-pair sums
+// (pairfin) straight into the rows; the candidate poses and the pose part of the LM scale follow.
+// Returns false (nothing written) when the landmark inversion failed upstream or a pivot is <= 0.
+// ---------------------------------------------------------------------------
+constexpr int kWaveSolveMaxK = 10;
+
+__device__ __forceinline__ double readlane64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
+struct WaveSolveLds {
+  double col[2][64];  // column broadcast, double-buffered by step parity
+  double Lm[60][61];  // Lm[j][i] = l_ij (column j of L); odd stride
+  double xs[64];      // solution, for the pose lanes
+};
+
+// pose pair index of (c, a), c <= a, row-major upper triangle of K poses
+__device__ __forceinline__ int pair_index(int c, int a, int K) { return c * K - c * (c - 1) / 2 + (a - c); }
+
+template <int N>
+__device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys& S, double lambda, WaveSolveLds& w,
+                                           bool coherent) {
+  constexpr int K = N / 6;
+  const int lane = threadIdx.x & 63;
+  // candidate-pose operands first (independent of the solve): lane = pose
+  int pose_a = -1;
+  double Tp0[8];
+  if (lane < P.np) {
+    pose_a = A.pidx[lane];
+#pragma unroll
+    for (int k = 0; k < 8; k++) Tp0[k] = P.T[8 * lane + k];
+  }
+  const int pa = lane / 6, r = lane - 6 * pa;
+  const bool row = lane < N;
+  auto ld = [&](int idx) {
+    return coherent ? __hip_atomic_load(S.pairfin + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : S.pairfin[idx];
+  };
+  double a[N];
+  double z = 0.0, bpl = 0.0;
+  {
+    const int dg = 48 * pair_index(pa, pa, K);
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      const int c = k / 6, cc = k - 6 * (k / 6);
+      double v = 0.0;
+      if (row && k <= lane) {
+        if (c == pa) v = ld(dg + r * 6 + cc);
+        else v = ld(48 * pair_index(c, pa, K) + cc * 6 + r);
+      }
+      a[k] = v;
+    }
+    if (row) {
+      bpl = ld(dg + 36 + r);
+      z = bpl - ld(dg + 42 + r);
+    }
+  }
+  const int failed = coherent ? __hip_atomic_load(S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *S.fail;
+  if (failed) return;  // uniform: a landmark block failed to invert
+  // damping on the diagonal (a[k] with k == lane: select, static register index)
+#pragma unroll
+  for (int k = 0; k < N; k++) a[k] += (k == lane) ? lambda : 0.0;
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < N; j++) {
+    const double dj = readlane64(a[j], j);
+    ok = ok && dj > 0.0;
+    const double rj = rcp64(dj);
+    const double wij = a[j];
+    const double l = lane > j ? wij * rj : 0.0;
+    w.col[j & 1][lane] = wij;
+    w.Lm[j][lane] = l;
+    const double zj = readlane64(z, j);
+    z = fma(-l, zj, z);
+    wave_sync();
+#pragma unroll
+    for (int k = j + 1; k < N; k++) a[k] = fma(-l, w.col[j & 1][k], a[k]);
+  }
+  if (!ok) {
+    if (lane == 0) atomicOr(S.fail, 1);
+    return;
+  }
+  // y = D^-1 z; backward L^T x = y (lane i: y_i -= L_ki x_k for k > i, k descending)
+  double y = 0.0;
+#pragma unroll
+  for (int k = 0; k < N; k++)
+    if (k == lane) y = z * rcp64(a[k]);
+  double lt[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) lt[k] = row && k > lane ? w.Lm[lane][k] : 0.0;
+#pragma unroll
+  for (int k = N - 1; k >= 0; k--) {
+    const double xk = readlane64(y, k);
+    y = fma(-lt[k], xk, y);  // lt[k] == 0 for k <= lane
+  }
+  const double x = y;
+  if (row) S.x[lane] = x;
+  w.xs[lane] = x;
+  wave_sync();
+  // candidate poses (lane = pose; np <= 64): T <- exp(xp) T, fixed poses copied (ping-pong),
+  // and the pose part of the LM scale x.(lambda x + bp)
+  double sc = row ? x * (lambda * x + bpl) : 0.0;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
+  if (lane < P.np) {
+    double* Tq = P.Tn + 8 * lane;
+    if (pose_a >= 0) {
+      double xp[6];
+#pragma unroll
+      for (int q = 0; q < 6; q++) xp[q] = w.xs[6 * pose_a + q];
+      const SE3 rr = se3_mul(se3_exp(xp), load_T(Tp0));
+      for (int k = 0; k < 4; k++) Tq[k] = rr.q[k];
+      for (int k = 0; k < 3; k++) Tq[4 + k] = rr.t[k];
+      Tq[7] = 0;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++) Tq[k] = Tp0[k];
+    }
+  }
+  if (lane == 0) S.out[4] = sc;
+}
+
+// standalone single-wave solve (sharded path: after the pairfin all-reduce)
+template <int N>
+__global__ __launch_bounds__(64) void schur_wave_kernel(Problem P, Active A, Sys S, double lambda) {
+  __shared__ WaveSolveLds w;
+  if (S.lm) {
+    LmView v;
+    if (!lm_view(S, v)) return;
+    lambda = v.lambda;
+    if (v.cur) bank_state(P);
+  }
+  solve_wave<N>(P, A, S, lambda, w, false);
+}
+
+// N > 0 (6K <= 60): the pose pair finished last (a second ticket over the pairs) solves the reduced
+// system in the same wave (solve_wave<N>), so the trial needs no separate solve launch.
+template <int N>
+__global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active A, Sys S, double lambda, Lin Ls,
+                                                        Sys Ss) {
+  constexpr int kRedLen = 64 * 49, kSolveLen = (int)(sizeof(WaveSolveLds) / sizeof(double));
+  __shared__ double smem[N > 0 && kSolveLen > kRedLen ? kSolveLen : kRedLen];
+  double* red = smem;
+  if (S.lm) {  // device-side LM: damping and bank from the control
+    LmView v;
+    if (!lm_view(S, v)) return;
+    lambda = v.lambda;
+    if (v.cur) {
+      bank_lin(L, Ls, S, Ss);
+      if (N > 0) bank_state(P);
+    }
+  }
+  // XCD-aware chunk order: workgroups go round-robin over the 8 XCDs (blockIdx % 8), so
+  // landmark range lb runs on XCD lb % 8 for every pose pair -- each XCD's L2 then holds only
+  // its ranges' records (~1/8 of them), which its ~k_g pose pairs per landmark re-read
+  const int lane = threadIdx.x;
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, rpx = (A.nchk + 7) >> 3;
+  const int lb = (slot % rpx) * 8 + xcd, pr0 = slot / rpx;
+  if (lb >= A.nchk || pr0 >= A.npairs) return;
+  const int c = pr0 * A.nchk + lb;
+  if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c);
+  const int pr = c / A.nchk;
+  const int beg = A.pp_off[c], end = A.pp_off[c + 1];
+  double acc[48];
+#pragma unroll
+  for (int v = 0; v < 48; v++) acc[v] = 0.0;
+  bool bad = false;
+  for (int k = beg + lane; k < end; k += 64) {
+    // every operand of the pair is requested before any arithmetic: one memory round trip
+    const int4 q = A.pp[k];
+    const int e1 = q.x, e2 = q.y, g = q.z;
+    const bool diag = e1 == e2;
+    const bool live = !(A.elevel && (A.elevel[e1] | A.elevel[e2]));  // else zero records: no contribution
+    double Hl[16], H1[24], H2[24], Hp[36], bpv[6], blv[4];
+    const double* hl = S.Hll + 16 * g;
+#pragma unroll
+    for (int i = 0; i < 16; i++) Hl[i] = hl[i];
+#pragma unroll
+    for (int i = 0; i < 24; i++) H1[i] = L.Hpl[24 * e1 + i];
+    if (diag) {
+#pragma unroll
+      for (int i = 0; i < 36; i++) Hp[i] = L.Hpp[36 * e1 + i];
+#pragma unroll
+      for (int i = 0; i < 6; i++) bpv[i] = L.bp[6 * e1 + i];
+#pragma unroll
+      for (int i = 0; i < 4; i++) blv[i] = S.bl[4 * g + i];
+#pragma unroll
+      for (int i = 0; i < 24; i++) H2[i] = H1[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < 24; i++) H2[i] = L.Hpl[24 * e2 + i];
+    }
+    if (!live) continue;
+    double D[16];
+    bad |= !lm_dinv(Hl, g < P.nq, lambda, D);
+    schur_pair(H1, H2, diag, Hp, bpv, blv, D, acc);
+  }
+  if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 1);
+  if (bad) atomicOr(S.fail, 1);
+#pragma unroll
+  for (int v = 0; v < 48; v++) red[lane * 49 + v] = acc[v];
+  __syncthreads();
+  // chunk partial, handed off write-through (sc1) to whichever chunk of this pose pair
+  // finishes last; that one sums the pair's chunks in chunk order (deterministic)
+  if (lane < 48) {  // 8 independent partial sums, combined in a fixed order
+    double p8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int l = 0; l < 64; l++) p8[l & 7] += red[l * 49 + lane];
+    const double s = ((p8[0] + p8[1]) + (p8[2] + p8[3])) + ((p8[4] + p8[5]) + (p8[6] + p8[7]));
+    __hip_atomic_store(S.chunk + 48 * c + lane, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int c0 = pr * A.nchk, c1 = c0 + A.nchk;
+  unsigned tk = 0;
+  if (lane == 0) tk = __hip_atomic_fetch_add(S.pair_ctr + pr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  tk = __shfl(tk, 0);
+  if (tk != (unsigned)(c1 - c0 - 1)) {
+    if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 2);
+    return;
+  }
+  if (lane == 0) __hip_atomic_store(S.pair_ctr + pr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (lane < 48) {
+    double s = 0;
+    for (int cb = c0; cb < c1; cb += 16) {  // 16 write-through loads in flight, summed in chunk order
+      double t[16];
+#pragma unroll
+      for (int u = 0; u < 16; u++)
+        t[u] = cb + u < c1 ? __hip_atomic_load(S.chunk + 48 * (cb + u) + lane, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT)
+                           : 0.0;
+#pragma unroll
+      for (int u = 0; u < 16; u++) s += t[u];
+    }
+    if (N > 0) __hip_atomic_store(S.pairfin + 48 * pr + lane, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else S.pairfin[48 * pr + lane] = s;
+  }
+  if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 3);
+  if constexpr (N > 0) {
+    // the last pose pair to finish solves: its wave has every pair sum (write-through) behind a
+    // second ticket; the counter is re-armed for the next trial
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    unsigned tp = 0;
+    if (lane == 0) tp = __hip_atomic_fetch_add(S.solve_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    tp = __shfl(tp, 0);
+    if (tp != (unsigned)(A.npairs - 1)) return;
+    if (lane == 0) __hip_atomic_store(S.solve_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();  // red[] is dead: the LDS becomes the solver's
+    if (lane == 0) prof_stamp(S, 0);
+    solve_wave<N>(P, A, S, lambda, *reinterpret_cast<WaveSolveLds*>(smem), true);
+    if (lane == 0) prof_stamp(S, 4);
+  }
+}
 
 // larger systems: one workgroup on global memory
 
@@ -1895,6 +2063,7 @@ __global__ __launch_bounds__(256) void shard_finish_kernel(Problem P, int E, con
 
 int shard_red_len(int K, int nranks) { return 6 * K + nranks + 3; }
 bool fast_path(int K) { return 6 * K > 0 && 6 * K <= kCholLdsMax; }
+bool wave_path(int K) { return K > 0 && K <= kWaveSolveMaxK; }
 
 // ---------------------------------------------------------------------------
 int errors_blocks(int Ea) { return Ea > 0 ? (Ea + 255) / 256 : 1; }
@@ -1941,16 +2110,43 @@ hipError_t ensure_schur_attr() {
 // pair_chunk grid: 8 XCD lanes x (landmark ranges per XCD) x pose pairs (idle slots exit)
 static int pair_chunk_blocks(const Active& A) { return 8 * ((A.nchk + 7) / 8) * A.npairs; }
 
+// Schur chunks; with fused = true (wave path) the last pose pair also solves (solve_wave<6K>)
+static void launch_chunks(const Problem& P, const Lin& L, const Active& A, const Sys& S, double lambda, const Lin& Ls,
+                          const Sys& Ss, bool fused, hipStream_t s) {
+  const dim3 g(pair_chunk_blocks(A)), b(64);
+  switch (fused ? A.K : 0) {
+#define RSPL_CHUNK_CASE(k) \
+  case k: hipLaunchKernelGGL(pair_chunk_kernel<6 * k>, g, b, 0, s, P, L, A, S, lambda, Ls, Ss); break;
+    RSPL_CHUNK_CASE(1) RSPL_CHUNK_CASE(2) RSPL_CHUNK_CASE(3) RSPL_CHUNK_CASE(4) RSPL_CHUNK_CASE(5)
+    RSPL_CHUNK_CASE(6) RSPL_CHUNK_CASE(7) RSPL_CHUNK_CASE(8) RSPL_CHUNK_CASE(9) RSPL_CHUNK_CASE(10)
+#undef RSPL_CHUNK_CASE
+    default: hipLaunchKernelGGL(pair_chunk_kernel<0>, g, b, 0, s, P, L, A, S, lambda, Ls, Ss); break;
+  }
+}
+
+static void launch_wave_solve(const Problem& P, const Active& A, const Sys& S, double lambda, hipStream_t s) {
+  switch (A.K) {
+#define RSPL_SOLVE_CASE(k) \
+  case k: hipLaunchKernelGGL(schur_wave_kernel<6 * k>, dim3(1), dim3(64), 0, s, P, A, S, lambda); break;
+    RSPL_SOLVE_CASE(1) RSPL_SOLVE_CASE(2) RSPL_SOLVE_CASE(3) RSPL_SOLVE_CASE(4) RSPL_SOLVE_CASE(5)
+    RSPL_SOLVE_CASE(6) RSPL_SOLVE_CASE(7) RSPL_SOLVE_CASE(8) RSPL_SOLVE_CASE(9) RSPL_SOLVE_CASE(10)
+#undef RSPL_SOLVE_CASE
+    default: break;
+  }
+}
+
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
                  hipStream_t s, const Spec* spec, bool* fused) {
   *fused = false;
-  if (A.npairs * A.nchk > 0)
-    hipLaunchKernelGGL(pair_chunk_kernel, dim3(pair_chunk_blocks(A)), dim3(64), 0, s, P, L, A, S, lambda, L, S);
+  const bool wave = wave_path(A.K);
+  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, lambda, L, S, wave, s);
   const int n = 6 * A.K;
   if (fast_path(A.K)) {
-    hipError_t e = ensure_schur_attr();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
+    if (!wave) {
+      hipError_t e = ensure_schur_attr();
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
+    }
     const int nbu = update_errors_blocks(A);
     if (spec) {
       const int nbl = A.n_lblk;
@@ -1978,13 +2174,14 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
 hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq, hipStream_t s,
                      const Spec& spec) {
   if (!S.lm || !fast_path(A.K)) return hipErrorInvalidValue;
-  if (A.npairs * A.nchk > 0)
-    hipLaunchKernelGGL(pair_chunk_kernel, dim3(pair_chunk_blocks(A)), dim3(64), 0, s, P, L, A, S, 0.0, spec.Ls,
-                       spec.Ss);
-  hipError_t e = ensure_schur_attr();
-  if (e != hipSuccess) return e;
-  const int n = 6 * A.K;
-  hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, 0.0);
+  const bool wave = wave_path(A.K);
+  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, 0.0, spec.Ls, spec.Ss, wave, s);
+  if (!wave) {
+    hipError_t e = ensure_schur_attr();
+    if (e != hipSuccess) return e;
+    const int n = 6 * A.K;
+    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, 0.0);
+  }
   const int nbu = update_errors_blocks(A), nbl = A.n_lblk;
   hipLaunchKernelGGL(update_errors_kernel<true>, dim3(nbu + nbl), dim3(256), 0, s, P, L, A, S, 0.0, seq, spec.Ls,
                      spec.Ss, nbu, spec.lflag, spec.tag);
@@ -2027,8 +2224,7 @@ hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8
 }
 
 hipError_t trial_chunks(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, hipStream_t s) {
-  if (A.npairs * A.nchk > 0)
-    hipLaunchKernelGGL(pair_chunk_kernel, dim3(pair_chunk_blocks(A)), dim3(64), 0, s, P, L, A, S, lambda, L, S);
+  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, lambda, L, S, false, s);
   hipLaunchKernelGGL(shard_fail_stage_kernel, dim3(1), dim3(1), 0, s, S, S.pairfin + (size_t)A.npairs * 48);
   return hipGetLastError();
 }
@@ -2037,9 +2233,13 @@ hipError_t trial_solve(const Problem& P, const Lin& L, const Active& A, Sys& S, 
   hipLaunchKernelGGL(shard_fail_adopt_kernel, dim3(1), dim3(1), 0, s, S, S.pairfin + (size_t)A.npairs * 48);
   const int n = 6 * A.K;
   if (fast_path(A.K)) {
-    hipError_t e = ensure_schur_attr();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
+    if (wave_path(A.K)) {
+      launch_wave_solve(P, A, S, lambda, s);
+    } else {
+      hipError_t e = ensure_schur_attr();
+      if (e != hipSuccess) return e;
+      hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
+    }
     hipLaunchKernelGGL(update_errors_kernel<false>, dim3(update_errors_blocks(A)), dim3(256), 0, s, P, L, A, S, lambda,
                        0ull, L, S, 0, nullptr, 0u);
     return hipGetLastError();

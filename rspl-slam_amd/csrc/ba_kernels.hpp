@@ -94,6 +94,7 @@ struct Sys {
   double* chunk;         // [npairs * nchk][48] Schur chunk partials
   double* pairfin;       // [npairs][48] per-pose-pair sums of the chunk partials
   unsigned* pair_ctr;    // [npairs] chunk tickets (re-armed to 0 by the last chunk)
+  unsigned* solve_ctr;   // [1] pose-pair ticket of the fused single-wave solve (re-armed by the solver)
   double* partial;       // [>= error blocks] chi2 partials
   double* partial2;      // [>= update blocks] scale partials
   double* out;           // [8]: 0 chi2, 1 scale, 2 maxdiag, 3 fail
@@ -181,6 +182,7 @@ hipError_t shard_finish(const Problem& P, int E_global, const double* G, uint8_t
                         double* Lh, Sys& S, unsigned long long seq, hipStream_t s);
 int shard_red_len(int K, int nranks);  // 6K + nranks + 3
 bool fast_path(int K);                 // the packed-LDS Schur/LDL^T path holds 6K
+bool wave_path(int K);                 // the single-wave LDL^T (fused into the Schur chunks) holds 6K
 int update_blocks(const Problem& P);
 int errors_blocks(int Ea);
 int update_errors_blocks(const Active& A);

@@ -43,6 +43,7 @@ struct rspl_sg {
   int ldv = 0;  // token stride of Vth (nmax rounded up to the 32-key attention tile; zero padded)
   unsigned long long *ug, *vg;  // Sinkhorn u / v exchange granules [B][ld] (row-block: ug = [B][2][rbG][ld])
   int rbG = 0;                  // row-block Sinkhorn workgroups per pair (0: slab kernel)
+  bool sink_sc = false;         // with rbG: the scaling-form kernel (default), else the log-domain row-block kernel
   float* cplT = nullptr;        // transposed column slabs when they exceed LDS [B][ld*ld]
   bool sink_scratch = false;
   unsigned* err = nullptr;      // [B] sticky Sinkhorn timeout flags, host-mapped (rspl_sg_status)
@@ -268,11 +269,9 @@ static hipError_t run_sinkhorn(rspl_sg* s, const float* cpl, float* Zp, const in
   sk.seq = s->sk_seq = (s->sk_seq % 0xFFFFFu) + 1;
   sk.spin_limit = s->spin_limit; sk.inject = s->inject;
   sk.err = s->d_err; sk.n0 = cn0; sk.n1 = cn1;
-  sk.nmax = s->nmax; sk.G = s->rbG ? s->rbG : s->G; sk.rb = s->rbG > 0; sk.iters = iters;
-  static const bool fx = !getenv("RSPL_SG_FEXP") || atoi(getenv("RSPL_SG_FEXP")) != 0;  // RSPL_SG_FEXP=0: expf
-  sk.fx = fx;
-  static const int sleep = getenv("RSPL_SG_SLEEP") ? std::max(0, atoi(getenv("RSPL_SG_SLEEP"))) : 1;
-  sk.sleep = sleep;
+  sk.nmax = s->nmax; sk.G = s->rbG ? s->rbG : s->G; sk.rb = s->rbG > 0; sk.sc = s->sink_sc; sk.iters = iters;
+  sk.fx = 1;
+  sk.sleep = 1;
   if ((e = sg::sinkhorn(sk, B, st, t0, t1)) != hipSuccess) return e;
   if (probing) {  // debug: Sinkhorn cycles per workgroup-iteration by phase
     unsigned long long h[5];
@@ -291,6 +290,8 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
   RSPL_CHECK_ARG(cfg->precision == RSPL_PREC_FP32 || cfg->precision == RSPL_PREC_FP16,
                  "precision must be RSPL_PREC_FP32 or RSPL_PREC_FP16");
   RSPL_CHECK_ARG(cfg->image_width > 0 && cfg->image_height > 0, "image size must be positive");
+  // the Sinkhorn exchange tag is (call sequence << 12) | (iteration + 1)
+  RSPL_CHECK_ARG(cfg->sinkhorn_iterations < 4096, "sinkhorn_iterations must be < 4096");
   *out = nullptr;
   std::vector<Tensor> ts;
   int rc = load_blob(weights_path, ts);
@@ -315,16 +316,21 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
     constexpr int kRows = 9;  // 45 workgroups per pair at N = 400 (tools/gpu_sink_ab.sh: 32 vs 48)
     int G = std::max(1, (s->ld + kRows - 1) / kRows);
     while (G < s->ld && sg::sinkhorn_lds_bytes(s->nmax, G, true) > sg::kSinkLdsMax) G++;
-    if (const char* e = getenv("RSPL_SG_SINK_G")) G = std::max(1, atoi(e));  // tuning knob
+    if (const char* e = getenv("RSPL_SG_SINK_G"); e && getenv("RSPL_SG_SINK") &&
+        std::string(getenv("RSPL_SG_SINK")) == "slab")
+      G = std::max(1, atoi(e));
     G = std::min(G, std::max(1, ncu / s->B));
     s->G = G;
     s->sink_scratch = sg::sinkhorn_lds_bytes(s->nmax, G, true) > sg::kSinkLdsMax;
-    // row-block kernel (rows in registers, one exchange per iteration) when nmax + 1 <= 448;
-    // RSPL_SG_SINK=slab keeps the slab kernel, RSPL_SG_RB_G picks its workgroups per pair
+    // nmax + 1 <= 448: rows in registers, one exchange per iteration -- the scaling-form kernel
+    // (default, 8 workgroups per pair) or the log-domain row-block kernel (RSPL_SG_SINK=rb, 16);
+    // RSPL_SG_SINK=slab keeps the slab kernel; RSPL_SG_SINK_G sets the workgroups per pair
     const char* sk = getenv("RSPL_SG_SINK");
-    if (!(sk && std::string(sk) == "slab")) {
-      int rg = 16;
-      if (const char* e = getenv("RSPL_SG_RB_G")) rg = atoi(e);
+    const std::string kind = sk ? sk : "sc";
+    if (kind != "slab") {
+      int rg = kind == "rb" ? 16 : 8;
+      if (const char* e = getenv("RSPL_SG_SINK_G")) rg = std::max(1, atoi(e));
+      s->sink_sc = kind != "rb";
       rg = std::min(rg, std::max(1, ncu / s->B));
       while (rg <= 32 && rg * s->B <= ncu && !sg::sinkhorn_rb_rpw(s->nmax, rg)) rg++;
       if (rg * s->B <= ncu && sg::sinkhorn_rb_rpw(s->nmax, rg)) s->rbG = rg;
@@ -715,7 +721,8 @@ extern "C" int rspl_sg_debug_inject(rspl_sg* s, int inject, unsigned spin_limit)
 extern "C" int rspl_sg_debug_sinkhorn(rspl_sg* s, const float* scores, int n0, int n1, float alpha, int iters,
                                       float* Z) {
   RSPL_CHECK_ARG(s && scores && Z, "rspl_sg_debug_sinkhorn: NULL argument");
-  RSPL_CHECK_ARG(n0 >= 1 && n1 >= 1 && n0 <= s->nmax && n1 <= s->nmax && iters >= 0, "bad shape");
+  RSPL_CHECK_ARG(n0 >= 1 && n1 >= 1 && n0 <= s->nmax && n1 <= s->nmax && iters >= 0 && iters < 4096,
+                 "bad shape or iteration count (< 4096)");
   const size_t ld = s->ld;
   hipStream_t st = s->stream;
   RSPL_HIP(hipStreamSynchronize(st));

@@ -1423,7 +1423,7 @@ __device__ __forceinline__ float sk_exp(float d) {
   if constexpr (!FX) {
     return expf(d);
   } else {
-    d = fmaxf(d, -150.f);  // -inf (masked rows / columns) -> exactly 0 below, not NaN
+    d = d < -150.f ? -150.f : d;  // -inf (masked rows / columns) -> exactly 0 below; NaN stays NaN
     const float a = d * 1.44269504f;
     const float e = fmaf(d, 1.44269504f, -a) + d * 1.9259630e-8f;
     const float r = __builtin_amdgcn_exp2f(a);
@@ -1613,6 +1613,246 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
     for (int q = 0; q < kRbQ; q++) {
       const int j = lane + 64 * q;
       if (j < Cc) Z[(size_t)(r0 + r) * ld + j] = ((x[k][q] + ur[k]) + vr[q]) - norm;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Scaling-form Sinkhorn (the default for nmax + 1 <= 448): the same iterations as
+// log_sinkhorn_iterations (superglue.py:176-183) written on the scalings U = exp(u - a),
+// V = exp(v - b) of absorbed log potentials a, b (stabilised Sinkhorn):
+//   K_ij = exp(C_ij + a_i + b_j)  (registers),   U_i = mu_i / sum_j K_ij V_j,
+//   V_j = nu_j / sum_i K_ij U_i,   u = a + log U,   v = b + log V,
+// so an iteration is two mat-vecs of register-resident K -- no exp per element.  Iteration 0's
+// row pass runs in the log domain exactly as the module (max-shifted LSE, v = 0) and seeds a = u,
+// which bounds K by mu (<= 1).  A scaling that leaves [2^-60, 2^60] is absorbed into a / b and K
+// is recomputed from C: rows per workgroup (a is workgroup-local), columns on every workgroup
+// alike (V is bit-identical everywhere, so every workgroup decides the same).  Layout, exchange
+// and determinism as the row-block kernel: G workgroups per pair hold whole rows (wave w rows
+// w + 16 k, lane L columns L + 64 q), the row pass is wave-local, the column sums go through LDS
+// across waves and ONE all-gather of per-column partial sums across workgroups per iteration,
+// merged in the same order everywhere.  Z = ((C + u) + v) - norm from C re-read at the end.
+// ---------------------------------------------------------------------------
+// orders this wave's LDS writes before its later LDS reads
+__device__ __forceinline__ void wave_barrier_lds() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+template <int RPW, int GM>
+__global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
+  __shared__ float ps[16][kRbQ * 64];   // per-wave column partial sums
+  __shared__ float vs[kRbQ * 64];       // merged V
+  __shared__ int flag[4];               // 0: exchange timeout, 1: column absorb, 2 + (it & 1): row absorb
+  __shared__ float as[16 * RPW];        // absorbed row potentials a (row wv + 16 k), read on absorption / at the end
+  __shared__ float bs[kRbQ * 64];       // absorbed column potentials b (identical on every workgroup)
+  const int p = blockIdx.y, g = blockIdx.x, G = gridDim.x;
+  const int m = a.n0[p], n = a.n1[p];
+  if (m <= 0 || n <= 0) return;
+  const int R = m + 1, Cc = n + 1, ld = a.nmax + 1;
+  const int rs = (R + G - 1) / G;
+  const int r0 = min(R, g * rs), nr = min(R, r0 + rs) - r0;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* Cg = a.cpl + (size_t)p * ld * ld;
+  const int nk = min(RPW, max(0, (nr - wv + 15) / 16));  // the wave's rows inside the slab
+  float x[RPW][kRbQ];
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int r = wv + 16 * k;
+#pragma unroll
+    for (int q = 0; q < kRbQ; q++) {
+      const int j = lane + 64 * q;
+      x[k][q] = (r < nr && j < Cc) ? Cg[(size_t)(r0 + r) * ld + j] : -INFINITY;
+    }
+  }
+  // log_mu / log_nu (superglue.py:198-200), float arithmetic as the module; mu / nu = exp of them
+  const float fm = (float)m, fn = (float)n;
+  const float norm = -logf(fm + fn);
+  const float lmu_bin = logf(fn) + norm, lnu_bin = logf(fm) + norm;
+  const float mu_in = expf(norm), mu_bin = expf(lmu_bin), nu_bin = expf(lnu_bin);
+  constexpr float kLo = 8.6736174e-19f, kHi = 1.1529215e18f;  // 2^-60, 2^60
+  if (tid < 4) flag[tid] = 0;
+  // iteration 0, row pass in the log domain (v = 0): a = u
+  float ur[RPW];
+  {
+    float mx[RPW], sm[RPW];
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      mx[k] = x[k][0];
+#pragma unroll
+      for (int q = 1; q < kRbQ; q++) mx[k] = fmaxf(mx[k], x[k][q]);
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; k++) mx[k] = wave_max_dpp(mx[k]);
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      sm[k] = 0.f;
+      if (k < nk)
+#pragma unroll
+        for (int q = 0; q < kRbQ; q++) sm[k] += sk_exp<true>(x[k][q] - mx[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; k++) sm[k] = wave_sum_dpp(sm[k]);
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      const int r = wv + 16 * k;
+      if (lane == 0) as[wv + 16 * k] = r < nr ? ((r0 + r) < m ? norm : lmu_bin) - (logf(sm[k]) + mx[k]) : 0.f;
+      ur[k] = 1.f;
+    }
+  }
+  float vr[kRbQ];
+#pragma unroll
+  for (int q = 0; q < kRbQ; q++) {
+    bs[lane + 64 * q] = 0.f;  // every wave writes the same zeros
+    vr[q] = 1.f;
+  }
+  wave_barrier_lds();
+  // K = exp(C + a + b), masked entries exactly 0
+  auto build_k = [&](bool reload) {
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      const int r = wv + 16 * k;
+#pragma unroll
+      for (int q = 0; q < kRbQ; q++) {
+        const int j = lane + 64 * q;
+        const bool in = r < nr && j < Cc;
+        const float c = reload ? (in ? Cg[(size_t)(r0 + r) * ld + j] : 0.f) : x[k][q];
+        x[k][q] = in ? sk_exp<true>((c + as[wv + 16 * k]) + bs[j]) : 0.f;
+      }
+    }
+  };
+  build_k(false);
+  __syncthreads();
+  bool failed = false;
+  for (int it = 0; it < a.iters; it++) {
+    const unsigned tag = (a.seq << 12) | (unsigned)(it + 1);
+    if (it > 0) {  // row pass: U_i = mu_i / sum_j K_ij V_j (wave-local)
+      float sm[RPW];
+#pragma unroll
+      for (int k = 0; k < RPW; k++) {
+        sm[k] = 0.f;
+        if (k < nk)
+#pragma unroll
+          for (int q = 0; q < kRbQ; q++) sm[k] = fmaf(x[k][q], vr[q], sm[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < RPW; k++) sm[k] = wave_sum_dpp(sm[k]);
+      bool out = false;
+#pragma unroll
+      for (int k = 0; k < RPW; k++) {
+        const int r = wv + 16 * k;
+        ur[k] = r < nr ? ((r0 + r) < m ? mu_in : mu_bin) / sm[k] : 0.f;
+        out |= r < nr && !(ur[k] >= kLo && ur[k] <= kHi);
+      }
+      if (out && lane == 0) flag[2 + (it & 1)] = 1;
+    }
+    // column partials over the wave's rows, then over the 16 waves
+#pragma unroll
+    for (int q = 0; q < kRbQ; q++) {
+      float cs = 0.f;
+#pragma unroll
+      for (int k = 0; k < RPW; k++)
+        if (k < nk) cs = fmaf(x[k][q], ur[k], cs);
+      ps[wv][lane + 64 * q] = cs;
+    }
+    __syncthreads();
+    if (tid == 0) flag[2 + ((it + 1) & 1)] = 0;  // next iteration's row flag (its readers are past)
+    unsigned long long* slot = a.ug + (size_t)(p * 2 + (it & 1)) * G * ld;
+    // two adjacent lanes per column: lane `half` sums waves 8 half .. 8 half + 7 and polls the
+    // peers h with (h & 1) == half; both lanes form the same total (fp addition commutes)
+    if (tid < 2 * Cc) {
+      const int j = tid >> 1, half = tid & 1;
+      float S = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; w++) S += ps[8 * half + w][j];
+      const float own = S + __shfl_xor(S, 1);
+      if (!half)
+        __hip_atomic_store(slot + (size_t)g * ld + j, sk_granule(own, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      constexpr int GH = GM / 2;
+      float l[GH];
+      unsigned long long gv[GH];
+      unsigned pend = 0;
+#pragma unroll
+      for (int k = 0; k < GH; k++) {
+        const int h = 2 * k + half;
+        l[k] = 0.f;
+        if (h < G) {
+          if (h == g) l[k] = own;
+          else pend |= 1u << k;
+        }
+      }
+      bool to = a.inject && p == 0 && g == 0 && it == 0;  // fault injection (rspl_sg_debug_inject)
+      unsigned spins = 0;
+      while (pend && !to) {
+#pragma unroll
+        for (int k = 0; k < GH; k++)
+          if (pend >> k & 1)
+            gv[k] = __hip_atomic_load(slot + (size_t)(2 * k + half) * ld + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int k = 0; k < GH; k++)
+          if ((pend >> k & 1) && (unsigned)(gv[k] >> 32) == tag) {
+            l[k] = __uint_as_float((unsigned)gv[k]);
+            pend &= ~(1u << k);
+          }
+        if (!pend) break;
+        if (++spins > a.spin_limit) { to = true; break; }
+        for (int z = 0; z < a.sleep; z++) __builtin_amdgcn_s_sleep(1);
+      }
+      if (to) flag[0] = 1;
+      float T = 0.f;
+#pragma unroll
+      for (int k = 0; k < GH; k++) T += l[k];
+      T = T + __shfl_xor(T, 1);
+      const float V = (j < n ? mu_in : nu_bin) / T;  // nu_j = mu_in for j < n: exp(norm)
+      if (!half) {
+        vs[j] = V;
+        if (!(V >= kLo && V <= kHi)) flag[1] = 1;
+      }
+    }
+    __syncthreads();
+    if (flag[0]) { failed = true; break; }
+#pragma unroll
+    for (int q = 0; q < kRbQ; q++) {
+      const int j = lane + 64 * q;
+      vr[q] = j < Cc ? vs[j] : 1.f;
+    }
+    const bool col_abs = flag[1] != 0, row_abs = flag[2 + (it & 1)] != 0;
+    if (col_abs || row_abs) {  // rare: absorb the scalings into the log potentials, rebuild K from C
+      __syncthreads();  // no wave still reads as / bs of the current K
+      if (row_abs) {
+#pragma unroll
+        for (int k = 0; k < RPW; k++) {
+          if (lane == 0) as[wv + 16 * k] += logf(ur[k] > 0.f ? ur[k] : 1.f);
+          ur[k] = 1.f;
+        }
+      }
+      if (col_abs) {
+        for (int j = tid; j < kRbQ * 64; j += kSinkThreads) bs[j] += logf(vs[j] > 0.f && j < Cc ? vs[j] : 1.f);
+#pragma unroll
+        for (int q = 0; q < kRbQ; q++) vr[q] = 1.f;
+      }
+      __syncthreads();
+      build_k(true);
+      __syncthreads();  // every thread has read flag[1] before it is cleared
+      if (tid == 0) flag[1] = 0;
+      __syncthreads();
+    }
+  }
+  if (failed) {
+    if (tid == 0) __hip_atomic_store(a.err + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  // Z = ((couplings + u) + v) - norm (superglue.py:203, :219), own rows; u = a + log U, v = b + log V
+  float* Z = a.Z + (size_t)p * ld * ld;
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int r = wv + 16 * k;
+    if (r >= nr) continue;
+    const float u = as[wv + 16 * k] + logf(ur[k]);
+#pragma unroll
+    for (int q = 0; q < kRbQ; q++) {
+      const int j = lane + 64 * q;
+      if (j < Cc) Z[(size_t)(r0 + r) * ld + j] = ((Cg[(size_t)(r0 + r) * ld + j] + u) + (bs[j] + logf(vr[q]))) - norm;
     }
   }
 }
@@ -1890,6 +2130,21 @@ int sinkhorn_rb_rpw(int nmax, int G) {
 hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   if (a.G < 1 || a.G > 1024) return hipErrorInvalidValue;
   dim3 grid(a.G, B);
+  if (a.rb && a.sc) {  // scaling-form kernel: the workgroup count must match an instantiated (RPW, GM)
+    switch (sinkhorn_rb_rpw(a.nmax, a.G)) {
+#define RSPL_SK_SC(R, M)                                                                                     \
+  case R:                                                                                                    \
+    hipExtLaunchKernelGGL((sinkhorn_sc_kernel<R, M>), grid, dim3(kSinkThreads), 0, s, t0, t1, 0, a);         \
+    break;
+      RSPL_SK_SC(8, 4)
+      RSPL_SK_SC(4, 8)
+      RSPL_SK_SC(2, 16)
+      RSPL_SK_SC(1, 32)
+#undef RSPL_SK_SC
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   if (a.rb) {  // row-block kernel: the workgroup count must match an instantiated (RPW, GM)
     switch (sinkhorn_rb_rpw(a.nmax, a.G)) {
 #define RSPL_SK_RB(R, M)                                                                                      \

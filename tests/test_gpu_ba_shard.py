@@ -78,7 +78,12 @@ def test_group_matches_oracle(G, seed, lines):
     prob, _ = SY.ba_problem(n_poses=8, n_points=600, n_lines=lines, seed=seed, pixel_sigma=0.8, outlier_frac=0.05)
     rs = run_group(prob, G)
     _identical(rs)
-    _compare(rs[0], oracle.ba_local(prob))
+    # >= 20 line landmarks: the numeric line Jacobians (g2o central differences, delta 1e-9) turn
+    # 1-ulp differences of the shard-summed system into ~1e-8 of the cost (as in test_gpu_ba.py's
+    # line-heavy cases) and, along weakly observed line directions, ~7e-3 in the Pluecker
+    # coordinates after 15 LM steps (G = 4, 30 lines; the cost still agrees to 1.5e-8)
+    heavy = lines >= 20
+    _compare(rs[0], oracle.ba_local(prob), chi2_rtol=5e-8 if heavy else 1e-8, tol_line=1e-2 if heavy else 5e-3)
 
 
 def test_group_c3_sized():

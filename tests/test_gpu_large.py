@@ -1,5 +1,5 @@
-"""C4 / C5-sized parity (at full size): SuperPoint at OIVIO 720x1280 (k=600)
-and synthetic 1080x1920 (k=2048), SuperGlue at N=600 and N=2048, and the C5 local BA (30 poses,
+"""C4 / C5-sized parity (at full size): SuperPoint at BASELINE.json's C4 shape
+640x512 and the reference's own OIVIO shape 1280x720 (configs/oivio.yaml:3-4; both k=600) and synthetic 1080x1920 (k=2048), SuperGlue at N=600 and N=2048, and the C5 local BA (30 poses,
 10k points, ~6e4 observations) -- the GPU through the C ABI vs the CPU oracle on the same inputs.
 The fp16 paths are held to SURVEY §8c's fp16 bar."""
 import numpy as np
@@ -45,7 +45,7 @@ def _restrict_to_common(F, G, score_tol):
             len(common) / max(1, len(sg)))
 
 
-@pytest.mark.parametrize("H,W,k,seed", [(720, 1280, 600, 4), (1080, 1920, 2048, 5)])
+@pytest.mark.parametrize("H,W,k,seed", [(512, 640, 600, 8), (720, 1280, 600, 4), (1080, 1920, 2048, 5)])
 def test_sp_large_vs_oracle(pkg, weight_blobs, H, W, k, seed):
     img = SY.textured_image(H, W, seed=seed, n_blobs=60)
     s, d = oracle.sp_forward(weight_blobs[0], post.image_to_input(img))
@@ -59,11 +59,11 @@ def test_sp_large_vs_oracle(pkg, weight_blobs, H, W, k, seed):
     compare_features(Fc, Gc)
 
 
-def test_sp_c5_fp16(pkg, weight_blobs):
-    """fp16 path (the reference's TensorRT kFP16 engine) at C5: keypoint overlap >= 99 %, descriptor
-    cosine >= 0.999 on the common keypoints."""
-    H, W, k = 1080, 1920, 2048
-    img = SY.textured_image(H, W, seed=5, n_blobs=60)
+@pytest.mark.parametrize("H,W,k,seed", [(512, 640, 600, 8), (1080, 1920, 2048, 5)])
+def test_sp_fp16_large(pkg, weight_blobs, H, W, k, seed):
+    """fp16 path (the reference's TensorRT kFP16 engine) at C4 (BASELINE.json's 640x512, k=600) and
+    C5: keypoint overlap >= 99 %, descriptor cosine >= 0.999 on the common keypoints."""
+    img = SY.textured_image(H, W, seed=seed, n_blobs=60)
     s, d = oracle.sp_forward(weight_blobs[0], post.image_to_input(img))
     G = post.sp_postprocess(s, d, 0.004, 4, k)
     sp = _sp(pkg, weight_blobs[0], k, H, W, precision=pkg.capi.RSPL_PREC_FP16)
@@ -74,7 +74,7 @@ def test_sp_c5_fp16(pkg, weight_blobs):
     common = sorted(set(kf) & set(kg))
     overlap = len(common) / k
     cos = np.array([F[3:, kf[c]] @ G[3:, kg[c]] for c in common])
-    print(f"fp16 SP C5: overlap {overlap:.4f}, min cosine {cos.min():.6f}")
+    print(f"fp16 SP {W}x{H}: overlap {overlap:.4f}, min cosine {cos.min():.6f}")
     assert overlap >= 0.99 and cos.min() >= 0.999
 
 

@@ -228,16 +228,19 @@ def test_sinkhorn_timeout_reaches_caller(pkg, weight_blobs):
     assert sg.status() == (True, 0)
 
 
-@pytest.mark.parametrize("kernel,G", [("slab", None), ("rb", 4), ("rb", 8), ("rb", 16), ("rb", 32)])
+@pytest.mark.parametrize("kernel,G", [("slab", None), ("rb", 4), ("rb", 16), ("rb", 32), ("sc", 4), ("sc", 8),
+                                      ("sc", 16), ("sc", 32)])
 def test_sinkhorn_kernels_vs_reference(pkg, golden, weight_blobs, monkeypatch, kernel, G):
-    """Both Sinkhorn kernels (the slab kernel: row + column slabs in LDS, two all-gathers per
-    iteration; the row-block kernel: whole rows in registers, one all-gather of per-column partial
-    LSEs per iteration) at every instantiated rows-per-wave, on the reference module's fixtures
-    (superglue.log_optimal_transport, convert2onnx/superglue.py:185-205): Z at atol 1e-4, identical
-    matches.  RSPL_SG_SINK / RSPL_SG_RB_G are read when the handle is created."""
+    """Every Sinkhorn kernel (the slab kernel: row + column slabs in LDS, two all-gathers per
+    iteration; the log-domain row-block kernel: whole rows in registers, one all-gather of
+    per-column partial LSEs per iteration; the scaling-form kernel, the default: the same layout
+    on register-resident exp(C + a + b), two mat-vecs per iteration) at every instantiated
+    rows-per-wave, on the reference module's fixtures (superglue.log_optimal_transport,
+    convert2onnx/superglue.py:185-205): Z at atol 1e-4, identical matches.  RSPL_SG_SINK /
+    RSPL_SG_SINK_G are read when the handle is created."""
     monkeypatch.setenv("RSPL_SG_SINK", kernel)
     if G:
-        monkeypatch.setenv("RSPL_SG_RB_G", str(G))
+        monkeypatch.setenv("RSPL_SG_SINK_G", str(G))
     g = golden("sinkhorn_unit")
     sg = _sg(pkg, weight_blobs[1], nmax=64)
     ok, Z = sg.debug_sinkhorn(g["scores"], float(g["alpha"]), int(g["iters"]))
@@ -254,3 +257,16 @@ def test_sinkhorn_kernels_vs_reference(pkg, golden, weight_blobs, monkeypatch, k
     np.testing.assert_allclose(Z, g["Z"], atol=1e-4, rtol=1e-5)
     np.testing.assert_array_equal(i0, g["idx0"])
     np.testing.assert_array_equal(i1, g["idx1"])
+
+
+def test_sinkhorn_scaling_absorption(pkg, weight_blobs):
+    """The scaling-form kernel on couplings with a large dynamic range (scores ~ N(0, 30)): its
+    scalings leave [2^-60, 2^60] and are absorbed into the log potentials (K rebuilt from C);
+    Z must still equal the oracle's log-domain Sinkhorn at atol 1e-4 (|Z| reaches hundreds)."""
+    rng = np.random.default_rng(3)
+    S = (rng.normal(size=(300, 280)) * 30).astype(np.float32)
+    sg = _sg(pkg, weight_blobs[1], nmax=300)
+    ok, Z = sg.debug_sinkhorn(S, 1.0, 100)
+    assert ok, sg.error
+    Zr = oracle.log_optimal_transport(S, 1.0, 100)
+    np.testing.assert_allclose(Z, Zr, atol=2e-4 * max(1.0, np.abs(Zr).max() / 100), rtol=0)

@@ -1,0 +1,147 @@
+"""BASELINE C1 plumbing (configs[0]: "first 100 stereo pairs, SuperPoint/SuperGlue + host g2o, plumbing"):
+100 synthetic EuRoC-shaped stereo pairs (480x752 u8, seeded textured scenes; EuRoC images are not in
+the container) through the keyframe front end twice, and the two compared pair by pair --
+
+  (a) the CPU path: the oracle's C restatement of SuperPoint (convert2onnx/superpoint.py + the
+      host post-processing of super_point.cpp:154-319) on the left and right image, SuperGlue on
+      (left, right) (superglue.py + super_glue.cpp decode), PointMatching's mutual re-check
+      (point_matching.cc:12-48), and the line part of Frame::AddRightFeatures (frame.cc:150-203:
+      disparity filter, AssignPointsToLines x2, MatchLines, right line per left line) restated in
+      oracle/lines_ref.py, on one frame's FLD-like segments merged by LineDetector (lines_ref);
+  (b) librspl: SuperPoint, PointMatching and the stereo line association on the GPU (fp32 parity
+      path), the merge passes in native C++ -- and the fp16 (TensorRT kFP16-equivalent) front end.
+
+Per pair it records keypoint agreement, descriptor error, match agreement (fp32 and fp16) and the
+agreement of the stereo line association.  MapBuilder / tracking are not built (out of scope); the
+map-side BA over a 100-keyframe sequence is tools/run_sequence.py.  Prints one JSON line; per-pair
+records go to --out."""
+import argparse
+import json
+import pathlib
+import sys
+import time
+
+import numpy as np
+
+ROOT = pathlib.Path(__file__).resolve().parents[1]
+sys.path.insert(0, str(ROOT))
+sys.path.insert(0, str(ROOT / "oracle"))
+import rspl_loader  # noqa: E402
+
+pkg = rspl_loader.load()
+pkg.capi.load()
+import lines_ref as LR  # noqa: E402  (the CPU path being compared against; test infrastructure)
+import oracle  # noqa: E402
+import post  # noqa: E402
+
+H, W, K = 480, 752, 400
+
+
+def key_index(F):
+    return {(int(x), int(y)): i for i, (x, y) in enumerate(zip(F[1], F[2]))}
+
+
+def match_set(m):
+    return {(int(q), int(t)) for q, t in np.asarray(m).reshape(-1, 2)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--pairs", type=int, default=100)
+    ap.add_argument("--threads", type=int, default=16)
+    ap.add_argument("--out", default="gpurun_out/c1_pairs.jsonl")
+    a = ap.parse_args()
+    oracle.set_threads(a.threads)
+    sp_w, sg_w = pkg.weights.ensure_blobs(str(ROOT / "weights"))
+    bf = pkg.synthetic.EUROC_BF
+    lim = (bf / 10.0, bf / 0.1, 2.0)  # MinXDiff, MaxXDiff, MaxYDiff (camera.cc:21-22)
+    C = pkg.capi
+    sps, pms = {}, {}
+    for name, prec in (("fp32", C.RSPL_PREC_FP32), ("fp16", C.RSPL_PREC_FP16)):
+        sps[name] = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=K, weights=sp_w, max_height=H, max_width=W,
+                                                        max_batch=1, precision=prec))
+        assert sps[name].build(), sps[name].error
+        pms[name] = pkg.PointMatching(pkg.SuperGlueConfig(image_width=W, image_height=H, weights=sg_w,
+                                                          max_keypoints=K, max_batch=1, precision=prec))
+    lm = pkg.lines.LineMatcher(max_lines=512, max_points=512)
+    out = pathlib.Path(a.out)
+    out.parent.mkdir(parents=True, exist_ok=True)
+    rows, t_cpu, t_gpu = [], 0.0, 0.0
+    with out.open("w") as fo:
+        for t in range(a.pairs):
+            L, R = pkg.synthetic.stereo_pair(H, W, seed=300 + t)
+            sc = pkg.synthetic.line_scene(n_lines=80, n_points=16, seed=300 + t, width=W, height=H)
+            # (a) CPU path
+            t0 = time.perf_counter()
+            Fc = []
+            for img in (L, R):
+                s, d = oracle.sp_forward(sp_w, post.image_to_input(img))
+                Fc.append(post.sp_postprocess(s, d, 0.004, 4, K))
+            g0, g1 = post.normalize_keypoints(Fc[0], W, H), post.normalize_keypoints(Fc[1], W, H)
+            Z = oracle.sg_forward(sg_w, *post.sg_inputs(g0), *post.sg_inputs(g1))
+            mc, _ = post.match_points(*post.decode(Z))
+            l0c, l1c = LR.line_extractor(sc["seg_left"]), LR.line_extractor(sc["seg_right"])
+            km = LR.stereo_filter(Fc[0][1], Fc[1][1], Fc[0][2], Fc[1][2], mc, *lim)
+            r0, r1 = LR.assign_points_to_lines(l0c, Fc[0][1:3].T), LR.assign_points_to_lines(l1c, Fc[1][1:3].T)
+            lrc, lvc = LR.right_lines(l1c, LR.match_lines(r0, r1, km, Fc[0].shape[1], Fc[1].shape[1]), len(l0c))
+            t_cpu += time.perf_counter() - t0
+            # (b) GPU path, fp32 (parity) and fp16
+            res = {}
+            for name in ("fp32", "fp16"):
+                t0 = time.perf_counter()
+                Fg = []
+                for img in (L, R):
+                    ok, F = sps[name].infer(img)
+                    assert ok, sps[name].error
+                    Fg.append(F)
+                nm, ml = pms[name].MatchingPoints(Fg[0], Fg[1])
+                mg = np.array([(q, tt) for q, tt, _ in ml], np.int32).reshape(-1, 2)
+                l0g, l1g = pkg.lines.LineExtractor(sc["seg_left"]), pkg.lines.LineExtractor(sc["seg_right"])
+                lrg, lvg, kept = lm.StereoLines(l0g, Fg[0], l1g, Fg[1], mg, lim)
+                if name == "fp32":
+                    t_gpu += time.perf_counter() - t0
+                res[name] = (Fg, mg, l0g, lrg, lvg)
+            Fg, mg, l0g, lrg, lvg = res["fp32"]
+            kc, kg = key_index(Fc[0]), key_index(Fg[0])
+            common = sorted(set(kc) & set(kg))
+            dmax = max(float(np.abs(Fg[0][3:, kg[c]] - Fc[0][3:, kc[c]]).max()) for c in common) if common else 0.0
+            sc_, sg_ = match_set(mc), match_set(mg)
+            h16 = match_set(res["fp16"][1])
+            lines_same = l0g.shape == l0c.shape and bool(np.array_equal(l0g, l0c))
+            row = {"pair": t,
+                   "keypoints": [int(Fc[0].shape[1]), int(Fc[1].shape[1])],
+                   "keypoint_sets_identical": bool(set(kc) == set(kg)) and
+                   set(key_index(Fc[1])) == set(key_index(Fg[1])),
+                   "desc_max_abs_diff": dmax,
+                   "matches_cpu": len(sc_), "matches_gpu_fp32": len(sg_),
+                   "match_agreement_fp32": len(sc_ & sg_) / max(1, len(sc_ | sg_)),
+                   "match_agreement_fp16": len(sc_ & h16) / max(1, len(sc_ | h16)),
+                   "lines_left": int(len(l0c)), "merged_lines_identical": lines_same,
+                   "right_lines_valid_cpu": int(lvc.sum()), "right_lines_valid_gpu": int(lvg.sum()),
+                   "line_association_identical": lines_same and bool(np.array_equal(lvc, lvg)) and
+                   bool(np.array_equal(lrc[lvc], lrg[lvg]))}
+            rows.append(row)
+            fo.write(json.dumps(row) + "\n")
+            if t % 10 == 0:
+                print(f"pair {t}: matches cpu {len(sc_)} gpu {len(sg_)} agreement {row['match_agreement_fp32']:.4f}",
+                      file=sys.stderr, flush=True)
+    agg = lambda k: float(np.mean([r[k] for r in rows]))
+    print(json.dumps({
+        "pairs": len(rows), "image": f"{W}x{H}", "max_keypoints": K,
+        "keypoint_sets_identical_frac": agg("keypoint_sets_identical"),
+        "desc_max_abs_diff": float(max(r["desc_max_abs_diff"] for r in rows)),
+        "match_agreement_fp32_mean": agg("match_agreement_fp32"),
+        "match_agreement_fp32_min": float(min(r["match_agreement_fp32"] for r in rows)),
+        "match_agreement_fp16_mean": agg("match_agreement_fp16"),
+        "match_agreement_fp16_min": float(min(r["match_agreement_fp16"] for r in rows)),
+        "matches_per_pair_cpu": agg("matches_cpu"),
+        "line_association_identical_frac": agg("line_association_identical"),
+        "right_lines_valid_per_pair": agg("right_lines_valid_cpu"),
+        "cpu_s_per_pair": round(t_cpu / len(rows), 3), "cpu_threads": a.threads,
+        "gpu_fp32_host_api_s_per_pair": round(t_gpu / len(rows), 4),
+        "note": "synthetic stereo pairs (EuRoC absent); the CPU path is the oracle restatement of the "
+                "reference's SP/SG modules + host code; GPU = librspl through its host-array API"}))
+
+
+if __name__ == "__main__":
+    main()
