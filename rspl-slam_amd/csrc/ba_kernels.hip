@@ -1382,6 +1382,7 @@ __device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys
   }
   const int failed = coherent ? __hip_atomic_load(S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *S.fail;
   if (failed) return;  // uniform: a landmark block failed to invert
+  if (lane == 0) prof_stamp(S, 1);
   // damping on the diagonal (a[k] with k == lane: select, static register index)
 #pragma unroll
   for (int k = 0; k < N; k++) a[k] += (k == lane) ? lambda : 0.0;
@@ -1405,6 +1406,7 @@ __device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys
     if (lane == 0) atomicOr(S.fail, 1);
     return;
   }
+  if (lane == 0) prof_stamp(S, 2);
   // y = D^-1 z; backward L^T x = y (lane i: y_i -= L_ki x_k for k > i, k descending)
   double y = 0.0;
 #pragma unroll
@@ -1419,6 +1421,7 @@ __device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys
     y = fma(-lt[k], xk, y);  // lt[k] == 0 for k <= lane
   }
   const double x = y;
+  if (lane == 0) prof_stamp(S, 3);
   if (row) S.x[lane] = x;
   w.xs[lane] = x;
   wave_sync();

@@ -264,21 +264,51 @@ __global__ __launch_bounds__(1024) void match_kernel(MatchArgs a) {
   }
 }
 
-__global__ __launch_bounds__(256) void stereo_filter_kernel(StereoArgs a) {
+// frame.cc:157-167 on the device: the stereo matches inside the disparity window, compacted in
+// left-keypoint order (= the reference's loop order) by one workgroup -- ballots and a prefix over
+// the 16 waves, no atomics -- so the kept list (and, past max_matches, which matches are dropped)
+// is the same on every run.  *n_out = the full count; status = 1 when it exceeds max_matches.
+__global__ __launch_bounds__(1024) void stereo_filter_kernel(StereoArgs a) {
 #pragma clang fp contract(off)
-  const int q = blockIdx.x * 256 + threadIdx.x;
-  if (q >= a.n_points[0]) return;
-  const int t = a.idx[q];
-  if (t < 0 || t >= a.n_points[1]) return;
-  const double* l = a.pts + (size_t)q * a.stride + a.xoff;
-  const double* r = a.pts + a.pt_batch + (size_t)t * a.stride + a.xoff;
-  const double dx = fabs(l[0] - r[0]), dy = fabs(l[1] - r[1]);
-  if (dx > a.min_x && dx < a.max_x && dy <= a.max_y) {
-    const int slot = atomicAdd(a.n_out, 1);
-    if (slot < a.max_matches) {
-      a.matches[2 * slot] = q;
-      a.matches[2 * slot + 1] = t;
+  __shared__ int wcnt[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nl = a.n_points[0], nr = a.n_points[1];
+  int run = 0;
+  for (int base = 0; base < nl; base += 1024) {
+    const int q = base + tid;
+    bool keep = false;
+    int t = -1;
+    if (q < nl) {
+      t = a.idx[q];
+      if (t >= 0 && t < nr) {
+        const double* l = a.pts + (size_t)q * a.stride + a.xoff;
+        const double* r = a.pts + a.pt_batch + (size_t)t * a.stride + a.xoff;
+        const double dx = fabs(l[0] - r[0]), dy = fabs(l[1] - r[1]);
+        keep = dx > a.min_x && dx < a.max_x && dy <= a.max_y;
+      }
     }
+    const unsigned long long bal = __ballot(keep);
+    if (lane == 0) wcnt[wv] = __popcll(bal);
+    __syncthreads();
+    int before = run, total = 0;
+    for (int w = 0; w < 16; w++) {
+      const int c = wcnt[w];
+      if (w < wv) before += c;
+      total += c;
+    }
+    if (keep) {
+      const int slot = before + __popcll(bal & ((1ull << lane) - 1ull));
+      if (slot < a.max_matches) {
+        a.matches[2 * slot] = q;
+        a.matches[2 * slot + 1] = t;
+      }
+    }
+    run += total;
+    __syncthreads();  // wcnt is rewritten by the next round
+  }
+  if (tid == 0) {
+    *a.n_out = run;
+    *a.status = run > a.max_matches ? 1 : 0;
   }
 }
 
@@ -309,7 +339,8 @@ hipError_t set_counts(int* n_lines, int nl0, int nl1, int* n_points, const int32
 }
 
 hipError_t stereo_filter(const StereoArgs& a, int max_left, hipStream_t s) {
-  hipLaunchKernelGGL(stereo_filter_kernel, dim3((max_left + 255) / 256), dim3(256), 0, s, a);
+  (void)max_left;
+  hipLaunchKernelGGL(stereo_filter_kernel, dim3(1), dim3(1024), 0, s, a);
   return hipGetLastError();
 }
 

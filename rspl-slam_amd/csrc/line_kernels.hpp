@@ -58,7 +58,8 @@ struct StereoArgs {
   int stride, xoff;
   double min_x, max_x, max_y;
   int* matches;           // [max_matches][2]
-  int* n_out;
+  int* n_out;             // the full count of kept matches (may exceed max_matches)
+  int* status;            // 1: more than max_matches passed the filter (the first max_matches kept)
   int max_matches;
 };
 // right line of each left line from the line matches (frame.cc:189-196, the reference's > 0 test)

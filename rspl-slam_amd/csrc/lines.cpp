@@ -256,7 +256,7 @@ extern "C" int rspl_lines_create(const rspl_lines_config* cfg, rspl_lines** out)
     };
     take(h->lines, 2 * L * 4); take(h->pts, 2 * N * 2); take(h->dist, 2 * C);
     take(h->n_lines, 2); take(h->n_points, 2); take(h->offsets, 2 * (L + 1)); take(h->idx, 2 * C);
-    take(h->status, 2); take(h->matches, 2 * Mm * 2); take(h->n_matches, 2); take(h->M, 2 * L * L);
+    take(h->status, 3); take(h->matches, 2 * Mm * 2); take(h->n_matches, 2); take(h->M, 2 * L * L);
     take(h->inv, 2 * 2 * C); take(h->out, 2 * L);
   };
   Sizer sz;
@@ -266,7 +266,8 @@ extern "C" int rspl_lines_create(const rspl_lines_config* cfg, rspl_lines** out)
     return rc;
   }
   carve(h->arena);
-  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
+      hipMemset(h->status, 0, sizeof(int) * 3) != hipSuccess) {
     rspl_lines_destroy(h);
     set_error("stream creation failed");
     return RSPL_E_DEVICE;
@@ -472,7 +473,8 @@ extern "C" int rspl_lines_stereo_device(rspl_lines* h, const double* d_lines_lef
   lines::StereoArgs sa{};
   sa.idx = d_match_idx; sa.n_points = h->n_points; sa.pts = d_features; sa.pt_batch = (size_t)feat_cap * 259;
   sa.stride = 259; sa.xoff = 1; sa.min_x = camera_limits[0]; sa.max_x = camera_limits[1]; sa.max_y = camera_limits[2];
-  sa.matches = h->matches; sa.n_out = h->n_matches; sa.max_matches = std::max(1, h->cfg.max_matches);
+  sa.matches = h->matches; sa.n_out = h->n_matches; sa.status = h->status + 2;
+  sa.max_matches = std::max(1, h->cfg.max_matches);
   RSPL_HIP(lines::stereo_filter(sa, feat_cap, st));
   lines::MatchArgs m{};
   m.off0 = m.off1 = h->offsets; m.idx0 = m.idx1 = h->idx; m.n_lines0 = m.n_lines1 = h->n_lines;
@@ -489,9 +491,9 @@ extern "C" int rspl_lines_stereo_device(rspl_lines* h, const double* d_lines_lef
 
 extern "C" int rspl_lines_status(rspl_lines* h, int* overflow) {
   RSPL_CHECK_ARG(h && overflow, "rspl_lines_status: NULL argument");
-  int st[2] = {0, 0};
+  int st[3] = {0, 0, 0};
   RSPL_HIP(hipMemcpy(st, h->status, sizeof(st), hipMemcpyDeviceToHost));
-  *overflow = st[0] | st[1];
+  *overflow = st[0] | st[1] | st[2];
   return RSPL_OK;
 }
 

@@ -64,6 +64,7 @@ struct rspl_sg {
   int *cn0, *cn1;                     // [2][B] the call's counts (the caller may reuse its own at once)
   hipEvent_t ev_ready = nullptr;      // main stream: couplings of this call written
   hipEvent_t ev_sink[2] = {nullptr, nullptr};  // post stream: Sinkhorn of parity p done with cpl[p]
+  hipEvent_t ev_done = nullptr;  // post stream: the last call's decode done (debug entry points wait on it)
   unsigned long long calls = 0;
   int last_parity = 0;
   StageTimer timer;
@@ -361,6 +362,7 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
       hipEventCreateWithFlags(&s->ev_ready, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&s->ev_sink[0], hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&s->ev_sink[1], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&s->ev_done, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(&s->h_f, sizeof(double) * nm * 259 * 2) != hipSuccess ||
       hipHostMalloc(&s->h_idx, sizeof(int32_t) * nm * 2 + 16) != hipSuccess ||
       hipHostMalloc(&s->h_ms, sizeof(double) * nm * 2) != hipSuccess ||
@@ -414,6 +416,7 @@ extern "C" void rspl_sg_destroy(rspl_sg* s) {
   if (s->h_ms) (void)hipHostFree(s->h_ms);
   if (s->err) (void)hipHostFree(s->err);
   if (s->ev_ready) (void)hipEventDestroy(s->ev_ready);
+  if (s->ev_done) (void)hipEventDestroy(s->ev_done);
   for (auto& e : s->ev_sink)
     if (e) (void)hipEventDestroy(e);
   if (s->stream) (void)hipStreamDestroy(s->stream);
@@ -592,10 +595,36 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
   dc.Z = Zp; dc.n0 = cn0; dc.n1 = cn1; dc.nmax = nm; dc.max0 = s->max0; dc.val0 = s->val0; dc.max1 = s->max1;
   dc.idx0 = d_idx0; dc.idx1 = d_idx1; dc.ms0 = d_ms0; dc.ms1 = d_ms1; dc.threshold = 0.2f;
   RSPL_HIP(sg::decode(dc, B, pst));
+  RSPL_HIP(hipEventRecord(s->ev_done, pst));
   s->timer.mark(6, pst);
   s->timer.end_call();
   s->last_B = B;
   s->last_parity = par;
+  return RSPL_OK;
+}
+
+// read and clear the sticky Sinkhorn flags of pairs [0, npairs) only (a host call launches pair 0:
+// a flag left by an unchecked device-path call of another pair is not reported as this call's)
+static int sink_status(rspl_sg* s, int npairs, uint32_t* pair_flags) {
+  uint32_t f = 0;
+  for (int p = 0; p < npairs && p < s->B; p++) {
+    volatile unsigned* e = s->err + p;
+    if (*e) f |= p < 32 ? (1u << p) : 0x80000000u;
+    *e = 0;
+  }
+  if (pair_flags) *pair_flags = f;
+  if (f) {
+    set_error("sinkhorn: cross-workgroup exchange timed out (pair mask 0x%x); results of those pairs are invalid", f);
+    return RSPL_E_DEVICE;
+  }
+  return RSPL_OK;
+}
+
+// the debug entry points reuse the exchange / scratch / Z buffers of pair 0: wait for any device-path
+// call still running on a caller's post stream first
+static int sync_all(rspl_sg* s) {
+  RSPL_HIP(hipStreamSynchronize(s->stream));
+  RSPL_HIP(hipEventSynchronize(s->ev_done));
   return RSPL_OK;
 }
 
@@ -620,7 +649,7 @@ static int sg_host_run(rspl_sg* s, const double* f0, int n0, const double* f1, i
   RSPL_HIP(hipMemcpyAsync(s->h_ms + nm, s->ms1, sizeof(double) * n1, hipMemcpyDeviceToHost, s->stream));
   RSPL_HIP(hipStreamSynchronize(s->stream));
   unsigned flags = 0;
-  if (int rc2 = rspl_sg_status(s, &flags)) return rc2;
+  if (int rc2 = sink_status(s, 1, &flags)) return rc2;
   s->last_n0 = n0;
   s->last_n1 = n1;
   if (n0 == 0 || n1 == 0) {  // no couplings: every keypoint unmatched
@@ -676,7 +705,7 @@ extern "C" int rspl_pm_match(rspl_sg* s, const double* f0, int n0, const double*
 
 extern "C" int rspl_sg_debug_scores(rspl_sg* s, int p, float* Z) {
   RSPL_CHECK_ARG(s && Z && p >= 0 && p < s->last_B, "rspl_sg_debug_scores: bad argument");
-  RSPL_HIP(hipStreamSynchronize(s->stream));
+  if (int rc = sync_all(s)) return rc;
   const int R = s->last_n0 + 1, Cc = s->last_n1 + 1;
   RSPL_HIP(hipMemcpy2D(Z, sizeof(float) * Cc, s->Z + ((size_t)s->last_parity * s->B + p) * s->ld * s->ld,
                        sizeof(float) * s->ld,
@@ -697,18 +726,7 @@ extern "C" int rspl_sg_stage_times(rspl_sg* s, float* ms, int* calls) {
 
 extern "C" int rspl_sg_status(rspl_sg* s, uint32_t* pair_flags) {
   RSPL_CHECK_ARG(s, "rspl_sg_status: NULL handle");
-  uint32_t f = 0;
-  for (int p = 0; p < s->B; p++) {
-    volatile unsigned* e = s->err + p;
-    if (*e) f |= p < 32 ? (1u << p) : 0x80000000u;
-    *e = 0;
-  }
-  if (pair_flags) *pair_flags = f;
-  if (f) {
-    set_error("sinkhorn: cross-workgroup exchange timed out (pair mask 0x%x); results of those pairs are invalid", f);
-    return RSPL_E_DEVICE;
-  }
-  return RSPL_OK;
+  return sink_status(s, s->B, pair_flags);
 }
 
 extern "C" int rspl_sg_debug_inject(rspl_sg* s, int inject, unsigned spin_limit) {
@@ -725,7 +743,7 @@ extern "C" int rspl_sg_debug_sinkhorn(rspl_sg* s, const float* scores, int n0, i
                  "bad shape or iteration count (< 4096)");
   const size_t ld = s->ld;
   hipStream_t st = s->stream;
-  RSPL_HIP(hipStreamSynchronize(st));
+  if (int rc = sync_all(s)) return rc;
   int cnt[2] = {n0, n1};
   const float al[4] = {alpha, 0.f, 0.f, 0.f};
   RSPL_HIP(hipMemcpy2DAsync(s->cpl, sizeof(float) * ld, scores, sizeof(float) * n1, sizeof(float) * n1, n0,
@@ -741,7 +759,7 @@ extern "C" int rspl_sg_debug_sinkhorn(rspl_sg* s, const float* scores, int n0, i
                             hipMemcpyDeviceToHost, st));
   RSPL_HIP(hipStreamSynchronize(st));
   s->last_B = 0;  // the debug call reused pair 0's buffers
-  return rspl_sg_status(s, nullptr);
+  return sink_status(s, 1, nullptr);
 }
 
 extern "C" int rspl_sg_debug_decode(rspl_sg* s, const float* Z, int n0, int n1, int32_t* indices0, int32_t* indices1,
@@ -750,7 +768,7 @@ extern "C" int rspl_sg_debug_decode(rspl_sg* s, const float* Z, int n0, int n1, 
   RSPL_CHECK_ARG(n0 >= 1 && n1 >= 1 && n0 <= s->nmax && n1 <= s->nmax, "bad shape");
   const size_t ld = s->ld;
   hipStream_t st = s->stream;
-  RSPL_HIP(hipStreamSynchronize(st));
+  if (int rc = sync_all(s)) return rc;
   int cnt[2] = {n0, n1};
   RSPL_HIP(hipMemcpy2DAsync(s->Z, sizeof(float) * ld, Z, sizeof(float) * (n1 + 1), sizeof(float) * (n1 + 1), n0 + 1,
                             hipMemcpyHostToDevice, st));

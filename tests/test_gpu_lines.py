@@ -119,3 +119,45 @@ def test_stereo_lines_device_matches_host(lm):
     np.testing.assert_array_equal(dV.download(len(L0), np.uint8).astype(bool), ref_valid)
     np.testing.assert_array_equal(dO.download((len(L0), 4), np.float64), ref_lr)
     assert ref_valid.sum() > 10
+
+
+def test_stereo_lines_device_match_overflow():
+    """More kept stereo matches than max_matches: the device filter keeps the first max_matches in
+    left-keypoint order (the reference's loop order), the same on every run, and rspl_lines_status
+    reports the overflow."""
+    C = pkg.capi
+    sc = SY.line_scene(n_lines=80, n_points=600, seed=6)
+    L0, L1 = LR.line_extractor(sc["seg_left"]), LR.line_extractor(sc["seg_right"])
+    F0, F1, m = sc["feat_left"], sc["feat_right"], sc["stereo_matches"]
+    lim = (2.0, 60.0, 2.0)
+    km = LR.stereo_filter(F0[:, 1], F1[:, 1], F0[:, 2], F1[:, 2], m, *lim)
+    cap_m = len(km) // 2
+    small = pkg.lines.LineMatcher(max_lines=512, max_points=2048, max_matches=cap_m)
+    ref = pkg.lines.LineMatcher(max_lines=512, max_points=2048)
+    first = km[np.argsort(km[:, 0], kind="stable")][:cap_m]  # left-keypoint order
+    ref_lr, ref_valid, _ = ref.StereoLines(L0, F0, L1, F1, first, (0.0, 1e9, 1e9))
+    cap = 800
+    feats = np.zeros((2, cap, 259))
+    feats[0, :len(F0)] = F0
+    feats[1, :len(F1)] = F1
+    idx = np.full(cap, -1, np.int32)
+    idx[m[:, 0]] = m[:, 1]
+    dF = C.DeviceBuffer(feats.nbytes).upload(feats)
+    dC = C.DeviceBuffer(8).upload(np.array([len(F0), len(F1)], np.int32))
+    dI = C.DeviceBuffer(idx.nbytes).upload(idx)
+    dL0 = C.DeviceBuffer(max(8, L0.nbytes)).upload(np.ascontiguousarray(L0))
+    dL1 = C.DeviceBuffer(max(8, L1.nbytes)).upload(np.ascontiguousarray(L1))
+    dO = C.DeviceBuffer(len(L0) * 32)
+    dV = C.DeviceBuffer(max(8, len(L0)))
+    runs = []
+    for _ in range(5):
+        small.stereo_lines_device(dL0.ptr, len(L0), dL1.ptr, len(L1), dF.ptr, cap, dC.ptr, dI.ptr, lim, dO.ptr,
+                                  dV.ptr)
+        C.load().rspl_device_synchronize()
+        assert small.status()  # more than max_matches passed the filter
+        runs.append((dV.download(len(L0), np.uint8).astype(bool), dO.download((len(L0), 4), np.float64)))
+    for v, o in runs[1:]:
+        np.testing.assert_array_equal(v, runs[0][0])
+        np.testing.assert_array_equal(o, runs[0][1])
+    np.testing.assert_array_equal(runs[0][0], ref_valid)
+    np.testing.assert_array_equal(runs[0][1], ref_lr)

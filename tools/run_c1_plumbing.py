@@ -11,8 +11,13 @@ the container) through the keyframe front end twice, and the two compared pair b
   (b) librspl: SuperPoint, PointMatching and the stereo line association on the GPU (fp32 parity
       path), the merge passes in native C++ -- and the fp16 (TensorRT kFP16-equivalent) front end.
 
-Per pair it records keypoint agreement, descriptor error, match agreement (fp32 and fp16) and the
-agreement of the stereo line association.  MapBuilder / tracking are not built (out of scope); the
+Per pair it records keypoint agreement, descriptor error, the log-assignment Z error, match agreement
+(fp32 and fp16) and the agreement of the stereo line association.  The weights are the seeded
+synthetic ones (no trained weights exist here), so SuperGlue's matching probabilities stay below the
+reference's 0.2 threshold (super_glue.cpp:355) on these scenes: the thresholded match lists are
+empty on both paths.  The pipeline is therefore also compared on the mutual nearest neighbours of Z
+with the threshold at 0 (decode's mutual check and argmaxes, point_matching.cc:24-31), and those
+pairs feed the stereo line association.  MapBuilder / tracking are not built (out of scope); the
 map-side BA over a 100-keyframe sequence is tools/run_sequence.py.  Prints one JSON line; per-pair
 records go to --out."""
 import argparse
@@ -80,8 +85,9 @@ def main():
             g0, g1 = post.normalize_keypoints(Fc[0], W, H), post.normalize_keypoints(Fc[1], W, H)
             Z = oracle.sg_forward(sg_w, *post.sg_inputs(g0), *post.sg_inputs(g1))
             mc, _ = post.match_points(*post.decode(Z))
+            nnc, _ = post.match_points(*post.decode(Z, threshold=0.0))  # mutual NN, no threshold
             l0c, l1c = LR.line_extractor(sc["seg_left"]), LR.line_extractor(sc["seg_right"])
-            km = LR.stereo_filter(Fc[0][1], Fc[1][1], Fc[0][2], Fc[1][2], mc, *lim)
+            km = LR.stereo_filter(Fc[0][1], Fc[1][1], Fc[0][2], Fc[1][2], nnc, *lim)
             r0, r1 = LR.assign_points_to_lines(l0c, Fc[0][1:3].T), LR.assign_points_to_lines(l1c, Fc[1][1:3].T)
             lrc, lvc = LR.right_lines(l1c, LR.match_lines(r0, r1, km, Fc[0].shape[1], Fc[1].shape[1]), len(l0c))
             t_cpu += time.perf_counter() - t0
@@ -96,26 +102,31 @@ def main():
                     Fg.append(F)
                 nm, ml = pms[name].MatchingPoints(Fg[0], Fg[1])
                 mg = np.array([(q, tt) for q, tt, _ in ml], np.int32).reshape(-1, 2)
+                Zg = pms[name].superglue.debug_scores(0, Fg[0].shape[1], Fg[1].shape[1])
+                nng, _ = post.match_points(*post.decode(Zg, threshold=0.0))
                 l0g, l1g = pkg.lines.LineExtractor(sc["seg_left"]), pkg.lines.LineExtractor(sc["seg_right"])
-                lrg, lvg, kept = lm.StereoLines(l0g, Fg[0], l1g, Fg[1], mg, lim)
+                lrg, lvg, kept = lm.StereoLines(l0g, Fg[0], l1g, Fg[1], nng, lim)
                 if name == "fp32":
                     t_gpu += time.perf_counter() - t0
-                res[name] = (Fg, mg, l0g, lrg, lvg)
-            Fg, mg, l0g, lrg, lvg = res["fp32"]
+                res[name] = (Fg, mg, nng, Zg, l0g, lrg, lvg)
+            Fg, mg, nng, Zg, l0g, lrg, lvg = res["fp32"]
             kc, kg = key_index(Fc[0]), key_index(Fg[0])
             common = sorted(set(kc) & set(kg))
             dmax = max(float(np.abs(Fg[0][3:, kg[c]] - Fc[0][3:, kc[c]]).max()) for c in common) if common else 0.0
             sc_, sg_ = match_set(mc), match_set(mg)
-            h16 = match_set(res["fp16"][1])
+            nc_, ng_, n16 = match_set(nnc), match_set(nng), match_set(res["fp16"][2])
+            zerr = float(np.abs(Zg - Z).max()) if Zg.shape == Z.shape else float("nan")
             lines_same = l0g.shape == l0c.shape and bool(np.array_equal(l0g, l0c))
             row = {"pair": t,
                    "keypoints": [int(Fc[0].shape[1]), int(Fc[1].shape[1])],
                    "keypoint_sets_identical": bool(set(kc) == set(kg)) and
                    set(key_index(Fc[1])) == set(key_index(Fg[1])),
                    "desc_max_abs_diff": dmax,
-                   "matches_cpu": len(sc_), "matches_gpu_fp32": len(sg_),
-                   "match_agreement_fp32": len(sc_ & sg_) / max(1, len(sc_ | sg_)),
-                   "match_agreement_fp16": len(sc_ & h16) / max(1, len(sc_ | h16)),
+                   "Z_max_abs_diff_fp32": zerr,
+                   "matches_cpu": len(sc_), "matches_gpu_fp32": len(sg_), "matches_identical": sc_ == sg_,
+                   "mutual_nn_cpu": len(nc_),
+                   "match_agreement_fp32": len(nc_ & ng_) / max(1, len(nc_ | ng_)),
+                   "match_agreement_fp16": len(nc_ & n16) / max(1, len(nc_ | n16)),
                    "lines_left": int(len(l0c)), "merged_lines_identical": lines_same,
                    "right_lines_valid_cpu": int(lvc.sum()), "right_lines_valid_gpu": int(lvg.sum()),
                    "line_association_identical": lines_same and bool(np.array_equal(lvc, lvg)) and
@@ -123,18 +134,21 @@ def main():
             rows.append(row)
             fo.write(json.dumps(row) + "\n")
             if t % 10 == 0:
-                print(f"pair {t}: matches cpu {len(sc_)} gpu {len(sg_)} agreement {row['match_agreement_fp32']:.4f}",
-                      file=sys.stderr, flush=True)
+                print(f"pair {t}: mutual NN cpu {len(nc_)} gpu {len(ng_)} agreement {row['match_agreement_fp32']:.4f}"
+                      f" fp16 {row['match_agreement_fp16']:.4f} |dZ| {zerr:.2e}", file=sys.stderr, flush=True)
     agg = lambda k: float(np.mean([r[k] for r in rows]))
     print(json.dumps({
         "pairs": len(rows), "image": f"{W}x{H}", "max_keypoints": K,
         "keypoint_sets_identical_frac": agg("keypoint_sets_identical"),
         "desc_max_abs_diff": float(max(r["desc_max_abs_diff"] for r in rows)),
+        "Z_max_abs_diff_fp32": float(max(r["Z_max_abs_diff_fp32"] for r in rows)),
+        "thresholded_matches_identical_frac": agg("matches_identical"),
+        "matches_per_pair_cpu": agg("matches_cpu"),
+        "mutual_nn_per_pair_cpu": agg("mutual_nn_cpu"),
         "match_agreement_fp32_mean": agg("match_agreement_fp32"),
         "match_agreement_fp32_min": float(min(r["match_agreement_fp32"] for r in rows)),
         "match_agreement_fp16_mean": agg("match_agreement_fp16"),
         "match_agreement_fp16_min": float(min(r["match_agreement_fp16"] for r in rows)),
-        "matches_per_pair_cpu": agg("matches_cpu"),
         "line_association_identical_frac": agg("line_association_identical"),
         "right_lines_valid_per_pair": agg("right_lines_valid_cpu"),
         "cpu_s_per_pair": round(t_cpu / len(rows), 3), "cpu_threads": a.threads,
