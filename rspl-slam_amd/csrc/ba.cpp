@@ -46,7 +46,6 @@ struct rspl_ba {
   unsigned long long* prof = nullptr;  // RSPL_BA_PROF: timing trace of one trial per call
   int prof_nb[3] = {0, 0, 0};          // its pair_chunk / update_errors grid sizes, group blocks
   // landmark CSR (filled on the device) and the Schur chunk / pose-pair sums
-  int *lm_edges, *lm_pose;
   double *chunk, *pairfin;
   unsigned* pair_ctr;  // [npairs] chunk tickets (zeroed at create, re-armed by the kernel)
   int *pp_cnt, *pp_off;  // [npairs * nchk (+1)] edge pairs per Schur chunk, segment offsets
@@ -65,6 +64,7 @@ struct rspl_ba {
   ba::Mail* mail_dev = nullptr;
   unsigned long long seq = 0;
   std::vector<uint8_t> pact;  // host scratch reused across calls
+  std::vector<int> lm_cnt;    // per-landmark edge counts, then fill cursors (host scratch)
   // landmark sharding (rspl_ba_set_shard): this rank keeps the edges of landmarks g % nranks == rank
   int rank = 0, nranks = 1;
   rspl_allreduce_fn allreduce = nullptr;
@@ -95,9 +95,9 @@ inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 
 // per-call upload layout (staging call region == device call buffer)
 struct CallLayout {
-  size_t cams, T, X, L, obs, type, pose, lm, cam, gmap, pidx, lm_off, lm_act, pairs, ltab, level, fill, flags, out,
+  size_t cams, T, X, L, obs, type, pose, lm, cam, gmap, lm_pose, pidx, lm_off, lm_act, pairs, ltab, level, flags, out,
       bytes;
-  CallLayout(int ncam, int np, int nq, int nl, int E, size_t nobs) {  // nobs: packed observation doubles
+  CallLayout(int ncam, int np, int nq, int nl, int E, size_t nobs) {  // nobs: observation doubles (4 / 8 per edge)
     const size_t nL = (size_t)nq + nl;
     size_t so = 0;
     auto place = [&](size_t n) {
@@ -108,10 +108,11 @@ struct CallLayout {
     cams = place(sizeof(double) * 5 * ncam); T = place(sizeof(double) * 8 * np); X = place(sizeof(double) * 3 * nq);
     L = place(sizeof(double) * 6 * nl); obs = place(sizeof(double) * nobs); type = place(E);
     pose = place(4 * (size_t)E); lm = place(4 * (size_t)E); cam = place(4 * (size_t)E); gmap = place(4 * (size_t)E);
+    lm_pose = place(4 * (size_t)E);
     pidx = place(4 * (size_t)np); lm_off = place(4 * (nL + 1)); lm_act = place(nL);
     pairs = place(8 * (size_t)np * (np + 1) / 2);
     ltab = place(16 * ((size_t)E + nl + 1));
-    level = place(E); fill = place(4 * nL); flags = place(4 * sizeof(int)); out = place(8 * sizeof(double));  // zeros
+    level = place(E); flags = place(4 * sizeof(int)); out = place(8 * sizeof(double));  // zeros
     bytes = so;
   }
 };
@@ -148,7 +149,6 @@ void carve(F& ar, rspl_ba* b) {
   take(b->lm_ctr, nl);
   take(b->lflag, nl);
   const size_t npairs = K * (K + 1) / 2, nchk = std::max<size_t>((NL + ba::kLmChunk - 1) / ba::kLmChunk, 1);
-  take(b->lm_edges, E); take(b->lm_pose, E);
   take(b->chunk, npairs * nchk * 48); take(b->pairfin, npairs * 48 + 8); take(b->pair_ctr, npairs + 1);  // + the solve ticket
   take(b->red, 6 * K + kMaxRanks + 8);
   take(b->lmctl, 2);
@@ -655,12 +655,30 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   };
   mark();
   // ---- one staging region for the whole call, mirrored by the device call buffer ----
-  size_t nobs = 0;  // packed observation doubles (all edges: an upper bound when sharded)
-  {
-    const int odt[4] = {2, 3, 4, 8};
-    for (int t = 0; t < 4; t++) nobs += (size_t)odt[t] * ne[t];
+  const int32_t* poses[4] = {pr->mono_pose, pr->stereo_pose, pr->mono_line_pose, pr->stereo_line_pose};
+  const int32_t* lms[4] = {pr->mono_point, pr->stereo_point, pr->mono_line_line, pr->stereo_line_line};
+  const int32_t* cams[4] = {pr->mono_camera, pr->stereo_camera, pr->mono_line_camera, pr->stereo_line_camera};
+  const double* obs[4] = {pr->mono_obs, pr->stereo_obs, pr->mono_line_obs, pr->stereo_line_obs};
+  const int od[4] = {2, 3, 4, 8};
+  // pass 1: validate, count the local edges per landmark, mark the poses with edges
+  b->lm_cnt.assign(nL + 1, 0);
+  b->pact.assign(np, 0);
+  int Ep = 0;  // local point edges
+  for (int t = 0; t < 4; t++) {
+    RSPL_CHECK_ARG(ne[t] == 0 || (poses[t] && lms[t] && obs[t]), "NULL edge arrays");
+    const int n = ne[t], lmax = t < 2 ? nq : nl, loff = t < 2 ? 0 : nq;
+    const int32_t *pt = poses[t], *lt = lms[t], *ct = cams[t];
+    for (int i = 0; i < n; i++) {
+      const int p = pt[i], l = lt[i], c = ct ? ct[i] : 0;
+      RSPL_CHECK_ARG(p >= 0 && p < np && l >= 0 && l < lmax && c >= 0 && c < pr->n_cameras,
+                     "edge %d of type %d references a missing vertex/camera", i, t);
+      b->pact[p] = 1;  // a pose is optimised when it has an edge on ANY rank: K agrees across ranks
+      if (!owned(t, i)) continue;
+      b->lm_cnt[loff + l + 1]++;
+      Ep += t < 2;
+    }
   }
-  const CallLayout cl(pr->n_cameras, np, nq, nl, E, nobs);
+  const CallLayout cl(pr->n_cameras, np, nq, nl, E, 4 * (size_t)Ep + 8 * (size_t)(E - Ep));
   const DownLayout dl(np, nq, nl, Eg);  // inlier flags by global edge id
   int rc;
   if ((rc = ensure_stage(b, std::max(cl.bytes, dl.bytes)))) return rc;
@@ -680,76 +698,50 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
     for (int k = 0; k < 3; k++) T[8 * p + 4 + k] = Tcw.t[k];
     T[8 * p + 7] = 0;
   }
-  // edges (unified, input order), written straight into the staging region
-  const int32_t* poses[4] = {pr->mono_pose, pr->stereo_pose, pr->mono_line_pose, pr->stereo_line_pose};
-  const int32_t* lms[4] = {pr->mono_point, pr->stereo_point, pr->mono_line_line, pr->stereo_line_line};
-  const int32_t* cams[4] = {pr->mono_camera, pr->stereo_camera, pr->mono_line_camera, pr->stereo_line_camera};
-  const double* obs[4] = {pr->mono_obs, pr->stereo_obs, pr->mono_line_obs, pr->stereo_line_obs};
-  const int od[4] = {2, 3, 4, 8};
-  double* eobs = reinterpret_cast<double*>(sg + cl.obs);
+  int* pidx = reinterpret_cast<int*>(sg + cl.pidx);
+  int K = 0;
+  for (int p = 0; p < np; p++) pidx[p] = (b->pact[p] && !pr->pose_fixed[p]) ? K++ : -1;
+  // CSR offsets: the edges of landmark g at positions [lm_off[g], lm_off[g+1]), point landmarks first
+  int* lm_off = reinterpret_cast<int*>(sg + cl.lm_off);
+  lm_off[0] = 0;
+  for (int g = 0; g < nL; g++) lm_off[g + 1] = lm_off[g] + b->lm_cnt[g + 1];
+  // pass 2: every local edge written at its CSR position (input order within a landmark: the
+  // order every per-landmark reduction follows), with its reduced pose and its caller's edge id
   int8_t* etype = reinterpret_cast<int8_t*>(sg + cl.type);
   int* epose = reinterpret_cast<int*>(sg + cl.pose);
   int* elm = reinterpret_cast<int*>(sg + cl.lm);
   int* ecam = reinterpret_cast<int*>(sg + cl.cam);
-  // per-landmark edge counts -> CSR offsets, poses with edges -> reduced pose ids (the
-  // device fills the CSR lists from these)
-  int* lm_off = reinterpret_cast<int*>(sg + cl.lm_off);
-  memset(lm_off, 0, sizeof(int) * (nL + 1));
-  b->pact.assign(np, 0);
   int* gmap = reinterpret_cast<int*>(sg + cl.gmap);
-  int e = 0, eg = 0;
-  size_t opos = 0;
-  int lstart[5], obase[4];
+  int* lpose = reinterpret_cast<int*>(sg + cl.lm_pose);
+  double* eobs = reinterpret_cast<double*>(sg + cl.obs);
+  double* lobs = eobs + 4 * (size_t)Ep;
+  int* fill = b->lm_cnt.data();  // reused as the per-landmark fill cursor
+  for (int g = 0; g < nL; g++) fill[g] = lm_off[g];
+  int eg = 0;
   for (int t = 0; t < 4; t++) {
-    RSPL_CHECK_ARG(ne[t] == 0 || (poses[t] && lms[t] && obs[t]), "NULL edge arrays");
-    lstart[t] = e;
-    obase[t] = (int)opos;
-    const int n = ne[t], lmax = t < 2 ? nq : nl, loff = t < 2 ? 0 : nq;
+    const int n = ne[t], loff = t < 2 ? 0 : nq, d = od[t];
     const int32_t *pt = poses[t], *lt = lms[t], *ct = cams[t];
-    if (!sh) {  // every edge is local: bulk copies, one validation pass
-      for (int i = 0; i < n; i++) {
-        const int p = pt[i], l = lt[i], c = ct ? ct[i] : 0;
-        RSPL_CHECK_ARG(p >= 0 && p < np && l >= 0 && l < lmax && c >= 0 && c < pr->n_cameras,
-                       "edge %d of type %d references a missing vertex/camera", i, t);
-        b->pact[p] = 1;
-        elm[e + i] = loff + l;
-        lm_off[loff + l + 1]++;
-      }
-      memset(etype + e, t, n);
-      memcpy(epose + e, pt, sizeof(int) * n);
-      if (ct) memcpy(ecam + e, ct, sizeof(int) * n);
-      else memset(ecam + e, 0, sizeof(int) * n);
-      memcpy(eobs + opos, obs[t], sizeof(double) * od[t] * n);
-      opos += (size_t)od[t] * n;
-      e += n;
-      eg += n;
-      continue;
-    }
+    const double* ob = obs[t];
     for (int i = 0; i < n; i++, eg++) {
-      const int p = pt[i], l = lt[i], c = ct ? ct[i] : 0;
-      RSPL_CHECK_ARG(p >= 0 && p < np && l >= 0 && l < lmax && c >= 0 && c < pr->n_cameras,
-                     "edge %d of type %d references a missing vertex/camera", i, t);
-      b->pact[p] = 1;  // a pose is optimised when it has an edge on ANY rank: K agrees across ranks
       if (!owned(t, i)) continue;
-      etype[e] = (int8_t)t;
-      epose[e] = p;
-      elm[e] = loff + l;
-      ecam[e] = c;
-      gmap[e] = eg;  // global edge id (sharded runs only)
-      lm_off[elm[e] + 1]++;
-      memcpy(eobs + opos, obs[t] + (size_t)od[t] * i, sizeof(double) * od[t]);
-      opos += od[t];
-      e++;
+      const int g = loff + lt[i], k = fill[g]++, p = pt[i];
+      etype[k] = (int8_t)t;
+      epose[k] = p;
+      elm[k] = g;
+      ecam[k] = ct ? ct[i] : 0;
+      gmap[k] = eg;
+      lpose[k] = pidx[p];
+      double* o = t < 2 ? eobs + 4 * (size_t)k : lobs + 8 * (size_t)(k - Ep);
+      for (int q = 0; q < d; q++) o[q] = ob[(size_t)d * i + q];
+      if (t == 0) o[2] = 0.0;
     }
   }
-  lstart[4] = e;
   uint8_t* lm_act = reinterpret_cast<uint8_t*>(sg + cl.lm_act);
   size_t pair_bound = 0;  // sum_g k_g^2 >= edge pairs of any pose pair
   for (int g = 0; g < nL; g++) {
-    const size_t k = lm_off[g + 1];
+    const size_t k = lm_off[g + 1] - lm_off[g];
     pair_bound += k * k;
     lm_act[g] = k > 0;
-    lm_off[g + 1] += lm_off[g];
   }
   if (pair_bound > b->pp_cap) {  // grow the edge-pair lists (the stream is idle between calls)
     RSPL_HIP(hipStreamSynchronize(st));
@@ -790,9 +782,6 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
     }
     flush();
   }
-  int* pidx = reinterpret_cast<int*>(sg + cl.pidx);
-  int K = 0;
-  for (int p = 0; p < np; p++) pidx[p] = (b->pact[p] && !pr->pose_fixed[p]) ? K++ : -1;
   int* pairs = reinterpret_cast<int*>(sg + cl.pairs);
   for (int a = 0, q = 0; a < K; a++)
     for (int c = a; c < K; c++, q++) {
@@ -811,18 +800,14 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   P.T = reinterpret_cast<double*>(cb + cl.T);
   P.X = reinterpret_cast<double*>(cb + cl.X);
   P.L = reinterpret_cast<double*>(cb + cl.L);
-  P.np = np; P.nq = nq; P.nl = nl;
+  P.np = np; P.nq = nq; P.nl = nl; P.ncam = pr->n_cameras;
   P.Tn = b->Tb; P.Xn = b->Xb; P.Ln = b->Lb;
   P.etype = reinterpret_cast<const int8_t*>(cb + cl.type);
   P.epose = reinterpret_cast<const int*>(cb + cl.pose);
   P.elm = reinterpret_cast<const int*>(cb + cl.lm);
   P.ecam = reinterpret_cast<const int*>(cb + cl.cam);
   P.eobs = reinterpret_cast<const double*>(cb + cl.obs);
-  for (int t = 0; t < 4; t++) {
-    P.lstart[t] = lstart[t];
-    P.obase[t] = obase[t];
-  }
-  P.lstart[4] = lstart[4];
+  P.Ep = Ep;
   const double th[4] = {pr->th_mono_point, pr->th_stereo_point, pr->th_mono_line, pr->th_stereo_line};
   for (int t = 0; t < 4; t++) {
     P.th[t] = th[t];
@@ -850,8 +835,7 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   A.Ea = E;
   A.pidx = reinterpret_cast<const int*>(cb + cl.pidx);
   A.lm_off = reinterpret_cast<const int*>(cb + cl.lm_off);
-  A.lm_edges = b->lm_edges;
-  A.lm_pose = b->lm_pose;
+  A.lm_pose = reinterpret_cast<const int*>(cb + cl.lm_pose);
   A.lm_act = reinterpret_cast<const uint8_t*>(cb + cl.lm_act);
   A.pairs = reinterpret_cast<const int*>(cb + cl.pairs);
   A.npairs = K * (K + 1) / 2;
@@ -865,7 +849,6 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   mark();
   A.pp_off = b->pp_off;
   A.pp = b->pp_buf;
-  RSPL_HIP(ba::build_csr(P, A, reinterpret_cast<int*>(cb + cl.fill), b->lm_edges, b->lm_pose, st));
   RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, st));
   mark();
   if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first)))
@@ -908,7 +891,7 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
     if (glen && (rc = allreduce(b, b->gbuf, glen))) return rc;
     RSPL_HIP(ba::shard_finish(P, Eg, b->gbuf, inl_h, T_h, X_h, L_h, S, q, st));
   } else {
-    RSPL_HIP(ba::finish(P, Lr, E, inl_h, T_h, X_h, L_h, S, q, st));
+    RSPL_HIP(ba::finish(P, Lr, E, reinterpret_cast<const int*>(cb + cl.gmap), inl_h, T_h, X_h, L_h, S, q, st));
   }
   if ((rc = wait_mail(b, q, nullptr))) return rc;
   if (b->prof && b->prof_nb[0]) report_prof(b);
@@ -926,7 +909,7 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   if (nl) memcpy(res->lines, b->stage + dl.L, sizeof(double) * 6 * nl);
   const double* Tout = reinterpret_cast<const double*>(b->stage + dl.T);
   uint8_t* outs[4] = {res->mono_inlier, res->stereo_inlier, res->mono_line_inlier, res->stereo_line_inlier};
-  e = 0;
+  int e = 0;
   for (int t = 0; t < 4; t++) {
     if (outs[t]) memcpy(outs[t], b->stage + dl.inl + e, ne[t]);
     e += ne[t];

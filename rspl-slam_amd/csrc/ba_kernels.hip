@@ -26,7 +26,7 @@ __device__ __forceinline__ void cross3(const double* a, const double* b, double*
 }
 
 // g2o::Line3D::oplus (orthonormal 4-DoF update; vertex_line3d.h:26-29)
-__device__ void line_oplus(double* L, const double* v) {
+__device__ __forceinline__ void line_oplus(double* L, const double* v) {
   const double* w = L;
   const double* d = L + 3;
   const double mx = n3(d), my = n3(w);
@@ -74,7 +74,7 @@ __device__ __forceinline__ SE3 load_T(const double* T) {
 }
 
 // Edge residual for pose estimate T and landmark values lm (point [3] or line [6]).
-__device__ void edge_error(int type, const double* cam, const double* obs, const SE3& T, const double* lm, double* e) {
+__device__ __forceinline__ void edge_error(int type, const double* cam, const double* obs, const SE3& T, const double* lm, double (&e)[4]) {
   double R[9];
   q_to_R(T.q, R);
   if (type < 2) {  // EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ: e = obs - proj(T p)
@@ -92,10 +92,9 @@ __device__ void edge_error(int type, const double* cam, const double* obs, const
   // EdgeSE3ProjectLine / EdgeStereoSE3ProjectLine (edge_project_line.cc:21-42, edge_project_stereo_line.cc:22-51)
   const double fx = cam[0], fy = cam[1], cx = cam[2], cy = cam[3];
   const double Kv0 = -fy * cx, Kv1 = -fx * cy, Kv2 = fx * fy;
-  const int sides = type == 3 ? 2 : 1;
-  for (int side = 0; side < sides; side++) {
-    double t[3] = {T.t[0], T.t[1], T.t[2]};
-    if (side == 1) t[0] -= cam[4] / fx;  // T_right(0,3) -= b, b = bf / fx
+  // both sides spelled out (every index of e / obs static: no scratch)
+  auto side_err = [&](double tx0, const double* o, double& ea, double& eb) {
+    const double t[3] = {tx0, T.t[1], T.t[2]};
     double Rw[3], Rd[3], tx[3];
     mat3_vec(R, lm, Rw);
     mat3_vec(R, lm + 3, Rd);
@@ -103,18 +102,46 @@ __device__ void edge_error(int type, const double* cam, const double* obs, const
     const double w0 = Rw[0] + tx[0], w1 = Rw[1] + tx[1], w2 = Rw[2] + tx[2];
     const double l0 = fy * w0, l1 = fx * w1, l2 = Kv0 * w0 + Kv1 * w1 + Kv2 * w2;
     const double nrm = sqrt(l0 * l0 + l1 * l1);
-    const double* o = obs + 4 * side;
-    e[2 * side + 0] = (o[0] * l0 + o[1] * l1 + l2) / nrm;
-    e[2 * side + 1] = (o[2] * l0 + o[3] * l1 + l2) / nrm;
-  }
+    ea = (o[0] * l0 + o[1] * l1 + l2) / nrm;
+    eb = (o[2] * l0 + o[3] * l1 + l2) / nrm;
+  };
+  side_err(T.t[0], obs, e[0], e[1]);
+  if (type == 3) side_err(T.t[0] - cam[4] / fx, obs + 4, e[2], e[3]);  // T_right(0,3) -= b, b = bf / fx
+}
+
+// a per-type constant of the kernel-argument structs with a select chain: a dynamic index would
+// copy the whole by-value struct to scratch
+__device__ __forceinline__ double pick4(const double (&a)[4], int t) {
+  return t == 0 ? a[0] : t == 1 ? a[1] : t == 2 ? a[2] : a[3];
 }
 
 __device__ __forceinline__ int edim(int t) { return t == 0 ? 2 : t == 1 ? 3 : t == 2 ? 2 : 4; }
 
-// edge e's observation (type t): packed per type
+// point edges only (t < 2), every index static: edge_error's point branch and its chi2 (info I)
+__device__ __forceinline__ double point_error(int t, const double* cam, const double* obs, const SE3& T,
+                                              const double* X, double (&e)[4]) {
+  double R[9], Xc[3];
+  q_to_R(T.q, R);
+  mat3_vec(R, X, Xc);
+  for (int i = 0; i < 3; i++) Xc[i] += T.t[i];
+  const double iz = 1.0 / Xc[2];
+  const double u = cam[0] * Xc[0] * iz + cam[2];
+  const double v = cam[1] * Xc[1] * iz + cam[3];
+  e[0] = obs[0] - u;
+  e[1] = obs[1] - v;
+  e[2] = t == 1 ? obs[2] - (u - cam[4] * iz) : 0.0;
+  e[3] = 0.0;
+  double chi2 = 0;
+  chi2 += e[0] * e[0];
+  chi2 += e[1] * e[1];
+  if (t == 1) chi2 += e[2] * e[2];
+  return chi2 * 1.0;
+}
+
+// edge e's observation (type t): point edges [0, Ep) at stride 4 (u, v, u_r), line edges [Ep, E)
+// at stride 8 after them (edges are in landmark-CSR order: point landmarks first)
 __device__ __forceinline__ const double* obs_of(const Problem& P, int e, int t) {
-  const int od = t == 0 ? 2 : t == 1 ? 3 : t == 2 ? 4 : 8;
-  return P.eobs + P.obase[t] + od * (e - P.lstart[t]);
+  return t < 2 ? P.eobs + 4 * e : P.eobs + 4 * P.Ep + 8 * (e - P.Ep);
 }
 __device__ __forceinline__ int ldim(int t) { return t < 2 ? 3 : 4; }
 __device__ __forceinline__ double einfo(int t) { return t < 2 ? 1.0 : 0.1; }
@@ -277,7 +304,7 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
     for (int k = 0; k < 4; k++) L.err[4 * e + k] = er[k];
     if (A.robust) {
       double r1;
-      huber(chi2, P.delta[t], c, r1);
+      huber(chi2, pick4(P.delta, t), c, r1);
     } else {
       c = chi2;
     }
@@ -415,7 +442,7 @@ __device__ __forceinline__ double edge_weight_of(const Problem& P, const Active&
     for (int k = 0; k < edim(t); k++) chi2 += er[k] * er[k];
     chi2 *= einfo(t);
     double r0, r1;
-    huber(chi2, P.delta[t], r0, r1);
+    huber(chi2, pick4(P.delta, t), r0, r1);
     w *= r1;  // robustInformation = rho'(chi2) * Omega
   }
   return w;
@@ -429,23 +456,10 @@ __device__ __forceinline__ double edge_weight(const Problem& P, const Lin& L, co
 // row, so every index below is a compile-time constant (register resident, no scratch).
 // Writes the pose-side records of edge e (when its pose is optimised) and accumulates
 // the landmark side (Hll 3x3, bl 3) into hl / bv.
-__device__ __forceinline__ void point_edge(const Problem& P, const Lin& L, const Active& A, int e, bool pose_opt,
-                                           const double* Tb, const double* Xg, double (&hl)[9], double (&bv)[3]) {
-  if (A.elevel && A.elevel[e]) {  // outside this phase: exact-zero records, no contribution
-    if (pose_opt) {
-#pragma unroll
-      for (int k = 0; k < 36; k++) L.Hpp[36 * e + k] = 0.0;
-#pragma unroll
-      for (int k = 0; k < 6; k++) L.bp[6 * e + k] = 0.0;
-#pragma unroll
-      for (int k = 0; k < 24; k++) L.Hpl[24 * e + k] = 0.0;
-    }
-    return;
-  }
-  const int t = P.etype[e];
-  const int pose = P.epose[e];
-  const double* cam = P.cams + 5 * P.ecam[e];
-  const SE3 T = load_T(Tb + 8 * pose);
+// point_edge_core: the operands in registers (pose T, camera, landmark, the edge's error er)
+__device__ __forceinline__ void point_edge_core(const Problem& P, const Lin& L, const Active& A, int e, int t,
+                                                bool pose_opt, const SE3& T, const double* cam, const double* Xg,
+                                                const double* er4, double (&hl)[9], double (&bv)[3]) {
   const double fx = cam[0], fy = cam[1], bf = cam[4];
   double R[9], Xc[3];
   q_to_R(T.q, R);
@@ -473,8 +487,7 @@ __device__ __forceinline__ void point_edge(const Problem& P, const Lin& L, const
       Jp[r][3 + c] = -D[r][c]; // -D * I
       Jl[r][c] = -sl;          // -D * R
     }
-  const double w = edge_weight(P, L, A, e, t);
-  const double* er4 = L.err + 4 * e;
+  const double w = edge_weight_of(P, A, er4, t);
   const double er[3] = {er4[0], er4[1], st ? er4[2] : 0.0};
 #pragma unroll
   for (int a = 0; a < 3; a++)
@@ -495,6 +508,31 @@ __device__ __forceinline__ void point_edge(const Problem& P, const Lin& L, const
     for (int b = 0; b < 3; b++) Hpl[a * 4 + b] = w * (Jp[0][a] * Jl[0][b] + Jp[1][a] * Jl[1][b] + Jp[2][a] * Jl[2][b]);
     Hpl[a * 4 + 3] = 0.0;
   }
+}
+
+// an edge outside this phase (level 1 in the second optimize): exact-zero records
+__device__ __forceinline__ void zero_pose_records(const Lin& L, int e) {
+#pragma unroll
+  for (int k = 0; k < 36; k++) L.Hpp[36 * e + k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 6; k++) L.bp[6 * e + k] = 0.0;
+#pragma unroll
+  for (int k = 0; k < 24; k++) L.Hpl[24 * e + k] = 0.0;
+}
+
+// point edges: analytic Jacobians (g2o types_sba).  Mono edges carry a zero third
+// row, so every index below is a compile-time constant (register resident, no scratch).
+// Writes the pose-side records of edge e (when its pose is optimised) and accumulates
+// the landmark side (Hll 3x3, bl 3) into hl / bv.
+__device__ __forceinline__ void point_edge(const Problem& P, const Lin& L, const Active& A, int e, bool pose_opt,
+                                           const double* Tb, const double* Xg, double (&hl)[9], double (&bv)[3]) {
+  if (A.elevel && A.elevel[e]) {  // outside this phase: exact-zero records, no contribution
+    if (pose_opt) zero_pose_records(L, e);
+    return;
+  }
+  const int t = P.etype[e];
+  point_edge_core(P, L, A, e, t, pose_opt, load_T(Tb + 8 * P.epose[e]), P.cams + 5 * P.ecam[e], Xg, L.err + 4 * e, hl,
+                  bv);
 }
 
 __device__ __forceinline__ void atomic_max_pos(double* addr, double v) {
@@ -529,7 +567,7 @@ __device__ __forceinline__ void lin_point_landmarks(const Problem& P, const Lin&
   if (in) {
     const int k1 = A.lm_off[g + 1];
     for (int k = A.lm_off[g] + j; k < k1; k += kGroup)
-      point_edge(P, L, A, A.lm_edges[k], A.lm_pose[k] >= 0, P.T, P.X + 3 * g, hl, bv);
+      point_edge(P, L, A, (k), A.lm_pose[k] >= 0, P.T, P.X + 3 * g, hl, bv);
   }
   group_sum(hl);
   group_sum(bv);
@@ -582,7 +620,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
   // per edge: its attributes and the current (or candidate) line, into LDS
   if (tid < kLineBlk) {
     const bool on = tid < cnt;
-    const int e = on ? A.lm_edges[p0 + tid] : 0;
+    const int e = on ? (p0 + tid) : 0;
     const int t = on ? P.etype[e] : 2;
     const bool live = on && !(A.elevel && A.elevel[e]);  // outside this phase: exact-zero records
     const bool popt = on && A.pidx[P.epose[e]] >= 0;
@@ -636,13 +674,15 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
       for (int k = 0; k < 6; k++) Lp[k] = Lsh[slot][k];
       double er[4] = {0, 0, 0, 0};
       if (wv == 0) {
-        double v[4] = {0, 0, 0, 0};
-        v[d] = sgn;
+        double v[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) v[q] = q == d ? sgn : 0.0;  // static indices: no scratch
         line_oplus(Lp, v);
         edge_error(t, cam, obs, T, Lp, er);
       } else if (wv < 3) {
-        double u[6] = {0, 0, 0, 0, 0, 0};
-        u[d - 4] = sgn;
+        double u[6];
+#pragma unroll
+        for (int q = 0; q < 6; q++) u[q] = q == d - 4 ? sgn : 0.0;
         edge_error(t, cam, obs, se3_mul(se3_exp(u), T), Lp, er);
       } else {
         edge_error(t, cam, obs, T, Lp, er);
@@ -730,7 +770,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
           const double* base = ln < 16 ? L.Hll + ln : L.bl + (ln - 16);
           const int str = ln < 16 ? 16 : 4;
           for (int k = k0; k < k1; k++)
-            sm += __hip_atomic_load(base + (size_t)str * A.lm_edges[k], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sm += __hip_atomic_load(base + (size_t)str * (k), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
           if (ln < 16) S.Hll[16 * gl + ln] = sm;
           else S.bl[4 * gl + ln - 16] = sm;
         }
@@ -818,32 +858,6 @@ __global__ __launch_bounds__(256) void pose_diag_kernel(Problem P, Lin L, Active
     __syncthreads();
   }
   (void)red;
-}
-
-// Landmark CSR, step 1: each edge takes a slot of its landmark's range (order arbitrary)
-__global__ __launch_bounds__(256) void csr_fill_kernel(Problem P, Active A, int* fill, int* lm_edges) {
-  const int e = blockIdx.x * 256 + threadIdx.x;
-  if (e >= A.Ea) return;
-  const int g = P.elm[e];
-  lm_edges[A.lm_off[g] + atomicAdd(fill + g, 1)] = e;
-}
-
-// step 2: one thread per landmark sorts its (short) list by edge id -- the order every
-// per-landmark reduction then follows -- and records the reduced pose of each entry
-__global__ __launch_bounds__(256) void csr_sort_kernel(Problem P, Active A, int* lm_edges, int* lm_pose) {
-  const int g = blockIdx.x * 256 + threadIdx.x;
-  if (g >= A.nL) return;
-  const int k0 = A.lm_off[g], k1 = A.lm_off[g + 1];
-  for (int i = k0 + 1; i < k1; i++) {
-    const int v = lm_edges[i];
-    int j = i - 1;
-    while (j >= k0 && lm_edges[j] > v) {
-      lm_edges[j + 1] = lm_edges[j];
-      j--;
-    }
-    lm_edges[j + 1] = v;
-  }
-  for (int k = k0; k < k1; k++) lm_pose[k] = A.pidx[P.epose[lm_edges[k]]];
 }
 
 // ---------------------------------------------------------------------------
@@ -994,17 +1008,17 @@ __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, c
     if (FILL && cnt && k1 - k0 <= 8) {  // emit from the masks: i ascending, then j ascending
       int q = base + pre - cnt;
       for (unsigned ma = ma1; ma; ma &= ma - 1) {
-        const int e1 = A.lm_edges[k0 + __ffs(ma) - 1];
-        for (unsigned mb = mb1; mb; mb &= mb - 1) pp[q++] = make_int4(e1, A.lm_edges[k0 + __ffs(mb) - 1], g, 0);
+        const int e1 = (k0 + __ffs(ma) - 1);
+        for (unsigned mb = mb1; mb; mb &= mb - 1) pp[q++] = make_int4(e1, (k0 + __ffs(mb) - 1), g, 0);
       }
     } else if (FILL && cnt) {
       int q = base + pre - cnt;
       for (int ib = k0; ib < k1; ib++) {
         if (A.lm_pose[ib] != pa) continue;
-        const int e1 = A.lm_edges[ib];
+        const int e1 = (ib);
         for (int jb = k0; jb < k1; jb++) {
           if (A.lm_pose[jb] != pb) continue;
-          pp[q] = make_int4(e1, A.lm_edges[jb], g, 0);
+          pp[q] = make_int4(e1, (jb), g, 0);
           q++;
         }
       }
@@ -1674,7 +1688,7 @@ __global__ __launch_bounds__(256) void update_kernel(Problem P, Lin L, Active A,
 #pragma unroll
         for (int u = 0; u < 4; u++) {
           const int k = min(kb + u, k1 - 1);
-          es[u] = A.lm_edges[k];
+          es[u] = (k);
           as[u] = kb + u < k1 ? A.lm_pose[k] : -1;
         }
 #pragma unroll
@@ -1754,23 +1768,79 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     return;
   }
   if (!SPEC) nbu = gridDim.x;
-  const int t = blockIdx.x * 256 + threadIdx.x, g = t / kGroup, j = t % kGroup;
-  const bool failed = *S.fail != 0;
+  // the candidate poses, cameras and pose steps of this trial go to LDS once per block, in the same
+  // round trip as each group's landmark-only operands; the group's first edge per lane is fetched
+  // in the next (every later access to them is LDS or registers: two dependent round trips)
+  __shared__ double sT[64 * 8], scam[16 * 5], sx[6 * 32];
+  const int tid = threadIdx.x;
+  const int t = blockIdx.x * 256 + tid, g = t / kGroup, j = t % kGroup;
   const bool in = g < A.nL;
   const bool point = g < P.nq;
   int k0 = 0, k1 = 0;
+  bool act = false;
+  double hll[16], blg[4], lm[6] = {0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int q = 0; q < 16; q++) hll[q] = 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) blg[q] = 0.0;
   if (in) {
     k0 = A.lm_off[g];
     k1 = A.lm_off[g + 1];
+    act = A.lm_act[g] != 0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) hll[q] = S.Hll[16 * g + q];
+#pragma unroll
+    for (int q = 0; q < 4; q++) blg[q] = S.bl[4 * g + q];
+    if (point) {
+#pragma unroll
+      for (int q = 0; q < 3; q++) lm[q] = P.X[3 * g + q];
+    } else {
+#pragma unroll
+      for (int q = 0; q < 6; q++) lm[q] = P.L[6 * (g - P.nq) + q];
+    }
   }
-  const bool upd = in && A.lm_act[g] && !failed;
+  for (int q = tid; q < 8 * P.np; q += 256) sT[q] = P.Tn[q];
+  for (int q = tid; q < 5 * P.ncam; q += 256) scam[q] = P.cams[q];
+  for (int q = tid; q < 6 * A.K; q += 256) sx[q] = S.x[q];
+  const bool failed = *S.fail != 0;
+  // the lane's first edge (most landmarks have <= kGroup edges): everything it needs in one round trip
+  const int kf = k0 + j;
+  const bool has = in && kf < k1;
+  int af = -1, tf = 0, pf = 0, cf = 0, lvf = 0;
+  double Bf[24], of[8];
+  if (has) {
+    af = A.lm_pose[kf];
+    tf = P.etype[kf];
+    pf = P.epose[kf];
+    cf = P.ecam[kf];
+    lvf = A.elevel ? A.elevel[kf] : 0;
+#pragma unroll
+    for (int q = 0; q < 24; q++) Bf[q] = L.Hpl[24 * kf + q];
+    const double* o = obs_of(P, kf, point ? 0 : 2);
+#pragma unroll
+    for (int q = 0; q < 8; q++) of[q] = (q < 3 || !point) ? o[q] : 0.0;
+  }
+  __syncthreads();
+  const bool upd = in && act && !failed;
+  // back-substitution xl = Dinv (bl - sum_e Hpl_e^T xp): the first edge from registers, any later
+  // ones (landmarks with more than kGroup edges) from memory
   double c[4] = {0, 0, 0, 0};
-  if (upd)
-    for (int k = k0 + j; k < k1; k += kGroup) {
+  if (upd) {
+    if (has && af >= 0) {
+      const double* xp = sx + 6 * af;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        double s = 0;
+#pragma unroll
+        for (int r = 0; r < 6; r++) s += Bf[r * 4 + q] * xp[r];
+        c[q] -= s;
+      }
+    }
+    for (int k = kf + kGroup; k < k1; k += kGroup) {
       const int a = A.lm_pose[k];
       if (a < 0) continue;
-      const double* B = L.Hpl + 24 * A.lm_edges[k];
-      const double* xp = S.x + 6 * a;
+      const double* B = L.Hpl + 24 * k;
+      const double* xp = sx + 6 * a;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         double s = 0;
@@ -1779,37 +1849,33 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
         c[q] -= s;
       }
     }
+  }
   group_sum(c);
   double xl[4] = {0, 0, 0, 0};
   double sc = 0, chi = 0;
   if (upd) {
-    double bl[4];
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-      bl[q] = S.bl[4 * g + q];
-      c[q] += bl[q];
-    }
+    for (int q = 0; q < 4; q++) c[q] += blg[q];
     double D[16];
-    const bool ok = lm_dinv(S.Hll + 16 * g, point, lambda, D);
+    const bool ok = lm_dinv(hll, point, lambda, D);
     if (!ok && j == 0) atomicOr(S.fail, 1);
 #pragma unroll
     for (int r = 0; r < 4; r++) xl[r] = D[r * 4] * c[0] + D[r * 4 + 1] * c[1] + D[r * 4 + 2] * c[2] + D[r * 4 + 3] * c[3];
     if (j == 0)
 #pragma unroll
-      for (int q = 0; q < 4; q++) sc += xl[q] * (lambda * xl[q] + bl[q]);
+      for (int q = 0; q < 4; q++) sc += xl[q] * (lambda * xl[q] + blg[q]);
   }
-  double lm[6] = {0, 0, 0, 0, 0, 0};
+  const bool lin_pts = SPEC && spec && in && point;  // linearise the point edges at the candidate
+  double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bv[3] = {0, 0, 0};
   if (in) {
     if (point) {
 #pragma unroll
-      for (int q = 0; q < 3; q++) lm[q] = P.X[3 * g + q] + xl[q];
+      for (int q = 0; q < 3; q++) lm[q] += xl[q];
       if (j == 0)
 #pragma unroll
         for (int q = 0; q < 3; q++) P.Xn[3 * g + q] = lm[q];
     } else {
       const int l = g - P.nq;
-#pragma unroll
-      for (int q = 0; q < 6; q++) lm[q] = P.L[6 * l + q];
       if (upd) line_oplus(lm, xl);
       if (j == 0)
 #pragma unroll
@@ -1822,36 +1888,52 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
         if (j == 0) __hip_atomic_store(lflag + l, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     }
-    for (int k = k0 + j; k < k1; k += kGroup) {
-      const int e = A.lm_edges[k];
-      if (A.elevel && A.elevel[e]) continue;
-      const int te = P.etype[e];
-      const SE3 T = load_T(P.Tn + 8 * P.epose[e]);
+    // robust cost of the landmark's edges at the candidate (+ the point edges' linearisation)
+    auto edge_cost = [&](int k, int te, int pose, int cam, int lev, const double (&ob)[8], int a) {
+      if (lev) {
+        if (lin_pts && a >= 0) zero_pose_records(Ls, k);
+        return;
+      }
+      const SE3 T = load_T(sT + 8 * pose);
+      const double* cm = scam + 5 * cam;
       double er[4] = {0, 0, 0, 0};
-      edge_error(te, P.cams + 5 * P.ecam[e], obs_of(P, e, te), T, lm, er);
-      double chi2 = 0;
-      for (int q = 0; q < edim(te); q++) chi2 += er[q] * er[q];
-      chi2 *= einfo(te);
+      double chi2;
+      if (point) {
+        chi2 = point_error(te, cm, ob, T, lm, er);
+      } else {
+        edge_error(te, cm, ob, T, lm, er);
+        chi2 = 0;
 #pragma unroll
-      for (int q = 0; q < 4; q++) L.err[4 * e + q] = er[q];
+        for (int q = 0; q < 4; q++)
+          if (q < edim(te)) chi2 += er[q] * er[q];
+        chi2 *= einfo(te);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; q++) L.err[4 * k + q] = er[q];
       double cst = chi2;
       if (A.robust) {
         double r1;
-        huber(chi2, P.delta[te], cst, r1);
+        huber(chi2, pick4(P.delta, te), cst, r1);
       }
-      L.rho0[e] = cst;
+      L.rho0[k] = cst;
       chi += cst;
+      if (lin_pts) point_edge_core(P, Ls, A, k, te, a >= 0, T, cm, lm, er, hl, bv);
+    };
+    if (has) edge_cost(kf, tf, pf, cf, lvf, of, af);
+    for (int k = kf + kGroup; k < k1; k += kGroup) {
+      const int te = P.etype[k];
+      const double* o = obs_of(P, k, te);
+      double ob[8];
+#pragma unroll
+      for (int q = 0; q < 8; q++) ob[q] = (q < 3 || !point) ? o[q] : 0.0;
+      edge_cost(k, te, P.epose[k], P.ecam[k], A.elevel ? A.elevel[k] : 0, ob, A.lm_pose[k]);
     }
   }
   if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 1);
-  if (SPEC && spec) {  // point landmarks: linearise at the candidate (the errors just written by this lane)
-    double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bv[3] = {0, 0, 0};
-    if (in && point)
-      for (int k = k0 + j; k < k1; k += kGroup)
-        point_edge(P, Ls, A, A.lm_edges[k], A.lm_pose[k] >= 0, P.Tn, lm, hl, bv);
+  if (SPEC && spec) {  // point landmarks: the landmark blocks of the candidate's linearisation
     group_sum(hl);
     group_sum(bv);
-    if (in && point && j == 0 && A.lm_act[g]) {
+    if (in && point && j == 0 && act) {
       double* H = Ss.Hll + 16 * g;
 #pragma unroll
       for (int i = 0; i < 9; i++) H[i] = hl[i];
@@ -1918,7 +2000,7 @@ __global__ __launch_bounds__(256) void landmark_active_kernel(Active A, const ui
   const int g = blockIdx.x * blockDim.x + threadIdx.x;
   if (g >= A.nL) return;
   uint8_t on = 0;
-  for (int k = A.lm_off[g]; k < A.lm_off[g + 1]; k++) on |= level[A.lm_edges[k]] == 0;
+  for (int k = A.lm_off[g]; k < A.lm_off[g + 1]; k++) on |= level[(k)] == 0;
   lm_act[g] = on;
 }
 
@@ -1941,7 +2023,7 @@ __device__ __forceinline__ bool edge_inlier(const Problem& P, const Lin& L, int 
   double chi2;
   bool depth_ok;
   edge_status(P, L, e, chi2, depth_ok);
-  return chi2 <= P.th[P.etype[e]] && depth_ok;
+  return chi2 <= pick4(P.th, P.etype[e]) && depth_ok;
 }
 __device__ __forceinline__ void classify_edge(const Problem& P, const Lin& L, int e, uint8_t* level, uint8_t* inlier,
                                               int final_pass) {
@@ -1952,7 +2034,7 @@ __device__ __forceinline__ void classify_edge(const Problem& P, const Lin& L, in
   double chi2;
   bool depth_ok;
   edge_status(P, L, e, chi2, depth_ok);
-  if (chi2 > P.th[P.etype[e]] || !depth_ok) level[e] = 1;
+  if (chi2 > pick4(P.th, P.etype[e]) || !depth_ok) level[e] = 1;
 }
 
 __global__ __launch_bounds__(256) void classify_kernel(Problem P, Lin L, int E, uint8_t* level, uint8_t* inlier,
@@ -1963,11 +2045,11 @@ __global__ __launch_bounds__(256) void classify_kernel(Problem P, Lin L, int E, 
 
 // end of a call: final inlier flags + the final T / X / L written straight into host-mapped
 // memory; the last block (ticket) posts the mailbox once every block's writes are out
-__global__ __launch_bounds__(256) void finish_kernel(Problem P, Lin L, int E, uint8_t* inl, double* Th, double* Xh,
-                                                     double* Lh, Sys S, unsigned long long seq) {
+__global__ __launch_bounds__(256) void finish_kernel(Problem P, Lin L, int E, const int* gmap, uint8_t* inl, double* Th,
+                                                     double* Xh, double* Lh, Sys S, unsigned long long seq) {
   __shared__ int last;
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < E) classify_edge(P, L, i, nullptr, inl, 1);
+  if (i < E) inl[gmap[i]] = edge_inlier(P, L, i) ? 1 : 0;
   if (i < 8 * P.np) Th[i] = P.T[i];
   if (i < 3 * P.nq) Xh[i] = P.X[i];
   if (i < 6 * P.nl) Lh[i] = P.L[i];
@@ -2191,17 +2273,11 @@ hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, un
   return hipGetLastError();
 }
 
-hipError_t finish(const Problem& P, const Lin& L, int E, uint8_t* inl, double* Th, double* Xh, double* Lh, Sys& S,
-                  unsigned long long seq, hipStream_t s) {
+hipError_t finish(const Problem& P, const Lin& L, int E, const int* gmap, uint8_t* inl, double* Th, double* Xh,
+                  double* Lh, Sys& S, unsigned long long seq, hipStream_t s) {
   const int n = std::max(std::max(E, 8 * P.np), std::max(3 * P.nq, 6 * P.nl));
-  hipLaunchKernelGGL(finish_kernel, dim3(std::max((n + 255) / 256, 1)), dim3(256), 0, s, P, L, E, inl, Th, Xh, Lh, S,
-                     seq);
-  return hipGetLastError();
-}
-
-hipError_t build_csr(const Problem& P, const Active& A, int* fill, int* lm_edges, int* lm_pose, hipStream_t s) {
-  if (A.Ea > 0) hipLaunchKernelGGL(csr_fill_kernel, dim3((A.Ea + 255) / 256), dim3(256), 0, s, P, A, fill, lm_edges);
-  if (A.nL > 0) hipLaunchKernelGGL(csr_sort_kernel, dim3((A.nL + 255) / 256), dim3(256), 0, s, P, A, lm_edges, lm_pose);
+  hipLaunchKernelGGL(finish_kernel, dim3(std::max((n + 255) / 256, 1)), dim3(256), 0, s, P, L, E, gmap, inl, Th, Xh,
+                     Lh, S, seq);
   return hipGetLastError();
 }
 

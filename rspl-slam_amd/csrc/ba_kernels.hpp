@@ -7,8 +7,11 @@ namespace rspl {
 namespace ba {
 
 // Edge types (same order as rspl_ba_problem): 0 mono point, 1 stereo point,
-// 2 mono line, 3 stereo line.  Unified edge arrays in type order; observations packed per type
-// (2 / 3 / 4 / 8 doubles per edge): edge e of type t at eobs + obase[t] + od(t) (e - lstart[t]).
+// 2 mono line, 3 stereo line.  Unified edge arrays in LANDMARK-CSR order, laid out by the host:
+// the edges of landmark g are [lm_off[g], lm_off[g+1]) (input order within a landmark), point
+// landmarks first, so an edge's position is its index everywhere (records, levels, errors) and
+// gmap maps it back to the caller's edge id.  Observations: point edges at eobs + 4 e (u, v, u_r),
+// line edges at eobs + 4 Ep + 8 (e - Ep).
 struct Problem {
   const double* cams;    // [nc][5] fx fy cx cy bf
   double* T;             // [np][8] T_cw: q (w x y z), t (x y z), pad   (current state)
@@ -18,13 +21,13 @@ struct Problem {
   double* Xn;
   double* Ln;
   int np, nq, nl;
+  int ncam;              // cameras (<= 16)
   const int8_t* etype;   // [E]
   const int* epose;      // [E]
   const int* elm;        // [E] landmark index: point id, or nq + line id
   const int* ecam;       // [E]
   const double* eobs;    // packed observations (see above)
-  int lstart[5];         // first edge of each type (lstart[4] = E)
-  int obase[4];          // offset of each type's observations in eobs
+  int Ep;                // point edges (the first line edge's position)
   double delta[4];       // Huber deltas per type
   double th[4];          // chi2 thresholds per type
 };
@@ -42,9 +45,8 @@ struct Lin {             // per-edge linearisation records (indexed by edge id)
 struct Active {          // active structure of one optimize() phase
   int Ea;                // active edges: every edge id in [0, Ea) (input order: points, then lines)
   const int* pidx;       // [np] reduced pose index or -1
-  const int* lm_off;     // [nL+1] CSR of the edges by landmark (edge ids ascending within a landmark)
-  const int* lm_edges;
-  const int* lm_pose;    // [Ea] reduced pose of lm_edges[k] (or -1)
+  const int* lm_off;     // [nL+1] CSR of the edges by landmark (= edge positions, see Problem)
+  const int* lm_pose;    // [Ea] reduced pose of edge k (or -1)
   const uint8_t* lm_act; // [nL]
   const int* pairs;      // [npairs][2] reduced pose pairs (a <= b)
   int npairs;
@@ -148,9 +150,6 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
 // (skipped on the device when the iteration is the last one).
 hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq, hipStream_t s,
                      const Spec& spec);
-// landmark CSR from the per-landmark offsets: atomic slots, then each landmark's list sorted by
-// edge id (deterministic) with its reduced poses; fill[] must be zero on entry
-hipError_t build_csr(const Problem& P, const Active& A, int* fill, int* lm_edges, int* lm_pose, hipStream_t s);
 // edge-pair lists of the pose pairs (count, offsets, fill; A.pp_* are not read)
 hipError_t build_pairs(const Active& A, int* pp_cnt, int* pp_off, int4* pp, hipStream_t s);
 // lm_act[g] = landmark g has an edge of level 0 (the second optimize's active landmarks)
@@ -158,8 +157,8 @@ hipError_t landmark_active(const Active& A, const uint8_t* level, uint8_t* lm_ac
 hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8_t* inlier, int final_pass,
                     hipStream_t s);
 // final inlier flags + T / X / L into host-mapped memory, then the mailbox post of seq
-hipError_t finish(const Problem& P, const Lin& L, int E, uint8_t* inl, double* Th, double* Xh, double* Lh, Sys& S,
-                  unsigned long long seq, hipStream_t s);
+hipError_t finish(const Problem& P, const Lin& L, int E, const int* gmap, uint8_t* inl, double* Th, double* Xh,
+                  double* Lh, Sys& S, unsigned long long seq, hipStream_t s);
 // ---- landmark-sharded pieces (rspl_ba_set_shard): the host interleaves the all-reduces ----
 // trial, part 1: Schur chunks of this rank's edge pairs -> pairfin; the landmark-inversion flag
 // is staged into pairfin[npairs * 48] so it is summed with the system
