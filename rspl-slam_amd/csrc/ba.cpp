@@ -18,6 +18,7 @@
 #include <cstring>
 #include <limits>
 #include <numeric>
+#include <string>
 #include <vector>
 
 #include "ba_kernels.hpp"
@@ -135,9 +136,9 @@ void carve(F& ar, rspl_ba* b) {
     else ar.template take<Tp>(n ? n : 1);
   };
   take(b->Tb, K * 8); take(b->Xb, nq * 3); take(b->Lb, nl * 6);
-  take(b->err, E * 4); take(b->rho0, E); take(b->Hpp_e, E * 36); take(b->bp_e, E * 6); take(b->Hll_e, E * 16);
+  take(b->err, E * 4); take(b->rho0, E); take(b->Hpp_e, E * 21); take(b->bp_e, E * 6); take(b->Hll_e, E * 16);
   take(b->bl_e, E * 4); take(b->Hpl_e, E * 24);
-  take(b->Hpp_s, E * 36); take(b->bp_s, E * 6); take(b->Hll_es, E * 16); take(b->bl_es, E * 4); take(b->Hpl_s, E * 24);
+  take(b->Hpp_s, E * 21); take(b->bp_s, E * 6); take(b->Hll_es, E * 16); take(b->bl_es, E * 4); take(b->Hpl_s, E * 24);
   take(b->Hll_s, NL * 16); take(b->bl_s, NL * 4);
   take(b->lm_act2, NL);
   take(b->Hll, NL * 16); take(b->bl, NL * 4); take(b->bp, K * 6);
@@ -257,7 +258,7 @@ void report_prof(rspl_ba* b) {
   const unsigned long long p0 = first(ba::kProfPc, 0, npc), u0 = first(ba::kProfUe, 0, nue);
   fprintf(stderr,
           "ba_prof us: pcstarts %.1f pcloop %.1f pcticket %.1f pcend %.1f gap %.1f asm %.1f factor %.1f back %.1f"
-          " poses %.1f gap %.1f uestarts %.1f upd %.1f pointlin %.1f groupsend %.1f lineswait %.1f linescomp %.1f"
+          " poses %.1f gap %.1f uestarts %.1f loaded %.1f grpdone %.1f groupsend %.1f lineswait %.1f linescomp %.1f"
           " linesend %.1f sApanel %.1f sAtrail %.1f sBpanel %.1f sBtrail %.1f\n",
           us(p0, last(ba::kProfPc, 0, npc, 0)), us(p0, last(ba::kProfPc, 0, npc, 1)),
           us(p0, last(ba::kProfPc, 0, npc, 2)), us(p0, last(ba::kProfPc, 0, npc, 3)),
@@ -266,6 +267,11 @@ void report_prof(rspl_ba* b) {
           us(u0, last(ba::kProfUe, 0, nbu, 2)), us(u0, last(ba::kProfUe, 0, nbu, 3)),
           us(u0, last(ba::kProfUe, nbu, nue, 1)), us(u0, last(ba::kProfUe, nbu, nue, 2)),
           us(u0, last(ba::kProfUe, nbu, nue, 3)), us(h[1], h[5]), us(h[5], h[6]), us(h[6], h[7]), us(h[7], h[8]));
+  if (getenv("RSPL_BA_SOLVE") == nullptr || std::string(getenv("RSPL_BA_SOLVE")) == "blk4") {
+    fprintf(stderr, "ba_steps us:");  // blocked solve: each pose block's panel, from the assembly's end
+    for (int k = 5; k < 15 && h[k]; k++) fprintf(stderr, " %.2f", us(h[1], h[k]));
+    fprintf(stderr, "\n");
+  }
   b->prof_nb[0] = 0;
   (void)hipMemset(b->prof, 0, sizeof(unsigned long long) * ba::kProfLen);
 }

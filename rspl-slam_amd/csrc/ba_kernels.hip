@@ -10,6 +10,9 @@
 #include <algorithm>
 #include <cfloat>
 #include <cstdint>
+#include <cstdlib>
+#include <string>
+#include <type_traits>
 
 #include "ba_kernels.hpp"
 #include "se3_device.hpp"
@@ -114,6 +117,10 @@ __device__ __forceinline__ void edge_error(int type, const double* cam, const do
 __device__ __forceinline__ double pick4(const double (&a)[4], int t) {
   return t == 0 ? a[0] : t == 1 ? a[1] : t == 2 ? a[2] : a[3];
 }
+
+// per-edge Hpp records keep the upper triangle (21 doubles, row-major): the blocks are exactly
+// symmetric (the same products summed in the same order for (a, b) and (b, a))
+__host__ __device__ constexpr int pk6(int a, int b) { return a * 6 - a * (a - 1) / 2 + (b - a); }
 
 __device__ __forceinline__ int edim(int t) { return t == 0 ? 2 : t == 1 ? 3 : t == 2 ? 2 : 4; }
 
@@ -430,7 +437,10 @@ __device__ __forceinline__ void store_contrib(const Lin& L, int e, int o, double
   if (o < 16) L.Hll[16 * e + o] = v;
   else if (o < 20) L.bl[4 * e + o - 16] = v;
   else if (!pose_opt) return;
-  else if (o < 56) L.Hpp[36 * e + o - 20] = v;
+  else if (o < 56) {
+    const int a = (o - 20) / 6, b = (o - 20) % 6;
+    if (b >= a) L.Hpp[21 * e + pk6(a, b)] = v;
+  }
   else if (o < 62) L.bp[6 * e + o - 56] = v;
   else L.Hpl[24 * e + o - 62] = v;
 }
@@ -496,13 +506,13 @@ __device__ __forceinline__ void point_edge_core(const Problem& P, const Lin& L, 
 #pragma unroll
   for (int a = 0; a < 3; a++) bv[a] += -w * (Jl[0][a] * er[0] + Jl[1][a] * er[1] + Jl[2][a] * er[2]);
   if (!pose_opt) return;
-  double* Hpp = L.Hpp + 36 * e;
+  double* Hpp = L.Hpp + 21 * e;
   double* bp = L.bp + 6 * e;
   double* Hpl = L.Hpl + 24 * e;
 #pragma unroll
   for (int a = 0; a < 6; a++) {
 #pragma unroll
-    for (int b = 0; b < 6; b++) Hpp[a * 6 + b] = w * (Jp[0][a] * Jp[0][b] + Jp[1][a] * Jp[1][b] + Jp[2][a] * Jp[2][b]);
+    for (int b = a; b < 6; b++) Hpp[pk6(a, b)] = w * (Jp[0][a] * Jp[0][b] + Jp[1][a] * Jp[1][b] + Jp[2][a] * Jp[2][b]);
     bp[a] = -w * (Jp[0][a] * er[0] + Jp[1][a] * er[1] + Jp[2][a] * er[2]);
 #pragma unroll
     for (int b = 0; b < 3; b++) Hpl[a * 4 + b] = w * (Jp[0][a] * Jl[0][b] + Jp[1][a] * Jl[1][b] + Jp[2][a] * Jl[2][b]);
@@ -513,7 +523,7 @@ __device__ __forceinline__ void point_edge_core(const Problem& P, const Lin& L, 
 // an edge outside this phase (level 1 in the second optimize): exact-zero records
 __device__ __forceinline__ void zero_pose_records(const Lin& L, int e) {
 #pragma unroll
-  for (int k = 0; k < 36; k++) L.Hpp[36 * e + k] = 0.0;
+  for (int k = 0; k < 21; k++) L.Hpp[21 * e + k] = 0.0;
 #pragma unroll
   for (int k = 0; k < 6; k++) L.bp[6 * e + k] = 0.0;
 #pragma unroll
@@ -825,9 +835,9 @@ __global__ __launch_bounds__(256) void pose_diag_kernel(Problem P, Lin L, Active
   if (e < A.Ea) {
     a = A.pidx[P.epose[e]];
     if (a >= 0) {
-      const double* H = L.Hpp + 36 * e;
+      const double* H = L.Hpp + 21 * e;
 #pragma unroll
-      for (int i = 0; i < 6; i++) d[i] = H[i * 7];
+      for (int i = 0; i < 6; i++) d[i] = H[pk6(i, i)];
     }
   }
   // per pose: each wave's butterfly (poses absent from the wave skipped), then the 4 wave sums in
@@ -1413,8 +1423,12 @@ __device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys
     const double zj = readlane64(z, j);
     z = fma(-l, zj, z);
     wave_sync();
+    // the column's entries below the pivot: every LDS read issued before the first use (one wait)
+    double wk[N];
 #pragma unroll
-    for (int k = j + 1; k < N; k++) a[k] = fma(-l, w.col[j & 1][k], a[k]);
+    for (int k = j + 1; k < N; k++) wk[k] = w.col[j & 1][k];
+#pragma unroll
+    for (int k = j + 1; k < N; k++) a[k] = fma(-l, wk[k], a[k]);
   }
   if (!ok) {
     if (lane == 0) atomicOr(S.fail, 1);
@@ -1422,10 +1436,10 @@ __device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys
   }
   if (lane == 0) prof_stamp(S, 2);
   // y = D^-1 z; backward L^T x = y (lane i: y_i -= L_ki x_k for k > i, k descending)
-  double y = 0.0;
+  double dgl = 1.0;
 #pragma unroll
-  for (int k = 0; k < N; k++)
-    if (k == lane) y = z * rcp64(a[k]);
+  for (int k = 0; k < N; k++) dgl = k == lane ? a[k] : dgl;
+  double y = z * rcp64(dgl);
   double lt[N];
 #pragma unroll
   for (int k = 0; k < N; k++) lt[k] = row && k > lane ? w.Lm[lane][k] : 0.0;
@@ -1460,6 +1474,189 @@ __device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys
     }
   }
   if (lane == 0) S.out[4] = sc;
+}
+
+// ---------------------------------------------------------------------------
+// Reduced camera system for K <= 10 optimised poses on one 256-thread workgroup, blocked by the
+// 6x6 pose blocks and held in REGISTERS: lane i of every wave owns row i; wave w owns the block
+// columns b = w, w + 4, w + 8 (a[q][cc] = S[i][6 (w + 4 q) + cc]).  Step s (right-looking LDL^T):
+//   the owner wave of block column s factors it column by column (pivots and the column's
+//   entries by readlane, no LDS) -> panel l_ic and W_ic = l_ic d_c into LDS -> one barrier ->
+//   every wave: z_i -= l_ic z_c (forward substitution, z replicated in every wave) and the trailing
+//   update a_ik -= sum_c l_ic W_kc of its own later block columns (W rows broadcast from LDS).
+// One barrier per pose block (the panel buffer alternates by step parity); then y = D^-1 z and the
+// backward substitution L^T x = y in wave 0 from the stored panels; candidate poses + LM scale.
+// ---------------------------------------------------------------------------
+template <int N, int I = 0, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+struct Blk4Lds {
+  double pan[2][64][6];    // l_ic of step s's block column (rows >= the pivot; 0 above)
+  double wpan[2][64][6];   // W_ic = l_ic d_c
+  double Lall[10][64][6];  // every step's l_ic (backward substitution)
+  double dg[64];           // pivots
+  double xs[64];           // solution (pose lanes)
+  int bad;
+};
+
+template <int K>
+__device__ __forceinline__ void solve_blk4(Problem P, const Active& A, const Sys& S, double lambda, Blk4Lds& w,
+                                           bool coherent) {
+  constexpr int N = 6 * K, NQ = (K + 3) / 4;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  int pose_a = -1;
+  double Tp0[8];
+  if (wv == 0 && lane < P.np) {
+    pose_a = A.pidx[lane];
+#pragma unroll
+    for (int k = 0; k < 8; k++) Tp0[k] = P.T[8 * lane + k];
+  }
+  const int pa = lane / 6, r = lane - 6 * pa;
+  const bool row = lane < N;
+  auto ld = [&](int idx) {
+    return coherent ? __hip_atomic_load(S.pairfin + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : S.pairfin[idx];
+  };
+  double a[NQ][6];
+  double z = 0.0, bpl = 0.0;
+#pragma unroll
+  for (int q = 0; q < NQ; q++) {
+    const int b = wv + 4 * q;
+#pragma unroll
+    for (int cc = 0; cc < 6; cc++) {
+      const int k = 6 * b + cc;
+      double v = 0.0;
+      if (row && b < K && k <= lane) {
+        if (b == pa) v = ld(48 * pair_index(pa, pa, K) + r * 6 + cc) + (cc == r ? lambda : 0.0);
+        else v = ld(48 * pair_index(b, pa, K) + cc * 6 + r);
+      }
+      a[q][cc] = v;
+    }
+  }
+  if (row) {
+    const int dg = 48 * pair_index(pa, pa, K);
+    bpl = ld(dg + 36 + r);
+    z = bpl - ld(dg + 42 + r);
+  }
+  if (tid == 0) w.bad = coherent ? __hip_atomic_load(S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *S.fail;
+  __syncthreads();
+  if (w.bad) return;  // uniform: a landmark block failed to invert
+  if (tid == 0) prof_stamp(S, 1);
+  // owner of block column s: LDL^T of its 6 columns, column by column (pivots and the column's
+  // entries by readlane) -> panel s into LDS
+  bool ok = true;
+  auto factor_block = [&](auto sc) {
+    constexpr int s = decltype(sc)::value, qs = s >> 2, buf = s & 1, c0 = 6 * s;
+#pragma unroll
+    for (int c = 0; c < 6; c++) {
+      const double d = readlane64(a[qs][c], c0 + c);
+      ok = ok && d > 0.0;
+      const double rc = rcp64(d);
+      const double wic = a[qs][c];
+      const double l = lane > c0 + c ? wic * rc : 0.0;
+#pragma unroll
+      for (int c2 = c + 1; c2 < 6; c2++) a[qs][c2] = fma(-l, readlane64(wic, c0 + c2), a[qs][c2]);
+      w.pan[buf][lane][c] = l;
+      w.wpan[buf][lane][c] = l * d;
+      w.Lall[s][lane][c] = l;
+      if (lane == c) w.dg[c0 + c] = d;
+    }
+    if (lane == 0 && !ok) w.bad = 1;
+  };
+  // trailing update of block column b (register slot q) with panel s
+  auto update_block = [&](int q, const double (&l6)[6], int buf, int b) {
+#pragma unroll
+    for (int cc = 0; cc < 6; cc++) {
+      const double* Wk = w.wpan[buf][6 * b + cc];
+      double t = a[q][cc];
+#pragma unroll
+      for (int c = 0; c < 6; c++) t = fma(-l6[c], Wk[c], t);
+      a[q][cc] = t;
+    }
+  };
+  if (wv == 0) factor_block(std::integral_constant<int, 0>{});
+  // step s: every wave applies panel s (forward substitution of z, its later block columns); the
+  // owner of block column s + 1 updates that one first and factors it before its other updates, so
+  // the next panel is out as early as possible.  One barrier per step (panel buffers alternate).
+  static_for<K>([&](auto sc) {
+    constexpr int s = decltype(sc)::value, buf = s & 1, c0 = 6 * s;
+    __syncthreads();
+    if (tid == 0) prof_stamp(S, 5 + s);  // step s's panel is out (RSPL_BA_PROF)
+    if (w.bad) return;
+    double l6[6];
+#pragma unroll
+    for (int c = 0; c < 6; c++) l6[c] = w.pan[buf][lane][c];
+#pragma unroll
+    for (int c = 0; c < 6; c++) z = fma(-l6[c], readlane64(z, c0 + c), z);
+    if constexpr (s + 1 < K) {
+      constexpr int sn = s + 1, qn = sn >> 2;
+      if (wv == (sn & 3)) {
+        update_block(qn, l6, buf, sn);
+        factor_block(std::integral_constant<int, sn>{});
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NQ; q++) {
+      const int b = wv + 4 * q;
+      if (b <= s + 1 || b >= K) continue;  // wave-uniform; block s + 1 was updated above
+      update_block(q, l6, buf, b);
+    }
+  });
+  if (w.bad) {
+    if (tid == 0) atomicOr(S.fail, 1);
+    return;
+  }
+  if (wv != 0) return;
+  if (tid == 0) prof_stamp(S, 2);
+  // y = D^-1 z; backward L^T x = y (lane i: y_i -= l_ki x_k for k > i, k descending)
+  double y = row ? z * rcp64(w.dg[lane]) : 0.0;
+  double lt[N];
+#pragma unroll
+  for (int k = 0; k < N; k++) lt[k] = row && k > lane ? w.Lall[pa][k][r] : 0.0;
+#pragma unroll
+  for (int k = N - 1; k >= 0; k--) y = fma(-lt[k], readlane64(y, k), y);
+  const double x = y;
+  if (tid == 0) prof_stamp(S, 3);
+  if (row) S.x[lane] = x;
+  w.xs[lane] = x;
+  wave_sync();
+  double sc = row ? x * (lambda * x + bpl) : 0.0;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
+  if (lane < P.np) {
+    double* Tq = P.Tn + 8 * lane;
+    if (pose_a >= 0) {
+      double xp[6];
+#pragma unroll
+      for (int q = 0; q < 6; q++) xp[q] = w.xs[6 * pose_a + q];
+      const SE3 rr = se3_mul(se3_exp(xp), load_T(Tp0));
+      for (int k = 0; k < 4; k++) Tq[k] = rr.q[k];
+      for (int k = 0; k < 3; k++) Tq[4 + k] = rr.t[k];
+      Tq[7] = 0;
+    } else {
+#pragma unroll
+      for (int k = 0; k < 8; k++) Tq[k] = Tp0[k];
+    }
+  }
+  if (lane == 0) S.out[4] = sc;
+}
+
+template <int K>
+__global__ __launch_bounds__(256) void schur_blk4_kernel(Problem P, Active A, Sys S, double lambda) {
+  __shared__ Blk4Lds w;
+  if (S.lm) {
+    LmView v;
+    if (!lm_view(S, v)) return;
+    lambda = v.lambda;
+    if (v.cur) bank_state(P);
+  }
+  if (threadIdx.x == 0) prof_stamp(S, 0);
+  solve_blk4<K>(P, A, S, lambda, w, false);
+  if (threadIdx.x == 0) prof_stamp(S, 4);
 }
 
 // standalone single-wave solve (sharded path: after the pairfin all-reduce)
@@ -1521,7 +1718,9 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
     for (int i = 0; i < 24; i++) H1[i] = L.Hpl[24 * e1 + i];
     if (diag) {
 #pragma unroll
-      for (int i = 0; i < 36; i++) Hp[i] = L.Hpp[36 * e1 + i];
+      for (int r = 0; r < 6; r++)
+#pragma unroll
+        for (int c = 0; c < 6; c++) Hp[r * 6 + c] = L.Hpp[21 * e1 + (r <= c ? pk6(r, c) : pk6(c, r))];
 #pragma unroll
       for (int i = 0; i < 6; i++) bpv[i] = L.bp[6 * e1 + i];
 #pragma unroll
@@ -1821,6 +2020,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     for (int q = 0; q < 8; q++) of[q] = (q < 3 || !point) ? o[q] : 0.0;
   }
   __syncthreads();
+  if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 1);  // operands loaded
   const bool upd = in && act && !failed;
   // back-substitution xl = Dinv (bl - sum_e Hpl_e^T xp): the first edge from registers, any later
   // ones (landmarks with more than kGroup edges) from memory
@@ -1929,7 +2129,6 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
       edge_cost(k, te, P.epose[k], P.ecam[k], A.elevel ? A.elevel[k] : 0, ob, A.lm_pose[k]);
     }
   }
-  if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 1);
   if (SPEC && spec) {  // point landmarks: the landmark blocks of the candidate's linearisation
     group_sum(hl);
     group_sum(bv);
@@ -2149,6 +2348,16 @@ __global__ __launch_bounds__(256) void shard_finish_kernel(Problem P, int E, con
 int shard_red_len(int K, int nranks) { return 6 * K + nranks + 3; }
 bool fast_path(int K) { return 6 * K > 0 && 6 * K <= kCholLdsMax; }
 bool wave_path(int K) { return K > 0 && K <= kWaveSolveMaxK; }
+// reduced-system solver for K <= 10 (RSPL_BA_SOLVE: "blk4" default, "wave", "lds"; K > 10: "lds")
+static int solve_mode(int K) {
+  static const int m = [] {
+    const char* e = getenv("RSPL_BA_SOLVE");
+    if (e && std::string(e) == "wave") return 1;
+    if (e && std::string(e) == "lds") return 0;
+    return 2;
+  }();
+  return wave_path(K) ? m : 0;
+}
 
 // ---------------------------------------------------------------------------
 int errors_blocks(int Ea) { return Ea > 0 ? (Ea + 255) / 256 : 1; }
@@ -2209,6 +2418,17 @@ static void launch_chunks(const Problem& P, const Lin& L, const Active& A, const
   }
 }
 
+static void launch_blk4_solve(const Problem& P, const Active& A, const Sys& S, double lambda, hipStream_t s) {
+  switch (A.K) {
+#define RSPL_BLK4_CASE(k) \
+  case k: hipLaunchKernelGGL(schur_blk4_kernel<k>, dim3(1), dim3(256), 0, s, P, A, S, lambda); break;
+    RSPL_BLK4_CASE(1) RSPL_BLK4_CASE(2) RSPL_BLK4_CASE(3) RSPL_BLK4_CASE(4) RSPL_BLK4_CASE(5)
+    RSPL_BLK4_CASE(6) RSPL_BLK4_CASE(7) RSPL_BLK4_CASE(8) RSPL_BLK4_CASE(9) RSPL_BLK4_CASE(10)
+#undef RSPL_BLK4_CASE
+    default: break;
+  }
+}
+
 static void launch_wave_solve(const Problem& P, const Active& A, const Sys& S, double lambda, hipStream_t s) {
   switch (A.K) {
 #define RSPL_SOLVE_CASE(k) \
@@ -2223,11 +2443,13 @@ static void launch_wave_solve(const Problem& P, const Active& A, const Sys& S, d
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
                  hipStream_t s, const Spec* spec, bool* fused) {
   *fused = false;
-  const bool wave = wave_path(A.K);
-  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, lambda, L, S, wave, s);
+  const int mode = solve_mode(A.K);
+  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, lambda, L, S, mode == 1, s);
   const int n = 6 * A.K;
   if (fast_path(A.K)) {
-    if (!wave) {
+    if (mode == 2) {
+      launch_blk4_solve(P, A, S, lambda, s);
+    } else if (mode == 0) {
       hipError_t e = ensure_schur_attr();
       if (e != hipSuccess) return e;
       hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
@@ -2259,9 +2481,11 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
 hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq, hipStream_t s,
                      const Spec& spec) {
   if (!S.lm || !fast_path(A.K)) return hipErrorInvalidValue;
-  const bool wave = wave_path(A.K);
-  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, 0.0, spec.Ls, spec.Ss, wave, s);
-  if (!wave) {
+  const int mode = solve_mode(A.K);
+  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, 0.0, spec.Ls, spec.Ss, mode == 1, s);
+  if (mode == 2) {
+    launch_blk4_solve(P, A, S, 0.0, s);
+  } else if (mode == 0) {
     hipError_t e = ensure_schur_attr();
     if (e != hipSuccess) return e;
     const int n = 6 * A.K;
@@ -2312,7 +2536,10 @@ hipError_t trial_solve(const Problem& P, const Lin& L, const Active& A, Sys& S, 
   hipLaunchKernelGGL(shard_fail_adopt_kernel, dim3(1), dim3(1), 0, s, S, S.pairfin + (size_t)A.npairs * 48);
   const int n = 6 * A.K;
   if (fast_path(A.K)) {
-    if (wave_path(A.K)) {
+    const int mode = solve_mode(A.K);
+    if (mode == 2) {
+      launch_blk4_solve(P, A, S, lambda, s);
+    } else if (mode == 1) {
       launch_wave_solve(P, A, S, lambda, s);
     } else {
       hipError_t e = ensure_schur_attr();

@@ -35,7 +35,7 @@ struct Problem {
 struct Lin {             // per-edge linearisation records (indexed by edge id)
   double* err;           // [E][4] last computed error
   double* rho0;          // [E] robust chi2 (or chi2)
-  double* Hpp;           // [E][36]
+  double* Hpp;           // [E][21] upper triangle, row-major (pk6)
   double* bp;            // [E][6]
   double* Hll;           // [E][16]
   double* bl;            // [E][4]
@@ -120,7 +120,7 @@ struct Sys {
 };
 constexpr int kProfPc = 16, kProfUe = kProfPc + 4 * 4096, kProfLen = kProfUe + 4 * 4096;
 
-constexpr int kLmChunk = 256;  // landmarks per Schur chunk (4 per lane)
+constexpr int kLmChunk = 128;  // landmarks per Schur chunk (2 per lane)
 constexpr int kLineBlk = 8;    // line edges per linearisation workgroup
 
 // errors (+ fused final reduction and mailbox post with sequence number seq)

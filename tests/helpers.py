@@ -57,3 +57,35 @@ def unexplained_match_disagreements(Zo, i0, i1, i0r, i1r, tol):
     bad = [("row", int(i)) for i in np.nonzero(i0 != i0r)[0] if not row_near(i)]
     bad += [("col", int(j)) for j in np.nonzero(i1 != i1r)[0] if not col_near(j)]
     return bad
+
+
+def _R_of_q(q):
+    """rotation of a unit quaternion (x, y, z, w)"""
+    x, y, z, w = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def line_residuals(prob, pose_q, pose_p, lines):
+    """Residuals of every line edge at a BA result (EdgeSE3ProjectLine / EdgeStereoSE3ProjectLine,
+    edge_project_line.cc:21-42, edge_project_stereo_line.cc:22-51): the quantity the BA minimises
+    for a line, independent of the Pluecker coordinates' weakly observed directions."""
+    out = []
+    for name, sides in (("mono_line", 1), ("stereo_line", 2)):
+        d = getattr(prob, name)
+        for p, l, c, o in zip(d["pose"], d["lm"], d["cam"], d["obs"]):
+            fx, fy, cx, cy, bf = prob.cameras[c]
+            Rwc = _R_of_q(pose_q[p] / np.linalg.norm(pose_q[p]))
+            Rcw, tcw = Rwc.T, -Rwc.T @ pose_p[p]
+            w, dv = lines[l][:3], lines[l][3:]
+            for side in range(sides):
+                t = tcw.copy()
+                if side == 1:
+                    t[0] -= bf / fx
+                wc = Rcw @ w + np.cross(t, Rcw @ dv)
+                l0, l1, l2 = fy * wc[0], fx * wc[1], -fy * cx * wc[0] - fx * cy * wc[1] + fx * fy * wc[2]
+                n = np.hypot(l0, l1)
+                ob = o[4 * side:4 * side + 4]
+                out += [(ob[0] * l0 + ob[1] * l1 + l2) / n, (ob[2] * l0 + ob[3] * l1 + l2) / n]
+    return np.array(out)
