@@ -103,6 +103,7 @@ void carve(F& ar, rspl_sg* s) {
   for (int i = 0; i < 2; i++) {
     take(s->Qf[i], T * 256); take(s->Kf[i], (size_t)B * 2 * 256 * s->ldv); take(s->Vf[i], (size_t)B * 2 * 256 * s->ldv);
   }
+
   take(s->cpl, 2 * B * ld * ld); take(s->Z, 2 * B * ld * ld); take(s->ug, B * ld * (s->rbG ? 2 * s->rbG : 1)); take(s->vg, B * ld);
   if (s->sink_scratch) take(s->cplT, B * ld * ld);
   take(s->dbg_alpha, 4);
@@ -483,6 +484,7 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
       const char* v = getenv("RSPL_SG_GNN");  // A/B knob: "unfused" = four launches per layer
       return v && std::string(v) == "unfused";
     }();
+    auto layer = [&](sg::LayerArgs& la, int) { return sg::gnn_layer(la, B, st); };
     if (!unfused) {  // layer 0's q / k / v (prologue launch), then one fused launch per layer
       static unsigned long long* lprobe = nullptr;  // debug: RSPL_SG_LPROBE
       static const bool lprobing = getenv("RSPL_SG_LPROBE") != nullptr;
@@ -496,7 +498,7 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
         la.X = s->X; la.Xh = s->Xh;
         la.Wq = s->fwqkv; la.bq = s->bqkv;
         la.n0 = d_n0; la.n1 = d_n1; la.nmax = nm; la.nt = s->ldv / 32; la.qkv_only = 1;
-        RSPL_HIP(sg::gnn_layer(la, B, st));
+        RSPL_HIP(layer(la, -1));
       }
       for (int l = 0; l < kLayers; l++) {
         sg::LayerArgs la{};
@@ -509,7 +511,7 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
         la.Wq = s->fwqkv + (size_t)ln * 256 * 768; la.bq = s->bqkv + (size_t)ln * 768;
         la.n0 = d_n0; la.n1 = d_n1; la.nmax = nm; la.nt = s->ldv / 32; la.cross = l & 1; la.last = l == kLayers - 1;
         la.probe = lprobe;
-        RSPL_HIP(sg::gnn_layer(la, B, st));
+        RSPL_HIP(layer(la, l));
       }
       if (lprobing) {
         unsigned long long h[8];
@@ -614,7 +616,8 @@ static int sink_status(rspl_sg* s, int npairs, uint32_t* pair_flags) {
   }
   if (pair_flags) *pair_flags = f;
   if (f) {
-    set_error("sinkhorn: cross-workgroup exchange timed out (pair mask 0x%x); results of those pairs are invalid", f);
+    set_error("superglue: cross-workgroup exchange (GNN quads / Sinkhorn) timed out (pair mask 0x%x); results of "
+              "those pairs are invalid", f);
     return RSPL_E_DEVICE;
   }
   return RSPL_OK;
