@@ -42,8 +42,6 @@ struct rspl_ba {
   // system
   double *Hll, *bl, *bp, *S, *x, *partial, *partial2;
   unsigned* lm_ctr;  // [max_lines] line-landmark tickets (zeroed at create, re-armed by the kernel)
-  unsigned* lflag;   // [max_lines] release flags of the fused speculative linearisation (zeroed at create)
-  unsigned tag = 0;  // last flag value used
   unsigned long long* prof = nullptr;  // RSPL_BA_PROF: timing trace of one trial per call
   int prof_nb[3] = {0, 0, 0};          // its pair_chunk / update_errors grid sizes, group blocks
   // landmark CSR (filled on the device) and the Schur chunk / pose-pair sums
@@ -148,7 +146,6 @@ void carve(F& ar, rspl_ba* b) {
   // partial2: scale partials, and the pose-diagonal partials (K x E/256 x 6) of the lambda init
   take(b->partial2, std::max(std::max((size_t)b->maxV / 256, nblk) + 2, K * (E / 256 + 1) * 6));
   take(b->lm_ctr, nl);
-  take(b->lflag, nl);
   const size_t npairs = K * (K + 1) / 2, nchk = std::max<size_t>((NL + ba::kLmChunk - 1) / ba::kLmChunk, 1);
   take(b->chunk, npairs * nchk * 48); take(b->pairfin, npairs * 48 + 8); take(b->pair_ctr, npairs + 1);  // + the solve ticket
   take(b->red, 6 * K + kMaxRanks + 8);
@@ -326,8 +323,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
   auto enqueue = [&](int n) -> int {
     for (int k = 0; k < n; k++, queued++) {
       q = ++b->seq;
-      if (++b->tag == 0) b->tag = 1;  // 0 is the flags' initial value
-      ba::Spec sp{Ls, Ss, b->lflag, b->tag};
+      ba::Spec sp{Ls, Ss};
       const bool traced = b->prof && queued == 3 && !b->prof_nb[0];
       if (traced) {
         S.prof = b->prof;
@@ -446,8 +442,7 @@ int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Acti
       Ss.Hll = b->Hll_s; Ss.bl = b->bl_s;
       bool fused = false;
       if (!sh) {
-        if (++b->tag == 0) b->tag = 1;  // 0 is the flags' initial value
-        ba::Spec sp{Ls, Ss, b->lflag, b->tag};
+          ba::Spec sp{Ls, Ss};
         const bool traced = b->prof && it == 3 && qmax == 0 && !b->prof_nb[0];
         if (traced) {
           S.prof = sp.Ss.prof = b->prof;
@@ -527,7 +522,6 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
       hipMalloc((void**)&b->cbuf, CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE, 8 * (size_t)b->maxE).bytes) !=
           hipSuccess ||
       hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
-      hipMemset(b->lflag, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
       hipMemset(b->pair_ctr, 0, sizeof(unsigned) * (b->maxK * (b->maxK + 1) / 2 + 1)) != hipSuccess) {
     set_error("BA stream / mailbox allocation failed");
     rspl_ba_destroy(b);
@@ -607,12 +601,10 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   const std::string msg = rspl_last_error();
   if (hipStreamSynchronize(b->stream) != hipSuccess ||
       hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
-      hipMemset(b->lflag, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
       hipMemset(b->pair_ctr, 0, sizeof(unsigned) * (b->maxK * (b->maxK + 1) / 2 + 1)) != hipSuccess) {
     set_error("%s; the BA stream could not be drained: recreate the handle", msg.c_str());
     return rc;
   }
-  b->tag = 0;
   set_error("%s", msg.c_str());
   return rc;
 }

@@ -593,6 +593,74 @@ __device__ __forceinline__ void lin_point_landmarks(const Problem& P, const Lin&
   if (maxd) atomic_max_pos(S.out + 2, fmax(fabs(hl[0]), fmax(fabs(hl[4]), fabs(hl[8]))));
 }
 
+// Gauss-Jordan inverse with partial pivoting, fully unrolled (register resident).
+// Progressive conditional row swaps select the same pivot as a max search.
+template <int N>
+__device__ __forceinline__ bool small_inv(const double* A, double* I) {
+  double M[N][2 * N];
+#pragma unroll
+  for (int i = 0; i < N; i++)
+#pragma unroll
+    for (int j = 0; j < N; j++) {
+      M[i][j] = A[i * N + j];
+      M[i][N + j] = (i == j) ? 1.0 : 0.0;
+    }
+  bool ok = true;
+#pragma unroll
+  for (int c = 0; c < N; c++) {
+#pragma unroll
+    for (int r = c + 1; r < N; r++) {
+      const bool sw = fabs(M[r][c]) > fabs(M[c][c]);
+#pragma unroll
+      for (int k = 0; k < 2 * N; k++) {
+        const double a = M[c][k], b = M[r][k];
+        M[c][k] = sw ? b : a;
+        M[r][k] = sw ? a : b;
+      }
+    }
+    ok = ok && (M[c][c] != 0.0);
+    const double iv = 1.0 / M[c][c];
+#pragma unroll
+    for (int k = 0; k < 2 * N; k++) M[c][k] *= iv;
+#pragma unroll
+    for (int r = 0; r < N; r++)
+      if (r != c) {
+        const double f = M[r][c];
+#pragma unroll
+        for (int k = 0; k < 2 * N; k++) M[r][k] -= f * M[c][k];
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < N; i++)
+#pragma unroll
+    for (int j = 0; j < N; j++) I[i * N + j] = M[i][N + j];
+  return ok;
+}
+
+// (Hll_g + lambda I)^-1, zero-padded to 4x4 for points
+__device__ __forceinline__ bool lm_dinv(const double* Hll, bool point, double lambda, double (&D)[16]) {
+  if (point) {
+    double H[9], Di[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) H[i] = Hll[i];
+    H[0] += lambda;
+    H[4] += lambda;
+    H[8] += lambda;
+    const bool ok = small_inv<3>(H, Di);
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 4; j++) D[i * 4 + j] = (i < 3 && j < 3) ? Di[i * 3 + j] : 0.0;
+    return ok;
+  }
+  double H[16];
+#pragma unroll
+  for (int i = 0; i < 16; i++) H[i] = Hll[i];
+#pragma unroll
+  for (int i = 0; i < 4; i++) H[i * 5] += lambda;
+  return small_inv<4>(H, D);
+}
+
 // line edges: g2o's numeric central difference (delta 1e-9).  A workgroup takes the
 // <= kLineBlk = 8 edges of a run of whole line landmarks (A.ltab, CSR order) and splits the 20
 // perturbed error evaluations of each by kind, so no
@@ -602,14 +670,15 @@ __device__ __forceinline__ void lin_point_landmarks(const Problem& P, const Lin&
 // records in CSR order into the landmark block itself; only a landmark with more than
 // kLineBlk edges (split over workgroups) goes through per-edge records written through (sc1)
 // and a last-edge ticket.
-// SPEC: the speculative linearisation (at the candidate P.Tn / P.Ln) inside
-// update_errors_kernel.  The block waits for the groups that update its edges' line landmarks
-// (lflag[l] == tag; the groups run in lower-numbered blocks, which are dispatched first),
-// takes the candidate lines from them through coherent loads and evaluates each edge's own
-// error there in wave 3.
+// SPEC: the speculative linearisation (at the candidate P.Tn / candidate lines) inside
+// update_errors_kernel, from the kernel's start: wave 0 forms the candidate of each of the block's
+// line landmarks itself -- the same back-substitution as the landmark groups (8 lanes per
+// landmark, the same butterfly, from the current records Lc / Sc) -- so it never waits for the
+// groups; wave 3 evaluates each edge's own error at the candidate.
 template <bool SPEC>
 __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const Active& A, const Sys& S, int blk,
-                                          bool maxd, const unsigned* lflag, unsigned tag,
+                                          bool maxd, const Lin* Lc = nullptr, const Sys* Sc = nullptr,
+                                          double lambda = 0.0, bool failed = false,
                                           unsigned long long* stamp = nullptr) {
   __shared__ double ev[kLineBlk][20][4];
   __shared__ double J[kLineBlk][4 * 6 + 4 * 4];
@@ -627,6 +696,49 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
     on = einfo_s[slot][2] & 1;
     live = einfo_s[slot][2] & 2;
   };
+  __shared__ double cand[kLineBlk][6];  // SPEC: the candidate line of landmark gb + m
+  if (SPEC && wv == 0) {
+    const int m = lane >> 3, j = lane & 7;
+    const int g = gb + m;
+    const bool in = g < ge;
+    const int l = g - P.nq;
+    const bool upd = in && A.lm_act[g] && !failed;
+    double c[4] = {0, 0, 0, 0};
+    if (upd)
+      for (int k = A.lm_off[g] + j; k < A.lm_off[g + 1]; k += kGroup) {
+        const int a = A.lm_pose[k];
+        if (a < 0) continue;
+        const double* B = Lc->Hpl + 24 * k;
+        const double* xp = S.x + 6 * a;
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          double sm = 0;
+#pragma unroll
+          for (int r = 0; r < 6; r++) sm += B[r * 4 + q] * xp[r];
+          c[q] -= sm;
+        }
+      }
+    group_sum(c);
+    double lmv[6] = {0, 0, 0, 0, 0, 0};
+    if (in) {
+#pragma unroll
+      for (int q = 0; q < 6; q++) lmv[q] = P.L[6 * l + q];
+    }
+    if (upd) {
+#pragma unroll
+      for (int q = 0; q < 4; q++) c[q] += Sc->bl[4 * g + q];
+      double D[16];
+      lm_dinv(Sc->Hll + 16 * g, false, lambda, D);
+      double xl[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) xl[r] = D[r * 4] * c[0] + D[r * 4 + 1] * c[1] + D[r * 4 + 2] * c[2] + D[r * 4 + 3] * c[3];
+      line_oplus(lmv, xl);
+    }
+    if (in && j == 0)
+#pragma unroll
+      for (int q = 0; q < 6; q++) cand[m][q] = lmv[q];
+  }
+  if (SPEC) __syncthreads();
   // per edge: its attributes and the current (or candidate) line, into LDS
   if (tid < kLineBlk) {
     const bool on = tid < cnt;
@@ -641,11 +753,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
     if (live) {
       const int l = P.elm[e] - P.nq;
       if (SPEC) {
-        while (__hip_atomic_load(lflag + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != tag)
-          __builtin_amdgcn_s_sleep(1);
-        asm volatile("" ::: "memory");
-        for (int k = 0; k < 6; k++) Lsh[tid][k] = __hip_atomic_load(P.Ln + 6 * l + k, __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_AGENT);
+        for (int k = 0; k < 6; k++) Lsh[tid][k] = cand[P.elm[e] - gb][k];
       } else {
         for (int k = 0; k < 6; k++) Lsh[tid][k] = P.L[6 * l + k];
       }
@@ -798,7 +906,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
 // diagonals to S.out[2] (computeLambdaInit); speculative passes leave it alone.
 __global__ __launch_bounds__(256) void linearize_kernel(Problem P, Lin L, Active A, Sys S, int nbq, int maxd) {
   if ((int)blockIdx.x < nbq) lin_point_landmarks(P, L, A, S, blockIdx.x * 256 + threadIdx.x, maxd != 0);
-  else lin_lines<false>(P, L, A, S, blockIdx.x - nbq, maxd != 0, nullptr, 0u);
+  else lin_lines<false>(P, L, A, S, blockIdx.x - nbq, maxd != 0);
 }
 
 // deterministic block reduction of NV values per thread: wave shuffles, then waves in order
@@ -876,74 +984,6 @@ __global__ __launch_bounds__(256) void pose_diag_kernel(Problem P, Lin L, Active
 // ---------------------------------------------------------------------------
 // Schur complement for damping lambda
 // ---------------------------------------------------------------------------
-// Gauss-Jordan inverse with partial pivoting, fully unrolled (register resident).
-// Progressive conditional row swaps select the same pivot as a max search.
-template <int N>
-__device__ __forceinline__ bool small_inv(const double* A, double* I) {
-  double M[N][2 * N];
-#pragma unroll
-  for (int i = 0; i < N; i++)
-#pragma unroll
-    for (int j = 0; j < N; j++) {
-      M[i][j] = A[i * N + j];
-      M[i][N + j] = (i == j) ? 1.0 : 0.0;
-    }
-  bool ok = true;
-#pragma unroll
-  for (int c = 0; c < N; c++) {
-#pragma unroll
-    for (int r = c + 1; r < N; r++) {
-      const bool sw = fabs(M[r][c]) > fabs(M[c][c]);
-#pragma unroll
-      for (int k = 0; k < 2 * N; k++) {
-        const double a = M[c][k], b = M[r][k];
-        M[c][k] = sw ? b : a;
-        M[r][k] = sw ? a : b;
-      }
-    }
-    ok = ok && (M[c][c] != 0.0);
-    const double iv = 1.0 / M[c][c];
-#pragma unroll
-    for (int k = 0; k < 2 * N; k++) M[c][k] *= iv;
-#pragma unroll
-    for (int r = 0; r < N; r++)
-      if (r != c) {
-        const double f = M[r][c];
-#pragma unroll
-        for (int k = 0; k < 2 * N; k++) M[r][k] -= f * M[c][k];
-      }
-  }
-#pragma unroll
-  for (int i = 0; i < N; i++)
-#pragma unroll
-    for (int j = 0; j < N; j++) I[i * N + j] = M[i][N + j];
-  return ok;
-}
-
-// (Hll_g + lambda I)^-1, zero-padded to 4x4 for points
-__device__ __forceinline__ bool lm_dinv(const double* Hll, bool point, double lambda, double (&D)[16]) {
-  if (point) {
-    double H[9], Di[9];
-#pragma unroll
-    for (int i = 0; i < 9; i++) H[i] = Hll[i];
-    H[0] += lambda;
-    H[4] += lambda;
-    H[8] += lambda;
-    const bool ok = small_inv<3>(H, Di);
-#pragma unroll
-    for (int i = 0; i < 4; i++)
-#pragma unroll
-      for (int j = 0; j < 4; j++) D[i * 4 + j] = (i < 3 && j < 3) ? Di[i * 3 + j] : 0.0;
-    return ok;
-  }
-  double H[16];
-#pragma unroll
-  for (int i = 0; i < 16; i++) H[i] = Hll[i];
-#pragma unroll
-  for (int i = 0; i < 4; i++) H[i * 5] += lambda;
-  return small_inv<4>(H, D);
-}
-
 // one edge pair's Schur terms (Y = Hpl_e1 Dinv_g formed on the fly) added into acc[48];
 // H1 / H2 / Hp / bpv / blv already in registers (diag: e1 == e2, H2 == H1)
 __device__ __forceinline__ void schur_pair(const double (&H1)[24], const double (&B)[24], bool diag,
@@ -1932,15 +1972,14 @@ __global__ __launch_bounds__(256) void update_kernel(Problem P, Lin L, Active A,
 // (ticket) sums the block partials in order and posts {chi2, scale, maxdiag, fail} + seq.
 // Spec: the speculative linearisation of the candidate fused into update_errors_kernel
 // (records into the spare set Ls / Ss).  Blocks [0, nbu) are the landmark groups: besides the
-// update and the errors, a point group linearises its landmark's edges at the candidate
-// (each lane re-reading only the errors it wrote itself) and a line group publishes the
-// candidate line as soon as it has it (coherent stores, then lflag[l] = tag).  Blocks
-// [nbu, ...) are line-edge waves (lin_lines<true>).  The mailbox ticket counts only the
-// group blocks, so the host decides while the line waves still run.
+// update and the errors, a point group linearises its landmark's edges at the candidate from
+// the errors in its registers, and a line group writes the candidate line.  Blocks [nbu, ...) are
+// line-edge workgroups (lin_lines<true>) that form their landmarks' candidates themselves, so
+// they run from the kernel's start.  The mailbox ticket counts only the group blocks, so the
+// host decides while the line workgroups still run.
 template <bool SPEC>
 __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Active A, Sys S, double lambda,
-                                                            unsigned long long seq, Lin Ls, Sys Ss, int nbu,
-                                                            unsigned* lflag, unsigned tag) {
+                                                            unsigned long long seq, Lin Ls, Sys Ss, int nbu) {
   __shared__ double red[4 * 2];
   __shared__ int last;
   const bool stamp = threadIdx.x == 0 && blockIdx.x < 4096;
@@ -1961,7 +2000,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
   }
   if (SPEC && (int)blockIdx.x >= nbu) {
     if (!spec) return;
-    lin_lines<true>(P, Ls, A, Ss, blockIdx.x - nbu, false, lflag, tag,
+    lin_lines<true>(P, Ls, A, Ss, blockIdx.x - nbu, false, &L, &S, lambda, *S.fail != 0,
                     S.prof ? S.prof + kProfUe + 4 * blockIdx.x + 1 : nullptr);
     if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 3);
     return;
@@ -2079,14 +2118,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
       if (upd) line_oplus(lm, xl);
       if (j == 0)
 #pragma unroll
-        for (int q = 0; q < 6; q++) {
-          if (SPEC) __hip_atomic_store(P.Ln + 6 * l + q, lm[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          else P.Ln[6 * l + q] = lm[q];
-        }
-      if (SPEC) {  // the candidate line is out: release its line-edge waves
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (j == 0) __hip_atomic_store(lflag + l, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
+        for (int q = 0; q < 6; q++) P.Ln[6 * l + q] = lm[q];
     }
     // robust cost of the landmark's edges at the candidate (+ the point edges' linearisation)
     auto edge_cost = [&](int k, int te, int pose, int cam, int lev, const double (&ob)[8], int a) {
@@ -2458,11 +2490,10 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
     if (spec) {
       const int nbl = A.n_lblk;
       hipLaunchKernelGGL(update_errors_kernel<true>, dim3(nbu + nbl), dim3(256), 0, s, P, L, A, S, lambda, seq,
-                         spec->Ls, spec->Ss, nbu, spec->lflag, spec->tag);
+                         spec->Ls, spec->Ss, nbu);
       *fused = true;
     } else {
-      hipLaunchKernelGGL(update_errors_kernel<false>, dim3(nbu), dim3(256), 0, s, P, L, A, S, lambda, seq, L, S, 0,
-                         nullptr, 0u);
+      hipLaunchKernelGGL(update_errors_kernel<false>, dim3(nbu), dim3(256), 0, s, P, L, A, S, lambda, seq, L, S, 0);
     }
     return hipGetLastError();
   }
@@ -2493,7 +2524,7 @@ hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, un
   }
   const int nbu = update_errors_blocks(A), nbl = A.n_lblk;
   hipLaunchKernelGGL(update_errors_kernel<true>, dim3(nbu + nbl), dim3(256), 0, s, P, L, A, S, 0.0, seq, spec.Ls,
-                     spec.Ss, nbu, spec.lflag, spec.tag);
+                     spec.Ss, nbu);
   return hipGetLastError();
 }
 
@@ -2547,7 +2578,7 @@ hipError_t trial_solve(const Problem& P, const Lin& L, const Active& A, Sys& S, 
       hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
     }
     hipLaunchKernelGGL(update_errors_kernel<false>, dim3(update_errors_blocks(A)), dim3(256), 0, s, P, L, A, S, lambda,
-                       0ull, L, S, 0, nullptr, 0u);
+                       0ull, L, S, 0);
     return hipGetLastError();
   }
   if (n > 0) {

@@ -120,7 +120,7 @@ struct Sys {
 };
 constexpr int kProfPc = 16, kProfUe = kProfPc + 4 * 4096, kProfLen = kProfUe + 4 * 4096;
 
-constexpr int kLmChunk = 128;  // landmarks per Schur chunk (2 per lane)
+constexpr int kLmChunk = 256;  // landmarks per Schur chunk (4 per lane; 128 measured: 1440 chunk waves exceed one dispatch round)
 constexpr int kLineBlk = 8;    // line edges per linearisation workgroup
 
 // errors (+ fused final reduction and mailbox post with sequence number seq)
@@ -137,8 +137,6 @@ hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A =
 struct Spec {
   Lin Ls;            // spare edge records (err / rho0 shared with the current set)
   Sys Ss;            // spare landmark blocks Hll / bl
-  unsigned* lflag;   // [max_lines] line-landmark release flags (zeroed at create)
-  unsigned tag;      // this trial's flag value (distinct per launch)
 };
 // one LM trial: Schur complement, Cholesky, back-substitution + candidate state, its cost;
 // with spec on the fast path also the candidate's linearisation (*fused = true)
