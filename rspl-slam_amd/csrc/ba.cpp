@@ -19,6 +19,7 @@
 #include <limits>
 #include <numeric>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "ba_kernels.hpp"
@@ -29,6 +30,11 @@ using namespace rspl;
 struct rspl_ba {
   rspl_ba_config cfg{};
   hipStream_t stream = nullptr;
+  // the per-call edge-pair lists are built on a side stream, beside the first errors /
+  // linearisation; the first trial waits for them (pairs_ready)
+  hipStream_t side = nullptr;
+  hipEvent_t staged = nullptr, pairs_ready = nullptr;
+  bool pairs_pending = false;
   Arena arena;
   int maxE = 0, maxL = 0, maxK = 0, maxV = 0;
   // candidate state (ping-pong partners of the call buffer's T / X / L)
@@ -286,6 +292,14 @@ void accept_swap(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, bool lin) 
   S.Hll = b->Hll; S.bl = b->bl;
 }
 
+// the first trial of a call waits for the side stream's edge-pair lists
+int join_pairs(rspl_ba* b) {
+  if (!b->pairs_pending) return RSPL_OK;
+  b->pairs_pending = false;
+  RSPL_HIP(hipStreamWaitEvent(b->stream, b->pairs_ready, 0));
+  return RSPL_OK;
+}
+
 // RSPL_BA_HOSTLM=1: the host decides every trial (the mailbox round trip per trial)
 bool host_lm() {
   static const bool v = getenv("RSPL_BA_HOSTLM") != nullptr;
@@ -302,7 +316,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
                  double* chi2_out, int* done_out) {
   hipStream_t st = b->stream;
   S.lm = b->lmctl;
-  unsigned long long q = ++b->seq;
+  unsigned long long q = 0;  // the first errors post nothing: the host waits for the trials only
   RSPL_HIP(ba::compute_errors(P, Lr, A, S, q, st));
   RSPL_HIP(ba::linearize(P, Lr, A, S, true, st));
   q = ++b->seq;
@@ -332,6 +346,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
         b->prof_nb[2] = ba::update_errors_blocks(A);
       }
       S.lm_slot = queued & 1;
+      S.lm_post = k == n - 1;
       const hipError_t e = ba::trial_dev(P, Lr, A, S, q, st, sp);
       S.prof = nullptr;
       if (e != hipSuccess) {
@@ -343,6 +358,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
     return RSPL_OK;
   };
   int rc;
+  if ((rc = join_pairs(b))) return rc;
   if ((rc = enqueue(iters))) return rc;
   double v[4];
   for (;;) {
@@ -415,6 +431,7 @@ int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Acti
     RSPL_HIP(ba::post(S, q, st, &A));  // posts chi2 (S.out[0]) and the max diagonal (S.out[2])
   }
   if ((rc = wait_mail(b, q, v))) return rc;
+  if ((rc = join_pairs(b))) return rc;
   double currentChi = v[0];
   double lambda = 1e-5 * v[2], ni = 2;  // computeLambdaInit: tau * max diagonal
   int done = 0;
@@ -517,6 +534,9 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipStreamCreateWithPriority(&b->side, hipStreamNonBlocking, prio_hi) != hipSuccess ||
+      hipEventCreateWithFlags(&b->staged, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&b->pairs_ready, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc((void**)&b->mail, sizeof(ba::Mail), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&b->mail_dev, b->mail, 0) != hipSuccess ||
       hipMalloc((void**)&b->cbuf, CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE, 8 * (size_t)b->maxE).bytes) !=
@@ -541,20 +561,25 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
 
 extern "C" int rspl_ba_use_reserved_cus(rspl_ba* b, int reserve_cus) {
   RSPL_CHECK_ARG(b, "rspl_ba_use_reserved_cus: NULL handle");
-  hipStream_t ns = nullptr;
-  if (reserve_cus > 0) {
-    std::vector<uint32_t> mask;
-    int rc = cu_mask(reserve_cus, true, mask);
-    if (rc) return rc;
-    RSPL_HIP(hipExtStreamCreateWithCUMask(&ns, (uint32_t)mask.size(), mask.data()));
-  } else {
-    int lo = 0, hi = 0;
-    RSPL_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    RSPL_HIP(hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, hi));
+  hipStream_t ns[2] = {nullptr, nullptr};
+  for (hipStream_t& n : ns) {
+    if (reserve_cus > 0) {
+      std::vector<uint32_t> mask;
+      int rc = cu_mask(reserve_cus, true, mask);
+      if (rc) return rc;
+      RSPL_HIP(hipExtStreamCreateWithCUMask(&n, (uint32_t)mask.size(), mask.data()));
+    } else {
+      int lo = 0, hi = 0;
+      RSPL_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+      RSPL_HIP(hipStreamCreateWithPriority(&n, hipStreamNonBlocking, hi));
+    }
   }
   RSPL_HIP(hipStreamSynchronize(b->stream));
+  RSPL_HIP(hipStreamSynchronize(b->side));
   RSPL_HIP(hipStreamDestroy(b->stream));
-  b->stream = ns;
+  RSPL_HIP(hipStreamDestroy(b->side));
+  b->stream = ns[0];
+  b->side = ns[1];
   return RSPL_OK;
 }
 
@@ -575,6 +600,7 @@ extern "C" int rspl_ba_set_shard(rspl_ba* b, int rank, int nranks, rspl_allreduc
 extern "C" void rspl_ba_destroy(rspl_ba* b) {
   if (!b) return;
   if (b->stream) (void)hipStreamSynchronize(b->stream);
+  if (b->side) (void)hipStreamSynchronize(b->side);
   if (b->gbuf) (void)hipFree(b->gbuf);
   b->arena.release();
   if (b->cbuf) (void)hipFree(b->cbuf);
@@ -583,6 +609,9 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
   if (b->stage) (void)hipHostFree(b->stage);
   if (b->mail) (void)hipHostFree(b->mail);
   if (b->stream) (void)hipStreamDestroy(b->stream);
+  if (b->side) (void)hipStreamDestroy(b->side);
+  if (b->staged) (void)hipEventDestroy(b->staged);
+  if (b->pairs_ready) (void)hipEventDestroy(b->pairs_ready);
   delete b;
 }
 
@@ -599,7 +628,8 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   const int rc = ba_local_impl(b, pr, res);
   if (rc != RSPL_E_DEVICE || !b) return rc;
   const std::string msg = rspl_last_error();
-  if (hipStreamSynchronize(b->stream) != hipSuccess ||
+  b->pairs_pending = false;
+  if (hipStreamSynchronize(b->stream) != hipSuccess || hipStreamSynchronize(b->side) != hipSuccess ||
       hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
       hipMemset(b->pair_ctr, 0, sizeof(unsigned) * (b->maxK * (b->maxK + 1) / 2 + 1)) != hipSuccess) {
     set_error("%s; the BA stream could not be drained: recreate the handle", msg.c_str());
@@ -643,39 +673,62 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
         }
     }
   }
-  // optional host-side stage timing (RSPL_BA_TIMING=1): prep, build1, opt1, classify, build2, opt2, final
+  // optional host-side stage timing (RSPL_BA_TIMING=1), in microseconds since the previous mark
   static const bool timing = getenv("RSPL_BA_TIMING") != nullptr;
   using clk = std::chrono::steady_clock;
-  clk::time_point tmark[8];
+  clk::time_point tmark[16];
+  const char* tname[16];
   int ntm = 0;
-  auto mark = [&]() {
-    if (timing) tmark[ntm++] = clk::now();
+  auto mark = [&](const char* name) {
+    if (timing && ntm < 16) {
+      tname[ntm] = name;
+      tmark[ntm++] = clk::now();
+    }
   };
-  mark();
+  mark("start");
   // ---- one staging region for the whole call, mirrored by the device call buffer ----
   const int32_t* poses[4] = {pr->mono_pose, pr->stereo_pose, pr->mono_line_pose, pr->stereo_line_pose};
   const int32_t* lms[4] = {pr->mono_point, pr->stereo_point, pr->mono_line_line, pr->stereo_line_line};
   const int32_t* cams[4] = {pr->mono_camera, pr->stereo_camera, pr->mono_line_camera, pr->stereo_line_camera};
   const double* obs[4] = {pr->mono_obs, pr->stereo_obs, pr->mono_line_obs, pr->stereo_line_obs};
-  const int od[4] = {2, 3, 4, 8};
   // pass 1: validate, count the local edges per landmark, mark the poses with edges
   b->lm_cnt.assign(nL + 1, 0);
   b->pact.assign(np, 0);
   int Ep = 0;  // local point edges
+  int* cnt = b->lm_cnt.data();
+  uint8_t* pact = b->pact.data();
   for (int t = 0; t < 4; t++) {
     RSPL_CHECK_ARG(ne[t] == 0 || (poses[t] && lms[t] && obs[t]), "NULL edge arrays");
     const int n = ne[t], lmax = t < 2 ? nq : nl, loff = t < 2 ? 0 : nq;
     const int32_t *pt = poses[t], *lt = lms[t], *ct = cams[t];
+    // branch-free validation (unsigned compares), the offending edge looked up only on failure
+    bool bad = false;
     for (int i = 0; i < n; i++) {
-      const int p = pt[i], l = lt[i], c = ct ? ct[i] : 0;
-      RSPL_CHECK_ARG(p >= 0 && p < np && l >= 0 && l < lmax && c >= 0 && c < pr->n_cameras,
-                     "edge %d of type %d references a missing vertex/camera", i, t);
-      b->pact[p] = 1;  // a pose is optimised when it has an edge on ANY rank: K agrees across ranks
-      if (!owned(t, i)) continue;
-      b->lm_cnt[loff + l + 1]++;
-      Ep += t < 2;
+      const unsigned p = (unsigned)pt[i], l = (unsigned)lt[i];
+      bad |= (p >= (unsigned)np) | (l >= (unsigned)lmax);
+    }
+    if (ct)
+      for (int i = 0; i < n; i++) bad |= (unsigned)ct[i] >= (unsigned)pr->n_cameras;
+    if (bad)
+      for (int i = 0; i < n; i++) {
+        const int p = pt[i], l = lt[i], c = ct ? ct[i] : 0;
+        RSPL_CHECK_ARG(p >= 0 && p < np && l >= 0 && l < lmax && c >= 0 && c < pr->n_cameras,
+                       "edge %d of type %d references a missing vertex/camera", i, t);
+      }
+    // a pose is optimised when it has an edge on ANY rank: K agrees across ranks
+    for (int i = 0; i < n; i++) pact[pt[i]] = 1;
+    if (!sh) {
+      for (int i = 0; i < n; i++) cnt[loff + lt[i] + 1]++;
+      Ep += t < 2 ? n : 0;
+    } else {
+      for (int i = 0; i < n; i++)
+        if (owned(t, i)) {
+          cnt[loff + lt[i] + 1]++;
+          Ep += t < 2;
+        }
     }
   }
+  mark("count");
   const CallLayout cl(pr->n_cameras, np, nq, nl, E, 4 * (size_t)Ep + 8 * (size_t)(E - Ep));
   const DownLayout dl(np, nq, nl, Eg);  // inlier flags by global edge id
   int rc;
@@ -713,15 +766,18 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   int* lpose = reinterpret_cast<int*>(sg + cl.lm_pose);
   double* eobs = reinterpret_cast<double*>(sg + cl.obs);
   double* lobs = eobs + 4 * (size_t)Ep;
+  mark("vertices");
   int* fill = b->lm_cnt.data();  // reused as the per-landmark fill cursor
   for (int g = 0; g < nL; g++) fill[g] = lm_off[g];
   int eg = 0;
-  for (int t = 0; t < 4; t++) {
-    const int n = ne[t], loff = t < 2 ? 0 : nq, d = od[t];
+  // one instantiation per edge type (D observation doubles: 2, 3, 4, 8)
+  auto scatter = [&](auto dc, int t) {
+    constexpr int D = decltype(dc)::value;
+    const int n = ne[t], loff = t < 2 ? 0 : nq;
     const int32_t *pt = poses[t], *lt = lms[t], *ct = cams[t];
     const double* ob = obs[t];
     for (int i = 0; i < n; i++, eg++) {
-      if (!owned(t, i)) continue;
+      if (sh && !owned(t, i)) continue;
       const int g = loff + lt[i], k = fill[g]++, p = pt[i];
       etype[k] = (int8_t)t;
       epose[k] = p;
@@ -729,11 +785,17 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
       ecam[k] = ct ? ct[i] : 0;
       gmap[k] = eg;
       lpose[k] = pidx[p];
-      double* o = t < 2 ? eobs + 4 * (size_t)k : lobs + 8 * (size_t)(k - Ep);
-      for (int q = 0; q < d; q++) o[q] = ob[(size_t)d * i + q];
-      if (t == 0) o[2] = 0.0;
+      double* o = D <= 3 ? eobs + 4 * (size_t)k : lobs + 8 * (size_t)(k - Ep);
+#pragma GCC unroll 8
+      for (int q = 0; q < D; q++) o[q] = ob[(size_t)D * i + q];
+      if (D == 2) o[2] = 0.0;  // mono: no right coordinate
     }
-  }
+  };
+  scatter(std::integral_constant<int, 2>{}, 0);
+  scatter(std::integral_constant<int, 3>{}, 1);
+  scatter(std::integral_constant<int, 4>{}, 2);
+  scatter(std::integral_constant<int, 8>{}, 3);
+  mark("scatter");
   uint8_t* lm_act = reinterpret_cast<uint8_t*>(sg + cl.lm_act);
   size_t pair_bound = 0;  // sum_g k_g^2 >= edge pairs of any pose pair
   for (int g = 0; g < nL; g++) {
@@ -786,11 +848,13 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
       pairs[2 * q] = a;
       pairs[2 * q + 1] = c;
     }
+  mark("tables");
   memcpy(sg + cl.cams, pr->cameras, sizeof(double) * 5 * pr->n_cameras);
   if (nq) memcpy(sg + cl.X, pr->points, sizeof(double) * 3 * nq);
   if (nl) memcpy(sg + cl.L, pr->lines, sizeof(double) * 6 * nl);
   memset(sg + cl.level, 0, cl.bytes - cl.level);  // level, flags, out start at zero
   RSPL_HIP(hipMemcpyAsync(b->cbuf, sg, cl.bytes, hipMemcpyHostToDevice, st));
+  mark("upload");
   char* cb = b->cbuf;
   uint8_t* level = reinterpret_cast<uint8_t*>(cb + cl.level);
   ba::Problem P{};
@@ -844,16 +908,18 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   A.K = K;
   A.nL = nL;
   A.robust = 1;
-  mark();
   A.pp_off = b->pp_off;
   A.pp = b->pp_buf;
-  RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, st));
-  mark();
+  RSPL_HIP(hipEventRecord(b->staged, st));  // the upload above
+  RSPL_HIP(hipStreamWaitEvent(b->side, b->staged, 0));
+  RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, b->side));
+  RSPL_HIP(hipEventRecord(b->pairs_ready, b->side));
+  b->pairs_pending = true;
+  mark("pairs");
   if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first)))
     return rc;
-  mark();
+  mark("opt1");
   RSPL_HIP(ba::classify(P, Lr, E, level, nullptr, 0, st));
-  mark();
   // ---- phase 2: level-0 edges, no kernel (initializeOptimization(0), :176-213) ----
   // Same active structure with the level-1 edges masked (exact-zero records, no cost, errors
   // kept as g2o keeps them), landmark activity recomputed from the levels on the device.
@@ -862,10 +928,9 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
     A.elevel = level;
     RSPL_HIP(ba::landmark_active(A, level, b->lm_act2, st));
     A.lm_act = b->lm_act2;
-    mark();
     if ((rc = optimize(b, P, Lr, S, A, pr->iterations_second, &res->chi2_second, &res->iterations_done_second)))
       return rc;
-    mark();
+    mark("opt2");
   }
   // ---- inlier flags + final state written by the GPU into the mapped staging buffer ----
   // (the staging call region was consumed by the upload long before: the stream is in order)
@@ -924,11 +989,12 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
     res->pose_q[4 * p + 3] = Twc.q[0];
     for (int k = 0; k < 3; k++) res->pose_p[3 * p + k] = Twc.t[k];
   }
-  mark();
-  if (timing && ntm == 8) {
-    auto us = [&](int i) { return std::chrono::duration<double, std::micro>(tmark[i + 1] - tmark[i]).count(); };
-    fprintf(stderr, "rspl_ba_local us: prep %.0f csr %.0f opt1 %.0f classify %.0f active2 %.0f opt2 %.0f final %.0f\n",
-            us(0), us(1), us(2), us(3), us(4), us(5), us(6));
+  mark("final");
+  if (timing) {
+    fprintf(stderr, "rspl_ba_local us:");
+    for (int i = 1; i < ntm; i++)
+      fprintf(stderr, " %s %.1f", tname[i], std::chrono::duration<double, std::micro>(tmark[i] - tmark[i - 1]).count());
+    fprintf(stderr, "\n");
   }
   return RSPL_OK;
 }

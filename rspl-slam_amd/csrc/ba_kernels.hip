@@ -349,7 +349,7 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
     __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(S.fail, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     S.out[2] = 0.0;
-    post_mail(S.mail, chi2, scale, mx, f, seq);
+    if (seq) post_mail(S.mail, chi2, scale, mx, f, seq);  // seq 0: nobody waits (device-side LM)
   }
 }
 
@@ -392,6 +392,7 @@ __global__ __launch_bounds__(256) void post_kernel(Sys S, int K, int npd, unsign
     c->stop = 0;
     c->iters = lm_iters;
     c->trials = 0;
+    return;  // the host waits for the trials only
   }
   post_mail(S.mail, S.out[0], S.out[1], S.out[2],
             (double)__hip_atomic_load(S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), seq);
@@ -675,6 +676,25 @@ __device__ __forceinline__ bool lm_dinv(const double* Hll, bool point, double la
 // line landmarks itself -- the same back-substitution as the landmark groups (8 lanes per
 // landmark, the same butterfly, from the current records Lc / Sc) -- so it never waits for the
 // groups; wave 3 evaluates each edge's own error at the candidate.
+// candidate pose i of this trial (g2o VertexSE3Expmap::oplusImpl, the left update exp(xp) T):
+// copied when the pose is not optimised or the solve failed
+__device__ __forceinline__ void cand_pose(const Problem& P, const Active& A, const double* x, int i, bool failed,
+                                          double (&o)[8]) {
+  const int a = A.pidx[i];
+#pragma unroll
+  for (int k = 0; k < 8; k++) o[k] = P.T[8 * i + k];
+  if (a < 0 || failed) return;
+  double xp[6];
+#pragma unroll
+  for (int k = 0; k < 6; k++) xp[k] = x[6 * a + k];
+  const SE3 r = se3_mul(se3_exp(xp), load_T(o));
+#pragma unroll
+  for (int k = 0; k < 4; k++) o[k] = r.q[k];
+#pragma unroll
+  for (int k = 0; k < 3; k++) o[4 + k] = r.t[k];
+  o[7] = 0;
+}
+
 template <bool SPEC>
 __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const Active& A, const Sys& S, int blk,
                                           bool maxd, const Lin* Lc = nullptr, const Sys* Sc = nullptr,
@@ -686,6 +706,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
   __shared__ double es[kLineBlk][4];
   __shared__ int einfo_s[kLineBlk][4];  // edge id, type, flags (1 on, 2 live, 4 pose optimised), landmark
   __shared__ double cv[kLineBlk][20];   // landmark-side records (Hll 16, bl 4) of each edge
+  __shared__ double Tsh[kLineBlk][8];   // SPEC: each edge's candidate pose
   const int tid = threadIdx.x, wv = tid >> 6, lane = tid & 63;
   const int4 tb = A.ltab[blk];
   const int p0 = tb.x, cnt = tb.y & 0xff, gb = tb.z, ge = tb.w;
@@ -703,7 +724,15 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
     const bool in = g < ge;
     const int l = g - P.nq;
     const bool upd = in && A.lm_act[g] && !failed;
-    double c[4] = {0, 0, 0, 0};
+    double c[4] = {0, 0, 0, 0}, hb[20], lmv[6] = {0, 0, 0, 0, 0, 0};
+    if (in) {  // the landmark-only operands in the first round trip
+#pragma unroll
+      for (int q = 0; q < 16; q++) hb[q] = Sc->Hll[16 * g + q];
+#pragma unroll
+      for (int q = 0; q < 4; q++) hb[16 + q] = Sc->bl[4 * g + q];
+#pragma unroll
+      for (int q = 0; q < 6; q++) lmv[q] = P.L[6 * l + q];
+    }
     if (upd)
       for (int k = A.lm_off[g] + j; k < A.lm_off[g + 1]; k += kGroup) {
         const int a = A.lm_pose[k];
@@ -719,16 +748,11 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
         }
       }
     group_sum(c);
-    double lmv[6] = {0, 0, 0, 0, 0, 0};
-    if (in) {
-#pragma unroll
-      for (int q = 0; q < 6; q++) lmv[q] = P.L[6 * l + q];
-    }
     if (upd) {
 #pragma unroll
-      for (int q = 0; q < 4; q++) c[q] += Sc->bl[4 * g + q];
+      for (int q = 0; q < 4; q++) c[q] += hb[16 + q];
       double D[16];
-      lm_dinv(Sc->Hll + 16 * g, false, lambda, D);
+      lm_dinv(hb, false, lambda, D);
       double xl[4];
 #pragma unroll
       for (int r = 0; r < 4; r++) xl[r] = D[r * 4] * c[0] + D[r * 4 + 1] * c[1] + D[r * 4 + 2] * c[2] + D[r * 4 + 3] * c[3];
@@ -738,9 +762,11 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
 #pragma unroll
       for (int q = 0; q < 6; q++) cand[m][q] = lmv[q];
   }
-  if (SPEC) __syncthreads();
-  // per edge: its attributes and the current (or candidate) line, into LDS
-  if (tid < kLineBlk) {
+  // per edge (SPEC: wave 1, beside wave 0's candidate lines): its attributes and the current line
+  // (SPEC: its candidate pose) into LDS
+  const int es_ = SPEC ? tid - 64 : tid;
+  if (es_ >= 0 && es_ < kLineBlk) {
+    const int tid = es_;
     const bool on = tid < cnt;
     const int e = on ? (p0 + tid) : 0;
     const int t = on ? P.etype[e] : 2;
@@ -753,7 +779,10 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
     if (live) {
       const int l = P.elm[e] - P.nq;
       if (SPEC) {
-        for (int k = 0; k < 6; k++) Lsh[tid][k] = cand[P.elm[e] - gb][k];
+        double Tc[8];
+        cand_pose(P, A, S.x, P.epose[e], failed, Tc);
+#pragma unroll
+        for (int k = 0; k < 8; k++) Tsh[tid][k] = Tc[k];
       } else {
         for (int k = 0; k < 6; k++) Lsh[tid][k] = P.L[6 * l + k];
       }
@@ -785,11 +814,11 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
     if (live) {
       const int d = m >> 1;
       const double sgn = (m & 1) ? -delta : delta;
-      const SE3 T = load_T((SPEC ? P.Tn : P.T) + 8 * P.epose[e]);
+      const SE3 T = load_T(SPEC ? &Tsh[slot][0] : P.T + 8 * P.epose[e]);
       const double* cam = P.cams + 5 * P.ecam[e];
       const double* obs = obs_of(P, e, t);
       double Lp[6];
-      for (int k = 0; k < 6; k++) Lp[k] = Lsh[slot][k];
+      for (int k = 0; k < 6; k++) Lp[k] = SPEC ? cand[einfo_s[slot][3] - gb][k] : Lsh[slot][k];
       double er[4] = {0, 0, 0, 0};
       if (wv == 0) {
         double v[4];
@@ -1225,14 +1254,7 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
   double* bpl = Ldg + 15 * K;               // [n] pose gradient bp (for the LM scale)
   const int tid = threadIdx.x;
   if (tid == 0) bad = 0;
-  // the candidate-pose step's operands, fetched before the factorisation (lane = pose)
-  int pose_a = -1;
-  double Tp0[8];
-  if (tid < P.np) {
-    pose_a = A.pidx[tid];
-#pragma unroll
-    for (int k = 0; k < 8; k++) Tp0[k] = P.T[8 * tid + k];
-  }
+  const int pose_a = tid < P.np ? A.pidx[tid] : -1;  // the pose part of the LM scale (lane = pose)
   if (tid == 0) prof_stamp(S, 0);
   // assembly: every thread issues its pairfin loads (8 at a time) before writing LDS; the
   // fail flag is checked after them (it would otherwise gate every load)
@@ -1349,27 +1371,12 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
   }
   for (int i = lane; i < n; i += 64) S.x[i] = z[i];
   if (tid == 0) prof_stamp(S, 3);
-  // candidate poses (lane = pose; np <= 64): T <- exp(xp) T, fixed poses copied (ping-pong),
-  // and the pose part of the LM scale x.(lambda x + bp)
+  // the pose part of the LM scale x.(lambda x + bp) (lane = pose; the candidate poses are formed
+  // by update_errors_kernel)
   double sc = 0;
-  if (lane < P.np) {
-    const int a = pose_a;
-    double* Tq = P.Tn + 8 * lane;
-    if (a >= 0) {
-      double xp[6];
+  if (lane < P.np && pose_a >= 0)
 #pragma unroll
-      for (int r = 0; r < 6; r++) xp[r] = z[6 * a + r];
-      const SE3 r = se3_mul(se3_exp(xp), load_T(Tp0));
-      for (int k = 0; k < 4; k++) Tq[k] = r.q[k];
-      for (int k = 0; k < 3; k++) Tq[4 + k] = r.t[k];
-      Tq[7] = 0;
-#pragma unroll
-      for (int k = 0; k < 6; k++) sc += xp[k] * (lambda * xp[k] + bpl[6 * a + k]);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; k++) Tq[k] = Tp0[k];
-    }
-  }
+    for (int k = 0; k < 6; k++) sc += z[6 * pose_a + k] * (lambda * z[6 * pose_a + k] + bpl[6 * pose_a + k]);
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
   if (lane == 0) S.out[4] = sc;
@@ -1401,7 +1408,6 @@ __device__ __forceinline__ double readlane64(double v, int l) {
 struct WaveSolveLds {
   double col[2][64];  // column broadcast, double-buffered by step parity
   double Lm[60][61];  // Lm[j][i] = l_ij (column j of L); odd stride
-  double xs[64];      // solution, for the pose lanes
 };
 
 // pose pair index of (c, a), c <= a, row-major upper triangle of K poses
@@ -1412,14 +1418,6 @@ __device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys
                                            bool coherent) {
   constexpr int K = N / 6;
   const int lane = threadIdx.x & 63;
-  // candidate-pose operands first (independent of the solve): lane = pose
-  int pose_a = -1;
-  double Tp0[8];
-  if (lane < P.np) {
-    pose_a = A.pidx[lane];
-#pragma unroll
-    for (int k = 0; k < 8; k++) Tp0[k] = P.T[8 * lane + k];
-  }
   const int pa = lane / 6, r = lane - 6 * pa;
   const bool row = lane < N;
   auto ld = [&](int idx) {
@@ -1491,28 +1489,10 @@ __device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys
   const double x = y;
   if (lane == 0) prof_stamp(S, 3);
   if (row) S.x[lane] = x;
-  w.xs[lane] = x;
-  wave_sync();
-  // candidate poses (lane = pose; np <= 64): T <- exp(xp) T, fixed poses copied (ping-pong),
-  // and the pose part of the LM scale x.(lambda x + bp)
+  // the pose part of the LM scale x.(lambda x + bp) (the candidate poses: update_errors_kernel)
   double sc = row ? x * (lambda * x + bpl) : 0.0;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
-  if (lane < P.np) {
-    double* Tq = P.Tn + 8 * lane;
-    if (pose_a >= 0) {
-      double xp[6];
-#pragma unroll
-      for (int q = 0; q < 6; q++) xp[q] = w.xs[6 * pose_a + q];
-      const SE3 rr = se3_mul(se3_exp(xp), load_T(Tp0));
-      for (int k = 0; k < 4; k++) Tq[k] = rr.q[k];
-      for (int k = 0; k < 3; k++) Tq[4 + k] = rr.t[k];
-      Tq[7] = 0;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; k++) Tq[k] = Tp0[k];
-    }
-  }
   if (lane == 0) S.out[4] = sc;
 }
 
@@ -1540,7 +1520,6 @@ struct Blk4Lds {
   double wpan[2][64][6];   // W_ic = l_ic d_c
   double Lall[10][64][6];  // every step's l_ic (backward substitution)
   double dg[64];           // pivots
-  double xs[64];           // solution (pose lanes)
   int bad;
 };
 
@@ -1549,13 +1528,6 @@ __device__ __forceinline__ void solve_blk4(Problem P, const Active& A, const Sys
                                            bool coherent) {
   constexpr int N = 6 * K, NQ = (K + 3) / 4;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  int pose_a = -1;
-  double Tp0[8];
-  if (wv == 0 && lane < P.np) {
-    pose_a = A.pidx[lane];
-#pragma unroll
-    for (int k = 0; k < 8; k++) Tp0[k] = P.T[8 * lane + k];
-  }
   const int pa = lane / 6, r = lane - 6 * pa;
   const bool row = lane < N;
   auto ld = [&](int idx) {
@@ -1662,26 +1634,9 @@ __device__ __forceinline__ void solve_blk4(Problem P, const Active& A, const Sys
   const double x = y;
   if (tid == 0) prof_stamp(S, 3);
   if (row) S.x[lane] = x;
-  w.xs[lane] = x;
-  wave_sync();
   double sc = row ? x * (lambda * x + bpl) : 0.0;
 #pragma unroll
   for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
-  if (lane < P.np) {
-    double* Tq = P.Tn + 8 * lane;
-    if (pose_a >= 0) {
-      double xp[6];
-#pragma unroll
-      for (int q = 0; q < 6; q++) xp[q] = w.xs[6 * pose_a + q];
-      const SE3 rr = se3_mul(se3_exp(xp), load_T(Tp0));
-      for (int k = 0; k < 4; k++) Tq[k] = rr.q[k];
-      for (int k = 0; k < 3; k++) Tq[4 + k] = rr.t[k];
-      Tq[7] = 0;
-    } else {
-#pragma unroll
-      for (int k = 0; k < 8; k++) Tq[k] = Tp0[k];
-    }
-  }
   if (lane == 0) S.out[4] = sc;
 }
 
@@ -2037,10 +1992,9 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
       for (int q = 0; q < 6; q++) lm[q] = P.L[6 * (g - P.nq) + q];
     }
   }
-  for (int q = tid; q < 8 * P.np; q += 256) sT[q] = P.Tn[q];
+  const bool failed = *S.fail != 0;
   for (int q = tid; q < 5 * P.ncam; q += 256) scam[q] = P.cams[q];
   for (int q = tid; q < 6 * A.K; q += 256) sx[q] = S.x[q];
-  const bool failed = *S.fail != 0;
   // the lane's first edge (most landmarks have <= kGroup edges): everything it needs in one round trip
   const int kf = k0 + j;
   const bool has = in && kf < k1;
@@ -2057,6 +2011,17 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     const double* o = obs_of(P, kf, point ? 0 : 2);
 #pragma unroll
     for (int q = 0; q < 8; q++) of[q] = (q < 3 || !point) ? o[q] : 0.0;
+  }
+  // the candidate poses (np <= 64) while the first edges are in flight; block 0 publishes them
+  // for the verdict and the next trial
+  if (tid < P.np) {
+    double Tc[8];
+    cand_pose(P, A, S.x, tid, failed, Tc);
+#pragma unroll
+    for (int k = 0; k < 8; k++) sT[8 * tid + k] = Tc[k];
+    if (blockIdx.x == 0)
+#pragma unroll
+      for (int k = 0; k < 8; k++) P.Tn[8 * tid + k] = Tc[k];
   }
   __syncthreads();
   if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 1);  // operands loaded
@@ -2220,7 +2185,8 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
         double* t = S.lm_trace + 8 * (c->trials - 1);
         t[0] = chi2; t[1] = scale; t[2] = f; t[3] = lam0; t[4] = chi0; t[5] = c->cur; t[6] = c->it; t[7] = c->qmax;
       }
-      post_mail(S.mail, c->chi, (double)c->it, (double)c->cur, (double)stop, seq);
+      // system-scope stores into host memory, each waited for: only when the host reads them
+      if (stop || S.lm_post) post_mail(S.mail, c->chi, (double)c->it, (double)c->cur, (double)stop, seq);
       return;
     }
     post_mail(S.mail, chi2, scale, mx, f, seq);

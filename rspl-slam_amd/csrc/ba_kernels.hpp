@@ -117,6 +117,8 @@ struct Sys {
   double* lm_trace;      // debug (RSPL_BA_LMTRACE): per trial {chi2, scale, fail, lambda, rho, cur, it, qmax}
   int lm_slot;           // trial k reads lm[k & 1] and its last block writes lm[(k + 1) & 1]: the
                          // control a trial's blocks read never changes under them
+  int lm_post;           // device LM: post the verdict even when it does not stop (the last trial the
+                         // host queued); otherwise only the stopping trial posts the mailbox
 };
 constexpr int kProfPc = 16, kProfUe = kProfPc + 4 * 4096, kProfLen = kProfUe + 4 * 4096;
 

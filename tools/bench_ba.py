@@ -4,6 +4,8 @@ import pathlib
 import sys
 import time
 
+import numpy as np
+
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 import rspl_loader  # noqa: E402
@@ -23,13 +25,16 @@ def main():
     probs = [pkg.synthetic.ba_problem(n_poses=a.poses, n_points=a.points, n_lines=a.lines, seed=s)[0] for s in range(3)]
     for p in probs:
         ba.run(p)
-    t = time.perf_counter()
+    ts = []
     for i in range(a.iters):
+        t = time.perf_counter()
         r = ba.run(probs[i % 3])
-    dt = (time.perf_counter() - t) / a.iters * 1e3
+        ts.append(time.perf_counter() - t)
+    dt = float(np.mean(ts)) * 1e3
     e = sum(probs[0].n_edges(k) for k in ("mono", "stereo", "mono_line", "stereo_line"))
     print(f"BA {a.poses} poses {probs[0].points.shape[0]} pts {probs[0].lines.shape[0]} lines {e} edges: "
-          f"{dt:.2f} ms/call, iters {r.iters_first}+{r.iters_second}")
+          f"{dt:.2f} ms/call (median {np.median(ts) * 1e3:.3f} min {np.min(ts) * 1e3:.3f}), "
+          f"iters {r.iters_first}+{r.iters_second}")
 
 
 if __name__ == "__main__":

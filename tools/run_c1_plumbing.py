@@ -50,6 +50,22 @@ def match_set(m):
     return {(int(q), int(t)) for q, t in np.asarray(m).reshape(-1, 2)}
 
 
+def match_coords(m, F0, F1):
+    """matches as keypoint-coordinate pairs: comparable across paths whose keypoint lists differ"""
+    return {(int(F0[1, q]), int(F0[2, q]), int(F1[1, t]), int(F1[2, t])) for q, t in np.asarray(m).reshape(-1, 2)}
+
+
+def z_errors(Zg, Z):
+    """max |exp(Zg) - exp(Z)| (assignment probabilities) and max |dZ| where the CPU probability >= 1e-4;
+    log-probabilities far below that amplify rounding and carry no decision"""
+    if Zg.shape != Z.shape:
+        return float("nan"), float("nan")
+    dp = float(np.abs(np.exp(Zg.astype(np.float64)) - np.exp(Z.astype(np.float64))).max())
+    sig = Z > np.log(1e-4)
+    dz = float(np.abs(Zg - Z)[sig].max()) if sig.any() else 0.0
+    return dp, dz
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--pairs", type=int, default=100)
@@ -114,8 +130,14 @@ def main():
             common = sorted(set(kc) & set(kg))
             dmax = max(float(np.abs(Fg[0][3:, kg[c]] - Fc[0][3:, kc[c]]).max()) for c in common) if common else 0.0
             sc_, sg_ = match_set(mc), match_set(mg)
-            nc_, ng_, n16 = match_set(nnc), match_set(nng), match_set(res["fp16"][2])
+            nc_, ng_ = match_set(nnc), match_set(nng)
+            cc_ = match_coords(nnc, Fc[0], Fc[1])
+            cg_ = match_coords(nng, Fg[0], Fg[1])
+            F16 = res["fp16"][0]
+            c16 = match_coords(res["fp16"][2], F16[0], F16[1])
             zerr = float(np.abs(Zg - Z).max()) if Zg.shape == Z.shape else float("nan")
+            dp, dzs = z_errors(Zg, Z)
+            dp16, _ = z_errors(res["fp16"][3], Z)
             lines_same = l0g.shape == l0c.shape and bool(np.array_equal(l0g, l0c))
             row = {"pair": t,
                    "keypoints": [int(Fc[0].shape[1]), int(Fc[1].shape[1])],
@@ -123,10 +145,14 @@ def main():
                    set(key_index(Fc[1])) == set(key_index(Fg[1])),
                    "desc_max_abs_diff": dmax,
                    "Z_max_abs_diff_fp32": zerr,
+                   "P_max_abs_diff_fp32": dp, "Z_sig_max_abs_diff_fp32": dzs, "P_max_abs_diff_fp16": dp16,
                    "matches_cpu": len(sc_), "matches_gpu_fp32": len(sg_), "matches_identical": sc_ == sg_,
                    "mutual_nn_cpu": len(nc_),
                    "match_agreement_fp32": len(nc_ & ng_) / max(1, len(nc_ | ng_)),
-                   "match_agreement_fp16": len(nc_ & n16) / max(1, len(nc_ | n16)),
+                   "match_agreement_fp32_coords": len(cc_ & cg_) / max(1, len(cc_ | cg_)),
+                   "match_agreement_fp16": len(cc_ & c16) / max(1, len(cc_ | c16)),
+                   "keypoint_sets_identical_fp16": set(key_index(Fc[0])) == set(key_index(F16[0])) and
+                   set(key_index(Fc[1])) == set(key_index(F16[1])),
                    "lines_left": int(len(l0c)), "merged_lines_identical": lines_same,
                    "right_lines_valid_cpu": int(lvc.sum()), "right_lines_valid_gpu": int(lvg.sum()),
                    "line_association_identical": lines_same and bool(np.array_equal(lvc, lvg)) and
@@ -135,18 +161,23 @@ def main():
             fo.write(json.dumps(row) + "\n")
             if t % 10 == 0:
                 print(f"pair {t}: mutual NN cpu {len(nc_)} gpu {len(ng_)} agreement {row['match_agreement_fp32']:.4f}"
-                      f" fp16 {row['match_agreement_fp16']:.4f} |dZ| {zerr:.2e}", file=sys.stderr, flush=True)
+                      f" fp16 {row['match_agreement_fp16']:.4f} |dZ| {zerr:.2e} |dP| {dp:.2e} |dP16| {dp16:.2e}", file=sys.stderr, flush=True)
     agg = lambda k: float(np.mean([r[k] for r in rows]))
     print(json.dumps({
         "pairs": len(rows), "image": f"{W}x{H}", "max_keypoints": K,
         "keypoint_sets_identical_frac": agg("keypoint_sets_identical"),
         "desc_max_abs_diff": float(max(r["desc_max_abs_diff"] for r in rows)),
         "Z_max_abs_diff_fp32": float(max(r["Z_max_abs_diff_fp32"] for r in rows)),
+        "P_max_abs_diff_fp32": float(max(r["P_max_abs_diff_fp32"] for r in rows)),
+        "Z_sig_max_abs_diff_fp32": float(max(r["Z_sig_max_abs_diff_fp32"] for r in rows)),
+        "P_max_abs_diff_fp16": float(max(r["P_max_abs_diff_fp16"] for r in rows)),
+        "keypoint_sets_identical_fp16_frac": agg("keypoint_sets_identical_fp16"),
         "thresholded_matches_identical_frac": agg("matches_identical"),
         "matches_per_pair_cpu": agg("matches_cpu"),
         "mutual_nn_per_pair_cpu": agg("mutual_nn_cpu"),
         "match_agreement_fp32_mean": agg("match_agreement_fp32"),
         "match_agreement_fp32_min": float(min(r["match_agreement_fp32"] for r in rows)),
+        "match_agreement_fp32_coords_mean": agg("match_agreement_fp32_coords"),
         "match_agreement_fp16_mean": agg("match_agreement_fp16"),
         "match_agreement_fp16_min": float(min(r["match_agreement_fp16"] for r in rows)),
         "line_association_identical_frac": agg("line_association_identical"),
