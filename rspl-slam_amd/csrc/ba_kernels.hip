@@ -1667,30 +1667,21 @@ __global__ __launch_bounds__(64) void schur_wave_kernel(Problem P, Active A, Sys
   solve_wave<N>(P, A, S, lambda, w, false);
 }
 
-// N > 0 (6K <= 60): the pose pair finished last (a second ticket over the pairs) solves the reduced
-// system in the same wave (solve_wave<N>), so the trial needs no separate solve launch.
-template <int N>
-__global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active A, Sys S, double lambda, Lin Ls,
-                                                        Sys Ss) {
-  constexpr int kRedLen = 64 * 49, kSolveLen = (int)(sizeof(WaveSolveLds) / sizeof(double));
-  __shared__ double smem[N > 0 && kSolveLen > kRedLen ? kSolveLen : kRedLen];
-  double* red = smem;
-  if (S.lm) {  // device-side LM: damping and bank from the control
-    LmView v;
-    if (!lm_view(S, v)) return;
-    lambda = v.lambda;
-    if (v.cur) {
-      bank_lin(L, Ls, S, Ss);
-      if (N > 0) bank_state(P);
-    }
-  }
+// One Schur chunk (pose pair, landmark range) on one wave: walks its segment of the edge-pair
+// lists, sums its 64 lanes in lane order (LDS transpose in red[64 * 49], this wave's own) and hands
+// the partial off write-through to whichever chunk of the pose pair finishes last; that one sums the
+// pair's chunks in chunk order (deterministic) into pairfin (write-through when `wt`: a solver in the
+// same launch reads it).  vb is the chunk's virtual workgroup id (XCD-aware order).  Returns true in
+// the wave that completed a pose pair.
+__device__ __forceinline__ bool chunk_wave(const Problem& P, const Lin& L, const Active& A, const Sys& S,
+                                           double lambda, int vb, double* red, bool wt) {
   // XCD-aware chunk order: workgroups go round-robin over the 8 XCDs (blockIdx % 8), so
   // landmark range lb runs on XCD lb % 8 for every pose pair -- each XCD's L2 then holds only
   // its ranges' records (~1/8 of them), which its ~k_g pose pairs per landmark re-read
-  const int lane = threadIdx.x;
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, rpx = (A.nchk + 7) >> 3;
+  const int lane = threadIdx.x & 63;
+  const int xcd = vb & 7, slot = vb >> 3, rpx = (A.nchk + 7) >> 3;
   const int lb = (slot % rpx) * 8 + xcd, pr0 = slot / rpx;
-  if (lb >= A.nchk || pr0 >= A.npairs) return;
+  if (lb >= A.nchk || pr0 >= A.npairs) return false;
   const int c = pr0 * A.nchk + lb;
   if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c);
   const int pr = c / A.nchk;
@@ -1699,9 +1690,12 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
 #pragma unroll
   for (int v = 0; v < 48; v++) acc[v] = 0.0;
   bool bad = false;
+  // the next pass's pair indices are fetched a pass ahead: one memory round trip per pass
+  int4 qn = beg + lane < end ? A.pp[beg + lane] : make_int4(0, 0, 0, 0);
   for (int k = beg + lane; k < end; k += 64) {
-    // every operand of the pair is requested before any arithmetic: one memory round trip
-    const int4 q = A.pp[k];
+    // every operand of the pair is requested before any arithmetic
+    const int4 q = qn;
+    if (k + 64 < end) qn = A.pp[k + 64];
     const int e1 = q.x, e2 = q.y, g = q.z;
     const bool diag = e1 == e2;
     const bool live = !(A.elevel && (A.elevel[e1] | A.elevel[e2]));  // else zero records: no contribution
@@ -1735,9 +1729,7 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
   if (bad) atomicOr(S.fail, 1);
 #pragma unroll
   for (int v = 0; v < 48; v++) red[lane * 49 + v] = acc[v];
-  __syncthreads();
-  // chunk partial, handed off write-through (sc1) to whichever chunk of this pose pair
-  // finishes last; that one sums the pair's chunks in chunk order (deterministic)
+  wave_sync();
   if (lane < 48) {  // 8 independent partial sums, combined in a fixed order
     double p8[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
@@ -1752,7 +1744,7 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
   tk = __shfl(tk, 0);
   if (tk != (unsigned)(c1 - c0 - 1)) {
     if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 2);
-    return;
+    return false;
   }
   if (lane == 0) __hip_atomic_store(S.pair_ctr + pr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (lane < 48) {
@@ -1767,25 +1759,52 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
 #pragma unroll
       for (int u = 0; u < 16; u++) s += t[u];
     }
-    if (N > 0) __hip_atomic_store(S.pairfin + 48 * pr + lane, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (wt) __hip_atomic_store(S.pairfin + 48 * pr + lane, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     else S.pairfin[48 * pr + lane] = s;
   }
   if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 3);
+  return true;
+}
+
+// second ticket over the pose pairs (re-armed by its winner): true in the wave that finished the
+// last pose pair -- every pair sum is then out (write-through)
+__device__ __forceinline__ bool last_pair(const Sys& S, int npairs) {
+  const int lane = threadIdx.x & 63;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  unsigned tp = 0;
+  if (lane == 0) tp = __hip_atomic_fetch_add(S.solve_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  tp = __shfl(tp, 0);
+  if (tp != (unsigned)(npairs - 1)) return false;
+  if (lane == 0) __hip_atomic_store(S.solve_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return true;
+}
+
+// N > 0 (6K <= 60): the pose pair finished last solves the reduced system in the same wave
+// (solve_wave<N>), so the trial needs no separate solve launch.
+template <int N>
+__global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active A, Sys S, double lambda, Lin Ls,
+                                                        Sys Ss) {
+  constexpr int kRedLen = 64 * 49, kSolveLen = (int)(sizeof(WaveSolveLds) / sizeof(double));
+  __shared__ double smem[N > 0 && kSolveLen > kRedLen ? kSolveLen : kRedLen];
+  if (S.lm) {  // device-side LM: damping and bank from the control
+    LmView v;
+    if (!lm_view(S, v)) return;
+    lambda = v.lambda;
+    if (v.cur) {
+      bank_lin(L, Ls, S, Ss);
+      if (N > 0) bank_state(P);
+    }
+  }
+  if (!chunk_wave(P, L, A, S, lambda, blockIdx.x, smem, N > 0)) return;
   if constexpr (N > 0) {
-    // the last pose pair to finish solves: its wave has every pair sum (write-through) behind a
-    // second ticket; the counter is re-armed for the next trial
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned tp = 0;
-    if (lane == 0) tp = __hip_atomic_fetch_add(S.solve_ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    tp = __shfl(tp, 0);
-    if (tp != (unsigned)(A.npairs - 1)) return;
-    if (lane == 0) __hip_atomic_store(S.solve_ctr, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __syncthreads();  // red[] is dead: the LDS becomes the solver's
-    if (lane == 0) prof_stamp(S, 0);
+    if (!last_pair(S, A.npairs)) return;
+    wave_sync();  // red[] is dead: the LDS becomes the solver's
+    if (threadIdx.x == 0) prof_stamp(S, 0);
     solve_wave<N>(P, A, S, lambda, *reinterpret_cast<WaveSolveLds*>(smem), true);
-    if (lane == 0) prof_stamp(S, 4);
+    if (threadIdx.x == 0) prof_stamp(S, 4);
   }
 }
+
 
 // larger systems: one workgroup on global memory
 
