@@ -440,6 +440,10 @@ typedef struct rspl_pnp rspl_pnp;
 int rspl_pnp_create(const rspl_pnp_config* cfg, rspl_pnp** out);
 int rspl_pnp_solve(rspl_pnp* h, const rspl_pnp_problem* problems, int batch, rspl_pnp_result* results);
 void rspl_pnp_destroy(rspl_pnp* h);
+/* debug (parity tests): frame `frame` of the last rspl_pnp_solve -- every hypothesis' inlier
+   count (-1: the minimal solver failed) and R (row-major) | t, up to `max` hypotheses; returns
+   the frame's hypothesis count or a negative error */
+int rspl_pnp_debug_hypotheses(rspl_pnp* h, int frame, int max, int32_t* counts, double* poses);
 
 /* ------------------------------------------------------------------------ */
 /* Map-side local BA: the keyframe / map-point / map-line */

@@ -150,6 +150,22 @@ def pnp(K4, pts3, pts2, iterations=100, reproj_err=20.0, confidence=0.99):
     return k, R.reshape(3, 3), t, inl[:n], used.value
 
 
+def pnp_hypotheses(K4, pts3, pts2, iterations=100, reproj_err=20.0):
+    """every RANSAC hypothesis of oracle/pnp.c: (counts [iters] int32, -1 = solver failed;
+    poses [iters, 12] = R row-major | t)"""
+    L = lib()
+    f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
+    L.orc_pnp_hypotheses.argtypes = [f64p, C.c_int, f64p, f64p, C.c_int, C.c_double,
+                                     np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS"), f64p]
+    L.orc_pnp_hypotheses.restype = None
+    p3 = np.ascontiguousarray(pts3, np.float64).reshape(-1, 3)
+    p2 = np.ascontiguousarray(pts2, np.float64).reshape(-1, 2)
+    cnt = np.zeros(iterations, np.int32)
+    poses = np.zeros((iterations, 12))
+    L.orc_pnp_hypotheses(np.ascontiguousarray(K4, np.float64), p3.shape[0], p3, p2, iterations, reproj_err, cnt, poses)
+    return cnt, poses
+
+
 def pnp_subsets(count, iterations):
     L = lib()
     L.orc_pnp_subsets.argtypes = [C.c_int, C.c_int, np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS")]

@@ -21,6 +21,9 @@
  * Object / image points are rounded to float first: the reference builds cv::Point3f /
  * cv::Point2f (:425-426).
  */
+/* no FMA contraction (the GPU kernel's rule, pnp_kernels.hip): EPnP's 5-point null space is
+   degenerate, and the basis the Jacobi leaves in it follows every rounding difference */
+#pragma GCC optimize("fp-contract=off")
 #include <float.h>
 #include <math.h>
 
@@ -51,7 +54,7 @@ void orc_pnp_subsets(int count, int iters, int32_t* idx /* [iters][5] */) {
 }
 
 /* ---------------- small dense linear algebra ---------------- */
-/* cyclic Jacobi eigen-decomposition of a symmetric n x n matrix (n <= 12): eigenvalues
+/* cyclic Jacobi eigen-decomposition of a symmetric n x n matrix (n <= 12; used for n = 3): eigenvalues
    descending in d, eigenvectors as ROWS of V (cvSVD's U^T order) */
 static void jacobi_eig(int n, const double* A0, double* d, double* V) {
   double A[144], U[144];
@@ -91,6 +94,119 @@ static void jacobi_eig(int n, const double* A0, double* d, double* V) {
       }
   }
   /* selection sort, descending */
+  int ord[12];
+  for (int i = 0; i < n; i++) ord[i] = i;
+  for (int i = 0; i < n; i++) {
+    int b = i;
+    for (int j = i + 1; j < n; j++)
+      if (A[ord[j] * n + ord[j]] > A[ord[b] * n + ord[b]]) b = j;
+    const int t = ord[i];
+    ord[i] = ord[b];
+    ord[b] = t;
+  }
+  for (int i = 0; i < n; i++) {
+    d[i] = A[ord[i] * n + ord[i]];
+    for (int k = 0; k < n; k++) V[i * n + k] = U[k * n + ord[i]];
+  }
+}
+
+/* Jacobi eigen-decomposition of the symmetric 12 x 12 M^T M in the parallel (round-robin)
+   order: a sweep is 11 rounds of 6 disjoint rotations, index 11 fixed and 0..10 on a circle
+   (round r: (r, 11) and ((r + k) % 11, (r - k) % 11), k = 1..5).  Each round takes its 6
+   angles from the matrix at the round's start, then applies every column rotation, then
+   every row rotation, then the eigenvector columns -- the operation order of the GPU's
+   wave-cooperative solver (pnp_kernels.hip: one rotation pair per lane group).  The sweep
+   test sums the squares in the GPU's order (per-lane partials over elements lane + 64 m,
+   then a butterfly over the 64 lanes).  cvSVD's own Jacobi order is OpenCV's (unpinned);
+   any converged Jacobi gives the same eigenvectors up to rounding and sign, which EPnP's
+   beta solve and solve_for_sign absorb.  Output as jacobi_eig. */
+/* the rotation annihilating a_pq from d = a_qq - a_pp, h = 2 a_pq != 0: the classic
+   theta = d / h, t = sgn(theta) / (|theta| + sqrt(theta^2 + 1)), c = 1 / sqrt(t^2 + 1), s = t c
+   rewritten with g = sqrt(d^2 + h^2) as t = sgn(theta) |h| / (|d| + g), c = sqrt((|d| + g) / (2 g))
+   -- the same rotation, three dependent sqrt / divide steps instead of five (the GPU's round
+   latency); sgn(theta) = +1 for theta = +-0 as in the classic test theta >= 0 */
+static void jacobi_cs(double d, double h, double* c, double* s) {
+  const double g = sqrt(d * d + h * h);
+  const double sg = d == 0.0 ? 1.0 : ((d > 0) == (h > 0) ? 1.0 : -1.0);
+  const double t = sg * fabs(h) / (fabs(d) + g);
+  *c = sqrt((fabs(d) + g) / (2.0 * g));
+  *s = t * *c;
+}
+
+static void jacobi12_rounds(const double* A0, double* d, double* V) {
+  enum { n = 12 };
+  double A[144], U[144];
+  memcpy(A, A0, sizeof(A));
+  for (int i = 0; i < 144; i++) U[i] = (i / n == i % n) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 60; sweep++) {
+    double po[64], pt[64];
+    for (int l = 0; l < 64; l++) {
+      po[l] = pt[l] = 0.0;
+      for (int e = l; e < 144; e += 64) {
+        const double v = A[e] * A[e];
+        pt[l] += v;
+        if (e / n != e % n) po[l] += v;
+      }
+    }
+    for (int o = 32; o >= 1; o >>= 1) {
+      double qo[64], qt[64];
+      for (int l = 0; l < 64; l++) {
+        qo[l] = po[l] + po[l ^ o];
+        qt[l] = pt[l] + pt[l ^ o];
+      }
+      memcpy(po, qo, sizeof(po));
+      memcpy(pt, qt, sizeof(pt));
+    }
+    const double off = po[0], tot = pt[0];
+    if (off <= 1e-30 * tot || off == 0.0) break;
+    for (int r = 0; r < 11; r++) {
+      int pp[6], qq[6], act[6];
+      double cc[6], ss[6];
+      for (int j = 0; j < 6; j++) {
+        int a = j == 0 ? r : (r + j) % 11, b = j == 0 ? 11 : (r - j + 11) % 11;
+        pp[j] = a < b ? a : b;
+        qq[j] = a < b ? b : a;
+        const int p = pp[j], q = qq[j];
+        const double apq = A[p * n + q];
+        act[j] = apq != 0.0;
+        cc[j] = 1.0;
+        ss[j] = 0.0;
+        if (!act[j]) continue;
+        const double app = A[p * n + p], aqq = A[q * n + q];
+        jacobi_cs(aqq - app, 2.0 * apq, &cc[j], &ss[j]);
+      }
+      for (int j = 0; j < 6; j++) {
+        if (!act[j]) continue;
+        const int p = pp[j], q = qq[j];
+        const double c = cc[j], s = ss[j];
+        for (int k = 0; k < n; k++) {
+          const double akp = A[k * n + p], akq = A[k * n + q];
+          A[k * n + p] = c * akp - s * akq;
+          A[k * n + q] = s * akp + c * akq;
+        }
+      }
+      for (int j = 0; j < 6; j++) {
+        if (!act[j]) continue;
+        const int p = pp[j], q = qq[j];
+        const double c = cc[j], s = ss[j];
+        for (int k = 0; k < n; k++) {
+          const double apk = A[p * n + k], aqk = A[q * n + k];
+          A[p * n + k] = c * apk - s * aqk;
+          A[q * n + k] = s * apk + c * aqk;
+        }
+      }
+      for (int j = 0; j < 6; j++) {
+        if (!act[j]) continue;
+        const int p = pp[j], q = qq[j];
+        const double c = cc[j], s = ss[j];
+        for (int k = 0; k < n; k++) {
+          const double ukp = U[k * n + p], ukq = U[k * n + q];
+          U[k * n + p] = c * ukp - s * ukq;
+          U[k * n + q] = s * ukp + c * ukq;
+        }
+      }
+    }
+  }
   int ord[12];
   for (int i = 0; i < n; i++) ord[i] = i;
   for (int i = 0; i < n; i++) {
@@ -374,7 +490,7 @@ static int epnp(const double* K4, int n, const double* pw, const double* uv, dou
       for (int b = 0; b < 12; b++) MtM[a * 12 + b] += M1[a] * M1[b] + M2[a] * M2[b];
   }
   double d[12], ut[144];
-  jacobi_eig(12, MtM, d, ut);
+  jacobi12_rounds(MtM, d, ut);
   double L[60], rho[6];
   epnp_L(ut, L);
   rho[0] = dist2(E.cws[0], E.cws[1]); rho[1] = dist2(E.cws[0], E.cws[2]); rho[2] = dist2(E.cws[0], E.cws[3]);
@@ -547,4 +663,34 @@ int orc_pnp(const double* K4, int n, const double* pts3, const double* pts2, int
   }
   free(pw); free(uv); free(sub);
   return ninl;
+}
+
+/* every hypothesis of orc_pnp's RANSAC (test infrastructure: per-hypothesis parity): the
+   inlier count (-1: the minimal solver failed) and R (row-major) | t of each of `iterations`
+   subsets, all evaluated (no adaptive stop) */
+void orc_pnp_hypotheses(const double* K4, int n, const double* pts3, const double* pts2, int iterations,
+                        double reproj_err, int32_t* counts, double* poses) {
+  double* pw = (double*)malloc(sizeof(double) * 3 * (n > 0 ? n : 1));
+  double* uv = (double*)malloc(sizeof(double) * 2 * (n > 0 ? n : 1));
+  for (int i = 0; i < 3 * n; i++) pw[i] = (double)(float)pts3[i];
+  for (int i = 0; i < 2 * n; i++) uv[i] = (double)(float)pts2[i];
+  int32_t* sub = (int32_t*)malloc(sizeof(int32_t) * 5 * iterations);
+  orc_pnp_subsets(n, iterations, sub);
+  const double thr2 = reproj_err * reproj_err;
+  for (int h = 0; h < iterations; h++) {
+    double sp[15], su[10], R[9] = {0}, t[3] = {0};
+    for (int k = 0; k < 5; k++) {
+      memcpy(sp + 3 * k, pw + 3 * sub[5 * h + k], sizeof(double) * 3);
+      memcpy(su + 2 * k, uv + 2 * sub[5 * h + k], sizeof(double) * 2);
+    }
+    int cnt = -1;
+    if (!epnp(K4, 5, sp, su, R, t)) {
+      cnt = 0;
+      for (int i = 0; i < n; i++) cnt += reproj2(K4, R, t, pw + 3 * i, uv + 2 * i) <= thr2;
+    }
+    counts[h] = cnt;
+    memcpy(poses + 12 * h, R, sizeof(R));
+    memcpy(poses + 12 * h + 9, t, sizeof(t));
+  }
+  free(pw); free(uv); free(sub);
 }

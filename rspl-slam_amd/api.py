@@ -474,6 +474,17 @@ class PnP:
         return [(r.n_inliers, np.array(r.Rwc[:]).reshape(3, 3), np.array(r.twc[:]), k[2][:k[0].shape[0]].copy(),
                  r.hypotheses) for r, k in zip(Ra, keep)]
 
+    def debug_hypotheses(self, frame=0, max_hyps=128):
+        """every hypothesis of frame `frame` of the last solve: (counts int32 [k], -1 = the
+        minimal solver failed; poses [k, 12] = R row-major | t)"""
+        cnt = np.zeros(max_hyps, np.int32)
+        poses = np.zeros((max_hyps, 12))
+        k = self._lib.rspl_pnp_debug_hypotheses(self._h, frame, max_hyps, cnt.ctypes.data_as(C.c_void_p),
+                                                poses.ctypes.data_as(C.c_void_p))
+        if k < 0:
+            capi.check(k, "rspl_pnp_debug_hypotheses")
+        return cnt[:k], poses[:k]
+
     def __del__(self):
         if getattr(self, "_h", None) and self._h.value:
             self._lib.rspl_pnp_destroy(self._h)

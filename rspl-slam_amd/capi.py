@@ -34,7 +34,7 @@ EXPORTS = [
     "rspl_frame_create", "rspl_frame_optimize", "rspl_frame_destroy",
     "rspl_ba_set_shard", "rspl_comm_unique_id", "rspl_comm_create", "rspl_comm_allreduce_sum", "rspl_comm_destroy",
     "rspl_ba_set_comm", "rspl_group_create", "rspl_group_destroy", "rspl_ba_set_group",
-    "rspl_pnp_create", "rspl_pnp_solve", "rspl_pnp_destroy",
+    "rspl_pnp_create", "rspl_pnp_solve", "rspl_pnp_destroy", "rspl_pnp_debug_hypotheses",
     "rspl_line_extract", "rspl_lines_create", "rspl_lines_destroy", "rspl_lines_assign", "rspl_lines_match",
     "rspl_lines_stereo", "rspl_lines_stereo_device", "rspl_lines_status",
 ]
@@ -167,6 +167,7 @@ def load(path: pathlib.Path = LIB_PATH):
         lib.rspl_pnp_solve.argtypes = [vp, vp, ip, vp]
         lib.rspl_pnp_destroy.argtypes = [vp]
         lib.rspl_pnp_destroy.restype = None
+        lib.rspl_pnp_debug_hypotheses.argtypes = [vp, C.c_int, C.c_int, vp, vp]
     if hasattr(lib, "rspl_frame_create"):
         lib.rspl_frame_create.argtypes = [C.POINTER(FrameConfig), C.POINTER(vp)]
         lib.rspl_frame_optimize.argtypes = [vp, vp, ip, vp]

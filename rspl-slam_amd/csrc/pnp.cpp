@@ -25,6 +25,9 @@ struct rspl_pnp {
   pnp::Out* out_dev = nullptr;
   uint8_t* inl = nullptr;
   uint8_t* inl_dev = nullptr;
+  double* hyp = nullptr;  // per-hypothesis poses and inlier counts (device)
+  int* hcnt = nullptr;
+  std::vector<int> last_iters;  // hypotheses per frame of the last solve
 };
 
 namespace {
@@ -73,7 +76,7 @@ extern "C" int rspl_pnp_create(const rspl_pnp_config* cfg, rspl_pnp** out) {
   RSPL_HIP(hipSetDevice(cfg->device));
   auto* h = new rspl_pnp();
   h->cfg = *cfg;
-  const Layout lay(cfg->max_batch, std::max(cfg->max_points, 1), (size_t)cfg->max_batch * pnp::kThreads);
+  const Layout lay(cfg->max_batch, std::max(cfg->max_points, 1), (size_t)cfg->max_batch * pnp::kMaxIters);
   h->dev_cap = h->stage_cap = lay.bytes;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
       hipMalloc((void**)&h->dev, lay.bytes) != hipSuccess || hipHostMalloc((void**)&h->stage, lay.bytes) != hipSuccess ||
@@ -82,7 +85,9 @@ extern "C" int rspl_pnp_create(const rspl_pnp_config* cfg, rspl_pnp** out) {
       hipHostGetDevicePointer((void**)&h->out_dev, h->out, 0) != hipSuccess ||
       hipHostMalloc((void**)&h->inl, std::max(cfg->max_points, 1), hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
-      hipHostGetDevicePointer((void**)&h->inl_dev, h->inl, 0) != hipSuccess) {
+      hipHostGetDevicePointer((void**)&h->inl_dev, h->inl, 0) != hipSuccess ||
+      hipMalloc((void**)&h->hyp, sizeof(double) * 12 * pnp::kMaxIters * cfg->max_batch) != hipSuccess ||
+      hipMalloc((void**)&h->hcnt, sizeof(int) * pnp::kMaxIters * cfg->max_batch) != hipSuccess) {
     set_error("rspl_pnp_create: allocation failed");
     rspl_pnp_destroy(h);
     return RSPL_E_DEVICE;
@@ -98,6 +103,8 @@ extern "C" void rspl_pnp_destroy(rspl_pnp* h) {
   if (h->stage) (void)hipHostFree(h->stage);
   if (h->out) (void)hipHostFree(h->out);
   if (h->inl) (void)hipHostFree(h->inl);
+  if (h->hyp) (void)hipFree(h->hyp);
+  if (h->hcnt) (void)hipFree(h->hcnt);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -110,8 +117,8 @@ extern "C" int rspl_pnp_solve(rspl_pnp* h, const rspl_pnp_problem* probs, int ba
   for (int b = 0; b < batch; b++) {
     const rspl_pnp_problem& p = probs[b];
     RSPL_CHECK_ARG(p.n >= 0 && (p.n == 0 || (p.points && p.keypoints)), "frame %d: bad correspondences", b);
-    RSPL_CHECK_ARG(p.iterations >= 1 && p.iterations <= pnp::kThreads, "frame %d: iterations must be 1..%d", b,
-                   pnp::kThreads);
+    RSPL_CHECK_ARG(p.iterations >= 1 && p.iterations <= pnp::kMaxIters, "frame %d: iterations must be 1..%d", b,
+                   pnp::kMaxIters);
     RSPL_CHECK_ARG(p.reprojection_error > 0 && p.confidence >= 0 && p.confidence <= 1, "frame %d: bad RANSAC params",
                    b);
     P += p.n;
@@ -125,6 +132,8 @@ extern "C" int rspl_pnp_solve(rspl_pnp* h, const rspl_pnp_problem* probs, int ba
   auto* kps = reinterpret_cast<double*>(sg + lay.kps);
   auto* sub = reinterpret_cast<int32_t*>(sg + lay.sub);
   size_t p0 = 0, s0 = 0;
+  int max_iters = 0;
+  h->last_iters.assign(batch, 0);
   for (int b = 0; b < batch; b++) {
     const rspl_pnp_problem& p = probs[b];
     pnp::Desc& d = D[b];
@@ -138,6 +147,8 @@ extern "C" int rspl_pnp_solve(rspl_pnp* h, const rspl_pnp_problem* probs, int ba
     for (int i = 0; i < 3 * p.n; i++) pts[3 * p0 + i] = (double)(float)p.points[i];      // cv::Point3f (:425)
     for (int i = 0; i < 2 * p.n; i++) kps[2 * p0 + i] = (double)(float)p.keypoints[i];   // cv::Point2f (:426)
     if (d.iters) subsets(p.n, d.iters, sub + 5 * s0);
+    max_iters = std::max(max_iters, d.iters);
+    h->last_iters[b] = d.iters;
     p0 += p.n;
     s0 += d.iters;
   }
@@ -150,7 +161,9 @@ extern "C" int rspl_pnp_solve(rspl_pnp* h, const rspl_pnp_problem* probs, int ba
   a.subsets = reinterpret_cast<const int32_t*>(h->dev + lay.sub);
   a.inl = h->inl_dev;
   a.out = h->out_dev;
-  RSPL_HIP(pnp::solve(a, batch, st));
+  a.hyp = h->hyp;
+  a.hcnt = h->hcnt;
+  RSPL_HIP(pnp::solve(a, batch, max_iters, st));
   RSPL_HIP(hipStreamSynchronize(st));
   for (int b = 0; b < batch; b++) {
     const pnp::Out& o = h->out[b];
@@ -164,4 +177,15 @@ extern "C" int rspl_pnp_solve(rspl_pnp* h, const rspl_pnp_problem* probs, int ba
     if (r.inlier) memcpy(r.inlier, h->inl + D[b].p0, probs[b].n);
   }
   return RSPL_OK;
+}
+
+extern "C" int rspl_pnp_debug_hypotheses(rspl_pnp* h, int frame, int max, int32_t* counts, double* poses) {
+  RSPL_CHECK_ARG(h && counts && poses && max >= 0, "rspl_pnp_debug_hypotheses: bad arguments");
+  RSPL_CHECK_ARG(frame >= 0 && frame < (int)h->last_iters.size(), "frame %d not in the last batch", frame);
+  const int n = std::min(max, h->last_iters[frame]);
+  if (n == 0) return 0;
+  RSPL_HIP(hipMemcpy(counts, h->hcnt + (size_t)frame * pnp::kMaxIters, sizeof(int32_t) * n, hipMemcpyDeviceToHost));
+  RSPL_HIP(hipMemcpy(poses, h->hyp + (size_t)frame * pnp::kMaxIters * 12, sizeof(double) * 12 * n,
+                     hipMemcpyDeviceToHost));
+  return n;
 }

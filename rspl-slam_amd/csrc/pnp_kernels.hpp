@@ -6,7 +6,8 @@
 namespace rspl {
 namespace pnp {
 
-constexpr int kThreads = 128;  // hypotheses per frame: RANSAC iterations <= 128
+constexpr int kMaxIters = 128;  // RANSAC iterations (hypotheses) per frame
+constexpr int kHypWaves = 4;   // hypotheses (one wave each) per workgroup of pnp_hyp_kernel
 
 struct Desc {      // one frame of the batch
   int p0, n;       // correspondences [p0, p0 + n)
@@ -29,9 +30,12 @@ struct Args {
   const int32_t* subsets; // [S][5]
   uint8_t* inl;           // [P] host-mapped
   Out* out;               // [B] host-mapped
+  double* hyp;            // [B][kMaxIters][12] hypothesis R (row-major) | t
+  int* hcnt;              // [B][kMaxIters] inlier count, -1: the minimal solver failed
 };
 
-hipError_t solve(const Args& a, int batch, hipStream_t s);
+// max_iters: the largest RANSAC iteration count of the batch (hypothesis grid width)
+hipError_t solve(const Args& a, int batch, int max_iters, hipStream_t s);
 
 }  // namespace pnp
 }  // namespace rspl

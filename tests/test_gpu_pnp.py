@@ -1,7 +1,9 @@
 """GPU SolvePnPWithCV (rspl_pnp_solve) vs the fp64 CPU restatement (oracle/pnp.c) on the same
-inputs: identical RANSAC decisions (inlier counts, inlier masks, hypotheses evaluated) and the
-refined pose within 1e-9 (rotation) / 1e-8 m.  Parity at the OpenCV boundary is unpinned
-(OpenCV is not vendored in the reference)."""
+inputs: every RANSAC hypothesis bit-exact (5-point EPnP pose and inlier count: both sides run the
+same IEEE operations in the same order, no FMA contraction -- the 5-point null space is
+degenerate, so anything less lets the Jacobi basis drift), identical RANSAC decisions (inlier
+counts, inlier masks, hypotheses evaluated) and the refined pose within 1e-9 (rotation) / 1e-8 m.
+Parity at the OpenCV boundary is unpinned (OpenCV is not vendored in the reference)."""
 import numpy as np
 import pytest
 
@@ -32,6 +34,18 @@ def _compare(g, ref):
 def test_pnp_matches_oracle(pnp, seed, n, outl, sig):
     K, X, kp, gt = SY.pnp_problem(n_points=n, outlier_frac=outl, pixel_sigma=sig, seed=seed)
     _compare(pnp.solve([(K, X, kp)])[0], oracle.pnp(K, X, kp))
+
+
+@pytest.mark.parametrize("seed,n,outl,sig", [(0, 300, 0.2, 0.8), (2, 300, 0.4, 0.8), (5, 60, 0.5, 0.8),
+                                             (7, 400, 0.25, 1.0)])
+def test_pnp_hypotheses_bit_exact(pnp, seed, n, outl, sig):
+    K, X, kp, gt = SY.pnp_problem(n_points=n, outlier_frac=outl, pixel_sigma=sig, seed=seed)
+    pnp.solve([(K, X, kp)])
+    cg, pg = pnp.debug_hypotheses(0)
+    cc, pc = oracle.pnp_hypotheses(K, X, kp, 100)
+    np.testing.assert_array_equal(cg, cc)
+    ok = cc >= 0
+    np.testing.assert_array_equal(pg[ok], pc[ok])
 
 
 def test_pnp_batch_and_edge_cases(pnp):
