@@ -300,12 +300,6 @@ int join_pairs(rspl_ba* b) {
   return RSPL_OK;
 }
 
-// RSPL_BA_HOSTLM=1: the host decides every trial (the mailbox round trip per trial)
-bool host_lm() {
-  static const bool v = getenv("RSPL_BA_HOSTLM") != nullptr;
-  return v;
-}
-
 // optimize(iters) with the LM control on the device (fast path, unsharded): the first errors, the
 // first linearisation and the control's initialisation, then `iters` trials queued back to back
 // with no host round trip -- each trial's last kernel takes the accept / reject decision (ba::LmCtrl)
@@ -321,7 +315,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
   RSPL_HIP(ba::linearize(P, Lr, A, S, true, st));
   q = ++b->seq;
   S.lm_slot = 0;
-  static const bool trace = getenv("RSPL_BA_LMTRACE") != nullptr, sync = getenv("RSPL_BA_DEVLM_SYNC") != nullptr;
+  static const bool trace = getenv("RSPL_BA_LMTRACE") != nullptr;
   if (trace && !b->lm_trace) {
     RSPL_HIP(hipMalloc((void**)&b->lm_trace, sizeof(double) * 8 * 64));
     RSPL_HIP(hipMemset(b->lm_trace, 0, sizeof(double) * 8 * 64));
@@ -353,7 +347,6 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
         set_error("BA trial launch failed: %s", hipGetErrorString(e));
         return RSPL_E_DEVICE;
       }
-      if (sync && hipStreamSynchronize(st) != hipSuccess) return RSPL_E_DEVICE;
     }
     return RSPL_OK;
   };
@@ -410,7 +403,7 @@ int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Acti
   double v[4];
   int rc;
   const bool sh = b->allreduce != nullptr;
-  if (!sh && iters > 0 && ba::fast_path(A.K) && !host_lm()) return optimize_dev(b, P, Lr, S, A, iters, chi2_out, done_out);
+  if (!sh && iters > 0 && ba::fast_path(A.K)) return optimize_dev(b, P, Lr, S, A, iters, chi2_out, done_out);
   const int n6 = 6 * A.K;
   double* so = b->red + n6 + b->nranks;  // this rank's {chi2, scale, fail} (S.shard_out)
   unsigned long long q = ++b->seq;

@@ -258,15 +258,8 @@ sg::GemmArgs G_(const float* A, int lda, const float* B, int ldb, const float* b
 // log_optimal_transport (superglue.py:185-205) on the couplings of B pairs, on stream st
 static hipError_t run_sinkhorn(rspl_sg* s, const float* cpl, float* Zp, const int* cn0, const int* cn1, int B,
                                int iters, hipStream_t st, hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr) {
-  static unsigned long long* probe = nullptr;  // debug only (RSPL_SG_PROBE)
-  static const bool probing = getenv("RSPL_SG_PROBE") != nullptr;
   hipError_t e;
-  if (probing && !probe) {
-    if ((e = hipMalloc(&probe, 5 * sizeof(unsigned long long))) != hipSuccess) return e;
-    if ((e = hipMemset(probe, 0, 5 * sizeof(unsigned long long))) != hipSuccess) return e;
-  }
   sg::SinkArgs sk{};
-  sk.probe = probe;
   sk.cpl = cpl; sk.Z = Zp; sk.cplT = s->cplT; sk.ug = s->ug; sk.vg = s->vg;
   sk.seq = s->sk_seq = (s->sk_seq % 0xFFFFFu) + 1;
   sk.spin_limit = s->spin_limit; sk.inject = s->inject;
@@ -274,16 +267,7 @@ static hipError_t run_sinkhorn(rspl_sg* s, const float* cpl, float* Zp, const in
   sk.nmax = s->nmax; sk.G = s->rbG ? s->rbG : s->G; sk.rb = s->rbG > 0; sk.sc = s->sink_sc; sk.iters = iters;
   sk.fx = 1;
   sk.sleep = 1;
-  if ((e = sg::sinkhorn(sk, B, st, t0, t1)) != hipSuccess) return e;
-  if (probing) {  // debug: Sinkhorn cycles per workgroup-iteration by phase
-    unsigned long long h[5];
-    if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-    if ((e = hipMemcpy(h, probe, sizeof(h), hipMemcpyDeviceToHost)) != hipSuccess) return e;
-    if ((e = hipMemset(probe, 0, sizeof(h))) != hipSuccess) return e;
-    if (h[4]) fprintf(stderr, "sinkhorn cycles/iter (G=%d): row %.0f gather-u %.0f col %.0f gather-v %.0f\n", s->G,
-                      (double)h[0] / h[4], (double)h[1] / h[4], (double)h[2] / h[4], (double)h[3] / h[4]);
-  }
-  return hipSuccess;
+  return sg::sinkhorn(sk, B, st, t0, t1);
 }
 
 extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_path, rspl_sg** out) {
@@ -315,7 +299,7 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
       delete s;
       return RSPL_E_DEVICE;
     }
-    constexpr int kRows = 9;  // 45 workgroups per pair at N = 400 (tools/gpu_sink_ab.sh: 32 vs 48)
+    constexpr int kRows = 9;  // 45 workgroups per pair at N = 400 (round-2 A/B: 32 vs 48)
     int G = std::max(1, (s->ld + kRows - 1) / kRows);
     while (G < s->ld && sg::sinkhorn_lds_bytes(s->nmax, G, true) > sg::kSinkLdsMax) G++;
     if (const char* e = getenv("RSPL_SG_SINK_G"); e && getenv("RSPL_SG_SINK") &&
@@ -486,12 +470,6 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
     }();
     auto layer = [&](sg::LayerArgs& la, int) { return sg::gnn_layer(la, B, st); };
     if (!unfused) {  // layer 0's q / k / v (prologue launch), then one fused launch per layer
-      static unsigned long long* lprobe = nullptr;  // debug: RSPL_SG_LPROBE
-      static const bool lprobing = getenv("RSPL_SG_LPROBE") != nullptr;
-      if (lprobing && !lprobe) {
-        RSPL_HIP(hipMalloc(&lprobe, 8 * sizeof(unsigned long long)));
-        RSPL_HIP(hipMemset(lprobe, 0, 8 * sizeof(unsigned long long)));
-      }
       {
         sg::LayerArgs la{};
         la.Qn = s->Qf[0]; la.Kn = s->Kf[0]; la.Vn = s->Vf[0];
@@ -510,17 +488,7 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
         const int ln = std::min(l + 1, kLayers - 1);
         la.Wq = s->fwqkv + (size_t)ln * 256 * 768; la.bq = s->bqkv + (size_t)ln * 768;
         la.n0 = d_n0; la.n1 = d_n1; la.nmax = nm; la.nt = s->ldv / 32; la.cross = l & 1; la.last = l == kLayers - 1;
-        la.probe = lprobe;
         RSPL_HIP(layer(la, l));
-      }
-      if (lprobing) {
-        unsigned long long h[8];
-        RSPL_HIP(hipStreamSynchronize(st));
-        RSPL_HIP(hipMemcpy(h, lprobe, sizeof(h), hipMemcpyDeviceToHost));
-        RSPL_HIP(hipMemset(lprobe, 0, sizeof(h)));
-        if (h[5])  // 100 MHz wall clock: us = ticks / 100 (17 non-last layers counted)
-          fprintf(stderr, "layer us: attention %.2f mlp0 %.2f mlp3 %.2f qkv %.2f\n", (h[1] - h[0]) / 100.0 / h[5],
-                  (h[2] - h[1]) / 100.0 / h[5], (h[3] - h[2]) / 100.0 / h[5], (h[4] - h[3]) / 100.0 / h[5]);
       }
     }
     for (int l = 0; l < kLayers && unfused; l++) {

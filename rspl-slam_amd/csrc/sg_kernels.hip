@@ -721,7 +721,6 @@ __global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, c = lane & 31, kh = lane >> 5;
   const size_t tok0 = (size_t)set * a.nmax + q0;   // first token of the tile
   const int kset = p * 2 + simg;
-  if (a.probe && !a.last && tid == 0 && bx == 0 && set == 0) a.probe[0] += wall_clock64();
   // x tile -> LDS (rows past the set clamp to its last token; never stored back)
   for (int e = tid; e < 32 * 32; e += 512) {
     const int row = e >> 5, ch = e & 31;
@@ -857,7 +856,6 @@ __global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
     }
     __syncthreads();
   }
-  if (a.probe && !a.last && tid == 0 && bx == 0 && set == 0) a.probe[1] += wall_clock64();
   const int r = lane & 31, hh = lane >> 5;
   if (!a.qkv_only) {
   // ---- (2) HID = ReLU([x | message] W1^T + b1): wave wv -> columns 64 wv .. 64 wv + 63 ----
@@ -881,7 +879,6 @@ __global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
     }
   }
   __syncthreads();
-  if (a.probe && !a.last && tid == 0 && bx == 0 && set == 0) a.probe[2] += wall_clock64();
   // ---- (3) x += HID W2^T + b2 (fp32 stream, fp16 shadow, new x into Ab): columns 32 wv .. +31 ----
   {
     floatx16 acc[1];
@@ -904,7 +901,6 @@ __global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
   if (a.last) return;
   __syncthreads();
   }
-  if (a.probe && !a.last && tid == 0 && bx == 0 && set == 0) a.probe[3] += wall_clock64();
   // ---- (4) next layer's q | k | v of these tokens: columns 96 wv .. 96 wv + 95 ----
   {
     floatx16 acc[3];
@@ -947,10 +943,6 @@ __global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
         *reinterpret_cast<half8*>(dst) = v;
       }
     }
-  }
-  if (a.probe && !a.last && tid == 0 && bx == 0 && set == 0) {
-    a.probe[4] += wall_clock64();
-    a.probe[5] += 1;
   }
 }
 
@@ -1345,13 +1337,11 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_kernel(SinkArgs a) {
   __syncthreads();  // also orders the transposed scratch copy (workgroup-private) before its reads
   unsigned long long* ug = a.ug + (size_t)p * ld;
   unsigned long long* vg = a.vg + (size_t)p * ld;
-  long long pr[4] = {0, 0, 0, 0};
   // one flag slot per exchange: a slot is rewritten only after a barrier every thread passes
   // after reading it, so all threads take the same branch
   bool failed = false;
   for (int it = 0; it < a.iters; it++) {
     const unsigned tag = (a.seq << 12) | (unsigned)(it + 1);
-    const long long q0 = __builtin_amdgcn_s_memtime();
     // u_i = log_mu_i - LSE_j(C_ij + v_j), own rows, one wave per row
     slab_lse(Rs, ld, v, Cc, nr, wv, lane, [&](int r, float lse) {
       if (lane == 0) {
@@ -1360,13 +1350,11 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_kernel(SinkArgs a) {
         __hip_atomic_store(ug + r0 + r, sk_granule(ui, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     });
-    const long long q1 = __builtin_amdgcn_s_memtime();
     bool to = sk_gather(ug, u, R, r0, r0 + nr, tag, a.spin_limit);
     if (a.inject && p == 0 && g == 0 && it == 0) to = true;  // fault injection (rspl_sg_debug_inject)
     if (to) flag[0] = 1;
     __syncthreads();
     if (flag[0]) { failed = true; break; }
-    const long long q2 = __builtin_amdgcn_s_memtime();
     // v_j = log_nu_j - LSE_i(C_ij + u_i), own columns, one wave per column
     slab_lse(Cs, ld, u, R, nc, wv, lane, [&](int c, float lse) {
       if (lane == 0) {
@@ -1375,21 +1363,13 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_kernel(SinkArgs a) {
         __hip_atomic_store(vg + c0 + c, sk_granule(vj, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
     });
-    const long long q3 = __builtin_amdgcn_s_memtime();
     if (sk_gather(vg, v, Cc, c0, c0 + nc, tag, a.spin_limit)) flag[1] = 1;
     __syncthreads();
-    const long long q4 = __builtin_amdgcn_s_memtime();
-    pr[0] += q1 - q0; pr[1] += q2 - q1; pr[2] += q3 - q2; pr[3] += q4 - q3;
     if (flag[1]) { failed = true; break; }
   }
   if (failed) {
     if (tid == 0) __hip_atomic_store(a.err + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
-  }
-  if (a.probe && tid == 0) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) atomicAdd(a.probe + k, (unsigned long long)pr[k]);
-    atomicAdd(a.probe + 4, (unsigned long long)a.iters);
   }
   // Z = ((couplings + u) + v) - norm (superglue.py:203, :219), own rows
   float* Z = a.Z + (size_t)p * ld * ld;
@@ -1466,11 +1446,9 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
   const float lmu_bin = logf(fn) + norm, lnu_bin = logf(fm) + norm;
   if (tid == 0) flag[0] = 0;
   __syncthreads();
-  long long pr[4] = {0, 0, 0, 0};
   bool failed = false;
   for (int it = 0; it < a.iters; it++) {
     const unsigned tag = (a.seq << 12) | (unsigned)(it + 1);
-    const long long q0 = __builtin_amdgcn_s_memtime();
     // row pass: all RPW rows of the wave together (independent DPP chains interleave)
     {
       float mx[RPW], sm[RPW];
@@ -1497,7 +1475,6 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
         ur[k] = r < nr ? ((r0 + r) < m ? norm : lmu_bin) - (logf(sm[k]) + mx[k]) : 0.f;
       }
     }
-    const long long q1 = __builtin_amdgcn_s_memtime();
     // column partials over the wave's rows, then over the 16 waves
 #pragma unroll
     for (int q = 0; q < kRbQ; q++) {
@@ -1517,7 +1494,6 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
       ps[wv][lane + 64 * q] = cs;
     }
     __syncthreads();
-    const long long q2 = __builtin_amdgcn_s_memtime();
     unsigned long long* slot = a.ug + (size_t)(p * 2 + (it & 1)) * G * ld;
     // two adjacent lanes per column: lane `half` merges waves 8 half .. 8 half + 7 and polls the
     // peers h with (h & 1) == half; the pair's results are combined by a lane swap in an order
@@ -1591,17 +1567,10 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
       const int j = lane + 64 * q;
       vr[q] = j < Cc ? vs[j] : 0.f;
     }
-    const long long q3 = __builtin_amdgcn_s_memtime();
-    pr[0] += q1 - q0; pr[1] += q2 - q1; pr[2] += q3 - q2;
   }
   if (failed) {
     if (tid == 0) __hip_atomic_store(a.err + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     return;
-  }
-  if (a.probe && tid == 0) {
-#pragma unroll
-    for (int k = 0; k < 4; k++) atomicAdd(a.probe + k, (unsigned long long)pr[k]);
-    atomicAdd(a.probe + 4, (unsigned long long)a.iters);
   }
   // Z = ((couplings + u) + v) - norm (superglue.py:203, :219), own rows straight from registers
   float* Z = a.Z + (size_t)p * ld * ld;

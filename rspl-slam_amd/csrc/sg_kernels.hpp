@@ -90,7 +90,6 @@ struct LayerArgs {
   int nmax, nt;          // tokens per image set; 32-key tiles per set in Kc / Vc (ldv / 32)
   int cross, last;
   int qkv_only;          // prologue: only phase (4) from the current x (layer 0's q / k / v)
-  unsigned long long* probe;  // debug (RSPL_SG_LPROBE): phase wall clocks of workgroup (0, 0)
   int nsets, xps, tpx;   // set by gnn_layer: token sets, XCDs per set (0 = plain grid), tiles per XCD
 };
 
@@ -134,7 +133,6 @@ struct SinkArgs {
   unsigned seq;       // per-call tag base (never 0; granules start zeroed)
   unsigned spin_limit;  // bounded polls per granule before the exchange is declared timed out
   int inject;         // debug: workgroup 0 of pair 0 reports a timeout at iteration 0
-  unsigned long long* probe;  // optional [5] cycle counters (RSPL_SG_PROBE): row, gather u, col, gather v, iters
   unsigned* err;      // [B] sticky timeout flags (host-mapped)
   const int* n0;
   const int* n1;

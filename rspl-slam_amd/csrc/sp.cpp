@@ -233,8 +233,8 @@ namespace {
 int nms_topk(rspl_sp* s, int B, int H, int W, int k, hipStream_t st) {
   using namespace sp;
   RSPL_HIP(hipMemsetAsync(s->cand_count, 0, sizeof(int) * B, st));
-  NmsArgs n{};
-  n.scores = s->scores; n.nms_out = s->nms; n.cand = s->cand; n.cand_count = s->cand_count; n.cand_cap = s->cand_cap;
+  NmsArgs n{};  // no NMS'd map: the candidates carry the scores, the samplers read the score map
+  n.scores = s->scores; n.nms_out = nullptr; n.cand = s->cand; n.cand_count = s->cand_count; n.cand_cap = s->cand_cap;
   n.H = H; n.W = W; n.threshold = s->cfg.keypoint_threshold; n.border = s->cfg.remove_borders;
   RSPL_HIP(nms(n, B, st));
   s->timer.mark(5, st);
@@ -302,7 +302,7 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
     TapArgs ta{};
     ta.cells = c.hout; ta.wDb = s->fwDb; ta.bDb = s->bDb;
     ta.sel = s->sel; ta.sel_count = s->sel_count; ta.sel_stride = kCandCap; ta.per_image = (k > 0 ? k : kCandCap);
-    ta.nms = s->nms; ta.features = d_features; ta.feat_cap = capacity; ta.counts = d_counts; ta.B = B; ta.H = H; ta.W = W;
+    ta.nms = s->scores; ta.features = d_features; ta.feat_cap = capacity; ta.counts = d_counts; ta.B = B; ta.H = H; ta.W = W;
     RSPL_HIP(sample_taps_h(ta, st));
     s->timer.mark(7, st);
     s->timer.end_call();
@@ -342,7 +342,7 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
   s->timer.mark(6, st);
   SampleArgs sa{};
   sa.sel = s->sel; sa.sel_count = s->sel_count; sa.sel_stride = kCandCap; sa.per_image = (k > 0 ? k : kCandCap);
-  sa.nms = s->nms; sa.desc = s->desc; sa.features = d_features; sa.feat_cap = capacity;
+  sa.nms = s->scores; sa.desc = s->desc; sa.features = d_features; sa.feat_cap = capacity;
   sa.counts = d_counts; sa.B = B; sa.H = H; sa.W = W;
   RSPL_HIP(sample(sa, st));
   s->timer.mark(7, st);
@@ -391,7 +391,16 @@ extern "C" int rspl_sp_debug_maps(rspl_sp* s, int b, float* scores, float* desc)
   RSPL_CHECK_ARG(s && b >= 0 && b < s->last_B, "no such image in the last batch");
   const int H = s->last_H, W = s->last_W;
   RSPL_HIP(hipStreamSynchronize(s->stream));
-  if (scores) RSPL_HIP(hipMemcpy(scores, s->nms + (size_t)b * H * W, sizeof(float) * H * W, hipMemcpyDeviceToHost));
+  if (scores) {  // the NMS'd map of image b, re-formed from its score map (the product path writes none)
+    RSPL_HIP(hipMemsetAsync(s->cand_count, 0, sizeof(int), s->stream));
+    sp::NmsArgs n{};
+    n.scores = s->scores + (size_t)b * H * W; n.nms_out = s->nms; n.cand = s->cand; n.cand_count = s->cand_count;
+    n.cand_cap = s->cand_cap; n.H = H; n.W = W; n.threshold = s->cfg.keypoint_threshold;
+    n.border = s->cfg.remove_borders;
+    RSPL_HIP(sp::nms(n, 1, s->stream));
+    RSPL_HIP(hipMemcpyAsync(scores, s->nms, sizeof(float) * H * W, hipMemcpyDeviceToHost, s->stream));
+    RSPL_HIP(hipStreamSynchronize(s->stream));
+  }
   if (desc) {
     RSPL_CHECK_ARG(s->cfg.precision == RSPL_PREC_FP32,
                    "RSPL_PREC_FP16 forms descriptors only at the sampled keypoints' taps (no dense map)");

@@ -755,18 +755,36 @@ __global__ __launch_bounds__(256) void sample_taps_h_kernel(TapArgs a) {
 // Fused simple_nms (5 x 9x9 max-pools) + threshold / border candidate extraction.  Scores are
 // softmax outputs (>= 0) and every window contains its centre, so zero padding outside the image
 // equals MaxPool2d's -inf padding here.  Tile 64 x 32 outputs with the 20-pixel halo the five
-// dependent pools need (104 x 72 in LDS: 3.7x the output area re-read instead of 5.1x with 32 x 32
-// tiles).  Each 1-D pass gives a thread 8 consecutive outputs from 16 register-held inputs
-// (van Herk / Gil-Werman with block 8: suffix maxima of the first 8, prefix maxima of the second,
-// out[i] = max(suffix[i], prefix[i]) = the 9-window [i, i+8]): 2 LDS reads per output instead of
-// 9.  Passes run over the whole region; values near its border are garbage that never reaches the
-// output tile (each pool shrinks the valid region by 4, five pools = the 20-pixel halo).
+// dependent pools need (104 x 72 in LDS).  Each 1-D pass gives a thread 8 consecutive outputs
+// from 16 register-held inputs (van Herk / Gil-Werman with block 8: suffix maxima of the first 8,
+// prefix maxima of the second, out[i] = max(suffix[i], prefix[i]) = the 9-window [i, i+8]): 2 LDS
+// reads per output instead of 9.  Passes run over the whole region; values near its border are
+// garbage that never reaches the output tile (each pool shrinks the valid region by 4, five pools =
+// the 20-pixel halo).
+// LDS: 10 bytes per region pixel (74.9 KB: two workgroups per CU, every tile of a C3 step in one
+// dispatch round) -- scores S and the row-pass scratch T in fp32, max_mask K and supp_mask M in
+// bytes; the two mask pools run on bytes (T reused as u8), supp_scores = M ? 0 : S is formed on the
+// fly by the score pools.  XCD-aware placement: tile order is row-major per image and the tiles are
+// dealt to the 8 XCDs in contiguous bands (blockIdx % 8 = XCD), so the halo rows a tile shares with
+// its vertical neighbours are fetched once into that XCD's L2, not once per XCD.
 // ---------------------------------------------------------------------------
 constexpr int NTX = 64, NTY = 32, NH = 20, RX = NTX + 2 * NH, RY = NTY + 2 * NH;  // 104 x 72
 static_assert(RX % 8 == 0 && (RX - 8) % 8 == 0 && (RY - 8) % 8 == 0, "8-output chunks tile the passes");
 
 // 9-window max of 16 register values: out[i] = max(v[i .. i+8]), i < 8
-__device__ __forceinline__ void window9(const float (&v)[16], float (&o)[8]) {
+template <typename V>
+__device__ __forceinline__ void window9(const V (&v)[16], V (&o)[8]) {
+  V suf[8], pre[8];
+  suf[7] = v[7];
+#pragma unroll
+  for (int i = 6; i >= 0; i--) suf[i] = v[i] > suf[i + 1] ? v[i] : suf[i + 1];
+  pre[0] = v[8];
+#pragma unroll
+  for (int i = 1; i < 8; i++) pre[i] = v[8 + i] > pre[i - 1] ? v[8 + i] : pre[i - 1];
+#pragma unroll
+  for (int i = 0; i < 8; i++) o[i] = suf[i] > pre[i] ? suf[i] : pre[i];
+}
+__device__ __forceinline__ void window9f(const float (&v)[16], float (&o)[8]) {
   float suf[8], pre[8];
   suf[7] = v[7];
 #pragma unroll
@@ -777,36 +795,63 @@ __device__ __forceinline__ void window9(const float (&v)[16], float (&o)[8]) {
 #pragma unroll
   for (int i = 0; i < 8; i++) o[i] = fmaxf(suf[i], pre[i]);
 }
-// dst[y][x] = max_{|k|<=4} src[y][x+k] for every row, x in [4, RX-4): (RX-8)/8 chunks per row
-__device__ __forceinline__ void rowpass9(const float* src, float* dst) {
+// dst[y][x] = max_{|k|<=4} src'[y][x+k] for every row, x in [4, RX-4), src' = M ? 0 : S when SUPP
+template <bool SUPP>
+__device__ __forceinline__ void rowpass9(const float* S, const unsigned char* M, float* dst) {
   constexpr int CPR = (RX - 8) / 8;
   for (int c = threadIdx.x; c < CPR * RY; c += blockDim.x) {
-    const int y = c / CPR, x0 = 4 + 8 * (c % CPR);
-    const float4* p = reinterpret_cast<const float4*>(src + y * RX + x0 - 4);
+    const int y = c / CPR, x0 = 4 + 8 * (c % CPR), b = y * RX + x0 - 4;
+    const float4* p = reinterpret_cast<const float4*>(S + b);
     float v[16];
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const float4 t = p[q];
       v[4 * q] = t.x; v[4 * q + 1] = t.y; v[4 * q + 2] = t.z; v[4 * q + 3] = t.w;
     }
+    if (SUPP) {
+      const uint2* mp = reinterpret_cast<const uint2*>(M + b);
+      const uint2 m0 = mp[0], m1 = mp[1];
+      const unsigned mw[4] = {m0.x, m0.y, m1.x, m1.y};
+#pragma unroll
+      for (int k = 0; k < 16; k++) v[k] = ((mw[k >> 2] >> (8 * (k & 3))) & 0xff) ? 0.f : v[k];
+    }
     float o[8];
-    window9(v, o);
+    window9f(v, o);
     float4* d = reinterpret_cast<float4*>(dst + y * RX + x0);
     d[0] = make_float4(o[0], o[1], o[2], o[3]);
     d[1] = make_float4(o[4], o[5], o[6], o[7]);
   }
 }
+// the byte (mask) row pass: dst[y][x] = max_{|k|<=4} src[y][x+k]
+__device__ __forceinline__ void rowpass9_u8(const unsigned char* src, unsigned char* dst) {
+  constexpr int CPR = (RX - 8) / 8;
+  for (int c = threadIdx.x; c < CPR * RY; c += blockDim.x) {
+    const int y = c / CPR, x0 = 4 + 8 * (c % CPR), b = y * RX + x0 - 4;
+    const uint2* mp = reinterpret_cast<const uint2*>(src + b);
+    const uint2 m0 = mp[0], m1 = mp[1];
+    const unsigned mw[4] = {m0.x, m0.y, m1.x, m1.y};
+    unsigned v[16];
+#pragma unroll
+    for (int k = 0; k < 16; k++) v[k] = (mw[k >> 2] >> (8 * (k & 3))) & 0xff;
+    unsigned o[8];
+    window9(v, o);
+    uint2 w;
+    w.x = o[0] | (o[1] << 8) | (o[2] << 16) | (o[3] << 24);
+    w.y = o[4] | (o[5] << 8) | (o[6] << 16) | (o[7] << 24);
+    *reinterpret_cast<uint2*>(dst + y * RX + x0) = w;
+  }
+}
 // dst[y][x] = max_{|k|<=4} src[y+k][x] for every column, y in [4, RY-4); F(o, x, y0) consumes the
-// 8 outputs of column x from row y0 (a store, or the max_mask update)
-template <typename F>
-__device__ __forceinline__ void colpass9(const float* src, F&& out) {
+// 8 outputs of column x from row y0
+template <typename V, typename F>
+__device__ __forceinline__ void colpass9(const V* src, F&& out) {
   constexpr int CPC = (RY - 8) / 8;
   for (int c = threadIdx.x; c < CPC * RX; c += blockDim.x) {
     const int x = c % RX, y0 = 4 + 8 * (c / RX);
-    float v[16];
+    V v[16];
 #pragma unroll
     for (int k = 0; k < 16; k++) v[k] = src[(y0 - 4 + k) * RX + x];
-    float o[8];
+    V o[8];
     window9(v, o);
     out(o, x, y0);
   }
@@ -814,25 +859,26 @@ __device__ __forceinline__ void colpass9(const float* src, F&& out) {
 
 __global__ __launch_bounds__(1024) void nms_kernel(NmsArgs a) {
   __shared__ __attribute__((aligned(16))) float S[RY * RX];  // scores (0 outside the image)
-  __shared__ __attribute__((aligned(16))) float T[RY * RX];  // row-pass result
-  __shared__ __attribute__((aligned(16))) float M[RY * RX];  // supp flag (1 / 0)
-  __shared__ __attribute__((aligned(16))) float F[RY * RX];  // mask as float / supp_scores
-  __shared__ unsigned char K[RY * RX];                       // max_mask
+  __shared__ __attribute__((aligned(16))) float T[RY * RX];  // row-pass result (fp32, or bytes)
+  __shared__ __attribute__((aligned(16))) unsigned char K[RY * RX];  // max_mask
+  __shared__ __attribute__((aligned(16))) unsigned char M[RY * RX];  // supp_mask
+  unsigned char* T8 = reinterpret_cast<unsigned char*>(T);
   const int H = a.H, W = a.W;
   const int tiles_x = (W + NTX - 1) / NTX, tiles_y = (H + NTY - 1) / NTY;
-  const int per = tiles_x * tiles_y;
-  const int bi = blockIdx.x / per, t = blockIdx.x % per;
+  const int per = tiles_x * tiles_y, total = a.B * per, band = (total + 7) / 8;
+  const int lt = ((int)blockIdx.x & 7) * band + ((int)blockIdx.x >> 3);  // XCD band placement
+  if (lt >= total) return;
+  const int bi = lt / per, t = lt % per;
   const int y0 = (t / tiles_x) * NTY - NH, x0 = (t % tiles_x) * NTX - NH;
   const float* sc = a.scores + (size_t)bi * H * W;
   for (int i = threadIdx.x; i < RY * RX; i += blockDim.x) {
     const int ly = i / RX, lx = i - ly * RX;
     const int y = y0 + ly, x = x0 + lx;
     S[i] = (y >= 0 && y < H && x >= 0 && x < W) ? sc[(size_t)y * W + x] : 0.f;
-    K[i] = 0;
   }
   __syncthreads();
   // max_mask = scores == max_pool(scores)
-  rowpass9(S, T);
+  rowpass9<false>(S, M, T);
   __syncthreads();
   colpass9(T, [&](const float (&o)[8], int x, int y) {
 #pragma unroll
@@ -840,31 +886,30 @@ __global__ __launch_bounds__(1024) void nms_kernel(NmsArgs a) {
   });
   __syncthreads();
   for (int it = 0; it < 2; it++) {
-    for (int i = threadIdx.x; i < RY * RX; i += blockDim.x) F[i] = K[i] ? 1.f : 0.f;
+    // supp_mask = max_pool(max_mask) > 0 (byte pools)
+    rowpass9_u8(K, T8);
     __syncthreads();
-    // supp_mask = max_pool(max_mask) > 0; supp_scores = where(supp_mask, 0, scores)
-    rowpass9(F, T);
-    __syncthreads();
-    colpass9(T, [&](const float (&o)[8], int x, int y) {
+    colpass9(T8, [&](const unsigned char (&o)[8], int x, int y) {
 #pragma unroll
-      for (int k = 0; k < 8; k++) M[(y + k) * RX + x] = o[k] > 0.f ? 1.f : 0.f;
+      for (int k = 0; k < 8; k++) M[(y + k) * RX + x] = o[k] > 0;
     });
     __syncthreads();
-    for (int i = threadIdx.x; i < RY * RX; i += blockDim.x) F[i] = M[i] > 0.f ? 0.f : S[i];
-    __syncthreads();
-    // new_max_mask = supp_scores == max_pool(supp_scores); max_mask |= new_max_mask & ~supp_mask
-    rowpass9(F, T);
+    // supp_scores = where(supp_mask, 0, scores); new_max_mask = supp_scores == max_pool(supp_scores);
+    // max_mask |= new_max_mask & ~supp_mask
+    rowpass9<true>(S, M, T);
     __syncthreads();
     colpass9(T, [&](const float (&o)[8], int x, int y) {
 #pragma unroll
       for (int k = 0; k < 8; k++) {
         const int i = (y + k) * RX + x;
-        K[i] = K[i] | ((F[i] == o[k]) && !(M[i] > 0.f));
+        const bool m = M[i] != 0;
+        const float f = m ? 0.f : S[i];
+        K[i] = K[i] | ((f == o[k]) && !m);
       }
     });
     __syncthreads();
   }
-  // output region [NH, NH+NTY) x [NH, NH+NTX): NMS'd map + candidates
+  // output region [NH, NH+NTY) x [NH, NH+NTX): NMS'd map (debug entry points only) + candidates
   for (int i = threadIdx.x; i < NTX * NTY; i += blockDim.x) {
     const int ly = NH + i / NTX, lx = NH + i % NTX;
     const int y = y0 + ly, x = x0 + lx;
@@ -1117,7 +1162,9 @@ hipError_t sample_taps_h(const TapArgs& a, hipStream_t s) {
 
 hipError_t nms(const NmsArgs& a, int B, hipStream_t s) {
   const int tiles = ((a.W + NTX - 1) / NTX) * ((a.H + NTY - 1) / NTY);
-  hipLaunchKernelGGL(nms_kernel, dim3(B * tiles), dim3(1024), 0, s, a);
+  NmsArgs b = a;
+  b.B = B;
+  hipLaunchKernelGGL(nms_kernel, dim3(8 * ((B * tiles + 7) / 8)), dim3(1024), 0, s, b);
   return hipGetLastError();
 }
 

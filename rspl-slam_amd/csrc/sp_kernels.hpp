@@ -53,7 +53,7 @@ struct TapArgs {         // descriptors at the sampled keypoints' bilinear taps 
   const int* sel_count;
   int sel_stride;
   int per_image;         // keypoint slots per image (>= max selected)
-  const float* nms;      // [B][H][W]
+  const float* nms;      // [B][H][W] score map: a kept keypoint's NMS'd value is its score
   double* features;      // [B][feat_cap][259]
   int feat_cap;
   int32_t* counts;       // [B]
@@ -62,13 +62,14 @@ struct TapArgs {         // descriptors at the sampled keypoints' bilinear taps 
 
 struct NmsArgs {
   const float* scores;   // [B][H][W]
-  float* nms_out;        // [B][H][W]
+  float* nms_out;        // [B][H][W] NMS'd map (debug entry points; null on the product path)
   unsigned long long* cand;  // [B][cand_cap]
   int* cand_count;       // [B]
   int cand_cap;
   int H, W;
   double threshold;
   int border;
+  int B;                 // images (set by nms())
 };
 
 struct TopkArgs {
@@ -87,7 +88,7 @@ struct SampleArgs {
   const int* sel_count;
   int sel_stride;        // row stride of sel
   int per_image;         // waves launched per image (>= max selected)
-  const float* nms;      // [B][H][W]
+  const float* nms;      // [B][H][W] score map: a kept keypoint's NMS'd value is its score
   const float* desc;     // [B][H/8][W/8][256]
   double* features;      // [B][feat_cap][259]
   int feat_cap;
