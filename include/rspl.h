@@ -530,8 +530,9 @@ int rspl_map_get_frame_slots(const rspl_map* m, int frame_id, int32_t* mappoints
 int rspl_map_save_trajectory(const rspl_map* m, const char* path);
 
 /* ------------------------------------------------------------------------------------------ */
-/* Line front end after the detector.  FLD (cv::ximgproc) and the RCF edge  */
-/* net are not rebuilt: detected segments enter here.                                          */
+/* Line front end: the detector (cv::resize + FLD, restated, parity         */
+/* unpinned), then the merge passes, the point-line assignment and the line matching.  The RCF */
+/* edge net is not rebuilt (no weights): its edge map is the detector's input.                */
 /* ------------------------------------------------------------------------------------------ */
 
 /* LineDetector::LineExtractor after fld->detect (src/line_processor.cc:460-490): segments
@@ -585,6 +586,24 @@ int rspl_lines_stereo_device(rspl_lines* h, const double* d_lines_left, int n_le
                              const int32_t* d_match_idx, const double* camera_limits, double* d_lines_right_out,
                              uint8_t* d_lines_right_valid, void* stream);
 int rspl_lines_status(rspl_lines* h, int* overflow);
+
+/* LineDetector's detector (src/line_processor.cc:455-466): cv::resize(image, 0.5, 0.5,
+ * INTER_LINEAR) and cv::ximgproc::FastLineDetector(length_threshold, distance_threshold,
+ * canny_th1, canny_th2, canny_aperture_size, do_merge = false)->detect on the half image, as the
+ * reference runs it on the RCF edge map (map_builder.cc:286, 327).  FLD is OpenCV contrib (not
+ * vendored, absent): restated (oracle/fld_ref.py), parity unpinned.  The resize, the Sobel
+ * gradients and Canny's non-maximum suppression / thresholds run on the GPU; hysteresis, chaining
+ * and segment fitting on the host.  segments [n][4] float (x1 y1 x2 y2) on the HALF image, as
+ * fld->detect returns them (rspl_line_extract scales and merges); even image sizes; *n_out is set
+ * even when it exceeds capacity (RSPL_E_CAPACITY). */
+typedef struct {
+  int length_threshold;          /* 10 (configs/configs_euroc.yaml:31) */
+  double distance_threshold;     /* 1.414213562 */
+  double canny_th1, canny_th2;   /* 200, 250 */
+  int canny_aperture_size;       /* 3 (the only size supported) */
+} rspl_fld_config;
+int rspl_lines_detect(rspl_lines* h, const uint8_t* image, int H, int W, int stride, const rspl_fld_config* cfg,
+                      float* segments, int capacity, int* n_out);
 
 #ifdef __cplusplus
 }

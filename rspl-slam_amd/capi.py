@@ -36,7 +36,7 @@ EXPORTS = [
     "rspl_ba_set_comm", "rspl_group_create", "rspl_group_destroy", "rspl_ba_set_group",
     "rspl_pnp_create", "rspl_pnp_solve", "rspl_pnp_destroy", "rspl_pnp_debug_hypotheses",
     "rspl_line_extract", "rspl_lines_create", "rspl_lines_destroy", "rspl_lines_assign", "rspl_lines_match",
-    "rspl_lines_stereo", "rspl_lines_stereo_device", "rspl_lines_status",
+    "rspl_lines_stereo", "rspl_lines_stereo_device", "rspl_lines_status", "rspl_lines_detect",
 ]
 
 

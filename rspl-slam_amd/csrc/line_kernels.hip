@@ -332,6 +332,81 @@ __global__ void set_counts_kernel(int* n_lines, int nl0, int nl1, int* n_points,
   }
 }
 
+// ---------------------------------------------------------------------------
+// Detector front: one 512-thread workgroup per 32 x 16 tile of the half image.  The half image
+// with a 2-pixel halo (clamped = BORDER_REPLICATE; each pixel (a + b + c + d + 2) >> 2 of its 2x2
+// full-size block, cv::resize's 11-bit fixed point at scale 1/2) goes to LDS, then the L1 Sobel
+// magnitudes with a 1-pixel halo (0 outside the image, as Canny's zero-padded magnitude rows),
+// then each pixel's class: the TG22 / TG67 fixed-point sector (canny.cpp), its strict / non-strict
+// neighbour tests, low / high thresholds.  Integer work: bit-exact with oracle/fld_ref.py.
+// ---------------------------------------------------------------------------
+constexpr int kCTX = 32, kCTY = 16;  // half-image tile per workgroup
+__global__ __launch_bounds__(512) void canny_kernel(CannyArgs a) {
+  constexpr int HX = kCTX + 4, HY = kCTY + 4, MX = kCTX + 2, MY = kCTY + 2;
+  __shared__ int hs[HY * HX];
+  __shared__ int mg[MY * MX];
+  const int h = a.H / 2, w = a.W / 2;
+  const int tx0 = blockIdx.x * kCTX, ty0 = blockIdx.y * kCTY, tid = threadIdx.x;
+  for (int i = tid; i < HY * HX; i += 512) {
+    const int ly = i / HX, lx = i - ly * HX;
+    const int y = min(max(ty0 - 2 + ly, 0), h - 1), x = min(max(tx0 - 2 + lx, 0), w - 1);
+    const uint8_t* r0 = a.img + (size_t)(2 * y) * a.stride + 2 * x;
+    const uint8_t* r1 = r0 + a.stride;
+    hs[i] = ((int)r0[0] + r0[1] + r1[0] + r1[1] + 2) >> 2;
+  }
+  __syncthreads();
+  auto sob = [&](int ly, int lx, int& dx, int& dy) {  // (ly, lx) in hs coordinates, interior
+    const int* p = hs + ly * HX + lx;
+    dx = (p[-HX + 1] - p[-HX - 1]) + 2 * (p[1] - p[-1]) + (p[HX + 1] - p[HX - 1]);
+    dy = (p[HX - 1] - p[-HX - 1]) + 2 * (p[HX] - p[-HX]) + (p[HX + 1] - p[-HX + 1]);
+  };
+  for (int i = tid; i < MY * MX; i += 512) {
+    const int ly = i / MX, lx = i - ly * MX;
+    const int y = ty0 - 1 + ly, x = tx0 - 1 + lx;
+    int m = 0;
+    if (y >= 0 && y < h && x >= 0 && x < w) {
+      int dx, dy;
+      sob(ly + 1, lx + 1, dx, dy);
+      m = abs(dx) + abs(dy);
+    }
+    mg[i] = m;
+  }
+  __syncthreads();
+  constexpr long long TG22 = 13573;  // (int)(0.41421356... * 2^15 + 0.5)
+  for (int i = tid; i < kCTX * kCTY; i += 512) {
+    const int ly = i / kCTX, lx = i - ly * kCTX;
+    const int y = ty0 + ly, x = tx0 + lx;
+    if (y >= h || x >= w) continue;
+    int dx, dy;
+    sob(ly + 2, lx + 2, dx, dy);
+    const int* mp = mg + (ly + 1) * MX + (lx + 1);
+    const int m = mp[0];
+    uint8_t c = 1;
+    if (m > a.low) {
+      const long long xa = abs(dx), ya = (long long)abs(dy) << 15;
+      const long long tg22x = xa * TG22;
+      bool ok;
+      if (ya < tg22x) {
+        ok = m > mp[-1] && m >= mp[1];
+      } else if (ya > tg22x + (xa << 16)) {
+        ok = m > mp[-MX] && m >= mp[MX];
+      } else {
+        const int s = (dx ^ dy) < 0 ? -1 : 1;
+        ok = m > mp[-MX - s] && m > mp[MX + s];
+      }
+      if (ok) c = m > a.high ? 2 : 0;
+    }
+    a.cls[(size_t)y * w + x] = c;
+    a.half[(size_t)y * w + x] = (uint8_t)hs[(ly + 2) * HX + lx + 2];
+  }
+}
+
+hipError_t canny_classes(const CannyArgs& a, hipStream_t s) {
+  const int h = a.H / 2, w = a.W / 2;
+  hipLaunchKernelGGL(canny_kernel, dim3((w + kCTX - 1) / kCTX, (h + kCTY - 1) / kCTY), dim3(512), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t set_counts(int* n_lines, int nl0, int nl1, int* n_points, const int32_t* counts, int* n_matches,
                       hipStream_t s) {
   hipLaunchKernelGGL(set_counts_kernel, dim3(1), dim3(64), 0, s, n_lines, nl0, nl1, n_points, counts, n_matches);

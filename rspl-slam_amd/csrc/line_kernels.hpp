@@ -71,6 +71,19 @@ struct RightArgs {
   uint8_t* valid;           // [n_left]
 };
 
+// the detector's front (LineDetector::LineExtractor, line_processor.cc:464-465): cv::resize(0.5,
+// INTER_LINEAR) of the u8 image and cv::Canny's per-pixel classification of the half image
+// (3x3 Sobel, replicated border, L1 magnitude, the non-maximum suppression sectors, thresholds):
+// half [h][w] u8, cls [h][w] u8 (2 strong, 0 candidate, 1 none), h = H / 2, w = W / 2
+struct CannyArgs {
+  const uint8_t* img;
+  int H, W, stride;
+  uint8_t* half;
+  uint8_t* cls;
+  int low, high;
+};
+hipError_t canny_classes(const CannyArgs& a, hipStream_t s);
+
 hipError_t assign(const AssignArgs& a, int B, hipStream_t s);
 // device-side counts of a device call: n_lines = {nl0, nl1}, n_points = counts[0..1], zeroed n_matches
 hipError_t set_counts(int* n_lines, int nl0, int nl1, int* n_points, const int32_t* counts, int* n_matches,

@@ -12,6 +12,7 @@
 // depends on the order): it stays on the host, in the reference's float / double types.  FLD
 // itself (cv::ximgproc) and the RCF edge net are not rebuilt: segments enter through the API.
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <cstring>
 #include <numeric>
@@ -233,6 +234,11 @@ struct rspl_lines {
   double *lines, *pts, *dist;
   int *n_lines, *n_points, *offsets, *idx, *status;
   int *matches, *n_matches, *M, *inv, *out;
+  // detector (rspl_lines_detect): device image / half image / classes, pinned host copies; grown on demand
+  uint8_t *d_img = nullptr, *d_det = nullptr, *h_img = nullptr, *h_det = nullptr;
+  size_t det_cap = 0;  // pixels of the largest full-size image so far
+  std::vector<uint8_t> edge;
+  std::vector<int> stack;
 };
 
 extern "C" int rspl_lines_create(const rspl_lines_config* cfg, rspl_lines** out) {
@@ -279,6 +285,10 @@ extern "C" int rspl_lines_create(const rspl_lines_config* cfg, rspl_lines** out)
 extern "C" void rspl_lines_destroy(rspl_lines* h) {
   if (!h) return;
   if (h->stream) (void)hipStreamSynchronize(h->stream);
+  if (h->d_img) (void)hipFree(h->d_img);
+  if (h->d_det) (void)hipFree(h->d_det);
+  if (h->h_img) (void)hipHostFree(h->h_img);
+  if (h->h_det) (void)hipHostFree(h->h_det);
   h->arena.release();
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
@@ -494,6 +504,262 @@ extern "C" int rspl_lines_status(rspl_lines* h, int* overflow) {
   int st[3] = {0, 0, 0};
   RSPL_HIP(hipMemcpy(st, h->status, sizeof(st), hipMemcpyDeviceToHost));
   *overflow = st[0] | st[1] | st[2];
+  return RSPL_OK;
+}
+
+// ---------------------------------------------------------------------------------------------
+// LineDetector's detector: cv::resize(0.5, INTER_LINEAR) + fld->detect (line_processor.cc:455-466,
+// FastLineDetector with do_merge false), restated as oracle/fld_ref.py.  The pixel-parallel front
+// (resize, Sobel, Canny's non-maximum suppression and thresholds) runs on the GPU
+// (line_kernels.hip canny_kernel); the order-dependent rest runs here on the host, exactly as the
+// restatement orders it: 8-connected hysteresis, the corner zeroing, chains from raster-order seeds
+// (getPointChain), straight runs (extractSegments, cv::fitLine DIST_L2 refits), the length and
+// border filters in float, and the brighter-side-left orientation.  Double / float types and
+// operation order follow the restatement (FP contraction is off in this file): bit-exact with it.
+// ---------------------------------------------------------------------------------------------
+namespace {
+
+struct FSeg {
+  float x1, y1, x2, y2;
+};
+struct HLine {
+  double a, b, c;
+};
+
+HLine line_through(double px, double py, double qx, double qy) {
+  const double a = py - qy, b = qx - px, c = px * qy - py * qx;
+  const double n = std::sqrt(a * a + b * b);
+  return {a / n, b / n, c / n};
+}
+
+HLine fit_line(const std::vector<std::pair<int, int>>& pts, size_t n) {  // the first n points
+  double sx = 0, sy = 0, sxx = 0, syy = 0, sxy = 0;
+  for (size_t k = 0; k < n; k++) {
+    const double x = pts[k].first, y = pts[k].second;
+    sx += x;
+    sy += y;
+    sxx += (double)((long long)pts[k].first * pts[k].first);
+    syy += (double)((long long)pts[k].second * pts[k].second);
+    sxy += (double)((long long)pts[k].first * pts[k].second);
+  }
+  const double cnt = (double)n, cx = sx / cnt, cy = sy / cnt;
+  const double dxx = sxx / cnt - cx * cx, dyy = syy / cnt - cy * cy, dxy = sxy / cnt - cx * cy;
+  const double t = std::atan2(2.0 * dxy, dxx - dyy) / 2.0;
+  const double vx = std::cos(t), vy = std::sin(t);
+  return line_through(cx, cy, cx + vx, cy + vy);
+}
+
+inline double ldist(const HLine& l, double x, double y) { return std::fabs(l.a * x + l.b * y + l.c); }
+
+void extract_segments(const std::vector<std::pair<int, int>>& pts, int len_thr, double dist_thr,
+                      std::vector<std::array<double, 4>>& out) {
+  const int total = (int)pts.size();
+  std::vector<std::pair<int, int>> run;
+  int i = 0;
+  while (i + len_thr < total) {
+    const auto ps = pts[i], pe = pts[i + len_thr];
+    HLine l = line_through(ps.first, ps.second, pe.first, pe.second);
+    bool is_line = true;
+    for (int j = 1; j < len_thr && is_line; j++) is_line = ldist(l, pts[i + j].first, pts[i + j].second) <= dist_thr;
+    if (!is_line) {
+      i++;
+      continue;
+    }
+    run.assign(pts.begin() + i, pts.begin() + i + len_thr + 1);
+    l = fit_line(run, run.size());
+    int j = i + len_thr + 1;
+    for (; j < total; j++) {
+      const double x = pts[j].first, y = pts[j].second;
+      if (ldist(l, x, y) > dist_thr) {
+        l = fit_line(run, run.size());
+        if (ldist(l, x, y) > dist_thr) break;
+      }
+      run.push_back(pts[j]);
+    }
+    l = fit_line(run, run.size());
+    auto proj = [&](const std::pair<int, int>& p, double& ox, double& oy) {
+      const double d = l.a * p.first + l.b * p.second + l.c;
+      ox = p.first - d * l.a;
+      oy = p.second - d * l.b;
+    };
+    std::array<double, 4> sg;
+    proj(run.front(), sg[0], sg[1]);
+    proj(run.back(), sg[2], sg[3]);
+    out.push_back(sg);
+    i = j;
+  }
+}
+
+// brighter side on the left: intensity difference at +-1.5 px along the normal, one sample per pixel
+FSeg orient(const uint8_t* img, int h, int w, FSeg s) {
+  const double x1 = s.x1, y1 = s.y1, x2 = s.x2, y2 = s.y2;
+  const double dx = x2 - x1, dy = y2 - y1;
+  const double L = std::sqrt(dx * dx + dy * dy);
+  const double nx = -dy / L, ny = dx / L;
+  const int n = std::max(1, (int)L);
+  long long acc = 0;
+  for (int k = 0; k < n; k++) {
+    const double t = (k + 0.5) / n;
+    const double px = x1 + t * dx, py = y1 + t * dy;
+    const int lx = (int)std::floor(px + 1.5 * nx + 0.5), ly = (int)std::floor(py + 1.5 * ny + 0.5);
+    const int rx = (int)std::floor(px - 1.5 * nx + 0.5), ry = (int)std::floor(py - 1.5 * ny + 0.5);
+    if (lx >= 0 && lx < w && ly >= 0 && ly < h && rx >= 0 && rx < w && ry >= 0 && ry < h)
+      acc += (int)img[(size_t)ly * w + lx] - (int)img[(size_t)ry * w + rx];
+  }
+  if (acc < 0) return {s.x2, s.y2, s.x1, s.y1};
+  return s;
+}
+
+// getPointChain: neighbour index order (dr, dc); step 0 takes the first edge neighbour, later
+// steps the most direction-consistent one (ties to the later index) if within 2
+const int kNb[8][2] = {{1, 1}, {1, 0}, {1, -1}, {0, -1}, {-1, -1}, {-1, 0}, {-1, 1}, {0, 1}};
+bool chain_step(const uint8_t* e, int h, int w, int& x, int& y, int& direction, int step) {
+  float best = 7.0f;
+  int bx = 0, by = 0, bd = 0;
+  bool found = false;
+  for (int i = 0; i < 8; i++) {
+    const int ci = x + kNb[i][1], ri = y + kNb[i][0];
+    if (ri < 0 || ri == h || ci < 0 || ci == w || e[(size_t)ri * w + ci] == 0) continue;
+    const int d = i > 4 ? i - 8 : i;
+    if (step == 0) {
+      x = ci;
+      y = ri;
+      direction = d;
+      return true;
+    }
+    float diff = std::fabs((float)d - (float)direction);
+    diff = diff > 4.0f ? 8.0f - diff : diff;
+    if (diff <= best) {
+      best = diff;
+      bx = ci;
+      by = ri;
+      bd = d;
+      found = true;
+    }
+  }
+  if (found && best < 2.0f) {
+    x = bx;
+    y = by;
+    direction = bd;
+    return true;
+  }
+  return false;
+}
+
+}  // namespace
+
+extern "C" int rspl_lines_detect(rspl_lines* h, const uint8_t* image, int H, int W, int stride,
+                                 const rspl_fld_config* cfg, float* segments, int capacity, int* n_out) {
+  RSPL_CHECK_ARG(h && image && cfg && n_out && (segments || capacity == 0), "rspl_lines_detect: NULL argument");
+  RSPL_CHECK_ARG(H >= 4 && W >= 4 && H % 2 == 0 && W % 2 == 0 && stride >= W,
+                 "image %dx%d (stride %d): even sizes >= 4 required", W, H, stride);
+  RSPL_CHECK_ARG(cfg->canny_aperture_size == 3, "canny_aperture_size %d: only 3 (the configs' value)",
+                 cfg->canny_aperture_size);
+  RSPL_CHECK_ARG(cfg->length_threshold >= 1 && cfg->distance_threshold >= 0, "bad FLD thresholds");
+  *n_out = 0;
+  const size_t px = (size_t)H * W, hp = px / 4;
+  const int hh = H / 2, hw = W / 2;
+  if (px > h->det_cap) {  // grow the detector buffers (the stream is idle between calls)
+    RSPL_HIP(hipStreamSynchronize(h->stream));
+    if (h->d_img) (void)hipFree(h->d_img);
+    if (h->d_det) (void)hipFree(h->d_det);
+    if (h->h_img) (void)hipHostFree(h->h_img);
+    if (h->h_det) (void)hipHostFree(h->h_det);
+    h->d_img = h->d_det = h->h_img = h->h_det = nullptr;
+    h->det_cap = 0;
+    RSPL_HIP(hipMalloc((void**)&h->d_img, px));
+    RSPL_HIP(hipMalloc((void**)&h->d_det, 2 * (px / 4)));
+    RSPL_HIP(hipHostMalloc((void**)&h->h_img, px));
+    RSPL_HIP(hipHostMalloc((void**)&h->h_det, 2 * (px / 4)));
+    h->det_cap = px;
+  }
+  for (int r = 0; r < H; r++) memcpy(h->h_img + (size_t)r * W, image + (size_t)r * stride, W);
+  hipStream_t st = h->stream;
+  RSPL_HIP(hipMemcpyAsync(h->d_img, h->h_img, px, hipMemcpyHostToDevice, st));
+  double lo = cfg->canny_th1, hi = cfg->canny_th2;
+  if (lo > hi) std::swap(lo, hi);
+  lines::CannyArgs a{};
+  a.img = h->d_img; a.H = H; a.W = W; a.stride = W;
+  a.half = h->d_det; a.cls = h->d_det + hp;
+  a.low = (int)std::floor(lo); a.high = (int)std::floor(hi);
+  RSPL_HIP(lines::canny_classes(a, st));
+  RSPL_HIP(hipMemcpyAsync(h->h_det, h->d_det, 2 * hp, hipMemcpyDeviceToHost, st));
+  RSPL_HIP(hipStreamSynchronize(st));
+  const uint8_t* half = h->h_det;
+  const uint8_t* cls = h->h_det + hp;
+  // hysteresis: strong pixels through 8-connected candidates (the edge set does not depend on order)
+  std::vector<uint8_t>& e = h->edge;
+  std::vector<int>& stk = h->stack;
+  e.assign(hp, 0);
+  stk.clear();
+  for (size_t i = 0; i < hp; i++)
+    if (cls[i] == 2) {
+      e[i] = 255;
+      stk.push_back((int)i);
+    }
+  while (!stk.empty()) {
+    const int i = stk.back();
+    stk.pop_back();
+    const int r = i / hw, c = i - r * hw;
+    for (int dr = -1; dr <= 1; dr++)
+      for (int dc = -1; dc <= 1; dc++) {
+        const int rr = r + dr, cc = c + dc;
+        if (rr < 0 || rr >= hh || cc < 0 || cc >= hw) continue;
+        const size_t k = (size_t)rr * hw + cc;
+        if (cls[k] == 0 && e[k] == 0) {
+          e[k] = 255;
+          stk.push_back((int)k);
+        }
+      }
+  }
+  // the corner zeroing of OpenCV's lineDetection (top-left 6 x 6, bottom-right 5 x 5)
+  for (int r = 0; r < std::min(6, hh); r++)
+    for (int c = 0; c < std::min(6, hw); c++) e[(size_t)r * hw + c] = 0;
+  for (int r = std::max(hh - 5, 0); r < hh; r++)
+    for (int c = std::max(hw - 5, 0); c < hw; c++) e[(size_t)r * hw + c] = 0;
+  const int lt = cfg->length_threshold;
+  const double dt = cfg->distance_threshold;
+  std::vector<std::pair<int, int>> pts;
+  std::vector<std::array<double, 4>> segs;
+  int n = 0;
+  for (int r = 0; r < hh; r++)
+    for (int c = 0; c < hw; c++) {
+      if (e[(size_t)r * hw + c] == 0) continue;
+      pts.clear();
+      pts.emplace_back(c, r);
+      e[(size_t)r * hw + c] = 0;
+      int x = c, y = r, direction = 0, step = 0;
+      while (chain_step(e.data(), hh, hw, x, y, direction, step)) {
+        pts.emplace_back(x, y);
+        step++;
+        e[(size_t)y * hw + x] = 0;
+      }
+      if ((int)pts.size() < lt + 1) continue;
+      segs.clear();
+      extract_segments(pts, lt, dt, segs);
+      for (const auto& sg : segs) {
+        const FSeg s{(float)sg[0], (float)sg[1], (float)sg[2], (float)sg[3]};
+        const float ddx = s.x1 - s.x2, ddy = s.y1 - s.y2;
+        const float length = std::sqrt(ddx * ddx + ddy * ddy);
+        if (length < (float)lt) continue;
+        if ((s.x1 <= 5.0f && s.x2 <= 5.0f) || (s.y1 <= 5.0f && s.y2 <= 5.0f) ||
+            (s.x1 >= hw - 5.0f && s.x2 >= hw - 5.0f) || (s.y1 >= hh - 5.0f && s.y2 >= hh - 5.0f))
+          continue;
+        const FSeg o = orient(half, hh, hw, s);
+        if (n < capacity) {
+          segments[4 * n + 0] = o.x1;
+          segments[4 * n + 1] = o.y1;
+          segments[4 * n + 2] = o.x2;
+          segments[4 * n + 3] = o.y2;
+        }
+        n++;
+      }
+    }
+  *n_out = n;
+  if (n > capacity) {
+    set_error("%d segments exceed capacity %d", n, capacity);
+    return RSPL_E_CAPACITY;
+  }
   return RSPL_OK;
 }
 

@@ -1,7 +1,10 @@
-"""Line front end after the detector over the rspl_line* C ABI.
+"""Line front end over the rspl_line* C ABI.
 
 Mirrors the reference's free functions and LineDetector (include/line_processor.h:22-61):
 
+  LineDetector              createFastLineDetector(config) + LineExtractor(image) (line_processor.cc:
+                            455-490): cv::resize(0.5) + FLD (restated: GPU resize / Sobel / Canny
+                            classification, host hysteresis / chaining / fitting), then the merges
   LineExtractor(segments)   LineDetector::LineExtractor after fld->detect (line_processor.cc:460-490):
                             the x2 scale and the two MergeLines / FilterShortLines passes (host C++)
   AssignPointsToLines       line_processor.cc:163-216 (GPU) -> list of {point index: distance}
@@ -11,8 +14,9 @@ Mirrors the reference's free functions and LineDetector (include/line_processor.
   stereo_lines_device       the same, device-resident (SuperPoint / SuperGlue device outputs in,
                             device right lines out, stream-ordered)
 
-FLD (cv::ximgproc::FastLineDetector) and the RCF edge network are not rebuilt: detected segments
-are the input.  There is no CPU path for the GPU functions.
+FLD (cv::ximgproc::FastLineDetector, OpenCV contrib, absent) is restated (parity unpinned); the
+RCF edge network is not rebuilt (no weights): its edge map is LineDetector's input.  There is no
+CPU path for the GPU functions.
 """
 from __future__ import annotations
 
@@ -31,6 +35,12 @@ class LinesConfig(C.Structure):
                 ("max_matches", C.c_int), ("device", C.c_int)]
 
 
+class FldConfig(C.Structure):
+    """rspl_fld_config = LineDetectorConfig's FLD fields (configs/configs_euroc.yaml:31-35)"""
+    _fields_ = [("length_threshold", C.c_int), ("distance_threshold", C.c_double), ("canny_th1", C.c_double),
+                ("canny_th2", C.c_double), ("canny_aperture_size", C.c_int)]
+
+
 def _declare(lib):
     if getattr(lib, "_rspl_lines_declared", False):
         return lib
@@ -45,6 +55,7 @@ def _declare(lib):
                                       C.POINTER(ip)]
     lib.rspl_lines_stereo_device.argtypes = [vp, vp, ip, vp, ip, vp, ip, vp, vp, _dp, vp, vp, vp]
     lib.rspl_lines_status.argtypes = [vp, C.POINTER(ip)]
+    lib.rspl_lines_detect.argtypes = [vp, _u8p, ip, ip, ip, C.POINTER(FldConfig), _fp, ip, C.POINTER(ip)]
     lib._rspl_lines_declared = True
     return lib
 
@@ -168,4 +179,37 @@ class LineMatcher:
         o = C.c_int()
         capi.check(self._lib.rspl_lines_status(self._h, C.byref(o)), "rspl_lines_status")
         return bool(o.value)
+
+
+class LineDetector:
+    """LineDetector (include/line_processor.h, line_processor.cc:455-490): the FLD of the half-size
+    image (rspl_lines_detect) and LineExtractor's scale + merge passes (rspl_line_extract)."""
+
+    def __init__(self, length_threshold=10, distance_threshold=1.414213562, canny_th1=200.0, canny_th2=250.0,
+                 canny_aperture_size=3, do_merge=True, max_segments=16384, device=0):
+        self._lib = _declare(capi.load())
+        self.cfg = FldConfig(length_threshold, distance_threshold, canny_th1, canny_th2, canny_aperture_size)
+        self.do_merge = do_merge
+        self._seg = np.zeros((max_segments, 4), np.float32)
+        self._h = C.c_void_p()
+        lc = LinesConfig(1, 1, 1, 0, device)
+        capi.check(self._lib.rspl_lines_create(C.byref(lc), C.byref(self._h)), "rspl_lines_create")
+
+    def __del__(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._lib.rspl_lines_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def detect(self, image: np.ndarray) -> np.ndarray:
+        """fld->detect(cv::resize(image, 0.5)): segments [n][4] float32 on the half image"""
+        img = np.ascontiguousarray(image, np.uint8)
+        n = C.c_int()
+        capi.check(self._lib.rspl_lines_detect(self._h, _p(img, C.c_uint8), img.shape[0], img.shape[1], img.shape[1],
+                                               C.byref(self.cfg), _p(self._seg, C.c_float), len(self._seg),
+                                               C.byref(n)), "rspl_lines_detect")
+        return self._seg[: n.value].copy()
+
+    def LineExtractor(self, image: np.ndarray) -> np.ndarray:
+        """lines [m][4] double at full size (x2 scale; the merges when do_merge)"""
+        return LineExtractor(self.detect(image), self.do_merge)
 

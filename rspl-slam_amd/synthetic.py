@@ -467,3 +467,38 @@ def line_scene(n_lines: int = 60, n_points: int = 400, seed: int = 0, width: int
     return {"seg_left": fragments(L, 0.0), "seg_right": fragments(L, disparity),
             "feat_left": feats(xy_left), "feat_right": feats(xy_right),
             "stereo_matches": m.astype(np.int32), "lines_left": L, "lines_right": Lr}
+
+
+def edge_map(h: int = 480, w: int = 752, n_lines: int = 40, seed: int = 0, width: float = 1.2, noise: float = 6.0):
+    """An RCF-like edge-probability image (the u8 map LineDetector::LineExtractor runs FLD on,
+    map_builder.cc:286): n_lines straight ridges with a Gaussian cross-profile (sigma `width` px,
+    peak 180..255) on a dark, noisy background, plus a few blobs.  Returns (image u8 [h][w],
+    segments [n][4] float64 -- the ridges' centre lines at full size)."""
+    rng = np.random.default_rng(seed)
+    img = rng.normal(12.0, noise, (h, w))
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    segs = []
+    for _ in range(n_lines):
+        length = rng.uniform(60, 300)
+        a = rng.uniform(-np.pi, np.pi)
+        cx, cy = rng.uniform(30, w - 30), rng.uniform(30, h - 30)
+        d = np.array([np.cos(a), np.sin(a)]) * length / 2
+        p = np.clip(np.array([cx, cy]) - d, 8, [w - 9, h - 9])
+        q = np.clip(np.array([cx, cy]) + d, 8, [w - 9, h - 9])
+        v = q - p
+        L2 = float(v @ v)
+        if L2 < 40.0 ** 2:
+            continue
+        x0, x1 = int(max(min(p[0], q[0]) - 6, 0)), int(min(max(p[0], q[0]) + 7, w))
+        y0, y1 = int(max(min(p[1], q[1]) - 6, 0)), int(min(max(p[1], q[1]) + 7, h))
+        X, Y = xx[y0:y1, x0:x1], yy[y0:y1, x0:x1]
+        t = np.clip(((X - p[0]) * v[0] + (Y - p[1]) * v[1]) / L2, 0.0, 1.0)
+        dist2 = (X - p[0] - t * v[0]) ** 2 + (Y - p[1] - t * v[1]) ** 2
+        peak = rng.uniform(180, 255)
+        img[y0:y1, x0:x1] = np.maximum(img[y0:y1, x0:x1], peak * np.exp(-dist2 / (2 * width * width)))
+        segs.append(np.concatenate([p, q]))
+    for _ in range(6):
+        bx, by, br = rng.uniform(20, w - 20), rng.uniform(20, h - 20), rng.uniform(3, 9)
+        img = np.maximum(img, 200.0 * np.exp(-((xx - bx) ** 2 + (yy - by) ** 2) / (2 * br * br)))
+    return np.clip(np.rint(img), 0, 255).astype(np.uint8), np.array(segs, np.float64).reshape(-1, 4)
+

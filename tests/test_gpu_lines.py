@@ -161,3 +161,38 @@ def test_stereo_lines_device_match_overflow():
         np.testing.assert_array_equal(o, runs[0][1])
     np.testing.assert_array_equal(runs[0][0], ref_valid)
     np.testing.assert_array_equal(runs[0][1], ref_lr)
+
+
+# --- the detector: rspl_lines_detect (GPU resize / Sobel / Canny classes + host FLD) vs oracle ---
+import fld_ref as FR  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def det():
+    return pkg.lines.LineDetector()
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 5])
+def test_line_detect_matches_oracle(det, seed):
+    """FLD segments bit-exact with the restatement (integer Canny, same double / float operation
+    order on the host), on RCF-like edge maps at the EuRoC size; then the full LineExtractor."""
+    img, _ = SY.edge_map(seed=seed)
+    got = det.detect(img)
+    ref = FR.line_detect(img)
+    assert len(ref) > 20
+    np.testing.assert_array_equal(got, ref)
+    np.testing.assert_array_equal(det.LineExtractor(img), LR.line_extractor(ref))
+
+
+def test_line_detect_textured_image_low_thresholds():
+    """An ordinary textured image with the uma_bumblebee thresholds (canny 50 / 50), odd tile edges"""
+    d = pkg.lines.LineDetector(canny_th1=50.0, canny_th2=50.0)
+    img = SY.textured_image(300, 420, seed=7)
+    np.testing.assert_array_equal(d.detect(img), FR.fld_detect(FR.resize_half(img), canny_th1=50.0, canny_th2=50.0))
+
+
+def test_line_detect_errors(det):
+    with pytest.raises(pkg.capi.RsplError):
+        det.detect(np.zeros((11, 20), np.uint8))  # odd height
+    blank = det.detect(np.zeros((64, 64), np.uint8))
+    assert blank.shape == (0, 4)
