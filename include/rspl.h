@@ -604,6 +604,9 @@ typedef struct {
 } rspl_fld_config;
 int rspl_lines_detect(rspl_lines* h, const uint8_t* image, int H, int W, int stride, const rspl_fld_config* cfg,
                       float* segments, int capacity, int* n_out);
+/* debug (parity tests): the last rspl_lines_detect's half image and Canny classes (2 strong, 0
+ * candidate, 1 none) for an H x W input, [H/2][W/2] each */
+int rspl_lines_debug_canny(rspl_lines* h, int H, int W, uint8_t* half, uint8_t* cls);
 
 #ifdef __cplusplus
 }

@@ -37,6 +37,7 @@ EXPORTS = [
     "rspl_pnp_create", "rspl_pnp_solve", "rspl_pnp_destroy", "rspl_pnp_debug_hypotheses",
     "rspl_line_extract", "rspl_lines_create", "rspl_lines_destroy", "rspl_lines_assign", "rspl_lines_match",
     "rspl_lines_stereo", "rspl_lines_stereo_device", "rspl_lines_status", "rspl_lines_detect",
+    "rspl_lines_debug_canny",
 ]
 
 

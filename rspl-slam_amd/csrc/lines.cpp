@@ -105,7 +105,9 @@ std::vector<Seg> merge_lines(const std::vector<Seg>& src, float angle_thr, float
   }
   std::vector<size_t> order(n);
   std::iota(order.begin(), order.end(), 0);
-  std::sort(order.begin(), order.end(), [&](size_t a, size_t b) { return ang[a] < ang[b]; });
+  // equal angles (axis-aligned segments, the two edges of one ridge) keep their input order: the
+  // reference's std::sort leaves ties unspecified, the restatement takes them stable
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return ang[a] < ang[b]; });
   const float ep2 = ep * ep, quarter = (float)(M_PI / 4.0);
   // neighbours in the reference's push_back order: by sorted position of the other line
   std::vector<std::vector<size_t>> nbr(n);
@@ -176,7 +178,7 @@ std::vector<Seg> merge_lines(const std::vector<Seg>& src, float angle_thr, float
       subs.push_back(cl);
       continue;
     }
-    std::sort(cl.begin(), cl.end(), [&](size_t a, size_t b) { return len[a] > len[b]; });
+    std::stable_sort(cl.begin(), cl.end(), [&](size_t a, size_t b) { return len[a] > len[b]; });
     std::unordered_map<size_t, size_t> at;
     for (size_t k = 0; k < cl.size(); k++) at[cl[k]] = k;
     std::vector<bool> taken(cl.size(), false);
@@ -646,50 +648,13 @@ bool chain_step(const uint8_t* e, int h, int w, int& x, int& y, int& direction, 
   return false;
 }
 
-}  // namespace
-
-extern "C" int rspl_lines_detect(rspl_lines* h, const uint8_t* image, int H, int W, int stride,
-                                 const rspl_fld_config* cfg, float* segments, int capacity, int* n_out) {
-  RSPL_CHECK_ARG(h && image && cfg && n_out && (segments || capacity == 0), "rspl_lines_detect: NULL argument");
-  RSPL_CHECK_ARG(H >= 4 && W >= 4 && H % 2 == 0 && W % 2 == 0 && stride >= W,
-                 "image %dx%d (stride %d): even sizes >= 4 required", W, H, stride);
-  RSPL_CHECK_ARG(cfg->canny_aperture_size == 3, "canny_aperture_size %d: only 3 (the configs' value)",
-                 cfg->canny_aperture_size);
-  RSPL_CHECK_ARG(cfg->length_threshold >= 1 && cfg->distance_threshold >= 0, "bad FLD thresholds");
-  *n_out = 0;
-  const size_t px = (size_t)H * W, hp = px / 4;
-  const int hh = H / 2, hw = W / 2;
-  if (px > h->det_cap) {  // grow the detector buffers (the stream is idle between calls)
-    RSPL_HIP(hipStreamSynchronize(h->stream));
-    if (h->d_img) (void)hipFree(h->d_img);
-    if (h->d_det) (void)hipFree(h->d_det);
-    if (h->h_img) (void)hipHostFree(h->h_img);
-    if (h->h_det) (void)hipHostFree(h->h_det);
-    h->d_img = h->d_det = h->h_img = h->h_det = nullptr;
-    h->det_cap = 0;
-    RSPL_HIP(hipMalloc((void**)&h->d_img, px));
-    RSPL_HIP(hipMalloc((void**)&h->d_det, 2 * (px / 4)));
-    RSPL_HIP(hipHostMalloc((void**)&h->h_img, px));
-    RSPL_HIP(hipHostMalloc((void**)&h->h_det, 2 * (px / 4)));
-    h->det_cap = px;
-  }
-  for (int r = 0; r < H; r++) memcpy(h->h_img + (size_t)r * W, image + (size_t)r * stride, W);
-  hipStream_t st = h->stream;
-  RSPL_HIP(hipMemcpyAsync(h->d_img, h->h_img, px, hipMemcpyHostToDevice, st));
-  double lo = cfg->canny_th1, hi = cfg->canny_th2;
-  if (lo > hi) std::swap(lo, hi);
-  lines::CannyArgs a{};
-  a.img = h->d_img; a.H = H; a.W = W; a.stride = W;
-  a.half = h->d_det; a.cls = h->d_det + hp;
-  a.low = (int)std::floor(lo); a.high = (int)std::floor(hi);
-  RSPL_HIP(lines::canny_classes(a, st));
-  RSPL_HIP(hipMemcpyAsync(h->h_det, h->d_det, 2 * hp, hipMemcpyDeviceToHost, st));
-  RSPL_HIP(hipStreamSynchronize(st));
-  const uint8_t* half = h->h_det;
-  const uint8_t* cls = h->h_det + hp;
+// the host part of the detector from the GPU's half image and Canny classes: hysteresis, the
+// corner zeroing, chains, runs, filters, orientation; returns the segment count (written up to
+// capacity)
+int fld_from_classes(const uint8_t* half, const uint8_t* cls, int hh, int hw, const rspl_fld_config* cfg,
+                     std::vector<uint8_t>& e, std::vector<int>& stk, float* segments, int capacity) {
+  const size_t hp = (size_t)hh * hw;
   // hysteresis: strong pixels through 8-connected candidates (the edge set does not depend on order)
-  std::vector<uint8_t>& e = h->edge;
-  std::vector<int>& stk = h->stack;
   e.assign(hp, 0);
   stk.clear();
   for (size_t i = 0; i < hp; i++)
@@ -755,11 +720,62 @@ extern "C" int rspl_lines_detect(rspl_lines* h, const uint8_t* image, int H, int
         n++;
       }
     }
+  return n;
+}
+
+}  // namespace
+
+extern "C" int rspl_lines_detect(rspl_lines* h, const uint8_t* image, int H, int W, int stride,
+                                 const rspl_fld_config* cfg, float* segments, int capacity, int* n_out) {
+  RSPL_CHECK_ARG(h && image && cfg && n_out && (segments || capacity == 0), "rspl_lines_detect: NULL argument");
+  RSPL_CHECK_ARG(H >= 4 && W >= 4 && H % 2 == 0 && W % 2 == 0 && stride >= W,
+                 "image %dx%d (stride %d): even sizes >= 4 required", W, H, stride);
+  RSPL_CHECK_ARG(cfg->canny_aperture_size == 3, "canny_aperture_size %d: only 3 (the configs' value)",
+                 cfg->canny_aperture_size);
+  RSPL_CHECK_ARG(cfg->length_threshold >= 1 && cfg->distance_threshold >= 0, "bad FLD thresholds");
+  *n_out = 0;
+  const size_t px = (size_t)H * W, hp = px / 4;
+  const int hh = H / 2, hw = W / 2;
+  if (px > h->det_cap) {  // grow the detector buffers (the stream is idle between calls)
+    RSPL_HIP(hipStreamSynchronize(h->stream));
+    if (h->d_img) (void)hipFree(h->d_img);
+    if (h->d_det) (void)hipFree(h->d_det);
+    if (h->h_img) (void)hipHostFree(h->h_img);
+    if (h->h_det) (void)hipHostFree(h->h_det);
+    h->d_img = h->d_det = h->h_img = h->h_det = nullptr;
+    h->det_cap = 0;
+    RSPL_HIP(hipMalloc((void**)&h->d_img, px));
+    RSPL_HIP(hipMalloc((void**)&h->d_det, 2 * (px / 4)));
+    RSPL_HIP(hipHostMalloc((void**)&h->h_img, px));
+    RSPL_HIP(hipHostMalloc((void**)&h->h_det, 2 * (px / 4)));
+    h->det_cap = px;
+  }
+  for (int r = 0; r < H; r++) memcpy(h->h_img + (size_t)r * W, image + (size_t)r * stride, W);
+  hipStream_t st = h->stream;
+  RSPL_HIP(hipMemcpyAsync(h->d_img, h->h_img, px, hipMemcpyHostToDevice, st));
+  double lo = cfg->canny_th1, hi = cfg->canny_th2;
+  if (lo > hi) std::swap(lo, hi);
+  lines::CannyArgs a{};
+  a.img = h->d_img; a.H = H; a.W = W; a.stride = W;
+  a.half = h->d_det; a.cls = h->d_det + hp;
+  a.low = (int)std::floor(lo); a.high = (int)std::floor(hi);
+  RSPL_HIP(lines::canny_classes(a, st));
+  RSPL_HIP(hipMemcpyAsync(h->h_det, h->d_det, 2 * hp, hipMemcpyDeviceToHost, st));
+  RSPL_HIP(hipStreamSynchronize(st));
+  const int n = fld_from_classes(h->h_det, h->h_det + hp, hh, hw, cfg, h->edge, h->stack, segments, capacity);
   *n_out = n;
   if (n > capacity) {
     set_error("%d segments exceed capacity %d", n, capacity);
     return RSPL_E_CAPACITY;
   }
+  return RSPL_OK;
+}
+
+extern "C" int rspl_lines_debug_canny(rspl_lines* h, int H, int W, uint8_t* half, uint8_t* cls) {
+  RSPL_CHECK_ARG(h && half && cls && (size_t)H * W <= h->det_cap, "rspl_lines_debug_canny: no such detection");
+  const size_t hp = (size_t)H * W / 4;
+  memcpy(half, h->h_det, hp);
+  memcpy(cls, h->h_det + hp, hp);
   return RSPL_OK;
 }
 

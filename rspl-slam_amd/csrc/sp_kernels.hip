@@ -909,25 +909,58 @@ __global__ __launch_bounds__(1024) void nms_kernel(NmsArgs a) {
     });
     __syncthreads();
   }
-  // output region [NH, NH+NTY) x [NH, NH+NTX): NMS'd map (debug entry points only) + candidates
-  for (int i = threadIdx.x; i < NTX * NTY; i += blockDim.x) {
+  // output region [NH, NH+NTY) x [NH, NH+NTX): NMS'd map (debug entry points only) + candidates.
+  // The workgroup reserves its candidates' slots with ONE atomic (wave ballots + a scan of the
+  // wave counts): a per-candidate atomic on the image's counter serialises thousands of
+  // candidates at one L2 address.  Slot order is free: top-k orders by (score, flat index).
+  static_assert(NTX * NTY == 2 * 1024, "two outputs per thread");
+  __shared__ int wcount[16], wbase[16], blk_base;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  unsigned long long key[2];
+  bool take[2];
+  int mine = 0;
+#pragma unroll
+  for (int q = 0; q < 2; q++) {
+    const int i = threadIdx.x + q * 1024;
     const int ly = NH + i / NTX, lx = NH + i % NTX;
     const int y = y0 + ly, x = x0 + lx;
+    take[q] = false;
+    key[q] = 0;
     if (y < H && x < W) {
       const float v = K[ly * RX + lx] ? S[ly * RX + lx] : 0.f;
       if (a.nms_out) a.nms_out[(size_t)bi * H * W + (size_t)y * W + x] = v;
       // find_high_score_index: float score > double threshold (src/super_point.cpp:158);
       // remove_borders: border <= y < H-border, border <= x < W-border (:244-245)
-      if ((double)v > a.threshold && y >= a.border && y < H - a.border && x >= a.border && x < W - a.border) {
-        const int slot = atomicAdd(&a.cand_count[bi], 1);
-        if (slot < a.cand_cap) {
-          const unsigned long long key =
-              ((unsigned long long)(0xFFFFFFFFu - __float_as_uint(v)) << 32) | (unsigned)(y * W + x);
-          a.cand[(size_t)bi * a.cand_cap + slot] = key;
-        }
-      }
+      take[q] = (double)v > a.threshold && y >= a.border && y < H - a.border && x >= a.border && x < W - a.border;
+      key[q] = ((unsigned long long)(0xFFFFFFFFu - __float_as_uint(v)) << 32) | (unsigned)(y * W + x);
     }
+    mine += take[q];
   }
+  // exclusive prefix of `mine` within the wave (lane order), then over the waves
+  int pre = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(pre, o);
+    if (lane >= o) pre += t;
+  }
+  if (lane == 63) wcount[wv] = pre;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int w = 0; w < 16; w++) {
+      wbase[w] = run;
+      run += wcount[w];
+    }
+    blk_base = run ? atomicAdd(&a.cand_count[bi], run) : 0;
+  }
+  __syncthreads();
+  int slot = blk_base + wbase[wv] + pre - mine;
+#pragma unroll
+  for (int q = 0; q < 2; q++)
+    if (take[q]) {
+      if (slot < a.cand_cap) a.cand[(size_t)bi * a.cand_cap + slot] = key[q];
+      slot++;
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -56,6 +56,7 @@ def _declare(lib):
     lib.rspl_lines_stereo_device.argtypes = [vp, vp, ip, vp, ip, vp, ip, vp, vp, _dp, vp, vp, vp]
     lib.rspl_lines_status.argtypes = [vp, C.POINTER(ip)]
     lib.rspl_lines_detect.argtypes = [vp, _u8p, ip, ip, ip, C.POINTER(FldConfig), _fp, ip, C.POINTER(ip)]
+    lib.rspl_lines_debug_canny.argtypes = [vp, ip, ip, _u8p, _u8p]
     lib._rspl_lines_declared = True
     return lib
 
@@ -208,6 +209,14 @@ class LineDetector:
                                                C.byref(self.cfg), _p(self._seg, C.c_float), len(self._seg),
                                                C.byref(n)), "rspl_lines_detect")
         return self._seg[: n.value].copy()
+
+    def debug_canny(self, H: int, W: int):
+        """the last detect's half image and Canny classes (2 strong, 0 candidate, 1 none)"""
+        half = np.zeros((H // 2, W // 2), np.uint8)
+        cls = np.zeros_like(half)
+        capi.check(self._lib.rspl_lines_debug_canny(self._h, H, W, _p(half, C.c_uint8), _p(cls, C.c_uint8)),
+                   "rspl_lines_debug_canny")
+        return half, cls
 
     def LineExtractor(self, image: np.ndarray) -> np.ndarray:
         """lines [m][4] double at full size (x2 scale; the merges when do_merge)"""

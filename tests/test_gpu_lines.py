@@ -178,6 +178,9 @@ def test_line_detect_matches_oracle(det, seed):
     order on the host), on RCF-like edge maps at the EuRoC size; then the full LineExtractor."""
     img, _ = SY.edge_map(seed=seed)
     got = det.detect(img)
+    half, cls = det.debug_canny(*img.shape)
+    np.testing.assert_array_equal(half, FR.resize_half(img))
+    np.testing.assert_array_equal(cls, FR.canny_classes(half, 200.0, 250.0))
     ref = FR.line_detect(img)
     assert len(ref) > 20
     np.testing.assert_array_equal(got, ref)

@@ -139,3 +139,12 @@ def test_fld_oracle_finds_the_ridges():
                 hit += 1
                 break
     assert hit >= 0.8 * len(long_gt), (hit, len(long_gt))
+
+
+@pytest.mark.parametrize("seed", [0, 1, 2, 6])
+def test_line_extract_on_detector_segments(seed):
+    """The merge passes on real detector output (restated FLD on RCF-like edge maps): the two edges
+    of a ridge give equal-angle segments, i.e. sort ties -- kept stable on both sides"""
+    img, _ = SY.edge_map(seed=seed)
+    segs = FR.line_detect(img)
+    np.testing.assert_array_equal(pkg.lines.LineExtractor(segs), LR.line_extractor(segs))
