@@ -1,7 +1,9 @@
-"""Line front end timing: one stereo frame's line association -- both images'
-AssignPointsToLines (one launch) + the stereo filter + MatchLines (rspl_lines_stereo, host
-arrays in / out, the reference's per-frame contract) -- on the GPU, the LineDetector merge passes
-(host C++), and the oracle restatement of the same work on one CPU core for comparison."""
+"""Line front end timing: the detector (cv::resize + FLD restated: GPU resize /
+Sobel / Canny classes + host chaining, rspl_lines_detect) on a 752x480 RCF-like edge map, one
+stereo frame's line association -- both images' AssignPointsToLines (one launch) + the stereo
+filter + MatchLines (rspl_lines_stereo, host arrays in / out, the reference's per-frame contract)
+-- on the GPU, the LineDetector merge passes (host C++), and the oracle restatements of the same
+work on one CPU core for comparison."""
 import argparse
 import json
 import pathlib
@@ -17,6 +19,7 @@ import rspl_loader  # noqa: E402
 
 pkg = rspl_loader.load()
 pkg.capi.load()
+import fld_ref as FR  # noqa: E402
 import lines_ref as LR  # noqa: E402
 
 
@@ -26,6 +29,17 @@ def main():
     ap.add_argument("--points", type=int, default=400)
     ap.add_argument("--iters", type=int, default=200)
     a = ap.parse_args()
+    img, _ = pkg.synthetic.edge_map(seed=11)
+    det = pkg.lines.LineDetector()
+    for _ in range(5):
+        segs = det.detect(img)
+    t = time.perf_counter()
+    for _ in range(a.iters // 4):
+        segs = det.detect(img)
+    detect_ms = (time.perf_counter() - t) / (a.iters // 4) * 1e3
+    t = time.perf_counter()
+    FR.line_detect(img)
+    detect_cpu_ms = (time.perf_counter() - t) * 1e3
     sc = pkg.synthetic.line_scene(n_lines=a.lines, n_points=a.points, seed=11)
     lm = pkg.lines.LineMatcher(max_lines=512, max_points=2048)
     lim = (2.0, 60.0, 2.0)
@@ -75,7 +89,9 @@ def main():
         r1 = LR.assign_points_to_lines(L1, F1[:, 1:3])
         LR.right_lines(L1, LR.match_lines(r0, r1, km, len(F0), len(F1)), len(L0))
     cpu_ms = (time.perf_counter() - t) / n_cpu * 1e3
-    print(json.dumps({"lines_left": len(L0), "lines_right": len(L1), "points": a.points,
+    print(json.dumps({"detect_segments": len(segs), "detect_ms_per_image": round(detect_ms, 4),
+                      "detect_ms_oracle_python_1core": round(detect_cpu_ms, 2),
+                      "lines_left": len(L0), "lines_right": len(L1), "points": a.points,
                       "stereo_matches_kept": kept, "right_lines_valid": int(valid.sum()),
                       "merge_ms_per_image_host": round(merge_ms, 4),
                       "stereo_association_ms_gpu_call": round(gpu_ms, 4),
