@@ -30,11 +30,6 @@ using namespace rspl;
 struct rspl_ba {
   rspl_ba_config cfg{};
   hipStream_t stream = nullptr;
-  // the per-call edge-pair lists are built on a side stream, beside the first errors /
-  // linearisation; the first trial waits for them (pairs_ready)
-  hipStream_t side = nullptr;
-  hipEvent_t staged = nullptr, pairs_ready = nullptr;
-  bool pairs_pending = false;
   Arena arena;
   int maxE = 0, maxL = 0, maxK = 0, maxV = 0;
   // candidate state (ping-pong partners of the call buffer's T / X / L)
@@ -292,14 +287,6 @@ void accept_swap(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, bool lin) 
   S.Hll = b->Hll; S.bl = b->bl;
 }
 
-// the first trial of a call waits for the side stream's edge-pair lists
-int join_pairs(rspl_ba* b) {
-  if (!b->pairs_pending) return RSPL_OK;
-  b->pairs_pending = false;
-  RSPL_HIP(hipStreamWaitEvent(b->stream, b->pairs_ready, 0));
-  return RSPL_OK;
-}
-
 // optimize(iters) with the LM control on the device (fast path, unsharded): the first errors, the
 // first linearisation and the control's initialisation, then `iters` trials queued back to back
 // with no host round trip -- each trial's last kernel takes the accept / reject decision (ba::LmCtrl)
@@ -351,7 +338,6 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
     return RSPL_OK;
   };
   int rc;
-  if ((rc = join_pairs(b))) return rc;
   if ((rc = enqueue(iters))) return rc;
   double v[4];
   for (;;) {
@@ -424,7 +410,6 @@ int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Acti
     RSPL_HIP(ba::post(S, q, st, &A));  // posts chi2 (S.out[0]) and the max diagonal (S.out[2])
   }
   if ((rc = wait_mail(b, q, v))) return rc;
-  if ((rc = join_pairs(b))) return rc;
   double currentChi = v[0];
   double lambda = 1e-5 * v[2], ni = 2;  // computeLambdaInit: tau * max diagonal
   int done = 0;
@@ -527,9 +512,7 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
   if (hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipStreamCreateWithPriority(&b->side, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-      hipEventCreateWithFlags(&b->staged, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&b->pairs_ready, hipEventDisableTiming) != hipSuccess ||
+
       hipHostMalloc((void**)&b->mail, sizeof(ba::Mail), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&b->mail_dev, b->mail, 0) != hipSuccess ||
       hipMalloc((void**)&b->cbuf, CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE, 8 * (size_t)b->maxE).bytes) !=
@@ -554,25 +537,20 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
 
 extern "C" int rspl_ba_use_reserved_cus(rspl_ba* b, int reserve_cus) {
   RSPL_CHECK_ARG(b, "rspl_ba_use_reserved_cus: NULL handle");
-  hipStream_t ns[2] = {nullptr, nullptr};
-  for (hipStream_t& n : ns) {
-    if (reserve_cus > 0) {
-      std::vector<uint32_t> mask;
-      int rc = cu_mask(reserve_cus, true, mask);
-      if (rc) return rc;
-      RSPL_HIP(hipExtStreamCreateWithCUMask(&n, (uint32_t)mask.size(), mask.data()));
-    } else {
-      int lo = 0, hi = 0;
-      RSPL_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
-      RSPL_HIP(hipStreamCreateWithPriority(&n, hipStreamNonBlocking, hi));
-    }
+  hipStream_t ns = nullptr;
+  if (reserve_cus > 0) {
+    std::vector<uint32_t> mask;
+    int rc = cu_mask(reserve_cus, true, mask);
+    if (rc) return rc;
+    RSPL_HIP(hipExtStreamCreateWithCUMask(&ns, (uint32_t)mask.size(), mask.data()));
+  } else {
+    int lo = 0, hi = 0;
+    RSPL_HIP(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    RSPL_HIP(hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, hi));
   }
   RSPL_HIP(hipStreamSynchronize(b->stream));
-  RSPL_HIP(hipStreamSynchronize(b->side));
   RSPL_HIP(hipStreamDestroy(b->stream));
-  RSPL_HIP(hipStreamDestroy(b->side));
-  b->stream = ns[0];
-  b->side = ns[1];
+  b->stream = ns;
   return RSPL_OK;
 }
 
@@ -593,7 +571,6 @@ extern "C" int rspl_ba_set_shard(rspl_ba* b, int rank, int nranks, rspl_allreduc
 extern "C" void rspl_ba_destroy(rspl_ba* b) {
   if (!b) return;
   if (b->stream) (void)hipStreamSynchronize(b->stream);
-  if (b->side) (void)hipStreamSynchronize(b->side);
   if (b->gbuf) (void)hipFree(b->gbuf);
   b->arena.release();
   if (b->cbuf) (void)hipFree(b->cbuf);
@@ -602,9 +579,6 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
   if (b->stage) (void)hipHostFree(b->stage);
   if (b->mail) (void)hipHostFree(b->mail);
   if (b->stream) (void)hipStreamDestroy(b->stream);
-  if (b->side) (void)hipStreamDestroy(b->side);
-  if (b->staged) (void)hipEventDestroy(b->staged);
-  if (b->pairs_ready) (void)hipEventDestroy(b->pairs_ready);
   delete b;
 }
 
@@ -621,8 +595,7 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   const int rc = ba_local_impl(b, pr, res);
   if (rc != RSPL_E_DEVICE || !b) return rc;
   const std::string msg = rspl_last_error();
-  b->pairs_pending = false;
-  if (hipStreamSynchronize(b->stream) != hipSuccess || hipStreamSynchronize(b->side) != hipSuccess ||
+  if (hipStreamSynchronize(b->stream) != hipSuccess ||
       hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
       hipMemset(b->pair_ctr, 0, sizeof(unsigned) * (b->maxK * (b->maxK + 1) / 2 + 1)) != hipSuccess) {
     set_error("%s; the BA stream could not be drained: recreate the handle", msg.c_str());
@@ -903,11 +876,10 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   A.robust = 1;
   A.pp_off = b->pp_off;
   A.pp = b->pp_buf;
-  RSPL_HIP(hipEventRecord(b->staged, st));  // the upload above
-  RSPL_HIP(hipStreamWaitEvent(b->side, b->staged, 0));
-  RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, b->side));
-  RSPL_HIP(hipEventRecord(b->pairs_ready, b->side));
-  b->pairs_pending = true;
+  // on the BA stream itself: a second stream would take a hardware queue of its own (streams map
+  // round-robin onto GPU_MAX_HW_QUEUES) and push a pipeline stream onto the BA's queue -- measured:
+  // bench 2.17 ms per step instead of 1.5 with a side stream for the pair lists
+  RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, st));
   mark("pairs");
   if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first)))
     return rc;
