@@ -133,7 +133,8 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
     """Achieved rate vs the bounding peak for the big stages (HIP-event stage times on the stage's
     launch stream, per step: 2 SuperPoint images, 2 SuperGlue pairs of N = M = K).  Algorithmic work
     as SURVEY.md 8(d): conv1a+conv1b 2*H*W*64*(9 + 576) FLOP per image; GNN 2*(655,360 N + 512 N M)
-    per image per layer; Sinkhorn streamed model 2*iters*4*(N+1)(M+1) bytes per pair; NMS 2*4*H*W
+    per image per layer; Sinkhorn streamed model 2*iters*4*(N+1)(M+1) bytes per pair; NMS 4*H*W (the score
+    map read once; the product path writes no NMS'd map, the candidates carry the scores)
     bytes per image.  Single-kernel stages carry the kernel name (pmc_kernel) whose PMC traffic
     summary under profiles/ gives `traffic`; the GNN is a launch family (single_kernel false)."""
     t = {**{f"sp:{n}": v / max(1, sp_calls) for n, v in zip(sp.STAGES, sp_ms)},
@@ -152,8 +153,8 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
              {"slab": "sinkhorn_kernel<", "rb": "sinkhorn_rb_kernel"}.get(os.environ.get("RSPL_SG_SINK", "sc"),
                                                                          "sinkhorn_sc_kernel"),
              True, "GB per launch (2 pairs, streamed model 2*iters*4*(N+1)(M+1))"),
-            ("sp:nms", 2 * 2 * 4 * H * W / 1e9, "GB/s", HBM_PEAK_GBS, "hbm", "nms_kernel", True,
-             "GB per launch (2 images, 2*4*H*W)"))
+            ("sp:nms", 2 * 4 * H * W / 1e9, "GB/s", HBM_PEAK_GBS, "hbm", "nms_kernel", True,
+             "GB per launch (2 images, 4*H*W: the score map read once)"))
     out = {}
     for key, work, unit, peak, bound, kern, single, what in rows:
         ms = t.get(key)
