@@ -469,7 +469,8 @@ def main():
             # keyframe i's local BA goes to the tracking thread (own high-priority stream) through a
             # 2-deep buffer, as the reference's feature thread blocks only while
             # _tracking_data_buffer.size() >= 2 (src/map_builder.cc:176)
-            ba_q.put(ba_item(i))
+            if "ba" not in skip:
+                ba_q.put(ba_item(i))
 
         line_t0 = None
         for i in range(args.warmup):

@@ -487,6 +487,9 @@ typedef struct {
   int n_point_outliers, n_line_outliers;
   double chi2_first, chi2_second;
   int iterations_first, iterations_second;
+  /* host wall time of the call's stages, microseconds: window + constraint assembly, the GPU
+   * LocalmapOptimization (rspl_ba_local incl. staging), outlier removal + covisibility + write-back */
+  double assembly_us, ba_us, finish_us;
 } rspl_map_report;
 
 enum { RSPL_MAP_UNTRIANGULATED = 0, RSPL_MAP_GOOD = 1, RSPL_MAP_BAD = 2 };  /* Mappoint::Type */

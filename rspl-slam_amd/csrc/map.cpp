@@ -446,6 +446,7 @@ struct rspl_map {
     auto mark = [&]() {
       if (timing) tm[ntm++] = clk::now();
     };
+    const auto t_start = clk::now();
     mark();
     update_connection(*nf);
     mark();
@@ -627,9 +628,18 @@ struct rspl_map {
     R.pose_q = rq.data(); R.pose_p = rp.data(); R.points = rX.data(); R.lines = rL.data();
     R.mono_inlier = c_inl[0].data(); R.stereo_inlier = c_inl[1].data();
     R.mono_line_inlier = c_inl[2].data(); R.stereo_line_inlier = c_inl[3].data();
+    const auto t_ba = clk::now();
     const int rc = rspl_ba_local(ba, &P, &R);
     if (rc) return rc;
-    return finish(R, rep);
+    const auto t_fin = clk::now();
+    const int rf = finish(R, rep);
+    if (rep) {
+      auto us = [](clk::time_point a, clk::time_point b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+      rep->assembly_us = us(t_start, t_ba);
+      rep->ba_us = us(t_ba, t_fin);
+      rep->finish_us = us(t_fin, clk::now());
+    }
+    return rf;
   }
 
   // the part of Map::LocalMapOptimization after LocalmapOptimization returns (map.cc:712-802), on

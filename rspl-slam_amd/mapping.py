@@ -39,7 +39,8 @@ class MapReport(C.Structure):
     _fields_ = [(n, C.c_int) for n in ("n_poses", "n_fixed", "n_points", "n_lines", "n_mono", "n_stereo",
                                        "n_mono_line", "n_stereo_line", "n_point_outliers", "n_line_outliers")] + \
                [("chi2_first", C.c_double), ("chi2_second", C.c_double),
-                ("iterations_first", C.c_int), ("iterations_second", C.c_int)]
+                ("iterations_first", C.c_int), ("iterations_second", C.c_int),
+                ("assembly_us", C.c_double), ("ba_us", C.c_double), ("finish_us", C.c_double)]
 
     def as_dict(self):
         return {f: getattr(self, f) for f, _ in self._fields_}

@@ -6,6 +6,8 @@ ground truth).  Tracking, keyframe selection and landmark triangulation are not 
 """
 from __future__ import annotations
 
+import time
+
 import numpy as np
 
 from .ba_types import OptimizationConfig
@@ -33,9 +35,13 @@ def run(seq: dict, ba, cfg: OptimizationConfig = OptimizationConfig(), iteration
     m = Map(seq["camera"], cfg, iterations)
     reports = []
     for k, kf in enumerate(seq["keyframes"]):
+        t = time.perf_counter()
         insert_keyframe(m, kf)
+        t_ins = time.perf_counter() - t
         if k >= 1:  # map.cc:29 (the first keyframe only initialises) and :105-107
-            reports.append(m.LocalMapOptimization(kf["id"], ba))
+            r = m.LocalMapOptimization(kf["id"], ba)
+            r["insert_us"] = 1e6 * t_ins  # the keyframe's bookkeeping through the Python API
+            reports.append(r)
         if on_keyframe:
             on_keyframe(k, m)
     return m, reports

@@ -80,7 +80,8 @@ static int layout(void) {
   F(rspl_map_report, n_lines); F(rspl_map_report, n_mono); F(rspl_map_report, n_stereo); F(rspl_map_report, n_mono_line);
   F(rspl_map_report, n_stereo_line); F(rspl_map_report, n_point_outliers); F(rspl_map_report, n_line_outliers);
   F(rspl_map_report, chi2_first); F(rspl_map_report, chi2_second); F(rspl_map_report, iterations_first);
-  F(rspl_map_report, iterations_second); END();
+  F(rspl_map_report, iterations_second);
+  F(rspl_map_report, assembly_us); F(rspl_map_report, ba_us); F(rspl_map_report, finish_us); END();
   BEGIN(rspl_lines_config); F(rspl_lines_config, max_lines); F(rspl_lines_config, max_points);
   F(rspl_lines_config, max_pairs); F(rspl_lines_config, max_matches); F(rspl_lines_config, device); END();
   printf("}\n");

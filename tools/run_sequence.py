@@ -69,7 +69,12 @@ def main():
            "point_outliers_removed": int(sum(r["n_point_outliers"] for r in reports)),
            "line_outliers_removed": int(sum(r["n_line_outliers"] for r in reports)),
            "gpu_map_local_ba_ms_per_keyframe": round(gpu_s * 1e3 / (len(ts) - 1), 3),
-           "cpu_oracle_ms_per_keyframe_1core": round(cpu_s * 1e3 / (len(ts) - 1), 1)}
+           "cpu_oracle_ms_per_keyframe_1core": round(cpu_s * 1e3 / (len(ts) - 1), 1),
+           # per keyframe: the Python-side insertion, then rspl_map_local_optimization's own stages
+           "gpu_path_ms_per_keyframe": {k: round(float(np.mean([r[k + "_us"] for r in reports])) / 1e3, 3)
+                                        for k in ("insert", "assembly", "ba", "finish")},
+           "window_mean": {k: round(float(np.mean([r[k] for r in reports])), 1)
+                           for k in ("n_poses", "n_points", "n_lines", "n_mono", "n_stereo")}}
     print(json.dumps(res))
 
 
