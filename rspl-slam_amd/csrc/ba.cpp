@@ -143,7 +143,9 @@ void carve(F& ar, rspl_ba* b) {
   take(b->Hll, NL * 16); take(b->bl, NL * 4); take(b->bp, K * 6);
   // block partials: edge-per-thread kernels (E / 256) and landmark-group kernels (NL * 8 / 256)
   const size_t nblk = std::max(E / 256, NL * 8 / 256) + 2;
-  take(b->S, 36 * K * K); take(b->x, 6 * K); take(b->partial, nblk);
+  // partial also holds the setup kernel's per-block costs: the landmark groups plus the line
+  // workgroups (at most one per line landmark plus one per kLineBlk line edges)
+  take(b->S, 36 * K * K); take(b->x, 6 * K); take(b->partial, nblk + NL + E / ba::kLineBlk + 8);
   // partial2: scale partials, and the pose-diagonal partials (K x E/256 x 6) of the lambda init
   take(b->partial2, std::max(std::max((size_t)b->maxV / 256, nblk) + 2, K * (E / 256 + 1) * 6));
   take(b->lm_ctr, nl);
@@ -294,13 +296,9 @@ void accept_swap(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, bool lin) 
 // optimize(); when rejected trials leave iterations undone it queues more.  At the end the host
 // pointer view follows the device's current bank.
 int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
-                 double* chi2_out, int* done_out) {
+                 double* chi2_out, int* done_out, uint8_t* cls_level, bool build_pp) {
   hipStream_t st = b->stream;
   S.lm = b->lmctl;
-  unsigned long long q = 0;  // the first errors post nothing: the host waits for the trials only
-  RSPL_HIP(ba::compute_errors(P, Lr, A, S, q, st));
-  RSPL_HIP(ba::linearize(P, Lr, A, S, true, st));
-  q = ++b->seq;
   S.lm_slot = 0;
   static const bool trace = getenv("RSPL_BA_LMTRACE") != nullptr;
   if (trace && !b->lm_trace) {
@@ -308,7 +306,25 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
     RSPL_HIP(hipMemset(b->lm_trace, 0, sizeof(double) * 8 * 64));
   }
   S.lm_trace = trace ? b->lm_trace + (iters == 10 ? 0 : 8 * 32) : nullptr;
-  RSPL_HIP(ba::post(S, q, st, &A, iters));  // + computeLambdaInit into the control (slot 0)
+  // errors, cost and linearisation at the current state (with cls_level: the second optimize's
+  // outlier levels and landmark activity first) + computeLambdaInit into the control (slot 0);
+  // nothing is posted: the host waits for the trials only
+  static const bool split_setup = getenv("RSPL_BA_SETUP") && std::string(getenv("RSPL_BA_SETUP")) == "split";
+  if (!split_setup) {
+    RSPL_HIP(ba::setup_dev(P, Lr, A, S, cls_level, cls_level ? const_cast<uint8_t*>(A.lm_act) : nullptr, iters,
+                           build_pp ? b->pp_cnt : nullptr, b->pp_off, b->pp_buf, st));
+  } else {  // A/B knob: the separate launches (build_pairs, classify, landmark_active, errors, linearize,
+            // pose_diag, post)
+    if (build_pp) RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, st));
+    if (cls_level) {
+      RSPL_HIP(ba::classify(P, Lr, A.Ea, cls_level, nullptr, 0, st));
+      RSPL_HIP(ba::landmark_active(A, cls_level, const_cast<uint8_t*>(A.lm_act), st));
+    }
+    RSPL_HIP(ba::compute_errors(P, Lr, A, S, 0, st));
+    RSPL_HIP(ba::linearize(P, Lr, A, S, true, st));
+    RSPL_HIP(ba::post(S, 0, st, &A, iters));
+  }
+  unsigned long long q = b->seq;
   const unsigned long long q_first = b->seq + 1;
   ba::Lin Ls = Lr;
   Ls.Hpp = b->Hpp_s; Ls.bp = b->bp_s; Ls.Hll = b->Hll_es; Ls.bl = b->bl_es; Ls.Hpl = b->Hpl_s;
@@ -382,14 +398,20 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
   return RSPL_OK;
 }
 
-// one g2o SparseOptimizer::optimize(iters) with OptimizationAlgorithmLevenberg
+bool dev_lm(const rspl_ba* b, const ba::Active& A, int iters) {
+  return b->allreduce == nullptr && iters > 0 && ba::fast_path(A.K);
+}
+
+// one g2o SparseOptimizer::optimize(iters); device LM only: cls_level -- classify the edges into it
+// first (the second optimize's levels), build_pp -- build the Schur chunks' edge-pair lists (see
+// setup_dev); the caller does both itself otherwise
 int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
-             double* chi2_out, int* done_out) {
+             double* chi2_out, int* done_out, uint8_t* cls_level = nullptr, bool build_pp = false) {
   hipStream_t st = b->stream;
   double v[4];
   int rc;
   const bool sh = b->allreduce != nullptr;
-  if (!sh && iters > 0 && ba::fast_path(A.K)) return optimize_dev(b, P, Lr, S, A, iters, chi2_out, done_out);
+  if (dev_lm(b, A, iters)) return optimize_dev(b, P, Lr, S, A, iters, chi2_out, done_out, cls_level, build_pp);
   const int n6 = 6 * A.K;
   double* so = b->red + n6 + b->nranks;  // this rank's {chi2, scale, fail} (S.shard_out)
   unsigned long long q = ++b->seq;
@@ -879,21 +901,28 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   // on the BA stream itself: a second stream would take a hardware queue of its own (streams map
   // round-robin onto GPU_MAX_HW_QUEUES) and push a pipeline stream onto the BA's queue -- measured:
   // bench 2.17 ms per step instead of 1.5 with a side stream for the pair lists
-  RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, st));
+  const bool pp_fused = dev_lm(b, A, pr->iterations_first);  // else: built here, before the first optimize
+  if (!pp_fused) RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, st));
   mark("pairs");
-  if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first)))
+  if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first, nullptr,
+                     pp_fused)))
     return rc;
   mark("opt1");
-  RSPL_HIP(ba::classify(P, Lr, E, level, nullptr, 0, st));
   // ---- phase 2: level-0 edges, no kernel (initializeOptimization(0), :176-213) ----
   // Same active structure with the level-1 edges masked (exact-zero records, no cost, errors
-  // kept as g2o keeps them), landmark activity recomputed from the levels on the device.
+  // kept as g2o keeps them), landmark activity recomputed from the levels on the device (device LM:
+  // inside the optimize's first launch).
   {
     A.robust = 0;
     A.elevel = level;
-    RSPL_HIP(ba::landmark_active(A, level, b->lm_act2, st));
     A.lm_act = b->lm_act2;
-    if ((rc = optimize(b, P, Lr, S, A, pr->iterations_second, &res->chi2_second, &res->iterations_done_second)))
+    const bool fused = dev_lm(b, A, pr->iterations_second);
+    if (!fused) {
+      RSPL_HIP(ba::classify(P, Lr, E, level, nullptr, 0, st));
+      RSPL_HIP(ba::landmark_active(A, level, b->lm_act2, st));
+    }
+    if ((rc = optimize(b, P, Lr, S, A, pr->iterations_second, &res->chi2_second, &res->iterations_done_second,
+                       fused ? level : nullptr)))
       return rc;
     mark("opt2");
   }

@@ -671,11 +671,17 @@ __device__ __forceinline__ bool lm_dinv(const double* Hll, bool point, double la
 // records in CSR order into the landmark block itself; only a landmark with more than
 // kLineBlk edges (split over workgroups) goes through per-edge records written through (sc1)
 // and a last-edge ticket.
-// SPEC: the speculative linearisation (at the candidate P.Tn / candidate lines) inside
+// MODE kLinSpec: the speculative linearisation (at the candidate P.Tn / candidate lines) inside
 // update_errors_kernel, from the kernel's start: wave 0 forms the candidate of each of the block's
 // line landmarks itself -- the same back-substitution as the landmark groups (8 lanes per
 // landmark, the same butterfly, from the current records Lc / Sc) -- so it never waits for the
 // groups; wave 3 evaluates each edge's own error at the candidate.
+// MODE kLinSetup: the first pass of a device-LM optimize() (setup_kernel): wave 3 evaluates each
+// edge's error at the current state (no separate error kernel), the block returns the robust cost of
+// its edges (*chi_out, slot order) and, with cls (the second optimize), classifies its edges from
+// their last computed errors itself (classify_edge) -- the landmark groups of the same launch write
+// the levels, so none is read here.  The line edges' errors are not stored: the first trial's update
+// rewrites every edge's error before anything reads them.
 // candidate pose i of this trial (g2o VertexSE3Expmap::oplusImpl, the left update exp(xp) T):
 // copied when the pose is not optimised or the solve failed
 __device__ __forceinline__ void cand_pose(const Problem& P, const Active& A, const double* x, int i, bool failed,
@@ -695,11 +701,43 @@ __device__ __forceinline__ void cand_pose(const Problem& P, const Active& A, con
   o[7] = 0;
 }
 
-template <bool SPEC>
+// outlier levels after the first optimize / final inlier flags (g2o_optimization.cc:176-231)
+__device__ __forceinline__ void edge_status(const Problem& P, const Lin& L, int e, double& chi2, bool& depth_ok) {
+  const int t = P.etype[e];
+  chi2 = 0;
+  for (int k = 0; k < edim(t); k++) chi2 += L.err[4 * e + k] * L.err[4 * e + k];
+  chi2 *= einfo(t);
+  depth_ok = true;
+  if (t < 2) {
+    const SE3 T = load_T(P.T + 8 * P.epose[e]);
+    double R[9], Xc[3];
+    q_to_R(T.q, R);
+    mat3_vec(R, P.X + 3 * P.elm[e], Xc);
+    depth_ok = Xc[2] + T.t[2] > 0.0;
+  }
+}
+constexpr int kLinPlain = 0, kLinSpec = 1, kLinSetup = 2;
+// phase-2 level of edge e from its last computed error (classify_edge, g2o_optimization.cc:176-213)
+__device__ __forceinline__ bool edge_outlier(const Problem& P, const Lin& L, int e) {
+  double chi2;
+  bool depth_ok;
+  edge_status(P, L, e, chi2, depth_ok);
+  return chi2 > pick4(P.th, P.etype[e]) || !depth_ok;
+}
+// line landmark g is active: it has an edge of level 0 (cls) / the phase's activity (A.lm_act)
+__device__ __forceinline__ bool line_active(const Problem& P, const Lin& L, const Active& A, int g, bool cls) {
+  if (!cls) return A.lm_act[g] != 0;
+  for (int k = A.lm_off[g]; k < A.lm_off[g + 1]; k++)
+    if (!edge_outlier(P, L, k)) return true;
+  return false;
+}
+template <int MODE>
 __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const Active& A, const Sys& S, int blk,
                                           bool maxd, const Lin* Lc = nullptr, const Sys* Sc = nullptr,
                                           double lambda = 0.0, bool failed = false,
-                                          unsigned long long* stamp = nullptr) {
+                                          unsigned long long* stamp = nullptr, bool cls = false,
+                                          double* chi_out = nullptr) {
+  constexpr bool SPEC = MODE == kLinSpec, SETUP = MODE == kLinSetup, OWN_ERR = SPEC || SETUP;
   __shared__ double ev[kLineBlk][20][4];
   __shared__ double J[kLineBlk][4 * 6 + 4 * 4];
   __shared__ double Lsh[kLineBlk][6];
@@ -770,7 +808,8 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
     const bool on = tid < cnt;
     const int e = on ? (p0 + tid) : 0;
     const int t = on ? P.etype[e] : 2;
-    const bool live = on && !(A.elevel && A.elevel[e]);  // outside this phase: exact-zero records
+    // outside this phase: exact-zero records (setup: the level from the edge's last error)
+    const bool live = on && !(SETUP ? (cls && edge_outlier(P, L, e)) : (A.elevel && A.elevel[e]));
     const bool popt = on && A.pidx[P.epose[e]] >= 0;
     einfo_s[tid][0] = e;
     einfo_s[tid][1] = t;
@@ -804,7 +843,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
         slot = idx / 12;
         m = 8 + idx % 12;  // ev row 2d + sign, d = 4..9
       }
-    } else if (SPEC && lane < kLineBlk) {
+    } else if (OWN_ERR && lane < kLineBlk) {
       slot = lane;
       m = 20;
     }
@@ -842,6 +881,25 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
   }
   __syncthreads();
   if (stamp && tid == 0) stamp[1] = wall_clock64();
+  if (SETUP && tid == 0) {  // the robust cost of the block's edges at the current state, slot order
+    double c = 0;
+    for (int slot = 0; slot < cnt; slot++) {
+      int e, t;
+      bool on, live;
+      edge(slot, e, t, on, live);
+      if (!live) continue;
+      double chi2 = 0;
+      for (int k = 0; k < edim(t); k++) chi2 += es[slot][k] * es[slot][k];
+      chi2 *= einfo(t);
+      double cst = chi2;
+      if (A.robust) {
+        double r1;
+        huber(chi2, pick4(P.delta, t), cst, r1);
+      }
+      c += cst;
+    }
+    *chi_out = c;
+  }
   // J layout per edge: Jp [4][6] at 0, Jl [4][4] at 24
   for (int idx = tid; idx < 40 * kLineBlk; idx += 256) {
     const int slot = idx / 40, rd = idx - 40 * slot, r = rd / 10, d = rd % 10;
@@ -861,7 +919,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
     bool on, live;
     edge(slot, e, t, on, live);
     if (!on) continue;
-    const double* er = SPEC ? &es[slot][0] : L.err + 4 * e;
+    const double* er = OWN_ERR ? &es[slot][0] : L.err + 4 * e;
     const double w = live ? edge_weight_of(P, A, er, t) : 0.0;
     const double v = live ? contrib(o, edim(t), 4, w, er, &J[slot][0], &J[slot][24]) : 0.0;
     if (o < 20) {
@@ -883,7 +941,10 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
         for (int q = s0; q < s1; q++) sm += cv[q][o];
         if (o < 16) S.Hll[16 * g + o] = sm;
         else S.bl[4 * g + o - 16] = sm;
-        if (maxd && o == 0 && A.lm_act[g]) {  // max |diagonal| of the block, as the ticket path
+        bool act = !SETUP && A.lm_act[g];
+        if (SETUP)
+          for (int q = s0; q < s1; q++) act = act || (einfo_s[q][2] & 2);
+        if (maxd && o == 0 && act) {  // max |diagonal| of the block, as the ticket path
           double mx = 0;
           for (int dgi = 0; dgi < 16; dgi += 5) {
             double sd = 0;
@@ -924,7 +985,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
         double mx = (ln < 16 && ln % 5 == 0) ? fabs(sm) : 0.0;
 #pragma unroll
         for (int o = 8; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
-        if (maxd && ln == 0 && A.lm_act[gl]) atomic_max_pos(S.out + 2, mx);
+        if (maxd && ln == 0 && (SETUP ? line_active(P, L, A, gl, cls) : A.lm_act[gl] != 0)) atomic_max_pos(S.out + 2, mx);
       }
     }
   }
@@ -935,7 +996,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
 // diagonals to S.out[2] (computeLambdaInit); speculative passes leave it alone.
 __global__ __launch_bounds__(256) void linearize_kernel(Problem P, Lin L, Active A, Sys S, int nbq, int maxd) {
   if ((int)blockIdx.x < nbq) lin_point_landmarks(P, L, A, S, blockIdx.x * 256 + threadIdx.x, maxd != 0);
-  else lin_lines<false>(P, L, A, S, blockIdx.x - nbq, maxd != 0);
+  else lin_lines<kLinPlain>(P, L, A, S, blockIdx.x - nbq, maxd != 0);
 }
 
 // deterministic block reduction of NV values per thread: wave shuffles, then waves in order
@@ -963,9 +1024,9 @@ __device__ __forceinline__ void block_reduce(double (&acc)[NV], double* lds /* [
 
 // max diagonal of the pose blocks (computeLambdaInit), first iteration only.  Block b sums
 // the Hpp diagonals of its 256 edges per reduced pose (fixed tree) into partial[a][b]; the
-// post kernel sums each pose's partials in block order and takes the max.
-__global__ __launch_bounds__(256) void pose_diag_kernel(Problem P, Lin L, Active A, Sys S) {
-  __shared__ double red[4 * 6];
+// post kernel (or pose_post_kernel's last block) sums each pose's partials in block order and takes
+// the max.  wt: the partials are written through (read by the last block of the same launch).
+__device__ __forceinline__ void pose_diag_block(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool wt) {
   const int e = blockIdx.x * 256 + threadIdx.x;
   int a = -1;
   double d[6] = {0, 0, 0, 0, 0, 0};
@@ -999,13 +1060,19 @@ __global__ __launch_bounds__(256) void pose_diag_kernel(Problem P, Lin L, Active
     __syncthreads();
     for (int q = threadIdx.x; q < 6 * pn; q += 256) {
       const int j = q / 6, i = q - 6 * j;
-      S.partial2[((size_t)(p0 + j) * gridDim.x + blockIdx.x) * 6 + i] =
-          ((wsum[0][j][i] + wsum[1][j][i]) + wsum[2][j][i]) + wsum[3][j][i];
+      const double v = ((wsum[0][j][i] + wsum[1][j][i]) + wsum[2][j][i]) + wsum[3][j][i];
+      double* dst = S.partial2 + ((size_t)(p0 + j) * gridDim.x + blockIdx.x) * 6 + i;
+      if (wt) __hip_atomic_store(dst, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      else *dst = v;
     }
     __syncthreads();
   }
-  (void)red;
 }
+
+__global__ __launch_bounds__(256) void pose_diag_kernel(Problem P, Lin L, Active A, Sys S) {
+  pose_diag_block(P, L, A, S, false);
+}
+
 
 // ---------------------------------------------------------------------------
 // Schur complement for damping lambda
@@ -1043,7 +1110,7 @@ __device__ __forceinline__ void schur_pair(const double (&H1)[24], const double 
 // CSR entries (independent loads) and placed by a wave prefix sum in lane order.
 template <bool FILL>
 __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, const int* pp_off, int4* pp) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;
   const int pr = c / A.nchk, lb = c - pr * A.nchk;
   const int pa = A.pairs[2 * pr], pb = A.pairs[2 * pr + 1];
   int base = FILL ? pp_off[c] : 0;
@@ -1134,6 +1201,169 @@ __global__ __launch_bounds__(1024) void pair_offsets_kernel(const int* cnt, int*
     run += cnt[i];
   }
   if (tid == 1023) off[n] = part[1023];
+}
+
+// ---------------------------------------------------------------------------
+// The first pass of a device-LM optimize() in two launches (was: errors, [classify,
+// landmark_active,] linearize, pose_diag, post).
+//   setup_kernel -- blocks [0, nbq): kGroup lanes per landmark (every landmark).  With `level` (the
+//     second optimize) the outlier levels of the landmark's edges from their last computed errors
+//     (classify_edge, g2o_optimization.cc:176-213) and its activity (landmark_active); for point
+//     landmarks the errors and robust cost at the current state and the linearisation (edge records,
+//     Hll / bl, the landmark diagonal maximum).  Blocks [nbq, nbq + n_lblk): the line workgroups
+//     (lin_lines<kLinSetup>: classification, cost and linearisation of their own edges).  The cost of
+//     block b goes to S.partial[b].
+//   pose_post_kernel -- pose_diag's blocks, then its last block (ticket): the cost (the setup
+//     partials in block order), the maximum diagonal, and the LM control (computeLambdaInit).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ double setup_landmark(const Problem& P, const Lin& L, const Active& A, const Sys& S, int t,
+                                                 uint8_t* level, uint8_t* lm_act2) {
+  const int g = t / kGroup, j = t % kGroup;
+  const bool in = g < A.nL, point = g < P.nq;
+  double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bv[3] = {0, 0, 0}, chi = 0;
+  int live = 0;
+  if (in) {
+    const int k1 = A.lm_off[g + 1];
+    const double* Xg = P.X + 3 * g;
+    for (int k = A.lm_off[g] + j; k < k1; k += kGroup) {
+      bool lev = false;
+      if (level && edge_outlier(P, L, k)) {
+        lev = true;
+        level[k] = 1;
+      }
+      live |= lev ? 0 : 1;
+      if (!point) continue;  // line edges: the line workgroups
+      const bool pose_opt = A.lm_pose[k] >= 0;
+      if (lev) {  // outside this phase: exact-zero records, no cost, error kept
+        if (pose_opt) zero_pose_records(L, k);
+        continue;
+      }
+      const int te = P.etype[k];
+      const SE3 T = load_T(P.T + 8 * P.epose[k]);
+      const double* cm = P.cams + 5 * P.ecam[k];
+      double er[4];
+      const double chi2 = point_error(te, cm, obs_of(P, k, te), T, Xg, er);
+#pragma unroll
+      for (int q = 0; q < 4; q++) L.err[4 * k + q] = er[q];
+      double cst = chi2;
+      if (A.robust) {
+        double r1;
+        huber(chi2, pick4(P.delta, te), cst, r1);
+      }
+      L.rho0[k] = cst;
+      chi += cst;
+      point_edge_core(P, L, A, k, te, pose_opt, T, cm, Xg, er, hl, bv);
+    }
+  }
+#pragma unroll
+  for (int o = 1; o < kGroup; o <<= 1) live |= __shfl_xor(live, o);
+  const bool act = level ? live != 0 : (in && A.lm_act[g] != 0);
+  if (level && in && j == 0) lm_act2[g] = act ? 1 : 0;
+  group_sum(hl);
+  group_sum(bv);
+  if (in && point && j == 0 && act) {
+    double* H = S.Hll + 16 * g;
+#pragma unroll
+    for (int i = 0; i < 9; i++) H[i] = hl[i];
+#pragma unroll
+    for (int i = 9; i < 16; i++) H[i] = 0.0;
+#pragma unroll
+    for (int i = 0; i < 3; i++) S.bl[4 * g + i] = bv[i];
+    S.bl[4 * g + 3] = 0.0;
+    atomic_max_pos(S.out + 2, fmax(fabs(hl[0]), fmax(fabs(hl[4]), fabs(hl[8]))));
+  }
+  return chi;
+}
+
+__global__ __launch_bounds__(256) void setup_kernel(Problem P, Lin L, Active A, Sys S, int nbq, int nb_lm,
+                                                    uint8_t* level, uint8_t* lm_act2, int* pp_cnt) {
+  __shared__ double red[4];
+  if ((int)blockIdx.x >= nb_lm) {  // the first optimize: edge pairs per Schur chunk, one wave per chunk
+    const int c = ((int)blockIdx.x - nb_lm) * 4 + (threadIdx.x >> 6);
+    if (c < A.npairs * A.nchk) pair_scan<false>(A, c, pp_cnt, nullptr, nullptr);
+    return;
+  }
+  if ((int)blockIdx.x >= nbq) {
+    double c = 0.0;  // set in thread 0
+    lin_lines<kLinSetup>(P, L, A, S, blockIdx.x - nbq, true, nullptr, nullptr, 0.0, false, nullptr, level != nullptr,
+                         &c);
+    if (threadIdx.x == 0) S.partial[blockIdx.x] = c;
+    return;
+  }
+  double acc[1] = {setup_landmark(P, L, A, S, blockIdx.x * 256 + threadIdx.x, level, lm_act2)};
+  block_reduce<1>(acc, red);
+  if (threadIdx.x == 0) S.partial[blockIdx.x] = red[0];
+}
+
+__global__ __launch_bounds__(256) void pose_post_kernel(Problem P, Lin L, Active A, Sys S, int nb_cost, int lm_iters,
+                                                        const int* pp_cnt, int* pp_off) {
+  __shared__ double red[4];
+  __shared__ double part[4][64];
+  __shared__ int last;
+  pose_diag_block(P, L, A, S, true);
+  if (threadIdx.x == 0) last = ticket(S.counter) == gridDim.x - 1;
+  __syncthreads();
+  if (!last) return;
+  double c[1] = {0.0};  // the cost: the setup blocks' partials (previous launch), fixed order
+  for (int k = threadIdx.x; k < nb_cost; k += 256) c[0] += S.partial[k];
+  block_reduce<1>(c, red);
+  const double chi2 = red[0];
+  if (pp_cnt) {  // exclusive scan of the chunks' edge-pair counts (setup_kernel) -> pp_off
+    __shared__ int sc[256];
+    const int tid = threadIdx.x, nc = A.npairs * A.nchk;
+    const int per = (nc + 255) / 256, b0 = min(tid * per, nc), b1 = min(b0 + per, nc);
+    int sm = 0;
+    for (int i = b0; i < b1; i++) sm += pp_cnt[i];
+    sc[tid] = sm;
+    __syncthreads();
+    for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan
+      const int t = tid >= o ? sc[tid - o] : 0;
+      __syncthreads();
+      sc[tid] += t;
+      __syncthreads();
+    }
+    int run = sc[tid] - sm;
+    for (int i = b0; i < b1; i++) {
+      pp_off[i] = run;
+      run += pp_cnt[i];
+    }
+    if (tid == 255) pp_off[nc] = sc[255];
+  }
+  // per pose and diagonal entry q = 6 pose + i: 4 waves each sum every 4th block partial (post_kernel)
+  const int lane = threadIdx.x & 63, pt = threadIdx.x >> 6, nq6 = 6 * A.K, npd = gridDim.x;
+  double mx = 0;
+  for (int q0 = 0; q0 < nq6; q0 += 64) {
+    const int q = q0 + lane;
+    double sacc = 0;
+    if (q < nq6) {
+      const int pa = q / 6, i = q - 6 * pa;
+      const double* src = S.partial2 + (size_t)pa * npd * 6 + i;
+      for (int b = pt; b < npd; b += 4)
+        sacc += __hip_atomic_load(src + (size_t)b * 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    part[pt][lane] = sacc;
+    __syncthreads();
+    if (pt == 0 && q < nq6) mx = fmax(mx, fabs(((part[0][lane] + part[1][lane]) + part[2][lane]) + part[3][lane]));
+    __syncthreads();
+  }
+  if (pt != 0) return;
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
+  if (lane != 0) return;
+  __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const double md = fmax(S.out[2], mx);
+  S.out[0] = chi2;
+  S.out[2] = md;
+  LmCtrl* ctl = S.lm;  // slot 0: the first trial's (computeLambdaInit: tau = 1e-5 x max diagonal)
+  ctl->lambda = 1e-5 * md;
+  ctl->ni = 2;
+  ctl->chi = chi2;
+  ctl->cur = 0;
+  ctl->it = 0;
+  ctl->qmax = 0;
+  ctl->stop = 0;
+  ctl->iters = lm_iters;
+  ctl->trials = 0;
 }
 
 // Schur complement, stage 1: one wave per chunk (pose pair, landmark range) walks its
@@ -1948,7 +2178,7 @@ __global__ __launch_bounds__(256) void update_kernel(Problem P, Lin L, Active A,
 // (records into the spare set Ls / Ss).  Blocks [0, nbu) are the landmark groups: besides the
 // update and the errors, a point group linearises its landmark's edges at the candidate from
 // the errors in its registers, and a line group writes the candidate line.  Blocks [nbu, ...) are
-// line-edge workgroups (lin_lines<true>) that form their landmarks' candidates themselves, so
+// line-edge workgroups (lin_lines<kLinSpec>) that form their landmarks' candidates themselves, so
 // they run from the kernel's start.  The mailbox ticket counts only the group blocks, so the
 // host decides while the line workgroups still run.
 template <bool SPEC>
@@ -1974,7 +2204,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
   }
   if (SPEC && (int)blockIdx.x >= nbu) {
     if (!spec) return;
-    lin_lines<true>(P, Ls, A, Ss, blockIdx.x - nbu, false, &L, &S, lambda, *S.fail != 0,
+    lin_lines<kLinSpec>(P, Ls, A, Ss, blockIdx.x - nbu, false, &L, &S, lambda, *S.fail != 0,
                     S.prof ? S.prof + kProfUe + 4 * blockIdx.x + 1 : nullptr);
     if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 3);
     return;
@@ -2220,21 +2450,6 @@ __global__ __launch_bounds__(256) void landmark_active_kernel(Active A, const ui
   lm_act[g] = on;
 }
 
-// outlier levels after the first optimize / final inlier flags (g2o_optimization.cc:176-231)
-__device__ __forceinline__ void edge_status(const Problem& P, const Lin& L, int e, double& chi2, bool& depth_ok) {
-  const int t = P.etype[e];
-  chi2 = 0;
-  for (int k = 0; k < edim(t); k++) chi2 += L.err[4 * e + k] * L.err[4 * e + k];
-  chi2 *= einfo(t);
-  depth_ok = true;
-  if (t < 2) {
-    const SE3 T = load_T(P.T + 8 * P.epose[e]);
-    double R[9], Xc[3];
-    q_to_R(T.q, R);
-    mat3_vec(R, P.X + 3 * P.elm[e], Xc);
-    depth_ok = Xc[2] + T.t[2] > 0.0;
-  }
-}
 __device__ __forceinline__ bool edge_inlier(const Problem& P, const Lin& L, int e) {
   double chi2;
   bool depth_ok;
@@ -2398,6 +2613,23 @@ hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys&
     hipLaunchKernelGGL(linearize_kernel, dim3(nbq + nbl), dim3(256), 0, s, P, L, A, S, nbq, with_maxdiag ? 1 : 0);
   if (with_maxdiag && A.K > 0 && A.Ea > 0)
     hipLaunchKernelGGL(pose_diag_kernel, dim3((A.Ea + 255) / 256), dim3(256), 0, s, P, L, A, S);
+  return hipGetLastError();
+}
+
+hipError_t setup_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, uint8_t* level, uint8_t* lm_act2,
+                     int lm_iters, int* pp_cnt, int* pp_off, int4* pp, hipStream_t s) {
+  if (!S.lm || lm_iters <= 0) return hipErrorInvalidValue;
+  Active A0 = A;
+  A0.elevel = nullptr;  // the levels are written by this launch (level != null), never read by it
+  const int nc = A.npairs * A.nchk;
+  if (nc == 0) pp_cnt = nullptr;
+  const int nbq = A.nL > 0 ? (A.nL * kGroup + 255) / 256 : 0, nb = nbq + A.n_lblk;
+  const int nbp = pp_cnt ? (nc + 3) / 4 : 0;
+  if (nb + nbp > 0)
+    hipLaunchKernelGGL(setup_kernel, dim3(nb + nbp), dim3(256), 0, s, P, L, A0, S, nbq, nb, level, lm_act2, pp_cnt);
+  const int npd = (A.K > 0 && A.Ea > 0) ? (A.Ea + 255) / 256 : 1;
+  hipLaunchKernelGGL(pose_post_kernel, dim3(npd), dim3(256), 0, s, P, L, A0, S, nb, lm_iters, pp_cnt, pp_off);
+  if (pp_cnt) hipLaunchKernelGGL(pair_fill_kernel, dim3(nc), dim3(64), 0, s, A, pp_off, pp);
   return hipGetLastError();
 }
 

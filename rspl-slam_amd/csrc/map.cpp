@@ -32,6 +32,69 @@ namespace {
 
 enum { kUnTriangulated = 0, kGood = 1, kBad = 2 };  // Mappoint::Type / Mapline::Type
 
+// The observer maps (frame id -> index) as a sorted vector: std::map's interface and ascending-key
+// iteration order, without a heap node per observation (a landmark has tens of observers; the
+// local-BA assembly walks every observer of every landmark of the window)
+template <typename V>
+struct FlatMap {
+  using Item = std::pair<int, V>;
+  std::vector<Item> v;
+  using iterator = typename std::vector<Item>::iterator;
+  using const_iterator = typename std::vector<Item>::const_iterator;
+  iterator begin() { return v.begin(); }
+  iterator end() { return v.end(); }
+  const_iterator begin() const { return v.begin(); }
+  const_iterator end() const { return v.end(); }
+  size_t size() const { return v.size(); }
+  bool empty() const { return v.empty(); }
+  void clear() { v.clear(); }
+  iterator lower(int k) {
+    return std::lower_bound(v.begin(), v.end(), k, [](const Item& a, int key) { return a.first < key; });
+  }
+  const_iterator lower(int k) const {
+    return std::lower_bound(v.begin(), v.end(), k, [](const Item& a, int key) { return a.first < key; });
+  }
+  iterator find(int k) {
+    auto it = lower(k);
+    return it != v.end() && it->first == k ? it : v.end();
+  }
+  const_iterator find(int k) const {
+    auto it = lower(k);
+    return it != v.end() && it->first == k ? it : v.end();
+  }
+  size_t count(int k) const { return find(k) != v.end(); }
+  V& operator[](int k) {
+    auto it = lower(k);
+    if (it == v.end() || it->first != k) it = v.insert(it, Item(k, V{}));
+    return it->second;
+  }
+  size_t erase(int k) {
+    auto it = find(k);
+    if (it == v.end()) return 0;
+    v.erase(it);
+    return 1;
+  }
+};
+
+// id -> element pointer: a dense table for ids in [0, kDenseIds) (frame / landmark ids are counters),
+// the hash map (which owns the elements; node-based, so pointers stay valid) for any other id
+constexpr int kDenseIds = 1 << 22;
+template <typename T>
+struct IdIndex {
+  std::vector<T*> dense;
+  T* get(const std::unordered_map<int, T>& store, int id) const {
+    if (id >= 0 && id < (int)dense.size()) return dense[id];
+    if (id >= 0 && id < kDenseIds) return nullptr;  // dense range: absent
+    auto it = store.find(id);
+    return it == store.end() ? nullptr : const_cast<T*>(&it->second);
+  }
+  void put(int id, T* p) {
+    if (id < 0 || id >= kDenseIds) return;
+    if (id >= (int)dense.size()) dense.resize(std::max<size_t>(id + 1, dense.size() * 2), nullptr);
+    dense[id] = p;
+  }
+};
+
 struct MFrame {
   int id = 0;
   double ts = 0;
@@ -91,7 +154,7 @@ struct MPoint {  // Mappoint
   int id = 0;
   double p[3] = {};
   int type = kUnTriangulated;
-  std::map<int, int> obs;  // _obversers: frame id -> keypoint index
+  FlatMap<int> obs;        // _obversers: frame id -> keypoint index
   int lmo = -1;
   int dense = -1;          // index in the last assembled problem
   int observers() const {  // ObverserNum
@@ -109,8 +172,8 @@ struct MLine {  // Mapline
   int id = 0;
   double L[6] = {};  // g2o::Line3D (w, d)
   int type = kUnTriangulated;
-  std::map<int, int> obs;   // frame id -> line index
-  std::map<int, int> incl;  // _included_endpoints
+  FlatMap<int> obs;         // frame id -> line index
+  FlatMap<int> incl;        // _included_endpoints
   int lmo = -1;
   int dense = -1;            // index in the last assembled problem
   double ep[6] = {};
@@ -201,6 +264,17 @@ struct rspl_map {
   // _mappoints / _maplines: looked up by id only, never iterated (node-based: element pointers stay valid)
   std::unordered_map<int, MPoint> mp;
   std::unordered_map<int, MLine> ml;
+  IdIndex<MFrame> kf_ix;
+  IdIndex<MPoint> mp_ix;
+  IdIndex<MLine> ml_ix;
+  // per-call scratch: a counter per frame id (dense range) and the ids touched
+  std::vector<int> cnt_f;
+  std::vector<int> touched;
+  int* frame_counter(int id) {
+    if (id < 0 || id >= kDenseIds) return nullptr;
+    if (id >= (int)cnt_f.size()) cnt_f.resize(std::max<size_t>(id + 1, cnt_f.size() * 2), 0);
+    return &cnt_f[id];
+  }
   // the last assembled problem (rspl_map_last_problem)
   std::vector<int> pose_ids, point_ids, line_ids;
   std::vector<uint8_t> pose_fixed;
@@ -208,46 +282,68 @@ struct rspl_map {
   std::vector<double> c_obs[4];
   std::vector<uint8_t> c_inl[4];
 
-  MFrame* frame(int id) {
-    auto it = kf.find(id);
-    return it == kf.end() ? nullptr : &it->second;
-  }
-  MPoint* point(int id) {
-    if (id < 0) return nullptr;
-    auto it = mp.find(id);
-    return it == mp.end() ? nullptr : &it->second;
-  }
-  MLine* line(int id) {
-    if (id < 0) return nullptr;
-    auto it = ml.find(id);
-    return it == ml.end() ? nullptr : &it->second;
-  }
+  MFrame* frame(int id) { return kf_ix.get(kf, id); }
+  MPoint* point(int id) { return id < 0 ? nullptr : mp_ix.get(mp, id); }
+  MLine* line(int id) { return id < 0 ? nullptr : ml_ix.get(ml, id); }
+
+  // counts per frame id of the ids pushed, handed back in ascending id order (a std::map<int, int>
+  // of counts) and reset; ids outside the dense range go through a std::map
+  struct Counter {
+    rspl_map* m;
+    std::map<int, int> big;
+    explicit Counter(rspl_map* mm) : m(mm) { m->touched.clear(); }
+    void add(int id, int w = 1) {
+      int* c = m->frame_counter(id);
+      if (!c) {
+        big[id] += w;
+        return;
+      }
+      if (*c == 0) m->touched.push_back(id);
+      *c += w;
+    }
+    template <typename F>
+    void drain(F&& f) {  // f(id, count) in ascending id order
+      std::sort(m->touched.begin(), m->touched.end());
+      auto bi = big.begin();
+      for (int id : m->touched) {
+        while (bi != big.end() && bi->first < id) { f(bi->first, bi->second); ++bi; }
+        const int c = m->cnt_f[id];
+        m->cnt_f[id] = 0;
+        f(id, c);
+      }
+      for (; bi != big.end(); ++bi) f(bi->first, bi->second);
+      m->touched.clear();
+      big.clear();
+    }
+  };
 
   // Map::UpdateFrameConnection (map.cc:897-937)
   void update_connection(MFrame& f) {
-    std::map<int, int> c;
+    Counter c(this);
+    bool any = false;
     for (int pid : f.mpt) {
       const MPoint* m = point(pid);
       if (!m || m->type == kBad) continue;
       for (auto& kv : m->obs) {
         if (kv.first == f.id || !frame(kv.first)) continue;
-        c[kv.first]++;
+        c.add(kv.first);
+        any = true;
       }
     }
-    if (c.empty()) return;
+    if (!any) return;
     std::set<std::pair<int, int>> good;
     int best = -1, best_w = -1;
-    for (auto& kv : c) {
-      MFrame* cf = frame(kv.first);
-      if (kv.second > best_w) {
-        best = kv.first;
-        best_w = kv.second;
+    c.drain([&](int id, int w) {  // ascending frame id (the reference's std::map)
+      MFrame* cf = frame(id);
+      if (w > best_w) {
+        best = id;
+        best_w = w;
       }
-      if (kv.second > 15) {
-        good.insert({kv.second, kv.first});
-        cf->add_connection(f.id, kv.second);
+      if (w > 15) {
+        good.insert({w, id});
+        cf->add_connection(f.id, w);
       }
-    }
+    });
     if (good.empty()) {
       good.insert({best_w, best});
       frame(best)->add_connection(f.id, best_w);
@@ -300,16 +396,16 @@ struct rspl_map {
   // Map::RemoveOutliers (map.cc:818-863).  frame->RemoveMappoint(mpt) runs after the observer was
   // removed, so it looks up index -1 and leaves the frame's slot as it is -- kept as in the reference.
   void remove_outliers(const std::vector<std::pair<int, int>>& outl) {
-    std::map<std::pair<int, int>, int> bad;
+    std::vector<std::pair<int, int>> bad;  // MakeFramePair per (outlier, other observer); counted below
     for (auto& fm : outl) {
       MFrame* f = frame(fm.first);
       MPoint* m = point(fm.second);
       if (!f || !m || m->type == kBad) continue;
       m->obs.erase(f->id);
-      const std::map<int, int> obs = m->obs;
+      const FlatMap<int>& obs = m->obs;  // read before the clear below (the reference copies it under its lock)
       for (auto& ob : obs) {
         MFrame* o = frame(ob.first);
-        if (o) bad[{std::max(f->id, o->id), std::min(f->id, o->id)}]++;  // MakeFramePair
+        if (o) bad.push_back({std::max(f->id, o->id), std::min(f->id, o->id)});  // MakeFramePair
       }
       if (m->observers() < 2 && m->type != kBad) {
         bool del = true;
@@ -332,9 +428,15 @@ struct rspl_map {
       }
       // frame->RemoveMappoint(mpt): GetKeypointIdx(frame id) is -1 by now -> no-op
     }
-    for (auto& kv : bad) {
-      frame(kv.first.first)->decrease_weight(kv.first.second, kv.second);
-      frame(kv.first.second)->decrease_weight(kv.first.first, kv.second);
+    // the reference's std::map<pair, int> of counts: pairs in ascending order, each with its count
+    std::sort(bad.begin(), bad.end());
+    for (size_t i = 0; i < bad.size();) {
+      size_t j = i;
+      while (j < bad.size() && bad[j] == bad[i]) j++;
+      const int n = (int)(j - i);
+      frame(bad[i].first)->decrease_weight(bad[i].second, n);
+      frame(bad[i].second)->decrease_weight(bad[i].first, n);
+      i = j;
     }
   }
 
@@ -346,7 +448,7 @@ struct rspl_map {
       if (!f || !l || l->type == kBad) continue;
       l->obs.erase(f->id);
       l->incl.erase(f->id);
-      const std::map<int, int> obs = l->obs;
+      const FlatMap<int>& obs = l->obs;
       if (l->observers() < 2 && l->type != kBad) {
         bool del = true;
         if (l->observers() > 0) {
@@ -459,7 +561,8 @@ struct rspl_map {
       fixed_num += fix;
       add_vertex(poses, *k, fix);
     }
-    std::map<int, int> fixed_frames;  // keyed by frame id (the reference: by FramePtr; only counted)
+    Counter fixed_frames(this);  // keyed by frame id (the reference: by FramePtr; only counted)
+    bool any_fixed = false;
     std::vector<int> mpts, mpls;
     for (MFrame* k : nb) {
       for (int pid : k->mpt) {
@@ -469,7 +572,10 @@ struct rspl_map {
         mpts.push_back(pid);
         for (auto& kv : m->obs) {
           MFrame* o = frame(kv.first);
-          if (o && o->lmo != fid) fixed_frames[o->id]++;
+          if (o && o->lmo != fid) {
+            fixed_frames.add(o->id);
+            any_fixed = true;
+          }
         }
       }
       for (int lid : k->mpl) {
@@ -480,9 +586,9 @@ struct rspl_map {
       }
     }
     const size_t max_fixed = 1;
-    if (!fixed_frames.empty() && max_fixed > fixed_num) {
-      std::set<std::pair<int, int>> ord;
-      for (auto& kv : fixed_frames) ord.insert({kv.second, kv.first});
+    std::set<std::pair<int, int>> ord;
+    fixed_frames.drain([&](int id, int w) { ord.insert({w, id}); });
+    if (any_fixed && max_fixed > fixed_num) {
       size_t add = std::min(max_fixed - fixed_num, ord.size());
       for (auto it = ord.rbegin(); add > 0; add--, ++it) {
         MFrame* o = frame(it->second);
@@ -659,6 +765,14 @@ struct rspl_map {
     }
     last_cons_ok = false;
     MFrame* nf = frame(last_fid);
+    static const bool timing = getenv("RSPL_MAP_TIMING") != nullptr;
+    using clk = std::chrono::steady_clock;
+    clk::time_point tm[8];
+    int ntm = 0;
+    auto mark = [&]() {
+      if (timing) tm[ntm++] = clk::now();
+    };
+    mark();
     const auto& cons = last_cons;
     const int np = (int)pose_ids.size();
     const double* rq = R.pose_q;
@@ -678,17 +792,20 @@ struct rspl_map {
     std::vector<std::pair<int, int>> outl, loutl;
     for (int t = 0; t < 2; t++)
       for (size_t i = 0; i < cons[t].size(); i++)
-        if (!c_inl[t][i] && frame(cons[t][i].pose) && mp.count(cons[t][i].lm)) outl.push_back({cons[t][i].pose, cons[t][i].lm});
+        if (!c_inl[t][i] && frame(cons[t][i].pose) && point(cons[t][i].lm)) outl.push_back({cons[t][i].pose, cons[t][i].lm});
     for (int t = 2; t < 4; t++)
       for (size_t i = 0; i < cons[t].size(); i++)
-        if (!c_inl[t][i] && frame(cons[t][i].pose) && ml.count(cons[t][i].lm)) loutl.push_back({cons[t][i].pose, cons[t][i].lm});
+        if (!c_inl[t][i] && frame(cons[t][i].pose) && line(cons[t][i].lm)) loutl.push_back({cons[t][i].pose, cons[t][i].lm});
     if (rep) {
       rep->n_point_outliers = (int)outl.size();
       rep->n_line_outliers = (int)loutl.size();
     }
+    mark();
     remove_outliers(outl);
     remove_line_outliers(loutl);
+    mark();
     update_connection(*nf);
+    mark();
     // write-back (map.cc:767-802)
     for (int i = 0; i < np; i++) {
       MFrame* f = frame(pose_ids[i]);
@@ -712,6 +829,12 @@ struct rspl_map {
       l->to_update = true;  // SetLine3D
       if (l->type == kUnTriangulated) l->type = kGood;
       l->ep_valid = update_mapline(*l);
+    }
+    mark();
+    if (timing && ntm == 5) {
+      auto us = [&](int i) { return std::chrono::duration<double, std::micro>(tm[i + 1] - tm[i]).count(); };
+      fprintf(stderr, "rspl_map finish us: outliers %.0f remove %.0f connections %.0f write-back %.0f\n", us(0), us(1),
+              us(2), us(3));
     }
     return RSPL_OK;
   }
@@ -759,7 +882,9 @@ extern "C" int rspl_map_add_keyframe(rspl_map* m, const rspl_map_keyframe* k) {
       for (int j = k->pol_offsets[i]; j < k->pol_offsets[i + 1]; j++) f.pol[i][k->pol_points[j]] = k->pol_dist[j];
   }
   f.parent = k->parent_id;
-  m->kf.emplace(f.id, std::move(f));
+  const int fid = f.id;
+  MFrame* fp = &m->kf.emplace(fid, std::move(f)).first->second;
+  m->kf_ix.put(fid, fp);
   m->kf_ids.push_back(k->frame_id);
   return RSPL_OK;
 }
@@ -771,7 +896,7 @@ extern "C" int rspl_map_add_mappoint(rspl_map* m, int id, const double* p, int t
   q.id = id;
   q.type = type;
   for (int i = 0; i < 3; i++) q.p[i] = p[i];
-  m->mp.emplace(id, q);
+  m->mp_ix.put(id, &m->mp.emplace(id, q).first->second);
   return RSPL_OK;
 }
 
@@ -782,7 +907,7 @@ extern "C" int rspl_map_add_mapline(rspl_map* m, int id, const double* line3d, i
   l.id = id;
   l.type = type;
   for (int i = 0; i < 6; i++) l.L[i] = line3d[i];
-  m->ml.emplace(id, l);
+  m->ml_ix.put(id, &m->ml.emplace(id, l).first->second);
   return RSPL_OK;
 }
 
