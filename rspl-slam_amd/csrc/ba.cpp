@@ -267,7 +267,7 @@ void report_prof(rspl_ba* b) {
           us(u0, last(ba::kProfUe, 0, nbu, 2)), us(u0, last(ba::kProfUe, 0, nbu, 3)),
           us(u0, last(ba::kProfUe, nbu, nue, 1)), us(u0, last(ba::kProfUe, nbu, nue, 2)),
           us(u0, last(ba::kProfUe, nbu, nue, 3)), us(h[1], h[5]), us(h[5], h[6]), us(h[6], h[7]), us(h[7], h[8]));
-  if (getenv("RSPL_BA_SOLVE") == nullptr || std::string(getenv("RSPL_BA_SOLVE")) == "blk4") {
+  if (getenv("RSPL_BA_SOLVE") && std::string(getenv("RSPL_BA_SOLVE")) == "blk4") {
     fprintf(stderr, "ba_steps us:");  // blocked solve: each pose block's panel, from the assembly's end
     for (int k = 5; k < 15 && h[k]; k++) fprintf(stderr, " %.2f", us(h[1], h[k]));
     fprintf(stderr, "\n");

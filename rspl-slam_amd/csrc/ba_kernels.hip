@@ -2580,14 +2580,15 @@ __global__ __launch_bounds__(256) void shard_finish_kernel(Problem P, int E, con
 int shard_red_len(int K, int nranks) { return 6 * K + nranks + 3; }
 bool fast_path(int K) { return 6 * K > 0 && 6 * K <= kCholLdsMax; }
 bool wave_path(int K) { return K > 0 && K <= kWaveSolveMaxK; }
-// reduced-system solver for K <= 10 (RSPL_BA_SOLVE: "blk4" default, "wave", "lds"; K > 10: "lds")
+// reduced-system solver for K <= 10 (RSPL_BA_SOLVE, read per trial: "wave" default -- the single-wave
+// LDL^T in the last Schur chunk, two launches per trial; "blk4" -- the 4-wave blocked LDL^T as a
+// third launch; "lds"; K > 10: "lds").  Pipeline A/B (profiles/r03_experiments.md): wave 788 vs blk4
+// 772 frames/s (mean of four alternating runs each, two boxes)
 static int solve_mode(int K) {
-  static const int m = [] {
-    const char* e = getenv("RSPL_BA_SOLVE");
-    if (e && std::string(e) == "wave") return 1;
-    if (e && std::string(e) == "lds") return 0;
-    return 2;
-  }();
+  const char* e = getenv("RSPL_BA_SOLVE");
+  int m = 1;
+  if (e && std::string(e) == "blk4") m = 2;
+  if (e && std::string(e) == "lds") m = 0;
   return wave_path(K) ? m : 0;
 }
 

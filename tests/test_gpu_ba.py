@@ -124,10 +124,13 @@ def test_ba_long_lines(ba):
     _compare(ba.run(prob), oracle.ba_local(prob), tol_pose=1e-6, tol_pt=1e-5, chi2_rtol=5e-8)
 
 
+@pytest.mark.parametrize("solver", ["wave", "blk4"])
 @pytest.mark.parametrize("n_poses", [2, 3, 4, 7, 11, 12])
-def test_ba_wave_solve_sizes(ba, n_poses):
+def test_ba_wave_solve_sizes(ba, n_poses, solver, monkeypatch):
     # K = n_poses - 1 optimised poses: K <= 10 solves the reduced system in one wavefront fused
-    # into the Schur chunks (single-wave LDL^T); K = 11 takes the blocked LDS solve
+    # into the Schur chunks (single-wave LDL^T, the default) or in the 4-wave blocked LDL^T launch
+    # (RSPL_BA_SOLVE=blk4, read per trial); K = 11 takes the blocked LDS solve
+    monkeypatch.setenv("RSPL_BA_SOLVE", solver)
     prob, gt = SY.ba_problem(n_poses=n_poses, n_points=500, n_lines=10, seed=60 + n_poses, pixel_sigma=0.8,
                              outlier_frac=0.05)
     _compare(ba.run(prob), oracle.ba_local(prob), tol_pose=1e-6, tol_pt=1e-5, chi2_rtol=5e-8)
