@@ -1338,8 +1338,16 @@ __global__ __launch_bounds__(256) void pose_post_kernel(Problem P, Lin L, Active
     if (q < nq6) {
       const int pa = q / 6, i = q - 6 * pa;
       const double* src = S.partial2 + (size_t)pa * npd * 6 + i;
-      for (int b = pt; b < npd; b += 4)
-        sacc += __hip_atomic_load(src + (size_t)b * 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      for (int b0 = pt; b0 < npd; b0 += 4 * 8) {  // 8 write-through loads in flight, summed in block order
+        double t[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const int b = b0 + 4 * u;
+          t[u] = b < npd ? __hip_atomic_load(src + (size_t)b * 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) sacc += t[u];
+      }
     }
     part[pt][lane] = sacc;
     __syncthreads();

@@ -55,6 +55,21 @@ def match_coords(m, F0, F1):
     return {(int(F0[1, q]), int(F0[2, q]), int(F1[1, t]), int(F1[2, t])) for q, t in np.asarray(m).reshape(-1, 2)}
 
 
+def align_z(Zg, Fg0, Fg1, Fc0, Fc1):
+    """Zg with its rows / columns put in the CPU path's keypoint order (the dustbin row / column last),
+    or None when the keypoint sets differ.  fp32 scores that differ in the last bits can swap the
+    top-k order of near-equal scores (std::sort by score, super_point.cpp:154-204) while the sets
+    agree; SuperGlue is permutation-equivariant, so Z is compared in one order."""
+    kg0, kg1 = key_index(Fg0), key_index(Fg1)
+    c0 = [(int(x), int(y)) for x, y in zip(Fc0[1], Fc0[2])]
+    c1 = [(int(x), int(y)) for x, y in zip(Fc1[1], Fc1[2])]
+    if set(c0) != set(kg0) or set(c1) != set(kg1):
+        return None
+    rows = [kg0[c] for c in c0] + [len(c0)]
+    cols = [kg1[c] for c in c1] + [len(c1)]
+    return Zg[np.ix_(rows, cols)]
+
+
 def z_errors(Zg, Z):
     """max |exp(Zg) - exp(Z)| (assignment probabilities) and max |dZ| where the CPU probability >= 1e-4;
     log-probabilities far below that amplify rounding and carry no decision"""
@@ -135,14 +150,18 @@ def main():
             cg_ = match_coords(nng, Fg[0], Fg[1])
             F16 = res["fp16"][0]
             c16 = match_coords(res["fp16"][2], F16[0], F16[1])
-            zerr = float(np.abs(Zg - Z).max()) if Zg.shape == Z.shape else float("nan")
-            dp, dzs = z_errors(Zg, Z)
-            dp16, _ = z_errors(res["fp16"][3], Z)
+            za = align_z(Zg, Fg[0], Fg[1], Fc[0], Fc[1])
+            za16 = align_z(res["fp16"][3], F16[0], F16[1], Fc[0], Fc[1])
+            zerr = float(np.abs(za - Z).max()) if za is not None else float("nan")
+            dp, dzs = z_errors(za, Z) if za is not None else (float("nan"), float("nan"))
+            dp16, _ = z_errors(za16, Z) if za16 is not None else (float("nan"), float("nan"))
+            order_same = all(np.array_equal(Fg[i][1:3], Fc[i][1:3]) for i in (0, 1) if Fg[i].shape == Fc[i].shape)
             lines_same = l0g.shape == l0c.shape and bool(np.array_equal(l0g, l0c))
             row = {"pair": t,
                    "keypoints": [int(Fc[0].shape[1]), int(Fc[1].shape[1])],
                    "keypoint_sets_identical": bool(set(kc) == set(kg)) and
                    set(key_index(Fc[1])) == set(key_index(Fg[1])),
+                   "keypoint_order_identical": bool(order_same and all(Fg[i].shape == Fc[i].shape for i in (0, 1))),
                    "desc_max_abs_diff": dmax,
                    "Z_max_abs_diff_fp32": zerr,
                    "P_max_abs_diff_fp32": dp, "Z_sig_max_abs_diff_fp32": dzs, "P_max_abs_diff_fp16": dp16,
@@ -167,10 +186,12 @@ def main():
         "pairs": len(rows), "image": f"{W}x{H}", "max_keypoints": K,
         "keypoint_sets_identical_frac": agg("keypoint_sets_identical"),
         "desc_max_abs_diff": float(max(r["desc_max_abs_diff"] for r in rows)),
-        "Z_max_abs_diff_fp32": float(max(r["Z_max_abs_diff_fp32"] for r in rows)),
-        "P_max_abs_diff_fp32": float(max(r["P_max_abs_diff_fp32"] for r in rows)),
-        "Z_sig_max_abs_diff_fp32": float(max(r["Z_sig_max_abs_diff_fp32"] for r in rows)),
-        "P_max_abs_diff_fp16": float(max(r["P_max_abs_diff_fp16"] for r in rows)),
+        "keypoint_order_identical_frac": agg("keypoint_order_identical"),
+        # Z / P over the pairs whose keypoint sets agree, in the CPU path's keypoint order (align_z)
+        "Z_max_abs_diff_fp32": float(np.nanmax([r["Z_max_abs_diff_fp32"] for r in rows])),
+        "P_max_abs_diff_fp32": float(np.nanmax([r["P_max_abs_diff_fp32"] for r in rows])),
+        "Z_sig_max_abs_diff_fp32": float(np.nanmax([r["Z_sig_max_abs_diff_fp32"] for r in rows])),
+        "P_max_abs_diff_fp16": float(np.nanmax([r["P_max_abs_diff_fp16"] for r in rows])),
         "keypoint_sets_identical_fp16_frac": agg("keypoint_sets_identical_fp16"),
         "thresholded_matches_identical_frac": agg("matches_identical"),
         "matches_per_pair_cpu": agg("matches_cpu"),
