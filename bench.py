@@ -27,8 +27,9 @@ max-over-ranks timing and the rank census (fails loudly if fewer than N distinct
 solves every step's N local BAs (one per rank's sequence) jointly, landmark-sharded over all
 ranks with an RCCL all-reduce of the reduced camera system per LM trial.
 
-Workloads: `--workload c3` (default, BASELINE configs[2]) or `c5` (configs[4]: synthetic
-1920x1080 stereo, 2048 keypoints, SG N=2048, 30-keyframe / 10k-landmark BA).
+Workloads: `--workload c3` (default, BASELINE configs[2]), `c4` (configs[3]'s per-GPU sequence:
+OIVIO-shaped 640x512 stereo, 600 keypoints, SG N=600; with --gpus 8 one sequence per GPU) or `c5`
+(configs[4]: synthetic 1920x1080 stereo, 2048 keypoints, SG N=2048, 30-keyframe / 10k-landmark BA).
 """
 import argparse
 import json
@@ -57,6 +58,9 @@ WORKLOADS = {
     "c3": dict(H=480, W=752, K=400, ba=dict(n_poses=10, n_points=4000, n_lines=100), ba_caps=(16, 6000, 200, 40000),
                desc="C3 EuRoC 752x480 stereo keyframe stream: SP batch 2 top-400, SG 2 pairs N=400, "
                     "local BA 10 poses / ~4k points / 100 lines"),
+    "c4": dict(H=512, W=640, K=600, ba=dict(n_poses=10, n_points=4000, n_lines=100), ba_caps=(16, 6000, 200, 40000),
+               desc="C4 OIVIO-shaped 640x512 stereo keyframe stream (one sequence per GPU): SP batch 2 top-600, SG 2 "
+                    "pairs N=600, local BA 10 poses / ~4k points / 100 lines"),
     "c5": dict(H=1080, W=1920, K=2048, ba=dict(n_poses=30, n_points=10000, n_lines=0, pixel_sigma=0.8,
                                                outlier_frac=0.05), ba_caps=(32, 10000, 16, 70000),
                desc="C5 synthetic 1920x1080 stereo stream: SP batch 2 top-2048, SG 2 pairs N=2048, "
@@ -533,9 +537,10 @@ def main():
     ba_it = float(np.mean(res["ba_iters"])) if res["ba_iters"] else None
     ba_bytes = float(np.mean([ba_bytes_per_iteration(p) for p in problems]))
     out = {
-        "metric": "stereo frames/sec SuperPoint+SuperGlue+localBA @752x480 (all-keyframe: 2xSP, 2xSG, 1 BA per frame)"
-                  if args.workload == "c3" else
-                  "stereo frames/sec SuperPoint+SuperGlue+localBA @1920x1080 (C5, all-keyframe: 2xSP, 2xSG, 1 BA per frame)",
+        "metric": {"c3": "stereo frames/sec SuperPoint+SuperGlue+localBA @752x480 (all-keyframe: 2xSP, 2xSG, 1 BA per frame)",
+                   "c4": "stereo frames/sec SuperPoint+SuperGlue+localBA @640x512 (C4, all-keyframe: 2xSP, 2xSG, 1 BA per frame)",
+                   "c5": "stereo frames/sec SuperPoint+SuperGlue+localBA @1920x1080 (C5, all-keyframe: 2xSP, 2xSG, 1 BA per frame)"
+                   }[args.workload],
         "value": round(value, 3),
         "unit": "frames/s",
         "n_gpus": world,
