@@ -74,6 +74,8 @@ struct rspl_ba {
   double* lm_trace = nullptr;   // RSPL_BA_LMTRACE: per-trial decisions (debug)
   double* gbuf = nullptr;      // final gather buffer (grown on demand)
   size_t gcap = 0;
+  double* pdg = nullptr;       // per-block pose-diagonal partials of the first pass (grown on demand)
+  size_t pdg_cap = 0;
 };
 
 namespace {
@@ -311,8 +313,18 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
   // nothing is posted: the host waits for the trials only
   static const bool split_setup = getenv("RSPL_BA_SETUP") && std::string(getenv("RSPL_BA_SETUP")) == "split";
   if (!split_setup) {
+    const size_t need = (size_t)ba::setup_pdg_len(A);
+    if (need > b->pdg_cap) {  // grow (the stream may still read the old buffer)
+      RSPL_HIP(hipStreamSynchronize(st));
+      if (b->pdg) (void)hipFree(b->pdg);
+      b->pdg = nullptr;
+      b->pdg_cap = 0;
+      const size_t cap = std::max(need, (size_t)1 << 14);
+      RSPL_HIP(hipMalloc((void**)&b->pdg, sizeof(double) * cap));
+      b->pdg_cap = cap;
+    }
     RSPL_HIP(ba::setup_dev(P, Lr, A, S, cls_level, cls_level ? const_cast<uint8_t*>(A.lm_act) : nullptr, iters,
-                           build_pp ? b->pp_cnt : nullptr, b->pp_off, b->pp_buf, st));
+                           build_pp ? b->pp_cnt : nullptr, b->pp_off, b->pp_buf, b->pdg, st));
   } else {  // A/B knob: the separate launches (build_pairs, classify, landmark_active, errors, linearize,
             // pose_diag, post)
     if (build_pp) RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, st));
@@ -594,6 +606,7 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
   if (!b) return;
   if (b->stream) (void)hipStreamSynchronize(b->stream);
   if (b->gbuf) (void)hipFree(b->gbuf);
+  if (b->pdg) (void)hipFree(b->pdg);
   b->arena.release();
   if (b->cbuf) (void)hipFree(b->cbuf);
   if (b->pp_buf) (void)hipFree(b->pp_buf);

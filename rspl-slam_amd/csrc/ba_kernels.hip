@@ -1024,7 +1024,7 @@ __device__ __forceinline__ void block_reduce(double (&acc)[NV], double* lds /* [
 
 // max diagonal of the pose blocks (computeLambdaInit), first iteration only.  Block b sums
 // the Hpp diagonals of its 256 edges per reduced pose (fixed tree) into partial[a][b]; the
-// post kernel (or pose_post_kernel's last block) sums each pose's partials in block order and takes
+// post kernel sums each pose's partials in block order and takes
 // the max.  wt: the partials are written through (read by the last block of the same launch).
 __device__ __forceinline__ void pose_diag_block(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool wt) {
   const int e = blockIdx.x * 256 + threadIdx.x;
@@ -1071,6 +1071,53 @@ __device__ __forceinline__ void pose_diag_block(const Problem& P, const Lin& L, 
 
 __global__ __launch_bounds__(256) void pose_diag_kernel(Problem P, Lin L, Active A, Sys S) {
   pose_diag_block(P, L, A, S, false);
+}
+
+// pose_diag_block over the edge range [e0, e1) (a setup block's own edges, any length; rounds of 256
+// summed per wave in round order): partial b of nb into dst[(a * nb + b) * 6 + i], written through.
+// The block's record stores must be complete and visible (s_waitcnt + barrier) before the call.
+__device__ __forceinline__ void pose_diag_range(const Problem& P, const Lin& L, const Active& A, double* dst, int nb,
+                                                int b, int e0, int e1) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  __shared__ double wsum[4][32][6];
+  for (int p0 = 0; p0 < A.K; p0 += 32) {
+    const int pn = min(32, A.K - p0);
+    for (int j = 0; j < pn; j++)
+      if (lane < 6) wsum[wv][j][lane] = 0.0;
+    for (int eb = e0; eb < e1; eb += 256) {  // block-uniform
+      const int e = eb + threadIdx.x;
+      int a = -1;
+      double d[6] = {0, 0, 0, 0, 0, 0};
+      if (e < e1) {
+        a = A.pidx[P.epose[e]];
+        if (a >= 0) {
+          const double* H = L.Hpp + 21 * e;
+#pragma unroll
+          for (int i = 0; i < 6; i++) d[i] = H[pk6(i, i)];
+        }
+      }
+      for (int j = 0; j < pn; j++) {
+        const int pa = p0 + j;
+        double acc[6];
+#pragma unroll
+        for (int i = 0; i < 6; i++) acc[i] = a == pa ? d[i] : 0.0;
+        if (__ballot(a == pa)) {  // wave-uniform
+#pragma unroll
+          for (int o = 32; o >= 1; o >>= 1)
+#pragma unroll
+            for (int i = 0; i < 6; i++) acc[i] += __shfl_xor(acc[i], o);
+        }
+        if (lane < 6) wsum[wv][j][lane] += acc[lane];
+      }
+    }
+    __syncthreads();
+    for (int q = threadIdx.x; q < 6 * pn; q += 256) {
+      const int j = q / 6, i = q - 6 * j;
+      const double v = ((wsum[0][j][i] + wsum[1][j][i]) + wsum[2][j][i]) + wsum[3][j][i];
+      __hip_atomic_store(dst + ((size_t)(p0 + j) * nb + b) * 6 + i, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+  }
 }
 
 
@@ -1171,7 +1218,7 @@ __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, c
     }
     base += total;
   }
-  if (!FILL && lane == 0) pp_cnt[c] = base;
+  if (!FILL && lane == 0) __hip_atomic_store(pp_cnt + c, base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 __global__ __launch_bounds__(64) void pair_count_kernel(Active A, int* pp_cnt) {
@@ -1204,17 +1251,16 @@ __global__ __launch_bounds__(1024) void pair_offsets_kernel(const int* cnt, int*
 }
 
 // ---------------------------------------------------------------------------
-// The first pass of a device-LM optimize() in two launches (was: errors, [classify,
-// landmark_active,] linearize, pose_diag, post).
+// The first pass of a device-LM optimize() in one launch (was: errors, [classify,
+// landmark_active,] linearize, pose_diag, post; build_pairs' count and scan in the first optimize).
 //   setup_kernel -- blocks [0, nbq): kGroup lanes per landmark (every landmark).  With `level` (the
 //     second optimize) the outlier levels of the landmark's edges from their last computed errors
 //     (classify_edge, g2o_optimization.cc:176-213) and its activity (landmark_active); for point
 //     landmarks the errors and robust cost at the current state and the linearisation (edge records,
 //     Hll / bl, the landmark diagonal maximum).  Blocks [nbq, nbq + n_lblk): the line workgroups
 //     (lin_lines<kLinSetup>: classification, cost and linearisation of their own edges).  The cost of
-//     block b goes to S.partial[b].
-//   pose_post_kernel -- pose_diag's blocks, then its last block (ticket): the cost (the setup
-//     partials in block order), the maximum diagonal, and the LM control (computeLambdaInit).
+//     block b goes to S.partial[b], its edges' pose-diagonal sums to pdg.  Then the last block of the
+//     launch (ticket): the cost, the maximum diagonal and the LM control (computeLambdaInit).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double setup_landmark(const Problem& P, const Lin& L, const Active& A, const Sys& S, int t,
                                                  uint8_t* level, uint8_t* lm_act2) {
@@ -1275,45 +1321,55 @@ __device__ __forceinline__ double setup_landmark(const Problem& P, const Lin& L,
   return chi;
 }
 
+// The first pass in ONE launch: blocks [0, nbq) landmark groups, [nbq, nb_lm) line workgroups,
+// [nb_lm, ...) pair counting; every landmark / line block then sums the pose diagonals of its own
+// edges (pose_diag_range -> pdg) and every block takes a ticket; the last block sums the cost
+// partials and the pose-diagonal partials in block order, scans the pair counts and writes the LM
+// control (round 3 did this in a second launch; one launch measured neutral, four per call instead of six).
 __global__ __launch_bounds__(256) void setup_kernel(Problem P, Lin L, Active A, Sys S, int nbq, int nb_lm,
-                                                    uint8_t* level, uint8_t* lm_act2, int* pp_cnt) {
-  __shared__ double red[4];
-  if ((int)blockIdx.x >= nb_lm) {  // the first optimize: edge pairs per Schur chunk, one wave per chunk
-    const int c = ((int)blockIdx.x - nb_lm) * 4 + (threadIdx.x >> 6);
-    if (c < A.npairs * A.nchk) pair_scan<false>(A, c, pp_cnt, nullptr, nullptr);
-    return;
-  }
-  if ((int)blockIdx.x >= nbq) {
-    double c = 0.0;  // set in thread 0
-    lin_lines<kLinSetup>(P, L, A, S, blockIdx.x - nbq, true, nullptr, nullptr, 0.0, false, nullptr, level != nullptr,
-                         &c);
-    if (threadIdx.x == 0) S.partial[blockIdx.x] = c;
-    return;
-  }
-  double acc[1] = {setup_landmark(P, L, A, S, blockIdx.x * 256 + threadIdx.x, level, lm_act2)};
-  block_reduce<1>(acc, red);
-  if (threadIdx.x == 0) S.partial[blockIdx.x] = red[0];
-}
-
-__global__ __launch_bounds__(256) void pose_post_kernel(Problem P, Lin L, Active A, Sys S, int nb_cost, int lm_iters,
-                                                        const int* pp_cnt, int* pp_off) {
+                                                    uint8_t* level, uint8_t* lm_act2, int* pp_cnt, int* pp_off,
+                                                    double* pdg, int lm_iters) {
   __shared__ double red[4];
   __shared__ double part[4][64];
   __shared__ int last;
-  pose_diag_block(P, L, A, S, true);
+  const int b = blockIdx.x;
+  if (b >= nb_lm) {  // the first optimize: edge pairs per Schur chunk, one wave per chunk
+    const int c = (b - nb_lm) * 4 + (threadIdx.x >> 6);
+    if (c < A.npairs * A.nchk) pair_scan<false>(A, c, pp_cnt, nullptr, nullptr);
+  } else if (b >= nbq) {
+    double c = 0.0;  // set in thread 0
+    lin_lines<kLinSetup>(P, L, A, S, b - nbq, true, nullptr, nullptr, 0.0, false, nullptr, level != nullptr, &c);
+    if (threadIdx.x == 0) __hip_atomic_store(S.partial + b, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const int4 tb = A.ltab[b - nbq];
+    pose_diag_range(P, L, A, pdg, nb_lm, b, tb.x, tb.x + (tb.y & 0xff));
+  } else {
+    double acc[1] = {setup_landmark(P, L, A, S, b * 256 + threadIdx.x, level, lm_act2)};
+    block_reduce<1>(acc, red);
+    if (threadIdx.x == 0) __hip_atomic_store(S.partial + b, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    // this block's point landmarks' edges: one CSR range
+    const int g0 = min(b * (256 / kGroup), P.nq), g1 = min(b * (256 / kGroup) + 256 / kGroup, P.nq);
+    pose_diag_range(P, L, A, pdg, nb_lm, b, A.lm_off[g0], A.lm_off[g1]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   if (threadIdx.x == 0) last = ticket(S.counter) == gridDim.x - 1;
   __syncthreads();
   if (!last) return;
-  double c[1] = {0.0};  // the cost: the setup blocks' partials (previous launch), fixed order
-  for (int k = threadIdx.x; k < nb_cost; k += 256) c[0] += S.partial[k];
-  block_reduce<1>(c, red);
+  // ---- the last block ----
+  double cs[1] = {0.0};  // the cost: the landmark / line blocks' partials, fixed order
+  for (int k = threadIdx.x; k < nb_lm; k += 256) cs[0] += __hip_atomic_load(S.partial + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  block_reduce<1>(cs, red);
   const double chi2 = red[0];
-  if (pp_cnt) {  // exclusive scan of the chunks' edge-pair counts (setup_kernel) -> pp_off
+  if (pp_cnt) {  // exclusive scan of the chunks' edge-pair counts -> pp_off
     __shared__ int sc[256];
     const int tid = threadIdx.x, nc = A.npairs * A.nchk;
     const int per = (nc + 255) / 256, b0 = min(tid * per, nc), b1 = min(b0 + per, nc);
     int sm = 0;
-    for (int i = b0; i < b1; i++) sm += pp_cnt[i];
+    for (int i = b0; i < b1; i++) sm += __hip_atomic_load(pp_cnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     sc[tid] = sm;
     __syncthreads();
     for (int o = 1; o < 256; o <<= 1) {  // Hillis-Steele inclusive scan
@@ -1325,25 +1381,25 @@ __global__ __launch_bounds__(256) void pose_post_kernel(Problem P, Lin L, Active
     int run = sc[tid] - sm;
     for (int i = b0; i < b1; i++) {
       pp_off[i] = run;
-      run += pp_cnt[i];
+      run += __hip_atomic_load(pp_cnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     if (tid == 255) pp_off[nc] = sc[255];
   }
-  // per pose and diagonal entry q = 6 pose + i: 4 waves each sum every 4th block partial (post_kernel)
-  const int lane = threadIdx.x & 63, pt = threadIdx.x >> 6, nq6 = 6 * A.K, npd = gridDim.x;
+  // per pose and diagonal entry q = 6 pose + i: 4 waves each sum every 4th block partial
+  const int lane = threadIdx.x & 63, pt = threadIdx.x >> 6, nq6 = 6 * A.K, npd = nb_lm;
   double mx = 0;
   for (int q0 = 0; q0 < nq6; q0 += 64) {
     const int q = q0 + lane;
     double sacc = 0;
     if (q < nq6) {
       const int pa = q / 6, i = q - 6 * pa;
-      const double* src = S.partial2 + (size_t)pa * npd * 6 + i;
+      const double* src = pdg + (size_t)pa * npd * 6 + i;
       for (int b0 = pt; b0 < npd; b0 += 4 * 8) {  // 8 write-through loads in flight, summed in block order
         double t[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          const int b = b0 + 4 * u;
-          t[u] = b < npd ? __hip_atomic_load(src + (size_t)b * 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+          const int bb = b0 + 4 * u;
+          t[u] = bb < npd ? __hip_atomic_load(src + (size_t)bb * 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) sacc += t[u];
@@ -1359,7 +1415,8 @@ __global__ __launch_bounds__(256) void pose_post_kernel(Problem P, Lin L, Active
   for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
   if (lane != 0) return;
   __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const double md = fmax(S.out[2], mx);
+  // the landmark diagonal maximum (atomic max of the landmark blocks: performed device-coherently)
+  const double md = fmax(__hip_atomic_load(S.out + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), mx);
   S.out[0] = chi2;
   S.out[2] = md;
   LmCtrl* ctl = S.lm;  // slot 0: the first trial's (computeLambdaInit: tau = 1e-5 x max diagonal)
@@ -2625,8 +2682,13 @@ hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys&
   return hipGetLastError();
 }
 
+int setup_pdg_len(const Active& A) {
+  const int nbq = A.nL > 0 ? (A.nL * kGroup + 255) / 256 : 0;
+  return 6 * A.K * (nbq + A.n_lblk) + 6;
+}
+
 hipError_t setup_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, uint8_t* level, uint8_t* lm_act2,
-                     int lm_iters, int* pp_cnt, int* pp_off, int4* pp, hipStream_t s) {
+                     int lm_iters, int* pp_cnt, int* pp_off, int4* pp, double* pdg, hipStream_t s) {
   if (!S.lm || lm_iters <= 0) return hipErrorInvalidValue;
   Active A0 = A;
   A0.elevel = nullptr;  // the levels are written by this launch (level != null), never read by it
@@ -2634,10 +2696,9 @@ hipError_t setup_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, ui
   if (nc == 0) pp_cnt = nullptr;
   const int nbq = A.nL > 0 ? (A.nL * kGroup + 255) / 256 : 0, nb = nbq + A.n_lblk;
   const int nbp = pp_cnt ? (nc + 3) / 4 : 0;
-  if (nb + nbp > 0)
-    hipLaunchKernelGGL(setup_kernel, dim3(nb + nbp), dim3(256), 0, s, P, L, A0, S, nbq, nb, level, lm_act2, pp_cnt);
-  const int npd = (A.K > 0 && A.Ea > 0) ? (A.Ea + 255) / 256 : 1;
-  hipLaunchKernelGGL(pose_post_kernel, dim3(npd), dim3(256), 0, s, P, L, A0, S, nb, lm_iters, pp_cnt, pp_off);
+  // at least one block: the last one writes the LM control
+  hipLaunchKernelGGL(setup_kernel, dim3(std::max(nb + nbp, 1)), dim3(256), 0, s, P, L, A0, S, nbq, nb, level, lm_act2,
+                     pp_cnt, pp_off, pdg, lm_iters);
   if (pp_cnt) hipLaunchKernelGGL(pair_fill_kernel, dim3(nc), dim3(64), 0, s, A, pp_off, pp);
   return hipGetLastError();
 }

@@ -134,15 +134,17 @@ hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys&
                      hipStream_t s);
 // mailbox post; with A, after linearize(with_maxdiag) it first folds the pose-block maxima in
 hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A = nullptr, int lm_iters = 0);
-// the first pass of a device-LM optimize() (S.lm set, lm_iters > 0) in two launches: errors, robust
+// the first pass of a device-LM optimize() (S.lm set, lm_iters > 0) in one launch: errors, robust
 // cost and linearisation at the current state, the pose / landmark diagonal maximum and the LM control
 // (computeLambdaInit) into S.lm[0].  level != null (the second optimize): the edges' outlier levels
 // from their last computed errors into level[] and the landmark activity into lm_act2 first (replaces
 // classify + landmark_active); A.elevel / A.lm_act are then the caller's level / lm_act2.  pp_cnt
 // != null (the call's first optimize): the Schur chunks' edge-pair lists too (replaces build_pairs:
 // counted in the first launch, scanned by the second's last block, filled by a third).
+// pdg: setup_pdg_len(A) doubles of per-block pose-diagonal partials.
 hipError_t setup_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, uint8_t* level, uint8_t* lm_act2,
-                     int lm_iters, int* pp_cnt, int* pp_off, int4* pp, hipStream_t s);
+                     int lm_iters, int* pp_cnt, int* pp_off, int4* pp, double* pdg, hipStream_t s);
+int setup_pdg_len(const Active& A);
 // speculative linearisation of a trial's candidate into a spare record set, fused into the
 // trial's last kernel (fast path only)
 struct Spec {
