@@ -138,8 +138,8 @@ struct SinkArgs {
   const int* n1;
   int nmax, G, iters;
   int rb;             // 1: row-block kernel (rows in registers, one exchange per iteration)
-  int sleep;          // row-block kernel: s_sleep(1) units between re-polls (RSPL_SG_SLEEP, default 1)
-  int fx;             // row-block kernel: v_exp_f32-based exp (default; RSPL_SG_FEXP=0 selects expf)
+  int sleep;          // row-block kernel: s_sleep(1) units between re-polls (run_sinkhorn: 1)
+  int fx;             // row-block kernel: v_exp_f32-based exp (1, what run_sinkhorn sets) or expf (0)
   int sc;             // with rb: the scaling-form kernel (register-resident exp(C + a + b), two mat-vecs per iteration)
 };
 
