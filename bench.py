@@ -269,6 +269,11 @@ def rank_census(group, world, want, local, cnt):
 
 
 def main():
+    # The BA runs on a tracking thread beside the feature loop (both Python here, C++ threads in the
+    # reference): RSPL_GIL_SWITCH_US sets the interpreter's GIL switch interval (A/B knob; default
+    # the interpreter's 5 ms)
+    if os.environ.get("RSPL_GIL_SWITCH_US"):
+        sys.setswitchinterval(float(os.environ["RSPL_GIL_SWITCH_US"]) * 1e-6)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -405,6 +410,7 @@ def main():
             """BA worker: the reference runs LocalmapOptimization on the tracking thread while the
             feature thread keeps extracting/matching (src/map_builder.cc:48-49, src/map.cc:105-107)."""
             capi.check(capi.load().rspl_set_device(local), "rspl_set_device")  # HIP device is per thread
+            outs_ba = {}  # one result buffer per problem, reused (the bench reads only the counters)
             while True:
                 item = ba_q.get()
                 if item is None:
@@ -413,7 +419,8 @@ def main():
                 t = time.perf_counter()
                 try:
                     for prob in item:
-                        r = ba.run(prob)
+                        r = ba.run(prob, out=outs_ba.get(id(prob)))
+                        outs_ba[id(prob)] = r
                         ba_iters.append(r.iters_first + r.iters_second)
                 except Exception as e:  # surfaced on the main thread
                     ba_err.append(e)

@@ -260,10 +260,11 @@ class LocalBA:
         cfg = capi.BaConfig(max_poses, max_points, max_lines, max_edges, device)
         capi.check(self._lib.rspl_ba_create(C.byref(cfg), C.byref(self._h)), "rspl_ba_create")
 
-    def run(self, problem):
-        """problem: ba_types.DenseProblem -> ba_types.DenseResult"""
+    def run(self, problem, out=None):
+        """problem: ba_types.DenseProblem -> ba_types.DenseResult.  out: a DenseResult of a problem with
+        the same shapes to write into (no per-call allocation; its previous contents are overwritten)."""
         from .ba_types import DenseResult
-        res = DenseResult.alloc(problem)
+        res = out if out is not None and out.fits(problem) else DenseResult.alloc(problem)
         P, R = problem.to_ctypes(), res.to_ctypes()
         capi.check(self._lib.rspl_ba_local(self._h, C.byref(P), C.byref(R)), "rspl_ba_local")
         res.read_back(R)

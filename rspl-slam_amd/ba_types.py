@@ -249,14 +249,24 @@ class DenseResult:
         r._buf, r._offs = buf, offs
         return r
 
+    def fits(self, p: DenseProblem) -> bool:
+        """this result's arrays have the shapes a result of problem p needs"""
+        return (self.pose_q.shape == p.pose_q.shape and self.pose_p.shape == p.pose_p.shape and
+                self.points.shape == p.points.shape and self.lines.shape == p.lines.shape and
+                all(self.inlier[k].shape[0] == p.n_edges(k) for k in DenseResult._KINDS))
+
     def to_ctypes(self) -> RsplBaResult:
-        R = RsplBaResult()
         buf = getattr(self, "_buf", None)
         if buf is not None:
-            base = buf.ctypes.data
-            (R.pose_q, R.pose_p, R.points, R.lines, R.mono_inlier, R.stereo_inlier, R.mono_line_inlier,
-             R.stereo_line_inlier) = (base + o for o in self._offs)
+            R = self.__dict__.get("_ct")
+            if R is None:  # one pointer struct per buffer (the scalars are rewritten by every call)
+                R = RsplBaResult()
+                base = buf.ctypes.data
+                (R.pose_q, R.pose_p, R.points, R.lines, R.mono_inlier, R.stereo_inlier, R.mono_line_inlier,
+                 R.stereo_line_inlier) = (base + o for o in self._offs)
+                self.__dict__["_ct"] = R
             return R
+        R = RsplBaResult()
         arrs = [self.pose_q, self.pose_p, self.points, self.lines] + [self.inlier[k] for k in self._KINDS]
         (R.pose_q, R.pose_p, R.points, R.lines, R.mono_inlier, R.stereo_inlier, R.mono_line_inlier,
          R.stereo_line_inlier) = (np.ascontiguousarray(a).ctypes.data for a in arrs)
