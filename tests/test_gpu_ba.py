@@ -134,3 +134,24 @@ def test_ba_wave_solve_sizes(ba, n_poses, solver, monkeypatch):
     prob, gt = SY.ba_problem(n_poses=n_poses, n_points=500, n_lines=10, seed=60 + n_poses, pixel_sigma=0.8,
                              outlier_frac=0.05)
     _compare(ba.run(prob), oracle.ba_local(prob), tol_pose=1e-6, tol_pt=1e-5, chi2_rtol=5e-8)
+
+
+def test_ba_run_into_reused_result(ba):
+    """LocalBA.run(problem, out=res): the same numbers as a fresh result, written into res's buffers
+    (the bench's tracking thread reuses one result per problem); a result of other shapes is not
+    reused."""
+    p1, _ = SY.ba_problem(n_poses=6, n_points=400, n_lines=12, seed=71, pixel_sigma=0.8, outlier_frac=0.05)
+    p2, _ = SY.ba_problem(n_poses=5, n_points=300, n_lines=8, seed=72, pixel_sigma=0.8, outlier_frac=0.05)
+    fresh = ba.run(p1)
+    out = ba.run(p1)
+    again = ba.run(p1, out=out)
+    assert again is out
+    np.testing.assert_array_equal(again.pose_q, fresh.pose_q)
+    np.testing.assert_array_equal(again.points, fresh.points)
+    np.testing.assert_array_equal(again.lines, fresh.lines)
+    for k in ("mono", "stereo", "mono_line", "stereo_line"):
+        np.testing.assert_array_equal(again.inlier[k], fresh.inlier[k])
+    assert (again.chi2_first, again.iters_first) == (fresh.chi2_first, fresh.iters_first)
+    other = ba.run(p2, out=out)  # shapes differ: a new result
+    assert other is not out and other.points.shape == p2.points.shape
+    _compare(other, oracle.ba_local(p2), tol_pose=1e-6, tol_pt=1e-5, chi2_rtol=5e-8)
