@@ -1,20 +1,22 @@
 // Tracking pose optimisation, FrameOptimization (src/g2o_optimization/g2o_optimization.cc:256-398),
-// as a single-launch fp64 Levenberg-Marquardt on gfx950: ONE wavefront owns one frame for the
-// whole call -- 4 rounds x optimize(10) x trials -- so there is no host round trip, no grid
-// synchronisation and no LDS.  Each lane linearises a strided subset of the frame's unary edges;
-// the 6x6 normal equations (21 + 6 + chi2 values) are all-reduced across the wave with DPP
-// (quad swaps, half-row / row mirrors, then the four row results through readlane: a fixed tree,
-// and because IEEE addition is commutative every lane ends with the bitwise-same sums).  Every
-// lane then factors the same 6x6 system in registers, so the LM control (g2o
+// as a single-launch fp64 Levenberg-Marquardt on gfx950: ONE workgroup (4 wavefronts; 1 with
+// RSPL_FRAME_WAVES=1) owns one frame for the whole call -- 4 rounds x optimize(10) x trials -- so
+// there is no host round trip and no grid synchronisation.  Each thread linearises a strided subset
+// of the frame's unary edges; the 6x6 normal equations (21 + 6 + chi2 values) are all-reduced across
+// each wave with DPP (quad swaps, half-row / row mirrors, then the four row results through
+// readlane: a fixed tree, and because IEEE addition is commutative every lane ends with the
+// bitwise-same sums), then the waves' sums are added in wave order through LDS.  Every thread then
+// factors the same 6x6 system in registers, so the LM control (g2o
 // OptimizationAlgorithmLevenberg: tau 1e-5, good-step scale clamp [1/3, 2/3], ni doubling,
-// 10 trials, stop on qmax == 10 || rho == 0) is wave-uniform and needs no broadcast.
+// 10 trials, stop on qmax == 10 || rho == 0) is uniform and needs no broadcast.
 // Latency bound by construction (a few hundred edges per frame): throughput comes from batching
-// frames -- one wave each -- into one launch.  Same algorithm as the CPU restatement
+// frames -- one workgroup each -- into one launch.  Same algorithm as the CPU restatement
 // orc_frame_opt (oracle/ba.c).
 #include <hip/hip_runtime.h>
 
 #include <cfloat>
 #include <cstdint>
+#include <cstdlib>
 
 #include "frame_kernels.hpp"
 #include "se3_device.hpp"
@@ -76,6 +78,44 @@ struct View {
   double delta0, delta1;  // Huber deltas (mono, stereo): scalars, never indexed (no scratch)
 };
 
+// The frame's waves (NW = 1 or 4 per frame): a wave-reduced value (equal on every lane) combined
+// across the NW waves of the workgroup in wave order through LDS; every thread gets the same sum.
+template <int NW, int N>
+__device__ __forceinline__ void block_combine(double (&v)[N]) {
+  if constexpr (NW > 1) {
+    __shared__ double cb[NW][N];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < N; k++) cb[wv][k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      double t = cb[0][k];
+#pragma unroll
+      for (int w = 1; w < NW; w++) t += cb[w][k];
+      v[k] = t;
+    }
+    __syncthreads();  // cb is reused by the next combine
+  }
+}
+template <int NW>
+__device__ __forceinline__ int block_sum_int(int v) {
+  v = wsum_int(v);
+  if constexpr (NW > 1) {
+    __shared__ int ci[NW];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) ci[wv] = v;
+    __syncthreads();
+    int t = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) t += ci[w];
+    __syncthreads();
+    v = t;
+  }
+  return v;
+}
+
 // robust (Huber) or plain chi2 of an error, for the edge type
 __device__ __forceinline__ double cost_of(const View& V, const double* ev, bool stereo, bool robust) {
   const double c2 = chi2_of(ev);
@@ -88,11 +128,13 @@ __device__ __forceinline__ double cost_of(const View& V, const double* ev, bool 
 // computeActiveErrors + activeRobustChi2 over this lane's edges (errors stored), wave-reduced.
 // Two edges per lane in flight (loads of both issued before either is used): a lone wave per
 // frame has no other wave to hide the LDS / fp64-divide latency behind.
+template <int NW>
 __device__ __forceinline__ double active_chi2(const View& V, const Pose& P, int lane, bool robust) {
+  constexpr int T = 64 * NW;
   double s = 0;
-  for (int e = lane; e < V.n; e += 128) {
-    const int e1 = e + 64 < V.n ? e + 64 : e;
-    const bool a0 = !V.lev[e], a1 = e + 64 < V.n && !V.lev[e1];
+  for (int e = lane; e < V.n; e += 2 * T) {
+    const int e1 = e + T < V.n ? e + T : e;
+    const bool a0 = !V.lev[e], a1 = e + T < V.n && !V.lev[e1];
     const Edge E0 = V.E[e], E1 = V.E[e1];
     double Xc0[3], Xc1[3], ev0[3], ev1[3];
     edge_error(E0, P, Xc0, ev0);
@@ -110,17 +152,20 @@ __device__ __forceinline__ double active_chi2(const View& V, const Pose& P, int 
       s += c1;
     }
   }
-  return wsum(s);
+  double r[1] = {wsum(s)};
+  block_combine<NW>(r);
+  return r[0];
 }
 
 
 __device__ __forceinline__ int hidx(int i, int j) { return i * 6 - i * (i - 1) / 2 + (j - i); }
 
 // errors at T (stored) + robust chi2 + H / b (Huber IRLS weights), wave-reduced
+template <int NW>
 __device__ __forceinline__ void linearize(const View& V, const Pose& P, int lane, bool robust, double (&acc)[kNV]) {
 #pragma unroll
   for (int k = 0; k < kNV; k++) acc[k] = 0.0;
-  for (int e = lane; e < V.n; e += 64) {
+  for (int e = lane; e < V.n; e += 64 * NW) {
     if (V.lev[e]) continue;
     const Edge E = V.E[e];
     double Xc[3], ev[3];
@@ -165,7 +210,8 @@ __device__ __forceinline__ void linearize(const View& V, const Pose& P, int lane
       for (int j = i; j < 6; j++) acc[hidx(i, j)] += w * (J[0][i] * J[0][j] + J[1][i] * J[1][j] + J[2][i] * J[2][j]);
     }
   }
-  wave_allreduce28(acc, lane);
+  wave_allreduce28(acc, lane & 63);
+  block_combine<NW>(acc);
 }
 
 // (H + lambda I) x = b by Cholesky, in registers (every lane the same); false if not SPD.
@@ -213,13 +259,14 @@ __device__ __forceinline__ bool solve6(const double (&acc)[kNV], double lambda, 
 }
 
 // SparseOptimizer::optimize(iters) with OptimizationAlgorithmLevenberg on the pose vertex
+template <int NW>
 __device__ __forceinline__ int optimize_pose(const View& V, Pose& P, int lane, bool robust, int iters,
                                              double& chi2_out) {
   double acc[kNV];
   double lambda = 0, ni = 2, currentChi = 0;
   int done = 0;
   for (int it = 0; it < iters; it++) {
-    linearize(V, P, lane, robust, acc);
+    linearize<NW>(V, P, lane, robust, acc);
     currentChi = acc[27];
     if (it == 0) {  // computeLambdaInit: tau * max diagonal
       double mx = 0;
@@ -235,7 +282,7 @@ __device__ __forceinline__ int optimize_pose(const View& V, Pose& P, int lane, b
       const bool ok = solve6(acc, lambda, x);
       Pose C = P;
       if (ok) C.set(ba::se3_mul(ba::se3_exp(x), P.T));
-      double tempChi = active_chi2(V, C, lane, robust);
+      double tempChi = active_chi2<NW>(V, C, lane, robust);
       if (!ok) tempChi = DBL_MAX;
       rho = currentChi - tempChi;
       double scale = 1.0;
@@ -267,12 +314,14 @@ __device__ __forceinline__ int optimize_pose(const View& V, Pose& P, int lane, b
   return done;
 }
 
-// one wavefront per frame; LDS: the frame's edges + errors + flags staged once (kLdsEdges cap)
-template <bool LDS>
-__global__ __launch_bounds__(64) void frame_opt_kernel(Args a, int batch) {
+// NW wavefronts per frame (1 or 4; the control is uniform over the workgroup: every thread holds the
+// same sums); LDS: the frame's edges + errors + flags staged once (kLdsEdges cap)
+template <bool LDS, int NW>
+__global__ __launch_bounds__(64 * NW) void frame_opt_kernel(Args a, int batch) {
   extern __shared__ double smem[];
+  constexpr int T = 64 * NW;
   const int f = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x;  // the thread's index in the frame's workgroup
   const Desc D = a.frames[f];
   View V;
   V.n = D.n;
@@ -283,7 +332,7 @@ __global__ __launch_bounds__(64) void frame_opt_kernel(Args a, int batch) {
     Edge* Es = reinterpret_cast<Edge*>(smem);
     const double* src = reinterpret_cast<const double*>(a.edges + D.e0);
     double* dst = smem;
-    for (int k = lane; k < D.n * (int)(sizeof(Edge) / 8); k += 64) dst[k] = src[k];
+    for (int k = lane; k < D.n * (int)(sizeof(Edge) / 8); k += T) dst[k] = src[k];
     V.E = Es;
     V.err = smem + D.n * (sizeof(Edge) / 8);
     V.lev = reinterpret_cast<uint8_t*>(V.err + 3 * D.n);
@@ -294,11 +343,11 @@ __global__ __launch_bounds__(64) void frame_opt_kernel(Args a, int batch) {
     V.lev = a.level + D.e0;
     V.inl = a.inl + D.e0;
   }
-  for (int e = lane; e < D.n; e += 64) {
+  for (int e = lane; e < D.n; e += T) {
     V.inl[e] = a.inl_in[D.e0 + e];
     V.lev[e] = 0;
   }
-  __syncthreads();  // single-wave block: orders the LDS staging
+  __syncthreads();  // orders the LDS staging
   SE3 T0;
   for (int k = 0; k < 4; k++) T0.q[k] = D.T0[k];
   for (int k = 0; k < 3; k++) T0.t[k] = D.T0[4 + k];
@@ -314,11 +363,11 @@ __global__ __launch_bounds__(64) void frame_opt_kernel(Args a, int batch) {
     P.set(T0);  // setEstimate(SE3Quat(pose).inverse()) every round (:337)
     const bool robust = r < 3;  // setRobustKernel(0) after round 2's classification (:363)
     int act = 0;
-    for (int e = lane; e < D.n; e += 64) act += V.lev[e] == 0;
-    act = wsum_int(act);
+    for (int e = lane; e < D.n; e += T) act += V.lev[e] == 0;
+    act = block_sum_int<NW>(act);
     int its = 0;
     double chi = 0;
-    if (act) its = optimize_pose(V, P, lane, robust, 10, chi);
+    if (act) its = optimize_pose<NW>(V, P, lane, robust, 10, chi);
 #pragma unroll
     for (int k = 0; k < 4; k++)
       if (k == r) {
@@ -326,7 +375,8 @@ __global__ __launch_bounds__(64) void frame_opt_kernel(Args a, int batch) {
         c2r[k] = chi;
       }
     int no = 0;
-    for (int e = lane; e < D.n; e += 64) {
+    __syncthreads();  // every thread's last errors are stored before any thread classifies
+    for (int e = lane; e < D.n; e += T) {
       double* er = V.err + 3 * e;
       const Edge E = V.E[e];
       double ev[3];
@@ -346,11 +396,11 @@ __global__ __launch_bounds__(64) void frame_opt_kernel(Args a, int batch) {
         V.lev[e] = 0;
       }
     }
-    num_outlier = wsum_int(no);
+    num_outlier = block_sum_int<NW>(no);  // (its barriers also order the level writes before the next round)
     rounds = r + 1;
     if (D.n < 10) break;  // optimizer.edges().size() < 10 (:383)
   }
-  for (int e = lane; e < D.n; e += 64) a.inl_out[D.e0 + e] = V.inl[e];
+  for (int e = lane; e < D.n; e += T) a.inl_out[D.e0 + e] = V.inl[e];
   if (lane == 0) {
     Out* o = a.out + f;
 #pragma unroll
@@ -369,10 +419,19 @@ __global__ __launch_bounds__(64) void frame_opt_kernel(Args a, int batch) {
 
 size_t lds_bytes(int n) { return (size_t)n * (sizeof(Edge) + 3 * sizeof(double) + 2); }
 
+// waves per frame: 4 for latency (one frame per CU at 256 VGPRs) while the batch leaves CUs idle,
+// 1 for throughput (two frames per SIMD) on large batches; RSPL_FRAME_WAVES=1 / 4 forces one (A/B)
 hipError_t optimize(const Args& a, int batch, int max_n, hipStream_t s) {
   if (batch <= 0) return hipSuccess;
-  if (max_n <= kLdsEdges) frame_opt_kernel<true><<<batch, 64, lds_bytes(max_n), s>>>(a, batch);
-  else frame_opt_kernel<false><<<batch, 64, 0, s>>>(a, batch);
+  const char* w = getenv("RSPL_FRAME_WAVES");
+  const bool one = w ? atoi(w) == 1 : batch > 256;
+  if (max_n <= kLdsEdges) {
+    if (one) frame_opt_kernel<true, 1><<<batch, 64, lds_bytes(max_n), s>>>(a, batch);
+    else frame_opt_kernel<true, 4><<<batch, 256, lds_bytes(max_n), s>>>(a, batch);
+  } else {
+    if (one) frame_opt_kernel<false, 1><<<batch, 64, 0, s>>>(a, batch);
+    else frame_opt_kernel<false, 4><<<batch, 256, 0, s>>>(a, batch);
+  }
   return hipGetLastError();
 }
 
