@@ -320,6 +320,13 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
       rg = std::min(rg, std::max(1, ncu / s->B));
       while (rg <= 32 && rg * s->B <= ncu && !sg::sinkhorn_rb_rpw(s->nmax, rg)) rg++;
       if (rg * s->B <= ncu && sg::sinkhorn_rb_rpw(s->nmax, rg)) s->rbG = rg;
+      // 448 < nmax + 1 <= 640 (e.g. C4's 600 keypoints): the scaling-form kernel with ten column
+      // sets per lane, ceil(ld / 48) workgroups of <= 48 rows per pair
+      if (!s->rbG && s->sink_sc) {
+        int g = (s->ld + 47) / 48;
+        if (const char* e = getenv("RSPL_SG_SINK_G")) g = std::max(1, atoi(e));
+        if (g * s->B <= ncu && sg::sinkhorn_sc10_ok(s->nmax, g)) s->rbG = g;
+      }
     }
     if (s->B * s->G > ncu && !s->rbG) {
       set_error("max_batch (%d) exceeds the CU count (%d): the Sinkhorn workgroups must be co-resident", s->B, ncu);

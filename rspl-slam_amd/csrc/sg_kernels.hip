@@ -1608,13 +1608,13 @@ __device__ __forceinline__ void wave_barrier_lds() {
   __builtin_amdgcn_wave_barrier();
 }
 
-template <int RPW, int GM>
+template <int RPW, int GM, int Q>  // Q: 64-column lane sets (7: nmax + 1 <= 448, 10: <= 640)
 __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
-  __shared__ float ps[16][kRbQ * 64];   // per-wave column partial sums
-  __shared__ float vs[kRbQ * 64];       // merged V
+  __shared__ float ps[16][Q * 64];   // per-wave column partial sums
+  __shared__ float vs[Q * 64];       // merged V
   __shared__ int flag[4];               // 0: exchange timeout, 1: column absorb, 2 + (it & 1): row absorb
   __shared__ float as[16 * RPW];        // absorbed row potentials a (row wv + 16 k), read on absorption / at the end
-  __shared__ float bs[kRbQ * 64];       // absorbed column potentials b (identical on every workgroup)
+  __shared__ float bs[Q * 64];       // absorbed column potentials b (identical on every workgroup)
   const int p = blockIdx.y, g = blockIdx.x, G = gridDim.x;
   const int m = a.n0[p], n = a.n1[p];
   if (m <= 0 || n <= 0) return;
@@ -1624,12 +1624,12 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const float* Cg = a.cpl + (size_t)p * ld * ld;
   const int nk = min(RPW, max(0, (nr - wv + 15) / 16));  // the wave's rows inside the slab
-  float x[RPW][kRbQ];
+  float x[RPW][Q];
 #pragma unroll
   for (int k = 0; k < RPW; k++) {
     const int r = wv + 16 * k;
 #pragma unroll
-    for (int q = 0; q < kRbQ; q++) {
+    for (int q = 0; q < Q; q++) {
       const int j = lane + 64 * q;
       x[k][q] = (r < nr && j < Cc) ? Cg[(size_t)(r0 + r) * ld + j] : -INFINITY;
     }
@@ -1649,7 +1649,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
     for (int k = 0; k < RPW; k++) {
       mx[k] = x[k][0];
 #pragma unroll
-      for (int q = 1; q < kRbQ; q++) mx[k] = fmaxf(mx[k], x[k][q]);
+      for (int q = 1; q < Q; q++) mx[k] = fmaxf(mx[k], x[k][q]);
     }
 #pragma unroll
     for (int k = 0; k < RPW; k++) mx[k] = wave_max_dpp(mx[k]);
@@ -1658,7 +1658,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
       sm[k] = 0.f;
       if (k < nk)
 #pragma unroll
-        for (int q = 0; q < kRbQ; q++) sm[k] += sk_exp<true>(x[k][q] - mx[k]);
+        for (int q = 0; q < Q; q++) sm[k] += sk_exp<true>(x[k][q] - mx[k]);
     }
 #pragma unroll
     for (int k = 0; k < RPW; k++) sm[k] = wave_sum_dpp(sm[k]);
@@ -1669,9 +1669,9 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
       ur[k] = 1.f;
     }
   }
-  float vr[kRbQ];
+  float vr[Q];
 #pragma unroll
-  for (int q = 0; q < kRbQ; q++) {
+  for (int q = 0; q < Q; q++) {
     bs[lane + 64 * q] = 0.f;  // every wave writes the same zeros
     vr[q] = 1.f;
   }
@@ -1682,7 +1682,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
     for (int k = 0; k < RPW; k++) {
       const int r = wv + 16 * k;
 #pragma unroll
-      for (int q = 0; q < kRbQ; q++) {
+      for (int q = 0; q < Q; q++) {
         const int j = lane + 64 * q;
         const bool in = r < nr && j < Cc;
         const float c = reload ? (in ? Cg[(size_t)(r0 + r) * ld + j] : 0.f) : x[k][q];
@@ -1702,7 +1702,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
         sm[k] = 0.f;
         if (k < nk)
 #pragma unroll
-          for (int q = 0; q < kRbQ; q++) sm[k] = fmaf(x[k][q], vr[q], sm[k]);
+          for (int q = 0; q < Q; q++) sm[k] = fmaf(x[k][q], vr[q], sm[k]);
       }
 #pragma unroll
       for (int k = 0; k < RPW; k++) sm[k] = wave_sum_dpp(sm[k]);
@@ -1717,7 +1717,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
     }
     // column partials over the wave's rows, then over the 16 waves
 #pragma unroll
-    for (int q = 0; q < kRbQ; q++) {
+    for (int q = 0; q < Q; q++) {
       float cs = 0.f;
 #pragma unroll
       for (int k = 0; k < RPW; k++)
@@ -1729,8 +1729,9 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
     unsigned long long* slot = a.ug + (size_t)(p * 2 + (it & 1)) * G * ld;
     // two adjacent lanes per column: lane `half` sums waves 8 half .. 8 half + 7 and polls the
     // peers h with (h & 1) == half; both lanes form the same total (fp addition commutes)
-    if (tid < 2 * Cc) {
-      const int j = tid >> 1, half = tid & 1;
+    // (more than 512 columns: a second pass of the column pairs)
+    for (int tt = tid; tt < 2 * Cc; tt += kSinkThreads) {
+      const int j = tt >> 1, half = tt & 1;
       float S = 0.f;
 #pragma unroll
       for (int w = 0; w < 8; w++) S += ps[8 * half + w][j];
@@ -1781,7 +1782,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
     __syncthreads();
     if (flag[0]) { failed = true; break; }
 #pragma unroll
-    for (int q = 0; q < kRbQ; q++) {
+    for (int q = 0; q < Q; q++) {
       const int j = lane + 64 * q;
       vr[q] = j < Cc ? vs[j] : 1.f;
     }
@@ -1796,9 +1797,9 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
         }
       }
       if (col_abs) {
-        for (int j = tid; j < kRbQ * 64; j += kSinkThreads) bs[j] += logf(vs[j] > 0.f && j < Cc ? vs[j] : 1.f);
+        for (int j = tid; j < Q * 64; j += kSinkThreads) bs[j] += logf(vs[j] > 0.f && j < Cc ? vs[j] : 1.f);
 #pragma unroll
-        for (int q = 0; q < kRbQ; q++) vr[q] = 1.f;
+        for (int q = 0; q < Q; q++) vr[q] = 1.f;
       }
       __syncthreads();
       build_k(true);
@@ -1819,7 +1820,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
     if (r >= nr) continue;
     const float u = as[wv + 16 * k] + logf(ur[k]);
 #pragma unroll
-    for (int q = 0; q < kRbQ; q++) {
+    for (int q = 0; q < Q; q++) {
       const int j = lane + 64 * q;
       if (j < Cc) Z[(size_t)(r0 + r) * ld + j] = ((Cg[(size_t)(r0 + r) * ld + j] + u) + (bs[j] + logf(vr[q]))) - norm;
     }
@@ -2086,6 +2087,12 @@ size_t sinkhorn_lds_bytes(int nmax, int G, bool slabs) {
   return sizeof(float) * (2 * ldp + 4 + (slabs ? 2 * per * ld : 0));
 }
 
+// the scaling-form kernel at 448 < nmax + 1 <= 640 (Q = 10, three rows per wave): G <= 16 workgroups of <= 48 rows
+bool sinkhorn_sc10_ok(int nmax, int G) {
+  const int ld = nmax + 1;
+  return ld > kRbQ * 64 && ld <= 640 && G >= 1 && G <= 16 && (ld + G - 1) / G <= 48;
+}
+
 int sinkhorn_rb_rpw(int nmax, int G) {
   const int ld = nmax + 1, rs = (ld + G - 1) / G;
   if (ld > kRbQ * 64 || G < 1) return 0;
@@ -2099,11 +2106,16 @@ int sinkhorn_rb_rpw(int nmax, int G) {
 hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   if (a.G < 1 || a.G > 1024) return hipErrorInvalidValue;
   dim3 grid(a.G, B);
+  if (a.rb && a.sc && a.nmax + 1 > kRbQ * 64) {  // 448 < nmax + 1 <= 640: ten column sets per lane
+    if (!sinkhorn_sc10_ok(a.nmax, a.G)) return hipErrorInvalidValue;
+    hipExtLaunchKernelGGL((sinkhorn_sc_kernel<3, 16, 10>), grid, dim3(kSinkThreads), 0, s, t0, t1, 0, a);
+    return hipGetLastError();
+  }
   if (a.rb && a.sc) {  // scaling-form kernel: the workgroup count must match an instantiated (RPW, GM)
     switch (sinkhorn_rb_rpw(a.nmax, a.G)) {
 #define RSPL_SK_SC(R, M)                                                                                     \
   case R:                                                                                                    \
-    hipExtLaunchKernelGGL((sinkhorn_sc_kernel<R, M>), grid, dim3(kSinkThreads), 0, s, t0, t1, 0, a);         \
+    hipExtLaunchKernelGGL((sinkhorn_sc_kernel<R, M, kRbQ>), grid, dim3(kSinkThreads), 0, s, t0, t1, 0, a);   \
     break;
       RSPL_SK_SC(8, 4)
       RSPL_SK_SC(4, 8)

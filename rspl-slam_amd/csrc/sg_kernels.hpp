@@ -177,6 +177,8 @@ hipError_t decode(const DecodeArgs& a, int B, hipStream_t s);
 size_t sinkhorn_lds_bytes(int nmax, int G, bool slabs);
 // rows per wave of the row-block Sinkhorn for G workgroups per pair (0: not supported)
 int sinkhorn_rb_rpw(int nmax, int G);
+// the scaling-form kernel for 448 < nmax + 1 <= 640 (ten 64-column sets per lane) takes this G
+bool sinkhorn_sc10_ok(int nmax, int G);
 constexpr size_t kSinkLdsMax = 150 * 1024;  // slab budget per workgroup (160 KB LDS per CU)
 
 }  // namespace sg

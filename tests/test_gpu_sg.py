@@ -270,3 +270,21 @@ def test_sinkhorn_scaling_absorption(pkg, weight_blobs):
     assert ok, sg.error
     Zr = oracle.log_optimal_transport(S, 1.0, 100)
     np.testing.assert_allclose(Z, Zr, atol=2e-4 * max(1.0, np.abs(Zr).max() / 100), rtol=0)
+
+
+@pytest.mark.parametrize("G,scale", [(None, 1.0), (16, 1.0), (None, 30.0)])
+def test_sinkhorn_sc10_vs_oracle(pkg, weight_blobs, monkeypatch, G, scale):
+    """The scaling-form kernel's wide instantiation (448 < nmax + 1 <= 640: ten 64-column sets per
+    lane, <= 48 rows per workgroup, the column exchange in two passes above 512 columns) -- C4's
+    600 keypoints -- against the oracle's log-domain Sinkhorn (superglue.py:185-205) on a 600 x 570
+    score matrix; scale 30 forces scaling absorption.  Z at atol 1e-4 (scaled with |Z| as above)."""
+    if G:
+        monkeypatch.setenv("RSPL_SG_SINK_G", str(G))
+    rng = np.random.default_rng(11)
+    S = (rng.normal(size=(600, 570)) * scale).astype(np.float32)
+    sg = _sg(pkg, weight_blobs[1], nmax=600)
+    ok, Z = sg.debug_sinkhorn(S, 1.0, 100)
+    assert ok, sg.error
+    Zr = oracle.log_optimal_transport(S, 1.0, 100)
+    print(f"sc10 G={G} scale={scale}: max |dZ| {np.abs(Z - Zr).max():.3g}")
+    np.testing.assert_allclose(Z, Zr, atol=1e-4 * max(1.0, 2 * np.abs(Zr).max() / 100), rtol=0)
