@@ -308,7 +308,7 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
     G = std::min(G, std::max(1, ncu / s->B));
     s->G = G;
     s->sink_scratch = sg::sinkhorn_lds_bytes(s->nmax, G, true) > sg::kSinkLdsMax;
-    // nmax + 1 <= 448: rows in registers, one exchange per iteration -- the scaling-form kernel
+    // nmax + 1 <= 448 (640 for the scaling form): rows in registers, one exchange per iteration -- the scaling-form kernel
     // (default, 8 workgroups per pair) or the log-domain row-block kernel (RSPL_SG_SINK=rb, 16);
     // RSPL_SG_SINK=slab keeps the slab kernel; RSPL_SG_SINK_G sets the workgroups per pair
     const char* sk = getenv("RSPL_SG_SINK");

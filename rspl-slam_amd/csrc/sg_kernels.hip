@@ -1587,7 +1587,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Scaling-form Sinkhorn (the default for nmax + 1 <= 448): the same iterations as
+// Scaling-form Sinkhorn (the default for nmax + 1 <= 640): the same iterations as
 // log_sinkhorn_iterations (superglue.py:176-183) written on the scalings U = exp(u - a),
 // V = exp(v - b) of absorbed log potentials a, b (stabilised Sinkhorn):
 //   K_ij = exp(C_ij + a_i + b_j)  (registers),   U_i = mu_i / sum_j K_ij V_j,
