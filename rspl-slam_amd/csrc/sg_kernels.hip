@@ -1729,15 +1729,31 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
     unsigned long long* slot = a.ug + (size_t)(p * 2 + (it & 1)) * G * ld;
     // two adjacent lanes per column: lane `half` sums waves 8 half .. 8 half + 7 and polls the
     // peers h with (h & 1) == half; both lanes form the same total (fp addition commutes)
-    // (more than 512 columns: a second pass of the column pairs)
-    for (int tt = tid; tt < 2 * Cc; tt += kSinkThreads) {
-      const int j = tt >> 1, half = tt & 1;
-      float S = 0.f;
+    // (more than 512 columns: every thread holds two column halves; both are published before
+    // either is polled, so the exchange stays one round trip)
+    constexpr int NP = (Q * 128 + kSinkThreads - 1) / kSinkThreads;
+    float own2[NP];
 #pragma unroll
-      for (int w = 0; w < 8; w++) S += ps[8 * half + w][j];
-      const float own = S + __shfl_xor(S, 1);
-      if (!half)
-        __hip_atomic_store(slot + (size_t)g * ld + j, sk_granule(own, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int u = 0; u < NP; u++) {
+      const int tt = tid + u * kSinkThreads;
+      own2[u] = 0.f;
+      if (tt < 2 * Cc) {
+        const int j = tt >> 1, half = tt & 1;
+        float S = 0.f;
+#pragma unroll
+        for (int w = 0; w < 8; w++) S += ps[8 * half + w][j];
+        own2[u] = S + __shfl_xor(S, 1);
+        if (!half)
+          __hip_atomic_store(slot + (size_t)g * ld + j, sk_granule(own2[u], tag), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < NP; u++) {
+      const int tt = tid + u * kSinkThreads;
+      if (tt >= 2 * Cc) continue;
+      const int j = tt >> 1, half = tt & 1;
+      const float own = own2[u];
       constexpr int GH = GM / 2;
       float l[GH];
       unsigned long long gv[GH];
