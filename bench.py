@@ -8,8 +8,8 @@ step is one stereo keyframe of a synthetic EuRoC-shaped stream:
   * the line part of the stereo keyframe (Frame::AddRightFeatures, src/frame.cc:150-203): both
     images' AssignPointsToLines, the stereo-match disparity filter and MatchLines on the GPU
     (rspl_lines_stereo_device), fed by SuperPoint's device features and SuperGlue's device match
-    index of the left(t)-right(t) pair; the ~80 segments per image come from the host merge passes
-    (LineDetector after FLD, which runs on the reference's own line thread and is not rebuilt),
+    index of the left(t)-right(t) pair, on each image's line segments (LineExtractor's merge passes
+    over FLD segments; the restated FLD detector is rspl_lines_detect),
   * one local BA (LocalmapOptimization) of a C3-sized problem: 10 keyframes (1 fixed),
     ~4k points / ~10^4 point observations, 100 lines (synthetic, with ground truth).
 Inputs (images) are resident in HBM before timing.  BA is host-driven and runs on its own
@@ -164,10 +164,57 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
         ms = t.get(key)
         if ms:
             ach = work / ms if unit == "TFLOP/s" else work / ms * 1e3
+            nl = 19 if key == "sg:gnn x18" and precision == "fp16" else 1  # launches per step of the kernel
             out[key] = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
-                        "frac": round(ach / peak, 4), "ms": round(ms, 4), "avg_launch_ms": round(ms, 4),
-                        "algorithmic": f"{work:.4g} {what}", "pmc_kernel": kern, "single_kernel": single}
+                        "frac": round(ach / peak, 4), "ms": round(ms, 4), "avg_launch_ms": round(ms / nl, 5),
+                        "launches_per_step": nl, "algorithmic": f"{work:.4g} {what}", "pmc_kernel": kern,
+                        "single_kernel": single or nl > 1}
+    if "sg:sinkhorn" in out:  # against the compulsory bytes too: couplings in + Z out, 2 pairs
+        comp = 2 * 2 * 4 * (N + 1) * (M + 1) / 1e9
+        r = out["sg:sinkhorn"]
+        r["compulsory"] = {"GB_per_launch": round(comp, 5), "achieved": round(comp / r["ms"] * 1e3, 2),
+                           "frac": round(comp / r["ms"] * 1e3 / HBM_PEAK_GBS, 5),
+                           "note": "couplings read + Z written once; the streamed model above is what a "
+                                   "non-resident kernel would move (the register-resident kernel does not)"}
     return out
+
+
+def ba_kernel_rows(prob, kt, timed_calls):
+    """Roofline rows of the local BA's two per-trial launches from their HIP-event times on the BA stream
+    (LocalBA.kernel_times over the sampled calls of the timed region).  Algorithmic bytes per launch =
+    the records the launch must read once plus what it writes:
+      Schur chunks + fused solve: per edge of an optimised pose Hpl (6 x ld) + Hpp (21) + bp (6), per
+        landmark Hll (ld x ld) + bl (ld), doubles; the 48-double sums of each pose pair written, the
+        reduced system read back by the solver and the 6K solution written;
+      update: per edge the observation (2 / 3 / 4 / 8 doubles), its ids (16 B) and Hpl (6 x ld), the
+        error (4) and robust cost written, the speculative records (Hpp 21 + bp 6 + Hpl 6 x ld) written;
+        per landmark its state read and written and Hll / bl read and written."""
+    names = ("mono", "stereo", "mono_line", "stereo_line")
+    ne = {n: prob.n_edges(n) for n in names}
+    npt, nln = len(prob.points), len(prob.lines)
+    Kp = int((prob.pose_fixed == 0).sum())
+    ld = {"mono": 3, "stereo": 3, "mono_line": 4, "stereo_line": 4}
+    dobs = {"mono": 2, "stereo": 3, "mono_line": 4, "stereo_line": 8}
+    rec = sum(ne[n] * (6 * ld[n] + 21 + 6) for n in names)
+    lmk = npt * (9 + 3) + nln * (16 + 4)
+    npairs = Kp * (Kp + 1) // 2
+    chunk_b = 8 * (rec + lmk + npairs * 48 * 2 + 6 * Kp)
+    upd_b = sum(ne[n] * (8 * (dobs[n] + 6 * ld[n] + 4 + 1 + 21 + 6 + 6 * ld[n]) + 16) for n in names) + \
+        8 * (2 * (3 * npt + 6 * nln) + npt * (9 + 3) * 2 + nln * (16 + 4) * 2)
+    rows = {}
+    for key, (ms, n), b, kern, what in (
+            ("ba:schur chunks+solve", kt["chunks+solve"], chunk_b, "pair_chunk_kernel",
+             "records read once (Hpl, Hpp, bp per edge; Hll, bl per landmark) + pose-pair sums + solve I/O"),
+            ("ba:update", kt["update"], upd_b, "update_errors_kernel",
+             "observations, ids and Hpl read; errors, costs and the speculative records written")):
+        if n:
+            avg = ms / n
+            rows[key] = {"bound": "hbm", "achieved": round(b / avg * 1e-6, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                         "frac": round(b / avg * 1e-6 / HBM_PEAK_GBS, 5), "avg_launch_ms": round(avg, 5),
+                         "ms": round(avg * n / max(1, timed_calls), 4), "launches_per_call": round(n / max(1, timed_calls), 2),
+                         "algorithmic": f"{b / 1e6:.4g} MB per launch: {what}", "pmc_kernel": kern,
+                         "single_kernel": True}
+    return rows
 
 
 def ate_report(ba):
@@ -292,6 +339,8 @@ def main():
     ap.add_argument("--ba-own-cus", type=int, default=int(os.environ.get("RSPL_BA_OWN_CUS", "1")),
                     help="1: the BA runs only on the reserved CUs (disjoint from SP/SG)")
     ap.add_argument("--skip", default="", help="diagnostics only: comma list of stages to leave out (sp,sg,ba)")
+    ap.add_argument("--ba-ktime-every", type=int, default=4,
+                    help="HIP-event timing of the BA's two per-trial launches on every N-th call (0: off)")
     ap.add_argument("--single-precision", action="store_true",
                     help="skip the second (other-precision) measurement")
     args = ap.parse_args()
@@ -429,6 +478,7 @@ def main():
 
         worker = threading.Thread(target=tracking_thread, daemon=True)
         worker.start()
+        ktime_every = args.ba_ktime_every  # HIP-event timing of the BA's launches (every N-th call)
         line_timers = []  # HIP-event timers around the line association (post stream), timed steps only
 
         def ba_item(i):
@@ -498,6 +548,8 @@ def main():
         ba_iters.clear()
         line_timers[:] = [capi.Timer() for _ in range(args.steps)]
         line_t0 = args.warmup
+        ba.kernel_timing(ktime_every)
+        ba.kernel_times()  # reset
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(args.warmup + i)
@@ -506,6 +558,9 @@ def main():
         elapsed = job_time(time.perf_counter() - t0, dist)
         ba_q.put(None)
         worker.join()
+        ba_kt = ba.kernel_times()
+        ba.kernel_timing(0)
+        ba_calls = len(ba_ms) * (world if shard else 1)
         if ba_err:
             raise ba_err[0]
         ok, mask = sg.status()  # Sinkhorn exchange health of every call in the timed region
@@ -522,7 +577,8 @@ def main():
         sg_ms, sg_calls = sg.stage_times()
         value = job_value(world, args.steps, elapsed)
         return {"value": value, "elapsed": elapsed, "sp": (sp_ms, sp_calls), "sg": (sg_ms, sg_calls),
-                "stages": (sp, sg), "ba_ms": list(ba_ms), "ba_iters": list(ba_iters), "lines_ms": lines_ms}
+                "stages": (sp, sg), "ba_ms": list(ba_ms), "ba_iters": list(ba_iters), "lines_ms": lines_ms,
+                "ba_kt": ba_kt, "ba_timed_calls": (ba_calls + ktime_every - 1) // ktime_every if ktime_every else 0}
 
     res = measure(args.precision)
     other = measure(precs[1]) if len(precs) > 1 else None  # the other precision, same run, for the record
@@ -533,9 +589,13 @@ def main():
     if rank != 0:
         return
     stages = stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, args.precision)
-    # the dominant single kernel by device time per step
+    if not shard:
+        stages.update(ba_kernel_rows(problems[0], res["ba_kt"], res["ba_timed_calls"]))
+    # the step-setting kernel: the largest device time per step over every timed kernel, the BA's
+    # launches included (its launches per call x one call per step)
     dom_key = max((k for k in stages if stages[k]["single_kernel"]), key=lambda k: stages[k]["ms"])
-    dom = {k: v for k, v in stages[dom_key].items() if k not in ("single_kernel", "ms")}
+    dom = {k: v for k, v in stages[dom_key].items() if k not in ("single_kernel",)}
+    dom["ms_per_step"] = dom.pop("ms")
     traffic, traffic_src = pmc_traffic(dom["pmc_kernel"])
     dom["traffic"] = round(traffic) if traffic else None
     dom["traffic_note"] = (f"HBM bytes per launch, rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE, profiles/{traffic_src}"

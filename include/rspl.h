@@ -45,6 +45,11 @@ enum { RSPL_PREC_FP32 = 0, RSPL_PREC_FP16 = 1 };
 
 const char* rspl_last_error(void);
 const char* rspl_version(void);
+/* ABI revision of the structs in this header; a consumer checks rspl_abi_version() ==
+ * RSPL_ABI_VERSION at startup (the library writes caller-allocated structs such as
+ * rspl_map_report at the size of ITS header).  2: rspl_map_report gained the stage times. */
+#define RSPL_ABI_VERSION 2
+int rspl_abi_version(void);
 
 /* ------------------------------------------------------------------------ */
 /* Runtime helpers (system ROCm HIP runtime).  Callers that share a process  */
@@ -305,6 +310,12 @@ void rspl_ba_destroy(rspl_ba* ba);
 /* Run this handle's kernels only on the reserve_cus CUs that rspl_stream_create_reserving
  * streams leave free (0 = all CUs, highest stream priority: the default). */
 int rspl_ba_use_reserved_cus(rspl_ba* ba, int reserve_cus);
+/* Kernel timing (measurement): every `every`-th rspl_ba_local call (0: off) records HIP events on the
+ * BA stream around each LM trial's two launches (device LM path); rspl_ba_kernel_times returns and
+ * resets the totals -- ms[0] / launches[0]: Schur chunks + fused reduced-system solve, ms[1] /
+ * launches[1]: update + cost + speculative linearisation -- over the trials that did work. */
+int rspl_ba_kernel_timing(rspl_ba* ba, int every);
+int rspl_ba_kernel_times(rspl_ba* ba, double* ms, long long* launches);
 
 /* ------------------------------------------------------------------------ */
 /* Landmark-sharded local BA: nranks handles -- one per  */
@@ -396,7 +407,9 @@ typedef struct {
 typedef struct rspl_frame rspl_frame;
 
 int rspl_frame_create(const rspl_frame_config* cfg, rspl_frame** out);
-/* batch independent FrameOptimization calls; results[b] receives frame b */
+/* batch independent FrameOptimization calls; results[b] receives frame b.  Batches of more than 256
+ * frames sum each frame's normal equations in another order (one wave per frame instead of four):
+ * results then differ from a small batch's in the last bits, within the oracle tolerances. */
 int rspl_frame_optimize(rspl_frame* h, const rspl_frame_problem* problems, int batch, rspl_frame_result* results);
 void rspl_frame_destroy(rspl_frame* h);
 

@@ -130,10 +130,19 @@ def frame_opt(problem):
     return res
 
 
-def pnp(K4, pts3, pts2, iterations=100, reproj_err=20.0, confidence=0.99):
+def _pnp_solver(L, independent):
+    L.orc_pnp_set_solver.argtypes = [C.c_int]
+    L.orc_pnp_set_solver.restype = None
+    L.orc_pnp_set_solver(1 if independent else 0)
+
+
+def pnp(K4, pts3, pts2, iterations=100, reproj_err=20.0, confidence=0.99, independent=False):
     """SolvePnPWithCV restatement (oracle/pnp.c): returns (n_inliers, Rwc [3,3], twc [3],
-    inlier mask [n] uint8, hypotheses evaluated)."""
+    inlier mask [n] uint8, hypotheses evaluated).  independent: EPnP's M^T M eigenvectors by the
+    classic cyclic Jacobi (an independent restatement) instead of the GPU kernel's round-robin
+    order (its CPU mirror, the default: per-hypothesis bit parity)."""
     L = lib()
+    _pnp_solver(L, independent)
     f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
     u8p = np.ctypeslib.ndpointer(np.uint8, flags="C_CONTIGUOUS")
     L.orc_pnp.argtypes = [f64p, C.c_int, f64p, f64p, C.c_int, C.c_double, C.c_double, f64p, f64p, u8p,
@@ -147,13 +156,15 @@ def pnp(K4, pts3, pts2, iterations=100, reproj_err=20.0, confidence=0.99):
     used = C.c_int(0)
     k = L.orc_pnp(np.ascontiguousarray(K4, np.float64), n, p3 if n else np.zeros(3), p2 if n else np.zeros(2),
                   iterations, reproj_err, confidence, R, t, inl, C.byref(used))
+    _pnp_solver(L, False)
     return k, R.reshape(3, 3), t, inl[:n], used.value
 
 
 def pnp_hypotheses(K4, pts3, pts2, iterations=100, reproj_err=20.0):
     """every RANSAC hypothesis of oracle/pnp.c: (counts [iters] int32, -1 = solver failed;
-    poses [iters, 12] = R row-major | t)"""
+    poses [iters, 12] = R row-major | t), with the GPU kernel's eigen solver order (its CPU mirror)"""
     L = lib()
+    _pnp_solver(L, False)
     f64p = np.ctypeslib.ndpointer(np.float64, flags="C_CONTIGUOUS")
     L.orc_pnp_hypotheses.argtypes = [f64p, C.c_int, f64p, f64p, C.c_int, C.c_double,
                                      np.ctypeslib.ndpointer(np.int32, flags="C_CONTIGUOUS"), f64p]

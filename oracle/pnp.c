@@ -22,8 +22,11 @@
  * cv::Point2f (:425-426).
  */
 /* no FMA contraction (the GPU kernel's rule, pnp_kernels.hip): EPnP's 5-point null space is
-   degenerate, and the basis the Jacobi leaves in it follows every rounding difference */
-#pragma GCC optimize("fp-contract=off")
+   degenerate, and the basis the Jacobi leaves in it follows every rounding difference.  The
+   Makefile builds with -ffp-contract=off (gcc does not implement the standard pragma; clang does). */
+#if defined(__clang__)
+#pragma STDC FP_CONTRACT OFF
+#endif
 #include <float.h>
 #include <math.h>
 
@@ -468,6 +471,12 @@ static double epnp_R_t(epnp_t* E, const double* ut, const double* be, double R[9
   return s2 / E->n;
 }
 
+/* The eigen solver of M^T M: 0 = the GPU kernel's round-robin order (jacobi12_rounds, the GPU's CPU
+   mirror: per-hypothesis bit parity), 1 = the classic cyclic Jacobi (jacobi_eig: an independent
+   restatement, used by the RANSAC-level parity test -- hypotheses may then differ in the degenerate
+   5-point null space, the RANSAC outcome on clean inliers may not). */
+static int g_eig_indep = 0;
+
 /* EPnP on n <= 8 correspondences; returns 0 and R (row-major), t on success */
 static int epnp(const double* K4, int n, const double* pw, const double* uv, double R[9], double t[3]) {
   epnp_t E;
@@ -490,7 +499,8 @@ static int epnp(const double* K4, int n, const double* pw, const double* uv, dou
       for (int b = 0; b < 12; b++) MtM[a * 12 + b] += M1[a] * M1[b] + M2[a] * M2[b];
   }
   double d[12], ut[144];
-  jacobi12_rounds(MtM, d, ut);
+  if (g_eig_indep) jacobi_eig(12, MtM, d, ut);
+  else jacobi12_rounds(MtM, d, ut);
   double L[60], rho[6];
   epnp_L(ut, L);
   rho[0] = dist2(E.cws[0], E.cws[1]); rho[1] = dist2(E.cws[0], E.cws[2]); rho[2] = dist2(E.cws[0], E.cws[3]);
@@ -616,6 +626,9 @@ static void refine(const double* K4, int n, const double* pw, const double* uv, 
     if (!accepted) return;
   }
 }
+
+/* the eigen solver for the following orc_pnp / orc_pnp_hypotheses calls (see g_eig_indep) */
+void orc_pnp_set_solver(int independent) { g_eig_indep = independent != 0; }
 
 /* returns the inlier count (0: fewer than 8 correspondences or no model); Twc out */
 int orc_pnp(const double* K4, int n, const double* pts3, const double* pts2, int iterations, double reproj_err,

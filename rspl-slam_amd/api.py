@@ -270,6 +270,16 @@ class LocalBA:
         res.read_back(R)
         return res
 
+    def kernel_timing(self, every: int):
+        """HIP-event timing of the LM trials' two launches on every `every`-th call (0: off)."""
+        capi.check(self._lib.rspl_ba_kernel_timing(self._h, every), "rspl_ba_kernel_timing")
+
+    def kernel_times(self):
+        """{"chunks+solve": (total ms, launches), "update": (total ms, launches)} since the last read."""
+        ms, n = (C.c_double * 2)(), (C.c_longlong * 2)()
+        capi.check(self._lib.rspl_ba_kernel_times(self._h, ms, n), "rspl_ba_kernel_times")
+        return {"chunks+solve": (ms[0], n[0]), "update": (ms[1], n[1])}
+
     def use_reserved_cus(self, reserve_cus: int):
         """Confine this handle's kernels to the CUs reserving streams leave free (0 = all CUs)."""
         capi.check(self._lib.rspl_ba_use_reserved_cus(self._h, reserve_cus), "rspl_ba_use_reserved_cus")

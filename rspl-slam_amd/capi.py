@@ -14,11 +14,12 @@ PKG = pathlib.Path(__file__).resolve().parent
 LIB_PATH = PKG / os.environ.get("RSPL_LIB", "librspl.so")
 
 RSPL_OK = 0
+RSPL_ABI_VERSION = 2  # include/rspl.h: the struct layouts the ctypes mirrors below follow
 RSPL_PREC_FP32 = 0
 RSPL_PREC_FP16 = 1
 
 EXPORTS = [
-    "rspl_last_error", "rspl_version",
+    "rspl_last_error", "rspl_version", "rspl_abi_version",
     "rspl_device_count", "rspl_set_device", "rspl_malloc", "rspl_free", "rspl_memcpy_h2d", "rspl_memcpy_d2h",
     "rspl_memset", "rspl_memcpy_d2d", "rspl_stream_create", "rspl_stream_create_priority", "rspl_stream_create_reserving", "rspl_stream_destroy", "rspl_stream_synchronize",
     "rspl_device_synchronize", "rspl_event_create", "rspl_event_record", "rspl_stream_wait_event",
@@ -30,7 +31,8 @@ EXPORTS = [
     "rspl_sg_status", "rspl_sg_debug_inject", "rspl_sg_debug_sinkhorn", "rspl_sg_debug_decode",
     "rspl_sg_stage_times", "rspl_sg_destroy",
     "rspl_pm_match",
-    "rspl_ba_create", "rspl_ba_local", "rspl_ba_destroy", "rspl_ba_use_reserved_cus",
+    "rspl_ba_create", "rspl_ba_local", "rspl_ba_destroy", "rspl_ba_use_reserved_cus", "rspl_ba_kernel_timing",
+    "rspl_ba_kernel_times",
     "rspl_frame_create", "rspl_frame_optimize", "rspl_frame_destroy",
     "rspl_ba_set_shard", "rspl_comm_unique_id", "rspl_comm_create", "rspl_comm_allreduce_sum", "rspl_comm_destroy",
     "rspl_ba_set_comm", "rspl_group_create", "rspl_group_destroy", "rspl_ba_set_group",
@@ -99,6 +101,8 @@ def load(path: pathlib.Path = LIB_PATH):
     vp, ip, dp = C.c_void_p, C.c_int, C.c_double
     lib.rspl_last_error.restype = C.c_char_p
     lib.rspl_version.restype = C.c_char_p
+    if lib.rspl_abi_version() != RSPL_ABI_VERSION:
+        raise RsplError(f"{path}: ABI {lib.rspl_abi_version()}, these bindings follow ABI {RSPL_ABI_VERSION}: rebuild")
     lib.rspl_sp_create.argtypes = [C.POINTER(SpConfig), C.c_char_p, C.POINTER(vp)]
     lib.rspl_sp_infer.argtypes = [vp, vp, ip, ip, ip, vp, ip, C.POINTER(ip)]
     lib.rspl_sp_infer_device.argtypes = [vp, vp, ip, ip, ip, ip, C.c_size_t, vp, ip, vp, vp]
@@ -149,6 +153,8 @@ def load(path: pathlib.Path = LIB_PATH):
         lib.rspl_ba_create.argtypes = [C.POINTER(BaConfig), C.POINTER(vp)]
         lib.rspl_ba_local.argtypes = [vp, vp, vp]
         lib.rspl_ba_use_reserved_cus.argtypes = [vp, ip]
+        lib.rspl_ba_kernel_timing.argtypes = [vp, ip]
+        lib.rspl_ba_kernel_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_longlong)]
         lib.rspl_ba_destroy.argtypes = [vp]
         lib.rspl_ba_destroy.restype = None
     if hasattr(lib, "rspl_ba_set_shard"):

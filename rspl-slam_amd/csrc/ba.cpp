@@ -44,7 +44,7 @@ struct rspl_ba {
   double *Hll, *bl, *bp, *S, *x, *partial, *partial2;
   unsigned* lm_ctr;  // [max_lines] line-landmark tickets (zeroed at create, re-armed by the kernel)
   unsigned long long* prof = nullptr;  // RSPL_BA_PROF: timing trace of one trial per call
-  int prof_nb[3] = {0, 0, 0};          // its pair_chunk / update_errors grid sizes, group blocks
+  int prof_nb[5] = {0, 0, 0, 0, 0};    // its pair_chunk / update_errors grid sizes, group blocks, nchk, K
   // landmark CSR (filled on the device) and the Schur chunk / pose-pair sums
   double *chunk, *pairfin;
   unsigned* pair_ctr;  // [npairs] chunk tickets (zeroed at create, re-armed by the kernel)
@@ -76,6 +76,17 @@ struct rspl_ba {
   size_t gcap = 0;
   double* pdg = nullptr;       // per-block pose-diagonal partials of the first pass (grown on demand)
   size_t pdg_cap = 0;
+  // kernel timing (rspl_ba_kernel_timing): HIP events around each device-LM trial's two launches on
+  // the BA stream, every ktime_every-th call; totals per launch kind (0: Schur chunks + fused solve,
+  // 1: update + speculative linearisation) over the trials that did work
+  int ktime_every = 0;
+  unsigned long long ncalls = 0;
+  bool ktime_on = false;
+  std::vector<hipEvent_t> kev;  // 3 per trial
+  std::vector<int> kev_eval;    // event-triple indices of the trials that did work (this call)
+  int kev_used = 0;
+  double kt_ms[2] = {0, 0};
+  long long kt_n[2] = {0, 0};
 };
 
 namespace {
@@ -269,6 +280,25 @@ void report_prof(rspl_ba* b) {
           us(u0, last(ba::kProfUe, 0, nbu, 2)), us(u0, last(ba::kProfUe, 0, nbu, 3)),
           us(u0, last(ba::kProfUe, nbu, nue, 1)), us(u0, last(ba::kProfUe, nbu, nue, 2)),
           us(u0, last(ba::kProfUe, nbu, nue, 3)), us(h[1], h[5]), us(h[5], h[6]), us(h[6], h[7]), us(h[7], h[8]));
+  {  // per chunk: start -> loop done, quantiles over the diagonal / off-diagonal pose pairs' chunks
+    const int nchk = b->prof_nb[3], K = b->prof_nb[4];
+    std::vector<double> dg, od;
+    for (int c = 0; c < std::min(npc, 4096) && nchk > 0; c++) {
+      const unsigned long long t0 = h[ba::kProfPc + 4 * c], t1 = h[ba::kProfPc + 4 * c + 1];
+      if (!t0 || !t1) continue;
+      int pr = c / nchk, a = 0, base = 0;
+      while (pr >= base + (K - a)) base += K - a++;
+      ((pr - base == 0) ? dg : od).push_back(((double)t1 - (double)t0) / 100.0);
+    }
+    auto q = [](std::vector<double>& v, double f) {
+      if (v.empty()) return -1.0;
+      std::sort(v.begin(), v.end());
+      return v[std::min(v.size() - 1, (size_t)(f * v.size()))];
+    };
+    fprintf(stderr, "ba_chunks us: diag50 %.1f diag90 %.1f diagmax %.1f off50 %.1f off90 %.1f offmax %.1f "
+            "ndiag %zu noff %zu\n", q(dg, 0.5), q(dg, 0.9), q(dg, 1.0), q(od, 0.5), q(od, 0.9), q(od, 1.0),
+            dg.size(), od.size());
+  }
   if (getenv("RSPL_BA_SOLVE") && std::string(getenv("RSPL_BA_SOLVE")) == "blk4") {
     fprintf(stderr, "ba_steps us:");  // blocked solve: each pose block's panel, from the assembly's end
     for (int k = 5; k < 15 && h[k]; k++) fprintf(stderr, " %.2f", us(h[1], h[k]));
@@ -343,6 +373,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
   ba::Sys Ss = S;
   Ss.Hll = b->Hll_s; Ss.bl = b->bl_s;
   int queued = 0;
+  const int kev0 = b->kev_used;  // this optimize's first event triple
   auto enqueue = [&](int n) -> int {
     for (int k = 0; k < n; k++, queued++) {
       q = ++b->seq;
@@ -353,10 +384,23 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
         b->prof_nb[0] = A.npairs * A.nchk;
         b->prof_nb[1] = ba::update_errors_blocks(A) + A.n_lblk;
         b->prof_nb[2] = ba::update_errors_blocks(A);
+        b->prof_nb[3] = A.nchk;
+        b->prof_nb[4] = A.K;
       }
       S.lm_slot = queued & 1;
       S.lm_post = k == n - 1;
-      const hipError_t e = ba::trial_dev(P, Lr, A, S, q, st, sp);
+      hipEvent_t* ev = nullptr;
+      if (b->ktime_on) {
+        if ((size_t)3 * (b->kev_used + 1) > b->kev.size()) {
+          for (int i = 0; i < 3; i++) {
+            hipEvent_t e;
+            RSPL_HIP(hipEventCreate(&e));
+            b->kev.push_back(e);
+          }
+        }
+        ev = &b->kev[3 * (size_t)b->kev_used++];
+      }
+      const hipError_t e = ba::trial_dev(P, Lr, A, S, q, st, sp, ev);
       S.prof = nullptr;
       if (e != hipSuccess) {
         set_error("BA trial launch failed: %s", hipGetErrorString(e));
@@ -399,7 +443,13 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
       }
       _mm_pause();
     }
-    if (v[3] != 0.0) break;
+    if (v[3] != 0.0) {
+      if (b->ktime_on) {  // the trials up to the stopping one did work (later ones are no-ops)
+        unsigned long long s1 = __atomic_load_n(&b->mail->seq, __ATOMIC_ACQUIRE);
+        for (unsigned long long t = q_first; t <= s1 && t <= q_last; t++) b->kev_eval.push_back(kev0 + (int)(t - q_first));
+      }
+      break;
+    }
     // rejected trials left iterations to do: queue one trial per remaining iteration
     if ((rc = enqueue(std::max(1, iters - (int)v[1])))) return rc;
   }
@@ -603,6 +653,8 @@ extern "C" int rspl_ba_set_shard(rspl_ba* b, int rank, int nranks, rspl_allreduc
 }
 
 extern "C" void rspl_ba_destroy(rspl_ba* b) {
+  if (b)
+    for (hipEvent_t e : b->kev) (void)hipEventDestroy(e);
   if (!b) return;
   if (b->stream) (void)hipStreamSynchronize(b->stream);
   if (b->gbuf) (void)hipFree(b->gbuf);
@@ -626,7 +678,30 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res);
 // (the next call restages the mapped buffers the old chain reads) and re-arm the cross-call
 // tickets and release flags the chain may have left half-counted.  If the drain itself fails the
 // device is gone and the handle must be recreated (the error says so).
+extern "C" int rspl_ba_kernel_timing(rspl_ba* b, int every) {
+  RSPL_CHECK_ARG(b && every >= 0, "rspl_ba_kernel_timing: NULL handle or every < 0");
+  b->ktime_every = every;
+  b->ncalls = 0;
+  return RSPL_OK;
+}
+
+extern "C" int rspl_ba_kernel_times(rspl_ba* b, double* ms, long long* launches) {
+  RSPL_CHECK_ARG(b && ms && launches, "rspl_ba_kernel_times: NULL argument");
+  for (int i = 0; i < 2; i++) {
+    ms[i] = b->kt_ms[i];
+    launches[i] = b->kt_n[i];
+    b->kt_ms[i] = 0;
+    b->kt_n[i] = 0;
+  }
+  return RSPL_OK;
+}
+
 extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
+  if (b) {
+    b->ktime_on = b->ktime_every > 0 && b->ncalls++ % (unsigned long long)b->ktime_every == 0;
+    b->kev_used = 0;
+    b->kev_eval.clear();
+  }
   const int rc = ba_local_impl(b, pr, res);
   if (rc != RSPL_E_DEVICE || !b) return rc;
   const std::string msg = rspl_last_error();
@@ -964,6 +1039,18 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
     RSPL_HIP(ba::finish(P, Lr, E, reinterpret_cast<const int*>(cb + cl.gmap), inl_h, T_h, X_h, L_h, S, q, st));
   }
   if ((rc = wait_mail(b, q, nullptr))) return rc;
+  if (b->ktime_on) {  // every timed trial precedes the finish kernel in the stream: its events are complete
+    for (int i : b->kev_eval) {
+      float a = 0.f, c = 0.f;
+      if (hipEventElapsedTime(&a, b->kev[3 * (size_t)i], b->kev[3 * (size_t)i + 1]) == hipSuccess &&
+          hipEventElapsedTime(&c, b->kev[3 * (size_t)i + 1], b->kev[3 * (size_t)i + 2]) == hipSuccess) {
+        b->kt_ms[0] += a;
+        b->kt_ms[1] += c;
+        b->kt_n[0]++;
+        b->kt_n[1]++;
+      }
+    }
+  }
   if (b->prof && b->prof_nb[0]) report_prof(b);
   if (b->lm_trace) {  // RSPL_BA_LMTRACE: the device LM decisions of both optimize() calls
     std::vector<double> h(8 * 64);

@@ -17,6 +17,7 @@
 #include "ba_kernels.hpp"
 #include "se3_device.hpp"
 
+
 namespace rspl {
 namespace ba {
 
@@ -1127,29 +1128,6 @@ __device__ __forceinline__ void pose_diag_range(const Problem& P, const Lin& L, 
 // ---------------------------------------------------------------------------
 // Schur complement for damping lambda
 // ---------------------------------------------------------------------------
-// one edge pair's Schur terms (Y = Hpl_e1 Dinv_g formed on the fly) added into acc[48];
-// H1 / H2 / Hp / bpv / blv already in registers (diag: e1 == e2, H2 == H1)
-__device__ __forceinline__ void schur_pair(const double (&H1)[24], const double (&B)[24], bool diag,
-                                           const double (&Hp)[36], const double (&bpv)[6], const double (&blv)[4],
-                                           const double (&D)[16], double (&acc)[48]) {
-#pragma unroll
-  for (int r = 0; r < 6; r++) {
-    const double h0 = H1[r * 4], h1 = H1[r * 4 + 1], h2 = H1[r * 4 + 2], h3 = H1[r * 4 + 3];
-    double y[4];
-#pragma unroll
-    for (int q = 0; q < 4; q++) y[q] = h0 * D[q] + h1 * D[4 + q] + h2 * D[8 + q] + h3 * D[12 + q];
-#pragma unroll
-    for (int cc = 0; cc < 6; cc++)
-      acc[r * 6 + cc] -= y[0] * B[cc * 4] + y[1] * B[cc * 4 + 1] + y[2] * B[cc * 4 + 2] + y[3] * B[cc * 4 + 3];
-    if (diag) {
-#pragma unroll
-      for (int cc = 0; cc < 6; cc++) acc[r * 6 + cc] += Hp[r * 6 + cc];
-      acc[36 + r] += bpv[r];
-      acc[42 + r] += y[0] * blv[0] + y[1] * blv[1] + y[2] * blv[2] + y[3] * blv[3];
-    }
-  }
-}
-
 // Edge-pair lists, built once per call on the device.  Chunk c = (pose pair pr, landmark
 // range lb) owns the segment [pp_off[c], pp_off[c+1]) of the (e1, e2) lists; within it the
 // pairs follow landmark order, then i, then j (deterministic).  Lane l of round r handles
@@ -1962,66 +1940,160 @@ __global__ __launch_bounds__(64) void schur_wave_kernel(Problem P, Active A, Sys
   solve_wave<N>(P, A, S, lambda, w, false);
 }
 
+// one edge pair's Schur terms with D = (Hll_g + lambda I)^-1, landmark dimension LD (3: points, 4: lines
+// or a mixed range; records of stride 4, the 4th row / column of a point is zero): Y = Hpl_e1 D,
+// acc -= Y Hpl_e2^T; diag (e1 == e2) adds Hpp_e1, bp_e1 and Y bl_g.  LOWER (a diagonal pose pair):
+// only the block's lower triangle (cc <= r) -- the only part any solver reads of a diagonal block.
+// Same products in the same order as the zero-padded 4-dim form.
+template <int LD, bool LOWER>
+__device__ __forceinline__ void schur_pair(const double (&H1)[6 * LD], const double (&B)[6 * LD], bool diag,
+                                           const double (&Hp)[21], const double (&bpv)[6], const double (&blv)[LD],
+                                           const double (&D)[LD * LD], double (&acc)[48]) {
+#pragma unroll
+  for (int r = 0; r < 6; r++) {
+    double y[LD];
+#pragma unroll
+    for (int q = 0; q < LD; q++) {
+      double t = H1[r * LD] * D[q];
+#pragma unroll
+      for (int c = 1; c < LD; c++) t += H1[r * LD + c] * D[c * LD + q];
+      y[q] = t;
+    }
+#pragma unroll
+    for (int cc = 0; cc < (LOWER ? r + 1 : 6); cc++) {
+      double t = y[0] * B[cc * LD];
+#pragma unroll
+      for (int q = 1; q < LD; q++) t += y[q] * B[cc * LD + q];
+      acc[r * 6 + cc] -= t;
+    }
+    if (LOWER && diag) {
+#pragma unroll
+      for (int cc = 0; cc <= r; cc++) acc[r * 6 + cc] += Hp[pk6(cc, r)];
+      acc[36 + r] += bpv[r];
+      double t = y[0] * blv[0];
+#pragma unroll
+      for (int q = 1; q < LD; q++) t += y[q] * blv[q];
+      acc[42 + r] += t;
+    }
+  }
+}
+
+// A chunk's walk over its edge-pair segment [beg, end), lane-strided, software-pipelined: the pair
+// indices two passes ahead and every operand of the next pass are requested before this pass's
+// arithmetic (ping-pong operand sets), so a wave waits on one memory round trip per segment rather than
+// per pass.  LD 3: a range of point landmarks only (3x3 D, 6x3 Hpl); 4: a range holding lines.  LOWER: a
+// diagonal pose pair (e1 == e2 pairs add Hpp / bp / Y bl; lower triangle only).
+template <int LD>
+struct PairOps {
+  double D[LD * LD], H1[6 * LD], H2[6 * LD], Hp[21], bpv[6], blv[LD];  // D: Hll of the landmark
+  bool diag, live, pt;
+};
+
+template <int LD, bool LOWER>
+__device__ __forceinline__ void load_pair(const Lin& L, const Active& A, const Sys& S, int nq, int4 q,
+                                          PairOps<LD>& o) {
+  const int e1 = q.x, e2 = q.y, g = q.z;
+  o.diag = LOWER && e1 == e2;
+  o.live = !(A.elevel && (A.elevel[e1] | A.elevel[e2]));  // else zero records: no contribution
+  const double* dg = S.Hll + 16 * g;  // the landmark block (inverted in use_pair)
+#pragma unroll
+  for (int i = 0; i < LD * LD; i++) o.D[i] = dg[i];
+#pragma unroll
+  for (int r = 0; r < 6; r++)
+#pragma unroll
+    for (int c = 0; c < LD; c++) o.H1[r * LD + c] = L.Hpl[24 * e1 + r * 4 + c];
+  if (o.diag) {
+#pragma unroll
+    for (int i = 0; i < 21; i++) o.Hp[i] = L.Hpp[21 * e1 + i];
+#pragma unroll
+    for (int i = 0; i < 6; i++) o.bpv[i] = L.bp[6 * e1 + i];
+#pragma unroll
+    for (int i = 0; i < LD; i++) o.blv[i] = S.bl[4 * g + i];
+  } else {
+#pragma unroll
+    for (int r = 0; r < 6; r++)
+#pragma unroll
+      for (int c = 0; c < LD; c++) o.H2[r * LD + c] = L.Hpl[24 * e2 + r * 4 + c];
+  }
+  o.pt = g < nq;
+}
+
+template <int LD, bool LOWER>
+__device__ __forceinline__ void use_pair(const PairOps<LD>& o, double lambda, bool& bad, double (&acc)[48]) {
+  if (!o.live) return;
+  double D[LD * LD];  // (Hll + lambda I)^-1 (Gauss-Jordan, partial pivoting; points 3x3, lines 4x4)
+  if constexpr (LD == 3) {
+    double Hd[9];
+#pragma unroll
+    for (int i = 0; i < 9; i++) Hd[i] = o.D[i] + ((i % 4 == 0) ? lambda : 0.0);
+    bad |= !small_inv<3>(Hd, D);
+  } else {
+    bad |= !lm_dinv(o.D, o.pt, lambda, D);
+  }
+  if (o.diag) schur_pair<LD, LOWER>(o.H1, o.H1, true, o.Hp, o.bpv, o.blv, D, acc);
+  else schur_pair<LD, LOWER>(o.H1, o.H2, false, o.Hp, o.bpv, o.blv, D, acc);
+}
+
+template <int LD, bool LOWER>
+__device__ __forceinline__ void chunk_loop(const Lin& L, const Active& A, const Sys& S, int nq, int beg, int end,
+                                           int4 qn, double lambda, bool& bad, double (&acc)[48]) {
+  const int lane = threadIdx.x & 63;
+  for (int k = beg + lane; k < end; k += 64) {
+    const int4 q = qn;
+    if (k + 64 < end) qn = A.pp[k + 64];
+    PairOps<LD> o;
+    load_pair<LD, LOWER>(L, A, S, nq, q, o);
+    use_pair<LD, LOWER>(o, lambda, bad, acc);
+  }
+}
+
 // One Schur chunk (pose pair, landmark range) on one wave: walks its segment of the edge-pair
 // lists, sums its 64 lanes in lane order (LDS transpose in red[64 * 49], this wave's own) and hands
 // the partial off write-through to whichever chunk of the pose pair finishes last; that one sums the
 // pair's chunks in chunk order (deterministic) into pairfin (write-through when `wt`: a solver in the
 // same launch reads it).  vb is the chunk's virtual workgroup id (XCD-aware order).  Returns true in
 // the wave that completed a pose pair.
-__device__ __forceinline__ bool chunk_wave(const Problem& P, const Lin& L, const Active& A, const Sys& S,
-                                           double lambda, int vb, double* red, bool wt) {
-  // XCD-aware chunk order: workgroups go round-robin over the 8 XCDs (blockIdx % 8), so
-  // landmark range lb runs on XCD lb % 8 for every pose pair -- each XCD's L2 then holds only
-  // its ranges' records (~1/8 of them), which its ~k_g pose pairs per landmark re-read
+// The chunk of virtual workgroup vb and its pair-list segment (bank-independent: requested before the
+// LM control is read).  XCD-aware chunk order: workgroups go round-robin over the 8 XCDs (blockIdx % 8),
+// so landmark range lb runs on XCD lb % 8 for every pose pair -- each XCD's L2 then holds only its
+// ranges' records (~1/8 of them), which its ~k_g pose pairs per landmark re-read.
+struct ChunkSeg {
+  int c, lb, beg, end;
+  int4 q0;  // the lane's first pair
+};
+__device__ __forceinline__ bool chunk_seg(const Active& A, int vb, ChunkSeg& cs) {
   const int lane = threadIdx.x & 63;
   const int xcd = vb & 7, slot = vb >> 3, rpx = (A.nchk + 7) >> 3;
-  const int lb = (slot % rpx) * 8 + xcd, pr0 = slot / rpx;
-  if (lb >= A.nchk || pr0 >= A.npairs) return false;
-  const int c = pr0 * A.nchk + lb;
+  cs.lb = (slot % rpx) * 8 + xcd;
+  const int pr0 = slot / rpx;
+  if (cs.lb >= A.nchk || pr0 >= A.npairs) return false;
+  cs.c = pr0 * A.nchk + cs.lb;
+  cs.beg = A.pp_off[cs.c];
+  cs.end = A.pp_off[cs.c + 1];
+  cs.q0 = cs.beg + lane < cs.end ? A.pp[cs.beg + lane] : make_int4(0, 0, 0, 0);
+  return true;
+}
+
+__device__ __forceinline__ bool chunk_wave(const Problem& P, const Lin& L, const Active& A, const Sys& S,
+                                           double lambda, const ChunkSeg& cs, double* red, bool wt) {
+  const int lane = threadIdx.x & 63;
+  const int c = cs.c, lb = cs.lb, beg = cs.beg, end = cs.end;
   if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c);
   const int pr = c / A.nchk;
-  const int beg = A.pp_off[c], end = A.pp_off[c + 1];
   double acc[48];
 #pragma unroll
   for (int v = 0; v < 48; v++) acc[v] = 0.0;
+  // a range of point landmarks only
+  // (all but the last range or two) takes the 3-dim loops, off-diagonal pose pairs without the e1 == e2 terms
+  const bool pts = (lb + 1) * kLmChunk <= P.nq;
+  const bool dpp = A.pairs[2 * pr] == A.pairs[2 * pr + 1];
   bool bad = false;
-  // the next pass's pair indices are fetched a pass ahead: one memory round trip per pass
-  int4 qn = beg + lane < end ? A.pp[beg + lane] : make_int4(0, 0, 0, 0);
-  for (int k = beg + lane; k < end; k += 64) {
-    // every operand of the pair is requested before any arithmetic
-    const int4 q = qn;
-    if (k + 64 < end) qn = A.pp[k + 64];
-    const int e1 = q.x, e2 = q.y, g = q.z;
-    const bool diag = e1 == e2;
-    const bool live = !(A.elevel && (A.elevel[e1] | A.elevel[e2]));  // else zero records: no contribution
-    double Hl[16], H1[24], H2[24], Hp[36], bpv[6], blv[4];
-    const double* hl = S.Hll + 16 * g;
-#pragma unroll
-    for (int i = 0; i < 16; i++) Hl[i] = hl[i];
-#pragma unroll
-    for (int i = 0; i < 24; i++) H1[i] = L.Hpl[24 * e1 + i];
-    if (diag) {
-#pragma unroll
-      for (int r = 0; r < 6; r++)
-#pragma unroll
-        for (int c = 0; c < 6; c++) Hp[r * 6 + c] = L.Hpp[21 * e1 + (r <= c ? pk6(r, c) : pk6(c, r))];
-#pragma unroll
-      for (int i = 0; i < 6; i++) bpv[i] = L.bp[6 * e1 + i];
-#pragma unroll
-      for (int i = 0; i < 4; i++) blv[i] = S.bl[4 * g + i];
-#pragma unroll
-      for (int i = 0; i < 24; i++) H2[i] = H1[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < 24; i++) H2[i] = L.Hpl[24 * e2 + i];
-    }
-    if (!live) continue;
-    double D[16];
-    bad |= !lm_dinv(Hl, g < P.nq, lambda, D);
-    schur_pair(H1, H2, diag, Hp, bpv, blv, D, acc);
-  }
-  if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 1);
+  if (pts && !dpp) chunk_loop<3, false>(L, A, S, P.nq, beg, end, cs.q0, lambda, bad, acc);
+  else if (pts) chunk_loop<3, true>(L, A, S, P.nq, beg, end, cs.q0, lambda, bad, acc);
+  else if (!dpp) chunk_loop<4, false>(L, A, S, P.nq, beg, end, cs.q0, lambda, bad, acc);
+  else chunk_loop<4, true>(L, A, S, P.nq, beg, end, cs.q0, lambda, bad, acc);
   if (bad) atomicOr(S.fail, 1);
+  if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 1);
 #pragma unroll
   for (int v = 0; v < 48; v++) red[lane * 49 + v] = acc[v];
   wave_sync();
@@ -2081,6 +2153,8 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
                                                         Sys Ss) {
   constexpr int kRedLen = 64 * 49, kSolveLen = (int)(sizeof(WaveSolveLds) / sizeof(double));
   __shared__ double smem[N > 0 && kSolveLen > kRedLen ? kSolveLen : kRedLen];
+  ChunkSeg cs;
+  if (!chunk_seg(A, blockIdx.x, cs)) return;  // in flight while the control is read
   if (S.lm) {  // device-side LM: damping and bank from the control
     LmView v;
     if (!lm_view(S, v)) return;
@@ -2090,7 +2164,7 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
       if (N > 0) bank_state(P);
     }
   }
-  if (!chunk_wave(P, L, A, S, lambda, blockIdx.x, smem, N > 0)) return;
+  if (!chunk_wave(P, L, A, S, lambda, cs, smem, N > 0)) return;
   if constexpr (N > 0) {
     if (!last_pair(S, A.npairs)) return;
     wave_sync();  // red[] is dead: the LDS becomes the solver's
@@ -2254,6 +2328,70 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
   const bool stamp = threadIdx.x == 0 && blockIdx.x < 4096;
   if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x);
   bool spec = SPEC;  // the candidate's speculative linearisation (device LM: not in the last iteration)
+  if (SPEC && (int)blockIdx.x >= nbu) {  // line workgroups
+    if (S.lm) {
+      LmView v;
+      if (!lm_view(S, v)) return;
+      lambda = v.lambda;
+      spec = v.spec;
+      if (v.cur) {
+        bank_state(P);
+        bank_lin(L, Ls, S, Ss);
+      }
+    }
+    if (!spec) return;
+    lin_lines<kLinSpec>(P, Ls, A, Ss, blockIdx.x - nbu, false, &L, &S, lambda, *S.fail != 0,
+                    S.prof ? S.prof + kProfUe + 4 * blockIdx.x + 1 : nullptr);
+    if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 3);
+    return;
+  }
+  if (!SPEC) nbu = gridDim.x;
+  // the candidate poses, cameras and pose steps of this trial go to LDS once per block, in the same
+  // round trip as each group's landmark-only operands; the group's first edge per lane is fetched
+  // in the next (every later access to them is LDS or registers: two dependent round trips).  The
+  // landmark-only operands of BOTH banks are requested before the LM control is read (the control
+  // picks the current bank), so that read is not a round trip of its own.
+  __shared__ double sT[64 * 8], scam[16 * 5], sx[6 * 32];
+  const int tid = threadIdx.x;
+  const int t = blockIdx.x * 256 + tid, g = t / kGroup, j = t % kGroup;
+  const bool in = g < A.nL;
+  const bool point = g < P.nq;
+  int k0 = 0, k1 = 0;
+  bool act = false;
+  double dl[16], blg[4], lm[6] = {0, 0, 0, 0, 0, 0};  // dl: Hll of the landmark (inverted below)
+  double dl2[16], blg2[4], lm2[6] = {0, 0, 0, 0, 0, 0};  // the other bank's
+#pragma unroll
+  for (int q = 0; q < 16; q++) dl[q] = dl2[q] = 0.0;
+#pragma unroll
+  for (int q = 0; q < 4; q++) blg[q] = blg2[q] = 0.0;
+  if (in) {
+    k0 = A.lm_off[g];
+    k1 = A.lm_off[g + 1];
+    act = A.lm_act[g] != 0;
+#pragma unroll
+    for (int q = 0; q < 16; q++) {
+      dl[q] = point && q >= 9 ? 0.0 : S.Hll[16 * g + q];
+      dl2[q] = point && q >= 9 ? 0.0 : Ss.Hll[16 * g + q];
+    }
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      blg[q] = S.bl[4 * g + q];
+      blg2[q] = Ss.bl[4 * g + q];
+    }
+    if (point) {
+#pragma unroll
+      for (int q = 0; q < 3; q++) {
+        lm[q] = P.X[3 * g + q];
+        lm2[q] = P.Xn[3 * g + q];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < 6; q++) {
+        lm[q] = P.L[6 * (g - P.nq) + q];
+        lm2[q] = P.Ln[6 * (g - P.nq) + q];
+      }
+    }
+  }
   if (S.lm) {
     LmView v;
     if (!lm_view(S, v)) {  // stopped: carry the control over to the next trial's slot
@@ -2265,45 +2403,12 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     if (v.cur) {
       bank_state(P);
       bank_lin(L, Ls, S, Ss);
-    }
-  }
-  if (SPEC && (int)blockIdx.x >= nbu) {
-    if (!spec) return;
-    lin_lines<kLinSpec>(P, Ls, A, Ss, blockIdx.x - nbu, false, &L, &S, lambda, *S.fail != 0,
-                    S.prof ? S.prof + kProfUe + 4 * blockIdx.x + 1 : nullptr);
-    if (stamp) prof_stamp(S, kProfUe + 4 * blockIdx.x + 3);
-    return;
-  }
-  if (!SPEC) nbu = gridDim.x;
-  // the candidate poses, cameras and pose steps of this trial go to LDS once per block, in the same
-  // round trip as each group's landmark-only operands; the group's first edge per lane is fetched
-  // in the next (every later access to them is LDS or registers: two dependent round trips)
-  __shared__ double sT[64 * 8], scam[16 * 5], sx[6 * 32];
-  const int tid = threadIdx.x;
-  const int t = blockIdx.x * 256 + tid, g = t / kGroup, j = t % kGroup;
-  const bool in = g < A.nL;
-  const bool point = g < P.nq;
-  int k0 = 0, k1 = 0;
-  bool act = false;
-  double hll[16], blg[4], lm[6] = {0, 0, 0, 0, 0, 0};
 #pragma unroll
-  for (int q = 0; q < 16; q++) hll[q] = 0.0;
+      for (int q = 0; q < 16; q++) dl[q] = dl2[q];
 #pragma unroll
-  for (int q = 0; q < 4; q++) blg[q] = 0.0;
-  if (in) {
-    k0 = A.lm_off[g];
-    k1 = A.lm_off[g + 1];
-    act = A.lm_act[g] != 0;
+      for (int q = 0; q < 4; q++) blg[q] = blg2[q];
 #pragma unroll
-    for (int q = 0; q < 16; q++) hll[q] = S.Hll[16 * g + q];
-#pragma unroll
-    for (int q = 0; q < 4; q++) blg[q] = S.bl[4 * g + q];
-    if (point) {
-#pragma unroll
-      for (int q = 0; q < 3; q++) lm[q] = P.X[3 * g + q];
-    } else {
-#pragma unroll
-      for (int q = 0; q < 6; q++) lm[q] = P.L[6 * (g - P.nq) + q];
+      for (int q = 0; q < 6; q++) lm[q] = lm2[q];
     }
   }
   const bool failed = *S.fail != 0;
@@ -2374,11 +2479,20 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
   if (upd) {
 #pragma unroll
     for (int q = 0; q < 4; q++) c[q] += blg[q];
-    double D[16];
-    const bool ok = lm_dinv(hll, point, lambda, D);
-    if (!ok && j == 0) atomicOr(S.fail, 1);
+    {
+      double D[16];
+      if (!lm_dinv(dl, point, lambda, D) && j == 0) atomicOr(S.fail, 1);
 #pragma unroll
-    for (int r = 0; r < 4; r++) xl[r] = D[r * 4] * c[0] + D[r * 4 + 1] * c[1] + D[r * 4 + 2] * c[2] + D[r * 4 + 3] * c[3];
+      for (int q = 0; q < 16; q++) dl[q] = point ? (q < 9 ? D[4 * (q / 3) + q % 3] : 0.0) : D[q];
+    }
+    if (point) {
+#pragma unroll
+      for (int r = 0; r < 3; r++) xl[r] = dl[r * 3] * c[0] + dl[r * 3 + 1] * c[1] + dl[r * 3 + 2] * c[2];
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; r++)
+        xl[r] = dl[r * 4] * c[0] + dl[r * 4 + 1] * c[1] + dl[r * 4 + 2] * c[2] + dl[r * 4 + 3] * c[3];
+    }
     if (j == 0)
 #pragma unroll
       for (int q = 0; q < 4; q++) sc += xl[q] * (lambda * xl[q] + blg[q]);
@@ -2797,9 +2911,10 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
 }
 
 hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq, hipStream_t s,
-                     const Spec& spec) {
+                     const Spec& spec, hipEvent_t* ev) {
   if (!S.lm || !fast_path(A.K)) return hipErrorInvalidValue;
   const int mode = solve_mode(A.K);
+  if (ev) (void)hipEventRecord(ev[0], s);
   if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, 0.0, spec.Ls, spec.Ss, mode == 1, s);
   if (mode == 2) {
     launch_blk4_solve(P, A, S, 0.0, s);
@@ -2810,8 +2925,10 @@ hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, un
     hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, 0.0);
   }
   const int nbu = update_errors_blocks(A), nbl = A.n_lblk;
+  if (ev) (void)hipEventRecord(ev[1], s);
   hipLaunchKernelGGL(update_errors_kernel<true>, dim3(nbu + nbl), dim3(256), 0, s, P, L, A, S, 0.0, seq, spec.Ls,
                      spec.Ss, nbu);
+  if (ev) (void)hipEventRecord(ev[2], s);
   return hipGetLastError();
 }
 

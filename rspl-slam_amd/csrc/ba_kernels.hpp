@@ -160,7 +160,8 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
 // {chi2, iterations done, current bank, stop} + seq.  Always fused with the speculative linearisation
 // (skipped on the device when the iteration is the last one).
 hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq, hipStream_t s,
-                     const Spec& spec);
+                     const Spec& spec, hipEvent_t* ev = nullptr);  // ev: [3] recorded before / between / after
+                                                                   // the trial's two launches (kernel timing)
 // edge-pair lists of the pose pairs (count, offsets, fill; A.pp_* are not read)
 hipError_t build_pairs(const Active& A, int* pp_cnt, int* pp_off, int4* pp, hipStream_t s);
 // lm_act[g] = landmark g has an edge of level 0 (the second optimize's active landmarks)

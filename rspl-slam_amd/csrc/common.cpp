@@ -71,4 +71,5 @@ const Tensor* find(const std::vector<Tensor>& ts, const std::string& name, int64
 }  // namespace rspl
 
 extern "C" const char* rspl_last_error(void) { return rspl::g_err; }
-extern "C" const char* rspl_version(void) { return "rspl-mi355x 0.1 (gfx950)"; }
+extern "C" const char* rspl_version(void) { return "rspl-mi355x 0.2 (gfx950)"; }
+extern "C" int rspl_abi_version(void) { return RSPL_ABI_VERSION; }

@@ -420,7 +420,10 @@ __global__ __launch_bounds__(64 * NW) void frame_opt_kernel(Args a, int batch) {
 size_t lds_bytes(int n) { return (size_t)n * (sizeof(Edge) + 3 * sizeof(double) + 2); }
 
 // waves per frame: 4 for latency (one frame per CU at 256 VGPRs) while the batch leaves CUs idle,
-// 1 for throughput (two frames per SIMD) on large batches; RSPL_FRAME_WAVES=1 / 4 forces one (A/B)
+// 1 for throughput (two frames per SIMD) on large batches; RSPL_FRAME_WAVES=1 / 4 forces one (A/B).
+// The wave count sets the summation order of H / b / chi2, so a frame's result depends on whether its
+// batch exceeds 256 frames at the last-ulp level (agreement to the oracle tolerances either way:
+// tests/test_gpu_frame.py::test_frame_alone_and_in_a_large_batch).
 hipError_t optimize(const Args& a, int batch, int max_n, hipStream_t s) {
   if (batch <= 0) return hipSuccess;
   const char* w = getenv("RSPL_FRAME_WAVES");

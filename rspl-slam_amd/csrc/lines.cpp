@@ -239,6 +239,7 @@ struct rspl_lines {
   // detector (rspl_lines_detect): device image / half image / classes, pinned host copies; grown on demand
   uint8_t *d_img = nullptr, *d_det = nullptr, *h_img = nullptr, *h_det = nullptr;
   size_t det_cap = 0;  // pixels of the largest full-size image so far
+  int det_H = 0, det_W = 0;  // the last detection's image size (rspl_lines_debug_canny must match it)
   std::vector<uint8_t> edge;
   std::vector<int> stack;
 };
@@ -762,6 +763,8 @@ extern "C" int rspl_lines_detect(rspl_lines* h, const uint8_t* image, int H, int
   RSPL_HIP(lines::canny_classes(a, st));
   RSPL_HIP(hipMemcpyAsync(h->h_det, h->d_det, 2 * hp, hipMemcpyDeviceToHost, st));
   RSPL_HIP(hipStreamSynchronize(st));
+  h->det_H = H;
+  h->det_W = W;
   const int n = fld_from_classes(h->h_det, h->h_det + hp, hh, hw, cfg, h->edge, h->stack, segments, capacity);
   *n_out = n;
   if (n > capacity) {
@@ -772,7 +775,9 @@ extern "C" int rspl_lines_detect(rspl_lines* h, const uint8_t* image, int H, int
 }
 
 extern "C" int rspl_lines_debug_canny(rspl_lines* h, int H, int W, uint8_t* half, uint8_t* cls) {
-  RSPL_CHECK_ARG(h && half && cls && (size_t)H * W <= h->det_cap, "rspl_lines_debug_canny: no such detection");
+  RSPL_CHECK_ARG(h && half && cls, "rspl_lines_debug_canny: NULL argument");
+  RSPL_CHECK_ARG(H == h->det_H && W == h->det_W && H > 0,
+                 "rspl_lines_debug_canny: %dx%d is not the last detection's size (%dx%d)", W, H, h->det_W, h->det_H);
   const size_t hp = (size_t)H * W / 4;
   memcpy(half, h->h_det, hp);
   memcpy(cls, h->h_det + hp, hp);

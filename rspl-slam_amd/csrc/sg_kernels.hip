@@ -1665,7 +1665,9 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
 #pragma unroll
     for (int k = 0; k < RPW; k++) {
       const int r = wv + 16 * k;
-      if (lane == 0) as[wv + 16 * k] = r < nr ? ((r0 + r) < m ? norm : lmu_bin) - (logf(sm[k]) + mx[k]) : 0.f;
+      // (no iterations: u = v = 0, Z = C - norm as superglue.py:202-205 -- no seed)
+      if (lane == 0)
+        as[wv + 16 * k] = r < nr && a.iters > 0 ? ((r0 + r) < m ? norm : lmu_bin) - (logf(sm[k]) + mx[k]) : 0.f;
       ur[k] = 1.f;
     }
   }

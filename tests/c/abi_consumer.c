@@ -261,6 +261,10 @@ static int run_ba(const char* dir) {
 }
 
 int main(int argc, char** argv) {
+  if (rspl_abi_version() != RSPL_ABI_VERSION) {  /* caller-allocated structs follow this header's layout */
+    fprintf(stderr, "librspl ABI %d, header ABI %d\n", rspl_abi_version(), RSPL_ABI_VERSION);
+    return 3;
+  }
   if (argc >= 2 && !strcmp(argv[1], "layout")) return layout();
   if (argc >= 5 && !strcmp(argv[1], "run")) {
     int rc = run_sp(argv[2], argv[3]);

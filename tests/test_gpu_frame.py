@@ -80,3 +80,13 @@ def test_reference_signature_in_place():
     assert np.abs(poses[42].p - ref.pose_p).max() < 1e-9
     assert [c.inlier for c in mono] == list(ref.inlier["mono"].astype(bool))
     assert [c.inlier for c in stereo] == list(ref.inlier["stereo"].astype(bool))
+
+
+def test_frame_alone_and_in_a_large_batch(fba):
+    """The wave count per frame follows the batch size (4 waves for <= 256 frames, 1 above), which
+    changes the summation order of H / b / chi2: the same frame solved alone and inside a batch of
+    300 agrees to the oracle tolerances (rounds, inlier flags, pose 1e-9), not bitwise."""
+    probs = [SY.frame_problem(n_points=400, outlier_frac=0.1, seed=2000 + i)[0] for i in range(300)]
+    alone = fba.run(probs[:1])[0]
+    batch = fba.run(probs)[0]
+    _compare(alone, batch)

@@ -246,6 +246,11 @@ def test_sinkhorn_kernels_vs_reference(pkg, golden, weight_blobs, monkeypatch, k
     ok, Z = sg.debug_sinkhorn(g["scores"], float(g["alpha"]), int(g["iters"]))
     assert ok, sg.error
     np.testing.assert_allclose(Z, g["Z"], atol=1e-4, rtol=0)
+    for it in (0, 1, 3):  # short runs, incl. no iteration at all (Z = C - norm): the oracle's restatement
+        ok, Z = sg.debug_sinkhorn(g["scores"], float(g["alpha"]), it)
+        assert ok, sg.error
+        np.testing.assert_allclose(Z, oracle.log_optimal_transport(g["scores"], float(g["alpha"]), it),
+                                   atol=1e-4, rtol=0)
     g = golden("sg_400")
     F0, F1 = g["F0"].astype(np.float64), g["F1"].astype(np.float64)
     G0, G1 = post.normalize_keypoints(F0, 752, 480), post.normalize_keypoints(F1, 752, 480)

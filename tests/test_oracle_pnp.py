@@ -61,3 +61,12 @@ def test_too_few_points():
     K, X, kp, gt = SY.pnp_problem(n_points=7, outlier_frac=0.0, seed=4)
     n, R, t, inl, used = oracle.pnp(K, X, kp)
     assert n == 0 and used == 0 and not inl.any()
+
+
+@pytest.mark.parametrize("seed,n,outl", [(0, 300, 0.2), (2, 300, 0.4), (7, 400, 0.25)])
+def test_independent_eigen_solver_same_outcome(seed, n, outl):
+    """The GPU-mirror eigen order and the independent cyclic Jacobi reach the same RANSAC outcome."""
+    K, X, kp, gt = SY.pnp_problem(n_points=n, outlier_frac=outl, seed=seed)
+    a, b = oracle.pnp(K, X, kp), oracle.pnp(K, X, kp, independent=True)
+    assert a[0] == b[0] and (a[3] == b[3]).all()
+    assert np.abs(a[1] - b[1]).max() < 1e-7 and np.abs(a[2] - b[2]).max() < 1e-6
