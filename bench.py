@@ -5,11 +5,14 @@ Workload (BASELINE.json configs[2], "C3", all-keyframe worst case of SURVEY.md Â
 step is one stereo keyframe of a synthetic EuRoC-shaped stream:
   * SuperPoint on the rectified stereo pair (batch 2, 480x752, top-400),
   * SuperGlue/PointMatching on 2 pairs: left(t) vs left(t-1) keyframe, left(t) vs right(t),
-  * the line part of the stereo keyframe (Frame::AddRightFeatures, src/frame.cc:150-203): both
-    images' AssignPointsToLines, the stereo-match disparity filter and MatchLines on the GPU
-    (rspl_lines_stereo_device), fed by SuperPoint's device features and SuperGlue's device match
-    index of the left(t)-right(t) pair, on each image's line segments (LineExtractor's merge passes
-    over FLD segments; the restated FLD detector is rspl_lines_detect),
+  * the line front end of the stereo keyframe: LineDetector::LineExtractor on both images' RCF-like edge
+    maps (the restated FLD, rspl_lines_detect: GPU resize / Sobel / Canny classes, host chaining and
+    fitting, then the host merge passes) on two host threads beside SuperPoint / SuperGlue, as the
+    reference's line threads run beside its point thread (src/map_builder.cc:285-290, 325-337), joined
+    before the line part of Frame::AddRightFeatures (src/frame.cc:150-203): both images'
+    AssignPointsToLines, the stereo-match disparity filter and MatchLines on the GPU
+    (rspl_lines_stereo_device), fed by SuperPoint's device features and SuperGlue's device match index of
+    the left(t)-right(t) pair,
   * one local BA (LocalmapOptimization) of a C3-sized problem: 10 keyframes (1 fixed),
     ~4k points / ~10^4 point observations, 100 lines (synthetic, with ground truth).
 Inputs (images) are resident in HBM before timing.  BA is host-driven and runs on its own
@@ -32,6 +35,7 @@ OIVIO-shaped 640x512 stereo, 600 keypoints, SG N=600; with --gpus 8 one sequence
 (configs[4]: synthetic 1920x1080 stereo, 2048 keypoints, SG N=2048, 30-keyframe / 10k-landmark BA).
 """
 import argparse
+import concurrent.futures
 import json
 import os
 import queue
@@ -427,20 +431,24 @@ def main():
     st_post = capi.Stream(reserve_cus=rc, priority=prio["post"])  # SG's Sinkhorn + decode: overlaps the next GNN
     ev_sp = [capi.Event() for _ in range(3)]
     ev_sg = [capi.Event() for _ in range(3)]
-    # line part of each stereo keyframe (frame.cc:150-203): per replica frame a left / right line set
-    # (host LineDetector merge passes over FLD-like fragments, run once: the reference's line thread),
-    # resident in HBM like the images; the association runs on the post stream after the decode
+    # line front end of each stereo keyframe: per replica frame a left / right RCF-like edge map in host
+    # memory (the reference reads image_rcf from disk); every step runs LineDetector::LineExtractor on both
+    # on two host threads (one detector handle each) and uploads the lines for the stereo association,
+    # which runs on the post stream after the decode (frame.cc:150-203)
     lm = pkg.lines.LineMatcher(max_lines=512, max_points=max(K, 512), device=local)
-    line_sets = []
-    for i in range(NP):
-        sc = syn.line_scene(n_lines=80, n_points=16, seed=seeds["images"][i], width=W, height=H)
-        L0, L1 = pkg.lines.LineExtractor(sc["seg_left"]), pkg.lines.LineExtractor(sc["seg_right"])
-        d0, d1 = capi.DeviceBuffer(max(1, L0.nbytes)), capi.DeviceBuffer(max(1, L1.nbytes))
-        d0.upload(L0)
-        d1.upload(L1)
-        line_sets.append((d0, len(L0), d1, len(L1)))
-    n_lines_step = float(np.mean([2 * ls[1] for ls in line_sets]))
+    edge_imgs = [syn.edge_stereo_pair(H, W, seed=seeds["images"][i]) for i in range(NP)]
+    detectors = [pkg.lines.LineDetector(device=local) for _ in range(2)]
+    line_pool = concurrent.futures.ThreadPoolExecutor(max_workers=2)
+    line_bufs = [(capi.DeviceBuffer(512 * 4 * 8), capi.DeviceBuffer(512 * 4 * 8)) for _ in range(3)]
+    line_host = [None] * 3  # keeps each slot's uploaded arrays alive until the stream has read them
     lines_out, lines_valid = capi.DeviceBuffer(512 * 4 * 8), capi.DeviceBuffer(512)
+    line_stats = {"detect_ms": [], "lines": []}
+
+    def detect_lines(k, img):
+        """one image's LineExtractor on this thread's detector: lines [m][4] at full size, host wall ms"""
+        t = time.perf_counter()
+        out = detectors[k].LineExtractor(img)[:512]
+        return out, (time.perf_counter() - t) * 1e3
     bf = pkg.synthetic.EUROC_BF
     cam_limits = (bf / 10.0, bf / 0.1, 2.0)  # MinXDiff, MaxXDiff, MaxYDiff (camera.cc:21-22, euroc.yaml)
 
@@ -490,7 +498,13 @@ def main():
             slot, pslot = i % 3, (i - 1) % 3
             cur, prev, ccur, cprev = feats[slot], feats[pslot], counts[slot], counts[pslot]
             skip = args.skip.split(",")
+            # the line threads of this keyframe, beside its SuperPoint / SuperGlue (map_builder.cc:325-337)
+            eL, eR = edge_imgs[i % NP]
+            jobs = None if "lines" in skip else (line_pool.submit(detect_lines, 0, eL),
+                                                  line_pool.submit(detect_lines, 1, eR))
             if "sp" in skip or "sg" in skip:  # diagnostics: stages left out (not a benchmark line)
+                if jobs is not None:
+                    jobs[0].result(), jobs[1].result()
                 if "sp" not in skip:
                     sp.infer_device(pool.offset((i % NP) * 2 * H * W), 2, H, W, W, H * W, cur.ptr, K, ccur.ptr,
                                     st_sp.handle)
@@ -516,16 +530,27 @@ def main():
             capi.memcpy_d2d(n1.offset(4), ccur.offset(4), 4, st_sg.handle)
             sg.infer_device(2, f0.ptr, n0.ptr, f1.ptr, n1.ptr, K, True, outs[0].ptr, outs[1].ptr, outs[2].ptr,
                             outs[3].ptr, st_sg.handle, post_stream=st_post.handle)
-            # stereo line association of frame t: SP's device records of (left, right) and SG's match
-            # index of pair 1 (left(t) -> right(t)), stream-ordered behind the decode
-            dl0, nl0, dl1, nl1 = line_sets[i % NP]
-            tm = line_timers[i - line_t0] if line_t0 is not None else None
-            if tm is not None:
-                tm.start(st_post.handle)
-            lm.stereo_lines_device(dl0.ptr, nl0, dl1.ptr, nl1, cur.ptr, K, ccur.ptr, outs[0].offset(K * 4),
-                                   cam_limits, lines_out.ptr, lines_valid.ptr, st_post.handle)
-            if tm is not None:
-                tm.stop(st_post.handle)
+            # stereo line association of frame t: the joined line threads' lines, SP's device records of
+            # (left, right) and SG's match index of pair 1 (left(t) -> right(t)), stream-ordered behind the
+            # decode
+            if jobs is not None:
+                (L0, t0ms), (L1, t1ms) = jobs[0].result(), jobs[1].result()
+                if line_t0 is not None:
+                    line_stats["detect_ms"].append(max(t0ms, t1ms))
+                    line_stats["lines"].append(len(L0) + len(L1))
+                dl0, dl1 = line_bufs[slot]
+                line_host[slot] = (L0, L1)
+                if len(L0):
+                    dl0.upload(L0, st_post.handle)
+                if len(L1):
+                    dl1.upload(L1, st_post.handle)
+                tm = line_timers[i - line_t0] if line_t0 is not None else None
+                if tm is not None:
+                    tm.start(st_post.handle)
+                lm.stereo_lines_device(dl0.ptr, len(L0), dl1.ptr, len(L1), cur.ptr, K, ccur.ptr, outs[0].offset(K * 4),
+                                       cam_limits, lines_out.ptr, lines_valid.ptr, st_post.handle)
+                if tm is not None:
+                    tm.stop(st_post.handle)
             ev_sg[slot].record(st_post.handle)  # matches and lines complete on the post stream
             # keyframe i's local BA goes to the tracking thread (own high-priority stream) through a
             # 2-deep buffer, as the reference's feature thread blocks only while
@@ -547,6 +572,8 @@ def main():
         ba_ms.clear()
         ba_iters.clear()
         line_timers[:] = [capi.Timer() for _ in range(args.steps)]
+        line_stats["detect_ms"].clear()
+        line_stats["lines"].clear()
         line_t0 = args.warmup
         ba.kernel_timing(ktime_every)
         ba.kernel_times()  # reset
@@ -571,13 +598,16 @@ def main():
 
         if lm.status():
             raise SystemExit("bench: the stereo line association overflowed its point-line pairs")
-        lines_ms = float(np.mean([tm.elapsed_ms() for tm in line_timers])) if line_timers else None
+        lines_ms = float(np.mean([tm.elapsed_ms() for tm in line_timers[:len(line_stats["detect_ms"])]])) \
+            if line_stats["detect_ms"] else None
         line_t0 = None
         sp_ms, sp_calls = sp.stage_times()
         sg_ms, sg_calls = sg.stage_times()
         value = job_value(world, args.steps, elapsed)
         return {"value": value, "elapsed": elapsed, "sp": (sp_ms, sp_calls), "sg": (sg_ms, sg_calls),
                 "stages": (sp, sg), "ba_ms": list(ba_ms), "ba_iters": list(ba_iters), "lines_ms": lines_ms,
+                "lines_detect_ms": float(np.mean(line_stats["detect_ms"])) if line_stats["detect_ms"] else None,
+                "lines_per_step": float(np.mean(line_stats["lines"])) if line_stats["lines"] else None,
                 "ba_kt": ba_kt, "ba_timed_calls": (ba_calls + ktime_every - 1) // ktime_every if ktime_every else 0}
 
     res = measure(args.precision)
@@ -629,11 +659,15 @@ def main():
         "stages_roofline": stages,
         "stages_ms_per_step": {**{f"sp:{n}": round(v / max(1, sp_calls), 4) for n, v in zip(sp.STAGES, sp_ms)},
                                **{f"sg:{n}": round(v / max(1, sg_calls), 4) for n, v in zip(sg.STAGES, sg_ms)},
+                               "lines:detect": round(res["lines_detect_ms"], 4) if res["lines_detect_ms"] else None,
                                "lines:stereo": round(res["lines_ms"], 4) if res["lines_ms"] else None,
                                "ba:wall": round(ba_wall, 4) if ba_wall else None},
-        "lines": {"segments_per_step": n_lines_step, "keypoints_per_image": K,
-                  "note": "stereo line association per keyframe on the GPU (AssignPointsToLines x2, disparity "
-                          "filter, MatchLines; frame.cc:150-203), post stream, HIP-event time per step"},
+        "lines": {"lines_per_step": res["lines_per_step"], "keypoints_per_image": K,
+                  "note": "lines:detect = host wall time per keyframe of LineDetector::LineExtractor on both images' "
+                          "RCF-like edge maps (restated FLD: GPU Canny classes + host chaining / fitting / merges), two "
+                          "host threads beside SP/SG, joined before the association; lines:stereo = the stereo line "
+                          "association on the GPU (AssignPointsToLines x2, disparity filter, MatchLines; "
+                          "frame.cc:150-203), post stream, HIP-event time per step"},
         "ba": {"ms_per_call": round(ba_wall, 4) if ba_wall else None,
                "lm_iterations_per_call": ba_it,
                "us_per_lm_iteration": round(1e3 * ba_wall / ba_it, 2) if ba_wall and ba_it else None,

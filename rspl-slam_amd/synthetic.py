@@ -469,6 +469,14 @@ def line_scene(n_lines: int = 60, n_points: int = 400, seed: int = 0, width: int
             "stereo_matches": m.astype(np.int32), "lines_left": L, "lines_right": Lr}
 
 
+def edge_stereo_pair(h: int, w: int, seed: int, n_lines: int = 40, disparity: int = 12):
+    """Left / right RCF-like edge images of one stereo frame (the u8 maps the reference's line thread runs
+    FLD on, map_builder.cc:285-290, 325-337): an edge_map of width w + disparity, the right view shifted by
+    the disparity, as stereo_pair does for the texture."""
+    img, _ = edge_map(h, w + disparity, n_lines=n_lines, seed=seed)
+    return np.ascontiguousarray(img[:, disparity:]), np.ascontiguousarray(img[:, :w])
+
+
 def edge_map(h: int = 480, w: int = 752, n_lines: int = 40, seed: int = 0, width: float = 1.2, noise: float = 6.0):
     """An RCF-like edge-probability image (the u8 map LineDetector::LineExtractor runs FLD on,
     map_builder.cc:286): n_lines straight ridges with a Gaussian cross-profile (sigma `width` px,

@@ -123,6 +123,15 @@ def superglue_shapes(n_layers: int = 18) -> "OrderedDict[str, tuple]":
 # mutual matches above the 0.2 threshold.
 SP_WEIGHT_GAIN = {"convPb.weight": 4.0}
 SG_WEIGHT_GAIN = {"kenc.encoder.12.weight": 0.05, "mlp.3.weight": 0.1, "final_proj.weight": 8.0}
+# "c1" SuperGlue profile (same seed and generator, other gains): a 6x stronger keypoint-encoder output and
+# a 2x final projection sharpen the assignment so that on the C1 stereo pairs (SuperPoint features of
+# synthetic.stereo_pair, seeded SuperPoint weights) 25-38 % of the keypoints are matched above the
+# reference's 0.2 threshold (super_glue.cpp:355; measured on seeds 300-305 through the oracle: 100-154
+# matches per pair of 400, median row gap of the matched log-assignments 0.5) -- the default profile keeps
+# every probability below 0.2 there, so the thresholded decode and the DMatch distances were never
+# exercised on SuperPoint-derived features.
+SG_WEIGHT_GAIN_C1 = {"kenc.encoder.12.weight": 0.3, "mlp.3.weight": 0.1, "final_proj.weight": 16.0}
+SG_PROFILES = {"default": SG_WEIGHT_GAIN, "c1": SG_WEIGHT_GAIN_C1}
 BIAS_RANGE = 0.05
 
 
@@ -178,8 +187,8 @@ def superpoint_synth(seed: int = 1) -> "OrderedDict[str, np.ndarray]":
     return synth(superpoint_shapes(), seed, SP_WEIGHT_GAIN)
 
 
-def superglue_synth(seed: int = 2) -> "OrderedDict[str, np.ndarray]":
-    return synth(superglue_shapes(), seed, SG_WEIGHT_GAIN)
+def superglue_synth(seed: int = 2, profile: str = "default") -> "OrderedDict[str, np.ndarray]":
+    return synth(superglue_shapes(), seed, SG_PROFILES[profile])
 
 
 # --------------------------------------------------------------------------
@@ -236,3 +245,13 @@ def ensure_blobs(directory, sp_seed: int = 1, sg_seed: int = 2):
     if not os.path.exists(sg):
         write_blob(sg, superglue_synth(sg_seed))
     return sp, sg
+
+
+def ensure_sg_profile_blob(directory, profile: str = "c1", sg_seed: int = 2):
+    """weights/superglue_synth_s{seed}_{profile}.bin (written if absent)."""
+    import os
+    os.makedirs(directory, exist_ok=True)
+    path = os.path.join(directory, f"superglue_synth_s{sg_seed}_{profile}.bin")
+    if not os.path.exists(path):
+        write_blob(path, superglue_synth(sg_seed, profile))
+    return path

@@ -31,6 +31,13 @@ def weight_blobs():
 
 
 @pytest.fixture(scope="session")
+def sg_c1_blob():
+    """SuperGlue weights of the "c1" profile (weights.SG_WEIGHT_GAIN_C1: C1 stereo matches above 0.2)."""
+    from rspl_slam_amd import weights as W
+    return W.ensure_sg_profile_blob(str(ROOT / "weights"), "c1")
+
+
+@pytest.fixture(scope="session")
 def golden():
     def load(name):
         return np.load(GOLDEN / f"{name}.npz")

@@ -293,3 +293,74 @@ def test_sinkhorn_sc10_vs_oracle(pkg, weight_blobs, monkeypatch, G, scale):
     Zr = oracle.log_optimal_transport(S, 1.0, 100)
     print(f"sc10 G={G} scale={scale}: max |dZ| {np.abs(Z - Zr).max():.3g}")
     np.testing.assert_allclose(Z, Zr, atol=1e-4 * max(1.0, 2 * np.abs(Zr).max() / 100), rtol=0)
+
+
+def _pm(pkg, blob, precision):
+    return pkg.PointMatching(pkg.SuperGlueConfig(image_width=752, image_height=480, weights=blob, max_keypoints=400,
+                                                 max_batch=1, precision=precision))
+
+
+def test_sg_c1_stereo_pair_fp32(pkg, golden, sg_c1_blob):
+    """The C1 stereo pair's SuperPoint features (reference modules) through PointMatching on the GPU at
+    fp32 with the "c1" SuperGlue profile: Z and the assignment probabilities vs the reference module
+    (the profile's 4x sharper scores scale fp32 accumulation noise: Z atol 1.5e-3, exp(Z) atol 1e-4),
+    identical decode and a NON-EMPTY thresholded DMatch list identical to the reference's
+    (point_matching.cc:12-48, super_glue.cpp:339-367), distances within the probability tolerance."""
+    g = golden("sg_c1")
+    F0, F1 = g["F0"].astype(np.float64), g["F1"].astype(np.float64)
+    pm = _pm(pkg, sg_c1_blob, pkg.capi.RSPL_PREC_FP32)
+    n, ml = pm.MatchingPoints(F0, F1)
+    Z = pm.superglue.debug_scores(0, F0.shape[1], F1.shape[1])
+    np.testing.assert_allclose(Z, g["Z"], atol=1.5e-3, rtol=0)
+    np.testing.assert_allclose(np.exp(Z.astype(np.float64)), np.exp(g["Z"].astype(np.float64)), atol=1e-4, rtol=0)
+    assert n == len(g["matches"]) >= 80
+    np.testing.assert_array_equal(np.array([(q, t) for q, t, _ in ml]), g["matches"])
+    np.testing.assert_allclose([d for _, _, d in ml], g["distances"], atol=1e-4)
+
+
+def test_sg_c1_images_to_matches_fp32(pkg, golden, weight_blobs, sg_c1_blob):
+    """Images -> matches on the GPU (fp32): SuperPoint on the C1 stereo images gives the reference
+    module's keypoint sets and descriptors, and PointMatching on those features gives the reference's
+    matches (compared as keypoint-coordinate pairs: the top-k order of near-equal scores may differ)."""
+    from helpers import compare_features
+    from rspl_slam_amd import synthetic as SY
+    g = golden("sg_c1")
+    L, R = SY.stereo_pair(480, 752, seed=int(g["seed"]))
+    sp = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=400, weights=weight_blobs[0], max_height=480,
+                                             max_width=752, max_batch=1))
+    assert sp.build(), sp.error
+    F = []
+    for img, Fr in ((L, g["F0"]), (R, g["F1"])):
+        ok, Fg = sp.infer(img)
+        assert ok, sp.error
+        compare_features(Fg, Fr.astype(np.float64), desc_atol=1e-5, score_atol=1e-5)
+        F.append(Fg)
+    pm = _pm(pkg, sg_c1_blob, pkg.capi.RSPL_PREC_FP32)
+    n, ml = pm.MatchingPoints(F[0], F[1])
+    got = {(F[0][1, q], F[0][2, q], F[1][1, t], F[1][2, t]) for q, t, _ in ml}
+    F0r, F1r = g["F0"], g["F1"]
+    ref = {(F0r[1, q], F0r[2, q], F1r[1, t], F1r[2, t]) for q, t in g["matches"]}
+    assert n >= 80 and got == ref
+
+
+def test_sg_c1_fp16_disagreements_explained(pkg, golden, sg_c1_blob):
+    """fp16 (the reference's TensorRT kFP16 engine, super_glue.cpp:132) vs the reference on the C1 pair:
+    every match-index disagreement must sit at a near-tie of the reference's own Z within the measured
+    fp16 |dZ| (helpers.unexplained_match_disagreements), and the thresholded match agreement is reported."""
+    from helpers import unexplained_match_disagreements
+    g = golden("sg_c1")
+    F0, F1 = g["F0"].astype(np.float64), g["F1"].astype(np.float64)
+    G0, G1 = post.normalize_keypoints(F0, 752, 480), post.normalize_keypoints(F1, 752, 480)
+    sg = pkg.SuperGlue(pkg.SuperGlueConfig(weights=sg_c1_blob, max_keypoints=400, max_batch=1,
+                                           precision=pkg.capi.RSPL_PREC_FP16))
+    assert sg.build(), sg.error
+    ok, i0, i1, m0, m1 = sg.infer(G0, G1)
+    assert ok, sg.error
+    Z = sg.debug_scores(0, F0.shape[1], F1.shape[1])
+    sig = g["Z"] > np.log(1e-4)
+    tol = 2.0 * float(np.abs(Z - g["Z"])[sig].max())  # a disagreement needs a gap below twice the fp16 error
+    bad = unexplained_match_disagreements(g["Z"], i0, i1, g["idx0"], g["idx1"], tol)
+    agree = ((i0 == g["idx0"]).mean() + (i1 == g["idx1"]).mean()) / 2
+    print(f"c1 fp16: index agreement {agree:.4f}, fp16 |dZ| (significant) {tol / 2:.3g}, "
+          f"matches {int((i0 >= 0).sum())} vs {int((g['idx0'] >= 0).sum())}, unexplained {bad}")
+    assert not bad

@@ -94,3 +94,32 @@ def test_sg_empty(weight_blobs):
     Z = oracle.sg_forward(weight_blobs[1], k, np.zeros(0, np.float32), np.zeros((256, 0), np.float32),
                           k, np.zeros(0, np.float32), np.zeros((256, 0), np.float32))
     assert Z.shape == (1, 1)
+
+
+def test_sg_c1_stereo_pair(golden, weight_blobs, sg_c1_blob):
+    """The C1 stereo pair through the reference modules (SuperPoint + SuperGlue "c1" profile): the
+    oracle's SuperPoint keypoint sets / descriptors, then its SuperGlue Z, decode and the thresholded
+    DMatch list (non-empty: 100 matches above 0.2) on the fixture's features."""
+    from rspl_slam_amd import synthetic as SY
+    g = golden("sg_c1")
+    L, R = SY.stereo_pair(480, 752, seed=int(g["seed"]))
+    for img, F in ((L, g["F0"]), (R, g["F1"])):
+        s, d = oracle.sp_forward(weight_blobs[0], post.image_to_input(img))
+        compare_features(post.sp_postprocess(s, d, 0.004, 4, 400), F.astype(np.float64), desc_atol=1e-5,
+                         score_atol=1e-5)
+    F0, F1 = g["F0"].astype(np.float64), g["F1"].astype(np.float64)
+    a = post.sg_inputs(post.normalize_keypoints(F0, 752, 480))
+    b = post.sg_inputs(post.normalize_keypoints(F1, 752, 480))
+    Z = oracle.sg_forward(sg_c1_blob, *a, *b)
+    # the c1 profile's scores are ~4x the default's (final_proj x2): fp32 accumulation noise between
+    # PyTorch's and the oracle's sums scales with them -- Z within 1.5e-3 (measured 1.0e-3; |Z| up to ~900),
+    # the assignment probabilities exp(Z) within 1e-4 (measured 8.4e-5), every decision identical
+    np.testing.assert_allclose(Z, g["Z"], atol=1.5e-3, rtol=0)
+    np.testing.assert_allclose(np.exp(Z.astype(np.float64)), np.exp(g["Z"].astype(np.float64)), atol=1e-4, rtol=0)
+    i0, i1, m0, m1 = post.decode(Z)
+    np.testing.assert_array_equal(i0, g["idx0"])
+    np.testing.assert_array_equal(i1, g["idx1"])
+    mt, md = post.match_points(i0, i1, m0, m1)
+    assert len(mt) == len(g["matches"]) >= 80
+    np.testing.assert_array_equal(mt, g["matches"])
+    np.testing.assert_allclose(md, g["distances"], atol=1e-4)  # 1 - (ms0 + ms1) / 2: the probability tolerance

@@ -62,12 +62,37 @@ def run_sg(torch, sg, F0, F1, width, height):
     return Z[0].numpy()
 
 
+def gen_sg_c1(torch, superglue, sp):
+    """C1 stereo pair (synthetic.stereo_pair seed 300, 480x752, k = 400) through the reference modules:
+    SuperPoint (seeded weights) on both images + the host post-processing restatement, then SuperGlue with
+    the "c1" weight profile (weights.SG_WEIGHT_GAIN_C1: matches above the 0.2 threshold), decode and
+    PointMatching's DMatches.  Features are rounded to float32 (SuperGlue::process_input packs floats)."""
+    sgc = superglue.SuperGlue().eval()
+    sgc.load_state_dict({k: torch.from_numpy(v) for k, v in W.superglue_synth(2, "c1").items()}, strict=False)
+    L, R = SY.stereo_pair(480, 752, seed=300)
+    F = []
+    for img in (L, R):
+        s, d = run_sp(torch, sp, img)
+        F.append(post.sp_postprocess(s, d, 0.004, 4, 400).astype(np.float32).astype(np.float64))
+    Z = run_sg(torch, sgc, F[0], F[1], 752, 480)
+    idx0, idx1, ms0, ms1 = post.decode(Z)
+    mt, md = post.match_points(idx0, idx1, ms0, ms1)
+    np.savez_compressed(OUT / "sg_c1.npz", seed=300, F0=F[0].astype(np.float32), F1=F[1].astype(np.float32),
+                        width=752, height=480, Z=Z, idx0=idx0, idx1=idx1, ms0=ms0, ms1=ms1, matches=mt,
+                        distances=md)
+    print("sg_c1", Z.shape, "matches", len(mt))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref", default="/root/reference")
+    ap.add_argument("--only", default=None, help="generate one fixture only (sg_c1)")
     args = ap.parse_args()
     OUT.mkdir(parents=True, exist_ok=True)
     torch, superpoint, superglue, sp, sg = load_reference(args.ref)
+    if args.only == "sg_c1":
+        gen_sg_c1(torch, superglue, sp)
+        return
 
     # 1. SP-small: 64x96, k=32 -----------------------------------------------------------
     img = SY.textured_image(64, 96, seed=1, n_blobs=8)
@@ -156,6 +181,9 @@ def main():
                                                      "gnn.layers.17.mlp.3.weight", "final_proj.weight"]})
     np.savez_compressed(OUT / "weights_pin.npz", **{k.replace(".", "__"): v for k, v in pins.items()})
     print("weights_pin")
+
+    # 8. C1 stereo pair with the "c1" SuperGlue profile -------------------------------------
+    gen_sg_c1(torch, superglue, sp)
 
 
 if __name__ == "__main__":

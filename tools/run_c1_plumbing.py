@@ -12,12 +12,16 @@ the container) through the keyframe front end twice, and the two compared pair b
       path), the merge passes in native C++ -- and the fp16 (TensorRT kFP16-equivalent) front end.
 
 Per pair it records keypoint agreement, descriptor error, the log-assignment Z error, match agreement
-(fp32 and fp16) and the agreement of the stereo line association.  The weights are the seeded
-synthetic ones (no trained weights exist here), so SuperGlue's matching probabilities stay below the
-reference's 0.2 threshold (super_glue.cpp:355) on these scenes: the thresholded match lists are
-empty on both paths.  The pipeline is therefore also compared on the mutual nearest neighbours of Z
-with the threshold at 0 (decode's mutual check and argmaxes, point_matching.cc:24-31), and those
-pairs feed the stereo line association.  MapBuilder / tracking are not built (out of scope); the
+(fp32 and fp16) and the agreement of the stereo line association.  The weights are seeded synthetic
+ones (no trained weights exist here): SuperPoint's default profile, and SuperGlue's "c1" profile
+(weights.SG_WEIGHT_GAIN_C1), under which 25-38 % of the keypoints are matched above the reference's
+0.2 threshold (super_glue.cpp:355) -- so the thresholded decode and the DMatch distances are compared
+pair by pair (the default profile left every probability below 0.2 here).  The mutual nearest
+neighbours of Z with the threshold at 0 are compared too, and feed the stereo line association.
+fp16 (the TensorRT kFP16 analogue) is checked twice: fp16 SuperGlue on the CPU path's features (every
+index disagreement must sit at a near-tie of the CPU Z within twice the measured fp16 |dZ|:
+helpers.unexplained_match_disagreements), and fp16 SuperPoint + SuperGlue end to end (keypoint overlap
+per image, match agreement by coordinates).  MapBuilder / tracking are not built (out of scope); the
 map-side BA over a 100-keyframe sequence is tools/run_sequence.py.  Prints one JSON line; per-pair
 records go to --out."""
 import argparse
@@ -31,10 +35,12 @@ import numpy as np
 ROOT = pathlib.Path(__file__).resolve().parents[1]
 sys.path.insert(0, str(ROOT))
 sys.path.insert(0, str(ROOT / "oracle"))
+sys.path.insert(0, str(ROOT / "tests"))
 import rspl_loader  # noqa: E402
 
 pkg = rspl_loader.load()
 pkg.capi.load()
+from helpers import unexplained_match_disagreements  # noqa: E402  (test infrastructure)
 import lines_ref as LR  # noqa: E402  (the CPU path being compared against; test infrastructure)
 import oracle  # noqa: E402
 import post  # noqa: E402
@@ -88,7 +94,8 @@ def main():
     ap.add_argument("--out", default="gpurun_out/c1_pairs.jsonl")
     a = ap.parse_args()
     oracle.set_threads(a.threads)
-    sp_w, sg_w = pkg.weights.ensure_blobs(str(ROOT / "weights"))
+    sp_w, _ = pkg.weights.ensure_blobs(str(ROOT / "weights"))
+    sg_w = pkg.weights.ensure_sg_profile_blob(str(ROOT / "weights"), "c1")
     bf = pkg.synthetic.EUROC_BF
     lim = (bf / 10.0, bf / 0.1, 2.0)  # MinXDiff, MaxXDiff, MaxYDiff (camera.cc:21-22)
     C = pkg.capi
@@ -140,6 +147,16 @@ def main():
                 if name == "fp32":
                     t_gpu += time.perf_counter() - t0
                 res[name] = (Fg, mg, nng, Zg, l0g, lrg, lvg)
+            # fp16 SuperGlue on the CPU path's own features: its disagreements vs the CPU Z must be near-ties
+            n16, ml16 = pms["fp16"].MatchingPoints(Fc[0], Fc[1])
+            Z16 = pms["fp16"].superglue.debug_scores(0, Fc[0].shape[1], Fc[1].shape[1])
+            d16 = post.decode(Z16)
+            dc = post.decode(Z)
+            sig = Z > np.log(1e-4)
+            dz16 = float(np.abs(Z16 - Z)[sig].max()) if sig.any() else 0.0
+            bad16 = unexplained_match_disagreements(Z, d16[0], d16[1], dc[0], dc[1], 2.0 * dz16)
+            agree16_idx = float(((d16[0] == dc[0]).mean() + (d16[1] == dc[1]).mean()) / 2)
+            m16 = match_set(np.array([(q, tt) for q, tt, _ in ml16], np.int32).reshape(-1, 2))
             Fg, mg, nng, Zg, l0g, lrg, lvg = res["fp32"]
             kc, kg = key_index(Fc[0]), key_index(Fg[0])
             common = sorted(set(kc) & set(kg))
@@ -157,6 +174,11 @@ def main():
             dp16, _ = z_errors(za16, Z) if za16 is not None else (float("nan"), float("nan"))
             order_same = all(np.array_equal(Fg[i][1:3], Fc[i][1:3]) for i in (0, 1) if Fg[i].shape == Fc[i].shape)
             lines_same = l0g.shape == l0c.shape and bool(np.array_equal(l0g, l0c))
+            F16e = res["fp16"][0]
+            overlap16 = [len(set(key_index(F16e[i])) & set(key_index(Fc[i]))) / max(1, Fc[i].shape[1]) for i in (0, 1)]
+            dist_c = {(int(q), int(tt)): d for (q, tt), d in zip(np.asarray(mc).reshape(-1, 2), post.match_points(*dc)[1])}
+            dist_g = {(int(q), int(tt)): d for q, tt, d in pms["fp32"].MatchingPoints(Fg[0], Fg[1])[1]}
+            dist_err = max((abs(dist_c[k] - dist_g[k]) for k in dist_c if k in dist_g), default=0.0)
             row = {"pair": t,
                    "keypoints": [int(Fc[0].shape[1]), int(Fc[1].shape[1])],
                    "keypoint_sets_identical": bool(set(kc) == set(kg)) and
@@ -166,6 +188,12 @@ def main():
                    "Z_max_abs_diff_fp32": zerr,
                    "P_max_abs_diff_fp32": dp, "Z_sig_max_abs_diff_fp32": dzs, "P_max_abs_diff_fp16": dp16,
                    "matches_cpu": len(sc_), "matches_gpu_fp32": len(sg_), "matches_identical": sc_ == sg_,
+                   "matches_identical_coords": match_coords(mc, Fc[0], Fc[1]) == match_coords(mg, Fg[0], Fg[1]),
+                   "match_distance_max_abs_diff_fp32": float(dist_err),
+                   "sg16_on_cpu_features": {"matches": int(n16), "matches_identical": m16 == sc_,
+                                            "index_agreement": agree16_idx, "dZ_sig_max": dz16,
+                                            "unexplained_disagreements": len(bad16)},
+                   "keypoint_overlap_fp16": overlap16,
                    "mutual_nn_cpu": len(nc_),
                    "match_agreement_fp32": len(nc_ & ng_) / max(1, len(nc_ | ng_)),
                    "match_agreement_fp32_coords": len(cc_ & cg_) / max(1, len(cc_ | cg_)),
@@ -194,7 +222,22 @@ def main():
         "P_max_abs_diff_fp16": float(np.nanmax([r["P_max_abs_diff_fp16"] for r in rows])),
         "keypoint_sets_identical_fp16_frac": agg("keypoint_sets_identical_fp16"),
         "thresholded_matches_identical_frac": agg("matches_identical"),
+        "thresholded_matches_identical_coords_frac": agg("matches_identical_coords"),
+        "match_distance_max_abs_diff_fp32": float(max(r["match_distance_max_abs_diff_fp32"] for r in rows)),
         "matches_per_pair_cpu": agg("matches_cpu"),
+        "matches_per_pair_min_cpu": int(min(r["matches_cpu"] for r in rows)),
+        "sg_fp16_on_cpu_features": {
+            "index_agreement_mean": float(np.mean([r["sg16_on_cpu_features"]["index_agreement"] for r in rows])),
+            "index_agreement_min": float(min(r["sg16_on_cpu_features"]["index_agreement"] for r in rows)),
+            "thresholded_matches_identical_frac": float(np.mean([r["sg16_on_cpu_features"]["matches_identical"]
+                                                                 for r in rows])),
+            "dZ_sig_max": float(max(r["sg16_on_cpu_features"]["dZ_sig_max"] for r in rows)),
+            "unexplained_disagreements_total": int(sum(r["sg16_on_cpu_features"]["unexplained_disagreements"]
+                                                       for r in rows)),
+            "note": "fp16 SuperGlue on the CPU path's features vs the CPU Z; a disagreement is explained when the "
+                    "CPU Z shows a near-tie (argmax runner-up or the 0.2 threshold) within 2x the pair's fp16 |dZ|"},
+        "keypoint_overlap_fp16_mean": float(np.mean([np.mean(r["keypoint_overlap_fp16"]) for r in rows])),
+        "keypoint_overlap_fp16_min": float(min(min(r["keypoint_overlap_fp16"]) for r in rows)),
         "mutual_nn_per_pair_cpu": agg("mutual_nn_cpu"),
         "match_agreement_fp32_mean": agg("match_agreement_fp32"),
         "match_agreement_fp32_min": float(min(r["match_agreement_fp32"] for r in rows)),
@@ -205,6 +248,7 @@ def main():
         "right_lines_valid_per_pair": agg("right_lines_valid_cpu"),
         "cpu_s_per_pair": round(t_cpu / len(rows), 3), "cpu_threads": a.threads,
         "gpu_fp32_host_api_s_per_pair": round(t_gpu / len(rows), 4),
+        "weights": "SuperPoint seeded default profile; SuperGlue seeded 'c1' profile (weights.SG_WEIGHT_GAIN_C1)",
         "note": "synthetic stereo pairs (EuRoC absent); the CPU path is the oracle restatement of the "
                 "reference's SP/SG modules + host code; GPU = librspl through its host-array API"}))
 
