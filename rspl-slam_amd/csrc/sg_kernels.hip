@@ -1329,6 +1329,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_kernel(SinkArgs a) {
       Cs[(size_t)c * ld + r] = Cg[(size_t)r * ld + c0 + c];
     }
   for (int j = tid; j < Cc; j += kSinkThreads) v[j] = 0.f;
+  for (int j = tid; j < R; j += kSinkThreads) u[j] = 0.f;  // iters == 0: Z = C - norm (u = v = 0)
   // log_mu / log_nu (superglue.py:198-200), float arithmetic as the module
   const float fm = (float)m, fn = (float)n;
   const float norm = -logf(fm + fn);
@@ -1439,6 +1440,8 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
 #pragma unroll
   for (int q = 0; q < kRbQ; q++) vr[q] = 0.f;
   float ur[RPW];
+#pragma unroll
+  for (int k = 0; k < RPW; k++) ur[k] = 0.f;  // iters == 0: Z = C - norm (u = v = 0)
   const int nk = min(RPW, max(0, (nr - wv + 15) / 16));  // the wave's rows inside the slab
   // log_mu / log_nu (superglue.py:198-200), float arithmetic as the module
   const float fm = (float)m, fn = (float)n;
