@@ -845,32 +845,61 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   mark("vertices");
   int* fill = b->lm_cnt.data();  // reused as the per-landmark fill cursor
   for (int g = 0; g < nL; g++) fill[g] = lm_off[g];
-  int eg = 0;
-  // one instantiation per edge type (D observation doubles: 2, 3, 4, 8)
-  auto scatter = [&](auto dc, int t) {
-    constexpr int D = decltype(dc)::value;
-    const int n = ne[t], loff = t < 2 ? 0 : nq;
-    const int32_t *pt = poses[t], *lt = lms[t], *ct = cams[t];
-    const double* ob = obs[t];
-    for (int i = 0; i < n; i++, eg++) {
-      if (sh && !owned(t, i)) continue;
-      const int g = loff + lt[i], k = fill[g]++, p = pt[i];
+  // pass 2a: the CSR permutation only -- each local edge's caller id at its CSR position (input order
+  // within a landmark: the order every per-landmark reduction follows); one random store per edge
+  {
+    int eg = 0;
+    for (int t = 0; t < 4; t++) {
+      const int n = ne[t], loff = t < 2 ? 0 : nq;
+      const int32_t* lt = lms[t];
+      if (!sh) {
+        for (int i = 0; i < n; i++) gmap[fill[loff + lt[i]]++] = eg + i;
+      } else {
+        for (int i = 0; i < n; i++)
+          if (owned(t, i)) gmap[fill[loff + lt[i]]++] = eg + i;
+      }
+      eg += n;
+    }
+  }
+  // pass 2b: every staged array written sequentially in CSR order, gathered from the caller's arrays
+  // (point edges: mono / stereo picked without a branch; the third observation of a mono edge is 0)
+  {
+    const int e1 = ne[0], e2 = ne[0] + ne[1], e3 = e2 + ne[2];
+    static const double zero = 0.0;
+    for (int k = 0; k < Ep; k++) {
+      const int eg = gmap[k];
+      const bool st = eg >= e1;
+      const int i = st ? eg - e1 : eg;
+      const int32_t* pt = st ? poses[1] : poses[0];
+      const int32_t* ct = st ? cams[1] : cams[0];
+      const int p = pt[i];
+      etype[k] = (int8_t)st;
+      epose[k] = p;
+      elm[k] = (st ? lms[1] : lms[0])[i];
+      ecam[k] = ct ? ct[i] : 0;
+      lpose[k] = pidx[p];
+      const double* ob = st ? obs[1] + 3 * (size_t)i : obs[0] + 2 * (size_t)i;
+      double* o = eobs + 4 * (size_t)k;
+      o[0] = ob[0];
+      o[1] = ob[1];
+      o[2] = *(st ? ob + 2 : &zero);  // no load past a mono record
+    }
+    for (int k = Ep; k < E; k++) {
+      const int eg = gmap[k];
+      const int t = eg >= e3 ? 3 : 2;
+      const int i = eg - (t == 3 ? e3 : e2);
+      const int p = poses[t][i];
       etype[k] = (int8_t)t;
       epose[k] = p;
-      elm[k] = g;
-      ecam[k] = ct ? ct[i] : 0;
-      gmap[k] = eg;
+      elm[k] = nq + lms[t][i];
+      ecam[k] = cams[t] ? cams[t][i] : 0;
       lpose[k] = pidx[p];
-      double* o = D <= 3 ? eobs + 4 * (size_t)k : lobs + 8 * (size_t)(k - Ep);
-#pragma GCC unroll 8
-      for (int q = 0; q < D; q++) o[q] = ob[(size_t)D * i + q];
-      if (D == 2) o[2] = 0.0;  // mono: no right coordinate
+      const int D = t == 3 ? 8 : 4;
+      const double* ob = obs[t] + (size_t)D * i;
+      double* o = lobs + 8 * (size_t)(k - Ep);
+      for (int q = 0; q < D; q++) o[q] = ob[q];
     }
-  };
-  scatter(std::integral_constant<int, 2>{}, 0);
-  scatter(std::integral_constant<int, 3>{}, 1);
-  scatter(std::integral_constant<int, 4>{}, 2);
-  scatter(std::integral_constant<int, 8>{}, 3);
+  }
   mark("scatter");
   uint8_t* lm_act = reinterpret_cast<uint8_t*>(sg + cl.lm_act);
   size_t pair_bound = 0;  // sum_g k_g^2 >= edge pairs of any pose pair

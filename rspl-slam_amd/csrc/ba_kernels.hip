@@ -561,6 +561,10 @@ __device__ __forceinline__ void wave_sync() {
 // sum over the kGroup lanes of a landmark group (fixed butterfly: deterministic; every
 // lane of the wave takes part)
 constexpr int kGroup = 8;
+#ifndef RSPL_UE_WAVES
+#define RSPL_UE_WAVES 4
+#endif
+constexpr int kUeWaves = RSPL_UE_WAVES;  // waves per update_errors workgroup that carry landmark groups
 template <int N>
 __device__ __forceinline__ void group_sum(double (&v)[N]) {
 #pragma unroll
@@ -1679,8 +1683,8 @@ __device__ __forceinline__ double readlane64(double v, int l) {
 }
 
 struct WaveSolveLds {
-  double col[2][64];  // column broadcast, double-buffered by step parity
-  double Lm[60][61];  // Lm[j][i] = l_ij (column j of L); odd stride
+  double W[2][64][6];  // the panel's unscaled column entries w_ij of row i, double-buffered by block parity
+  double Lm[60][61];   // Lm[j][i] = l_ij (column j of L); odd stride
 };
 
 // pose pair index of (c, a), c <= a, row-major upper triangle of K poses
@@ -1700,15 +1704,16 @@ __device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys
   double z = 0.0, bpl = 0.0;
   {
     const int dg = 48 * pair_index(pa, pa, K);
+    // branch-free: every lane issues all N loads (lanes / entries outside the lower triangle read
+    // slot 0 and discard it), so the loads go out back to back without exec-mask branches
 #pragma unroll
     for (int k = 0; k < N; k++) {
       const int c = k / 6, cc = k - 6 * (k / 6);
-      double v = 0.0;
-      if (row && k <= lane) {
-        if (c == pa) v = ld(dg + r * 6 + cc);
-        else v = ld(48 * pair_index(c, pa, K) + cc * 6 + r);
-      }
-      a[k] = v;
+      const bool valid = row && k <= lane;  // then c <= pa
+      int idx = c == pa ? dg + r * 6 + cc : 48 * pair_index(c, pa, K) + cc * 6 + r;
+      idx = valid ? idx : 0;
+      const double v = ld(idx);
+      a[k] = valid ? v : 0.0;
     }
     if (row) {
       bpl = ld(dg + 36 + r);
@@ -1721,25 +1726,49 @@ __device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys
   // damping on the diagonal (a[k] with k == lane: select, static register index)
 #pragma unroll
   for (int k = 0; k < N; k++) a[k] += (k == lane) ? lambda : 0.0;
+  // Right-looking LDL^T blocked by the 6x6 pose blocks.  Panel b (pivots j = 6b .. 6b + 5): each lane
+  // updates its own row's panel entries, the column entries of the panel's later rows broadcast by
+  // readlane (no LDS on the pivot chain); then the lane's unscaled panel entries w_ij go to LDS once
+  // (one wave_sync per pose block instead of per pivot) and every lane applies the rank-6 update
+  // a_ik -= sum_j l_ij w_kj to its later columns k, j ascending -- the same FMAs in the same order as
+  // the unblocked elimination.
   bool ok = true;
 #pragma unroll
-  for (int j = 0; j < N; j++) {
-    const double dj = readlane64(a[j], j);
-    ok = ok && dj > 0.0;
-    const double rj = rcp64(dj);
-    const double wij = a[j];
-    const double l = lane > j ? wij * rj : 0.0;
-    w.col[j & 1][lane] = wij;
-    w.Lm[j][lane] = l;
-    const double zj = readlane64(z, j);
-    z = fma(-l, zj, z);
-    wave_sync();
-    // the column's entries below the pivot: every LDS read issued before the first use (one wait)
-    double wk[N];
+  for (int b = 0; b < K; b++) {
+    double l6[6], w6[6];
 #pragma unroll
-    for (int k = j + 1; k < N; k++) wk[k] = w.col[j & 1][k];
+    for (int jj = 0; jj < 6; jj++) {
+      const int j = 6 * b + jj;
+      const double dj = readlane64(a[j], j);
+      ok = ok && dj > 0.0;
+      const double rj = rcp64(dj);
+      const double wij = a[j];
+      const double l = lane > j ? wij * rj : 0.0;
+      w6[jj] = wij;
+      l6[jj] = l;
+      w.Lm[j][lane] = l;
+      const double zj = readlane64(z, j);
+      z = fma(-l, zj, z);
 #pragma unroll
-    for (int k = j + 1; k < N; k++) a[k] = fma(-l, wk[k], a[k]);
+      for (int c = j + 1; c < 6 * b + 6; c++) a[c] = fma(-l, readlane64(wij, c), a[c]);
+    }
+    if (b + 1 < K) {
+#pragma unroll
+      for (int jj = 0; jj < 6; jj++) w.W[b & 1][lane][jj] = w6[jj];
+      wave_sync();
+#pragma unroll
+      for (int kb = b + 1; kb < K; kb++) {  // one later pose block (6 columns) at a time
+        double wk[6][6];
+#pragma unroll
+        for (int c = 0; c < 6; c++)
+#pragma unroll
+          for (int jj = 0; jj < 6; jj++) wk[c][jj] = w.W[b & 1][6 * kb + c][jj];
+#pragma unroll
+        for (int c = 0; c < 6; c++)
+#pragma unroll
+          for (int jj = 0; jj < 6; jj++) a[6 * kb + c] = fma(-l6[jj], wk[c][jj], a[6 * kb + c]);
+      }
+    }
   }
   if (!ok) {
     if (lane == 0) atomicOr(S.fail, 1);
@@ -2009,6 +2038,8 @@ __device__ __forceinline__ void load_pair(const Lin& L, const Active& A, const S
     for (int i = 0; i < 6; i++) o.bpv[i] = L.bp[6 * e1 + i];
 #pragma unroll
     for (int i = 0; i < LD; i++) o.blv[i] = S.bl[4 * g + i];
+#pragma unroll
+    for (int i = 0; i < 6 * LD; i++) o.H2[i] = o.H1[i];  // e2 == e1: one schur_pair call site below
   } else {
 #pragma unroll
     for (int r = 0; r < 6; r++)
@@ -2030,8 +2061,9 @@ __device__ __forceinline__ void use_pair(const PairOps<LD>& o, double lambda, bo
   } else {
     bad |= !lm_dinv(o.D, o.pt, lambda, D);
   }
-  if (o.diag) schur_pair<LD, LOWER>(o.H1, o.H1, true, o.Hp, o.bpv, o.blv, D, acc);
-  else schur_pair<LD, LOWER>(o.H1, o.H2, false, o.Hp, o.bpv, o.blv, D, acc);
+  // one call site with B = H2 (a copy of H1 on the diagonal): two call sites on H1 / H2 were merged
+  // by the compiler into one through a selected pointer, which put both arrays in scratch memory
+  schur_pair<LD, LOWER>(o.H1, o.H2, o.diag, o.Hp, o.bpv, o.blv, D, acc);
 }
 
 template <int LD, bool LOWER>
@@ -2353,8 +2385,10 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
   // picks the current bank), so that read is not a round trip of its own.
   __shared__ double sT[64 * 8], scam[16 * 5], sx[6 * 32];
   const int tid = threadIdx.x;
-  const int t = blockIdx.x * 256 + tid, g = t / kGroup, j = t % kGroup;
-  const bool in = g < A.nL;
+  // kUeWaves of the 4 waves carry landmark groups: fewer landmarks per workgroup spread the groups over
+  // more CUs (the others only stage the block's poses and take part in the barriers)
+  const int t = blockIdx.x * (64 * kUeWaves) + tid, g = t / kGroup, j = t % kGroup;
+  const bool in = tid < 64 * kUeWaves && g < A.nL;
   const bool point = g < P.nq;
   int k0 = 0, k1 = 0;
   bool act = false;
@@ -2784,7 +2818,9 @@ hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& 
   return hipGetLastError();
 }
 
-int update_errors_blocks(const Active& A) { return A.nL > 0 ? (A.nL * kGroup + 255) / 256 : 1; }
+int update_errors_blocks(const Active& A) {
+  return A.nL > 0 ? (A.nL * kGroup + 64 * kUeWaves - 1) / (64 * kUeWaves) : 1;
+}
 
 hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool with_maxdiag,
                      hipStream_t s) {

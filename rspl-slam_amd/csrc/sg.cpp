@@ -44,6 +44,7 @@ struct rspl_sg {
   unsigned long long *ug, *vg;  // Sinkhorn u / v exchange granules [B][ld] (row-block: ug = [B][2][rbG][ld])
   int rbG = 0;                  // row-block Sinkhorn workgroups per pair (0: slab kernel)
   bool sink_sc = false;         // with rbG: the scaling-form kernel (default), else the log-domain row-block kernel
+  bool sink_wide = false;       // with sink_sc: the wide two-hop kernel (640 < nmax + 1 <= 2112)
   float* cplT = nullptr;        // transposed column slabs when they exceed LDS [B][ld*ld]
   bool sink_scratch = false;
   unsigned* err = nullptr;      // [B] sticky Sinkhorn timeout flags, host-mapped (rspl_sg_status)
@@ -71,6 +72,16 @@ struct rspl_sg {
 };
 
 namespace {
+
+// Sinkhorn exchange granules: ug = [B][ld] (slab), [B][2][rbG][ld] (row-block / scaling form) or the wide
+// kernel's hop-1 buffers [B][2][G][G][cs]; vg = [B][ld] or the wide kernel's hop-2 buffers [B][2][G cs]
+size_t ug_len(const rspl_sg* s) {
+  if (s->sink_wide) return (size_t)s->B * sg::sinkhorn_wide_hop1_len(s->nmax);
+  return (size_t)s->B * s->ld * (s->rbG ? 2 * s->rbG : 1);
+}
+size_t vg_len(const rspl_sg* s) {
+  return s->sink_wide ? (size_t)s->B * sg::sinkhorn_wide_hop2_len(s->nmax) : (size_t)s->B * s->ld;
+}
 
 template <typename F>
 void carve(F& ar, rspl_sg* s) {
@@ -104,7 +115,7 @@ void carve(F& ar, rspl_sg* s) {
     take(s->Qf[i], T * 256); take(s->Kf[i], (size_t)B * 2 * 256 * s->ldv); take(s->Vf[i], (size_t)B * 2 * 256 * s->ldv);
   }
 
-  take(s->cpl, 2 * B * ld * ld); take(s->Z, 2 * B * ld * ld); take(s->ug, B * ld * (s->rbG ? 2 * s->rbG : 1)); take(s->vg, B * ld);
+  take(s->cpl, 2 * B * ld * ld); take(s->Z, 2 * B * ld * ld); take(s->ug, ug_len(s)); take(s->vg, vg_len(s));
   if (s->sink_scratch) take(s->cplT, B * ld * ld);
   take(s->dbg_alpha, 4);
   take(s->cn0, 2 * B); take(s->cn1, 2 * B);
@@ -265,6 +276,7 @@ static hipError_t run_sinkhorn(rspl_sg* s, const float* cpl, float* Zp, const in
   sk.spin_limit = s->spin_limit; sk.inject = s->inject;
   sk.err = s->d_err; sk.n0 = cn0; sk.n1 = cn1;
   sk.nmax = s->nmax; sk.G = s->rbG ? s->rbG : s->G; sk.rb = s->rbG > 0; sk.sc = s->sink_sc; sk.iters = iters;
+  sk.wide = s->sink_wide;
   sk.fx = 1;
   sk.sleep = 1;
   return sg::sinkhorn(sk, B, st, t0, t1);
@@ -327,6 +339,15 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
         if (const char* e = getenv("RSPL_SG_SINK_G")) g = std::max(1, atoi(e));
         if (g * s->B <= ncu && sg::sinkhorn_sc10_ok(s->nmax, g)) s->rbG = g;
       }
+      // 640 < nmax + 1 <= 2112 (C5's 2048 keypoints): the wide scaling-form kernel, 32 rows per workgroup,
+      // the column exchange in two hops (reduce-scatter to the column owners, broadcast of V)
+      if (!s->rbG && s->sink_sc) {
+        const int g = sg::sinkhorn_wide_groups(s->nmax);
+        if (g * s->B <= ncu && sg::sinkhorn_wide_ok(s->nmax, g)) {
+          s->rbG = g;
+          s->sink_wide = true;
+        }
+      }
     }
     if (s->B * s->G > ncu && !s->rbG) {
       set_error("max_batch (%d) exceeds the CU count (%d): the Sinkhorn workgroups must be co-resident", s->B, ncu);
@@ -338,8 +359,8 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
   carve(sz, s);
   if ((rc = s->arena.reserve(sz.used))) { delete s; return rc; }
   carve(s->arena, s);
-  if (hipMemset(s->ug, 0, sizeof(unsigned long long) * s->B * s->ld * (s->rbG ? 2 * s->rbG : 1)) != hipSuccess ||
-      hipMemset(s->vg, 0, sizeof(unsigned long long) * s->B * s->ld) != hipSuccess ||
+  if (hipMemset(s->ug, 0, sizeof(unsigned long long) * ug_len(s)) != hipSuccess ||
+      hipMemset(s->vg, 0, sizeof(unsigned long long) * vg_len(s)) != hipSuccess ||
       hipMemset(s->Vth, 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess ||
       hipMemset(s->Kf[0], 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess ||
       hipMemset(s->Kf[1], 0, sizeof(_Float16) * s->B * 2 * 256 * s->ldv) != hipSuccess ||

@@ -1849,6 +1849,288 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_sc_kernel(SinkArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Wide scaling-form Sinkhorn (640 < nmax + 1 <= 64 Q: C5's 2048 keypoints), the same iteration as
+// sinkhorn_sc_kernel (K = exp(C + a + b) register resident for whole rows, plain sums, scalings absorbed
+// into the log potentials outside [2^-60, 2^60]) on G = ceil(ld / (8 RPW)) workgroups of 512 threads per
+// pair: wave w owns rows w + 8 k (k < RPW), lane L columns L + 64 q.  An all-gather of per-column
+// partials would move G x ld granules into every workgroup per iteration (G ~ 65), so the column pass
+// exchanges in TWO hops:
+//   hop 1 (reduce-scatter): every workgroup publishes its partial sum of column j to the column's owner
+//     o = j / cs (cs = ceil(ld / G) <= 64 columns per owner), laid out [parity][owner][source][cs] so an
+//     owner's inputs are one contiguous run; the owner sums its columns over the G sources in a fixed
+//     order (source subsets g = w (mod 8) per wave, then the 8 wave sums in wave order) and forms V_j;
+//   hop 2 (broadcast): the owner publishes V_j, every workgroup reads all of V into LDS.
+// Every workgroup therefore holds a bit-identical V (and takes the same column absorption decisions).
+// Parity reuse: a workgroup writes hop 1 of iteration it + 2 only after reading all of V(it + 1), which
+// an owner publishes only after it has read every hop-1 input of it + 1 (and of it before that); the
+// owner writes V(it + 2) only after every source's hop 1 of it + 2, which follows their reads of V(it).
+// ---------------------------------------------------------------------------
+constexpr int kWThreads = 512;  // 8 waves: two per SIMD at <= 256 VGPRs, the partial-sum table fits LDS
+constexpr int kWideRPW = 4, kWideQ = 33;  // 32 rows per workgroup, 2112 columns
+
+bool sinkhorn_wide_ok(int nmax, int G) {
+  const int ld = nmax + 1;
+  return ld > 640 && ld <= kWideQ * 64 && G == (ld + 8 * kWideRPW - 1) / (8 * kWideRPW) && (ld + G - 1) / G <= 64;
+}
+int sinkhorn_wide_groups(int nmax) { return (nmax + 1 + 8 * kWideRPW - 1) / (8 * kWideRPW); }
+size_t sinkhorn_wide_hop1_len(int nmax) {  // granules per pair: [2][G][G][cs]
+  const int ld = nmax + 1, G = sinkhorn_wide_groups(nmax), cs = (ld + G - 1) / G;
+  return (size_t)2 * G * G * cs;
+}
+size_t sinkhorn_wide_hop2_len(int nmax) {  // granules per pair: [2][G * cs]
+  const int ld = nmax + 1, G = sinkhorn_wide_groups(nmax), cs = (ld + G - 1) / G;
+  return (size_t)2 * G * cs;
+}
+
+template <int RPW, int Q>
+__global__ __launch_bounds__(kWThreads) void sinkhorn_w_kernel(SinkArgs a) {
+  constexpr int NW = kWThreads / 64;
+  __shared__ float ps[NW][Q * 64];  // per-wave column partial sums
+  __shared__ float vs[Q * 64];      // V (identical on every workgroup)
+  __shared__ float bs[Q * 64];      // absorbed column potentials b
+  __shared__ float as[NW * RPW];    // absorbed row potentials a (row wv + NW k)
+  __shared__ float red[NW][64];     // owner: per-wave sums over its source subset
+  __shared__ int flag[4];           // 0: exchange timeout, 1: column absorb, 2 + (it & 1): row absorb
+  const int p = blockIdx.y, g = blockIdx.x, G = gridDim.x;
+  const int m = a.n0[p], n = a.n1[p];
+  if (m <= 0 || n <= 0) return;
+  const int R = m + 1, Cc = n + 1, ld = a.nmax + 1;
+  const int rs = NW * RPW, cs = (ld + G - 1) / G;
+  const int r0 = min(R, g * rs), nr = min(R, r0 + rs) - r0;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const float* Cg = a.cpl + (size_t)p * ld * ld;
+  const int nk = min(RPW, max(0, (nr - wv + NW - 1) / NW));  // the wave's rows inside the slab
+  // row r of the slab into v[q] = C[r0 + r][lane + 64 q]: unconditional loads off one row pointer (the
+  // row clamped into the matrix, the last lane set's column clamped to ld - 1), masked afterwards --
+  // per-element conditional loads would keep an address per element live
+  auto load_row = [&](int r, float (&v)[Q]) {
+    const float* rp = Cg + (size_t)min(r0 + r, ld - 1) * ld;
+#pragma unroll
+    for (int q = 0; q < Q - 1; q++) v[q] = rp[lane + 64 * q];
+    v[Q - 1] = rp[min(lane + 64 * (Q - 1), ld - 1)];
+  };
+  float x[RPW][Q];
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int r = wv + NW * k;
+    load_row(r, x[k]);
+#pragma unroll
+    for (int q = 0; q < Q; q++) x[k][q] = (r < nr && lane + 64 * q < Cc) ? x[k][q] : -INFINITY;
+  }
+  // log_mu / log_nu (superglue.py:198-200), float arithmetic as the module; mu / nu = exp of them
+  const float fm = (float)m, fn = (float)n;
+  const float norm = -logf(fm + fn);
+  const float lmu_bin = logf(fn) + norm, lnu_bin = logf(fm) + norm;
+  const float mu_in = expf(norm), mu_bin = expf(lmu_bin), nu_bin = expf(lnu_bin);
+  constexpr float kLo = 8.6736174e-19f, kHi = 1.1529215e18f;  // 2^-60, 2^60
+  if (tid < 4) flag[tid] = 0;
+  // iteration 0, row pass in the log domain (v = 0): a = u
+  float ur[RPW];
+  {
+    float mx[RPW], sm[RPW];
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      mx[k] = x[k][0];
+#pragma unroll
+      for (int q = 1; q < Q; q++) mx[k] = fmaxf(mx[k], x[k][q]);
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; k++) mx[k] = wave_max_dpp(mx[k]);
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      sm[k] = 0.f;
+      if (k < nk)
+#pragma unroll
+        for (int q = 0; q < Q; q++) sm[k] += sk_exp<true>(x[k][q] - mx[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < RPW; k++) sm[k] = wave_sum_dpp(sm[k]);
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      const int r = wv + NW * k;
+      // (no iterations: u = v = 0, Z = C - norm as superglue.py:202-205 -- no seed)
+      if (lane == 0)
+        as[wv + NW * k] = r < nr && a.iters > 0 ? ((r0 + r) < m ? norm : lmu_bin) - (logf(sm[k]) + mx[k]) : 0.f;
+      ur[k] = 1.f;
+    }
+  }
+  for (int j = tid; j < Q * 64; j += kWThreads) {
+    bs[j] = 0.f;
+    vs[j] = 1.f;
+  }
+  __syncthreads();
+  // K = exp(C + a + b), masked entries exactly 0
+  auto build_k = [&](bool reload) {
+#pragma unroll
+    for (int k = 0; k < RPW; k++) {
+      const int r = wv + NW * k;
+      if (reload) load_row(r, x[k]);
+      const float ak = as[wv + NW * k];
+#pragma unroll
+      for (int q = 0; q < Q; q++) {
+        const int j = lane + 64 * q;
+        const bool in = r < nr && j < Cc;
+        x[k][q] = in ? sk_exp<true>((x[k][q] + ak) + bs[j]) : 0.f;
+      }
+    }
+  };
+  build_k(false);
+  unsigned long long* h1 = a.ug + (size_t)p * 2 * G * G * cs;  // [2][owner][source][cs]
+  unsigned long long* h2 = a.vg + (size_t)p * 2 * G * cs;      // [2][G * cs]
+  const int c0 = g * cs, nc = max(0, min(Cc, c0 + cs) - c0);   // the columns this workgroup owns
+  bool failed = false;
+  for (int it = 0; it < a.iters; it++) {
+    const unsigned tag = (a.seq << 12) | (unsigned)(it + 1);
+    const int par = it & 1;
+    if (it > 0) {  // row pass: U_i = mu_i / sum_j K_ij V_j (wave-local)
+      float sm[RPW];
+#pragma unroll
+      for (int k = 0; k < RPW; k++) sm[k] = 0.f;
+#pragma unroll
+      for (int q = 0; q < Q; q++) {
+        const float v = vs[lane + 64 * q];
+#pragma unroll
+        for (int k = 0; k < RPW; k++)
+          if (k < nk) sm[k] = fmaf(x[k][q], v, sm[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < RPW; k++) sm[k] = wave_sum_dpp(sm[k]);
+      bool out = false;
+#pragma unroll
+      for (int k = 0; k < RPW; k++) {
+        const int r = wv + NW * k;
+        ur[k] = r < nr ? ((r0 + r) < m ? mu_in : mu_bin) / sm[k] : 0.f;
+        out |= r < nr && !(ur[k] >= kLo && ur[k] <= kHi);
+      }
+      if (out && lane == 0) flag[2 + (it & 1)] = 1;
+    }
+    // column partials over the wave's rows, then over the 8 waves
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      float s = 0.f;
+#pragma unroll
+      for (int k = 0; k < RPW; k++)
+        if (k < nk) s = fmaf(x[k][q], ur[k], s);
+      ps[wv][lane + 64 * q] = s;
+    }
+    __syncthreads();
+    if (tid == 0) flag[2 + ((it + 1) & 1)] = 0;  // next iteration's row flag (its readers are past)
+    // hop 1: this workgroup's partial of column j to its owner
+    for (int j = tid; j < Cc; j += kWThreads) {
+      float s = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; w++) s += ps[w][j];
+      const int o = j / cs;
+      __hip_atomic_store(h1 + (((size_t)par * G + o) * G + g) * cs + (j - o * cs), sk_granule(s, tag),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // owner: lane = owned column, wave wv sums the sources g' = wv, wv + 8, ... in order
+    bool to = a.inject && p == 0 && g == 0 && it == 0;  // fault injection (rspl_sg_debug_inject)
+    if (lane < nc) {
+      constexpr int kSrc = 9;  // <= 9 sources per wave: G <= 72 (ld <= 2112 at 32 rows per workgroup)
+      const unsigned long long* src = h1 + ((size_t)par * G + g) * G * cs + lane;
+      float l[kSrc];
+      unsigned long long gv[kSrc];
+      unsigned pend = 0;
+#pragma unroll
+      for (int i = 0; i < kSrc; i++) {
+        l[i] = 0.f;
+        if (wv + NW * i < G) pend |= 1u << i;
+      }
+      unsigned spins = 0;
+      while (pend && !to) {
+#pragma unroll
+        for (int i = 0; i < kSrc; i++)
+          if (pend >> i & 1) gv[i] = __hip_atomic_load(src + (size_t)(wv + NW * i) * cs, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int i = 0; i < kSrc; i++)
+          if ((pend >> i & 1) && (unsigned)(gv[i] >> 32) == tag) {
+            l[i] = __uint_as_float((unsigned)gv[i]);
+            pend &= ~(1u << i);
+          }
+        if (!pend) break;
+        if (++spins > a.spin_limit) { to = true; break; }
+        for (int z = 0; z < a.sleep; z++) __builtin_amdgcn_s_sleep(1);
+      }
+      float T = 0.f;
+#pragma unroll
+      for (int i = 0; i < kSrc; i++) T += l[i];
+      red[wv][lane] = T;
+    }
+    if (to) flag[0] = 1;
+    __syncthreads();
+    if (wv == 0 && lane < nc) {
+      float T = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; w++) T += red[w][lane];
+      const int j = c0 + lane;
+      const float V = (j < n ? mu_in : nu_bin) / T;  // nu_j = mu_in for j < n: exp(norm)
+      __hip_atomic_store(h2 + (size_t)par * G * cs + j, sk_granule(V, tag), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // hop 2: every column's V from its owner
+    bool to2 = false;
+    for (int j = tid; j < Cc; j += kWThreads) {
+      const unsigned long long* q = h2 + (size_t)par * G * cs + j;
+      unsigned long long gv = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned spins = 0;
+      while ((unsigned)(gv >> 32) != tag && !to2) {
+        if (++spins > a.spin_limit) { to2 = true; break; }
+        for (int z = 0; z < a.sleep; z++) __builtin_amdgcn_s_sleep(1);
+        gv = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const float V = __uint_as_float((unsigned)gv);
+      vs[j] = V;
+      if (!(V >= kLo && V <= kHi)) flag[1] = 1;
+    }
+    if (to2) flag[0] = 1;
+    __syncthreads();
+    if (flag[0]) { failed = true; break; }
+    const bool col_abs = flag[1] != 0, row_abs = flag[2 + (it & 1)] != 0;
+    if (col_abs || row_abs) {  // rare: absorb the scalings into the log potentials, rebuild K from C
+      if (row_abs) {
+#pragma unroll
+        for (int k = 0; k < RPW; k++) {
+          if (lane == 0) as[wv + NW * k] += logf(ur[k] > 0.f ? ur[k] : 1.f);
+          ur[k] = 1.f;
+        }
+      }
+      if (col_abs)
+        for (int j = tid; j < Q * 64; j += kWThreads) {
+          bs[j] += logf(vs[j] > 0.f && j < Cc ? vs[j] : 1.f);
+          vs[j] = 1.f;
+        }
+      __syncthreads();
+      build_k(true);
+      __syncthreads();  // every thread has read flag[1] before it is cleared
+      if (tid == 0) flag[1] = 0;
+      __syncthreads();
+    }
+  }
+  if (failed) {
+    if (tid == 0) __hip_atomic_store(a.err + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    return;
+  }
+  // Z = ((couplings + u) + v) - norm (superglue.py:203, :219), own rows; u = a + log U, v = b + log V
+  float* Z = a.Z + (size_t)p * ld * ld;
+#pragma unroll
+  for (int k = 0; k < RPW; k++) {
+    const int r = wv + NW * k;
+    if (r >= nr) continue;
+    const float u = as[wv + NW * k] + logf(ur[k]);
+    float c[Q];
+    load_row(r, c);
+    float* zr = Z + (size_t)(r0 + r) * ld;
+#pragma unroll
+    for (int q = 0; q < Q; q++) {
+      const int j = lane + 64 * q;
+      if (j < Cc) zr[j] = ((c[q] + u) + (bs[j] + logf(vs[j]))) - norm;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // decode (super_glue.cpp:339-367).  Pass 1: row / column argmax (strict '<'
 // from -FLT_MAX: first maximum wins).  Pass 2: mutual check, exp, threshold.
 // ---------------------------------------------------------------------------
@@ -2127,6 +2409,11 @@ int sinkhorn_rb_rpw(int nmax, int G) {
 hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s, hipEvent_t t0, hipEvent_t t1) {
   if (a.G < 1 || a.G > 1024) return hipErrorInvalidValue;
   dim3 grid(a.G, B);
+  if (a.rb && a.sc && a.wide) {  // 640 < nmax + 1 <= 2112: two-hop column exchange
+    if (!sinkhorn_wide_ok(a.nmax, a.G)) return hipErrorInvalidValue;
+    hipExtLaunchKernelGGL((sinkhorn_w_kernel<kWideRPW, kWideQ>), grid, dim3(kWThreads), 0, s, t0, t1, 0, a);
+    return hipGetLastError();
+  }
   if (a.rb && a.sc && a.nmax + 1 > kRbQ * 64) {  // 448 < nmax + 1 <= 640: ten column sets per lane
     if (!sinkhorn_sc10_ok(a.nmax, a.G)) return hipErrorInvalidValue;
     hipExtLaunchKernelGGL((sinkhorn_sc_kernel<3, 16, 10>), grid, dim3(kSinkThreads), 0, s, t0, t1, 0, a);

@@ -141,6 +141,7 @@ struct SinkArgs {
   int sleep;          // row-block kernel: s_sleep(1) units between re-polls (run_sinkhorn: 1)
   int fx;             // row-block kernel: v_exp_f32-based exp (1, what run_sinkhorn sets) or expf (0)
   int sc;             // with rb: the scaling-form kernel (register-resident exp(C + a + b), two mat-vecs per iteration)
+  int wide;           // with sc: the wide two-hop kernel (640 < nmax + 1 <= 2112; ug / vg laid out as its hop buffers)
 };
 
 struct DecodeArgs {
@@ -179,6 +180,12 @@ size_t sinkhorn_lds_bytes(int nmax, int G, bool slabs);
 int sinkhorn_rb_rpw(int nmax, int G);
 // the scaling-form kernel for 448 < nmax + 1 <= 640 (ten 64-column sets per lane) takes this G
 bool sinkhorn_sc10_ok(int nmax, int G);
+// the wide two-hop scaling-form kernel (640 < nmax + 1 <= 2112): its workgroups per pair, the check, and
+// its exchange buffers in granules per pair (hop 1 -> ug, hop 2 -> vg)
+int sinkhorn_wide_groups(int nmax);
+bool sinkhorn_wide_ok(int nmax, int G);
+size_t sinkhorn_wide_hop1_len(int nmax);
+size_t sinkhorn_wide_hop2_len(int nmax);
 constexpr size_t kSinkLdsMax = 150 * 1024;  // slab budget per workgroup (160 KB LDS per CU)
 
 }  // namespace sg

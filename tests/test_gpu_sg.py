@@ -295,6 +295,30 @@ def test_sinkhorn_sc10_vs_oracle(pkg, weight_blobs, monkeypatch, G, scale):
     np.testing.assert_allclose(Z, Zr, atol=1e-4 * max(1.0, 2 * np.abs(Zr).max() / 100), rtol=0)
 
 
+@pytest.mark.parametrize("M,N,scale", [(2048, 1900, 1.0), (2048, 2048, 30.0), (1500, 2048, 1.0)])
+def test_sinkhorn_wide_vs_oracle(pkg, weight_blobs, M, N, scale):
+    """The wide scaling-form kernel (640 < nmax + 1 <= 2112: C5's 2048 keypoints, 65 workgroups per pair,
+    the column exchange in two hops -- reduce-scatter to the column owners, broadcast of V) against the
+    oracle's log-domain Sinkhorn (superglue.py:185-205), incl. a run that forces scaling absorption
+    (scale 30) and pairs smaller than nmax in either dimension.  Z at atol 1e-4, scaled with max |Z| as
+    the 600-column test above but by 3 instead of 2: an error of the potentials u_i / v_j shifts whole
+    rows / columns of Z, and it grows with the fp32 rounding of the 2049-term sums (sqrt(2049 / 571) ~ 1.9x
+    the 600-column case: measured 5.6e-4 at max |Z| ~270 vs 1.9e-4 there); at scale 1, max |dZ| 4.8e-6."""
+    rng = np.random.default_rng(21)
+    S = (rng.normal(size=(M, N)) * scale).astype(np.float32)
+    sg = _sg(pkg, weight_blobs[1], nmax=2048)
+    ok, Z = sg.debug_sinkhorn(S, 1.0, 100)
+    assert ok, sg.error
+    assert sg.status() == (True, 0)
+    Zr = oracle.log_optimal_transport(S, 1.0, 100)
+    print(f"wide {M}x{N} scale={scale}: max |dZ| {np.abs(Z - Zr).max():.3g}")
+    np.testing.assert_allclose(Z, Zr, atol=1e-4 * max(1.0, 3 * np.abs(Zr).max() / 100), rtol=0)
+    for it in (0, 1):  # short runs incl. no iteration (Z = C - norm)
+        ok, Z = sg.debug_sinkhorn(S, 1.0, it)
+        assert ok, sg.error
+        np.testing.assert_allclose(Z, oracle.log_optimal_transport(S, 1.0, it), atol=1e-4, rtol=0)
+
+
 def _pm(pkg, blob, precision):
     return pkg.PointMatching(pkg.SuperGlueConfig(image_width=752, image_height=480, weights=blob, max_keypoints=400,
                                                  max_batch=1, precision=precision))
