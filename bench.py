@@ -7,7 +7,7 @@ step is one stereo keyframe of a synthetic EuRoC-shaped stream:
   * SuperGlue/PointMatching on 2 pairs: left(t) vs left(t-1) keyframe, left(t) vs right(t),
   * the line front end of the stereo keyframe: LineDetector::LineExtractor on both images' RCF-like edge
     maps (the restated FLD, rspl_lines_detect: GPU resize / Sobel / Canny classes, host chaining and
-    fitting, then the host merge passes) on two host threads beside SuperPoint / SuperGlue, as the
+    fitting, then the host merge passes) on two native worker threads beside SuperPoint / SuperGlue, as the
     reference's line threads run beside its point thread (src/map_builder.cc:285-290, 325-337), joined
     before the line part of Frame::AddRightFeatures (src/frame.cc:150-203): both images'
     AssignPointsToLines, the stereo-match disparity filter and MatchLines on the GPU
@@ -35,7 +35,6 @@ OIVIO-shaped 640x512 stereo, 600 keypoints, SG N=600; with --gpus 8 one sequence
 (configs[4]: synthetic 1920x1080 stereo, 2048 keypoints, SG N=2048, 30-keyframe / 10k-landmark BA).
 """
 import argparse
-import concurrent.futures
 import json
 import os
 import queue
@@ -437,18 +436,14 @@ def main():
     # which runs on the post stream after the decode (frame.cc:150-203)
     lm = pkg.lines.LineMatcher(max_lines=512, max_points=max(K, 512), device=local)
     edge_imgs = [syn.edge_stereo_pair(H, W, seed=seeds["images"][i]) for i in range(NP)]
+    # one detector handle per image, each with its native worker thread (rspl_lines_extract_async): the
+    # feature thread only submits and joins, as the reference's line threads (no Python threads)
     detectors = [pkg.lines.LineDetector(device=local) for _ in range(2)]
-    line_pool = concurrent.futures.ThreadPoolExecutor(max_workers=2)
     line_bufs = [(capi.DeviceBuffer(512 * 4 * 8), capi.DeviceBuffer(512 * 4 * 8)) for _ in range(3)]
     line_host = [None] * 3  # keeps each slot's uploaded arrays alive until the stream has read them
     lines_out, lines_valid = capi.DeviceBuffer(512 * 4 * 8), capi.DeviceBuffer(512)
     line_stats = {"detect_ms": [], "lines": []}
 
-    def detect_lines(k, img):
-        """one image's LineExtractor on this thread's detector: lines [m][4] at full size, host wall ms"""
-        t = time.perf_counter()
-        out = detectors[k].LineExtractor(img)[:512]
-        return out, (time.perf_counter() - t) * 1e3
     bf = pkg.synthetic.EUROC_BF
     cam_limits = (bf / 10.0, bf / 0.1, 2.0)  # MinXDiff, MaxXDiff, MaxYDiff (camera.cc:21-22, euroc.yaml)
 
@@ -500,11 +495,14 @@ def main():
             skip = args.skip.split(",")
             # the line threads of this keyframe, beside its SuperPoint / SuperGlue (map_builder.cc:325-337)
             eL, eR = edge_imgs[i % NP]
-            jobs = None if "lines" in skip else (line_pool.submit(detect_lines, 0, eL),
-                                                  line_pool.submit(detect_lines, 1, eR))
+            jobs = None
+            if "lines" not in skip:
+                detectors[0].submit(eL)
+                detectors[1].submit(eR)
+                jobs = detectors
             if "sp" in skip or "sg" in skip:  # diagnostics: stages left out (not a benchmark line)
                 if jobs is not None:
-                    jobs[0].result(), jobs[1].result()
+                    jobs[0].wait(), jobs[1].wait()
                 if "sp" not in skip:
                     sp.infer_device(pool.offset((i % NP) * 2 * H * W), 2, H, W, W, H * W, cur.ptr, K, ccur.ptr,
                                     st_sp.handle)
@@ -514,10 +512,13 @@ def main():
                 if "ba" not in skip:
                     ba_q.put(ba_item(i))
                 return
+            tw = time.perf_counter()
             if i >= 2:
                 ev_sg[(i - 2) % 3].wait_on(st_sp.handle)
             sp.infer_device(pool.offset((i % NP) * 2 * H * W), 2, H, W, W, H * W, cur.ptr, K, ccur.ptr, st_sp.handle)
             ev_sp[slot].record(st_sp.handle)
+            host_wait["sp_calls"] += time.perf_counter() - tw
+            tw = time.perf_counter()
             ev_sp[slot].wait_on(st_sg.handle)
             # PointMatching pairs: (L_t, L_kf) and (L_t, R_t)
             capi.memcpy_d2d(f0.ptr, cur.ptr, FB, st_sg.handle)
@@ -530,11 +531,15 @@ def main():
             capi.memcpy_d2d(n1.offset(4), ccur.offset(4), 4, st_sg.handle)
             sg.infer_device(2, f0.ptr, n0.ptr, f1.ptr, n1.ptr, K, True, outs[0].ptr, outs[1].ptr, outs[2].ptr,
                             outs[3].ptr, st_sg.handle, post_stream=st_post.handle)
+            host_wait["sg_calls"] += time.perf_counter() - tw
             # stereo line association of frame t: the joined line threads' lines, SP's device records of
             # (left, right) and SG's match index of pair 1 (left(t) -> right(t)), stream-ordered behind the
             # decode
             if jobs is not None:
-                (L0, t0ms), (L1, t1ms) = jobs[0].result(), jobs[1].result()
+                tw = time.perf_counter()
+                (L0, t0ms), (L1, t1ms) = jobs[0].wait(), jobs[1].wait()
+                L0, L1 = L0[:512], L1[:512]
+                host_wait["lines"] += time.perf_counter() - tw
                 if line_t0 is not None:
                     line_stats["detect_ms"].append(max(t0ms, t1ms))
                     line_stats["lines"].append(len(L0) + len(L1))
@@ -544,6 +549,7 @@ def main():
                     dl0.upload(L0, st_post.handle)
                 if len(L1):
                     dl1.upload(L1, st_post.handle)
+                tw = time.perf_counter()
                 tm = line_timers[i - line_t0] if line_t0 is not None else None
                 if tm is not None:
                     tm.start(st_post.handle)
@@ -551,13 +557,17 @@ def main():
                                        cam_limits, lines_out.ptr, lines_valid.ptr, st_post.handle)
                 if tm is not None:
                     tm.stop(st_post.handle)
+                host_wait["line_assoc_calls"] += time.perf_counter() - tw
             ev_sg[slot].record(st_post.handle)  # matches and lines complete on the post stream
             # keyframe i's local BA goes to the tracking thread (own high-priority stream) through a
             # 2-deep buffer, as the reference's feature thread blocks only while
             # _tracking_data_buffer.size() >= 2 (src/map_builder.cc:176)
             if "ba" not in skip:
+                tw = time.perf_counter()
                 ba_q.put(ba_item(i))
+                host_wait["ba_queue"] += time.perf_counter() - tw
 
+        host_wait = {"lines": 0.0, "ba_queue": 0.0, "sp_calls": 0.0, "sg_calls": 0.0, "line_assoc_calls": 0.0}
         line_t0 = None
         for i in range(args.warmup):
             step(i)
@@ -575,6 +585,8 @@ def main():
         line_stats["detect_ms"].clear()
         line_stats["lines"].clear()
         line_t0 = args.warmup
+        for k in host_wait:
+            host_wait[k] = 0.0
         ba.kernel_timing(ktime_every)
         ba.kernel_times()  # reset
         t0 = time.perf_counter()
@@ -608,7 +620,8 @@ def main():
                 "stages": (sp, sg), "ba_ms": list(ba_ms), "ba_iters": list(ba_iters), "lines_ms": lines_ms,
                 "lines_detect_ms": float(np.mean(line_stats["detect_ms"])) if line_stats["detect_ms"] else None,
                 "lines_per_step": float(np.mean(line_stats["lines"])) if line_stats["lines"] else None,
-                "ba_kt": ba_kt, "ba_timed_calls": (ba_calls + ktime_every - 1) // ktime_every if ktime_every else 0}
+                "ba_kt": ba_kt, "ba_timed_calls": (ba_calls + ktime_every - 1) // ktime_every if ktime_every else 0,
+                "host_wait_ms": {k: round(v * 1e3 / args.steps, 4) for k, v in host_wait.items()}}
 
     res = measure(args.precision)
     other = measure(precs[1]) if len(precs) > 1 else None  # the other precision, same run, for the record
@@ -662,10 +675,13 @@ def main():
                                "lines:detect": round(res["lines_detect_ms"], 4) if res["lines_detect_ms"] else None,
                                "lines:stereo": round(res["lines_ms"], 4) if res["lines_ms"] else None,
                                "ba:wall": round(ba_wall, 4) if ba_wall else None},
+        # feature thread per step: blocked on the line threads / the BA queue, and its own SP / SG / association calls
+        "host_ms_per_step": res["host_wait_ms"],
         "lines": {"lines_per_step": res["lines_per_step"], "keypoints_per_image": K,
-                  "note": "lines:detect = host wall time per keyframe of LineDetector::LineExtractor on both images' "
-                          "RCF-like edge maps (restated FLD: GPU Canny classes + host chaining / fitting / merges), two "
-                          "host threads beside SP/SG, joined before the association; lines:stereo = the stereo line "
+                  "note": "lines:detect = per keyframe, the longer of the two images' LineDetector::LineExtractor jobs "
+                          "on the RCF-like edge maps (restated FLD: GPU Canny classes + host chaining / fitting / "
+                          "merges), each on its detector handle's native worker thread beside SP/SG "
+                          "(rspl_lines_extract_async), joined before the association; lines:stereo = the stereo line "
                           "association on the GPU (AssignPointsToLines x2, disparity filter, MatchLines; "
                           "frame.cc:150-203), post stream, HIP-event time per step"},
         "ba": {"ms_per_call": round(ba_wall, 4) if ba_wall else None,

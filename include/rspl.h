@@ -620,6 +620,16 @@ typedef struct {
 } rspl_fld_config;
 int rspl_lines_detect(rspl_lines* h, const uint8_t* image, int H, int W, int stride, const rspl_fld_config* cfg,
                       float* segments, int capacity, int* n_out);
+/* LineDetector::LineExtractor (src/line_processor.cc:460-490) asynchronously: rspl_lines_detect +
+ * rspl_line_extract (x2 scale, the merge passes when do_merge) on a native worker thread of the handle,
+ * as the reference runs its line threads beside the point thread (map_builder.cc:285-290, 325-337).
+ * The image must stay valid until rspl_lines_extract_wait returns; one job in flight per handle, and
+ * no other call on the handle meanwhile.  _wait blocks for the job and writes lines [n][4] (full-size
+ * x1 y1 x2 y2) and, when job_us is not NULL, the job's own duration on the worker (microseconds);
+ * *n_out is set even when it exceeds capacity (RSPL_E_CAPACITY). */
+int rspl_lines_extract_async(rspl_lines* h, const uint8_t* image, int H, int W, int stride,
+                             const rspl_fld_config* cfg, int do_merge);
+int rspl_lines_extract_wait(rspl_lines* h, double* lines, int capacity, int* n_out, double* job_us);
 /* debug (parity tests): the last rspl_lines_detect's half image and Canny classes (2 strong, 0
  * candidate, 1 none) for an H x W input, [H/2][W/2] each */
 int rspl_lines_debug_canny(rspl_lines* h, int H, int W, uint8_t* half, uint8_t* cls);

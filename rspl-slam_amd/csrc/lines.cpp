@@ -12,6 +12,11 @@
 // depends on the order): it stays on the host, in the reference's float / double types.  FLD
 // itself (cv::ximgproc) and the RCF edge net are not rebuilt: segments enter through the API.
 #include <algorithm>
+#include <chrono>
+#include <condition_variable>
+#include <mutex>
+#include <string>
+#include <thread>
 #include <array>
 #include <cmath>
 #include <cstring>
@@ -242,6 +247,20 @@ struct rspl_lines {
   int det_H = 0, det_W = 0;  // the last detection's image size (rspl_lines_debug_canny must match it)
   std::vector<uint8_t> edge;
   std::vector<int> stack;
+  // asynchronous LineExtractor (rspl_lines_extract_async / _wait): a native worker thread of the handle
+  // runs detect + the merge passes, so a caller's feature thread only submits and joins (the reference's
+  // line threads, map_builder.cc:285-290, 325-337)
+  std::thread worker;
+  std::mutex mu;
+  std::condition_variable cv;
+  bool job = false, done = false, quit = false;
+  const uint8_t* a_img = nullptr;
+  int a_H = 0, a_W = 0, a_stride = 0, a_merge = 1, a_rc = 0, a_n = 0;
+  double a_us = 0;  // the job's own duration on the worker
+  rspl_fld_config a_cfg{};
+  std::vector<float> a_seg;
+  std::vector<double> a_lines;
+  std::string a_err;
 };
 
 extern "C" int rspl_lines_create(const rspl_lines_config* cfg, rspl_lines** out) {
@@ -287,6 +306,14 @@ extern "C" int rspl_lines_create(const rspl_lines_config* cfg, rspl_lines** out)
 
 extern "C" void rspl_lines_destroy(rspl_lines* h) {
   if (!h) return;
+  if (h->worker.joinable()) {
+    {
+      std::lock_guard<std::mutex> lk(h->mu);
+      h->quit = true;
+    }
+    h->cv.notify_all();
+    h->worker.join();
+  }
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->d_img) (void)hipFree(h->d_img);
   if (h->d_det) (void)hipFree(h->d_det);
@@ -784,3 +811,83 @@ extern "C" int rspl_lines_debug_canny(rspl_lines* h, int H, int W, uint8_t* half
   return RSPL_OK;
 }
 
+
+namespace {
+
+// the worker's job: rspl_lines_detect into a growing segment buffer, then rspl_line_extract
+void extract_job(rspl_lines* h) {
+  const auto t0 = std::chrono::steady_clock::now();
+  int n = 0, rc;
+  for (;;) {
+    if (h->a_seg.size() < 4096) h->a_seg.resize(4096 * 4);
+    const int cap = (int)(h->a_seg.size() / 4);
+    rc = rspl_lines_detect(h, h->a_img, h->a_H, h->a_W, h->a_stride, &h->a_cfg, h->a_seg.data(), cap, &n);
+    if (rc != RSPL_E_CAPACITY || n <= cap) break;
+    h->a_seg.resize((size_t)n * 4);
+  }
+  h->a_n = 0;
+  if (rc == RSPL_OK) {
+    h->a_lines.resize((size_t)std::max(n, 1) * 4);  // the merges never add lines
+    rc = rspl_line_extract(h->a_seg.data(), n, h->a_merge, h->a_lines.data(), std::max(n, 1), &h->a_n);
+  }
+  h->a_rc = rc;
+  h->a_err = rc == RSPL_OK ? std::string() : std::string(rspl_last_error());
+  h->a_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+}
+
+}  // namespace
+
+extern "C" int rspl_lines_extract_async(rspl_lines* h, const uint8_t* image, int H, int W, int stride,
+                                        const rspl_fld_config* cfg, int do_merge) {
+  RSPL_CHECK_ARG(h && image && cfg, "rspl_lines_extract_async: NULL argument");
+  {
+    std::lock_guard<std::mutex> lk(h->mu);
+    RSPL_CHECK_ARG(!h->job, "rspl_lines_extract_async: the previous job has not been waited for");
+    h->a_img = image;
+    h->a_H = H;
+    h->a_W = W;
+    h->a_stride = stride;
+    h->a_cfg = *cfg;
+    h->a_merge = do_merge;
+    h->job = true;
+    h->done = false;
+  }
+  if (!h->worker.joinable()) {
+    const int dev = h->cfg.device;
+    h->worker = std::thread([h, dev]() {
+      (void)hipSetDevice(dev);  // the HIP device is per thread
+      std::unique_lock<std::mutex> lk(h->mu);
+      for (;;) {
+        h->cv.wait(lk, [h] { return h->quit || (h->job && !h->done); });
+        if (h->quit) return;
+        lk.unlock();
+        extract_job(h);
+        lk.lock();
+        h->done = true;
+        h->cv.notify_all();
+      }
+    });
+  }
+  h->cv.notify_all();
+  return RSPL_OK;
+}
+
+extern "C" int rspl_lines_extract_wait(rspl_lines* h, double* lines, int capacity, int* n_out, double* job_us) {
+  RSPL_CHECK_ARG(h && n_out && (capacity == 0 || lines) && capacity >= 0, "rspl_lines_extract_wait: bad argument");
+  std::unique_lock<std::mutex> lk(h->mu);
+  RSPL_CHECK_ARG(h->job, "rspl_lines_extract_wait: no job submitted");
+  h->cv.wait(lk, [h] { return h->done; });
+  h->job = false;
+  *n_out = h->a_n;
+  if (job_us) *job_us = h->a_us;
+  if (h->a_rc != RSPL_OK) {
+    set_error("%s", h->a_err.c_str());
+    return h->a_rc;
+  }
+  if (h->a_n > capacity) {
+    set_error("%d lines exceed capacity %d", h->a_n, capacity);
+    return RSPL_E_CAPACITY;
+  }
+  if (h->a_n) memcpy(lines, h->a_lines.data(), sizeof(double) * 4 * h->a_n);
+  return RSPL_OK;
+}

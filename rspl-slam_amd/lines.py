@@ -57,6 +57,8 @@ def _declare(lib):
     lib.rspl_lines_status.argtypes = [vp, C.POINTER(ip)]
     lib.rspl_lines_detect.argtypes = [vp, _u8p, ip, ip, ip, C.POINTER(FldConfig), _fp, ip, C.POINTER(ip)]
     lib.rspl_lines_debug_canny.argtypes = [vp, ip, ip, _u8p, _u8p]
+    lib.rspl_lines_extract_async.argtypes = [vp, _u8p, ip, ip, ip, C.POINTER(FldConfig), ip]
+    lib.rspl_lines_extract_wait.argtypes = [vp, _dp, ip, C.POINTER(ip), _dp]
     lib._rspl_lines_declared = True
     return lib
 
@@ -221,4 +223,23 @@ class LineDetector:
     def LineExtractor(self, image: np.ndarray) -> np.ndarray:
         """lines [m][4] double at full size (x2 scale; the merges when do_merge)"""
         return LineExtractor(self.detect(image), self.do_merge)
+
+    def submit(self, image: np.ndarray):
+        """LineExtractor(image) on the handle's native worker thread (rspl_lines_extract_async); the
+        image is kept alive until wait() returns its lines"""
+        img = np.ascontiguousarray(image, np.uint8)
+        self._job_img = img
+        capi.check(self._lib.rspl_lines_extract_async(self._h, _p(img, C.c_uint8), img.shape[0], img.shape[1],
+                                                      img.shape[1], C.byref(self.cfg), int(self.do_merge)),
+                   "rspl_lines_extract_async")
+
+    def wait(self, capacity: int = 4096):
+        """the submitted job's lines [m][4] double at full size and the job's duration on the worker in ms
+        (rspl_lines_extract_wait)"""
+        out = np.zeros((capacity, 4), np.float64)
+        n, us = C.c_int(), C.c_double()
+        rc = self._lib.rspl_lines_extract_wait(self._h, _p(out, C.c_double), capacity, C.byref(n), C.byref(us))
+        self._job_img = None
+        capi.check(rc, "rspl_lines_extract_wait")
+        return out[: n.value], us.value / 1e3
 

@@ -187,6 +187,27 @@ def test_line_detect_matches_oracle(det, seed):
     np.testing.assert_array_equal(det.LineExtractor(img), LR.line_extractor(ref))
 
 
+def test_line_extract_async_matches_sync():
+    """rspl_lines_extract_async / _wait (the handle's native worker thread) give the synchronous
+    LineExtractor's lines, on two handles in flight at once (the bench's left / right line threads), job
+    after job; a second submit before the wait and a wait without a job are refused."""
+    dets = [pkg.lines.LineDetector(), pkg.lines.LineDetector()]
+    for seed in (0, 3):
+        imgs = [SY.edge_map(seed=seed)[0], SY.edge_map(seed=seed + 10)[0]]
+        for d, img in zip(dets, imgs):
+            d.submit(img)
+        for d, img in zip(dets, imgs):
+            got, ms = d.wait()
+            assert ms > 0
+            np.testing.assert_array_equal(got, LR.line_extractor(FR.line_detect(img)))
+    dets[0].submit(imgs[0])
+    with pytest.raises(pkg.capi.RsplError):
+        dets[0].submit(imgs[0])
+    dets[0].wait()
+    with pytest.raises(pkg.capi.RsplError):
+        dets[0].wait()
+
+
 def test_line_detect_textured_image_low_thresholds():
     """An ordinary textured image with the uma_bumblebee thresholds (canny 50 / 50), odd tile edges"""
     d = pkg.lines.LineDetector(canny_th1=50.0, canny_th2=50.0)
