@@ -247,7 +247,7 @@ __device__ int lm_decide(const LmCtrl* c, LmCtrl* n, double chi2, double scale, 
   bool brk = false;
   *n = *c;
   if (rho > 0 && isfinite(tempChi) && ok) {
-    double alpha = 1. - pow(2 * rho - 1, 3.0);
+    double alpha = 1. - cube(2 * rho - 1);  // pow(2 rho - 1, 3)
     alpha = fmin(alpha, 2. / 3.);
     lambda *= fmax(1. / 3., alpha);
     ni = 2;

@@ -294,7 +294,7 @@ __device__ __forceinline__ int optimize_pose(const View& V, Pose& P, int lane, b
       }
       rho /= scale;
       if (rho > 0 && isfinite(tempChi) && ok) {
-        double alpha = 1. - pow(2 * rho - 1, 3);
+        double alpha = 1. - ba::cube(2 * rho - 1);  // pow(2 rho - 1, 3)
         alpha = fmin(alpha, 2. / 3.);
         lambda *= fmax(1. / 3., alpha);
         ni = 2;
