@@ -440,7 +440,6 @@ def main():
     # feature thread only submits and joins, as the reference's line threads (no Python threads)
     detectors = [pkg.lines.LineDetector(device=local) for _ in range(2)]
     line_bufs = [(capi.DeviceBuffer(512 * 4 * 8), capi.DeviceBuffer(512 * 4 * 8)) for _ in range(3)]
-    line_host = [None] * 3  # keeps each slot's uploaded arrays alive until the stream has read them
     lines_out, lines_valid = capi.DeviceBuffer(512 * 4 * 8), capi.DeviceBuffer(512)
     line_stats = {"detect_ms": [], "lines": []}
 
@@ -497,9 +496,11 @@ def main():
             eL, eR = edge_imgs[i % NP]
             jobs = None
             if "lines" not in skip:
+                tw = time.perf_counter()
                 detectors[0].submit(eL)
                 detectors[1].submit(eR)
                 jobs = detectors
+                host_wait["line_submit"] += time.perf_counter() - tw
             if "sp" in skip or "sg" in skip:  # diagnostics: stages left out (not a benchmark line)
                 if jobs is not None:
                     jobs[0].wait(), jobs[1].wait()
@@ -536,24 +537,20 @@ def main():
             # (left, right) and SG's match index of pair 1 (left(t) -> right(t)), stream-ordered behind the
             # decode
             if jobs is not None:
+                # join the line workers; their lines go to the device in post-stream order (no host sync)
                 tw = time.perf_counter()
-                (L0, t0ms), (L1, t1ms) = jobs[0].wait(), jobs[1].wait()
-                L0, L1 = L0[:512], L1[:512]
+                dl0, dl1 = line_bufs[slot]
+                nl0, t0ms = jobs[0].wait_device(dl0.ptr, 512, st_post.handle)
+                nl1, t1ms = jobs[1].wait_device(dl1.ptr, 512, st_post.handle)
                 host_wait["lines"] += time.perf_counter() - tw
                 if line_t0 is not None:
                     line_stats["detect_ms"].append(max(t0ms, t1ms))
-                    line_stats["lines"].append(len(L0) + len(L1))
-                dl0, dl1 = line_bufs[slot]
-                line_host[slot] = (L0, L1)
-                if len(L0):
-                    dl0.upload(L0, st_post.handle)
-                if len(L1):
-                    dl1.upload(L1, st_post.handle)
+                    line_stats["lines"].append(nl0 + nl1)
                 tw = time.perf_counter()
                 tm = line_timers[i - line_t0] if line_t0 is not None else None
                 if tm is not None:
                     tm.start(st_post.handle)
-                lm.stereo_lines_device(dl0.ptr, len(L0), dl1.ptr, len(L1), cur.ptr, K, ccur.ptr, outs[0].offset(K * 4),
+                lm.stereo_lines_device(dl0.ptr, nl0, dl1.ptr, nl1, cur.ptr, K, ccur.ptr, outs[0].offset(K * 4),
                                        cam_limits, lines_out.ptr, lines_valid.ptr, st_post.handle)
                 if tm is not None:
                     tm.stop(st_post.handle)
@@ -567,7 +564,8 @@ def main():
                 ba_q.put(ba_item(i))
                 host_wait["ba_queue"] += time.perf_counter() - tw
 
-        host_wait = {"lines": 0.0, "ba_queue": 0.0, "sp_calls": 0.0, "sg_calls": 0.0, "line_assoc_calls": 0.0}
+        host_wait = {"lines": 0.0, "ba_queue": 0.0, "sp_calls": 0.0, "sg_calls": 0.0, "line_assoc_calls": 0.0,
+                     "line_submit": 0.0}
         line_t0 = None
         for i in range(args.warmup):
             step(i)

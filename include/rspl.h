@@ -630,6 +630,11 @@ int rspl_lines_detect(rspl_lines* h, const uint8_t* image, int H, int W, int str
 int rspl_lines_extract_async(rspl_lines* h, const uint8_t* image, int H, int W, int stride,
                              const rspl_fld_config* cfg, int do_merge);
 int rspl_lines_extract_wait(rspl_lines* h, double* lines, int capacity, int* n_out, double* job_us);
+/* the same join, the lines copied into DEVICE memory d_lines [capacity][4] in stream order (from the
+ * handle's pinned result buffer; no host synchronisation with the stream) -- the feed of
+ * rspl_lines_stereo_device */
+int rspl_lines_extract_wait_device(rspl_lines* h, double* d_lines, int capacity, int* n_out, double* job_us,
+                                   void* stream);
 /* debug (parity tests): the last rspl_lines_detect's half image and Canny classes (2 strong, 0
  * candidate, 1 none) for an H x W input, [H/2][W/2] each */
 int rspl_lines_debug_canny(rspl_lines* h, int H, int W, uint8_t* half, uint8_t* cls);

@@ -257,6 +257,15 @@ struct rspl_lines {
   const uint8_t* a_img = nullptr;
   int a_H = 0, a_W = 0, a_stride = 0, a_merge = 1, a_rc = 0, a_n = 0;
   double a_us = 0;  // the job's own duration on the worker
+  // rspl_lines_extract_wait_device: the worker's lines staged in pinned memory and copied to the device in
+  // stream order, through a ring of kPinSlots buffers: a slot is rewritten only once its copy of
+  // kPinSlots joins ago has completed (copy_ev), so a join never waits for the stream in practice
+  static constexpr int kPinSlots = 4;
+  double* pin_lines[kPinSlots] = {};
+  int pin_cap = 0;  // lines per slot
+  hipEvent_t copy_ev[kPinSlots] = {};
+  bool copy_pending[kPinSlots] = {};
+  int pin_next = 0;
   rspl_fld_config a_cfg{};
   std::vector<float> a_seg;
   std::vector<double> a_lines;
@@ -313,6 +322,13 @@ extern "C" void rspl_lines_destroy(rspl_lines* h) {
     }
     h->cv.notify_all();
     h->worker.join();
+  }
+  for (int k = 0; k < rspl_lines::kPinSlots; k++) {
+    if (h->copy_ev[k]) {
+      (void)hipEventSynchronize(h->copy_ev[k]);
+      (void)hipEventDestroy(h->copy_ev[k]);
+    }
+    if (h->pin_lines[k]) (void)hipHostFree(h->pin_lines[k]);
   }
   if (h->stream) (void)hipStreamSynchronize(h->stream);
   if (h->d_img) (void)hipFree(h->d_img);
@@ -889,5 +905,40 @@ extern "C" int rspl_lines_extract_wait(rspl_lines* h, double* lines, int capacit
     return RSPL_E_CAPACITY;
   }
   if (h->a_n) memcpy(lines, h->a_lines.data(), sizeof(double) * 4 * h->a_n);
+  return RSPL_OK;
+}
+
+extern "C" int rspl_lines_extract_wait_device(rspl_lines* h, double* d_lines, int capacity, int* n_out,
+                                              double* job_us, void* stream) {
+  RSPL_CHECK_ARG(h && n_out && (capacity == 0 || d_lines) && capacity >= 0,
+                 "rspl_lines_extract_wait_device: bad argument");
+  constexpr int S = rspl_lines::kPinSlots;
+  if (h->pin_cap < capacity) {  // grow every slot (their pending copies drained first)
+    for (int k = 0; k < S; k++) {
+      if (h->copy_pending[k]) RSPL_HIP(hipEventSynchronize(h->copy_ev[k]));
+      h->copy_pending[k] = false;
+      if (h->pin_lines[k]) (void)hipHostFree(h->pin_lines[k]);
+      h->pin_lines[k] = nullptr;
+    }
+    h->pin_cap = 0;
+    for (int k = 0; k < S; k++)
+      RSPL_HIP(hipHostMalloc((void**)&h->pin_lines[k], sizeof(double) * 4 * capacity, hipHostMallocDefault));
+    h->pin_cap = capacity;
+  }
+  const int k = h->pin_next;
+  if (!h->copy_ev[k]) RSPL_HIP(hipEventCreateWithFlags(&h->copy_ev[k], hipEventDisableTiming));
+  if (h->copy_pending[k]) {  // this slot's copy S joins ago
+    RSPL_HIP(hipEventSynchronize(h->copy_ev[k]));
+    h->copy_pending[k] = false;
+  }
+  int rc = rspl_lines_extract_wait(h, h->pin_lines[k], capacity, n_out, job_us);
+  if (rc != RSPL_OK) return rc;
+  if (*n_out) {
+    RSPL_HIP(hipMemcpyAsync(d_lines, h->pin_lines[k], sizeof(double) * 4 * *n_out, hipMemcpyHostToDevice,
+                            (hipStream_t)stream));
+    RSPL_HIP(hipEventRecord(h->copy_ev[k], (hipStream_t)stream));
+    h->copy_pending[k] = true;
+    h->pin_next = (k + 1) % S;
+  }
   return RSPL_OK;
 }

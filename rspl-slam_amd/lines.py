@@ -59,6 +59,7 @@ def _declare(lib):
     lib.rspl_lines_debug_canny.argtypes = [vp, ip, ip, _u8p, _u8p]
     lib.rspl_lines_extract_async.argtypes = [vp, _u8p, ip, ip, ip, C.POINTER(FldConfig), ip]
     lib.rspl_lines_extract_wait.argtypes = [vp, _dp, ip, C.POINTER(ip), _dp]
+    lib.rspl_lines_extract_wait_device.argtypes = [vp, vp, ip, C.POINTER(ip), _dp, vp]
     lib._rspl_lines_declared = True
     return lib
 
@@ -242,4 +243,13 @@ class LineDetector:
         self._job_img = None
         capi.check(rc, "rspl_lines_extract_wait")
         return out[: n.value], us.value / 1e3
+
+    def wait_device(self, d_lines: int, capacity: int, stream=None):
+        """the submitted job's lines copied to device memory d_lines [capacity][4] in stream order
+        (rspl_lines_extract_wait_device); returns (n, job ms)"""
+        n, us = C.c_int(), C.c_double()
+        rc = self._lib.rspl_lines_extract_wait_device(self._h, d_lines, capacity, C.byref(n), C.byref(us), stream)
+        self._job_img = None
+        capi.check(rc, "rspl_lines_extract_wait_device")
+        return n.value, us.value / 1e3
 

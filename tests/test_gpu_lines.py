@@ -200,6 +200,17 @@ def test_line_extract_async_matches_sync():
             got, ms = d.wait()
             assert ms > 0
             np.testing.assert_array_equal(got, LR.line_extractor(FR.line_detect(img)))
+    # the device-delivery join (the bench's feed of the stereo association): same lines, in stream order
+    st = pkg.capi.Stream()
+    bufs = [pkg.capi.DeviceBuffer(512 * 4 * 8) for _ in dets]
+    for rep in range(2):
+        for d, img in zip(dets, imgs):
+            d.submit(img)
+        for d, b, img in zip(dets, bufs, imgs):
+            n, _ = d.wait_device(b.ptr, 512, st.handle)
+            ref = LR.line_extractor(FR.line_detect(img))
+            assert n == len(ref)
+            np.testing.assert_array_equal(b.download((n, 4), np.float64, st.handle), ref)
     dets[0].submit(imgs[0])
     with pytest.raises(pkg.capi.RsplError):
         dets[0].submit(imgs[0])
