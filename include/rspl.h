@@ -316,6 +316,15 @@ int rspl_ba_use_reserved_cus(rspl_ba* ba, int reserve_cus);
  * launches[1]: update + cost + speculative linearisation -- over the trials that did work. */
 int rspl_ba_kernel_timing(rspl_ba* ba, int every);
 int rspl_ba_kernel_times(rspl_ba* ba, double* ms, long long* launches);
+/* Test hook (host only, no device): the host staging of rspl_ba_local -- the edges of rank `rank` of
+ * `nranks` (1: all) in landmark-CSR order -- with the host workers from par_edges edges (0: serial).
+ * n_local = {local edges E, local point edges Ep}; lm_off [n_points + n_lines + 1]; per CSR position
+ * k < E: type (0..3), pose, landmark (lines offset by n_points), camera, caller edge id (over the four
+ * types in order), reduced pose id (-1: fixed or without edges); eobs: 4 doubles per point edge, then
+ * 8 per line edge (arrays sized for all edges). */
+int rspl_ba_debug_stage(const rspl_ba_problem* problem, int par_edges, int rank, int nranks, int* n_local,
+                        int* lm_off, int8_t* etype, int* epose, int* elm, int* ecam, int* gmap, int* lpose,
+                        double* eobs);
 
 /* ------------------------------------------------------------------------ */
 /* Landmark-sharded local BA: nranks handles -- one per  */

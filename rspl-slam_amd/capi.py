@@ -32,7 +32,7 @@ EXPORTS = [
     "rspl_sg_stage_times", "rspl_sg_destroy",
     "rspl_pm_match",
     "rspl_ba_create", "rspl_ba_local", "rspl_ba_destroy", "rspl_ba_use_reserved_cus", "rspl_ba_kernel_timing",
-    "rspl_ba_kernel_times",
+    "rspl_ba_kernel_times", "rspl_ba_debug_stage",
     "rspl_frame_create", "rspl_frame_optimize", "rspl_frame_destroy",
     "rspl_ba_set_shard", "rspl_comm_unique_id", "rspl_comm_create", "rspl_comm_allreduce_sum", "rspl_comm_destroy",
     "rspl_ba_set_comm", "rspl_group_create", "rspl_group_destroy", "rspl_ba_set_group",
@@ -157,6 +157,7 @@ def load(path: pathlib.Path = LIB_PATH):
         lib.rspl_ba_kernel_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_longlong)]
         lib.rspl_ba_destroy.argtypes = [vp]
         lib.rspl_ba_destroy.restype = None
+        lib.rspl_ba_debug_stage.argtypes = [vp, ip, ip, ip] + [vp] * 9
     if hasattr(lib, "rspl_ba_set_shard"):
         lib.rspl_ba_set_shard.argtypes = [vp, ip, ip, vp, vp]
         lib.rspl_comm_unique_id.argtypes = [vp]

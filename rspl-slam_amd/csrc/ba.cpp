@@ -20,10 +20,12 @@
 #include <numeric>
 #include <string>
 #include <type_traits>
+#include <memory>
 #include <vector>
 
 #include "ba_kernels.hpp"
 #include "common.hpp"
+#include "ba_stage.hpp"
 
 using namespace rspl;
 
@@ -63,8 +65,7 @@ struct rspl_ba {
   ba::Mail* mail = nullptr;
   ba::Mail* mail_dev = nullptr;
   unsigned long long seq = 0;
-  std::vector<uint8_t> pact;  // host scratch reused across calls
-  std::vector<int> lm_cnt;    // per-landmark edge counts, then fill cursors (host scratch)
+  ba::Stager stg;  // host staging into landmark-CSR order (scratch and host workers reused across calls)
   // landmark sharding (rspl_ba_set_shard): this rank keeps the edges of landmarks g % nranks == rank
   int rank = 0, nranks = 1;
   rspl_allreduce_fn allreduce = nullptr;
@@ -93,7 +94,8 @@ namespace {
 
 constexpr int kMaxCams = 16;
 constexpr int kMaxRanks = 64;
-
+constexpr int kParEdges = 8192;  // staging on the host workers from this many edges
+constexpr int kChunkWaves = 1024; // Schur chunk waves of one dispatch round (one wave per SIMD)
 // the rank's sum all-reduce, stream-ordered on the BA stream
 int allreduce(rspl_ba* b, double* d, size_t n) {
   const int rc = b->allreduce(b->ar_ctx, d, n, b->stream);
@@ -715,6 +717,29 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
   return rc;
 }
 
+extern "C" int rspl_ba_debug_stage(const rspl_ba_problem* pr, int par_edges, int rank, int nranks, int* n_local,
+                                   int* lm_off, int8_t* etype, int* epose, int* elm, int* ecam, int* gmap,
+                                   int* lpose, double* eobs) {
+  RSPL_CHECK_ARG(pr && n_local && lm_off && etype && epose && elm && ecam && gmap && lpose && eobs,
+                 "rspl_ba_debug_stage: NULL argument");
+  RSPL_CHECK_ARG(pr->n_poses >= 0 && pr->n_points >= 0 && pr->n_lines >= 0 && pr->n_mono >= 0 &&
+                     pr->n_stereo >= 0 && pr->n_mono_line >= 0 && pr->n_stereo_line >= 0 &&
+                     (pr->n_poses == 0 || pr->pose_fixed) && pr->n_cameras >= 1,
+                 "rspl_ba_debug_stage: bad problem sizes");
+  RSPL_CHECK_ARG(nranks >= 1 && rank >= 0 && rank < nranks, "rspl_ba_debug_stage: bad rank");
+  ba::Stager stg;
+  int rc;
+  if ((rc = stg.count(pr, nranks > 1, rank, nranks, par_edges))) return rc;
+  std::vector<int> pidx(pr->n_poses);
+  int K = 0;
+  for (int p = 0; p < pr->n_poses; p++) pidx[p] = (stg.pose_has_edge[p] && !pr->pose_fixed[p]) ? K++ : -1;
+  ba::Stager::Out so{lm_off, etype, epose, elm, ecam, gmap, lpose, eobs, pidx.data()};
+  stg.place(pr, so);
+  n_local[0] = stg.E;
+  n_local[1] = stg.Ep;
+  return RSPL_OK;
+}
+
 namespace {
 int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   RSPL_CHECK_ARG(b && pr && res, "rspl_ba_local: NULL argument");
@@ -731,24 +756,6 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   const int Eg = ne[0] + ne[1] + ne[2] + ne[3], nL = nq + nl;
   // landmark sharding: this rank keeps the edges of its landmarks (g % nranks == rank)
   const bool sh = b->allreduce != nullptr;
-  const int32_t* lms_[4] = {pr->mono_point, pr->stereo_point, pr->mono_line_line, pr->stereo_line_line};
-  auto owned = [&](int t, int i) {
-    const int g = t < 2 ? lms_[t][i] : nq + lms_[t][i];
-    return !sh || g % b->nranks == b->rank;
-  };
-  int E = Eg, n_line_local = ne[2] + ne[3];
-  if (sh) {
-    E = 0;
-    n_line_local = 0;
-    for (int t = 0; t < 4; t++) {
-      RSPL_CHECK_ARG(ne[t] == 0 || lms_[t], "NULL edge arrays");
-      for (int i = 0; i < ne[t]; i++)
-        if (lms_[t][i] >= 0 && lms_[t][i] < (t < 2 ? nq : nl) && owned(t, i)) {
-          E++;
-          n_line_local += t >= 2;
-        }
-    }
-  }
   // optional host-side stage timing (RSPL_BA_TIMING=1), in microseconds since the previous mark
   static const bool timing = getenv("RSPL_BA_TIMING") != nullptr;
   using clk = std::chrono::steady_clock;
@@ -763,51 +770,14 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   };
   mark("start");
   // ---- one staging region for the whole call, mirrored by the device call buffer ----
-  const int32_t* poses[4] = {pr->mono_pose, pr->stereo_pose, pr->mono_line_pose, pr->stereo_line_pose};
-  const int32_t* lms[4] = {pr->mono_point, pr->stereo_point, pr->mono_line_line, pr->stereo_line_line};
-  const int32_t* cams[4] = {pr->mono_camera, pr->stereo_camera, pr->mono_line_camera, pr->stereo_line_camera};
-  const double* obs[4] = {pr->mono_obs, pr->stereo_obs, pr->mono_line_obs, pr->stereo_line_obs};
-  // pass 1: validate, count the local edges per landmark, mark the poses with edges
-  b->lm_cnt.assign(nL + 1, 0);
-  b->pact.assign(np, 0);
-  int Ep = 0;  // local point edges
-  int* cnt = b->lm_cnt.data();
-  uint8_t* pact = b->pact.data();
-  for (int t = 0; t < 4; t++) {
-    RSPL_CHECK_ARG(ne[t] == 0 || (poses[t] && lms[t] && obs[t]), "NULL edge arrays");
-    const int n = ne[t], lmax = t < 2 ? nq : nl, loff = t < 2 ? 0 : nq;
-    const int32_t *pt = poses[t], *lt = lms[t], *ct = cams[t];
-    // branch-free validation (unsigned compares), the offending edge looked up only on failure
-    bool bad = false;
-    for (int i = 0; i < n; i++) {
-      const unsigned p = (unsigned)pt[i], l = (unsigned)lt[i];
-      bad |= (p >= (unsigned)np) | (l >= (unsigned)lmax);
-    }
-    if (ct)
-      for (int i = 0; i < n; i++) bad |= (unsigned)ct[i] >= (unsigned)pr->n_cameras;
-    if (bad)
-      for (int i = 0; i < n; i++) {
-        const int p = pt[i], l = lt[i], c = ct ? ct[i] : 0;
-        RSPL_CHECK_ARG(p >= 0 && p < np && l >= 0 && l < lmax && c >= 0 && c < pr->n_cameras,
-                       "edge %d of type %d references a missing vertex/camera", i, t);
-      }
-    // a pose is optimised when it has an edge on ANY rank: K agrees across ranks
-    for (int i = 0; i < n; i++) pact[pt[i]] = 1;
-    if (!sh) {
-      for (int i = 0; i < n; i++) cnt[loff + lt[i] + 1]++;
-      Ep += t < 2 ? n : 0;
-    } else {
-      for (int i = 0; i < n; i++)
-        if (owned(t, i)) {
-          cnt[loff + lt[i] + 1]++;
-          Ep += t < 2;
-        }
-    }
-  }
+  int rc;
+  // pass 1: validate, count the local edges per landmark, mark the poses with edges (ba_stage.cpp;
+  // large unsharded calls on the handle's host workers)
+  if ((rc = b->stg.count(pr, sh, b->rank, b->nranks, kParEdges))) return rc;
+  const int E = b->stg.E, Ep = b->stg.Ep, n_line_local = E - Ep;
   mark("count");
   const CallLayout cl(pr->n_cameras, np, nq, nl, E, 4 * (size_t)Ep + 8 * (size_t)(E - Ep));
   const DownLayout dl(np, nq, nl, Eg);  // inlier flags by global edge id
-  int rc;
   if ((rc = ensure_stage(b, std::max(cl.bytes, dl.bytes)))) return rc;
   char* sg = b->stage;
   // vertices: VertexSE3Expmap estimate = SE3Quat(q, p).inverse() (g2o_optimization.cc:42)
@@ -827,78 +797,24 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   }
   int* pidx = reinterpret_cast<int*>(sg + cl.pidx);
   int K = 0;
-  for (int p = 0; p < np; p++) pidx[p] = (b->pact[p] && !pr->pose_fixed[p]) ? K++ : -1;
-  // CSR offsets: the edges of landmark g at positions [lm_off[g], lm_off[g+1]), point landmarks first
+  for (int p = 0; p < np; p++) pidx[p] = (b->stg.pose_has_edge[p] && !pr->pose_fixed[p]) ? K++ : -1;
+  // pass 2: lm_off, and every local edge at its CSR position with its reduced pose and its caller's
+  // edge id (landmark-CSR order, input order within a landmark: the order every per-landmark
+  // reduction follows)
   int* lm_off = reinterpret_cast<int*>(sg + cl.lm_off);
-  lm_off[0] = 0;
-  for (int g = 0; g < nL; g++) lm_off[g + 1] = lm_off[g] + b->lm_cnt[g + 1];
-  // pass 2: every local edge written at its CSR position (input order within a landmark: the
-  // order every per-landmark reduction follows), with its reduced pose and its caller's edge id
-  int8_t* etype = reinterpret_cast<int8_t*>(sg + cl.type);
-  int* epose = reinterpret_cast<int*>(sg + cl.pose);
-  int* elm = reinterpret_cast<int*>(sg + cl.lm);
-  int* ecam = reinterpret_cast<int*>(sg + cl.cam);
-  int* gmap = reinterpret_cast<int*>(sg + cl.gmap);
-  int* lpose = reinterpret_cast<int*>(sg + cl.lm_pose);
-  double* eobs = reinterpret_cast<double*>(sg + cl.obs);
-  double* lobs = eobs + 4 * (size_t)Ep;
   mark("vertices");
-  int* fill = b->lm_cnt.data();  // reused as the per-landmark fill cursor
-  for (int g = 0; g < nL; g++) fill[g] = lm_off[g];
-  // pass 2a: the CSR permutation only -- each local edge's caller id at its CSR position (input order
-  // within a landmark: the order every per-landmark reduction follows); one random store per edge
   {
-    int eg = 0;
-    for (int t = 0; t < 4; t++) {
-      const int n = ne[t], loff = t < 2 ? 0 : nq;
-      const int32_t* lt = lms[t];
-      if (!sh) {
-        for (int i = 0; i < n; i++) gmap[fill[loff + lt[i]]++] = eg + i;
-      } else {
-        for (int i = 0; i < n; i++)
-          if (owned(t, i)) gmap[fill[loff + lt[i]]++] = eg + i;
-      }
-      eg += n;
-    }
-  }
-  // pass 2b: every staged array written sequentially in CSR order, gathered from the caller's arrays
-  // (point edges: mono / stereo picked without a branch; the third observation of a mono edge is 0)
-  {
-    const int e1 = ne[0], e2 = ne[0] + ne[1], e3 = e2 + ne[2];
-    static const double zero = 0.0;
-    for (int k = 0; k < Ep; k++) {
-      const int eg = gmap[k];
-      const bool st = eg >= e1;
-      const int i = st ? eg - e1 : eg;
-      const int32_t* pt = st ? poses[1] : poses[0];
-      const int32_t* ct = st ? cams[1] : cams[0];
-      const int p = pt[i];
-      etype[k] = (int8_t)st;
-      epose[k] = p;
-      elm[k] = (st ? lms[1] : lms[0])[i];
-      ecam[k] = ct ? ct[i] : 0;
-      lpose[k] = pidx[p];
-      const double* ob = st ? obs[1] + 3 * (size_t)i : obs[0] + 2 * (size_t)i;
-      double* o = eobs + 4 * (size_t)k;
-      o[0] = ob[0];
-      o[1] = ob[1];
-      o[2] = *(st ? ob + 2 : &zero);  // no load past a mono record
-    }
-    for (int k = Ep; k < E; k++) {
-      const int eg = gmap[k];
-      const int t = eg >= e3 ? 3 : 2;
-      const int i = eg - (t == 3 ? e3 : e2);
-      const int p = poses[t][i];
-      etype[k] = (int8_t)t;
-      epose[k] = p;
-      elm[k] = nq + lms[t][i];
-      ecam[k] = cams[t] ? cams[t][i] : 0;
-      lpose[k] = pidx[p];
-      const int D = t == 3 ? 8 : 4;
-      const double* ob = obs[t] + (size_t)D * i;
-      double* o = lobs + 8 * (size_t)(k - Ep);
-      for (int q = 0; q < D; q++) o[q] = ob[q];
-    }
+    ba::Stager::Out so;
+    so.lm_off = lm_off;
+    so.etype = reinterpret_cast<int8_t*>(sg + cl.type);
+    so.epose = reinterpret_cast<int*>(sg + cl.pose);
+    so.elm = reinterpret_cast<int*>(sg + cl.lm);
+    so.ecam = reinterpret_cast<int*>(sg + cl.cam);
+    so.gmap = reinterpret_cast<int*>(sg + cl.gmap);
+    so.lpose = reinterpret_cast<int*>(sg + cl.lm_pose);
+    so.eobs = reinterpret_cast<double*>(sg + cl.obs);
+    so.pidx = pidx;
+    b->stg.place(pr, so);
   }
   mark("scatter");
   uint8_t* lm_act = reinterpret_cast<uint8_t*>(sg + cl.lm_act);
@@ -1006,7 +922,15 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   A.lm_act = reinterpret_cast<const uint8_t*>(cb + cl.lm_act);
   A.pairs = reinterpret_cast<const int*>(cb + cl.pairs);
   A.npairs = K * (K + 1) / 2;
-  A.nchk = std::max((nL + ba::kLmChunk - 1) / ba::kLmChunk, 1);
+  // Schur chunks: ranges of kLmChunk landmarks per pose pair while the chunk waves fit one dispatch
+  // round (C3: 45 pairs x 16 ranges); with many pose pairs (C5: K = 29, 435 pairs) fewer, wider
+  // ranges -- each wave then walks more passes, but the chip runs them in one round instead of ~17
+  {
+    const int npairs = std::max(A.npairs, 1);
+    A.nchk = std::max(1, std::min((nL + ba::kLmChunk - 1) / ba::kLmChunk, kChunkWaves / npairs));
+    A.lmchunk = std::max(ba::kLmChunk, ((nL + A.nchk - 1) / A.nchk + 63) / 64 * 64);
+    A.nchk = std::max((nL + A.lmchunk - 1) / A.lmchunk, 1);
+  }
   A.n_line_edges = n_line_local;
   A.ltab = reinterpret_cast<const int4*>(cb + cl.ltab);
   A.n_lblk = n_lblk;

@@ -1135,7 +1135,7 @@ __device__ __forceinline__ void pose_diag_range(const Problem& P, const Lin& L, 
 // Edge-pair lists, built once per call on the device.  Chunk c = (pose pair pr, landmark
 // range lb) owns the segment [pp_off[c], pp_off[c+1]) of the (e1, e2) lists; within it the
 // pairs follow landmark order, then i, then j (deterministic).  Lane l of round r handles
-// landmark lb * kLmChunk + 64 r + l; its matches are found from bit masks over batches of 8
+// landmark lb * lmchunk + 64 r + l; its matches are found from bit masks over batches of 8
 // CSR entries (independent loads) and placed by a wave prefix sum in lane order.
 template <bool FILL>
 __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, const int* pp_off, int4* pp) {
@@ -1143,8 +1143,8 @@ __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, c
   const int pr = c / A.nchk, lb = c - pr * A.nchk;
   const int pa = A.pairs[2 * pr], pb = A.pairs[2 * pr + 1];
   int base = FILL ? pp_off[c] : 0;
-  for (int r = 0; r < kLmChunk / 64; r++) {
-    const int g = lb * kLmChunk + 64 * r + lane;
+  for (int r = 0; r < A.lmchunk / 64; r++) {
+    const int g = lb * A.lmchunk + 64 * r + lane;
     int k0 = 0, k1 = 0;
     if (g < A.nL && A.lm_act[g]) {
       k0 = A.lm_off[g];
@@ -2095,9 +2095,15 @@ struct ChunkSeg {
 };
 __device__ __forceinline__ bool chunk_seg(const Active& A, int vb, ChunkSeg& cs) {
   const int lane = threadIdx.x & 63;
-  const int xcd = vb & 7, slot = vb >> 3, rpx = (A.nchk + 7) >> 3;
-  cs.lb = (slot % rpx) * 8 + xcd;
-  const int pr0 = slot / rpx;
+  int pr0;
+  if (A.nchk >= 8) {
+    const int xcd = vb & 7, slot = vb >> 3, rpx = (A.nchk + 7) >> 3;
+    cs.lb = (slot % rpx) * 8 + xcd;
+    pr0 = slot / rpx;
+  } else {  // fewer ranges than XCDs (many pose pairs, wide chunks): plain order, every XCD busy
+    pr0 = vb / A.nchk;
+    cs.lb = vb - pr0 * A.nchk;
+  }
   if (cs.lb >= A.nchk || pr0 >= A.npairs) return false;
   cs.c = pr0 * A.nchk + cs.lb;
   cs.beg = A.pp_off[cs.c];
@@ -2117,7 +2123,7 @@ __device__ __forceinline__ bool chunk_wave(const Problem& P, const Lin& L, const
   for (int v = 0; v < 48; v++) acc[v] = 0.0;
   // a range of point landmarks only
   // (all but the last range or two) takes the 3-dim loops, off-diagonal pose pairs without the e1 == e2 terms
-  const bool pts = (lb + 1) * kLmChunk <= P.nq;
+  const bool pts = (lb + 1) * A.lmchunk <= P.nq;
   const bool dpp = A.pairs[2 * pr] == A.pairs[2 * pr + 1];
   bool bad = false;
   if (pts && !dpp) chunk_loop<3, false>(L, A, S, P.nq, beg, end, cs.q0, lambda, bad, acc);
@@ -2871,7 +2877,9 @@ hipError_t ensure_schur_attr() {
 }
 
 // pair_chunk grid: 8 XCD lanes x (landmark ranges per XCD) x pose pairs (idle slots exit)
-static int pair_chunk_blocks(const Active& A) { return 8 * ((A.nchk + 7) / 8) * A.npairs; }
+static int pair_chunk_blocks(const Active& A) {
+  return A.nchk >= 8 ? 8 * ((A.nchk + 7) / 8) * A.npairs : A.nchk * A.npairs;
+}
 
 // Schur chunks; with fused = true (wave path) the last pose pair also solves (solve_wave<6K>)
 static void launch_chunks(const Problem& P, const Lin& L, const Active& A, const Sys& S, double lambda, const Lin& Ls,

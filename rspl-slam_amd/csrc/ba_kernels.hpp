@@ -50,7 +50,9 @@ struct Active {          // active structure of one optimize() phase
   const uint8_t* lm_act; // [nL]
   const int* pairs;      // [npairs][2] reduced pose pairs (a <= b)
   int npairs;
-  int nchk;              // Schur chunks per pose pair: landmark ranges of kLmChunk
+  int nchk;              // Schur chunks per pose pair: landmark ranges of lmchunk
+  int lmchunk;           // landmarks per Schur chunk (a multiple of 64; kLmChunk unless the pose pairs
+                         //   are so many that the chunk waves would need several dispatch rounds)
   const int* pp_off;     // [npairs * nchk + 1] segment of each chunk in the edge-pair lists
   const int4* pp;        // edge pairs {e1 of pose a, e2 of pose b, their landmark, 0}, chunk-major,
                          //   landmark order within a chunk
