@@ -334,6 +334,9 @@ def main():
                          "jointly, landmark-sharded over all ranks (RCCL all-reduce of the reduced camera system)")
     ap.add_argument("--cpu-frames", type=int, default=None, help="keyframes in the bounded CPU-baseline sample")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--ba-thread", choices=["native", "python"], default="native",
+                    help="the tracking thread that runs the local BAs: the BA handle's native host thread "
+                         "(rspl_ba_submit) or a Python thread around rspl_ba_local (A/B)")
     ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp16",
                     help="SP/SG MFMA precision: fp16 = the reference's own TensorRT kFP16 engines "
                          "(src/super_point.cpp:98, src/super_glue.cpp:132; default), fp32 = the parity path")
@@ -478,8 +481,30 @@ def main():
                 ba_ms.append((time.perf_counter() - t) * 1e3 / len(item))
                 ba_q.task_done()
 
-        worker = threading.Thread(target=tracking_thread, daemon=True)
-        worker.start()
+        native = args.ba_thread == "native"
+        if not native:
+            worker = threading.Thread(target=tracking_thread, daemon=True)
+            worker.start()
+        outs_nat = {}  # native tracking thread: one result buffer per problem, reused
+
+        def ba_put(item):
+            """hand keyframe i's local BA to the tracking thread: the handle's native host thread
+            (rspl_ba_submit: blocks while two calls wait, map_builder.cc:176), or the Python one (A/B)"""
+            if not native:
+                ba_q.put(item)
+                return
+            for prob in item:
+                outs_nat[id(prob)] = ba.submit(prob, out=outs_nat.get(id(prob)))
+
+        def ba_drain():
+            if not native:
+                ba_q.join()
+                return
+            n, its, ms = ba.join()
+            if n:
+                per = len(ba_item(0))
+                ba_ms.extend([ms / n] * (n // per))
+                ba_iters.extend([its / n] * (n // per))
         ktime_every = args.ba_ktime_every  # HIP-event timing of the BA's launches (every N-th call)
         line_timers = []  # HIP-event timers around the line association (post stream), timed steps only
 
@@ -511,7 +536,7 @@ def main():
                     sg.infer_device(2, f0.ptr, n0.ptr, f1.ptr, n1.ptr, K, True, outs[0].ptr, outs[1].ptr,
                                     outs[2].ptr, outs[3].ptr, st_sg.handle, post_stream=st_post.handle)
                 if "ba" not in skip:
-                    ba_q.put(ba_item(i))
+                    ba_put(ba_item(i))
                 return
             tw = time.perf_counter()
             if i >= 2:
@@ -561,7 +586,7 @@ def main():
             # _tracking_data_buffer.size() >= 2 (src/map_builder.cc:176)
             if "ba" not in skip:
                 tw = time.perf_counter()
-                ba_q.put(ba_item(i))
+                ba_put(ba_item(i))
                 host_wait["ba_queue"] += time.perf_counter() - tw
 
         host_wait = {"lines": 0.0, "ba_queue": 0.0, "sp_calls": 0.0, "sg_calls": 0.0, "line_assoc_calls": 0.0,
@@ -569,7 +594,7 @@ def main():
         line_t0 = None
         for i in range(args.warmup):
             step(i)
-        ba_q.join()
+        ba_drain()
         capi.synchronize()
         if not sg.status()[0]:
             raise SystemExit(f"bench: SuperGlue device path failed during warmup: {sg.error}")
@@ -590,11 +615,12 @@ def main():
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(args.warmup + i)
-        ba_q.join()
+        ba_drain()
         capi.synchronize()
         elapsed = job_time(time.perf_counter() - t0, dist)
-        ba_q.put(None)
-        worker.join()
+        if not native:
+            ba_q.put(None)
+            worker.join()
         ba_kt = ba.kernel_times()
         ba.kernel_timing(0)
         ba_calls = len(ba_ms) * (world if shard else 1)

@@ -307,6 +307,16 @@ typedef struct rspl_ba rspl_ba;
 int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out);
 int rspl_ba_local(rspl_ba* ba, const rspl_ba_problem* problem, rspl_ba_result* result);
 void rspl_ba_destroy(rspl_ba* ba);
+/* The reference's tracking thread (map_builder.cc:48-49, 188-276): rspl_ba_submit queues one local BA
+ * call for the handle's native host thread, which runs the queued calls in order (rspl_ba_local each);
+ * like the reference's feature thread it blocks while two calls are already waiting
+ * (_tracking_data_buffer, map_builder.cc:176).  problem, its arrays and result must stay valid until
+ * the call has run.  rspl_ba_join waits until every queued call has run and returns the first failure
+ * since the previous join (0: none), with the number of calls, their LM iterations (first + second
+ * optimize) and their summed wall time in ms (each may be NULL).  Do not call rspl_ba_local on the
+ * handle while calls are queued; rspl_ba_destroy runs the queued calls before it frees the handle. */
+int rspl_ba_submit(rspl_ba* ba, const rspl_ba_problem* problem, rspl_ba_result* result);
+int rspl_ba_join(rspl_ba* ba, long long* calls, long long* iterations, double* ms);
 /* Run this handle's kernels only on the reserve_cus CUs that rspl_stream_create_reserving
  * streams leave free (0 = all CUs, highest stream priority: the default). */
 int rspl_ba_use_reserved_cus(rspl_ba* ba, int reserve_cus);

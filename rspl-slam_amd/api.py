@@ -270,6 +270,29 @@ class LocalBA:
         res.read_back(R)
         return res
 
+    def submit(self, problem, out=None):
+        """Queue `problem` for the handle's native tracking thread (rspl_ba_submit: runs the queued calls
+        in order; blocks while two are waiting, as the reference's feature thread).  Returns the result
+        buffer the call will write (read it after join()); problem and out are kept alive until then."""
+        from .ba_types import DenseResult
+        res = out if out is not None and out.fits(problem) else DenseResult.alloc(problem)
+        P, R = problem.to_ctypes(), res.to_ctypes()
+        inflight = self.__dict__.setdefault("_inflight", [])
+        inflight.append((problem, res, P, R))
+        capi.check(self._lib.rspl_ba_submit(self._h, C.byref(P), C.byref(R)), "rspl_ba_submit")
+        return res
+
+    def join(self):
+        """Wait for every submitted call (rspl_ba_join); raises on the first failure.  Returns
+        (calls, LM iterations summed over them, their summed wall time in ms) since the last join."""
+        n, it, ms = C.c_longlong(), C.c_longlong(), C.c_double()
+        rc = self._lib.rspl_ba_join(self._h, C.byref(n), C.byref(it), C.byref(ms))
+        inflight, self._inflight = self.__dict__.get("_inflight", []), []
+        for _, res, _, R in inflight:
+            res.read_back(R)
+        capi.check(rc, "rspl_ba_join")
+        return n.value, it.value, ms.value
+
     def kernel_timing(self, every: int):
         """HIP-event timing of the LM trials' two launches on every `every`-th call (0: off)."""
         capi.check(self._lib.rspl_ba_kernel_timing(self._h, every), "rspl_ba_kernel_timing")

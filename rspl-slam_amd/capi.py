@@ -31,7 +31,7 @@ EXPORTS = [
     "rspl_sg_status", "rspl_sg_debug_inject", "rspl_sg_debug_sinkhorn", "rspl_sg_debug_decode",
     "rspl_sg_stage_times", "rspl_sg_destroy",
     "rspl_pm_match",
-    "rspl_ba_create", "rspl_ba_local", "rspl_ba_destroy", "rspl_ba_use_reserved_cus", "rspl_ba_kernel_timing",
+    "rspl_ba_create", "rspl_ba_local", "rspl_ba_submit", "rspl_ba_join", "rspl_ba_destroy", "rspl_ba_use_reserved_cus", "rspl_ba_kernel_timing",
     "rspl_ba_kernel_times", "rspl_ba_debug_stage",
     "rspl_frame_create", "rspl_frame_optimize", "rspl_frame_destroy",
     "rspl_ba_set_shard", "rspl_comm_unique_id", "rspl_comm_create", "rspl_comm_allreduce_sum", "rspl_comm_destroy",
@@ -152,6 +152,8 @@ def load(path: pathlib.Path = LIB_PATH):
     if hasattr(lib, "rspl_ba_create"):
         lib.rspl_ba_create.argtypes = [C.POINTER(BaConfig), C.POINTER(vp)]
         lib.rspl_ba_local.argtypes = [vp, vp, vp]
+        lib.rspl_ba_submit.argtypes = [vp, vp, vp]
+        lib.rspl_ba_join.argtypes = [vp, vp, vp, vp]
         lib.rspl_ba_use_reserved_cus.argtypes = [vp, ip]
         lib.rspl_ba_kernel_timing.argtypes = [vp, ip]
         lib.rspl_ba_kernel_times.argtypes = [vp, C.POINTER(C.c_double), C.POINTER(C.c_longlong)]

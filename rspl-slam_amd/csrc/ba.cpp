@@ -22,6 +22,10 @@
 #include <type_traits>
 #include <memory>
 #include <vector>
+#include <condition_variable>
+#include <deque>
+#include <mutex>
+#include <thread>
 
 #include "ba_kernels.hpp"
 #include "common.hpp"
@@ -88,6 +92,21 @@ struct rspl_ba {
   int kev_used = 0;
   double kt_ms[2] = {0, 0};
   long long kt_n[2] = {0, 0};
+  // native tracking thread (rspl_ba_submit / rspl_ba_join): a FIFO of calls run in order by one host
+  // thread of the handle, as the reference's TrackingThread drains _tracking_data_buffer
+  struct Job {
+    const rspl_ba_problem* pr;
+    rspl_ba_result* res;
+  };
+  std::thread worker;
+  std::mutex qmu;
+  std::condition_variable qcv;  // the worker waits for jobs; submitters for room; joiners for idle
+  std::deque<Job> jobs;
+  bool busy = false, quit = false;
+  int q_err = 0;                // first failed call since the last join
+  std::string q_msg;
+  long long q_done = 0, q_iters = 0;
+  double q_ms = 0.0;
 };
 
 namespace {
@@ -126,7 +145,10 @@ struct CallLayout {
     lm_pose = place(4 * (size_t)E);
     pidx = place(4 * (size_t)np); lm_off = place(4 * (nL + 1)); lm_act = place(nL);
     pairs = place(8 * (size_t)np * (np + 1) / 2);
-    ltab = place(16 * ((size_t)E + nl + 1));
+    // line-workgroup table: at most one entry per line landmark plus one per kLineBlk line edges (a
+    // landmark with more edges is split) -- sized tight, as the call uploads [0, bytes) in one copy
+    const size_t line_edges = nobs >= 4 * (size_t)E ? (nobs - 4 * (size_t)E) / 4 : 0;
+    ltab = place(16 * ((size_t)nl + line_edges / ba::kLineBlk + 2));
     level = place(E); flags = place(4 * sizeof(int)); out = place(8 * sizeof(double));  // zeros
     bytes = so;
   }
@@ -655,9 +677,16 @@ extern "C" int rspl_ba_set_shard(rspl_ba* b, int rank, int nranks, rspl_allreduc
 }
 
 extern "C" void rspl_ba_destroy(rspl_ba* b) {
-  if (b)
-    for (hipEvent_t e : b->kev) (void)hipEventDestroy(e);
   if (!b) return;
+  if (b->worker.joinable()) {  // finish the queued calls, then stop the tracking thread
+    {
+      std::lock_guard<std::mutex> lk(b->qmu);
+      b->quit = true;
+    }
+    b->qcv.notify_all();
+    b->worker.join();
+  }
+  for (hipEvent_t e : b->kev) (void)hipEventDestroy(e);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
   if (b->gbuf) (void)hipFree(b->gbuf);
   if (b->pdg) (void)hipFree(b->pdg);
@@ -714,6 +743,66 @@ extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_resu
     return rc;
   }
   set_error("%s", msg.c_str());
+  return rc;
+}
+
+// ---- native tracking thread ----
+namespace {
+constexpr size_t kTrackingBuffer = 2;  // map_builder.cc:176: the feature thread waits while 2 are queued
+
+void tracking_loop(rspl_ba* b) {
+  (void)hipSetDevice(b->cfg.device);
+  std::unique_lock<std::mutex> lk(b->qmu);
+  for (;;) {
+    b->qcv.wait(lk, [&] { return !b->jobs.empty() || b->quit; });
+    if (b->jobs.empty()) return;  // quit with nothing left
+    const rspl_ba::Job j = b->jobs.front();
+    b->jobs.pop_front();
+    b->busy = true;
+    lk.unlock();
+    b->qcv.notify_all();  // room for a submitter
+    const auto t0 = std::chrono::steady_clock::now();
+    const int rc = rspl_ba_local(b, j.pr, j.res);
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    const std::string msg = rc ? std::string(rspl_last_error()) : std::string();
+    lk.lock();
+    b->busy = false;
+    b->q_done++;
+    b->q_ms += ms;
+    if (!rc) b->q_iters += j.res->iterations_done_first + j.res->iterations_done_second;
+    if (rc && !b->q_err) {
+      b->q_err = rc;
+      b->q_msg = msg;
+    }
+    b->qcv.notify_all();  // a joiner may be waiting for idle
+  }
+}
+}  // namespace
+
+extern "C" int rspl_ba_submit(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
+  RSPL_CHECK_ARG(b && pr && res, "rspl_ba_submit: NULL argument");
+  std::unique_lock<std::mutex> lk(b->qmu);
+  if (!b->worker.joinable()) b->worker = std::thread(tracking_loop, b);
+  b->qcv.wait(lk, [&] { return b->jobs.size() < kTrackingBuffer; });
+  b->jobs.push_back({pr, res});
+  lk.unlock();
+  b->qcv.notify_all();
+  return RSPL_OK;
+}
+
+extern "C" int rspl_ba_join(rspl_ba* b, long long* calls, long long* iterations, double* ms) {
+  RSPL_CHECK_ARG(b, "rspl_ba_join: NULL handle");
+  std::unique_lock<std::mutex> lk(b->qmu);
+  b->qcv.wait(lk, [&] { return b->jobs.empty() && !b->busy; });
+  if (calls) *calls = b->q_done;
+  if (iterations) *iterations = b->q_iters;
+  if (ms) *ms = b->q_ms;
+  b->q_done = b->q_iters = 0;
+  b->q_ms = 0.0;
+  const int rc = b->q_err;
+  if (rc) set_error("%s", b->q_msg.c_str());
+  b->q_err = 0;
+  b->q_msg.clear();
   return rc;
 }
 

@@ -2012,6 +2012,11 @@ __device__ __forceinline__ void schur_pair(const double (&H1)[6 * LD], const dou
 // arithmetic (ping-pong operand sets), so a wave waits on one memory round trip per segment rather than
 // per pass.  LD 3: a range of point landmarks only (3x3 D, 6x3 Hpl); 4: a range holding lines.  LOWER: a
 // diagonal pose pair (e1 == e2 pairs add Hpp / bp / Y bl; lower triangle only).
+// Register budget: only the off-diagonal point chunks (most of them) keep the PairOps operand set; the
+// diagonal chunks take e1 == e2 without a copy of H1, and line ranges invert the landmark block before
+// their edge operands are requested, so the kernel fits 256 VGPRs with no AGPRs (was 255 + 52): a
+// chunk wave then fits on a SIMD beside one front-end wave (a fp16 conv or GNN layer wave, <= 224
+// registers) instead of waiting for the SIMD to drain.  The same FMAs in the same order as before.
 template <int LD>
 struct PairOps {
   double D[LD * LD], H1[6 * LD], H2[6 * LD], Hp[21], bpv[6], blv[LD];  // D: Hll of the landmark
@@ -2073,9 +2078,98 @@ __device__ __forceinline__ void chunk_loop(const Lin& L, const Active& A, const 
   for (int k = beg + lane; k < end; k += 64) {
     const int4 q = qn;
     if (k + 64 < end) qn = A.pp[k + 64];
-    PairOps<LD> o;
-    load_pair<LD, LOWER>(L, A, S, nq, q, o);
-    use_pair<LD, LOWER>(o, lambda, bad, acc);
+    if constexpr (LD == 4 && LOWER) {
+      // diagonal pose pairs over line ranges (a few chunks per trial): the landmark inverse first, the
+      // edge operands after it (no operand in flight across the 4x4 Gauss-Jordan) -- this path otherwise
+      // sets the kernel's register budget above 256 (one wave per SIMD, none beside a front-end wave)
+      const int e1 = q.x, e2 = q.y, g = q.z;
+      const bool live = !(A.elevel && (A.elevel[e1] | A.elevel[e2]));
+      double Hd[16], D[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) Hd[i] = S.Hll[16 * g + i];
+      bad |= live && !lm_dinv(Hd, g < nq, lambda, D);
+      asm volatile("" ::: "memory");
+      if (live && e1 == e2) {  // the edge with itself: H1 twice, + Hp / bp / Y bl
+        double H1[24], Hp[21], bpv[6], blv[4];
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+          for (int c = 0; c < 4; c++) H1[r * 4 + c] = L.Hpl[24 * e1 + r * 4 + c];
+#pragma unroll
+        for (int i = 0; i < 21; i++) Hp[i] = L.Hpp[21 * e1 + i];
+#pragma unroll
+        for (int i = 0; i < 6; i++) bpv[i] = L.bp[6 * e1 + i];
+#pragma unroll
+        for (int i = 0; i < 4; i++) blv[i] = S.bl[4 * g + i];
+        schur_pair<LD, LOWER>(H1, H1, true, Hp, bpv, blv, D, acc);
+      } else if (live) {  // two edges of one landmark on the same pose (rare)
+        double H1[24], H2[24], Hp[21], bpv[6], blv[4];
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            H1[r * 4 + c] = L.Hpl[24 * e1 + r * 4 + c];
+            H2[r * 4 + c] = L.Hpl[24 * e2 + r * 4 + c];
+          }
+        schur_pair<LD, LOWER>(H1, H2, false, Hp, bpv, blv, D, acc);
+      }
+    } else if constexpr (LD == 4) {  // off-diagonal pose pairs over line ranges: the inverse first as well
+      const int e1 = q.x, e2 = q.y, g = q.z;
+      const bool live = !(A.elevel && (A.elevel[e1] | A.elevel[e2]));
+      double Hd[16], D[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) Hd[i] = S.Hll[16 * g + i];
+      bad |= live && !lm_dinv(Hd, g < nq, lambda, D);
+      asm volatile("" ::: "memory");
+      if (live) {
+        double H1[24], H2[24], Hp[21], bpv[6], blv[4];
+#pragma unroll
+        for (int r = 0; r < 6; r++)
+#pragma unroll
+          for (int c = 0; c < 4; c++) {
+            H1[r * 4 + c] = L.Hpl[24 * e1 + r * 4 + c];
+            H2[r * 4 + c] = L.Hpl[24 * e2 + r * 4 + c];
+          }
+        schur_pair<LD, LOWER>(H1, H2, false, Hp, bpv, blv, D, acc);
+      }
+    } else if constexpr (LOWER) {  // diagonal pose pairs over point ranges: e1 == e2 without an H2 copy
+      const int e1 = q.x, e2 = q.y, g = q.z;
+      const bool live = !(A.elevel && (A.elevel[e1] | A.elevel[e2]));
+      double Hd[9], D[9], H1[18], Hp[21], bpv[6], blv[3];
+#pragma unroll
+      for (int i = 0; i < 9; i++) Hd[i] = S.Hll[16 * g + i];
+#pragma unroll
+      for (int r = 0; r < 6; r++)
+#pragma unroll
+        for (int c = 0; c < 3; c++) H1[r * 3 + c] = L.Hpl[24 * e1 + r * 4 + c];
+      if (e1 == e2) {
+#pragma unroll
+        for (int i = 0; i < 21; i++) Hp[i] = L.Hpp[21 * e1 + i];
+#pragma unroll
+        for (int i = 0; i < 6; i++) bpv[i] = L.bp[6 * e1 + i];
+#pragma unroll
+        for (int i = 0; i < 3; i++) blv[i] = S.bl[4 * g + i];
+      }
+      if (live) {
+#pragma unroll
+        for (int i = 0; i < 9; i++) Hd[i] += (i % 4 == 0) ? lambda : 0.0;
+        bad |= !small_inv<3>(Hd, D);
+        if (e1 == e2) {
+          schur_pair<LD, LOWER>(H1, H1, true, Hp, bpv, blv, D, acc);
+        } else {
+          double H2[18];
+#pragma unroll
+          for (int r = 0; r < 6; r++)
+#pragma unroll
+            for (int c = 0; c < 3; c++) H2[r * 3 + c] = L.Hpl[24 * e2 + r * 4 + c];
+          schur_pair<LD, LOWER>(H1, H2, false, Hp, bpv, blv, D, acc);
+        }
+      }
+    } else {
+      PairOps<LD> o;
+      load_pair<LD, LOWER>(L, A, S, nq, q, o);
+      use_pair<LD, LOWER>(o, lambda, bad, acc);
+    }
   }
 }
 

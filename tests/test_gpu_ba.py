@@ -162,3 +162,35 @@ def test_ba_run_into_reused_result(ba):
     other = ba.run(p2, out=out)  # shapes differ: a new result
     assert other is not out and other.points.shape == p2.points.shape
     _compare(other, oracle.ba_local(p2), **LINE_TOL)
+
+
+def test_ba_native_tracking_thread(ba):
+    """rspl_ba_submit / rspl_ba_join (the handle's native tracking thread, map_builder.cc:188-276): queued
+    calls run in order and give the same bytes as rspl_ba_local; the join reports calls, LM iterations
+    and the first failure (a problem with an out-of-range pose id), after which the queue keeps working."""
+    probs = [SY.ba_problem(n_poses=4 + k, n_points=250 + 50 * k, n_lines=6 + 2 * k, seed=90 + k, pixel_sigma=0.8,
+                           outlier_frac=0.05)[0] for k in range(5)]
+    want = [ba.run(p) for p in probs]
+    outs = [ba.submit(p) for p in probs + probs[:2]]  # 7 calls: more than the 2-deep buffer
+    n, its, ms = ba.join()
+    assert n == 7 and ms > 0
+    assert its == sum(w.iters_first + w.iters_second for w in want + want[:2])
+    for got, w in zip(outs, want + want[:2]):
+        np.testing.assert_array_equal(got.pose_q, w.pose_q)
+        np.testing.assert_array_equal(got.pose_p, w.pose_p)
+        np.testing.assert_array_equal(got.points, w.points)
+        np.testing.assert_array_equal(got.lines, w.lines)
+        for k in ("mono", "stereo", "mono_line", "stereo_line"):
+            np.testing.assert_array_equal(got.inlier[k], w.inlier[k])
+        assert (got.chi2_second, got.iters_second) == (w.chi2_second, w.iters_second)
+    bad = SY.ba_problem(n_poses=4, n_points=250, n_lines=6, seed=90, pixel_sigma=0.8, outlier_frac=0.05)[0]
+    bad.mono["pose"] = bad.mono["pose"].copy()
+    bad.mono["pose"][0] = bad.pose_q.shape[0]  # references a missing pose
+    ba.submit(probs[1])
+    ba.submit(bad)
+    ba.submit(probs[2])
+    with pytest.raises(Exception, match="missing vertex"):
+        ba.join()
+    got = ba.submit(probs[3])
+    assert ba.join()[0] == 1
+    np.testing.assert_array_equal(got.points, want[3].points)

@@ -46,6 +46,7 @@ import oracle  # noqa: E402
 import post  # noqa: E402
 
 H, W, K = 480, 752, 400
+DISP = 12  # synthetic.stereo_pair's default disparity
 
 
 def key_index(F):
@@ -179,7 +180,16 @@ def main():
             dist_c = {(int(q), int(tt)): d for (q, tt), d in zip(np.asarray(mc).reshape(-1, 2), post.match_points(*dc)[1])}
             dist_g = {(int(q), int(tt)): d for q, tt, d in pms["fp32"].MatchingPoints(Fg[0], Fg[1])[1]}
             dist_err = max((abs(dist_c[k] - dist_g[k]) for k in dist_c if k in dist_g), default=0.0)
+            # geometry: stereo_pair's right view is the left texture shifted by +DISP px (plus sensor
+            # noise), so keypoint (x, y) of the left image sits at (x + DISP, y) in the right one
+            kl, kr = Fc[0][1:3].T, Fc[1][1:3].T
+            rep = float(np.mean([np.hypot(kr[:, 0] - (x + DISP), kr[:, 1] - y).min() <= 2.0 for x, y in kl])) \
+                if len(kl) and len(kr) else 0.0
+            mcc = np.asarray(mc).reshape(-1, 2)
+            geo = int(np.sum((np.abs(Fc[1][1, mcc[:, 1]] - Fc[0][1, mcc[:, 0]] - DISP) <= 2.0) &
+                             (np.abs(Fc[1][2, mcc[:, 1]] - Fc[0][2, mcc[:, 0]]) <= 2.0))) if len(mcc) else 0
             row = {"pair": t,
+                   "keypoint_repeatability_cpu": rep, "thresholded_matches_geometric_cpu": geo,
                    "keypoints": [int(Fc[0].shape[1]), int(Fc[1].shape[1])],
                    "keypoint_sets_identical": bool(set(kc) == set(kg)) and
                    set(key_index(Fc[1])) == set(key_index(Fg[1])),
@@ -226,6 +236,12 @@ def main():
         "match_distance_max_abs_diff_fp32": float(max(r["match_distance_max_abs_diff_fp32"] for r in rows)),
         "matches_per_pair_cpu": agg("matches_cpu"),
         "matches_per_pair_min_cpu": int(min(r["matches_cpu"] for r in rows)),
+        # the seeded (untrained) networks: how many keypoints repeat under the pair's pure +DISP px shift,
+        # and how many thresholded matches are geometrically right -- the C1 record is plumbing (the
+        # same bytes through two implementations), not a tracking-quality measurement
+        "keypoint_repeatability_cpu_mean": agg("keypoint_repeatability_cpu"),
+        "thresholded_matches_geometric_frac_cpu": float(sum(r["thresholded_matches_geometric_cpu"] for r in rows) /
+                                                       max(1, sum(r["matches_cpu"] for r in rows))),
         "sg_fp16_on_cpu_features": {
             "index_agreement_mean": float(np.mean([r["sg16_on_cpu_features"]["index_agreement"] for r in rows])),
             "index_agreement_min": float(min(r["sg16_on_cpu_features"]["index_agreement"] for r in rows)),
