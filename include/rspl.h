@@ -311,7 +311,9 @@ void rspl_ba_destroy(rspl_ba* ba);
  * call for the handle's native host thread, which runs the queued calls in order (rspl_ba_local each);
  * like the reference's feature thread it blocks while two calls are already waiting
  * (_tracking_data_buffer, map_builder.cc:176).  problem, its arrays and result must stay valid until
- * the call has run.  rspl_ba_join waits until every queued call has run and returns the first failure
+ * the call has run.  A queued call's inputs are read (staged) by a second host thread of the handle as
+ * soon as a staging slot is free -- while the previous call still runs on the device -- so do not
+ * modify a problem after submitting it.  rspl_ba_join waits until every queued call has run and returns the first failure
  * since the previous join (0: none), with the number of calls, their LM iterations (first + second
  * optimize) and their summed wall time in ms (each may be NULL).  Do not call rspl_ba_local on the
  * handle while calls are queued; rspl_ba_destroy runs the queued calls before it frees the handle. */

@@ -33,6 +33,12 @@
 
 using namespace rspl;
 
+namespace rspl {
+namespace ba {
+struct StagedCall;  // one call's host staging (below)
+}
+}  // namespace rspl
+
 struct rspl_ba {
   rspl_ba_config cfg{};
   hipStream_t stream = nullptr;
@@ -61,10 +67,12 @@ struct rspl_ba {
   // zeroed level / fill / flags / out), laid out exactly like the staging buffer's call
   // region: one upload per call (capacity fixed at create)
   char* cbuf = nullptr;
-  // pinned, host-mapped staging for uploads; the final kernel writes results straight into it
-  char* stage = nullptr;
-  char* stage_dev = nullptr;
-  size_t stage_cap = 0;
+  // pinned, host-mapped staging for uploads; the final kernel writes results straight into it.
+  // Two slots: the tracking thread's next queued call is staged into one while the running call
+  // reads its results from the other
+  char* stage[2] = {nullptr, nullptr};
+  char* stage_dev[2] = {nullptr, nullptr};
+  size_t stage_cap[2] = {0, 0};
   // host-mapped mailbox
   ba::Mail* mail = nullptr;
   ba::Mail* mail_dev = nullptr;
@@ -97,8 +105,12 @@ struct rspl_ba {
   struct Job {
     const rspl_ba_problem* pr;
     rspl_ba_result* res;
+    std::shared_ptr<ba::StagedCall> sc;  // its host staging (made by the staging thread)
+    int state;                            // 0 waiting, 1 being staged, 2 staged
   };
   std::thread worker;
+  std::thread stager;  // stages the next queued call into the free slot while the worker runs one
+  bool slot_busy[2] = {false, false};
   std::mutex qmu;
   std::condition_variable qcv;  // the worker waits for jobs; submitters for room; joiners for idle
   std::deque<Job> jobs;
@@ -131,6 +143,7 @@ inline size_t al256(size_t x) { return (x + 255) & ~size_t(255); }
 struct CallLayout {
   size_t cams, T, X, L, obs, type, pose, lm, cam, gmap, lm_pose, pidx, lm_off, lm_act, pairs, ltab, level, flags, out,
       bytes;
+  CallLayout() = default;
   CallLayout(int ncam, int np, int nq, int nl, int E, size_t nobs) {  // nobs: observation doubles (4 / 8 per edge)
     const size_t nL = (size_t)nq + nl;
     size_t so = 0;
@@ -157,11 +170,52 @@ struct CallLayout {
 // result layout written by the final kernel into the mapped staging buffer
 struct DownLayout {
   size_t inl, T, X, L, bytes;
+  DownLayout() = default;
   DownLayout(int np, int nq, int nl, int E) {
     inl = 0; T = al256(E); X = T + al256(sizeof(double) * 8 * np); L = X + al256(sizeof(double) * 3 * nq);
     bytes = L + al256(sizeof(double) * 6 * nl);
   }
 };
+
+// RSPL_BA_TIMING=1: host stage times of a call, microseconds since the previous mark, one stderr line
+struct HostMarks {
+  static bool on() {
+    static const bool t = getenv("RSPL_BA_TIMING") != nullptr;
+    return t;
+  }
+  std::chrono::steady_clock::time_point t[16];
+  const char* name[16];
+  int n = 0;
+  void mark(const char* s) {
+    if (on() && n < 16) {
+      name[n] = s;
+      t[n++] = std::chrono::steady_clock::now();
+    }
+  }
+  void print(const char* label) const {
+    if (!on()) return;
+    fprintf(stderr, "%s", label);
+    for (int i = 1; i < n; i++)
+      fprintf(stderr, " %s %.1f", name[i], std::chrono::duration<double, std::micro>(t[i] - t[i - 1]).count());
+    fprintf(stderr, "\n");
+  }
+};
+
+}  // namespace
+
+// one call's host staging: its slot and what the device part needs of it
+struct rspl::ba::StagedCall {
+  int slot = 0;
+  int rc = RSPL_OK;  // staging failed (argument errors): reported when the call's turn comes
+  std::string msg;
+  int E = 0, Ep = 0, K = 0, n_lblk = 0;
+  size_t pair_bound = 0;
+  CallLayout cl;
+  DownLayout dl;
+  HostMarks tm;
+};
+
+namespace {
 
 template <typename F>
 void carve(F& ar, rspl_ba* b) {
@@ -193,17 +247,17 @@ void carve(F& ar, rspl_ba* b) {
   take(b->pp_cnt, npairs * nchk); take(b->pp_off, npairs * nchk + 1);
 }
 
-int ensure_stage(rspl_ba* b, size_t bytes) {
-  if (bytes <= b->stage_cap) return RSPL_OK;
+int ensure_stage(rspl_ba* b, int slot, size_t bytes) {
+  if (bytes <= b->stage_cap[slot]) return RSPL_OK;
   // copies from the old buffer may still be in flight
   RSPL_HIP(hipStreamSynchronize(b->stream));
-  if (b->stage) (void)hipHostFree(b->stage);
-  b->stage = nullptr;
-  const size_t cap = std::max(bytes, b->stage_cap * 2);
-  b->stage_cap = 0;
-  RSPL_HIP(hipHostMalloc((void**)&b->stage, cap, hipHostMallocMapped | hipHostMallocCoherent));
-  RSPL_HIP(hipHostGetDevicePointer((void**)&b->stage_dev, b->stage, 0));
-  b->stage_cap = cap;
+  if (b->stage[slot]) (void)hipHostFree(b->stage[slot]);
+  b->stage[slot] = nullptr;
+  const size_t cap = std::max(bytes, b->stage_cap[slot] * 2);
+  b->stage_cap[slot] = 0;
+  RSPL_HIP(hipHostMalloc((void**)&b->stage[slot], cap, hipHostMallocMapped | hipHostMallocCoherent));
+  RSPL_HIP(hipHostGetDevicePointer((void**)&b->stage_dev[slot], b->stage[slot], 0));
+  b->stage_cap[slot] = cap;
   return RSPL_OK;
 }
 
@@ -685,6 +739,7 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
     }
     b->qcv.notify_all();
     b->worker.join();
+    b->stager.join();
   }
   for (hipEvent_t e : b->kev) (void)hipEventDestroy(e);
   if (b->stream) (void)hipStreamSynchronize(b->stream);
@@ -694,7 +749,8 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
   if (b->cbuf) (void)hipFree(b->cbuf);
   if (b->pp_buf) (void)hipFree(b->pp_buf);
   if (b->prof) (void)hipFree(b->prof);
-  if (b->stage) (void)hipHostFree(b->stage);
+  for (char* sg : b->stage)
+    if (sg) (void)hipHostFree(sg);
   if (b->mail) (void)hipHostFree(b->mail);
   if (b->stream) (void)hipStreamDestroy(b->stream);
   delete b;
@@ -702,6 +758,13 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
 
 namespace {
 int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res);
+int stage_call(rspl_ba* b, int slot, const rspl_ba_problem* pr, rspl_ba_result* res, ba::StagedCall& c);
+int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rspl_ba_result* res);
+
+void begin_call(rspl_ba* b) {
+  b->ktime_on = b->ktime_every > 0 && b->ncalls++ % (unsigned long long)b->ktime_every == 0;
+  b->kev_used = 0;
+  b->kev_eval.clear();
 }
 
 // A device-side failure can return while the call's kernel chain is still queued or running (a
@@ -709,6 +772,20 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res);
 // (the next call restages the mapped buffers the old chain reads) and re-arm the cross-call
 // tickets and release flags the chain may have left half-counted.  If the drain itself fails the
 // device is gone and the handle must be recreated (the error says so).
+int end_call(rspl_ba* b, int rc) {
+  if (rc != RSPL_E_DEVICE) return rc;
+  const std::string msg = rspl_last_error();
+  if (hipStreamSynchronize(b->stream) != hipSuccess ||
+      hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
+      hipMemset(b->pair_ctr, 0, sizeof(unsigned) * (b->maxK * (b->maxK + 1) / 2 + 1)) != hipSuccess) {
+    set_error("%s; the BA stream could not be drained: recreate the handle", msg.c_str());
+    return rc;
+  }
+  set_error("%s", msg.c_str());
+  return rc;
+}
+}  // namespace
+
 extern "C" int rspl_ba_kernel_timing(rspl_ba* b, int every) {
   RSPL_CHECK_ARG(b && every >= 0, "rspl_ba_kernel_timing: NULL handle or every < 0");
   b->ktime_every = every;
@@ -728,33 +805,57 @@ extern "C" int rspl_ba_kernel_times(rspl_ba* b, double* ms, long long* launches)
 }
 
 extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
-  if (b) {
-    b->ktime_on = b->ktime_every > 0 && b->ncalls++ % (unsigned long long)b->ktime_every == 0;
-    b->kev_used = 0;
-    b->kev_eval.clear();
-  }
-  const int rc = ba_local_impl(b, pr, res);
-  if (rc != RSPL_E_DEVICE || !b) return rc;
-  const std::string msg = rspl_last_error();
-  if (hipStreamSynchronize(b->stream) != hipSuccess ||
-      hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
-      hipMemset(b->pair_ctr, 0, sizeof(unsigned) * (b->maxK * (b->maxK + 1) / 2 + 1)) != hipSuccess) {
-    set_error("%s; the BA stream could not be drained: recreate the handle", msg.c_str());
-    return rc;
-  }
-  set_error("%s", msg.c_str());
-  return rc;
+  if (!b) return ba_local_impl(b, pr, res);
+  begin_call(b);
+  return end_call(b, ba_local_impl(b, pr, res));
 }
 
 // ---- native tracking thread ----
+// Two host threads per handle: the staging thread stages each queued call (validation, landmark-CSR
+// scatter, tables: host work only) into a free staging slot as soon as it is queued; the tracking
+// thread runs the staged calls on the device in order.  The next call's staging therefore overlaps
+// the current call's LM trials instead of preceding them on the tracking thread's critical path; the
+// calls still run one at a time and in submission order, each on the inputs given at submission.
 namespace {
 constexpr size_t kTrackingBuffer = 2;  // map_builder.cc:176: the feature thread waits while 2 are queued
+
+void staging_loop(rspl_ba* b) {
+  (void)hipSetDevice(b->cfg.device);
+  std::unique_lock<std::mutex> lk(b->qmu);
+  for (;;) {
+    rspl_ba::Job* j = nullptr;
+    int slot = -1;
+    b->qcv.wait(lk, [&] {
+      j = nullptr;
+      for (rspl_ba::Job& q : b->jobs)
+        if (q.state == 0) {
+          j = &q;
+          break;
+        }
+      slot = !b->slot_busy[0] ? 0 : !b->slot_busy[1] ? 1 : -1;
+      return (j && slot >= 0) || (b->quit && !j);
+    });
+    if (!j) return;  // quit with every queued call staged
+    j->state = 1;    // (deque elements stay in place while others are pushed; j is popped only when staged)
+    b->slot_busy[slot] = true;
+    const std::shared_ptr<ba::StagedCall> sc = j->sc;
+    const rspl_ba_problem* pr = j->pr;
+    rspl_ba_result* res = j->res;
+    lk.unlock();
+    sc->slot = slot;
+    sc->rc = stage_call(b, slot, pr, res, *sc);
+    if (sc->rc) sc->msg = rspl_last_error();
+    lk.lock();
+    j->state = 2;
+    b->qcv.notify_all();  // the tracking thread may be waiting for it
+  }
+}
 
 void tracking_loop(rspl_ba* b) {
   (void)hipSetDevice(b->cfg.device);
   std::unique_lock<std::mutex> lk(b->qmu);
   for (;;) {
-    b->qcv.wait(lk, [&] { return !b->jobs.empty() || b->quit; });
+    b->qcv.wait(lk, [&] { return (!b->jobs.empty() && b->jobs.front().state == 2) || (b->quit && b->jobs.empty()); });
     if (b->jobs.empty()) return;  // quit with nothing left
     const rspl_ba::Job j = b->jobs.front();
     b->jobs.pop_front();
@@ -762,10 +863,18 @@ void tracking_loop(rspl_ba* b) {
     lk.unlock();
     b->qcv.notify_all();  // room for a submitter
     const auto t0 = std::chrono::steady_clock::now();
-    const int rc = rspl_ba_local(b, j.pr, j.res);
+    int rc;
+    if (j.sc->rc) {
+      set_error("%s", j.sc->msg.c_str());
+      rc = j.sc->rc;
+    } else {
+      begin_call(b);
+      rc = end_call(b, run_call(b, *j.sc, j.pr, j.res));
+    }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     const std::string msg = rc ? std::string(rspl_last_error()) : std::string();
     lk.lock();
+    b->slot_busy[j.sc->slot] = false;
     b->busy = false;
     b->q_done++;
     b->q_ms += ms;
@@ -774,7 +883,7 @@ void tracking_loop(rspl_ba* b) {
       b->q_err = rc;
       b->q_msg = msg;
     }
-    b->qcv.notify_all();  // a joiner may be waiting for idle
+    b->qcv.notify_all();  // a joiner may be waiting for idle; the staging thread for a free slot
   }
 }
 }  // namespace
@@ -782,9 +891,12 @@ void tracking_loop(rspl_ba* b) {
 extern "C" int rspl_ba_submit(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   RSPL_CHECK_ARG(b && pr && res, "rspl_ba_submit: NULL argument");
   std::unique_lock<std::mutex> lk(b->qmu);
-  if (!b->worker.joinable()) b->worker = std::thread(tracking_loop, b);
+  if (!b->worker.joinable()) {
+    b->worker = std::thread(tracking_loop, b);
+    b->stager = std::thread(staging_loop, b);
+  }
   b->qcv.wait(lk, [&] { return b->jobs.size() < kTrackingBuffer; });
-  b->jobs.push_back({pr, res});
+  b->jobs.push_back({pr, res, std::make_shared<ba::StagedCall>(), 0});
   lk.unlock();
   b->qcv.notify_all();
   return RSPL_OK;
@@ -830,7 +942,9 @@ extern "C" int rspl_ba_debug_stage(const rspl_ba_problem* pr, int par_edges, int
 }
 
 namespace {
-int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
+// Host staging of one call into stage slot `slot` (inputs only: nothing touches the device or the
+// stream in steady state, so the tracking thread's next call is staged while the current one runs)
+int stage_call(rspl_ba* b, int slot, const rspl_ba_problem* pr, rspl_ba_result* res, ba::StagedCall& c) {
   RSPL_CHECK_ARG(b && pr && res, "rspl_ba_local: NULL argument");
   const int np = pr->n_poses, nq = pr->n_points, nl = pr->n_lines;
   const int ne[4] = {pr->n_mono, pr->n_stereo, pr->n_mono_line, pr->n_stereo_line};
@@ -841,34 +955,22 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   RSPL_CHECK_ARG(pr->n_cameras >= 1 && pr->n_cameras <= kMaxCams && pr->cameras, "1..16 cameras required");
   RSPL_CHECK_ARG(res->pose_q && res->pose_p && (res->points || !nq) && (res->lines || !nl), "NULL result arrays");
   RSPL_CHECK_ARG(np == 0 || pr->pose_fixed, "NULL pose_fixed");
-  hipStream_t st = b->stream;
   const int Eg = ne[0] + ne[1] + ne[2] + ne[3], nL = nq + nl;
   // landmark sharding: this rank keeps the edges of its landmarks (g % nranks == rank)
   const bool sh = b->allreduce != nullptr;
-  // optional host-side stage timing (RSPL_BA_TIMING=1), in microseconds since the previous mark
-  static const bool timing = getenv("RSPL_BA_TIMING") != nullptr;
-  using clk = std::chrono::steady_clock;
-  clk::time_point tmark[16];
-  const char* tname[16];
-  int ntm = 0;
-  auto mark = [&](const char* name) {
-    if (timing && ntm < 16) {
-      tname[ntm] = name;
-      tmark[ntm++] = clk::now();
-    }
-  };
-  mark("start");
+  HostMarks tm;
+  tm.mark("start");
   // ---- one staging region for the whole call, mirrored by the device call buffer ----
   int rc;
   // pass 1: validate, count the local edges per landmark, mark the poses with edges (ba_stage.cpp;
   // large unsharded calls on the handle's host workers)
   if ((rc = b->stg.count(pr, sh, b->rank, b->nranks, kParEdges))) return rc;
   const int E = b->stg.E, Ep = b->stg.Ep, n_line_local = E - Ep;
-  mark("count");
+  tm.mark("count");
   const CallLayout cl(pr->n_cameras, np, nq, nl, E, 4 * (size_t)Ep + 8 * (size_t)(E - Ep));
   const DownLayout dl(np, nq, nl, Eg);  // inlier flags by global edge id
-  if ((rc = ensure_stage(b, std::max(cl.bytes, dl.bytes)))) return rc;
-  char* sg = b->stage;
+  if ((rc = ensure_stage(b, slot, std::max(cl.bytes, dl.bytes)))) return rc;
+  char* sg = b->stage[slot];
   // vertices: VertexSE3Expmap estimate = SE3Quat(q, p).inverse() (g2o_optimization.cc:42)
   double* T = reinterpret_cast<double*>(sg + cl.T);
   for (int p = 0; p < np; p++) {
@@ -891,7 +993,7 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   // edge id (landmark-CSR order, input order within a landmark: the order every per-landmark
   // reduction follows)
   int* lm_off = reinterpret_cast<int*>(sg + cl.lm_off);
-  mark("vertices");
+  tm.mark("vertices");
   {
     ba::Stager::Out so;
     so.lm_off = lm_off;
@@ -905,22 +1007,13 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
     so.pidx = pidx;
     b->stg.place(pr, so);
   }
-  mark("scatter");
+  tm.mark("scatter");
   uint8_t* lm_act = reinterpret_cast<uint8_t*>(sg + cl.lm_act);
   size_t pair_bound = 0;  // sum_g k_g^2 >= edge pairs of any pose pair
   for (int g = 0; g < nL; g++) {
     const size_t k = lm_off[g + 1] - lm_off[g];
     pair_bound += k * k;
     lm_act[g] = k > 0;
-  }
-  if (pair_bound > b->pp_cap) {  // grow the edge-pair lists (the stream is idle between calls)
-    RSPL_HIP(hipStreamSynchronize(st));
-    if (b->pp_buf) (void)hipFree(b->pp_buf);
-    b->pp_buf = nullptr;
-    b->pp_cap = 0;
-    const size_t cap = std::max(pair_bound, (size_t)1 << 16);
-    RSPL_HIP(hipMalloc((void**)&b->pp_buf, sizeof(int4) * cap));
-    b->pp_cap = cap;
   }
   // line workgroups: consecutive line landmarks packed whole into <= kLineBlk edges (and <=
   // kLineBlk landmarks), so a workgroup sums their blocks itself; a landmark with more edges
@@ -958,13 +1051,49 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
       pairs[2 * q] = a;
       pairs[2 * q + 1] = c;
     }
-  mark("tables");
+  tm.mark("tables");
   memcpy(sg + cl.cams, pr->cameras, sizeof(double) * 5 * pr->n_cameras);
   if (nq) memcpy(sg + cl.X, pr->points, sizeof(double) * 3 * nq);
   if (nl) memcpy(sg + cl.L, pr->lines, sizeof(double) * 6 * nl);
   memset(sg + cl.level, 0, cl.bytes - cl.level);  // level, flags, out start at zero
+  c.slot = slot;
+  c.E = E;
+  c.Ep = Ep;
+  c.K = K;
+  c.n_lblk = n_lblk;
+  c.pair_bound = pair_bound;
+  c.cl = cl;
+  c.dl = dl;
+  c.tm = tm;
+  return RSPL_OK;
+}
+
+// The device part of one staged call: upload, both optimize() calls, results
+int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rspl_ba_result* res) {
+  const int np = pr->n_poses, nq = pr->n_points, nl = pr->n_lines;
+  const int ne[4] = {pr->n_mono, pr->n_stereo, pr->n_mono_line, pr->n_stereo_line};
+  hipStream_t st = b->stream;
+  const int Eg = ne[0] + ne[1] + ne[2] + ne[3], nL = nq + nl;
+  const bool sh = b->allreduce != nullptr;
+  const int E = c.E, Ep = c.Ep, n_line_local = E - Ep, K = c.K, n_lblk = c.n_lblk;
+  const size_t pair_bound = c.pair_bound;
+  const CallLayout& cl = c.cl;
+  const DownLayout& dl = c.dl;
+  char* sg = b->stage[c.slot];
+  HostMarks tm = c.tm;
+  int rc;
+  tm.mark("run");
+  if (pair_bound > b->pp_cap) {  // grow the edge-pair lists (the stream is idle between calls)
+    RSPL_HIP(hipStreamSynchronize(st));
+    if (b->pp_buf) (void)hipFree(b->pp_buf);
+    b->pp_buf = nullptr;
+    b->pp_cap = 0;
+    const size_t cap = std::max(pair_bound, (size_t)1 << 16);
+    RSPL_HIP(hipMalloc((void**)&b->pp_buf, sizeof(int4) * cap));
+    b->pp_cap = cap;
+  }
   RSPL_HIP(hipMemcpyAsync(b->cbuf, sg, cl.bytes, hipMemcpyHostToDevice, st));
-  mark("upload");
+  tm.mark("upload");
   char* cb = b->cbuf;
   uint8_t* level = reinterpret_cast<uint8_t*>(cb + cl.level);
   ba::Problem P{};
@@ -1033,11 +1162,11 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   // bench 2.17 ms per step instead of 1.5 with a side stream for the pair lists
   const bool pp_fused = dev_lm(b, A, pr->iterations_first);  // else: built here, before the first optimize
   if (!pp_fused) RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, st));
-  mark("pairs");
+  tm.mark("pairs");
   if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first, nullptr,
                      pp_fused)))
     return rc;
-  mark("opt1");
+  tm.mark("opt1");
   // ---- phase 2: level-0 edges, no kernel (initializeOptimization(0), :176-213) ----
   // Same active structure with the level-1 edges masked (exact-zero records, no cost, errors
   // kept as g2o keeps them), landmark activity recomputed from the levels on the device (device LM:
@@ -1054,15 +1183,15 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
     if ((rc = optimize(b, P, Lr, S, A, pr->iterations_second, &res->chi2_second, &res->iterations_done_second,
                        fused ? level : nullptr)))
       return rc;
-    mark("opt2");
+    tm.mark("opt2");
   }
   // ---- inlier flags + final state written by the GPU into the mapped staging buffer ----
   // (the staging call region was consumed by the upload long before: the stream is in order)
   const unsigned long long q = ++b->seq;
-  uint8_t* inl_h = reinterpret_cast<uint8_t*>(b->stage_dev + dl.inl);
-  double* T_h = reinterpret_cast<double*>(b->stage_dev + dl.T);
-  double* X_h = reinterpret_cast<double*>(b->stage_dev + dl.X);
-  double* L_h = reinterpret_cast<double*>(b->stage_dev + dl.L);
+  uint8_t* inl_h = reinterpret_cast<uint8_t*>(b->stage_dev[c.slot] + dl.inl);
+  double* T_h = reinterpret_cast<double*>(b->stage_dev[c.slot] + dl.T);
+  double* X_h = reinterpret_cast<double*>(b->stage_dev[c.slot] + dl.X);
+  double* L_h = reinterpret_cast<double*>(b->stage_dev[c.slot] + dl.L);
   if (sh) {  // owned landmarks + local edge flags gathered by one more all-reduce: complete on every rank
     const size_t glen = 3 * (size_t)nq + 6 * (size_t)nl + Eg;
     if (glen > b->gcap) {
@@ -1104,13 +1233,13 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
                   h[8 * k + 6], h[8 * k + 7]);
     (void)hipMemset(b->lm_trace, 0, sizeof(double) * h.size());
   }
-  if (nq) memcpy(res->points, b->stage + dl.X, sizeof(double) * 3 * nq);
-  if (nl) memcpy(res->lines, b->stage + dl.L, sizeof(double) * 6 * nl);
-  const double* Tout = reinterpret_cast<const double*>(b->stage + dl.T);
+  if (nq) memcpy(res->points, b->stage[c.slot] + dl.X, sizeof(double) * 3 * nq);
+  if (nl) memcpy(res->lines, b->stage[c.slot] + dl.L, sizeof(double) * 6 * nl);
+  const double* Tout = reinterpret_cast<const double*>(b->stage[c.slot] + dl.T);
   uint8_t* outs[4] = {res->mono_inlier, res->stereo_inlier, res->mono_line_inlier, res->stereo_line_inlier};
   int e = 0;
   for (int t = 0; t < 4; t++) {
-    if (outs[t]) memcpy(outs[t], b->stage + dl.inl + e, ne[t]);
+    if (outs[t]) memcpy(outs[t], b->stage[c.slot] + dl.inl + e, ne[t]);
     e += ne[t];
   }
   // write back T_wc = estimate().inverse() (:235-240)
@@ -1125,13 +1254,15 @@ int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
     res->pose_q[4 * p + 3] = Twc.q[0];
     for (int k = 0; k < 3; k++) res->pose_p[3 * p + k] = Twc.t[k];
   }
-  mark("final");
-  if (timing) {
-    fprintf(stderr, "rspl_ba_local us:");
-    for (int i = 1; i < ntm; i++)
-      fprintf(stderr, " %s %.1f", tname[i], std::chrono::duration<double, std::micro>(tmark[i] - tmark[i - 1]).count());
-    fprintf(stderr, "\n");
-  }
+  tm.mark("final");
+  tm.print("rspl_ba_local us:");
   return RSPL_OK;
+}
+
+int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
+  RSPL_CHECK_ARG(b && pr && res, "rspl_ba_local: NULL argument");
+  ba::StagedCall c;
+  const int rc = stage_call(b, 0, pr, res, c);
+  return rc ? rc : run_call(b, c, pr, res);
 }
 }  // namespace
