@@ -6,7 +6,7 @@
 # GPU step has its own time limit; the chain stops at the first failure.
 set -o pipefail
 R=$PWD
-ROUND=${ROUND:-r03}
+ROUND=${ROUND:-r04}
 mkdir -p gpurun_out
 if [ -z "$SKIP_TESTS" ]; then
 timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/gpu_tests.log; exit 1; }
