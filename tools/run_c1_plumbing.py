@@ -171,6 +171,13 @@ def main():
             za = align_z(Zg, Fg[0], Fg[1], Fc[0], Fc[1])
             za16 = align_z(res["fp16"][3], F16[0], F16[1], Fc[0], Fc[1])
             zerr = float(np.abs(za - Z).max()) if za is not None else float("nan")
+            # fp32 thresholded-decode disagreements (GPU Z in the CPU order) must be near-ties of the CPU Z
+            bad32 = -1
+            if za is not None:
+                sig32 = Z > np.log(1e-4)
+                dz32 = float(np.abs(za - Z)[sig32].max()) if sig32.any() else 0.0
+                da = post.decode(za)
+                bad32 = len(unexplained_match_disagreements(Z, da[0], da[1], dc[0], dc[1], 2.0 * dz32))
             dp, dzs = z_errors(za, Z) if za is not None else (float("nan"), float("nan"))
             dp16, _ = z_errors(za16, Z) if za16 is not None else (float("nan"), float("nan"))
             order_same = all(np.array_equal(Fg[i][1:3], Fc[i][1:3]) for i in (0, 1) if Fg[i].shape == Fc[i].shape)
@@ -200,6 +207,7 @@ def main():
                    "matches_cpu": len(sc_), "matches_gpu_fp32": len(sg_), "matches_identical": sc_ == sg_,
                    "matches_identical_coords": match_coords(mc, Fc[0], Fc[1]) == match_coords(mg, Fg[0], Fg[1]),
                    "match_distance_max_abs_diff_fp32": float(dist_err),
+                   "unexplained_disagreements_fp32": bad32,
                    "sg16_on_cpu_features": {"matches": int(n16), "matches_identical": m16 == sc_,
                                             "index_agreement": agree16_idx, "dZ_sig_max": dz16,
                                             "unexplained_disagreements": len(bad16)},
@@ -234,6 +242,10 @@ def main():
         "thresholded_matches_identical_frac": agg("matches_identical"),
         "thresholded_matches_identical_coords_frac": agg("matches_identical_coords"),
         "match_distance_max_abs_diff_fp32": float(max(r["match_distance_max_abs_diff_fp32"] for r in rows)),
+        # pairs whose keypoint sets agree: decode disagreements of the fp32 GPU Z that the CPU Z does not show as
+        # a near-tie (argmax runner-up or the 0.2 threshold within 2x the pair's fp32 |dZ|)
+        "unexplained_disagreements_fp32_total": int(sum(max(r["unexplained_disagreements_fp32"], 0) for r in rows)),
+        "pairs_compared_fp32": int(sum(r["unexplained_disagreements_fp32"] >= 0 for r in rows)),
         "matches_per_pair_cpu": agg("matches_cpu"),
         "matches_per_pair_min_cpu": int(min(r["matches_cpu"] for r in rows)),
         # the seeded (untrained) networks: how many keypoints repeat under the pair's pure +DISP px shift,
