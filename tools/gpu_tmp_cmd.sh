@@ -1,12 +1,17 @@
 #!/bin/bash
 # Scratch GPU command of the current experiment (rewritten per experiment).
-# SP conv workgroups capped at one per CU (RSPL_SP_LDS_PAD: unused dynamic LDS) so a BA wave fits beside a
-# conv wave on every SIMD: 0 (default) vs 8192 (conv1 only: 76 + 8 KB) vs 24576 (every conv layer).
+# C5 LDS solve: in-kernel trace (assembly, factor, back-substitution; first two steps' panel / trailing
+# update) for HEAD vs the working tree.
 set -o pipefail
 mkdir -p gpurun_out
-for r in 1 2 3; do
-  for pad in 0 8192 24576; do
-    RSPL_SP_LDS_PAD=$pad timeout -k 10 200 python3 bench.py --steps 300 --warmup 10 --no-cpu-baseline --single-precision > gpurun_out/ab.json 2> gpurun_out/ab.err || { echo "bench $pad failed"; tail -5 gpurun_out/ab.err; exit 1; }
-    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); s=d['stages_ms_per_step']; print('pad', sys.argv[2], d['value'], d['ms_per_step'], 'ba', s.get('ba:wall'), 'conv1', s.get('sp:conv1a+1b+pool'), 'conv2-4', s.get('sp:conv2a..conv4b'), 'gnn', s.get('sg:gnn x18'))" gpurun_out/ab.json $pad
-  done
+for lib in librspl_base.so librspl.so; do
+  RSPL_LIB=$lib RSPL_BA_PROF=1 timeout -k 10 120 python -u tools/bench_ba.py --iters 6 --poses 30 --points 10000 --lines 0 > /dev/null 2> gpurun_out/bprof.err || exit 1
+  LIB=$lib python3 - <<'PY'
+import os, re, numpy as np
+lines = [l for l in open("gpurun_out/bprof.err") if l.startswith("ba_prof ")]
+names = re.findall(r"([a-zA-Z]+) -?[0-9.]+", lines[0].split(":", 1)[1])
+rows = [[float(v) for v in re.findall(r"(-?[0-9.]+)", l.split(":", 1)[1])] for l in lines]
+a = np.median(np.array(rows[2:]), 0).round(1)
+print(os.environ['LIB'], "median us:", " ".join(f"{n}={v}" for n, v in zip(names, a) if v >= 0))
+PY
 done
