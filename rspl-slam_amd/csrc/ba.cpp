@@ -399,6 +399,20 @@ void accept_swap(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, bool lin) 
   S.Hll = b->Hll; S.bl = b->bl;
 }
 
+// the call's final kernel (inlier flags, final T / X / L into the staging slot) queued right behind the
+// last optimize()'s trials instead of after the host has seen that optimize() stop: it reads the control
+// after the last queued trial and does nothing unless the optimize() stopped there (then the host queues
+// top-up trials and another one).  q: the sequence the finish that will post carries.
+struct SpecFinish {
+  bool on = false;
+  ba::Lin L{};
+  int E = 0;
+  const int* gmap = nullptr;
+  uint8_t* inl = nullptr;
+  double *Th = nullptr, *Xh = nullptr, *Lh = nullptr;
+  unsigned long long q = 0;
+};
+
 // optimize(iters) with the LM control on the device (fast path, unsharded): the first errors, the
 // first linearisation and the control's initialisation, then `iters` trials queued back to back
 // with no host round trip -- each trial's last kernel takes the accept / reject decision (ba::LmCtrl)
@@ -406,7 +420,7 @@ void accept_swap(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, bool lin) 
 // optimize(); when rejected trials leave iterations undone it queues more.  At the end the host
 // pointer view follows the device's current bank.
 int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
-                 double* chi2_out, int* done_out, uint8_t* cls_level, bool build_pp) {
+                 double* chi2_out, int* done_out, uint8_t* cls_level, bool build_pp, SpecFinish* fin) {
   hipStream_t st = b->stream;
   S.lm = b->lmctl;
   S.lm_slot = 0;
@@ -488,10 +502,25 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
     return RSPL_OK;
   };
   int rc;
-  if ((rc = enqueue(iters))) return rc;
+  unsigned long long q_last = 0;
+  auto enqueue_batch = [&](int n) -> int {  // n trials (+ the speculative finish behind them)
+    int r;
+    if ((r = enqueue(n))) return r;
+    q_last = b->seq;
+    if (fin) {
+      ba::Sys Sf = S;
+      Sf.lm = b->lmctl;
+      Sf.lm_slot = queued & 1;  // the control slot the last queued trial writes
+      Sf.prof = nullptr;
+      fin->q = ++b->seq;
+      fin->on = true;
+      RSPL_HIP(ba::finish(P, fin->L, fin->E, fin->gmap, fin->inl, fin->Th, fin->Xh, fin->Lh, Sf, fin->q, st));
+    }
+    return RSPL_OK;
+  };
+  if ((rc = enqueue_batch(iters))) return rc;
   double v[4];
   for (;;) {
-    const unsigned long long q_last = b->seq;
     // wait for the stopping trial (trials queued after it post nothing) or the last queued one
     using clk = std::chrono::steady_clock;
     const auto t0 = clk::now();
@@ -503,6 +532,12 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
         for (int k = 0; k < 4; k++) v[k] = mv[k];
         __atomic_thread_fence(__ATOMIC_ACQUIRE);
         if (__atomic_load_n(&b->mail->vseq, __ATOMIC_ACQUIRE) == s1 && (s1 == q_last || v[3] != 0.0)) break;
+      } else if (fin && s1 == fin->q) {  // the speculative finish already posted over the stopping trial's
+        volatile const double* mv = b->mail->v;  // seq (it posts only the seq: v / vseq stay the trial's)
+        for (int k = 0; k < 4; k++) v[k] = mv[k];
+        __atomic_thread_fence(__ATOMIC_ACQUIRE);
+        const unsigned long long vs = __atomic_load_n(&b->mail->vseq, __ATOMIC_ACQUIRE);
+        if (vs >= q_first && vs <= q_last && v[3] != 0.0) break;
       }
       if ((spin & 4095) == 0) {
         const hipError_t e = hipStreamQuery(st);
@@ -529,7 +564,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
       break;
     }
     // rejected trials left iterations to do: queue one trial per remaining iteration
-    if ((rc = enqueue(std::max(1, iters - (int)v[1])))) return rc;
+    if ((rc = enqueue_batch(std::max(1, iters - (int)v[1])))) return rc;
   }
   S.lm = nullptr;
   if (v[2] != 0.0) accept_swap(b, P, Lr, S, true);  // the device's current bank is the host's spare one
@@ -546,12 +581,13 @@ bool dev_lm(const rspl_ba* b, const ba::Active& A, int iters) {
 // first (the second optimize's levels), build_pp -- build the Schur chunks' edge-pair lists (see
 // setup_dev); the caller does both itself otherwise
 int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
-             double* chi2_out, int* done_out, uint8_t* cls_level = nullptr, bool build_pp = false) {
+             double* chi2_out, int* done_out, uint8_t* cls_level = nullptr, bool build_pp = false,
+             SpecFinish* fin = nullptr) {
   hipStream_t st = b->stream;
   double v[4];
   int rc;
   const bool sh = b->allreduce != nullptr;
-  if (dev_lm(b, A, iters)) return optimize_dev(b, P, Lr, S, A, iters, chi2_out, done_out, cls_level, build_pp);
+  if (dev_lm(b, A, iters)) return optimize_dev(b, P, Lr, S, A, iters, chi2_out, done_out, cls_level, build_pp, fin);
   const int n6 = 6 * A.K;
   double* so = b->red + n6 + b->nranks;  // this rank's {chi2, scale, fail} (S.shard_out)
   unsigned long long q = ++b->seq;
@@ -1167,6 +1203,11 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
                      pp_fused)))
     return rc;
   tm.mark("opt1");
+  uint8_t* inl_h = reinterpret_cast<uint8_t*>(b->stage_dev[c.slot] + dl.inl);
+  double* T_h = reinterpret_cast<double*>(b->stage_dev[c.slot] + dl.T);
+  double* X_h = reinterpret_cast<double*>(b->stage_dev[c.slot] + dl.X);
+  double* L_h = reinterpret_cast<double*>(b->stage_dev[c.slot] + dl.L);
+  SpecFinish fin;
   // ---- phase 2: level-0 edges, no kernel (initializeOptimization(0), :176-213) ----
   // Same active structure with the level-1 edges masked (exact-zero records, no cost, errors
   // kept as g2o keeps them), landmark activity recomputed from the levels on the device (device LM:
@@ -1180,19 +1221,29 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
       RSPL_HIP(ba::classify(P, Lr, E, level, nullptr, 0, st));
       RSPL_HIP(ba::landmark_active(A, level, b->lm_act2, st));
     }
+    // the final kernel queued behind optimize(5)'s trials (device LM, unsharded): no host round trip
+    // between that optimize()'s stop and the final kernel
+    const bool spec_fin = fused && !sh && !b->ktime_on;  // (kernel timing maps events to contiguous trial seqs)
+    if (spec_fin) {
+      fin.L = Lr;
+      fin.E = E;
+      fin.gmap = reinterpret_cast<const int*>(cb + cl.gmap);
+      fin.inl = inl_h;
+      fin.Th = T_h;
+      fin.Xh = X_h;
+      fin.Lh = L_h;
+    }
     if ((rc = optimize(b, P, Lr, S, A, pr->iterations_second, &res->chi2_second, &res->iterations_done_second,
-                       fused ? level : nullptr)))
+                       fused ? level : nullptr, false, spec_fin ? &fin : nullptr)))
       return rc;
     tm.mark("opt2");
   }
   // ---- inlier flags + final state written by the GPU into the mapped staging buffer ----
   // (the staging call region was consumed by the upload long before: the stream is in order)
-  const unsigned long long q = ++b->seq;
-  uint8_t* inl_h = reinterpret_cast<uint8_t*>(b->stage_dev[c.slot] + dl.inl);
-  double* T_h = reinterpret_cast<double*>(b->stage_dev[c.slot] + dl.T);
-  double* X_h = reinterpret_cast<double*>(b->stage_dev[c.slot] + dl.X);
-  double* L_h = reinterpret_cast<double*>(b->stage_dev[c.slot] + dl.L);
-  if (sh) {  // owned landmarks + local edge flags gathered by one more all-reduce: complete on every rank
+  const unsigned long long q = fin.on ? fin.q : ++b->seq;
+  if (fin.on) {
+    // already queued (SpecFinish)
+  } else if (sh) {  // owned landmarks + local edge flags gathered by one more all-reduce: complete on every rank
     const size_t glen = 3 * (size_t)nq + 6 * (size_t)nl + Eg;
     if (glen > b->gcap) {
       RSPL_HIP(hipStreamSynchronize(st));

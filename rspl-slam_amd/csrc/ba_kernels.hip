@@ -2792,6 +2792,12 @@ __global__ __launch_bounds__(256) void classify_kernel(Problem P, Lin L, int E, 
 __global__ __launch_bounds__(256) void finish_kernel(Problem P, Lin L, int E, const int* gmap, uint8_t* inl, double* Th,
                                                      double* Xh, double* Lh, Sys S, unsigned long long seq) {
   __shared__ int last;
+  if (S.lm) {  // queued behind the last optimize()'s trials (S.lm_slot: the control after the last one):
+               // a no-op unless that optimize() has stopped; the current bank from its control
+    const LmCtrl* c = S.lm + S.lm_slot;
+    if (!c->stop) return;
+    if (c->cur) bank_state(P);
+  }
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < E) inl[gmap[i]] = edge_inlier(P, L, i) ? 1 : 0;
   if (i < 8 * P.np) Th[i] = P.T[i];
