@@ -449,6 +449,11 @@ def main():
     bf = pkg.synthetic.EUROC_BF
     cam_limits = (bf / 10.0, bf / 0.1, 2.0)  # MinXDiff, MaxXDiff, MaxYDiff (camera.cc:21-22, euroc.yaml)
 
+    trace_path = os.environ.get("RSPL_BENCH_TRACE")  # diagnostics: per-step / per-BA-call host timeline
+    trace_on = bool(trace_path)
+    trace_out = []
+    step_tr = []
+
     def measure(precision):
         """One full timed run of the pipeline at `precision`; returns its measurements."""
         sp, sg = handles[precision]
@@ -514,6 +519,8 @@ def main():
             return [problems[i % len(problems)]]
 
         def step(i):
+            if trace_on:  # host timeline of the step (RSPL_BENCH_TRACE): its start, then named marks
+                step_tr.append({"i": i, "t": time.perf_counter()})
             slot, pslot = i % 3, (i - 1) % 3
             cur, prev, ccur, cprev = feats[slot], feats[pslot], counts[slot], counts[pslot]
             skip = args.skip.split(",")
@@ -545,6 +552,8 @@ def main():
             ev_sp[slot].record(st_sp.handle)
             host_wait["sp_calls"] += time.perf_counter() - tw
             tw = time.perf_counter()
+            if trace_on:
+                step_tr[-1]["sp"] = tw
             ev_sp[slot].wait_on(st_sg.handle)
             # PointMatching pairs: (L_t, L_kf) and (L_t, R_t)
             capi.memcpy_d2d(f0.ptr, cur.ptr, FB, st_sg.handle)
@@ -558,6 +567,8 @@ def main():
             sg.infer_device(2, f0.ptr, n0.ptr, f1.ptr, n1.ptr, K, True, outs[0].ptr, outs[1].ptr, outs[2].ptr,
                             outs[3].ptr, st_sg.handle, post_stream=st_post.handle)
             host_wait["sg_calls"] += time.perf_counter() - tw
+            if trace_on:
+                step_tr[-1]["sg"] = time.perf_counter()
             # stereo line association of frame t: the joined line threads' lines, SP's device records of
             # (left, right) and SG's match index of pair 1 (left(t) -> right(t)), stream-ordered behind the
             # decode
@@ -568,6 +579,8 @@ def main():
                 nl0, t0ms = jobs[0].wait_device(dl0.ptr, 512, st_post.handle)
                 nl1, t1ms = jobs[1].wait_device(dl1.ptr, 512, st_post.handle)
                 host_wait["lines"] += time.perf_counter() - tw
+                if trace_on:
+                    step_tr[-1]["lines"] = time.perf_counter()
                 if line_t0 is not None:
                     line_stats["detect_ms"].append(max(t0ms, t1ms))
                     line_stats["lines"].append(nl0 + nl1)
@@ -586,8 +599,12 @@ def main():
             # _tracking_data_buffer.size() >= 2 (src/map_builder.cc:176)
             if "ba" not in skip:
                 tw = time.perf_counter()
+                if trace_on:
+                    step_tr[-1]["ba_put0"] = tw
                 ba_put(ba_item(i))
                 host_wait["ba_queue"] += time.perf_counter() - tw
+                if trace_on:
+                    step_tr[-1]["ba_put1"] = time.perf_counter()
 
         host_wait = {"lines": 0.0, "ba_queue": 0.0, "sp_calls": 0.0, "sg_calls": 0.0, "line_assoc_calls": 0.0,
                      "line_submit": 0.0}
@@ -612,12 +629,25 @@ def main():
             host_wait[k] = 0.0
         ba.kernel_timing(ktime_every)
         ba.kernel_times()  # reset
+        ba.trace()  # reset (warmup calls)
+        step_tr.clear()
         t0 = time.perf_counter()
         for i in range(args.steps):
             step(args.warmup + i)
+        t_fed = time.perf_counter()
         ba_drain()
+        t_drained = time.perf_counter()
         capi.synchronize()
-        elapsed = job_time(time.perf_counter() - t0, dist)
+        t_end = time.perf_counter()
+        elapsed = job_time(t_end - t0, dist)
+        if trace_on:  # the timed region's host timeline, relative to its start (ms)
+            rel = lambda t: round((t - t0) * 1e3, 4)  # noqa: E731
+            trace_out.append({"precision": precision, "steps": args.steps, "warmup": args.warmup,
+                              "elapsed_ms": rel(t_end), "fed_ms": rel(t_fed), "drained_ms": rel(t_drained),
+                              "step": [{k: (v if k == "i" else rel(v)) for k, v in r.items()} for r in step_tr],
+                              "ba": [{k: (rel(v) if k in ("submit", "stage0", "stage1", "run0", "upload", "opt1",
+                                                          "opt2", "end") else v) for k, v in r.items()}
+                                     for r in ba.trace()]})
         if not native:
             ba_q.put(None)
             worker.join()
@@ -649,6 +679,8 @@ def main():
 
     res = measure(args.precision)
     other = measure(precs[1]) if len(precs) > 1 else None  # the other precision, same run, for the record
+    if trace_on:
+        pathlib.Path(trace_path).write_text(json.dumps(trace_out))
     value, elapsed, ba_ms = res["value"], res["elapsed"], res["ba_ms"]
     sp_ms, sp_calls = res["sp"]
     sg_ms, sg_calls = res["sg"]

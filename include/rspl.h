@@ -328,6 +328,16 @@ int rspl_ba_use_reserved_cus(rspl_ba* ba, int reserve_cus);
  * launches[1]: update + cost + speculative linearisation -- over the trials that did work. */
 int rspl_ba_kernel_timing(rspl_ba* ba, int every);
 int rspl_ba_kernel_times(rspl_ba* ba, double* ms, long long* launches);
+/* Per-call host timeline (measurement): the handle keeps the host timestamps of its last 4096 calls
+ * (CLOCK_MONOTONIC seconds -- the clock of Python's time.perf_counter / time.monotonic on Linux).
+ * Record of RSPL_BA_TRACE_W doubles: [0] submitted (rspl_ba_submit; rspl_ba_local: entry), [1] staging
+ * started, [2] staging done, [3] device part started (tracking thread), [4] upload queued, [5] optimize(10)
+ * stopped (mailbox read), [6] optimize(5) stopped, [7] call done (results written back), [8] staging slot,
+ * [9] resize flags (1 staging slot, 2 edge-pair list, 4 pose-diagonal partials, 8 timing events: a buffer
+ * grown inside the call), [10] LM iterations, [11] 1 for rspl_ba_local, 0 for a submitted call.
+ * rspl_ba_trace copies the oldest min(cap, recorded) records and clears the ring; *n = records copied. */
+#define RSPL_BA_TRACE_W 12
+int rspl_ba_trace(rspl_ba* ba, double* out, int cap, int* n);
 /* Test hook (host only, no device): the host staging of rspl_ba_local -- the edges of rank `rank` of
  * `nranks` (1: all) in landmark-CSR order -- with the host workers from par_edges edges (0: serial).
  * n_local = {local edges E, local point edges Ep}; lm_off [n_points + n_lines + 1]; per CSR position

@@ -303,6 +303,16 @@ class LocalBA:
         capi.check(self._lib.rspl_ba_kernel_times(self._h, ms, n), "rspl_ba_kernel_times")
         return {"chunks+solve": (ms[0], n[0]), "update": (ms[1], n[1])}
 
+    def trace(self, cap=4096):
+        """The host timeline of the calls since the last read (rspl_ba_trace): a list of dicts with
+        capi.BA_TRACE_FIELDS (times in time.perf_counter seconds); [] with a library that lacks it."""
+        if not hasattr(self._lib, "rspl_ba_trace"):
+            return []
+        buf, n = (C.c_double * (cap * capi.BA_TRACE_W))(), C.c_int()
+        capi.check(self._lib.rspl_ba_trace(self._h, buf, cap, C.byref(n)), "rspl_ba_trace")
+        a = np.frombuffer(buf, np.float64, n.value * capi.BA_TRACE_W).reshape(n.value, capi.BA_TRACE_W)
+        return [dict(zip(capi.BA_TRACE_FIELDS, map(float, row))) for row in a]
+
     def use_reserved_cus(self, reserve_cus: int):
         """Confine this handle's kernels to the CUs reserving streams leave free (0 = all CUs)."""
         capi.check(self._lib.rspl_ba_use_reserved_cus(self._h, reserve_cus), "rspl_ba_use_reserved_cus")

@@ -18,6 +18,10 @@ RSPL_ABI_VERSION = 2  # include/rspl.h: the struct layouts the ctypes mirrors be
 RSPL_PREC_FP32 = 0
 RSPL_PREC_FP16 = 1
 
+BA_TRACE_W = 12  # RSPL_BA_TRACE_W
+BA_TRACE_FIELDS = ("submit", "stage0", "stage1", "run0", "upload", "opt1", "opt2", "end", "slot", "grew", "iters",
+                   "sync")
+
 EXPORTS = [
     "rspl_last_error", "rspl_version", "rspl_abi_version",
     "rspl_device_count", "rspl_set_device", "rspl_malloc", "rspl_free", "rspl_memcpy_h2d", "rspl_memcpy_d2h",
@@ -32,7 +36,7 @@ EXPORTS = [
     "rspl_sg_stage_times", "rspl_sg_destroy",
     "rspl_pm_match",
     "rspl_ba_create", "rspl_ba_local", "rspl_ba_submit", "rspl_ba_join", "rspl_ba_destroy", "rspl_ba_use_reserved_cus", "rspl_ba_kernel_timing",
-    "rspl_ba_kernel_times", "rspl_ba_debug_stage",
+    "rspl_ba_kernel_times", "rspl_ba_trace", "rspl_ba_debug_stage",
     "rspl_frame_create", "rspl_frame_optimize", "rspl_frame_destroy",
     "rspl_ba_set_shard", "rspl_comm_unique_id", "rspl_comm_create", "rspl_comm_allreduce_sum", "rspl_comm_destroy",
     "rspl_ba_set_comm", "rspl_group_create", "rspl_group_destroy", "rspl_ba_set_group",
@@ -160,6 +164,8 @@ def load(path: pathlib.Path = LIB_PATH):
         lib.rspl_ba_destroy.argtypes = [vp]
         lib.rspl_ba_destroy.restype = None
         lib.rspl_ba_debug_stage.argtypes = [vp, ip, ip, ip] + [vp] * 9
+    if hasattr(lib, "rspl_ba_trace"):  # (absent from older builds used as A/B baselines)
+        lib.rspl_ba_trace.argtypes = [vp, C.POINTER(C.c_double), ip, C.POINTER(ip)]
     if hasattr(lib, "rspl_ba_set_shard"):
         lib.rspl_ba_set_shard.argtypes = [vp, ip, ip, vp, vp]
         lib.rspl_comm_unique_id.argtypes = [vp]

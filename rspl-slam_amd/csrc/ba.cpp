@@ -119,6 +119,11 @@ struct rspl_ba {
   std::string q_msg;
   long long q_done = 0, q_iters = 0;
   double q_ms = 0.0;
+  // per-call host timeline (rspl_ba_trace): a ring of the last kTraceCap calls, under qmu
+  static constexpr int kTraceCap = 4096;
+  std::vector<double> trace;  // kTraceCap x RSPL_BA_TRACE_W
+  long long trace_n = 0;      // records written since the last read
+  unsigned grew = 0;          // device-side buffers grown during the running call (tracking thread)
 };
 
 namespace {
@@ -127,6 +132,7 @@ constexpr int kMaxCams = 16;
 constexpr int kMaxRanks = 64;
 constexpr int kParEdges = 8192;  // staging on the host workers from this many edges
 constexpr int kChunkWaves = 1024; // Schur chunk waves of one dispatch round (one wave per SIMD)
+constexpr int kEventTrials = 64;  // timing-event triples created by rspl_ba_kernel_timing
 // the rank's sum all-reduce, stream-ordered on the BA stream
 int allreduce(rspl_ba* b, double* d, size_t n) {
   const int rc = b->allreduce(b->ar_ctx, d, n, b->stream);
@@ -201,6 +207,13 @@ struct HostMarks {
   }
 };
 
+// CLOCK_MONOTONIC seconds (Python's time.perf_counter clock): the per-call timeline's time base
+double mono_s() {
+  timespec ts;
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
 }  // namespace
 
 // one call's host staging: its slot and what the device part needs of it
@@ -213,6 +226,7 @@ struct rspl::ba::StagedCall {
   CallLayout cl;
   DownLayout dl;
   HostMarks tm;
+  double tr[RSPL_BA_TRACE_W] = {};  // its host timeline record (rspl_ba_trace)
 };
 
 namespace {
@@ -247,17 +261,25 @@ void carve(F& ar, rspl_ba* b) {
   take(b->pp_cnt, npairs * nchk); take(b->pp_off, npairs * nchk + 1);
 }
 
-int ensure_stage(rspl_ba* b, int slot, size_t bytes) {
+// Staging slots are allocated at create for the handle's capacities (stage_bytes), so in use this never
+// grows; it stays for a handle created without them.  The slot being grown is not in use (a slot is
+// handed out only when its previous call has finished), so the new buffer is taken before the old one
+// is released and nothing waits for the stream.
+int ensure_stage(rspl_ba* b, int slot, size_t bytes, bool* grew = nullptr) {
   if (bytes <= b->stage_cap[slot]) return RSPL_OK;
-  // copies from the old buffer may still be in flight
-  RSPL_HIP(hipStreamSynchronize(b->stream));
-  if (b->stage[slot]) (void)hipHostFree(b->stage[slot]);
-  b->stage[slot] = nullptr;
   const size_t cap = std::max(bytes, b->stage_cap[slot] * 2);
-  b->stage_cap[slot] = 0;
-  RSPL_HIP(hipHostMalloc((void**)&b->stage[slot], cap, hipHostMallocMapped | hipHostMallocCoherent));
-  RSPL_HIP(hipHostGetDevicePointer((void**)&b->stage_dev[slot], b->stage[slot], 0));
+  char *nh = nullptr, *nd = nullptr;
+  RSPL_HIP(hipHostMalloc((void**)&nh, cap, hipHostMallocMapped | hipHostMallocCoherent));
+  if (hipHostGetDevicePointer((void**)&nd, nh, 0) != hipSuccess) {
+    (void)hipHostFree(nh);
+    set_error("BA staging slot: no device mapping");
+    return RSPL_E_DEVICE;
+  }
+  if (b->stage[slot]) (void)hipHostFree(b->stage[slot]);
+  b->stage[slot] = nh;
+  b->stage_dev[slot] = nd;
   b->stage_cap[slot] = cap;
+  if (grew) *grew = true;
   return RSPL_OK;
 }
 
@@ -444,6 +466,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
       const size_t cap = std::max(need, (size_t)1 << 14);
       RSPL_HIP(hipMalloc((void**)&b->pdg, sizeof(double) * cap));
       b->pdg_cap = cap;
+      b->grew |= 4;
     }
     RSPL_HIP(ba::setup_dev(P, Lr, A, S, cls_level, cls_level ? const_cast<uint8_t*>(A.lm_act) : nullptr, iters,
                            build_pp ? b->pp_cnt : nullptr, b->pp_off, b->pp_buf, b->pdg, st));
@@ -483,12 +506,13 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
       S.lm_post = k == n - 1;
       hipEvent_t* ev = nullptr;
       if (b->ktime_on) {
-        if ((size_t)3 * (b->kev_used + 1) > b->kev.size()) {
+        if ((size_t)3 * (b->kev_used + 1) > b->kev.size()) {  // (pre-created by rspl_ba_kernel_timing)
           for (int i = 0; i < 3; i++) {
             hipEvent_t e;
             RSPL_HIP(hipEventCreate(&e));
             b->kev.push_back(e);
           }
+          b->grew |= 8;
         }
         ev = &b->kev[3 * (size_t)b->kev_used++];
       }
@@ -722,6 +746,32 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
     return RSPL_E_DEVICE;
   }
   memset(b->mail, 0, sizeof(ba::Mail));
+  // everything a call can need, allocated once here for the handle's capacities (never inside a call:
+  // a pinned allocation or a hipFree there stalls the device and the pipeline beside it): both staging
+  // slots, the pose-diagonal partials of the first pass and the edge-pair lists (sum over landmarks of
+  // k^2 edge pairs, k = edges of the landmark; sized for 8 edges per landmark on average -- beyond that
+  // the list still grows on demand, flagged in the call's trace record)
+  {
+    const size_t sb = std::max(CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE,
+                                          8 * (size_t)b->maxE).bytes,
+                               DownLayout(b->maxK, cfg->max_points, cfg->max_lines, b->maxE).bytes);
+    ba::Active Amax{};  // the largest call: every landmark, the most line workgroups
+    Amax.nL = b->maxL;
+    Amax.K = b->maxK;
+    Amax.n_lblk = cfg->max_lines + b->maxE / ba::kLineBlk + 2;
+    const size_t pdg = (size_t)ba::setup_pdg_len(Amax);
+    const size_t pp = std::max<size_t>((size_t)1 << 16, 8 * (size_t)b->maxE);
+    if (ensure_stage(b, 0, sb) || ensure_stage(b, 1, sb) ||
+        hipMalloc((void**)&b->pdg, sizeof(double) * pdg) != hipSuccess ||
+        hipMalloc((void**)&b->pp_buf, sizeof(int4) * pp) != hipSuccess) {
+      set_error("BA staging / scratch allocation failed");
+      rspl_ba_destroy(b);
+      return RSPL_E_DEVICE;
+    }
+    b->pdg_cap = pdg;
+    b->pp_cap = pp;
+  }
+  b->trace.assign((size_t)rspl_ba::kTraceCap * RSPL_BA_TRACE_W, 0.0);
   if (getenv("RSPL_BA_PROF") &&
       (hipMalloc((void**)&b->prof, sizeof(unsigned long long) * ba::kProfLen) != hipSuccess ||
        hipMemset(b->prof, 0, sizeof(unsigned long long) * ba::kProfLen) != hipSuccess)) {
@@ -752,8 +802,13 @@ extern "C" int rspl_ba_use_reserved_cus(rspl_ba* b, int reserve_cus) {
   return RSPL_OK;
 }
 
+namespace {
+bool queue_active(rspl_ba* b);
+}
+
 extern "C" int rspl_ba_set_shard(rspl_ba* b, int rank, int nranks, rspl_allreduce_fn fn, void* ctx) {
   RSPL_CHECK_ARG(b, "rspl_ba_set_shard: NULL handle");
+  RSPL_CHECK_ARG(!queue_active(b), "rspl_ba_set_shard: calls are queued on the tracking thread (rspl_ba_join first)");
   RSPL_CHECK_ARG(nranks >= 1 && nranks <= kMaxRanks && rank >= 0 && rank < nranks, "rank %d of %d (1..%d ranks)", rank,
                  nranks, kMaxRanks);
   RSPL_CHECK_ARG(nranks == 1 || fn, "an all-reduce function is required for nranks > 1");
@@ -795,7 +850,14 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
 namespace {
 int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res);
 int stage_call(rspl_ba* b, int slot, const rspl_ba_problem* pr, rspl_ba_result* res, ba::StagedCall& c);
-int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rspl_ba_result* res);
+int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rspl_ba_result* res, double* tr);
+void push_trace(rspl_ba* b, const double* tr);
+
+// calls queued on / running in the native tracking thread (rspl_ba_submit) and not yet joined
+bool queue_active(rspl_ba* b) {
+  std::lock_guard<std::mutex> lk(b->qmu);
+  return !b->jobs.empty() || b->busy;
+}
 
 void begin_call(rspl_ba* b) {
   b->ktime_on = b->ktime_every > 0 && b->ncalls++ % (unsigned long long)b->ktime_every == 0;
@@ -824,8 +886,32 @@ int end_call(rspl_ba* b, int rc) {
 
 extern "C" int rspl_ba_kernel_timing(rspl_ba* b, int every) {
   RSPL_CHECK_ARG(b && every >= 0, "rspl_ba_kernel_timing: NULL handle or every < 0");
+  RSPL_CHECK_ARG(!queue_active(b), "rspl_ba_kernel_timing: calls are queued on the tracking thread (rspl_ba_join first)");
+  // the events of a call's trials, created here rather than inside a timed call (a call queues 15 trials
+  // plus top-ups after rejected ones; more are created on demand, flagged in the trace record)
+  for (size_t n = b->kev.size(); every > 0 && n < 3 * (size_t)kEventTrials; n++) {
+    hipEvent_t e;
+    RSPL_HIP(hipEventCreate(&e));
+    b->kev.push_back(e);
+  }
   b->ktime_every = every;
   b->ncalls = 0;
+  return RSPL_OK;
+}
+
+extern "C" int rspl_ba_trace(rspl_ba* b, double* out, int cap, int* n) {
+  RSPL_CHECK_ARG(b && n && cap >= 0 && (out || cap == 0), "rspl_ba_trace: NULL argument or cap < 0");
+  std::lock_guard<std::mutex> lk(b->qmu);
+  const long long have = std::min<long long>(b->trace_n, rspl_ba::kTraceCap);
+  const long long first = b->trace_n - have;  // oldest record still in the ring
+  const int m = (int)std::min<long long>(have, cap);
+  for (int i = 0; i < m; i++) {
+    const size_t r = (size_t)((first + i) % rspl_ba::kTraceCap);
+    std::copy(b->trace.begin() + r * RSPL_BA_TRACE_W, b->trace.begin() + (r + 1) * RSPL_BA_TRACE_W,
+              out + (size_t)i * RSPL_BA_TRACE_W);
+  }
+  *n = m;
+  b->trace_n = 0;
   return RSPL_OK;
 }
 
@@ -842,6 +928,8 @@ extern "C" int rspl_ba_kernel_times(rspl_ba* b, double* ms, long long* launches)
 
 extern "C" int rspl_ba_local(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   if (!b) return ba_local_impl(b, pr, res);
+  // the synchronous call stages into slot 0 and runs on the BA stream: never beside queued calls
+  RSPL_CHECK_ARG(!queue_active(b), "rspl_ba_local: calls are queued on the tracking thread (rspl_ba_join first)");
   begin_call(b);
   return end_call(b, ba_local_impl(b, pr, res));
 }
@@ -879,7 +967,10 @@ void staging_loop(rspl_ba* b) {
     rspl_ba_result* res = j->res;
     lk.unlock();
     sc->slot = slot;
+    sc->tr[1] = mono_s();
     sc->rc = stage_call(b, slot, pr, res, *sc);
+    sc->tr[2] = mono_s();
+    sc->tr[8] = slot;
     if (sc->rc) sc->msg = rspl_last_error();
     lk.lock();
     j->state = 2;
@@ -899,13 +990,14 @@ void tracking_loop(rspl_ba* b) {
     lk.unlock();
     b->qcv.notify_all();  // room for a submitter
     const auto t0 = std::chrono::steady_clock::now();
+    j.sc->tr[3] = mono_s();
     int rc;
     if (j.sc->rc) {
       set_error("%s", j.sc->msg.c_str());
       rc = j.sc->rc;
     } else {
       begin_call(b);
-      rc = end_call(b, run_call(b, *j.sc, j.pr, j.res));
+      rc = end_call(b, run_call(b, *j.sc, j.pr, j.res, j.sc->tr));
     }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     const std::string msg = rc ? std::string(rspl_last_error()) : std::string();
@@ -914,6 +1006,7 @@ void tracking_loop(rspl_ba* b) {
     b->busy = false;
     b->q_done++;
     b->q_ms += ms;
+    if (!rc) push_trace(b, j.sc->tr);
     if (!rc) b->q_iters += j.res->iterations_done_first + j.res->iterations_done_second;
     if (rc && !b->q_err) {
       b->q_err = rc;
@@ -931,8 +1024,10 @@ extern "C" int rspl_ba_submit(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_res
     b->worker = std::thread(tracking_loop, b);
     b->stager = std::thread(staging_loop, b);
   }
+  const double t_sub = mono_s();
   b->qcv.wait(lk, [&] { return b->jobs.size() < kTrackingBuffer; });
   b->jobs.push_back({pr, res, std::make_shared<ba::StagedCall>(), 0});
+  b->jobs.back().sc->tr[0] = t_sub;
   lk.unlock();
   b->qcv.notify_all();
   return RSPL_OK;
@@ -1005,7 +1100,9 @@ int stage_call(rspl_ba* b, int slot, const rspl_ba_problem* pr, rspl_ba_result* 
   tm.mark("count");
   const CallLayout cl(pr->n_cameras, np, nq, nl, E, 4 * (size_t)Ep + 8 * (size_t)(E - Ep));
   const DownLayout dl(np, nq, nl, Eg);  // inlier flags by global edge id
-  if ((rc = ensure_stage(b, slot, std::max(cl.bytes, dl.bytes)))) return rc;
+  bool grew = false;
+  if ((rc = ensure_stage(b, slot, std::max(cl.bytes, dl.bytes), &grew))) return rc;
+  if (grew) c.tr[9] = (double)((unsigned)c.tr[9] | 1u);
   char* sg = b->stage[slot];
   // vertices: VertexSE3Expmap estimate = SE3Quat(q, p).inverse() (g2o_optimization.cc:42)
   double* T = reinterpret_cast<double*>(sg + cl.T);
@@ -1105,7 +1202,7 @@ int stage_call(rspl_ba* b, int slot, const rspl_ba_problem* pr, rspl_ba_result* 
 }
 
 // The device part of one staged call: upload, both optimize() calls, results
-int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rspl_ba_result* res) {
+int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rspl_ba_result* res, double* tr) {
   const int np = pr->n_poses, nq = pr->n_points, nl = pr->n_lines;
   const int ne[4] = {pr->n_mono, pr->n_stereo, pr->n_mono_line, pr->n_stereo_line};
   hipStream_t st = b->stream;
@@ -1119,6 +1216,7 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
   HostMarks tm = c.tm;
   int rc;
   tm.mark("run");
+  b->grew = 0;
   if (pair_bound > b->pp_cap) {  // grow the edge-pair lists (the stream is idle between calls)
     RSPL_HIP(hipStreamSynchronize(st));
     if (b->pp_buf) (void)hipFree(b->pp_buf);
@@ -1127,9 +1225,11 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
     const size_t cap = std::max(pair_bound, (size_t)1 << 16);
     RSPL_HIP(hipMalloc((void**)&b->pp_buf, sizeof(int4) * cap));
     b->pp_cap = cap;
+    b->grew |= 2;
   }
   RSPL_HIP(hipMemcpyAsync(b->cbuf, sg, cl.bytes, hipMemcpyHostToDevice, st));
   tm.mark("upload");
+  tr[4] = mono_s();
   char* cb = b->cbuf;
   uint8_t* level = reinterpret_cast<uint8_t*>(cb + cl.level);
   ba::Problem P{};
@@ -1203,6 +1303,7 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
                      pp_fused)))
     return rc;
   tm.mark("opt1");
+  tr[5] = mono_s();
   uint8_t* inl_h = reinterpret_cast<uint8_t*>(b->stage_dev[c.slot] + dl.inl);
   double* T_h = reinterpret_cast<double*>(b->stage_dev[c.slot] + dl.T);
   double* X_h = reinterpret_cast<double*>(b->stage_dev[c.slot] + dl.X);
@@ -1237,6 +1338,7 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
                        fused ? level : nullptr, false, spec_fin ? &fin : nullptr)))
       return rc;
     tm.mark("opt2");
+    tr[6] = mono_s();
   }
   // ---- inlier flags + final state written by the GPU into the mapped staging buffer ----
   // (the staging call region was consumed by the upload long before: the stream is in order)
@@ -1274,6 +1376,7 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
     }
   }
   if (b->prof && b->prof_nb[0]) report_prof(b);
+  tr[9] = (double)((unsigned)tr[9] | b->grew);
   if (b->lm_trace) {  // RSPL_BA_LMTRACE: the device LM decisions of both optimize() calls
     std::vector<double> h(8 * 64);
     if (hipMemcpy(h.data(), b->lm_trace, sizeof(double) * h.size(), hipMemcpyDeviceToHost) == hipSuccess)
@@ -1307,13 +1410,30 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
   }
   tm.mark("final");
   tm.print("rspl_ba_local us:");
+  tr[7] = mono_s();
+  tr[10] = res->iterations_done_first + res->iterations_done_second;
   return RSPL_OK;
 }
 
 int ba_local_impl(rspl_ba* b, const rspl_ba_problem* pr, rspl_ba_result* res) {
   RSPL_CHECK_ARG(b && pr && res, "rspl_ba_local: NULL argument");
   ba::StagedCall c;
-  const int rc = stage_call(b, 0, pr, res, c);
-  return rc ? rc : run_call(b, c, pr, res);
+  c.tr[0] = c.tr[1] = mono_s();
+  c.tr[11] = 1;
+  int rc = stage_call(b, 0, pr, res, c);
+  c.tr[2] = c.tr[3] = mono_s();
+  if (!rc) rc = run_call(b, c, pr, res, c.tr);
+  if (!rc) {
+    std::lock_guard<std::mutex> lk(b->qmu);
+    push_trace(b, c.tr);
+  }
+  return rc;
+}
+
+// append one record to the handle's timeline ring (qmu held)
+void push_trace(rspl_ba* b, const double* tr) {
+  if (b->trace.empty()) return;
+  const size_t i = (size_t)(b->trace_n++ % rspl_ba::kTraceCap);
+  std::copy(tr, tr + RSPL_BA_TRACE_W, b->trace.begin() + i * RSPL_BA_TRACE_W);
 }
 }  // namespace

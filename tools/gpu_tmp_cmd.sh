@@ -1,17 +1,26 @@
 #!/bin/bash
 # Scratch GPU command of the current experiment (rewritten per experiment).
-# The call's final kernel queued behind optimize(5)'s trials (gated on the LM control's stop flag): BA GPU
-# tests, standalone BA, then alternating headline benches HEAD vs the working tree.
+# Round 5, item 1: the driver's exact bench command (20 steps, warmup 5) with the host timeline
+# (RSPL_BENCH_TRACE) on HEAD's library (librspl_base.so) and the working tree's (staging slots, scratch and
+# timing events allocated up front), then the 200-step runs for the steady state.
 set -o pipefail
-mkdir -p gpurun_out
-timeout -k 10 400 python3 -u -m pytest tests/test_gpu_ba.py tests/test_gpu_map.py tests/test_gpu_large.py tests/test_gpu_ba_shard.py -k "ba or map" -x -q --timeout 200 --timeout-method thread > gpurun_out/ba_tests.log 2>&1 || { echo "BA tests failed"; tail -30 gpurun_out/ba_tests.log; exit 1; }
-tail -1 gpurun_out/ba_tests.log
-for lib in librspl_base.so librspl.so; do
-  RSPL_LIB=$lib timeout -k 10 120 python -u tools/bench_ba.py --iters 30 || exit 1
-done
-for r in 1 2 3; do
-  for lib in librspl_base.so librspl.so; do
-    RSPL_LIB=$lib timeout -k 10 200 python3 bench.py --steps 300 --warmup 10 --no-cpu-baseline --single-precision > gpurun_out/ab.json 2> gpurun_out/ab.err || { echo "bench $lib failed"; tail -5 gpurun_out/ab.err; exit 1; }
-    python3 -c "import json,sys; d=json.load(open(sys.argv[1])); s=d['stages_ms_per_step']; print(sys.argv[2], d['value'], d['ms_per_step'], 'ba', s.get('ba:wall'))" gpurun_out/ab.json $lib
-  done
-done
+mkdir -p gpurun_out/r05
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_ba.py -x -q --timeout 120 --timeout-method thread > gpurun_out/r05/ba_tests.log 2>&1 || { echo "BA tests failed"; tail -30 gpurun_out/r05/ba_tests.log; exit 1; }
+tail -1 gpurun_out/r05/ba_tests.log
+echo "cpu.max: $(cat /sys/fs/cgroup/cpu.max 2>/dev/null)  nproc: $(nproc)  $(grep Cpus_allowed_list /proc/self/status)"
+run() {  # tag lib args...
+  local tag=$1 lib=$2; shift 2
+  RSPL_LIB=$lib RSPL_BENCH_TRACE=gpurun_out/r05/trace_$tag.json timeout -k 10 240 python3 bench.py "$@" \
+    > gpurun_out/r05/$tag.json 2> gpurun_out/r05/$tag.err || { echo "bench $tag failed"; tail -20 gpurun_out/r05/$tag.err; exit 1; }
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['stages_ms_per_step']
+print(sys.argv[2], d['value'], d['ms_per_step'], 'ba', s.get('ba:wall'), 'queue', d['host_ms_per_step'].get('ba_queue'))" gpurun_out/r05/$tag.json $tag
+}
+run new20a librspl.so --gpus 1 --steps 20 --warmup 5
+run base20a librspl_base.so --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
+run new20b librspl.so --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
+run base20b librspl_base.so --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
+run new200 librspl.so --steps 200 --warmup 10 --no-cpu-baseline --single-precision
+run base200 librspl_base.so --steps 200 --warmup 10 --no-cpu-baseline --single-precision
+timeout -k 10 200 python3 -u tools/ba_parity_cases.py > gpurun_out/r05/parity_new.jsonl 2>&1 || { echo "parity failed"; tail gpurun_out/r05/parity_new.jsonl; exit 1; }
+RSPL_LIB=librspl_base.so timeout -k 10 200 python3 -u tools/ba_parity_cases.py > gpurun_out/r05/parity_base.jsonl 2>&1 || { echo "parity base failed"; exit 1; }
+echo parity done
