@@ -336,6 +336,11 @@ int rspl_ba_kernel_times(rspl_ba* ba, double* ms, long long* launches);
  * [9] resize flags (1 staging slot, 2 edge-pair list, 4 pose-diagonal partials, 8 timing events: a buffer
  * grown inside the call), [10] LM iterations, [11] 1 for rspl_ba_local, 0 for a submitted call.
  * rspl_ba_trace copies the oldest min(cap, recorded) records and clears the ring; *n = records copied. */
+/* Line edges' Jacobians (EdgeSE3ProjectLine / EdgeStereoSE3ProjectLine do not override linearizeOplus, so
+ * g2o differentiates them numerically: central difference, delta 1e-9).  0 (default): that central
+ * difference; 1: its analytic delta -> 0 limit (truncation ~1e-18 relative; the central difference's own
+ * cancellation noise, ~1e-7 relative, is absent -- results become smooth in the inputs). */
+int rspl_ba_set_line_jacobian(rspl_ba* ba, int analytic);
 #define RSPL_BA_TRACE_W 12
 int rspl_ba_trace(rspl_ba* ba, double* out, int cap, int* n);
 /* Test hook (host only, no device): the host staging of rspl_ba_local -- the edges of rank `rank` of

@@ -324,6 +324,104 @@ static int depth_positive(const ba_t* b, int t, int e) {
   return Xc[2] > 0.0;
 }
 
+/* Line-edge Jacobians, analytic: the delta -> 0 limit of g2o's central difference below (its O(delta^2)
+ * truncation is ~1e-18 relative at delta 1e-9; the quotient's cancellation noise, ~1e-7 relative, is what
+ * this removes).  Restated from the same definitions:
+ *  - pose: VertexSE3Expmap::oplusImpl T' = exp(u) T, u = [omega; upsilon]; with a = R w, b = R d and
+ *    wc = a + t x b (operator*(Isometry3, Line3D)): d wc / d omega = -[wc]x, d wc / d upsilon = -[b]x; the
+ *    right camera of a stereo edge (t_x -= bf / fx after the perturbation, g2o_optimization.cc:165) adds
+ *    [b]x [c]x with c = (bf / fx, 0, 0);
+ *  - line: Line3D::oplus (line_oplus above) at v = 0, after its normalisation to |d| = 1: with u1 = w / |w|,
+ *    u2 = d / |d|, u3 = (w x d) / |w x d|, rho = |w| / |d|: d w'' / dv = [0, -2 rho u3, 2 rho u2, -(1 + rho^2) u1],
+ *    d d'' / dv = [2 u3, 0, -2 u1, 0] (the quaternion part rotates U by 2 [v]x, the angle part rotates W);
+ *  - error (edge_project_line.cc:21-42): l = [fy wc0, fx wc1, Kv . wc], e_k = (o_k . l01 + l2) / |l01|.
+ * The error is homogeneous of degree 0 in the line, so everything is evaluated at L / |d|. */
+static int g_line_jac_analytic = 0;
+void orc_ba_set_line_jacobian(int analytic) { g_line_jac_analytic = analytic != 0; }
+
+static void skew(const double* v, double* S) { /* S x = v x x */
+  S[0] = 0; S[1] = -v[2]; S[2] = v[1];
+  S[3] = v[2]; S[4] = 0; S[5] = -v[0];
+  S[6] = -v[1]; S[7] = v[0]; S[8] = 0;
+}
+
+static void line_jac_analytic(const double* cam, const se3* T, const double* L, const double* obs, int stereo,
+                              double* Jp, double* Jl) {
+  const double fx = cam[0], fy = cam[1], cx = cam[2], cy = cam[3], bf = cam[4];
+  const double M[9] = {fy, 0, 0, 0, fx, 0, -fy * cx, -fx * cy, fx * fy};
+  const double dn = n3(L + 3), wn = n3(L);
+  double w[3], d[3], u1[3], u3[3], wxd[3];
+  for (int i = 0; i < 3; i++) {
+    w[i] = L[i] / dn;
+    d[i] = L[3 + i] / dn;
+    u1[i] = L[i] / wn;
+  }
+  cross3(L, L + 3, wxd);
+  const double cn = n3(wxd);
+  for (int i = 0; i < 3; i++) u3[i] = wxd[i] / cn;
+  const double rho = wn / dn;
+  /* d w / dv_k, d d / dv_k (columns k = 0..3) */
+  double dw[4][3], dd[4][3];
+  for (int i = 0; i < 3; i++) {
+    dw[0][i] = 0;                dd[0][i] = 2 * u3[i];
+    dw[1][i] = -2 * rho * u3[i]; dd[1][i] = 0;
+    dw[2][i] = 2 * rho * d[i];   dd[2][i] = -2 * u1[i];
+    dw[3][i] = -(1 + rho * rho) * u1[i]; dd[3][i] = 0;
+  }
+  double R[9], a[3], bb[3];
+  q_to_R(T->q, R);
+  mat3_vec(R, w, a);
+  mat3_vec(R, d, bb);
+  double Sb[9];
+  skew(bb, Sb);
+  for (int side = 0; side < (stereo ? 2 : 1); side++) {
+    double t[3] = {T->t[0], T->t[1], T->t[2]};
+    const double c[3] = {side == 1 ? bf / fx : 0.0, 0.0, 0.0};
+    t[0] -= c[0];
+    double txb[3], wc[3];
+    cross3(t, bb, txb);
+    for (int i = 0; i < 3; i++) wc[i] = a[i] + txb[i];
+    double l[3];
+    mat3_vec(M, wc, l);
+    const double n = sqrt(l[0] * l[0] + l[1] * l[1]);
+    /* d wc / d pose [3][6] */
+    double Sw[9], Sc[9], BC[9];
+    skew(wc, Sw);
+    skew(c, Sc);
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        double s = 0;
+        for (int k = 0; k < 3; k++) s += Sb[i * 3 + k] * Sc[k * 3 + j];
+        BC[i * 3 + j] = s;
+      }
+    double Gp[3][6];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        Gp[i][j] = -Sw[i * 3 + j] + BC[i * 3 + j];
+        Gp[i][3 + j] = -Sb[i * 3 + j];
+      }
+    /* d wc / dv [3][4] = R dw + t x (R dd) */
+    double Gl[3][4];
+    for (int k = 0; k < 4; k++) {
+      double Rw[3], Rd[3], tx[3];
+      mat3_vec(R, dw[k], Rw);
+      mat3_vec(R, dd[k], Rd);
+      cross3(t, Rd, tx);
+      for (int i = 0; i < 3; i++) Gl[i][k] = Rw[i] + tx[i];
+    }
+    for (int ep = 0; ep < 2; ep++) {
+      const double* o = obs + 4 * side + 2 * ep;
+      const double num = o[0] * l[0] + o[1] * l[1] + l[2];
+      const double de_dl[3] = {o[0] / n - num * l[0] / (n * n * n), o[1] / n - num * l[1] / (n * n * n), 1.0 / n};
+      double de_dwc[3];
+      for (int j = 0; j < 3; j++) de_dwc[j] = de_dl[0] * M[0 * 3 + j] + de_dl[1] * M[1 * 3 + j] + de_dl[2] * M[2 * 3 + j];
+      const int r = 2 * side + ep;
+      for (int j = 0; j < 6; j++) Jp[r * 6 + j] = de_dwc[0] * Gp[0][j] + de_dwc[1] * Gp[1][j] + de_dwc[2] * Gp[2][j];
+      for (int k = 0; k < 4; k++) Jl[r * 4 + k] = de_dwc[0] * Gl[0][k] + de_dwc[1] * Gl[1][k] + de_dwc[2] * Gl[2][k];
+    }
+  }
+}
+
 /* Jacobians: Jp [edim][6] wrt pose update, Jl [edim][ldim] wrt landmark update. */
 static void linearize(ba_t* b, int t, int e, double* Jp, double* Jl) {
   const rspl_ba_problem* P = b->P;
@@ -351,6 +449,12 @@ static void linearize(ba_t* b, int t, int e, double* Jp, double* Jl) {
         Jl[r * 3 + c] = -sl;
       }
     }
+  } else if (g_line_jac_analytic) {
+    if (t == 2)
+      line_jac_analytic(cam_of(b, P->mono_line_camera, e), &b->T[pi], b->L + 6 * l, P->mono_line_obs + 4 * e, 0, Jp, Jl);
+    else
+      line_jac_analytic(cam_of(b, P->stereo_line_camera, e), &b->T[pi], b->L + 6 * l, P->stereo_line_obs + 8 * e, 1, Jp,
+                        Jl);
   } else {
     /* numeric central difference, delta 1e-9 (g2o BaseBinaryEdge::linearizeOplus) */
     const double delta = 1e-9, scal = 1.0 / (2 * delta);
@@ -842,6 +946,45 @@ int orc_ba_local(const rspl_ba_problem* P, rspl_ba_result* R) {
 
 /* exported helpers for tests: single-edge residual / line oplus */
 void orc_line_oplus(double* L, const double* v) { line_oplus(L, v); }
+
+/* one line edge's Jacobians at T_cw = (q w x y z, t): Jp [rows][6], Jl [rows][4] (rows 2 mono, 4 stereo),
+ * analytic or g2o's central difference (test hook) */
+void orc_line_jacobian(const double* cam, const double* q, const double* t, const double* L, const double* obs,
+                       int stereo, int analytic, double* Jp, double* Jl) {
+  se3 T;
+  memcpy(T.q, q, sizeof(T.q));
+  memcpy(T.t, t, sizeof(T.t));
+  if (analytic) {
+    line_jac_analytic(cam, &T, L, obs, stereo, Jp, Jl);
+    return;
+  }
+  const double delta = 1e-9, scal = 1.0 / (2 * delta);
+  const int rows = stereo ? 4 : 2;
+  double ep[4], em[4], Lp[6];
+  for (int d = 0; d < 4; d++) {
+    double v[4] = {0, 0, 0, 0};
+    v[d] = delta;
+    memcpy(Lp, L, sizeof(Lp));
+    line_oplus(Lp, v);
+    line_err(cam, &T, Lp, obs, stereo, ep);
+    v[d] = -delta;
+    memcpy(Lp, L, sizeof(Lp));
+    line_oplus(Lp, v);
+    line_err(cam, &T, Lp, obs, stereo, em);
+    for (int r = 0; r < rows; r++) Jl[r * 4 + d] = scal * (ep[r] - em[r]);
+  }
+  for (int d = 0; d < 6; d++) {
+    double u[6] = {0, 0, 0, 0, 0, 0};
+    u[d] = delta;
+    se3 dT = se3_exp(u), Tp = se3_mul(&dT, &T);
+    line_err(cam, &Tp, L, obs, stereo, ep);
+    u[d] = -delta;
+    dT = se3_exp(u);
+    Tp = se3_mul(&dT, &T);
+    line_err(cam, &Tp, L, obs, stereo, em);
+    for (int r = 0; r < rows; r++) Jp[r * 6 + d] = scal * (ep[r] - em[r]);
+  }
+}
 
 /* ====================================================================== */
 /* FrameOptimization (src/g2o_optimization/g2o_optimization.cc:256-398):   */

@@ -110,6 +110,27 @@ def ba_local(problem):
     return res
 
 
+def ba_set_line_jacobian(analytic: bool):
+    """Line edges' Jacobians in ba_local: g2o's central difference (False, the default) or its analytic
+    delta -> 0 limit (True)."""
+    lib().orc_ba_set_line_jacobian.argtypes = [C.c_int]
+    lib().orc_ba_set_line_jacobian.restype = None
+    lib().orc_ba_set_line_jacobian(1 if analytic else 0)
+
+
+def line_jacobian(cam, q_wxyz, t, L, obs, stereo: bool, analytic: bool):
+    """One line edge's (Jp [rows, 6], Jl [rows, 4]) at T_cw = (q, t): analytic or central difference."""
+    f64 = lambda a: np.ascontiguousarray(a, np.float64)  # noqa: E731
+    rows = 4 if stereo else 2
+    Jp, Jl = np.zeros((rows, 6)), np.zeros((rows, 4))
+    fn = lib().orc_line_jacobian
+    fn.argtypes = [C.c_void_p] * 5 + [C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    fn.restype = None
+    args = [f64(cam), f64(q_wxyz), f64(t), f64(L), f64(obs)]
+    fn(*[a.ctypes.data for a in args], int(stereo), int(analytic), Jp.ctypes.data, Jl.ctypes.data)
+    return Jp, Jl
+
+
 def line_oplus(L: np.ndarray, v: np.ndarray) -> np.ndarray:
     L = np.ascontiguousarray(L, np.float64).copy()
     lib().orc_line_oplus(L, np.ascontiguousarray(v, np.float64))

@@ -303,6 +303,10 @@ class LocalBA:
         capi.check(self._lib.rspl_ba_kernel_times(self._h, ms, n), "rspl_ba_kernel_times")
         return {"chunks+solve": (ms[0], n[0]), "update": (ms[1], n[1])}
 
+    def set_line_jacobian(self, analytic: bool):
+        """Line edges' Jacobians: g2o's central difference (False, the default) or its analytic limit (True)."""
+        capi.check(self._lib.rspl_ba_set_line_jacobian(self._h, 1 if analytic else 0), "rspl_ba_set_line_jacobian")
+
     def trace(self, cap=4096):
         """The host timeline of the calls since the last read (rspl_ba_trace): a list of dicts with
         capi.BA_TRACE_FIELDS (times in time.perf_counter seconds); [] with a library that lacks it."""

@@ -36,7 +36,7 @@ EXPORTS = [
     "rspl_sg_stage_times", "rspl_sg_destroy",
     "rspl_pm_match",
     "rspl_ba_create", "rspl_ba_local", "rspl_ba_submit", "rspl_ba_join", "rspl_ba_destroy", "rspl_ba_use_reserved_cus", "rspl_ba_kernel_timing",
-    "rspl_ba_kernel_times", "rspl_ba_trace", "rspl_ba_debug_stage",
+    "rspl_ba_kernel_times", "rspl_ba_trace", "rspl_ba_set_line_jacobian", "rspl_ba_debug_stage",
     "rspl_frame_create", "rspl_frame_optimize", "rspl_frame_destroy",
     "rspl_ba_set_shard", "rspl_comm_unique_id", "rspl_comm_create", "rspl_comm_allreduce_sum", "rspl_comm_destroy",
     "rspl_ba_set_comm", "rspl_group_create", "rspl_group_destroy", "rspl_ba_set_group",
@@ -166,6 +166,7 @@ def load(path: pathlib.Path = LIB_PATH):
         lib.rspl_ba_debug_stage.argtypes = [vp, ip, ip, ip] + [vp] * 9
     if hasattr(lib, "rspl_ba_trace"):  # (absent from older builds used as A/B baselines)
         lib.rspl_ba_trace.argtypes = [vp, C.POINTER(C.c_double), ip, C.POINTER(ip)]
+        lib.rspl_ba_set_line_jacobian.argtypes = [vp, ip]
     if hasattr(lib, "rspl_ba_set_shard"):
         lib.rspl_ba_set_shard.argtypes = [vp, ip, ip, vp, vp]
         lib.rspl_comm_unique_id.argtypes = [vp]

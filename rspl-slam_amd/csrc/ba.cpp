@@ -124,6 +124,7 @@ struct rspl_ba {
   std::vector<double> trace;  // kTraceCap x RSPL_BA_TRACE_W
   long long trace_n = 0;      // records written since the last read
   unsigned grew = 0;          // device-side buffers grown during the running call (tracking thread)
+  int line_jac = 0;           // rspl_ba_set_line_jacobian: 0 g2o's central difference, 1 its analytic limit
 };
 
 namespace {
@@ -899,6 +900,13 @@ extern "C" int rspl_ba_kernel_timing(rspl_ba* b, int every) {
   return RSPL_OK;
 }
 
+extern "C" int rspl_ba_set_line_jacobian(rspl_ba* b, int analytic) {
+  RSPL_CHECK_ARG(b && (analytic == 0 || analytic == 1), "rspl_ba_set_line_jacobian: NULL handle or mode not 0 / 1");
+  RSPL_CHECK_ARG(!queue_active(b), "rspl_ba_set_line_jacobian: calls are queued on the tracking thread (rspl_ba_join first)");
+  b->line_jac = analytic;
+  return RSPL_OK;
+}
+
 extern "C" int rspl_ba_trace(rspl_ba* b, double* out, int cap, int* n) {
   RSPL_CHECK_ARG(b && n && cap >= 0 && (out || cap == 0), "rspl_ba_trace: NULL argument or cap < 0");
   std::lock_guard<std::mutex> lk(b->qmu);
@@ -1250,6 +1258,7 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
     P.th[t] = th[t];
     P.delta[t] = (double)(float)std::sqrt(th[t]);  // const float thHuber = sqrt(cfg.x) (:77-78, 125-126)
   }
+  P.line_jac = b->line_jac;
   ba::Lin Lr{};
   Lr.err = b->err; Lr.rho0 = b->rho0; Lr.Hpp = b->Hpp_e; Lr.bp = b->bp_e; Lr.Hll = b->Hll_e; Lr.bl = b->bl_e;
   Lr.Hpl = b->Hpl_e;

@@ -22,8 +22,12 @@ namespace rspl {
 namespace ba {
 
 
-__device__ __forceinline__ double n3(const double* v) { return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]); }
+__device__ __forceinline__ double n3(const double* v) {
+  #pragma clang fp contract(off)  // bit-identical to the CPU restatement (oracle/ba.c, -ffp-contract=off)
+  return sqrt(v[0] * v[0] + v[1] * v[1] + v[2] * v[2]);
+}
 __device__ __forceinline__ void cross3(const double* a, const double* b, double* o) {
+  #pragma clang fp contract(off)  // bit-identical to the CPU restatement (oracle/ba.c, -ffp-contract=off)
   o[0] = a[1] * b[2] - a[2] * b[1];
   o[1] = a[2] * b[0] - a[0] * b[2];
   o[2] = a[0] * b[1] - a[1] * b[0];
@@ -31,6 +35,7 @@ __device__ __forceinline__ void cross3(const double* a, const double* b, double*
 
 // g2o::Line3D::oplus (orthonormal 4-DoF update; vertex_line3d.h:26-29)
 __device__ __forceinline__ void line_oplus(double* L, const double* v) {
+  #pragma clang fp contract(off)  // bit-identical to the CPU restatement (oracle/ba.c, -ffp-contract=off)
   const double* w = L;
   const double* d = L + 3;
   const double mx = n3(d), my = n3(w);
@@ -79,6 +84,7 @@ __device__ __forceinline__ SE3 load_T(const double* T) {
 
 // Edge residual for pose estimate T and landmark values lm (point [3] or line [6]).
 __device__ __forceinline__ void edge_error(int type, const double* cam, const double* obs, const SE3& T, const double* lm, double (&e)[4]) {
+  #pragma clang fp contract(off)  // bit-identical to the CPU restatement (oracle/ba.c, -ffp-contract=off)
   double R[9];
   q_to_R(T.q, R);
   if (type < 2) {  // EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ: e = obs - proj(T p)
@@ -111,6 +117,92 @@ __device__ __forceinline__ void edge_error(int type, const double* cam, const do
   };
   side_err(T.t[0], obs, e[0], e[1]);
   if (type == 3) side_err(T.t[0] - cam[4] / fx, obs + 4, e[2], e[3]);  // T_right(0,3) -= b, b = bf / fx
+}
+
+// Line-edge Jacobians, analytic (Problem::line_jac = 1): the delta -> 0 limit of g2o's central difference
+// (truncation O(delta^2) ~ 1e-18 relative at delta 1e-9; the central difference itself carries ~1e-7 relative
+// cancellation noise).  The same derivation and operation order as oracle/ba.c line_jac_analytic (FP
+// contraction off: bit-identical to it): pose d wc / d omega = -[wc]x (+ [b]x [c]x on the right camera of a
+// stereo edge, c = (bf / fx, 0, 0)), d wc / d upsilon = -[b]x with b = R d; line (Line3D::oplus at 0 after
+// its |d| = 1 normalisation) d w / dv = [0, -2 rho u3, 2 rho u2, -(1 + rho^2) u1], d d / dv = [2 u3, 0, -2 u1, 0];
+// error e_k = (o_k . l01 + l2) / |l01|, l = [fy wc0, fx wc1, Kv . wc].  Jp [4][6], Jl [4][4] (rows 2 / 4).
+__device__ __forceinline__ void skew3(const double* v, double* S) {
+  S[0] = 0; S[1] = -v[2]; S[2] = v[1];
+  S[3] = v[2]; S[4] = 0; S[5] = -v[0];
+  S[6] = -v[1]; S[7] = v[0]; S[8] = 0;
+}
+
+__device__ __forceinline__ void line_jac_analytic(const double* cam, const SE3& T, const double* L, const double* obs,
+                                                  bool stereo, double* Jp, double* Jl) {
+  #pragma clang fp contract(off)  // bit-identical to the CPU restatement (oracle/ba.c, -ffp-contract=off)
+  const double fx = cam[0], fy = cam[1], cx = cam[2], cy = cam[3], bf = cam[4];
+  const double M[9] = {fy, 0, 0, 0, fx, 0, -fy * cx, -fx * cy, fx * fy};
+  const double dn = n3(L + 3), wn = n3(L);
+  double w[3], d[3], u1[3], u3[3], wxd[3];
+  for (int i = 0; i < 3; i++) {
+    w[i] = L[i] / dn;
+    d[i] = L[3 + i] / dn;
+    u1[i] = L[i] / wn;
+  }
+  cross3(L, L + 3, wxd);
+  const double cn = n3(wxd);
+  for (int i = 0; i < 3; i++) u3[i] = wxd[i] / cn;
+  const double rho = wn / dn;
+  double dw[4][3], dd[4][3];
+  for (int i = 0; i < 3; i++) {
+    dw[0][i] = 0;                dd[0][i] = 2 * u3[i];
+    dw[1][i] = -2 * rho * u3[i]; dd[1][i] = 0;
+    dw[2][i] = 2 * rho * d[i];   dd[2][i] = -2 * u1[i];
+    dw[3][i] = -(1 + rho * rho) * u1[i]; dd[3][i] = 0;
+  }
+  double R[9], a[3], bb[3], Sb[9];
+  q_to_R(T.q, R);
+  mat3_vec(R, w, a);
+  mat3_vec(R, d, bb);
+  skew3(bb, Sb);
+  for (int side = 0; side < (stereo ? 2 : 1); side++) {
+    double t[3] = {T.t[0], T.t[1], T.t[2]};
+    const double c[3] = {side == 1 ? bf / fx : 0.0, 0.0, 0.0};
+    t[0] -= c[0];
+    double txb[3], wc[3];
+    cross3(t, bb, txb);
+    for (int i = 0; i < 3; i++) wc[i] = a[i] + txb[i];
+    double l[3];
+    mat3_vec(M, wc, l);
+    const double n = sqrt(l[0] * l[0] + l[1] * l[1]);
+    double Sw[9], Sc[9], BC[9];
+    skew3(wc, Sw);
+    skew3(c, Sc);
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        double s = 0;
+        for (int k = 0; k < 3; k++) s += Sb[i * 3 + k] * Sc[k * 3 + j];
+        BC[i * 3 + j] = s;
+      }
+    double Gp[3][6], Gl[3][4];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) {
+        Gp[i][j] = -Sw[i * 3 + j] + BC[i * 3 + j];
+        Gp[i][3 + j] = -Sb[i * 3 + j];
+      }
+    for (int k = 0; k < 4; k++) {
+      double Rw[3], Rd[3], tx[3];
+      mat3_vec(R, dw[k], Rw);
+      mat3_vec(R, dd[k], Rd);
+      cross3(t, Rd, tx);
+      for (int i = 0; i < 3; i++) Gl[i][k] = Rw[i] + tx[i];
+    }
+    for (int ep = 0; ep < 2; ep++) {
+      const double* o = obs + 4 * side + 2 * ep;
+      const double num = o[0] * l[0] + o[1] * l[1] + l[2];
+      const double de_dl[3] = {o[0] / n - num * l[0] / (n * n * n), o[1] / n - num * l[1] / (n * n * n), 1.0 / n};
+      double de_dwc[3];
+      for (int j = 0; j < 3; j++) de_dwc[j] = de_dl[0] * M[0 * 3 + j] + de_dl[1] * M[1 * 3 + j] + de_dl[2] * M[2 * 3 + j];
+      const int r = 2 * side + ep;
+      for (int j = 0; j < 6; j++) Jp[r * 6 + j] = de_dwc[0] * Gp[0][j] + de_dwc[1] * Gp[1][j] + de_dwc[2] * Gp[2][j];
+      for (int k = 0; k < 4; k++) Jl[r * 4 + k] = de_dwc[0] * Gl[0][k] + de_dwc[1] * Gl[1][k] + de_dwc[2] * Gl[2][k];
+    }
+  }
 }
 
 // a per-type constant of the kernel-argument structs with a select chain: a dynamic index would
@@ -852,10 +944,29 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
       slot = lane;
       m = 20;
     }
+    if (P.line_jac) {  // analytic: one lane per edge (wave 0), its error too (OWN_ERR)
+      slot = (wv == 0 && lane < kLineBlk) ? lane : -1;
+      m = OWN_ERR ? 20 : 21;
+    }
     int e = 0, t = 2;
     bool on = false, live = false;
     if (slot >= 0) edge(slot, e, t, on, live);
-    if (live) {
+    if (live && P.line_jac) {
+      const SE3 T = load_T(SPEC ? &Tsh[slot][0] : P.T + 8 * P.epose[e]);
+      const double* cam = P.cams + 5 * P.ecam[e];
+      const double* obs = obs_of(P, e, t);
+      double Lp[6];
+      for (int k = 0; k < 6; k++) Lp[k] = SPEC ? cand[einfo_s[slot][3] - gb][k] : Lsh[slot][k];
+      double Jp[24], Jl[16];
+      line_jac_analytic(cam, T, Lp, obs, t == 3, Jp, Jl);
+      for (int k = 0; k < 4 * edim(t); k++) J[slot][24 + k] = Jl[k];
+      for (int k = 0; k < 6 * edim(t); k++) J[slot][k] = Jp[k];
+      if (OWN_ERR) {
+        double er[4] = {0, 0, 0, 0};
+        edge_error(t, cam, obs, T, Lp, er);
+        for (int k = 0; k < 4; k++) es[slot][k] = er[k];
+      }
+    } else if (live) {
       const int d = m >> 1;
       const double sgn = (m & 1) ? -delta : delta;
       const SE3 T = load_T(SPEC ? &Tsh[slot][0] : P.T + 8 * P.epose[e]);
@@ -905,8 +1016,8 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
     }
     *chi_out = c;
   }
-  // J layout per edge: Jp [4][6] at 0, Jl [4][4] at 24
-  for (int idx = tid; idx < 40 * kLineBlk; idx += 256) {
+  // J layout per edge: Jp [4][6] at 0, Jl [4][4] at 24 (the analytic path wrote it directly)
+  for (int idx = tid; idx < (P.line_jac ? 0 : 40 * kLineBlk); idx += 256) {
     const int slot = idx / 40, rd = idx - 40 * slot, r = rd / 10, d = rd % 10;
     int e, t;
     bool on, live;
@@ -1660,6 +1771,197 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
   if (tid == 0) prof_stamp(S, 4);
 }
 
+
+// ---------------------------------------------------------------------------
+// The same blocked LDL^T with the trailing matrix in REGISTERS (K > kWaveSolveMaxK: C5's 30-keyframe
+// window, n = 174): schur_solve_kernel's trailing update re-reads and rewrites the whole packed triangle
+// in LDS every pose step (29 steps x ~15k entries: LDS-bandwidth bound, ~4 us per step).  Here the lower
+// triangle (+ the bordered rhs row n) is cut into 3x3 tiles, column-major, dealt cyclically to 512 threads
+// (<= kRegTiles each); a tile lives in its owner's registers from the assembly to the step that factors
+// its block column.  Pose step s: the owners of tile columns 2s, 2s+1 write them to LDS; barrier; wave 0
+// factors the 6x6 diagonal block and forms the panel rows (X = A L^-T D^-1, into LDS as the factor's
+// L, exactly as schur_solve_kernel); barrier; every owner of a trailing tile applies A_ik -= sum_l (X_il d_l)
+// X_kl from the panel in LDS, in registers.  The same operations in the same order as
+// schur_solve_kernel (bitwise the same factor); backward substitution, solution and LM scale as there.
+constexpr int kRegThreads = 512, kRegTiles = 5;  // (64 * 65 / 2 + 64 = 2144 tiles at n = 192) <= 512 x 5
+
+__global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Active A, Sys S, int n, double lambda) {
+  extern __shared__ double Al[];
+  __shared__ int bad;
+  if (S.lm) {
+    LmView v;
+    if (!lm_view(S, v)) return;
+    lambda = v.lambda;
+    if (v.cur) bank_state(P);
+  }
+  const int K = n / 6, R = n / 3;  // R: the tile row of the rhs row n
+  double* z = Al + pk(n, 0);
+  double* rdg = Al + pk(n + 1, 0);
+  double* ddg = rdg + n;
+  double* Ldg = ddg + n;
+  double* bpl = Ldg + 15 * K;
+  const int tid = threadIdx.x;
+  if (tid == 0) bad = 0;
+  const int pose_a = tid < P.np ? A.pidx[tid] : -1;
+  if (tid == 0) prof_stamp(S, 0);
+  const int nent = A.npairs * 42;
+  for (int q0 = tid; q0 < nent; q0 += 8 * kRegThreads) {
+    double v1[8], v2[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int idx = q0 + u * kRegThreads;
+      const int pr = idx / 42, v = idx - 42 * pr;
+      v1[u] = idx < nent ? S.pairfin[48 * pr + v] : 0.0;
+      v2[u] = (idx < nent && v >= 36) ? S.pairfin[48 * pr + v + 6] : 0.0;
+    }
+    if (*S.fail) return;
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      const int idx = q0 + u * kRegThreads;
+      if (idx >= nent) break;
+      const int pr = idx / 42, v = idx - 42 * pr;
+      int pa, pb;
+      pair_of(pr, K, pa, pb);
+      if (v < 36) {
+        const int r = v / 6, cc = v - 6 * r;
+        if (pa == pb) {
+          if (cc <= r) Al[pk(6 * pa + r, 6 * pa + cc)] = v1[u] + (r == cc ? lambda : 0.0);
+        } else {
+          Al[pk(6 * pb + cc, 6 * pa + r)] = v1[u];
+        }
+      } else if (pa == pb) {
+        const int r = v - 36;
+        bpl[6 * pa + r] = v1[u];
+        z[6 * pa + r] = v1[u] - v2[u];
+      }
+    }
+  }
+  __syncthreads();
+  // this thread's tiles (column-major over the lower triangle + the rhs row tile R of each column)
+  int tr[kRegTiles], tc[kRegTiles];
+  double T[kRegTiles][9];
+  {
+    int q = tid, c = 0, base = 0;
+#pragma unroll
+    for (int u = 0; u < kRegTiles; u++, q += kRegThreads) {
+      while (c < R && q >= base + (R - c + 1)) {
+        base += R - c + 1;
+        c++;
+      }
+      tc[u] = c < R ? c : -1;
+      tr[u] = c < R ? c + (q - base) : -1;
+#pragma unroll
+      for (int e = 0; e < 9; e++) {
+        const int i = 3 * tr[u] + e / 3, k = 3 * tc[u] + e % 3;
+        T[u][e] = (tc[u] >= 0 && i <= n && k <= i) ? Al[pk(i, k)] : 0.0;
+      }
+    }
+  }
+  if (tid == 0) prof_stamp(S, 1);
+  const int wv = tid >> 6, lane = tid & 63;
+  for (int s = 0; s < K; s++) {
+    const int c0 = 6 * s, r0 = c0 + 6;
+    // (a) the block column's tiles to LDS
+#pragma unroll
+    for (int u = 0; u < kRegTiles; u++) {
+      if (tc[u] != 2 * s && tc[u] != 2 * s + 1) continue;
+#pragma unroll
+      for (int e = 0; e < 9; e++) {
+        const int i = 3 * tr[u] + e / 3, k = 3 * tc[u] + e % 3;
+        if (i <= n && k <= i) Al[pk(i, k)] = T[u][e];
+      }
+    }
+    __syncthreads();
+    if (wv == 0) {  // (b) diagonal block + panel rows (as schur_solve_kernel)
+      double L6[15], d6[6], r6[6];
+      const bool ok = ldl6(Al, c0, L6, d6, r6);
+      if (lane == 0) {
+#pragma unroll
+        for (int q = 0; q < 15; q++) Ldg[15 * s + q] = L6[q];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+          rdg[c0 + k] = r6[k];
+          ddg[c0 + k] = d6[k];
+        }
+        if (!ok) bad = 1;
+      }
+      for (int i = r0 + lane; i <= n; i += 64) {
+        double* row = Al + pk(i, c0);
+        double w[6];
+#pragma unroll
+        for (int k = 0; k < 6; k++) w[k] = row[k];
+#pragma unroll
+        for (int k = 0, q = 0; k < 6; k++) {
+#pragma unroll
+          for (int l = 0; l < k; l++, q++) w[k] -= w[l] * L6[q];
+        }
+#pragma unroll
+        for (int k = 0; k < 6; k++) row[k] = w[k] * r6[k];
+      }
+    }
+    __syncthreads();
+    if (tid == 0 && s < 2) prof_stamp(S, 5 + 2 * s);
+    if (bad) {
+      if (tid == 0) atomicOr(S.fail, 1);
+      return;
+    }
+    // (c) trailing tiles in registers
+#pragma unroll
+    for (int u = 0; u < kRegTiles; u++) {
+      if (tc[u] < 2 * s + 2) continue;
+      const int i0 = 3 * tr[u], k0 = 3 * tc[u];
+      double wi[3][6], xk[3][6];
+#pragma unroll
+      for (int a = 0; a < 3; a++)
+#pragma unroll
+        for (int l = 0; l < 6; l++) {
+          wi[a][l] = (i0 + a <= n) ? Al[pk(i0 + a, c0 + l)] * ddg[c0 + l] : 0.0;
+          xk[a][l] = Al[pk(k0 + a, c0 + l)];
+        }
+#pragma unroll
+      for (int e = 0; e < 9; e++) {
+        double t = T[u][e];
+#pragma unroll
+        for (int l = 0; l < 6; l++) t -= wi[e / 3][l] * xk[e % 3][l];
+        T[u][e] = t;
+      }
+    }
+    if (tid == 0 && s < 2) prof_stamp(S, 6 + 2 * s);
+  }
+  __syncthreads();
+  if (wv != 0) return;
+  if (tid == 0) prof_stamp(S, 2);
+  for (int s = K - 1; s >= 0; s--) {
+    const int c0 = 6 * s;
+    double xb[6];
+#pragma unroll
+    for (int k = 5; k >= 0; k--) {
+      double v = z[c0 + k];
+#pragma unroll
+      for (int l = k + 1; l < 6; l++) v -= Ldg[15 * s + l * (l - 1) / 2 + k] * xb[l];
+      xb[k] = v;
+    }
+    for (int i = lane; i < c0; i += 64) {
+      double v = z[i];
+#pragma unroll
+      for (int l = 0; l < 6; l++) v -= Al[pk(c0 + l, i)] * xb[l];
+      z[i] = v;
+    }
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < 6; k++) z[c0 + k] = xb[k];
+  }
+  for (int i = lane; i < n; i += 64) S.x[i] = z[i];
+  if (tid == 0) prof_stamp(S, 3);
+  double sc = 0;
+  if (lane < P.np && pose_a >= 0)
+#pragma unroll
+    for (int k = 0; k < 6; k++) sc += z[6 * pose_a + k] * (lambda * z[6 * pose_a + k] + bpl[6 * pose_a + k]);
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
+  if (lane == 0) S.out[4] = sc;
+  if (tid == 0) prof_stamp(S, 4);
+}
 
 // ---------------------------------------------------------------------------
 // Reduced camera system for n = 6K <= 60 (K <= kWaveSolveMaxK optimised poses: the C3 window)
@@ -2972,8 +3274,22 @@ hipError_t ensure_schur_attr() {
   if (attr) return hipSuccess;
   hipError_t e = hipFuncSetAttribute((const void*)schur_solve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                      (int)schur_lds_bytes(kCholLdsMax));
+  if (e == hipSuccess)
+    e = hipFuncSetAttribute((const void*)schur_reg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)schur_lds_bytes(kCholLdsMax));
   if (e == hipSuccess) attr = true;
   return e;
+}
+
+// the LDS-resident blocked LDL^T of the reduced system (K > kWaveSolveMaxK, or RSPL_BA_SOLVE=lds): the
+// register-tiled kernel (RSPL_BA_SOLVE_LDS=packed: the packed-LDS one, A/B)
+static void launch_lds_solve(const Problem& P, const Active& A, const Sys& S, double lambda, hipStream_t s) {
+  static const bool packed = getenv("RSPL_BA_SOLVE_LDS") && std::string(getenv("RSPL_BA_SOLVE_LDS")) == "packed";
+  const int n = 6 * A.K;
+  if (packed)
+    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
+  else
+    hipLaunchKernelGGL(schur_reg_kernel, dim3(1), dim3(kRegThreads), schur_lds_bytes(n), s, P, A, S, n, lambda);
 }
 
 // pair_chunk grid: 8 XCD lanes x (landmark ranges per XCD) x pose pairs (idle slots exit)
@@ -3029,7 +3345,7 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
     } else if (mode == 0) {
       hipError_t e = ensure_schur_attr();
       if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
+      launch_lds_solve(P, A, S, lambda, s);
     }
     const int nbu = update_errors_blocks(A);
     if (spec) {
@@ -3065,8 +3381,7 @@ hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, un
   } else if (mode == 0) {
     hipError_t e = ensure_schur_attr();
     if (e != hipSuccess) return e;
-    const int n = 6 * A.K;
-    hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, 0.0);
+    launch_lds_solve(P, A, S, 0.0, s);
   }
   const int nbu = update_errors_blocks(A), nbl = A.n_lblk;
   if (ev) (void)hipEventRecord(ev[1], s);
@@ -3123,7 +3438,7 @@ hipError_t trial_solve(const Problem& P, const Lin& L, const Active& A, Sys& S, 
     } else {
       hipError_t e = ensure_schur_attr();
       if (e != hipSuccess) return e;
-      hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
+      launch_lds_solve(P, A, S, lambda, s);
     }
     hipLaunchKernelGGL(update_errors_kernel<false>, dim3(update_errors_blocks(A)), dim3(256), 0, s, P, L, A, S, lambda,
                        0ull, L, S, 0);

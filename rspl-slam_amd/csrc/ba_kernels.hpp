@@ -30,6 +30,7 @@ struct Problem {
   int Ep;                // point edges (the first line edge's position)
   double delta[4];       // Huber deltas per type
   double th[4];          // chi2 thresholds per type
+  int line_jac;          // line edges' Jacobians: 0 g2o's central difference (delta 1e-9), 1 its analytic limit
 };
 
 struct Lin {             // per-edge linearisation records (indexed by edge id)

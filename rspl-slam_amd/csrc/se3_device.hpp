@@ -23,6 +23,7 @@ __device__ __forceinline__ double cube(double x) {
 }
 
 __device__ __forceinline__ void q_to_R(const double* q, double* R) {
+  #pragma clang fp contract(off)  // bit-identical to the CPU restatement (oracle/ba.c, -ffp-contract=off)
   const double w = q[0], x = q[1], y = q[2], z = q[3];
   const double tx = 2 * x, ty = 2 * y, tz = 2 * z;
   const double twx = tx * w, twy = ty * w, twz = tz * w;
@@ -34,12 +35,14 @@ __device__ __forceinline__ void q_to_R(const double* q, double* R) {
 }
 
 __device__ __forceinline__ void mat3_vec(const double* R, const double* v, double* o) {
+  #pragma clang fp contract(off)  // bit-identical to the CPU restatement (oracle/ba.c, -ffp-contract=off)
   o[0] = R[0] * v[0] + R[1] * v[1] + R[2] * v[2];
   o[1] = R[3] * v[0] + R[4] * v[1] + R[5] * v[2];
   o[2] = R[6] * v[0] + R[7] * v[1] + R[8] * v[2];
 }
 
 __device__ __forceinline__ void se3_normalize(SE3& T) {
+  #pragma clang fp contract(off)  // bit-identical to the CPU restatement (oracle/ba.c, -ffp-contract=off)
   if (T.q[0] < 0)
     for (int i = 0; i < 4; i++) T.q[i] = -T.q[i];
   const double n = sqrt(T.q[0] * T.q[0] + T.q[1] * T.q[1] + T.q[2] * T.q[2] + T.q[3] * T.q[3]);
@@ -47,6 +50,7 @@ __device__ __forceinline__ void se3_normalize(SE3& T) {
 }
 
 __device__ __forceinline__ void R_to_q(const double* m, double* q) {
+  #pragma clang fp contract(off)  // bit-identical to the CPU restatement (oracle/ba.c, -ffp-contract=off)
   const double t = m[0] + m[4] + m[8];
   if (t > 0) {
     double s = sqrt(t + 1.0);
@@ -77,6 +81,7 @@ __device__ __forceinline__ void R_to_q(const double* m, double* q) {
 }
 
 __device__ __forceinline__ SE3 se3_mul(const SE3& a, const SE3& b) {
+  #pragma clang fp contract(off)  // bit-identical to the CPU restatement (oracle/ba.c, -ffp-contract=off)
   SE3 r;
   double R[9], t[3];
   q_to_R(a.q, R);
@@ -92,6 +97,7 @@ __device__ __forceinline__ SE3 se3_mul(const SE3& a, const SE3& b) {
 
 // SE3Quat::exp, update = [omega; upsilon]
 __device__ inline SE3 se3_exp(const double* u) {
+  #pragma clang fp contract(off)  // bit-identical to the CPU restatement (oracle/ba.c, -ffp-contract=off)
   const double* w = u;
   const double th = sqrt(w[0] * w[0] + w[1] * w[1] + w[2] * w[2]);
   const double O[9] = {0, -w[2], w[1], w[2], 0, -w[0], -w[1], w[0], 0};

@@ -19,6 +19,9 @@ import oracle  # noqa: E402
 
 SY = pkg.synthetic
 ba = pkg.LocalBA(max_poses=40, max_points=12000, max_lines=400, max_edges=80000)
+ANALYTIC = "--analytic" in sys.argv  # line Jacobians: analytic limit on both sides (else g2o's central difference)
+ba.set_line_jacobian(ANALYTIC)
+oracle.ba_set_line_jacobian(ANALYTIC)
 cases = []
 for s, l, o in [(1, 20, 0.0), (2, 30, 0.05), (3, 0, 0.05), (4, 10, 0.1)]:
     cases.append(("matches_oracle", dict(n_poses=8, n_points=600, n_lines=l, seed=s, pixel_sigma=0.8, outlier_frac=o,
@@ -50,7 +53,7 @@ for name, c, env in cases:
     dpt = np.abs(r.points - o.points).max(1) if r.points.size else np.zeros(0)
     rel = lambda a, b: abs(a - b) / max(abs(b), 1e-300)  # noqa: E731
     print(json.dumps({
-        "case": name, **{k: c[k] for k in ("n_poses", "n_points", "n_lines", "seed")}, **env,
+        "case": name, "line_jac": "analytic" if ANALYTIC else "numeric", **{k: c[k] for k in ("n_poses", "n_points", "n_lines", "seed")}, **env,
         "iters": [r.iters_first, r.iters_second], "iters_oracle": [o.iters_first, o.iters_second],
         "chi2_rel": [rel(r.chi2_first, o.chi2_first), rel(r.chi2_second, o.chi2_second)],
         "pose": max(float(np.abs(r.pose_p - o.pose_p).max()), qdiff(r.pose_q, o.pose_q)),

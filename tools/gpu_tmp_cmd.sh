@@ -22,5 +22,13 @@ run base20b librspl_base.so --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
 run new200 librspl.so --steps 200 --warmup 10 --no-cpu-baseline --single-precision
 run base200 librspl_base.so --steps 200 --warmup 10 --no-cpu-baseline --single-precision
 timeout -k 10 200 python3 -u tools/ba_parity_cases.py > gpurun_out/r05/parity_new.jsonl 2>&1 || { echo "parity failed"; tail gpurun_out/r05/parity_new.jsonl; exit 1; }
-RSPL_LIB=librspl_base.so timeout -k 10 200 python3 -u tools/ba_parity_cases.py > gpurun_out/r05/parity_base.jsonl 2>&1 || { echo "parity base failed"; exit 1; }
+timeout -k 10 200 python3 -u tools/ba_parity_cases.py --analytic > gpurun_out/r05/parity_analytic.jsonl 2>&1 || { echo "parity analytic failed"; tail gpurun_out/r05/parity_analytic.jsonl; exit 1; }
 echo parity done
+timeout -k 10 500 python -u tools/run_c1_plumbing.py --pairs 100 --out gpurun_out/r05/c1_pairs.jsonl > gpurun_out/r05/c1_plumbing.json 2> gpurun_out/r05/c1.err || { echo "c1 failed"; tail -5 gpurun_out/r05/c1.err; exit 1; }
+python3 -c "import json; d=json.load(open('gpurun_out/r05/c1_plumbing.json')); print({k: d[k] for k in d if 'e2e' in k or 'unexpl' in k or 'P_max' in k})"
+for v in reg packed; do
+  [ $v = packed ] && export RSPL_BA_SOLVE_LDS=packed
+  timeout -k 10 120 python -u tools/bench_ba.py --iters 10 --poses 30 --points 10000 --lines 0 > gpurun_out/r05/c5ba_$v.txt 2>&1 || { echo "c5 ba $v failed"; tail gpurun_out/r05/c5ba_$v.txt; exit 1; }
+  echo "c5 ba $v: $(tail -2 gpurun_out/r05/c5ba_$v.txt)"
+done
+unset RSPL_BA_SOLVE_LDS

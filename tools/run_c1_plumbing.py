@@ -40,7 +40,7 @@ import rspl_loader  # noqa: E402
 
 pkg = rspl_loader.load()
 pkg.capi.load()
-from helpers import unexplained_match_disagreements  # noqa: E402  (test infrastructure)
+from helpers import E2E_CLASSES, classify_e2e_disagreements, unexplained_match_disagreements  # noqa: E402
 import lines_ref as LR  # noqa: E402  (the CPU path being compared against; test infrastructure)
 import oracle  # noqa: E402
 import post  # noqa: E402
@@ -75,6 +75,48 @@ def align_z(Zg, Fg0, Fg1, Fc0, Fc1):
     rows = [kg0[c] for c in c0] + [len(c0)]
     cols = [kg1[c] for c in c1] + [len(c1)]
     return Zg[np.ix_(rows, cols)]
+
+
+def shared_z(Zg, Fg0, Fg1, Zc, Fc0, Fc1):
+    """Zg and Zc restricted to the keypoints both paths kept (rows / columns in the CPU path's order, the
+    dustbin row / column last): comparable whatever the two keypoint sets are (with different sets the
+    difference includes the effect of the keypoints only one path has -- attention and Sinkhorn see all)."""
+    kg0, kg1 = key_index(Fg0), key_index(Fg1)
+    c0 = [(int(x), int(y)) for x, y in zip(Fc0[1], Fc0[2])]
+    c1 = [(int(x), int(y)) for x, y in zip(Fc1[1], Fc1[2])]
+    rc = [i for i, c in enumerate(c0) if c in kg0] + [len(c0)]
+    cc = [j for j, c in enumerate(c1) if c in kg1] + [len(c1)]
+    rg = [kg0[c0[i]] for i in rc[:-1]] + [Fg0.shape[1]]
+    cg = [kg1[c1[j]] for j in cc[:-1]] + [Fg1.shape[1]]
+    return Zg[np.ix_(rg, cg)], Zc[np.ix_(rc, cc)]
+
+
+def score_error(Fa, Fb):
+    """max |score| difference over the keypoints both paths kept, both images"""
+    e = 0.0
+    for A, B in zip(Fa, Fb):
+        ka, kb = key_index(A), key_index(B)
+        for c in set(ka) & set(kb):
+            e = max(e, abs(float(A[0, ka[c]]) - float(B[0, kb[c]])))
+    return e
+
+
+def e2e(Fc, Z, Fg, Zg):
+    """end-to-end disagreements of the GPU path (its own keypoints, its Z) vs the CPU path, thresholded
+    (0.2, the reference's decode) and mutual-NN (threshold 0), classified (helpers.classify_e2e_disagreements)
+    with the pair's own measured errors as the tie margins: 2x the score error on the shared keypoints and 2x
+    the significant-entry |dZ| on them (floors 1e-7 / 1e-6)"""
+    zg, zc = shared_z(Zg, Fg[0], Fg[1], Z, Fc[0], Fc[1])
+    sig = zc > np.log(1e-4)
+    dz = float(np.abs(zg - zc)[sig].max()) if sig.any() else 0.0
+    s_tol = max(2.0 * score_error(Fc, Fg), 1e-7)
+    z_tol = max(2.0 * dz, 1e-6)
+    out = {"score_tol": s_tol, "z_tol": z_tol}
+    for name, thr in (("thresholded", 0.2), ("mutual_nn", 0.0)):
+        cnt, bad = classify_e2e_disagreements(Fc, Fg, Z, Zg, thr, s_tol, z_tol, k=K)
+        out[name] = cnt
+        out[name + "_unexplained"] = [list(map(int, m)) for _, m in bad][:8]
+    return out
 
 
 def z_errors(Zg, Z):
@@ -170,6 +212,12 @@ def main():
             c16 = match_coords(res["fp16"][2], F16[0], F16[1])
             za = align_z(Zg, Fg[0], Fg[1], Fc[0], Fc[1])
             za16 = align_z(res["fp16"][3], F16[0], F16[1], Fc[0], Fc[1])
+            # every pair: Z on the keypoints both paths kept (the sets may differ)
+            zs32 = shared_z(Zg, Fg[0], Fg[1], Z, Fc[0], Fc[1])
+            zs16 = shared_z(res["fp16"][3], F16[0], F16[1], Z, Fc[0], Fc[1])
+            dps32, _ = z_errors(*zs32)
+            dps16, dzs16 = z_errors(*zs16)
+            e32, e16 = e2e(Fc, Z, Fg, Zg), e2e(Fc, Z, F16, res["fp16"][3])
             zerr = float(np.abs(za - Z).max()) if za is not None else float("nan")
             # fp32 thresholded-decode disagreements (GPU Z in the CPU order) must be near-ties of the CPU Z
             bad32 = -1
@@ -203,7 +251,9 @@ def main():
                    "keypoint_order_identical": bool(order_same and all(Fg[i].shape == Fc[i].shape for i in (0, 1))),
                    "desc_max_abs_diff": dmax,
                    "Z_max_abs_diff_fp32": zerr,
-                   "P_max_abs_diff_fp32": dp, "Z_sig_max_abs_diff_fp32": dzs, "P_max_abs_diff_fp16": dp16,
+                   "P_max_abs_diff_fp32": dp, "Z_sig_max_abs_diff_fp32": dzs, "P_max_abs_diff_fp16_same_set": dp16,
+                   "P_max_abs_diff_fp32_shared": dps32, "P_max_abs_diff_fp16": dps16, "Z_sig_max_abs_diff_fp16": dzs16,
+                   "e2e_fp32": e32, "e2e_fp16": e16,
                    "matches_cpu": len(sc_), "matches_gpu_fp32": len(sg_), "matches_identical": sc_ == sg_,
                    "matches_identical_coords": match_coords(mc, Fc[0], Fc[1]) == match_coords(mg, Fg[0], Fg[1]),
                    "match_distance_max_abs_diff_fp32": float(dist_err),
@@ -237,7 +287,23 @@ def main():
         "Z_max_abs_diff_fp32": float(np.nanmax([r["Z_max_abs_diff_fp32"] for r in rows])),
         "P_max_abs_diff_fp32": float(np.nanmax([r["P_max_abs_diff_fp32"] for r in rows])),
         "Z_sig_max_abs_diff_fp32": float(np.nanmax([r["Z_sig_max_abs_diff_fp32"] for r in rows])),
+        # fp16 end to end (fp16 SuperPoint + SuperGlue): Z on the keypoints both paths kept, every pair
         "P_max_abs_diff_fp16": float(np.nanmax([r["P_max_abs_diff_fp16"] for r in rows])),
+        "P_max_abs_diff_fp16_pairs": int(sum(np.isfinite(r["P_max_abs_diff_fp16"]) for r in rows)),
+        "P_max_abs_diff_fp16_p50": float(np.nanmedian([r["P_max_abs_diff_fp16"] for r in rows])),
+        "Z_sig_max_abs_diff_fp16": float(np.nanmax([r["Z_sig_max_abs_diff_fp16"] for r in rows])),
+        "P_max_abs_diff_fp16_same_set_pairs": int(sum(np.isfinite(r["P_max_abs_diff_fp16_same_set"]) for r in rows)),
+        "P_max_abs_diff_fp32_shared": float(np.nanmax([r["P_max_abs_diff_fp32_shared"] for r in rows])),
+        # every end-to-end match disagreement (matches as keypoint-coordinate pairs, each path with its own
+        # keypoints), classified: keypoint absent near the top-k cut / at an NMS near-tie, decision going to a
+        # keypoint the other path lacks, near-tie of the CPU Z, or unexplained (helpers.classify_e2e_disagreements)
+        **{f"e2e_{p}_{kind}": {c: int(sum(r[f"e2e_{p}"][kind][c] for r in rows)) for c in E2E_CLASSES}
+           for p in ("fp32", "fp16") for kind in ("thresholded", "mutual_nn")},
+        "unexplained_end_to_end_fp16": int(sum(r["e2e_fp16"][k]["unexplained"] for r in rows
+                                               for k in ("thresholded", "mutual_nn"))),
+        "unexplained_end_to_end_fp32": int(sum(r["e2e_fp32"][k]["unexplained"] for r in rows
+                                               for k in ("thresholded", "mutual_nn"))),
+        "thresholded_matches_coords_differ_pairs_fp32": [r["pair"] for r in rows if not r["matches_identical_coords"]],
         "keypoint_sets_identical_fp16_frac": agg("keypoint_sets_identical_fp16"),
         "thresholded_matches_identical_frac": agg("matches_identical"),
         "thresholded_matches_identical_coords_frac": agg("matches_identical_coords"),
