@@ -798,7 +798,11 @@ __device__ __forceinline__ void cand_pose(const Problem& P, const Active& A, con
   o[7] = 0;
 }
 
-// outlier levels after the first optimize / final inlier flags (g2o_optimization.cc:176-231)
+// outlier levels after the first optimize / final inlier flags (g2o_optimization.cc:176-231).
+// Reads only fields that are NOT banked: L.err (swapped by neither bank_lin nor accept_swap) and the state
+// P.T / P.X.  The speculative final kernel (SpecFinish, ba.cpp) reuses the Lin captured before optimize(5)
+// and banks only the state; a classification that read a banked Lin field (Hpp, bp, Hll, bl, Hpl) would
+// differ between that path and the host-ordered one (tests/test_gpu_ba.py test_ba_final_kernel_paths_agree).
 __device__ __forceinline__ void edge_status(const Problem& P, const Lin& L, int e, double& chi2, bool& depth_ok) {
   const int t = P.etype[e];
   chi2 = 0;
