@@ -608,7 +608,14 @@ def main():
 
         host_wait = {"lines": 0.0, "ba_queue": 0.0, "sp_calls": 0.0, "sg_calls": 0.0, "line_assoc_calls": 0.0,
                      "line_submit": 0.0}
-        line_t0 = None
+        # the warmup steps run exactly the timed steps' code path, measurement included (stage timers, the BA's
+        # kernel timing, the line-association timers): the HIP runtime sets up timing events lazily, and the
+        # first timed call paid ~8 ms for it when the warmup ran without them (profiles/r05_bench_20step.json)
+        sp.profile(True)
+        sg.profile(True)
+        ba.kernel_timing(ktime_every)
+        line_timers[:] = [capi.Timer() for _ in range(args.warmup)]
+        line_t0 = 0
         for i in range(args.warmup):
             step(i)
         ba_drain()
@@ -617,7 +624,7 @@ def main():
             raise SystemExit(f"bench: SuperGlue device path failed during warmup: {sg.error}")
         if dist:
             dist.barrier()
-        sp.profile(True)
+        sp.profile(True)  # (resets the stage accumulators)
         sg.profile(True)
         ba_ms.clear()
         ba_iters.clear()

@@ -1782,9 +1782,10 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
 // in LDS every pose step (29 steps x ~15k entries: LDS-bandwidth bound, ~4 us per step).  Here the lower
 // triangle (+ the bordered rhs row n) is cut into 3x3 tiles, column-major, dealt cyclically to 512 threads
 // (<= kRegTiles each); a tile lives in its owner's registers from the assembly to the step that factors
-// its block column.  Pose step s: the owners of tile columns 2s, 2s+1 write them to LDS; barrier; wave 0
-// factors the 6x6 diagonal block and forms the panel rows (X = A L^-T D^-1, into LDS as the factor's
-// L, exactly as schur_solve_kernel); barrier; every owner of a trailing tile applies A_ik -= sum_l (X_il d_l)
+// its block column.  Pose step s: the owners of tile columns 2s, 2s+1 write them to LDS; barrier; every wave
+// factors the 6x6 diagonal block (redundantly: no broadcast) and each thread forms one panel row (X = A L^-T
+// D^-1, into LDS as the factor's L, exactly as schur_solve_kernel); barrier; every owner of a trailing tile
+// applies A_ik -= sum_l (X_il d_l)
 // X_kl from the panel in LDS, in registers.  The same operations in the same order as
 // schur_solve_kernel (bitwise the same factor); backward substitution, solution and LM scale as there.
 constexpr int kRegThreads = 512, kRegTiles = 5;  // (64 * 65 / 2 + 64 = 2144 tiles at n = 192) <= 512 x 5
@@ -1824,8 +1825,7 @@ __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Activ
       const int idx = q0 + u * kRegThreads;
       if (idx >= nent) break;
       const int pr = idx / 42, v = idx - 42 * pr;
-      int pa, pb;
-      pair_of(pr, K, pa, pb);
+      const int pa = A.pairs[2 * pr], pb = A.pairs[2 * pr + 1];  // (the host's pair table: no decode loop)
       if (v < 36) {
         const int r = v / 6, cc = v - 6 * r;
         if (pa == pb) {
@@ -1876,10 +1876,10 @@ __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Activ
       }
     }
     __syncthreads();
-    if (wv == 0) {  // (b) diagonal block + panel rows (as schur_solve_kernel)
+    {  // (b) every wave factors the 6x6 diagonal block itself (uniform, no broadcast), one panel row per thread
       double L6[15], d6[6], r6[6];
       const bool ok = ldl6(Al, c0, L6, d6, r6);
-      if (lane == 0) {
+      if (tid == 0) {
 #pragma unroll
         for (int q = 0; q < 15; q++) Ldg[15 * s + q] = L6[q];
 #pragma unroll
@@ -1889,7 +1889,7 @@ __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Activ
         }
         if (!ok) bad = 1;
       }
-      for (int i = r0 + lane; i <= n; i += 64) {
+      for (int i = r0 + tid; i <= n; i += kRegThreads) {  // X = a L_dd^-T D^-1 (as schur_solve_kernel)
         double* row = Al + pk(i, c0);
         double w[6];
 #pragma unroll

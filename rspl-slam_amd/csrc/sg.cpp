@@ -40,6 +40,8 @@ struct rspl_sg {
   // RSPL_PREC_FP16 GNN activations: fp16 shadow of X, Q | K, V^T per head, messages, hidden
   _Float16 *Xh, *QKh, *Vth, *Oh, *MSGh, *HIDh;
   _Float16 *Qf[2], *Kf[2], *Vf[2];  // fused layers: q (row-major) / k, v (MFMA fragment order), ping-pong
+  unsigned long long *l4M, *l4H, *l4X;  // layer4_kernel exchange tiles (message, HID, new x) per 32-token tile
+  unsigned* l4ctr;                      // its per-tile ticket counters (zeroed per call)
   int ldv = 0;  // token stride of Vth (nmax rounded up to the 32-key attention tile; zero padded)
   unsigned long long *ug, *vg;  // Sinkhorn u / v exchange granules [B][ld] (row-block: ug = [B][2][rbG][ld])
   int rbG = 0;                  // row-block Sinkhorn workgroups per pair (0: slab kernel)
@@ -113,6 +115,11 @@ void carve(F& ar, rspl_sg* s) {
   take(s->MSGh, T * 256); take(s->HIDh, T * 512);
   for (int i = 0; i < 2; i++) {
     take(s->Qf[i], T * 256); take(s->Kf[i], (size_t)B * 2 * 256 * s->ldv); take(s->Vf[i], (size_t)B * 2 * 256 * s->ldv);
+  }
+  {
+    const size_t nt4 = (size_t)sg::gnn_layer4_tiles((int)B, s->nmax);
+    take(s->l4M, nt4 * 32 * 256 / 4); take(s->l4H, nt4 * 32 * 512 / 4); take(s->l4X, nt4 * 32 * 256 / 4);
+    take(s->l4ctr, nt4);
   }
 
   take(s->cpl, 2 * B * ld * ld); take(s->Z, 2 * B * ld * ld); take(s->ug, ug_len(s)); take(s->vg, vg_len(s));
@@ -492,11 +499,21 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
       g.nmax = nm; g.ldv = s->ldv;
       return g;
     };
-    static const bool unfused = [] {
-      const char* v = getenv("RSPL_SG_GNN");  // A/B knob: "unfused" = four launches per layer
-      return v && std::string(v) == "unfused";
+    // RSPL_SG_GNN (A/B knob): default one launch per layer on four workgroups per 32-token tile (layer4_kernel);
+    // "tile1" one workgroup per tile (layer_kernel, the same bits); "unfused" four launches per layer
+    static const int gnn_mode = [] {
+      const char* v = getenv("RSPL_SG_GNN");
+      return v && std::string(v) == "unfused" ? 2 : v && std::string(v) == "tile1" ? 1 : 0;
     }();
-    auto layer = [&](sg::LayerArgs& la, int) { return sg::gnn_layer(la, B, st); };
+    const bool unfused = gnn_mode == 2;
+    if (gnn_mode == 0)
+      RSPL_HIP(hipMemsetAsync(s->l4ctr, 0, sizeof(unsigned) * sg::gnn_layer4_tiles(B, nm), st));
+    auto layer = [&](sg::LayerArgs& la, int l) {
+      if (gnn_mode == 1) return sg::gnn_layer(la, B, st);
+      la.xM = s->l4M; la.xH = s->l4H; la.xX = s->l4X; la.ctr = s->l4ctr;
+      la.base = 12u * (unsigned)(l < 0 ? 0 : l);
+      return sg::gnn_layer4(la, B, st);
+    };
     if (!unfused) {  // layer 0's q / k / v (prologue launch), then one fused launch per layer
       {
         sg::LayerArgs la{};

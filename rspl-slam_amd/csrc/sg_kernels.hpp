@@ -91,6 +91,12 @@ struct LayerArgs {
   int cross, last;
   int qkv_only;          // prologue: only phase (4) from the current x (layer 0's q / k / v)
   int nsets, xps, tpx;   // set by gnn_layer: token sets, XCDs per set (0 = plain grid), tiles per XCD
+  // layer4_kernel (four workgroups per 32-token tile): exchange tiles of the message [tile][32][256], HID
+  // [tile][32][512] and new x [tile][32][256] (fp16 as 8-byte granules), a ticket counter per tile (zeroed per
+  // SuperGlue call) and this launch's counter base (12 per layer)
+  unsigned long long *xM, *xH, *xX;
+  unsigned* ctr;
+  unsigned base;
 };
 
 struct PrepArgs {
@@ -166,6 +172,9 @@ hipError_t to_frag(const _Float16* Wt, int N, int K, _Float16* out, hipStream_t 
 hipError_t gemm_h(const GemmHArgs& a, int mode, hipStream_t s);
 hipError_t attention_h(const AttnHArgs& a, int B, hipStream_t s);
 hipError_t gnn_layer(const LayerArgs& a, int B, hipStream_t s);
+// the same layer on four workgroups per 32-token tile (layer4_kernel; a.xM / xH / xX / ctr / base set)
+hipError_t gnn_layer4(const LayerArgs& a, int B, hipStream_t s);
+int gnn_layer4_tiles(int B, int nmax);  // exchange tiles / counters the handle allocates
 // fp32 -> fp16, n elements
 hipError_t to_half(const float* x, _Float16* y, size_t n, hipStream_t s);
 hipError_t prep(const PrepArgs& a, hipStream_t s);

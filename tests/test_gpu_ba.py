@@ -46,7 +46,7 @@ def _compare(res, ref, tol_pose=1e-7, tol_pt=1e-6, tol_line=5e-3, chi2_rtol=1e-8
 
 
 LINES = dict(tol_pose=1e-6, tol_pt=1e-5, chi2_rtol=5e-8)  # numeric line Jacobians (see above)
-ANALYTIC = dict(tol_pose=1e-9, tol_pt=1e-8, tol_line=1e-7, chi2_rtol=1e-10)
+ANALYTIC = dict(tol_pose=1e-11, tol_pt=1e-9, tol_line=1e-9, chi2_rtol=1e-12)  # measured: 2e-14 / 3e-11 / 9e-12 / 2e-14
 
 
 @pytest.fixture()
@@ -173,7 +173,10 @@ def test_ba_run_into_reused_result(ba):
     assert (again.chi2_first, again.iters_first) == (fresh.chi2_first, fresh.iters_first)
     other = ba.run(p2, out=out)  # shapes differ: a new result
     assert other is not out and other.points.shape == p2.points.shape
-    _compare(other, oracle.ba_local(p2), **LINES)
+    fresh2 = ba.run(p2)
+    np.testing.assert_array_equal(other.points, fresh2.points)
+    np.testing.assert_array_equal(other.pose_q, fresh2.pose_q)
+    # (p2 against the oracle: test_ba_within_reference_order_spread -- its numeric-Jacobian spread exceeds LINES)
 
 
 def test_ba_native_tracking_thread(ba):
@@ -255,3 +258,39 @@ def test_ba_local_refused_while_queued(ba):
         ba.run(p)
     ba.join()
     ba.run(p)  # fine after the join
+
+
+def test_ba_within_reference_order_spread(ba):
+    """A line problem whose numeric-Jacobian chaos exceeds LINES (5 poses, 8 lines, seed 72): the oracle against
+    ITSELF with its edges permuted differs by up to ~1.7e-5 in points and ~4.5e-8 in chi2 (the central
+    difference's noise, see _compare's note).  The GPU must stay inside that envelope of the reference algorithm
+    (measured here over four permutations, x2), and equal the oracle to rounding level with the analytic line
+    Jacobian."""
+    import sys
+    import pathlib
+    sys.path.insert(0, str(pathlib.Path(__file__).resolve().parent))
+    from test_oracle_ba_linejac import _permuted
+    p, _ = SY.ba_problem(n_poses=5, n_points=300, n_lines=8, seed=72, pixel_sigma=0.8, outlier_frac=0.05)
+    ref = oracle.ba_local(p)
+    env = dict(chi2=0.0, pose=0.0, pts=0.0)
+    for seed in range(4):
+        q = _permuted(p, seed)
+        env["chi2"] = max(env["chi2"], abs(q.chi2_second - ref.chi2_second) / ref.chi2_second)
+        env["pose"] = max(env["pose"], float(np.abs(q.pose_p - ref.pose_p).max()))
+        env["pts"] = max(env["pts"], float(np.abs(q.points - ref.points).max()))
+    got = ba.run(p)
+    assert (got.iters_first, got.iters_second) == (ref.iters_first, ref.iters_second)
+    for k in got.inlier:
+        np.testing.assert_array_equal(got.inlier[k], ref.inlier[k])
+    print("reference order spread", env, "GPU", abs(got.chi2_second - ref.chi2_second) / ref.chi2_second,
+          np.abs(got.pose_p - ref.pose_p).max(), np.abs(got.points - ref.points).max())
+    assert abs(got.chi2_second - ref.chi2_second) / ref.chi2_second <= 2 * env["chi2"]
+    assert np.abs(got.pose_p - ref.pose_p).max() <= 2 * env["pose"]
+    assert np.abs(got.points - ref.points).max() <= 2 * env["pts"]
+    ba.set_line_jacobian(True)
+    oracle.ba_set_line_jacobian(True)
+    try:
+        _compare(ba.run(p), oracle.ba_local(p), **ANALYTIC)
+    finally:
+        ba.set_line_jacobian(False)
+        oracle.ba_set_line_jacobian(False)
