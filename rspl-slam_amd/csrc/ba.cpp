@@ -1235,7 +1235,10 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
     b->pp_cap = cap;
     b->grew |= 2;
   }
-  RSPL_HIP(hipMemcpyAsync(b->cbuf, sg, cl.bytes, hipMemcpyHostToDevice, st));
+  // the call's inputs in one upload (RSPL_BA_UPLOAD=kernel: a copy kernel reading the host-mapped slot, A/B)
+  static const bool up_kernel = getenv("RSPL_BA_UPLOAD") && std::string(getenv("RSPL_BA_UPLOAD")) == "kernel";
+  if (up_kernel) RSPL_HIP(ba::upload(b->cbuf, b->stage_dev[c.slot], cl.bytes, st));
+  else RSPL_HIP(hipMemcpyAsync(b->cbuf, sg, cl.bytes, hipMemcpyHostToDevice, st));
   tm.mark("upload");
   tr[4] = mono_s();
   char* cb = b->cbuf;

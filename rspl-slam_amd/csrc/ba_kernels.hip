@@ -3395,6 +3395,17 @@ hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, un
   return hipGetLastError();
 }
 
+__global__ __launch_bounds__(256) void upload_kernel(uint4* dst, const uint4* src, size_t n) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+}
+
+hipError_t upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t s) {
+  const size_t n = bytes / 16;
+  if (n) hipLaunchKernelGGL(upload_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 1024)), dim3(256), 0, s,
+                           static_cast<uint4*>(dst), static_cast<const uint4*>(src_mapped), n);
+  return hipGetLastError();
+}
+
 hipError_t finish(const Problem& P, const Lin& L, int E, const int* gmap, uint8_t* inl, double* Th, double* Xh,
                   double* Lh, Sys& S, unsigned long long seq, hipStream_t s) {
   const int n = std::max(std::max(E, 8 * P.np), std::max(3 * P.nq, 6 * P.nl));

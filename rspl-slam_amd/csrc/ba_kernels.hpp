@@ -171,6 +171,9 @@ hipError_t build_pairs(const Active& A, int* pp_cnt, int* pp_off, int4* pp, hipS
 hipError_t landmark_active(const Active& A, const uint8_t* level, uint8_t* lm_act, hipStream_t s);
 hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8_t* inlier, int final_pass,
                     hipStream_t s);
+// the call's upload as a kernel: bytes (a multiple of 16) from host-mapped pinned memory (its device
+// pointer) into device memory, 16-byte loads over the link (no copy engine)
+hipError_t upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t s);
 // final inlier flags + T / X / L into host-mapped memory, then the mailbox post of seq
 hipError_t finish(const Problem& P, const Lin& L, int E, const int* gmap, uint8_t* inl, double* Th, double* Xh,
                   double* Lh, Sys& S, unsigned long long seq, hipStream_t s);

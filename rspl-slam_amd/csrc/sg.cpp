@@ -499,11 +499,13 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
       g.nmax = nm; g.ldv = s->ldv;
       return g;
     };
-    // RSPL_SG_GNN (A/B knob): default one launch per layer on four workgroups per 32-token tile (layer4_kernel);
-    // "tile1" one workgroup per tile (layer_kernel, the same bits); "unfused" four launches per layer
+    // RSPL_SG_GNN (A/B knob): default one launch per layer on one workgroup per 32-token tile (layer_kernel);
+    // "tile4" on four workgroups per tile (layer4_kernel, the same bits: measured slower in the pipeline -- three
+    // exchanges per layer, and 4x the CU footprint beside the BA, profiles/r05_experiments.md); "unfused" four
+    // launches per layer
     static const int gnn_mode = [] {
       const char* v = getenv("RSPL_SG_GNN");
-      return v && std::string(v) == "unfused" ? 2 : v && std::string(v) == "tile1" ? 1 : 0;
+      return v && std::string(v) == "unfused" ? 2 : v && std::string(v) == "tile4" ? 0 : 1;
     }();
     const bool unfused = gnn_mode == 2;
     if (gnn_mode == 0)

@@ -385,6 +385,9 @@ def test_sg_c1_fp16_disagreements_explained(pkg, golden, sg_c1_blob):
     Z = sg.debug_scores(0, F0.shape[1], F1.shape[1])
     sig = g["Z"] > np.log(1e-4)
     tol = 2.0 * float(np.abs(Z - g["Z"])[sig].max())  # a disagreement needs a gap below twice the fp16 error
+    # and that error itself is bounded absolutely: 0.084 measured on this fixture (round 5), the bound 3x that,
+    # so a change that degrades the fp16 path cannot widen the tie margin unnoticed
+    assert tol / 2 < 0.25, f"fp16 |dZ| on significant entries {tol / 2:.3g}"
     bad = unexplained_match_disagreements(g["Z"], i0, i1, g["idx0"], g["idx1"], tol)
     agree = ((i0 == g["idx0"]).mean() + (i1 == g["idx1"]).mean()) / 2
     print(f"c1 fp16: index agreement {agree:.4f}, fp16 |dZ| (significant) {tol / 2:.3g}, "
@@ -414,8 +417,8 @@ np.savez(sys.argv[3], **out)
 
 
 def test_sg_gnn_layer4_equals_tile1(pkg, weight_blobs, tmp_path):
-    """The fp16 GNN layer on four workgroups per 32-token tile (layer4_kernel, default) gives the same bits as
-    the one-workgroup-per-tile kernel (layer_kernel, RSPL_SG_GNN=tile1): the same MFMA operands in the same
+    """The fp16 GNN layer on four workgroups per 32-token tile (layer4_kernel, RSPL_SG_GNN=tile4) gives the same
+    bits as the one-workgroup-per-tile kernel (layer_kernel, the default): the same MFMA operands in the same
     order.  N = 400 (C3, ragged) and N = 2048 (C5: 256 tiles, more workgroups than one dispatch round)."""
     import os
     import pathlib
@@ -425,14 +428,14 @@ def test_sg_gnn_layer4_equals_tile1(pkg, weight_blobs, tmp_path):
     script = tmp_path / "z.py"
     script.write_text(_GNN_Z_SCRIPT)
     zs = {}
-    for mode in ("default", "tile1"):
+    for mode in ("default", "tile4"):
         env = dict(os.environ)
         env.pop("RSPL_SG_GNN", None)
-        if mode == "tile1":
-            env["RSPL_SG_GNN"] = "tile1"
+        if mode == "tile4":
+            env["RSPL_SG_GNN"] = "tile4"
         out = tmp_path / f"{mode}.npz"
         subprocess.run([sys.executable, str(script), root, weight_blobs[1], str(out)], env=env, check=True,
                        timeout=240)
         zs[mode] = np.load(out)
     for k in zs["default"].files:
-        np.testing.assert_array_equal(zs["default"][k], zs["tile1"][k], err_msg=k)
+        np.testing.assert_array_equal(zs["default"][k], zs["tile4"][k], err_msg=k)

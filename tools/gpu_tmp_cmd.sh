@@ -1,31 +1,23 @@
 #!/bin/bash
 # Scratch GPU command of the current experiment (rewritten per experiment).
-# Round 5: GNN layer on four workgroups per tile (fixed), warmup with the timed path's instrumentation; the
-# driver's command twice, 200-step A/B of the GNN kernels and HEAD's library, the C1 record.
+# Round 5: the first timed BA call's 7-8 ms stall inside hipMemcpyAsync -- the upload as a kernel vs the
+# copy, and a HIP API log of the copy case; the C5 BA solve's phases (in-kernel trace).
 set -o pipefail
-mkdir -p gpurun_out/r05b
-timeout -k 10 600 python3 -u -m pytest tests/test_gpu_sg.py tests/test_gpu_ba.py -q --timeout 250 --timeout-method thread > gpurun_out/r05b/tests.log 2>&1
-rc=$?; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "tests rc $rc"; tail -30 gpurun_out/r05b/tests.log; exit 1; fi
-grep -E "FAILED|passed|failed" gpurun_out/r05b/tests.log | tail -12
-timeout -k 10 300 python3 -u -m pytest tests/test_gpu_sg.py -k "c1_fp16 or fp16_vs" -q -s --timeout 250 --timeout-method thread 2>&1 | grep -E "fp16|passed|failed" | head -8
-run() {  # tag lib args...
-  local tag=$1 lib=$2; shift 2
-  RSPL_LIB=$lib RSPL_BENCH_TRACE=gpurun_out/r05b/trace_$tag.json timeout -k 10 240 python3 bench.py "$@" \
-    > gpurun_out/r05b/$tag.json 2> gpurun_out/r05b/$tag.err || { echo "bench $tag failed"; tail -20 gpurun_out/r05b/$tag.err; exit 1; }
+mkdir -p gpurun_out/r05c
+timeout -k 10 400 python3 -u -m pytest tests/test_gpu_ba.py tests/test_gpu_sg.py -q -x --timeout 250 --timeout-method thread > gpurun_out/r05c/tests.log 2>&1 || { echo "tests failed"; tail -30 gpurun_out/r05c/tests.log; exit 1; }
+tail -1 gpurun_out/r05c/tests.log
+run() {  # tag args...
+  local tag=$1; shift
+  RSPL_BENCH_TRACE=gpurun_out/r05c/trace_$tag.json timeout -k 10 240 python3 bench.py "$@" \
+    > gpurun_out/r05c/$tag.json 2> gpurun_out/r05c/$tag.err || { echo "bench $tag failed"; tail -20 gpurun_out/r05c/$tag.err; exit 1; }
   python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); s=d['stages_ms_per_step']
-print(sys.argv[2], d['value'], d['ms_per_step'], 'ba', s.get('ba:wall'), 'gnn', s.get('sg:gnn x18'), 'sink', s.get('sg:sinkhorn'), 'roof', d['roofline']['kernel'], d['roofline']['frac'])" gpurun_out/r05b/$tag.json $tag
+print(sys.argv[2], d['value'], d['ms_per_step'], 'ba', s.get('ba:wall'), 'gnn', s.get('sg:gnn x18'))" gpurun_out/r05c/$tag.json $tag
+  python3 tools/bench_trace.py gpurun_out/r05c/trace_$tag.json | sed -n 3p
 }
-run drv1 librspl.so --gpus 1 --steps 20 --warmup 5
-run drv2 librspl.so --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
-RSPL_SG_GNN=tile1 run drv_t1 librspl.so --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline
-run s200 librspl.so --steps 200 --warmup 10 --no-cpu-baseline --single-precision
-RSPL_SG_GNN=tile1 run s200_t1 librspl.so --steps 200 --warmup 10 --no-cpu-baseline --single-precision
-run s200_base librspl_base.so --steps 200 --warmup 10 --no-cpu-baseline --single-precision
-RSPL_SG_GNN=tile1 run s200_t1b librspl.so --steps 200 --warmup 10 --no-cpu-baseline --single-precision
-run s200b librspl.so --steps 200 --warmup 10 --no-cpu-baseline --single-precision
-timeout -k 10 500 python -u tools/run_c1_plumbing.py --pairs 100 --out gpurun_out/r05b/c1_pairs.jsonl > gpurun_out/r05b/c1_plumbing.json 2> gpurun_out/r05b/c1.err || { echo "c1 failed"; tail -5 gpurun_out/r05b/c1.err; exit 1; }
-python3 -c "import json; d=json.load(open('gpurun_out/r05b/c1_plumbing.json')); print({k: d[k] for k in d if 'e2e' in k or 'unexpl' in k or 'P_max' in k or 'identical' in k})"
-timeout -k 10 120 python -u tools/bench_ba.py --iters 10 --poses 30 --points 10000 --lines 0 > gpurun_out/r05b/c5ba.txt 2>&1 || { echo "c5 ba failed"; tail gpurun_out/r05b/c5ba.txt; exit 1; }
-echo "c5 ba: $(tail -1 gpurun_out/r05b/c5ba.txt)"
-timeout -k 10 120 python -u tools/bench_ba.py --iters 30 > gpurun_out/r05b/c3ba.txt 2>&1 || { echo "c3 ba failed"; exit 1; }
-echo "c3 ba: $(tail -1 gpurun_out/r05b/c3ba.txt)"
+run copy --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --single-precision
+RSPL_BA_UPLOAD=kernel run kern --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --single-precision
+AMD_LOG_LEVEL=4 AMD_LOG_MASK=0x105 run copylog --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --single-precision
+grep -c . gpurun_out/r05c/copylog.err
+RSPL_BA_UPLOAD=kernel run kern2 --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline --single-precision
+RSPL_BA_PROF=1 timeout -k 10 120 python -u tools/bench_ba.py --iters 4 --poses 30 --points 10000 --lines 0 > gpurun_out/r05c/c5prof.txt 2>&1 || { echo "c5 prof failed"; tail gpurun_out/r05c/c5prof.txt; exit 1; }
+grep -E "ba_prof|BA " gpurun_out/r05c/c5prof.txt | tail -4

@@ -119,6 +119,41 @@ def e2e(Fc, Z, Fg, Zg):
     return out
 
 
+def e2e_fp16_decomposed(F16, Z16g, Fc, Z, sg_w):
+    """Every end-to-end fp16 match disagreement (fp16 SuperPoint + fp16 SuperGlue vs the CPU path), split by
+    cause with the reference's own fp32 SuperGlue run on the fp16 SuperPoint features (Z16c):
+      fp16_superpoint_input    the fp32 SuperGlue makes the GPU's decision on those features too: the fp16
+                               SuperPoint outputs (scores, descriptors, a keypoint at the top-k cut) changed
+                               SuperGlue's input, the reference algorithm does the same on that input;
+      fp16_superglue_near_tie  the GPU fp16 SuperGlue and the fp32 one disagree on the same features, and Z16c
+                               shows a near-tie within 2x the pair's fp16 SuperGlue |dZ| (significant entries);
+      unexplained              neither."""
+    g0, g1 = post.normalize_keypoints(F16[0], W, H), post.normalize_keypoints(F16[1], W, H)
+    Z16c = oracle.sg_forward(sg_w, *post.sg_inputs(g0), *post.sg_inputs(g1))
+    sig = Z16c > np.log(1e-4)
+    dz = float(np.abs(Z16g - Z16c)[sig].max()) if sig.any() else 0.0
+    out = {"sg_only_dZ_sig": dz}
+    for name, thr in (("thresholded", 0.2), ("mutual_nn", 0.0)):
+        dg, dcc, dc = post.decode(Z16g, threshold=thr), post.decode(Z16c, threshold=thr), post.decode(Z, threshold=thr)
+        mg = match_coords(post.match_points(*dg)[0], F16[0], F16[1])
+        m16c = match_coords(post.match_points(*dcc)[0], F16[0], F16[1])
+        mc = match_coords(post.match_points(*dc)[0], Fc[0], Fc[1])
+        bad_sg = {(int(F16[0][1, i]), int(F16[0][2, i])) for kind, i in
+                  unexplained_match_disagreements(Z16c, dg[0], dg[1], dcc[0], dcc[1], 2.0 * dz) if kind == "row"}
+        bad_sg |= {("col", int(F16[1][1, j]), int(F16[1][2, j])) for kind, j in
+                   unexplained_match_disagreements(Z16c, dg[0], dg[1], dcc[0], dcc[1], 2.0 * dz) if kind == "col"}
+        cnt = {"fp16_superpoint_input": 0, "fp16_superglue_near_tie": 0, "unexplained": 0}
+        for m in (mc ^ mg):
+            if (m in mg) == (m in m16c):
+                cnt["fp16_superpoint_input"] += 1
+            elif (m[0], m[1]) in bad_sg or ("col", m[2], m[3]) in bad_sg:
+                cnt["unexplained"] += 1
+            else:
+                cnt["fp16_superglue_near_tie"] += 1
+        out[name] = cnt
+    return out
+
+
 def z_errors(Zg, Z):
     """max |exp(Zg) - exp(Z)| (assignment probabilities) and max |dZ| where the CPU probability >= 1e-4;
     log-probabilities far below that amplify rounding and carry no decision"""
@@ -218,6 +253,7 @@ def main():
             dps32, _ = z_errors(*zs32)
             dps16, dzs16 = z_errors(*zs16)
             e32, e16 = e2e(Fc, Z, Fg, Zg), e2e(Fc, Z, F16, res["fp16"][3])
+            e16d = e2e_fp16_decomposed(F16, res["fp16"][3], Fc, Z, sg_w)
             zerr = float(np.abs(za - Z).max()) if za is not None else float("nan")
             # fp32 thresholded-decode disagreements (GPU Z in the CPU order) must be near-ties of the CPU Z
             bad32 = -1
@@ -253,7 +289,7 @@ def main():
                    "Z_max_abs_diff_fp32": zerr,
                    "P_max_abs_diff_fp32": dp, "Z_sig_max_abs_diff_fp32": dzs, "P_max_abs_diff_fp16_same_set": dp16,
                    "P_max_abs_diff_fp32_shared": dps32, "P_max_abs_diff_fp16": dps16, "Z_sig_max_abs_diff_fp16": dzs16,
-                   "e2e_fp32": e32, "e2e_fp16": e16,
+                   "e2e_fp32": e32, "e2e_fp16": e16, "e2e_fp16_by_cause": e16d,
                    "matches_cpu": len(sc_), "matches_gpu_fp32": len(sg_), "matches_identical": sc_ == sg_,
                    "matches_identical_coords": match_coords(mc, Fc[0], Fc[1]) == match_coords(mg, Fg[0], Fg[1]),
                    "match_distance_max_abs_diff_fp32": float(dist_err),
@@ -299,8 +335,16 @@ def main():
         # keypoint the other path lacks, near-tie of the CPU Z, or unexplained (helpers.classify_e2e_disagreements)
         **{f"e2e_{p}_{kind}": {c: int(sum(r[f"e2e_{p}"][kind][c] for r in rows)) for c in E2E_CLASSES}
            for p in ("fp32", "fp16") for kind in ("thresholded", "mutual_nn")},
-        "unexplained_end_to_end_fp16": int(sum(r["e2e_fp16"][k]["unexplained"] for r in rows
+        # the same disagreements split by cause (e2e_fp16_decomposed: the reference's fp32 SuperGlue re-run on the
+        # fp16 SuperPoint features separates the SuperPoint input change from SuperGlue's own fp16 rounding)
+        **{f"e2e_fp16_by_cause_{kind}": {c: int(sum(r["e2e_fp16_by_cause"][kind][c] for r in rows))
+                                         for c in ("fp16_superpoint_input", "fp16_superglue_near_tie", "unexplained")}
+           for kind in ("thresholded", "mutual_nn")},
+        "sg_only_fp16_dZ_sig_max": float(max(r["e2e_fp16_by_cause"]["sg_only_dZ_sig"] for r in rows)),
+        "unexplained_end_to_end_fp16": int(sum(r["e2e_fp16_by_cause"][k]["unexplained"] for r in rows
                                                for k in ("thresholded", "mutual_nn"))),
+        "unexplained_end_to_end_fp16_self_calibrated_classes": int(sum(r["e2e_fp16"][k]["unexplained"] for r in rows
+                                                                       for k in ("thresholded", "mutual_nn"))),
         "unexplained_end_to_end_fp32": int(sum(r["e2e_fp32"][k]["unexplained"] for r in rows
                                                for k in ("thresholded", "mutual_nn"))),
         "thresholded_matches_coords_differ_pairs_fp32": [r["pair"] for r in rows if not r["matches_identical_coords"]],
