@@ -1235,9 +1235,12 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
     b->pp_cap = cap;
     b->grew |= 2;
   }
-  // the call's inputs in one upload (RSPL_BA_UPLOAD=kernel: a copy kernel reading the host-mapped slot, A/B)
-  static const bool up_kernel = getenv("RSPL_BA_UPLOAD") && std::string(getenv("RSPL_BA_UPLOAD")) == "kernel";
-  if (up_kernel) RSPL_HIP(ba::upload(b->cbuf, b->stage_dev[c.slot], cl.bytes, st));
+  // the call's inputs in one upload: a copy kernel reading the host-mapped staging slot over PCIe.  Not
+  // hipMemcpyAsync: its H2D path stalled the first calls after the warmup by 7-10 ms each (the SDMA engine /
+  // blit-kernel choice settling; profiles/r05_bench_20step_before.json), which cost the driver's 20-step bench
+  // a quarter of its rate.  RSPL_BA_UPLOAD=copy keeps the old path for A/B.
+  static const bool up_copy = getenv("RSPL_BA_UPLOAD") && std::string(getenv("RSPL_BA_UPLOAD")) == "copy";
+  if (!up_copy) RSPL_HIP(ba::upload(b->cbuf, b->stage_dev[c.slot], cl.bytes, st));
   else RSPL_HIP(hipMemcpyAsync(b->cbuf, sg, cl.bytes, hipMemcpyHostToDevice, st));
   tm.mark("upload");
   tr[4] = mono_s();
