@@ -47,7 +47,7 @@ struct rspl_ba {
   // candidate state (ping-pong partners of the call buffer's T / X / L)
   double *Tb, *Xb, *Lb;
   // per-edge linearisation records
-  double *err, *rho0, *Hpp_e, *bp_e, *Hll_e, *bl_e, *Hpl_e;
+  double *err, *Hpp_e, *bp_e, *Hll_e, *bl_e, *Hpl_e;
   // spare linearisation set (per-edge records + landmark blocks): each trial's candidate is
   // linearised speculatively into it, and becomes current by a pointer swap when accepted
   double *Hpp_s, *bp_s, *Hll_es, *bl_es, *Hpl_s, *Hll_s, *bl_s;
@@ -241,7 +241,7 @@ void carve(F& ar, rspl_ba* b) {
     else ar.template take<Tp>(n ? n : 1);
   };
   take(b->Tb, K * 8); take(b->Xb, nq * 3); take(b->Lb, nl * 6);
-  take(b->err, E * 4); take(b->rho0, E); take(b->Hpp_e, E * 21); take(b->bp_e, E * 6); take(b->Hll_e, E * 16);
+  take(b->err, E * 4); take(b->Hpp_e, E * 21); take(b->bp_e, E * 6); take(b->Hll_e, E * 16);
   take(b->bl_e, E * 4); take(b->Hpl_e, E * 24);
   take(b->Hpp_s, E * 21); take(b->bp_s, E * 6); take(b->Hll_es, E * 16); take(b->bl_es, E * 4); take(b->Hpl_s, E * 24);
   take(b->Hll_s, NL * 16); take(b->bl_s, NL * 4);
@@ -1240,7 +1240,7 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
   // blit-kernel choice settling; profiles/r05_bench_20step_before.json), which cost the driver's 20-step bench
   // a quarter of its rate.  RSPL_BA_UPLOAD=copy keeps the old path for A/B.
   static const bool up_copy = getenv("RSPL_BA_UPLOAD") && std::string(getenv("RSPL_BA_UPLOAD")) == "copy";
-  if (!up_copy) RSPL_HIP(ba::upload(b->cbuf, b->stage_dev[c.slot], cl.bytes, st));
+  if (!up_copy) RSPL_HIP(upload_mapped(b->cbuf, b->stage_dev[c.slot], cl.bytes, st));
   else RSPL_HIP(hipMemcpyAsync(b->cbuf, sg, cl.bytes, hipMemcpyHostToDevice, st));
   tm.mark("upload");
   tr[4] = mono_s();
@@ -1266,7 +1266,7 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
   }
   P.line_jac = b->line_jac;
   ba::Lin Lr{};
-  Lr.err = b->err; Lr.rho0 = b->rho0; Lr.Hpp = b->Hpp_e; Lr.bp = b->bp_e; Lr.Hll = b->Hll_e; Lr.bl = b->bl_e;
+  Lr.err = b->err; Lr.Hpp = b->Hpp_e; Lr.bp = b->bp_e; Lr.Hll = b->Hll_e; Lr.bl = b->bl_e;
   Lr.Hpl = b->Hpl_e;
   ba::Sys S{};
   S.Hll = b->Hll; S.bl = b->bl; S.bp = b->bp; S.S = b->S; S.x = b->x; S.partial = b->partial;

@@ -215,15 +215,30 @@ __device__ __forceinline__ double pick4(const double (&a)[4], int t) {
 // symmetric (the same products summed in the same order for (a, b) and (b, a))
 __host__ __device__ constexpr int pk6(int a, int b) { return a * 6 - a * (a - 1) / 2 + (b - a); }
 
+// Hpl records: a point edge (positions [0, Ep)) 6 x 3 at 18 e (row stride 3), a line edge 6 x 4 at
+// 18 Ep + 24 (e - Ep) (row stride 4) -- a point record carries no zero column (144 instead of 192 bytes,
+// written once and read by the Schur chunks and the next update per trial)
+__device__ __forceinline__ int hpl_off(int Ep, int e) { return e < Ep ? 18 * e : 18 * Ep + 24 * (e - Ep); }
+// edge e's record as 6 x 4 (column 3 zero for a point edge); every load at a valid address, then selected
+__device__ __forceinline__ void load_hpl4(const double* H, int Ep, int e, double (&B)[24]) {
+  const int o = hpl_off(Ep, e), st = e < Ep ? 3 : 4;
+#pragma unroll
+  for (int r = 0; r < 6; r++)
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      const double v = H[o + r * st + (c < st ? c : st - 1)];
+      B[r * 4 + c] = c < st ? v : 0.0;
+    }
+}
+
 __device__ __forceinline__ int edim(int t) { return t == 0 ? 2 : t == 1 ? 3 : t == 2 ? 2 : 4; }
 
 // point edges only (t < 2), every index static: edge_error's point branch and its chi2 (info I)
-__device__ __forceinline__ double point_error(int t, const double* cam, const double* obs, const SE3& T,
-                                              const double* X, double (&e)[4]) {
-  double R[9], Xc[3];
-  q_to_R(T.q, R);
+__device__ __forceinline__ double point_error_R(int t, const double* cam, const double* obs, const double (&R)[9],
+                                                const double* tt, const double* X, double (&e)[4]) {
+  double Xc[3];
   mat3_vec(R, X, Xc);
-  for (int i = 0; i < 3; i++) Xc[i] += T.t[i];
+  for (int i = 0; i < 3; i++) Xc[i] += tt[i];
   const double iz = 1.0 / Xc[2];
   const double u = cam[0] * Xc[0] * iz + cam[2];
   const double v = cam[1] * Xc[1] * iz + cam[3];
@@ -236,6 +251,12 @@ __device__ __forceinline__ double point_error(int t, const double* cam, const do
   chi2 += e[1] * e[1];
   if (t == 1) chi2 += e[2] * e[2];
   return chi2 * 1.0;
+}
+__device__ __forceinline__ double point_error(int t, const double* cam, const double* obs, const SE3& T,
+                                              const double* X, double (&e)[4]) {
+  double R[9];
+  q_to_R(T.q, R);
+  return point_error_R(t, cam, obs, R, T.t, X, e);
 }
 
 // edge e's observation (type t): point edges [0, Ep) at stride 4 (u, v, u_r), line edges [Ep, E)
@@ -408,7 +429,6 @@ __global__ __launch_bounds__(256) void errors_kernel(Problem P, Lin L, Active A,
     } else {
       c = chi2;
     }
-    L.rho0[e] = c;
   }
   const double bsum = block_sum256(c, red);
   if (threadIdx.x == 0) {
@@ -527,7 +547,7 @@ __device__ __forceinline__ double contrib(int o, int rows, int ld, double w, con
   return w * s;
 }
 
-__device__ __forceinline__ void store_contrib(const Lin& L, int e, int o, double v, bool pose_opt) {
+__device__ __forceinline__ void store_contrib(const Lin& L, int Ep, int e, int o, double v, bool pose_opt) {
   if (o < 16) L.Hll[16 * e + o] = v;
   else if (o < 20) L.bl[4 * e + o - 16] = v;
   else if (!pose_opt) return;
@@ -536,7 +556,7 @@ __device__ __forceinline__ void store_contrib(const Lin& L, int e, int o, double
     if (b >= a) L.Hpp[21 * e + pk6(a, b)] = v;
   }
   else if (o < 62) L.bp[6 * e + o - 56] = v;
-  else L.Hpl[24 * e + o - 62] = v;
+  else L.Hpl[hpl_off(Ep, e) + o - 62] = v;  // (line edges: 6 x 4)
 }
 
 __device__ __forceinline__ double edge_weight_of(const Problem& P, const Active& A, const double* er, int t) {
@@ -556,27 +576,22 @@ __device__ __forceinline__ double edge_weight(const Problem& P, const Lin& L, co
   return edge_weight_of(P, A, L.err + 4 * e, t);
 }
 
-// point edges: analytic Jacobians (g2o types_sba).  Mono edges carry a zero third
-// row, so every index below is a compile-time constant (register resident, no scratch).
-// Writes the pose-side records of edge e (when its pose is optimised) and accumulates
-// the landmark side (Hll 3x3, bl 3) into hl / bv.
-// point_edge_core: the operands in registers (pose T, camera, landmark, the edge's error er)
-__device__ __forceinline__ void point_edge_core(const Problem& P, const Lin& L, const Active& A, int e, int t,
-                                                bool pose_opt, const SE3& T, const double* cam, const double* Xg,
-                                                const double* er4, double (&hl)[9], double (&bv)[3]) {
+// point edges: analytic Jacobians (g2o types_sba, EdgeSE3ProjectXYZ / EdgeStereoSE3ProjectXYZ::linearizeOplus).
+// Mono edges carry a zero third row, so every index below is a compile-time constant (register resident, no
+// scratch).
+__device__ __forceinline__ void point_jac_R(int t, const double (&R)[9], const double* tt, const double* cam,
+                                            const double* Xg, double (&Jp)[3][6], double (&Jl)[3][3]) {
   const double fx = cam[0], fy = cam[1], bf = cam[4];
-  double R[9], Xc[3];
-  q_to_R(T.q, R);
+  double Xc[3];
   mat3_vec(R, Xg, Xc);
 #pragma unroll
-  for (int k = 0; k < 3; k++) Xc[k] += T.t[k];
+  for (int k = 0; k < 3; k++) Xc[k] += tt[k];
   const double x = Xc[0], y = Xc[1], z = Xc[2], iz = 1.0 / z, iz2 = iz * iz;
   const bool st = t == 1;
   const double D[3][3] = {{fx * iz, 0, -fx * x * iz2},
                           {0, fy * iz, -fy * y * iz2},
                           {st ? fx * iz : 0.0, 0, st ? -fx * x * iz2 + bf * iz2 : 0.0}};
   const double SX[9] = {0, -z, y, z, 0, -x, -y, x, 0};
-  double Jp[3][6], Jl[3][3];
 #pragma unroll
   for (int r = 0; r < 3; r++)
 #pragma unroll
@@ -591,6 +606,38 @@ __device__ __forceinline__ void point_edge_core(const Problem& P, const Lin& L, 
       Jp[r][3 + c] = -D[r][c]; // -D * I
       Jl[r][c] = -sl;          // -D * R
     }
+}
+__device__ __forceinline__ void point_jac(int t, const SE3& T, const double* cam, const double* Xg, double (&Jp)[3][6],
+                                          double (&Jl)[3][3]) {
+  double R[9];
+  q_to_R(T.q, R);
+  point_jac_R(t, R, T.t, cam, Xg, Jp, Jl);
+}
+
+// the pose block of one point edge: Hpp (upper triangle, pk6) = w Jp^T Jp, bp = -w Jp^T e
+__device__ __forceinline__ void point_pose_terms(const double (&Jp)[3][6], double w, const double (&er)[3],
+                                                 double (&Hp)[21], double (&bpv)[6]) {
+#pragma unroll
+  for (int a = 0; a < 6; a++) {
+#pragma unroll
+    for (int b = a; b < 6; b++) Hp[pk6(a, b)] = w * (Jp[0][a] * Jp[0][b] + Jp[1][a] * Jp[1][b] + Jp[2][a] * Jp[2][b]);
+    bpv[a] = -w * (Jp[0][a] * er[0] + Jp[1][a] * er[1] + Jp[2][a] * er[2]);
+  }
+}
+
+// Writes the pose-side records of point edge e (when its pose is optimised): Hpl, and -- only with PDIAG
+// (the first linearisation of an optimize(), read by computeLambdaInit's pose_diag) -- the six diagonal
+// entries of Hpp.  The pose block itself (Hpp, bp) is never stored for a point edge: the diagonal pose
+// pair's Schur chunk recomputes it from the state (point_pose_block), which costs less than the 216 bytes
+// per edge and trial of writing it and reading it back.  Accumulates the landmark side (Hll 3x3, bl 3) into
+// hl / bv.  The operands in registers (pose T, camera, landmark, the edge's error er).
+template <bool PDIAG>
+__device__ __forceinline__ void point_edge_core(const Problem& P, const Lin& L, const Active& A, int e, int t,
+                                                bool pose_opt, const SE3& T, const double* cam, const double* Xg,
+                                                const double* er4, double (&hl)[9], double (&bv)[3]) {
+  double Jp[3][6], Jl[3][3];
+  point_jac(t, T, cam, Xg, Jp, Jl);
+  const bool st = t == 1;
   const double w = edge_weight_of(P, A, er4, t);
   const double er[3] = {er4[0], er4[1], st ? er4[2] : 0.0};
 #pragma unroll
@@ -600,28 +647,50 @@ __device__ __forceinline__ void point_edge_core(const Problem& P, const Lin& L, 
 #pragma unroll
   for (int a = 0; a < 3; a++) bv[a] += -w * (Jl[0][a] * er[0] + Jl[1][a] * er[1] + Jl[2][a] * er[2]);
   if (!pose_opt) return;
-  double* Hpp = L.Hpp + 21 * e;
-  double* bp = L.bp + 6 * e;
-  double* Hpl = L.Hpl + 24 * e;
+  double* Hpl = L.Hpl + 18 * e;  // (hpl_off: a point edge)
 #pragma unroll
   for (int a = 0; a < 6; a++) {
+    if (PDIAG) L.Hpp[21 * e + pk6(a, a)] = w * (Jp[0][a] * Jp[0][a] + Jp[1][a] * Jp[1][a] + Jp[2][a] * Jp[2][a]);
 #pragma unroll
-    for (int b = a; b < 6; b++) Hpp[pk6(a, b)] = w * (Jp[0][a] * Jp[0][b] + Jp[1][a] * Jp[1][b] + Jp[2][a] * Jp[2][b]);
-    bp[a] = -w * (Jp[0][a] * er[0] + Jp[1][a] * er[1] + Jp[2][a] * er[2]);
-#pragma unroll
-    for (int b = 0; b < 3; b++) Hpl[a * 4 + b] = w * (Jp[0][a] * Jl[0][b] + Jp[1][a] * Jl[1][b] + Jp[2][a] * Jl[2][b]);
-    Hpl[a * 4 + 3] = 0.0;
+    for (int b = 0; b < 3; b++) Hpl[a * 3 + b] = w * (Jp[0][a] * Jl[0][b] + Jp[1][a] * Jl[1][b] + Jp[2][a] * Jl[2][b]);
   }
 }
 
-// an edge outside this phase (level 1 in the second optimize): exact-zero records
+// The pose block (Hpp upper triangle, bp) of a live point edge of type t on an optimised pose at the state
+// its records were linearised at (pose rotation R / translation tt, camera cam, observation ob, point Xg of
+// the current bank): the error, the robust weight and the pose Jacobian formed again, exactly as
+// point_edge_core's linearisation (same operations on the same operands).
+__device__ __forceinline__ void point_pose_block(const Problem& P, const Active& A, int t, const double* Rt,
+                                                 const double* cam, const double* ob, const double* Xg,
+                                                 double (&Hp)[21], double (&bpv)[6]) {
+  double R[9];
+#pragma unroll
+  for (int i = 0; i < 9; i++) R[i] = Rt[i];
+  const double* tt = Rt + 9;
+  double er4[4];
+  point_error_R(t, cam, ob, R, tt, Xg, er4);
+  double Jp[3][6], Jl[3][3];
+  point_jac_R(t, R, tt, cam, Xg, Jp, Jl);
+  const double w = edge_weight_of(P, A, er4, t);
+  const double er[3] = {er4[0], er4[1], t == 1 ? er4[2] : 0.0};
+  point_pose_terms(Jp, w, er, Hp, bpv);
+}
+
+// A diagonal pose pair's chunk: its pose (every e1 of its pairs is on it) and the cameras, for
+// point_pose_block; the cameras in the chunk wave's LDS
+struct DiagPose {
+  const double* pose;  // R (9, row-major) and t (3) of the pose
+  const double* cams;  // [ncam][5]
+};
+
+// (point edges: Hpl, and with PDIAG the Hpp diagonal pose_diag reads; see point_edge_core)
+template <bool PDIAG>
 __device__ __forceinline__ void zero_pose_records(const Lin& L, int e) {
+  if (PDIAG)
 #pragma unroll
-  for (int k = 0; k < 21; k++) L.Hpp[21 * e + k] = 0.0;
+    for (int k = 0; k < 6; k++) L.Hpp[21 * e + pk6(k, k)] = 0.0;
 #pragma unroll
-  for (int k = 0; k < 6; k++) L.bp[6 * e + k] = 0.0;
-#pragma unroll
-  for (int k = 0; k < 24; k++) L.Hpl[24 * e + k] = 0.0;
+  for (int k = 0; k < 18; k++) L.Hpl[18 * e + k] = 0.0;
 }
 
 // point edges: analytic Jacobians (g2o types_sba).  Mono edges carry a zero third
@@ -631,11 +700,11 @@ __device__ __forceinline__ void zero_pose_records(const Lin& L, int e) {
 __device__ __forceinline__ void point_edge(const Problem& P, const Lin& L, const Active& A, int e, bool pose_opt,
                                            const double* Tb, const double* Xg, double (&hl)[9], double (&bv)[3]) {
   if (A.elevel && A.elevel[e]) {  // outside this phase: exact-zero records, no contribution
-    if (pose_opt) zero_pose_records(L, e);
+    if (pose_opt) zero_pose_records<true>(L, e);
     return;
   }
   const int t = P.etype[e];
-  point_edge_core(P, L, A, e, t, pose_opt, load_T(Tb + 8 * P.epose[e]), P.cams + 5 * P.ecam[e], Xg, L.err + 4 * e, hl,
+  point_edge_core<true>(P, L, A, e, t, pose_opt, load_T(Tb + 8 * P.epose[e]), P.cams + 5 * P.ecam[e], Xg, L.err + 4 * e, hl,
                   bv);
 }
 
@@ -876,7 +945,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
       for (int k = A.lm_off[g] + j; k < A.lm_off[g + 1]; k += kGroup) {
         const int a = A.lm_pose[k];
         if (a < 0) continue;
-        const double* B = Lc->Hpl + 24 * k;
+        const double* B = Lc->Hpl + hpl_off(P.Ep, k);  // (a line edge: 6 x 4)
         const double* xp = S.x + 6 * a;
 #pragma unroll
         for (int q = 0; q < 4; q++) {
@@ -962,9 +1031,16 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
       double Lp[6];
       for (int k = 0; k < 6; k++) Lp[k] = SPEC ? cand[einfo_s[slot][3] - gb][k] : Lsh[slot][k];
       double Jp[24], Jl[16];
+#pragma unroll
+      for (int k = 0; k < 24; k++) Jp[k] = 0.0;
+#pragma unroll
+      for (int k = 0; k < 16; k++) Jl[k] = 0.0;
       line_jac_analytic(cam, T, Lp, obs, t == 3, Jp, Jl);
-      for (int k = 0; k < 4 * edim(t); k++) J[slot][24 + k] = Jl[k];
-      for (int k = 0; k < 6 * edim(t); k++) J[slot][k] = Jp[k];
+      // whole rows (static indices: no scratch); rows >= edim(t) are zero and never read
+#pragma unroll
+      for (int k = 0; k < 16; k++) J[slot][24 + k] = Jl[k];
+#pragma unroll
+      for (int k = 0; k < 24; k++) J[slot][k] = Jp[k];
       if (OWN_ERR) {
         double er[4] = {0, 0, 0, 0};
         edge_error(t, cam, obs, T, Lp, er);
@@ -1048,7 +1124,7 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
         __hip_atomic_store(o < 16 ? L.Hll + 16 * e + o : L.bl + 4 * e + o - 16, v, __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_AGENT);
     } else {
-      store_contrib(L, e, o, v, (einfo_s[slot][2] & 4) != 0);
+      store_contrib(L, P.Ep, e, o, v, (einfo_s[slot][2] & 4) != 0);
     }
   }
   if (!split) {  // whole landmarks: their blocks from this workgroup's records, CSR (slot) order
@@ -1378,7 +1454,7 @@ __device__ __forceinline__ double setup_landmark(const Problem& P, const Lin& L,
       if (!point) continue;  // line edges: the line workgroups
       const bool pose_opt = A.lm_pose[k] >= 0;
       if (lev) {  // outside this phase: exact-zero records, no cost, error kept
-        if (pose_opt) zero_pose_records(L, k);
+        if (pose_opt) zero_pose_records<true>(L, k);
         continue;
       }
       const int te = P.etype[k];
@@ -1393,9 +1469,8 @@ __device__ __forceinline__ double setup_landmark(const Problem& P, const Lin& L,
         double r1;
         huber(chi2, pick4(P.delta, te), cst, r1);
       }
-      L.rho0[k] = cst;
       chi += cst;
-      point_edge_core(P, L, A, k, te, pose_opt, T, cm, Xg, er, hl, bv);
+      point_edge_core<true>(P, L, A, k, te, pose_opt, T, cm, Xg, er, hl, bv);
     }
   }
 #pragma unroll
@@ -1788,6 +1863,14 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
 // applies A_ik -= sum_l (X_il d_l)
 // X_kl from the panel in LDS, in registers.  The same operations in the same order as
 // schur_solve_kernel (bitwise the same factor); backward substitution, solution and LM scale as there.
+// lane l's double, read by every lane (l uniform)
+__device__ __forceinline__ double readlane64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
+  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
+  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
+}
+
 constexpr int kRegThreads = 512, kRegTiles = 5;  // (64 * 65 / 2 + 64 = 2144 tiles at n = 192) <= 512 x 5
 
 __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Active A, Sys S, int n, double lambda) {
@@ -1809,39 +1892,57 @@ __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Activ
   if (tid == 0) bad = 0;
   const int pose_a = tid < P.np ? A.pidx[tid] : -1;
   if (tid == 0) prof_stamp(S, 0);
-  const int nent = A.npairs * 42;
-  for (int q0 = tid; q0 < nent; q0 += 8 * kRegThreads) {
-    double v1[8], v2[8];
+  // Assembly.  The pose-pair sums (pairfin, pair-major, 48 per pair) are read coalesced -- 512 consecutive
+  // doubles per load instruction, every load of a batch in flight at once -- and scattered into the packed
+  // LDS triangle: entry (r, cc) of pair (pa, pb) is (6 pb + cc, 6 pa + r) for pa < pb and (6 pa + r, 6 pa + cc),
+  // cc <= r, on a diagonal pair (+ lambda on the diagonal); the rhs row n is z = bp - sum Y bl of the diagonal
+  // pairs.  The same values as schur_solve_kernel's assembly.  Then each thread reads its tiles from LDS.  (A
+  // per-thread gather of the tiles from pairfin was uncoalesced: 16.6 us at n = 174.)
+  const int nent = A.npairs * 48;
+  int* ptab = reinterpret_cast<int*>(ddg);  // pair -> (a, b) during the assembly (ddg / Ldg are formed later)
+  double* ybl = rdg;                        // sum Y bl of each pose during the assembly
+  constexpr int kAsmBatch = 25;             // 2 batches x 25 x 512 >= 528 pairs x 48 (K <= 32)
+  static_assert(2 * kAsmBatch * kRegThreads >= (kCholLdsMax / 6) * (kCholLdsMax / 6 + 1) / 2 * 48, "assembly batches");
+  {
+    double va[kAsmBatch];
 #pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int idx = q0 + u * kRegThreads;
-      const int pr = idx / 42, v = idx - 42 * pr;
-      v1[u] = idx < nent ? S.pairfin[48 * pr + v] : 0.0;
-      v2[u] = (idx < nent && v >= 36) ? S.pairfin[48 * pr + v + 6] : 0.0;
+    for (int u = 0; u < kAsmBatch; u++) va[u] = S.pairfin[min(tid + kRegThreads * u, nent - 1)];
+    for (int pr = tid; pr < A.npairs; pr += kRegThreads) {  // (while the first batch is in flight)
+      int a, b;
+      pair_of(pr, K, a, b);
+      ptab[2 * pr] = a;
+      ptab[2 * pr + 1] = b;
     }
-    if (*S.fail) return;
-#pragma unroll
-    for (int u = 0; u < 8; u++) {
-      const int idx = q0 + u * kRegThreads;
-      if (idx >= nent) break;
-      const int pr = idx / 42, v = idx - 42 * pr;
-      const int pa = A.pairs[2 * pr], pb = A.pairs[2 * pr + 1];  // (the host's pair table: no decode loop)
+    __syncthreads();
+    auto scatter = [&](int idx, double val) {
+      if (idx >= nent) return;
+      const int pr = idx / 48, v = idx - 48 * pr;
+      const int pa = ptab[2 * pr], pb = ptab[2 * pr + 1];
       if (v < 36) {
         const int r = v / 6, cc = v - 6 * r;
         if (pa == pb) {
-          if (cc <= r) Al[pk(6 * pa + r, 6 * pa + cc)] = v1[u] + (r == cc ? lambda : 0.0);
+          if (cc <= r) Al[pk(6 * pa + r, 6 * pa + cc)] = val + (r == cc ? lambda : 0.0);
         } else {
-          Al[pk(6 * pb + cc, 6 * pa + r)] = v1[u];
+          Al[pk(6 * pb + cc, 6 * pa + r)] = val;
         }
       } else if (pa == pb) {
-        const int r = v - 36;
-        bpl[6 * pa + r] = v1[u];
-        z[6 * pa + r] = v1[u] - v2[u];
+        if (v < 42) bpl[6 * pa + v - 36] = val;
+        else ybl[6 * pa + v - 42] = val;
       }
-    }
+    };
+#pragma unroll
+    for (int u = 0; u < kAsmBatch; u++) scatter(tid + kRegThreads * u, va[u]);
+#pragma unroll
+    for (int u = 0; u < kAsmBatch; u++) va[u] = S.pairfin[min(tid + kRegThreads * (u + kAsmBatch), nent - 1)];
+#pragma unroll
+    for (int u = 0; u < kAsmBatch; u++) scatter(tid + kRegThreads * (u + kAsmBatch), va[u]);
   }
+  if (*S.fail) return;  // uniform: a landmark block failed to invert (its flag is out with the sums)
   __syncthreads();
-  // this thread's tiles (column-major over the lower triangle + the rhs row tile R of each column)
+  for (int i = tid; i < n; i += kRegThreads) z[i] = bpl[i] - ybl[i];
+  __syncthreads();
+  // this thread's tiles (column-major over the lower triangle + the rhs row tile R of each column), from LDS
+  // at clamped addresses, then selected (entries above the diagonal or past row n are zero)
   int tr[kRegTiles], tc[kRegTiles];
   double T[kRegTiles][9];
   {
@@ -1857,7 +1958,9 @@ __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Activ
 #pragma unroll
       for (int e = 0; e < 9; e++) {
         const int i = 3 * tr[u] + e / 3, k = 3 * tc[u] + e % 3;
-        T[u][e] = (tc[u] >= 0 && i <= n && k <= i) ? Al[pk(i, k)] : 0.0;
+        const bool ok = tc[u] >= 0 && i <= n && k <= i;
+        T[u][e] = Al[ok ? pk(i, k) : 0];
+        T[u][e] = ok ? T[u][e] : 0.0;
       }
     }
   }
@@ -1919,7 +2022,7 @@ __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Activ
       for (int a = 0; a < 3; a++)
 #pragma unroll
         for (int l = 0; l < 6; l++) {
-          wi[a][l] = (i0 + a <= n) ? Al[pk(i0 + a, c0 + l)] * ddg[c0 + l] : 0.0;
+          wi[a][l] = Al[pk(min(i0 + a, n), c0 + l)] * ddg[c0 + l];  // (rows > n: entries never stored)
           xk[a][l] = Al[pk(k0 + a, c0 + l)];
         }
 #pragma unroll
@@ -1935,26 +2038,54 @@ __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Activ
   __syncthreads();
   if (wv != 0) return;
   if (tid == 0) prof_stamp(S, 2);
-  for (int s = K - 1; s >= 0; s--) {
-    const int c0 = 6 * s;
+  // backward substitution L^T x = z in wave 0 with z in registers (row i: lane i % 64, slot i / 64, n <= 192):
+  // the 6x6 block solve of pose step s on readlane'd values (uniform), then each lane's rows i < 6s; the
+  // panel entries L[6s + l][i] and the block's L of step s - 1 are requested one step ahead, so the
+  // dependent chain per step is registers only (was: two LDS round trips per step, 13 us at n = 174).  The
+  // same operations per element, in the same order, as schur_solve_kernel's loop.
+  double zr[3];
+#pragma unroll
+  for (int j = 0; j < 3; j++) zr[j] = z[min(lane + 64 * j, n - 1)];  // (rows >= n: never read or stored)
+  double Ac[3][6], Lc[15];
+  auto fetch = [&](int st, double (&Ad)[3][6], double (&Ld)[15]) {
+    const int c0 = 6 * st;
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+#pragma unroll
+      for (int l = 0; l < 6; l++) Ad[j][l] = Al[pk(c0 + l, min(lane + 64 * j, c0))];  // (i >= c0: not used)
+#pragma unroll
+    for (int q = 0; q < 15; q++) Ld[q] = Ldg[15 * st + q];
+  };
+  fetch(K - 1, Ac, Lc);
+  for (int st = K - 1; st >= 0; st--) {
+    const int c0 = 6 * st;
     double xb[6];
 #pragma unroll
     for (int k = 5; k >= 0; k--) {
-      double v = z[c0 + k];
+      const int i = c0 + k, sl = i >> 6;
+      double v = readlane64(sl == 0 ? zr[0] : sl == 1 ? zr[1] : zr[2], i & 63);
 #pragma unroll
-      for (int l = k + 1; l < 6; l++) v -= Ldg[15 * s + l * (l - 1) / 2 + k] * xb[l];
+      for (int l = k + 1; l < 6; l++) v -= Lc[l * (l - 1) / 2 + k] * xb[l];
       xb[k] = v;
     }
-    for (int i = lane; i < c0; i += 64) {
-      double v = z[i];
+    // branch-free: every row formed, then selected (rows >= c0 + 6 keep theirs, rows c0 .. c0 + 5 take x)
 #pragma unroll
-      for (int l = 0; l < 6; l++) v -= Al[pk(c0 + l, i)] * xb[l];
-      z[i] = v;
+    for (int j = 0; j < 3; j++) {
+      const int i = lane + 64 * j, d = i - c0;
+      double v = zr[j];
+#pragma unroll
+      for (int l = 0; l < 6; l++) v -= Ac[j][l] * xb[l];
+      double xs = xb[0];
+#pragma unroll
+      for (int l = 1; l < 6; l++) xs = d == l ? xb[l] : xs;
+      zr[j] = d < 0 ? v : (d < 6 ? xs : zr[j]);
     }
-    if (lane == 0)
-#pragma unroll
-      for (int k = 0; k < 6; k++) z[c0 + k] = xb[k];
+    if (st > 0) fetch(st - 1, Ac, Lc);  // the next step's panel entries and block L, behind this step's chain
   }
+#pragma unroll
+  for (int j = 0; j < 3; j++)
+    if (lane + 64 * j < n) z[lane + 64 * j] = zr[j];
+  wave_sync();
   for (int i = lane; i < n; i += 64) S.x[i] = z[i];
   if (tid == 0) prof_stamp(S, 3);
   double sc = 0;
@@ -1981,12 +2112,6 @@ __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Activ
 // ---------------------------------------------------------------------------
 constexpr int kWaveSolveMaxK = 10;
 
-__device__ __forceinline__ double readlane64(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const unsigned lo = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)b, l);
-  const unsigned hi = (unsigned)__builtin_amdgcn_readlane((int)(unsigned)(b >> 32), l);
-  return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
-}
 
 struct WaveSolveLds {
   double W[2][64][6];  // the panel's unscaled column entries w_ij of row i, double-buffered by block parity
@@ -2276,7 +2401,7 @@ __global__ __launch_bounds__(64) void schur_wave_kernel(Problem P, Active A, Sys
 }
 
 // one edge pair's Schur terms with D = (Hll_g + lambda I)^-1, landmark dimension LD (3: points, 4: lines
-// or a mixed range; records of stride 4, the 4th row / column of a point is zero): Y = Hpl_e1 D,
+// or a mixed range; 6 x 4 operands, the 4th column of a point's Hpl is zero): Y = Hpl_e1 D,
 // acc -= Y Hpl_e2^T; diag (e1 == e2) adds Hpp_e1, bp_e1 and Y bl_g.  LOWER (a diagonal pose pair):
 // only the block's lower triangle (cc <= r) -- the only part any solver reads of a diagonal block.
 // Same products in the same order as the zero-padded 4-dim form.
@@ -2332,8 +2457,9 @@ struct PairOps {
 template <int LD, bool LOWER>
 __device__ __forceinline__ void load_pair(const Lin& L, const Active& A, const Sys& S, int nq, int4 q,
                                           PairOps<LD>& o) {
+  static_assert(!LOWER && LD == 3, "off-diagonal pose pairs of point ranges only (chunk_loop takes the others)");
   const int e1 = q.x, e2 = q.y, g = q.z;
-  o.diag = LOWER && e1 == e2;
+  o.diag = false;
   o.live = !(A.elevel && (A.elevel[e1] | A.elevel[e2]));  // else zero records: no contribution
   const double* dg = S.Hll + 16 * g;  // the landmark block (inverted in use_pair)
 #pragma unroll
@@ -2341,22 +2467,10 @@ __device__ __forceinline__ void load_pair(const Lin& L, const Active& A, const S
 #pragma unroll
   for (int r = 0; r < 6; r++)
 #pragma unroll
-    for (int c = 0; c < LD; c++) o.H1[r * LD + c] = L.Hpl[24 * e1 + r * 4 + c];
-  if (o.diag) {
-#pragma unroll
-    for (int i = 0; i < 21; i++) o.Hp[i] = L.Hpp[21 * e1 + i];
-#pragma unroll
-    for (int i = 0; i < 6; i++) o.bpv[i] = L.bp[6 * e1 + i];
-#pragma unroll
-    for (int i = 0; i < LD; i++) o.blv[i] = S.bl[4 * g + i];
-#pragma unroll
-    for (int i = 0; i < 6 * LD; i++) o.H2[i] = o.H1[i];  // e2 == e1: one schur_pair call site below
-  } else {
-#pragma unroll
-    for (int r = 0; r < 6; r++)
-#pragma unroll
-      for (int c = 0; c < LD; c++) o.H2[r * LD + c] = L.Hpl[24 * e2 + r * 4 + c];
-  }
+    for (int c = 0; c < LD; c++) {
+      o.H1[r * LD + c] = L.Hpl[18 * e1 + r * 3 + c];
+      o.H2[r * LD + c] = L.Hpl[18 * e2 + r * 3 + c];
+    }
   o.pt = g < nq;
 }
 
@@ -2378,8 +2492,9 @@ __device__ __forceinline__ void use_pair(const PairOps<LD>& o, double lambda, bo
 }
 
 template <int LD, bool LOWER>
-__device__ __forceinline__ void chunk_loop(const Lin& L, const Active& A, const Sys& S, int nq, int beg, int end,
-                                           int4 qn, double lambda, bool& bad, double (&acc)[48]) {
+__device__ __forceinline__ void chunk_loop(const Problem& P, const Lin& L, const Active& A, const Sys& S,
+                                           const DiagPose& dp, int nq, int beg, int end, int4 qn, double lambda,
+                                           bool& bad, double (&acc)[48]) {
   const int lane = threadIdx.x & 63;
   for (int k = beg + lane; k < end; k += 64) {
     const int4 q = qn;
@@ -2397,26 +2512,29 @@ __device__ __forceinline__ void chunk_loop(const Lin& L, const Active& A, const 
       asm volatile("" ::: "memory");
       if (live && e1 == e2) {  // the edge with itself: H1 twice, + Hp / bp / Y bl
         double H1[24], Hp[21], bpv[6], blv[4];
-#pragma unroll
-        for (int r = 0; r < 6; r++)
-#pragma unroll
-          for (int c = 0; c < 4; c++) H1[r * 4 + c] = L.Hpl[24 * e1 + r * 4 + c];
-#pragma unroll
-        for (int i = 0; i < 21; i++) Hp[i] = L.Hpp[21 * e1 + i];
-#pragma unroll
-        for (int i = 0; i < 6; i++) bpv[i] = L.bp[6 * e1 + i];
+        // a point edge's pose block from the state (point_pose_block; its operands requested with H1 at
+        // clamped addresses), a line edge's from its records
+        const bool pt = g < nq;
+        const int te = P.etype[e1], ci = P.ecam[e1];
+        const double* obp = pt ? P.eobs + 4 * e1 : P.eobs;
+        const double* xgp = pt ? P.X + 3 * g : P.cams;
+        const double ob[3] = {obp[0], obp[1], obp[2]}, Xg[3] = {xgp[0], xgp[1], xgp[2]};
+        load_hpl4(L.Hpl, P.Ep, e1, H1);
 #pragma unroll
         for (int i = 0; i < 4; i++) blv[i] = S.bl[4 * g + i];
+        if (pt) {
+          point_pose_block(P, A, te, dp.pose, dp.cams + 5 * ci, ob, Xg, Hp, bpv);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 21; i++) Hp[i] = L.Hpp[21 * e1 + i];
+#pragma unroll
+          for (int i = 0; i < 6; i++) bpv[i] = L.bp[6 * e1 + i];
+        }
         schur_pair<LD, LOWER>(H1, H1, true, Hp, bpv, blv, D, acc);
       } else if (live) {  // two edges of one landmark on the same pose (rare)
         double H1[24], H2[24], Hp[21], bpv[6], blv[4];
-#pragma unroll
-        for (int r = 0; r < 6; r++)
-#pragma unroll
-          for (int c = 0; c < 4; c++) {
-            H1[r * 4 + c] = L.Hpl[24 * e1 + r * 4 + c];
-            H2[r * 4 + c] = L.Hpl[24 * e2 + r * 4 + c];
-          }
+        load_hpl4(L.Hpl, P.Ep, e1, H1);
+        load_hpl4(L.Hpl, P.Ep, e2, H2);
         schur_pair<LD, LOWER>(H1, H2, false, Hp, bpv, blv, D, acc);
       }
     } else if constexpr (LD == 4) {  // off-diagonal pose pairs over line ranges: the inverse first as well
@@ -2429,45 +2547,43 @@ __device__ __forceinline__ void chunk_loop(const Lin& L, const Active& A, const 
       asm volatile("" ::: "memory");
       if (live) {
         double H1[24], H2[24], Hp[21], bpv[6], blv[4];
-#pragma unroll
-        for (int r = 0; r < 6; r++)
-#pragma unroll
-          for (int c = 0; c < 4; c++) {
-            H1[r * 4 + c] = L.Hpl[24 * e1 + r * 4 + c];
-            H2[r * 4 + c] = L.Hpl[24 * e2 + r * 4 + c];
-          }
+        load_hpl4(L.Hpl, P.Ep, e1, H1);
+        load_hpl4(L.Hpl, P.Ep, e2, H2);
         schur_pair<LD, LOWER>(H1, H2, false, Hp, bpv, blv, D, acc);
       }
     } else if constexpr (LOWER) {  // diagonal pose pairs over point ranges: e1 == e2 without an H2 copy
+      // every operand in one round trip, unconditionally (the edge's pose block is formed from the state by
+      // point_pose_block: the pose and cameras in dp, the edge's type / camera / observation and the point
+      // requested here with the records)
       const int e1 = q.x, e2 = q.y, g = q.z;
       const bool live = !(A.elevel && (A.elevel[e1] | A.elevel[e2]));
-      double Hd[9], D[9], H1[18], Hp[21], bpv[6], blv[3];
+      double Hd[9], D[9], H1[18], Hp[21], bpv[6], blv[3], ob[3], Xg[3];
 #pragma unroll
       for (int i = 0; i < 9; i++) Hd[i] = S.Hll[16 * g + i];
 #pragma unroll
       for (int r = 0; r < 6; r++)
 #pragma unroll
-        for (int c = 0; c < 3; c++) H1[r * 3 + c] = L.Hpl[24 * e1 + r * 4 + c];
-      if (e1 == e2) {
+        for (int c = 0; c < 3; c++) H1[r * 3 + c] = L.Hpl[18 * e1 + r * 3 + c];
+      const int te = P.etype[e1], ci = P.ecam[e1];
 #pragma unroll
-        for (int i = 0; i < 21; i++) Hp[i] = L.Hpp[21 * e1 + i];
-#pragma unroll
-        for (int i = 0; i < 6; i++) bpv[i] = L.bp[6 * e1 + i];
-#pragma unroll
-        for (int i = 0; i < 3; i++) blv[i] = S.bl[4 * g + i];
+      for (int i = 0; i < 3; i++) {
+        blv[i] = S.bl[4 * g + i];
+        ob[i] = P.eobs[4 * e1 + i];
+        Xg[i] = P.X[3 * g + i];
       }
       if (live) {
 #pragma unroll
         for (int i = 0; i < 9; i++) Hd[i] += (i % 4 == 0) ? lambda : 0.0;
         bad |= !small_inv<3>(Hd, D);
         if (e1 == e2) {
+          point_pose_block(P, A, te, dp.pose, dp.cams + 5 * ci, ob, Xg, Hp, bpv);
           schur_pair<LD, LOWER>(H1, H1, true, Hp, bpv, blv, D, acc);
         } else {
           double H2[18];
 #pragma unroll
           for (int r = 0; r < 6; r++)
 #pragma unroll
-            for (int c = 0; c < 3; c++) H2[r * 3 + c] = L.Hpl[24 * e2 + r * 4 + c];
+            for (int c = 0; c < 3; c++) H2[r * 3 + c] = L.Hpl[18 * e2 + r * 3 + c];
           schur_pair<LD, LOWER>(H1, H2, false, Hp, bpv, blv, D, acc);
         }
       }
@@ -2524,13 +2640,32 @@ __device__ __forceinline__ bool chunk_wave(const Problem& P, const Lin& L, const
   // a range of point landmarks only
   // (all but the last range or two) takes the 3-dim loops, off-diagonal pose pairs without the e1 == e2 terms
   const bool pts = (lb + 1) * A.lmchunk <= P.nq;
-  const bool dpp = A.pairs[2 * pr] == A.pairs[2 * pr + 1];
+  const int pa = A.pairs[2 * pr];
+  const bool dpp = pa == A.pairs[2 * pr + 1];
+  DiagPose dp;
+  if (dpp) {  // a diagonal pose pair: its pose's rotation / translation and the cameras, in this wave's LDS
+    const unsigned long long m = __ballot(lane < P.np && A.pidx[lane] == pa);
+    if (lane == 0) {
+      const SE3 T = load_T(P.T + 8 * (__ffsll((long long)m) - 1));
+      double R[9];
+      q_to_R(T.q, R);
+#pragma unroll
+      for (int i = 0; i < 9; i++) red[i] = R[i];
+#pragma unroll
+      for (int i = 0; i < 3; i++) red[9 + i] = T.t[i];
+    }
+    for (int i = lane; i < 5 * P.ncam; i += 64) red[12 + i] = P.cams[i];
+    dp.pose = red;
+    dp.cams = red + 12;
+    wave_sync();
+  }
   bool bad = false;
-  if (pts && !dpp) chunk_loop<3, false>(L, A, S, P.nq, beg, end, cs.q0, lambda, bad, acc);
-  else if (pts) chunk_loop<3, true>(L, A, S, P.nq, beg, end, cs.q0, lambda, bad, acc);
-  else if (!dpp) chunk_loop<4, false>(L, A, S, P.nq, beg, end, cs.q0, lambda, bad, acc);
-  else chunk_loop<4, true>(L, A, S, P.nq, beg, end, cs.q0, lambda, bad, acc);
+  if (pts && !dpp) chunk_loop<3, false>(P, L, A, S, dp, P.nq, beg, end, cs.q0, lambda, bad, acc);
+  else if (pts) chunk_loop<3, true>(P, L, A, S, dp, P.nq, beg, end, cs.q0, lambda, bad, acc);
+  else if (!dpp) chunk_loop<4, false>(P, L, A, S, dp, P.nq, beg, end, cs.q0, lambda, bad, acc);
+  else chunk_loop<4, true>(P, L, A, S, dp, P.nq, beg, end, cs.q0, lambda, bad, acc);
   if (bad) atomicOr(S.fail, 1);
+  wave_sync();  // (the cameras' LDS reads before the transpose below overwrites them)
   if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c + 1);
 #pragma unroll
   for (int v = 0; v < 48; v++) red[lane * 49 + v] = acc[v];
@@ -2597,9 +2732,9 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
     LmView v;
     if (!lm_view(S, v)) return;
     lambda = v.lambda;
-    if (v.cur) {
+    if (v.cur) {  // (the state too: the diagonal chunks form their point edges' pose blocks from it)
       bank_lin(L, Ls, S, Ss);
-      if (N > 0) bank_state(P);
+      bank_state(P);
     }
   }
   if (!chunk_wave(P, L, A, S, lambda, cs, smem, N > 0)) return;
@@ -2713,7 +2848,8 @@ __global__ __launch_bounds__(256) void update_kernel(Problem P, Lin L, Active A,
         }
 #pragma unroll
         for (int u = 0; u < 4; u++) {
-          const double* B = L.Hpl + 24 * es[u];
+          double B[24];
+          load_hpl4(L.Hpl, P.Ep, es[u], B);
           const double* xp = S.x + 6 * max(as[u], 0);
 #pragma unroll
           for (int j = 0; j < 4; j++) {
@@ -2865,8 +3001,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     pf = P.epose[kf];
     cf = P.ecam[kf];
     lvf = A.elevel ? A.elevel[kf] : 0;
-#pragma unroll
-    for (int q = 0; q < 24; q++) Bf[q] = L.Hpl[24 * kf + q];
+    load_hpl4(L.Hpl, P.Ep, kf, Bf);
     const double* o = obs_of(P, kf, point ? 0 : 2);
 #pragma unroll
     for (int q = 0; q < 8; q++) of[q] = (q < 3 || !point) ? o[q] : 0.0;
@@ -2902,7 +3037,8 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     for (int k = kf + kGroup; k < k1; k += kGroup) {
       const int a = A.lm_pose[k];
       if (a < 0) continue;
-      const double* B = L.Hpl + 24 * k;
+      double B[24];
+      load_hpl4(L.Hpl, P.Ep, k, B);
       const double* xp = sx + 6 * a;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
@@ -2956,7 +3092,7 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
     // robust cost of the landmark's edges at the candidate (+ the point edges' linearisation)
     auto edge_cost = [&](int k, int te, int pose, int cam, int lev, const double (&ob)[8], int a) {
       if (lev) {
-        if (lin_pts && a >= 0) zero_pose_records(Ls, k);
+        if (lin_pts && a >= 0) zero_pose_records<false>(Ls, k);
         return;
       }
       const SE3 T = load_T(sT + 8 * pose);
@@ -2980,9 +3116,8 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
         double r1;
         huber(chi2, pick4(P.delta, te), cst, r1);
       }
-      L.rho0[k] = cst;
       chi += cst;
-      if (lin_pts) point_edge_core(P, Ls, A, k, te, a >= 0, T, cm, lm, er, hl, bv);
+      if (lin_pts) point_edge_core<false>(P, Ls, A, k, te, a >= 0, T, cm, lm, er, hl, bv);
     };
     if (has) edge_cost(kf, tf, pf, cf, lvf, of, af);
     for (int k = kf + kGroup; k < k1; k += kGroup) {
@@ -3392,17 +3527,6 @@ hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, un
   hipLaunchKernelGGL(update_errors_kernel<true>, dim3(nbu + nbl), dim3(256), 0, s, P, L, A, S, 0.0, seq, spec.Ls,
                      spec.Ss, nbu);
   if (ev) (void)hipEventRecord(ev[2], s);
-  return hipGetLastError();
-}
-
-__global__ __launch_bounds__(256) void upload_kernel(uint4* dst, const uint4* src, size_t n) {
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] = src[i];
-}
-
-hipError_t upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t s) {
-  const size_t n = bytes / 16;
-  if (n) hipLaunchKernelGGL(upload_kernel, dim3((unsigned)std::min<size_t>((n + 255) / 256, 1024)), dim3(256), 0, s,
-                           static_cast<uint4*>(dst), static_cast<const uint4*>(src_mapped), n);
   return hipGetLastError();
 }
 

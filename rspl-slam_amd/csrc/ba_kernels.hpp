@@ -35,12 +35,13 @@ struct Problem {
 
 struct Lin {             // per-edge linearisation records (indexed by edge id)
   double* err;           // [E][4] last computed error
-  double* rho0;          // [E] robust chi2 (or chi2)
-  double* Hpp;           // [E][21] upper triangle, row-major (pk6)
-  double* bp;            // [E][6]
+  double* Hpp;           // [E][21] upper triangle, row-major (pk6): line edges; a point edge's pose block is
+                         //   formed again by the diagonal Schur chunk (point_pose_block), only its diagonal
+                         //   is written by the first linearisation of an optimize() (computeLambdaInit)
+  double* bp;            // [E][6] line edges
   double* Hll;           // [E][16]
   double* bl;            // [E][4]
-  double* Hpl;           // [E][24]  6 x 4 (row stride 4; column 3 is zero for points)
+  double* Hpl;           // point edge e < Ep: 6 x 3 at 18 e; line edge: 6 x 4 at 18 Ep + 24 (e - Ep) (hpl_off)
 };
 
 struct Active {          // active structure of one optimize() phase
@@ -151,7 +152,7 @@ int setup_pdg_len(const Active& A);
 // speculative linearisation of a trial's candidate into a spare record set, fused into the
 // trial's last kernel (fast path only)
 struct Spec {
-  Lin Ls;            // spare edge records (err / rho0 shared with the current set)
+  Lin Ls;            // spare edge records (err shared with the current set)
   Sys Ss;            // spare landmark blocks Hll / bl
 };
 // one LM trial: Schur complement, Cholesky, back-substitution + candidate state, its cost;
@@ -171,9 +172,6 @@ hipError_t build_pairs(const Active& A, int* pp_cnt, int* pp_off, int4* pp, hipS
 hipError_t landmark_active(const Active& A, const uint8_t* level, uint8_t* lm_act, hipStream_t s);
 hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8_t* inlier, int final_pass,
                     hipStream_t s);
-// the call's upload as a kernel: bytes (a multiple of 16) from host-mapped pinned memory (its device
-// pointer) into device memory, 16-byte loads over the link (no copy engine)
-hipError_t upload(void* dst, const void* src_mapped, size_t bytes, hipStream_t s);
 // final inlier flags + T / X / L into host-mapped memory, then the mailbox post of seq
 hipError_t finish(const Problem& P, const Lin& L, int E, const int* gmap, uint8_t* inl, double* Th, double* Xh,
                   double* Lh, Sys& S, unsigned long long seq, hipStream_t s);

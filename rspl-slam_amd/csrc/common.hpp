@@ -141,6 +141,10 @@ struct Tensor {
   std::vector<float> data;
 };
 int load_blob(const char* path, std::vector<Tensor>& out);
+
+// bytes from host-mapped pinned memory (src_mapped: its device pointer) into device memory by a copy
+// kernel on stream s (copy_kernels.hip)
+hipError_t upload_mapped(void* dst, const void* src_mapped, size_t bytes, hipStream_t s);
 const Tensor* find(const std::vector<Tensor>& ts, const std::string& name, int64_t numel);
 
 }  // namespace rspl

@@ -23,7 +23,8 @@ struct rspl_frame {
   uint8_t *level = nullptr, *inl = nullptr;
   double* err = nullptr;
   // pinned upload staging (descs | edges | inlier-in), mirrors the device layout
-  char* stage = nullptr;
+  char* stage = nullptr;      // pinned, host-mapped staging of the upload region
+  char* stage_dev = nullptr;  // its device pointer (the upload kernel reads it)
   // host-mapped results
   frame::Out* out = nullptr;
   frame::Out* out_dev = nullptr;
@@ -99,7 +100,8 @@ extern "C" int rspl_frame_create(const rspl_frame_config* cfg, rspl_frame** out)
   h->level = h->arena.take<uint8_t>(E);
   h->inl = h->arena.take<uint8_t>(E);
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipHostMalloc((void**)&h->stage, lay.bytes) != hipSuccess ||
+      hipHostMalloc((void**)&h->stage, lay.bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&h->stage_dev, h->stage, 0) != hipSuccess ||
       hipHostMalloc((void**)&h->out, sizeof(frame::Out) * B, hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer((void**)&h->out_dev, h->out, 0) != hipSuccess ||
@@ -192,7 +194,7 @@ extern "C" int rspl_frame_optimize(rspl_frame* h, const rspl_frame_problem* prob
   }
   hipStream_t st = h->stream;
   // staging mirrors the upload region: descs + edges (+ gap) + inlier flags in one copy
-  RSPL_HIP(hipMemcpyAsync(h->up, sg, lay.bytes, hipMemcpyHostToDevice, st));
+  RSPL_HIP(upload_mapped(h->up, h->stage_dev, lay.bytes, st));
   frame::Args a{};
   a.frames = reinterpret_cast<const frame::Desc*>(h->up + lay.desc);
   a.edges = reinterpret_cast<const frame::Edge*>(h->up + lay.edges);

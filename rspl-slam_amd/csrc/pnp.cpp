@@ -19,7 +19,8 @@ struct rspl_pnp {
   hipStream_t stream = nullptr;
   char* dev = nullptr;   // upload region: descs | points | keypoints | subsets
   size_t dev_cap = 0;
-  char* stage = nullptr; // pinned staging, same layout
+  char* stage = nullptr; // pinned, host-mapped staging, same layout
+  char* stage_dev = nullptr;  // its device pointer (the upload kernel reads it)
   size_t stage_cap = 0;
   pnp::Out* out = nullptr;
   pnp::Out* out_dev = nullptr;
@@ -27,6 +28,7 @@ struct rspl_pnp {
   uint8_t* inl_dev = nullptr;
   double* hyp = nullptr;  // per-hypothesis poses and inlier counts (device)
   int* hcnt = nullptr;
+  unsigned long long* prof = nullptr;  // RSPL_PNP_PROF: in-kernel phase stamps
   std::vector<int> last_iters;  // hypotheses per frame of the last solve
 };
 
@@ -79,7 +81,9 @@ extern "C" int rspl_pnp_create(const rspl_pnp_config* cfg, rspl_pnp** out) {
   const Layout lay(cfg->max_batch, std::max(cfg->max_points, 1), (size_t)cfg->max_batch * pnp::kMaxIters);
   h->dev_cap = h->stage_cap = lay.bytes;
   if (hipStreamCreateWithFlags(&h->stream, hipStreamNonBlocking) != hipSuccess ||
-      hipMalloc((void**)&h->dev, lay.bytes) != hipSuccess || hipHostMalloc((void**)&h->stage, lay.bytes) != hipSuccess ||
+      hipMalloc((void**)&h->dev, lay.bytes) != hipSuccess ||
+      hipHostMalloc((void**)&h->stage, lay.bytes, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer((void**)&h->stage_dev, h->stage, 0) != hipSuccess ||
       hipHostMalloc((void**)&h->out, sizeof(pnp::Out) * cfg->max_batch, hipHostMallocMapped | hipHostMallocCoherent) !=
           hipSuccess ||
       hipHostGetDevicePointer((void**)&h->out_dev, h->out, 0) != hipSuccess ||
@@ -105,6 +109,7 @@ extern "C" void rspl_pnp_destroy(rspl_pnp* h) {
   if (h->inl) (void)hipHostFree(h->inl);
   if (h->hyp) (void)hipFree(h->hyp);
   if (h->hcnt) (void)hipFree(h->hcnt);
+  if (h->prof) (void)hipFree(h->prof);
   if (h->stream) (void)hipStreamDestroy(h->stream);
   delete h;
 }
@@ -153,7 +158,7 @@ extern "C" int rspl_pnp_solve(rspl_pnp* h, const rspl_pnp_problem* probs, int ba
     s0 += d.iters;
   }
   hipStream_t st = h->stream;
-  RSPL_HIP(hipMemcpyAsync(h->dev, sg, lay.bytes, hipMemcpyHostToDevice, st));
+  RSPL_HIP(upload_mapped(h->dev, h->stage_dev, lay.bytes, st));
   pnp::Args a{};
   a.frames = reinterpret_cast<const pnp::Desc*>(h->dev + lay.desc);
   a.pts = reinterpret_cast<const double*>(h->dev + lay.pts);
@@ -163,8 +168,24 @@ extern "C" int rspl_pnp_solve(rspl_pnp* h, const rspl_pnp_problem* probs, int ba
   a.out = h->out_dev;
   a.hyp = h->hyp;
   a.hcnt = h->hcnt;
+  static const bool prof = getenv("RSPL_PNP_PROF") != nullptr;
+  if (prof && !h->prof) {
+    RSPL_HIP(hipMalloc((void**)&h->prof, sizeof(unsigned long long) * 16));
+    RSPL_HIP(hipMemset(h->prof, 0, sizeof(unsigned long long) * 16));
+  }
+  a.prof = prof ? h->prof : nullptr;
   RSPL_HIP(pnp::solve(a, batch, max_iters, st));
   RSPL_HIP(hipStreamSynchronize(st));
+  if (prof) {  // in-kernel phases of frame 0 (us): hypothesis 0's EPnP + count, then the acceptance / refinement
+    unsigned long long t[16];
+    RSPL_HIP(hipMemcpy(t, h->prof, sizeof(t), hipMemcpyDeviceToHost));
+    auto us = [&](int i, int j) { return t[i] && t[j] ? ((double)t[j] - (double)t[i]) / 100.0 : -1.0; };
+    fprintf(stderr,
+            "pnp_prof us: ctrl %.1f bary+MtM %.1f jacobi12 %.1f L+betas %.1f gn %.1f Rt %.1f count %.1f | hyp->final %.1f "
+            "accept+inl %.1f refine %.1f\n",
+            us(0, 1), us(1, 2), us(2, 3), us(3, 4), us(4, 5), us(5, 6), us(6, 7), us(7, 8), us(8, 9), us(9, 10));
+    RSPL_HIP(hipMemset(h->prof, 0, sizeof(unsigned long long) * 16));
+  }
   for (int b = 0; b < batch; b++) {
     const pnp::Out& o = h->out[b];
     rspl_pnp_result& r = res[b];

@@ -544,8 +544,11 @@ __device__ __forceinline__ double epnp_R_t(const Epnp& E, const double (&Vn)[4][
 }
 
 /* EPnP of one 5-point subset on one wave (every lane returns the same R, t): 0 on success */
+__device__ __forceinline__ void pstamp(unsigned long long* pf, int i) {
+  if (pf) pf[i] = wall_clock64();
+}
 __device__ int epnp_wave(const double* K4, const double (&pw)[3 * kN], const double (&uv)[2 * kN], WaveLds& w,
-                         int lane, double (&R)[9], double (&t)[3]) {
+                         int lane, double (&R)[9], double (&t)[3], unsigned long long* pf) {
   Epnp E;
   E.fu = K4[0]; E.fv = K4[1]; E.uc = K4[2]; E.vc = K4[3];
 #pragma unroll
@@ -553,6 +556,7 @@ __device__ int epnp_wave(const double* K4, const double (&pw)[3 * kN], const dou
 #pragma unroll
   for (int i = 0; i < 2 * kN; i++) E.us[i] = uv[i];
   epnp_control_points(E);
+  pstamp(pf, 1);
   if (epnp_barycentric(E)) return -1;  // uniform
   if (lane == 0)
 #pragma unroll
@@ -579,7 +583,9 @@ __device__ int epnp_wave(const double* K4, const double (&pw)[3 * kN], const dou
     w.A[0][e] = s;
   }
   wave_sync();
+  pstamp(pf, 2);
   jacobi12_wave(w, lane);
+  pstamp(pf, 3);
   const double(&Vn)[4][12] = w.Vn;  // LDS broadcast reads
   double L[60], rho[6];
   epnp_L(Vn, L);
@@ -593,8 +599,11 @@ __device__ int epnp_wave(const double* K4, const double (&pw)[3 * kN], const dou
   if (k == 1) betas_1(L, rho, be);
   else if (k == 2) betas_2(L, rho, be);
   else betas_3(L, rho, be);
+  pstamp(pf, 4);
   gauss_newton(L, rho, be);
+  pstamp(pf, 5);
   const double ek = epnp_R_t(E, Vn, be, Rk, tk);
+  pstamp(pf, 6);
   const double e1 = wave::rdlaned(ek, 0), e2 = wave::rdlaned(ek, 1), e3 = wave::rdlaned(ek, 2);
   int N = 1;
   if (e2 < e1) N = 2;
@@ -780,11 +789,14 @@ __global__ __launch_bounds__(256) void pnp_hyp_kernel(Args a) {
     for (int j = 0; j < 2; j++) su[2 * k + j] = uv[2 * s + j];
   }
   int cnt = -1;
-  if (epnp_wave(D.K, sp, su, wl[wv], lane, R, t) == 0) {
+  unsigned long long* pf = (a.prof && f == 0 && h == 0 && lane == 0) ? a.prof : nullptr;
+  pstamp(pf, 0);
+  if (epnp_wave(D.K, sp, su, wl[wv], lane, R, t, pf) == 0) {
     int c = 0;
     for (int i = lane; i < D.n; i += 64) c += reproj2(D.K, R, t, pw + 3 * i, uv + 2 * i) <= D.thr2;
     cnt = wave::wsum_int(c);
   }
+  pstamp(pf, 7);
   if (lane == 0) {
     double* hr = a.hyp + ((size_t)f * kMaxIters + h) * 12;
 #pragma unroll
@@ -798,6 +810,8 @@ __global__ __launch_bounds__(256) void pnp_hyp_kernel(Args a) {
 // stage 2: one wave per frame -- RANSAC's acceptance in hypothesis order, inliers, refinement
 __global__ __launch_bounds__(64) void pnp_final_kernel(Args a) {
   const int f = blockIdx.x, lane = threadIdx.x;
+  unsigned long long* pf = (a.prof && f == 0 && lane == 0) ? a.prof : nullptr;
+  pstamp(pf, 8);
   const Desc D = a.frames[f];
   const int n = D.n;
   const int* hc = a.hcnt + (size_t)f * kMaxIters;
@@ -840,7 +854,9 @@ __global__ __launch_bounds__(64) void pnp_final_kernel(Args a) {
     ninl += in;
   }
   ninl = wave::wsum_int(ninl);
+  pstamp(pf, 9);
   refine(D.K, n, pw, uv, inl, lane, R, t);
+  pstamp(pf, 10);
   if (lane == 0) {
     for (int i = 0; i < 3; i++)
       for (int j = 0; j < 3; j++) o->Rwc[3 * i + j] = R[3 * j + i];

@@ -32,6 +32,8 @@ struct Args {
   Out* out;               // [B] host-mapped
   double* hyp;            // [B][kMaxIters][12] hypothesis R (row-major) | t
   int* hcnt;              // [B][kMaxIters] inlier count, -1: the minimal solver failed
+  unsigned long long* prof;  // RSPL_PNP_PROF (null otherwise): wall_clock64 stamps of frame 0's hypothesis 0
+                             // [0, 8) and of its acceptance / refinement [8, 12)
 };
 
 // max_iters: the largest RANSAC iteration count of the batch (hypothesis grid width)
