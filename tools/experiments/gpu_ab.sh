@@ -1,6 +1,6 @@
 #!/bin/bash
 # Alternating A/B of the headline bench under environment variants (same box, same tree).
-# Usage: tools/gpu_ab.sh "A_ENV" "B_ENV" [rounds] [extra bench args]; each variant's line goes to
+# Usage: tools/experiments/gpu_ab.sh "A_ENV" "B_ENV" [rounds] [extra bench args]; each variant's line goes to
 # gpurun_out/ab_<i>_<A|B>.json and a summary (frames/s, ba:wall, lines) is printed.
 set -o pipefail
 A="$1"; B="$2"; N=${3:-2}; shift 3 2>/dev/null; EXTRA="$*"

@@ -29,5 +29,5 @@ PY
 done
 if [ -n "$BENCH_AB" ]; then
   set -- $LIBS
-  bash tools/gpu_ab.sh "RSPL_LIB=$1" "RSPL_LIB=$2" ${BENCH_AB} || exit 1
+  bash tools/experiments/gpu_ab.sh "RSPL_LIB=$1" "RSPL_LIB=$2" ${BENCH_AB} || exit 1
 fi
