@@ -609,8 +609,9 @@ def main():
         host_wait = {"lines": 0.0, "ba_queue": 0.0, "sp_calls": 0.0, "sg_calls": 0.0, "line_assoc_calls": 0.0,
                      "line_submit": 0.0}
         # the warmup steps run exactly the timed steps' code path, measurement included (stage timers, the BA's
-        # kernel timing, the line-association timers): the HIP runtime sets up timing events lazily, and the
-        # first timed call paid ~8 ms for it when the warmup ran without them (profiles/r05_bench_20step.json)
+        # kernel timing, the line-association timers), so no first-use cost lands in the timed region.  (The 7-10
+        # ms stall of the first timed BA calls that round 4's 20-step bench showed was the H2D hipMemcpyAsync, not
+        # this: fixed by the upload kernel, profiles/r05_bench_20step.json.)
         sp.profile(True)
         sg.profile(True)
         ba.kernel_timing(ktime_every)

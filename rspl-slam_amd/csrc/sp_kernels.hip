@@ -205,22 +205,47 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
 
   const int H = a.H, W = a.W, COUT = a.cout;
   const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
-  const int per_img = tiles_x * tiles_y;
-  const int bi = blockIdx.x / per_img;
-  const int t = blockIdx.x % per_img;
-  const int y0 = (t / tiles_x) * TH, x0 = (t % tiles_x) * TW;
+  const int per_img = tiles_x * tiles_y, ntiles = a.B * per_img;  // (a.B: set by the launcher)
   const int co0 = blockIdx.y * 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int ml = lane & 31, kl = lane >> 5;
 
-  if constexpr (FUSE1A) {
-    const uint8_t* img = a.img + (size_t)bi * a.img_pitch;
-    for (int i = tid; i < (TH + 4) * (TW + 4); i += 256) {
-      const int py = i / (TW + 4), px = i % (TW + 4);
-      const int y = y0 - 2 + py, x = x0 - 2 + px;
-      patch[i] = (y >= 0 && y < H && x >= 0 && x < W) ? a.lut[img[(size_t)y * a.img_stride + x]] : 0.f;
+  // FUSE1A (conv1): persistent -- a workgroup walks tiles blockIdx.x, + gridDim.x, ... with the conv1a
+  // weights staged once, and the next tile's image patch (2 pixels per thread, raw u8) fetched while the
+  // current tile's last stage runs on MFMA; every other layer: one tile per workgroup (grid = tiles)
+  constexpr int PP = FUSE1A ? ((TH + 4) * (TW + 4) + 255) / 256 : 1;
+  int pv[PP];  // the prefetched patch pixels: u8 value, -1 outside the image (zero padding)
+  auto load_patch = [&](int tile_) {
+    const int bi_ = tile_ / per_img, t_ = tile_ % per_img;
+    const int y0_ = (t_ / tiles_x) * TH, x0_ = (t_ % tiles_x) * TW;
+    const uint8_t* img = a.img + (size_t)bi_ * a.img_pitch;
+#pragma unroll
+    for (int r = 0; r < PP; r++) {
+      const int i = tid + 256 * r, py = i / (TW + 4), px = i % (TW + 4);
+      const int y = y0_ - 2 + py, x = x0_ - 2 + px;
+      pv[r] = (i < (TH + 4) * (TW + 4) && tile_ < ntiles && y >= 0 && y < H && x >= 0 && x < W)
+                  ? (int)img[(size_t)y * a.img_stride + x]
+                  : -1;
     }
+  };
+  if constexpr (FUSE1A) {
+    load_patch(blockIdx.x);
     for (int i = tid; i < 64 * 10; i += 256) w1a[i] = (i % 10 < 9) ? a.w1a[(i / 10) * 9 + i % 10] : a.b1a[i / 10];
+  }
+  constexpr int HALO8 = HY * HX * (HCK / 8), HPT = (HALO8 + 255) / 256;
+  half8 pw[9], ph[FUSE1A ? 1 : HPT];  // the next stage's weights / halo in flight (across tiles too)
+  for (int tile = blockIdx.x; tile < ntiles; tile += FUSE1A ? gridDim.x : ntiles) {
+  const int bi = tile / per_img;
+  const int t = tile % per_img;
+  const int y0 = (t / tiles_x) * TH, x0 = (t % tiles_x) * TW;
+  if constexpr (FUSE1A) {
+    // (the previous tile's readers of patch finished before its epilogue's barrier)
+#pragma unroll
+    for (int r = 0; r < PP; r++) {
+      const int i = tid + 256 * r;
+      // src/super_point.cpp:146-150 normalisation, (float)(u / 255.0) in double (= the host LUT)
+      if (i < (TH + 4) * (TW + 4)) patch[i] = pv[r] >= 0 ? (float)((double)pv[r] / 255.0) : 0.f;
+    }
   }
 
   floatx16 acc[MT][2];
@@ -234,8 +259,6 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
   // software pipeline over the input-channel stages: the next stage's weights (and halo, unless
   // conv1a computes it) are fetched into registers while the current stage's MFMAs run, and
   // written to LDS after the next barrier
-  constexpr int HALO8 = HY * HX * (HCK / 8), HPT = (HALO8 + 255) / 256;
-  half8 pw[9], ph[FUSE1A ? 1 : HPT];
   auto fetch = [&](int c0) {
 #pragma unroll
     for (int r = 0; r < 9; r++) {  // weights [9][64 co][32 ci]: 2304 half8, 9 per thread
@@ -257,7 +280,7 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
       }
     }
   };
-  fetch(0);
+  if (!FUSE1A || tile == (int)blockIdx.x) fetch(0);  // (FUSE1A: later tiles' first stage came with the last)
   for (int c0 = 0; c0 < CIN; c0 += HCK) {
     __syncthreads();
     if constexpr (FUSE1A) {
@@ -273,6 +296,11 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
         const int k = 8 * kl + j;
         bw[j] = (_Float16)(k <= 9 ? w1a[(c0 + ml) * 10 + k] : 0.f);
       }
+      // transposed product D[c][px] = W1a[c][k] P[k][px]: lane (px, kl) then holds channels
+      // 8 q + 4 kl + 0..3 of halo pixel px -- four 8-byte LDS stores per lane instead of sixteen
+      // 2-byte ones (the same products summed over the same k)
+      const int hx = ml;
+      const int x = x0 - 1 + hx;
       for (int hy = wv; hy < HY; hy += 4) {
         const int y = y0 - 1 + hy;
         half8 av;
@@ -280,21 +308,22 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
         for (int j = 0; j < 8; j++) {
           const int k = 8 * kl + j;
           float v = 0.f;
-          if (ml < HX) v = k < 9 ? patch[(hy + k / 3) * (TW + 4) + ml + k % 3] : (k == 9 ? 1.f : 0.f);
+          if (hx < HX) v = k < 9 ? patch[(hy + k / 3) * (TW + 4) + hx + k % 3] : (k == 9 ? 1.f : 0.f);
           av[j] = (_Float16)v;
         }
         floatx16 d;
 #pragma unroll
         for (int r = 0; r < 16; r++) d[r] = 0.f;
-        d = mfma16(av, bw, d);
-        const bool yin = y >= 0 && y < H;
+        d = mfma16(bw, av, d);
+        const bool in = y >= 0 && y < H && x >= 0 && x < W;
+        if (hx < HX) {
 #pragma unroll
-        for (int r = 0; r < 16; r++) {
-          const int hx = (r & 3) + 8 * (r >> 2) + 4 * kl;  // halo column of accumulator row r
-          if (hx < HX) {
-            const int x = x0 - 1 + hx;
-            const float v = (yin && x >= 0 && x < W) ? fmaxf(d[r], 0.f) : 0.f;
-            halo[(hy * HX + hx) * HCS + ml] = (_Float16)v;
+          for (int q = 0; q < 4; q++) {
+            typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+            half4 h4;
+#pragma unroll
+            for (int e = 0; e < 4; e++) h4[e] = (_Float16)(in ? fmaxf(d[4 * q + e], 0.f) : 0.f);
+            *reinterpret_cast<half4*>(&halo[(hy * HX + hx) * HCS + 8 * q + 4 * kl]) = h4;
           }
         }
       }
@@ -312,6 +341,10 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
     }
     __syncthreads();
     if (c0 + HCK < CIN) fetch(c0 + HCK);
+    else if (FUSE1A && tile + (int)gridDim.x < ntiles) {  // the next tile's first stage and image patch
+      fetch(0);
+      load_patch(tile + gridDim.x);
+    }
 #pragma unroll
     for (int kk = 0; kk < 9; kk++) {
       const int ky = kk / 3, kx = kk % 3;
@@ -362,7 +395,7 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
         *reinterpret_cast<half8*>(a.hout + (size_t)bi * H * W * COUT + ((size_t)y * W + x) * COUT + co0 + 8 * q) =
             *reinterpret_cast<const half8*>(&wts[px * OS + 8 * q]);
     }
-    return;
+    continue;
   }
   if constexpr (POOL && !OUT_F32) {
     // 2x2-pooled output tile (TH/2 x 8 pixels x 64 channels) staged through LDS the same way
@@ -394,7 +427,7 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
         *reinterpret_cast<half8*>(a.hout + (size_t)bi * H2 * W2 * COUT + ((size_t)py * W2 + pxx) * COUT + co0 + 8 * q) =
             *reinterpret_cast<const half8*>(&wts[px * OS + 8 * q]);
     }
-    return;
+    continue;
   }
 #pragma unroll
   for (int n = 0; n < 2; n++) {
@@ -435,6 +468,7 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
       }
     }
   }
+  }  // tile loop
 }
 
 // ---------------------------------------------------------------------------
@@ -1149,12 +1183,27 @@ hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hi
   return hipErrorInvalidValue;
 }
 
+// workgroups of the persistent conv1 (FUSE1A): two per CU (76 KB of LDS each)
+static int conv1_workgroups() {
+  static int n = 0;
+  if (!n) {
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || cus <= 0)
+      cus = 256;
+    n = 2 * cus;
+  }
+  return n;
+}
+
 template <int CIN, int TH, bool POOL, bool FUSE1A, bool OUT_F32>
 static hipError_t launch_conv_h(const ConvArgs& a, int B, hipStream_t s, hipEvent_t t0 = nullptr,
                                 hipEvent_t t1 = nullptr) {
   const int tiles = ((a.W + TW - 1) / TW) * ((a.H + TH - 1) / TH);
-  dim3 grid(B * tiles, a.cout / 64);
-  hipExtLaunchKernelGGL((conv3x3_h_kernel<CIN, TH, POOL, FUSE1A, OUT_F32>), grid, dim3(256), 0, s, t0, t1, 0, a);
+  ConvArgs b = a;
+  b.B = B;
+  dim3 grid(FUSE1A ? std::min(B * tiles, conv1_workgroups()) : B * tiles, a.cout / 64);
+  hipExtLaunchKernelGGL((conv3x3_h_kernel<CIN, TH, POOL, FUSE1A, OUT_F32>), grid, dim3(256), 0, s, t0, t1, 0, b);
   return hipGetLastError();
 }
 

@@ -12,6 +12,7 @@ struct ConvArgs {
   const float* bias;     // [Cout]
   float* out;            // NHWC [B][H(/2)][W(/2)][Cout]
   int H, W, cout;
+  int B;                 // images (set by the fp16 launcher: the persistent conv1 walks B x tiles)
   // conv1a fusion (conv1b only)
   const uint8_t* img;    // u8 images, row stride img_stride, image pitch img_pitch
   int img_stride;
