@@ -1854,14 +1854,14 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
 // ---------------------------------------------------------------------------
 // The same blocked LDL^T with the trailing matrix in REGISTERS (K > kWaveSolveMaxK: C5's 30-keyframe
 // window, n = 174): schur_solve_kernel's trailing update re-reads and rewrites the whole packed triangle
-// in LDS every pose step (29 steps x ~15k entries: LDS-bandwidth bound, ~4 us per step).  Here the lower
-// triangle (+ the bordered rhs row n) is cut into 3x3 tiles, column-major, dealt cyclically to 512 threads
-// (<= kRegTiles each); a tile lives in its owner's registers from the assembly to the step that factors
-// its block column.  Pose step s: the owners of tile columns 2s, 2s+1 write them to LDS; barrier; every wave
-// factors the 6x6 diagonal block (redundantly: no broadcast) and each thread forms one panel row (X = A L^-T
-// D^-1, into LDS as the factor's L, exactly as schur_solve_kernel); barrier; every owner of a trailing tile
-// applies A_ik -= sum_l (X_il d_l)
-// X_kl from the panel in LDS, in registers.  The same operations in the same order as
+// in LDS every pose step (29 steps x ~15k entries: LDS-bandwidth bound, ~4 us per step).  Here each of
+// 512 threads owns one 6x6 pose block of the lower triangle (or the rhs row's 6 entries of a block column),
+// held in registers from the assembly to the step that factors its block column.  Pose step s: the owners of
+// block column s write it to LDS; barrier; every wave factors the 6x6 diagonal block (redundantly: no
+// broadcast) and each thread forms one panel row (X = A L^-T D^-1, into LDS as the factor's L, exactly as
+// schur_solve_kernel); barrier; every owner of a trailing block applies A_ik -= sum_l (X_il d_l) X_kl,
+// l ascending, from the panel in LDS: 72 panel reads per block and step (3x3 tiles needed 36 per 9
+// entries: the trailing update was LDS-bound).  The same operations in the same order per element as
 // schur_solve_kernel (bitwise the same factor); backward substitution, solution and LM scale as there.
 // lane l's double, read by every lane (l uniform)
 __device__ __forceinline__ double readlane64(double v, int l) {
@@ -1871,7 +1871,9 @@ __device__ __forceinline__ double readlane64(double v, int l) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-constexpr int kRegThreads = 512, kRegTiles = 5;  // (64 * 65 / 2 + 64 = 2144 tiles at n = 192) <= 512 x 5
+constexpr int kRegThreads = 512;  // one pose block per thread: K (K + 3) / 2 <= 512 blocks, K <= 30 (n <= 180);
+                                  // larger windows take schur_solve_kernel (launch_lds_solve)
+constexpr int kRegMaxK = 30;
 
 __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Active A, Sys S, int n, double lambda) {
   extern __shared__ double Al[];
@@ -1882,7 +1884,7 @@ __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Activ
     lambda = v.lambda;
     if (v.cur) bank_state(P);
   }
-  const int K = n / 6, R = n / 3;  // R: the tile row of the rhs row n
+  const int K = n / 6;
   double* z = Al + pk(n, 0);
   double* rdg = Al + pk(n + 1, 0);
   double* ddg = rdg + n;
@@ -1901,8 +1903,8 @@ __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Activ
   const int nent = A.npairs * 48;
   int* ptab = reinterpret_cast<int*>(ddg);  // pair -> (a, b) during the assembly (ddg / Ldg are formed later)
   double* ybl = rdg;                        // sum Y bl of each pose during the assembly
-  constexpr int kAsmBatch = 25;             // 2 batches x 25 x 512 >= 528 pairs x 48 (K <= 32)
-  static_assert(2 * kAsmBatch * kRegThreads >= (kCholLdsMax / 6) * (kCholLdsMax / 6 + 1) / 2 * 48, "assembly batches");
+  constexpr int kAsmBatch = 22;             // 2 batches x 22 x 512 >= 465 pairs x 48 (K <= 30)
+  static_assert(2 * kAsmBatch * kRegThreads >= kRegMaxK * (kRegMaxK + 1) / 2 * 48, "assembly batches");
   {
     double va[kAsmBatch];
 #pragma unroll
@@ -1941,43 +1943,44 @@ __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Activ
   __syncthreads();
   for (int i = tid; i < n; i += kRegThreads) z[i] = bpl[i] - ybl[i];
   __syncthreads();
-  // this thread's tiles (column-major over the lower triangle + the rhs row tile R of each column), from LDS
-  // at clamped addresses, then selected (entries above the diagonal or past row n are zero)
-  int tr[kRegTiles], tc[kRegTiles];
-  double T[kRegTiles][9];
+  // this thread's pose block (column-major over the lower triangle's 6x6 blocks + the rhs row's block of each
+  // column: K - c + 1 per block column c), from LDS at clamped addresses; entries above the diagonal, and the
+  // rhs block's rows 1..5, are never stored
+  int br = -1, bc = -1;
   {
-    int q = tid, c = 0, base = 0;
-#pragma unroll
-    for (int u = 0; u < kRegTiles; u++, q += kRegThreads) {
-      while (c < R && q >= base + (R - c + 1)) {
-        base += R - c + 1;
-        c++;
-      }
-      tc[u] = c < R ? c : -1;
-      tr[u] = c < R ? c + (q - base) : -1;
-#pragma unroll
-      for (int e = 0; e < 9; e++) {
-        const int i = 3 * tr[u] + e / 3, k = 3 * tc[u] + e % 3;
-        const bool ok = tc[u] >= 0 && i <= n && k <= i;
-        T[u][e] = Al[ok ? pk(i, k) : 0];
-        T[u][e] = ok ? T[u][e] : 0.0;
-      }
+    int c = 0, base = 0;
+    while (c < K && tid >= base + (K - c + 1)) {
+      base += K - c + 1;
+      c++;
+    }
+    if (c < K) {
+      bc = c;
+      br = c + (tid - base);  // K: the rhs row
     }
   }
+  const bool own = bc >= 0;
+  auto row_of = [&](int a) { return br < K ? 6 * br + a : n; };  // (rhs block: row n for every a)
+  auto valid = [&](int a, int b) { return own && (br < K ? (br > bc || b <= a) : a == 0); };
+  double T[6][6];
+#pragma unroll
+  for (int a = 0; a < 6; a++)
+#pragma unroll
+    for (int b = 0; b < 6; b++) {
+      const bool ok = valid(a, b);
+      T[a][b] = Al[ok ? pk(row_of(a), 6 * bc + b) : 0];
+      T[a][b] = ok ? T[a][b] : 0.0;
+    }
   if (tid == 0) prof_stamp(S, 1);
   const int wv = tid >> 6, lane = tid & 63;
   for (int s = 0; s < K; s++) {
     const int c0 = 6 * s, r0 = c0 + 6;
-    // (a) the block column's tiles to LDS
+    // (a) the block column to LDS
+    if (bc == s)
 #pragma unroll
-    for (int u = 0; u < kRegTiles; u++) {
-      if (tc[u] != 2 * s && tc[u] != 2 * s + 1) continue;
+      for (int a = 0; a < 6; a++)
 #pragma unroll
-      for (int e = 0; e < 9; e++) {
-        const int i = 3 * tr[u] + e / 3, k = 3 * tc[u] + e % 3;
-        if (i <= n && k <= i) Al[pk(i, k)] = T[u][e];
-      }
-    }
+        for (int b = 0; b < 6; b++)
+          if (valid(a, b)) Al[pk(row_of(a), c0 + b)] = T[a][b];
     __syncthreads();
     {  // (b) every wave factors the 6x6 diagonal block itself (uniform, no broadcast), one panel row per thread
       double L6[15], d6[6], r6[6];
@@ -2012,25 +2015,21 @@ __global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Activ
       if (tid == 0) atomicOr(S.fail, 1);
       return;
     }
-    // (c) trailing tiles in registers
+    // (c) the trailing block in registers: T_ab -= (X_il d_l) X_kl, l ascending per entry
+    if (own && bc > s) {
 #pragma unroll
-    for (int u = 0; u < kRegTiles; u++) {
-      if (tc[u] < 2 * s + 2) continue;
-      const int i0 = 3 * tr[u], k0 = 3 * tc[u];
-      double wi[3][6], xk[3][6];
+      for (int l = 0; l < 6; l++) {
+        const double dl = ddg[c0 + l];
+        double wi[6], xk[6];
 #pragma unroll
-      for (int a = 0; a < 3; a++)
-#pragma unroll
-        for (int l = 0; l < 6; l++) {
-          wi[a][l] = Al[pk(min(i0 + a, n), c0 + l)] * ddg[c0 + l];  // (rows > n: entries never stored)
-          xk[a][l] = Al[pk(k0 + a, c0 + l)];
+        for (int a = 0; a < 6; a++) {
+          wi[a] = Al[pk(row_of(a), c0 + l)] * dl;
+          xk[a] = Al[pk(6 * bc + a, c0 + l)];
         }
 #pragma unroll
-      for (int e = 0; e < 9; e++) {
-        double t = T[u][e];
+        for (int a = 0; a < 6; a++)
 #pragma unroll
-        for (int l = 0; l < 6; l++) t -= wi[e / 3][l] * xk[e % 3][l];
-        T[u][e] = t;
+          for (int b = 0; b < 6; b++) T[a][b] -= wi[a] * xk[b];
       }
     }
     if (tid == 0 && s < 2) prof_stamp(S, 6 + 2 * s);
@@ -3425,7 +3424,7 @@ hipError_t ensure_schur_attr() {
 static void launch_lds_solve(const Problem& P, const Active& A, const Sys& S, double lambda, hipStream_t s) {
   static const bool packed = getenv("RSPL_BA_SOLVE_LDS") && std::string(getenv("RSPL_BA_SOLVE_LDS")) == "packed";
   const int n = 6 * A.K;
-  if (packed)
+  if (packed || A.K > kRegMaxK)
     hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
   else
     hipLaunchKernelGGL(schur_reg_kernel, dim3(1), dim3(kRegThreads), schur_lds_bytes(n), s, P, A, S, n, lambda);
