@@ -472,6 +472,175 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// conv1 (conv1a 1->64 + ReLU + conv1b 64->64 + ReLU + 2x2 max-pool, superpoint.py:120-124) with the
+// whole conv1b weight tensor RESIDENT in LDS: one persistent 256-thread workgroup per CU walks 16x16-pixel
+// output tiles.  conv3x3_h_kernel<FUSE1A> restages each 32-channel half of the weights per tile and per
+// stage (two workgroups per CU, 76 KB each, phases separated by barriers: 29 % MFMA-busy SIMD time,
+// profiles/r05_experiments.md).  Here per tile: the image patch (prefetched during the previous tile's
+// MFMAs) -> LDS; conv1a of all 64 channels on MFMA (transposed product: 8-byte LDS stores) into the halo;
+// 144 v_mfma_f32_32x32x16_f16 per wave from LDS; bias + ReLU + pool through LDS to 16-byte stores.
+// LDS: weights 9 x 64 x 72 halves (82.9 KB) + halo 18 x 18 x 72 halves (46.7 KB) + patch + conv1a weights.
+// The same fp16 roundings of the same fp32 accumulations as conv3x3_h_kernel<64, 16, true, true>
+// (conv1a: one MFMA over the 9 taps + bias; conv1b: the MFMA k-steps in the same channel order).
+// ---------------------------------------------------------------------------
+constexpr int C1S = 72;  // LDS row stride (halves) of the weight and halo rows: 64 channels + 8
+
+__global__ __launch_bounds__(256) void conv1_res_kernel(ConvArgs a) {
+  constexpr int TH = 16, HX = TW + 2, HY = TH + 2, MT = TH / 8, CIN = 64;
+  extern __shared__ __attribute__((aligned(16))) _Float16 c1lds[];
+  _Float16* wts = c1lds;                              // [9][64 co][C1S]
+  _Float16* halo = wts + 9 * 64 * C1S;                // [HY][HX][C1S]; the pooled output staging afterwards
+  float* patch = reinterpret_cast<float*>(halo + HY * HX * C1S);  // [TH + 4][TW + 4]
+  float* w1a = patch + (TH + 4) * (TW + 4);           // [64][10] taps + bias
+
+  const int H = a.H, W = a.W;
+  const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
+  const int per_img = tiles_x * tiles_y, ntiles = a.B * per_img;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ml = lane & 31, kl = lane >> 5;
+
+  constexpr int PP = ((TH + 4) * (TW + 4) + 255) / 256;
+  int pv[PP];
+  auto load_patch = [&](int tile_) {
+    const int bi_ = tile_ / per_img, t_ = tile_ % per_img;
+    const int y0_ = (t_ / tiles_x) * TH, x0_ = (t_ % tiles_x) * TW;
+    const uint8_t* img = a.img + (size_t)bi_ * a.img_pitch;
+#pragma unroll
+    for (int r = 0; r < PP; r++) {
+      const int i = tid + 256 * r, py = i / (TW + 4), px = i % (TW + 4);
+      const int y = y0_ - 2 + py, x = x0_ - 2 + px;
+      pv[r] = (i < (TH + 4) * (TW + 4) && tile_ < ntiles && y >= 0 && y < H && x >= 0 && x < W)
+                  ? (int)img[(size_t)y * a.img_stride + x]
+                  : -1;
+    }
+  };
+  load_patch(blockIdx.x);
+  // the workgroup's resident weights: conv1b [9][64 co][64 ci] (16-byte pieces) and conv1a
+  for (int i = tid; i < 9 * 64 * 8; i += 256) {
+    const int q = i & 7, row = i >> 3;
+    *reinterpret_cast<half8*>(&wts[row * C1S + 8 * q]) = *reinterpret_cast<const half8*>(a.hw + (size_t)row * CIN + 8 * q);
+  }
+  for (int i = tid; i < 64 * 10; i += 256) w1a[i] = (i % 10 < 9) ? a.w1a[(i / 10) * 9 + i % 10] : a.b1a[i / 10];
+  __syncthreads();
+  // conv1a B operands of the two 32-channel halves (A[c][k]: lane (c, kl) holds k = 8 kl .. 8 kl + 7)
+  half8 bw[2];
+#pragma unroll
+  for (int hf = 0; hf < 2; hf++)
+#pragma unroll
+    for (int j = 0; j < 8; j++) {
+      const int k = 8 * kl + j;
+      bw[hf][j] = (_Float16)(k <= 9 ? w1a[(32 * hf + ml) * 10 + k] : 0.f);
+    }
+  float bias[2];
+#pragma unroll
+  for (int n = 0; n < 2; n++) bias[n] = a.bias[n * 32 + ml];
+
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    const int bi = tile / per_img, t = tile % per_img;
+    const int y0 = (t / tiles_x) * TH, x0 = (t % tiles_x) * TW;
+#pragma unroll
+    for (int r = 0; r < PP; r++) {  // (every reader of the previous tile's patch and staging has passed a barrier)
+      const int i = tid + 256 * r;
+      // src/super_point.cpp:146-150 normalisation, (float)(u / 255.0) in double (= the host LUT)
+      if (i < (TH + 4) * (TW + 4)) patch[i] = pv[r] >= 0 ? (float)((double)pv[r] / 255.0) : 0.f;
+    }
+    __syncthreads();
+    // conv1a -> ReLU -> fp16 halo, all 64 channels: D[c][px] = W1a[c][k] P[k][px] per halo row and channel half
+    {
+      const int hx = ml, x = x0 - 1 + hx;
+      for (int hy = wv; hy < HY; hy += 4) {
+        const int y = y0 - 1 + hy;
+        half8 av;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const int k = 8 * kl + j;
+          float v = 0.f;
+          if (hx < HX) v = k < 9 ? patch[(hy + k / 3) * (TW + 4) + hx + k % 3] : (k == 9 ? 1.f : 0.f);
+          av[j] = (_Float16)v;
+        }
+        const bool in = y >= 0 && y < H && x >= 0 && x < W;
+#pragma unroll
+        for (int hf = 0; hf < 2; hf++) {
+          floatx16 d;
+#pragma unroll
+          for (int r = 0; r < 16; r++) d[r] = 0.f;
+          d = mfma16(bw[hf], av, d);
+          if (hx < HX) {
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+              typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+              half4 h4;
+#pragma unroll
+              for (int e = 0; e < 4; e++) h4[e] = (_Float16)(in ? fmaxf(d[4 * q + e], 0.f) : 0.f);
+              *reinterpret_cast<half4*>(&halo[(hy * HX + hx) * C1S + 32 * hf + 8 * q + 4 * kl]) = h4;
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntiles) load_patch(tile + gridDim.x);  // in flight during the MFMAs
+    floatx16 acc[MT][2];
+#pragma unroll
+    for (int m = 0; m < MT; m++)
+#pragma unroll
+      for (int n = 0; n < 2; n++)
+#pragma unroll
+        for (int r = 0; r < 16; r++) acc[m][n][r] = 0.f;
+    // the two 32-channel stages of conv3x3_h_kernel in the same order: stage, tap, k-step
+#pragma unroll
+    for (int c0 = 0; c0 < CIN; c0 += 32)
+#pragma unroll
+      for (int kk = 0; kk < 9; kk++) {
+        const int ky = kk / 3, kx = kk % 3;
+#pragma unroll
+        for (int ks = 0; ks < 32; ks += 16) {
+          half8 av[MT], bv[2];
+#pragma unroll
+          for (int m = 0; m < MT; m++) {
+            const int ly = wv * (TH / 4) + 2 * m + (ml >> 4);
+            av[m] = *reinterpret_cast<const half8*>(&halo[((ly + ky) * HX + (ml & 15) + kx) * C1S + c0 + ks + 8 * kl]);
+          }
+#pragma unroll
+          for (int n = 0; n < 2; n++)
+            bv[n] = *reinterpret_cast<const half8*>(&wts[(kk * 64 + n * 32 + ml) * C1S + c0 + ks + 8 * kl]);
+#pragma unroll
+          for (int m = 0; m < MT; m++)
+#pragma unroll
+            for (int n = 0; n < 2; n++) acc[m][n] = mfma16(av[m], bv[n], acc[m][n]);
+        }
+      }
+    // bias + ReLU + 2x2 max-pool, the pooled (TH / 2) x 8 x 64 tile staged in LDS (the halo, now free)
+    constexpr int OS = 72;
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < 2; n++) {
+#pragma unroll
+      for (int m = 0; m < MT; m++) {
+        const int pyl = wv * (TH / 8) + m;
+#pragma unroll
+        for (int g = 0; g < 4; g++) {
+          const int r0 = (g & 1) * 2 + (g >> 1) * 4;
+          const int pc = (r0 & 3) + 8 * ((r0 >> 2) & 1) + 4 * kl;
+          float v = fmaxf(fmaxf(acc[m][n][r0], acc[m][n][r0 + 1]), fmaxf(acc[m][n][r0 + 8], acc[m][n][r0 + 9]));
+          v += bias[n];
+          halo[(pyl * 8 + (pc >> 1)) * OS + n * 32 + ml] = (_Float16)(v > 0.f ? v : 0.f);
+        }
+      }
+    }
+    __syncthreads();
+    const int H2 = H / 2, W2 = W / 2;
+    for (int i = tid; i < (TH / 2) * 8 * 8; i += 256) {
+      const int px = i >> 3, q = i & 7;
+      const int py = (y0 >> 1) + (px >> 3), pxx = (x0 >> 1) + (px & 7);
+      if (py < H2 && pxx < W2)
+        *reinterpret_cast<half8*>(a.hout + (size_t)bi * H2 * W2 * 64 + ((size_t)py * W2 + pxx) * 64 + 8 * q) =
+            *reinterpret_cast<const half8*>(&halo[px * OS + 8 * q]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // 1x1 heads on the H/8 x W/8 cell grid.  in = [P][512] (convPa | convDa, ReLU'd).
 //   MODE 0: convPb 256->65, softmax over 65, drop dustbin, depth-to-space ->
 //           scores [H][W]  (superpoint.py:131-135)
@@ -1210,7 +1379,23 @@ static hipError_t launch_conv_h(const ConvArgs& a, int B, hipStream_t s, hipEven
 hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool out_f32, int B, hipStream_t s,
                      hipEvent_t t0, hipEvent_t t1) {
   const bool small = (a.H * a.W) <= 128 * 192;
-  if (fuse1a) return launch_conv_h<64, 16, true, true, false>(a, B, s, t0, t1);
+  if (fuse1a) {
+    static const bool staged = getenv("RSPL_SP_CONV1") && std::string(getenv("RSPL_SP_CONV1")) == "stage";
+    if (staged) return launch_conv_h<64, 16, true, true, false>(a, B, s, t0, t1);
+    constexpr size_t lds = sizeof(_Float16) * (9 * 64 * C1S + 18 * 18 * C1S) + sizeof(float) * (20 * 20 + 64 * 10);
+    static bool attr = false;
+    if (!attr) {
+      const hipError_t e = hipFuncSetAttribute((const void*)conv1_res_kernel,
+                                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return e;
+      attr = true;
+    }
+    ConvArgs b = a;
+    b.B = B;
+    const int tiles = B * ((a.W + TW - 1) / TW) * ((a.H + 15) / 16);
+    hipExtLaunchKernelGGL(conv1_res_kernel, dim3(std::min(tiles, conv1_workgroups() / 2)), dim3(256), lds, s, t0, t1, 0, b);
+    return hipGetLastError();
+  }
   if (out_f32) return launch_conv_h<128, 8, false, false, true>(a, B, s);
   if (cin == 64 && pool) return launch_conv_h<64, 16, true, false, false>(a, B, s);
   if (cin == 64 && !pool) return small ? launch_conv_h<64, 8, false, false, false>(a, B, s)
