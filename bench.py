@@ -184,7 +184,7 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
 
 def ba_kernel_rows(prob, kt, timed_calls):
     """Roofline rows of the local BA's two per-trial launches from their HIP-event times on the BA stream
-    (LocalBA.kernel_times over the sampled calls of the timed region).  Algorithmic bytes per launch =
+    (LocalBA.kernel_times over every call of the instrumented pass that follows the timed region).  Algorithmic bytes per launch =
     the records the launch must read once plus what it writes:
       Schur chunks + fused solve: per edge of an optimised pose Hpl (6 x ld) + Hpp (21) + bp (6), per
         landmark Hll (ld x ld) + bl (ld), doubles; the 48-double sums of each pose pair written, the
@@ -345,8 +345,9 @@ def main():
     ap.add_argument("--ba-own-cus", type=int, default=int(os.environ.get("RSPL_BA_OWN_CUS", "1")),
                     help="1: the BA runs only on the reserved CUs (disjoint from SP/SG)")
     ap.add_argument("--skip", default="", help="diagnostics only: comma list of stages to leave out (sp,sg,ba)")
-    ap.add_argument("--ba-ktime-every", type=int, default=4,
-                    help="HIP-event timing of the BA's two per-trial launches on every N-th call (0: off)")
+    ap.add_argument("--ba-ktime-steps", type=int, default=20,
+                    help="steps of the instrumented pass after the timed region whose BA calls time the BA's two "
+                         "per-trial launches with HIP events (0: off); the timed region carries no BA events")
     ap.add_argument("--single-precision", action="store_true",
                     help="skip the second (other-precision) measurement")
     args = ap.parse_args()
@@ -510,7 +511,7 @@ def main():
                 per = len(ba_item(0))
                 ba_ms.extend([ms / n] * (n // per))
                 ba_iters.extend([its / n] * (n // per))
-        ktime_every = args.ba_ktime_every  # HIP-event timing of the BA's launches (every N-th call)
+        kt_steps = 0 if shard else args.ba_ktime_steps  # instrumented BA pass after the timed region
         line_timers = []  # HIP-event timers around the line association (post stream), timed steps only
 
         def ba_item(i):
@@ -608,13 +609,15 @@ def main():
 
         host_wait = {"lines": 0.0, "ba_queue": 0.0, "sp_calls": 0.0, "sg_calls": 0.0, "line_assoc_calls": 0.0,
                      "line_submit": 0.0}
-        # the warmup steps run exactly the timed steps' code path, measurement included (stage timers, the BA's
-        # kernel timing, the line-association timers), so no first-use cost lands in the timed region.  (The 7-10
-        # ms stall of the first timed BA calls that round 4's 20-step bench showed was the H2D hipMemcpyAsync, not
-        # this: fixed by the upload kernel, profiles/r05_bench_20step.json.)
+        # the warmup steps run exactly the timed steps' code path, measurement included (stage timers, the
+        # line-association timers), so no first-use cost lands in the timed region.  (The 7-10 ms stall of the
+        # first timed BA calls that round 4's 20-step bench showed was the H2D hipMemcpyAsync, not this: fixed by
+        # the upload kernel, profiles/r05_bench_20step.json.)  The BA's per-launch HIP events are NOT in the timed
+        # region: they cost every timed call a host round trip (the final kernel is then host-ordered) and 45
+        # event records (918 vs 883 frames/s on one box); they run in the instrumented pass after it.
         sp.profile(True)
         sg.profile(True)
-        ba.kernel_timing(ktime_every)
+        ba.kernel_timing(0)
         line_timers[:] = [capi.Timer() for _ in range(args.warmup)]
         line_t0 = 0
         for i in range(args.warmup):
@@ -635,7 +638,6 @@ def main():
         line_t0 = args.warmup
         for k in host_wait:
             host_wait[k] = 0.0
-        ba.kernel_timing(ktime_every)
         ba.kernel_times()  # reset
         ba.trace()  # reset (warmup calls)
         step_tr.clear()
@@ -656,12 +658,34 @@ def main():
                               "ba": [{k: (rel(v) if k in ("submit", "stage0", "stage1", "run0", "upload", "opt1",
                                                           "opt2", "end") else v) for k, v in r.items()}
                                      for r in ba.trace()]})
+        if ba_err:
+            raise ba_err[0]
+        # measurements of the timed region, read before the instrumented pass adds to them
+        ba_ms_timed, ba_iters_timed = list(ba_ms), list(ba_iters)
+        host_wait_timed = {k: round(v * 1e3 / args.steps, 4) for k, v in host_wait.items()}
+        sp_ms, sp_calls = sp.stage_times()
+        sg_ms, sg_calls = sg.stage_times()
+        lines_ms = float(np.mean([tm.elapsed_ms() for tm in line_timers[:len(line_stats["detect_ms"])]])) \
+            if line_stats["detect_ms"] else None
+        lines_detect = float(np.mean(line_stats["detect_ms"])) if line_stats["detect_ms"] else None
+        lines_per_step = float(np.mean(line_stats["lines"])) if line_stats["lines"] else None
+        line_t0 = None
+        # instrumented pass (untimed): the same steps with HIP events around the BA's two per-trial launches on
+        # every call, for the BA rows of stages_roofline
+        ba_kt, ba_timed_calls = None, 0
+        if kt_steps > 0 and "ba" not in args.skip.split(","):
+            ba.kernel_timing(1)
+            ba.kernel_times()  # reset
+            for i in range(kt_steps):
+                step(args.warmup + args.steps + i)
+            ba_drain()
+            capi.synchronize()
+            ba_kt = ba.kernel_times()
+            ba.kernel_timing(0)
+            ba_timed_calls = kt_steps * (world if shard else 1)
         if not native:
             ba_q.put(None)
             worker.join()
-        ba_kt = ba.kernel_times()
-        ba.kernel_timing(0)
-        ba_calls = len(ba_ms) * (world if shard else 1)
         if ba_err:
             raise ba_err[0]
         ok, mask = sg.status()  # Sinkhorn exchange health of every call in the timed region
@@ -672,18 +696,11 @@ def main():
 
         if lm.status():
             raise SystemExit("bench: the stereo line association overflowed its point-line pairs")
-        lines_ms = float(np.mean([tm.elapsed_ms() for tm in line_timers[:len(line_stats["detect_ms"])]])) \
-            if line_stats["detect_ms"] else None
-        line_t0 = None
-        sp_ms, sp_calls = sp.stage_times()
-        sg_ms, sg_calls = sg.stage_times()
         value = job_value(world, args.steps, elapsed)
         return {"value": value, "elapsed": elapsed, "sp": (sp_ms, sp_calls), "sg": (sg_ms, sg_calls),
-                "stages": (sp, sg), "ba_ms": list(ba_ms), "ba_iters": list(ba_iters), "lines_ms": lines_ms,
-                "lines_detect_ms": float(np.mean(line_stats["detect_ms"])) if line_stats["detect_ms"] else None,
-                "lines_per_step": float(np.mean(line_stats["lines"])) if line_stats["lines"] else None,
-                "ba_kt": ba_kt, "ba_timed_calls": (ba_calls + ktime_every - 1) // ktime_every if ktime_every else 0,
-                "host_wait_ms": {k: round(v * 1e3 / args.steps, 4) for k, v in host_wait.items()}}
+                "stages": (sp, sg), "ba_ms": ba_ms_timed, "ba_iters": ba_iters_timed, "lines_ms": lines_ms,
+                "lines_detect_ms": lines_detect, "lines_per_step": lines_per_step,
+                "ba_kt": ba_kt, "ba_timed_calls": ba_timed_calls, "host_wait_ms": host_wait_timed}
 
     res = measure(args.precision)
     other = measure(precs[1]) if len(precs) > 1 else None  # the other precision, same run, for the record
@@ -696,7 +713,7 @@ def main():
     if rank != 0:
         return
     stages = stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, args.precision)
-    if not shard:
+    if not shard and res["ba_kt"]:
         stages.update(ba_kernel_rows(problems[0], res["ba_kt"], res["ba_timed_calls"]))
     # the step-setting kernel: the largest device time per step over every timed kernel, the BA's
     # launches included (its launches per call x one call per step)

@@ -1393,7 +1393,9 @@ hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool ou
     ConvArgs b = a;
     b.B = B;
     const int tiles = B * ((a.W + TW - 1) / TW) * ((a.H + 15) / 16);
-    hipExtLaunchKernelGGL(conv1_res_kernel, dim3(std::min(tiles, conv1_workgroups() / 2)), dim3(256), lds, s, t0, t1, 0, b);
+    static const int wg_env = getenv("RSPL_SP_CONV1_WG") ? atoi(getenv("RSPL_SP_CONV1_WG")) : 0;
+    const int wgs = wg_env > 0 ? wg_env : conv1_workgroups() / 2;
+    hipExtLaunchKernelGGL(conv1_res_kernel, dim3(std::min(tiles, wgs)), dim3(256), lds, s, t0, t1, 0, b);
     return hipGetLastError();
   }
   if (out_f32) return launch_conv_h<128, 8, false, false, true>(a, B, s);
