@@ -65,8 +65,10 @@ struct rspl_ba {
   size_t pp_cap = 0;      // capacity in pairs
   // per-call inputs (cameras, T / X / L, edges, reduced pose ids, landmark offsets, pose pairs,
   // zeroed level / fill / flags / out), laid out exactly like the staging buffer's call
-  // region: one upload per call (capacity fixed at create)
-  char* cbuf = nullptr;
+  // region: one upload per call (capacity fixed at create).  One per staging slot: the tracking
+  // thread uploads the next staged call into its slot's buffer behind the current call's last kernels
+  // (preupload_next), so a call's upload is off its own critical path
+  char* cbuf[2] = {nullptr, nullptr};
   // pinned, host-mapped staging for uploads; the final kernel writes results straight into it.
   // Two slots: the tracking thread's next queued call is staged into one while the running call
   // reads its results from the other
@@ -115,6 +117,7 @@ struct rspl_ba {
   std::condition_variable qcv;  // the worker waits for jobs; submitters for room; joiners for idle
   std::deque<Job> jobs;
   bool busy = false, quit = false;
+  bool tracking_call = false;  // run_call is running on the tracking thread (preupload_next may look ahead)
   int q_err = 0;                // first failed call since the last join
   std::string q_msg;
   long long q_done = 0, q_iters = 0;
@@ -228,6 +231,7 @@ struct rspl::ba::StagedCall {
   DownLayout dl;
   HostMarks tm;
   double tr[RSPL_BA_TRACE_W] = {};  // its host timeline record (rspl_ba_trace)
+  bool uploaded = false;  // its inputs already queued for upload into cbuf[slot] (tracking thread only)
 };
 
 namespace {
@@ -442,6 +446,8 @@ struct SpecFinish {
 // and the next trial's kernels read it.  The host waits once, for the trial that stops the
 // optimize(); when rejected trials leave iterations undone it queues more.  At the end the host
 // pointer view follows the device's current bank.
+void preupload_next(rspl_ba* b);
+
 int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
                  double* chi2_out, int* done_out, uint8_t* cls_level, bool build_pp, SpecFinish* fin) {
   hipStream_t st = b->stream;
@@ -544,6 +550,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
     return RSPL_OK;
   };
   if ((rc = enqueue_batch(iters))) return rc;
+  if (fin) preupload_next(b);  // the call's last kernels are queued: the next call's upload behind them
   double v[4];
   for (;;) {
     // wait for the stopping trial (trials queued after it post nothing) or the last queued one
@@ -738,7 +745,9 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
 
       hipHostMalloc((void**)&b->mail, sizeof(ba::Mail), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer((void**)&b->mail_dev, b->mail, 0) != hipSuccess ||
-      hipMalloc((void**)&b->cbuf, CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE, 8 * (size_t)b->maxE).bytes) !=
+      hipMalloc((void**)&b->cbuf[0], CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE, 8 * (size_t)b->maxE).bytes) !=
+          hipSuccess ||
+      hipMalloc((void**)&b->cbuf[1], CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE, 8 * (size_t)b->maxE).bytes) !=
           hipSuccess ||
       hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
       hipMemset(b->pair_ctr, 0, sizeof(unsigned) * (b->maxK * (b->maxK + 1) / 2 + 1)) != hipSuccess) {
@@ -838,7 +847,8 @@ extern "C" void rspl_ba_destroy(rspl_ba* b) {
   if (b->gbuf) (void)hipFree(b->gbuf);
   if (b->pdg) (void)hipFree(b->pdg);
   b->arena.release();
-  if (b->cbuf) (void)hipFree(b->cbuf);
+  for (char* cb : b->cbuf)
+    if (cb) (void)hipFree(cb);
   if (b->pp_buf) (void)hipFree(b->pp_buf);
   if (b->prof) (void)hipFree(b->prof);
   for (char* sg : b->stage)
@@ -1005,7 +1015,9 @@ void tracking_loop(rspl_ba* b) {
       rc = j.sc->rc;
     } else {
       begin_call(b);
+      b->tracking_call = true;
       rc = end_call(b, run_call(b, *j.sc, j.pr, j.res, j.sc->tr));
+      b->tracking_call = false;
     }
     const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
     const std::string msg = rc ? std::string(rspl_last_error()) : std::string();
@@ -1210,6 +1222,29 @@ int stage_call(rspl_ba* b, int slot, const rspl_ba_problem* pr, rspl_ba_result* 
 }
 
 // The device part of one staged call: upload, both optimize() calls, results
+bool upload_copy() {
+  static const bool c = getenv("RSPL_BA_UPLOAD") && std::string(getenv("RSPL_BA_UPLOAD")) == "copy";
+  return c;
+}
+
+// The next queued call's inputs, uploaded into its slot's call buffer behind the current call's last
+// queued kernels (optimize(5)'s trials and the gated final kernel): the upload (~40 us over PCIe at C3)
+// then runs while the host notices the current call's end and queues the next one, instead of first in
+// the next call's chain.  Tracking thread only; the next call must already be staged (its slot is then
+// busy until it completes, and differs from the running call's).
+void preupload_next(rspl_ba* b) {
+  static const bool off = getenv("RSPL_BA_PREUPLOAD") && std::string(getenv("RSPL_BA_PREUPLOAD")) == "0";  // A/B
+  if (!b->tracking_call || upload_copy() || off) return;
+  std::shared_ptr<ba::StagedCall> nx;
+  {
+    std::lock_guard<std::mutex> lk(b->qmu);
+    if (!b->jobs.empty() && b->jobs.front().state == 2 && b->jobs.front().sc->rc == RSPL_OK) nx = b->jobs.front().sc;
+  }
+  if (!nx || nx->uploaded) return;
+  if (upload_mapped(b->cbuf[nx->slot], b->stage_dev[nx->slot], nx->cl.bytes, b->stream) == hipSuccess)
+    nx->uploaded = true;
+}
+
 int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rspl_ba_result* res, double* tr) {
   const int np = pr->n_poses, nq = pr->n_points, nl = pr->n_lines;
   const int ne[4] = {pr->n_mono, pr->n_stereo, pr->n_mono_line, pr->n_stereo_line};
@@ -1239,12 +1274,13 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
   // hipMemcpyAsync: its H2D path stalled the first calls after the warmup by 7-10 ms each (the SDMA engine /
   // blit-kernel choice settling; profiles/r05_bench_20step_before.json), which cost the driver's 20-step bench
   // a quarter of its rate.  RSPL_BA_UPLOAD=copy keeps the old path for A/B.
-  static const bool up_copy = getenv("RSPL_BA_UPLOAD") && std::string(getenv("RSPL_BA_UPLOAD")) == "copy";
-  if (!up_copy) RSPL_HIP(upload_mapped(b->cbuf, b->stage_dev[c.slot], cl.bytes, st));
-  else RSPL_HIP(hipMemcpyAsync(b->cbuf, sg, cl.bytes, hipMemcpyHostToDevice, st));
+  char* cb = b->cbuf[c.slot];
+  if (!c.uploaded) {  // (else queued behind the previous call's final kernel: preupload_next)
+    if (!upload_copy()) RSPL_HIP(upload_mapped(cb, b->stage_dev[c.slot], cl.bytes, st));
+    else RSPL_HIP(hipMemcpyAsync(cb, sg, cl.bytes, hipMemcpyHostToDevice, st));
+  }
   tm.mark("upload");
   tr[4] = mono_s();
-  char* cb = b->cbuf;
   uint8_t* level = reinterpret_cast<uint8_t*>(cb + cl.level);
   ba::Problem P{};
   P.cams = reinterpret_cast<double*>(cb + cl.cams);
