@@ -1393,8 +1393,13 @@ hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool ou
     ConvArgs b = a;
     b.B = B;
     const int tiles = B * ((a.W + TW - 1) / TW) * ((a.H + 15) / 16);
+    // one persistent workgroup on every other CU (conv1_workgroups() / 4): each holds 131 KB of a CU's LDS for
+    // the whole conv1, so on a CU it occupies no local-BA Schur chunk wave (35 KB) fits -- with a workgroup on
+    // every CU the BA chain stalled for the length of conv1 every step.  Measured in the C3 pipeline (r05
+    // experiments): 256 workgroups 936 frames/s, 192 951-967, 128 976-977 (conv1 0.15 -> 0.19 ms, off the
+    // critical path).  RSPL_SP_CONV1_WG overrides (A/B).
     static const int wg_env = getenv("RSPL_SP_CONV1_WG") ? atoi(getenv("RSPL_SP_CONV1_WG")) : 0;
-    const int wgs = wg_env > 0 ? wg_env : conv1_workgroups() / 2;
+    const int wgs = wg_env > 0 ? wg_env : std::max(1, conv1_workgroups() / 4);
     hipExtLaunchKernelGGL(conv1_res_kernel, dim3(std::min(tiles, wgs)), dim3(256), lds, s, t0, t1, 0, b);
     return hipGetLastError();
   }
