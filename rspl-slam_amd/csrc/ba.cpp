@@ -260,7 +260,8 @@ void carve(F& ar, rspl_ba* b) {
   take(b->partial2, std::max(std::max((size_t)b->maxV / 256, nblk) + 2, K * (E / 256 + 1) * 6));
   take(b->lm_ctr, nl);
   const size_t npairs = K * (K + 1) / 2, nchk = std::max<size_t>((NL + ba::kLmChunk - 1) / ba::kLmChunk, 1);
-  take(b->chunk, npairs * nchk * 48); take(b->pairfin, npairs * 48 + 8); take(b->pair_ctr, npairs + 1);  // + the solve ticket
+  // pair_ctr: + the solve ticket
+  take(b->chunk, npairs * nchk * 48); take(b->pairfin, npairs * 48 + 8); take(b->pair_ctr, npairs + 1);
   take(b->red, 6 * K + kMaxRanks + 8);
   take(b->lmctl, 2);
   take(b->pp_cnt, npairs * nchk); take(b->pp_off, npairs * nchk + 1);
@@ -741,19 +742,30 @@ extern "C" int rspl_ba_create(const rspl_ba_config* cfg, rspl_ba** out) {
   // SuperPoint/SuperGlue work instead of waiting behind it
   int prio_lo = 0, prio_hi = 0;
   (void)hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi);
-  if (hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, prio_hi) != hipSuccess ||
-
-      hipHostMalloc((void**)&b->mail, sizeof(ba::Mail), hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
-      hipHostGetDevicePointer((void**)&b->mail_dev, b->mail, 0) != hipSuccess ||
-      hipMalloc((void**)&b->cbuf[0], CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE, 8 * (size_t)b->maxE).bytes) !=
-          hipSuccess ||
-      hipMalloc((void**)&b->cbuf[1], CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE, 8 * (size_t)b->maxE).bytes) !=
-          hipSuccess ||
-      hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)) != hipSuccess ||
-      hipMemset(b->pair_ctr, 0, sizeof(unsigned) * (b->maxK * (b->maxK + 1) / 2 + 1)) != hipSuccess) {
-    set_error("BA stream / mailbox allocation failed");
-    rspl_ba_destroy(b);
-    return RSPL_E_DEVICE;
+  {
+    const size_t cbytes = CallLayout(kMaxCams, b->maxK, cfg->max_points, cfg->max_lines, b->maxE, 8 * (size_t)b->maxE).bytes;
+    const char* what = nullptr;
+    hipError_t e = hipSuccess;
+    auto step = [&](hipError_t r, const char* w) {
+      if (e == hipSuccess && r != hipSuccess) {
+        e = r;
+        what = w;
+      }
+    };
+    step(hipStreamCreateWithPriority(&b->stream, hipStreamNonBlocking, prio_hi), "hipStreamCreateWithPriority");
+    if (e == hipSuccess)
+      step(hipHostMalloc((void**)&b->mail, sizeof(ba::Mail), hipHostMallocMapped | hipHostMallocCoherent), "hipHostMalloc(mailbox)");
+    if (e == hipSuccess) step(hipHostGetDevicePointer((void**)&b->mail_dev, b->mail, 0), "hipHostGetDevicePointer(mailbox)");
+    for (int i = 0; i < 2 && e == hipSuccess; i++) step(hipMalloc((void**)&b->cbuf[i], cbytes), "hipMalloc(call buffer)");
+    if (e == hipSuccess) step(hipMemset(b->lm_ctr, 0, sizeof(unsigned) * std::max(b->cfg.max_lines, 1)), "hipMemset(lm_ctr)");
+    if (e == hipSuccess)
+      step(hipMemset(b->pair_ctr, 0, sizeof(unsigned) * (b->maxK * (b->maxK + 1) / 2 + 1)), "hipMemset(pair_ctr)");
+    if (e != hipSuccess) {
+      set_error("BA stream / mailbox allocation failed: %s: %s (call buffer %zu bytes, arena %zu bytes)", what,
+                hipGetErrorString(e), cbytes, b->arena.size);
+      rspl_ba_destroy(b);
+      return RSPL_E_DEVICE;
+    }
   }
   memset(b->mail, 0, sizeof(ba::Mail));
   // everything a call can need, allocated once here for the handle's capacities (never inside a call:
