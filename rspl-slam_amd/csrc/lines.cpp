@@ -257,6 +257,7 @@ struct rspl_lines {
   const uint8_t* a_img = nullptr;
   int a_H = 0, a_W = 0, a_stride = 0, a_merge = 1, a_rc = 0, a_n = 0;
   double a_us = 0;  // the job's own duration on the worker
+  double ph_us[4] = {0, 0, 0, 0};  // the last detection's phases (image staged, GPU classes back, FLD), us
   // rspl_lines_extract_wait_device: the worker's lines staged in pinned memory and copied to the device in
   // stream order, through a ring of kPinSlots buffers: a slot is rewritten only once its copy of
   // kPinSlots joins ago has completed (copy_ev), so a join never waits for the stream in practice
@@ -794,7 +795,9 @@ extern "C" int rspl_lines_detect(rspl_lines* h, const uint8_t* image, int H, int
     RSPL_HIP(hipHostMalloc((void**)&h->h_det, 2 * (px / 4)));
     h->det_cap = px;
   }
+  const auto tp0 = std::chrono::steady_clock::now();
   for (int r = 0; r < H; r++) memcpy(h->h_img + (size_t)r * W, image + (size_t)r * stride, W);
+  const auto tp1 = std::chrono::steady_clock::now();
   hipStream_t st = h->stream;
   RSPL_HIP(hipMemcpyAsync(h->d_img, h->h_img, px, hipMemcpyHostToDevice, st));
   double lo = cfg->canny_th1, hi = cfg->canny_th2;
@@ -806,9 +809,15 @@ extern "C" int rspl_lines_detect(rspl_lines* h, const uint8_t* image, int H, int
   RSPL_HIP(lines::canny_classes(a, st));
   RSPL_HIP(hipMemcpyAsync(h->h_det, h->d_det, 2 * hp, hipMemcpyDeviceToHost, st));
   RSPL_HIP(hipStreamSynchronize(st));
+  const auto tp2 = std::chrono::steady_clock::now();
   h->det_H = H;
   h->det_W = W;
   const int n = fld_from_classes(h->h_det, h->h_det + hp, hh, hw, cfg, h->edge, h->stack, segments, capacity);
+  const auto tp3 = std::chrono::steady_clock::now();
+  auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+  h->ph_us[0] = us(tp0, tp1);
+  h->ph_us[1] = us(tp1, tp2);
+  h->ph_us[2] = us(tp2, tp3);
   *n_out = n;
   if (n > capacity) {
     set_error("%d segments exceed capacity %d", n, capacity);
@@ -849,6 +858,10 @@ void extract_job(rspl_lines* h) {
   h->a_rc = rc;
   h->a_err = rc == RSPL_OK ? std::string() : std::string(rspl_last_error());
   h->a_us = std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count();
+  static const bool timing = getenv("RSPL_LINES_TIMING") != nullptr;  // diagnostics
+  if (timing)
+    fprintf(stderr, "lines_job us: stage %.1f gpu %.1f fld %.1f merge+rest %.1f total %.1f segs %d lines %d\n", h->ph_us[0],
+            h->ph_us[1], h->ph_us[2], h->a_us - h->ph_us[0] - h->ph_us[1] - h->ph_us[2], h->a_us, n, h->a_n);
 }
 
 }  // namespace
