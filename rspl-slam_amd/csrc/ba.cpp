@@ -255,9 +255,10 @@ void carve(F& ar, rspl_ba* b) {
   const size_t nblk = std::max(E / 256, NL * 8 / 256) + 2;
   // partial also holds the setup kernel's per-block costs: the landmark groups plus the line
   // workgroups (at most one per line landmark plus one per kLineBlk line edges)
-  take(b->S, 36 * K * K); take(b->x, 6 * K); take(b->partial, nblk + NL + E / ba::kLineBlk + 8);
+  // (+ 1024: update_errors' XCD-aligned grid rounds the landmark blocks up to whole ranges per XCD)
+  take(b->S, 36 * K * K); take(b->x, 6 * K); take(b->partial, nblk + NL + E / ba::kLineBlk + 1032);
   // partial2: scale partials, and the pose-diagonal partials (K x E/256 x 6) of the lambda init
-  take(b->partial2, std::max(std::max((size_t)b->maxV / 256, nblk) + 2, K * (E / 256 + 1) * 6));
+  take(b->partial2, std::max(std::max((size_t)b->maxV / 256, nblk) + 1026, K * (E / 256 + 1) * 6));
   take(b->lm_ctr, nl);
   const size_t npairs = K * (K + 1) / 2, nchk = std::max<size_t>((NL + ba::kLmChunk - 1) / ba::kLmChunk, 1);
   // pair_ctr: + the solve ticket
@@ -1347,6 +1348,7 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
     A.nchk = std::max(1, std::min((nL + ba::kLmChunk - 1) / ba::kLmChunk, kChunkWaves / npairs));
     A.lmchunk = std::max(ba::kLmChunk, ((nL + A.nchk - 1) / A.nchk + 63) / 64 * 64);
     A.nchk = std::max((nL + A.lmchunk - 1) / A.lmchunk, 1);
+    ba::set_update_geometry(A);
   }
   A.n_line_edges = n_line_local;
   A.ltab = reinterpret_cast<const int4*>(cb + cl.ltab);

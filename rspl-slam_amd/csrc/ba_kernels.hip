@@ -2928,7 +2928,14 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
   const int tid = threadIdx.x;
   // kUeWaves of the 4 waves carry landmark groups: fewer landmarks per workgroup spread the groups over
   // more CUs (the others only stage the block's poses and take part in the barriers)
-  const int t = blockIdx.x * (64 * kUeWaves) + tid, g = t / kGroup, j = t % kGroup;
+  // the landmark block: with A.ue_bpr the workgroups of Schur chunk range lb (its lmchunk landmarks) go to
+  // the XCD that ran the range's chunks (lb % 8, chunk_seg): their records are in that XCD's L2
+  int ub = blockIdx.x;
+  if (SPEC && A.ue_bpr > 0) {
+    const int b = blockIdx.x, x = b & 7, sl = b >> 3, r = sl / A.ue_bpr, lb = 8 * r + x;
+    ub = lb < A.nchk ? lb * A.ue_bpr + (sl - r * A.ue_bpr) : (A.nL + 31) / 32 + 1;  // (else: no landmark)
+  }
+  const int t = ub * (64 * kUeWaves) + tid, g = t / kGroup, j = t % kGroup;
   const bool in = tid < 64 * kUeWaves && g < A.nL;
   const bool point = g < P.nq;
   int k0 = 0, k1 = 0;
@@ -3365,7 +3372,14 @@ hipError_t compute_errors(const Problem& P, const Lin& L, const Active& A, Sys& 
 }
 
 int update_errors_blocks(const Active& A) {
+  if (A.ue_bpr > 0) return 8 * ((A.nchk + 7) / 8) * A.ue_bpr;
   return A.nL > 0 ? (A.nL * kGroup + 64 * kUeWaves - 1) / (64 * kUeWaves) : 1;
+}
+
+void set_update_geometry(Active& A) {
+  static const bool off = getenv("RSPL_BA_UEXCD") && std::string(getenv("RSPL_BA_UEXCD")) == "0";
+  constexpr int per = 64 * kUeWaves / kGroup;  // landmarks per update workgroup
+  A.ue_bpr = !off && A.nchk >= 8 && A.lmchunk % per == 0 ? A.lmchunk / per : 0;
 }
 
 hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool with_maxdiag,

@@ -55,6 +55,8 @@ struct Active {          // active structure of one optimize() phase
   int nchk;              // Schur chunks per pose pair: landmark ranges of lmchunk
   int lmchunk;           // landmarks per Schur chunk (a multiple of 64; kLmChunk unless the pose pairs
                          //   are so many that the chunk waves would need several dispatch rounds)
+  int ue_bpr;            // update_errors<true> workgroups per Schur chunk range when their landmark blocks
+                         //   are dealt to the XCD that ran the range's chunks (0: plain order)
   const int* pp_off;     // [npairs * nchk + 1] segment of each chunk in the edge-pair lists
   const int4* pp;        // edge pairs {e1 of pose a, e2 of pose b, their landmark, 0}, chunk-major,
                          //   landmark order within a chunk
@@ -201,6 +203,9 @@ bool wave_path(int K);                 // the single-wave LDL^T (fused into the 
 int update_blocks(const Problem& P);
 int errors_blocks(int Ea);
 int update_errors_blocks(const Active& A);
+// sets A.ue_bpr (after nchk / lmchunk): the trial's update workgroups on the XCD whose L2 the Schur chunks of
+// their landmarks just filled (RSPL_BA_UEXCD=0: plain order, A/B)
+void set_update_geometry(Active& A);
 
 }  // namespace ba
 }  // namespace rspl
