@@ -109,6 +109,7 @@ struct MFrame {
   std::set<std::pair<int, int>> oconn;        // _ordered_connections: (weight, frame id)
   int parent = -1;
   int lmo = -1, lmo_fix = -1;                 // local_map_optimization_(fix_)frame_id
+  int pidx = -1;                              // pose index in the last assembled problem
 
   // Frame::AddConnection(frame, weight) (frame.cc:458-469)
   void add_connection(int f, int w) {
@@ -156,7 +157,6 @@ struct MPoint {  // Mappoint
   int type = kUnTriangulated;
   FlatMap<int> obs;        // _obversers: frame id -> keypoint index
   int lmo = -1;
-  int dense = -1;          // index in the last assembled problem
   int observers() const {  // ObverserNum
     int n = 0;
     for (auto& kv : obs) n += kv.second >= 0;
@@ -175,7 +175,6 @@ struct MLine {  // Mapline
   FlatMap<int> obs;         // frame id -> line index
   FlatMap<int> incl;        // _included_endpoints
   int lmo = -1;
-  int dense = -1;            // index in the last assembled problem
   double ep[6] = {};
   bool ep_valid = false, to_update = false;
   int observers() const {
@@ -281,6 +280,16 @@ struct rspl_map {
   std::vector<int32_t> c_pose[4], c_lm[4];
   std::vector<double> c_obs[4];
   std::vector<uint8_t> c_inl[4];
+  // assembly scratch (kept across calls for their capacity): the window's landmarks, their
+  // observers flattened, the kept landmarks (id, ordinal) and the ordinal -> dense index map
+  struct Obs {
+    const MFrame* f;
+    int kp;
+  };
+  std::vector<MPoint*> lm_pts, kept_ptr;
+  std::vector<int> lm_beg, lm_rank;
+  std::vector<Obs> lm_obs;
+  std::vector<std::pair<int, int>> kept_pts;
 
   MFrame* frame(int id) { return kf_ix.get(kf, id); }
   MPoint* point(int id) { return id < 0 ? nullptr : mp_ix.get(mp, id); }
@@ -563,16 +572,31 @@ struct rspl_map {
     }
     Counter fixed_frames(this);  // keyed by frame id (the reference: by FramePtr; only counted)
     bool any_fixed = false;
-    std::vector<int> mpts, mpls;
+    // the window's landmarks in the reference's order (frame by frame, slot by slot), each with its
+    // observers (frame, keypoint index) copied into one flat array, so the constraint pass below reads
+    // them sequentially instead of chasing every landmark's observer list a second time
+    lm_pts.clear();
+    lm_beg.clear();
+    lm_obs.clear();
+    std::vector<int> mpls;
     for (MFrame* k : nb) {
-      for (int pid : k->mpt) {
-        MPoint* m = point(pid);
+      const int nslot = (int)k->mpt.size();
+      for (int s = 0; s < nslot; s++) {
+        // the landmarks are scattered heap nodes: fetch the node 8 slots ahead and its observer list 4 ahead
+        if (s + 8 < nslot)
+          if (const MPoint* q = point(k->mpt[s + 8])) __builtin_prefetch(q);
+        if (s + 4 < nslot)
+          if (const MPoint* q = point(k->mpt[s + 4])) __builtin_prefetch(q->obs.v.data());
+        MPoint* m = point(k->mpt[s]);
         if (!m || m->type != kGood || m->lmo == fid) continue;
         m->lmo = fid;
-        mpts.push_back(pid);
+        lm_pts.push_back(m);
+        lm_beg.push_back((int)lm_obs.size());
         for (auto& kv : m->obs) {
           MFrame* o = frame(kv.first);
-          if (o && o->lmo != fid) {
+          if (!o) continue;
+          lm_obs.push_back({o, kv.second});
+          if (o->lmo != fid) {
             fixed_frames.add(o->id);
             any_fixed = true;
           }
@@ -585,6 +609,7 @@ struct rspl_map {
         mpls.push_back(lid);
       }
     }
+    lm_beg.push_back((int)lm_obs.size());
     const size_t max_fixed = 1;
     std::set<std::pair<int, int>> ord;
     fixed_frames.drain([&](int id, int w) { ord.insert({w, id}); });
@@ -596,102 +621,112 @@ struct rspl_map {
         add_vertex(poses, *o, true);
       }
     }
-    mark();
-    auto in_window = [&](const MFrame* o) { return o && (o->lmo == fid || o->lmo_fix == fid); };
-    // constraints in the reference's order: landmark by landmark, observers by frame id
-    std::vector<Con> cons[4];  // mono, stereo, mono line, stereo line
-    std::vector<MPoint*> points;  // kept landmarks (dense order = ascending id, set below)
-    std::vector<MLine*> lines;
-    std::vector<Con> mono, stereo;
-    for (int pid : mpts) {
-      MPoint* m = point(pid);
-      if (!m || m->type != kGood) continue;
-      mono.clear();
-      stereo.clear();
-      for (auto& kv : m->obs) {
-        MFrame* o = frame(kv.first);
-        if (!in_window(o)) continue;
-        double k[3];
-        if (!o->keypoint(kv.second, k)) continue;
-        if (k[2] > 0) stereo.push_back({kv.first, pid, {k[0], k[1], k[2]}});
-        else mono.push_back({kv.first, pid, {k[0], k[1]}});
-      }
-      if (!stereo.empty() || mono.size() > 1) {
-        points.push_back(m);
-        cons[0].insert(cons[0].end(), mono.begin(), mono.end());
-        cons[1].insert(cons[1].end(), stereo.begin(), stereo.end());
-      }
-    }
-    for (int lid : mpls) {
-      MLine* l = line(lid);
-      if (!l || l->type != kGood) continue;
-      mono.clear();
-      stereo.clear();
-      for (auto& kv : l->obs) {
-        MFrame* o = frame(kv.first);
-        if (!in_window(o)) continue;
-        if (kv.second < 0 || kv.second >= (int)o->ll.size()) continue;  // GetLine
-        Con c{kv.first, lid, {}};
-        for (int i = 0; i < 4; i++) c.obs[i] = o->ll[kv.second][i];
-        if (o->right_line_status(kv.second)) {  // GetLineRight
-          for (int i = 0; i < 4; i++) c.obs[4 + i] = o->lr[kv.second][i];
-          stereo.push_back(c);
-        } else {
-          mono.push_back(c);
-        }
-      }
-      if (!stereo.empty() || mono.size() > 1) {
-        lines.push_back(l);
-        cons[2].insert(cons[2].end(), mono.begin(), mono.end());
-        cons[3].insert(cons[3].end(), stereo.begin(), stereo.end());
-      }
-    }
-    mark();
-    // dense problem: std::map ids in ascending order (LocalmapOptimization's vertex order)
+    // dense poses: std::map ids in ascending order (LocalmapOptimization's vertex order); every
+    // frame of the window (lmo or lmo_fix == fid) is a vertex and learns its index here
     pose_ids.clear(); point_ids.clear(); line_ids.clear(); pose_fixed.clear();
-    std::map<int, int> pidx;
     std::vector<double> pq, pp, X, Ls;
     for (auto& kv : poses) {
-      pidx[kv.first] = (int)pose_ids.size();
+      frame(kv.first)->pidx = (int)pose_ids.size();
       pose_ids.push_back(kv.first);
       pose_fixed.push_back(kv.second.fixed);
       pq.insert(pq.end(), kv.second.q, kv.second.q + 4);
       pp.insert(pp.end(), kv.second.p, kv.second.p + 3);
     }
-    std::sort(points.begin(), points.end(), [](const MPoint* a, const MPoint* b) { return a->id < b->id; });
-    std::sort(lines.begin(), lines.end(), [](const MLine* a, const MLine* b) { return a->id < b->id; });
-    X.reserve(3 * points.size());
-    Ls.reserve(6 * lines.size());
-    for (MPoint* m : points) {
-      m->dense = (int)point_ids.size();
-      point_ids.push_back(m->id);
-      X.insert(X.end(), m->p, m->p + 3);
-    }
-    for (MLine* l : lines) {
-      l->dense = (int)line_ids.size();
-      line_ids.push_back(l->id);
-      Ls.insert(Ls.end(), l->L, l->L + 6);
-    }
-    static const int od[4] = {2, 3, 4, 8};
+    mark();
+    auto in_window = [&](const MFrame* o) { return o->lmo == fid || o->lmo_fix == fid; };
+    // constraints in the reference's order: landmark by landmark, observers by frame id, written
+    // straight into the dense arrays; a landmark that is dropped (no stereo and at most one mono
+    // observation) has its rows taken back.  c_lm holds the kept landmark's ordinal until the
+    // landmarks are numbered by id below.
     for (int t = 0; t < 4; t++) {
       c_pose[t].clear(); c_lm[t].clear(); c_obs[t].clear();
-      for (auto& c : cons[t]) {
-        c_pose[t].push_back(pidx.at(c.pose));
-        c_lm[t].push_back(t < 2 ? point(c.lm)->dense : line(c.lm)->dense);
-        c_obs[t].insert(c_obs[t].end(), c.obs, c.obs + od[t]);
-      }
-      c_inl[t].assign(cons[t].size(), 1);
     }
+    kept_pts.clear();
+    kept_ptr.clear();
+    for (size_t li = 0; li < lm_pts.size(); li++) {
+      const size_t b0 = c_pose[0].size(), b1 = c_pose[1].size();
+      const int ord_lm = (int)kept_pts.size();
+      for (int j = lm_beg[li]; j < lm_beg[li + 1]; j++) {
+        const MFrame* o = lm_obs[j].f;
+        const int kpi = lm_obs[j].kp;
+        if (!in_window(o) || kpi < 0 || kpi >= (int)o->kp.size()) continue;  // GetKeypointPosition
+        const double* k = o->kp[kpi].data();
+        const int t = k[2] > 0 ? 1 : 0;
+        c_pose[t].push_back(o->pidx);
+        c_lm[t].push_back(ord_lm);
+        c_obs[t].insert(c_obs[t].end(), k, k + 2 + t);
+      }
+      if (c_pose[1].size() > b1 || c_pose[0].size() > b0 + 1) {
+        kept_pts.push_back({lm_pts[li]->id, ord_lm});
+        kept_ptr.push_back(lm_pts[li]);
+      } else {
+        c_pose[0].resize(b0); c_lm[0].resize(b0); c_obs[0].resize(2 * b0);
+        c_pose[1].resize(b1); c_lm[1].resize(b1); c_obs[1].resize(3 * b1);
+      }
+    }
+    std::vector<std::pair<int, MLine*>> kept_lines;
+    for (int lid : mpls) {
+      MLine* l = line(lid);
+      if (!l || l->type != kGood) continue;
+      const size_t b0 = c_pose[2].size(), b1 = c_pose[3].size();
+      const int ord_lm = (int)kept_lines.size();
+      for (auto& kv : l->obs) {
+        MFrame* o = frame(kv.first);
+        if (!o || !in_window(o)) continue;
+        if (kv.second < 0 || kv.second >= (int)o->ll.size()) continue;  // GetLine
+        const int t = o->right_line_status(kv.second) ? 3 : 2;          // GetLineRight
+        c_pose[t].push_back(o->pidx);
+        c_lm[t].push_back(ord_lm);
+        c_obs[t].insert(c_obs[t].end(), o->ll[kv.second].begin(), o->ll[kv.second].end());
+        if (t == 3) c_obs[t].insert(c_obs[t].end(), o->lr[kv.second].begin(), o->lr[kv.second].end());
+      }
+      if (c_pose[3].size() > b1 || c_pose[2].size() > b0 + 1) {
+        kept_lines.push_back({lid, l});
+      } else {
+        c_pose[2].resize(b0); c_lm[2].resize(b0); c_obs[2].resize(4 * b0);
+        c_pose[3].resize(b1); c_lm[3].resize(b1); c_obs[3].resize(8 * b1);
+      }
+    }
+    mark();
+    // dense landmarks: ascending id; constraint rows renumbered from the ordinal
+    std::sort(kept_pts.begin(), kept_pts.end());
+    lm_rank.resize(kept_pts.size());
+    X.resize(3 * kept_pts.size());
+    point_ids.resize(kept_pts.size());
+    for (size_t i = 0; i < kept_pts.size(); i++) {
+      const MPoint* m = kept_ptr[kept_pts[i].second];
+      lm_rank[kept_pts[i].second] = (int)i;
+      point_ids[i] = kept_pts[i].first;
+      for (int c = 0; c < 3; c++) X[3 * i + c] = m->p[c];
+    }
+    for (int t = 0; t < 2; t++)
+      for (auto& v : c_lm[t]) v = lm_rank[v];
+    std::vector<int> line_rank(kept_lines.size());
+    {
+      std::vector<int> o(kept_lines.size());
+      for (size_t i = 0; i < o.size(); i++) o[i] = (int)i;
+      std::sort(o.begin(), o.end(), [&](int a, int b) { return kept_lines[a].first < kept_lines[b].first; });
+      Ls.resize(6 * o.size());
+      line_ids.resize(o.size());
+      for (size_t i = 0; i < o.size(); i++) {
+        line_rank[o[i]] = (int)i;
+        line_ids[i] = kept_lines[o[i]].first;
+        std::copy(kept_lines[o[i]].second->L, kept_lines[o[i]].second->L + 6, Ls.begin() + 6 * i);
+      }
+    }
+    for (int t = 2; t < 4; t++)
+      for (auto& v : c_lm[t]) v = line_rank[v];
+    for (int t = 0; t < 4; t++) c_inl[t].assign(c_pose[t].size(), 1);
     if (rep) {
       memset(rep, 0, sizeof(*rep));
       rep->n_poses = (int)pose_ids.size();
       for (uint8_t f : pose_fixed) rep->n_fixed += f;
       rep->n_points = (int)point_ids.size();
       rep->n_lines = (int)line_ids.size();
-      rep->n_mono = (int)cons[0].size();
-      rep->n_stereo = (int)cons[1].size();
-      rep->n_mono_line = (int)cons[2].size();
-      rep->n_stereo_line = (int)cons[3].size();
+      rep->n_mono = (int)c_pose[0].size();
+      rep->n_stereo = (int)c_pose[1].size();
+      rep->n_mono_line = (int)c_pose[2].size();
+      rep->n_stereo_line = (int)c_pose[3].size();
     }
     mark();
     if (timing && ntm == 5) {
@@ -701,11 +736,6 @@ struct rspl_map {
     }
     last_fid = fid;
     last_cons_ok = true;
-    for (int t = 0; t < 4; t++) last_cons[t] = cons[t];
-    last_X = X;
-    last_L = Ls;
-    last_pq = pq;
-    last_pp = pp;
     if (!ba) return RSPL_OK;  // assembly only (rspl_map_assemble)
     const int np = (int)pose_ids.size();
     std::vector<double> rq(4 * (size_t)np), rp(3 * (size_t)np), rX(X.size()), rL(Ls.size());
@@ -750,14 +780,8 @@ struct rspl_map {
 
   // the part of Map::LocalMapOptimization after LocalmapOptimization returns (map.cc:712-802), on
   // the last assembled problem: outliers, covisibility, write-back
-  struct Con {
-    int pose, lm;
-    double obs[8];
-  };
   int last_fid = -1;
   bool last_cons_ok = false;
-  std::vector<Con> last_cons[4];
-  std::vector<double> last_X, last_L, last_pq, last_pp;
   int finish(const rspl_ba_result& R, rspl_map_report* rep) {
     if (!last_cons_ok || !frame(last_fid)) {
       set_error("rspl_map_finish: no assembled problem");
@@ -773,7 +797,6 @@ struct rspl_map {
       if (timing) tm[ntm++] = clk::now();
     };
     mark();
-    const auto& cons = last_cons;
     const int np = (int)pose_ids.size();
     const double* rq = R.pose_q;
     const double* rp = R.pose_p;
@@ -781,7 +804,7 @@ struct rspl_map {
     const double* rL = R.lines;
     const uint8_t* inl[4] = {R.mono_inlier, R.stereo_inlier, R.mono_line_inlier, R.stereo_line_inlier};
     for (int t = 0; t < 4; t++)
-      if (inl[t]) std::copy(inl[t], inl[t] + cons[t].size(), c_inl[t].begin());
+      if (inl[t]) std::copy(inl[t], inl[t] + c_pose[t].size(), c_inl[t].begin());
     if (rep) {
       rep->chi2_first = R.chi2_first;
       rep->chi2_second = R.chi2_second;
@@ -790,12 +813,16 @@ struct rspl_map {
     }
     // outliers (map.cc:712-757), in constraint order: mono then stereo points, then lines
     std::vector<std::pair<int, int>> outl, loutl;
-    for (int t = 0; t < 2; t++)
-      for (size_t i = 0; i < cons[t].size(); i++)
-        if (!c_inl[t][i] && frame(cons[t][i].pose) && point(cons[t][i].lm)) outl.push_back({cons[t][i].pose, cons[t][i].lm});
-    for (int t = 2; t < 4; t++)
-      for (size_t i = 0; i < cons[t].size(); i++)
-        if (!c_inl[t][i] && frame(cons[t][i].pose) && line(cons[t][i].lm)) loutl.push_back({cons[t][i].pose, cons[t][i].lm});
+    for (int t = 0; t < 4; t++) {
+      const std::vector<int>& ids = t < 2 ? point_ids : line_ids;
+      for (size_t i = 0; i < c_pose[t].size(); i++) {
+        if (c_inl[t][i]) continue;
+        const int f = pose_ids[c_pose[t][i]], l = ids[c_lm[t][i]];
+        if (!frame(f)) continue;
+        if (t < 2 && point(l)) outl.push_back({f, l});
+        if (t >= 2 && line(l)) loutl.push_back({f, l});
+      }
+    }
     if (rep) {
       rep->n_point_outliers = (int)outl.size();
       rep->n_line_outliers = (int)loutl.size();
