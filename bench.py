@@ -157,8 +157,7 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
              "GFLOP per step (2 pairs x 2 images x 18 layers; fp16: 19 launches of the fused layer kernel, "
              "fp32: 4 GEMM/attention launches per layer)"),
             ("sg:sinkhorn", 2 * 2 * 100 * 4 * (N + 1) * (M + 1) / 1e9, "GB/s", HBM_PEAK_GBS, "hbm",
-             {"slab": "sinkhorn_kernel<", "rb": "sinkhorn_rb_kernel"}.get(os.environ.get("RSPL_SG_SINK", "sc"),
-                                                                         "sinkhorn_sc_kernel"),
+             "sinkhorn_kernel<" if os.environ.get("RSPL_SG_SINK") == "slab" else "sinkhorn_sc_kernel",
              True, "GB per launch (2 pairs, streamed model 2*iters*4*(N+1)(M+1))"),
             ("sp:nms", 2 * 4 * H * W / 1e9, "GB/s", HBM_PEAK_GBS, "hbm", "nms_kernel", True,
              "GB per launch (2 images, 4*H*W: the score map read once)"))

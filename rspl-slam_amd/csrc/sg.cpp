@@ -40,12 +40,10 @@ struct rspl_sg {
   // RSPL_PREC_FP16 GNN activations: fp16 shadow of X, Q | K, V^T per head, messages, hidden
   _Float16 *Xh, *QKh, *Vth, *Oh, *MSGh, *HIDh;
   _Float16 *Qf[2], *Kf[2], *Vf[2];  // fused layers: q (row-major) / k, v (MFMA fragment order), ping-pong
-  unsigned long long *l4M, *l4H, *l4X;  // layer4_kernel exchange tiles (message, HID, new x) per 32-token tile
-  unsigned* l4ctr;                      // its per-tile ticket counters (zeroed per call)
   int ldv = 0;  // token stride of Vth (nmax rounded up to the 32-key attention tile; zero padded)
   unsigned long long *ug, *vg;  // Sinkhorn u / v exchange granules [B][ld] (row-block: ug = [B][2][rbG][ld])
   int rbG = 0;                  // row-block Sinkhorn workgroups per pair (0: slab kernel)
-  bool sink_sc = false;         // with rbG: the scaling-form kernel (default), else the log-domain row-block kernel
+  bool sink_sc = false;         // with rbG: the scaling-form kernel
   bool sink_wide = false;       // with sink_sc: the wide two-hop kernel (640 < nmax + 1 <= 2112)
   float* cplT = nullptr;        // transposed column slabs when they exceed LDS [B][ld*ld]
   bool sink_scratch = false;
@@ -115,11 +113,6 @@ void carve(F& ar, rspl_sg* s) {
   take(s->MSGh, T * 256); take(s->HIDh, T * 512);
   for (int i = 0; i < 2; i++) {
     take(s->Qf[i], T * 256); take(s->Kf[i], (size_t)B * 2 * 256 * s->ldv); take(s->Vf[i], (size_t)B * 2 * 256 * s->ldv);
-  }
-  {
-    const size_t nt4 = (size_t)sg::gnn_layer4_tiles((int)B, s->nmax);
-    take(s->l4M, nt4 * 32 * 256 / 4); take(s->l4H, nt4 * 32 * 512 / 4); take(s->l4X, nt4 * 32 * 256 / 4);
-    take(s->l4ctr, nt4);
   }
 
   take(s->cpl, 2 * B * ld * ld); take(s->Z, 2 * B * ld * ld); take(s->ug, ug_len(s)); take(s->vg, vg_len(s));
@@ -284,7 +277,6 @@ static hipError_t run_sinkhorn(rspl_sg* s, const float* cpl, float* Zp, const in
   sk.err = s->d_err; sk.n0 = cn0; sk.n1 = cn1;
   sk.nmax = s->nmax; sk.G = s->rbG ? s->rbG : s->G; sk.rb = s->rbG > 0; sk.sc = s->sink_sc; sk.iters = iters;
   sk.wide = s->sink_wide;
-  sk.fx = 1;
   sk.sleep = 1;
   return sg::sinkhorn(sk, B, st, t0, t1);
 }
@@ -327,15 +319,14 @@ extern "C" int rspl_sg_create(const rspl_sg_config* cfg, const char* weights_pat
     G = std::min(G, std::max(1, ncu / s->B));
     s->G = G;
     s->sink_scratch = sg::sinkhorn_lds_bytes(s->nmax, G, true) > sg::kSinkLdsMax;
-    // nmax + 1 <= 448 (640 for the scaling form): rows in registers, one exchange per iteration -- the scaling-form kernel
-    // (default, 8 workgroups per pair) or the log-domain row-block kernel (RSPL_SG_SINK=rb, 16);
-    // RSPL_SG_SINK=slab keeps the slab kernel; RSPL_SG_SINK_G sets the workgroups per pair
+    // nmax + 1 <= 640: rows in registers, one exchange per iteration -- the scaling-form kernel (8 workgroups
+    // per pair); RSPL_SG_SINK=slab keeps the slab kernel; RSPL_SG_SINK_G sets the workgroups per pair
     const char* sk = getenv("RSPL_SG_SINK");
     const std::string kind = sk ? sk : "sc";
     if (kind != "slab") {
-      int rg = kind == "rb" ? 16 : 8;
+      int rg = 8;
       if (const char* e = getenv("RSPL_SG_SINK_G")) rg = std::max(1, atoi(e));
-      s->sink_sc = kind != "rb";
+      s->sink_sc = true;
       rg = std::min(rg, std::max(1, ncu / s->B));
       while (rg <= 32 && rg * s->B <= ncu && !sg::sinkhorn_rb_rpw(s->nmax, rg)) rg++;
       if (rg * s->B <= ncu && sg::sinkhorn_rb_rpw(s->nmax, rg)) s->rbG = rg;
@@ -500,22 +491,13 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
       return g;
     };
     // RSPL_SG_GNN (A/B knob): default one launch per layer on one workgroup per 32-token tile (layer_kernel);
-    // "tile4" on four workgroups per tile (layer4_kernel, the same bits: measured slower in the pipeline -- three
-    // exchanges per layer, and 4x the CU footprint beside the BA, profiles/r05_experiments.md); "unfused" four
-    // launches per layer
-    static const int gnn_mode = [] {
+    // "unfused" four launches per layer.  (Round 5 measured the layer on four workgroups per tile -- the same
+    // bits, slower in the pipeline: profiles/r05_experiments.md -- and removed it.)
+    static const bool unfused = [] {
       const char* v = getenv("RSPL_SG_GNN");
-      return v && std::string(v) == "unfused" ? 2 : v && std::string(v) == "tile4" ? 0 : 1;
+      return v && std::string(v) == "unfused";
     }();
-    const bool unfused = gnn_mode == 2;
-    if (gnn_mode == 0)
-      RSPL_HIP(hipMemsetAsync(s->l4ctr, 0, sizeof(unsigned) * sg::gnn_layer4_tiles(B, nm), st));
-    auto layer = [&](sg::LayerArgs& la, int l) {
-      if (gnn_mode == 1) return sg::gnn_layer(la, B, st);
-      la.xM = s->l4M; la.xH = s->l4H; la.xX = s->l4X; la.ctr = s->l4ctr;
-      la.base = 12u * (unsigned)(l < 0 ? 0 : l);
-      return sg::gnn_layer4(la, B, st);
-    };
+    auto layer = [&](sg::LayerArgs& la, int) { return sg::gnn_layer(la, B, st); };
     if (!unfused) {  // layer 0's q / k / v (prologue launch), then one fused launch per layer
       {
         sg::LayerArgs la{};

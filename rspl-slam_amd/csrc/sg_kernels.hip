@@ -947,364 +947,6 @@ __global__ __launch_bounds__(512) void layer_kernel(LayerArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// One AttentionalGNN layer on FOUR workgroups per 32-token tile (fp16 engine; superglue.py:88-173).
-// layer_kernel runs a tile on one workgroup, so a layer is ~52 workgroups at C3 (N = 400, 4 token sets)
-// each streaming all 1.15 MB of the layer's weights.  Here workgroup j (256 threads) of a tile owns a
-// quarter of every phase's output columns and the four exchange their quarters through memory:
-//   (1) attention of head j (4 waves split the key tiles, merged through LDS) -> message columns 64 j..;
-//   (2) mlp.0 (merge folded) + ReLU, HID columns 128 j .. 128 j + 127 (one 32-column n-tile per wave);
-//   (3) mlp.3 + the residual, x columns 64 j .. 64 j + 63 (fp32 stream + fp16 shadow);
-//   (4) the next layer's q | k | v columns 192 j .. 192 j + 191 (three whole heads: q rows / k, v in
-//       fragment order, as layer_kernel writes them).
-// After (1), (2) and (3) a workgroup publishes its quarter (agent-scope 8-byte stores, drained, then one
-// ticket on the tile's counter) and reads the other three once the counter shows all four (a tile's
-// workgroups are dealt to one XCD).  The same MFMA operands in the same order, fp32 accumulation and
-// roundings to fp16 as layer_kernel (its attention split over two waves per head, single-chain n-tiles
-// in mlp.0 and q | k | v): the two give the same bits.  Counters are zeroed per SuperGlue call; layer l waits for
-// base + 4 (phase + 1) with base = 12 l.
-// ---------------------------------------------------------------------------
-constexpr int kL4Threads = 256;
-constexpr int kLdX = 264;  // halves per LDS row of a 256-column tile (+8: 16-byte aligned, bank spread)
-constexpr int kLdQ = 200;  // halves per row of the 192-column q | k | v staging tile
-
-__device__ __forceinline__ void st8(unsigned long long* p, unsigned long long v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ unsigned long long ld8(const unsigned long long* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// this workgroup's quarter is out (every store drained first); wait until the tile's four quarters are
-__device__ __forceinline__ void l4_exchange(unsigned* ctr, unsigned target) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) __builtin_amdgcn_s_sleep(1);
-  }
-  __syncthreads();
-}
-
-// rows x [c0, c0 + w) of an LDS tile (row stride ld halves) <-> the exchange tile (row stride lg halves),
-// 8-byte (4-half) granules, every thread a strided share
-__device__ __forceinline__ void l4_put(const _Float16* lds, int ld, int lc0, unsigned long long* g, int lg, int c0,
-                                       int w) {
-  const int per = w / 4;
-  for (int e = threadIdx.x; e < 32 * per; e += kL4Threads) {
-    const int row = e / per, q = e - row * per;
-    st8(g + (row * lg + c0) / 4 + q, *reinterpret_cast<const unsigned long long*>(lds + row * ld + lc0 + 4 * q));
-  }
-}
-__device__ __forceinline__ void l4_get(_Float16* lds, int ld, const unsigned long long* g, int lg, int c0, int w,
-                                       int skip0, int skipw) {
-  const int per = w / 4;
-  for (int e = threadIdx.x; e < 32 * per; e += kL4Threads) {
-    const int row = e / per, q = e - row * per, c = c0 + 4 * q;
-    if (c >= skip0 && c < skip0 + skipw) continue;  // this workgroup's own quarter is in LDS already
-    *reinterpret_cast<unsigned long long*>(lds + row * ld + c) = ld8(g + (row * lg + c) / 4);
-  }
-}
-
-__global__ __launch_bounds__(kL4Threads) void layer4_kernel(LayerArgs a) {
-  extern __shared__ _Float16 lds_4[];
-  _Float16* Ab = lds_4;                  // [32][kLdA]: x (0..255) | message (256..511)
-  _Float16* Ub = lds_4 + 32 * kLdA;      // union: HID [32][kLdA] | attention merge | new x [32][kLdX] + q|k|v
-  float* Om = reinterpret_cast<float*>(Ub);   // [64 d][32 q]: attention part 1's state
-  _Float16* Xn = Ub;                          // [32][kLdX] the new x (phase 4)
-  _Float16* Tq = Ub + 32 * kLdX;              // [32][kLdQ] this quarter's q | k | v
-  __shared__ float Ml[4][32], Ll[4][32];
-  const int ntl = (a.nmax + 31) / 32, ntiles = a.nsets * ntl;
-  // tile T -> XCD T % 8; its four workgroups are slots 4 (T / 8) + j of that XCD
-  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, j = slot & 3;
-  const int T = (slot >> 2) * 8 + xcd;
-  if (T >= ntiles) return;  // whole workgroup
-  const int set = T / ntl, bx = T - set * ntl;
-  const int p = set >> 1, img = set & 1;
-  const int simg = a.cross ? 1 - img : img;
-  const int nk = simg ? a.n1[p] : a.n0[p];
-  const int q0 = bx * 32;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, c = lane & 31, kh = lane >> 5;
-  const int r = lane & 31, hh = lane >> 5;
-  const size_t tok0 = (size_t)set * a.nmax + q0;
-  const int kset = p * 2 + simg;
-  unsigned long long* gM = a.xM + (size_t)T * 32 * 256 / 4;
-  unsigned long long* gH = a.xH + (size_t)T * 32 * 512 / 4;
-  unsigned long long* gX = a.xX + (size_t)T * 32 * 256 / 4;
-  unsigned* ctr = a.ctr + T;
-  if (a.qkv_only) {  // prologue: the x tile straight into Xn, then only phase (4)
-    for (int e = tid; e < 32 * 32; e += kL4Threads) {
-      const int row = e >> 5, ch = e & 31;
-      const int q = min(q0 + row, a.nmax - 1);
-      *reinterpret_cast<uint4*>(Xn + row * kLdX + 8 * ch) =
-          *reinterpret_cast<const uint4*>(a.Xh + ((size_t)set * a.nmax + q) * 256 + 8 * ch);
-    }
-    __syncthreads();
-  } else {
-    for (int e = tid; e < 32 * 32; e += kL4Threads) {
-      const int row = e >> 5, ch = e & 31;
-      const int q = min(q0 + row, a.nmax - 1);
-      *reinterpret_cast<uint4*>(Ab + row * kLdA + 8 * ch) =
-          *reinterpret_cast<const uint4*>(a.Xh + ((size_t)set * a.nmax + q) * 256 + 8 * ch);
-    }
-    // the fp32 residual values this lane updates in (3) (waves 0, 1: x columns 64 j + 32 wv + r)
-    float xres[16];
-    if (wv < 2) {
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
-        const int q = min(q0 + row, a.nmax - 1);
-        xres[i] = a.X[((size_t)set * a.nmax + q) * 256 + 64 * j + 32 * wv + r];
-      }
-    }
-    // ---- (1) attention, head h = j, as layer_kernel: waves 0 / 1 take key tiles part, part + 2, ... (two tiles
-    //      ahead in flight); part 1's state goes through LDS to part 0, which merges it into the message
-    //      columns 64 h .. 64 h + 63 of Ab (the same operations as layer_kernel: the same bits) ----
-    {
-      const int h = j, part = wv;
-      floatx16 o0, o1;
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        o0[i] = 0.f;
-        o1[i] = 0.f;
-      }
-      float m_run = -INFINITY, l_run = 0.f;
-      if (wv < 2) {
-        const _Float16* Qb = a.Qc + (size_t)set * a.nmax * 256 + h * 64;
-        const _Float16* Kb = a.Kc + ((size_t)(kset * 4 + h) * a.nt) * 4 * 512 + 8 * lane;
-        const _Float16* Vb = a.Vc + ((size_t)(kset * 4 + h) * a.nt) * 4 * 512 + 8 * lane;
-        half8 qf[4];
-        {
-          const _Float16* qr = Qb + (size_t)min(q0 + c, a.nmax - 1) * 256 + 8 * kh;
-#pragma unroll
-          for (int s4 = 0; s4 < 4; s4++) qf[s4] = *reinterpret_cast<const half8*>(qr + 16 * s4);
-        }
-        const int nkt = (nk + 31) / 32;
-        half8 kA[4], vA[2][2], kB[4], vB[2][2];
-        auto fetch = [&](int t, half8 (&kf)[4], half8 (&vf)[2][2]) {
-#pragma unroll
-          for (int s4 = 0; s4 < 4; s4++) kf[s4] = *reinterpret_cast<const half8*>(Kb + ((size_t)t * 4 + s4) * 512);
-#pragma unroll
-          for (int dt = 0; dt < 2; dt++)
-#pragma unroll
-            for (int jj = 0; jj < 2; jj++)
-              vf[dt][jj] = *reinterpret_cast<const half8*>(Vb + ((size_t)t * 4 + 2 * dt + jj) * 512);
-        };
-        auto tile = [&](int t, const half8 (&kc_)[4], const half8 (&vc)[2][2]) {
-          floatx16 st;
-#pragma unroll
-          for (int i = 0; i < 16; i++) st[i] = 0.f;
-#pragma unroll
-          for (int s4 = 0; s4 < 4; s4++) st = mfma16(kc_[s4], qf[s4], st);
-          float x[16];
-          float mx = -INFINITY;
-#pragma unroll
-          for (int i = 0; i < 16; i++) {
-            const int key = t * 32 + (i & 3) + 8 * (i >> 2) + 4 * kh;
-            x[i] = key < nk ? st[i] * 0.125f : -INFINITY;  // scores / dim**.5 (superglue.py:90)
-            mx = fmaxf(mx, x[i]);
-          }
-          mx = fmaxf(mx, __shfl_xor(mx, 32));
-          const float m_new = fmaxf(m_run, mx);
-          const float alpha = __expf(m_run - m_new);
-          float sum = 0.f;
-#pragma unroll
-          for (int i = 0; i < 16; i++) {
-            x[i] = __expf(x[i] - m_new);
-            sum += x[i];
-          }
-          sum += __shfl_xor(sum, 32);
-          l_run = l_run * alpha + sum;
-          m_run = m_new;
-#pragma unroll
-          for (int i = 0; i < 16; i++) {
-            o0[i] *= alpha;
-            o1[i] *= alpha;
-          }
-#pragma unroll
-          for (int jj = 0; jj < 2; jj++) {
-            half8 pf;
-#pragma unroll
-            for (int u = 0; u < 8; u++) pf[u] = (_Float16)x[8 * jj + u];
-            o0 = mfma16(vc[0][jj], pf, o0);
-            o1 = mfma16(vc[1][jj], pf, o1);
-          }
-        };
-        if (part < nkt) fetch(part, kA, vA);
-        if (part + 2 < nkt) fetch(part + 2, kB, vB);
-        for (int t = part; t < nkt; t += 4) {
-          tile(t, kA, vA);
-          if (t + 4 < nkt) fetch(t + 4, kA, vA);
-          if (t + 2 >= nkt) break;
-          tile(t + 2, kB, vB);
-          if (t + 6 < nkt) fetch(t + 6, kB, vB);
-        }
-        if (part == 1) {
-#pragma unroll
-          for (int i = 0; i < 16; i++) {
-            const int d = (i & 3) + 8 * (i >> 2) + 4 * kh;
-            Om[d * 32 + c] = o0[i];
-            Om[(32 + d) * 32 + c] = o1[i];
-          }
-          if (kh == 0) {
-            Ml[0][c] = m_run;
-            Ll[0][c] = l_run;
-          }
-        }
-      }
-      __syncthreads();
-      if (wv == 0) {
-        const float m1 = Ml[0][c], l1 = Ll[0][c];
-        const float M = fmaxf(m_run, m1);
-        const float e0 = m_run == -INFINITY ? 0.f : __expf(m_run - M);
-        const float e1 = m1 == -INFINITY ? 0.f : __expf(m1 - M);
-        const float L = e0 * l_run + e1 * l1;
-        const float inv = L > 0.f ? 1.f / L : 0.f;
-#pragma unroll
-        for (int i = 0; i < 16; i++) {
-          const int d = (i & 3) + 8 * (i >> 2) + 4 * kh;
-          const float v0 = (e0 * o0[i] + e1 * Om[d * 32 + c]) * inv;
-          const float v1 = (e0 * o1[i] + e1 * Om[(32 + d) * 32 + c]) * inv;
-          Ab[c * kLdA + 256 + h * 64 + d] = (_Float16)v0;
-          Ab[c * kLdA + 256 + h * 64 + 32 + d] = (_Float16)v1;
-        }
-      }
-      __syncthreads();
-    }
-    // ---- exchange the message quarters ----
-    l4_put(Ab, kLdA, 256 + 64 * j, gM, 256, 64 * j, 64);  // (the exchange tile holds message columns 0..255)
-    l4_exchange(ctr, a.base + 4);
-    {
-      const int per = 64;  // granules per row of the message
-      for (int e = tid; e < 32 * per; e += kL4Threads) {
-        const int row = e / per, cq = 4 * (e - row * per);
-        if (cq >= 64 * j && cq < 64 * j + 64) continue;
-        *reinterpret_cast<unsigned long long*>(Ab + row * kLdA + 256 + cq) = ld8(gM + (row * 256 + cq) / 4);
-      }
-    }
-    __syncthreads();
-    // ---- (2) HID = ReLU([x | message] W1^T + b1): wave wv -> columns 128 j + 32 wv .. + 31 ----
-    {
-      floatx16 acc[1];
-#pragma unroll
-      for (int i = 0; i < 16; i++) acc[0][i] = 0.f;
-      wave_mm<1, false>(Ab, a.W1, 128 * j + 32 * wv, 512, acc);
-      const int n = 128 * j + 32 * wv + r;
-      const float b = a.b1[n];
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
-        const float v = acc[0][i] + b;
-        Ub[row * kLdA + n] = (_Float16)(v > 0.f ? v : 0.f);
-      }
-    }
-    __syncthreads();
-    l4_put(Ub, kLdA, 128 * j, gH, 512, 128 * j, 128);
-    l4_exchange(ctr, a.base + 8);
-    l4_get(Ub, kLdA, gH, 512, 0, 512, 128 * j, 128);
-    __syncthreads();
-    // ---- (3) x += HID W2^T + b2: waves 0, 1 -> x columns 64 j + 32 wv .. + 31 ----
-    _Float16 xh_new[16];
-    if (wv < 2) {
-      floatx16 acc[1];
-#pragma unroll
-      for (int i = 0; i < 16; i++) acc[0][i] = 0.f;
-      wave_mm<1>(Ub, a.W2, 64 * j + 32 * wv, 512, acc);
-      const int n = 64 * j + 32 * wv + r;
-      const float b = a.b2[n];
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
-        const float x = xres[i] + (acc[0][i] + b);
-        xh_new[i] = (_Float16)x;
-        if (q0 + row < a.nmax) {
-          a.X[(tok0 + row) * 256 + n] = x;
-          a.Xh[(tok0 + row) * 256 + n] = xh_new[i];
-        }
-      }
-    }
-    if (a.last) return;
-    __syncthreads();  // HID is dead: Ub becomes the new x (+ q | k | v staging)
-    if (wv < 2) {
-      const int n = 64 * j + 32 * wv + r;
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
-        Xn[row * kLdX + n] = xh_new[i];
-      }
-    }
-    __syncthreads();
-    l4_put(Xn, kLdX, 64 * j, gX, 256, 64 * j, 64);
-    l4_exchange(ctr, a.base + 12);
-    l4_get(Xn, kLdX, gX, 256, 0, 256, 64 * j, 64);
-    __syncthreads();
-  }
-  // ---- (4) the next layer's q | k | v, columns 192 j .. 192 j + 191 (n-tiles wv and wv + 4 < 6) ----
-  {
-    const int nt = wv < 2 ? 2 : 1;
-    floatx16 acc[2];
-#pragma unroll
-    for (int t = 0; t < 2; t++)
-#pragma unroll
-      for (int i = 0; i < 16; i++) acc[t][i] = 0.f;
-    if (nt == 2) {
-      floatx16 a0[1], a1[1];
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        a0[0][i] = 0.f;
-        a1[0][i] = 0.f;
-      }
-      wave_mm<1, false>(Xn, a.Wq, 192 * j + 32 * wv, 256, a0, kLdX);
-      wave_mm<1, false>(Xn, a.Wq, 192 * j + 32 * (wv + 4), 256, a1, kLdX);
-      acc[0] = a0[0];
-      acc[1] = a1[0];
-    } else {
-      floatx16 a0[1];
-#pragma unroll
-      for (int i = 0; i < 16; i++) a0[0][i] = 0.f;
-      wave_mm<1, false>(Xn, a.Wq, 192 * j + 32 * wv, 256, a0, kLdX);
-      acc[0] = a0[0];
-    }
-    for (int t = 0; t < nt; t++) {
-      const int nl = 32 * (wv + 4 * t) + r;  // column within this quarter
-      const float b = a.bq[192 * j + nl];
-#pragma unroll
-      for (int i = 0; i < 16; i++) {
-        const int row = (i & 3) + 8 * (i >> 2) + 4 * hh;
-        Tq[row * kLdQ + nl] = (_Float16)(acc[t][i] + b);
-      }
-    }
-    __syncthreads();
-    // three whole heads of q | k | v: head slot hs covers global columns 192 j + 64 hs ..
-    const int kt = q0 >> 5;
-    for (int hs = 0; hs < 3; hs++) {
-      const int g0 = 192 * j + 64 * hs, kind = g0 / 256, hd = (g0 % 256) / 64, cl0 = 64 * hs;
-      if (kind == 0) {  // q rows: tokens x 64 dims, 16-byte stores
-        for (int e = tid; e < 32 * 8; e += kL4Threads) {
-          const int row = e >> 3, ch = e & 7;
-          if (q0 + row < a.nmax)
-            *reinterpret_cast<uint4*>(a.Qn + (tok0 + row) * 256 + 64 * hd + 8 * ch) =
-                *reinterpret_cast<const uint4*>(Tq + row * kLdQ + cl0 + 8 * ch);
-        }
-      } else {  // k / v of head hd in fragment order: 4 blocks of 1 KB
-        for (int e = tid; e < 4 * 64; e += kL4Threads) {
-          const int q4 = e >> 6, L = e & 63, cl = L & 31, kl = L >> 5;
-          _Float16* dst = (kind == 2 ? a.Vn : a.Kn) + (((size_t)(set * 4 + hd) * a.nt + kt) * 4 + q4) * 512 + 8 * L;
-          if (kind == 1) {  // k: key cl, dims 16 q4 + 8 kl .. +7
-            *reinterpret_cast<uint4*>(dst) = *reinterpret_cast<const uint4*>(Tq + cl * kLdQ + cl0 + 16 * q4 + 8 * kl);
-          } else {  // v: dim 32 dt + cl, keys 16 jj + 4 kl + {0..3, 8..11} (q4 = 2 dt + jj)
-            const int dt = q4 >> 1, jj = q4 & 1, d = cl0 + 32 * dt + cl, k0 = 16 * jj + 4 * kl;
-            half8 v;
-#pragma unroll
-            for (int u = 0; u < 8; u++) v[u] = Tq[(k0 + (u < 4 ? u : u + 4)) * kLdQ + d];
-            *reinterpret_cast<half8*>(dst) = v;
-          }
-        }
-      }
-    }
-  }
-}
-
-// ---------------------------------------------------------------------------
 // process_input + NormalizeKeypoints: one wave per token.
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void prep_kernel(PrepArgs a) {
@@ -1739,19 +1381,21 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_kernel(SinkArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Row-block log-domain Sinkhorn (superglue.py:176-205), one exchange per iteration.
-// G workgroups per pair; workgroup g holds WHOLE rows [r0, r0 + nr) of the couplings in
+// Row-block layout of the register-resident Sinkhorn (superglue.py:176-205), one exchange per
+// iteration.  G workgroups per pair; workgroup g holds WHOLE rows [r0, r0 + nr) of the couplings in
 // registers: wave w owns rows w + 16 k (k < RPW), lane L columns L + 64 q (q < kRbQ).
 // Since every wave holds full rows and a replicated v, the row pass
 //   u_i = log_mu_i - LSE_j(C_ij + v_j)
 // is wave-local (no barrier, no exchange).  The column pass
 //   v_j = log_nu_j - LSE_i(C_ij + u_i)
 // reduces each lane's columns over its wave's rows in registers, the 16 waves through LDS,
-// and the G workgroups through one all-gather of per-column partial LSEs (tagged 8-byte
+// and the G workgroups through one all-gather of per-column partials (tagged 8-byte
 // granules, double-buffered by iteration parity).  Every workgroup merges the G partials
 // in the same order (g = 0 .. G-1), so all hold a bit-identical v.  Parity reuse is safe:
 // workgroup g publishes iteration it + 2 into slot (it & 1) only after every peer has
 // published it + 1, which each peer does only after reading all of iteration it.
+// (Rounds 2-4 ran these passes in the log domain, an exp per element and iteration; the
+// scaling form below replaced that kernel.)
 // ---------------------------------------------------------------------------
 constexpr int kRbQ = 7;                 // 7 x 64 = 448 >= nmax + 1 columns per lane set
 // exp for the LSE terms: FX = false -> expf; FX = true -> v_exp_f32 on the split product
@@ -1770,183 +1414,6 @@ __device__ __forceinline__ float sk_exp(float d) {
   }
 }
 
-template <int RPW, int GM, bool FX>  // rows per wave, max workgroups per pair, fast exp
-__global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
-  __shared__ float pm[16][kRbQ * 64];   // per-wave column partial max
-  __shared__ float ps[16][kRbQ * 64];   // per-wave column partial sum
-  __shared__ float vs[kRbQ * 64];       // merged v
-  __shared__ int flag[1];
-  const int p = blockIdx.y, g = blockIdx.x, G = gridDim.x;
-  const int m = a.n0[p], n = a.n1[p];
-  if (m <= 0 || n <= 0) return;
-  const int R = m + 1, Cc = n + 1, ld = a.nmax + 1;
-  const int rs = (R + G - 1) / G;
-  const int r0 = min(R, g * rs), nr = min(R, r0 + rs) - r0;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const float* Cg = a.cpl + (size_t)p * ld * ld;
-  float x[RPW][kRbQ];
-#pragma unroll
-  for (int k = 0; k < RPW; k++) {
-    const int r = wv + 16 * k;
-#pragma unroll
-    for (int q = 0; q < kRbQ; q++) {
-      const int j = lane + 64 * q;
-      x[k][q] = (r < nr && j < Cc) ? Cg[(size_t)(r0 + r) * ld + j] : -INFINITY;
-    }
-  }
-  float vr[kRbQ];
-#pragma unroll
-  for (int q = 0; q < kRbQ; q++) vr[q] = 0.f;
-  float ur[RPW];
-#pragma unroll
-  for (int k = 0; k < RPW; k++) ur[k] = 0.f;  // iters == 0: Z = C - norm (u = v = 0)
-  const int nk = min(RPW, max(0, (nr - wv + 15) / 16));  // the wave's rows inside the slab
-  // log_mu / log_nu (superglue.py:198-200), float arithmetic as the module
-  const float fm = (float)m, fn = (float)n;
-  const float norm = -logf(fm + fn);
-  const float lmu_bin = logf(fn) + norm, lnu_bin = logf(fm) + norm;
-  if (tid == 0) flag[0] = 0;
-  __syncthreads();
-  bool failed = false;
-  for (int it = 0; it < a.iters; it++) {
-    const unsigned tag = (a.seq << 12) | (unsigned)(it + 1);
-    // row pass: all RPW rows of the wave together (independent DPP chains interleave)
-    {
-      float mx[RPW], sm[RPW];
-#pragma unroll
-      for (int k = 0; k < RPW; k++) {
-        mx[k] = x[k][0] + vr[0];
-#pragma unroll
-        for (int q = 1; q < kRbQ; q++) mx[k] = fmaxf(mx[k], x[k][q] + vr[q]);
-      }
-#pragma unroll
-      for (int k = 0; k < RPW; k++) mx[k] = wave_max_dpp(mx[k]);
-#pragma unroll
-      for (int k = 0; k < RPW; k++) {
-        sm[k] = 0.f;
-        if (k < nk)  // wave-uniform: rows past the slab end cost nothing
-#pragma unroll
-          for (int q = 0; q < kRbQ; q++) sm[k] += sk_exp<FX>((x[k][q] + vr[q]) - mx[k]);
-      }
-#pragma unroll
-      for (int k = 0; k < RPW; k++) sm[k] = wave_sum_dpp(sm[k]);
-#pragma unroll
-      for (int k = 0; k < RPW; k++) {
-        const int r = wv + 16 * k;
-        ur[k] = r < nr ? ((r0 + r) < m ? norm : lmu_bin) - (logf(sm[k]) + mx[k]) : 0.f;
-      }
-    }
-    // column partials over the wave's rows, then over the 16 waves
-#pragma unroll
-    for (int q = 0; q < kRbQ; q++) {
-      float t[RPW], cm = -INFINITY;
-#pragma unroll
-      for (int k = 0; k < RPW; k++) {
-        t[k] = x[k][q] + ur[k];
-        cm = fmaxf(cm, t[k]);
-      }
-      float cs = 0.f;
-      if (cm != -INFINITY) {
-#pragma unroll
-        for (int k = 0; k < RPW; k++)
-          if (k < nk) cs += sk_exp<FX>(t[k] - cm);
-      }
-      pm[wv][lane + 64 * q] = cm;
-      ps[wv][lane + 64 * q] = cs;
-    }
-    __syncthreads();
-    unsigned long long* slot = a.ug + (size_t)(p * 2 + (it & 1)) * G * ld;
-    // two adjacent lanes per column: lane `half` merges waves 8 half .. 8 half + 7 and polls the
-    // peers h with (h & 1) == half; the pair's results are combined by a lane swap in an order
-    // both lanes (and every workgroup) share
-    if (tid < 2 * Cc) {
-      const int j = tid >> 1, half = tid & 1;
-      float M = -INFINITY;
-#pragma unroll
-      for (int w = 0; w < 8; w++) M = fmaxf(M, pm[8 * half + w][j]);
-      float S = 0.f;
-      if (M != -INFINITY) {
-#pragma unroll
-        for (int w = 0; w < 8; w++) S += ps[8 * half + w][j] * sk_exp<FX>(pm[8 * half + w][j] - M);
-      }
-      const float Mo = __shfl_xor(M, 1), So = __shfl_xor(S, 1);
-      const float MM = fmaxf(M, Mo);
-      float own = -INFINITY;
-      if (MM != -INFINITY) {
-        const float e0 = M == -INFINITY ? 0.f : S * sk_exp<FX>(M - MM), e1 = Mo == -INFINITY ? 0.f : So * sk_exp<FX>(Mo - MM);
-        own = logf(half ? e1 + e0 : e0 + e1) + MM;  // lane 0's term first in both lanes
-      }
-      if (!half)
-        __hip_atomic_store(slot + (size_t)g * ld + j, sk_granule(own, tag), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      // all-gather of the G partials: every stale granule of this lane re-polled together
-      constexpr int GH = GM / 2;
-      float l[GH];
-      unsigned long long gv[GH];
-      unsigned pend = 0;
-#pragma unroll
-      for (int k = 0; k < GH; k++) {
-        const int h = 2 * k + half;
-        l[k] = -INFINITY;
-        if (h < G) {
-          if (h == g) l[k] = own;
-          else pend |= 1u << k;
-        }
-      }
-      bool to = a.inject && p == 0 && g == 0 && it == 0;  // fault injection (rspl_sg_debug_inject)
-      unsigned spins = 0;
-      while (pend && !to) {
-#pragma unroll
-        for (int k = 0; k < GH; k++)
-          if (pend >> k & 1)
-            gv[k] = __hip_atomic_load(slot + (size_t)(2 * k + half) * ld + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#pragma unroll
-        for (int k = 0; k < GH; k++)
-          if ((pend >> k & 1) && (unsigned)(gv[k] >> 32) == tag) {
-            l[k] = __uint_as_float((unsigned)gv[k]);
-            pend &= ~(1u << k);
-          }
-        if (!pend) break;
-        if (++spins > a.spin_limit) { to = true; break; }
-        for (int z = 0; z < a.sleep; z++) __builtin_amdgcn_s_sleep(1);  // poll spacing (fabric traffic)
-      }
-      if (to) flag[0] = 1;
-      float LM = -INFINITY;
-#pragma unroll
-      for (int k = 0; k < GH; k++) LM = fmaxf(LM, l[k]);
-      LM = fmaxf(LM, __shfl_xor(LM, 1));
-      float LS = 0.f;
-#pragma unroll
-      for (int k = 0; k < GH; k++)
-        if (l[k] != -INFINITY) LS += sk_exp<FX>(l[k] - LM);
-      const float LSo = __shfl_xor(LS, 1);
-      if (!half) vs[j] = (j < n ? norm : lnu_bin) - (logf(LS + LSo) + LM);
-    }
-    __syncthreads();
-    if (flag[0]) { failed = true; break; }
-#pragma unroll
-    for (int q = 0; q < kRbQ; q++) {
-      const int j = lane + 64 * q;
-      vr[q] = j < Cc ? vs[j] : 0.f;
-    }
-  }
-  if (failed) {
-    if (tid == 0) __hip_atomic_store(a.err + p, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    return;
-  }
-  // Z = ((couplings + u) + v) - norm (superglue.py:203, :219), own rows straight from registers
-  float* Z = a.Z + (size_t)p * ld * ld;
-#pragma unroll
-  for (int k = 0; k < RPW; k++) {
-    const int r = wv + 16 * k;
-    if (r >= nr) continue;
-#pragma unroll
-    for (int q = 0; q < kRbQ; q++) {
-      const int j = lane + 64 * q;
-      if (j < Cc) Z[(size_t)(r0 + r) * ld + j] = ((x[k][q] + ur[k]) + vr[q]) - norm;
-    }
-  }
-}
-
 // ---------------------------------------------------------------------------
 // Scaling-form Sinkhorn (the default for nmax + 1 <= 640): the same iterations as
 // log_sinkhorn_iterations (superglue.py:176-183) written on the scalings U = exp(u - a),
@@ -1958,7 +1425,7 @@ __global__ __launch_bounds__(kSinkThreads) void sinkhorn_rb_kernel(SinkArgs a) {
 // which bounds K by mu (<= 1).  A scaling that leaves [2^-60, 2^60] is absorbed into a / b and K
 // is recomputed from C: rows per workgroup (a is workgroup-local), columns on every workgroup
 // alike (V is bit-identical everywhere, so every workgroup decides the same).  Layout, exchange
-// and determinism as the row-block kernel: G workgroups per pair hold whole rows (wave w rows
+// and determinism as the row-block layout above: G workgroups per pair hold whole rows (wave w rows
 // w + 16 k, lane L columns L + 64 q), the row pass is wave-local, the column sums go through LDS
 // across waves and ONE all-gather of per-column partial sums across workgroups per iteration,
 // merged in the same order everywhere.  Z = ((C + u) + v) - norm from C re-read at the end.
@@ -2703,26 +2170,6 @@ hipError_t gnn_layer(const LayerArgs& a, int B, hipStream_t s) {
   return hipGetLastError();
 }
 
-int gnn_layer4_tiles(int B, int nmax) { return B * 2 * ((nmax + 31) / 32); }
-
-hipError_t gnn_layer4(const LayerArgs& a, int B, hipStream_t s) {
-  constexpr size_t lds = sizeof(_Float16) * 2 * 32 * kLdA;  // x | message, and the HID / merge / new x + q|k|v union
-  static_assert(32 * kLdX + 32 * kLdQ <= 32 * kLdA, "new x + q | k | v staging exceeds the HID carve");
-  static bool attr = false;
-  if (!attr) {
-    const hipError_t e = hipFuncSetAttribute((const void*)layer4_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                             (int)lds);
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
-  LayerArgs la = a;
-  la.nsets = B * 2;
-  const int tiles = gnn_layer4_tiles(B, a.nmax);
-  // tile T on XCD T % 8, its four workgroups at slots 4 (T / 8) .. + 3 of that XCD (block = 8 slot + xcd)
-  hipLaunchKernelGGL(layer4_kernel, dim3(8 * 4 * ((tiles + 7) / 8)), dim3(kL4Threads), lds, s, la);
-  return hipGetLastError();
-}
-
 // n-major fp16 weights Wt [N][K] -> 32x32x16 MFMA B-fragment order: block (nt, ks) = the 64 lanes'
 // 16-byte operands of n-tile nt, k-step ks, lane L = r + 32 h holding Wt[32 nt + r][16 ks + 8 h ..];
 // a wave's operand load is then one contiguous 1 KB read
@@ -2812,22 +2259,7 @@ hipError_t sinkhorn(const SinkArgs& a, int B, hipStream_t s, hipEvent_t t0, hipE
     }
     return hipGetLastError();
   }
-  if (a.rb) {  // row-block kernel: the workgroup count must match an instantiated (RPW, GM)
-    switch (sinkhorn_rb_rpw(a.nmax, a.G)) {
-#define RSPL_SK_RB(R, M)                                                                                      \
-  case R:                                                                                                     \
-    if (a.fx) hipExtLaunchKernelGGL((sinkhorn_rb_kernel<R, M, true>), grid, dim3(kSinkThreads), 0, s, t0, t1, 0, a); \
-    else hipExtLaunchKernelGGL((sinkhorn_rb_kernel<R, M, false>), grid, dim3(kSinkThreads), 0, s, t0, t1, 0, a);    \
-    break;
-      RSPL_SK_RB(8, 4)
-      RSPL_SK_RB(4, 8)
-      RSPL_SK_RB(2, 16)
-      RSPL_SK_RB(1, 32)
-#undef RSPL_SK_RB
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
+  if (a.rb) return hipErrorInvalidValue;  // (the row-block layout runs the scaling form only)
   const size_t full = sinkhorn_lds_bytes(a.nmax, a.G, true);
   if (full <= kSinkLdsMax) {
     static size_t attr = 0;

@@ -91,12 +91,6 @@ struct LayerArgs {
   int cross, last;
   int qkv_only;          // prologue: only phase (4) from the current x (layer 0's q / k / v)
   int nsets, xps, tpx;   // set by gnn_layer: token sets, XCDs per set (0 = plain grid), tiles per XCD
-  // layer4_kernel (four workgroups per 32-token tile): exchange tiles of the message [tile][32][256], HID
-  // [tile][32][512] and new x [tile][32][256] (fp16 as 8-byte granules), a ticket counter per tile (zeroed per
-  // SuperGlue call) and this launch's counter base (12 per layer)
-  unsigned long long *xM, *xH, *xX;
-  unsigned* ctr;
-  unsigned base;
 };
 
 struct PrepArgs {
@@ -134,7 +128,7 @@ struct SinkArgs {
   const float* cpl;   // couplings [B][ld*ld]
   float* Z;           // [B][ld*ld]
   float* cplT;        // [B][ld*ld] transposed column slabs (scratch; only when the slabs exceed LDS)
-  unsigned long long* ug;  // [B][ld] tagged u granules {f32 bits, tag}; row-block kernel: [B][2][G][ld] partial LSEs
+  unsigned long long* ug;  // [B][ld] tagged u granules {f32 bits, tag}; row-block layout: [B][2][G][ld] partial sums
   unsigned long long* vg;  // [B][ld] tagged v granules
   unsigned seq;       // per-call tag base (never 0; granules start zeroed)
   unsigned spin_limit;  // bounded polls per granule before the exchange is declared timed out
@@ -143,9 +137,8 @@ struct SinkArgs {
   const int* n0;
   const int* n1;
   int nmax, G, iters;
-  int rb;             // 1: row-block kernel (rows in registers, one exchange per iteration)
-  int sleep;          // row-block kernel: s_sleep(1) units between re-polls (run_sinkhorn: 1)
-  int fx;             // row-block kernel: v_exp_f32-based exp (1, what run_sinkhorn sets) or expf (0)
+  int rb;             // 1: row-block layout (rows in registers, one exchange per iteration; with sc)
+  int sleep;          // row-block layout: s_sleep(1) units between re-polls (run_sinkhorn: 1)
   int sc;             // with rb: the scaling-form kernel (register-resident exp(C + a + b), two mat-vecs per iteration)
   int wide;           // with sc: the wide two-hop kernel (640 < nmax + 1 <= 2112; ug / vg laid out as its hop buffers)
 };
@@ -172,9 +165,6 @@ hipError_t to_frag(const _Float16* Wt, int N, int K, _Float16* out, hipStream_t 
 hipError_t gemm_h(const GemmHArgs& a, int mode, hipStream_t s);
 hipError_t attention_h(const AttnHArgs& a, int B, hipStream_t s);
 hipError_t gnn_layer(const LayerArgs& a, int B, hipStream_t s);
-// the same layer on four workgroups per 32-token tile (layer4_kernel; a.xM / xH / xX / ctr / base set)
-hipError_t gnn_layer4(const LayerArgs& a, int B, hipStream_t s);
-int gnn_layer4_tiles(int B, int nmax);  // exchange tiles / counters the handle allocates
 // fp32 -> fp16, n elements
 hipError_t to_half(const float* x, _Float16* y, size_t n, hipStream_t s);
 hipError_t prep(const PrepArgs& a, hipStream_t s);
