@@ -387,6 +387,11 @@ void report_prof(rspl_ba* b) {
           us(u0, last(ba::kProfUe, 0, nbu, 2)), us(u0, last(ba::kProfUe, 0, nbu, 3)),
           us(u0, last(ba::kProfUe, nbu, nue, 1)), us(u0, last(ba::kProfUe, nbu, nue, 2)),
           us(u0, last(ba::kProfUe, nbu, nue, 3)), us(h[1], h[5]), us(h[5], h[6]), us(h[6], h[7]), us(h[7], h[8]));
+  fprintf(stderr,
+          "ba_prof setup us: landmarks %.1f +pdiag %.1f lines %.1f +pdiag %.1f pairs %.1f | blocks done %.1f scan %.1f "
+          "pose diagonals + control %.1f\n",
+          us(h[9], h[13]), us(h[9], h[14]), us(h[9], h[15]), us(h[9], h[5]), us(h[9], h[6]), us(h[9], h[10]),
+          us(h[10], h[11]), us(h[11], h[12]));
   {  // per chunk: start -> loop done, quantiles over the diagonal / off-diagonal pose pairs' chunks
     const int nchk = b->prof_nb[3], K = b->prof_nb[4];
     std::vector<double> dg, od;
@@ -477,7 +482,9 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
       b->pdg_cap = cap;
       b->grew |= 4;
     }
-    RSPL_HIP(ba::setup_dev(P, Lr, A, S, cls_level, cls_level ? const_cast<uint8_t*>(A.lm_act) : nullptr, iters,
+    ba::Sys Su = S;  // RSPL_BA_PROF: the first optimize's setup phases too
+    Su.prof = b->prof && !b->prof_nb[0] && !cls_level ? b->prof : nullptr;
+    RSPL_HIP(ba::setup_dev(P, Lr, A, Su, cls_level, cls_level ? const_cast<uint8_t*>(A.lm_act) : nullptr, iters,
                            build_pp ? b->pp_cnt : nullptr, b->pp_off, b->pp_buf, b->pdg, st));
   } else {  // A/B knob: the separate launches (build_pairs, classify, landmark_active, errors, linearize,
             // pose_diag, post)

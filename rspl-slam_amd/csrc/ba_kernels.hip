@@ -1493,6 +1493,13 @@ __device__ __forceinline__ double setup_landmark(const Problem& P, const Lin& L,
   return chi;
 }
 
+__device__ __forceinline__ void prof_stamp(const Sys& S, int slot) {
+  if (S.prof) S.prof[slot] = wall_clock64();
+}
+__device__ __forceinline__ void prof_max(const Sys& S, int slot) {  // latest over the blocks
+  if (S.prof) atomicMax(S.prof + slot, (unsigned long long)wall_clock64());
+}
+
 // The first pass in ONE launch: blocks [0, nbq) landmark groups, [nbq, nb_lm) line workgroups,
 // [nb_lm, ...) pair counting; every landmark / line block then sums the pose diagonals of its own
 // edges (pose_diag_range -> pdg) and every block takes a ticket; the last block sums the cost
@@ -1505,26 +1512,32 @@ __global__ __launch_bounds__(256) void setup_kernel(Problem P, Lin L, Active A, 
   __shared__ double part[4][64];
   __shared__ int last;
   const int b = blockIdx.x;
+  if (b == 0 && threadIdx.x == 0) prof_stamp(S, 9);
   if (b >= nb_lm) {  // the first optimize: edge pairs per Schur chunk, one wave per chunk
     const int c = (b - nb_lm) * 4 + (threadIdx.x >> 6);
     if (c < A.npairs * A.nchk) pair_scan<false>(A, c, pp_cnt, nullptr, nullptr);
+    if (threadIdx.x == 0) prof_max(S, 6);
   } else if (b >= nbq) {
     double c = 0.0;  // set in thread 0
     lin_lines<kLinSetup>(P, L, A, S, b - nbq, true, nullptr, nullptr, 0.0, false, nullptr, level != nullptr, &c);
     if (threadIdx.x == 0) __hip_atomic_store(S.partial + b, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (threadIdx.x == 0) prof_max(S, 15);
     const int4 tb = A.ltab[b - nbq];
     pose_diag_range(P, L, A, pdg, nb_lm, b, tb.x, tb.x + (tb.y & 0xff));
+    if (threadIdx.x == 0) prof_max(S, 5);
   } else {
     double acc[1] = {setup_landmark(P, L, A, S, b * 256 + threadIdx.x, level, lm_act2)};
     block_reduce<1>(acc, red);
     if (threadIdx.x == 0) __hip_atomic_store(S.partial + b, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    if (threadIdx.x == 0) prof_max(S, 13);
     // this block's point landmarks' edges: one CSR range
     const int g0 = min(b * (256 / kGroup), P.nq), g1 = min(b * (256 / kGroup) + 256 / kGroup, P.nq);
     pose_diag_range(P, L, A, pdg, nb_lm, b, A.lm_off[g0], A.lm_off[g1]);
+    if (threadIdx.x == 0) prof_max(S, 14);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1532,6 +1545,7 @@ __global__ __launch_bounds__(256) void setup_kernel(Problem P, Lin L, Active A, 
   __syncthreads();
   if (!last) return;
   // ---- the last block ----
+  if (threadIdx.x == 0) prof_stamp(S, 10);
   double cs[1] = {0.0};  // the cost: the landmark / line blocks' partials, fixed order
   for (int k = threadIdx.x; k < nb_lm; k += 256) cs[0] += __hip_atomic_load(S.partial + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   block_reduce<1>(cs, red);
@@ -1557,6 +1571,7 @@ __global__ __launch_bounds__(256) void setup_kernel(Problem P, Lin L, Active A, 
     }
     if (tid == 255) pp_off[nc] = sc[255];
   }
+  if (threadIdx.x == 0) prof_stamp(S, 11);
   // per pose and diagonal entry q = 6 pose + i: 4 waves each sum every 4th block partial
   const int lane = threadIdx.x & 63, pt = threadIdx.x >> 6, nq6 = 6 * A.K, npd = nb_lm;
   double mx = 0;
@@ -1587,6 +1602,7 @@ __global__ __launch_bounds__(256) void setup_kernel(Problem P, Lin L, Active A, 
   for (int o = 32; o >= 1; o >>= 1) mx = fmax(mx, __shfl_xor(mx, o));
   if (lane != 0) return;
   __hip_atomic_store(S.counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  prof_stamp(S, 12);
   // the landmark diagonal maximum (atomic max of the landmark blocks: performed device-coherently)
   const double md = fmax(__hip_atomic_load(S.out + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), mx);
   S.out[0] = chi2;
@@ -1607,9 +1623,6 @@ __global__ __launch_bounds__(256) void setup_kernel(Problem P, Lin L, Active A, 
 // segment of the edge-pair lists, forming Y = Hpl_e1 Dinv_g on the fly:
 //   [0,36)  [e1==e2] Hpp_e1 - Y Hpl_e2^T,   [36,42) [e1==e2] bp_e1,   [42,48) [e1==e2] Y bl_g
 // then the wave sums its 64 lanes in lane order (LDS transpose).
-__device__ __forceinline__ void prof_stamp(const Sys& S, int slot) {
-  if (S.prof) S.prof[slot] = wall_clock64();
-}
 
 // larger systems, stage 2: one thread per (pose pair, entry) scatters the pair sums.
 //   S_ab = [a==b] lambda I + pair sum,  bp_a,  bs_a = bp_a - sum Y bl  (solved in place in x)
