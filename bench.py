@@ -148,7 +148,9 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
          **{f"sg:{n}": v / max(1, sg_calls) for n, v in zip(sg.STAGES, sg_ms)}}
     N = M = K
     mfma_peak = FP16_MFMA_PEAK if precision == "fp16" else FP32_MFMA_PEAK
-    conv1_k = ("conv3x3_h_kernel<64, 16, true, true, false>" if precision == "fp16"
+    # fp16: the persistent conv1 kernel (RSPL_SP_CONV1=stage: the per-stage fused conv1a kernel)
+    conv1_k = (("conv3x3_h_kernel<64, 16, true, true, false>" if os.environ.get("RSPL_SP_CONV1") == "stage"
+                else "conv1_res_kernel") if precision == "fp16"
                else "conv3x3_kernel<64, 16, true, true>")
     rows = (("sp:conv1a+1b+pool", 2 * conv1_gflop_per_image(), "TFLOP/s", mfma_peak, "mfma", conv1_k, True,
              "GFLOP per launch (2 images, conv1a+conv1b)"),
