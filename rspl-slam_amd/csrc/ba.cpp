@@ -411,6 +411,25 @@ void report_prof(rspl_ba* b) {
             "ndiag %zu noff %zu\n", q(dg, 0.5), q(dg, 0.9), q(dg, 1.0), q(od, 0.5), q(od, 0.9), q(od, 1.0),
             dg.size(), od.size());
   }
+  {  // line workgroups of update_errors: per block start -> operands (wait), -> evaluations (comp), -> end
+    std::vector<double> w, c, e, tot;
+    for (int i = nbu; i < std::min(nue, 4096); i++) {
+      const unsigned long long* r = &h[ba::kProfUe + 4 * i];
+      if (!r[0] || !r[1] || !r[2] || !r[3]) continue;
+      w.push_back((r[1] - (double)r[0]) / 100.0);
+      c.push_back((r[2] - (double)r[1]) / 100.0);
+      e.push_back((r[3] - (double)r[2]) / 100.0);
+      tot.push_back((r[3] - (double)u0) / 100.0);
+    }
+    auto q = [](std::vector<double> v, double f) {
+      if (v.empty()) return -1.0;
+      std::sort(v.begin(), v.end());
+      return v[std::min(v.size() - 1, (size_t)(f * v.size()))];
+    };
+    fprintf(stderr, "ba_lines us (p50/p90/max): operands %.1f/%.1f/%.1f evals %.1f/%.1f/%.1f tail %.1f/%.1f/%.1f "
+            "end %.1f/%.1f/%.1f n %zu\n", q(w, .5), q(w, .9), q(w, 1), q(c, .5), q(c, .9), q(c, 1), q(e, .5), q(e, .9),
+            q(e, 1), q(tot, .5), q(tot, .9), q(tot, 1), w.size());
+  }
   if (getenv("RSPL_BA_SOLVE") && std::string(getenv("RSPL_BA_SOLVE")) == "blk4") {
     fprintf(stderr, "ba_steps us:");  // blocked solve: each pose block's panel, from the assembly's end
     for (int k = 5; k < 15 && h[k]; k++) fprintf(stderr, " %.2f", us(h[1], h[k]));

@@ -1097,34 +1097,97 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
     *chi_out = c;
   }
   // J layout per edge: Jp [4][6] at 0, Jl [4][4] at 24 (the analytic path wrote it directly)
+  // every J entry of every slot (rows >= edim(t) and slots that are not live: exact zeros), and each
+  // slot's robust weight once (SPEC / SETUP: the slot's own error; else the edge's stored one)
+  __shared__ double wsh[kLineBlk];
   for (int idx = tid; idx < (P.line_jac ? 0 : 40 * kLineBlk); idx += 256) {
     const int slot = idx / 40, rd = idx - 40 * slot, r = rd / 10, d = rd % 10;
     int e, t;
     bool on, live;
     edge(slot, e, t, on, live);
-    if (live && r < edim(t)) {
-      const double v = scal * (ev[slot][2 * d][r] - ev[slot][2 * d + 1][r]);
-      if (d < 4) J[slot][24 + r * 4 + d] = v;
-      else J[slot][r * 6 + (d - 4)] = v;
-    }
+    const double v = (live && r < edim(t)) ? scal * (ev[slot][2 * d][r] - ev[slot][2 * d + 1][r]) : 0.0;
+    if (d < 4) J[slot][24 + r * 4 + d] = v;
+    else J[slot][r * 6 + (d - 4)] = v;
   }
-  __syncthreads();
-  for (int idx = tid; idx < 86 * kLineBlk; idx += 256) {
-    const int slot = idx / 86, o = idx - 86 * slot;
+  if (tid >= 192 && tid < 192 + kLineBlk) {
+    const int slot = tid - 192;
     int e, t;
     bool on, live;
     edge(slot, e, t, on, live);
-    if (!on) continue;
     const double* er = OWN_ERR ? &es[slot][0] : L.err + 4 * e;
-    const double w = live ? edge_weight_of(P, A, er, t) : 0.0;
-    const double v = live ? contrib(o, edim(t), 4, w, er, &J[slot][0], &J[slot][24]) : 0.0;
-    if (o < 20) {
-      cv[slot][o] = v;
-      if (split)
-        __hip_atomic_store(o < 16 ? L.Hll + 16 * e + o : L.bl + 4 * e + o - 16, v, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+    wsh[slot] = live ? edge_weight_of(P, A, er, t) : 0.0;
+  }
+  __syncthreads();
+  // the 86 contributions per edge (contrib's layout: Hll, bl, Hpp, bp, Hpl), one kind per pass so that
+  // a wave never diverges between kinds; four rows unrolled (the rows past edim(t) are zeros and add
+  // exact zeros: the same sums, in the same order, as contrib()).  Hpp: the 21 upper entries stored.
+  auto rowsum = [&](const double* x, int sx, const double* y, int sy) {
+    double t0 = x[0], t1 = x[sx], t2 = x[2 * sx], t3 = x[3 * sx];
+    double u0 = y[0], u1 = y[sy], u2 = y[2 * sy], u3 = y[3 * sy];
+    double s = 0;
+    s += t0 * u0;
+    s += t1 * u1;
+    s += t2 * u2;
+    s += t3 * u3;
+    return s;
+  };
+  auto slot_of = [&](int idx, int per, int& e, int& t, bool& live, bool& popt) {
+    const int slot = idx / per;
+    bool on;
+    edge(slot, e, t, on, live);
+    popt = (einfo_s[slot][2] & 4) != 0;
+    return on ? slot : -1;
+  };
+  for (int idx = tid; idx < 20 * kLineBlk; idx += 256) {  // Hll (o < 16), bl
+    int e, t;
+    bool live, popt;
+    const int slot = slot_of(idx, 20, e, t, live, popt);
+    if (slot < 0) continue;
+    const int o = idx - 20 * slot;
+    const double* Jl = &J[slot][24];
+    double v;
+    if (o < 16) {
+      v = live ? wsh[slot] * rowsum(Jl + o / 4, 4, Jl + o % 4, 4) : 0.0;
     } else {
-      store_contrib(L, P.Ep, e, o, v, (einfo_s[slot][2] & 4) != 0);
+      const double* er = OWN_ERR ? &es[slot][0] : L.err + 4 * e;
+      double eb[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) eb[r] = r < edim(t) ? er[r] : 0.0;
+      v = live ? -wsh[slot] * rowsum(Jl + (o - 16), 4, eb, 1) : 0.0;
+    }
+    cv[slot][o] = v;
+    if (split)
+      __hip_atomic_store(o < 16 ? L.Hll + 16 * e + o : L.bl + 4 * e + o - 16, v, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  }
+  for (int idx = tid; idx < 21 * kLineBlk; idx += 256) {  // Hpp, upper triangle (pk6 order)
+    int e, t;
+    bool live, popt;
+    const int slot = slot_of(idx, 21, e, t, live, popt);
+    if (slot < 0 || !popt) continue;
+    const int q = idx - 21 * slot;
+    int a = 0, base = 0;
+    while (q >= base + 6 - a) base += 6 - a++;
+    const int b = a + (q - base);
+    const double* Jp = &J[slot][0];
+    L.Hpp[21 * e + q] = live ? wsh[slot] * rowsum(Jp + a, 6, Jp + b, 6) : 0.0;
+  }
+  for (int idx = tid; idx < 30 * kLineBlk; idx += 256) {  // bp (k < 6), Hpl (6 x 4)
+    int e, t;
+    bool live, popt;
+    const int slot = slot_of(idx, 30, e, t, live, popt);
+    if (slot < 0 || !popt) continue;
+    const int k = idx - 30 * slot;
+    const double* Jp = &J[slot][0];
+    if (k < 6) {
+      const double* er = OWN_ERR ? &es[slot][0] : L.err + 4 * e;
+      double eb[4];
+#pragma unroll
+      for (int r = 0; r < 4; r++) eb[r] = r < edim(t) ? er[r] : 0.0;
+      L.bp[6 * e + k] = live ? -wsh[slot] * rowsum(Jp + k, 6, eb, 1) : 0.0;
+    } else {
+      const int a = (k - 6) / 4, b = (k - 6) % 4;
+      L.Hpl[hpl_off(P.Ep, e) + k - 6] = live ? wsh[slot] * rowsum(Jp + a, 6, &J[slot][24] + b, 4) : 0.0;
     }
   }
   if (!split) {  // whole landmarks: their blocks from this workgroup's records, CSR (slot) order
