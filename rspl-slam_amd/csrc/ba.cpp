@@ -390,7 +390,8 @@ void report_prof(rspl_ba* b) {
   fprintf(stderr,
           "ba_prof setup us: landmarks %.1f +pdiag %.1f lines %.1f +pdiag %.1f pairs %.1f | blocks done %.1f scan %.1f "
           "pose diagonals + control %.1f\n",
-          us(h[9], h[13]), us(h[9], h[14]), us(h[9], h[15]), us(h[9], h[5]), us(h[9], h[6]), us(h[9], h[10]),
+          us(h[9], h[ba::kProfX]), us(h[9], h[ba::kProfX + 1]), us(h[9], h[ba::kProfX + 2]),
+          us(h[9], h[ba::kProfX + 3]), us(h[9], h[ba::kProfX + 4]), us(h[9], h[10]),
           us(h[10], h[11]), us(h[11], h[12]));
   {  // per chunk: start -> loop done, quantiles over the diagonal / off-diagonal pose pairs' chunks
     const int nchk = b->prof_nb[3], K = b->prof_nb[4];

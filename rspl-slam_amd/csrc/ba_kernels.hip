@@ -634,7 +634,8 @@ __device__ __forceinline__ void point_pose_terms(const double (&Jp)[3][6], doubl
 template <bool PDIAG>
 __device__ __forceinline__ void point_edge_core(const Problem& P, const Lin& L, const Active& A, int e, int t,
                                                 bool pose_opt, const SE3& T, const double* cam, const double* Xg,
-                                                const double* er4, double (&hl)[9], double (&bv)[3]) {
+                                                const double* er4, double (&hl)[9], double (&bv)[3],
+                                                double* dg6 = nullptr) {
   double Jp[3][6], Jl[3][3];
   point_jac(t, T, cam, Xg, Jp, Jl);
   const bool st = t == 1;
@@ -650,7 +651,11 @@ __device__ __forceinline__ void point_edge_core(const Problem& P, const Lin& L, 
   double* Hpl = L.Hpl + 18 * e;  // (hpl_off: a point edge)
 #pragma unroll
   for (int a = 0; a < 6; a++) {
-    if (PDIAG) L.Hpp[21 * e + pk6(a, a)] = w * (Jp[0][a] * Jp[0][a] + Jp[1][a] * Jp[1][a] + Jp[2][a] * Jp[2][a]);
+    if (PDIAG) {
+      const double d = w * (Jp[0][a] * Jp[0][a] + Jp[1][a] * Jp[1][a] + Jp[2][a] * Jp[2][a]);
+      L.Hpp[21 * e + pk6(a, a)] = d;
+      if (dg6) dg6[a] = d;
+    }
 #pragma unroll
     for (int b = 0; b < 3; b++) Hpl[a * 3 + b] = w * (Jp[0][a] * Jl[0][b] + Jp[1][a] * Jl[1][b] + Jp[2][a] * Jl[2][b]);
   }
@@ -906,7 +911,8 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
                                           bool maxd, const Lin* Lc = nullptr, const Sys* Sc = nullptr,
                                           double lambda = 0.0, bool failed = false,
                                           unsigned long long* stamp = nullptr, bool cls = false,
-                                          double* chi_out = nullptr) {
+                                          double* chi_out = nullptr, double* pdg = nullptr, int pd_nb = 0,
+                                          int pd_b = 0) {
   constexpr bool SPEC = MODE == kLinSpec, SETUP = MODE == kLinSetup, OWN_ERR = SPEC || SETUP;
   __shared__ double ev[kLineBlk][20][4];
   __shared__ double J[kLineBlk][4 * 6 + 4 * 4];
@@ -1190,6 +1196,21 @@ __device__ __forceinline__ void lin_lines(const Problem& P, const Lin& L, const 
       L.Hpl[hpl_off(P.Ep, e) + k - 6] = live ? wsh[slot] * rowsum(Jp + a, 6, &J[slot][24] + b, 4) : 0.0;
     }
   }
+  if (SETUP && pdg)  // computeLambdaInit's pose-diagonal partials of this workgroup's edges (slot order), as
+                    // the Hpp pass's diagonal entries (pose_diag_range's slots)
+    for (int q = tid; q < 6 * A.K; q += 256) {
+      const int j = q / 6, i = q - 6 * j;
+      double sm = 0;
+      for (int slot = 0; slot < cnt; slot++) {
+        int e, t;
+        bool on, live;
+        edge(slot, e, t, on, live);
+        if (!(einfo_s[slot][2] & 4) || A.pidx[P.epose[e]] != j) continue;
+        const double* Jp = &J[slot][0];
+        sm += live ? wsh[slot] * rowsum(Jp + i, 6, Jp + i, 6) : 0.0;
+      }
+      __hip_atomic_store(pdg + ((size_t)j * pd_nb + pd_b) * 6 + i, sm, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   if (!split) {  // whole landmarks: their blocks from this workgroup's records, CSR (slot) order
     __syncthreads();
     if (tid < 20 * (ge - gb)) {
@@ -1379,6 +1400,40 @@ __device__ __forceinline__ void pose_diag_range(const Problem& P, const Lin& L, 
   }
 }
 
+// pose_diag_range from the per-edge diagonals a landmark block staged in LDS (pd / pa: the block's n CSR edges,
+// pose index or -1): wave w sums its quarter of the edges per (pose, entry) in edge order, the four quarters
+// then in wave order -- no wait for the block's record stores, no reload
+constexpr int kPdCap = 512;  // edges per landmark block staged (more: pose_diag_range)
+__device__ __forceinline__ void pose_diag_lds(const Active& A, const double (*pd)[6], const int* pa, int n, double* dst,
+                                              int nb, int b) {
+  __shared__ double ws[4][64];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int l0 = (n * wv) / 4, l1 = (n * (wv + 1)) / 4, nq = 6 * A.K;
+  for (int q0 = 0; q0 < nq; q0 += 64) {
+    const int q = q0 + lane, j = q / 6, i = q - 6 * j;
+    double sm = 0;
+    if (q < nq)
+      for (int l = l0; l < l1; l += 8) {  // eight LDS reads in flight, summed in edge order
+        int pv[8];
+        double dv[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          const bool ok = l + u < l1;
+          pv[u] = ok ? pa[l + u] : -1;
+          dv[u] = ok ? pd[l + u][i] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) sm += pv[u] == j ? dv[u] : 0.0;
+      }
+    ws[wv][lane] = sm;
+    __syncthreads();
+    if (wv == 0 && q < nq)
+      __hip_atomic_store(dst + ((size_t)j * nb + b) * 6 + i, ((ws[0][lane] + ws[1][lane]) + ws[2][lane]) + ws[3][lane],
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+  }
+}
+
 
 // ---------------------------------------------------------------------------
 // Schur complement for damping lambda
@@ -1397,62 +1452,80 @@ __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, c
   const int pr = c / A.nchk, lb = c - pr * A.nchk;
   const int pa = A.pairs[2 * pr], pb = A.pairs[2 * pr + 1];
   int base = FILL ? pp_off[c] : 0;
-  for (int r = 0; r < A.lmchunk / 64; r++) {
-    const int g = lb * A.lmchunk + 64 * r + lane;
-    int k0 = 0, k1 = 0;
-    if (g < A.nL && A.lm_act[g]) {
-      k0 = A.lm_off[g];
-      k1 = A.lm_off[g + 1];
+  const int nr = A.lmchunk / 64;
+  // four landmark rounds at a time: their CSR ranges, then the first eight edge poses of each (a landmark's
+  // whole edge list when it has <= 8 edges, the common case), every load of a group in flight at once
+  for (int r0 = 0; r0 < nr; r0 += 4) {
+    int k0[4], k1[4], pz[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const int g = lb * A.lmchunk + 64 * (r0 + u) + lane;
+      const bool in = r0 + u < nr && g < A.nL;
+      const int o0 = in ? A.lm_off[g] : 0, o1 = in ? A.lm_off[g + 1] : 0;
+      const bool act = in && A.lm_act[g];
+      k0[u] = act ? o0 : 0;
+      k1[u] = act ? o1 : 0;
     }
-    int cnt = 0;
-    unsigned ma1 = 0, mb1 = 0;  // the masks when the landmark has <= 8 edges (one block each)
-    for (int ib = k0; ib < k1; ib += 8) {  // i blocks
-      unsigned ma = 0;
-      int pi[8];
 #pragma unroll
-      for (int u = 0; u < 8; u++) pi[u] = A.lm_pose[min(ib + u, k1 - 1)];
+    for (int u = 0; u < 4; u++)
 #pragma unroll
-      for (int u = 0; u < 8; u++) ma |= (ib + u < k1 && pi[u] == pa) ? 1u << u : 0u;
-      if (!ma) continue;
-      for (int jb = k0; jb < k1; jb += 8) {  // j blocks
-        unsigned mb = 0;
-        int pj[8];
+      for (int v = 0; v < 8; v++) pz[u][v] = k1[u] > k0[u] ? A.lm_pose[min(k0[u] + v, k1[u] - 1)] : -1;
 #pragma unroll
-        for (int u = 0; u < 8; u++) pj[u] = A.lm_pose[min(jb + u, k1 - 1)];
+    for (int u = 0; u < 4; u++) {
+      if (r0 + u >= nr) break;  // uniform
+      const int g = lb * A.lmchunk + 64 * (r0 + u) + lane;
+      const int e0 = k0[u], e1 = k1[u];
+      int cnt = 0;
+      unsigned ma1 = 0, mb1 = 0;  // the masks when the landmark has <= 8 edges (one block each)
+      if (e1 - e0 <= 8) {
+        unsigned ma = 0, mb = 0;
 #pragma unroll
-        for (int u = 0; u < 8; u++) mb |= (jb + u < k1 && pj[u] == pb) ? 1u << u : 0u;
-        cnt += __popc(ma) * __popc(mb);
+        for (int v = 0; v < 8; v++) {
+          ma |= (e0 + v < e1 && pz[u][v] == pa) ? 1u << v : 0u;
+          mb |= (e0 + v < e1 && pz[u][v] == pb) ? 1u << v : 0u;
+        }
+        cnt = ma ? __popc(ma) * __popc(mb) : 0;
         ma1 = ma;
         mb1 = mb;
-      }
-    }
-    // wave exclusive prefix of the per-lane counts (lane order)
-    int pre = cnt;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int t = __shfl_up(pre, o);
-      if (lane >= o) pre += t;
-    }
-    const int total = __shfl(pre, 63);
-    if (FILL && cnt && k1 - k0 <= 8) {  // emit from the masks: i ascending, then j ascending
-      int q = base + pre - cnt;
-      for (unsigned ma = ma1; ma; ma &= ma - 1) {
-        const int e1 = (k0 + __ffs(ma) - 1);
-        for (unsigned mb = mb1; mb; mb &= mb - 1) pp[q++] = make_int4(e1, (k0 + __ffs(mb) - 1), g, 0);
-      }
-    } else if (FILL && cnt) {
-      int q = base + pre - cnt;
-      for (int ib = k0; ib < k1; ib++) {
-        if (A.lm_pose[ib] != pa) continue;
-        const int e1 = (ib);
-        for (int jb = k0; jb < k1; jb++) {
-          if (A.lm_pose[jb] != pb) continue;
-          pp[q] = make_int4(e1, (jb), g, 0);
-          q++;
+      } else {
+        for (int ib = e0; ib < e1; ib += 8) {  // i blocks
+          unsigned ma = 0;
+          for (int v = 0; v < 8 && ib + v < e1; v++) ma |= A.lm_pose[ib + v] == pa ? 1u << v : 0u;
+          if (!ma) continue;
+          for (int jb = e0; jb < e1; jb += 8) {  // j blocks
+            unsigned mb = 0;
+            for (int v = 0; v < 8 && jb + v < e1; v++) mb |= A.lm_pose[jb + v] == pb ? 1u << v : 0u;
+            cnt += __popc(ma) * __popc(mb);
+          }
         }
       }
+      // wave exclusive prefix of the per-lane counts (lane order)
+      int pre = cnt;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int t = __shfl_up(pre, o);
+        if (lane >= o) pre += t;
+      }
+      const int total = __shfl(pre, 63);
+      if (FILL && cnt && e1 - e0 <= 8) {  // emit from the masks: i ascending, then j ascending
+        int q = base + pre - cnt;
+        for (unsigned ma = ma1; ma; ma &= ma - 1) {
+          const int ea = (e0 + __ffs(ma) - 1);
+          for (unsigned mb = mb1; mb; mb &= mb - 1) pp[q++] = make_int4(ea, (e0 + __ffs(mb) - 1), g, 0);
+        }
+      } else if (FILL && cnt) {
+        int q = base + pre - cnt;
+        for (int ib = e0; ib < e1; ib++) {
+          if (A.lm_pose[ib] != pa) continue;
+          for (int jb = e0; jb < e1; jb++) {
+            if (A.lm_pose[jb] != pb) continue;
+            pp[q] = make_int4(ib, jb, g, 0);
+            q++;
+          }
+        }
+      }
+      base += total;
     }
-    base += total;
   }
   if (!FILL && lane == 0) __hip_atomic_store(pp_cnt + c, base, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -1499,7 +1572,8 @@ __global__ __launch_bounds__(1024) void pair_offsets_kernel(const int* cnt, int*
 //     launch (ticket): the cost, the maximum diagonal and the LM control (computeLambdaInit).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ double setup_landmark(const Problem& P, const Lin& L, const Active& A, const Sys& S, int t,
-                                                 uint8_t* level, uint8_t* lm_act2) {
+                                                 uint8_t* level, uint8_t* lm_act2, double (*pd)[6] = nullptr,
+                                                 int* pa = nullptr, int pe0 = 0) {
   const int g = t / kGroup, j = t % kGroup;
   const bool in = g < A.nL, point = g < P.nq;
   double hl[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, bv[3] = {0, 0, 0}, chi = 0;
@@ -1516,8 +1590,12 @@ __device__ __forceinline__ double setup_landmark(const Problem& P, const Lin& L,
       live |= lev ? 0 : 1;
       if (!point) continue;  // line edges: the line workgroups
       const bool pose_opt = A.lm_pose[k] >= 0;
+      if (pd) pa[k - pe0] = pose_opt ? A.lm_pose[k] : -1;  // (the block's edges: its pose-diagonal partials)
       if (lev) {  // outside this phase: exact-zero records, no cost, error kept
         if (pose_opt) zero_pose_records<true>(L, k);
+        if (pd)
+#pragma unroll
+          for (int i = 0; i < 6; i++) pd[k - pe0][i] = 0.0;
         continue;
       }
       const int te = P.etype[k];
@@ -1533,7 +1611,11 @@ __device__ __forceinline__ double setup_landmark(const Problem& P, const Lin& L,
         huber(chi2, pick4(P.delta, te), cst, r1);
       }
       chi += cst;
-      point_edge_core<true>(P, L, A, k, te, pose_opt, T, cm, Xg, er, hl, bv);
+      double dg6[6] = {0, 0, 0, 0, 0, 0};
+      point_edge_core<true>(P, L, A, k, te, pose_opt, T, cm, Xg, er, hl, bv, dg6);
+      if (pd)
+#pragma unroll
+        for (int i = 0; i < 6; i++) pd[k - pe0][i] = dg6[i];
     }
   }
 #pragma unroll
@@ -1579,28 +1661,32 @@ __global__ __launch_bounds__(256) void setup_kernel(Problem P, Lin L, Active A, 
   if (b >= nb_lm) {  // the first optimize: edge pairs per Schur chunk, one wave per chunk
     const int c = (b - nb_lm) * 4 + (threadIdx.x >> 6);
     if (c < A.npairs * A.nchk) pair_scan<false>(A, c, pp_cnt, nullptr, nullptr);
-    if (threadIdx.x == 0) prof_max(S, 6);
+    if (threadIdx.x == 0) prof_max(S, kProfX + 4);
   } else if (b >= nbq) {
     double c = 0.0;  // set in thread 0
-    lin_lines<kLinSetup>(P, L, A, S, b - nbq, true, nullptr, nullptr, 0.0, false, nullptr, level != nullptr, &c);
+    lin_lines<kLinSetup>(P, L, A, S, b - nbq, true, nullptr, nullptr, 0.0, false, nullptr, level != nullptr, &c, pdg,
+                         nb_lm, b);  // (its edges' pose-diagonal partials too)
     if (threadIdx.x == 0) __hip_atomic_store(S.partial + b, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) prof_max(S, 15);
-    const int4 tb = A.ltab[b - nbq];
-    pose_diag_range(P, L, A, pdg, nb_lm, b, tb.x, tb.x + (tb.y & 0xff));
-    if (threadIdx.x == 0) prof_max(S, 5);
+    if (threadIdx.x == 0) prof_max(S, kProfX + 2);
   } else {
-    double acc[1] = {setup_landmark(P, L, A, S, b * 256 + threadIdx.x, level, lm_act2)};
-    block_reduce<1>(acc, red);
-    if (threadIdx.x == 0) __hip_atomic_store(S.partial + b, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (threadIdx.x == 0) prof_max(S, 13);
-    // this block's point landmarks' edges: one CSR range
+    // this block's point landmarks' edges: one CSR range; their pose diagonals staged in LDS when they fit
+    __shared__ double pd[kPdCap][6];
+    __shared__ int pa[kPdCap];
     const int g0 = min(b * (256 / kGroup), P.nq), g1 = min(b * (256 / kGroup) + 256 / kGroup, P.nq);
-    pose_diag_range(P, L, A, pdg, nb_lm, b, A.lm_off[g0], A.lm_off[g1]);
-    if (threadIdx.x == 0) prof_max(S, 14);
+    const int e0 = A.lm_off[g0], e1 = A.lm_off[g1];
+    const bool staged = e1 - e0 <= kPdCap;
+    double acc[1] = {setup_landmark(P, L, A, S, b * 256 + threadIdx.x, level, lm_act2, staged ? pd : nullptr, pa, e0)};
+    block_reduce<1>(acc, red);  // (its barriers also order the staged diagonals)
+    if (threadIdx.x == 0) __hip_atomic_store(S.partial + b, red[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) prof_max(S, kProfX + 0);
+    if (staged) {
+      pose_diag_lds(A, pd, pa, e1 - e0, pdg, nb_lm, b);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      pose_diag_range(P, L, A, pdg, nb_lm, b, e0, e1);
+    }
+    if (threadIdx.x == 0) prof_max(S, kProfX + 1);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -1644,15 +1730,15 @@ __global__ __launch_bounds__(256) void setup_kernel(Problem P, Lin L, Active A, 
     if (q < nq6) {
       const int pa = q / 6, i = q - 6 * pa;
       const double* src = pdg + (size_t)pa * npd * 6 + i;
-      for (int b0 = pt; b0 < npd; b0 += 4 * 8) {  // 8 write-through loads in flight, summed in block order
-        double t[8];
+      for (int b0 = pt; b0 < npd; b0 += 4 * 16) {  // 16 write-through loads in flight, summed in block order
+        double t[16];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
+        for (int u = 0; u < 16; u++) {
           const int bb = b0 + 4 * u;
           t[u] = bb < npd ? __hip_atomic_load(src + (size_t)bb * 6, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
         }
 #pragma unroll
-        for (int u = 0; u < 8; u++) sacc += t[u];
+        for (int u = 0; u < 16; u++) sacc += t[u];
       }
     }
     part[pt][lane] = sacc;

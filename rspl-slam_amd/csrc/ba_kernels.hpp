@@ -126,7 +126,9 @@ struct Sys {
   int lm_post;           // device LM: post the verdict even when it does not stop (the last trial the
                          // host queued); otherwise only the stopping trial posts the mailbox
 };
-constexpr int kProfPc = 16, kProfUe = kProfPc + 4 * 4096, kProfLen = kProfUe + 4 * 4096;
+constexpr int kProfPc = 16, kProfUe = kProfPc + 4 * 4096, kProfX = kProfUe + 4 * 4096, kProfLen = kProfX + 8;
+// [kProfX + i]: setup_kernel's latest landmark / landmark + pose-diagonal / line / line + pose-diagonal / pair
+// block (atomic max over the blocks)
 
 constexpr int kLmChunk = 256;  // landmarks per Schur chunk (4 per lane; 128 measured: 1440 chunk waves exceed one dispatch round)
 constexpr int kLineBlk = 8;    // line edges per linearisation workgroup
