@@ -453,6 +453,17 @@ void accept_swap(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, bool lin) 
   S.Hll = b->Hll; S.bl = b->bl;
 }
 
+// the second optimize()'s setup launch queued right behind the first optimize()'s first batch of trials,
+// before the host has seen them: a no-op unless that optimize() stopped within the batch (setup_dev's gate);
+// then the second optimize() starts from it instead of queueing its own after the host's round trip
+struct SpecSetup {
+  ba::Active A2{};           // the second optimize()'s active structure (levels, landmark activity)
+  uint8_t* level = nullptr;  // where its setup classifies the edges
+  int iters2 = 0;
+  bool queued = false;  // queued behind the first batch
+  bool extra = false;   // the first optimize() needed more trials: the queued setup did nothing
+};
+
 // the call's final kernel (inlier flags, final T / X / L into the staging slot) queued right behind the
 // last optimize()'s trials instead of after the host has seen that optimize() stop: it reads the control
 // after the last queued trial and does nothing unless the optimize() stopped there (then the host queues
@@ -476,7 +487,8 @@ struct SpecFinish {
 void preupload_next(rspl_ba* b);
 
 int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
-                 double* chi2_out, int* done_out, uint8_t* cls_level, bool build_pp, SpecFinish* fin) {
+                 double* chi2_out, int* done_out, uint8_t* cls_level, bool build_pp, SpecFinish* fin,
+                 SpecSetup* nxt, bool setup_done) {
   hipStream_t st = b->stream;
   S.lm = b->lmctl;
   S.lm_slot = 0;
@@ -490,7 +502,9 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
   // outlier levels and landmark activity first) + computeLambdaInit into the control (slot 0);
   // nothing is posted: the host waits for the trials only
   static const bool split_setup = getenv("RSPL_BA_SETUP") && std::string(getenv("RSPL_BA_SETUP")) == "split";
-  if (!split_setup) {
+  if (setup_done) {
+    // (queued behind the previous optimize()'s trials: SpecSetup)
+  } else if (!split_setup) {
     const size_t need = (size_t)ba::setup_pdg_len(A);
     if (need > b->pdg_cap) {  // grow (the stream may still read the old buffer)
       RSPL_HIP(hipStreamSynchronize(st));
@@ -580,6 +594,17 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
   };
   if ((rc = enqueue_batch(iters))) return rc;
   if (fin) preupload_next(b);  // the call's last kernels are queued: the next call's upload behind them
+  if (nxt && !split_setup && (size_t)ba::setup_pdg_len(nxt->A2) <= b->pdg_cap) {
+    // the second optimize()'s setup behind this batch, gated on the control the batch's last trial writes
+    ba::Sys S2 = S;
+    S2.lm = b->lmctl;
+    S2.lm_slot = 0;
+    S2.prof = nullptr;
+    S2.lm_trace = nullptr;
+    RSPL_HIP(ba::setup_dev(P, Lr, nxt->A2, S2, nxt->level, const_cast<uint8_t*>(nxt->A2.lm_act), nxt->iters2,
+                           nullptr, b->pp_off, b->pp_buf, b->pdg, st, queued & 1, &Ls, &Ss));
+    nxt->queued = true;
+  }
   double v[4];
   for (;;) {
     // wait for the stopping trial (trials queued after it post nothing) or the last queued one
@@ -625,6 +650,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
       break;
     }
     // rejected trials left iterations to do: queue one trial per remaining iteration
+    if (nxt) nxt->extra = true;
     if ((rc = enqueue_batch(std::max(1, iters - (int)v[1])))) return rc;
   }
   S.lm = nullptr;
@@ -643,12 +669,13 @@ bool dev_lm(const rspl_ba* b, const ba::Active& A, int iters) {
 // setup_dev); the caller does both itself otherwise
 int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Active& A, int iters,
              double* chi2_out, int* done_out, uint8_t* cls_level = nullptr, bool build_pp = false,
-             SpecFinish* fin = nullptr) {
+             SpecFinish* fin = nullptr, SpecSetup* nxt = nullptr, bool setup_done = false) {
   hipStream_t st = b->stream;
   double v[4];
   int rc;
   const bool sh = b->allreduce != nullptr;
-  if (dev_lm(b, A, iters)) return optimize_dev(b, P, Lr, S, A, iters, chi2_out, done_out, cls_level, build_pp, fin);
+  if (dev_lm(b, A, iters))
+    return optimize_dev(b, P, Lr, S, A, iters, chi2_out, done_out, cls_level, build_pp, fin, nxt, setup_done);
   const int n6 = 6 * A.K;
   double* so = b->red + n6 + b->nranks;  // this rank's {chi2, scale, fail} (S.shard_out)
   unsigned long long q = ++b->seq;
@@ -1391,8 +1418,18 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
   const bool pp_fused = dev_lm(b, A, pr->iterations_first);  // else: built here, before the first optimize
   if (!pp_fused) RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, st));
   tm.mark("pairs");
+  // phase 2's setup queued behind phase 1's trials (device LM on both, unsharded; RSPL_BA_SPECSETUP=0: off)
+  static const bool spec_setup_on = !(getenv("RSPL_BA_SPECSETUP") && std::string(getenv("RSPL_BA_SPECSETUP")) == "0");
+  SpecSetup nxt;
+  nxt.A2 = A;
+  nxt.A2.robust = 0;
+  nxt.A2.elevel = level;
+  nxt.A2.lm_act = b->lm_act2;
+  nxt.level = level;
+  nxt.iters2 = pr->iterations_second;
+  const bool spec_setup = spec_setup_on && pp_fused && !sh && !b->ktime_on && dev_lm(b, nxt.A2, pr->iterations_second);
   if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first, nullptr,
-                     pp_fused)))
+                     pp_fused, nullptr, spec_setup ? &nxt : nullptr)))
     return rc;
   tm.mark("opt1");
   tr[5] = mono_s();
@@ -1427,7 +1464,8 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
       fin.Lh = L_h;
     }
     if ((rc = optimize(b, P, Lr, S, A, pr->iterations_second, &res->chi2_second, &res->iterations_done_second,
-                       fused ? level : nullptr, false, spec_fin ? &fin : nullptr)))
+                       fused ? level : nullptr, false, spec_fin ? &fin : nullptr, nullptr,
+                       nxt.queued && !nxt.extra)))
       return rc;
     tm.mark("opt2");
     tr[6] = mono_s();

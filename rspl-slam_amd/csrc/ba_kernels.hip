@@ -1652,10 +1652,18 @@ __device__ __forceinline__ void prof_max(const Sys& S, int slot) {  // latest ov
 // control (round 3 did this in a second launch; one launch measured neutral, four per call instead of six).
 __global__ __launch_bounds__(256) void setup_kernel(Problem P, Lin L, Active A, Sys S, int nbq, int nb_lm,
                                                     uint8_t* level, uint8_t* lm_act2, int* pp_cnt, int* pp_off,
-                                                    double* pdg, int lm_iters) {
+                                                    double* pdg, int lm_iters, int gate, Lin Ls, Sys Ss) {
   __shared__ double red[4];
   __shared__ double part[4][64];
   __shared__ int last;
+  if (gate >= 0) {  // queued behind the previous optimize()'s trials: only once it has stopped, on its bank
+    const LmCtrl* c = S.lm + gate;
+    if (!c->stop) return;
+    if (c->cur) {
+      bank_state(P);
+      bank_lin(L, Ls, S, Ss);
+    }
+  }
   const int b = blockIdx.x;
   if (b == 0 && threadIdx.x == 0) prof_stamp(S, 9);
   if (b >= nb_lm) {  // the first optimize: edge pairs per Schur chunk, one wave per chunk
@@ -3560,7 +3568,9 @@ int setup_pdg_len(const Active& A) {
 }
 
 hipError_t setup_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, uint8_t* level, uint8_t* lm_act2,
-                     int lm_iters, int* pp_cnt, int* pp_off, int4* pp, double* pdg, hipStream_t s) {
+                     int lm_iters, int* pp_cnt, int* pp_off, int4* pp, double* pdg, hipStream_t s, int gate,
+                     const Lin* Ls, const Sys* Ss) {
+  if (gate >= 0 && (!Ls || !Ss || pp_cnt)) return hipErrorInvalidValue;
   if (!S.lm || lm_iters <= 0) return hipErrorInvalidValue;
   Active A0 = A;
   A0.elevel = nullptr;  // the levels are written by this launch (level != null), never read by it
@@ -3570,7 +3580,7 @@ hipError_t setup_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, ui
   const int nbp = pp_cnt ? (nc + 3) / 4 : 0;
   // at least one block: the last one writes the LM control
   hipLaunchKernelGGL(setup_kernel, dim3(std::max(nb + nbp, 1)), dim3(256), 0, s, P, L, A0, S, nbq, nb, level, lm_act2,
-                     pp_cnt, pp_off, pdg, lm_iters);
+                     pp_cnt, pp_off, pdg, lm_iters, gate, Ls ? *Ls : L, Ss ? *Ss : S);
   if (pp_cnt) hipLaunchKernelGGL(pair_fill_kernel, dim3(nc), dim3(64), 0, s, A, pp_off, pp);
   return hipGetLastError();
 }

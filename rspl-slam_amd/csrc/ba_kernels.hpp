@@ -150,8 +150,12 @@ hipError_t post(Sys& S, unsigned long long seq, hipStream_t s, const Active* A =
 // != null (the call's first optimize): the Schur chunks' edge-pair lists too (replaces build_pairs:
 // counted in the first launch, scanned by the second's last block, filled by a third).
 // pdg: setup_pdg_len(A) doubles of per-block pose-diagonal partials.
+// gate >= 0 (the second optimize's setup queued behind the first one's trials before the host has seen them):
+// a no-op unless the control slot `gate` shows that optimize stopped; then the current bank from that control
+// (Ls / Ss: the spare records, as the trials bank them)
 hipError_t setup_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, uint8_t* level, uint8_t* lm_act2,
-                     int lm_iters, int* pp_cnt, int* pp_off, int4* pp, double* pdg, hipStream_t s);
+                     int lm_iters, int* pp_cnt, int* pp_off, int4* pp, double* pdg, hipStream_t s, int gate = -1,
+                     const Lin* Ls = nullptr, const Sys* Ss = nullptr);
 int setup_pdg_len(const Active& A);
 // speculative linearisation of a trial's candidate into a spare record set, fused into the
 // trial's last kernel (fast path only)

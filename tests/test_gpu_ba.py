@@ -227,10 +227,15 @@ def test_ba_analytic_line_jacobian(ba, analytic, case):
 
 
 def test_ba_final_kernel_paths_agree(ba):
-    """The call's final kernel queued speculatively behind optimize(5) (default) and the host-ordered one
-    (taken on calls with kernel timing) give bit-identical inlier flags, poses, points and lines."""
+    """The call's final kernel queued speculatively behind optimize(5) and optimize(5)'s setup queued
+    speculatively behind optimize(10)'s first trials (default) against the host-ordered launches (taken on
+    calls with kernel timing): bit-identical inlier flags, poses, points and lines.  The last problems are
+    noisy enough for rejected LM trials (optimize(10) then needs trials beyond its first batch and the
+    speculative setup stays a no-op)."""
     probs = [SY.ba_problem(n_poses=6 + k, n_points=400, n_lines=12, seed=80 + k, pixel_sigma=0.8,
                            outlier_frac=0.05)[0] for k in range(3)]
+    probs += [SY.ba_problem(n_poses=8, n_points=300, n_lines=6, seed=90 + k, pixel_sigma=4.0,
+                            outlier_frac=0.3)[0] for k in range(2)]
     spec = [ba.run(p) for p in probs]
     ba.kernel_timing(1)  # every call timed: the final kernel is queued after the host has seen optimize(5) stop
     try:
