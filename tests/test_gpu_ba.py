@@ -66,6 +66,15 @@ def test_ba_matches_oracle(ba, seed, lines, outl):
     _compare(ba.run(prob), oracle.ba_local(prob))
 
 
+@pytest.mark.parametrize("obs", [14, 24])
+def test_ba_dense_observations(ba, obs):
+    """Landmarks seen by many poses: 32 landmarks per setup block carry 448 (staged in LDS) / 768 (more than
+    kPdCap = 512: the block's pose diagonals re-read from its records) edges for computeLambdaInit."""
+    prob, gt = SY.ba_problem(n_poses=26, n_points=500, n_lines=0, obs_per_point=obs, seed=60 + obs,
+                             pixel_sigma=0.8, outlier_frac=0.05)
+    _compare(ba.run(prob), oracle.ba_local(prob), tol_pose=1e-6, tol_pt=1e-5, chi2_rtol=5e-8)
+
+
 def test_ba_lines_only(ba):
     prob, gt = SY.ba_problem(n_poses=6, n_points=0, n_lines=40, seed=12, pixel_sigma=0.8, outlier_frac=0.0)
     res, ref = ba.run(prob), oracle.ba_local(prob)
