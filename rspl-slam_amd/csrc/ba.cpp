@@ -460,8 +460,8 @@ struct SpecSetup {
   ba::Active A2{};           // the second optimize()'s active structure (levels, landmark activity)
   uint8_t* level = nullptr;  // where its setup classifies the edges
   int iters2 = 0;
-  bool queued = false;  // queued behind the first batch
-  bool extra = false;   // the first optimize() needed more trials: the queued setup did nothing
+  bool queued = false;  // queued behind a batch of the first optimize()'s trials
+  bool extra = false;   // a later batch was queued after it: that setup did nothing (and none followed yet)
 };
 
 // the call's final kernel (inlier flags, final T / X / L into the staging slot) queued right behind the
@@ -594,8 +594,10 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
   };
   if ((rc = enqueue_batch(iters))) return rc;
   if (fin) preupload_next(b);  // the call's last kernels are queued: the next call's upload behind them
-  if (nxt && !split_setup && (size_t)ba::setup_pdg_len(nxt->A2) <= b->pdg_cap) {
-    // the second optimize()'s setup behind this batch, gated on the control the batch's last trial writes
+  // the second optimize()'s setup behind each batch, gated on the control the batch's last trial writes (the
+  // one behind the batch in which this optimize() stops is the one that runs)
+  auto queue_spec_setup = [&]() -> int {
+    if (!nxt || split_setup || (size_t)ba::setup_pdg_len(nxt->A2) > b->pdg_cap) return RSPL_OK;
     ba::Sys S2 = S;
     S2.lm = b->lmctl;
     S2.lm_slot = 0;
@@ -604,7 +606,10 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
     RSPL_HIP(ba::setup_dev(P, Lr, nxt->A2, S2, nxt->level, const_cast<uint8_t*>(nxt->A2.lm_act), nxt->iters2,
                            nullptr, b->pp_off, b->pp_buf, b->pdg, st, queued & 1, &Ls, &Ss));
     nxt->queued = true;
-  }
+    nxt->extra = false;
+    return RSPL_OK;
+  };
+  if ((rc = queue_spec_setup())) return rc;
   double v[4];
   for (;;) {
     // wait for the stopping trial (trials queued after it post nothing) or the last queued one
@@ -652,6 +657,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
     // rejected trials left iterations to do: queue one trial per remaining iteration
     if (nxt) nxt->extra = true;
     if ((rc = enqueue_batch(std::max(1, iters - (int)v[1])))) return rc;
+    if ((rc = queue_spec_setup())) return rc;
   }
   S.lm = nullptr;
   if (v[2] != 0.0) accept_swap(b, P, Lr, S, true);  // the device's current bank is the host's spare one
