@@ -35,6 +35,7 @@ OIVIO-shaped 640x512 stereo, 600 keypoints, SG N=600; with --gpus 8 one sequence
 (configs[4]: synthetic 1920x1080 stereo, 2048 keypoints, SG N=2048, 30-keyframe / 10k-landmark BA).
 """
 import argparse
+import gc
 import json
 import os
 import queue
@@ -621,6 +622,13 @@ def main():
         ba.kernel_timing(0)
         line_timers[:] = [capi.Timer() for _ in range(args.warmup)]
         line_t0 = 0
+        # the cyclic garbage collector off for the warmup and the timed steps (as timeit does): a full
+        # collection walks every object torch has created -- a multi-ms pause of the Python feature thread
+        # that drains the pipeline (seen as single ~5-8 ms stalls in 20-step runs); reference counting still
+        # frees each step's temporaries
+        gc.collect()
+        gc.freeze()
+        gc.disable()
         for i in range(args.warmup):
             step(i)
         ba_drain()
@@ -650,6 +658,8 @@ def main():
         t_drained = time.perf_counter()
         capi.synchronize()
         t_end = time.perf_counter()
+        gc.enable()
+        gc.unfreeze()
         elapsed = job_time(t_end - t0, dist)
         if trace_on:  # the timed region's host timeline, relative to its start (ms)
             rel = lambda t: round((t - t0) * 1e3, 4)  # noqa: E731
