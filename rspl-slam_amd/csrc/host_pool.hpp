@@ -1,7 +1,7 @@
 // A few persistent host worker threads for the per-call host passes of a handle (the BA's edge
 // staging): run(fn, ctx) calls fn(ctx, part) for part in [0, parts()), part 0 on the calling thread.
-// Between calls a worker spins for a short while (the BA runs back to back in a pipeline, so the next
-// call usually comes within a millisecond and finds the workers awake), then sleeps on a condition
+// Between calls a worker spins for a short while (50 us: a longer spin kept three workers busy between
+// the calls of a pipelined BA, against the box's 16-CPU quota), then sleeps on a condition
 // variable.  Not re-entrant: one run at a time per pool, as a handle serves one call at a time.
 #pragma once
 
@@ -68,7 +68,7 @@ class HostPool {
     }
   }
 
-  static constexpr std::chrono::microseconds kSpin{3000};
+  static constexpr std::chrono::microseconds kSpin{50};
   std::vector<std::thread> th_;
   std::atomic<unsigned> gen_{0};
   std::atomic<int> left_{0};
