@@ -126,22 +126,45 @@ def cpu_baseline(sp_w, sg_w, frames, threads, wl):
                       f"through the oracle's C restatement, OMP_NUM_THREADS={threads}, {dt:.1f} s"}
 
 
-def pmc_traffic(kernel_substr):
-    """HBM bytes per launch of a kernel from the newest committed PMC summary
-    (profiles/*_pmc_traffic.json, written by tools/pmc_traffic.py from two rocprofv3
+def _pmc_files(kind, workload):
+    """Committed PMC summaries of `kind` ("traffic" / "mfma") for the workload, newest round first.
+    C3 (the headline) files are profiles/rNN_pmc_<kind>_fp16.json; the side workloads carry their own
+    passes as profiles/rNN_pmc_<kind>_fp16_<workload>.json -- a summary is never borrowed across configs."""
+    files = sorted((ROOT / "profiles").glob(f"*_pmc_{kind}*.json"), reverse=True)
+    if workload == "c3":
+        return [f for f in files if not any(f.stem.endswith("_" + w) for w in WORKLOADS if w != "c3")]
+    return [f for f in files if f.stem.endswith("_" + workload)]
+
+
+def pmc_traffic(kernel_substr, workload="c3"):
+    """HBM bytes per launch of a kernel from the newest committed PMC summary for this workload
+    (profiles/*_pmc_traffic*.json, written by tools/pmc_traffic.py from two rocprofv3
     --pmc passes, FETCH_SIZE x2 gfx950 correction), or None."""
-    for f in sorted((ROOT / "profiles").glob("*_pmc_traffic*.json"), reverse=True):  # newest first
+    for f in _pmc_files("traffic", workload):
         for name, v in json.loads(f.read_text()).items():
             if kernel_substr in name:
                 return v["traffic_bytes"], f.name
     return None, None
 
 
-def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
+def pmc_mfma(kernel_substr, workload="c3"):
+    """MFMA-busy of a kernel from the newest committed rocprofv3 PMC pass for this workload
+    (profiles/*_pmc_mfma*.json, tools/pmc_mfma.py: SQ_VALU_MFMA_BUSY_CYCLES over GRBM_GUI_ACTIVE x 1024
+    SIMDs = rocprofv3's MfmaUtil, and over the busy CUs' SIMD cycles), or None."""
+    for f in _pmc_files("mfma", workload):
+        for name, v in json.loads(f.read_text()).items():
+            if kernel_substr in name:
+                return {"chip": round(v["mfma_busy_chip"], 4),
+                        "per_busy_cu": round(v["mfma_busy_per_busy_cu"], 4) if v.get("mfma_busy_per_busy_cu") else None,
+                        "source": f"profiles/{f.name}"}
+    return None
+
+
+def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision, workload):
     """Achieved rate vs the bounding peak for the big stages (HIP-event stage times on the stage's
     launch stream, per step: 2 SuperPoint images, 2 SuperGlue pairs of N = M = K).  Algorithmic work
     as SURVEY.md 8(d): conv1a+conv1b 2*H*W*64*(9 + 576) FLOP per image; GNN 2*(655,360 N + 512 N M)
-    per image per layer; Sinkhorn streamed model 2*iters*4*(N+1)(M+1) bytes per pair; NMS 4*H*W (the score
+    per image per layer; Sinkhorn compulsory 2*4*(N+1)(M+1) bytes per pair (couplings in, Z out); NMS 4*H*W (the score
     map read once; the product path writes no NMS'd map, the candidates carry the scores)
     bytes per image.  Single-kernel stages carry the kernel name (pmc_kernel) whose PMC traffic
     summary under profiles/ gives `traffic`; the GNN is a launch family (single_kernel false)."""
@@ -159,9 +182,11 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
              "layer_kernel" if precision == "fp16" else "gemm_kernel", False,
              "GFLOP per step (2 pairs x 2 images x 18 layers; fp16: 19 launches of the fused layer kernel, "
              "fp32: 4 GEMM/attention launches per layer)"),
-            ("sg:sinkhorn", 2 * 2 * 100 * 4 * (N + 1) * (M + 1) / 1e9, "GB/s", HBM_PEAK_GBS, "hbm",
-             "sinkhorn_kernel<" if os.environ.get("RSPL_SG_SINK") == "slab" else "sinkhorn_sc_kernel",
-             True, "GB per launch (2 pairs, streamed model 2*iters*4*(N+1)(M+1))"),
+            ("sg:sinkhorn", 2 * 2 * 4 * (N + 1) * (M + 1) / 1e9, "GB/s", HBM_PEAK_GBS, "hbm",
+             "sinkhorn_kernel<" if os.environ.get("RSPL_SG_SINK") == "slab" else
+             ("sinkhorn_w_kernel" if N + 1 > 640 else "sinkhorn_sc_kernel"),
+             True, "GB per launch (2 pairs, compulsory: couplings read + Z written once, 2*4*(N+1)(M+1) per pair; "
+                   "the kernel holds K = exp(C + a + b) in registers across the 100 iterations)"),
             ("sp:nms", 2 * 4 * H * W / 1e9, "GB/s", HBM_PEAK_GBS, "hbm", "nms_kernel", True,
              "GB per launch (2 images, 4*H*W: the score map read once)"))
     out = {}
@@ -174,17 +199,15 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision):
                         "frac": round(ach / peak, 4), "ms": round(ms, 4), "avg_launch_ms": round(ms / nl, 5),
                         "launches_per_step": nl, "algorithmic": f"{work:.4g} {what}", "pmc_kernel": kern,
                         "single_kernel": single or nl > 1}
-    if "sg:sinkhorn" in out:  # against the compulsory bytes too: couplings in + Z out, 2 pairs
-        comp = 2 * 2 * 4 * (N + 1) * (M + 1) / 1e9
-        r = out["sg:sinkhorn"]
-        r["compulsory"] = {"GB_per_launch": round(comp, 5), "achieved": round(comp / r["ms"] * 1e3, 2),
-                           "frac": round(comp / r["ms"] * 1e3 / HBM_PEAK_GBS, 5),
-                           "note": "couplings read + Z written once; the streamed model above is what a "
-                                   "non-resident kernel would move (the register-resident kernel does not)"}
+    for r in out.values():
+        if r["bound"] == "mfma":
+            r["mfma_busy"] = pmc_mfma(r["pmc_kernel"], workload)
+        tr, src = pmc_traffic(r["pmc_kernel"], workload)
+        r["traffic"] = round(tr) if tr and r["single_kernel"] else None
     return out
 
 
-def ba_kernel_rows(prob, kt, timed_calls):
+def ba_kernel_rows(prob, kt, timed_calls, workload):
     """Roofline rows of the local BA's two per-trial launches from their HIP-event times on the BA stream
     (LocalBA.kernel_times over every call of the instrumented pass that follows the timed region).  Algorithmic bytes per launch =
     the records the launch must read once plus what it writes:
@@ -219,6 +242,8 @@ def ba_kernel_rows(prob, kt, timed_calls):
                          "ms": round(avg * n / max(1, timed_calls), 4), "launches_per_call": round(n / max(1, timed_calls), 2),
                          "algorithmic": f"{b / 1e6:.4g} MB per launch: {what}", "pmc_kernel": kern,
                          "single_kernel": True}
+            tr, _ = pmc_traffic(kern, workload)
+            rows[key]["traffic"] = round(tr) if tr else None
     return rows
 
 
@@ -723,15 +748,15 @@ def main():
     sp, sg = res["stages"]
     if rank != 0:
         return
-    stages = stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, args.precision)
+    stages = stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, args.precision, args.workload)
     if not shard and res["ba_kt"]:
-        stages.update(ba_kernel_rows(problems[0], res["ba_kt"], res["ba_timed_calls"]))
+        stages.update(ba_kernel_rows(problems[0], res["ba_kt"], res["ba_timed_calls"], args.workload))
     # the step-setting kernel: the largest device time per step over every timed kernel, the BA's
     # launches included (its launches per call x one call per step)
     dom_key = max((k for k in stages if stages[k]["single_kernel"]), key=lambda k: stages[k]["ms"])
     dom = {k: v for k, v in stages[dom_key].items() if k not in ("single_kernel",)}
     dom["ms_per_step"] = dom.pop("ms")
-    traffic, traffic_src = pmc_traffic(dom["pmc_kernel"])
+    traffic, traffic_src = pmc_traffic(dom["pmc_kernel"], args.workload)
     dom["traffic"] = round(traffic) if traffic else None
     dom["traffic_note"] = (f"HBM bytes per launch, rocprofv3 FETCH_SIZE(x2)+WRITE_SIZE, profiles/{traffic_src}"
                            if traffic else "no PMC summary for this kernel under profiles/")
@@ -759,7 +784,9 @@ def main():
         "config": {"workload": wl["desc"], "global_batch": world,
                    "parallelism": (f"replicas x{world} (one sequence per GPU)" if not shard else
                                    f"replicas x{world} front end; every step's {world} local BAs landmark-sharded "
-                                   f"over {world} ranks (RCCL all-reduce per LM trial)")},
+                                   f"over {world} ranks (RCCL all-reduce per LM trial)"),
+                   "python_gc": "cyclic GC frozen and disabled for the warmup and timed steps (reference counting "
+                                "still frees; the feature loop is a Python driver, the reference's is C++)"},
         "roofline": {"kernel": dom_key, **dom},
         "stages_roofline": stages,
         "stages_ms_per_step": {**{f"sp:{n}": round(v / max(1, sp_calls), 4) for n, v in zip(sp.STAGES, sp_ms)},

@@ -65,3 +65,46 @@ def test_gpu_map_sequence_vs_oracle(tmp_path):
     ate_o = TJ.ape(ts_o, P_o, ts, P)
     assert ate_o["rmse"] < 1e-6
     assert ate["rmse"] < 0.5 * ate_in["rmse"], (ate, ate_in)
+
+
+def test_gpu_map_sequence_analytic_identical_trajectory(tmp_path):
+    """Trajectory-level BA parity (round-5 verdict item 1).  With the analytic limit of g2o's central-
+    difference line Jacobian on both sides (rspl_ba_set_line_jacobian / oracle.ba_set_line_jacobian) the GPU
+    map path and the oracle map path make the same LM decisions on every keyframe, so the keyframe
+    trajectories written by SaveKeyframeTrajectory (map.cc:1007-1024) are byte-identical and the poses agree
+    to 1e-9 after every keyframe (tools/run_sequence.py --analytic-line-jacobian: identical TUM files over 100
+    keyframes, profiles/r06_sequence100_analytic.json).  In g2o's numeric mode the central difference's
+    rounding noise (edge_project_line.h:16-31, delta 1e-9) flips an accept / reject decision after ~66
+    keyframes and the two paths end mm apart, as two edge orders of the oracle itself do."""
+    seq = SY.map_sequence(n_keyframes=48, n_points=4000, n_lines=60, seed=100, outlier_frac=0.03)
+    ba = pkg.LocalBA(max_poses=32, max_points=4100, max_lines=70, max_edges=80000)
+    ba.set_line_jacobian(True)
+    oracle.ba_set_line_jacobian(True)
+    try:
+        mr = map_ref.Map(seq["camera"])
+        iters = []
+
+        def check(k, m):
+            kf = seq["keyframes"][k]
+            map_ref.insert_keyframe(mr, kf)
+            if k == 0:
+                return
+            _, res, n_out, n_lout = map_ref.local_map_optimization(mr, kf["id"], oracle.ba_local)
+            iters.append((res.iters_first, res.iters_second, n_out, n_lout))
+            for f in seq["keyframes"][:k + 1]:
+                np.testing.assert_allclose(m.GetPose(f["id"]), mr.keyframes[f["id"]].pose, rtol=0, atol=1e-9,
+                                           err_msg=f"keyframe {k}: pose {f['id']}")
+
+        m, reports = SQ.run(seq, ba, on_keyframe=check)
+    finally:
+        ba.set_line_jacobian(False)
+        oracle.ba_set_line_jacobian(False)
+    assert len(reports) == len(iters) == len(seq["keyframes"]) - 1
+    for rep, (i1, i2, n_out, n_lout) in zip(reports, iters):
+        assert (rep["iterations_first"], rep["iterations_second"]) == (i1, i2)
+        assert (rep["n_point_outliers"], rep["n_line_outliers"]) == (n_out, n_lout)
+    assert sum(r["n_line_outliers"] + r["n_point_outliers"] for r in reports) > 0
+    assert sum(r["n_lines"] for r in reports) > 0
+    path = tmp_path / "kf.txt"
+    m.SaveKeyframeTrajectory(path)
+    assert path.read_text() == "".join(l + "\n" for l in mr.trajectory_lines())

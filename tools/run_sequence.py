@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--points", type=int, default=12000)
     ap.add_argument("--lines", type=int, default=120)
     ap.add_argument("--seed", type=int, default=100)
+    ap.add_argument("--analytic-line-jacobian", action="store_true",
+                    help="both sides use the analytic limit of g2o's central-difference line Jacobian "
+                         "(rspl_ba_set_line_jacobian / oracle.ba_set_line_jacobian)")
     ap.add_argument("--out", default="gpurun_out/sequence")
     a = ap.parse_args()
     from rspl_slam_amd import sequence as SQ, trajectory as TJ
@@ -39,6 +42,9 @@ def main():
     seq = pkg.synthetic.map_sequence(n_keyframes=a.keyframes, n_points=a.points, n_lines=a.lines, seed=a.seed,
                                      outlier_frac=0.03)
     ba = pkg.LocalBA(max_poses=32, max_points=a.points + 100, max_lines=a.lines + 10, max_edges=200000)
+    if a.analytic_line_jacobian:
+        ba.set_line_jacobian(True)
+        oracle.ba_set_line_jacobian(True)
     t = time.perf_counter()
     m, reports = SQ.run(seq, ba)
     print(f"gpu path: {len(reports)} keyframes, {time.perf_counter() - t:.2f} s", file=sys.stderr, flush=True)
@@ -60,6 +66,7 @@ def main():
     gt = seq["gt_Twc"][:, :3, 3]
     tracked = np.array([kf["Twc"][:3, 3] for kf in seq["keyframes"]])
     res = {"keyframes": len(ts), "points": a.points, "lines": a.lines,
+           "analytic_line_jacobian": bool(a.analytic_line_jacobian),
            "ate_gpu_vs_cpu_m": TJ.ape(tc[0], tc[1], tg[0], tg[1])["rmse"],
            "ate_gpu_vs_ground_truth_m": TJ.ape(ts, gt, tg[0], tg[1])["rmse"],
            "ate_cpu_vs_ground_truth_m": TJ.ape(ts, gt, tc[0], tc[1])["rmse"],

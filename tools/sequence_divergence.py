@@ -26,12 +26,18 @@ def main():
     ap.add_argument("--points", type=int, default=12000)
     ap.add_argument("--lines", type=int, default=120)
     ap.add_argument("--seed", type=int, default=100)
+    ap.add_argument("--analytic-line-jacobian", action="store_true",
+                    help="both sides use the analytic limit of g2o's central-difference line Jacobian "
+                         "(rspl_ba_set_line_jacobian / oracle.ba_set_line_jacobian)")
     ap.add_argument("--show", type=int, default=6)
     a = ap.parse_args()
     from rspl_slam_amd.sequence import insert_keyframe
     seq = pkg.synthetic.map_sequence(n_keyframes=a.keyframes, n_points=a.points, n_lines=a.lines, seed=a.seed,
                                      outlier_frac=0.03)
     ba = pkg.LocalBA(max_poses=32, max_points=a.points + 100, max_lines=a.lines + 10, max_edges=200000)
+    if a.analytic_line_jacobian:
+        ba.set_line_jacobian(True)
+        oracle.ba_set_line_jacobian(True)
     m = pkg.mapping.Map(seq["camera"])
     mr = map_ref.Map(seq["camera"])
     shown = 0
