@@ -171,15 +171,17 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision, workload
     t = {**{f"sp:{n}": v / max(1, sp_calls) for n, v in zip(sp.STAGES, sp_ms)},
          **{f"sg:{n}": v / max(1, sg_calls) for n, v in zip(sg.STAGES, sg_ms)}}
     N = M = K
-    mfma_peak = FP16_MFMA_PEAK if precision == "fp16" else FP32_MFMA_PEAK
+    h16 = precision in ("fp16", "fp16x3")  # fp16 MFMA operands (fp16x3: SuperPoint split into hi + lo)
+    mfma_peak = FP16_MFMA_PEAK if h16 else FP32_MFMA_PEAK
     # fp16: the persistent conv1 kernel (RSPL_SP_CONV1=stage: the per-stage fused conv1a kernel)
     conv1_k = (("conv3x3_h_kernel<64, 16, true, true, false>" if os.environ.get("RSPL_SP_CONV1") == "stage"
-                else "conv1_res_kernel") if precision == "fp16"
+                else "conv1_res_kernel") if precision == "fp16" else "conv3x3_x3_kernel<64, 16, true, true>"
+               if precision == "fp16x3"
                else "conv3x3_kernel<64, 16, true, true>")
     rows = (("sp:conv1a+1b+pool", 2 * conv1_gflop_per_image(), "TFLOP/s", mfma_peak, "mfma", conv1_k, True,
              "GFLOP per launch (2 images, conv1a+conv1b)"),
             ("sg:gnn x18", 2 * 2 * 18 * 2 * (655360 * N + 512 * N * M) / 1e9, "TFLOP/s", mfma_peak, "mfma",
-             "layer_kernel" if precision == "fp16" else "gemm_kernel", False,
+             "layer_kernel" if h16 else "gemm_kernel", False,
              "GFLOP per step (2 pairs x 2 images x 18 layers; fp16: 19 launches of the fused layer kernel, "
              "fp32: 4 GEMM/attention launches per layer)"),
             ("sg:sinkhorn", 2 * 2 * 4 * (N + 1) * (M + 1) / 1e9, "GB/s", HBM_PEAK_GBS, "hbm",
@@ -194,7 +196,7 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision, workload
         ms = t.get(key)
         if ms:
             ach = work / ms if unit == "TFLOP/s" else work / ms * 1e3
-            nl = 19 if key == "sg:gnn x18" and precision == "fp16" else 1  # launches per step of the kernel
+            nl = 19 if key == "sg:gnn x18" and h16 else 1  # launches per step of the kernel
             out[key] = {"bound": bound, "achieved": round(ach, 2), "peak": peak, "unit": unit,
                         "frac": round(ach / peak, 4), "ms": round(ms, 4), "avg_launch_ms": round(ms / nl, 5),
                         "launches_per_step": nl, "algorithmic": f"{work:.4g} {what}", "pmc_kernel": kern,
@@ -364,8 +366,10 @@ def main():
     ap.add_argument("--ba-thread", choices=["native", "python"], default="native",
                     help="the tracking thread that runs the local BAs: the BA handle's native host thread "
                          "(rspl_ba_submit) or a Python thread around rspl_ba_local (A/B)")
-    ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp16",
-                    help="SP/SG MFMA precision: fp16 = the reference's own TensorRT kFP16 engines "
+    ap.add_argument("--precision", choices=["fp32", "fp16", "fp16x3"], default="fp16",
+                    help="SP/SG MFMA precision: fp16x3 = SuperPoint in split fp16 (hi + lo operands, three fp16 MFMA "
+                         "products: the fp32 path's keypoint sets) with SuperGlue in fp16; "
+                         "fp16 = the reference's own TensorRT kFP16 engines "
                          "(src/super_point.cpp:98, src/super_glue.cpp:132; default), fp32 = the parity path")
     ap.add_argument("--reserve-cus", type=int, default=int(os.environ.get("RSPL_RESERVE_CUS", "0")),
                     help="CUs the SuperPoint/SuperGlue streams leave free for the BA chain (CU-masked streams)")
@@ -397,13 +401,16 @@ def main():
     capi.check(capi.load().rspl_set_device(local), "rspl_set_device")
 
     sp_w, sg_w = pkg.weights.ensure_blobs(str(ROOT / "weights"))
-    precs = [args.precision] + (["fp32" if args.precision == "fp16" else "fp16"]
-                                if world == 1 and not args.single_precision else [])
+    # the second measurement of the same run: the fp16 headline is paired with the split-fp16 SuperPoint (the
+    # fp32 path's keypoint sets, profiles/r06_c1_plumbing.json), the others with fp16
+    other_prec = {"fp16": "fp16x3", "fp16x3": "fp16", "fp32": "fp16"}
+    precs = [args.precision] + ([other_prec[args.precision]] if world == 1 and not args.single_precision else [])
     handles = {}
     for pr in precs:  # all handles and streams created once, up front: fixed HW-queue placement
-        code = capi.RSPL_PREC_FP16 if pr == "fp16" else capi.RSPL_PREC_FP32
+        code = capi.RSPL_PREC_FP16 if pr in ("fp16", "fp16x3") else capi.RSPL_PREC_FP32  # SuperGlue
+        sp_code = capi.RSPL_PREC_FP16X3 if pr == "fp16x3" else code
         sp_h = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=K, weights=sp_w, max_height=H, max_width=W,
-                                                   max_batch=2, precision=code, device=local))
+                                                   max_batch=2, precision=sp_code, device=local))
         assert sp_h.build(), sp_h.error
         sg_h = pkg.SuperGlue(pkg.SuperGlueConfig(image_width=W, image_height=H, weights=sg_w, max_keypoints=K,
                                                  max_batch=2, precision=code, device=local))
@@ -777,9 +784,12 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": ("fp16 MFMA with fp32 accumulation for SuperPoint/SuperGlue (the reference's TensorRT kFP16 "
-                  "engines), fp32 Sinkhorn/decode, fp64 BA") if args.precision == "fp16"
-                 else "fp32 (SuperPoint/SuperGlue MFMA), fp64 (BA)",
+        "dtype": {"fp16": "fp16 MFMA with fp32 accumulation for SuperPoint/SuperGlue (the reference's TensorRT kFP16 "
+                          "engines), fp32 Sinkhorn/decode, fp64 BA",
+                  "fp16x3": "SuperPoint split fp16 (hi + lo operands, three fp16 MFMA products, fp32 accumulation: "
+                            "fp32-grade results), SuperGlue fp16 MFMA with fp32 accumulation (the reference's TensorRT "
+                            "kFP16), fp32 Sinkhorn/decode, fp64 BA",
+                  "fp32": "fp32 (SuperPoint/SuperGlue MFMA), fp64 (BA)"}[args.precision],
         "data": f"synthetic (seeded textured stereo {W}x{H}, seeded weights, synthetic local-BA problems)",
         "config": {"workload": wl["desc"], "global_batch": world,
                    "parallelism": (f"replicas x{world} (one sequence per GPU)" if not shard else
@@ -813,11 +823,13 @@ def main():
                        "pipeline's contention, host-array hand-over included"},
     }
     if other is not None:
-        oname = "fp32" if args.precision == "fp16" else "fp16"
+        oname = other_prec[args.precision]
         out[f"{oname}_run"] = {"value": round(other["value"], 3),
                                "ms_per_step": round(1e3 * other["elapsed"] / args.steps, 3),
                                "note": "same workload and run, SP/SG at " + oname +
-                                       (" (the bit-parity path)" if oname == "fp32" else "")}
+                                       {"fp32": " (the bit-parity path)",
+                                        "fp16x3": " (SuperPoint split fp16: the fp32 keypoint sets; SuperGlue fp16)",
+                                        "fp16": ""}[oname]}
     if world == 1 and not args.no_cpu_baseline:
         nproc = os.cpu_count() or 1
         threads = min(16, nproc)  # the GPU box's CPU share is 16 cores per GPU

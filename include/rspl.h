@@ -41,7 +41,11 @@ extern "C" {
 
 #define RSPL_FEATURE_ROWS 259
 
-enum { RSPL_PREC_FP32 = 0, RSPL_PREC_FP16 = 1 };
+/* RSPL_PREC_FP16: fp16 MFMA operands, fp32 accumulation (the reference's TensorRT kFP16 engines,
+ * src/super_point.cpp:97-99, src/super_glue.cpp:132).  RSPL_PREC_FP16X3 (SuperPoint only): split fp16 --
+ * every activation and weight carried as hi + lo fp16, three fp16 MFMA products per step, fp32-grade
+ * results (keypoint sets of the fp32 path) at the fp16 MFMA rate. */
+enum { RSPL_PREC_FP32 = 0, RSPL_PREC_FP16 = 1, RSPL_PREC_FP16X3 = 2 };
 
 const char* rspl_last_error(void);
 const char* rspl_version(void);
@@ -101,7 +105,7 @@ typedef struct {
   int max_height;            /* arena sizing; H, W must be multiples of 8 */
   int max_width;
   int max_batch;             /* images per batched device call (>= 1) */
-  int precision;             /* RSPL_PREC_FP32 (parity) or RSPL_PREC_FP16 */
+  int precision;             /* RSPL_PREC_FP32 (parity), RSPL_PREC_FP16 or RSPL_PREC_FP16X3 */
   int device;                /* HIP device ordinal */
 } rspl_sp_config;
 

@@ -17,6 +17,7 @@ RSPL_OK = 0
 RSPL_ABI_VERSION = 2  # include/rspl.h: the struct layouts the ctypes mirrors below follow
 RSPL_PREC_FP32 = 0
 RSPL_PREC_FP16 = 1
+RSPL_PREC_FP16X3 = 2  # SuperPoint only: split fp16 (hi + lo planes, three fp16 MFMA products per step)
 
 BA_TRACE_W = 12  # RSPL_BA_TRACE_W
 BA_TRACE_FIELDS = ("submit", "stage0", "stage1", "run0", "upload", "opt1", "opt2", "end", "slot", "grew", "iters",

@@ -24,6 +24,8 @@ struct rspl_sp {
   // RSPL_PREC_FP16: the 3x3 conv weights as fp16 [9][Cout][Cin]
   _Float16 *hw1b, *hw2a, *hw2b, *hw3a, *hw3b, *hw4a, *hw4b, *hwPD;
   _Float16 *fwPb, *fwDb;  // convPb / convDb in MFMA B-fragment order (sp::HeadHArgs / TapArgs)
+  // RSPL_PREC_FP16X3: the lo halves (w - (float)(half)w) of the same arrays, same layouts
+  _Float16 *lw1b, *lw2a, *lw2b, *lw3a, *lw3b, *lw4a, *lw4b, *lwPD, *lfwPb, *lfwDb;
   // activations
   float *actA, *actB, *cells, *scores, *nms, *desc;
   unsigned long long* cand;
@@ -47,11 +49,18 @@ namespace {
 
 // torch conv weight [co][ci][3][3] -> [ky][kx][ci][co_total] at column offset co_off
 // fp16 layout [9][Cout][Cin] (input channels contiguous: one 16-byte MFMA operand read)
-void relayout3x3_h(const Tensor& t, int cin, int cout, std::vector<_Float16>& dst, int co_total, int co_off) {
+// lo = true: the lo half of the split-fp16 pair, (half)(w - (float)(half)w)
+_Float16 half_part(float w, bool lo) {
+  const _Float16 hi = (_Float16)w;
+  return lo ? (_Float16)(w - (float)hi) : hi;
+}
+
+void relayout3x3_h(const Tensor& t, int cin, int cout, std::vector<_Float16>& dst, int co_total, int co_off,
+                   bool lo = false) {
   for (int co = 0; co < cout; co++)
     for (int ci = 0; ci < cin; ci++)
       for (int k = 0; k < 9; k++)
-        dst[((size_t)k * co_total + co_off + co) * cin + ci] = (_Float16)t.data[((size_t)co * cin + ci) * 9 + k];
+        dst[((size_t)k * co_total + co_off + co) * cin + ci] = half_part(t.data[((size_t)co * cin + ci) * 9 + k], lo);
 }
 
 void relayout3x3(const Tensor& t, int cin, int cout, std::vector<float>& dst, int co_total, int co_off) {
@@ -84,6 +93,10 @@ void carve(F& ar, rspl_sp* s, int B, int H, int W, int cap) {
   take(s->wPb, 256 * 96); take(s->bPb, 96);
   take(s->wDb, 256 * 256); take(s->bDb, 256);
   take(s->fwPb, 256 * 96); take(s->fwDb, 256 * 256);
+  take(s->lw1b, 9 * 64 * 64); take(s->lw2a, 9 * 64 * 64); take(s->lw2b, 9 * 64 * 64); take(s->lw3a, 9 * 64 * 128);
+  take(s->lw3b, 9 * 128 * 128); take(s->lw4a, 9 * 128 * 128); take(s->lw4b, 9 * 128 * 128);
+  take(s->lwPD, 9 * 128 * 512);
+  take(s->lfwPb, 256 * 96); take(s->lfwDb, 256 * 256);
   take(s->actA, B * HW * 16);
   take(s->actB, B * HW * 16);
   take(s->cells, B * P * 512);
@@ -105,8 +118,9 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
   RSPL_CHECK_ARG(cfg && out, "rspl_sp_create: NULL argument");
   RSPL_CHECK_ARG(cfg->max_height > 0 && cfg->max_width > 0 && cfg->max_height % 8 == 0 && cfg->max_width % 8 == 0,
                  "max_height/max_width must be positive multiples of 8");
-  RSPL_CHECK_ARG(cfg->precision == RSPL_PREC_FP32 || cfg->precision == RSPL_PREC_FP16,
-                 "precision must be RSPL_PREC_FP32 or RSPL_PREC_FP16");
+  RSPL_CHECK_ARG(cfg->precision == RSPL_PREC_FP32 || cfg->precision == RSPL_PREC_FP16 ||
+                     cfg->precision == RSPL_PREC_FP16X3,
+                 "precision must be RSPL_PREC_FP32, RSPL_PREC_FP16 or RSPL_PREC_FP16X3");
   RSPL_CHECK_ARG(cfg->remove_borders >= 0, "remove_borders must be >= 0");
   *out = nullptr;
   std::vector<Tensor> ts;
@@ -136,11 +150,11 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
   }
 
   // ---- weights: relayout once (convert2onnx/superpoint.py:88-105) ----
-  struct C3 { const char* name; int cin, cout; float *w, *b; _Float16* hw; };
-  const C3 convs[] = {{"conv1b", 64, 64, s->w1b, s->b1b, s->hw1b}, {"conv2a", 64, 64, s->w2a, s->b2a, s->hw2a},
-                      {"conv2b", 64, 64, s->w2b, s->b2b, s->hw2b}, {"conv3a", 64, 128, s->w3a, s->b3a, s->hw3a},
-                      {"conv3b", 128, 128, s->w3b, s->b3b, s->hw3b}, {"conv4a", 128, 128, s->w4a, s->b4a, s->hw4a},
-                      {"conv4b", 128, 128, s->w4b, s->b4b, s->hw4b}};
+  struct C3 { const char* name; int cin, cout; float *w, *b; _Float16 *hw, *lw; };
+  const C3 convs[] = {{"conv1b", 64, 64, s->w1b, s->b1b, s->hw1b, s->lw1b}, {"conv2a", 64, 64, s->w2a, s->b2a, s->hw2a, s->lw2a},
+                      {"conv2b", 64, 64, s->w2b, s->b2b, s->hw2b, s->lw2b}, {"conv3a", 64, 128, s->w3a, s->b3a, s->hw3a, s->lw3a},
+                      {"conv3b", 128, 128, s->w3b, s->b3b, s->hw3b, s->lw3b}, {"conv4a", 128, 128, s->w4a, s->b4a, s->hw4a, s->lw4a},
+                      {"conv4b", 128, 128, s->w4b, s->b4b, s->hw4b, s->lw4b}};
   auto uph = [&](_Float16* dst, const std::vector<_Float16>& src) {
     return hipMemcpy(dst, src.data(), src.size() * sizeof(_Float16), hipMemcpyHostToDevice) == hipSuccess;
   };
@@ -154,9 +168,10 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
     if (!w || !b) { rspl_sp_destroy(s); return RSPL_E_WEIGHTS; }
     std::vector<float> r((size_t)9 * c.cin * c.cout);
     relayout3x3(*w, c.cin, c.cout, r, c.cout, 0);
-    std::vector<_Float16> rh((size_t)9 * c.cin * c.cout);
+    std::vector<_Float16> rh((size_t)9 * c.cin * c.cout), rl(rh.size());
     relayout3x3_h(*w, c.cin, c.cout, rh, c.cout, 0);
-    ok &= up(c.w, r) && up(c.b, b->data) && uph(c.hw, rh);
+    relayout3x3_h(*w, c.cin, c.cout, rl, c.cout, 0, true);
+    ok &= up(c.w, r) && up(c.b, b->data) && uph(c.hw, rh) && uph(c.lw, rl);
   }
   const Tensor *w1a = find(ts, "conv1a.weight", 64 * 9), *b1a = find(ts, "conv1a.bias", 64);
   const Tensor *wPa = find(ts, "convPa.weight", 256 * 128 * 9), *bPa = find(ts, "convPa.bias", 256);
@@ -172,10 +187,12 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
     std::vector<float> r((size_t)9 * 128 * 512), b(512);
     relayout3x3(*wPa, 128, 256, r, 512, 0);
     relayout3x3(*wDa, 128, 256, r, 512, 256);
-    std::vector<_Float16> rh((size_t)9 * 128 * 512);
+    std::vector<_Float16> rh((size_t)9 * 128 * 512), rl(rh.size());
     relayout3x3_h(*wPa, 128, 256, rh, 512, 0);
     relayout3x3_h(*wDa, 128, 256, rh, 512, 256);
-    ok &= uph(s->hwPD, rh);
+    relayout3x3_h(*wPa, 128, 256, rl, 512, 0, true);
+    relayout3x3_h(*wDa, 128, 256, rl, 512, 256, true);
+    ok &= uph(s->hwPD, rh) && uph(s->lwPD, rl);
     for (int i = 0; i < 256; i++) { b[i] = bPa->data[i]; b[256 + i] = bDa->data[i]; }
     ok &= up(s->wPD, r) && up(s->bPD, b);
   }
@@ -189,17 +206,18 @@ extern "C" int rspl_sp_create(const rspl_sp_config* cfg, const char* weights_pat
       for (int ci = 0; ci < 256; ci++) d[ci * 256 + co] = wDb->data[co * 256 + ci];
     ok &= up(s->wPb, r) && up(s->bPb, b) && up(s->wDb, d) && up(s->bDb, bDb->data);
     // fp16 fragments: [N-tile][k-step][lane][8], lane (c, h) holding W[16 t + 8 h + j][32 n + c]
-    auto frag = [](const std::vector<float>& wkn, int N) {
+    auto frag = [](const std::vector<float>& wkn, int N, bool lo) {
       std::vector<_Float16> f((size_t)256 * N);
       for (int n = 0; n < N / 32; n++)
         for (int t = 0; t < 16; t++)
           for (int lane = 0; lane < 64; lane++)
             for (int j = 0; j < 8; j++)
               f[(((size_t)n * 16 + t) * 64 + lane) * 8 + j] =
-                  (_Float16)wkn[(size_t)(16 * t + 8 * (lane >> 5) + j) * N + 32 * n + (lane & 31)];
+                  half_part(wkn[(size_t)(16 * t + 8 * (lane >> 5) + j) * N + 32 * n + (lane & 31)], lo);
       return f;
     };
-    ok &= uph(s->fwPb, frag(r, 96)) && uph(s->fwDb, frag(d, 256));
+    ok &= uph(s->fwPb, frag(r, 96, false)) && uph(s->fwDb, frag(d, 256, false)) && uph(s->lfwPb, frag(r, 96, true)) &&
+          uph(s->lfwDb, frag(d, 256, true));
   }
   {  // src/super_point.cpp:148: float(u8) / 255.0 computed in double, stored as float
     std::vector<float> lut(256);
@@ -268,7 +286,53 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
   c.w1a = s->w1a;
   c.b1a = s->b1a;
   // encoder (superpoint.py:117-127)
-  if (s->cfg.precision == RSPL_PREC_FP16) {  // the reference's TensorRT kFP16 engine (super_point.cpp:98)
+  if (s->cfg.precision == RSPL_PREC_FP16X3) {
+    // split fp16: every activation a pair of fp16 planes (hi at the buffer's start, lo half a buffer on: the
+    // fp32-sized arenas hold both), three MFMA products per step (sp_kernels.hip conv3x3_x3_kernel)
+    const size_t act_pl = (size_t)B * H * W * 16, cell_pl = (size_t)B * P * 512;  // halves per lo-plane offset
+    _Float16* hA = reinterpret_cast<_Float16*>(s->actA);
+    _Float16* hB = reinterpret_cast<_Float16*>(s->actB);
+    _Float16* hC = reinterpret_cast<_Float16*>(s->cells);
+    auto layer = [&](const _Float16* in, const _Float16* hw, const _Float16* lw, const float* bias, _Float16* out) {
+      c.hin = in; c.hin_lo = in ? in + act_pl : nullptr; c.hw = hw; c.hw_lo = lw; c.bias = bias;
+      c.hout = out; c.hout_lo = out + (out == hC ? cell_pl : act_pl);
+    };
+    c.H = H; c.W = W; c.cout = 64;
+    layer(nullptr, s->hw1b, s->lw1b, s->b1b, hA);
+    RSPL_HIP(conv3x3_x3(c, 64, true, true, B, st, s->timer.slot(0), s->timer.slot(1)));  // conv1a+1b+pool
+    c.H = H2; c.W = W2; c.cout = 64; layer(hA, s->hw2a, s->lw2a, s->b2a, hB);
+    RSPL_HIP(conv3x3_x3(c, 64, false, false, B, st));                                   // conv2a
+    layer(hB, s->hw2b, s->lw2b, s->b2b, hA);
+    RSPL_HIP(conv3x3_x3(c, 64, true, false, B, st));                                    // conv2b+pool
+    c.H = H4; c.W = W4; c.cout = 128; layer(hA, s->hw3a, s->lw3a, s->b3a, hB);
+    RSPL_HIP(conv3x3_x3(c, 64, false, false, B, st));                                   // conv3a
+    layer(hB, s->hw3b, s->lw3b, s->b3b, hA);
+    RSPL_HIP(conv3x3_x3(c, 128, true, false, B, st));                                   // conv3b+pool
+    c.H = H8; c.W = W8; layer(hA, s->hw4a, s->lw4a, s->b4a, hB);
+    RSPL_HIP(conv3x3_x3(c, 128, false, false, B, st));                                  // conv4a
+    layer(hB, s->hw4b, s->lw4b, s->b4b, hA);
+    RSPL_HIP(conv3x3_x3(c, 128, false, false, B, st));                                  // conv4b
+    s->timer.mark(2, st);
+    c.cout = 512; layer(hA, s->hwPD, s->lwPD, s->bPD, hC);
+    RSPL_HIP(conv3x3_x3(c, 128, false, false, B, st));                                  // convPa | convDa
+    s->timer.mark(3, st);
+    HeadHArgs h{};
+    h.cells = hC; h.cells_lo = hC + cell_pl; h.wPb = s->fwPb; h.wPb_lo = s->lfwPb; h.bPb = s->bPb;
+    h.scores = s->scores; h.B = B; h.P = P; h.W8 = W8;
+    RSPL_HIP(det_head_h(h, true, st));
+    s->timer.mark(4, st);
+    if (int rc = nms_topk(s, B, H, W, k, st)) return rc;
+    s->timer.mark(6, st);
+    TapArgs ta{};
+    ta.cells = hC; ta.cells_lo = hC + cell_pl; ta.wDb = s->fwDb; ta.wDb_lo = s->lfwDb; ta.bDb = s->bDb;
+    ta.sel = s->sel; ta.sel_count = s->sel_count; ta.sel_stride = kCandCap; ta.per_image = (k > 0 ? k : kCandCap);
+    ta.nms = s->scores; ta.features = d_features; ta.feat_cap = capacity; ta.counts = d_counts; ta.B = B; ta.H = H; ta.W = W;
+    RSPL_HIP(sample_taps_h(ta, true, st));
+    s->timer.mark(7, st);
+    s->timer.end_call();
+    s->last_B = B; s->last_H = H; s->last_W = W;
+    return RSPL_OK;
+  } else if (s->cfg.precision == RSPL_PREC_FP16) {  // the reference's TensorRT kFP16 engine (super_point.cpp:98)
     _Float16* hA = reinterpret_cast<_Float16*>(s->actA);
     _Float16* hB = reinterpret_cast<_Float16*>(s->actB);
     c.H = H; c.W = W; c.cout = 64; c.hw = s->hw1b; c.bias = s->b1b; c.hout = hA;
@@ -293,7 +357,7 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
     // detector head (superpoint.py:130-135) on fp16 MFMA
     HeadHArgs h{};
     h.cells = c.hout; h.wPb = s->fwPb; h.bPb = s->bPb; h.scores = s->scores; h.B = B; h.P = P; h.W8 = W8;
-    RSPL_HIP(det_head_h(h, st));
+    RSPL_HIP(det_head_h(h, false, st));
     s->timer.mark(4, st);
     if (int rc = nms_topk(s, B, H, W, k, st)) return rc;
     // descriptor head at the sampled taps + sampling + packing (superpoint.py:159-161,
@@ -303,7 +367,7 @@ extern "C" int rspl_sp_infer_device(rspl_sp* s, const uint8_t* d_images, int B, 
     ta.cells = c.hout; ta.wDb = s->fwDb; ta.bDb = s->bDb;
     ta.sel = s->sel; ta.sel_count = s->sel_count; ta.sel_stride = kCandCap; ta.per_image = (k > 0 ? k : kCandCap);
     ta.nms = s->scores; ta.features = d_features; ta.feat_cap = capacity; ta.counts = d_counts; ta.B = B; ta.H = H; ta.W = W;
-    RSPL_HIP(sample_taps_h(ta, st));
+    RSPL_HIP(sample_taps_h(ta, false, st));
     s->timer.mark(7, st);
     s->timer.end_call();
     s->last_B = B; s->last_H = H; s->last_W = W;

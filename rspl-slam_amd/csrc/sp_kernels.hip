@@ -641,6 +641,250 @@ __global__ __launch_bounds__(256) void conv1_res_kernel(ConvArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Split-fp16 3x3 conv (RSPL_PREC_FP16X3): fp32-grade accuracy at the fp16 MFMA rate.  Every operand is
+// carried as a pair of fp16 planes, v = hi + lo (hi = (half)v, lo = (half)(v - hi): 22 significant bits,
+// lo unscaled -- below |v| ~ 0.125 it is subnormal, its absolute error then under 3e-8), and each k-step
+// accumulates the three products hi*hi + lo*hi + hi*lo on v_mfma_f32_32x32x16_f16 into ONE fp32
+// accumulator (the dropped lo*lo term is 2^-22 relative).  Against the fp32 oracle this keeps SuperPoint's
+// keypoint sets identical where the fp16 path loses 1-5 of 400 keypoints per image near the top-k cut
+// (tools/sp_fp16_split.py: a CPU emulation of both paths over the C1 images).  Same tiling as
+// conv3x3_h_kernel with 16 input channels per stage (LDS: hi + lo halo and weights, 86 KB at TH = 16, so a
+// local-BA Schur chunk wave (35 KB) still fits beside a workgroup); conv1a (FUSE1A) runs split on MFMA
+// too, from the image in fp32 (u8 / 255 as src/super_point.cpp:146-150) split into hi + lo.
+// Output planes: hout (hi) and hout_lo (lo), the same NHWC layout.
+// ---------------------------------------------------------------------------
+constexpr int XCK = 16;       // input channels per stage
+constexpr int XCS = XCK + 8;  // LDS row stride in halves (48-byte rows: conflict-free ds_read_b128)
+
+struct Half2 {
+  _Float16 hi, lo;
+};
+__device__ __forceinline__ Half2 split16(float v) {
+  const _Float16 hi = (_Float16)v;
+  return {hi, (_Float16)(v - (float)hi)};
+}
+
+template <int CIN, int TH, bool POOL, bool FUSE1A>
+__global__ __launch_bounds__(256) void conv3x3_x3_kernel(ConvArgs a) {
+  static_assert(CIN % 32 == 0, "Cin must be a multiple of 32");
+  constexpr int HX = TW + 2, HY = TH + 2, MT = TH / 8;
+  constexpr int HALO = HY * HX * XCS, WTS = 9 * 64 * XCS;
+  __shared__ __attribute__((aligned(16))) _Float16 halo[2 * HALO];  // [hi | lo]
+  __shared__ __attribute__((aligned(16))) _Float16 wts[2 * WTS];    // [hi | lo]: [9][64 co][XCS]
+  __shared__ float patch[FUSE1A ? (TH + 4) * (TW + 4) : 1];
+
+  const int H = a.H, W = a.W, COUT = a.cout;
+  const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
+  const int per_img = tiles_x * tiles_y;
+  const int bi = blockIdx.x / per_img, t = blockIdx.x % per_img;
+  const int y0 = (t / tiles_x) * TH, x0 = (t % tiles_x) * TW;
+  const int co0 = blockIdx.y * 64;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int ml = lane & 31, kl = lane >> 5;
+
+  if constexpr (FUSE1A) {
+    const uint8_t* img = a.img + (size_t)bi * a.img_pitch;
+    for (int i = tid; i < (TH + 4) * (TW + 4); i += 256) {
+      const int py = i / (TW + 4), px = i % (TW + 4);
+      const int y = y0 - 2 + py, x = x0 - 2 + px;
+      // src/super_point.cpp:146-150 normalisation, (float)(u / 255.0) in double (= the host LUT)
+      patch[i] = (y >= 0 && y < H && x >= 0 && x < W) ? (float)((double)img[(size_t)y * a.img_stride + x] / 255.0)
+                                                      : 0.f;
+    }
+  }
+  floatx16 acc[MT][2];
+#pragma unroll
+  for (int m = 0; m < MT; m++)
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+      for (int r = 0; r < 16; r++) acc[m][n][r] = 0.f;
+
+  // next stage's weights / halo (hi and lo) in registers while the current stage runs on MFMA
+  constexpr int W8 = 9 * 64 * (XCK / 8);               // half8 per weight plane per stage
+  constexpr int WPT = 2 * W8 / 256;                    // 9
+  static_assert(2 * W8 % 256 == 0, "weight staging");
+  constexpr int HALO8 = HY * HX * (XCK / 8), HPT = (2 * HALO8 + 255) / 256;
+  half8 pw[WPT], ph[FUSE1A ? 1 : HPT];
+  auto fetch = [&](int c0) {
+#pragma unroll
+    for (int r = 0; r < WPT; r++) {
+      const int i = tid + 256 * r, pl = i / W8, j = i % W8, q = j % (XCK / 8), rr = j / (XCK / 8);
+      const int kk = rr / 64, co = rr % 64;
+      pw[r] = *reinterpret_cast<const half8*>((pl ? a.hw_lo : a.hw) + ((size_t)kk * COUT + co0 + co) * CIN + c0 + 8 * q);
+    }
+    if constexpr (!FUSE1A) {
+#pragma unroll
+      for (int r = 0; r < HPT; r++) {
+        const int i = tid + 256 * r, pl = i / HALO8, j = i % HALO8, q = j % (XCK / 8), pix = j / (XCK / 8);
+        const int hy = pix / HX, hx = pix % HX;
+        const int y = y0 - 1 + hy, x = x0 - 1 + hx;
+        half8 v = {};
+        if (i < 2 * HALO8 && y >= 0 && y < H && x >= 0 && x < W)
+          v = *reinterpret_cast<const half8*>((pl ? a.hin_lo : a.hin) + (size_t)bi * H * W * CIN +
+                                              ((size_t)y * W + x) * CIN + c0 + 8 * q);
+        ph[r] = v;
+      }
+    }
+  };
+  // conv1a operands (FUSE1A): B[k][c] = W1a[c][k] (k < 9), the bias at k = 9, split hi / lo
+  half8 bwh[FUSE1A ? 2 : 1], bwl[FUSE1A ? 2 : 1];
+  if constexpr (FUSE1A) {
+#pragma unroll
+    for (int hf = 0; hf < 2; hf++)
+#pragma unroll
+      for (int j = 0; j < 8; j++) {
+        const int k = 8 * kl + j, c = 32 * hf + ml;
+        const Half2 w = split16(k < 9 ? a.w1a[c * 9 + k] : (k == 9 ? a.b1a[c] : 0.f));
+        bwh[hf][j] = w.hi;
+        bwl[hf][j] = w.lo;
+      }
+  }
+  fetch(0);
+  for (int c0 = 0; c0 < CIN; c0 += XCK) {
+    __syncthreads();
+    if constexpr (FUSE1A) {
+      // conv1a -> ReLU for channels c0 .. c0 + 15 of the halo: the transposed product D[c][px] =
+      // W1a[c][k] P[k][px] of the 32-channel half holding them (lane (px, kl) gets channels 8 q + 4 kl + e;
+      // this stage keeps q = 2 (c0 % 32 / 16), + 1), three products per MFMA step
+      const int hf = (c0 % 64) / 32, q0 = 2 * ((c0 % 32) / 16);
+      const int hx = ml, x = x0 - 1 + hx;
+      for (int hy = wv; hy < HY; hy += 4) {
+        const int y = y0 - 1 + hy;
+        half8 ah, al;
+#pragma unroll
+        for (int j = 0; j < 8; j++) {
+          const int k = 8 * kl + j;
+          float v = 0.f;
+          if (hx < HX) v = k < 9 ? patch[(hy + k / 3) * (TW + 4) + hx + k % 3] : (k == 9 ? 1.f : 0.f);
+          const Half2 p = split16(v);
+          ah[j] = p.hi;
+          al[j] = p.lo;
+        }
+        floatx16 d;
+#pragma unroll
+        for (int r = 0; r < 16; r++) d[r] = 0.f;
+        d = mfma16(bwh[hf], ah, d);
+        d = mfma16(bwh[hf], al, d);
+        d = mfma16(bwl[hf], ah, d);
+        const bool in = y >= 0 && y < H && x >= 0 && x < W;
+        if (hx < HX) {
+#pragma unroll
+          for (int qq = 0; qq < 2; qq++) {
+            typedef _Float16 half4 __attribute__((ext_vector_type(4)));
+            half4 h4, l4;
+#pragma unroll
+            for (int e = 0; e < 4; e++) {
+              const Half2 p = split16(in ? fmaxf(d[4 * (q0 + qq) + e], 0.f) : 0.f);
+              h4[e] = p.hi;
+              l4[e] = p.lo;
+            }
+            const int o = (hy * HX + hx) * XCS + 8 * qq + 4 * kl;
+            *reinterpret_cast<half4*>(&halo[o]) = h4;
+            *reinterpret_cast<half4*>(&halo[HALO + o]) = l4;
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < HPT; r++) {
+        const int i = tid + 256 * r, pl = i / HALO8, j = i % HALO8;
+        if (i < 2 * HALO8) *reinterpret_cast<half8*>(&halo[pl * HALO + (j / (XCK / 8)) * XCS + 8 * (j % (XCK / 8))]) = ph[r];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < WPT; r++) {
+      const int i = tid + 256 * r, pl = i / W8, j = i % W8;
+      *reinterpret_cast<half8*>(&wts[pl * WTS + (j / (XCK / 8)) * XCS + 8 * (j % (XCK / 8))]) = pw[r];
+    }
+    __syncthreads();
+    if (c0 + XCK < CIN) fetch(c0 + XCK);
+#pragma unroll
+    for (int kk = 0; kk < 9; kk++) {
+      const int ky = kk / 3, kx = kk % 3;
+      half8 ah[MT], al[MT], bh[2], bl[2];
+#pragma unroll
+      for (int m = 0; m < MT; m++) {
+        const int ly = wv * (TH / 4) + 2 * m + (ml >> 4);
+        const int o = ((ly + ky) * HX + (ml & 15) + kx) * XCS + 8 * kl;
+        ah[m] = *reinterpret_cast<const half8*>(&halo[o]);
+        al[m] = *reinterpret_cast<const half8*>(&halo[HALO + o]);
+      }
+#pragma unroll
+      for (int n = 0; n < 2; n++) {
+        const int o = (kk * 64 + n * 32 + ml) * XCS + 8 * kl;
+        bh[n] = *reinterpret_cast<const half8*>(&wts[o]);
+        bl[n] = *reinterpret_cast<const half8*>(&wts[WTS + o]);
+      }
+#pragma unroll
+      for (int m = 0; m < MT; m++)
+#pragma unroll
+        for (int n = 0; n < 2; n++) {
+          acc[m][n] = mfma16(al[m], bh[n], acc[m][n]);
+          acc[m][n] = mfma16(ah[m], bl[n], acc[m][n]);
+          acc[m][n] = mfma16(ah[m], bh[n], acc[m][n]);
+        }
+    }
+  }
+
+  // epilogue: bias + ReLU (+ 2x2 max-pool), split into hi / lo, staged through LDS (the weight buffer) so
+  // the global stores are 16-byte rows of 8 channels
+  constexpr int OS = 72;  // halves per pixel row in LDS (64 channels + pad)
+  constexpr int OPIX = POOL ? (TH / 2) * 8 : TH * 16;
+  static_assert((POOL ? 2 : 1) * OPIX * OS <= 2 * WTS, "output tile exceeds the weight buffer");
+  float bias[2];
+#pragma unroll
+  for (int n = 0; n < 2; n++) bias[n] = a.bias[co0 + n * 32 + ml];
+  const int Ho = POOL ? H / 2 : H, Wo = POOL ? W / 2 : W;
+  // POOL: both planes staged at once; otherwise hi, then lo (each fills most of the buffer)
+#pragma unroll
+  for (int pass = 0; pass < (POOL ? 1 : 2); pass++) {
+    __syncthreads();
+#pragma unroll
+    for (int n = 0; n < 2; n++)
+#pragma unroll
+      for (int m = 0; m < MT; m++) {
+        if constexpr (POOL) {
+          const int pyl = wv * (TH / 8) + m;
+#pragma unroll
+          for (int g = 0; g < 4; g++) {
+            const int r0 = (g & 1) * 2 + (g >> 1) * 4;
+            const int pc = (r0 & 3) + 8 * ((r0 >> 2) & 1) + 4 * kl;
+            float v = fmaxf(fmaxf(acc[m][n][r0], acc[m][n][r0 + 1]), fmaxf(acc[m][n][r0 + 8], acc[m][n][r0 + 9]));
+            v += bias[n];
+            const Half2 p = split16(v > 0.f ? v : 0.f);
+            const int o = (pyl * 8 + (pc >> 1)) * OS + n * 32 + ml;
+            wts[o] = p.hi;
+            wts[OPIX * OS + o] = p.lo;
+          }
+        } else {
+          const int ly = wv * (TH / 4) + 2 * m;
+#pragma unroll
+          for (int r = 0; r < 16; r++) {
+            const int mm = (r & 3) + 8 * (r >> 2) + 4 * kl;
+            const float v = acc[m][n][r] + bias[n];
+            const Half2 p = split16(v > 0.f ? v : 0.f);
+            wts[((ly + (mm >> 4)) * 16 + (mm & 15)) * OS + n * 32 + ml] = pass ? p.lo : p.hi;
+          }
+        }
+      }
+    __syncthreads();
+#pragma unroll
+    for (int pl = 0; pl < (POOL ? 2 : 1); pl++) {
+      _Float16* out = (POOL ? (pl ? a.hout_lo : a.hout) : (pass ? a.hout_lo : a.hout)) + (size_t)bi * Ho * Wo * COUT;
+      for (int i = tid; i < OPIX * 8; i += 256) {
+        const int px = i >> 3, q = i & 7;
+        const int y = POOL ? (y0 >> 1) + (px >> 3) : y0 + (px >> 4);
+        const int x = POOL ? (x0 >> 1) + (px & 7) : x0 + (px & 15);
+        if (y < Ho && x < Wo)
+          *reinterpret_cast<half8*>(out + ((size_t)y * Wo + x) * COUT + co0 + 8 * q) =
+              *reinterpret_cast<const half8*>(&wts[pl * OPIX * OS + px * OS + 8 * q]);
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // 1x1 heads on the H/8 x W/8 cell grid.  in = [P][512] (convPa | convDa, ReLU'd).
 //   MODE 0: convPb 256->65, softmax over 65, drop dustbin, depth-to-space ->
 //           scores [H][W]  (superpoint.py:131-135)
@@ -764,29 +1008,45 @@ __global__ __launch_bounds__(256) void head_kernel(HeadArgs a) {
 //                  src/super_point.cpp:206-319.  A workgroup takes 8 keypoints = 32 tap rows
 //                  (one M-tile); wave w owns output channels 64w .. 64w+63.
 // ---------------------------------------------------------------------------
+// X3 (RSPL_PREC_FP16X3): cells and weights as hi + lo fp16 planes, three products per MFMA step (the split
+// arithmetic of conv3x3_x3_kernel)
+template <bool X3>
 __global__ __launch_bounds__(256) void det_head_h_kernel(HeadHArgs a) {
   constexpr int NT = 3;  // 96 columns, 65 real
   const int total = a.B * a.P;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, ml = lane & 31, kl = lane >> 5;
   const int base = (blockIdx.x * 4 + wv) * 32;
   if (base >= total) return;  // per wave: no barriers below
-  const _Float16* row = a.cells + (size_t)min(base + ml, total - 1) * 512 + 8 * kl;
-  half8 av[16];
+  const size_t ro = (size_t)min(base + ml, total - 1) * 512 + 8 * kl;
+  half8 av[16], al[X3 ? 16 : 1];
 #pragma unroll
-  for (int t = 0; t < 16; t++) av[t] = *reinterpret_cast<const half8*>(row + 16 * t);
+  for (int t = 0; t < 16; t++) av[t] = *reinterpret_cast<const half8*>(a.cells + ro + 16 * t);
+  if constexpr (X3)
+#pragma unroll
+    for (int t = 0; t < 16; t++) al[t] = *reinterpret_cast<const half8*>(a.cells_lo + ro + 16 * t);
   floatx16 acc[NT];
 #pragma unroll
   for (int n = 0; n < NT; n++)
 #pragma unroll
     for (int r = 0; r < 16; r++) acc[n][r] = 0.f;
   const half8* wf = reinterpret_cast<const half8*>(a.wPb) + lane;
+  const half8* wfl = reinterpret_cast<const half8*>(a.wPb_lo) + lane;
 #pragma unroll
   for (int t = 0; t < 16; t++) {
-    half8 bv[NT];
+    half8 bv[NT], bl[X3 ? NT : 1];
 #pragma unroll
     for (int n = 0; n < NT; n++) bv[n] = wf[(n * 16 + t) * 64];
+    if constexpr (X3)
 #pragma unroll
-    for (int n = 0; n < NT; n++) acc[n] = mfma16(av[t], bv[n], acc[n]);
+      for (int n = 0; n < NT; n++) bl[n] = wfl[(n * 16 + t) * 64];
+#pragma unroll
+    for (int n = 0; n < NT; n++) {
+      if constexpr (X3) {
+        acc[n] = mfma16(al[t], bv[n], acc[n]);
+        acc[n] = mfma16(av[t], bl[n], acc[n]);
+      }
+      acc[n] = mfma16(av[t], bv[n], acc[n]);
+    }
   }
 #pragma unroll
   for (int n = 0; n < NT; n++) {
@@ -833,6 +1093,7 @@ __global__ __launch_bounds__(256) void det_head_h_kernel(HeadHArgs a) {
   }
 }
 
+template <bool X3>
 __global__ __launch_bounds__(256) void sample_taps_h_kernel(TapArgs a) {
   __shared__ int tcell[32];      // tap row 4 kp + q: cell of tap q (nw, ne, sw, se) of keypoint kp
   __shared__ double twt[32];     // its bilinear weight
@@ -882,19 +1143,30 @@ __global__ __launch_bounds__(256) void sample_taps_h_kernel(TapArgs a) {
     }
   }
   __syncthreads();
-  const _Float16* row = a.cells + ((size_t)bi * P + tcell[ml]) * 512 + 256 + 8 * kl;
-  half8 av[16];
+  const size_t ro = ((size_t)bi * P + tcell[ml]) * 512 + 256 + 8 * kl;
+  half8 av[16], al[X3 ? 16 : 1];
 #pragma unroll
-  for (int t = 0; t < 16; t++) av[t] = *reinterpret_cast<const half8*>(row + 16 * t);
+  for (int t = 0; t < 16; t++) av[t] = *reinterpret_cast<const half8*>(a.cells + ro + 16 * t);
+  if constexpr (X3)
+#pragma unroll
+    for (int t = 0; t < 16; t++) al[t] = *reinterpret_cast<const half8*>(a.cells_lo + ro + 16 * t);
   floatx16 acc[2];
 #pragma unroll
   for (int j = 0; j < 2; j++)
 #pragma unroll
     for (int r = 0; r < 16; r++) acc[j][r] = 0.f;
   const half8* wf = reinterpret_cast<const half8*>(a.wDb) + lane;
+  const half8* wfl = reinterpret_cast<const half8*>(a.wDb_lo) + lane;
 #pragma unroll
   for (int t = 0; t < 16; t++) {
     const half8 b0 = wf[((2 * wv) * 16 + t) * 64], b1 = wf[((2 * wv + 1) * 16 + t) * 64];
+    if constexpr (X3) {
+      const half8 l0 = wfl[((2 * wv) * 16 + t) * 64], l1 = wfl[((2 * wv + 1) * 16 + t) * 64];
+      acc[0] = mfma16(al[t], b0, acc[0]);
+      acc[0] = mfma16(av[t], l0, acc[0]);
+      acc[1] = mfma16(al[t], b1, acc[1]);
+      acc[1] = mfma16(av[t], l1, acc[1]);
+    }
     acc[0] = mfma16(av[t], b0, acc[0]);
     acc[1] = mfma16(av[t], b1, acc[1]);
   }
@@ -1422,16 +1694,40 @@ hipError_t heads(const HeadArgs& a, int mode, hipStream_t s) {
   return hipGetLastError();
 }
 
-hipError_t det_head_h(const HeadHArgs& a, hipStream_t s) {
+hipError_t det_head_h(const HeadHArgs& a, bool x3, hipStream_t s) {
   const int blocks = (a.B * a.P + 127) / 128;
-  hipLaunchKernelGGL(det_head_h_kernel, dim3(blocks), dim3(256), 0, s, a);
+  if (x3) hipLaunchKernelGGL(det_head_h_kernel<true>, dim3(blocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(det_head_h_kernel<false>, dim3(blocks), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t sample_taps_h(const TapArgs& a, hipStream_t s) {
+hipError_t sample_taps_h(const TapArgs& a, bool x3, hipStream_t s) {
   const int blocks = a.B * ((a.per_image + 7) / 8);
-  hipLaunchKernelGGL(sample_taps_h_kernel, dim3(blocks), dim3(256), 0, s, a);
+  if (x3) hipLaunchKernelGGL(sample_taps_h_kernel<true>, dim3(blocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(sample_taps_h_kernel<false>, dim3(blocks), dim3(256), 0, s, a);
   return hipGetLastError();
+}
+
+template <int CIN, int TH, bool POOL, bool FUSE1A>
+static hipError_t launch_conv_x3(const ConvArgs& a, int B, hipStream_t s, hipEvent_t t0 = nullptr,
+                                 hipEvent_t t1 = nullptr) {
+  const int tiles = ((a.W + TW - 1) / TW) * ((a.H + TH - 1) / TH);
+  dim3 grid(B * tiles, a.cout / 64);
+  hipExtLaunchKernelGGL((conv3x3_x3_kernel<CIN, TH, POOL, FUSE1A>), grid, dim3(256), 0, s, t0, t1, 0, a);
+  return hipGetLastError();
+}
+
+hipError_t conv3x3_x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hipStream_t s, hipEvent_t t0,
+                      hipEvent_t t1) {
+  const bool small = (a.H * a.W) <= 128 * 192;
+  if (fuse1a) return launch_conv_x3<64, 16, true, true>(a, B, s, t0, t1);
+  if (cin == 64 && pool) return launch_conv_x3<64, 16, true, false>(a, B, s);
+  if (cin == 64 && !pool) return small ? launch_conv_x3<64, 8, false, false>(a, B, s)
+                                       : launch_conv_x3<64, 16, false, false>(a, B, s);
+  if (cin == 128 && pool) return launch_conv_x3<128, 16, true, false>(a, B, s);
+  if (cin == 128 && !pool) return small ? launch_conv_x3<128, 8, false, false>(a, B, s)
+                                        : launch_conv_x3<128, 16, false, false>(a, B, s);
+  return hipErrorInvalidValue;
 }
 
 hipError_t nms(const NmsArgs& a, int B, hipStream_t s) {

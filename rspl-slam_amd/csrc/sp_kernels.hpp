@@ -25,6 +25,10 @@ struct ConvArgs {
   const _Float16* hin;   // NHWC [B][H][W][Cin]
   const _Float16* hw;    // [9][Cout][Cin]
   _Float16* hout;        // NHWC [B][H(/2)][W(/2)][Cout] (or `out` in fp32 for the heads)
+  // RSPL_PREC_FP16X3 (split fp16, conv3x3_x3): the lo planes of hin / hw / hout (v = hi + lo)
+  const _Float16* hin_lo;
+  const _Float16* hw_lo;
+  _Float16* hout_lo;
 };
 
 struct HeadArgs {
@@ -44,6 +48,8 @@ struct HeadHArgs {
   const float* bPb;      // [96]
   float* scores;         // [B][H][W]
   int B, P, W8;
+  const _Float16* cells_lo;  // RSPL_PREC_FP16X3: lo planes of cells / wPb
+  const _Float16* wPb_lo;
 };
 
 struct TapArgs {         // descriptors at the sampled keypoints' bilinear taps only
@@ -59,6 +65,8 @@ struct TapArgs {         // descriptors at the sampled keypoints' bilinear taps 
   int feat_cap;
   int32_t* counts;       // [B]
   int B, H, W;
+  const _Float16* cells_lo;  // RSPL_PREC_FP16X3: lo planes of cells / wDb
+  const _Float16* wDb_lo;
 };
 
 struct NmsArgs {
@@ -103,9 +111,12 @@ hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hi
 // t0 / t1 (may be null): events stamped with the fused conv1 kernel's own start / end
 hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool out_f32, int B, hipStream_t s,
                      hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
+// split-fp16 (RSPL_PREC_FP16X3) variant: hi + lo planes, three MFMA products per k-step
+hipError_t conv3x3_x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hipStream_t s,
+                      hipEvent_t t0 = nullptr, hipEvent_t t1 = nullptr);
 hipError_t heads(const HeadArgs& a, int mode, hipStream_t s);
-hipError_t det_head_h(const HeadHArgs& a, hipStream_t s);
-hipError_t sample_taps_h(const TapArgs& a, hipStream_t s);
+hipError_t det_head_h(const HeadHArgs& a, bool x3, hipStream_t s);
+hipError_t sample_taps_h(const TapArgs& a, bool x3, hipStream_t s);
 hipError_t nms(const NmsArgs& a, int B, hipStream_t s);
 hipError_t topk(const TopkArgs& a, int B, hipStream_t s);
 hipError_t sample(const SampleArgs& a, hipStream_t s);

@@ -185,3 +185,50 @@ def test_sp_conv1_resident_equals_staged(weight_blobs, tmp_path):
         res[mode] = np.load(out)
     for k in res["default"].files:
         np.testing.assert_array_equal(res["default"][k], res["stage"][k], err_msg=k)
+
+
+def _sp_x3(pkg, w, k, H, W, B=1):
+    sp = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=k, weights=w, max_height=H, max_width=W, max_batch=B,
+                                             precision=pkg.capi.RSPL_PREC_FP16X3))
+    assert sp.build(), sp.error
+    return sp
+
+
+def test_sp_fp16x3_vs_reference(pkg, golden, weight_blobs):
+    """RSPL_PREC_FP16X3 (split fp16: hi + lo planes, three fp16 MFMA products per step) at the fp32 bar:
+    identical keypoint set, scores and descriptors at the fp32 path's tolerances against the reference
+    module's outputs (sp_small, sp_euroc)."""
+    g = golden("sp_small")
+    sp = _sp_x3(pkg, weight_blobs[0], 32, 64, 96)
+    ok, F = sp.infer(g["image"])
+    assert ok, sp.error
+    compare_features(F, g["features"])
+    g = golden("sp_euroc")
+    sp = _sp_x3(pkg, weight_blobs[0], 400, 480, 752)
+    ok, F = sp.infer(g["image"])
+    assert ok, sp.error
+    G = np.concatenate([g["feat_head"], g["feat_desc"].astype(np.float64)])
+    compare_features(F, G)
+
+
+def test_sp_fp16x3_c1_images_vs_oracle(pkg, weight_blobs):
+    """The C1 images (tools/run_c1_plumbing.py: synthetic.stereo_pair seeds 300..) through the split-fp16
+    path, batched on the device, against the fp32 oracle: every image's keypoint set identical (the fp16
+    path loses 1-5 of 400 keypoints per image near the top-k cut), scores and descriptors at the fp32
+    tolerances."""
+    from rspl_slam_amd import capi
+    H, W, k = 480, 752, 400
+    sp = _sp_x3(pkg, weight_blobs[0], k, H, W, B=2)
+    imgs = capi.DeviceBuffer(2 * H * W)
+    feats, counts = capi.DeviceBuffer(2 * k * 259 * 8), capi.DeviceBuffer(2 * 4)
+    st = capi.Stream()
+    for t in range(8):
+        left, right = pkg.synthetic.stereo_pair(H, W, seed=300 + t)
+        imgs.upload(np.stack([left, right]))
+        sp.infer_device(imgs.ptr, 2, H, W, W, H * W, feats.ptr, k, counts.ptr, st.handle)
+        st.synchronize()
+        F = feats.download((2, k, 259), np.float64)
+        cnt = counts.download((2,), np.int32)
+        for b, img in enumerate((left, right)):
+            s, d = oracle.sp_forward(weight_blobs[0], post.image_to_input(img))
+            compare_features(F[b, :cnt[b]].T, post.sp_postprocess(s, d, 0.004, 4, k))

@@ -20,13 +20,14 @@ def main():
     ap.add_argument("--B", type=int, default=2)
     ap.add_argument("--k", type=int, default=400)
     ap.add_argument("--iters", type=int, default=20)
-    ap.add_argument("--precision", choices=["fp32", "fp16"], default="fp16")
+    ap.add_argument("--precision", choices=["fp32", "fp16", "fp16x3"], default="fp16")
     a = ap.parse_args()
     capi.load()
     sp_w, _ = pkg.weights.ensure_blobs(str(ROOT / "weights"))
     sp = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=a.k, weights=sp_w, max_height=a.H, max_width=a.W,
                                              max_batch=a.B,
-                                             precision=capi.RSPL_PREC_FP16 if a.precision == "fp16" else capi.RSPL_PREC_FP32))
+                                             precision={"fp16": capi.RSPL_PREC_FP16, "fp16x3": capi.RSPL_PREC_FP16X3,
+                                                        "fp32": capi.RSPL_PREC_FP32}[a.precision]))
     assert sp.build(), sp.error
     st = capi.Stream()
     imgs = capi.DeviceBuffer(a.B * a.H * a.W).upload(

@@ -184,6 +184,11 @@ def main():
         assert sps[name].build(), sps[name].error
         pms[name] = pkg.PointMatching(pkg.SuperGlueConfig(image_width=W, image_height=H, weights=sg_w,
                                                           max_keypoints=K, max_batch=1, precision=prec))
+    # split-fp16 SuperPoint (RSPL_PREC_FP16X3) in front of the fp16 SuperGlue
+    sps["fp16x3"] = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=K, weights=sp_w, max_height=H, max_width=W,
+                                                        max_batch=1, precision=C.RSPL_PREC_FP16X3))
+    assert sps["fp16x3"].build(), sps["fp16x3"].error
+    pms["fp16x3"] = pms["fp16"]
     lm = pkg.lines.LineMatcher(max_lines=512, max_points=512)
     out = pathlib.Path(a.out)
     out.parent.mkdir(parents=True, exist_ok=True)
@@ -209,7 +214,7 @@ def main():
             t_cpu += time.perf_counter() - t0
             # (b) GPU path, fp32 (parity) and fp16
             res = {}
-            for name in ("fp32", "fp16"):
+            for name in ("fp32", "fp16", "fp16x3"):
                 t0 = time.perf_counter()
                 Fg = []
                 for img in (L, R):
@@ -268,6 +273,13 @@ def main():
             lines_same = l0g.shape == l0c.shape and bool(np.array_equal(l0g, l0c))
             F16e = res["fp16"][0]
             overlap16 = [len(set(key_index(F16e[i])) & set(key_index(Fc[i]))) / max(1, Fc[i].shape[1]) for i in (0, 1)]
+            F3 = res["fp16x3"][0]
+            c3 = match_coords(res["fp16x3"][2], F3[0], F3[1])
+            m3 = match_coords(res["fp16x3"][1], F3[0], F3[1])
+            overlap3 = [len(set(key_index(F3[i])) & set(key_index(Fc[i]))) / max(1, Fc[i].shape[1]) for i in (0, 1)]
+            e3 = e2e(Fc, Z, F3, res["fp16x3"][3])
+            desc3 = max((float(np.abs(F3[i][3:, key_index(F3[i])[c]] - Fc[i][3:, key_index(Fc[i])[c]]).max())
+                         for i in (0, 1) for c in set(key_index(F3[i])) & set(key_index(Fc[i]))), default=0.0)
             dist_c = {(int(q), int(tt)): d for (q, tt), d in zip(np.asarray(mc).reshape(-1, 2), post.match_points(*dc)[1])}
             dist_g = {(int(q), int(tt)): d for q, tt, d in pms["fp32"].MatchingPoints(Fg[0], Fg[1])[1]}
             dist_err = max((abs(dist_c[k] - dist_g[k]) for k in dist_c if k in dist_g), default=0.0)
@@ -304,6 +316,12 @@ def main():
                    "match_agreement_fp16": len(cc_ & c16) / max(1, len(cc_ | c16)),
                    "keypoint_sets_identical_fp16": set(key_index(Fc[0])) == set(key_index(F16[0])) and
                    set(key_index(Fc[1])) == set(key_index(F16[1])),
+                   "keypoint_overlap_fp16x3": overlap3,
+                   "keypoint_sets_identical_fp16x3": all(set(key_index(Fc[i])) == set(key_index(F3[i])) for i in (0, 1)),
+                   "desc_max_abs_diff_fp16x3": desc3,
+                   "match_agreement_fp16x3": len(cc_ & c3) / max(1, len(cc_ | c3)),
+                   "thresholded_matches_identical_coords_fp16x3": m3 == match_coords(mc, Fc[0], Fc[1]),
+                   "e2e_fp16x3": e3,
                    "lines_left": int(len(l0c)), "merged_lines_identical": lines_same,
                    "right_lines_valid_cpu": int(lvc.sum()), "right_lines_valid_gpu": int(lvg.sum()),
                    "line_association_identical": lines_same and bool(np.array_equal(lvc, lvg)) and
@@ -382,6 +400,19 @@ def main():
         "match_agreement_fp32_coords_mean": agg("match_agreement_fp32_coords"),
         "match_agreement_fp16_mean": agg("match_agreement_fp16"),
         "match_agreement_fp16_min": float(min(r["match_agreement_fp16"] for r in rows)),
+        # split-fp16 SuperPoint (RSPL_PREC_FP16X3: hi + lo operands, three fp16 MFMA products) + fp16 SuperGlue
+        "fp16x3": {
+            "keypoint_overlap_min": float(min(min(r["keypoint_overlap_fp16x3"]) for r in rows)),
+            "keypoint_overlap_mean": float(np.mean([np.mean(r["keypoint_overlap_fp16x3"]) for r in rows])),
+            "keypoint_sets_identical_frac": agg("keypoint_sets_identical_fp16x3"),
+            "desc_max_abs_diff": float(max(r["desc_max_abs_diff_fp16x3"] for r in rows)),
+            "match_agreement_mean": agg("match_agreement_fp16x3"),
+            "match_agreement_min": float(min(r["match_agreement_fp16x3"] for r in rows)),
+            "thresholded_matches_identical_coords_frac": agg("thresholded_matches_identical_coords_fp16x3"),
+            **{f"e2e_{kind}": {c: int(sum(r["e2e_fp16x3"][kind][c] for r in rows)) for c in E2E_CLASSES}
+               for kind in ("thresholded", "mutual_nn")},
+            "note": "SuperPoint in split fp16 (RSPL_PREC_FP16X3), SuperGlue fp16; vs the CPU path by keypoint "
+                    "coordinates; the remaining disagreements are the fp16 SuperGlue's, classified as for fp32"},
         "line_association_identical_frac": agg("line_association_identical"),
         "right_lines_valid_per_pair": agg("right_lines_valid_cpu"),
         "cpu_s_per_pair": round(t_cpu / len(rows), 3), "cpu_threads": a.threads,

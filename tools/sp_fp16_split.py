@@ -43,6 +43,10 @@ SPLITS = {
     "conv1_32": set(ENC[2:] + HEADS),                    # fp32 conv1a / conv1b
     "conv4_32": set(ENC[:6] + HEADS),                    # fp32 conv4a / conv4b
     "late32": set(ENC[:6] + ["convDa", "convDb"]),       # fp32 conv4 + detector head
+    "x3_all": {n: "x3" for n in ENC + HEADS},             # split fp16 everywhere (3 MFMA products)
+    "x2a_all": {n: "x2a" for n in ENC + HEADS},           # activations split only
+    "x2w_all": {n: "x2w" for n in ENC + HEADS},           # weights split only
+    "x3_enc16c1": {**{n: "x3" for n in ENC[2:] + HEADS}, "conv1a": "16", "conv1b": "16"},  # conv1 fp16, rest split
 }
 
 
@@ -50,33 +54,60 @@ def r16(t):
     return t.half().float()
 
 
+def split16(t):
+    """t = hi + lo, both fp16 (lo unscaled: it goes subnormal below |t| ~ 0.125, where its absolute error
+    stays under fp16's subnormal spacing of 6e-8)"""
+    hi = r16(t)
+    return hi, r16(t - hi)
+
+
 class Emu:
+    """Per layer one of: "16" (fp16 operands, fp32 accumulation), "x3" (split fp16: activations and weights as
+    hi + lo fp16 pairs, three MFMA products hi*hi + lo*hi + hi*lo accumulated in fp32), "x2a" / "x2w" (only the
+    activations / only the weights split: two products), anything else fp32.  A layer's output is stored fp16
+    only when the next layer is "16" (x2w too reads fp16 activations); otherwise it stays fp32 (x3 / x2a split
+    it at load)."""
     def __init__(self, blob):
         self.w = {k: torch.from_numpy(np.asarray(v, np.float32)) for k, v in pkg.weights.read_blob(blob).items()}
 
-    def conv(self, x, name, half_in, half_out, relu=True, pad=1):
+    def conv(self, x, name, mode, out16, relu=True, pad=1):
         w, b = self.w[name + ".weight"], self.w[name + ".bias"]
-        if half_in:
-            x, w = r16(x), r16(w)
-            if name == "conv1a":  # conv1_res_kernel: the bias rides the MFMA as the tenth tap (fp16)
-                b = r16(b)
-        y = Fn.conv2d(x, w, b, padding=pad)
+        if mode in ("16", "x2w"):
+            x = r16(x)
+        if mode == "16" and name == "conv1a":  # conv1_res_kernel: the bias rides the MFMA as the tenth tap (fp16)
+            b = r16(b)
+        if mode == "16":
+            y = Fn.conv2d(x, r16(w), b, padding=pad)
+        elif mode in ("x3", "x2a", "x2w"):
+            xh, xl = split16(x)
+            wh, wl = split16(w)
+            y = Fn.conv2d(xh, wh, b, padding=pad)
+            if mode in ("x3", "x2a"):
+                y = y + Fn.conv2d(xl, wh, None, padding=pad)
+            if mode in ("x3", "x2w"):
+                y = y + Fn.conv2d(xh, wl, None, padding=pad)
+        else:
+            y = Fn.conv2d(x, w, b, padding=pad)
         if relu:
             y = Fn.relu(y)
-        return r16(y) if half_out else y
+        return r16(y) if out16 else y
 
     def forward(self, img_u8, half):
+        """half: a set of fp16 layers, or a dict layer -> mode"""
+        md = half if isinstance(half, dict) else {n: "16" for n in half}
+        m = lambda n: md.get(n, "32")  # noqa: E731
+        o16 = lambda n: m(n) in ("16", "x2w")  # noqa: E731  (the layer reads fp16 activations)
         x = torch.from_numpy(post.image_to_input(img_u8))[None, None]
         seq = ENC + ["convPa"]
         for i, name in enumerate(ENC):
             nxt = seq[i + 1]
-            x = self.conv(x, name, name in half, name in half and nxt in half)
+            x = self.conv(x, name, m(name), m(name) != "32" and o16(nxt))
             if name in ("conv1b", "conv2b", "conv3b"):
                 x = Fn.max_pool2d(x, 2, 2)
-        pa = self.conv(x, "convPa", "convPa" in half, "convPa" in half and "convPb" in half)
-        da = self.conv(x, "convDa", "convDa" in half, "convDa" in half and "convDb" in half)
-        semi = self.conv(pa, "convPb", "convPb" in half, False, relu=False, pad=0)
-        desc = self.conv(da, "convDb", "convDb" in half, False, relu=False, pad=0)
+        pa = self.conv(x, "convPa", m("convPa"), m("convPa") != "32" and o16("convPb"))
+        da = self.conv(x, "convDa", m("convDa"), m("convDa") != "32" and o16("convDb"))
+        semi = self.conv(pa, "convPb", m("convPb"), False, relu=False, pad=0)
+        desc = self.conv(da, "convDb", m("convDb"), False, relu=False, pad=0)
         s = torch.softmax(semi, 1)[:, :-1]
         h8, w8 = s.shape[2], s.shape[3]
         s = s.permute(0, 2, 3, 1).reshape(1, h8, w8, 8, 8).permute(0, 1, 3, 2, 4).reshape(h8 * 8, w8 * 8)
@@ -141,7 +172,8 @@ def main():
     out = {}
     for n in names:
         s = stats[n]
-        out[n] = {"fp16_layers": sorted(SPLITS[n]), "images": len(s["overlap"]),
+        out[n] = {"layers": SPLITS[n] if isinstance(SPLITS[n], dict) else {k: "16" for k in sorted(SPLITS[n])},
+                  "images": len(s["overlap"]),
                   "keypoint_overlap_mean": float(np.mean(s["overlap"])), "keypoint_overlap_min": float(np.min(s["overlap"])),
                   "keypoint_sets_identical_frac": float(np.mean([o == 1.0 for o in s["overlap"]])),
                   "desc_cos_min": float(np.min(s["cos"])) if s["cos"] else None}
