@@ -78,43 +78,8 @@ struct View {
   double delta0, delta1;  // Huber deltas (mono, stereo): scalars, never indexed (no scratch)
 };
 
-// The frame's waves (NW = 1 or 4 per frame): a wave-reduced value (equal on every lane) combined
-// across the NW waves of the workgroup in wave order through LDS; every thread gets the same sum.
-template <int NW, int N>
-__device__ __forceinline__ void block_combine(double (&v)[N]) {
-  if constexpr (NW > 1) {
-    __shared__ double cb[NW][N];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (lane == 0)
-#pragma unroll
-      for (int k = 0; k < N; k++) cb[wv][k] = v[k];
-    __syncthreads();
-#pragma unroll
-    for (int k = 0; k < N; k++) {
-      double t = cb[0][k];
-#pragma unroll
-      for (int w = 1; w < NW; w++) t += cb[w][k];
-      v[k] = t;
-    }
-    __syncthreads();  // cb is reused by the next combine
-  }
-}
-template <int NW>
-__device__ __forceinline__ int block_sum_int(int v) {
-  v = wsum_int(v);
-  if constexpr (NW > 1) {
-    __shared__ int ci[NW];
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    if (lane == 0) ci[wv] = v;
-    __syncthreads();
-    int t = 0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) t += ci[w];
-    __syncthreads();
-    v = t;
-  }
-  return v;
-}
+using wave::block_combine;  // (wave_reduce.hpp: the NW waves' sums added in wave order through LDS)
+using wave::block_sum_int;
 
 // robust (Huber) or plain chi2 of an error, for the edge type
 __device__ __forceinline__ double cost_of(const View& V, const double* ev, bool stereo, bool robust) {
@@ -330,9 +295,21 @@ __global__ __launch_bounds__(64 * NW) void frame_opt_kernel(Args a, int batch) {
   const double th0 = D.th[0], th1 = D.th[1];
   if constexpr (LDS) {
     Edge* Es = reinterpret_cast<Edge*>(smem);
-    const double* src = reinterpret_cast<const double*>(a.edges + D.e0);
-    double* dst = smem;
-    for (int k = lane; k < D.n * (int)(sizeof(Edge) / 8); k += T) dst[k] = src[k];
+    // 16-byte pieces, eight loads in flight per thread before their LDS stores: the source is the
+    // host-mapped staging (PCIe round trips of ~1-2 us) for a single frame, device memory otherwise
+    static_assert(sizeof(Edge) % 16 == 0, "edge records in 16-byte pieces");
+    const uint4* src = reinterpret_cast<const uint4*>(a.edges + D.e0);
+    uint4* dst = reinterpret_cast<uint4*>(smem);
+    const int n16 = D.n * (int)(sizeof(Edge) / 16);
+    for (int k0 = lane; k0 < n16; k0 += 8 * T) {
+      uint4 v[8];
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+        if (k0 + j * T < n16) v[j] = src[k0 + j * T];
+#pragma unroll
+      for (int j = 0; j < 8; j++)
+        if (k0 + j * T < n16) dst[k0 + j * T] = v[j];
+    }
     V.E = Es;
     V.err = smem + D.n * (sizeof(Edge) / 8);
     V.lev = reinterpret_cast<uint8_t*>(V.err + 3 * D.n);
@@ -420,14 +397,13 @@ __global__ __launch_bounds__(64 * NW) void frame_opt_kernel(Args a, int batch) {
 size_t lds_bytes(int n) { return (size_t)n * (sizeof(Edge) + 3 * sizeof(double) + 2); }
 
 // waves per frame: 4 for latency (one frame per CU at 256 VGPRs) while the batch leaves CUs idle,
-// 1 for throughput (two frames per SIMD) on large batches; RSPL_FRAME_WAVES=1 / 4 forces one (A/B).
+// 1 for throughput (two frames per SIMD) on large batches (profiles/r03_bench_frame.json).
 // The wave count sets the summation order of H / b / chi2, so a frame's result depends on whether its
 // batch exceeds 256 frames at the last-ulp level (agreement to the oracle tolerances either way:
 // tests/test_gpu_frame.py::test_frame_alone_and_in_a_large_batch).
 hipError_t optimize(const Args& a, int batch, int max_n, hipStream_t s) {
   if (batch <= 0) return hipSuccess;
-  const char* w = getenv("RSPL_FRAME_WAVES");
-  const bool one = w ? atoi(w) == 1 : batch > 256;
+  const bool one = batch > 256;
   if (max_n <= kLdsEdges) {
     if (one) frame_opt_kernel<true, 1><<<batch, 64, lds_bytes(max_n), s>>>(a, batch);
     else frame_opt_kernel<true, 4><<<batch, 256, lds_bytes(max_n), s>>>(a, batch);

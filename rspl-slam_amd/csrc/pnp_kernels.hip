@@ -643,16 +643,19 @@ __device__ double reproj2(const double* K4, const double R[9], const double t[3]
 
 
 // Levenberg-Marquardt on the inliers' squared reprojection error (orc_pnp's refine, oracle/pnp.c):
-// pose T_cw (R, t) with the left exp-map update; lanes own strided correspondences, the 6x6
-// normal equations and the costs are wave-reduced, so every lane takes the same decisions
-__device__ void refine(const double* K4, int n, const double* pw, const double* uv, const uint8_t* inl, int lane,
+// pose T_cw (R, t) with the left exp-map update; the NW waves' threads own strided correspondences, the
+// 6x6 normal equations and the costs are wave-reduced and then added over the waves in wave order
+// (wave::block_combine), so every thread takes the same decisions
+template <int NW>
+__device__ void refine(const double* K4, int n, const double* pw, const double* uv, const uint8_t* inl, int tid,
                        double R[9], double t[3]) {
 #pragma clang fp contract(fast)  // the refinement is held to a tolerance, not to bits
+  const int lane = tid & 63;
   double lambda = 1e-3;
   for (int it = 0; it < 20; it++) {
     double acc[wave::kNV];
     for (int k = 0; k < wave::kNV; k++) acc[k] = 0.0;
-    for (int i = lane; i < n; i += 64) {
+    for (int i = tid; i < n; i += 64 * NW) {
       if (!inl[i]) continue;
       const double* p = pw + 3 * i;
       const double x = dot3(R, p) + t[0], y = dot3(R + 3, p) + t[1], z = dot3(R + 6, p) + t[2];
@@ -675,6 +678,7 @@ __device__ void refine(const double* K4, int n, const double* pw, const double* 
       }
     }
     wave::wave_allreduce28(acc, lane);
+    wave::block_combine<NW>(acc);
     const double cost = acc[27];
     auto H = [&](int a, int b) { return a <= b ? acc[a * 6 - a * (a - 1) / 2 + (b - a)] : acc[b * 6 - b * (b - 1) / 2 + (a - b)]; };
     bool accepted = false;
@@ -745,16 +749,17 @@ __device__ void refine(const double* K4, int n, const double* pw, const double* 
         for (int b = 0; b < 3; b++) Rn[a * 3 + b] = dR[a * 3] * R[b] + dR[a * 3 + 1] * R[3 + b] + dR[a * 3 + 2] * R[6 + b];
       }
       for (int a = 0; a < 3; a++) tn[a] = dot3(dR + 3 * a, t) + dt[a];
-      double cn = 0;
-      for (int i = lane; i < n; i += 64)
-        if (inl[i]) cn += reproj2(K4, Rn, tn, pw + 3 * i, uv + 2 * i);
-      cn = wave::wsum(cn);
-      if (cn < cost) {
+      double cn[1] = {0};
+      for (int i = tid; i < n; i += 64 * NW)
+        if (inl[i]) cn[0] += reproj2(K4, Rn, tn, pw + 3 * i, uv + 2 * i);
+      cn[0] = wave::wsum(cn[0]);
+      wave::block_combine<NW>(cn);
+      if (cn[0] < cost) {
         for (int k = 0; k < 9; k++) R[k] = Rn[k];
         for (int k = 0; k < 3; k++) t[k] = tn[k];
         lambda = fmax(lambda * 0.1, 1e-12);
         accepted = true;
-        if (cost - cn <= 1e-14 * cost) return;
+        if (cost - cn[0] <= 1e-14 * cost) return;
       } else {
         lambda *= 10;
       }
@@ -807,10 +812,13 @@ __global__ __launch_bounds__(256) void pnp_hyp_kernel(Args a) {
   }
 }
 
-// stage 2: one wave per frame -- RANSAC's acceptance in hypothesis order, inliers, refinement
-__global__ __launch_bounds__(64) void pnp_final_kernel(Args a) {
-  const int f = blockIdx.x, lane = threadIdx.x;
-  unsigned long long* pf = (a.prof && f == 0 && lane == 0) ? a.prof : nullptr;
+// stage 2: one workgroup of kFinalWaves waves per frame -- RANSAC's acceptance in hypothesis order (replayed
+// by every thread), inliers, refinement (its sums over the four waves: 52 us on one wave, r05_experiments.md)
+constexpr int kFinalWaves = 4;
+__global__ __launch_bounds__(64 * kFinalWaves) void pnp_final_kernel(Args a) {
+  const int f = blockIdx.x, tid = threadIdx.x;
+  constexpr int T = 64 * kFinalWaves;
+  unsigned long long* pf = (a.prof && f == 0 && tid == 0) ? a.prof : nullptr;
   pstamp(pf, 8);
   const Desc D = a.frames[f];
   const int n = D.n;
@@ -832,8 +840,8 @@ __global__ __launch_bounds__(64) void pnp_final_kernel(Args a) {
   Out* o = a.out + f;
   uint8_t* inl = a.inl + D.p0;
   if (best < 0) {
-    for (int i = lane; i < n; i += 64) inl[i] = 0;
-    if (lane == 0) {
+    for (int i = tid; i < n; i += T) inl[i] = 0;
+    if (tid == 0) {
       o->n_inliers = 0;
       o->hyps = used;
     }
@@ -848,16 +856,16 @@ __global__ __launch_bounds__(64) void pnp_final_kernel(Args a) {
 #pragma unroll
   for (int k = 0; k < 3; k++) t[k] = hr[9 + k];
   int ninl = 0;
-  for (int i = lane; i < n; i += 64) {
+  for (int i = tid; i < n; i += T) {
     const uint8_t in = reproj2(D.K, R, t, pw + 3 * i, uv + 2 * i) <= D.thr2;
     inl[i] = in;
     ninl += in;
   }
-  ninl = wave::wsum_int(ninl);
+  ninl = wave::block_sum_int<kFinalWaves>(ninl);  // (its barriers order the inlier flags before the refinement)
   pstamp(pf, 9);
-  refine(D.K, n, pw, uv, inl, lane, R, t);
+  refine<kFinalWaves>(D.K, n, pw, uv, inl, tid, R, t);
   pstamp(pf, 10);
-  if (lane == 0) {
+  if (tid == 0) {
     for (int i = 0; i < 3; i++)
       for (int j = 0; j < 3; j++) o->Rwc[3 * i + j] = R[3 * j + i];
     for (int i = 0; i < 3; i++) o->twc[i] = -(R[i] * t[0] + R[3 + i] * t[1] + R[6 + i] * t[2]);
@@ -869,7 +877,7 @@ __global__ __launch_bounds__(64) void pnp_final_kernel(Args a) {
 hipError_t solve(const Args& a, int batch, int max_iters, hipStream_t s) {
   if (batch <= 0) return hipSuccess;
   if (max_iters > 0) pnp_hyp_kernel<<<dim3((max_iters + kHypWaves - 1) / kHypWaves, batch), 256, 0, s>>>(a);
-  pnp_final_kernel<<<batch, 64, 0, s>>>(a);
+  pnp_final_kernel<<<batch, 64 * kFinalWaves, 0, s>>>(a);
   return hipGetLastError();
 }
 

@@ -816,14 +816,19 @@ __global__ __launch_bounds__(256) void conv3x3_x3_kernel(ConvArgs a) {
         bh[n] = *reinterpret_cast<const half8*>(&wts[o]);
         bl[n] = *reinterpret_cast<const half8*>(&wts[WTS + o]);
       }
+      // the three products in three sweeps over the (m, n) accumulators: consecutive MFMAs independent
 #pragma unroll
       for (int m = 0; m < MT; m++)
 #pragma unroll
-        for (int n = 0; n < 2; n++) {
-          acc[m][n] = mfma16(al[m], bh[n], acc[m][n]);
-          acc[m][n] = mfma16(ah[m], bl[n], acc[m][n]);
-          acc[m][n] = mfma16(ah[m], bh[n], acc[m][n]);
-        }
+        for (int n = 0; n < 2; n++) acc[m][n] = mfma16(al[m], bh[n], acc[m][n]);
+#pragma unroll
+      for (int m = 0; m < MT; m++)
+#pragma unroll
+        for (int n = 0; n < 2; n++) acc[m][n] = mfma16(ah[m], bl[n], acc[m][n]);
+#pragma unroll
+      for (int m = 0; m < MT; m++)
+#pragma unroll
+        for (int n = 0; n < 2; n++) acc[m][n] = mfma16(ah[m], bh[n], acc[m][n]);
     }
   }
 
@@ -1039,14 +1044,14 @@ __global__ __launch_bounds__(256) void det_head_h_kernel(HeadHArgs a) {
     if constexpr (X3)
 #pragma unroll
       for (int n = 0; n < NT; n++) bl[n] = wfl[(n * 16 + t) * 64];
+    if constexpr (X3) {
 #pragma unroll
-    for (int n = 0; n < NT; n++) {
-      if constexpr (X3) {
-        acc[n] = mfma16(al[t], bv[n], acc[n]);
-        acc[n] = mfma16(av[t], bl[n], acc[n]);
-      }
-      acc[n] = mfma16(av[t], bv[n], acc[n]);
+      for (int n = 0; n < NT; n++) acc[n] = mfma16(al[t], bv[n], acc[n]);
+#pragma unroll
+      for (int n = 0; n < NT; n++) acc[n] = mfma16(av[t], bl[n], acc[n]);
     }
+#pragma unroll
+    for (int n = 0; n < NT; n++) acc[n] = mfma16(av[t], bv[n], acc[n]);
   }
 #pragma unroll
   for (int n = 0; n < NT; n++) {
@@ -1163,8 +1168,8 @@ __global__ __launch_bounds__(256) void sample_taps_h_kernel(TapArgs a) {
     if constexpr (X3) {
       const half8 l0 = wfl[((2 * wv) * 16 + t) * 64], l1 = wfl[((2 * wv + 1) * 16 + t) * 64];
       acc[0] = mfma16(al[t], b0, acc[0]);
-      acc[0] = mfma16(av[t], l0, acc[0]);
       acc[1] = mfma16(al[t], b1, acc[1]);
+      acc[0] = mfma16(av[t], l0, acc[0]);
       acc[1] = mfma16(av[t], l1, acc[1]);
     }
     acc[0] = mfma16(av[t], b0, acc[0]);

@@ -73,6 +73,43 @@ __device__ __forceinline__ double rcp64(double d) {
   return fma(r, fma(-d, r, 1.0), r);
 }
 
+// A workgroup of NW waves (FrameOptimization's frame, PnP's refinement): a wave-reduced value (equal on every
+// lane) combined across the NW waves in wave order through LDS; every thread gets the same sum.
+template <int NW, int N>
+__device__ __forceinline__ void block_combine(double (&v)[N]) {
+  if constexpr (NW > 1) {
+    __shared__ double cb[NW][N];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0)
+#pragma unroll
+      for (int k = 0; k < N; k++) cb[wv][k] = v[k];
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < N; k++) {
+      double t = cb[0][k];
+#pragma unroll
+      for (int w = 1; w < NW; w++) t += cb[w][k];
+      v[k] = t;
+    }
+    __syncthreads();  // cb is reused by the next combine
+  }
+}
+template <int NW>
+__device__ __forceinline__ int block_sum_int(int v) {
+  v = wsum_int(v);
+  if constexpr (NW > 1) {
+    __shared__ int ci[NW];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    if (lane == 0) ci[wv] = v;
+    __syncthreads();
+    int t = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) t += ci[w];
+    __syncthreads();
+    v = t;
+  }
+  return v;
+}
 
 }  // namespace wave
 }  // namespace rspl

@@ -35,6 +35,7 @@ def main():
                     help="both sides use the analytic limit of g2o's central-difference line Jacobian "
                          "(rspl_ba_set_line_jacobian / oracle.ba_set_line_jacobian)")
     ap.add_argument("--out", default="gpurun_out/sequence")
+    ap.add_argument("--no-cpu", action="store_true", help="GPU path only (stage timing A/B): no oracle run, no ATE")
     a = ap.parse_args()
     from rspl_slam_amd import sequence as SQ, trajectory as TJ
     out = pathlib.Path(a.out)
@@ -50,6 +51,12 @@ def main():
     print(f"gpu path: {len(reports)} keyframes, {time.perf_counter() - t:.2f} s", file=sys.stderr, flush=True)
     gpu_s = time.perf_counter() - t
     m.SaveKeyframeTrajectory(str(out / "keyframe_trajectory_gpu.txt"))
+    if a.no_cpu:
+        print(json.dumps({"keyframes": len(seq["keyframes"]), "gpu_map_local_ba_ms_per_keyframe":
+                          round(gpu_s * 1e3 / (len(seq["keyframes"]) - 1), 3),
+                          "gpu_path_ms_per_keyframe": {k: round(float(np.mean([r[k + "_us"] for r in reports])) / 1e3, 3)
+                                                       for k in ("insert", "assembly", "ba", "finish")}}))
+        return
     t = time.perf_counter()
     mr = map_ref.Map(seq["camera"])
     for k, kf in enumerate(seq["keyframes"]):
