@@ -173,11 +173,9 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision, workload
     N = M = K
     h16 = precision in ("fp16", "fp16x3")  # fp16 MFMA operands (fp16x3: SuperPoint split into hi + lo)
     mfma_peak = FP16_MFMA_PEAK if h16 else FP32_MFMA_PEAK
-    # fp16: the persistent conv1 kernel (RSPL_SP_CONV1=stage: the per-stage fused conv1a kernel)
-    conv1_k = (("conv3x3_h_kernel<64, 16, true, true, false>" if os.environ.get("RSPL_SP_CONV1") == "stage"
-                else "conv1_res_kernel") if precision == "fp16" else "conv3x3_x3_kernel<64, 16, true, true>"
-               if precision == "fp16x3"
-               else "conv3x3_kernel<64, 16, true, true>")
+    # the fused conv1a + conv1b + pool kernel of each precision (fp16: persistent, conv1b weights resident in LDS)
+    conv1_k = {"fp16": "conv1_res_kernel", "fp16x3": "conv3x3_x3_kernel<64, 16, true, true>",
+               "fp32": "conv3x3_kernel<64, 16, true, true>"}[precision]
     rows = (("sp:conv1a+1b+pool", 2 * conv1_gflop_per_image(), "TFLOP/s", mfma_peak, "mfma", conv1_k, True,
              "GFLOP per launch (2 images, conv1a+conv1b)"),
             ("sg:gnn x18", 2 * 2 * 18 * 2 * (655360 * N + 512 * N * M) / 1e9, "TFLOP/s", mfma_peak, "mfma",
@@ -185,8 +183,7 @@ def stage_roofline(sp, sg, sp_ms, sp_calls, sg_ms, sg_calls, precision, workload
              "GFLOP per step (2 pairs x 2 images x 18 layers; fp16: 19 launches of the fused layer kernel, "
              "fp32: 4 GEMM/attention launches per layer)"),
             ("sg:sinkhorn", 2 * 2 * 4 * (N + 1) * (M + 1) / 1e9, "GB/s", HBM_PEAK_GBS, "hbm",
-             "sinkhorn_kernel<" if os.environ.get("RSPL_SG_SINK") == "slab" else
-             ("sinkhorn_w_kernel" if N + 1 > 640 else "sinkhorn_sc_kernel"),
+             "sinkhorn_w_kernel" if N + 1 > 640 else "sinkhorn_sc_kernel",
              True, "GB per launch (2 pairs, compulsory: couplings read + Z written once, 2*4*(N+1)(M+1) per pair; "
                    "the kernel holds K = exp(C + a + b) in registers across the 100 iterations)"),
             ("sp:nms", 2 * 4 * H * W / 1e9, "GB/s", HBM_PEAK_GBS, "hbm", "nms_kernel", True,
@@ -348,11 +345,6 @@ def rank_census(group, world, want, local, cnt):
 
 
 def main():
-    # The BA runs on a tracking thread beside the feature loop (both Python here, C++ threads in the
-    # reference): RSPL_GIL_SWITCH_US sets the interpreter's GIL switch interval (A/B knob; default
-    # the interpreter's 5 ms)
-    if os.environ.get("RSPL_GIL_SWITCH_US"):
-        sys.setswitchinterval(float(os.environ["RSPL_GIL_SWITCH_US"]) * 1e-6)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=200)
@@ -371,9 +363,9 @@ def main():
                          "products: the fp32 path's keypoint sets) with SuperGlue in fp16; "
                          "fp16 = the reference's own TensorRT kFP16 engines "
                          "(src/super_point.cpp:98, src/super_glue.cpp:132; default), fp32 = the parity path")
-    ap.add_argument("--reserve-cus", type=int, default=int(os.environ.get("RSPL_RESERVE_CUS", "0")),
+    ap.add_argument("--reserve-cus", type=int, default=0,
                     help="CUs the SuperPoint/SuperGlue streams leave free for the BA chain (CU-masked streams)")
-    ap.add_argument("--ba-own-cus", type=int, default=int(os.environ.get("RSPL_BA_OWN_CUS", "1")),
+    ap.add_argument("--ba-own-cus", type=int, default=1,
                     help="1: the BA runs only on the reserved CUs (disjoint from SP/SG)")
     ap.add_argument("--skip", default="", help="diagnostics only: comma list of stages to leave out (sp,sg,ba)")
     ap.add_argument("--ba-ktime-steps", type=int, default=20,
@@ -460,10 +452,8 @@ def main():
     # (and, with --ba-own-cus, the BA confined to them).  Measured: no gain -- the BA's slowdown
     # under load is memory-latency contention, not CU slots -- so the default is 0 (unmasked)
     rc = args.reserve_cus
-    # stream priorities (RSPL_STREAM_PRIO="sp=normal,sg=high,post=high", the defaults): the BA's
-    # own stream is always high
+    # stream priorities: SG and its post stream high (the BA's own stream is always high), SP normal
     prio = dict(sp="normal", sg="high", post="high")
-    prio.update(kv.split("=") for kv in os.environ.get("RSPL_STREAM_PRIO", "").split(",") if "=" in kv)
     st_sp, st_sg = capi.Stream(reserve_cus=rc, priority=prio["sp"]), capi.Stream(reserve_cus=rc, priority=prio["sg"])
     st_post = capi.Stream(reserve_cus=rc, priority=prio["post"])  # SG's Sinkhorn + decode: overlaps the next GNN
     ev_sp = [capi.Event() for _ in range(3)]

@@ -337,8 +337,9 @@ int rspl_ba_kernel_times(rspl_ba* ba, double* ms, long long* launches);
  * Record of RSPL_BA_TRACE_W doubles: [0] submitted (rspl_ba_submit; rspl_ba_local: entry), [1] staging
  * started, [2] staging done, [3] device part started (tracking thread), [4] upload queued, [5] optimize(10)
  * stopped (mailbox read), [6] optimize(5) stopped, [7] call done (results written back), [8] staging slot,
- * [9] resize flags (1 staging slot, 2 edge-pair list, 4 pose-diagonal partials, 8 timing events: a buffer
- * grown inside the call), [10] LM iterations, [11] 1 for rspl_ba_local, 0 for a submitted call.
+ * [9] flags (1 staging slot, 2 edge-pair list, 4 pose-diagonal partials, 8 timing events: a buffer grown inside
+ * the call; 16 optimize(5)'s setup ran from the speculative queue behind optimize(10)'s trials, 32 optimize(10)
+ * needed trials beyond its first batch), [10] LM iterations, [11] 1 for rspl_ba_local, 0 for a submitted call.
  * rspl_ba_trace copies the oldest min(cap, recorded) records and clears the ring; *n = records copied. */
 /* Line edges' Jacobians (EdgeSE3ProjectLine / EdgeStereoSE3ProjectLine do not override linearizeOplus, so
  * g2o differentiates them numerically: central difference, delta 1e-9).  0 (default): that central

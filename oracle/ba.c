@@ -345,6 +345,40 @@ static void skew(const double* v, double* S) { /* S x = v x x */
   S[6] = -v[1]; S[7] = v[0]; S[8] = 0;
 }
 
+/* g2o's numeric central difference of one line edge (BaseBinaryEdge::linearizeOplus, delta 1e-9): the pose by
+ * the left exp-map increment, the line by Line3D::oplus, each +-delta, the quotient (e+ - e-) / (2 delta) --
+ * used by linearize() and by the orc_line_jacobian test hook alike */
+static void line_jac_numeric(const double* cam, const se3* T0, const double* L, const double* obs, int stereo,
+                             double* Jp, double* Jl) {
+  const se3 T = *T0;
+  const double delta = 1e-9, scal = 1.0 / (2 * delta);
+  const int rows = stereo ? 4 : 2;
+  double ep[4], em[4], Lp[6];
+  for (int d = 0; d < 4; d++) {
+    double v[4] = {0, 0, 0, 0};
+    v[d] = delta;
+    memcpy(Lp, L, sizeof(Lp));
+    line_oplus(Lp, v);
+    line_err(cam, &T, Lp, obs, stereo, ep);
+    v[d] = -delta;
+    memcpy(Lp, L, sizeof(Lp));
+    line_oplus(Lp, v);
+    line_err(cam, &T, Lp, obs, stereo, em);
+    for (int r = 0; r < rows; r++) Jl[r * 4 + d] = scal * (ep[r] - em[r]);
+  }
+  for (int d = 0; d < 6; d++) {
+    double u[6] = {0, 0, 0, 0, 0, 0};
+    u[d] = delta;
+    se3 dT = se3_exp(u), Tp = se3_mul(&dT, &T);
+    line_err(cam, &Tp, L, obs, stereo, ep);
+    u[d] = -delta;
+    dT = se3_exp(u);
+    Tp = se3_mul(&dT, &T);
+    line_err(cam, &Tp, L, obs, stereo, em);
+    for (int r = 0; r < rows; r++) Jp[r * 6 + d] = scal * (ep[r] - em[r]);
+  }
+}
+
 static void line_jac_analytic(const double* cam, const se3* T, const double* L, const double* obs, int stereo,
                               double* Jp, double* Jl) {
   const double fx = cam[0], fy = cam[1], cx = cam[2], cy = cam[3], bf = cam[4];
@@ -455,39 +489,11 @@ static void linearize(ba_t* b, int t, int e, double* Jp, double* Jl) {
     else
       line_jac_analytic(cam_of(b, P->stereo_line_camera, e), &b->T[pi], b->L + 6 * l, P->stereo_line_obs + 8 * e, 1, Jp,
                         Jl);
+  } else if (t == 2) {
+    line_jac_numeric(cam_of(b, P->mono_line_camera, e), &b->T[pi], b->L + 6 * l, P->mono_line_obs + 4 * e, 0, Jp, Jl);
   } else {
-    /* numeric central difference, delta 1e-9 (g2o BaseBinaryEdge::linearizeOplus) */
-    const double delta = 1e-9, scal = 1.0 / (2 * delta);
-    const int rows = EDIM[t];
-    double ep[4], em[4];
-    double Lsave[6];
-    memcpy(Lsave, b->L + 6 * l, sizeof(Lsave));
-    for (int d = 0; d < 4; d++) {
-      double v[4] = {0, 0, 0, 0};
-      v[d] = delta;
-      line_oplus(b->L + 6 * l, v);
-      compute_error(b, t, e, ep);
-      memcpy(b->L + 6 * l, Lsave, sizeof(Lsave));
-      v[d] = -delta;
-      line_oplus(b->L + 6 * l, v);
-      compute_error(b, t, e, em);
-      memcpy(b->L + 6 * l, Lsave, sizeof(Lsave));
-      for (int r = 0; r < rows; r++) Jl[r * 4 + d] = scal * (ep[r] - em[r]);
-    }
-    const se3 Tsave = b->T[pi];
-    for (int d = 0; d < 6; d++) {
-      double u[6] = {0, 0, 0, 0, 0, 0};
-      u[d] = delta;
-      se3 dT = se3_exp(u);
-      b->T[pi] = se3_mul(&dT, &Tsave);
-      compute_error(b, t, e, ep);
-      u[d] = -delta;
-      dT = se3_exp(u);
-      b->T[pi] = se3_mul(&dT, &Tsave);
-      compute_error(b, t, e, em);
-      b->T[pi] = Tsave;
-      for (int r = 0; r < rows; r++) Jp[r * 6 + d] = scal * (ep[r] - em[r]);
-    }
+    line_jac_numeric(cam_of(b, P->stereo_line_camera, e), &b->T[pi], b->L + 6 * l, P->stereo_line_obs + 8 * e, 1, Jp,
+                     Jl);
   }
 }
 
@@ -958,32 +964,7 @@ void orc_line_jacobian(const double* cam, const double* q, const double* t, cons
     line_jac_analytic(cam, &T, L, obs, stereo, Jp, Jl);
     return;
   }
-  const double delta = 1e-9, scal = 1.0 / (2 * delta);
-  const int rows = stereo ? 4 : 2;
-  double ep[4], em[4], Lp[6];
-  for (int d = 0; d < 4; d++) {
-    double v[4] = {0, 0, 0, 0};
-    v[d] = delta;
-    memcpy(Lp, L, sizeof(Lp));
-    line_oplus(Lp, v);
-    line_err(cam, &T, Lp, obs, stereo, ep);
-    v[d] = -delta;
-    memcpy(Lp, L, sizeof(Lp));
-    line_oplus(Lp, v);
-    line_err(cam, &T, Lp, obs, stereo, em);
-    for (int r = 0; r < rows; r++) Jl[r * 4 + d] = scal * (ep[r] - em[r]);
-  }
-  for (int d = 0; d < 6; d++) {
-    double u[6] = {0, 0, 0, 0, 0, 0};
-    u[d] = delta;
-    se3 dT = se3_exp(u), Tp = se3_mul(&dT, &T);
-    line_err(cam, &Tp, L, obs, stereo, ep);
-    u[d] = -delta;
-    dT = se3_exp(u);
-    Tp = se3_mul(&dT, &T);
-    line_err(cam, &Tp, L, obs, stereo, em);
-    for (int r = 0; r < rows; r++) Jp[r * 6 + d] = scal * (ep[r] - em[r]);
-  }
+  line_jac_numeric(cam, &T, L, obs, stereo, Jp, Jl);
 }
 
 /* ====================================================================== */

@@ -20,7 +20,7 @@ RSPL_PREC_FP16 = 1
 RSPL_PREC_FP16X3 = 2  # SuperPoint only: split fp16 (hi + lo planes, three fp16 MFMA products per step)
 
 BA_TRACE_W = 12  # RSPL_BA_TRACE_W
-BA_TRACE_FIELDS = ("submit", "stage0", "stage1", "run0", "upload", "opt1", "opt2", "end", "slot", "grew", "iters",
+BA_TRACE_FIELDS = ("submit", "stage0", "stage1", "run0", "upload", "opt1", "opt2", "end", "slot", "grew", "iters",  # grew: rspl_ba_trace [9] flags
                    "sync")
 
 EXPORTS = [

@@ -431,11 +431,6 @@ void report_prof(rspl_ba* b) {
             "end %.1f/%.1f/%.1f n %zu\n", q(w, .5), q(w, .9), q(w, 1), q(c, .5), q(c, .9), q(c, 1), q(e, .5), q(e, .9),
             q(e, 1), q(tot, .5), q(tot, .9), q(tot, 1), w.size());
   }
-  if (getenv("RSPL_BA_SOLVE") && std::string(getenv("RSPL_BA_SOLVE")) == "blk4") {
-    fprintf(stderr, "ba_steps us:");  // blocked solve: each pose block's panel, from the assembly's end
-    for (int k = 5; k < 15 && h[k]; k++) fprintf(stderr, " %.2f", us(h[1], h[k]));
-    fprintf(stderr, "\n");
-  }
   b->prof_nb[0] = 0;
   (void)hipMemset(b->prof, 0, sizeof(unsigned long long) * ba::kProfLen);
 }
@@ -462,6 +457,7 @@ struct SpecSetup {
   int iters2 = 0;
   bool queued = false;  // queued behind a batch of the first optimize()'s trials
   bool extra = false;   // a later batch was queued after it: that setup did nothing (and none followed yet)
+  bool topped_up = false;  // the first optimize() needed trials beyond its first batch
 };
 
 // the call's final kernel (inlier flags, final T / X / L into the staging slot) queued right behind the
@@ -501,10 +497,9 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
   // errors, cost and linearisation at the current state (with cls_level: the second optimize's
   // outlier levels and landmark activity first) + computeLambdaInit into the control (slot 0);
   // nothing is posted: the host waits for the trials only
-  static const bool split_setup = getenv("RSPL_BA_SETUP") && std::string(getenv("RSPL_BA_SETUP")) == "split";
   if (setup_done) {
     // (queued behind the previous optimize()'s trials: SpecSetup)
-  } else if (!split_setup) {
+  } else {
     const size_t need = (size_t)ba::setup_pdg_len(A);
     if (need > b->pdg_cap) {  // grow (the stream may still read the old buffer)
       RSPL_HIP(hipStreamSynchronize(st));
@@ -520,16 +515,6 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
     Su.prof = b->prof && !b->prof_nb[0] && !cls_level ? b->prof : nullptr;
     RSPL_HIP(ba::setup_dev(P, Lr, A, Su, cls_level, cls_level ? const_cast<uint8_t*>(A.lm_act) : nullptr, iters,
                            build_pp ? b->pp_cnt : nullptr, b->pp_off, b->pp_buf, b->pdg, st));
-  } else {  // A/B knob: the separate launches (build_pairs, classify, landmark_active, errors, linearize,
-            // pose_diag, post)
-    if (build_pp) RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, st));
-    if (cls_level) {
-      RSPL_HIP(ba::classify(P, Lr, A.Ea, cls_level, nullptr, 0, st));
-      RSPL_HIP(ba::landmark_active(A, cls_level, const_cast<uint8_t*>(A.lm_act), st));
-    }
-    RSPL_HIP(ba::compute_errors(P, Lr, A, S, 0, st));
-    RSPL_HIP(ba::linearize(P, Lr, A, S, true, st));
-    RSPL_HIP(ba::post(S, 0, st, &A, iters));
   }
   unsigned long long q = b->seq;
   const unsigned long long q_first = b->seq + 1;
@@ -597,7 +582,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
   // the second optimize()'s setup behind each batch, gated on the control the batch's last trial writes (the
   // one behind the batch in which this optimize() stops is the one that runs)
   auto queue_spec_setup = [&]() -> int {
-    if (!nxt || split_setup || (size_t)ba::setup_pdg_len(nxt->A2) > b->pdg_cap) return RSPL_OK;
+    if (!nxt || (size_t)ba::setup_pdg_len(nxt->A2) > b->pdg_cap) return RSPL_OK;
     ba::Sys S2 = S;
     S2.lm = b->lmctl;
     S2.lm_slot = 0;
@@ -655,7 +640,7 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
       break;
     }
     // rejected trials left iterations to do: queue one trial per remaining iteration
-    if (nxt) nxt->extra = true;
+    if (nxt) nxt->extra = nxt->topped_up = true;
     if ((rc = enqueue_batch(std::max(1, iters - (int)v[1])))) return rc;
     if ((rc = queue_spec_setup())) return rc;
   }
@@ -1295,19 +1280,13 @@ int stage_call(rspl_ba* b, int slot, const rspl_ba_problem* pr, rspl_ba_result* 
 }
 
 // The device part of one staged call: upload, both optimize() calls, results
-bool upload_copy() {
-  static const bool c = getenv("RSPL_BA_UPLOAD") && std::string(getenv("RSPL_BA_UPLOAD")) == "copy";
-  return c;
-}
-
 // The next queued call's inputs, uploaded into its slot's call buffer behind the current call's last
 // queued kernels (optimize(5)'s trials and the gated final kernel): the upload (~40 us over PCIe at C3)
 // then runs while the host notices the current call's end and queues the next one, instead of first in
 // the next call's chain.  Tracking thread only; the next call must already be staged (its slot is then
 // busy until it completes, and differs from the running call's).
 void preupload_next(rspl_ba* b) {
-  static const bool off = getenv("RSPL_BA_PREUPLOAD") && std::string(getenv("RSPL_BA_PREUPLOAD")) == "0";  // A/B
-  if (!b->tracking_call || upload_copy() || off) return;
+  if (!b->tracking_call) return;
   std::shared_ptr<ba::StagedCall> nx;
   {
     std::lock_guard<std::mutex> lk(b->qmu);
@@ -1346,12 +1325,10 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
   // the call's inputs in one upload: a copy kernel reading the host-mapped staging slot over PCIe.  Not
   // hipMemcpyAsync: its H2D path stalled the first calls after the warmup by 7-10 ms each (the SDMA engine /
   // blit-kernel choice settling; profiles/r05_bench_20step_before.json), which cost the driver's 20-step bench
-  // a quarter of its rate.  RSPL_BA_UPLOAD=copy keeps the old path for A/B.
+  // a quarter of its rate.
   char* cb = b->cbuf[c.slot];
-  if (!c.uploaded) {  // (else queued behind the previous call's final kernel: preupload_next)
-    if (!upload_copy()) RSPL_HIP(upload_mapped(cb, b->stage_dev[c.slot], cl.bytes, st));
-    else RSPL_HIP(hipMemcpyAsync(cb, sg, cl.bytes, hipMemcpyHostToDevice, st));
-  }
+  if (!c.uploaded)  // (else queued behind the previous call's final kernel: preupload_next)
+    RSPL_HIP(upload_mapped(cb, b->stage_dev[c.slot], cl.bytes, st));
   tm.mark("upload");
   tr[4] = mono_s();
   uint8_t* level = reinterpret_cast<uint8_t*>(cb + cl.level);
@@ -1424,8 +1401,7 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
   const bool pp_fused = dev_lm(b, A, pr->iterations_first);  // else: built here, before the first optimize
   if (!pp_fused) RSPL_HIP(ba::build_pairs(A, b->pp_cnt, b->pp_off, b->pp_buf, st));
   tm.mark("pairs");
-  // phase 2's setup queued behind phase 1's trials (device LM on both, unsharded; RSPL_BA_SPECSETUP=0: off)
-  static const bool spec_setup_on = !(getenv("RSPL_BA_SPECSETUP") && std::string(getenv("RSPL_BA_SPECSETUP")) == "0");
+  // phase 2's setup queued behind phase 1's trials (device LM on both, unsharded)
   SpecSetup nxt;
   nxt.A2 = A;
   nxt.A2.robust = 0;
@@ -1433,7 +1409,7 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
   nxt.A2.lm_act = b->lm_act2;
   nxt.level = level;
   nxt.iters2 = pr->iterations_second;
-  const bool spec_setup = spec_setup_on && pp_fused && !sh && !b->ktime_on && dev_lm(b, nxt.A2, pr->iterations_second);
+  const bool spec_setup = pp_fused && !sh && !b->ktime_on && dev_lm(b, nxt.A2, pr->iterations_second);
   if ((rc = optimize(b, P, Lr, S, A, pr->iterations_first, &res->chi2_first, &res->iterations_done_first, nullptr,
                      pp_fused, nullptr, spec_setup ? &nxt : nullptr)))
     return rc;
@@ -1475,6 +1451,8 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
       return rc;
     tm.mark("opt2");
     tr[6] = mono_s();
+    // trace flags: 16 optimize(5)'s setup ran from the speculative queue, 32 optimize(10) was topped up
+    tr[9] = (double)((unsigned)tr[9] | (nxt.queued && !nxt.extra ? 16u : 0u) | (nxt.topped_up ? 32u : 0u));
   }
   // ---- inlier flags + final state written by the GPU into the mapped staging buffer ----
   // (the staging call region was consumed by the upload long before: the stream is in order)

@@ -2398,164 +2398,6 @@ __device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys
   if (lane == 0) S.out[4] = sc;
 }
 
-// ---------------------------------------------------------------------------
-// Reduced camera system for K <= 10 optimised poses on one 256-thread workgroup, blocked by the
-// 6x6 pose blocks and held in REGISTERS: lane i of every wave owns row i; wave w owns the block
-// columns b = w, w + 4, w + 8 (a[q][cc] = S[i][6 (w + 4 q) + cc]).  Step s (right-looking LDL^T):
-//   the owner wave of block column s factors it column by column (pivots and the column's
-//   entries by readlane, no LDS) -> panel l_ic and W_ic = l_ic d_c into LDS -> one barrier ->
-//   every wave: z_i -= l_ic z_c (forward substitution, z replicated in every wave) and the trailing
-//   update a_ik -= sum_c l_ic W_kc of its own later block columns (W rows broadcast from LDS).
-// One barrier per pose block (the panel buffer alternates by step parity); then y = D^-1 z and the
-// backward substitution L^T x = y in wave 0 from the stored panels; candidate poses + LM scale.
-// ---------------------------------------------------------------------------
-template <int N, int I = 0, typename F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<N, I + 1>(f);
-  }
-}
-
-struct Blk4Lds {
-  double pan[2][64][6];    // l_ic of step s's block column (rows >= the pivot; 0 above)
-  double wpan[2][64][6];   // W_ic = l_ic d_c
-  double Lall[10][64][6];  // every step's l_ic (backward substitution)
-  double dg[64];           // pivots
-  int bad;
-};
-
-template <int K>
-__device__ __forceinline__ void solve_blk4(Problem P, const Active& A, const Sys& S, double lambda, Blk4Lds& w,
-                                           bool coherent) {
-  constexpr int N = 6 * K, NQ = (K + 3) / 4;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int pa = lane / 6, r = lane - 6 * pa;
-  const bool row = lane < N;
-  auto ld = [&](int idx) {
-    return coherent ? __hip_atomic_load(S.pairfin + idx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : S.pairfin[idx];
-  };
-  double a[NQ][6];
-  double z = 0.0, bpl = 0.0;
-#pragma unroll
-  for (int q = 0; q < NQ; q++) {
-    const int b = wv + 4 * q;
-#pragma unroll
-    for (int cc = 0; cc < 6; cc++) {
-      const int k = 6 * b + cc;
-      double v = 0.0;
-      if (row && b < K && k <= lane) {
-        if (b == pa) v = ld(48 * pair_index(pa, pa, K) + r * 6 + cc) + (cc == r ? lambda : 0.0);
-        else v = ld(48 * pair_index(b, pa, K) + cc * 6 + r);
-      }
-      a[q][cc] = v;
-    }
-  }
-  if (row) {
-    const int dg = 48 * pair_index(pa, pa, K);
-    bpl = ld(dg + 36 + r);
-    z = bpl - ld(dg + 42 + r);
-  }
-  if (tid == 0) w.bad = coherent ? __hip_atomic_load(S.fail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *S.fail;
-  __syncthreads();
-  if (w.bad) return;  // uniform: a landmark block failed to invert
-  if (tid == 0) prof_stamp(S, 1);
-  // owner of block column s: LDL^T of its 6 columns, column by column (pivots and the column's
-  // entries by readlane) -> panel s into LDS
-  bool ok = true;
-  auto factor_block = [&](auto sc) {
-    constexpr int s = decltype(sc)::value, qs = s >> 2, buf = s & 1, c0 = 6 * s;
-#pragma unroll
-    for (int c = 0; c < 6; c++) {
-      const double d = readlane64(a[qs][c], c0 + c);
-      ok = ok && d > 0.0;
-      const double rc = rcp64(d);
-      const double wic = a[qs][c];
-      const double l = lane > c0 + c ? wic * rc : 0.0;
-#pragma unroll
-      for (int c2 = c + 1; c2 < 6; c2++) a[qs][c2] = fma(-l, readlane64(wic, c0 + c2), a[qs][c2]);
-      w.pan[buf][lane][c] = l;
-      w.wpan[buf][lane][c] = l * d;
-      w.Lall[s][lane][c] = l;
-      if (lane == c) w.dg[c0 + c] = d;
-    }
-    if (lane == 0 && !ok) w.bad = 1;
-  };
-  // trailing update of block column b (register slot q) with panel s
-  auto update_block = [&](int q, const double (&l6)[6], int buf, int b) {
-#pragma unroll
-    for (int cc = 0; cc < 6; cc++) {
-      const double* Wk = w.wpan[buf][6 * b + cc];
-      double t = a[q][cc];
-#pragma unroll
-      for (int c = 0; c < 6; c++) t = fma(-l6[c], Wk[c], t);
-      a[q][cc] = t;
-    }
-  };
-  if (wv == 0) factor_block(std::integral_constant<int, 0>{});
-  // step s: every wave applies panel s (forward substitution of z, its later block columns); the
-  // owner of block column s + 1 updates that one first and factors it before its other updates, so
-  // the next panel is out as early as possible.  One barrier per step (panel buffers alternate).
-  static_for<K>([&](auto sc) {
-    constexpr int s = decltype(sc)::value, buf = s & 1, c0 = 6 * s;
-    __syncthreads();
-    if (tid == 0) prof_stamp(S, 5 + s);  // step s's panel is out (RSPL_BA_PROF)
-    if (w.bad) return;
-    double l6[6];
-#pragma unroll
-    for (int c = 0; c < 6; c++) l6[c] = w.pan[buf][lane][c];
-#pragma unroll
-    for (int c = 0; c < 6; c++) z = fma(-l6[c], readlane64(z, c0 + c), z);
-    if constexpr (s + 1 < K) {
-      constexpr int sn = s + 1, qn = sn >> 2;
-      if (wv == (sn & 3)) {
-        update_block(qn, l6, buf, sn);
-        factor_block(std::integral_constant<int, sn>{});
-      }
-    }
-#pragma unroll
-    for (int q = 0; q < NQ; q++) {
-      const int b = wv + 4 * q;
-      if (b <= s + 1 || b >= K) continue;  // wave-uniform; block s + 1 was updated above
-      update_block(q, l6, buf, b);
-    }
-  });
-  if (w.bad) {
-    if (tid == 0) atomicOr(S.fail, 1);
-    return;
-  }
-  if (wv != 0) return;
-  if (tid == 0) prof_stamp(S, 2);
-  // y = D^-1 z; backward L^T x = y (lane i: y_i -= l_ki x_k for k > i, k descending)
-  double y = row ? z * rcp64(w.dg[lane]) : 0.0;
-  double lt[N];
-#pragma unroll
-  for (int k = 0; k < N; k++) lt[k] = row && k > lane ? w.Lall[pa][k][r] : 0.0;
-#pragma unroll
-  for (int k = N - 1; k >= 0; k--) y = fma(-lt[k], readlane64(y, k), y);
-  const double x = y;
-  if (tid == 0) prof_stamp(S, 3);
-  if (row) S.x[lane] = x;
-  double sc = row ? x * (lambda * x + bpl) : 0.0;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
-  if (lane == 0) S.out[4] = sc;
-}
-
-template <int K>
-__global__ __launch_bounds__(256) void schur_blk4_kernel(Problem P, Active A, Sys S, double lambda) {
-  __shared__ Blk4Lds w;
-  if (S.lm) {
-    LmView v;
-    if (!lm_view(S, v)) return;
-    lambda = v.lambda;
-    if (v.cur) bank_state(P);
-  }
-  if (threadIdx.x == 0) prof_stamp(S, 0);
-  solve_blk4<K>(P, A, S, lambda, w, false);
-  if (threadIdx.x == 0) prof_stamp(S, 4);
-}
-
 // standalone single-wave solve (sharded path: after the pairfin all-reduce)
 template <int N>
 __global__ __launch_bounds__(64) void schur_wave_kernel(Problem P, Active A, Sys S, double lambda) {
@@ -3103,7 +2945,8 @@ __global__ __launch_bounds__(256) void update_errors_kernel(Problem P, Lin L, Ac
   int ub = blockIdx.x;
   if (SPEC && A.ue_bpr > 0) {
     const int b = blockIdx.x, x = b & 7, sl = b >> 3, r = sl / A.ue_bpr, lb = 8 * r + x;
-    ub = lb < A.nchk ? lb * A.ue_bpr + (sl - r * A.ue_bpr) : (A.nL + 31) / 32 + 1;  // (else: no landmark)
+    constexpr int per = 64 * kUeWaves / kGroup;  // landmarks per workgroup (as set_update_geometry)
+    ub = lb < A.nchk ? lb * A.ue_bpr + (sl - r * A.ue_bpr) : (A.nL + per - 1) / per + 1;  // (else: no landmark)
   }
   const int t = ub * (64 * kUeWaves) + tid, g = t / kGroup, j = t % kGroup;
   const bool in = tid < 64 * kUeWaves && g < A.nL;
@@ -3516,18 +3359,9 @@ __global__ __launch_bounds__(256) void shard_finish_kernel(Problem P, int E, con
 int shard_red_len(int K, int nranks) { return 6 * K + nranks + 3; }
 bool fast_path(int K) { return 6 * K > 0 && 6 * K <= kCholLdsMax; }
 bool wave_path(int K) { return K > 0 && K <= kWaveSolveMaxK; }
-// reduced-system solver for K <= 10 (RSPL_BA_SOLVE, read per trial: "wave" default -- the single-wave
-// LDL^T in the last Schur chunk, two launches per trial; "blk4" -- the 4-wave blocked LDL^T as a
-// third launch; "lds"; K > 10: "lds").  Pipeline A/B (profiles/r03_experiments.md): wave 788 vs blk4
-// 772 frames/s (mean of four alternating runs each, two boxes)
-static int solve_mode(int K) {
-  const char* e = getenv("RSPL_BA_SOLVE");
-  int m = 1;
-  if (e && std::string(e) == "blk4") m = 2;
-  if (e && std::string(e) == "lds") m = 0;
-  return wave_path(K) ? m : 0;
-}
-
+// reduced-system solver for K <= 10: the single-wave LDL^T fused into the last Schur chunk (two launches per
+// trial); a 4-wave blocked LDL^T as a third launch lost in the pipeline (788 vs 772 frames/s, four alternating runs
+// on two boxes, profiles/r03_experiments.md) and was removed in round 6.  K > 10: the LDS / register solves.
 // ---------------------------------------------------------------------------
 int errors_blocks(int Ea) { return Ea > 0 ? (Ea + 255) / 256 : 1; }
 int update_blocks(const Problem& P) {
@@ -3547,9 +3381,8 @@ int update_errors_blocks(const Active& A) {
 }
 
 void set_update_geometry(Active& A) {
-  static const bool off = getenv("RSPL_BA_UEXCD") && std::string(getenv("RSPL_BA_UEXCD")) == "0";
   constexpr int per = 64 * kUeWaves / kGroup;  // landmarks per update workgroup
-  A.ue_bpr = !off && A.nchk >= 8 && A.lmchunk % per == 0 ? A.lmchunk / per : 0;
+  A.ue_bpr = A.nchk >= 8 && A.lmchunk % per == 0 ? A.lmchunk / per : 0;
 }
 
 hipError_t linearize(const Problem& P, const Lin& L, const Active& A, const Sys& S, bool with_maxdiag,
@@ -3605,12 +3438,11 @@ hipError_t ensure_schur_attr() {
   return e;
 }
 
-// the LDS-resident blocked LDL^T of the reduced system (K > kWaveSolveMaxK, or RSPL_BA_SOLVE=lds): the
-// register-tiled kernel (RSPL_BA_SOLVE_LDS=packed: the packed-LDS one, A/B)
+// the LDS-resident blocked LDL^T of the reduced system (K > kWaveSolveMaxK): the register-resident kernel for
+// K <= kRegMaxK, the packed-LDS one beyond
 static void launch_lds_solve(const Problem& P, const Active& A, const Sys& S, double lambda, hipStream_t s) {
-  static const bool packed = getenv("RSPL_BA_SOLVE_LDS") && std::string(getenv("RSPL_BA_SOLVE_LDS")) == "packed";
   const int n = 6 * A.K;
-  if (packed || A.K > kRegMaxK)
+  if (A.K > kRegMaxK)
     hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
   else
     hipLaunchKernelGGL(schur_reg_kernel, dim3(1), dim3(kRegThreads), schur_lds_bytes(n), s, P, A, S, n, lambda);
@@ -3635,17 +3467,6 @@ static void launch_chunks(const Problem& P, const Lin& L, const Active& A, const
   }
 }
 
-static void launch_blk4_solve(const Problem& P, const Active& A, const Sys& S, double lambda, hipStream_t s) {
-  switch (A.K) {
-#define RSPL_BLK4_CASE(k) \
-  case k: hipLaunchKernelGGL(schur_blk4_kernel<k>, dim3(1), dim3(256), 0, s, P, A, S, lambda); break;
-    RSPL_BLK4_CASE(1) RSPL_BLK4_CASE(2) RSPL_BLK4_CASE(3) RSPL_BLK4_CASE(4) RSPL_BLK4_CASE(5)
-    RSPL_BLK4_CASE(6) RSPL_BLK4_CASE(7) RSPL_BLK4_CASE(8) RSPL_BLK4_CASE(9) RSPL_BLK4_CASE(10)
-#undef RSPL_BLK4_CASE
-    default: break;
-  }
-}
-
 static void launch_wave_solve(const Problem& P, const Active& A, const Sys& S, double lambda, hipStream_t s) {
   switch (A.K) {
 #define RSPL_SOLVE_CASE(k) \
@@ -3660,13 +3481,11 @@ static void launch_wave_solve(const Problem& P, const Active& A, const Sys& S, d
 hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, unsigned long long seq,
                  hipStream_t s, const Spec* spec, bool* fused) {
   *fused = false;
-  const int mode = solve_mode(A.K);
-  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, lambda, L, S, mode == 1, s);
+  const bool wave = wave_path(A.K);
+  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, lambda, L, S, wave, s);
   const int n = 6 * A.K;
   if (fast_path(A.K)) {
-    if (mode == 2) {
-      launch_blk4_solve(P, A, S, lambda, s);
-    } else if (mode == 0) {
+    if (!wave) {
       hipError_t e = ensure_schur_attr();
       if (e != hipSuccess) return e;
       launch_lds_solve(P, A, S, lambda, s);
@@ -3697,12 +3516,10 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
 hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, unsigned long long seq, hipStream_t s,
                      const Spec& spec, hipEvent_t* ev) {
   if (!S.lm || !fast_path(A.K)) return hipErrorInvalidValue;
-  const int mode = solve_mode(A.K);
+  const bool wave = wave_path(A.K);
   if (ev) (void)hipEventRecord(ev[0], s);
-  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, 0.0, spec.Ls, spec.Ss, mode == 1, s);
-  if (mode == 2) {
-    launch_blk4_solve(P, A, S, 0.0, s);
-  } else if (mode == 0) {
+  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, 0.0, spec.Ls, spec.Ss, wave, s);
+  if (!wave) {
     hipError_t e = ensure_schur_attr();
     if (e != hipSuccess) return e;
     launch_lds_solve(P, A, S, 0.0, s);
@@ -3754,10 +3571,7 @@ hipError_t trial_solve(const Problem& P, const Lin& L, const Active& A, Sys& S, 
   hipLaunchKernelGGL(shard_fail_adopt_kernel, dim3(1), dim3(1), 0, s, S, S.pairfin + (size_t)A.npairs * 48);
   const int n = 6 * A.K;
   if (fast_path(A.K)) {
-    const int mode = solve_mode(A.K);
-    if (mode == 2) {
-      launch_blk4_solve(P, A, S, lambda, s);
-    } else if (mode == 1) {
+    if (wave_path(A.K)) {
       launch_wave_solve(P, A, S, lambda, s);
     } else {
       hipError_t e = ensure_schur_attr();

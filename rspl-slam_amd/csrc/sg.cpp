@@ -490,15 +490,11 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
       g.nmax = nm; g.ldv = s->ldv;
       return g;
     };
-    // RSPL_SG_GNN (A/B knob): default one launch per layer on one workgroup per 32-token tile (layer_kernel);
-    // "unfused" four launches per layer.  (Round 5 measured the layer on four workgroups per tile -- the same
-    // bits, slower in the pipeline: profiles/r05_experiments.md -- and removed it.)
-    static const bool unfused = [] {
-      const char* v = getenv("RSPL_SG_GNN");
-      return v && std::string(v) == "unfused";
-    }();
+    // one launch per layer on one workgroup per 32-token tile (layer_kernel).  (Four launches per layer --
+    // QKV GEMM, attention, mlp.0, mlp.3 -- were slower and were removed in round 6; round 5 measured the layer on
+    // four workgroups per tile -- the same bits, slower in the pipeline: profiles/r05_experiments.md.)
     auto layer = [&](sg::LayerArgs& la, int) { return sg::gnn_layer(la, B, st); };
-    if (!unfused) {  // layer 0's q / k / v (prologue launch), then one fused launch per layer
+    {  // layer 0's q / k / v (prologue launch), then one fused launch per layer
       {
         sg::LayerArgs la{};
         la.Qn = s->Qf[0]; la.Kn = s->Kf[0]; la.Vn = s->Vf[0];
@@ -519,23 +515,6 @@ extern "C" int rspl_sg_infer_device2(rspl_sg* s, int B, const double* d_feat0, c
         la.n0 = d_n0; la.n1 = d_n1; la.nmax = nm; la.nt = s->ldv / 32; la.cross = l & 1; la.last = l == kLayers - 1;
         RSPL_HIP(layer(la, l));
       }
-    }
-    for (int l = 0; l < kLayers && unfused; l++) {
-      sg::GemmHArgs q = gh(s->Xh, 256, s->hwqkv + (size_t)l * 256 * 768, 768, 256, s->bqkv + (size_t)l * 768);
-      q.C16 = s->QKh; q.ldc16 = 512; q.Vt = s->Vth;
-      RSPL_HIP(sg::gemm_h(q, 4, st));
-      sg::AttnHArgs at{};
-      at.QK = s->QKh; at.Vt = s->Vth; at.O = s->Oh; at.n0 = d_n0; at.n1 = d_n1; at.nmax = nm; at.ldv = s->ldv;
-      at.cross = l & 1;
-      RSPL_HIP(sg::attention_h(at, B, st));
-      // torch.cat([x, merge(o)], dim=1) through mlp.0, the merge folded into hw1 (upload_weights)
-      sg::GemmHArgs m1 = gh(s->Xh, 256, s->hw1 + (size_t)l * 512 * 512, 512, 512, s->b1m + (size_t)l * 512);
-      m1.A2 = s->Oh; m1.lda2 = 256; m1.ksplit = 256;
-      m1.C16 = s->HIDh; m1.ldc16 = 512;
-      RSPL_HIP(sg::gemm_h(m1, 2, st));
-      sg::GemmHArgs m2 = gh(s->HIDh, 512, s->hw2 + (size_t)l * 512 * 256, 256, 512, s->b2 + (size_t)l * 256);
-      m2.C32 = s->X; m2.ldc32 = 256; m2.C16 = s->Xh; m2.ldc16 = 256;
-      RSPL_HIP(sg::gemm_h(m2, 3, st));
     }
   }
   for (int l = 0; l < kLayers && !h16; l++) {

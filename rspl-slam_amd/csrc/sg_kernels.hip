@@ -496,142 +496,12 @@ __global__ void to_half_kernel(const float* x, _Float16* y, size_t n) {
 }
 
 // ---------------------------------------------------------------------------
-// fp16 multi-head attention (flash, online softmax), one head and 32 queries per
-// workgroup, the 4 waves splitting the key tiles.  Swapped product S^T = K Q^T on
-// v_mfma_f32_32x32x16_f16 (keys on registers, queries on lanes: in-lane softmax + one
-// xor-32); P^T feeds O^T = V^T P^T as the B operand straight from registers: k-step j,
-// lane group kh takes the keys of its registers 8j..8j+7, i.e. runs [16j+4kh, +4) and
-// [16j+8+4kh, +4), and V^T is read with exactly that key order from Vt (two 8-byte loads).
-// K/V fragments come from global memory, the next tile prefetched during the current one.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void attn_h_kernel(AttnHArgs a) {
-  __shared__ float Om[4][64][33];
-  __shared__ float Ml[4][32], Ll[4][32];
-  const int pz = blockIdx.z, p = pz >> 1, img = pz & 1;
-  const int simg = a.cross ? 1 - img : img;
-  const int nq = img ? a.n1[p] : a.n0[p];
-  const int nk = simg ? a.n1[p] : a.n0[p];
-  const int q0 = blockIdx.x * 32;
-  if (q0 >= nq || nk <= 0) return;
-  const int h = blockIdx.y;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, c = lane & 31, kh = lane >> 5;
-  const int qset = p * 2 + img, kset = p * 2 + simg;
-  const _Float16* Qb = a.QK + (size_t)qset * a.nmax * 512 + h * 64;
-  const _Float16* Kb = a.QK + (size_t)kset * a.nmax * 512 + 256 + h * 64;
-  const _Float16* Vb = a.Vt + (size_t)(kset * 4 + h) * 64 * a.ldv;
-  half8 qf[4];
-  {
-    const _Float16* qr = Qb + (size_t)min(q0 + c, nq - 1) * 512 + 8 * kh;
-#pragma unroll
-    for (int s = 0; s < 4; s++) qf[s] = *reinterpret_cast<const half8*>(qr + 16 * s);
-  }
-  floatx16 o0, o1;
-#pragma unroll
-  for (int r = 0; r < 16; r++) {
-    o0[r] = 0.f;
-    o1[r] = 0.f;
-  }
-  float m_run = -INFINITY, l_run = 0.f;
-  const int ntiles = (nk + 31) / 32;
-  half8 kf[4], vf[2][2];
-  auto fetch = [&](int t) {
-    const _Float16* kr = Kb + (size_t)min(t * 32 + c, nk - 1) * 512 + 8 * kh;
-#pragma unroll
-    for (int s = 0; s < 4; s++) kf[s] = *reinterpret_cast<const half8*>(kr + 16 * s);
-#pragma unroll
-    for (int dt = 0; dt < 2; dt++)
-#pragma unroll
-      for (int j = 0; j < 2; j++) {
-        const _Float16* vr = Vb + (size_t)(32 * dt + c) * a.ldv + t * 32 + 16 * j + 4 * kh;
-        const uint2 lo = *reinterpret_cast<const uint2*>(vr), hi = *reinterpret_cast<const uint2*>(vr + 8);
-        uint4 w = make_uint4(lo.x, lo.y, hi.x, hi.y);
-        vf[dt][j] = *reinterpret_cast<const half8*>(&w);
-      }
-  };
-  if (wv < ntiles) fetch(wv);
-  for (int t = wv; t < ntiles; t += 4) {
-    half8 kc_[4], vc[2][2];
-#pragma unroll
-    for (int s = 0; s < 4; s++) kc_[s] = kf[s];
-#pragma unroll
-    for (int dt = 0; dt < 2; dt++)
-#pragma unroll
-      for (int j = 0; j < 2; j++) vc[dt][j] = vf[dt][j];
-    if (t + 4 < ntiles) fetch(t + 4);
-    floatx16 st;
-#pragma unroll
-    for (int r = 0; r < 16; r++) st[r] = 0.f;
-#pragma unroll
-    for (int s = 0; s < 4; s++) st = mfma16(kc_[s], qf[s], st);
-    float x[16];
-    float mx = -INFINITY;
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-      const int key = t * 32 + (r & 3) + 8 * (r >> 2) + 4 * kh;
-      x[r] = key < nk ? st[r] * 0.125f : -INFINITY;  // scores / dim**.5 (superglue.py:90)
-      mx = fmaxf(mx, x[r]);
-    }
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = __expf(m_run - m_new);
-    float sum = 0.f;
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-      x[r] = __expf(x[r] - m_new);
-      sum += x[r];
-    }
-    sum += __shfl_xor(sum, 32);
-    l_run = l_run * alpha + sum;
-    m_run = m_new;
-#pragma unroll
-    for (int r = 0; r < 16; r++) {
-      o0[r] *= alpha;
-      o1[r] *= alpha;
-    }
-#pragma unroll
-    for (int j = 0; j < 2; j++) {
-      half8 pf;
-#pragma unroll
-      for (int u = 0; u < 8; u++) pf[u] = (_Float16)x[8 * j + u];
-      o0 = mfma16(vc[0][j], pf, o0);
-      o1 = mfma16(vc[1][j], pf, o1);
-    }
-  }
-  // merge the 4 waves' partial (m, l, O^T) per query
-#pragma unroll
-  for (int r = 0; r < 16; r++) {
-    const int d = (r & 3) + 8 * (r >> 2) + 4 * kh;
-    Om[wv][d][c] = o0[r];
-    Om[wv][32 + d][c] = o1[r];
-  }
-  if (kh == 0) {
-    Ml[wv][c] = m_run;
-    Ll[wv][c] = l_run;
-  }
-  __syncthreads();
-  _Float16* O = a.O + (size_t)qset * a.nmax * 256 + h * 64;
-  for (int idx = tid; idx < 32 * 64; idx += 256) {
-    const int q = idx >> 6, d = idx & 63;
-    float M = -INFINITY;
-#pragma unroll
-    for (int w = 0; w < 4; w++) M = fmaxf(M, Ml[w][q]);
-    float L = 0.f, acc = 0.f;
-#pragma unroll
-    for (int w = 0; w < 4; w++) {
-      const float e = (Ml[w][q] == -INFINITY) ? 0.f : __expf(Ml[w][q] - M);
-      L += e * Ll[w][q];
-      acc += e * Om[w][d][q];
-    }
-    if (q0 + q < nq) O[(size_t)(q0 + q) * 256 + d] = (_Float16)(acc / L);
-  }
-}
-
-// ---------------------------------------------------------------------------
 // One AttentionalGNN layer, fused (fp16 engine; superglue.py:88-173): a 512-thread workgroup
 // owns 32 tokens of one image and runs, without leaving the CU,
 //   (1) multi-head attention of its 32 queries against all keys / values of the source image
-//       (self or cross), flash-style as attn_h_kernel: wave w takes head w & 3 and every
-//       other 32-key tile; the two partial softmax states per head merge through LDS;
+//       (self or cross), flash-style (online softmax; swapped product S^T = K Q^T, keys on registers,
+//       queries on lanes): wave w takes head w & 3 and every other 32-key tile; the two partial
+//       softmax states per head merge through LDS;
 //   (2) mlp.0 on [x | message] (merge folded into W1, BN folded) + ReLU -> HID in LDS;
 //   (3) mlp.3 + the residual: x += delta (fp32 stream, fp16 shadow, and the new fp16 x in LDS);
 //   (4) the NEXT layer's q / k / v projections of the same 32 tokens (v stored transposed).
@@ -2113,16 +1983,10 @@ static hipError_t gemm_rk_launch(const GemmHArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
-// RSPL_SG_GEMM=lds: the LDS-staged 64x64 kernel (timing comparisons); default the K-split one
-static bool gemm_lds() {
-  const char* v = getenv("RSPL_SG_GEMM");
-  return v && std::string(v) == "lds";
-}
-
+// the K-split register kernel where K allows, else the LDS-staged 64x64 one
 hipError_t gemm_h(const GemmHArgs& a, int mode, hipStream_t s) {
   if (a.K > kGhMaxK || a.K % 16 != 0) return hipErrorInvalidValue;
-  static const bool lds = gemm_lds();
-  if (!lds && a.K % 64 == 0 && a.K <= 64 * kRdU && (!a.A2 || a.ksplit % 16 == 0)) {
+  if (a.K % 64 == 0 && a.K <= 64 * kRdU && (!a.A2 || a.ksplit % 16 == 0)) {
     switch (mode) {
       case 0: return gemm_rk_launch<0, 1>(a, s);
       case 1: return gemm_rk_launch<1, 1>(a, s);
@@ -2142,11 +2006,6 @@ hipError_t gemm_h(const GemmHArgs& a, int mode, hipStream_t s) {
   return hipErrorInvalidValue;
 }
 
-hipError_t attention_h(const AttnHArgs& a, int B, hipStream_t s) {
-  hipLaunchKernelGGL(attn_h_kernel, dim3((a.nmax + 31) / 32, 4, B * 2), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
 hipError_t gnn_layer(const LayerArgs& a, int B, hipStream_t s) {
   constexpr size_t lds = sizeof(_Float16) * 2 * 32 * kLdA;  // x | message, HID (>= the 32 x 776 q|k|v stage)
   static_assert(2 * kLdA >= 776, "q | k | v staging tile exceeds the LDS carve");
@@ -2160,8 +2019,7 @@ hipError_t gnn_layer(const LayerArgs& a, int B, hipStream_t s) {
   LayerArgs la = a;
   const int sets = B * 2, tiles = (a.nmax + 31) / 32;
   la.nsets = sets;
-  static const bool noxcd = getenv("RSPL_SG_NOXCD") != nullptr;  // A/B knob: the plain (tile, set) grid
-  la.xps = sets <= 8 && !noxcd ? 8 / sets : 0;                      // XCDs per token set
+  la.xps = sets <= 8 ? 8 / sets : 0;                                // XCDs per token set
   la.tpx = la.xps ? (tiles + la.xps - 1) / la.xps : 0;            // tiles per XCD
   if (la.xps)
     hipLaunchKernelGGL(layer_kernel, dim3(8 * la.tpx), dim3(512), lds, s, la);

@@ -54,17 +54,6 @@ struct GemmHArgs {
   int nmax, ldv;
 };
 
-// fp16 multi-head attention: QK [set][nmax][512] (Q | K, head-contiguous), Vt as above,
-// O [set][nmax][256] fp16
-struct AttnHArgs {
-  const _Float16* QK;
-  const _Float16* Vt;
-  _Float16* O;
-  const int* n0;
-  const int* n1;
-  int nmax, ldv;
-  int cross;
-};
 
 // One fused AttentionalGNN layer (fp16 engine): attention -> [x | message] MLP -> residual ->
 // the next layer's Q / K / V^T, per 32-token tile of one image (layer_kernel).  QK / Vt of the
@@ -163,7 +152,6 @@ hipError_t gemm(const GemmArgs& a, int batch, hipStream_t s);
 hipError_t to_half_t(const float* W, int K, int N, _Float16* Wt, hipStream_t s);
 hipError_t to_frag(const _Float16* Wt, int N, int K, _Float16* out, hipStream_t s);
 hipError_t gemm_h(const GemmHArgs& a, int mode, hipStream_t s);
-hipError_t attention_h(const AttnHArgs& a, int B, hipStream_t s);
 hipError_t gnn_layer(const LayerArgs& a, int B, hipStream_t s);
 // fp32 -> fp16, n elements
 hipError_t to_half(const float* x, _Float16* y, size_t n, hipStream_t s);

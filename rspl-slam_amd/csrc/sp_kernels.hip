@@ -193,61 +193,27 @@ __device__ __forceinline__ floatx16 mfma16(half8 a, half8 b, floatx16 c) {
 constexpr int HCK = 32;       // input channels per stage
 constexpr int HCS = HCK + 8;  // LDS row stride in halves
 
-template <int CIN, int TH, bool POOL, bool FUSE1A, bool OUT_F32>
+template <int CIN, int TH, bool POOL, bool OUT_F32>
 __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
   static_assert(CIN % HCK == 0, "Cin must be a multiple of 32");
   constexpr int HX = TW + 2, HY = TH + 2;
   constexpr int MT = TH / 8;
   __shared__ __attribute__((aligned(16))) _Float16 halo[HY * HX * HCS];
   __shared__ __attribute__((aligned(16))) _Float16 wts[9 * 64 * HCS];
-  __shared__ float patch[FUSE1A ? (TH + 4) * (TW + 4) : 1];
-  __shared__ float w1a[FUSE1A ? 64 * 10 : 1];
 
   const int H = a.H, W = a.W, COUT = a.cout;
   const int tiles_x = (W + TW - 1) / TW, tiles_y = (H + TH - 1) / TH;
-  const int per_img = tiles_x * tiles_y, ntiles = a.B * per_img;  // (a.B: set by the launcher)
+  const int per_img = tiles_x * tiles_y;
   const int co0 = blockIdx.y * 64;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int ml = lane & 31, kl = lane >> 5;
 
-  // FUSE1A (conv1): persistent -- a workgroup walks tiles blockIdx.x, + gridDim.x, ... with the conv1a
-  // weights staged once, and the next tile's image patch (2 pixels per thread, raw u8) fetched while the
-  // current tile's last stage runs on MFMA; every other layer: one tile per workgroup (grid = tiles)
-  constexpr int PP = FUSE1A ? ((TH + 4) * (TW + 4) + 255) / 256 : 1;
-  int pv[PP];  // the prefetched patch pixels: u8 value, -1 outside the image (zero padding)
-  auto load_patch = [&](int tile_) {
-    const int bi_ = tile_ / per_img, t_ = tile_ % per_img;
-    const int y0_ = (t_ / tiles_x) * TH, x0_ = (t_ % tiles_x) * TW;
-    const uint8_t* img = a.img + (size_t)bi_ * a.img_pitch;
-#pragma unroll
-    for (int r = 0; r < PP; r++) {
-      const int i = tid + 256 * r, py = i / (TW + 4), px = i % (TW + 4);
-      const int y = y0_ - 2 + py, x = x0_ - 2 + px;
-      pv[r] = (i < (TH + 4) * (TW + 4) && tile_ < ntiles && y >= 0 && y < H && x >= 0 && x < W)
-                  ? (int)img[(size_t)y * a.img_stride + x]
-                  : -1;
-    }
-  };
-  if constexpr (FUSE1A) {
-    load_patch(blockIdx.x);
-    for (int i = tid; i < 64 * 10; i += 256) w1a[i] = (i % 10 < 9) ? a.w1a[(i / 10) * 9 + i % 10] : a.b1a[i / 10];
-  }
   constexpr int HALO8 = HY * HX * (HCK / 8), HPT = (HALO8 + 255) / 256;
-  half8 pw[9], ph[FUSE1A ? 1 : HPT];  // the next stage's weights / halo in flight (across tiles too)
-  for (int tile = blockIdx.x; tile < ntiles; tile += FUSE1A ? gridDim.x : ntiles) {
+  half8 pw[9], ph[HPT];  // the next stage's weights / halo in flight
+  const int tile = blockIdx.x;  // one tile per workgroup (grid = tiles)
   const int bi = tile / per_img;
   const int t = tile % per_img;
   const int y0 = (t / tiles_x) * TH, x0 = (t % tiles_x) * TW;
-  if constexpr (FUSE1A) {
-    // (the previous tile's readers of patch finished before its epilogue's barrier)
-#pragma unroll
-    for (int r = 0; r < PP; r++) {
-      const int i = tid + 256 * r;
-      // src/super_point.cpp:146-150 normalisation, (float)(u / 255.0) in double (= the host LUT)
-      if (i < (TH + 4) * (TW + 4)) patch[i] = pv[r] >= 0 ? (float)((double)pv[r] / 255.0) : 0.f;
-    }
-  }
-
   floatx16 acc[MT][2];
 #pragma unroll
   for (int m = 0; m < MT; m++)
@@ -256,9 +222,8 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; r++) acc[m][n][r] = 0.f;
 
-  // software pipeline over the input-channel stages: the next stage's weights (and halo, unless
-  // conv1a computes it) are fetched into registers while the current stage's MFMAs run, and
-  // written to LDS after the next barrier
+  // software pipeline over the input-channel stages: the next stage's weights and halo are fetched into
+  // registers while the current stage's MFMAs run, and written to LDS after the next barrier
   auto fetch = [&](int c0) {
 #pragma unroll
     for (int r = 0; r < 9; r++) {  // weights [9][64 co][32 ci]: 2304 half8, 9 per thread
@@ -266,7 +231,7 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
       const int kk = rr / 64, co = rr % 64;
       pw[r] = *reinterpret_cast<const half8*>(a.hw + ((size_t)kk * COUT + co0 + co) * CIN + c0 + 8 * q);
     }
-    if constexpr (!FUSE1A) {
+    {
       const _Float16* in = a.hin + (size_t)bi * H * W * CIN;
 #pragma unroll
       for (int r = 0; r < HPT; r++) {
@@ -280,54 +245,10 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
       }
     }
   };
-  if (!FUSE1A || tile == (int)blockIdx.x) fetch(0);  // (FUSE1A: later tiles' first stage came with the last)
+  fetch(0);
   for (int c0 = 0; c0 < CIN; c0 += HCK) {
     __syncthreads();
-    if constexpr (FUSE1A) {
-      // conv1a -> ReLU -> fp16 halo, itself on MFMA: D[pix][c] = A[pix][k] B[k][c] with
-      // k = the 9 taps of the image patch, k = 9 the bias (A = 1), k > 9 zero -- one
-      // v_mfma_f32_32x32x16_f16 per 32 halo pixels x 32 channels (11 per stage) instead of
-      // 9 scalar FMAs and 19 LDS reads per halo value
-      // one M-tile per halo row (32 columns, HX of them real): every output's halo position
-      // is a compile-time function of the accumulator register, no per-element division
-      half8 bw;
-#pragma unroll
-      for (int j = 0; j < 8; j++) {
-        const int k = 8 * kl + j;
-        bw[j] = (_Float16)(k <= 9 ? w1a[(c0 + ml) * 10 + k] : 0.f);
-      }
-      // transposed product D[c][px] = W1a[c][k] P[k][px]: lane (px, kl) then holds channels
-      // 8 q + 4 kl + 0..3 of halo pixel px -- four 8-byte LDS stores per lane instead of sixteen
-      // 2-byte ones (the same products summed over the same k)
-      const int hx = ml;
-      const int x = x0 - 1 + hx;
-      for (int hy = wv; hy < HY; hy += 4) {
-        const int y = y0 - 1 + hy;
-        half8 av;
-#pragma unroll
-        for (int j = 0; j < 8; j++) {
-          const int k = 8 * kl + j;
-          float v = 0.f;
-          if (hx < HX) v = k < 9 ? patch[(hy + k / 3) * (TW + 4) + hx + k % 3] : (k == 9 ? 1.f : 0.f);
-          av[j] = (_Float16)v;
-        }
-        floatx16 d;
-#pragma unroll
-        for (int r = 0; r < 16; r++) d[r] = 0.f;
-        d = mfma16(bw, av, d);
-        const bool in = y >= 0 && y < H && x >= 0 && x < W;
-        if (hx < HX) {
-#pragma unroll
-          for (int q = 0; q < 4; q++) {
-            typedef _Float16 half4 __attribute__((ext_vector_type(4)));
-            half4 h4;
-#pragma unroll
-            for (int e = 0; e < 4; e++) h4[e] = (_Float16)(in ? fmaxf(d[4 * q + e], 0.f) : 0.f);
-            *reinterpret_cast<half4*>(&halo[(hy * HX + hx) * HCS + 8 * q + 4 * kl]) = h4;
-          }
-        }
-      }
-    } else {
+    {
 #pragma unroll
       for (int r = 0; r < HPT; r++) {
         const int i = tid + 256 * r;
@@ -341,10 +262,6 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
     }
     __syncthreads();
     if (c0 + HCK < CIN) fetch(c0 + HCK);
-    else if (FUSE1A && tile + (int)gridDim.x < ntiles) {  // the next tile's first stage and image patch
-      fetch(0);
-      load_patch(tile + gridDim.x);
-    }
 #pragma unroll
     for (int kk = 0; kk < 9; kk++) {
       const int ky = kk / 3, kx = kk % 3;
@@ -395,7 +312,7 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
         *reinterpret_cast<half8*>(a.hout + (size_t)bi * H * W * COUT + ((size_t)y * W + x) * COUT + co0 + 8 * q) =
             *reinterpret_cast<const half8*>(&wts[px * OS + 8 * q]);
     }
-    continue;
+    return;
   }
   if constexpr (POOL && !OUT_F32) {
     // 2x2-pooled output tile (TH/2 x 8 pixels x 64 channels) staged through LDS the same way
@@ -427,7 +344,7 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
         *reinterpret_cast<half8*>(a.hout + (size_t)bi * H2 * W2 * COUT + ((size_t)py * W2 + pxx) * COUT + co0 + 8 * q) =
             *reinterpret_cast<const half8*>(&wts[px * OS + 8 * q]);
     }
-    continue;
+    return;
   }
 #pragma unroll
   for (int n = 0; n < 2; n++) {
@@ -468,20 +385,19 @@ __global__ __launch_bounds__(256) void conv3x3_h_kernel(ConvArgs a) {
       }
     }
   }
-  }  // tile loop
 }
 
 // ---------------------------------------------------------------------------
 // conv1 (conv1a 1->64 + ReLU + conv1b 64->64 + ReLU + 2x2 max-pool, superpoint.py:120-124) with the
 // whole conv1b weight tensor RESIDENT in LDS: one persistent 256-thread workgroup per CU walks 16x16-pixel
-// output tiles.  conv3x3_h_kernel<FUSE1A> restages each 32-channel half of the weights per tile and per
-// stage (two workgroups per CU, 76 KB each, phases separated by barriers: 29 % MFMA-busy SIMD time,
-// profiles/r05_experiments.md).  Here per tile: the image patch (prefetched during the previous tile's
+// output tiles.  The round-4 per-stage kernel (removed in round 6) restaged each 32-channel half of the weights
+// per tile and per stage (two workgroups per CU, 76 KB each, phases separated by barriers: 29 % MFMA-busy SIMD
+// time, profiles/r05_experiments.md).  Here per tile: the image patch (prefetched during the previous tile's
 // MFMAs) -> LDS; conv1a of all 64 channels on MFMA (transposed product: 8-byte LDS stores) into the halo;
 // 144 v_mfma_f32_32x32x16_f16 per wave from LDS; bias + ReLU + pool through LDS to 16-byte stores.
 // LDS: weights 9 x 64 x 72 halves (82.9 KB) + halo 18 x 18 x 72 halves (46.7 KB) + patch + conv1a weights.
-// The same fp16 roundings of the same fp32 accumulations as conv3x3_h_kernel<64, 16, true, true>
-// (conv1a: one MFMA over the 9 taps + bias; conv1b: the MFMA k-steps in the same channel order).
+// The same fp16 roundings of the same fp32 accumulations as that kernel (bitwise equal in round 5's A/B):
+// conv1a one MFMA over the 9 taps + bias, conv1b the MFMA k-steps in the same channel order.
 // ---------------------------------------------------------------------------
 constexpr int C1S = 72;  // LDS row stride (halves) of the weight and halo rows: 64 channels + 8
 
@@ -1629,27 +1545,24 @@ hipError_t conv3x3(const ConvArgs& a, int cin, bool pool, bool fuse1a, int B, hi
   return hipErrorInvalidValue;
 }
 
-// workgroups of the persistent conv1 (FUSE1A): two per CU (76 KB of LDS each)
-static int conv1_workgroups() {
+// the device's CU count (the persistent conv1's grid)
+static int device_cus() {
   static int n = 0;
   if (!n) {
     int dev = 0, cus = 0;
     if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) !=
                                                  hipSuccess || cus <= 0)
       cus = 256;
-    n = 2 * cus;
+    n = cus;
   }
   return n;
 }
 
-template <int CIN, int TH, bool POOL, bool FUSE1A, bool OUT_F32>
-static hipError_t launch_conv_h(const ConvArgs& a, int B, hipStream_t s, hipEvent_t t0 = nullptr,
-                                hipEvent_t t1 = nullptr) {
+template <int CIN, int TH, bool POOL, bool OUT_F32>
+static hipError_t launch_conv_h(const ConvArgs& a, int B, hipStream_t s) {
   const int tiles = ((a.W + TW - 1) / TW) * ((a.H + TH - 1) / TH);
-  ConvArgs b = a;
-  b.B = B;
-  dim3 grid(FUSE1A ? std::min(B * tiles, conv1_workgroups()) : B * tiles, a.cout / 64);
-  hipExtLaunchKernelGGL((conv3x3_h_kernel<CIN, TH, POOL, FUSE1A, OUT_F32>), grid, dim3(256), 0, s, t0, t1, 0, b);
+  dim3 grid(B * tiles, a.cout / 64);
+  hipLaunchKernelGGL((conv3x3_h_kernel<CIN, TH, POOL, OUT_F32>), grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1657,8 +1570,6 @@ hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool ou
                      hipEvent_t t0, hipEvent_t t1) {
   const bool small = (a.H * a.W) <= 128 * 192;
   if (fuse1a) {
-    static const bool staged = getenv("RSPL_SP_CONV1") && std::string(getenv("RSPL_SP_CONV1")) == "stage";
-    if (staged) return launch_conv_h<64, 16, true, true, false>(a, B, s, t0, t1);
     constexpr size_t lds = sizeof(_Float16) * (9 * 64 * C1S + 18 * 18 * C1S) + sizeof(float) * (20 * 20 + 64 * 10);
     static bool attr = false;
     if (!attr) {
@@ -1670,23 +1581,21 @@ hipError_t conv3x3_h(const ConvArgs& a, int cin, bool pool, bool fuse1a, bool ou
     ConvArgs b = a;
     b.B = B;
     const int tiles = B * ((a.W + TW - 1) / TW) * ((a.H + 15) / 16);
-    // one persistent workgroup on every other CU (conv1_workgroups() / 4): each holds 131 KB of a CU's LDS for
-    // the whole conv1, so on a CU it occupies no local-BA Schur chunk wave (35 KB) fits -- with a workgroup on
-    // every CU the BA chain stalled for the length of conv1 every step.  Measured in the C3 pipeline (r05
-    // experiments): 256 workgroups 936 frames/s, 192 951-967, 128 976-977 (conv1 0.15 -> 0.19 ms, off the
-    // critical path).  RSPL_SP_CONV1_WG overrides (A/B).
-    static const int wg_env = getenv("RSPL_SP_CONV1_WG") ? atoi(getenv("RSPL_SP_CONV1_WG")) : 0;
-    const int wgs = wg_env > 0 ? wg_env : std::max(1, conv1_workgroups() / 4);
+    // one persistent workgroup on every other CU: each holds 131 KB of a CU's LDS for the whole conv1, so on a
+    // CU it occupies no local-BA Schur chunk wave (35 KB) fits -- with a workgroup on every CU the BA chain
+    // stalled for the length of conv1 every step.  Measured in the C3 pipeline (r05 experiments): 256 workgroups
+    // 936 frames/s, 192 951-967, 128 976-977 (conv1 0.15 -> 0.19 ms, off the critical path).
+    const int wgs = std::max(1, device_cus() / 2);
     hipExtLaunchKernelGGL(conv1_res_kernel, dim3(std::min(tiles, wgs)), dim3(256), lds, s, t0, t1, 0, b);
     return hipGetLastError();
   }
-  if (out_f32) return launch_conv_h<128, 8, false, false, true>(a, B, s);
-  if (cin == 64 && pool) return launch_conv_h<64, 16, true, false, false>(a, B, s);
-  if (cin == 64 && !pool) return small ? launch_conv_h<64, 8, false, false, false>(a, B, s)
-                                       : launch_conv_h<64, 16, false, false, false>(a, B, s);
-  if (cin == 128 && pool) return launch_conv_h<128, 16, true, false, false>(a, B, s);
-  if (cin == 128 && !pool) return small ? launch_conv_h<128, 8, false, false, false>(a, B, s)
-                                        : launch_conv_h<128, 16, false, false, false>(a, B, s);
+  if (out_f32) return launch_conv_h<128, 8, false, true>(a, B, s);
+  if (cin == 64 && pool) return launch_conv_h<64, 16, true, false>(a, B, s);
+  if (cin == 64 && !pool) return small ? launch_conv_h<64, 8, false, false>(a, B, s)
+                                       : launch_conv_h<64, 16, false, false>(a, B, s);
+  if (cin == 128 && pool) return launch_conv_h<128, 16, true, false>(a, B, s);
+  if (cin == 128 && !pool) return small ? launch_conv_h<128, 8, false, false>(a, B, s)
+                                        : launch_conv_h<128, 16, false, false>(a, B, s);
   return hipErrorInvalidValue;
 }
 

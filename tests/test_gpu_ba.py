@@ -152,13 +152,10 @@ def test_ba_long_lines(ba):
     _compare(ba.run(prob), oracle.ba_local(prob), **LINES)
 
 
-@pytest.mark.parametrize("solver", ["wave", "blk4"])
 @pytest.mark.parametrize("n_poses", [2, 3, 4, 7, 11, 12])
-def test_ba_wave_solve_sizes(ba, n_poses, solver, monkeypatch):
+def test_ba_wave_solve_sizes(ba, n_poses):
     # K = n_poses - 1 optimised poses: K <= 10 solves the reduced system in one wavefront fused
-    # into the Schur chunks (single-wave LDL^T, the default) or in the 4-wave blocked LDL^T launch
-    # (RSPL_BA_SOLVE=blk4, read per trial); K = 11 takes the blocked LDS solve
-    monkeypatch.setenv("RSPL_BA_SOLVE", solver)
+    # into the Schur chunks (single-wave LDL^T); K = 11 takes the register-resident LDS solve
     prob, gt = SY.ba_problem(n_poses=n_poses, n_points=500, n_lines=10, seed=60 + n_poses, pixel_sigma=0.8,
                              outlier_frac=0.05)
     _compare(ba.run(prob), oracle.ba_local(prob), **LINES)
@@ -237,15 +234,21 @@ def test_ba_analytic_line_jacobian(ba, analytic, case):
 
 def test_ba_final_kernel_paths_agree(ba):
     """The call's final kernel queued speculatively behind optimize(5) and optimize(5)'s setup queued
-    speculatively behind optimize(10)'s first trials (default) against the host-ordered launches (taken on
-    calls with kernel timing): bit-identical inlier flags, poses, points and lines.  The last problems are
-    noisy enough for rejected LM trials (optimize(10) then needs trials beyond its first batch and the
-    speculative setup stays a no-op)."""
+    speculatively behind each batch of optimize(10)'s trials (default) against the host-ordered launches (taken
+    on calls with kernel timing): bit-identical inlier flags, poses, points and lines.  The last problems are
+    noisy enough for rejected LM trials: optimize(10) then needs a top-up batch and the setup queued behind the
+    batch it stops in is the one that runs.  The call trace (rspl_ba_trace flags 16 / 32) shows that the
+    speculative setup ran on every call and that both the single-batch and the topped-up case occurred."""
     probs = [SY.ba_problem(n_poses=6 + k, n_points=400, n_lines=12, seed=80 + k, pixel_sigma=0.8,
                            outlier_frac=0.05)[0] for k in range(3)]
     probs += [SY.ba_problem(n_poses=8, n_points=300, n_lines=6, seed=90 + k, pixel_sigma=4.0,
                             outlier_frac=0.3)[0] for k in range(2)]
+    ba.trace()  # (drop earlier records)
     spec = [ba.run(p) for p in probs]
+    flags = [int(r["grew"]) for r in ba.trace()]
+    assert len(flags) == len(probs)
+    assert all(f & 16 for f in flags), flags  # optimize(5)'s setup came from the speculative queue
+    assert any(f & 32 for f in flags) and any(not f & 32 for f in flags), flags  # topped-up and single-batch
     ba.kernel_timing(1)  # every call timed: the final kernel is queued after the host has seen optimize(5) stop
     try:
         host = [ba.run(p) for p in probs]

@@ -138,55 +138,6 @@ def test_nms_unit_vs_reference(pkg, golden, weight_blobs):
         np.testing.assert_array_equal(out, g[f"out{k}"], err_msg=f"map {k}")
 
 
-_SP_F16_SCRIPT = r'''
-import sys
-import numpy as np
-sys.path.insert(0, sys.argv[1])
-import rspl_loader
-pkg = rspl_loader.load()
-capi, SY = pkg.capi, pkg.synthetic
-out = {}
-for H, W, B in ((480, 752, 2), (72, 104, 1)):
-    sp = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=400, weights=sys.argv[2], max_height=H, max_width=W,
-                                             max_batch=B, precision=capi.RSPL_PREC_FP16))
-    assert sp.build(), sp.error
-    st = capi.Stream()
-    imgs = capi.DeviceBuffer(B * H * W).upload(np.stack([SY.textured_image(H, W, seed=20 + b) for b in range(B)]))
-    feats = capi.DeviceBuffer(B * 400 * 259 * 8)
-    counts = capi.DeviceBuffer(B * 4)
-    sp.infer_device(imgs.ptr, B, H, W, W, H * W, feats.ptr, 400, counts.ptr, st.handle)
-    st.synchronize()
-    out[f"F{H}"] = feats.download((B, 400, 259), np.float64)
-    out[f"n{H}"] = counts.download((B,), np.int32)
-np.savez(sys.argv[3], **out)
-'''
-
-
-def test_sp_conv1_resident_equals_staged(weight_blobs, tmp_path):
-    """The fp16 conv1 with the conv1b weights resident in LDS (conv1_res_kernel, the default) gives the same bits
-    as the per-stage kernel (conv3x3_h_kernel<FUSE1A>, RSPL_SP_CONV1=stage): the same conv1a MFMA and the same
-    conv1b MFMA k-steps in the same order.  C3 size (two images: persistent workgroups over 2820 tiles) and a
-    small ragged one."""
-    import os
-    import pathlib
-    import subprocess
-    import sys
-    root = str(pathlib.Path(__file__).resolve().parents[1])
-    script = tmp_path / "sp.py"
-    script.write_text(_SP_F16_SCRIPT)
-    res = {}
-    for mode in ("default", "stage"):
-        env = dict(os.environ)
-        env.pop("RSPL_SP_CONV1", None)
-        if mode == "stage":
-            env["RSPL_SP_CONV1"] = "stage"
-        out = tmp_path / f"{mode}.npz"
-        subprocess.run([sys.executable, str(script), root, weight_blobs[0], str(out)], env=env, check=True, timeout=240)
-        res[mode] = np.load(out)
-    for k in res["default"].files:
-        np.testing.assert_array_equal(res["default"][k], res["stage"][k], err_msg=k)
-
-
 def _sp_x3(pkg, w, k, H, W, B=1):
     sp = pkg.SuperPoint(pkg.SuperPointConfig(max_keypoints=k, weights=w, max_height=H, max_width=W, max_batch=B,
                                              precision=pkg.capi.RSPL_PREC_FP16X3))
