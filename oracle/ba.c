@@ -337,6 +337,12 @@ static int depth_positive(const ba_t* b, int t, int e) {
  *  - error (edge_project_line.cc:21-42): l = [fy wc0, fx wc1, Kv . wc], e_k = (o_k . l01 + l2) / |l01|.
  * The error is homogeneous of degree 0 in the line, so everything is evaluated at L / |d|. */
 static int g_line_jac_analytic = 0;
+/* LM trials (accepted + rejected) of the last orc_ba_local's two optimize() calls (test hook) */
+static int g_trials[2] = {0, 0};
+void orc_ba_last_trials(int* out) {
+  out[0] = g_trials[0];
+  out[1] = g_trials[1];
+}
 void orc_ba_set_line_jacobian(int analytic) { g_line_jac_analytic = analytic != 0; }
 
 static void skew(const double* v, double* S) { /* S x = v x x */
@@ -870,6 +876,7 @@ static int optimize(ba_t* b, int phase, int iters, double* chi2_out) {
       qmax++;
     } while (rho < 0 && qmax < 10);
     done++;
+    g_trials[phase - 1] += qmax;
     if (qmax == 10 || rho == 0 || !isfinite(lambda)) break;
   }
   *chi2_out = currentChi;
@@ -917,6 +924,7 @@ int orc_ba_local(const rspl_ba_problem* P, rspl_ba_result* R) {
   const double th[4] = {P->th_mono_point, P->th_stereo_point, P->th_mono_line, P->th_stereo_line};
   /* phase 1: all edges, Huber */
   b.robust = 1;
+  g_trials[0] = g_trials[1] = 0;
   R->iterations_done_first = optimize(&b, 1, P->iterations_first, &R->chi2_first);
   for (int t = 0; t < 4; t++)
     for (int e = 0; e < b.ne[t]; e++) {

@@ -110,6 +110,15 @@ def ba_local(problem):
     return res
 
 
+def ba_last_trials():
+    """LM trials (accepted + rejected) of the last ba_local's optimize(10) and optimize(5)."""
+    out = (C.c_int * 2)()
+    lib().orc_ba_last_trials.argtypes = [C.c_void_p]
+    lib().orc_ba_last_trials.restype = None
+    lib().orc_ba_last_trials(out)
+    return int(out[0]), int(out[1])
+
+
 def ba_set_line_jacobian(analytic: bool):
     """Line edges' Jacobians in ba_local: g2o's central difference (False, the default) or its analytic
     delta -> 0 limit (True)."""

@@ -241,8 +241,14 @@ def test_ba_final_kernel_paths_agree(ba):
     speculative setup ran on every call and that both the single-batch and the topped-up case occurred."""
     probs = [SY.ba_problem(n_poses=6 + k, n_points=400, n_lines=12, seed=80 + k, pixel_sigma=0.8,
                            outlier_frac=0.05)[0] for k in range(3)]
-    probs += [SY.ba_problem(n_poses=8, n_points=300, n_lines=6, seed=90 + k, pixel_sigma=4.0,
-                            outlier_frac=0.3)[0] for k in range(2)]
+    # rejected trials inside optimize(10) that still does all 10 iterations (the oracle's restatement needs 12 / 13
+    # trials for them: oracle.ba_last_trials), so the GPU queues a top-up batch
+    probs += [SY.ba_problem(n_poses=10, n_points=300, n_lines=6, seed=92, pixel_sigma=4.0, outlier_frac=0.3)[0],
+              SY.ba_problem(n_poses=10, n_points=300, n_lines=6, seed=94, pixel_sigma=0.8, outlier_frac=0.05,
+                            init_noise=3.0)[0]]
+    for p in probs[3:]:
+        r = oracle.ba_local(p)
+        assert r.iters_first == 10 and oracle.ba_last_trials()[0] > 10
     ba.trace()  # (drop earlier records)
     spec = [ba.run(p) for p in probs]
     flags = [int(r["grew"]) for r in ba.trace()]
