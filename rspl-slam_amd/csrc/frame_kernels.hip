@@ -90,39 +90,6 @@ __device__ __forceinline__ double cost_of(const View& V, const double* ev, bool 
   return r0;
 }
 
-// computeActiveErrors + activeRobustChi2 over this lane's edges (errors stored), wave-reduced.
-// Two edges per lane in flight (loads of both issued before either is used): a lone wave per
-// frame has no other wave to hide the LDS / fp64-divide latency behind.
-template <int NW>
-__device__ __forceinline__ double active_chi2(const View& V, const Pose& P, int lane, bool robust) {
-  constexpr int T = 64 * NW;
-  double s = 0;
-  for (int e = lane; e < V.n; e += 2 * T) {
-    const int e1 = e + T < V.n ? e + T : e;
-    const bool a0 = !V.lev[e], a1 = e + T < V.n && !V.lev[e1];
-    const Edge E0 = V.E[e], E1 = V.E[e1];
-    double Xc0[3], Xc1[3], ev0[3], ev1[3];
-    edge_error(E0, P, Xc0, ev0);
-    edge_error(E1, P, Xc1, ev1);
-    const double c0 = cost_of(V, ev0, E0.stereo != 0.0, robust);
-    const double c1 = cost_of(V, ev1, E1.stereo != 0.0, robust);
-    if (a0) {
-      double* er = V.err + 3 * e;
-      er[0] = ev0[0]; er[1] = ev0[1]; er[2] = ev0[2];
-      s += c0;
-    }
-    if (a1) {
-      double* er = V.err + 3 * e1;
-      er[0] = ev1[0]; er[1] = ev1[1]; er[2] = ev1[2];
-      s += c1;
-    }
-  }
-  double r[1] = {wsum(s)};
-  block_combine<NW>(r);
-  return r[0];
-}
-
-
 __device__ __forceinline__ int hidx(int i, int j) { return i * 6 - i * (i - 1) / 2 + (j - i); }
 
 // errors at T (stored) + robust chi2 + H / b (Huber IRLS weights), wave-reduced
@@ -227,11 +194,17 @@ __device__ __forceinline__ bool solve6(const double (&acc)[kNV], double lambda, 
 template <int NW>
 __device__ __forceinline__ int optimize_pose(const View& V, Pose& P, int lane, bool robust, int iters,
                                              double& chi2_out) {
+  // The linearisation at the current estimate that every iteration starts with is the one the accepted
+  // candidate of the previous iteration already computed: each trial evaluates its candidate's errors, robust
+  // cost AND normal equations in one pass over the edges (one 28-value reduction), and an accepted candidate's
+  // system becomes the next iteration's -- the same operations on the same estimate as linearising it again
+  // (g2o computes the candidate's errors, then re-linearises the accepted estimate), one edge pass and one
+  // reduction fewer per iteration.
   double acc[kNV];
   double lambda = 0, ni = 2, currentChi = 0;
   int done = 0;
+  if (iters > 0) linearize<NW>(V, P, lane, robust, acc);
   for (int it = 0; it < iters; it++) {
-    linearize<NW>(V, P, lane, robust, acc);
     currentChi = acc[27];
     if (it == 0) {  // computeLambdaInit: tau * max diagonal
       double mx = 0;
@@ -244,11 +217,17 @@ __device__ __forceinline__ int optimize_pose(const View& V, Pose& P, int lane, b
     int qmax = 0;
     do {
       double x[6];
-      const bool ok = solve6(acc, lambda, x);
+      const bool ok = solve6(acc, lambda, x);  // (uniform: every thread factors the same system)
       Pose C = P;
-      if (ok) C.set(ba::se3_mul(ba::se3_exp(x), P.T));
-      double tempChi = active_chi2<NW>(V, C, lane, robust);
-      if (!ok) tempChi = DBL_MAX;
+      double cacc[kNV];
+      double tempChi = DBL_MAX;
+      if (ok) {
+        C.set(ba::se3_mul(ba::se3_exp(x), P.T));
+        linearize<NW>(V, C, lane, robust, cacc);  // the candidate's errors (stored), cost and system
+        tempChi = cacc[27];
+      } else {
+        linearize<NW>(V, P, lane, robust, cacc);  // (as g2o: the errors recomputed at the unchanged estimate)
+      }
       rho = currentChi - tempChi;
       double scale = 1.0;
       if (ok) {
@@ -265,6 +244,8 @@ __device__ __forceinline__ int optimize_pose(const View& V, Pose& P, int lane, b
         ni = 2;
         currentChi = tempChi;
         P = C;
+#pragma unroll
+        for (int k = 0; k < kNV; k++) acc[k] = cacc[k];
       } else {
         lambda *= ni;
         ni *= 2;
@@ -301,15 +282,15 @@ __global__ __launch_bounds__(64 * NW) void frame_opt_kernel(Args a, int batch) {
     const uint4* src = reinterpret_cast<const uint4*>(a.edges + D.e0);
     uint4* dst = reinterpret_cast<uint4*>(smem);
     const int n16 = D.n * (int)(sizeof(Edge) / 16);
-    for (int k0 = lane; k0 < n16; k0 += 8 * T) {
+    int k0 = lane;
+    for (; k0 + 7 * T < n16; k0 += 8 * T) {  // whole batches: unconditional, register-resident
       uint4 v[8];
 #pragma unroll
-      for (int j = 0; j < 8; j++)
-        if (k0 + j * T < n16) v[j] = src[k0 + j * T];
+      for (int j = 0; j < 8; j++) v[j] = src[k0 + j * T];
 #pragma unroll
-      for (int j = 0; j < 8; j++)
-        if (k0 + j * T < n16) dst[k0 + j * T] = v[j];
+      for (int j = 0; j < 8; j++) dst[k0 + j * T] = v[j];
     }
+    for (; k0 < n16; k0 += T) dst[k0] = src[k0];  // the tail
     V.E = Es;
     V.err = smem + D.n * (sizeof(Edge) / 8);
     V.lev = reinterpret_cast<uint8_t*>(V.err + 3 * D.n);
