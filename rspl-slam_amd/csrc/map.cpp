@@ -260,20 +260,13 @@ struct rspl_map {
   rspl_map_config cfg{};
   std::unordered_map<int, MFrame> kf;  // _keyframes (by id; id order where the reference iterates it)
   std::vector<int> kf_ids;      // _keyframe_ids (insertion order)
+  std::vector<int> kf_sorted;   // the same ids, ascending
   // _mappoints / _maplines: looked up by id only, never iterated (node-based: element pointers stay valid)
   std::unordered_map<int, MPoint> mp;
   std::unordered_map<int, MLine> ml;
   IdIndex<MFrame> kf_ix;
   IdIndex<MPoint> mp_ix;
   IdIndex<MLine> ml_ix;
-  // per-call scratch: a counter per frame id (dense range) and the ids touched
-  std::vector<int> cnt_f;
-  std::vector<int> touched;
-  int* frame_counter(int id) {
-    if (id < 0 || id >= kDenseIds) return nullptr;
-    if (id >= (int)cnt_f.size()) cnt_f.resize(std::max<size_t>(id + 1, cnt_f.size() * 2), 0);
-    return &cnt_f[id];
-  }
   // the last assembled problem (rspl_map_last_problem)
   std::vector<int> pose_ids, point_ids, line_ids;
   std::vector<uint8_t> pose_fixed;
@@ -290,59 +283,50 @@ struct rspl_map {
   std::vector<int> lm_beg, lm_rank;
   std::vector<Obs> lm_obs;
   std::vector<std::pair<int, int>> kept_pts;
+  // per call, by keyframe id: the frame's class for the window walk and its count of observations
+  // outside the window (ids past the table: frame() and a std::map)
+  enum : uint8_t { kNoFrame = 0, kWin = 1, kOut = 2, kOutFix = 3 };
+  std::vector<uint8_t> fcls;
+  std::vector<int> fcnt;
+  std::vector<uint64_t> bad;  // remove_outliers scratch: pair keys, the pair table and its used cells
+  std::vector<int> pair_cnt, pair_hit;
 
   MFrame* frame(int id) { return kf_ix.get(kf, id); }
   MPoint* point(int id) { return id < 0 ? nullptr : mp_ix.get(mp, id); }
   MLine* line(int id) { return id < 0 ? nullptr : ml_ix.get(ml, id); }
 
-  // counts per frame id of the ids pushed, handed back in ascending id order (a std::map<int, int>
-  // of counts) and reset; ids outside the dense range go through a std::map
-  struct Counter {
-    rspl_map* m;
-    std::map<int, int> big;
-    explicit Counter(rspl_map* mm) : m(mm) { m->touched.clear(); }
-    void add(int id, int w = 1) {
-      int* c = m->frame_counter(id);
-      if (!c) {
-        big[id] += w;
-        return;
-      }
-      if (*c == 0) m->touched.push_back(id);
-      *c += w;
-    }
-    template <typename F>
-    void drain(F&& f) {  // f(id, count) in ascending id order
-      std::sort(m->touched.begin(), m->touched.end());
-      auto bi = big.begin();
-      for (int id : m->touched) {
-        while (bi != big.end() && bi->first < id) { f(bi->first, bi->second); ++bi; }
-        const int c = m->cnt_f[id];
-        m->cnt_f[id] = 0;
-        f(id, c);
-      }
-      for (; bi != big.end(); ++bi) f(bi->first, bi->second);
-      m->touched.clear();
-      big.clear();
-    }
-  };
-
-  // Map::UpdateFrameConnection (map.cc:897-937)
+  // Map::UpdateFrameConnection (map.cc:897-937).  Counts per keyframe id in fcnt (ids past the
+  // dense keyframe table in a std::map), read back in ascending id order.
   void update_connection(MFrame& f) {
-    Counter c(this);
+    const std::vector<MFrame*>& kfd = kf_ix.dense;
+    if (fcnt.size() < kfd.size()) fcnt.resize(kfd.size(), 0);
+    std::map<int, int> big;
     bool any = false;
-    for (int pid : f.mpt) {
-      const MPoint* m = point(pid);
+    const int nslot = (int)f.mpt.size();
+    for (int s = 0; s < nslot; s++) {
+      if (s + 8 < nslot)
+        if (const MPoint* q = point(f.mpt[s + 8])) __builtin_prefetch(q);
+      if (s + 4 < nslot)
+        if (const MPoint* q = point(f.mpt[s + 4])) __builtin_prefetch(q->obs.v.data());
+      const MPoint* m = point(f.mpt[s]);
       if (!m || m->type == kBad) continue;
       for (auto& kv : m->obs) {
-        if (kv.first == f.id || !frame(kv.first)) continue;
-        c.add(kv.first);
+        const int id = kv.first;
+        if (id == f.id) continue;
+        if ((unsigned)id < kfd.size()) {
+          if (!kfd[id]) continue;
+          fcnt[id]++;
+        } else {
+          if (!frame(id)) continue;
+          big[id]++;
+        }
         any = true;
       }
     }
     if (!any) return;
     std::set<std::pair<int, int>> good;
     int best = -1, best_w = -1;
-    c.drain([&](int id, int w) {  // ascending frame id (the reference's std::map)
+    auto visit = [&](int id, int w) {  // ascending frame id (the reference's std::map)
       MFrame* cf = frame(id);
       if (w > best_w) {
         best = id;
@@ -352,7 +336,16 @@ struct rspl_map {
         good.insert({w, id});
         cf->add_connection(f.id, w);
       }
-    });
+    };
+    auto bi = big.begin();
+    for (; bi != big.end() && bi->first < 0; ++bi) visit(bi->first, bi->second);
+    for (int id : kf_sorted) {
+      if (id < 0 || id >= (int)kfd.size() || !fcnt[id]) continue;
+      const int w = fcnt[id];
+      fcnt[id] = 0;
+      visit(id, w);
+    }
+    for (; bi != big.end(); ++bi) visit(bi->first, bi->second);
     if (good.empty()) {
       good.insert({best_w, best});
       frame(best)->add_connection(f.id, best_w);
@@ -405,16 +398,39 @@ struct rspl_map {
   // Map::RemoveOutliers (map.cc:818-863).  frame->RemoveMappoint(mpt) runs after the observer was
   // removed, so it looks up index -1 and leaves the frame's slot as it is -- kept as in the reference.
   void remove_outliers(const std::vector<std::pair<int, int>>& outl) {
-    std::vector<std::pair<int, int>> bad;  // MakeFramePair per (outlier, other observer); counted below
+    // MakeFramePair per (outlier, other observer) as one key, ascending (max, min) order when sorted
+    // as unsigned.  Frame ids are offset by 2^31 so that negative ids order too.
+    auto key = [](int a, int b) {
+      return (uint64_t)((uint32_t)a ^ 0x80000000u) << 32 | (uint32_t)((uint32_t)b ^ 0x80000000u);
+    };
+    // the pairs are counted first in a (outlier frame, observer id) table -- the outlier frames are
+    // the window's few poses -- and only the distinct pairs are sorted; observers past the dense
+    // keyframe table go to the key list directly
+    const std::vector<MFrame*>& kfd = kf_ix.dense;
+    const size_t ncol = kfd.size();
+    std::vector<int> rows;  // outlier frame ids, one table row each
+    bad.clear();
+    pair_hit.clear();
     for (auto& fm : outl) {
       MFrame* f = frame(fm.first);
       MPoint* m = point(fm.second);
       if (!f || !m || m->type == kBad) continue;
       m->obs.erase(f->id);
       const FlatMap<int>& obs = m->obs;  // read before the clear below (the reference copies it under its lock)
+      const size_t r = std::find(rows.begin(), rows.end(), f->id) - rows.begin();
+      if (r == rows.size()) {
+        rows.push_back(f->id);
+        if (pair_cnt.size() < rows.size() * ncol) pair_cnt.resize(rows.size() * ncol, 0);
+      }
+      int* row = pair_cnt.data() + r * ncol;
       for (auto& ob : obs) {
-        MFrame* o = frame(ob.first);
-        if (o) bad.push_back({std::max(f->id, o->id), std::min(f->id, o->id)});  // MakeFramePair
+        const int id = ob.first;
+        if ((unsigned)id < ncol) {
+          if (!kfd[id]) continue;
+          if (row[id]++ == 0) pair_hit.push_back((int)(r * ncol) + id);
+        } else if (frame(id)) {
+          bad.push_back(key(std::max(f->id, id), std::min(f->id, id)));  // MakeFramePair
+        }
       }
       if (m->observers() < 2 && m->type != kBad) {
         bool del = true;
@@ -438,13 +454,22 @@ struct rspl_map {
       // frame->RemoveMappoint(mpt): GetKeypointIdx(frame id) is -1 by now -> no-op
     }
     // the reference's std::map<pair, int> of counts: pairs in ascending order, each with its count
-    std::sort(bad.begin(), bad.end());
-    for (size_t i = 0; i < bad.size();) {
+    std::vector<std::pair<uint64_t, int>> cnt;
+    cnt.reserve(pair_hit.size() + bad.size());
+    for (int h : pair_hit) {
+      const int f = rows[h / ncol], o = h % ncol;
+      cnt.push_back({key(std::max(f, o), std::min(f, o)), pair_cnt[h]});
+      pair_cnt[h] = 0;
+    }
+    for (uint64_t k : bad) cnt.push_back({k, 1});
+    std::sort(cnt.begin(), cnt.end(), [](const auto& x, const auto& y) { return x.first < y.first; });
+    for (size_t i = 0; i < cnt.size();) {
       size_t j = i;
-      while (j < bad.size() && bad[j] == bad[i]) j++;
-      const int n = (int)(j - i);
-      frame(bad[i].first)->decrease_weight(bad[i].second, n);
-      frame(bad[i].second)->decrease_weight(bad[i].first, n);
+      int n = 0;
+      for (; j < cnt.size() && cnt[j].first == cnt[i].first; j++) n += cnt[j].second;
+      const int a = (int)((uint32_t)(cnt[i].first >> 32) ^ 0x80000000u), b = (int)((uint32_t)cnt[i].first ^ 0x80000000u);
+      frame(a)->decrease_weight(b, n);
+      frame(b)->decrease_weight(a, n);
       i = j;
     }
   }
@@ -570,11 +595,27 @@ struct rspl_map {
       fixed_num += fix;
       add_vertex(poses, *k, fix);
     }
-    Counter fixed_frames(this);  // keyed by frame id (the reference: by FramePtr; only counted)
+    // frame classes: in the window (lmo), outside it, or outside it but marked lmo_fix by an earlier
+    // call for this frame id (counted as outside, yet in the window for the constraints, as the
+    // reference's two checks read it)
+    auto classify = [&](const MFrame* o) -> uint8_t {
+      return o->lmo == fid ? kWin : o->lmo_fix == fid ? kOutFix : kOut;
+    };
+    {
+      int top = -1;
+      for (int id : kf_ids)
+        if (id < kDenseIds) top = std::max(top, id);
+      fcls.assign((size_t)(top + 1), kNoFrame);
+      if (fcnt.size() < fcls.size()) fcnt.resize(fcls.size(), 0);
+      for (int id : kf_ids)
+        if (id >= 0 && id <= top) fcls[id] = classify(frame(id));
+    }
+    std::map<int, int> big_cnt;
     bool any_fixed = false;
     // the window's landmarks in the reference's order (frame by frame, slot by slot), each with its
-    // observers (frame, keypoint index) copied into one flat array, so the constraint pass below reads
-    // them sequentially instead of chasing every landmark's observer list a second time
+    // window observers (frame, keypoint index) copied into one flat array, so the constraint pass below
+    // reads them sequentially instead of chasing every landmark's observer list a second time; the
+    // other observers are only counted per frame (the fixed-frame choice, map.cc:588-602)
     lm_pts.clear();
     lm_beg.clear();
     lm_obs.clear();
@@ -593,13 +634,19 @@ struct rspl_map {
         lm_pts.push_back(m);
         lm_beg.push_back((int)lm_obs.size());
         for (auto& kv : m->obs) {
-          MFrame* o = frame(kv.first);
-          if (!o) continue;
-          lm_obs.push_back({o, kv.second});
-          if (o->lmo != fid) {
-            fixed_frames.add(o->id);
-            any_fixed = true;
+          const int id = kv.first;
+          uint8_t c;
+          if ((unsigned)id < fcls.size()) {
+            c = fcls[id];
+            if (c >= kOut) fcnt[id]++;
+          } else {
+            const MFrame* o = frame(id);
+            c = o ? classify(o) : kNoFrame;
+            if (c >= kOut) big_cnt[id]++;
           }
+          if (c == kNoFrame) continue;
+          any_fixed |= c >= kOut;
+          if (c != kOut) lm_obs.push_back({frame(id), kv.second});
         }
       }
       for (int lid : k->mpl) {
@@ -611,15 +658,27 @@ struct rspl_map {
     }
     lm_beg.push_back((int)lm_obs.size());
     const size_t max_fixed = 1;
-    std::set<std::pair<int, int>> ord;
-    fixed_frames.drain([&](int id, int w) { ord.insert({w, id}); });
-    if (any_fixed && max_fixed > fixed_num) {
-      size_t add = std::min(max_fixed - fixed_num, ord.size());
-      for (auto it = ord.rbegin(); add > 0; add--, ++it) {
-        MFrame* o = frame(it->second);
-        o->lmo_fix = fid;
-        add_vertex(poses, *o, true);
+    // the frame with the most observations, ties to the larger id (the reference's
+    // std::set<pair<int, FramePtr>> read from rbegin; max_fixed - fixed_num is at most 1)
+    int fx_id = -1, fx_w = 0;
+    auto consider = [&](int id, int w) {
+      if (w > fx_w || (w == fx_w && w > 0 && id > fx_id)) {
+        fx_id = id;
+        fx_w = w;
       }
+    };
+    for (int id : kf_ids)
+      if (id >= 0 && id < (int)fcls.size()) {
+        consider(id, fcnt[id]);
+        fcnt[id] = 0;
+      }
+    for (auto& kv : big_cnt) consider(kv.first, kv.second);
+    const MFrame* fx = nullptr;  // the fixed frame, when its observations are not in lm_obs yet
+    if (any_fixed && max_fixed > fixed_num) {
+      MFrame* o = frame(fx_id);
+      if (o->lmo_fix != fid) fx = o;
+      o->lmo_fix = fid;
+      add_vertex(poses, *o, true);
     }
     // dense poses: std::map ids in ascending order (LocalmapOptimization's vertex order); every
     // frame of the window (lmo or lmo_fix == fid) is a vertex and learns its index here
@@ -634,7 +693,8 @@ struct rspl_map {
     }
     mark();
     auto in_window = [&](const MFrame* o) { return o->lmo == fid || o->lmo_fix == fid; };
-    // constraints in the reference's order: landmark by landmark, observers by frame id, written
+    // constraints in the reference's order: landmark by landmark, observers by frame id (the fixed
+    // frame's observation, looked up in the landmark's observer map, merged into that order), written
     // straight into the dense arrays; a landmark that is dropped (no stereo and at most one mono
     // observation) has its rows taken back.  c_lm holds the kept landmark's ordinal until the
     // landmarks are numbered by id below.
@@ -646,16 +706,24 @@ struct rspl_map {
     for (size_t li = 0; li < lm_pts.size(); li++) {
       const size_t b0 = c_pose[0].size(), b1 = c_pose[1].size();
       const int ord_lm = (int)kept_pts.size();
-      for (int j = lm_beg[li]; j < lm_beg[li + 1]; j++) {
-        const MFrame* o = lm_obs[j].f;
-        const int kpi = lm_obs[j].kp;
-        if (!in_window(o) || kpi < 0 || kpi >= (int)o->kp.size()) continue;  // GetKeypointPosition
+      auto emit = [&](const MFrame* o, int kpi) {
+        if (kpi < 0 || kpi >= (int)o->kp.size()) return;  // GetKeypointPosition
         const double* k = o->kp[kpi].data();
         const int t = k[2] > 0 ? 1 : 0;
         c_pose[t].push_back(o->pidx);
         c_lm[t].push_back(ord_lm);
         c_obs[t].insert(c_obs[t].end(), k, k + 2 + t);
+      };
+      int fx_kp = fx ? lm_pts[li]->keypoint_idx(fx->id) : -1;
+      for (int j = lm_beg[li]; j < lm_beg[li + 1]; j++) {
+        const MFrame* o = lm_obs[j].f;
+        if (fx_kp >= 0 && o->id > fx->id) {
+          emit(fx, fx_kp);
+          fx_kp = -1;
+        }
+        emit(o, lm_obs[j].kp);
       }
+      if (fx_kp >= 0) emit(fx, fx_kp);
       if (c_pose[1].size() > b1 || c_pose[0].size() > b0 + 1) {
         kept_pts.push_back({lm_pts[li]->id, ord_lm});
         kept_ptr.push_back(lm_pts[li]);
@@ -844,6 +912,7 @@ struct rspl_map {
       memcpy(f->Twc, T, sizeof(T));
     }
     for (size_t i = 0; i < point_ids.size(); i++) {
+      if (i + 8 < point_ids.size()) __builtin_prefetch(point(point_ids[i + 8]), 1);
       MPoint* m = point(point_ids[i]);
       if (!m) continue;
       for (int k = 0; k < 3; k++) m->p[k] = rX[3 * i + k];
@@ -913,6 +982,7 @@ extern "C" int rspl_map_add_keyframe(rspl_map* m, const rspl_map_keyframe* k) {
   MFrame* fp = &m->kf.emplace(fid, std::move(f)).first->second;
   m->kf_ix.put(fid, fp);
   m->kf_ids.push_back(k->frame_id);
+  m->kf_sorted.insert(std::upper_bound(m->kf_sorted.begin(), m->kf_sorted.end(), fid), fid);
   return RSPL_OK;
 }
 

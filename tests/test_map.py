@@ -41,7 +41,7 @@ def _compare_state(m, mr, seq, upto):
             np.testing.assert_allclose(ep, l.endpoints, rtol=1e-12, atol=1e-12)
 
 
-@pytest.mark.parametrize("seed,n_kf,n_pts", [(3, 14, 1500), (11, 12, 900)])
+@pytest.mark.parametrize("seed,n_kf,n_pts", [(3, 14, 1500), (11, 12, 900), (21, 28, 2500)])
 def test_map_local_optimization_vs_oracle(seed, n_kf, n_pts):
     seq = SY.map_sequence(n_keyframes=n_kf, n_points=n_pts, n_lines=25, seed=seed, outlier_frac=0.06)
     m = pkg.mapping.Map(seq["camera"])
@@ -71,8 +71,20 @@ def test_map_local_optimization_vs_oracle(seed, n_kf, n_pts):
         removed += n_out
         _compare_state(m, mr, seq, k)
     assert removed > 0  # the outlier path was exercised
-    # window: at most 9 neighbours + 1 fixed frame once the map has more than 9 keyframes
-    assert rep["n_poses"] <= 10
+    # window: 9 frames (+ the parent when it is not among them) + 1 fixed frame
+    assert rep["n_poses"] <= 11
+    # the same frame id assembled again: the window / landmark markers of the first call still read
+    # as set (frames and landmarks already marked with this id), as in the reference
+    fid = seq["keyframes"][-1]["id"]
+    rep = m.Assemble(fid)
+    mr.assemble(fid)
+    d = mr.dense_problem()
+    got = m.LastProblem(rep)
+    for key in ("pose_ids", "pose_fixed", "point_ids", "line_ids"):
+        np.testing.assert_array_equal(got[key], d[key], err_msg=f"repeat {key}")
+    for kind in KINDS:
+        for a in ("pose", "lm", "obs"):
+            np.testing.assert_array_equal(got[kind][a], d[kind][a], err_msg=f"repeat {kind}.{a}")
 
 
 def test_map_window_rules():

@@ -12,7 +12,7 @@ import time
 
 import numpy as np
 
-ROOT = pathlib.Path(__file__).resolve().parents[1]
+ROOT = pathlib.Path(__file__).resolve().parents[2]
 sys.path.insert(0, str(ROOT))
 import rspl_loader  # noqa: E402
 
