@@ -15,6 +15,7 @@
 #include <type_traits>
 
 #include "ba_kernels.hpp"
+#include "ba_solve_reg.hpp"
 #include "se3_device.hpp"
 
 
@@ -2022,17 +2023,11 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
 
 
 // ---------------------------------------------------------------------------
-// The same blocked LDL^T with the trailing matrix in REGISTERS (K > kWaveSolveMaxK: C5's 30-keyframe
-// window, n = 174): schur_solve_kernel's trailing update re-reads and rewrites the whole packed triangle
-// in LDS every pose step (29 steps x ~15k entries: LDS-bandwidth bound, ~4 us per step).  Here each of
-// 512 threads owns one 6x6 pose block of the lower triangle (or the rhs row's 6 entries of a block column),
-// held in registers from the assembly to the step that factors its block column.  Pose step s: the owners of
-// block column s write it to LDS; barrier; every wave factors the 6x6 diagonal block (redundantly: no
-// broadcast) and each thread forms one panel row (X = A L^-T D^-1, into LDS as the factor's L, exactly as
-// schur_solve_kernel); barrier; every owner of a trailing block applies A_ik -= sum_l (X_il d_l) X_kl,
-// l ascending, from the panel in LDS: 72 panel reads per block and step (3x3 tiles needed 36 per 9
-// entries: the trailing update was LDS-bound).  The same operations in the same order per element as
-// schur_solve_kernel (bitwise the same factor); backward substitution, solution and LM scale as there.
+// 10 < K <= kRegMaxK (C5's 30-keyframe window, n = 174): rspl::ba::solve_reg (ba_solve_reg.hpp) -- the matrix as
+// fp64 MFMA accumulator tiles on SIMDs 1..3, the pivot chain alone on SIMD 0, look-ahead between the two, one
+// 768-thread workgroup.  (Replaced the round-5 block-per-thread register kernel: 108 -> 95 us per solve at K = 29 in
+// tools/experiments/solve_bench.hip, results within 1e-14 of it.)
+// ---------------------------------------------------------------------------
 // lane l's double, read by every lane (l uniform)
 __device__ __forceinline__ double readlane64(double v, int l) {
   const long long b = __double_as_longlong(v);
@@ -2041,230 +2036,27 @@ __device__ __forceinline__ double readlane64(double v, int l) {
   return __longlong_as_double((long long)(((unsigned long long)hi << 32) | lo));
 }
 
-constexpr int kRegThreads = 512;  // one pose block per thread: K (K + 3) / 2 <= 512 blocks, K <= 30 (n <= 180);
-                                  // larger windows take schur_solve_kernel (launch_lds_solve)
-constexpr int kRegMaxK = 30;
+constexpr int kRegMaxK = kSolveRegMaxK;
 
-__global__ __launch_bounds__(kRegThreads) void schur_reg_kernel(Problem P, Active A, Sys S, int n, double lambda) {
-  extern __shared__ double Al[];
-  __shared__ int bad;
-  if (S.lm) {
+struct BaSolveStamp {  // RSPL_BA_PROF slots of the solve (ba.cpp report_prof)
+  const Sys& S;
+  __device__ void at(int slot) const {
+    if (threadIdx.x == 0) prof_stamp(S, slot);
+  }
+  __device__ void step(int s, int) const {
+    if (threadIdx.x == 0 && s < 2) prof_stamp(S, 5 + 2 * s);
+  }
+  __device__ void wave(int, int) const {}
+};
+
+__global__ __launch_bounds__(kSolveRegThreads) void schur_reg_kernel(Problem P, Active A, Sys S, int n, double lambda) {
+  extern __shared__ double lds_sr[];
+  if (S.lm) {  // device-side LM: damping from the control
     LmView v;
     if (!lm_view(S, v)) return;
     lambda = v.lambda;
-    if (v.cur) bank_state(P);
   }
-  const int K = n / 6;
-  double* z = Al + pk(n, 0);
-  double* rdg = Al + pk(n + 1, 0);
-  double* ddg = rdg + n;
-  double* Ldg = ddg + n;
-  double* bpl = Ldg + 15 * K;
-  const int tid = threadIdx.x;
-  if (tid == 0) bad = 0;
-  const int pose_a = tid < P.np ? A.pidx[tid] : -1;
-  if (tid == 0) prof_stamp(S, 0);
-  // Assembly.  The pose-pair sums (pairfin, pair-major, 48 per pair) are read coalesced -- 512 consecutive
-  // doubles per load instruction, every load of a batch in flight at once -- and scattered into the packed
-  // LDS triangle: entry (r, cc) of pair (pa, pb) is (6 pb + cc, 6 pa + r) for pa < pb and (6 pa + r, 6 pa + cc),
-  // cc <= r, on a diagonal pair (+ lambda on the diagonal); the rhs row n is z = bp - sum Y bl of the diagonal
-  // pairs.  The same values as schur_solve_kernel's assembly.  Then each thread reads its tiles from LDS.  (A
-  // per-thread gather of the tiles from pairfin was uncoalesced: 16.6 us at n = 174.)
-  const int nent = A.npairs * 48;
-  int* ptab = reinterpret_cast<int*>(ddg);  // pair -> (a, b) during the assembly (ddg / Ldg are formed later)
-  double* ybl = rdg;                        // sum Y bl of each pose during the assembly
-  constexpr int kAsmBatch = 22;             // 2 batches x 22 x 512 >= 465 pairs x 48 (K <= 30)
-  static_assert(2 * kAsmBatch * kRegThreads >= kRegMaxK * (kRegMaxK + 1) / 2 * 48, "assembly batches");
-  {
-    double va[kAsmBatch];
-#pragma unroll
-    for (int u = 0; u < kAsmBatch; u++) va[u] = S.pairfin[min(tid + kRegThreads * u, nent - 1)];
-    for (int pr = tid; pr < A.npairs; pr += kRegThreads) {  // (while the first batch is in flight)
-      int a, b;
-      pair_of(pr, K, a, b);
-      ptab[2 * pr] = a;
-      ptab[2 * pr + 1] = b;
-    }
-    __syncthreads();
-    auto scatter = [&](int idx, double val) {
-      if (idx >= nent) return;
-      const int pr = idx / 48, v = idx - 48 * pr;
-      const int pa = ptab[2 * pr], pb = ptab[2 * pr + 1];
-      if (v < 36) {
-        const int r = v / 6, cc = v - 6 * r;
-        if (pa == pb) {
-          if (cc <= r) Al[pk(6 * pa + r, 6 * pa + cc)] = val + (r == cc ? lambda : 0.0);
-        } else {
-          Al[pk(6 * pb + cc, 6 * pa + r)] = val;
-        }
-      } else if (pa == pb) {
-        if (v < 42) bpl[6 * pa + v - 36] = val;
-        else ybl[6 * pa + v - 42] = val;
-      }
-    };
-#pragma unroll
-    for (int u = 0; u < kAsmBatch; u++) scatter(tid + kRegThreads * u, va[u]);
-#pragma unroll
-    for (int u = 0; u < kAsmBatch; u++) va[u] = S.pairfin[min(tid + kRegThreads * (u + kAsmBatch), nent - 1)];
-#pragma unroll
-    for (int u = 0; u < kAsmBatch; u++) scatter(tid + kRegThreads * (u + kAsmBatch), va[u]);
-  }
-  if (*S.fail) return;  // uniform: a landmark block failed to invert (its flag is out with the sums)
-  __syncthreads();
-  for (int i = tid; i < n; i += kRegThreads) z[i] = bpl[i] - ybl[i];
-  __syncthreads();
-  // this thread's pose block (column-major over the lower triangle's 6x6 blocks + the rhs row's block of each
-  // column: K - c + 1 per block column c), from LDS at clamped addresses; entries above the diagonal, and the
-  // rhs block's rows 1..5, are never stored
-  int br = -1, bc = -1;
-  {
-    int c = 0, base = 0;
-    while (c < K && tid >= base + (K - c + 1)) {
-      base += K - c + 1;
-      c++;
-    }
-    if (c < K) {
-      bc = c;
-      br = c + (tid - base);  // K: the rhs row
-    }
-  }
-  const bool own = bc >= 0;
-  auto row_of = [&](int a) { return br < K ? 6 * br + a : n; };  // (rhs block: row n for every a)
-  auto valid = [&](int a, int b) { return own && (br < K ? (br > bc || b <= a) : a == 0); };
-  double T[6][6];
-#pragma unroll
-  for (int a = 0; a < 6; a++)
-#pragma unroll
-    for (int b = 0; b < 6; b++) {
-      const bool ok = valid(a, b);
-      T[a][b] = Al[ok ? pk(row_of(a), 6 * bc + b) : 0];
-      T[a][b] = ok ? T[a][b] : 0.0;
-    }
-  if (tid == 0) prof_stamp(S, 1);
-  const int wv = tid >> 6, lane = tid & 63;
-  for (int s = 0; s < K; s++) {
-    const int c0 = 6 * s, r0 = c0 + 6;
-    // (a) the block column to LDS
-    if (bc == s)
-#pragma unroll
-      for (int a = 0; a < 6; a++)
-#pragma unroll
-        for (int b = 0; b < 6; b++)
-          if (valid(a, b)) Al[pk(row_of(a), c0 + b)] = T[a][b];
-    __syncthreads();
-    {  // (b) every wave factors the 6x6 diagonal block itself (uniform, no broadcast), one panel row per thread
-      double L6[15], d6[6], r6[6];
-      const bool ok = ldl6(Al, c0, L6, d6, r6);
-      if (tid == 0) {
-#pragma unroll
-        for (int q = 0; q < 15; q++) Ldg[15 * s + q] = L6[q];
-#pragma unroll
-        for (int k = 0; k < 6; k++) {
-          rdg[c0 + k] = r6[k];
-          ddg[c0 + k] = d6[k];
-        }
-        if (!ok) bad = 1;
-      }
-      for (int i = r0 + tid; i <= n; i += kRegThreads) {  // X = a L_dd^-T D^-1 (as schur_solve_kernel)
-        double* row = Al + pk(i, c0);
-        double w[6];
-#pragma unroll
-        for (int k = 0; k < 6; k++) w[k] = row[k];
-#pragma unroll
-        for (int k = 0, q = 0; k < 6; k++) {
-#pragma unroll
-          for (int l = 0; l < k; l++, q++) w[k] -= w[l] * L6[q];
-        }
-#pragma unroll
-        for (int k = 0; k < 6; k++) row[k] = w[k] * r6[k];
-      }
-    }
-    __syncthreads();
-    if (tid == 0 && s < 2) prof_stamp(S, 5 + 2 * s);
-    if (bad) {
-      if (tid == 0) atomicOr(S.fail, 1);
-      return;
-    }
-    // (c) the trailing block in registers: T_ab -= (X_il d_l) X_kl, l ascending per entry
-    if (own && bc > s) {
-#pragma unroll
-      for (int l = 0; l < 6; l++) {
-        const double dl = ddg[c0 + l];
-        double wi[6], xk[6];
-#pragma unroll
-        for (int a = 0; a < 6; a++) {
-          wi[a] = Al[pk(row_of(a), c0 + l)] * dl;
-          xk[a] = Al[pk(6 * bc + a, c0 + l)];
-        }
-#pragma unroll
-        for (int a = 0; a < 6; a++)
-#pragma unroll
-          for (int b = 0; b < 6; b++) T[a][b] -= wi[a] * xk[b];
-      }
-    }
-    if (tid == 0 && s < 2) prof_stamp(S, 6 + 2 * s);
-  }
-  __syncthreads();
-  if (wv != 0) return;
-  if (tid == 0) prof_stamp(S, 2);
-  // backward substitution L^T x = z in wave 0 with z in registers (row i: lane i % 64, slot i / 64, n <= 192):
-  // the 6x6 block solve of pose step s on readlane'd values (uniform), then each lane's rows i < 6s; the
-  // panel entries L[6s + l][i] and the block's L of step s - 1 are requested one step ahead, so the
-  // dependent chain per step is registers only (was: two LDS round trips per step, 13 us at n = 174).  The
-  // same operations per element, in the same order, as schur_solve_kernel's loop.
-  double zr[3];
-#pragma unroll
-  for (int j = 0; j < 3; j++) zr[j] = z[min(lane + 64 * j, n - 1)];  // (rows >= n: never read or stored)
-  double Ac[3][6], Lc[15];
-  auto fetch = [&](int st, double (&Ad)[3][6], double (&Ld)[15]) {
-    const int c0 = 6 * st;
-#pragma unroll
-    for (int j = 0; j < 3; j++)
-#pragma unroll
-      for (int l = 0; l < 6; l++) Ad[j][l] = Al[pk(c0 + l, min(lane + 64 * j, c0))];  // (i >= c0: not used)
-#pragma unroll
-    for (int q = 0; q < 15; q++) Ld[q] = Ldg[15 * st + q];
-  };
-  fetch(K - 1, Ac, Lc);
-  for (int st = K - 1; st >= 0; st--) {
-    const int c0 = 6 * st;
-    double xb[6];
-#pragma unroll
-    for (int k = 5; k >= 0; k--) {
-      const int i = c0 + k, sl = i >> 6;
-      double v = readlane64(sl == 0 ? zr[0] : sl == 1 ? zr[1] : zr[2], i & 63);
-#pragma unroll
-      for (int l = k + 1; l < 6; l++) v -= Lc[l * (l - 1) / 2 + k] * xb[l];
-      xb[k] = v;
-    }
-    // branch-free: every row formed, then selected (rows >= c0 + 6 keep theirs, rows c0 .. c0 + 5 take x)
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-      const int i = lane + 64 * j, d = i - c0;
-      double v = zr[j];
-#pragma unroll
-      for (int l = 0; l < 6; l++) v -= Ac[j][l] * xb[l];
-      double xs = xb[0];
-#pragma unroll
-      for (int l = 1; l < 6; l++) xs = d == l ? xb[l] : xs;
-      zr[j] = d < 0 ? v : (d < 6 ? xs : zr[j]);
-    }
-    if (st > 0) fetch(st - 1, Ac, Lc);  // the next step's panel entries and block L, behind this step's chain
-  }
-#pragma unroll
-  for (int j = 0; j < 3; j++)
-    if (lane + 64 * j < n) z[lane + 64 * j] = zr[j];
-  wave_sync();
-  for (int i = lane; i < n; i += 64) S.x[i] = z[i];
-  if (tid == 0) prof_stamp(S, 3);
-  double sc = 0;
-  if (lane < P.np && pose_a >= 0)
-#pragma unroll
-    for (int k = 0; k < 6; k++) sc += z[6 * pose_a + k] * (lambda * z[6 * pose_a + k] + bpl[6 * pose_a + k]);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
-  if (lane == 0) S.out[4] = sc;
-  if (tid == 0) prof_stamp(S, 4);
+  solve_reg(S.pairfin, n / 6, lambda, S.x, S.out + 4, S.fail, A.pidx, P.np, lds_sr, BaSolveStamp{S});
 }
 
 // ---------------------------------------------------------------------------
@@ -3433,7 +3225,7 @@ hipError_t ensure_schur_attr() {
                                      (int)schur_lds_bytes(kCholLdsMax));
   if (e == hipSuccess)
     e = hipFuncSetAttribute((const void*)schur_reg_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)schur_lds_bytes(kCholLdsMax));
+                            (int)solve_reg_lds_bytes(kRegMaxK));
   if (e == hipSuccess) attr = true;
   return e;
 }
@@ -3445,7 +3237,8 @@ static void launch_lds_solve(const Problem& P, const Active& A, const Sys& S, do
   if (A.K > kRegMaxK)
     hipLaunchKernelGGL(schur_solve_kernel, dim3(1), dim3(256), schur_lds_bytes(n), s, P, A, S, n, lambda);
   else
-    hipLaunchKernelGGL(schur_reg_kernel, dim3(1), dim3(kRegThreads), schur_lds_bytes(n), s, P, A, S, n, lambda);
+    hipLaunchKernelGGL(schur_reg_kernel, dim3(1), dim3(kSolveRegThreads), solve_reg_lds_bytes(A.K), s, P, A, S, n,
+                       lambda);
 }
 
 // pair_chunk grid: 8 XCD lanes x (landmark ranges per XCD) x pose pairs (idle slots exit)

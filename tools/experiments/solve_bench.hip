@@ -85,6 +85,9 @@ __device__ __forceinline__ void stamp(unsigned long long* st, int i) {
   if (st && threadIdx.x == 0) st[i] = __builtin_readcyclecounter();
 }
 
+__device__ __forceinline__ void wstamp(unsigned long long* st, int s, int k) {
+  if (st && (threadIdx.x & 63) == 0 && s < 30) st[256 + (s * 8 + (threadIdx.x >> 6)) * 5 + k] = __builtin_readcyclecounter();
+}
 __global__ __launch_bounds__(kRegThreads) void kernel(const double* pairfin, int K, double lambda, double* xo,
                                                      double* out, int* fail, unsigned long long* st) {
   extern __shared__ double Al[];
@@ -175,9 +178,11 @@ __global__ __launch_bounds__(kRegThreads) void kernel(const double* pairfin, int
           if (valid(a, b)) Al[pk(row_of(a), c0 + b)] = T[a][b];
     __syncthreads();
     stamp(st, 8 + 3 * s);
+    wstamp(st, s, 0);
     {
       double L6[15], d6[6], r6[6];
       const bool ok = ldl6(Al, c0, L6, d6, r6);
+      wstamp(st, s, 1);
       if (tid == 0) {
 #pragma unroll
         for (int q = 0; q < 15; q++) Ldg[15 * s + q] = L6[q];
@@ -202,8 +207,10 @@ __global__ __launch_bounds__(kRegThreads) void kernel(const double* pairfin, int
         for (int k = 0; k < 6; k++) row[k] = w[k] * r6[k];
       }
     }
+    wstamp(st, s, 2);
     __syncthreads();
     stamp(st, 9 + 3 * s);
+    wstamp(st, s, 3);
     if (bad) {
       if (tid == 0) atomicOr(fail, 1);
       return;
@@ -225,6 +232,7 @@ __global__ __launch_bounds__(kRegThreads) void kernel(const double* pairfin, int
       }
     }
     stamp(st, 10 + 3 * s);
+    wstamp(st, s, 4);
   }
   __syncthreads();
   if (wv != 0) return;
@@ -290,17 +298,120 @@ size_t lds_bytes(int n) {
 struct CycleStamp {
   unsigned long long* st;
   __device__ void at(int i) const {
-    if (st && threadIdx.x == 64 * kSrBulkWaves) st[i] = __builtin_readcyclecounter();
+    if (st && threadIdx.x == 0) st[i] = __builtin_readcyclecounter();
   }
   __device__ void step(int s, int ph) const {
-    if (st && threadIdx.x == 64 * kSrBulkWaves) st[8 + 3 * s + ph] = __builtin_readcyclecounter();
+    if (st && threadIdx.x == 0) st[8 + 3 * s + ph] = __builtin_readcyclecounter();
+  }
+  __device__ void wave(int s, int k) const {
+    if (st && (threadIdx.x & 63) == 0 && s < 30) st[1024 + (s * 16 + (threadIdx.x >> 6)) * 4 + k] = __builtin_readcyclecounter();
   }
 };
 __device__ int g_pidx[64];
+template <int kAb>
+__global__ __launch_bounds__(kSolveRegThreads) void vab_kernel(const double* pairfin, int K, double lambda, double* x,
+                                                              double* out, int* fail, unsigned long long* st) {
+  extern __shared__ double lds[];
+  if (kAb == 3 && st) {  // clock probe: a 1024-long dependent fp64 FMA chain on wave 0 inside this kernel's context
+    double a = lambda + threadIdx.x;
+    const unsigned long long t0 = __builtin_readcyclecounter();
+#pragma unroll 16
+    for (int i = 0; i < 1024; i++) a = fma(a, 1.0000001, 1e-9);
+    const unsigned long long t1 = __builtin_readcyclecounter();
+    if (threadIdx.x == 0) st[2000] = t1 - t0;
+    if (a == 12345.0) x[0] = a;
+  }
+  solve_reg<NoStamp, kAb>(pairfin, K, lambda, x, out, fail, g_pidx, K, lds, NoStamp{});
+}
 __global__ __launch_bounds__(kSolveRegThreads) void v1_kernel(const double* pairfin, int K, double lambda, double* x,
                                                              double* out, int* fail, unsigned long long* st) {
   extern __shared__ double lds[];
   solve_reg(pairfin, K, lambda, x, out, fail, g_pidx, K, lds, CycleStamp{st});
+}
+
+// the pivot phase alone (one wave, no other work): ldl6 of a fixed SPD block from LDS + three panel rows per lane,
+// repeated; cycles per repetition
+__global__ void piv_kernel(double* out, unsigned long long* cyc, int nrows) {
+  __shared__ double Col[6 * 192];
+  __shared__ double Pn[6 * 192];
+  __shared__ double Lg[64];
+  const int lane = threadIdx.x;
+  for (int i = lane; i < 6 * 192; i += 64) Col[i] = (i % 7 == 0) ? 4.0 + (i % 5) : 0.1 * ((i * 37) % 11) / 11.0;
+  __syncthreads();
+  double acc = 0.0;
+  const unsigned long long t0 = __builtin_readcyclecounter();
+  for (int rep = 0; rep < 64; rep++) {
+    double a[6][6], L6[15], d6[6], r6[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++)
+#pragma unroll
+      for (int k = 0; k <= i; k++) a[i][k] = Col[6 * i + k] + (i == k ? acc * 1e-30 : 0.0);
+    double w[3][6];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const int row = 6 + lane + 64 * j;
+      if (row < nrows) sr_ld6(Col + 6 * row, w[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < 6; j++) {
+      const double d = a[j][j];
+      const double r = sr_rcp64(d);
+      d6[j] = d;
+      r6[j] = r;
+      double u[6];
+#pragma unroll
+      for (int i = j + 1; i < 6; i++) u[i] = a[i][j];
+#pragma unroll
+      for (int i = j + 1; i < 6; i++) {
+        const double l = u[i] * r;
+        a[i][j] = l;
+#pragma unroll
+        for (int k = j + 1; k <= i; k++) a[i][k] -= l * u[k];
+      }
+    }
+#pragma unroll
+    for (int i = 0, q = 0; i < 6; i++)
+#pragma unroll
+      for (int k = 0; k < i; k++, q++) L6[q] = a[i][k];
+    if (lane == 0)
+#pragma unroll
+      for (int q = 0; q < 15; q++) Lg[q] = L6[q];
+#pragma unroll
+    for (int j = 0; j < 3; j++) {
+      const int row = 6 + lane + 64 * j;
+      if (row < nrows) {
+#pragma unroll
+        for (int k = 0, q = 0; k < 6; k++)
+#pragma unroll
+          for (int l = 0; l < k; l++, q++) w[j][k] -= w[j][l] * L6[q];
+#pragma unroll
+        for (int k = 0; k < 6; k++) {
+          const double xv = w[j][k] * r6[k];
+          Pn[k * 192 + row] = xv;
+          acc += xv * d6[k];
+        }
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  }
+  const unsigned long long t1 = __builtin_readcyclecounter();
+  if (lane == 0) cyc[0] = t1 - t0;
+  out[lane] = acc;
+}
+
+// the backward substitution alone (1024 threads, synthetic panels): cycles per pose step
+__global__ __launch_bounds__(kSolveRegThreads) void bs_kernel(double* out, unsigned long long* cyc, int K) {
+  extern __shared__ double lds[];
+  const SolveRegLayout Ly(K);
+  for (int i = threadIdx.x; i < Ly.total; i += blockDim.x) lds[i] = 1e-3 * ((i * 37) % 101);
+  __syncthreads();
+  const unsigned long long t0 = __builtin_readcyclecounter();
+  if (threadIdx.x < 64) sr_backsub(lds, lds + Ly.ld, lds + Ly.xs, K);
+  const unsigned long long t1 = __builtin_readcyclecounter();
+  if (threadIdx.x == 0) cyc[0] = t1 - t0;
+  if (threadIdx.x < 64) out[threadIdx.x] = lds[Ly.xs + threadIdx.x];
 }
 
 static int pair_index_h(int c, int a, int K) { return c * K - c * (c - 1) / 2 + (a - c); }
@@ -370,7 +481,7 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&d_x, 256 * sizeof(double)));
   CK(hipMalloc(&d_out, 8 * sizeof(double)));
   CK(hipMalloc(&d_fail, sizeof(int)));
-  CK(hipMalloc(&d_st, 1024 * sizeof(unsigned long long)));
+  CK(hipMalloc(&d_st, 4096 * sizeof(unsigned long long)));
   CK(hipMemcpy(d_pf, pf.data(), pf.size() * sizeof(double), hipMemcpyHostToDevice));
   CK(hipMemset(d_fail, 0, sizeof(int)));
   {
@@ -381,7 +492,57 @@ int main(int argc, char** argv) {
   const size_t l0 = v0::lds_bytes(n), l1 = solve_reg_lds_bytes(K);
   CK(hipFuncSetAttribute((const void*)v0::kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l0));
   CK(hipFuncSetAttribute((const void*)v1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1));
+  {
+    CK(hipFuncSetAttribute((const void*)bs_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
+    hipLaunchKernelGGL(bs_kernel, dim3(1), dim3(kSolveRegThreads), solve_reg_lds_bytes(K), 0, d_x, d_st, K);
+    CK(hipDeviceSynchronize());
+    unsigned long long c;
+    CK(hipMemcpy(&c, d_st, sizeof(c), hipMemcpyDeviceToHost));
+    printf("backward substitution alone: %.0f cycles (%.0f per pose step)\n", (double)c, (double)c / K);
+  }
+  for (int nr : {6, 70, 175}) {
+    hipLaunchKernelGGL(piv_kernel, dim3(1), dim3(64), 0, 0, d_x, d_st, nr);
+    CK(hipDeviceSynchronize());
+    unsigned long long c;
+    CK(hipMemcpy(&c, d_st, sizeof(c), hipMemcpyDeviceToHost));
+    printf("pivot phase alone (one wave, %d rows): %.0f cycles per step\n", nr - 6, (double)c / 64);
+  }
   hipEvent_t e0, e1;
+  {
+    CK(hipFuncSetAttribute((const void*)vab_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
+    CK(hipFuncSetAttribute((const void*)vab_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
+    CK(hipFuncSetAttribute((const void*)vab_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
+    CK(hipFuncSetAttribute((const void*)vab_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
+    hipEvent_t a0, a1;
+    CK(hipEventCreate(&a0));
+    CK(hipEventCreate(&a1));
+    for (int ab = 0; ab < 4; ab++) {
+      auto L = [&]() {
+        const size_t lb = solve_reg_lds_bytes(K);
+        if (ab == 0) hipLaunchKernelGGL(vab_kernel<0>, dim3(1), dim3(kSolveRegThreads), lb, 0, d_pf, K, lambda, d_x, d_out, d_fail, nullptr);
+        if (ab == 1) hipLaunchKernelGGL(vab_kernel<1>, dim3(1), dim3(kSolveRegThreads), lb, 0, d_pf, K, lambda, d_x, d_out, d_fail, nullptr);
+        if (ab == 2) hipLaunchKernelGGL(vab_kernel<2>, dim3(1), dim3(kSolveRegThreads), lb, 0, d_pf, K, lambda, d_x, d_out, d_fail, nullptr);
+        if (ab == 3) hipLaunchKernelGGL(vab_kernel<3>, dim3(1), dim3(kSolveRegThreads), lb, 0, d_pf, K, lambda, d_x, d_out, d_fail, nullptr);
+      };
+      for (int i = 0; i < 3; i++) L();
+      CK(hipEventRecord(a0));
+      for (int i = 0; i < reps; i++) L();
+      CK(hipEventRecord(a1));
+      CK(hipEventSynchronize(a1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, a0, a1));
+      CK(hipMemset(d_fail, 0, sizeof(int)));
+      if (ab == 3) {
+        hipLaunchKernelGGL(vab_kernel<3>, dim3(1), dim3(kSolveRegThreads), solve_reg_lds_bytes(K), 0, d_pf, K, lambda, d_x, d_out, d_fail, d_st);
+        CK(hipDeviceSynchronize());
+        unsigned long long c;
+        CK(hipMemcpy(&c, d_st + 2000, sizeof(c), hipMemcpyDeviceToHost));
+        printf("clock probe in the solver's context: %.2f ticks per dependent fp64 FMA (lat_bench: 6.5-7.5)\n", c / 1024.0);
+      }
+      printf("ablation %d (%s): %.2f us per solve\n", ab,
+             ab == 0 ? "full" : ab == 1 ? "no trailing MFMA" : ab == 2 ? "no pivot arithmetic" : "neither", 1e3 * ms / reps);
+    }
+  }
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   std::vector<double> x0;
@@ -394,17 +555,17 @@ int main(int argc, char** argv) {
     };
     CK(hipMemset(d_x, 0, 256 * sizeof(double)));
     CK(hipMemset(d_fail, 0, sizeof(int)));
-    CK(hipMemset(d_st, 0, 1024 * sizeof(unsigned long long)));
+    CK(hipMemset(d_st, 0, 4096 * sizeof(unsigned long long)));
     launch(d_st);
     CK(hipDeviceSynchronize());
     std::vector<double> x(n);
     double sc;
     int fl;
-    std::vector<unsigned long long> st(1024);
+    std::vector<unsigned long long> st(4096);
     CK(hipMemcpy(x.data(), d_x, n * sizeof(double), hipMemcpyDeviceToHost));
     CK(hipMemcpy(&sc, d_out, sizeof(double), hipMemcpyDeviceToHost));
     CK(hipMemcpy(&fl, d_fail, sizeof(int), hipMemcpyDeviceToHost));
-    CK(hipMemcpy(st.data(), d_st, 1024 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+    CK(hipMemcpy(st.data(), d_st, 4096 * sizeof(unsigned long long), hipMemcpyDeviceToHost));
     double err = 0, xm = 0;
     for (int i = 0; i < n; i++) {
       err = fmax(err, fabs((double)(x[i] - xr[i])));
@@ -437,6 +598,30 @@ int main(int argc, char** argv) {
       }
       printf("\n");
     }
+    if (v == 1)
+      for (int s : {0, 1, 5, 10, 20}) {
+        if (s >= K) continue;
+        printf("  v3 step %d: pivot waves [bar A -> ldl6 | -> panel | -> bar B], tile waves [extract+bars | MFMA issue]:", s);
+        for (int w = 0; w < 16; w++) {
+          const unsigned long long* q = st.data() + 1024 + (s * 16 + w) * 4;
+          if (!q[0]) continue;
+          if (w < 3) printf(" w%d[%lld|%lld|%lld]", w, (long long)(q[1] - q[0]), (long long)(q[2] - q[1]), (long long)(q[3] - q[2]));
+          else printf(" w%d[%lld|%lld]", w, (long long)(q[1] - q[0]), (long long)(q[2] - q[1]));
+        }
+        printf("\n");
+      }
+    if (v == 0)
+      for (int s : {0, 1, 5, 10, 20}) {
+        if (s >= K) continue;
+        printf("  v0 step %d per wave [bar1->ldl6 | ->panel done | ->bar2 | ->trail done]:", s);
+        for (int w = 0; w < 8; w++) {
+          const unsigned long long* q = st.data() + 256 + (s * 8 + w) * 5;
+          if (!q[0]) continue;
+          printf(" w%d[%lld|%lld|%lld|%lld]", w, (long long)(q[1] - q[0]), (long long)(q[2] - q[1]),
+                 (long long)(q[3] - q[2]), q[4] ? (long long)(q[4] - q[3]) : -1LL);
+        }
+        printf("\n");
+      }
   }
   return 0;
 }
