@@ -186,6 +186,32 @@ __global__ void mix_kernel(double* out, unsigned long long* cyc, int mode, doubl
     for (int i = 0; i < kN; i++) a = fma(a, 1.0000001, 1e-9);
     const unsigned long long t1 = now();
     if (threadIdx.x == 0) cyc[0] = t1 - t0;
+  } else if (mode == 3 && (w & 3) == 0) {  // fp16 MFMA stream (the front end's convolutions / GNN)
+    typedef _Float16 half8 __attribute__((ext_vector_type(8)));
+    typedef float floatx16 __attribute__((ext_vector_type(16)));
+    half8 x;
+#pragma unroll
+    for (int i = 0; i < 8; i++) x[i] = (_Float16)(a * 1e-3);
+    floatx16 acc[4];
+#pragma unroll
+    for (int i = 0; i < 4; i++)
+#pragma unroll
+      for (int j = 0; j < 16; j++) acc[i][j] = 0.f;
+#pragma unroll 4
+    for (int it = 0; it < 1024; it++)
+#pragma unroll
+      for (int i = 0; i < 4; i++) acc[i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(x, x, acc[i], 0, 0, 0);
+    a = acc[0][0] + acc[1][1] + acc[2][2] + acc[3][3];
+  } else if (mode == 4 && (w & 3) == 0) {  // fp32 VALU stream
+    float x0 = a, x1 = a + 1, x2 = a + 2, x3 = a + 3;
+#pragma unroll 16
+    for (int it = 0; it < 8 * kN; it++) {
+      x0 = fmaf(x0, 1.0001f, 1e-9f);
+      x1 = fmaf(x1, 1.0001f, 1e-9f);
+      x2 = fmaf(x2, 1.0001f, 1e-9f);
+      x3 = fmaf(x3, 1.0001f, 1e-9f);
+    }
+    a = x0 + x1 + x2 + x3;
   } else if ((mode == 1 && (w & 3) == 0) || (mode == 2 && w < 4)) {
     double4_t acc[4];
 #pragma unroll
@@ -273,11 +299,12 @@ int main() {
     hipLaunchKernelGGL(mres_kernel, dim3(1), dim3(64), 0, 0, d_out, d_c, 1.0);
     get();
     printf("LDS load -> 2 dependent fp64 MFMAs -> VALU read -> LDS store: %.1f ticks per round\n", (double)c[0] / 256);
-    for (int mode : {0, 1, 2}) {
+    for (int mode : {0, 1, 2, 3, 4}) {
       hipLaunchKernelGGL(mix_kernel, dim3(1), dim3(1024), 0, 0, d_out, d_c, mode, 1.0);
       get();
       printf("fp64 FMA chain with %s: %.1f ticks per FMA\n",
-             mode == 0 ? "idle waves" : mode == 1 ? "3 MFMA-streaming waves on its SIMD" : "MFMA waves on the other SIMDs",
+             mode == 0 ? "idle waves" : mode == 1 ? "3 fp64-MFMA-streaming waves on its SIMD" : mode == 2 ? "fp64 MFMA waves on the other SIMDs"
+             : mode == 3 ? "3 fp16-MFMA (32x32x16) streaming waves on its SIMD" : "3 fp32-VALU streaming waves on its SIMD",
              (double)c[0] / kN);
     }
     for (int th : {64, 256, 512}) {
