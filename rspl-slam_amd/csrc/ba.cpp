@@ -57,10 +57,12 @@ struct rspl_ba {
   unsigned* lm_ctr;  // [max_lines] line-landmark tickets (zeroed at create, re-armed by the kernel)
   unsigned long long* prof = nullptr;  // RSPL_BA_PROF: timing trace of one trial per call
   int prof_nb[5] = {0, 0, 0, 0, 0};    // its pair_chunk / update_errors grid sizes, group blocks, nchk, K
+  rspl::ba::Active prof_A{};           // the traced trial's chunk geometry (chunk_geo)
   // landmark CSR (filled on the device) and the Schur chunk / pose-pair sums
   double *chunk, *pairfin;
   unsigned* pair_ctr;  // [npairs] chunk tickets (zeroed at create, re-armed by the kernel)
   int *pp_cnt, *pp_off;  // [npairs * nchk (+1)] edge pairs per Schur chunk, segment offsets
+  size_t chunk_slots = 0;  // Schur chunks the buffers hold (capacity pose pairs x landmark ranges)
   int4* pp_buf = nullptr;  // edge-pair list {e1, e2, landmark, 0}, growable
   size_t pp_cap = 0;      // capacity in pairs
   // per-call inputs (cameras, T / X / L, edges, reduced pose ids, landmark offsets, pose pairs,
@@ -266,6 +268,7 @@ void carve(F& ar, rspl_ba* b) {
   take(b->red, 6 * K + kMaxRanks + 8);
   take(b->lmctl, 2);
   take(b->pp_cnt, npairs * nchk); take(b->pp_off, npairs * nchk + 1);
+  b->chunk_slots = npairs * nchk;
 }
 
 // Staging slots are allocated at create for the handle's capacities (stage_bytes), so in use this never
@@ -399,7 +402,7 @@ void report_prof(rspl_ba* b) {
     for (int c = 0; c < std::min(npc, 4096) && nchk > 0; c++) {
       const unsigned long long t0 = h[ba::kProfPc + 4 * c], t1 = h[ba::kProfPc + 4 * c + 1];
       if (!t0 || !t1) continue;
-      int pr = c / nchk, a = 0, base = 0;
+      int pr = ba::chunk_geo(b->prof_A, c).pr, a = 0, base = 0;
       while (pr >= base + (K - a)) base += K - a++;
       ((pr - base == 0) ? dg : od).push_back(((double)t1 - (double)t0) / 100.0);
     }
@@ -531,7 +534,8 @@ int optimize_dev(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::
       const bool traced = b->prof && queued == 3 && !b->prof_nb[0];
       if (traced) {
         S.prof = b->prof;
-        b->prof_nb[0] = A.npairs * A.nchk;
+        b->prof_nb[0] = ba::chunk_count(A);
+        b->prof_A = A;
         b->prof_nb[1] = ba::update_errors_blocks(A) + A.n_lblk;
         b->prof_nb[2] = ba::update_errors_blocks(A);
         b->prof_nb[3] = A.nchk;
@@ -718,7 +722,9 @@ int optimize(rspl_ba* b, ba::Problem& P, ba::Lin& Lr, ba::Sys& S, const ba::Acti
         const bool traced = b->prof && it == 3 && qmax == 0 && !b->prof_nb[0];
         if (traced) {
           S.prof = sp.Ss.prof = b->prof;
-          b->prof_nb[0] = A.npairs * A.nchk;
+          b->prof_nb[0] = ba::chunk_count(A);
+          b->prof_A = A;
+        b->prof_A = A;
           b->prof_nb[1] = ba::update_errors_blocks(A) + A.n_lblk;
           b->prof_nb[2] = ba::update_errors_blocks(A);
         }
@@ -1385,6 +1391,17 @@ int run_call(rspl_ba* b, const ba::StagedCall& c, const rspl_ba_problem* pr, rsp
     A.nchk = std::max(1, std::min((nL + ba::kLmChunk - 1) / ba::kLmChunk, kChunkWaves / npairs));
     A.lmchunk = std::max(ba::kLmChunk, ((nL + A.nchk - 1) / A.nchk + 63) / 64 * 64);
     A.nchk = std::max((nL + A.lmchunk - 1) / A.lmchunk, 1);
+    // wide windows (K > the single-wave solve's, fewer than 8 ranges per pair): a diagonal pose pair walks about
+    // (K - 1) / (obs - 1) times an off-diagonal pair's edge pairs (C5: ~970 vs ~170 per range) and set the chunk
+    // phase alone -- its ranges are cut into kDiagSub sub-chunks (the off-diagonal pairs keep theirs)
+    constexpr int kDiagSub = 8;
+    A.dsub = 1;
+    A.lmsub = A.lmchunk;
+    A.K = K;
+    if (!ba::wave_path(K) && A.nchk < 8 && (size_t)A.nchk * (A.npairs + (kDiagSub - 1) * K) <= b->chunk_slots) {
+      A.dsub = kDiagSub;
+      A.lmsub = ((A.lmchunk + kDiagSub - 1) / kDiagSub + 63) / 64 * 64;
+    }
     ba::set_update_geometry(A);
   }
   A.n_line_edges = n_line_local;

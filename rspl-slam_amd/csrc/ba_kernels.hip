@@ -1450,18 +1450,19 @@ __device__ __forceinline__ void pose_diag_lds(const Active& A, const double (*pd
 template <bool FILL>
 __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, const int* pp_off, int4* pp) {
   const int lane = threadIdx.x & 63;
-  const int pr = c / A.nchk, lb = c - pr * A.nchk;
+  const ChunkGeo cg = chunk_geo(A, c);
+  const int pr = cg.pr;
   const int pa = A.pairs[2 * pr], pb = A.pairs[2 * pr + 1];
   int base = FILL ? pp_off[c] : 0;
-  const int nr = A.lmchunk / 64;
+  const int nr = (cg.g1 - cg.g0 + 63) / 64;
   // four landmark rounds at a time: their CSR ranges, then the first eight edge poses of each (a landmark's
   // whole edge list when it has <= 8 edges, the common case), every load of a group in flight at once
   for (int r0 = 0; r0 < nr; r0 += 4) {
     int k0[4], k1[4], pz[4][8];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const int g = lb * A.lmchunk + 64 * (r0 + u) + lane;
-      const bool in = r0 + u < nr && g < A.nL;
+      const int g = cg.g0 + 64 * (r0 + u) + lane;
+      const bool in = r0 + u < nr && g < cg.g1;
       const int o0 = in ? A.lm_off[g] : 0, o1 = in ? A.lm_off[g + 1] : 0;
       const bool act = in && A.lm_act[g];
       k0[u] = act ? o0 : 0;
@@ -1474,7 +1475,7 @@ __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, c
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       if (r0 + u >= nr) break;  // uniform
-      const int g = lb * A.lmchunk + 64 * (r0 + u) + lane;
+      const int g = cg.g0 + 64 * (r0 + u) + lane;
       const int e0 = k0[u], e1 = k1[u];
       int cnt = 0;
       unsigned ma1 = 0, mb1 = 0;  // the masks when the landmark has <= 8 edges (one block each)
@@ -1669,7 +1670,7 @@ __global__ __launch_bounds__(256) void setup_kernel(Problem P, Lin L, Active A, 
   if (b == 0 && threadIdx.x == 0) prof_stamp(S, 9);
   if (b >= nb_lm) {  // the first optimize: edge pairs per Schur chunk, one wave per chunk
     const int c = (b - nb_lm) * 4 + (threadIdx.x >> 6);
-    if (c < A.npairs * A.nchk) pair_scan<false>(A, c, pp_cnt, nullptr, nullptr);
+    if (c < chunk_count(A)) pair_scan<false>(A, c, pp_cnt, nullptr, nullptr);
     if (threadIdx.x == 0) prof_max(S, kProfX + 4);
   } else if (b >= nbq) {
     double c = 0.0;  // set in thread 0
@@ -1710,7 +1711,7 @@ __global__ __launch_bounds__(256) void setup_kernel(Problem P, Lin L, Active A, 
   const double chi2 = red[0];
   if (pp_cnt) {  // exclusive scan of the chunks' edge-pair counts -> pp_off
     __shared__ int sc[256];
-    const int tid = threadIdx.x, nc = A.npairs * A.nchk;
+    const int tid = threadIdx.x, nc = chunk_count(A);
     const int per = (nc + 255) / 256, b0 = min(tid * per, nc), b1 = min(b0 + per, nc);
     int sm = 0;
     for (int i = b0; i < b1; i++) sm += __hip_atomic_load(pp_cnt + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -2410,21 +2411,27 @@ __device__ __forceinline__ void chunk_loop(const Problem& P, const Lin& L, const
 // ranges' records (~1/8 of them), which its ~k_g pose pairs per landmark re-read.
 struct ChunkSeg {
   int c, lb, beg, end;
-  int4 q0;  // the lane's first pair
+  int pr, c0, c1;  // its pose pair and that pair's chunks
+  bool pts;        // a range of point landmarks only
+  int4 q0;         // the lane's first pair
 };
-__device__ __forceinline__ bool chunk_seg(const Active& A, int vb, ChunkSeg& cs) {
+__device__ __forceinline__ bool chunk_seg(const Active& A, int nq, int vb, ChunkSeg& cs) {
   const int lane = threadIdx.x & 63;
-  int pr0;
   if (A.nchk >= 8) {
     const int xcd = vb & 7, slot = vb >> 3, rpx = (A.nchk + 7) >> 3;
-    cs.lb = (slot % rpx) * 8 + xcd;
-    pr0 = slot / rpx;
+    const int lb = (slot % rpx) * 8 + xcd, pr0 = slot / rpx;
+    if (lb >= A.nchk || pr0 >= A.npairs) return false;
+    cs.c = pr0 * A.nchk + lb;
   } else {  // fewer ranges than XCDs (many pose pairs, wide chunks): plain order, every XCD busy
-    pr0 = vb / A.nchk;
-    cs.lb = vb - pr0 * A.nchk;
+    if (vb >= chunk_count(A)) return false;
+    cs.c = vb;
   }
-  if (cs.lb >= A.nchk || pr0 >= A.npairs) return false;
-  cs.c = pr0 * A.nchk + cs.lb;
+  const ChunkGeo cg = chunk_geo(A, cs.c);
+  cs.lb = cg.lb;
+  cs.pr = cg.pr;
+  cs.c0 = cg.c0;
+  cs.c1 = cg.c1;
+  cs.pts = cg.gend <= nq;
   cs.beg = A.pp_off[cs.c];
   cs.end = A.pp_off[cs.c + 1];
   cs.q0 = cs.beg + lane < cs.end ? A.pp[cs.beg + lane] : make_int4(0, 0, 0, 0);
@@ -2434,15 +2441,15 @@ __device__ __forceinline__ bool chunk_seg(const Active& A, int vb, ChunkSeg& cs)
 __device__ __forceinline__ bool chunk_wave(const Problem& P, const Lin& L, const Active& A, const Sys& S,
                                            double lambda, const ChunkSeg& cs, double* red, bool wt) {
   const int lane = threadIdx.x & 63;
-  const int c = cs.c, lb = cs.lb, beg = cs.beg, end = cs.end;
+  const int c = cs.c, beg = cs.beg, end = cs.end;
   if (lane == 0 && c < 4096) prof_stamp(S, kProfPc + 4 * c);
-  const int pr = c / A.nchk;
+  const int pr = cs.pr;
   double acc[48];
 #pragma unroll
   for (int v = 0; v < 48; v++) acc[v] = 0.0;
   // a range of point landmarks only
   // (all but the last range or two) takes the 3-dim loops, off-diagonal pose pairs without the e1 == e2 terms
-  const bool pts = (lb + 1) * A.lmchunk <= P.nq;
+  const bool pts = cs.pts;
   const int pa = A.pairs[2 * pr];
   const bool dpp = pa == A.pairs[2 * pr + 1];
   DiagPose dp;
@@ -2481,7 +2488,7 @@ __device__ __forceinline__ bool chunk_wave(const Problem& P, const Lin& L, const
     __hip_atomic_store(S.chunk + 48 * c + lane, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  const int c0 = pr * A.nchk, c1 = c0 + A.nchk;
+  const int c0 = cs.c0, c1 = cs.c1;
   unsigned tk = 0;
   if (lane == 0) tk = __hip_atomic_fetch_add(S.pair_ctr + pr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   tk = __shfl(tk, 0);
@@ -2530,7 +2537,7 @@ __global__ __launch_bounds__(64) void pair_chunk_kernel(Problem P, Lin L, Active
   constexpr int kRedLen = 64 * 49, kSolveLen = (int)(sizeof(WaveSolveLds) / sizeof(double));
   __shared__ double smem[N > 0 && kSolveLen > kRedLen ? kSolveLen : kRedLen];
   ChunkSeg cs;
-  if (!chunk_seg(A, blockIdx.x, cs)) return;  // in flight while the control is read
+  if (!chunk_seg(A, P.nq, blockIdx.x, cs)) return;  // in flight while the control is read
   if (S.lm) {  // device-side LM: damping and bank from the control
     LmView v;
     if (!lm_view(S, v)) return;
@@ -3199,7 +3206,7 @@ hipError_t setup_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, ui
   if (!S.lm || lm_iters <= 0) return hipErrorInvalidValue;
   Active A0 = A;
   A0.elevel = nullptr;  // the levels are written by this launch (level != null), never read by it
-  const int nc = A.npairs * A.nchk;
+  const int nc = chunk_count(A);
   if (nc == 0) pp_cnt = nullptr;
   const int nbq = A.nL > 0 ? (A.nL * kGroup + 255) / 256 : 0, nb = nbq + A.n_lblk;
   const int nbp = pp_cnt ? (nc + 3) / 4 : 0;
@@ -3243,7 +3250,7 @@ static void launch_lds_solve(const Problem& P, const Active& A, const Sys& S, do
 
 // pair_chunk grid: 8 XCD lanes x (landmark ranges per XCD) x pose pairs (idle slots exit)
 static int pair_chunk_blocks(const Active& A) {
-  return A.nchk >= 8 ? 8 * ((A.nchk + 7) / 8) * A.npairs : A.nchk * A.npairs;
+  return A.nchk >= 8 ? 8 * ((A.nchk + 7) / 8) * A.npairs : chunk_count(A);
 }
 
 // Schur chunks; with fused = true (wave path) the last pose pair also solves (solve_wave<6K>)
@@ -3275,7 +3282,7 @@ hipError_t trial(const Problem& P, const Lin& L, const Active& A, Sys& S, double
                  hipStream_t s, const Spec* spec, bool* fused) {
   *fused = false;
   const bool wave = wave_path(A.K);
-  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, lambda, L, S, wave, s);
+  if (chunk_count(A) > 0) launch_chunks(P, L, A, S, lambda, L, S, wave, s);
   const int n = 6 * A.K;
   if (fast_path(A.K)) {
     if (!wave) {
@@ -3311,7 +3318,7 @@ hipError_t trial_dev(const Problem& P, const Lin& L, const Active& A, Sys& S, un
   if (!S.lm || !fast_path(A.K)) return hipErrorInvalidValue;
   const bool wave = wave_path(A.K);
   if (ev) (void)hipEventRecord(ev[0], s);
-  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, 0.0, spec.Ls, spec.Ss, wave, s);
+  if (chunk_count(A) > 0) launch_chunks(P, L, A, S, 0.0, spec.Ls, spec.Ss, wave, s);
   if (!wave) {
     hipError_t e = ensure_schur_attr();
     if (e != hipSuccess) return e;
@@ -3334,7 +3341,7 @@ hipError_t finish(const Problem& P, const Lin& L, int E, const int* gmap, uint8_
 }
 
 hipError_t build_pairs(const Active& A, int* pp_cnt, int* pp_off, int4* pp, hipStream_t s) {
-  const int nc = A.npairs * A.nchk;
+  const int nc = chunk_count(A);
   if (nc == 0) return hipSuccess;
   hipLaunchKernelGGL(pair_count_kernel, dim3(nc), dim3(64), 0, s, A, pp_cnt);
   hipLaunchKernelGGL(pair_offsets_kernel, dim3(1), dim3(1024), 0, s, pp_cnt, pp_off, nc);
@@ -3355,7 +3362,7 @@ hipError_t classify(const Problem& P, const Lin& L, int E, uint8_t* level, uint8
 }
 
 hipError_t trial_chunks(const Problem& P, const Lin& L, const Active& A, Sys& S, double lambda, hipStream_t s) {
-  if (A.npairs * A.nchk > 0) launch_chunks(P, L, A, S, lambda, L, S, false, s);
+  if (chunk_count(A) > 0) launch_chunks(P, L, A, S, lambda, L, S, false, s);
   hipLaunchKernelGGL(shard_fail_stage_kernel, dim3(1), dim3(1), 0, s, S, S.pairfin + (size_t)A.npairs * 48);
   return hipGetLastError();
 }

@@ -55,6 +55,10 @@ struct Active {          // active structure of one optimize() phase
   int nchk;              // Schur chunks per pose pair: landmark ranges of lmchunk
   int lmchunk;           // landmarks per Schur chunk (a multiple of 64; kLmChunk unless the pose pairs
                          //   are so many that the chunk waves would need several dispatch rounds)
+  int dsub;              // Schur chunks per landmark range of a DIAGONAL pose pair: 1, or more on wide windows
+                         //   (C5: a diagonal pair walks ~(K - 1) / (obs - 1) times an off-diagonal pair's edge
+                         //   pairs and set the chunk phase alone); see chunk_geo
+  int lmsub;             // landmarks per diagonal sub-chunk (a multiple of 64; lmchunk when dsub == 1)
   int ue_bpr;            // update_errors<true> workgroups per Schur chunk range when their landmark blocks
                          //   are dealt to the XCD that ran the range's chunks (0: plain order)
   const int* pp_off;     // [npairs * nchk + 1] segment of each chunk in the edge-pair lists
@@ -69,6 +73,51 @@ struct Active {          // active structure of one optimize() phase
   int K, nL;
   int robust;
 };
+
+// Schur chunk geometry.  Chunks are numbered pose pair by pose pair (row-major upper triangle); a pair owns nchk
+// landmark ranges of lmchunk, a diagonal pair nchk * dsub sub-ranges of lmsub (dsub == 1: every pair nchk, chunk
+// c = pr * nchk + lb, as before).  g0 .. g1: the chunk's landmarks (clamped to nL), gend its nominal end (the
+// points-only test), c0 .. c1 the chunks of its pose pair.
+struct ChunkGeo {
+  int pr, lb, g0, g1, gend, c0, c1;
+};
+__host__ __device__ inline int chunk_count(const Active& A) { return A.nchk * (A.npairs + (A.dsub - 1) * A.K); }
+__host__ __device__ inline ChunkGeo chunk_geo(const Active& A, int c) {
+  ChunkGeo q;
+  if (A.dsub <= 1) {
+    q.pr = c / A.nchk;
+    q.lb = c - q.pr * A.nchk;
+    q.g0 = q.lb * A.lmchunk;
+    q.gend = q.g0 + A.lmchunk;
+    q.c0 = q.pr * A.nchk;
+    q.c1 = q.c0 + A.nchk;
+  } else {
+    // row a (pose a's pairs a..K-1): pair base a K - a (a - 1) / 2, chunk base nchk (pair base + (dsub - 1) a)
+    int a = 0;
+    while (a + 1 < A.K && c >= A.nchk * ((a + 1) * A.K - (a + 1) * a / 2 + (A.dsub - 1) * (a + 1))) a++;
+    const int pa = a * A.K - a * (a - 1) / 2, base = A.nchk * (pa + (A.dsub - 1) * a), nd = A.nchk * A.dsub;
+    const int l = c - base;
+    if (l < nd) {
+      q.pr = pa;
+      q.lb = l / A.dsub;
+      q.g0 = q.lb * A.lmchunk + (l - q.lb * A.dsub) * A.lmsub;
+      q.gend = q.g0 + A.lmsub < (q.lb + 1) * A.lmchunk ? q.g0 + A.lmsub : (q.lb + 1) * A.lmchunk;
+      q.c0 = base;
+      q.c1 = base + nd;
+    } else {
+      const int m = l - nd, j = m / A.nchk;
+      q.pr = pa + 1 + j;
+      q.lb = m - j * A.nchk;
+      q.g0 = q.lb * A.lmchunk;
+      q.gend = q.g0 + A.lmchunk;
+      q.c0 = base + nd + j * A.nchk;
+      q.c1 = q.c0 + A.nchk;
+    }
+  }
+  q.g1 = q.gend < A.nL ? q.gend : A.nL;
+  if (q.g1 < q.g0) q.g1 = q.g0;
+  return q;
+}
 
 struct Mail {            // pinned, host-mapped: the per-trial result the host spins on
   double v[4];           // chi2, scale, maxdiag, fail

@@ -1,5 +1,5 @@
 #!/bin/bash
-# C5 reduced-system solver swap (solve_reg: MFMA tiles on SIMDs 1..3, pivot chain on SIMD 0): BA GPU tests, C5 parity,
+# C5 Schur chunk split (diagonal pose pairs in sub-chunks) and earlier solver swap: BA GPU tests, C5 parity,
 # standalone C5 BA A/B against the previous library, C5 bench line.
 set -o pipefail
 mkdir -p gpurun_out
