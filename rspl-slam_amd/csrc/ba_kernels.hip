@@ -1450,19 +1450,29 @@ __device__ __forceinline__ void pose_diag_lds(const Active& A, const double (*pd
 template <bool FILL>
 __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, const int* pp_off, int4* pp) {
   const int lane = threadIdx.x & 63;
-  const ChunkGeo cg = chunk_geo(A, c);
-  const int pr = cg.pr;
+  int pr, g0, g1, nr;
+  if (A.dsub <= 1) {  // (every pair nchk ranges of lmchunk)
+    pr = c / A.nchk;
+    g0 = (c - pr * A.nchk) * A.lmchunk;
+    g1 = A.nL;
+    nr = A.lmchunk / 64;
+  } else {
+    const ChunkGeo cg = chunk_geo(A, c);
+    pr = cg.pr;
+    g0 = cg.g0;
+    g1 = cg.g1;
+    nr = (cg.g1 - cg.g0 + 63) / 64;
+  }
   const int pa = A.pairs[2 * pr], pb = A.pairs[2 * pr + 1];
   int base = FILL ? pp_off[c] : 0;
-  const int nr = (cg.g1 - cg.g0 + 63) / 64;
   // four landmark rounds at a time: their CSR ranges, then the first eight edge poses of each (a landmark's
   // whole edge list when it has <= 8 edges, the common case), every load of a group in flight at once
   for (int r0 = 0; r0 < nr; r0 += 4) {
     int k0[4], k1[4], pz[4][8];
 #pragma unroll
     for (int u = 0; u < 4; u++) {
-      const int g = cg.g0 + 64 * (r0 + u) + lane;
-      const bool in = r0 + u < nr && g < cg.g1;
+      const int g = g0 + 64 * (r0 + u) + lane;
+      const bool in = r0 + u < nr && g < g1;
       const int o0 = in ? A.lm_off[g] : 0, o1 = in ? A.lm_off[g + 1] : 0;
       const bool act = in && A.lm_act[g];
       k0[u] = act ? o0 : 0;
@@ -1475,7 +1485,7 @@ __device__ __forceinline__ void pair_scan(const Active& A, int c, int* pp_cnt, c
 #pragma unroll
     for (int u = 0; u < 4; u++) {
       if (r0 + u >= nr) break;  // uniform
-      const int g = cg.g0 + 64 * (r0 + u) + lane;
+      const int g = g0 + 64 * (r0 + u) + lane;
       const int e0 = k0[u], e1 = k1[u];
       int cnt = 0;
       unsigned ma1 = 0, mb1 = 0;  // the masks when the landmark has <= 8 edges (one block each)
@@ -2417,21 +2427,25 @@ struct ChunkSeg {
 };
 __device__ __forceinline__ bool chunk_seg(const Active& A, int nq, int vb, ChunkSeg& cs) {
   const int lane = threadIdx.x & 63;
-  if (A.nchk >= 8) {
+  if (A.nchk >= 8) {  // (dsub == 1)
     const int xcd = vb & 7, slot = vb >> 3, rpx = (A.nchk + 7) >> 3;
-    const int lb = (slot % rpx) * 8 + xcd, pr0 = slot / rpx;
-    if (lb >= A.nchk || pr0 >= A.npairs) return false;
-    cs.c = pr0 * A.nchk + lb;
+    cs.lb = (slot % rpx) * 8 + xcd;
+    cs.pr = slot / rpx;
+    if (cs.lb >= A.nchk || cs.pr >= A.npairs) return false;
+    cs.c = cs.pr * A.nchk + cs.lb;
+    cs.c0 = cs.pr * A.nchk;
+    cs.c1 = cs.c0 + A.nchk;
+    cs.pts = (cs.lb + 1) * A.lmchunk <= nq;
   } else {  // fewer ranges than XCDs (many pose pairs, wide chunks): plain order, every XCD busy
     if (vb >= chunk_count(A)) return false;
     cs.c = vb;
+    const ChunkGeo cg = chunk_geo(A, cs.c);
+    cs.lb = cg.lb;
+    cs.pr = cg.pr;
+    cs.c0 = cg.c0;
+    cs.c1 = cg.c1;
+    cs.pts = cg.gend <= nq;
   }
-  const ChunkGeo cg = chunk_geo(A, cs.c);
-  cs.lb = cg.lb;
-  cs.pr = cg.pr;
-  cs.c0 = cg.c0;
-  cs.c1 = cg.c1;
-  cs.pts = cg.gend <= nq;
   cs.beg = A.pp_off[cs.c];
   cs.end = A.pp_off[cs.c + 1];
   cs.q0 = cs.beg + lane < cs.end ? A.pp[cs.beg + lane] : make_int4(0, 0, 0, 0);
