@@ -196,7 +196,8 @@ struct NoStamp {
 // pidx / np: the pose part of the LM scale runs over the problem's poses p < np (lane p) with pidx[p] >= 0, as the
 // other solvers.  Writes x[0 .. 6K) and *sc_out, or sets *fail.  Launch: 1 workgroup of kSolveRegThreads,
 // solve_reg_lds_bytes(K) of dynamic LDS, 10 < K <= kSolveRegMaxK.
-template <class Stamp, int kAblate = 0>  // kAblate (benchmarks only): 1 no trailing MFMAs, 2 no pivot arithmetic
+template <class Stamp, int kAblate = 0>  // kAblate (benchmarks only): 1 no trailing MFMAs, 2 no pivot arithmetic,
+                                         // 4 no tile assembly, 8 no pairfin loads
 __device__ void solve_reg(const double* __restrict__ pairfin, int K, double lambda, double* __restrict__ x,
                           double* __restrict__ sc_out, int* fail, const int* pidx, int np, double* lds,
                           const Stamp& stamp) {
@@ -224,7 +225,8 @@ __device__ void solve_reg(const double* __restrict__ pairfin, int K, double lamb
     const int nent = npairs * 48;
     double va[kB];
 #pragma unroll
-    for (int u = 0; u < kB; u++) va[u] = pairfin[min(tid + kSolveRegThreads * u, nent - 1)];
+    for (int u = 0; u < kB; u++)
+      va[u] = (kAblate & 8) ? 1.0 + u : pairfin[min(tid + kSolveRegThreads * u, nent - 1)];
     double vb = 0.0;
     if (tid < 12 * K) {
       const int a = tid / 12;
@@ -262,7 +264,7 @@ __device__ void solve_reg(const double* __restrict__ pairfin, int K, double lamb
     for (int i = 0; i < 4; i++) {
       const int r = 16 * tI[q] + 4 * i + lq, pr = r / 6, rr = r - 6 * pr;
       double v = 0.0;
-      if (t < ntiles && c < n && r <= n && r >= c) {
+      if (!(kAblate & 4) && t < ntiles && c < n && r <= n && r >= c) {
         if (r == n) {
           v = bpl[c] - ybl[c];
         } else {

@@ -513,16 +513,24 @@ int main(int argc, char** argv) {
     CK(hipFuncSetAttribute((const void*)vab_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
     CK(hipFuncSetAttribute((const void*)vab_kernel<3>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
     CK(hipFuncSetAttribute((const void*)vab_kernel<0>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
+    CK(hipFuncSetAttribute((const void*)vab_kernel<4>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
+    CK(hipFuncSetAttribute((const void*)vab_kernel<8>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
+    CK(hipFuncSetAttribute((const void*)vab_kernel<12>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
+    CK(hipFuncSetAttribute((const void*)vab_kernel<15>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
     hipEvent_t a0, a1;
     CK(hipEventCreate(&a0));
     CK(hipEventCreate(&a1));
-    for (int ab = 0; ab < 4; ab++) {
+    for (int ab : {0, 1, 2, 3, 4, 8, 12, 15}) {
       auto L = [&]() {
         const size_t lb = solve_reg_lds_bytes(K);
         if (ab == 0) hipLaunchKernelGGL(vab_kernel<0>, dim3(1), dim3(kSolveRegThreads), lb, 0, d_pf, K, lambda, d_x, d_out, d_fail, nullptr);
         if (ab == 1) hipLaunchKernelGGL(vab_kernel<1>, dim3(1), dim3(kSolveRegThreads), lb, 0, d_pf, K, lambda, d_x, d_out, d_fail, nullptr);
         if (ab == 2) hipLaunchKernelGGL(vab_kernel<2>, dim3(1), dim3(kSolveRegThreads), lb, 0, d_pf, K, lambda, d_x, d_out, d_fail, nullptr);
         if (ab == 3) hipLaunchKernelGGL(vab_kernel<3>, dim3(1), dim3(kSolveRegThreads), lb, 0, d_pf, K, lambda, d_x, d_out, d_fail, nullptr);
+        if (ab == 4) hipLaunchKernelGGL(vab_kernel<4>, dim3(1), dim3(kSolveRegThreads), lb, 0, d_pf, K, lambda, d_x, d_out, d_fail, nullptr);
+        if (ab == 8) hipLaunchKernelGGL(vab_kernel<8>, dim3(1), dim3(kSolveRegThreads), lb, 0, d_pf, K, lambda, d_x, d_out, d_fail, nullptr);
+        if (ab == 12) hipLaunchKernelGGL(vab_kernel<12>, dim3(1), dim3(kSolveRegThreads), lb, 0, d_pf, K, lambda, d_x, d_out, d_fail, nullptr);
+        if (ab == 15) hipLaunchKernelGGL(vab_kernel<15>, dim3(1), dim3(kSolveRegThreads), lb, 0, d_pf, K, lambda, d_x, d_out, d_fail, nullptr);
       };
       for (int i = 0; i < 3; i++) L();
       CK(hipEventRecord(a0));
@@ -540,7 +548,7 @@ int main(int argc, char** argv) {
         printf("clock probe in the solver's context: %.2f ticks per dependent fp64 FMA (lat_bench: 6.5-7.5)\n", c / 1024.0);
       }
       printf("ablation %d (%s): %.2f us per solve\n", ab,
-             ab == 0 ? "full" : ab == 1 ? "no trailing MFMA" : ab == 2 ? "no pivot arithmetic" : "neither", 1e3 * ms / reps);
+             ab == 0 ? "full" : ab == 1 ? "no trailing MFMA" : ab == 2 ? "no pivot arithmetic" : ab == 3 ? "neither" : ab == 4 ? "no tile assembly" : ab == 8 ? "no pairfin loads" : ab == 12 ? "neither assembly part" : "skeleton only", 1e3 * ms / reps);
     }
   }
   CK(hipEventCreate(&e0));
