@@ -28,7 +28,6 @@ namespace frame {
 using ba::SE3;
 using wave::kNV;
 using wave::rcp64;
-using wave::wave_allreduce28;
 using wave::wsum;
 using wave::wsum_int;
 
@@ -78,7 +77,22 @@ struct View {
   double delta0, delta1;  // Huber deltas (mono, stereo): scalars, never indexed (no scratch)
 };
 
-using wave::block_combine;  // (wave_reduce.hpp: the NW waves' sums added in wave order through LDS)
+
+#ifdef RSPL_FRAME_PROF  // experiment build only (tools/experiments): per-phase cycle sums of block 0, printed at exit
+struct FProf {
+  unsigned long long t[8];
+  int n;
+};
+#define FP_DECL , FProf& pf
+#define FP_ARG , pf
+#define FP_NOW(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#define FP_ADD(k, a, b) pf.t[k] += (b) - (a)
+#else
+#define FP_DECL
+#define FP_ARG
+#define FP_NOW(v)
+#define FP_ADD(k, a, b)
+#endif
 using wave::block_sum_int;
 
 // robust (Huber) or plain chi2 of an error, for the edge type
@@ -94,7 +108,9 @@ __device__ __forceinline__ int hidx(int i, int j) { return i * 6 - i * (i - 1) /
 
 // errors at T (stored) + robust chi2 + H / b (Huber IRLS weights), wave-reduced
 template <int NW>
-__device__ __forceinline__ void linearize(const View& V, const Pose& P, int lane, bool robust, double (&acc)[kNV]) {
+__device__ __forceinline__ void linearize(const View& V, const Pose& P, int lane, bool robust,
+                                          double (&acc)[kNV] FP_DECL) {
+  FP_NOW(l0);
 #pragma unroll
   for (int k = 0; k < kNV; k++) acc[k] = 0.0;
   for (int e = lane; e < V.n; e += 64 * NW) {
@@ -142,8 +158,13 @@ __device__ __forceinline__ void linearize(const View& V, const Pose& P, int lane
       for (int j = i; j < 6; j++) acc[hidx(i, j)] += w * (J[0][i] * J[0][j] + J[1][i] * J[1][j] + J[2][i] * J[2][j]);
     }
   }
-  wave_allreduce28(acc, lane & 63);
-  block_combine<NW>(acc);
+  FP_NOW(l1);
+  wave::block_allreduce28<NW>(acc, lane & 63);
+  FP_NOW(l2);
+  FP_NOW(l3);
+  FP_ADD(2, l0, l1);
+  FP_ADD(3, l1, l2);
+  FP_ADD(4, l2, l3);
 }
 
 // (H + lambda I) x = b by Cholesky, in registers (every lane the same); false if not SPD.
@@ -193,7 +214,7 @@ __device__ __forceinline__ bool solve6(const double (&acc)[kNV], double lambda, 
 // SparseOptimizer::optimize(iters) with OptimizationAlgorithmLevenberg on the pose vertex
 template <int NW>
 __device__ __forceinline__ int optimize_pose(const View& V, Pose& P, int lane, bool robust, int iters,
-                                             double& chi2_out) {
+                                             double& chi2_out FP_DECL) {
   // The linearisation at the current estimate that every iteration starts with is the one the accepted
   // candidate of the previous iteration already computed: each trial evaluates its candidate's errors, robust
   // cost AND normal equations in one pass over the edges (one 28-value reduction), and an accepted candidate's
@@ -203,7 +224,7 @@ __device__ __forceinline__ int optimize_pose(const View& V, Pose& P, int lane, b
   double acc[kNV];
   double lambda = 0, ni = 2, currentChi = 0;
   int done = 0;
-  if (iters > 0) linearize<NW>(V, P, lane, robust, acc);
+  if (iters > 0) linearize<NW>(V, P, lane, robust, acc FP_ARG);
   for (int it = 0; it < iters; it++) {
     currentChi = acc[27];
     if (it == 0) {  // computeLambdaInit: tau * max diagonal
@@ -217,16 +238,20 @@ __device__ __forceinline__ int optimize_pose(const View& V, Pose& P, int lane, b
     int qmax = 0;
     do {
       double x[6];
+      FP_NOW(q0);
       const bool ok = solve6(acc, lambda, x);  // (uniform: every thread factors the same system)
+      FP_NOW(q1);
       Pose C = P;
       double cacc[kNV];
       double tempChi = DBL_MAX;
       if (ok) {
         C.set(ba::se3_mul(ba::se3_exp(x), P.T));
-        linearize<NW>(V, C, lane, robust, cacc);  // the candidate's errors (stored), cost and system
+        FP_NOW(q2);
+        FP_ADD(1, q1, q2);
+        linearize<NW>(V, C, lane, robust, cacc FP_ARG);  // the candidate's errors (stored), cost and system
         tempChi = cacc[27];
       } else {
-        linearize<NW>(V, P, lane, robust, cacc);  // (as g2o: the errors recomputed at the unchanged estimate)
+        linearize<NW>(V, P, lane, robust, cacc FP_ARG);  // (as g2o: the errors recomputed at the unchanged estimate)
       }
       rho = currentChi - tempChi;
       double scale = 1.0;
@@ -252,6 +277,12 @@ __device__ __forceinline__ int optimize_pose(const View& V, Pose& P, int lane, b
         if (!isfinite(lambda)) break;
       }
       qmax++;
+      FP_NOW(q3);
+      FP_ADD(0, q0, q1);
+      FP_ADD(5, q0, q3);
+#ifdef RSPL_FRAME_PROF
+      pf.n++;
+#endif
     } while (rho < 0 && qmax < 10);
     done++;
     if (qmax == 10 || rho == 0 || !isfinite(lambda)) break;
@@ -316,6 +347,10 @@ __global__ __launch_bounds__(64 * NW) void frame_opt_kernel(Args a, int batch) {
   int itr[4] = {0, 0, 0, 0};
   int rounds = 0;
   int num_outlier = 0;
+#ifdef RSPL_FRAME_PROF
+  FProf pf{};
+  FP_NOW(k0);
+#endif
 #pragma unroll 1
   for (int r = 0; r < 4; r++) {
     P.set(T0);  // setEstimate(SE3Quat(pose).inverse()) every round (:337)
@@ -325,7 +360,7 @@ __global__ __launch_bounds__(64 * NW) void frame_opt_kernel(Args a, int batch) {
     act = block_sum_int<NW>(act);
     int its = 0;
     double chi = 0;
-    if (act) its = optimize_pose<NW>(V, P, lane, robust, 10, chi);
+    if (act) its = optimize_pose<NW>(V, P, lane, robust, 10, chi FP_ARG);
 #pragma unroll
     for (int k = 0; k < 4; k++)
       if (k == r) {
@@ -358,6 +393,13 @@ __global__ __launch_bounds__(64 * NW) void frame_opt_kernel(Args a, int batch) {
     rounds = r + 1;
     if (D.n < 10) break;  // optimizer.edges().size() < 10 (:383)
   }
+#ifdef RSPL_FRAME_PROF
+  FP_NOW(k1);
+  if (f == 0 && lane == 0 && pf.n)
+    printf("fprof NW %d n %d trials %d: total %llu | per trial: solve6 %llu se3 %llu edges %llu wred %llu bcomb %llu "
+           "trial %llu\n", NW, D.n, pf.n, k1 - k0, pf.t[0] / pf.n, pf.t[1] / pf.n, pf.t[2] / pf.n, pf.t[3] / pf.n,
+           pf.t[4] / pf.n, pf.t[5] / pf.n);
+#endif
   for (int e = lane; e < D.n; e += T) a.inl_out[D.e0 + e] = V.inl[e];
   if (lane == 0) {
     Out* o = a.out + f;

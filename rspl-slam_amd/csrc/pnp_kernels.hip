@@ -645,7 +645,7 @@ __device__ double reproj2(const double* K4, const double R[9], const double t[3]
 // Levenberg-Marquardt on the inliers' squared reprojection error (orc_pnp's refine, oracle/pnp.c):
 // pose T_cw (R, t) with the left exp-map update; the NW waves' threads own strided correspondences, the
 // 6x6 normal equations and the costs are wave-reduced and then added over the waves in wave order
-// (wave::block_combine), so every thread takes the same decisions
+// (wave::block_allreduce28), so every thread takes the same decisions
 template <int NW>
 __device__ void refine(const double* K4, int n, const double* pw, const double* uv, const uint8_t* inl, int tid,
                        double R[9], double t[3]) {
@@ -677,8 +677,7 @@ __device__ void refine(const double* K4, int n, const double* pw, const double* 
         for (int b = a; b < 6; b++) acc[a * 6 - a * (a - 1) / 2 + (b - a)] += J[0][a] * J[0][b] + J[1][a] * J[1][b];
       }
     }
-    wave::wave_allreduce28(acc, lane);
-    wave::block_combine<NW>(acc);
+    wave::block_allreduce28<NW>(acc, lane);
     const double cost = acc[27];
     auto H = [&](int a, int b) { return a <= b ? acc[a * 6 - a * (a - 1) / 2 + (b - a)] : acc[b * 6 - b * (b - 1) / 2 + (a - b)]; };
     bool accepted = false;

@@ -42,13 +42,40 @@ __device__ __forceinline__ int wsum_int(int v) {
 // completes the sum, then every value is read back from its owner lane with readlane (wave-
 // uniform).  32 double exchanges instead of 28 x 6 for per-value butterflies; each value is
 // summed by one fixed tree (a + b == b + a in the pair), so the result is deterministic.
+// The xor-32 and xor-16 steps (24 of the 32 exchanges) are gfx950's v_permlane32_swap /
+// v_permlane16_swap (VALU lane swaps, no LDS-unit round trip); xor 2 and 1 are DPP quad
+// permutes; only xor 8 and 4 go through ds_bpermute.  Same pairs, same operands: the sums are
+// bitwise those of a plain shuffle tree.
 __device__ __forceinline__ double shx(double v, int o) { return __shfl_xor(v, o); }
-__device__ __forceinline__ void wave_allreduce28(double (&acc)[kNV], int lane) {
+// lanes (l, l ^ 32) [K32] or (l, l ^ 16) [!K32]: a + partner's a in the lower lane, b + partner's b in the upper
+template <bool K32>
+__device__ __forceinline__ double swap_sum(double a, double b) {
+  const unsigned long long x = __double_as_longlong(a), y = __double_as_longlong(b);
+  unsigned p0, p1, q0, q1;
+  if constexpr (K32) {
+    const auto lo = __builtin_amdgcn_permlane32_swap((unsigned)x, (unsigned)y, false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap((unsigned)(x >> 32), (unsigned)(y >> 32), false, false);
+    p0 = lo[0]; q0 = lo[1]; p1 = hi[0]; q1 = hi[1];
+  } else {
+    const auto lo = __builtin_amdgcn_permlane16_swap((unsigned)x, (unsigned)y, false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap((unsigned)(x >> 32), (unsigned)(y >> 32), false, false);
+    p0 = lo[0]; q0 = lo[1]; p1 = hi[0]; q1 = hi[1];
+  }
+  // lower lane: p = own a, q = partner's a; upper lane: p = partner's b, q = own b
+  return __longlong_as_double((long long)((unsigned long long)p1 << 32 | p0)) +
+         __longlong_as_double((long long)((unsigned long long)q1 << 32 | q0));
+}
+// the reduce-scatter: lane L returns the wave's sum of value L >> 1 (values 28..31: 0)
+__device__ __forceinline__ double wave_scatter28(const double (&acc)[kNV], int lane) {
   double v[32];
 #pragma unroll
   for (int k = 0; k < 32; k++) v[k] = k < kNV ? acc[k] : 0.0;
 #pragma unroll
-  for (int o = 32, h = 16; o >= 2; o >>= 1, h >>= 1) {
+  for (int k = 0; k < 16; k++) v[k] = swap_sum<true>(v[k], v[16 + k]);
+#pragma unroll
+  for (int k = 0; k < 8; k++) v[k] = swap_sum<false>(v[k], v[8 + k]);
+#pragma unroll
+  for (int o = 8, h = 4; o >= 4; o >>= 1, h >>= 1) {
     const bool up = lane & o;  // keep the upper half of the current h*2 values
 #pragma unroll
     for (int k = 0; k < h; k++) {
@@ -57,14 +84,17 @@ __device__ __forceinline__ void wave_allreduce28(double (&acc)[kNV], int lane) {
       v[k] = keep + shx(send, o);
     }
   }
-  v[0] += shx(v[0], 1);
-  // lane L holds value index j(L): bit 5 of L -> bit 4 of j, bit 4 -> bit 3, ..., bit 1 -> bit 0
-#pragma unroll
-  for (int j = 0; j < kNV; j++) {
-    const int owner = ((j >> 4) & 1) << 5 | ((j >> 3) & 1) << 4 | ((j >> 2) & 1) << 3 | ((j >> 1) & 1) << 2 |
-                      (j & 1) << 1;
-    acc[j] = rdlaned(v[0], owner);
+  {
+    const bool up = lane & 2;
+    const double keep = up ? v[1] : v[0], send = up ? v[0] : v[1];
+    v[0] = keep + dppd<0x4E>(send);  // quad_perm [2,3,0,1]: lane ^ 2
   }
+  return v[0] + dppd<0xB1>(v[0]);  // quad_perm [1,0,3,2]: lane ^ 1
+}
+__device__ __forceinline__ void wave_allreduce28(double (&acc)[kNV], int lane) {
+  const double s = wave_scatter28(acc, lane);
+#pragma unroll
+  for (int j = 0; j < kNV; j++) acc[j] = rdlaned(s, 2 * j);
 }
 
 __device__ __forceinline__ double rcp64(double d) {
@@ -92,6 +122,28 @@ __device__ __forceinline__ void block_combine(double (&v)[N]) {
       v[k] = t;
     }
     __syncthreads();  // cb is reused by the next combine
+  }
+}
+// wave_allreduce28 + block_combine in one: the waves' scattered sums (lane 2j: value j) go to LDS, lane j < 28 of
+// every wave adds value j over the waves in wave order, and readlane hands each sum to the whole wave -- NW reads
+// per lane instead of NW x 28, the same additions in the same order (bitwise the two-step result)
+template <int NW>
+__device__ __forceinline__ void block_allreduce28(double (&acc)[kNV], int lane) {
+  const double s = wave_scatter28(acc, lane);
+  if constexpr (NW == 1) {
+#pragma unroll
+    for (int j = 0; j < kNV; j++) acc[j] = rdlaned(s, 2 * j);
+  } else {
+    __shared__ double cs[NW][32];
+    const int wv = threadIdx.x >> 6;
+    if (!(lane & 1)) cs[wv][lane >> 1] = s;
+    __syncthreads();
+    double t = cs[0][lane & 31];
+#pragma unroll
+    for (int w = 1; w < NW; w++) t += cs[w][lane & 31];
+#pragma unroll
+    for (int j = 0; j < kNV; j++) acc[j] = rdlaned(t, j);
+    __syncthreads();  // cs is reused by the next combine
   }
 }
 template <int NW>
