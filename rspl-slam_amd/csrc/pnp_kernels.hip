@@ -231,21 +231,19 @@ constexpr int kN = 5;  // RANSAC's minimal subset (solvePnPRansac with SOLVEPNP_
 
 struct WaveLds {      // one hypothesis' wave
   double A[2][144], U[2][144];  // M^T M -> diagonalised; eigenvector columns (double-buffered by round)
-  double cf[12][2];             // this round's update of index i: self / partner coefficients
-  int act[12];                  // rotation applied to index i's pair
   double alph[4 * kN];          // barycentric coordinates
   double Vn[4][12];             // eigenvectors of the 4 smallest eigenvalues (ut rows 8..11)
 };
 
 /* Jacobi of the 12 x 12 M^T M in w.A[0], the round-robin order of oracle jacobi12_rounds.  A
-   round: lanes 0..5 form its 6 rotations (c, s from the round's start matrix) -> barrier -> each
-   lane takes its elements (e = lane + 64 m) through the column rotation of the element's column
-   pair and then the row rotation of its row pair -- element (i, j) needs (i, j), (i, j'), (i', j),
-   (i', j') of the round's start matrix, j' / i' the partners -- the same IEEE operations in the
-   same order as the oracle's column pass then row pass; the eigenvector columns likewise ->
-   the other buffer -> barrier.  Partners are arithmetic: index 11 pairs with r, r with 11, any
-   other i with (2 r - i) mod 11.  Leaves the eigenvectors of the 4 smallest eigenvalues in
-   w.Vn (ut row 8 + r). */
+   round's 6 rotations pair the indices (index 11 with r, r with 11, any other i with (2 r - i) mod 11),
+   so A splits into 36 2 x 2 blocks (row pair x column pair): lane < 36 owns one, forms the block's
+   row and column rotations itself from the round's start matrix (c, s of the pairs' (p, q), (p, p),
+   (q, q)), takes its four elements through the column pass and then the row pass -- the same IEEE
+   operations in the same order as the oracle -- and the same block of the eigenvector columns
+   through the column pass, into the other buffer -> wave barrier.  One LDS round trip per round
+   (it was three: rotations by lanes 0..5 -> LDS -> every element's lane).  Leaves the eigenvectors
+   of the 4 smallest eigenvalues in w.Vn (ut row 8 + r). */
 /* the rotation annihilating a_pq from d = a_qq - a_pp, h = 2 a_pq != 0 (oracle jacobi_cs):
    t = sgn(theta) |h| / (|d| + g), c = sqrt((|d| + g) / (2 g)), g = sqrt(d^2 + h^2) -- the classic
    Rutishauser rotation with three dependent sqrt / divide steps instead of five */
@@ -288,38 +286,43 @@ __device__ __forceinline__ void jacobi12_wave(WaveLds& w, int lane) {
     }
     if (po <= 1e-30 * pt || po == 0.0) break;  // uniform: identical bits in every lane
     for (int r = 0; r < 11; r++) {
+      // lane < 36: the 2 x 2 block (rows of pair rp) x (columns of pair cp) of A and of U -- its two rotations
+      // formed in the lane itself from the round's start matrix (no broadcast through LDS), all reads issued
+      // together; the same IEEE operations per element as the column pass then row pass (and U's column pass)
       const double* A = w.A[b];
-      if (lane < 6) {
-        const int j = lane;
-        const int a0 = j == 0 ? r : (r + j) % 11, b0 = j == 0 ? 11 : (r - j + 11) % 11;
-        const int p = a0 < b0 ? a0 : b0, q = a0 < b0 ? b0 : a0;
-        const double apq = A[p * n + q];
-        const int ac = apq != 0.0;
-        double c = 1.0, s = 0.0;
-        if (ac) {
-          const double app = A[p * n + p], aqq = A[q * n + q];
-          jacobi_cs(aqq - app, 2.0 * apq, c, s);
+      const double* U = w.U[b];
+      if (lane < 36) {
+        const int rp = lane / 6, cp = lane - 6 * rp;
+        int pi, qi, pj, qj;
+        {
+          const int a0 = rp == 0 ? r : (r + rp) % 11, b0 = rp == 0 ? 11 : (r - rp + 11) % 11;
+          pi = a0 < b0 ? a0 : b0;
+          qi = a0 < b0 ? b0 : a0;
+          const int a1 = cp == 0 ? r : (r + cp) % 11, b1 = cp == 0 ? 11 : (r - cp + 11) % 11;
+          pj = a1 < b1 ? a1 : b1;
+          qj = a1 < b1 ? b1 : a1;
         }
-        w.cf[p][0] = c;
-        w.cf[p][1] = -s;
-        w.cf[q][0] = c;
-        w.cf[q][1] = s;
-        w.act[p] = ac;
-        w.act[q] = ac;
-      }
-      wave_sync();
-#pragma unroll
-      for (int m = 0; m < 3; m++) {
-        if (ee[m] >= 144) continue;
-        const int i = ei[m], j = ej[m], ip = partner(i, r), jp = partner(j, r);
-        const double cj = w.cf[j][0], sj = w.cf[j][1], ci = w.cf[i][0], si = w.cf[i][1];
-        const bool aj = w.act[j], ai = w.act[i];
-        const double aij = A[i * n + j], aijp = A[i * n + jp], aipj = A[ip * n + j], aipjp = A[ip * n + jp];
-        const double xij = aj ? cj * aij + sj * aijp : aij;      // column pass
-        const double xipj = aj ? cj * aipj + sj * aipjp : aipj;
-        w.A[b ^ 1][ee[m]] = ai ? ci * xij + si * xipj : xij;     // row pass
-        const double* U = w.U[b];
-        w.U[b ^ 1][ee[m]] = aj ? cj * U[i * n + j] + sj * U[i * n + jp] : U[i * n + j];
+        const double rpq = A[pi * n + qi], rpp = A[pi * n + pi], rqq = A[qi * n + qi];
+        const double cpq = A[pj * n + qj], cpp = A[pj * n + pj], cqq = A[qj * n + qj];
+        const double a_pp = A[pi * n + pj], a_pq = A[pi * n + qj], a_qp = A[qi * n + pj], a_qq = A[qi * n + qj];
+        const double u_pp = U[pi * n + pj], u_pq = U[pi * n + qj], u_qp = U[qi * n + pj], u_qq = U[qi * n + qj];
+        const bool ai = rpq != 0.0, aj = cpq != 0.0;
+        double ci, si, cj, sj;  // both formed unconditionally (two independent chains), an inactive pair's discarded
+        jacobi_cs(rqq - rpp, 2.0 * rpq, ci, si);
+        jacobi_cs(cqq - cpp, 2.0 * cpq, cj, sj);
+        // column pass (index pj takes (c, -s), qj takes (c, s))
+        const double x_pp = aj ? cj * a_pp + (-sj) * a_pq : a_pp, x_qp = aj ? cj * a_qp + (-sj) * a_qq : a_qp;
+        const double x_pq = aj ? cj * a_pq + sj * a_pp : a_pq, x_qq = aj ? cj * a_qq + sj * a_qp : a_qq;
+        double* An = w.A[b ^ 1];
+        An[pi * n + pj] = ai ? ci * x_pp + (-si) * x_qp : x_pp;  // row pass
+        An[qi * n + pj] = ai ? ci * x_qp + si * x_pp : x_qp;
+        An[pi * n + qj] = ai ? ci * x_pq + (-si) * x_qq : x_pq;
+        An[qi * n + qj] = ai ? ci * x_qq + si * x_pq : x_qq;
+        double* Un = w.U[b ^ 1];
+        Un[pi * n + pj] = aj ? cj * u_pp + (-sj) * u_pq : u_pp;
+        Un[pi * n + qj] = aj ? cj * u_pq + sj * u_pp : u_pq;
+        Un[qi * n + pj] = aj ? cj * u_qp + (-sj) * u_qq : u_qp;
+        Un[qi * n + qj] = aj ? cj * u_qq + sj * u_qp : u_qq;
       }
       wave_sync();
       b ^= 1;
