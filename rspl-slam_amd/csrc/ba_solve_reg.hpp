@@ -105,77 +105,141 @@ __device__ __forceinline__ double sr_readlane64(double v, int l) {
 // y_i = X_{s(i)}(n, i % 6).  Pose step st: the block's six y by readlane from the lanes that hold them (no LDS on the
 // chain: a wave fence there would also wait for the prefetches), x_k = y_k - sum_{l > k} L(l, k) x_l with the
 // block's unit L, then every row i < 6 st: y_i -= sum_l L(6 st + l, i) x_l with L(6 st + l, i) =
-// X_{s(i)}(6 st + l, i % 6).  The next step's L entries (three 16-byte loads per row) are requested a step ahead,
-// the block's unit L (eight) at the step's start, behind the readlanes.  x -> xv[0 .. n) (written by lane 0).
+// X_{s(i)}(6 st + l, i % 6).  The next step's L entries (three 16-byte loads per row) and unit L (eight) are
+// requested a step ahead into the other of two operand sets (two steps per loop iteration: no register copies), by
+// every lane (no exec mask, so the compiler waits for exactly the loads a step needs; rows >= 6 st take in-bounds
+// entries of no meaning -- their y was read before the step's update and is never read again).  Micro-benchmark
+// (solve_bench.hip, K = 29): 1,038 -> 739 cycles per pose step, x bitwise the same.  x -> xv[0 .. n) (lane 0).
+// (sr_backsub's unrolled form) step st's operands: the panel entries of every lane's rows (in-bounds for all lanes,
+// no exec mask) and the block's unit L
+__device__ __forceinline__ void sr_bs_fetch(const double* P, const double* Ldg, const int (&pb)[3], int st,
+                                            double (&A)[3][6], double (&L)[16]) {
+#pragma unroll
+  for (int j = 0; j < 3; j++) sr_ld6(P + max(pb[j] + 6 * st, 0), A[j]);
+  const double2* q = reinterpret_cast<const double2*>(Ldg + 16 * st);
+#pragma unroll
+  for (int i = 0; i < 8; i++) {
+    const double2 t = q[i];
+    L[2 * i] = t.x;
+    L[2 * i + 1] = t.y;
+  }
+}
+__device__ __forceinline__ void sr_bs_step(const double* P, const double* Ldg, double* xv, const int (&pb)[3], int st,
+                                           int lane, double& z0, double& z1, double& z2, const double (&Ac)[3][6],
+                                           const double (&Lc)[16], double (&An)[3][6], double (&Ln)[16]) {
+  const int c0 = 6 * st;
+  sr_bs_fetch(P, Ldg, pb, max(st - 1, 0), An, Ln);  // the next step's operands, ahead of this step's chain
+  double yb[6], xb[6];
+  const int s0 = c0 >> 6, s5 = (c0 + 5) >> 6;
+  if (s0 == s5) {
+    const double src = s0 == 0 ? z0 : (s0 == 1 ? z1 : z2);
+#pragma unroll
+    for (int k = 0; k < 6; k++) yb[k] = sr_readlane64(src, (c0 + k) & 63);
+  } else {  // (rows 60..65 or 126..131: the block straddles two slots)
+    const double lo = s0 == 0 ? z0 : z1, hi = s0 == 0 ? z1 : z2;
+#pragma unroll
+    for (int k = 0; k < 6; k++) yb[k] = sr_readlane64(((c0 + k) >> 6) == s0 ? lo : hi, (c0 + k) & 63);
+  }
+#pragma unroll
+  for (int k = 5; k >= 0; k--) {
+    double v = yb[k];
+#pragma unroll
+    for (int l = 5; l > k; l--) v -= Lc[l * (l - 1) / 2 + k] * xb[l];
+    xb[k] = v;
+  }
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < 6; k++) xv[c0 + k] = xb[k];
+  }
+#pragma unroll
+  for (int l = 5; l >= 0; l--) {
+    z0 -= Ac[0][l] * xb[l];
+    z1 -= Ac[1][l] * xb[l];
+    z2 -= Ac[2][l] * xb[l];
+  }
+}
+
+template <bool kPingPong = true>  // false: the previous form (micro-benchmark reference, tools/experiments/solve_bench.hip)
 __device__ __forceinline__ void sr_backsub(const double* P, const double* Ldg, double* xv, int K) {
   const int n = 6 * K, lane = threadIdx.x & 63;
-  const double* Pi[3];
+  int pb[3];
   double zr[3];
 #pragma unroll
   for (int j = 0; j < 3; j++) {
     const int i = min(lane + 64 * j, n - 1), si = i / 6;
-    Pi[j] = P + sr_panel_off(si, n) + (i - 6 * si) * sr_panel_ld(si, n) - (6 * si + 6);
-    zr[j] = Pi[j][n];
+    pb[j] = sr_panel_off(si, n) + (i - 6 * si) * sr_panel_ld(si, n) - (6 * si + 6);
+    zr[j] = P[pb[j] + n];
   }
-  double Ac[3][6];
-  auto fetch = [&](int st, double (&Ad)[3][6]) {
-#pragma unroll
-    for (int j = 0; j < 3; j++) {
-      if (lane + 64 * j < 6 * st) sr_ld6(Pi[j] + 6 * st, Ad[j]);
-      else
-#pragma unroll
-        for (int l = 0; l < 6; l++) Ad[j][l] = 0.0;  // rows >= 6 st: final, never updated
+  if constexpr (kPingPong) {
+    double A0[3][6], A1[3][6], L0[16], L1[16];
+    double z0 = zr[0], z1 = zr[1], z2 = zr[2];
+    sr_bs_fetch(P, Ldg, pb, K - 1, A0, L0);
+    int st = K - 1;
+    for (; st >= 1; st -= 2) {
+      sr_bs_step(P, Ldg, xv, pb, st, lane, z0, z1, z2, A0, L0, A1, L1);
+      sr_bs_step(P, Ldg, xv, pb, st - 1, lane, z0, z1, z2, A1, L1, A0, L0);
     }
-  };
-  fetch(K - 1, Ac);
-  for (int st = K - 1; st >= 0; st--) {
-    const int c0 = 6 * st;
-    double Lc[16];
-    {
-      const double2* q = reinterpret_cast<const double2*>(Ldg + 16 * st);
+    if (st == 0) sr_bs_step(P, Ldg, xv, pb, 0, lane, z0, z1, z2, A0, L0, A1, L1);
+  } else {
+    double Ac[3][6];
+    auto fetch = [&](int st, double (&Ad)[3][6]) {
 #pragma unroll
-      for (int i = 0; i < 8; i++) {
-        const double2 t = q[i];
-        Lc[2 * i] = t.x;
-        Lc[2 * i + 1] = t.y;
+      for (int j = 0; j < 3; j++) {
+        if (lane + 64 * j < 6 * st) sr_ld6(P + pb[j] + 6 * st, Ad[j]);
+        else
+#pragma unroll
+          for (int l = 0; l < 6; l++) Ad[j][l] = 0.0;  // rows >= 6 st: final, never updated
       }
-    }
-    double An[3][6];
-    if (st > 0) fetch(st - 1, An);  // the next step's entries, requested before this step's chain
-    double yb[6], xb[6];
-    const int s0 = c0 >> 6, s5 = (c0 + 5) >> 6;  // (uniform) the slot(s) holding rows c0 .. c0 + 5
-    if (s0 == s5) {
-      const double src = s0 == 0 ? zr[0] : (s0 == 1 ? zr[1] : zr[2]);
+    };
+    fetch(K - 1, Ac);
+    for (int st = K - 1; st >= 0; st--) {
+      const int c0 = 6 * st;
+      double Lc[16];
+      {
+        const double2* q = reinterpret_cast<const double2*>(Ldg + 16 * st);
 #pragma unroll
-      for (int k = 0; k < 6; k++) yb[k] = sr_readlane64(src, (c0 + k) & 63);
-    } else {
-#pragma unroll
-      for (int k = 0; k < 6; k++) {
-        const int sl = (c0 + k) >> 6;
-        yb[k] = sr_readlane64(sl == 0 ? zr[0] : (sl == 1 ? zr[1] : zr[2]), (c0 + k) & 63);
+        for (int i = 0; i < 8; i++) {
+          const double2 t = q[i];
+          Lc[2 * i] = t.x;
+          Lc[2 * i + 1] = t.y;
+        }
       }
-    }
-    // x_k = y_k - sum_{l > k} L(l, k) x_l (l descending: the newest x last, one FMA after it)
+      double An[3][6];
+      if (st > 0) fetch(st - 1, An);
+      double yb[6], xb[6];
+      const int s0 = c0 >> 6, s5 = (c0 + 5) >> 6;
+      if (s0 == s5) {
+        const double src = s0 == 0 ? zr[0] : (s0 == 1 ? zr[1] : zr[2]);
 #pragma unroll
-    for (int k = 5; k >= 0; k--) {
-      double v = yb[k];
+        for (int k = 0; k < 6; k++) yb[k] = sr_readlane64(src, (c0 + k) & 63);
+      } else {
 #pragma unroll
-      for (int l = 5; l > k; l--) v -= Lc[l * (l - 1) / 2 + k] * xb[l];
-      xb[k] = v;
-    }
-    if (lane == 0) {
+        for (int k = 0; k < 6; k++) {
+          const int sl = (c0 + k) >> 6;
+          yb[k] = sr_readlane64(sl == 0 ? zr[0] : (sl == 1 ? zr[1] : zr[2]), (c0 + k) & 63);
+        }
+      }
 #pragma unroll
-      for (int k = 0; k < 6; k++) xv[c0 + k] = xb[k];
-    }
+      for (int k = 5; k >= 0; k--) {
+        double v = yb[k];
 #pragma unroll
-    for (int j = 0; j < 3; j++)
+        for (int l = 5; l > k; l--) v -= Lc[l * (l - 1) / 2 + k] * xb[l];
+        xb[k] = v;
+      }
+      if (lane == 0) {
 #pragma unroll
-      for (int l = 5; l >= 0; l--) zr[j] -= Ac[j][l] * xb[l];
-    if (st > 0) {
+        for (int k = 0; k < 6; k++) xv[c0 + k] = xb[k];
+      }
 #pragma unroll
       for (int j = 0; j < 3; j++)
 #pragma unroll
-        for (int l = 0; l < 6; l++) Ac[j][l] = An[j][l];
+        for (int l = 5; l >= 0; l--) zr[j] -= Ac[j][l] * xb[l];
+      if (st > 0) {
+#pragma unroll
+        for (int j = 0; j < 3; j++)
+#pragma unroll
+          for (int l = 0; l < 6; l++) Ac[j][l] = An[j][l];
+      }
     }
   }
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");

@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <random>
 #include <vector>
+#include <cstring>
 
 #include "ba_solve_reg.hpp"
 
@@ -401,17 +402,18 @@ __global__ void piv_kernel(double* out, unsigned long long* cyc, int nrows) {
   out[lane] = acc;
 }
 
-// the backward substitution alone (1024 threads, synthetic panels): cycles per pose step
+// the backward substitution alone (1024 threads, synthetic panels): cycles per pose step; kV: sr_backsub variant
+template <bool kV>
 __global__ __launch_bounds__(kSolveRegThreads) void bs_kernel(double* out, unsigned long long* cyc, int K) {
   extern __shared__ double lds[];
   const SolveRegLayout Ly(K);
   for (int i = threadIdx.x; i < Ly.total; i += blockDim.x) lds[i] = 1e-3 * ((i * 37) % 101);
   __syncthreads();
   const unsigned long long t0 = __builtin_readcyclecounter();
-  if (threadIdx.x < 64) sr_backsub(lds, lds + Ly.ld, lds + Ly.xs, K);
+  if (threadIdx.x < 64) sr_backsub<kV>(lds, lds + Ly.ld, lds + Ly.xs, K);
   const unsigned long long t1 = __builtin_readcyclecounter();
   if (threadIdx.x == 0) cyc[0] = t1 - t0;
-  if (threadIdx.x < 64) out[threadIdx.x] = lds[Ly.xs + threadIdx.x];
+  for (int i = threadIdx.x; i < 6 * K; i += blockDim.x) out[i] = lds[Ly.xs + i];
 }
 
 static int pair_index_h(int c, int a, int K) { return c * K - c * (c - 1) / 2 + (a - c); }
@@ -493,12 +495,24 @@ int main(int argc, char** argv) {
   CK(hipFuncSetAttribute((const void*)v0::kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l0));
   CK(hipFuncSetAttribute((const void*)v1_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)l1));
   {
-    CK(hipFuncSetAttribute((const void*)bs_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
-    hipLaunchKernelGGL(bs_kernel, dim3(1), dim3(kSolveRegThreads), solve_reg_lds_bytes(K), 0, d_x, d_st, K);
-    CK(hipDeviceSynchronize());
-    unsigned long long c;
-    CK(hipMemcpy(&c, d_st, sizeof(c), hipMemcpyDeviceToHost));
-    printf("backward substitution alone: %.0f cycles (%.0f per pose step)\n", (double)c, (double)c / K);
+    std::vector<double> xb0(n), xb(n);
+    auto run_bs = [&](auto kern, int v) {
+      CK(hipFuncSetAttribute((const void*)kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)solve_reg_lds_bytes(K)));
+      unsigned long long best = ~0ull;
+      for (int r = 0; r < 5; r++) {
+        hipLaunchKernelGGL(kern, dim3(1), dim3(kSolveRegThreads), solve_reg_lds_bytes(K), 0, d_x, d_st, K);
+        CK(hipDeviceSynchronize());
+        unsigned long long c;
+        CK(hipMemcpy(&c, d_st, sizeof(c), hipMemcpyDeviceToHost));
+        best = c < best ? c : best;
+      }
+      CK(hipMemcpy(v == 0 ? xb0.data() : xb.data(), d_x, n * sizeof(double), hipMemcpyDeviceToHost));
+      const bool same = v == 0 || memcmp(xb0.data(), xb.data(), n * sizeof(double)) == 0;
+      printf("backward substitution alone, variant %d: %.0f cycles (%.0f per pose step)%s\n", v, (double)best,
+             (double)best / K, same ? "" : "  RESULT DIFFERS");
+    };
+    run_bs(bs_kernel<false>, 0);  // (variant 0: the previous form; 1: the ping-pong form of the library)
+    run_bs(bs_kernel<true>, 1);
   }
   for (int nr : {6, 70, 175}) {
     hipLaunchKernelGGL(piv_kernel, dim3(1), dim3(64), 0, 0, d_x, d_st, nr);
