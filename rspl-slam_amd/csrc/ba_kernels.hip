@@ -17,6 +17,7 @@
 #include "ba_kernels.hpp"
 #include "ba_solve_reg.hpp"
 #include "se3_device.hpp"
+#include "wave_reduce.hpp"
 
 
 namespace rspl {
@@ -1286,10 +1287,7 @@ __device__ __forceinline__ void block_reduce(double (&acc)[NV], double* lds /* [
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nw = blockDim.x >> 6;
 #pragma unroll
   for (int i = 0; i < NV; i++) {
-    double v = acc[i];
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-    acc[i] = v;
+    acc[i] = wave::xsum64(acc[i]);  // (the xor butterfly's sums, on lane moves)
   }
   if (lane == 0)
 #pragma unroll
@@ -2026,8 +2024,7 @@ __global__ __launch_bounds__(256) void schur_solve_kernel(Problem P, Active A, S
   if (lane < P.np && pose_a >= 0)
 #pragma unroll
     for (int k = 0; k < 6; k++) sc += z[6 * pose_a + k] * (lambda * z[6 * pose_a + k] + bpl[6 * pose_a + k]);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
+  sc = wave::xsum64(sc);
   if (lane == 0) S.out[4] = sc;
   if (tid == 0) prof_stamp(S, 4);
 }
@@ -2196,8 +2193,7 @@ __device__ __forceinline__ void solve_wave(Problem P, const Active& A, const Sys
   if (row) S.x[lane] = x;
   // the pose part of the LM scale x.(lambda x + bp) (the candidate poses: update_errors_kernel)
   double sc = row ? x * (lambda * x + bpl) : 0.0;
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
+  sc = wave::xsum64(sc);
   if (lane == 0) S.out[4] = sc;
 }
 

@@ -24,6 +24,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include "wave_reduce.hpp"
+
 namespace rspl {
 namespace ba {
 
@@ -494,8 +496,7 @@ __device__ void solve_reg(const double* __restrict__ pairfin, int K, double lamb
   if (pose_a >= 0)
 #pragma unroll
     for (int k = 0; k < 6; k++) sc += xv[6 * pose_a + k] * (lambda * xv[6 * pose_a + k] + bpl[6 * pose_a + k]);
-#pragma unroll
-  for (int o = 32; o >= 1; o >>= 1) sc += __shfl_xor(sc, o);
+  sc = wave::xsum64(sc);
   if (lane == 0) *sc_out = sc;
   stamp.at(4);
 }

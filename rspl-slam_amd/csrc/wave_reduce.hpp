@@ -65,6 +65,21 @@ __device__ __forceinline__ double swap_sum(double a, double b) {
   return __longlong_as_double((long long)((unsigned long long)p1 << 32 | p0)) +
          __longlong_as_double((long long)((unsigned long long)q1 << 32 | q0));
 }
+// wave64 all-reduce (sum) with the partners of the xor butterfly (32, 16, 8, 4, 2, 1) -- bitwise the result of
+// `for (o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o)` (each step adds the same pair; a + b == b + a) -- on VALU lane
+// moves: v_permlane32_swap / v_permlane16_swap, DPP row_ror:8 (= xor 8 in a 16-lane row), row_shl:4 / row_shr:4
+// selected by lane bit 2, quad permutes; no ds_bpermute round trips on the chain
+__device__ __forceinline__ double xsum64(double v) {
+  v = swap_sum<true>(v, v);
+  v = swap_sum<false>(v, v);
+  v += dppd<0x128>(v);  // row_ror:8
+  {
+    const double up = dppd<0x104>(v), dn = dppd<0x114>(v);  // row_shl:4 (lane + 4) / row_shr:4 (lane - 4)
+    v += (threadIdx.x & 4) ? dn : up;
+  }
+  v += dppd<0x4E>(v);
+  return v + dppd<0xB1>(v);
+}
 // the reduce-scatter: lane L returns the wave's sum of value L >> 1 (values 28..31: 0)
 __device__ __forceinline__ double wave_scatter28(const double (&acc)[kNV], int lane) {
   double v[32];
